@@ -1,0 +1,172 @@
+"""MI355X-native per-frame odometry hot path of Adaptive-RGBD-Localization-Mapping.
+
+The compute path is libodo_hip.so (hand-written HIP for gfx950, C-ABI in
+include/odo.h). This package is a thin Python binding used by tests and
+bench.py; the reference-shaped C++ adapters (Extractor / Matcher / Ransac /
+PnPSolver / Kabsch) live in csrc/host/odo_reference_api.hpp.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _abi
+from ._abi import (Calib, Config, DMatch, DMATCH_DTYPE, KP_DTYPE, OrbParams, PAIR_DTYPE, PairResult,
+                   RansacParams, Rng, check, load, ptr)
+
+__all__ = ["Odometry", "default_config", "load", "KP_DTYPE", "DMATCH_DTYPE", "PAIR_DTYPE", "rng_stream",
+           "kabsch", "Calib", "OrbParams", "RansacParams", "Config"]
+
+
+def default_config(width=640, height=480, max_batch=1, nfeatures=1000, iterations=200, seed=0x5EED0000,
+                   calib=None) -> Config:
+    """Reference defaults (extractor.cpp:86, odometry.cpp:28, common.h FR1)."""
+    cfg = Config()
+    load().odo_default_config(ptr(cfg), width, height, max_batch)
+    cfg.orb.nfeatures = nfeatures
+    cfg.ransac.iterations = iterations
+    cfg.seed = seed
+    if calib is not None:
+        for k, v in calib.items():
+            setattr(cfg.calib, k, v)
+    return cfg
+
+
+class Odometry:
+    """One context = one HIP stream + HBM scratch + previous-frame/latch state."""
+
+    def __init__(self, cfg: Config, device: int = 0):
+        self.lib = load()
+        self.cfg = cfg
+        h = self.lib.odo_create(ptr(cfg), device)
+        if not h:
+            raise RuntimeError("odo_create failed: " + self.lib.odo_last_error().decode())
+        self.h = h
+        self.kp_cap = cfg.orb.nfeatures + 4 * cfg.orb.nlevels + 64
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.odo_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self) -> int:
+        return self.lib.odo_stream(self.h) or 0
+
+    def reset(self):
+        check(self.lib.odo_reset(self.h))
+
+    def set_latch(self, v: float):
+        check(self.lib.odo_set_latch(self.h, v))
+
+    @property
+    def latch(self) -> float:
+        return self.lib.odo_get_latch(self.h)
+
+    def track_batch(self, bgr_ptr: int, depth_ptr: int, n: int, want_results=True):
+        """Device-resident inputs (e.g. torch tensor .data_ptr())."""
+        out = np.zeros(n, PAIR_DTYPE) if want_results else None
+        check(self.lib.odo_track_batch(self.h, C.c_void_p(bgr_ptr), C.c_void_p(depth_ptr), n,
+                                       ptr(out) if want_results else None))
+        return out
+
+    def track_batch_host(self, bgr: np.ndarray, depth: np.ndarray):
+        bgr = np.ascontiguousarray(bgr, np.uint8)
+        depth = np.ascontiguousarray(depth, np.uint16)
+        n = bgr.shape[0]
+        out = np.zeros(n, PAIR_DTYPE)
+        check(self.lib.odo_track_batch_host(self.h, ptr(bgr), ptr(depth), n, ptr(out)))
+        return out
+
+    def synchronize(self):
+        check(self.lib.odo_synchronize(self.h))
+
+    def frame(self, i: int):
+        cap = self.kp_cap
+        kps = np.zeros(cap, KP_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        kun = np.zeros((cap, 2), np.float32)
+        xyz = np.zeros((cap, 3), np.float32)
+        ur = np.zeros(cap, np.float32)
+        n = C.c_int(0)
+        check(self.lib.odo_get_frame(self.h, i, ptr(kps), ptr(desc), ptr(kun), ptr(xyz), ptr(ur), cap, C.byref(n)))
+        m = n.value
+        return dict(kps=kps[:m], desc=desc[:m], kun=kun[:m], xyz=xyz[:m], ur=ur[:m])
+
+    def pair(self, i: int):
+        cap = self.kp_cap
+        matches = np.zeros(cap, DMATCH_DTYPE)
+        good = np.zeros(cap, DMATCH_DTYPE)
+        rin = np.zeros(cap, np.uint8)
+        pin = np.zeros(cap, np.uint8)
+        src = np.zeros(cap, np.int32)
+        nm, ng = C.c_int(0), C.c_int(0)
+        check(self.lib.odo_get_pair(self.h, i, ptr(matches), cap, C.byref(nm), ptr(good), C.byref(ng), ptr(rin),
+                                    ptr(pin), ptr(src)))
+        return dict(matches=matches[:nm.value], good=good[:ng.value], ransac_inliers=rin[:ng.value],
+                    pnp_inliers=pin, f2_src=src)
+
+    def debug_pyramid(self, i: int, total: int):
+        out = np.zeros(total + 4096, np.uint8)
+        n = self.lib.odo_debug_pyramid(self.h, i, ptr(out), out.size)
+        if n < 0:
+            check(n)
+        return out[:n]
+
+    def debug_blur(self, i: int, total: int):
+        out = np.zeros(total + 4096, np.uint8)
+        n = self.lib.odo_debug_blur(self.h, i, ptr(out), out.size)
+        if n < 0:
+            check(n)
+        return out[:n]
+
+    def debug_fast(self, i: int, level: int, cap: int = 1 << 18):
+        out = np.zeros(cap, KP_DTYPE)
+        n = C.c_int(0)
+        check(self.lib.odo_debug_fast(self.h, i, level, ptr(out), cap, C.byref(n)))
+        return out[:n.value]
+
+    def debug_octree(self, i: int, level: int, cap: int = 1 << 14):
+        out = np.zeros(cap, KP_DTYPE)
+        n = C.c_int(0)
+        check(self.lib.odo_debug_octree(self.h, i, level, ptr(out), cap, C.byref(n)))
+        return out[:n.value]
+
+    def timings(self):
+        ms = np.zeros(16, np.float32)
+        names = (C.c_char_p * 16)()
+        n = self.lib.odo_last_timings(self.h, ptr(ms), 16, C.cast(names, C.c_void_p))
+        return {names[i].decode(): float(ms[i]) for i in range(n)}
+
+
+def rng_stream(seed: int, n: int) -> np.ndarray:
+    """glibc rand() stream as restated by the library (host helper)."""
+    r = Rng()
+    L = load()
+    L.odo_rng_seed(ptr(r), seed)
+    return np.array([L.odo_rng_next(ptr(r)) for _ in range(n)], np.int32)
+
+
+def pair_seed(base: int, pair: int) -> int:
+    """Per-pair RANSAC seed of the batched contract: splitmix64(base ^ pair), low 32 bits."""
+    m = (1 << 64) - 1
+    z = ((base ^ pair) + 0x9E3779B97F4A7C15) & m
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & m
+    z ^= z >> 31
+    return z & 0xFFFFFFFF
+
+
+def kabsch(A: np.ndarray, B: np.ndarray) -> np.ndarray:
+    A = np.ascontiguousarray(A, np.float32)
+    B = np.ascontiguousarray(B, np.float32)
+    T = np.zeros(16, np.float32)
+    check(load().odo_kabsch(ptr(A), ptr(B), A.shape[0], ptr(T)))
+    return T.reshape(4, 4)

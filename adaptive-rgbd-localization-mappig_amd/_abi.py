@@ -1,0 +1,128 @@
+"""ctypes view of include/odo.h (the C-ABI of libodo_hip.so).
+
+The product path is the HIP library; this module only binds it. There is no
+CPU fallback: if the shared library or a gfx950 device is missing, loading or
+odo_create() fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libodo_hip.so")
+
+P = C.c_void_p
+
+
+class OrbKP(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("size", C.c_float), ("angle", C.c_float),
+                ("response", C.c_float), ("octave", C.c_int32), ("class_id", C.c_int32)]
+
+
+class DMatch(C.Structure):
+    _fields_ = [("queryIdx", C.c_int32), ("trainIdx", C.c_int32), ("imgIdx", C.c_int32), ("distance", C.c_float)]
+
+
+class Calib(C.Structure):
+    _fields_ = [(n, C.c_float) for n in ("fx", "fy", "cx", "cy", "k1", "k2", "p1", "p2", "k3",
+                                         "depth_factor", "mbf", "th_depth")]
+
+
+class OrbParams(C.Structure):
+    _fields_ = [("nfeatures", C.c_int32), ("scale_factor", C.c_float), ("nlevels", C.c_int32),
+                ("ini_th_fast", C.c_int32), ("min_th_fast", C.c_int32)]
+
+
+class RansacParams(C.Structure):
+    _fields_ = [("iterations", C.c_int32), ("min_inlier_th", C.c_int32), ("max_mahalanobis", C.c_float),
+                ("sample_size", C.c_int32), ("check_depth", C.c_int32)]
+
+
+class Rng(C.Structure):
+    _fields_ = [("state", C.c_int32 * 31), ("fpos", C.c_int32), ("rpos", C.c_int32)]
+
+
+class PairResult(C.Structure):
+    _fields_ = [("T12", C.c_float * 16), ("Tcw", C.c_float * 16), ("rmse", C.c_float),
+                ("n_matches", C.c_int32), ("n_good", C.c_int32), ("n_inliers", C.c_int32),
+                ("ransac_ok", C.c_int32), ("pnp_inliers", C.c_int32), ("visited", C.c_int32),
+                ("pad", C.c_int32)]
+
+
+class Config(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("max_batch", C.c_int32),
+                ("orb", OrbParams), ("calib", Calib), ("nn_ratio", C.c_float),
+                ("ransac", RansacParams), ("seed", C.c_uint32)]
+
+
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+DMATCH_DTYPE = np.dtype([("queryIdx", "<i4"), ("trainIdx", "<i4"), ("imgIdx", "<i4"), ("distance", "<f4")])
+PAIR_DTYPE = np.dtype([("T12", "<f4", 16), ("Tcw", "<f4", 16), ("rmse", "<f4"), ("n_matches", "<i4"),
+                       ("n_good", "<i4"), ("n_inliers", "<i4"), ("ransac_ok", "<i4"), ("pnp_inliers", "<i4"),
+                       ("visited", "<i4"), ("pad", "<i4")])
+
+# Every symbol include/odo.h declares, with its ctypes signature.
+SIGNATURES = {
+    "odo_default_config": (None, [P, C.c_int, C.c_int, C.c_int]),
+    "odo_create": (P, [P, C.c_int]),
+    "odo_destroy": (None, [P]),
+    "odo_last_error": (C.c_char_p, []),
+    "odo_stream": (P, [P]),
+    "odo_reset": (C.c_int, [P]),
+    "odo_set_latch": (C.c_int, [P, C.c_double]),
+    "odo_get_latch": (C.c_double, [P]),
+    "odo_track_batch": (C.c_int, [P, P, P, C.c_int, P]),
+    "odo_track_batch_host": (C.c_int, [P, P, P, C.c_int, P]),
+    "odo_extract_batch": (C.c_int, [P, P, P, C.c_int]),
+    "odo_synchronize": (C.c_int, [P]),
+    "odo_get_frame": (C.c_int, [P, C.c_int, P, P, P, P, P, C.c_int, P]),
+    "odo_get_pair": (C.c_int, [P, C.c_int, P, C.c_int, P, P, P, P, P, P]),
+    "odo_extract": (C.c_int, [P, P, C.c_int, P, P, P, P, P, P, C.c_int, P]),
+    "odo_knn2_hamming": (C.c_int, [P, P, C.c_int, P, C.c_int, P, P]),
+    "odo_ransac": (C.c_int, [P, P, C.c_int, P, C.c_int, P, C.c_int, P, P, P, P, P, P, P, P]),
+    "odo_pnp_motion_ba": (C.c_int, [P, P, P, C.c_int, P, P, P, P, P]),
+    "odo_kabsch": (C.c_int, [P, P, C.c_int, P]),
+    "odo_rng_seed": (None, [P, C.c_uint32]),
+    "odo_rng_next": (C.c_int32, [P]),
+    "odo_debug_pyramid": (C.c_int, [P, C.c_int, P, C.c_size_t]),
+    "odo_debug_fast": (C.c_int, [P, C.c_int, C.c_int, P, C.c_int, P]),
+    "odo_debug_octree": (C.c_int, [P, C.c_int, C.c_int, P, C.c_int, P]),
+    "odo_debug_blur": (C.c_int, [P, C.c_int, P, C.c_size_t]),
+    "odo_last_timings": (C.c_int, [P, P, C.c_int, P]),
+}
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load libodo_hip.so and bind every C-ABI symbol. Raises if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} not built: run __graft_entry__.build() (make -C adaptive-rgbd-localization-mappig_amd)")
+    L = C.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def ptr(a):
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data_as(P)
+    return C.cast(C.pointer(a), P) if not isinstance(a, int) else P(a)
+
+
+def check(rc: int):
+    if rc != 0:
+        raise RuntimeError(f"odo error {rc}: {load().odo_last_error().decode()}")
+    return rc

@@ -1,0 +1,849 @@
+// ORB-SLAM2 extraction kernels for gfx950 (Features/orbextractor.cpp,
+// Core/frame.cpp). One launch processes a batch of frames; all per-level
+// geometry lives in device tables built once per image size (odo_capi.cpp).
+//
+//   k_gray        cvtColor(BGR2GRAY)                 frame.cpp:23
+//   k_resize      ComputePyramid (INTER_LINEAR 8U)    orbextractor.cpp:833-857
+//   k_fast_cells  FAST-9/16 + NMS per 30px cell       orbextractor.cpp:669-723
+//   k_octree      DistributeOctTree                   orbextractor.cpp:466-663
+//   k_blur        GaussianBlur 7x7 s=2 REFLECT_101    orbextractor.cpp:795-796
+//   k_finalize    IC_Angle + rBRIEF + scale + undistort + depth back-projection
+//                 orbextractor.cpp:14-85,805-811; frame.cpp:139-164,286-313
+#include "odo_device.h"
+#include "odo_internal.h"
+#include "../../include/odo_orb_pattern.h"
+
+namespace odo {
+
+__constant__ int8_t c_pattern[1024];
+__constant__ int c_umax[16];
+
+// ============================================================ gray
+// gray = (B*1868 + G*9617 + R*4899 + 8192) >> 14, 4 pixels per thread.
+__global__ void __launch_bounds__(256) k_gray(const uint8_t* __restrict__ bgr, uint8_t* __restrict__ pyr,
+                                              int npix, size_t in_stride, size_t pyr_stride) {
+    const int f = blockIdx.y;
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;  // quad index
+    const uint8_t* src = bgr + (size_t)f * in_stride;
+    uint8_t* dst = pyr + (size_t)f * pyr_stride;
+    const int p0 = q * 4;
+    if (p0 + 3 < npix) {
+        const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src + (size_t)p0 * 3);
+        uint32_t w0 = s32[0], w1 = s32[1], w2 = s32[2];
+        uint8_t b[12];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            b[i] = (w0 >> (8 * i)) & 0xff;
+            b[4 + i] = (w1 >> (8 * i)) & 0xff;
+            b[8 + i] = (w2 >> (8 * i)) & 0xff;
+        }
+        uint32_t out = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            uint32_t g = ((uint32_t)b[3 * i] * 1868u + (uint32_t)b[3 * i + 1] * 9617u + (uint32_t)b[3 * i + 2] * 4899u +
+                          8192u) >> 14;
+            out |= g << (8 * i);
+        }
+        *reinterpret_cast<uint32_t*>(dst + p0) = out;
+    } else {
+        for (int p = p0; p < npix; p++) {
+            const uint8_t* s = src + (size_t)p * 3;
+            dst[p] = (uint8_t)(((uint32_t)s[0] * 1868u + (uint32_t)s[1] * 9617u + (uint32_t)s[2] * 4899u + 8192u) >> 14);
+        }
+    }
+}
+
+// ============================================================ resize
+// One output pixel per thread; x/y tables precomputed on the host with the
+// OpenCV generic-path rules (xmax rule folded into a0=2048,a1=0).
+__global__ void __launch_bounds__(256) k_resize(uint8_t* __restrict__ pyr, size_t pyr_stride, int src_off,
+                                                int sw, int dst_off, int dw, int dh,
+                                                const ResizeX* __restrict__ xt, const ResizeY* __restrict__ yt) {
+    const int f = blockIdx.z;
+    const int dx = blockIdx.x * blockDim.x + threadIdx.x;
+    const int dy = blockIdx.y;
+    if (dx >= dw) return;
+    uint8_t* base = pyr + (size_t)f * pyr_stride;
+    const uint8_t* S = base + src_off;
+    const ResizeX X = xt[dx];
+    const ResizeY Y = yt[dy];
+    const uint8_t* r0 = S + (size_t)Y.sy0 * sw;
+    const uint8_t* r1 = S + (size_t)Y.sy1 * sw;
+    int h0 = r0[X.sx0] * X.a0 + r0[X.sx1] * X.a1;
+    int h1 = r1[X.sx0] * X.a0 + r1[X.sx1] * X.a1;
+    int v = (h0 * Y.b0 + h1 * Y.b1 + (1 << 21)) >> 22;
+    v = v < 0 ? 0 : (v > 255 ? 255 : v);
+    base[dst_off + (size_t)dy * dw + dx] = (uint8_t)v;
+}
+
+// ============================================================ FAST per cell
+__constant__ int c_circle_dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+__constant__ int c_circle_dy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
+
+// cornerScore<16> restated (min/max over arcs), d[k] = v - p[k].
+ODO_INLINE int corner_score16(const int* d, int threshold) {
+    int a0 = threshold;
+#pragma unroll
+    for (int k = 0; k < 16; k += 2) {
+        int a = min(d[(k + 1) & 15], d[(k + 2) & 15]);
+        a = min(a, d[(k + 3) & 15]);
+        a = min(a, d[(k + 4) & 15]);
+        a = min(a, d[(k + 5) & 15]);
+        a = min(a, d[(k + 6) & 15]);
+        a = min(a, d[(k + 7) & 15]);
+        a = min(a, d[(k + 8) & 15]);
+        a0 = max(a0, min(a, d[k]));
+        a0 = max(a0, min(a, d[(k + 9) & 15]));
+    }
+    int b0 = -a0;
+#pragma unroll
+    for (int k = 0; k < 16; k += 2) {
+        int b = max(d[(k + 1) & 15], d[(k + 2) & 15]);
+        b = max(b, d[(k + 3) & 15]);
+        b = max(b, d[(k + 4) & 15]);
+        b = max(b, d[(k + 5) & 15]);
+        b = max(b, d[(k + 6) & 15]);
+        b = max(b, d[(k + 7) & 15]);
+        b = max(b, d[(k + 8) & 15]);
+        b0 = min(b0, max(b, d[k]));
+        b0 = min(b0, max(b, d[(k + 9) & 15]));
+    }
+    return -b0 - 1;
+}
+
+ODO_INLINE bool has_run9(uint32_t m16) {
+    uint32_t x = m16 | (m16 << 16);
+    uint32_t a = x & (x >> 1);
+    uint32_t b = a & (a >> 2);
+    uint32_t c = b & (b >> 4);
+    return (c & (x >> 8)) != 0;
+}
+
+// One wave (64 lanes) per cell ROI. Candidates packed as (resp<<24)|(y<<12)|x
+// with x,y relative to the 16px border (vToDistributeKeys coordinates),
+// emitted in row-major order within the cell.
+__global__ void __launch_bounds__(64) k_fast_cells(const uint8_t* __restrict__ pyr, size_t pyr_stride,
+                                                   const CellDesc* __restrict__ cells, const LevelDesc* __restrict__ lv,
+                                                   uint32_t* __restrict__ cand, int* __restrict__ cand_cnt,
+                                                   int ncells, int cell_cap, int ini_th, int min_th) {
+    __shared__ uint8_t roi[FAST_ROI_MAX * FAST_ROI_MAX];
+    __shared__ uint8_t score[FAST_ROI_MAX * FAST_ROI_MAX];
+    __shared__ uint8_t isc[FAST_ROI_MAX * FAST_ROI_MAX];
+    const int f = blockIdx.y;
+    const int ci = blockIdx.x;
+    const int lane = threadIdx.x;
+    const CellDesc C = cells[ci];
+    const LevelDesc L = lv[C.level];
+    const uint8_t* img = pyr + (size_t)f * pyr_stride + L.off;
+    const int rows = C.rows, cols = C.cols;
+    for (int p = lane; p < rows * cols; p += 64) {
+        int r = p / cols, c = p - r * cols;
+        roi[r * FAST_ROI_MAX + c] = img[(size_t)(C.y0 + r) * L.w + (C.x0 + c)];
+    }
+    __syncthreads();
+    uint32_t* out = cand + ((size_t)f * ncells + ci) * cell_cap;
+    const int drows = rows - 6, dcols = cols - 6;
+    const int nd = drows > 0 && dcols > 0 ? drows * dcols : 0;
+    int count = 0;
+    for (int attempt = 0; attempt < 2; attempt++) {
+        const int th = attempt == 0 ? ini_th : min_th;
+        const int thc = th < 0 ? 0 : (th > 255 ? 255 : th);
+        for (int p = lane; p < rows * FAST_ROI_MAX; p += 64) {
+            score[p] = 0;
+            isc[p] = 0;
+        }
+        __syncthreads();
+        for (int p = lane; p < nd; p += 64) {
+            const int i = 3 + p / dcols, j = 3 + p % dcols;
+            const int v = roi[i * FAST_ROI_MAX + j];
+            int d[16];
+            uint32_t dark = 0, bright = 0;
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const int px = roi[(i + c_circle_dy[k]) * FAST_ROI_MAX + j + c_circle_dx[k]];
+                d[k] = v - px;
+                dark |= (uint32_t)(px < v - thc) << k;
+                bright |= (uint32_t)(px > v + thc) << k;
+            }
+            if (has_run9(dark) || has_run9(bright)) {
+                isc[i * FAST_ROI_MAX + j] = 1;
+                score[i * FAST_ROI_MAX + j] = (uint8_t)corner_score16(d, thc);
+            }
+        }
+        __syncthreads();
+        // NMS + ordered compaction, 64 pixels of the detection region per step
+        for (int base = 0; base < nd; base += 64) {
+            const int p = base + lane;
+            bool keep = false;
+            uint32_t packed = 0;
+            if (p < nd) {
+                const int i = 3 + p / dcols, j = 3 + p % dcols;
+                const int o = i * FAST_ROI_MAX + j;
+                if (isc[o]) {
+                    const int s = score[o];
+                    keep = s > score[o - FAST_ROI_MAX - 1] && s > score[o - FAST_ROI_MAX] &&
+                           s > score[o - FAST_ROI_MAX + 1] && s > score[o - 1] && s > score[o + 1] &&
+                           s > score[o + FAST_ROI_MAX - 1] && s > score[o + FAST_ROI_MAX] &&
+                           s > score[o + FAST_ROI_MAX + 1];
+                    const uint32_t x = (uint32_t)(j + C.offx), y = (uint32_t)(i + C.offy);
+                    packed = ((uint32_t)s << 24) | (y << 12) | x;
+                }
+            }
+            const uint64_t m = __ballot(keep);
+            if (keep) {
+                const int pos = count + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+                if (pos < cell_cap) out[pos] = packed;
+            }
+            count += __popcll(m);
+        }
+        if (count > 0) break;
+        __syncthreads();
+    }
+    if (lane == 0) cand_cnt[(size_t)f * ncells + ci] = count < cell_cap ? count : cell_cap;
+}
+
+// ============================================================ octree
+// DistributeOctTree as a parallel restatement: the std::list is an array in
+// list order rebuilt every pass with scans; push_front order, creation order
+// (the pinned tie-break for the (size, pointer) sort) and "first max wins"
+// are reproduced exactly.
+struct ONode {
+    int16_t x0, y0, x1, y1;
+    int32_t cnt;
+    int32_t seq;
+};
+
+#define OT_THREADS 256
+
+// vSizeAndPointerToNode entry: sorts by (size, creation seq); low 16 bits carry
+// the node's list position (never compared: seq is unique).
+ODO_INLINE uint64_t ot_key(int cnt, int seq, int pos) {
+    return ((uint64_t)(uint32_t)cnt << 40) | ((uint64_t)(uint32_t)(seq & 0xFFFFFF) << 16) | (uint64_t)(pos & 0xFFFF);
+}
+
+template <typename T>
+ODO_INLINE T block_exclusive_scan(T v, T* tmp, T* total) {
+    // tmp: OT_THREADS entries; returns exclusive prefix of v over threadIdx order
+    const int t = threadIdx.x;
+    tmp[t] = v;
+    __syncthreads();
+    for (int off = 1; off < OT_THREADS; off <<= 1) {
+        T a = t >= off ? tmp[t - off] : (T)0;
+        __syncthreads();
+        tmp[t] += a;
+        __syncthreads();
+    }
+    T incl = tmp[t];
+    *total = tmp[OT_THREADS - 1];
+    __syncthreads();
+    return incl - v;
+}
+
+__global__ void __launch_bounds__(OT_THREADS) k_octree(const uint32_t* __restrict__ cand,
+                                                       const int* __restrict__ cand_cnt, const LevelDesc* __restrict__ lv,
+                                                       int ncells, int cell_cap, int nlevels,
+                                                       uint32_t* __restrict__ keys_g, int32_t* __restrict__ knode_g,
+                                                       uint8_t* __restrict__ kquad_g, size_t keys_stride_frame,
+                                                       uint32_t* __restrict__ okp, int* __restrict__ ocnt, int okp_stride,
+                                                       int node_cap) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int f = blockIdx.y;
+    const int l = blockIdx.x;
+    const int t = threadIdx.x;
+    const LevelDesc L = lv[l];
+    // carve LDS
+    ONode* nodesA = reinterpret_cast<ONode*>(smem);
+    ONode* nodesB = nodesA + node_cap;
+    int* cc = reinterpret_cast<int*>(nodesB + node_cap);          // node_cap*4 child counts / scratch
+    int* npos = cc + 4 * node_cap;                                 // node_cap*4 child positions
+    int* iscr = npos + 4 * node_cap;                               // node_cap ints scratch
+    int* scan = iscr + node_cap;                                   // OT_THREADS
+    uint64_t* sortk = reinterpret_cast<uint64_t*>(scan + OT_THREADS + 2);  // node_cap (pow2) sort keys
+    __shared__ __attribute__((aligned(16))) int s_vars[16];
+    int& s_size = s_vars[0];
+    int& s_prev = s_vars[1];
+    int& s_seq = s_vars[2];
+    int& s_phase = s_vars[3];
+    int& s_finish = s_vars[4];
+    int& s_vcnt = s_vars[5];
+
+    const size_t kbase = (size_t)f * keys_stride_frame + (size_t)L.key_off;
+    uint32_t* keys = keys_g + kbase;
+    int32_t* knode = knode_g + kbase;
+    uint8_t* kquad = kquad_g + kbase;
+    uint32_t* out = okp + ((size_t)f * nlevels + l) * okp_stride;
+
+    // ---- gather candidates of this level's cells in cell order
+    const int c0 = L.cell_begin, nc = L.cell_end - L.cell_begin;
+    int n = 0;
+    for (int cb = 0; cb < nc; cb += OT_THREADS) {
+        const int c = cb + t;
+        const int cnt = c < nc ? cand_cnt[(size_t)f * ncells + c0 + c] : 0;
+        int tot;
+        const int ex = block_exclusive_scan<int>(cnt, scan, &tot);
+        if (c < nc) {
+            const uint32_t* src = cand + ((size_t)f * ncells + c0 + c) * cell_cap;
+            for (int k = 0; k < cnt; k++) keys[n + ex + k] = src[k];
+        }
+        n += tot;
+    }
+    __syncthreads();
+    if (n == 0) {
+        if (t == 0) ocnt[f * nlevels + l] = 0;
+        return;
+    }
+    const int minX = 16, maxX = L.w - 16, minY = 16, maxY = L.h - 16;
+    const int N = L.quota;
+    const int nIni = (int)roundf((float)(maxX - minX) / (float)(maxY - minY));
+    const float hX = (float)(maxX - minX) / (float)nIni;
+
+    // ---- initial nodes
+    for (int i = t; i < nIni; i += OT_THREADS) {
+        ONode nd;
+        nd.x0 = (int16_t)(int)(hX * (float)i);
+        nd.x1 = (int16_t)(int)(hX * (float)(i + 1));
+        nd.y0 = 0;
+        nd.y1 = (int16_t)(maxY - minY);
+        nd.cnt = 0;
+        nd.seq = i;
+        nodesA[i] = nd;
+    }
+    __syncthreads();
+    for (int k = t; k < n; k += OT_THREADS) {
+        const uint32_t key = keys[k];
+        const float x = (float)(key & 0xfff);
+        const int ni = (int)(x / hX);
+        knode[k] = ni;
+        atomicAdd(&nodesA[ni].cnt, 1);
+    }
+    __syncthreads();
+    // erase empty initial nodes (keep order)
+    if (t == 0) {
+        int w = 0;
+        for (int i = 0; i < nIni; i++) {
+            iscr[i] = -1;
+            if (nodesA[i].cnt > 0) {
+                iscr[i] = w;
+                nodesB[w++] = nodesA[i];
+            }
+        }
+        s_size = w;
+        s_seq = nIni;
+        s_finish = 0;
+        s_phase = 1;
+    }
+    __syncthreads();
+    for (int k = t; k < n; k += OT_THREADS) knode[k] = iscr[knode[k]];
+    for (int i = t; i < s_size; i += OT_THREADS) nodesA[i] = nodesB[i];
+    __syncthreads();
+
+    ONode* cur = nodesA;
+    ONode* nxt = nodesB;
+    // vSizeAndPtr entries live in sortk as (cnt<<32 | seq); positions resolved by seq lookup
+    int vcount = 0;
+
+    while (!s_finish) {
+        const int S = s_size;
+        if (s_phase == 1) {
+            // ---------------- phase 1: divide every node with >1 keys
+            for (int i = t; i < 4 * S; i += OT_THREADS) cc[i] = 0;
+            __syncthreads();
+            for (int k = t; k < n; k += OT_THREADS) {
+                const int nd = knode[k];
+                const ONode N0 = cur[nd];
+                if (N0.cnt > 1) {
+                    const uint32_t key = keys[k];
+                    const int x = key & 0xfff, y = (key >> 12) & 0xfff;
+                    const int hx = (N0.x1 - N0.x0 + 1) >> 1;  // ceil((x1-x0)/2), x1>=x0
+                    const int hy = (N0.y1 - N0.y0 + 1) >> 1;
+                    const int q = (x < N0.x0 + hx) ? (y < N0.y0 + hy ? 0 : 2) : (y < N0.y0 + hy ? 1 : 3);
+                    kquad[k] = (uint8_t)q;
+                    atomicAdd(&cc[nd * 4 + q], 1);
+                }
+            }
+            __syncthreads();
+            // per-node children stats, scans over list order (chunks of OT_THREADS)
+            int childBase = 0, survBase = 0, expBase = 0;
+            int totalChildren = 0;
+            // first: total children (for survivor offset) and reverse positions
+            // pass A: e_i forward exclusive scan (seq, vSizeAndPtr order)
+            for (int cb = 0; cb < S; cb += OT_THREADS) {
+                const int i = cb + t;
+                int e = 0, ne = 0, s = 0;
+                if (i < S) {
+                    if (cur[i].cnt > 1) {
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            e += cc[i * 4 + q] > 0;
+                            ne += cc[i * 4 + q] > 1;
+                        }
+                    } else s = 1;
+                }
+                int te, tne, ts;
+                const int ex_e = block_exclusive_scan<int>(e, scan, &te);
+                const int ex_ne = block_exclusive_scan<int>(ne, scan, &tne);
+                const int ex_s = block_exclusive_scan<int>(s, scan, &ts);
+                if (i < S) {
+                    iscr[i] = childBase + ex_e;          // forward children prefix
+                    npos[i * 4 + 0] = e;                 // stash e
+                    npos[i * 4 + 1] = ex_ne + expBase;   // vSizeAndPtr base
+                    npos[i * 4 + 2] = survBase + ex_s;   // survivor rank
+                    npos[i * 4 + 3] = s;
+                }
+                childBase += te;
+                expBase += tne;
+                survBase += ts;
+                __syncthreads();
+            }
+            totalChildren = childBase;
+            const int newSize = totalChildren + survBase;
+            // build new list
+            for (int i = t; i < S; i += OT_THREADS) {
+                const ONode P = cur[i];
+                const int e = npos[i * 4 + 0];
+                const int vb = npos[i * 4 + 1];
+                const int sr = npos[i * 4 + 2];
+                if (npos[i * 4 + 3]) {
+                    const int pos = totalChildren + sr;
+                    nxt[pos] = P;
+                    cc[i * 4 + 0] = pos;  // survivor mapping
+                } else {
+                    // reverse-chronological block start: children of later nodes come first
+                    const int blockStart = totalChildren - (iscr[i] + e);
+                    const int hx = (P.x1 - P.x0 + 1) >> 1, hy = (P.y1 - P.y0 + 1) >> 1;
+                    int r = 0, v = vb;
+                    int cpos[4];
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const int c = cc[i * 4 + q];
+                        cpos[q] = -1;
+                        if (c > 0) {
+                            ONode C;
+                            const int qx = q & 1, qy = q >> 1;
+                            C.x0 = (int16_t)(qx ? P.x0 + hx : P.x0);
+                            C.x1 = (int16_t)(qx ? P.x1 : P.x0 + hx);
+                            C.y0 = (int16_t)(qy ? P.y0 + hy : P.y0);
+                            C.y1 = (int16_t)(qy ? P.y1 : P.y0 + hy);
+                            C.cnt = c;
+                            C.seq = s_seq + iscr[i] + r;
+                            const int pos = blockStart + (e - 1 - r);
+                            nxt[pos] = C;
+                            cpos[q] = pos;
+                            if (c > 1) {
+                                sortk[v] = ot_key(c, C.seq, pos);
+                                v++;
+                            }
+                            r++;
+                        }
+                    }
+#pragma unroll
+                    for (int q = 0; q < 4; q++) cc[i * 4 + q] = cpos[q];
+                }
+            }
+            __syncthreads();
+            for (int k = t; k < n; k += OT_THREADS) {
+                const int nd = knode[k];
+                if (cur[nd].cnt > 1) knode[k] = cc[nd * 4 + kquad[k]];
+                else knode[k] = cc[nd * 4 + 0];
+            }
+            __syncthreads();
+            if (t == 0) {
+                s_prev = S;
+                s_size = newSize;
+                s_seq += totalChildren;
+                s_vcnt = expBase;
+                if (newSize >= N || newSize == S) s_finish = 1;
+                else if (newSize + expBase * 3 > N) s_phase = 2;
+            }
+            vcount = expBase;
+            __syncthreads();
+            ONode* tmpp = cur;
+            cur = nxt;
+            nxt = tmpp;
+        } else {
+            // ---------------- phase 2: divide the largest nodes first
+            vcount = s_vcnt;
+            // bitonic sort of sortk[0..vcount) ascending by (cnt, seq)
+            int pw = 1;
+            while (pw < vcount) pw <<= 1;
+            for (int i = vcount + t; i < pw; i += OT_THREADS) sortk[i] = ~0ull;
+            __syncthreads();
+            for (int kk = 2; kk <= pw; kk <<= 1) {
+                for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+                    for (int i = t; i < pw; i += OT_THREADS) {
+                        const int ixj = i ^ jj;
+                        if (ixj > i) {
+                            const uint64_t a = sortk[i], b = sortk[ixj];
+                            const bool up = (i & kk) == 0;
+                            if ((a > b) == up) {
+                                sortk[i] = b;
+                                sortk[ixj] = a;
+                            }
+                        }
+                    }
+                    __syncthreads();
+                }
+            }
+            // processing rank per node: node of sortk[vcount-1-j] is processed j-th
+            for (int i = t; i < S; i += OT_THREADS) iscr[i] = -1;
+            __syncthreads();
+            for (int j = t; j < vcount; j += OT_THREADS) iscr[(int)(sortk[vcount - 1 - j] & 0xFFFF)] = j;
+            __syncthreads();
+            for (int i = t; i < 4 * S; i += OT_THREADS) cc[i] = 0;
+            __syncthreads();
+            for (int k = t; k < n; k += OT_THREADS) {
+                const int nd = knode[k];
+                if (iscr[nd] >= 0) {
+                    const ONode N0 = cur[nd];
+                    const uint32_t key = keys[k];
+                    const int x = key & 0xfff, y = (key >> 12) & 0xfff;
+                    const int hx = (N0.x1 - N0.x0 + 1) >> 1;
+                    const int hy = (N0.y1 - N0.y0 + 1) >> 1;
+                    const int q = (x < N0.x0 + hx) ? (y < N0.y0 + hy ? 0 : 2) : (y < N0.y0 + hy ? 1 : 3);
+                    kquad[k] = (uint8_t)q;
+                    atomicAdd(&cc[nd * 4 + q], 1);
+                }
+            }
+            __syncthreads();
+            // sequential part (one thread): break point, positions, seq numbers
+            if (t == 0) {
+                // processing list: proc[j] = node index
+                int* proc = npos;  // reuse: first vcount entries
+                for (int i = 0; i < S; i++)
+                    if (iscr[i] >= 0) proc[iscr[i]] = i;
+                int size = S, J = 0;
+                for (int j = 0; j < vcount; j++) {
+                    const int i = proc[j];
+                    int e = 0;
+                    for (int q = 0; q < 4; q++) e += cc[i * 4 + q] > 0;
+                    size += e - 1;
+                    J = j + 1;
+                    if (size >= N) break;
+                }
+                // children blocks in reverse processing order at the front
+                int pos = 0;
+                int seq = s_seq;
+                int nv = 0;
+                // seq numbers in processing order
+                int* childSeqBase = npos + vcount;  // J entries
+                for (int j = 0; j < J; j++) {
+                    const int i = proc[j];
+                    childSeqBase[j] = seq;
+                    for (int q = 0; q < 4; q++) seq += cc[i * 4 + q] > 0;
+                }
+                for (int j = J - 1; j >= 0; j--) {
+                    const int i = proc[j];
+                    const ONode P = cur[i];
+                    const int hx = (P.x1 - P.x0 + 1) >> 1, hy = (P.y1 - P.y0 + 1) >> 1;
+                    int e = 0;
+                    for (int q = 0; q < 4; q++) e += cc[i * 4 + q] > 0;
+                    int r = 0;
+                    int cpos[4];
+                    for (int q = 0; q < 4; q++) {
+                        const int c = cc[i * 4 + q];
+                        cpos[q] = -1;
+                        if (c > 0) {
+                            ONode C;
+                            const int qx = q & 1, qy = q >> 1;
+                            C.x0 = (int16_t)(qx ? P.x0 + hx : P.x0);
+                            C.x1 = (int16_t)(qx ? P.x1 : P.x0 + hx);
+                            C.y0 = (int16_t)(qy ? P.y0 + hy : P.y0);
+                            C.y1 = (int16_t)(qy ? P.y1 : P.y0 + hy);
+                            C.cnt = c;
+                            C.seq = childSeqBase[j] + r;
+                            const int p = pos + (e - 1 - r);
+                            nxt[p] = C;
+                            cpos[q] = p;
+                            r++;
+                        }
+                    }
+                    for (int q = 0; q < 4; q++) cc[i * 4 + q] = cpos[q];
+                    pos += e;
+                }
+                // new vSizeAndPtr: children with cnt>1 in processing order, n1..n4
+                for (int j = 0; j < J; j++) {
+                    const int i = proc[j];
+                    for (int q = 0; q < 4; q++) {
+                        const int p = cc[i * 4 + q];
+                        if (p >= 0 && nxt[p].cnt > 1) sortk[nv++] = ot_key(nxt[p].cnt, nxt[p].seq, p);
+                    }
+                }
+                // survivors: all nodes not processed (j >= J), original order
+                for (int i = 0; i < S; i++) {
+                    const int j = iscr[i];
+                    if (j >= 0 && j < J) continue;
+                    nxt[pos] = cur[i];
+                    cc[i * 4 + 0] = pos;
+                    iscr[i] = -2;  // survivor marker
+                    pos++;
+                }
+                for (int i = 0; i < S; i++)
+                    if (iscr[i] >= 0 && iscr[i] >= J) iscr[i] = -2;
+                s_prev = S;
+                s_size = pos;
+                s_seq = seq;
+                s_vcnt = nv;
+                if (pos >= N || pos == S) s_finish = 1;
+            }
+            __syncthreads();
+            for (int k = t; k < n; k += OT_THREADS) {
+                const int nd = knode[k];
+                if (iscr[nd] == -2 || iscr[nd] == -1) knode[k] = cc[nd * 4 + 0];
+                else knode[k] = cc[nd * 4 + kquad[k]];
+            }
+            __syncthreads();
+            ONode* tmpp = cur;
+            cur = nxt;
+            nxt = tmpp;
+        }
+        __syncthreads();
+    }
+    // ---- retain best key per node (max response, first in candidate order)
+    const int S = s_size;
+    unsigned* best = reinterpret_cast<unsigned*>(cc);
+    for (int i = t; i < S; i += OT_THREADS) best[i] = 0;
+    __syncthreads();
+    for (int k = t; k < n; k += OT_THREADS) {
+        const uint32_t key = keys[k];
+        const unsigned v = ((key >> 24) << 23) | (0x7FFFFFu - (unsigned)k);
+        atomicMax(&best[knode[k]], v);
+    }
+    __syncthreads();
+    const int cap = okp_stride;
+    for (int i = t; i < S && i < cap; i += OT_THREADS) {
+        const int k = 0x7FFFFF - (int)(best[i] & 0x7FFFFF);
+        out[i] = keys[k];
+    }
+    if (t == 0) ocnt[f * nlevels + l] = S < cap ? S : cap;
+}
+
+// ============================================================ blur
+// Separable 7-tap Q8 kernel {18,34,48,56,48,34,18}, REFLECT_101, exact integer.
+#define BLUR_TX 64
+#define BLUR_TY 16
+ODO_INLINE int reflect101(int i, int n) {
+    while (i < 0 || i >= n) i = i < 0 ? -i : 2 * n - 2 - i;
+    return i;
+}
+
+__global__ void __launch_bounds__(256) k_blur(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
+                                              size_t pyr_stride, const LevelDesc* __restrict__ lv) {
+    __shared__ uint8_t tile[(BLUR_TY + 6) * (BLUR_TX + 8)];
+    __shared__ uint16_t hrow[(BLUR_TY + 6) * BLUR_TX];
+    const int f = blockIdx.z;
+    const int l = blockIdx.y;
+    const LevelDesc L = lv[l];
+    const int tilesX = (L.w + BLUR_TX - 1) / BLUR_TX;
+    const int tilesY = (L.h + BLUR_TY - 1) / BLUR_TY;
+    if ((int)blockIdx.x >= tilesX * tilesY) return;
+    const int tx0 = (blockIdx.x % tilesX) * BLUR_TX, ty0 = (blockIdx.x / tilesX) * BLUR_TY;
+    const uint8_t* src = pyr + (size_t)f * pyr_stride + L.off;
+    uint8_t* dst = blur + (size_t)f * pyr_stride + L.off;
+    const int TW = BLUR_TX + 6, TH = BLUR_TY + 6;
+    for (int p = threadIdx.x; p < TW * TH; p += 256) {
+        const int r = p / TW, c = p % TW;
+        const int y = reflect101(ty0 + r - 3, L.h), x = reflect101(tx0 + c - 3, L.w);
+        tile[r * (BLUR_TX + 8) + c] = src[(size_t)y * L.w + x];
+    }
+    __syncthreads();
+    const int kq[7] = {18, 34, 48, 56, 48, 34, 18};
+    for (int p = threadIdx.x; p < TH * BLUR_TX; p += 256) {
+        const int r = p / BLUR_TX, c = p % BLUR_TX;
+        const uint8_t* s = &tile[r * (BLUR_TX + 8) + c];
+        uint32_t h = 0;
+#pragma unroll
+        for (int j = 0; j < 7; j++) h += (uint32_t)kq[j] * s[j];
+        hrow[r * BLUR_TX + c] = (uint16_t)h;
+    }
+    __syncthreads();
+    for (int p = threadIdx.x; p < BLUR_TY * BLUR_TX; p += 256) {
+        const int r = p / BLUR_TX, c = p % BLUR_TX;
+        const int y = ty0 + r, x = tx0 + c;
+        if (y < L.h && x < L.w) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int j = 0; j < 7; j++) v += (uint32_t)kq[j] * hrow[(r + j) * BLUR_TX + c];
+            dst[(size_t)y * L.w + x] = (uint8_t)((v + 32768u) >> 16);
+        }
+    }
+}
+
+// ============================================================ finalize
+// One wave per output keypoint (level-major order): IC angle on the raw
+// level, rBRIEF on the blurred level (4 bit-tests per lane, ballots pack the
+// bytes), coordinate scaling, cv::undistortPoints, depth back-projection.
+__global__ void __launch_bounds__(256) k_finalize(const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
+                                                  size_t pyr_stride, const LevelDesc* __restrict__ lv, int nlevels,
+                                                  const uint32_t* __restrict__ okp, const int* __restrict__ ocnt,
+                                                  int okp_stride, const uint16_t* __restrict__ depth,
+                                                  size_t depth_stride, int img_w, FrameCalib cal,
+                                                  orb_kp* __restrict__ kps, uint8_t* __restrict__ desc,
+                                                  float* __restrict__ kun, float* __restrict__ xyz,
+                                                  float* __restrict__ ur, int* __restrict__ nkp, int kp_cap) {
+    const int f = blockIdx.y;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int idx = blockIdx.x * 4 + wave;
+    // level lookup from per-level counts
+    int lvl = -1, k = 0, acc = 0, total = 0;
+    for (int i = 0; i < nlevels; i++) {
+        const int c = ocnt[f * nlevels + i];
+        if (lvl < 0 && idx < acc + c) {
+            lvl = i;
+            k = idx - acc;
+        }
+        acc += c;
+    }
+    total = acc < kp_cap ? acc : kp_cap;
+    if (blockIdx.x == 0 && threadIdx.x == 0) nkp[f] = total;
+    if (lvl < 0 || idx >= kp_cap) return;
+    const LevelDesc L = lv[lvl];
+    const uint32_t key = okp[((size_t)f * nlevels + lvl) * okp_stride + k];
+    const int kx = (int)(key & 0xfff) + 16, ky = (int)((key >> 12) & 0xfff) + 16;
+    const float resp = (float)(key >> 24);
+    const uint8_t* img = pyr + (size_t)f * pyr_stride + L.off;
+    // ---- IC_Angle: lane u in [0,31) owns column offset u-15
+    int m10 = 0, m01 = 0;
+    if (lane < 31) {
+        const int u = lane - 15;
+        const int au = u < 0 ? -u : u;
+        const uint8_t* col = img + (size_t)ky * L.w + kx + u;
+        m10 += u * col[0];
+        for (int v = 1; v <= 15; v++) {
+            if (au <= c_umax[v]) {
+                const int vp = col[(size_t)v * L.w], vm = col[-(ptrdiff_t)v * L.w];
+                m01 += v * (vp - vm);
+                m10 += u * (vp + vm);
+            }
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        m10 += __shfl_xor(m10, off);
+        m01 += __shfl_xor(m01, off);
+    }
+    const float angle = fast_atan2((float)m01, (float)m10);
+    // ---- rBRIEF
+    const float factorPI = (float)(3.14159265358979323846 / 180.f);
+    const float ang = angle * factorPI;
+    const float a = (float)cos((double)ang), b = (float)sin((double)ang);
+    const uint8_t* bl = blur + (size_t)f * pyr_stride + L.off;
+    const uint8_t* center = bl + (size_t)ky * L.w + kx;
+    uint64_t words[4];
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        const int bit = w * 64 + lane;  // pair index
+        const float x0 = (float)c_pattern[4 * bit + 0], y0 = (float)c_pattern[4 * bit + 1];
+        const float x1 = (float)c_pattern[4 * bit + 2], y1 = (float)c_pattern[4 * bit + 3];
+        const int t0 = center[cv_round(x0 * b + y0 * a) * L.w + cv_round(x0 * a - y0 * b)];
+        const int t1 = center[cv_round(x1 * b + y1 * a) * L.w + cv_round(x1 * a - y1 * b)];
+        words[w] = __ballot(t0 < t1);
+    }
+    const int o = idx;
+    orb_kp* kp = kps + (size_t)f * kp_cap + o;
+    if (lane < 4) {
+        reinterpret_cast<uint64_t*>(desc + ((size_t)f * kp_cap + o) * 32)[lane] = words[lane];
+    }
+    if (lane == 0) {
+        float px = (float)kx, py = (float)ky;
+        if (lvl != 0) {
+            px *= L.scale;
+            py *= L.scale;
+        }
+        kp->x = px;
+        kp->y = py;
+        kp->size = (float)(int)(31 * L.scale);
+        kp->angle = angle;
+        kp->response = resp;
+        kp->octave = lvl;
+        kp->class_id = -1;
+        // UndistortKeyPoints: cv::undistortPoints, 5 iterations in double
+        float uu = px, vv = py;
+        float ux = uu, uy = vv;
+        if (cal.k1 != 0.0f) {
+            const double fx = cal.fx, fy = cal.fy, cx = cal.cx, cy = cal.cy;
+            const double ifx = 1. / fx, ify = 1. / fy;
+            const double k0 = cal.k1, k1 = cal.k2, k2 = cal.p1, k3 = cal.p2, k4 = cal.k3;
+            double x = uu, y = vv;
+            x = (x - cx) * ifx;
+            y = (y - cy) * ify;
+            const double x0 = x, y0 = y;
+            for (int j = 0; j < 5; j++) {
+                double r2 = x * x + y * y;
+                double icdist = 1 / (1 + ((k4 * r2 + k1) * r2 + k0) * r2);
+                double deltaX = 2 * k2 * x * y + k3 * (r2 + 2 * x * x);
+                double deltaY = k2 * (r2 + 2 * y * y) + 2 * k3 * x * y;
+                x = (x0 - deltaX) * icdist;
+                y = (y0 - deltaY) * icdist;
+            }
+            ux = (float)(fx * x + cx);
+            uy = (float)(fy * y + cy);
+        }
+        float* ku = kun + ((size_t)f * kp_cap + o) * 2;
+        ku[0] = ux;
+        ku[1] = uy;
+        float* p3 = xyz + ((size_t)f * kp_cap + o) * 3;
+        float urv = -1.f, X = 0.f, Y = 0.f, Z = 0.f;
+        const uint16_t d16 = depth[(size_t)f * depth_stride + (size_t)((int)vv) * img_w + (int)uu];
+        const float z = (float)d16 * cal.depth_factor + 0.0f;
+        if (z > 0) {
+            urv = ux - cal.mbf / z;
+            X = (ux - cal.cx) * z * cal.invfx;
+            Y = (uy - cal.cy) * z * cal.invfy;
+            Z = z;
+        }
+        p3[0] = X;
+        p3[1] = Y;
+        p3[2] = Z;
+        ur[(size_t)f * kp_cap + o] = urv;
+    }
+}
+
+// ============================================================ host-side launch helpers
+void upload_extract_constants() {
+    hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), ODO_ORB_PATTERN, sizeof(ODO_ORB_PATTERN));
+    const int umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
+    hipMemcpyToSymbol(HIP_SYMBOL(c_umax), umax, sizeof(umax));
+}
+
+}  // namespace odo
+
+// ============================================================ launch wrappers
+namespace odo {
+void launch_gray(hipStream_t st, const uint8_t* bgr, uint8_t* pyr, int npix, size_t in_stride, size_t pyr_stride,
+                 int nframes) {
+    dim3 g((npix / 4 + 255) / 256 + 1, nframes);
+    hipLaunchKernelGGL(k_gray, g, dim3(256), 0, st, bgr, pyr, npix, in_stride, pyr_stride);
+}
+void launch_resize(hipStream_t st, uint8_t* pyr, size_t pyr_stride, int src_off, int sw, int dst_off, int dw, int dh,
+                   const ResizeX* xt, const ResizeY* yt, int nframes) {
+    dim3 g((dw + 255) / 256, dh, nframes);
+    hipLaunchKernelGGL(k_resize, g, dim3(256), 0, st, pyr, pyr_stride, src_off, sw, dst_off, dw, dh, xt, yt);
+}
+void launch_fast(hipStream_t st, const uint8_t* pyr, size_t pyr_stride, const CellDesc* cells, const LevelDesc* lv,
+                 uint32_t* cand, int* cand_cnt, int ncells, int cell_cap, int ini_th, int min_th, int nframes) {
+    dim3 g(ncells, nframes);
+    hipLaunchKernelGGL(k_fast_cells, g, dim3(64), 0, st, pyr, pyr_stride, cells, lv, cand, cand_cnt, ncells, cell_cap,
+                       ini_th, min_th);
+}
+size_t octree_lds_bytes(int node_cap) { return (size_t)76 * node_cap + 1032; }
+void launch_octree(hipStream_t st, const uint32_t* cand, const int* cand_cnt, const LevelDesc* lv, int ncells,
+                   int cell_cap, int nlevels, uint32_t* keys, int32_t* knode, uint8_t* kquad, size_t keys_stride,
+                   uint32_t* okp, int* ocnt, int okp_stride, int node_cap, int nframes) {
+    dim3 g(nlevels, nframes);
+    hipLaunchKernelGGL(k_octree, g, dim3(OT_THREADS), octree_lds_bytes(node_cap), st, cand, cand_cnt, lv, ncells,
+                       cell_cap, nlevels, keys, knode, kquad, keys_stride, okp, ocnt, okp_stride, node_cap);
+}
+void launch_blur(hipStream_t st, const uint8_t* pyr, uint8_t* blur, size_t pyr_stride, const LevelDesc* lv, int nlevels,
+                 int max_tiles, int nframes) {
+    dim3 g(max_tiles, nlevels, nframes);
+    hipLaunchKernelGGL(k_blur, g, dim3(256), 0, st, pyr, blur, pyr_stride, lv);
+}
+void launch_finalize(hipStream_t st, const uint8_t* pyr, const uint8_t* blur, size_t pyr_stride, const LevelDesc* lv,
+                     int nlevels, const uint32_t* okp, const int* ocnt, int okp_stride, const uint16_t* depth,
+                     size_t depth_stride, int img_w, FrameCalib cal, orb_kp* kps, uint8_t* desc, float* kun, float* xyz,
+                     float* ur, int* nkp, int kp_cap, int nframes) {
+    dim3 g((kp_cap + 3) / 4, nframes);
+    hipLaunchKernelGGL(k_finalize, g, dim3(256), 0, st, pyr, blur, pyr_stride, lv, nlevels, okp, ocnt, okp_stride,
+                       depth, depth_stride, img_w, cal, kps, desc, kun, xyz, ur, nkp, kp_cap);
+}
+}  // namespace odo

@@ -1,0 +1,451 @@
+// Matching kernels for gfx950.
+//
+//   k_knn2        cv::BFMatcher(NORM_HAMMING).knnMatch(k=2)   Features/matcher.cpp:60 (App. A.6)
+//   k_pair_match  per frame pair: UpdateLastFrame VO landmarks (tracking.cpp:146-190),
+//                 ratio test + landmark bookkeeping (matcher.cpp:62-85),
+//                 Ransac good-match filter + std::sort (ransac.cpp:175-199)
+//   k_latch       Ransac::DepthCovariance first-call latch (ransac.cpp:416-421)
+#include "odo_device.h"
+#include "odo_internal.h"
+
+namespace odo {
+
+// ============================================================ kNN-2 Hamming
+// One query per lane (256-bit descriptor in 8 VGPRs), train descriptors staged
+// through LDS in tiles and read as wave-uniform broadcasts. The top-2 is kept
+// as packed keys (dist<<20 | trainIdx): the BFMatcher insertion rule (ties keep
+// the lower train index, equal-to-second does not replace) is exactly "the two
+// smallest (dist, idx) pairs", so min/max updates reproduce it.
+#define KNN_Q 256
+#define KNN_T 256
+
+__global__ void __launch_bounds__(KNN_Q) k_knn2(const uint8_t* __restrict__ qdesc, const int* __restrict__ qn,
+                                                size_t q_stride, const uint8_t* __restrict__ tdesc,
+                                                const int* __restrict__ tn, size_t t_stride,
+                                                int2* __restrict__ out_idx, int2* __restrict__ out_dist,
+                                                size_t out_stride) {
+    __shared__ uint4 tile[KNN_T * 2];
+    const int p = blockIdx.y;
+    const int nq = qn[p], nt = tn[p];
+    const int qi = blockIdx.x * KNN_Q + threadIdx.x;
+    if ((int)(blockIdx.x * KNN_Q) >= nq) return;
+    const uint8_t* Q = qdesc + (size_t)p * q_stride;
+    const uint8_t* T = tdesc + (size_t)p * t_stride;
+    uint4 qa = make_uint4(0, 0, 0, 0), qb = make_uint4(0, 0, 0, 0);
+    if (qi < nq) {
+        qa = reinterpret_cast<const uint4*>(Q + (size_t)qi * 32)[0];
+        qb = reinterpret_cast<const uint4*>(Q + (size_t)qi * 32)[1];
+    }
+    uint32_t k0 = 0xFFFFFFFFu, k1 = 0xFFFFFFFFu;
+    for (int t0 = 0; t0 < nt; t0 += KNN_T) {
+        const int tcount = min(KNN_T, nt - t0);
+        __syncthreads();
+        for (int i = threadIdx.x; i < tcount * 2; i += KNN_Q)
+            tile[i] = reinterpret_cast<const uint4*>(T + (size_t)t0 * 32)[i];
+        __syncthreads();
+#pragma unroll 4
+        for (int j = 0; j < tcount; j++) {
+            const uint4 ta = tile[2 * j], tb = tile[2 * j + 1];
+            uint32_t d = __builtin_popcount(qa.x ^ ta.x);
+            d += __builtin_popcount(qa.y ^ ta.y);
+            d += __builtin_popcount(qa.z ^ ta.z);
+            d += __builtin_popcount(qa.w ^ ta.w);
+            d += __builtin_popcount(qb.x ^ tb.x);
+            d += __builtin_popcount(qb.y ^ tb.y);
+            d += __builtin_popcount(qb.z ^ tb.z);
+            d += __builtin_popcount(qb.w ^ tb.w);
+            const uint32_t key = (d << 20) | (uint32_t)(t0 + j);
+            k1 = min(k1, max(k0, key));
+            k0 = min(k0, key);
+        }
+    }
+    if (qi < nq) {
+        int2 I, D;
+        I.x = k0 == 0xFFFFFFFFu ? -1 : (int)(k0 & 0xFFFFF);
+        D.x = k0 == 0xFFFFFFFFu ? 0x7FFFFFFF : (int)(k0 >> 20);
+        I.y = k1 == 0xFFFFFFFFu ? -1 : (int)(k1 & 0xFFFFF);
+        D.y = k1 == 0xFFFFFFFFu ? 0x7FFFFFFF : (int)(k1 >> 20);
+        out_idx[(size_t)p * out_stride + qi] = I;
+        out_dist[(size_t)p * out_stride + qi] = D;
+    }
+}
+
+// ============================================================ libstdc++ std::sort emulation
+// Exactly the GNU introsort (std::__introsort_loop + __final_insertion_sort,
+// threshold 16, median-of-3 pivot, unguarded Hoare partition, heap fallback) on
+// 64-bit (key = distance bits, payload = position) elements compared by key
+// only: reproduces the unstable order of std::sort(vector<DMatch>) in
+// ransac.cpp:199 (App. B.4). Runs on one lane over an LDS/global array.
+struct SortEl {
+    uint32_t key;  // float bits of a non-negative distance (monotonic)
+    uint32_t val;
+};
+
+template <typename A>
+ODO_INLINE void st_swap(A a, int i, int j) {
+    SortEl t = a[i];
+    a[i] = a[j];
+    a[j] = t;
+}
+
+template <typename A>
+ODO_INLINE void st_move_median_to_first(A a, int result, int x, int y, int z) {
+    const uint32_t ax = a[x].key, ay = a[y].key, az = a[z].key;
+    if (ax < ay) {
+        if (ay < az) st_swap(a, result, y);
+        else if (ax < az) st_swap(a, result, z);
+        else st_swap(a, result, x);
+    } else if (ax < az) st_swap(a, result, x);
+    else if (ay < az) st_swap(a, result, z);
+    else st_swap(a, result, y);
+}
+
+template <typename A>
+ODO_INLINE int st_unguarded_partition(A a, int first, int last, int pivot) {
+    const uint32_t pk = a[pivot].key;
+    while (true) {
+        while (a[first].key < pk) ++first;
+        --last;
+        while (pk < a[last].key) --last;
+        if (!(first < last)) return first;
+        st_swap(a, first, last);
+        ++first;
+    }
+}
+
+template <typename A>
+ODO_INLINE void st_adjust_heap(A a, int first, int holeIndex, int len, SortEl value) {
+    const int topIndex = holeIndex;
+    int secondChild = holeIndex;
+    while (secondChild < (len - 1) / 2) {
+        secondChild = 2 * (secondChild + 1);
+        if (a[first + secondChild].key < a[first + secondChild - 1].key) secondChild--;
+        a[first + holeIndex] = a[first + secondChild];
+        holeIndex = secondChild;
+    }
+    if ((len & 1) == 0 && secondChild == (len - 2) / 2) {
+        secondChild = 2 * (secondChild + 1);
+        a[first + holeIndex] = a[first + secondChild - 1];
+        holeIndex = secondChild - 1;
+    }
+    // __push_heap
+    int parent = (holeIndex - 1) / 2;
+    while (holeIndex > topIndex && a[first + parent].key < value.key) {
+        a[first + holeIndex] = a[first + parent];
+        holeIndex = parent;
+        parent = (holeIndex - 1) / 2;
+    }
+    a[first + holeIndex] = value;
+}
+
+template <typename A>
+ODO_INLINE void st_heap_sort_range(A a, int first, int middle, int last) {
+    // std::__partial_sort(first, middle=last, last): __heap_select + __sort_heap
+    const int len = middle - first;
+    if (len >= 2) {
+        for (int parent = (len - 2) / 2;; parent--) {
+            SortEl v = a[first + parent];
+            st_adjust_heap(a, first, parent, len, v);
+            if (parent == 0) break;
+        }
+    }
+    for (int i = middle; i < last; ++i)
+        if (a[i].key < a[first].key) {
+            SortEl v = a[i];
+            a[i] = a[first];
+            st_adjust_heap(a, first, 0, len, v);
+        }
+    for (int l2 = middle; l2 - first > 1;) {
+        --l2;
+        SortEl v = a[l2];
+        a[l2] = a[first];
+        st_adjust_heap(a, first, 0, l2 - first, v);
+    }
+}
+
+template <typename A>
+ODO_INLINE void st_insertion_sort(A a, int first, int last) {
+    if (first == last) return;
+    for (int i = first + 1; i != last; ++i) {
+        SortEl val = a[i];
+        if (val.key < a[first].key) {
+            for (int k = i; k > first; --k) a[k] = a[k - 1];
+            a[first] = val;
+        } else {
+            int next = i - 1, cur = i;
+            while (val.key < a[next].key) {
+                a[cur] = a[next];
+                cur = next;
+                --next;
+            }
+            a[cur] = val;
+        }
+    }
+}
+
+template <typename A>
+ODO_INLINE void st_unguarded_insertion_sort(A a, int first, int last) {
+    for (int i = first; i != last; ++i) {
+        SortEl val = a[i];
+        int next = i - 1, cur = i;
+        while (val.key < a[next].key) {
+            a[cur] = a[next];
+            cur = next;
+            --next;
+        }
+        a[cur] = val;
+    }
+}
+
+template <typename A>
+ODO_INLINE void gnu_sort(A a, int n) {
+    if (n < 2) return;
+    // __introsort_loop with an explicit stack (recursion on the right part)
+    int lg = 31 - __builtin_clz((unsigned)n);
+    int stk_first[64], stk_last[64], stk_depth[64];
+    int sp = 0;
+    stk_first[sp] = 0;
+    stk_last[sp] = n;
+    stk_depth[sp] = 2 * lg;
+    sp++;
+    while (sp > 0) {
+        sp--;
+        int first = stk_first[sp], last = stk_last[sp], depth = stk_depth[sp];
+        while (last - first > 16) {
+            if (depth == 0) {
+                st_heap_sort_range(a, first, last, last);
+                break;
+            }
+            --depth;
+            const int mid = first + (last - first) / 2;
+            st_move_median_to_first(a, first, first + 1, mid, last - 1);
+            const int cut = st_unguarded_partition(a, first + 1, last, first);
+            // recurse on [cut, last) first (it is processed before the left loop
+            // continues in libstdc++, but the two ranges are disjoint, so order
+            // of processing does not change the result)
+            stk_first[sp] = cut;
+            stk_last[sp] = last;
+            stk_depth[sp] = depth;
+            sp++;
+            last = cut;
+        }
+    }
+    if (n > 16) {
+        st_insertion_sort(a, 0, 16);
+        st_unguarded_insertion_sort(a, 16, n);
+    } else st_insertion_sort(a, 0, n);
+}
+
+// ============================================================ per-pair match stage
+// One workgroup (256 threads) per pair (F1 = previous frame, F2 = current).
+// Outputs: good matches sorted per std::sort (query/train/distance), counts,
+// f2_src[i2] = F1 index whose landmark sits in F2 slot i2 (-1 if none).
+#define PM_THREADS 256
+
+__global__ void __launch_bounds__(PM_THREADS) k_pair_match(
+    const int2* __restrict__ knn_idx, const int2* __restrict__ knn_dist, size_t knn_stride,
+    const float* __restrict__ xyz, const int* __restrict__ nkp, int kp_cap, int slot0, float ratio,
+    float th_depth_m, int check_depth, odo_dmatch* __restrict__ matches, int* __restrict__ n_matches,
+    SortEl* __restrict__ good, int* __restrict__ n_good, int32_t* __restrict__ f2_src,
+    uint64_t* __restrict__ sort_scratch, int match_cap) {
+    __shared__ int s_cnt[PM_THREADS];
+    __shared__ int s_tot, s_total_valid, s_cle, s_K, s_nm;
+    const int p = blockIdx.x;                  // pair index
+    const int s1 = slot0 + p, s2 = slot0 + p + 1;
+    const int n1 = nkp[s1], n2 = nkp[s2];
+    const int t = threadIdx.x;
+    const float* X1 = xyz + (size_t)s1 * kp_cap * 3;
+    const float* X2 = xyz + (size_t)s2 * kp_cap * 3;
+    uint64_t* sk = sort_scratch + (size_t)p * kp_cap;
+    int32_t* src = f2_src + (size_t)p * kp_cap;
+    for (int i = t; i < n2; i += PM_THREADS) src[i] = -1;
+    // ---- VO landmarks on F1 (UpdateLastFrame, tracking.cpp:146-190): the K smallest
+    // (z, index) pairs among z>0, K = min(valid, max(#(z<=th)+1, 101)).
+    int cv = 0, cle = 0;
+    for (int i = t; i < n1; i += PM_THREADS) {
+        const float z = X1[3 * i + 2];
+        if (z > 0) {
+            cv++;
+            cle += z <= th_depth_m;
+        }
+    }
+    if (t == 0) {
+        s_total_valid = 0;
+        s_cle = 0;
+    }
+    __syncthreads();
+    atomicAdd(&s_total_valid, cv);
+    atomicAdd(&s_cle, cle);
+    __syncthreads();
+    const int valid = s_total_valid;
+    int K = s_cle + 1 > 101 ? s_cle + 1 : 101;
+    if (K > valid) K = valid;
+    // rank selection: sort (z_bits<<32 | i) ascending with a bitonic sort in global scratch
+    int pw = 1;
+    while (pw < n1) pw <<= 1;
+    for (int i = t; i < pw; i += PM_THREADS) {
+        uint64_t key = ~0ull;
+        if (i < n1) {
+            const float z = X1[3 * i + 2];
+            if (z > 0) key = ((uint64_t)__float_as_uint(z) << 32) | (uint32_t)i;
+        }
+        sk[i] = key;
+    }
+    __syncthreads();
+    for (int kk = 2; kk <= pw; kk <<= 1)
+        for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+            for (int i = t; i < pw; i += PM_THREADS) {
+                const int ixj = i ^ jj;
+                if (ixj > i) {
+                    const uint64_t a = sk[i], b = sk[ixj];
+                    const bool up = (i & kk) == 0;
+                    if ((a > b) == up) {
+                        sk[i] = b;
+                        sk[ixj] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    // has_lm flag for F1 index i: stored in the low bit field of a second pass over sk
+    // (reuse sk[pw + ..] is not available; mark via s2 knn output? use a bitmap in LDS)
+    __shared__ uint32_t lm_bits[(8192 + 31) / 32];
+    for (int i = t; i < (kp_cap + 31) / 32 && i < (8192 + 31) / 32; i += PM_THREADS) lm_bits[i] = 0;
+    __syncthreads();
+    for (int r = t; r < K; r += PM_THREADS) {
+        const int i = (int)(uint32_t)sk[r];
+        atomicOr(&lm_bits[i >> 5], 1u << (i & 31));
+    }
+    __syncthreads();
+    // ---- ratio test + bookkeeping in query order (all F1 landmarks are fresh
+    // VO landmarks with 0 observations and F2 starts empty, so no match is
+    // skipped by the Observations()>0 rule; the last query wins a train slot).
+    const int2* KI = knn_idx + (size_t)p * knn_stride;
+    const int2* KD = knn_dist + (size_t)p * knn_stride;
+    odo_dmatch* M = matches + (size_t)p * match_cap;
+    int base = 0;
+    for (int c0 = 0; c0 < n1; c0 += PM_THREADS) {
+        const int i = c0 + t;
+        bool acc = false;
+        int2 I = make_int2(-1, -1), D = make_int2(0, 0);
+        if (i < n1) {
+            I = KI[i];
+            D = KD[i];
+            if (I.x >= 0) {
+                const float d0 = (float)D.x, d1 = (float)D.y;
+                acc = (d0 < ratio * d1) && ((lm_bits[i >> 5] >> (i & 31)) & 1);
+            }
+        }
+        s_cnt[t] = acc;
+        __syncthreads();
+        for (int off = 1; off < PM_THREADS; off <<= 1) {
+            int a = t >= off ? s_cnt[t - off] : 0;
+            __syncthreads();
+            s_cnt[t] += a;
+            __syncthreads();
+        }
+        const int incl = s_cnt[t];
+        const int tot = s_cnt[PM_THREADS - 1];
+        if (acc) {
+            const int pos = base + incl - 1;
+            if (pos < match_cap) M[pos] = odo_dmatch{i, I.x, 0, (float)D.x};
+            atomicMax(&src[I.x], i);
+        }
+        base += tot;
+        __syncthreads();
+    }
+    const int nm = base < match_cap ? base : match_cap;
+    if (t == 0) n_matches[p] = nm;
+    __syncthreads();
+    // ---- good-match filter (ransac.cpp:175-189), order preserved
+    SortEl* G = good + (size_t)p * match_cap;
+    int gbase = 0;
+    for (int c0 = 0; c0 < nm; c0 += PM_THREADS) {
+        const int i = c0 + t;
+        bool g = false;
+        odo_dmatch m;
+        if (i < nm) {
+            m = M[i];
+            const float zs = X1[3 * m.queryIdx + 2], zt = X2[3 * m.trainIdx + 2];
+            g = true;
+            if (check_depth) {
+                if (__builtin_isnan(zs) || __builtin_isnan(zt)) g = false;
+                if (zs <= 0 || zt <= 0) g = false;
+            }
+        }
+        s_cnt[t] = g;
+        __syncthreads();
+        for (int off = 1; off < PM_THREADS; off <<= 1) {
+            int a = t >= off ? s_cnt[t - off] : 0;
+            __syncthreads();
+            s_cnt[t] += a;
+            __syncthreads();
+        }
+        const int incl = s_cnt[t];
+        const int tot = s_cnt[PM_THREADS - 1];
+        if (g) G[gbase + incl - 1] = SortEl{__float_as_uint(m.distance), (uint32_t)i};
+        gbase += tot;
+        __syncthreads();
+    }
+    // ---- std::sort(vGoodMatches) by distance (one lane, exact libstdc++ algorithm)
+    if (t == 0) {
+        n_good[p] = gbase;
+        gnu_sort(G, gbase);
+    }
+    (void)n2;
+}
+
+// Ransac::DepthCovariance latches on its first call in the process
+// (ransac.cpp:416-421): z0 = source z of the first sorted good match whose
+// target.x != 0 in the first pair that reaches ComputeInliersAndError.
+__global__ void k_latch(double* __restrict__ latch, const SortEl* __restrict__ good, const int* __restrict__ n_good,
+                        const int* __restrict__ n_matches, const odo_dmatch* __restrict__ matches,
+                        const float* __restrict__ xyz, int kp_cap, int slot0, int npairs, int match_cap,
+                        int min_inl, int sample_size, int iterations, const int* __restrict__ pair_valid) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    if (!__builtin_isnan(*latch)) return;
+    for (int p = 0; p < npairs; p++) {
+        if (!pair_valid[p]) continue;
+        if (n_matches[p] < 20 || n_matches[p] < min_inl) continue;
+        const int ng = n_good[p];
+        if (ng < min_inl) continue;
+        (void)iterations;
+        (void)sample_size;
+        const SortEl* G = good + (size_t)p * match_cap;
+        const odo_dmatch* M = matches + (size_t)p * match_cap;
+        const float* X1 = xyz + (size_t)(slot0 + p) * kp_cap * 3;
+        const float* X2 = xyz + (size_t)(slot0 + p + 1) * kp_cap * 3;
+        for (int k = 0; k < ng; k++) {
+            const odo_dmatch m = M[G[k].val];
+            if (X1[3 * m.queryIdx + 2] == 0.0f || X2[3 * m.trainIdx] == 0.0f) continue;
+            const double z = (double)X1[3 * m.queryIdx + 2];
+            const double sd = 0.01 * z * z;
+            *latch = sd * sd;
+            return;
+        }
+    }
+}
+
+}  // namespace odo
+
+namespace odo {
+void launch_knn2(hipStream_t st, const uint8_t* q, const int* qn, size_t q_stride, const uint8_t* t, const int* tn,
+                 size_t t_stride, int2* idx, int2* dist, size_t out_stride, int max_q, int npairs) {
+    dim3 g((max_q + KNN_Q - 1) / KNN_Q, npairs);
+    hipLaunchKernelGGL(k_knn2, g, dim3(KNN_Q), 0, st, q, qn, q_stride, t, tn, t_stride, idx, dist, out_stride);
+}
+void launch_pair_match(hipStream_t st, const int2* knn_idx, const int2* knn_dist, size_t knn_stride, const float* xyz,
+                       const int* nkp, int kp_cap, int slot0, float ratio, float th_depth_m, int check_depth,
+                       odo_dmatch* matches, int* n_matches, void* good, int* n_good, int32_t* f2_src,
+                       uint64_t* sort_scratch, int match_cap, int npairs) {
+    hipLaunchKernelGGL(k_pair_match, dim3(npairs), dim3(PM_THREADS), 0, st, knn_idx, knn_dist, knn_stride, xyz, nkp,
+                       kp_cap, slot0, ratio, th_depth_m, check_depth, matches, n_matches, (SortEl*)good, n_good, f2_src,
+                       sort_scratch, match_cap);
+}
+void launch_latch(hipStream_t st, double* latch, const void* good, const int* n_good, const int* n_matches,
+                  const odo_dmatch* matches, const float* xyz, int kp_cap, int slot0, int npairs, int match_cap,
+                  int min_inl, int sample_size, int iterations, const int* pair_valid) {
+    hipLaunchKernelGGL(k_latch, dim3(1), dim3(64), 0, st, latch, (const SortEl*)good, n_good, n_matches, matches, xyz,
+                       kp_cap, slot0, npairs, match_cap, min_inl, sample_size, iterations, pair_valid);
+}
+}  // namespace odo

@@ -1,0 +1,951 @@
+// Host orchestration and C-ABI (include/odo.h) of the MI355X odometry path.
+//
+// A context owns one HIP stream, all HBM scratch sized for max_batch frames,
+// the per-image-size geometry tables (pyramid levels, FAST cells, resize
+// coefficients) and the cross-frame state the reference keeps in globals:
+// the previous frame (Tracking::mpLastFrame) and the DepthCovariance latch.
+// Frame slot 0 holds the previous frame, slots 1..n the current batch.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+#include <algorithm>
+
+#include "../../include/odo.h"
+#include "odo_device.h"
+#include "odo_internal.h"
+
+using namespace odo;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(x)                                                                                   \
+    do {                                                                                            \
+        hipError_t e_ = (x);                                                                        \
+        if (e_ != hipSuccess) return fail(ODO_ERR_DEVICE, std::string(#x) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+inline int cvRoundH(float v) { return (int)lrintf(v); }
+inline int cvFloorH(float v) {
+    int i = (int)v;
+    return i - (i > v);
+}
+inline int satShort(float v) {
+    int r = cvRoundH(v);
+    return std::min(std::max(r, -32768), 32767);
+}
+
+template <typename T>
+int dalloc(T** p, size_t count) {
+    if (count == 0) count = 1;
+    hipError_t e = hipMalloc((void**)p, count * sizeof(T));
+    if (e != hipSuccess) return fail(ODO_ERR_DEVICE, std::string("hipMalloc: ") + hipGetErrorString(e));
+    return ODO_OK;
+}
+
+uint32_t splitmix_host(uint64_t base, uint64_t pair) { return pair_seed(base, pair); }
+
+}  // namespace
+
+struct odo_ctx {
+    odo_config cfg{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int W = 0, H = 0, maxb = 0, slots = 0, nlevels = 0;
+    std::vector<LevelDesc> lv_h;
+    std::vector<CellDesc> cells_h;
+    std::vector<int> rx_off, ry_off;
+    LevelDesc* lv = nullptr;
+    CellDesc* cells = nullptr;
+    ResizeX* rx = nullptr;
+    ResizeY* ry = nullptr;
+    int ncells = 0, cell_cap = 0, kp_cap = 0, okp_stride = 0, node_cap = 0, match_cap = 0, mask_words = 0;
+    int max_blur_tiles = 0;
+    size_t pyr_size = 0, keys_per_frame = 0;
+    FrameCalib cal{};
+    RansacCfg rcfg{};
+    // frame buffers ([slots])
+    uint8_t *pyr = nullptr, *blur = nullptr;
+    uint32_t* cand = nullptr;
+    int* cand_cnt = nullptr;
+    uint32_t* keys = nullptr;
+    int32_t* knode = nullptr;
+    uint8_t* kquad = nullptr;
+    uint32_t* okp = nullptr;
+    int* ocnt = nullptr;
+    orb_kp* kps = nullptr;
+    uint8_t* desc = nullptr;
+    float *kun = nullptr, *xyz = nullptr, *ur = nullptr;
+    int* nkp = nullptr;
+    // staging for host inputs
+    uint8_t* bgr_in = nullptr;
+    uint16_t* depth_in = nullptr;
+    // pair buffers ([maxb])
+    int2 *knn_idx = nullptr, *knn_dist = nullptr;
+    odo_dmatch* matches = nullptr;
+    int *n_matches = nullptr, *n_good = nullptr, *pair_valid = nullptr;
+    void* good = nullptr;  // SortEl
+    int32_t* f2_src = nullptr;
+    uint64_t* sort_scratch = nullptr;
+    double* latch = nullptr;
+    void* gpts = nullptr;
+    uint32_t *masks = nullptr, *best_mask = nullptr;
+    odo_pair_result* res = nullptr;
+    float* T12 = nullptr;
+    void* edges = nullptr;
+    uint8_t* pnp_mask = nullptr;
+    // sequence state
+    bool has_prev = false;
+    uint64_t pair_counter = 0;
+    int last_n = 0;
+    std::vector<int> valid_h;
+    hipEvent_t ev[16];
+    int nev = 0;
+};
+
+static void free_ctx(odo_ctx* c) {
+    if (!c) return;
+    void* ptrs[] = {c->lv, c->cells, c->rx, c->ry, c->pyr, c->blur, c->cand, c->cand_cnt, c->keys, c->knode, c->kquad,
+                    c->okp, c->ocnt, c->kps, c->desc, c->kun, c->xyz, c->ur, c->nkp, c->bgr_in, c->depth_in,
+                    c->knn_idx, c->knn_dist, c->matches, c->n_matches, c->n_good, c->pair_valid, c->good, c->f2_src,
+                    c->sort_scratch, c->latch, c->gpts, c->masks, c->best_mask, c->res, c->T12, c->edges,
+                    c->pnp_mask};
+    for (void* p : ptrs)
+        if (p) hipFree(p);
+    for (int i = 0; i < c->nev; i++) hipEventDestroy(c->ev[i]);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+static int build_geometry(odo_ctx* c) {
+    const odo_orb_params& p = c->cfg.orb;
+    const int W = c->W, H = c->H;
+    c->nlevels = p.nlevels;
+    // ORBextractor tables (orbextractor.cpp:353-381); scaleFactor member is double
+    std::vector<float> scale(p.nlevels), inv(p.nlevels);
+    scale[0] = 1.0f;
+    for (int i = 1; i < p.nlevels; i++) scale[i] = (float)((double)scale[i - 1] * (double)p.scale_factor);
+    for (int i = 0; i < p.nlevels; i++) inv[i] = 1.0f / scale[i];
+    std::vector<int> quota(p.nlevels);
+    const double sf = (double)p.scale_factor;
+    float factor = (float)(1.0f / sf);
+    float nDesired = p.nfeatures * (1 - factor) / (1 - (float)pow((double)factor, (double)p.nlevels));
+    int sum = 0;
+    for (int l = 0; l < p.nlevels - 1; l++) {
+        quota[l] = cvRoundH(nDesired);
+        sum += quota[l];
+        nDesired *= factor;
+    }
+    quota[p.nlevels - 1] = std::max(p.nfeatures - sum, 0);
+
+    c->lv_h.resize(p.nlevels);
+    int off = 0, maxq = 0, max_nini = 1;
+    size_t key_off = 0;
+    c->cells_h.clear();
+    int max_tiles = 0;
+    for (int l = 0; l < p.nlevels; l++) {
+        LevelDesc& L = c->lv_h[l];
+        L.w = cvRoundH((float)W * inv[l]);
+        L.h = cvRoundH((float)H * inv[l]);
+        L.off = off;
+        L.scale = scale[l];
+        L.quota = quota[l];
+        off += L.w * L.h;
+        off = (off + 15) & ~15;
+        maxq = std::max(maxq, quota[l]);
+        if (L.w < 40 || L.h < 40) return fail(ODO_ERR_ARG, "pyramid level too small (< 40 px)");
+        // FAST cells (orbextractor.cpp:669-703)
+        const float Wc = 30;
+        const int minBorderX = 16, minBorderY = 16;
+        const int maxBorderX = L.w - 16, maxBorderY = L.h - 16;
+        const float width = (float)(maxBorderX - minBorderX), height = (float)(maxBorderY - minBorderY);
+        const int nCols = (int)(width / Wc), nRows = (int)(height / Wc);
+        const int wCell = (int)ceil(width / nCols), hCell = (int)ceil(height / nRows);
+        L.cell_begin = (int)c->cells_h.size();
+        for (int i = 0; i < nRows; i++) {
+            const float iniY = (float)(minBorderY + i * hCell);
+            float maxY = iniY + hCell + 6;
+            if (iniY >= maxBorderY - 3) continue;
+            if (maxY > maxBorderY) maxY = (float)maxBorderY;
+            for (int j = 0; j < nCols; j++) {
+                const float iniX = (float)(minBorderX + j * wCell);
+                float maxX = iniX + wCell + 6;
+                if (iniX >= maxBorderX - 6) continue;
+                if (maxX > maxBorderX) maxX = (float)maxBorderX;
+                CellDesc C;
+                C.level = (int16_t)l;
+                C.y0 = (int16_t)(int)iniY;
+                C.x0 = (int16_t)(int)iniX;
+                C.rows = (int16_t)((int)maxY - (int)iniY);
+                C.cols = (int16_t)((int)maxX - (int)iniX);
+                C.offx = (int16_t)(j * wCell);
+                C.offy = (int16_t)(i * hCell);
+                C.pad = 0;
+                if (C.rows > FAST_ROI_MAX || C.cols > FAST_ROI_MAX) return fail(ODO_ERR_ARG, "FAST cell exceeds ROI max");
+                c->cells_h.push_back(C);
+                c->cell_cap = std::max(c->cell_cap, ((C.rows - 6 + 1) / 2) * ((C.cols - 6 + 1) / 2) + 1);
+            }
+        }
+        L.cell_end = (int)c->cells_h.size();
+        L.key_off = (int)key_off;
+        const int nIni = (int)roundf((float)(maxBorderX - minBorderX) / (float)(maxBorderY - minBorderY));
+        max_nini = std::max(max_nini, nIni);
+        const int tiles = ((L.w + 63) / 64) * ((L.h + 15) / 16);
+        max_tiles = std::max(max_tiles, tiles);
+    }
+    c->ncells = (int)c->cells_h.size();
+    c->cell_cap = (c->cell_cap + 3) & ~3;
+    for (int l = 0; l < p.nlevels; l++) {
+        LevelDesc& L = c->lv_h[l];
+        L.key_off = 0;
+    }
+    size_t koff = 0;
+    for (int l = 0; l < p.nlevels; l++) {
+        c->lv_h[l].key_off = (int)koff;
+        koff += (size_t)(c->lv_h[l].cell_end - c->lv_h[l].cell_begin) * c->cell_cap;
+    }
+    c->keys_per_frame = koff;
+    c->pyr_size = (size_t)off;
+    c->max_blur_tiles = max_tiles;
+    c->okp_stride = maxq + 8;
+    int nc = 64;
+    while (nc < std::max(maxq + 8, 4 * max_nini + 8)) nc <<= 1;
+    c->node_cap = nc;
+    if (octree_lds_bytes(nc) > 160 * 1024) return fail(ODO_ERR_ARG, "octree node capacity exceeds LDS");
+    c->kp_cap = ((p.nfeatures + 4 * p.nlevels + 8) + 63) & ~63;
+    if (c->kp_cap > 8192) return fail(ODO_ERR_ARG, "nfeatures too large (kp cap 8192)");
+    c->match_cap = c->kp_cap;
+    c->mask_words = (c->match_cap + 31) / 32;
+    // resize tables (cv::resize generic INTER_LINEAR, App. A.2)
+    std::vector<ResizeX> rx;
+    std::vector<ResizeY> ry;
+    c->rx_off.assign(p.nlevels, 0);
+    c->ry_off.assign(p.nlevels, 0);
+    for (int l = 1; l < p.nlevels; l++) {
+        const LevelDesc& S = c->lv_h[l - 1];
+        const LevelDesc& D = c->lv_h[l];
+        const double inv_sx = (double)D.w / S.w, inv_sy = (double)D.h / S.h;
+        const double scale_x = 1. / inv_sx, scale_y = 1. / inv_sy;
+        c->rx_off[l] = (int)rx.size();
+        std::vector<int> xofs(D.w);
+        std::vector<int> a0(D.w), a1(D.w);
+        int xmax = D.w;
+        for (int dx = 0; dx < D.w; dx++) {
+            float fx = (float)((dx + 0.5) * scale_x - 0.5);
+            int sx = cvFloorH(fx);
+            fx -= sx;
+            if (sx < 0) {
+                fx = 0;
+                sx = 0;
+            }
+            if (sx + 1 >= S.w) {
+                xmax = std::min(xmax, dx);
+                if (sx >= S.w - 1) {
+                    fx = 0;
+                    sx = S.w - 1;
+                }
+            }
+            xofs[dx] = sx;
+            a0[dx] = satShort((1.f - fx) * 2048);
+            a1[dx] = satShort(fx * 2048);
+        }
+        for (int dx = 0; dx < D.w; dx++) {
+            ResizeX X;
+            X.sx0 = xofs[dx];
+            if (dx < xmax) {
+                X.sx1 = xofs[dx] + 1;
+                X.a0 = a0[dx];
+                X.a1 = a1[dx];
+            } else {
+                X.sx1 = xofs[dx];
+                X.a0 = 2048;
+                X.a1 = 0;
+            }
+            rx.push_back(X);
+        }
+        c->ry_off[l] = (int)ry.size();
+        for (int dy = 0; dy < D.h; dy++) {
+            float fy = (float)((dy + 0.5) * scale_y - 0.5);
+            int sy = cvFloorH(fy);
+            fy -= sy;
+            ResizeY Y;
+            Y.b0 = satShort((1.f - fy) * 2048);
+            Y.b1 = satShort(fy * 2048);
+            Y.sy0 = std::min(std::max(sy, 0), S.h - 1);
+            Y.sy1 = std::min(std::max(sy + 1, 0), S.h - 1);
+            ry.push_back(Y);
+        }
+    }
+    int e;
+    if ((e = dalloc(&c->lv, c->lv_h.size()))) return e;
+    if ((e = dalloc(&c->cells, c->cells_h.size()))) return e;
+    if ((e = dalloc(&c->rx, rx.size()))) return e;
+    if ((e = dalloc(&c->ry, ry.size()))) return e;
+    HIPCHK(hipMemcpy(c->lv, c->lv_h.data(), c->lv_h.size() * sizeof(LevelDesc), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->cells, c->cells_h.data(), c->cells_h.size() * sizeof(CellDesc), hipMemcpyHostToDevice));
+    if (!rx.empty()) HIPCHK(hipMemcpy(c->rx, rx.data(), rx.size() * sizeof(ResizeX), hipMemcpyHostToDevice));
+    if (!ry.empty()) HIPCHK(hipMemcpy(c->ry, ry.data(), ry.size() * sizeof(ResizeY), hipMemcpyHostToDevice));
+    return ODO_OK;
+}
+
+static int alloc_buffers(odo_ctx* c) {
+    const size_t S = (size_t)c->slots, B = (size_t)c->maxb;
+    int e;
+    if ((e = dalloc(&c->pyr, S * c->pyr_size))) return e;
+    if ((e = dalloc(&c->blur, S * c->pyr_size))) return e;
+    if ((e = dalloc(&c->cand, S * c->ncells * c->cell_cap))) return e;
+    if ((e = dalloc(&c->cand_cnt, S * c->ncells))) return e;
+    if ((e = dalloc(&c->keys, S * c->keys_per_frame))) return e;
+    if ((e = dalloc(&c->knode, S * c->keys_per_frame))) return e;
+    if ((e = dalloc(&c->kquad, S * c->keys_per_frame))) return e;
+    if ((e = dalloc(&c->okp, S * c->nlevels * c->okp_stride))) return e;
+    if ((e = dalloc(&c->ocnt, S * c->nlevels))) return e;
+    if ((e = dalloc(&c->kps, S * c->kp_cap))) return e;
+    if ((e = dalloc(&c->desc, S * c->kp_cap * 32))) return e;
+    if ((e = dalloc(&c->kun, S * c->kp_cap * 2))) return e;
+    if ((e = dalloc(&c->xyz, S * c->kp_cap * 3))) return e;
+    if ((e = dalloc(&c->ur, S * c->kp_cap))) return e;
+    if ((e = dalloc(&c->nkp, S))) return e;
+    if ((e = dalloc(&c->bgr_in, B * c->W * c->H * 3))) return e;
+    if ((e = dalloc(&c->depth_in, B * c->W * c->H))) return e;
+    if ((e = dalloc(&c->knn_idx, B * c->kp_cap))) return e;
+    if ((e = dalloc(&c->knn_dist, B * c->kp_cap))) return e;
+    if ((e = dalloc(&c->matches, B * c->match_cap))) return e;
+    if ((e = dalloc(&c->n_matches, B))) return e;
+    if ((e = dalloc(&c->n_good, B))) return e;
+    if ((e = dalloc(&c->pair_valid, B))) return e;
+    if ((e = dalloc((uint64_t**)&c->good, B * c->match_cap))) return e;
+    if ((e = dalloc(&c->f2_src, B * c->kp_cap))) return e;
+    int pw = 1;
+    while (pw < c->kp_cap) pw <<= 1;
+    if ((e = dalloc(&c->sort_scratch, B * std::max(pw, c->kp_cap)))) return e;
+    if ((e = dalloc(&c->latch, 1))) return e;
+    if ((e = dalloc((uint8_t**)&c->gpts, B * c->match_cap * ransac_gpt_bytes()))) return e;
+    if ((e = dalloc(&c->masks, B * 2 * c->mask_words * 256))) return e;
+    if ((e = dalloc(&c->best_mask, B * c->mask_words))) return e;
+    if ((e = dalloc(&c->res, B))) return e;
+    if ((e = dalloc(&c->T12, B * 16))) return e;
+    if ((e = dalloc((uint8_t**)&c->edges, B * c->kp_cap * pnp_edge_bytes()))) return e;
+    if ((e = dalloc(&c->pnp_mask, B * c->kp_cap))) return e;
+    HIPCHK(hipMemset(c->nkp, 0, S * sizeof(int)));
+    const double nan = std::nan("");
+    HIPCHK(hipMemcpy(c->latch, &nan, sizeof(double), hipMemcpyHostToDevice));
+    return ODO_OK;
+}
+
+extern "C" {
+
+const char* odo_last_error(void) { return g_err.c_str(); }
+
+void odo_default_config(odo_config* cfg, int width, int height, int max_batch) {
+    memset(cfg, 0, sizeof(*cfg));
+    cfg->width = width;
+    cfg->height = height;
+    cfg->max_batch = max_batch;
+    cfg->orb = odo_orb_params{1000, 1.2f, 8, 20, 7};
+    cfg->calib = odo_calib{517.3f, 516.5f, 318.6f, 255.3f, 0.262383f, -0.953104f, -0.005358f, 0.002628f, 1.163314f,
+                           1.0f / 5000.0f, 40.0f, 40.0f};
+    cfg->nn_ratio = 0.9f;
+    cfg->ransac = odo_ransac_params{200, 20, 3.0f, 4, 1};
+    cfg->seed = 0x5EED0000u;
+}
+
+odo_ctx* odo_create(const odo_config* cfg, int device) {
+    if (!cfg || cfg->width <= 0 || cfg->height <= 0 || cfg->max_batch <= 0 || cfg->orb.nlevels <= 0 ||
+        cfg->orb.nlevels > 16) {
+        fail(ODO_ERR_ARG, "invalid config");
+        return nullptr;
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device) {
+        fail(ODO_ERR_DEVICE, "no HIP device available (the MI355X path has no CPU fallback)");
+        return nullptr;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess || strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        fail(ODO_ERR_DEVICE, std::string("device is not gfx950: ") + prop.gcnArchName);
+        return nullptr;
+    }
+    hipSetDevice(device);
+    odo_ctx* c = new odo_ctx();
+    c->cfg = *cfg;
+    c->device = device;
+    c->W = cfg->width;
+    c->H = cfg->height;
+    c->maxb = cfg->max_batch;
+    c->slots = cfg->max_batch + 1;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        fail(ODO_ERR_DEVICE, "hipStreamCreate failed");
+        free_ctx(c);
+        return nullptr;
+    }
+    if (build_geometry(c) != ODO_OK || alloc_buffers(c) != ODO_OK) {
+        free_ctx(c);
+        return nullptr;
+    }
+    upload_extract_constants();
+    const odo_calib& k = cfg->calib;
+    c->cal = FrameCalib{k.fx, k.fy, k.cx, k.cy, k.k1, k.k2, k.p1, k.p2, k.k3, k.depth_factor, k.mbf,
+                        1.0f / k.fx, 1.0f / k.fy};
+    // ErrorFunction2 statics (ransac.cpp:352-359)
+    const double cam_angle_x = 58.0 / 180.0 * M_PI, cam_angle_y = 45.0 / 180.0 * M_PI;
+    const double rsx = 3 * tan(cam_angle_x / 640.0), rsy = 3 * tan(cam_angle_y / 480.0);
+    c->rcfg = RansacCfg{cfg->ransac.iterations, cfg->ransac.min_inlier_th, cfg->ransac.max_mahalanobis,
+                        cfg->ransac.sample_size, cfg->ransac.check_depth, rsx * rsx, rsy * rsy};
+    c->nev = 12;
+    for (int i = 0; i < c->nev; i++) hipEventCreate(&c->ev[i]);
+    return c;
+}
+
+void odo_destroy(odo_ctx* ctx) { free_ctx(ctx); }
+
+void* odo_stream(odo_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int odo_reset(odo_ctx* c) {
+    if (!c) return fail(ODO_ERR_ARG, "null ctx");
+    c->has_prev = false;
+    c->pair_counter = 0;
+    const double nan = std::nan("");
+    HIPCHK(hipMemcpyAsync(c->latch, &nan, sizeof(double), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return ODO_OK;
+}
+
+int odo_set_latch(odo_ctx* c, double cov) {
+    if (!c) return fail(ODO_ERR_ARG, "null ctx");
+    HIPCHK(hipMemcpyAsync(c->latch, &cov, sizeof(double), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return ODO_OK;
+}
+
+double odo_get_latch(odo_ctx* c) {
+    double v = std::nan("");
+    if (!c) return v;
+    hipStreamSynchronize(c->stream);
+    hipMemcpy(&v, c->latch, sizeof(double), hipMemcpyDeviceToHost);
+    return v;
+}
+
+int odo_synchronize(odo_ctx* c) {
+    if (!c) return fail(ODO_ERR_ARG, "null ctx");
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return ODO_OK;
+}
+
+static int run_extract(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, int n, int slot) {
+    hipStream_t st = c->stream;
+    const size_t P = c->pyr_size;
+    uint8_t* pyr = c->pyr + (size_t)slot * P;
+    if (d_bgr) launch_gray(st, d_bgr, pyr, c->W * c->H, (size_t)c->W * c->H * 3, P, n);
+    for (int l = 1; l < c->nlevels; l++) {
+        const LevelDesc& S = c->lv_h[l - 1];
+        const LevelDesc& D = c->lv_h[l];
+        launch_resize(st, pyr, P, S.off, S.w, D.off, D.w, D.h, c->rx + c->rx_off[l], c->ry + c->ry_off[l], n);
+    }
+    hipEventRecord(c->ev[1], st);
+    launch_fast(st, pyr, P, c->cells, c->lv, c->cand + (size_t)slot * c->ncells * c->cell_cap,
+                c->cand_cnt + (size_t)slot * c->ncells, c->ncells, c->cell_cap, c->cfg.orb.ini_th_fast,
+                c->cfg.orb.min_th_fast, n);
+    hipEventRecord(c->ev[2], st);
+    launch_octree(st, c->cand + (size_t)slot * c->ncells * c->cell_cap, c->cand_cnt + (size_t)slot * c->ncells, c->lv,
+                  c->ncells, c->cell_cap, c->nlevels, c->keys + (size_t)slot * c->keys_per_frame,
+                  c->knode + (size_t)slot * c->keys_per_frame, c->kquad + (size_t)slot * c->keys_per_frame,
+                  c->keys_per_frame, c->okp + (size_t)slot * c->nlevels * c->okp_stride,
+                  c->ocnt + (size_t)slot * c->nlevels, c->okp_stride, c->node_cap, n);
+    hipEventRecord(c->ev[3], st);
+    launch_blur(st, pyr, c->blur + (size_t)slot * P, P, c->lv, c->nlevels, c->max_blur_tiles, n);
+    hipEventRecord(c->ev[4], st);
+    launch_finalize(st, pyr, c->blur + (size_t)slot * P, P, c->lv, c->nlevels,
+                    c->okp + (size_t)slot * c->nlevels * c->okp_stride, c->ocnt + (size_t)slot * c->nlevels,
+                    c->okp_stride, d_depth, (size_t)c->W * c->H, c->W, c->cal, c->kps + (size_t)slot * c->kp_cap,
+                    c->desc + (size_t)slot * c->kp_cap * 32, c->kun + (size_t)slot * c->kp_cap * 2,
+                    c->xyz + (size_t)slot * c->kp_cap * 3, c->ur + (size_t)slot * c->kp_cap, c->nkp + slot, c->kp_cap,
+                    n);
+    hipEventRecord(c->ev[5], st);
+    HIPCHK(hipGetLastError());
+    return ODO_OK;
+}
+
+// Extraction when level 0 (the gray image) is already in the pyramid slot.
+static int run_extract_from_gray(odo_ctx* c, const uint16_t* d_depth, int n, int slot) {
+    return run_extract(c, nullptr, d_depth, n, slot);
+}
+
+int odo_extract_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, int n) {
+    if (!c || !d_bgr || !d_depth || n <= 0 || n > c->maxb) return fail(ODO_ERR_ARG, "bad extract args");
+    hipEventRecord(c->ev[0], c->stream);
+    int e = run_extract(c, d_bgr, d_depth, n, 1);
+    c->last_n = n;
+    return e;
+}
+
+static int run_pairs(odo_ctx* c, int n) {
+    hipStream_t st = c->stream;
+    // pair p: F1 = slot p, F2 = slot p+1; pair 0 valid only with a previous frame
+    c->valid_h.assign(n, 1);
+    c->valid_h[0] = c->has_prev ? 1 : 0;
+    HIPCHK(hipMemcpyAsync(c->pair_valid, c->valid_h.data(), n * sizeof(int), hipMemcpyHostToDevice, st));
+    const size_t KC = (size_t)c->kp_cap;
+    launch_knn2(st, c->desc, c->nkp, KC * 32, c->desc + KC * 32, c->nkp + 1, KC * 32, c->knn_idx, c->knn_dist, KC,
+                c->kp_cap, n);
+    hipEventRecord(c->ev[6], st);
+    const float mThDepth = c->cfg.calib.mbf * c->cfg.calib.th_depth / c->cfg.calib.fx;
+    launch_pair_match(st, c->knn_idx, c->knn_dist, KC, c->xyz, c->nkp, c->kp_cap, 0, c->cfg.nn_ratio, mThDepth,
+                      c->cfg.ransac.check_depth, c->matches, c->n_matches, c->good, c->n_good, c->f2_src,
+                      c->sort_scratch, c->match_cap, n);
+    launch_latch(st, c->latch, c->good, c->n_good, c->n_matches, c->matches, c->xyz, c->kp_cap, 0, n, c->match_cap,
+                 c->cfg.ransac.min_inlier_th, c->cfg.ransac.sample_size, c->cfg.ransac.iterations, c->pair_valid);
+    hipEventRecord(c->ev[7], st);
+    launch_ransac(st, c->good, c->n_good, c->n_matches, c->matches, c->xyz, c->kp_cap, 0, c->match_cap, c->rcfg,
+                  c->latch, (uint64_t)c->cfg.seed, c->pair_counter, c->pair_valid, 20, nullptr, c->gpts, c->masks,
+                  c->best_mask, c->mask_words, c->res, c->T12, n);
+    hipEventRecord(c->ev[8], st);
+    launch_pnp(st, c->f2_src, c->xyz, c->kun, c->ur, c->nkp, c->kp_cap, 0, c->cal, c->T12, c->pair_valid,
+               c->n_matches, 20, c->edges, c->res, c->pnp_mask, n);
+    hipEventRecord(c->ev[9], st);
+    HIPCHK(hipGetLastError());
+    return ODO_OK;
+}
+
+static int finish_batch(odo_ctx* c, int n, odo_pair_result* h_results) {
+    hipStream_t st = c->stream;
+    // n_matches/n_good into the result records
+    if (h_results) {
+        HIPCHK(hipMemcpyAsync(h_results, c->res, n * sizeof(odo_pair_result), hipMemcpyDeviceToHost, st));
+        std::vector<int> nm(n);
+        HIPCHK(hipMemcpyAsync(nm.data(), c->n_matches, n * sizeof(int), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        for (int i = 0; i < n; i++) {
+            h_results[i].n_matches = c->valid_h[i] ? nm[i] : 0;
+        }
+    }
+    return ODO_OK;
+}
+
+// Copy slot n's features to slot 0 (it becomes the previous frame).
+static int roll_slots(odo_ctx* c, int n) {
+    hipStream_t st = c->stream;
+    const size_t KC = (size_t)c->kp_cap;
+    HIPCHK(hipMemcpyAsync(c->kps, c->kps + n * KC, KC * sizeof(orb_kp), hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemcpyAsync(c->desc, c->desc + n * KC * 32, KC * 32, hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemcpyAsync(c->kun, c->kun + n * KC * 2, KC * 2 * sizeof(float), hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemcpyAsync(c->xyz, c->xyz + n * KC * 3, KC * 3 * sizeof(float), hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemcpyAsync(c->ur, c->ur + n * KC, KC * sizeof(float), hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemcpyAsync(c->nkp, c->nkp + n, sizeof(int), hipMemcpyDeviceToDevice, st));
+    return ODO_OK;
+}
+
+int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, int n, odo_pair_result* h_results) {
+    if (!c || !d_bgr || !d_depth || n <= 0 || n > c->maxb) return fail(ODO_ERR_ARG, "bad track args");
+    int e;
+    hipEventRecord(c->ev[0], c->stream);
+    if ((e = run_extract(c, d_bgr, d_depth, n, 1))) return e;
+    if ((e = run_pairs(c, n))) return e;
+    c->last_n = n;
+    if ((e = finish_batch(c, n, h_results))) return e;
+    if ((e = roll_slots(c, n))) return e;
+    c->has_prev = true;
+    c->pair_counter += (uint64_t)n;
+    if (h_results) HIPCHK(hipStreamSynchronize(c->stream));
+    return ODO_OK;
+}
+
+int odo_track_batch_host(odo_ctx* c, const uint8_t* bgr, const uint16_t* depth, int n, odo_pair_result* h_results) {
+    if (!c || !bgr || !depth || n <= 0 || n > c->maxb) return fail(ODO_ERR_ARG, "bad track args");
+    HIPCHK(hipMemcpyAsync(c->bgr_in, bgr, (size_t)n * c->W * c->H * 3, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->depth_in, depth, (size_t)n * c->W * c->H * 2, hipMemcpyHostToDevice, c->stream));
+    return odo_track_batch(c, c->bgr_in, c->depth_in, n, h_results);
+}
+
+int odo_get_frame(odo_ctx* c, int i, orb_kp* kps, uint8_t* desc, float* kps_un, float* xyz, float* u_right, int cap,
+                  int* n) {
+    if (!c || i < 0 || i >= c->last_n) return fail(ODO_ERR_ARG, "bad frame index");
+    HIPCHK(hipStreamSynchronize(c->stream));
+    // after a track_batch the slots were rolled: slot i+1 still holds frame i
+    const int slot = i + 1;
+    int cnt = 0;
+    HIPCHK(hipMemcpy(&cnt, c->nkp + slot, sizeof(int), hipMemcpyDeviceToHost));
+    *n = cnt;
+    const int m = std::min(cnt, cap);
+    const size_t KC = (size_t)c->kp_cap;
+    if (kps) HIPCHK(hipMemcpy(kps, c->kps + slot * KC, m * sizeof(orb_kp), hipMemcpyDeviceToHost));
+    if (desc) HIPCHK(hipMemcpy(desc, c->desc + slot * KC * 32, (size_t)m * 32, hipMemcpyDeviceToHost));
+    if (kps_un) HIPCHK(hipMemcpy(kps_un, c->kun + slot * KC * 2, (size_t)m * 8, hipMemcpyDeviceToHost));
+    if (xyz) HIPCHK(hipMemcpy(xyz, c->xyz + slot * KC * 3, (size_t)m * 12, hipMemcpyDeviceToHost));
+    if (u_right) HIPCHK(hipMemcpy(u_right, c->ur + slot * KC, (size_t)m * 4, hipMemcpyDeviceToHost));
+    return cnt > cap ? fail(ODO_ERR_CAPACITY, "cap too small") : ODO_OK;
+}
+
+int odo_get_pair(odo_ctx* c, int i, odo_dmatch* matches, int match_cap, int* n_matches, odo_dmatch* good_sorted,
+                 int* n_good, uint8_t* ransac_inliers, uint8_t* pnp_inliers, int32_t* f2_src) {
+    if (!c || i < 0 || i >= c->last_n) return fail(ODO_ERR_ARG, "bad pair index");
+    HIPCHK(hipStreamSynchronize(c->stream));
+    int nm = 0, ng = 0, n2 = 0;
+    HIPCHK(hipMemcpy(&nm, c->n_matches + i, sizeof(int), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&ng, c->n_good + i, sizeof(int), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&n2, c->nkp + i + 1, sizeof(int), hipMemcpyDeviceToHost));
+    if (n_matches) *n_matches = nm;
+    if (n_good) *n_good = ng;
+    std::vector<odo_dmatch> M(std::max(nm, 1));
+    HIPCHK(hipMemcpy(M.data(), c->matches + (size_t)i * c->match_cap, nm * sizeof(odo_dmatch), hipMemcpyDeviceToHost));
+    if (matches) memcpy(matches, M.data(), std::min(nm, match_cap) * sizeof(odo_dmatch));
+    if (good_sorted || ransac_inliers) {
+        std::vector<uint64_t> G(std::max(ng, 1));
+        HIPCHK(hipMemcpy(G.data(), (uint64_t*)c->good + (size_t)i * c->match_cap, ng * sizeof(uint64_t),
+                         hipMemcpyDeviceToHost));
+        if (good_sorted)
+            for (int k = 0; k < ng && k < match_cap; k++) good_sorted[k] = M[(uint32_t)(G[k] >> 32)];
+        if (ransac_inliers) {
+            std::vector<uint32_t> bm(c->mask_words);
+            HIPCHK(hipMemcpy(bm.data(), c->best_mask + (size_t)i * c->mask_words, c->mask_words * 4,
+                             hipMemcpyDeviceToHost));
+            for (int k = 0; k < ng && k < match_cap; k++) ransac_inliers[k] = (bm[k >> 5] >> (k & 31)) & 1;
+        }
+    }
+    if (pnp_inliers) HIPCHK(hipMemcpy(pnp_inliers, c->pnp_mask + (size_t)i * c->kp_cap, n2, hipMemcpyDeviceToHost));
+    if (f2_src) HIPCHK(hipMemcpy(f2_src, c->f2_src + (size_t)i * c->kp_cap, n2 * sizeof(int32_t), hipMemcpyDeviceToHost));
+    return ODO_OK;
+}
+
+int odo_debug_pyramid(odo_ctx* c, int i, uint8_t* out, size_t cap) {
+    if (!c || i < 0 || i >= c->last_n || cap < c->pyr_size) return fail(ODO_ERR_ARG, "bad args");
+    HIPCHK(hipStreamSynchronize(c->stream));
+    // compact levels back to back (device layout pads levels to 16 bytes)
+    std::vector<uint8_t> buf(c->pyr_size);
+    HIPCHK(hipMemcpy(buf.data(), c->pyr + (size_t)(i + 1) * c->pyr_size, c->pyr_size, hipMemcpyDeviceToHost));
+    size_t o = 0;
+    for (auto& L : c->lv_h) {
+        memcpy(out + o, buf.data() + L.off, (size_t)L.w * L.h);
+        o += (size_t)L.w * L.h;
+    }
+    return (int)o;
+}
+
+int odo_debug_blur(odo_ctx* c, int i, uint8_t* out, size_t cap) {
+    if (!c || i < 0 || i >= c->last_n || cap < c->pyr_size) return fail(ODO_ERR_ARG, "bad args");
+    HIPCHK(hipStreamSynchronize(c->stream));
+    std::vector<uint8_t> buf(c->pyr_size);
+    HIPCHK(hipMemcpy(buf.data(), c->blur + (size_t)(i + 1) * c->pyr_size, c->pyr_size, hipMemcpyDeviceToHost));
+    size_t o = 0;
+    for (auto& L : c->lv_h) {
+        memcpy(out + o, buf.data() + L.off, (size_t)L.w * L.h);
+        o += (size_t)L.w * L.h;
+    }
+    return (int)o;
+}
+
+static orb_kp unpack_key(uint32_t k) {
+    orb_kp r;
+    r.x = (float)(k & 0xfff);
+    r.y = (float)((k >> 12) & 0xfff);
+    r.size = 7.f;
+    r.angle = -1.f;
+    r.response = (float)(k >> 24);
+    r.octave = 0;
+    r.class_id = -1;
+    return r;
+}
+
+int odo_debug_fast(odo_ctx* c, int i, int level, orb_kp* out, int cap, int* n) {
+    if (!c || i < 0 || i >= c->last_n || level < 0 || level >= c->nlevels) return fail(ODO_ERR_ARG, "bad args");
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const int slot = i + 1;
+    const LevelDesc& L = c->lv_h[level];
+    const int nc = L.cell_end - L.cell_begin;
+    std::vector<int> cnt(nc);
+    std::vector<uint32_t> cand((size_t)nc * c->cell_cap);
+    HIPCHK(hipMemcpy(cnt.data(), c->cand_cnt + (size_t)slot * c->ncells + L.cell_begin, nc * sizeof(int),
+                     hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(cand.data(), c->cand + ((size_t)slot * c->ncells + L.cell_begin) * c->cell_cap,
+                     cand.size() * 4, hipMemcpyDeviceToHost));
+    int m = 0;
+    for (int ci = 0; ci < nc; ci++)
+        for (int k = 0; k < cnt[ci]; k++) {
+            if (m < cap) out[m] = unpack_key(cand[(size_t)ci * c->cell_cap + k]);
+            m++;
+        }
+    *n = m;
+    return ODO_OK;
+}
+
+int odo_debug_octree(odo_ctx* c, int i, int level, orb_kp* out, int cap, int* n) {
+    if (!c || i < 0 || i >= c->last_n || level < 0 || level >= c->nlevels) return fail(ODO_ERR_ARG, "bad args");
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const int slot = i + 1;
+    int cnt = 0;
+    HIPCHK(hipMemcpy(&cnt, c->ocnt + (size_t)slot * c->nlevels + level, sizeof(int), hipMemcpyDeviceToHost));
+    std::vector<uint32_t> k(std::max(cnt, 1));
+    HIPCHK(hipMemcpy(k.data(), c->okp + ((size_t)slot * c->nlevels + level) * c->okp_stride, cnt * 4,
+                     hipMemcpyDeviceToHost));
+    for (int j = 0; j < cnt && j < cap; j++) out[j] = unpack_key(k[j]);
+    *n = cnt;
+    return ODO_OK;
+}
+
+int odo_last_timings(odo_ctx* c, float* ms, int cap, const char** names) {
+    static const char* kNames[] = {"gray+pyramid", "fast", "octree", "blur", "finalize", "knn2", "match+sort",
+                                   "ransac", "pnp"};
+    if (!c) return fail(ODO_ERR_ARG, "null ctx");
+    HIPCHK(hipStreamSynchronize(c->stream));
+    int m = 0;
+    for (int i = 0; i < 9 && i < cap; i++) {
+        float t = 0;
+        if (hipEventElapsedTime(&t, c->ev[i], c->ev[i + 1]) != hipSuccess) t = -1;
+        ms[i] = t;
+        if (names) names[i] = kNames[i];
+        m++;
+    }
+    return m;
+}
+
+void odo_rng_seed(odo_rng* r, uint32_t seed) {
+    // glibc __srandom_r (TYPE_3): Schrage LCG fill, fptr=3, rptr=0, 310 discards
+    if (seed == 0) seed = 1;
+    r->state[0] = (int32_t)seed;
+    int32_t word = (int32_t)seed;
+    for (int i = 1; i < 31; ++i) {
+        long hi = word / 127773, lo = word % 127773;
+        long w2 = 16807 * lo - 2836 * hi;
+        if (w2 < 0) w2 += 2147483647;
+        word = (int32_t)w2;
+        r->state[i] = word;
+    }
+    r->fpos = 3;
+    r->rpos = 0;
+    for (int k = 0; k < 310; k++) odo_rng_next(r);
+}
+
+int32_t odo_rng_next(odo_rng* r) {
+    uint32_t val = (uint32_t)r->state[r->fpos] + (uint32_t)r->state[r->rpos];
+    r->state[r->fpos] = (int32_t)val;
+    int32_t out = (int32_t)(val >> 1);
+    if (++r->fpos >= 31) {
+        r->fpos = 0;
+        ++r->rpos;
+    } else if (++r->rpos >= 31) r->rpos = 0;
+    return out;
+}
+
+}  // extern "C"
+
+// ====================================================================== per-stage entry points
+namespace {
+struct DevBuf {
+    void* p = nullptr;
+    explicit DevBuf(size_t bytes) { hipMalloc(&p, bytes ? bytes : 1); }
+    ~DevBuf() {
+        if (p) hipFree(p);
+    }
+    template <typename T>
+    T* as() {
+        return (T*)p;
+    }
+};
+}  // namespace
+
+extern "C" {
+
+int odo_extract(odo_ctx* c, const uint8_t* img, int channels, const uint16_t* depth, orb_kp* kps, uint8_t* desc,
+                float* kps_un, float* xyz, float* u_right, int cap, int* n) {
+    if (!c || !img || (channels != 1 && channels != 3) || !n) return fail(ODO_ERR_ARG, "bad extract args");
+    hipStream_t st = c->stream;
+    const size_t npix = (size_t)c->W * c->H;
+    const int slot = 1;
+    if (depth) HIPCHK(hipMemcpyAsync(c->depth_in, depth, npix * 2, hipMemcpyHostToDevice, st));
+    else HIPCHK(hipMemsetAsync(c->depth_in, 0, npix * 2, st));
+    if (channels == 3) {
+        HIPCHK(hipMemcpyAsync(c->bgr_in, img, npix * 3, hipMemcpyHostToDevice, st));
+        hipEventRecord(c->ev[0], st);
+        int e = run_extract(c, c->bgr_in, c->depth_in, 1, slot);
+        if (e) return e;
+    } else {
+        // ORBextractor::operator() on a gray image: level 0 = the image itself
+        HIPCHK(hipMemcpyAsync(c->pyr + (size_t)slot * c->pyr_size, img, npix, hipMemcpyHostToDevice, st));
+        hipEventRecord(c->ev[0], st);
+        int e = run_extract_from_gray(c, c->depth_in, 1, slot);
+        if (e) return e;
+    }
+    c->last_n = std::max(c->last_n, 1);
+    return odo_get_frame(c, 0, kps, desc, kps_un, xyz, u_right, cap, n);
+}
+
+int odo_knn2_hamming(odo_ctx* c, const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* idx, int32_t* dist) {
+    if (!c || nq < 0 || nt < 0 || (nq && !q) || (nt && !t) || !idx || !dist) return fail(ODO_ERR_ARG, "bad knn args");
+    if (nq == 0) return ODO_OK;
+    if (nq > (1 << 20) || nt > (1 << 20)) return fail(ODO_ERR_CAPACITY, "knn2: at most 2^20 descriptors");
+    hipStream_t st = c->stream;
+    DevBuf dq((size_t)nq * 32), dt((size_t)std::max(nt, 1) * 32), dn(2 * sizeof(int));
+    DevBuf di((size_t)nq * sizeof(int2)), dd((size_t)nq * sizeof(int2));
+    const int cnt[2] = {nq, nt};
+    HIPCHK(hipMemcpyAsync(dq.p, q, (size_t)nq * 32, hipMemcpyHostToDevice, st));
+    if (nt) HIPCHK(hipMemcpyAsync(dt.p, t, (size_t)nt * 32, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(dn.p, cnt, sizeof(cnt), hipMemcpyHostToDevice, st));
+    launch_knn2(st, dq.as<uint8_t>(), dn.as<int>(), 0, dt.as<uint8_t>(), dn.as<int>() + 1, 0, di.as<int2>(),
+                dd.as<int2>(), 0, nq, 1);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(idx, di.p, (size_t)nq * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(dist, dd.p, (size_t)nq * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return ODO_OK;
+}
+
+int odo_ransac(odo_ctx* c, const odo_dmatch* m12, int n12, const float* xyz1, int n1, const float* xyz2, int n2,
+               const odo_ransac_params* p, odo_rng* rng, double* latch, float T12[16], float* rmse,
+               odo_dmatch* inliers, int* n_inliers, int* ok) {
+    if (!c || !p || !rng || !latch || !T12 || !rmse || !n_inliers || !ok || n12 < 0 || (n12 && !m12))
+        return fail(ODO_ERR_ARG, "bad ransac args");
+    // Iterate() resets its outputs first (ransac.cpp:157-159)
+    for (int i = 0; i < 16; i++) T12[i] = (i % 5 == 0) ? 1.f : 0.f;
+    *rmse = 1e6f;
+    *n_inliers = 0;
+    *ok = 0;
+    if (n12 < p->min_inlier_th) return ODO_OK;
+    // depth filter (ransac.cpp:175-189) and std::sort by distance (ransac.cpp:199)
+    std::vector<odo_dmatch> good;
+    good.reserve(n12);
+    for (int i = 0; i < n12; i++) {
+        const odo_dmatch& m = m12[i];
+        if (m.queryIdx < 0 || m.queryIdx >= n1 || m.trainIdx < 0 || m.trainIdx >= n2)
+            return fail(ODO_ERR_ARG, "match index out of range");
+        const float zs = xyz1[3 * m.queryIdx + 2], zt = xyz2[3 * m.trainIdx + 2];
+        if (p->check_depth) {
+            if (std::isnan(zs) || std::isnan(zt)) continue;
+            if (zs <= 0 || zt <= 0) continue;
+        }
+        good.push_back(m);
+    }
+    if ((int)good.size() < p->min_inlier_th) return ODO_OK;
+    std::sort(good.begin(), good.end(), [](const odo_dmatch& a, const odo_dmatch& b) { return a.distance < b.distance; });
+    const int ng = (int)good.size();
+    if (ng > c->match_cap * 64) return fail(ODO_ERR_CAPACITY, "too many matches");
+    // DepthCovariance first-call latch (ransac.cpp:416-421)
+    if (std::isnan(*latch)) {
+        for (const odo_dmatch& m : good) {
+            const float* o = &xyz1[3 * m.queryIdx];
+            const float* tg = &xyz2[3 * m.trainIdx];
+            if (o[2] == 0.0f || tg[0] == 0.0f) continue;
+            if (std::isnan(o[2]) || std::isnan(tg[2])) continue;
+            const double z = (double)o[2];
+            const double sd = 0.01 * z * z;
+            *latch = sd * sd;
+            break;
+        }
+    }
+    hipStream_t st = c->stream;
+    const int kc = std::max(std::max(n1, n2), 1);
+    const int words = (ng + 31) / 32;
+    DevBuf dxyz((size_t)2 * kc * 3 * sizeof(float)), dm((size_t)ng * sizeof(odo_dmatch)), dg((size_t)ng * 8);
+    DevBuf dint(4 * sizeof(int)), dlatch(sizeof(double)), drng(sizeof(odo_rng)), dres(sizeof(odo_pair_result));
+    DevBuf dT(16 * sizeof(float)), dgp((size_t)ng * ransac_gpt_bytes()), dmask((size_t)2 * words * 256 * 4),
+        dbm((size_t)words * 4);
+    std::vector<uint64_t> gl(ng);
+    for (int k = 0; k < ng; k++) {
+        uint32_t bits;
+        memcpy(&bits, &good[k].distance, 4);
+        gl[k] = ((uint64_t)(uint32_t)k << 32) | bits;
+    }
+    const int ints[4] = {ng, ng, 1, 0};  // n_good, n_matches, pair_valid
+    HIPCHK(hipMemcpyAsync(dxyz.p, xyz1, (size_t)n1 * 12, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(dxyz.as<float>() + (size_t)kc * 3, xyz2, (size_t)n2 * 12, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(dm.p, good.data(), (size_t)ng * sizeof(odo_dmatch), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(dg.p, gl.data(), (size_t)ng * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(dint.p, ints, sizeof(ints), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(dlatch.p, latch, sizeof(double), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(drng.p, rng, sizeof(odo_rng), hipMemcpyHostToDevice, st));
+    const double cam_angle_x = 58.0 / 180.0 * M_PI, cam_angle_y = 45.0 / 180.0 * M_PI;
+    const double rsx = 3 * tan(cam_angle_x / 640.0), rsy = 3 * tan(cam_angle_y / 480.0);
+    RansacCfg cfg{p->iterations, p->min_inlier_th, p->max_mahalanobis, p->sample_size, p->check_depth, rsx * rsx,
+                  rsy * rsy};
+    launch_ransac(st, dg.p, dint.as<int>(), dint.as<int>() + 1, dm.as<odo_dmatch>(), dxyz.as<float>(), kc, 0, ng, cfg,
+                  dlatch.as<double>(), 0, 0, dint.as<int>() + 2, 0, drng.as<odo_rng>(), dgp.p, dmask.as<uint32_t>(),
+                  dbm.as<uint32_t>(), words, dres.as<odo_pair_result>(), dT.as<float>(), 1);
+    HIPCHK(hipGetLastError());
+    odo_pair_result r;
+    std::vector<uint32_t> bm(words);
+    HIPCHK(hipMemcpyAsync(&r, dres.p, sizeof(r), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(bm.data(), dbm.p, (size_t)words * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(rng, drng.p, sizeof(odo_rng), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    memcpy(T12, r.T12, sizeof(r.T12));
+    *rmse = r.rmse;
+    int k2 = 0;
+    for (int k = 0; k < ng; k++)
+        if ((bm[k >> 5] >> (k & 31)) & 1) {
+            if (inliers) inliers[k2] = good[k];
+            k2++;
+        }
+    *n_inliers = k2;
+    *ok = r.ransac_ok;
+    return ODO_OK;
+}
+
+int odo_pnp_motion_ba(odo_ctx* c, const float* Xw, const float* obs, int n, const odo_calib* calib,
+                      const float Tcw_init[16], float Tcw_out[16], uint8_t* outlier, int* n_inliers) {
+    if (!c || n < 0 || (n && (!Xw || !obs)) || !Tcw_init || !Tcw_out || !n_inliers) return fail(ODO_ERR_ARG, "bad pnp args");
+    hipStream_t st = c->stream;
+    const int kc = std::max(n, 1);
+    DevBuf dx((size_t)kc * 12), dkun((size_t)2 * kc * 8), dur((size_t)2 * kc * 4), dsrc((size_t)kc * 4);
+    DevBuf dint(4 * sizeof(int)), dT(16 * 4), dres(sizeof(odo_pair_result)), dedges((size_t)kc * pnp_edge_bytes()),
+        dmask((size_t)kc);
+    std::vector<float> kun(2 * kc), ur(kc);
+    std::vector<int32_t> src(kc);
+    for (int i = 0; i < n; i++) {
+        kun[2 * i] = obs[3 * i];
+        kun[2 * i + 1] = obs[3 * i + 1];
+        ur[i] = obs[3 * i + 2];
+        src[i] = i;
+    }
+    const int ints[4] = {0, n, 1, 1 << 30};  // nkp[slot0], nkp[slot1], pair_valid, n_matches
+    if (n) {
+        HIPCHK(hipMemcpyAsync(dx.p, Xw, (size_t)n * 12, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(dkun.as<float>() + 2 * kc, kun.data(), (size_t)n * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(dur.as<float>() + kc, ur.data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(dsrc.p, src.data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
+    }
+    HIPCHK(hipMemcpyAsync(dint.p, ints, sizeof(ints), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(dT.p, Tcw_init, 64, hipMemcpyHostToDevice, st));
+    const odo_calib& k = calib ? *calib : c->cfg.calib;
+    FrameCalib cal{k.fx, k.fy, k.cx, k.cy, k.k1, k.k2, k.p1, k.p2, k.k3, k.depth_factor, k.mbf, 1.0f / k.fx, 1.0f / k.fy};
+    launch_pnp(st, dsrc.as<int32_t>(), dx.as<float>(), dkun.as<float>(), dur.as<float>(), dint.as<int>(), kc, 0, cal,
+               dT.as<float>(), dint.as<int>() + 2, dint.as<int>() + 3, 0, dedges.p, dres.as<odo_pair_result>(),
+               dmask.as<uint8_t>(), 1);
+    HIPCHK(hipGetLastError());
+    odo_pair_result r;
+    std::vector<uint8_t> mask(kc);
+    HIPCHK(hipMemcpyAsync(&r, dres.p, sizeof(r), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(mask.data(), dmask.p, kc, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    memcpy(Tcw_out, r.Tcw, 64);
+    *n_inliers = r.pnp_inliers;
+    if (outlier)
+        for (int i = 0; i < n; i++) outlier[i] = mask[i] ? 0 : 1;
+    return ODO_OK;
+}
+
+int odo_kabsch(const float* A, const float* B, int n, float T[16]) {
+    if (n < 0 || (n && (!A || !B)) || !T) return fail(ODO_ERR_ARG, "bad kabsch args");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(ODO_ERR_DEVICE, "no HIP device");
+    const int kc = std::max(n, 1);
+    DevBuf da((size_t)kc * 12), db((size_t)kc * 12), dT(64);
+    if (n) {
+        HIPCHK(hipMemcpy(da.p, A, (size_t)n * 12, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(db.p, B, (size_t)n * 12, hipMemcpyHostToDevice));
+    }
+    launch_kabsch(0, da.as<float>(), db.as<float>(), n, dT.as<float>());
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpy(T, dT.p, 64, hipMemcpyDeviceToHost));
+    return ODO_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,375 @@
+// Device-side scalar math for the MI355X odometry kernels (gfx950).
+//
+// Every routine here restates a third-party or reference computation with a
+// FIXED operation order so that float/double
+// results are bit-identical to the CPU oracle; the library is compiled with
+// -ffp-contract=off so no FMA contraction reorders rounding.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define ODO_INLINE __device__ __forceinline__
+
+namespace odo {
+
+// ----------------------------------------------------------------- rounding
+ODO_INLINE int cv_round(float v) { return __float2int_rn(v); }  // cvRound: half to even
+ODO_INLINE int cv_floor(float v) { int i = (int)v; return i - (i > v); }
+
+// --------------------------------------------------------- fastAtan2 (A.5)
+ODO_INLINE float fast_atan2(float y, float x) {
+    const float k = (float)(180.0 / 3.14159265358979323846);
+    const float p1 = 0.9997878412794807f * k;
+    const float p3 = -0.3258083974640975f * k;
+    const float p5 = 0.1555786518463281f * k;
+    const float p7 = -0.04432655554792128f * k;
+    const float eps = (float)2.220446049250313080847e-16;
+    float ax = fabsf(x), ay = fabsf(y);
+    float a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + eps);
+        c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = ax / (ay + eps);
+        c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+// ---------------------------------------------- Eigen JacobiSVD<3x3f> (A.8)
+struct Rot {
+    float c, s;
+};
+
+ODO_INLINE float sum3f(float a, float b, float c) { return a + (b + c); }
+ODO_INLINE double sum3d(double a, double b, double c) { return a + (b + c); }
+
+ODO_INLINE void rot_rows(float W[3][3], int p, int q, Rot j) {
+    if (j.c == 1.f && j.s == 0.f) return;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        float xi = W[p][i], yi = W[q][i];
+        W[p][i] = j.c * xi + j.s * yi;
+        W[q][i] = -j.s * xi + j.c * yi;
+    }
+}
+ODO_INLINE void rot_cols(float W[3][3], int p, int q, Rot j) {
+    Rot t{j.c, -j.s};
+    if (t.c == 1.f && t.s == 0.f) return;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        float xi = W[i][p], yi = W[i][q];
+        W[i][p] = t.c * xi + t.s * yi;
+        W[i][q] = -t.s * xi + t.c * yi;
+    }
+}
+ODO_INLINE Rot make_jacobi(float x, float y, float z) {
+    float deno = 2.f * fabsf(y);
+    if (deno < 1.17549435082228750797e-38f) return Rot{1.f, 0.f};
+    float tau = (x - z) / deno;
+    float w = sqrtf(tau * tau + 1.f);
+    float t = tau > 0.f ? 1.f / (tau + w) : 1.f / (tau - w);
+    float sign_t = t > 0.f ? 1.f : -1.f;
+    float n = 1.f / sqrtf(t * t + 1.f);
+    Rot r;
+    r.s = ((-sign_t) * (y / fabsf(y))) * fabsf(t) * n;
+    r.c = n;
+    return r;
+}
+ODO_INLINE void real_2x2_jacobi_svd(const float W[3][3], int p, int q, Rot* jl, Rot* jr) {
+    float m00 = W[p][p], m01 = W[p][q], m10 = W[q][p], m11 = W[q][q];
+    Rot rot1;
+    float t = m00 + m11;
+    float d = m10 - m01;
+    if (fabsf(d) < 1.17549435082228750797e-38f) {
+        rot1.s = 0.f;
+        rot1.c = 1.f;
+    } else {
+        float u = t / d;
+        float tmp = sqrtf(1.f + u * u);
+        rot1.s = 1.f / tmp;
+        rot1.c = u / tmp;
+    }
+    if (!(rot1.c == 1.f && rot1.s == 0.f)) {
+        float x0 = m00, y0 = m10;
+        m00 = rot1.c * x0 + rot1.s * y0;
+        m10 = -rot1.s * x0 + rot1.c * y0;
+        float x1 = m01, y1 = m11;
+        m01 = rot1.c * x1 + rot1.s * y1;
+        m11 = -rot1.s * x1 + rot1.c * y1;
+    }
+    *jr = make_jacobi(m00, m01, m11);
+    float c2 = jr->c, s2 = -jr->s;
+    jl->c = rot1.c * c2 - rot1.s * s2;
+    jl->s = rot1.c * s2 + rot1.s * c2;
+}
+
+ODO_INLINE void svd3(const float A[3][3], float U[3][3], float S[3], float V[3][3]) {
+    const float precision = 2.f * 1.1920928955078125e-07f;
+    const float considerAsZero = 1.17549435082228750797e-38f;
+    float scale = 0.f;
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) scale = fmaxf(scale, fabsf(A[i][j]));
+    if (scale == 0.f) scale = 1.f;
+    float W[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            W[i][j] = A[i][j] / scale;
+            U[i][j] = (i == j) ? 1.f : 0.f;
+            V[i][j] = (i == j) ? 1.f : 0.f;
+        }
+    float maxDiag = fmaxf(fabsf(W[0][0]), fmaxf(fabsf(W[1][1]), fabsf(W[2][2])));
+    bool finished = false;
+    int sweeps = 0;
+    while (!finished && sweeps < 100) {
+        finished = true;
+        sweeps++;
+        for (int p = 1; p < 3; ++p)
+            for (int q = 0; q < p; ++q) {
+                float threshold = fmaxf(considerAsZero, precision * maxDiag);
+                if (fabsf(W[p][q]) > threshold || fabsf(W[q][p]) > threshold) {
+                    finished = false;
+                    Rot jl, jr;
+                    real_2x2_jacobi_svd(W, p, q, &jl, &jr);
+                    rot_rows(W, p, q, jl);
+                    rot_cols(U, p, q, Rot{jl.c, -jl.s});
+                    rot_cols(W, p, q, jr);
+                    rot_cols(V, p, q, jr);
+                    maxDiag = fmaxf(maxDiag, fmaxf(fabsf(W[p][p]), fabsf(W[q][q])));
+                }
+            }
+    }
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        float a = W[i][i];
+        S[i] = fabsf(a);
+        if (a < 0.f)
+#pragma unroll
+            for (int r = 0; r < 3; r++) U[r][i] = -U[r][i];
+    }
+#pragma unroll
+    for (int i = 0; i < 3; i++) S[i] *= scale;
+    for (int i = 0; i < 3; i++) {
+        int pos = i;
+        float mx = S[i];
+        for (int k = i + 1; k < 3; k++)
+            if (S[k] > mx) {
+                mx = S[k];
+                pos = k;
+            }
+        if (mx == 0.f) break;
+        if (pos != i) {
+            float t = S[i];
+            S[i] = S[pos];
+            S[pos] = t;
+            for (int r = 0; r < 3; r++) {
+                float a = U[r][i];
+                U[r][i] = U[r][pos];
+                U[r][pos] = a;
+                float b = V[r][i];
+                V[r][i] = V[r][pos];
+                V[r][pos] = b;
+            }
+        }
+    }
+}
+
+ODO_INLINE float det3(const float M[3][3]) {
+    float h012 = M[0][0] * (M[1][1] * M[2][2] - M[1][2] * M[2][1]);
+    float h102 = M[0][1] * (M[1][0] * M[2][2] - M[1][2] * M[2][0]);
+    float h201 = M[0][2] * (M[1][0] * M[2][1] - M[1][1] * M[2][0]);
+    return h012 - h102 + h201;
+}
+
+// ------------------------------------------------ PCL TFC (A.7) accumulator
+struct TFC {
+    float accW;
+    float m1[3], m2[3];
+    float cov[3][3];
+    ODO_INLINE void reset() {
+        accW = 0.f;
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            m1[i] = m2[i] = 0.f;
+#pragma unroll
+            for (int j = 0; j < 3; j++) cov[i][j] = 0.f;
+        }
+    }
+    ODO_INLINE void add(float px, float py, float pz, float qx, float qy, float qz, float w) {
+        if (w == 0.0f) return;
+        accW += w;
+        float alpha = w / accW;
+        float d1[3] = {px - m1[0], py - m1[1], pz - m1[2]};
+        float d2[3] = {qx - m2[0], qy - m2[1], qz - m2[2]};
+        const float oma = 1.0f - alpha;
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            const float ad2 = alpha * d2[i];
+#pragma unroll
+            for (int j = 0; j < 3; j++) cov[i][j] = oma * (cov[i][j] + ad2 * d1[j]);
+        }
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            m1[i] += alpha * d1[i];
+            m2[i] += alpha * d2[i];
+        }
+    }
+    // getTransformation(): row-major 3x4 [R|t]
+    ODO_INLINE void get(float T[12]) const {
+        float U[3][3], S[3], V[3][3];
+        svd3(cov, U, S, V);
+        float s22 = (det3(U) * det3(V) < 0.0f) ? -1.0f : 1.0f;
+        float US[3][3];
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            // (U*S)(i,j) = U(i,0)S(0,j) + (U(i,1)S(1,j) + U(i,2)S(2,j)), S diagonal
+            US[i][0] = sum3f(U[i][0] * 1.f, U[i][1] * 0.f, U[i][2] * 0.f);
+            US[i][1] = sum3f(U[i][0] * 0.f, U[i][1] * 1.f, U[i][2] * 0.f);
+            US[i][2] = sum3f(U[i][0] * 0.f, U[i][1] * 0.f, U[i][2] * s22);
+        }
+        float R[3][3];
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+            for (int j = 0; j < 3; j++) R[i][j] = sum3f(US[i][0] * V[j][0], US[i][1] * V[j][1], US[i][2] * V[j][2]);
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            float t = m2[i] - sum3f(R[i][0] * m1[0], R[i][1] * m1[1], R[i][2] * m1[2]);
+            T[i * 4 + 0] = R[i][0];
+            T[i * 4 + 1] = R[i][1];
+            T[i * 4 + 2] = R[i][2];
+            T[i * 4 + 3] = t;
+        }
+    }
+};
+
+// ---------------------------------- Ransac::ErrorFunction2 (ransac.cpp:350)
+// Returns DBL_MAX for rejected points (shortcut / NaN / non-PD), like the reference.
+struct MahalConst {
+    double raster_cov_x, raster_cov_y;
+    double depth_cov;  // latched DepthCovariance value
+};
+
+#define ODO_DBL_MAX 1.7976931348623157e308
+
+ODO_INLINE double error_function2(const float x1[3], const float x2[3], const double T[12], const MahalConst& K) {
+    if (__builtin_isnan(x1[2]) || __builtin_isnan(x2[2])) return ODO_DBL_MAX;
+    const double a0 = x1[0], a1 = x1[1], a2 = x1[2];
+    const double mu0 = x2[0], mu1 = x2[1], mu2 = x2[2];
+    double m0 = ((T[0] * a0 + T[1] * a1) + T[2] * a2) + T[3] * 1.0;
+    double m1 = ((T[4] * a0 + T[5] * a1) + T[6] * a2) + T[7] * 1.0;
+    double m2 = ((T[8] * a0 + T[9] * a1) + T[10] * a2) + T[11] * 1.0;
+    double d0 = m0 - mu0, d1 = m1 - mu1, d2 = m2 - mu2;
+    {
+        double dsq = sum3d(d0 * d0, d1 * d1, d2 * d2);
+        double s1 = fmax(K.raster_cov_x, K.depth_cov);
+        double s2 = fmax(K.raster_cov_x, K.depth_cov);
+        if (dsq > 2.0 * (s1 + s2)) return ODO_DBL_MAX;
+    }
+    const double R00 = T[0], R01 = T[1], R02 = T[2];
+    const double R10 = T[4], R11 = T[5], R12 = T[6];
+    const double R20 = T[8], R21 = T[9], R22 = T[10];
+    const double c00 = K.raster_cov_x * a2, c11 = K.raster_cov_y * a2, c22 = K.depth_cov;
+    // RtC[i][j] = R[0][i]*C[0][j] + (R[1][i]*C[1][j] + R[2][i]*C[2][j]), C diagonal
+    const double R[3][3] = {{R00, R01, R02}, {R10, R11, R12}, {R20, R21, R22}};
+    const double C[3][3] = {{c00, 0.0, 0.0}, {0.0, c11, 0.0}, {0.0, 0.0, c22}};
+    double RtC[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) RtC[i][j] = sum3d(R[0][i] * C[0][j], R[1][i] * C[1][j], R[2][i] * C[2][j]);
+    // lower triangle of C1 = RtC * R, plus cov2 (diagonal)
+    const double cov2_0 = K.raster_cov_x * mu2, cov2_1 = K.raster_cov_y * mu2, cov2_2 = K.depth_cov;
+    double A00 = sum3d(RtC[0][0] * R00, RtC[0][1] * R10, RtC[0][2] * R20) + cov2_0;
+    double A10 = sum3d(RtC[1][0] * R00, RtC[1][1] * R10, RtC[1][2] * R20) + 0.0;
+    double A11 = sum3d(RtC[1][0] * R01, RtC[1][1] * R11, RtC[1][2] * R21) + cov2_1;
+    double A20 = sum3d(RtC[2][0] * R00, RtC[2][1] * R10, RtC[2][2] * R20) + 0.0;
+    double A21 = sum3d(RtC[2][0] * R01, RtC[2][1] * R11, RtC[2][2] * R21) + 0.0;
+    double A22 = sum3d(RtC[2][0] * R02, RtC[2][1] * R12, RtC[2][2] * R22) + cov2_2;
+    if (__builtin_isnan(d2)) return ODO_DBL_MAX;
+    // Eigen LLT<Matrix3d> (lower, unblocked); solve() ignores info()
+    double L00 = A00, L10 = A10, L20 = A20, L11 = A11, L21 = A21, L22 = A22;
+    {
+        double x = L00;
+        if (x > 0) {
+            L00 = x = sqrt(x);
+            L10 /= x;
+            L20 /= x;
+            x = L11 - L10 * L10;
+            if (x > 0) {
+                L11 = x = sqrt(x);
+                L21 -= L20 * L10;
+                L21 /= x;
+                x = L22 - (L20 * L20 + L21 * L21);
+                if (x > 0) L22 = sqrt(x);
+            }
+        }
+    }
+    double y0 = d0 / L00;
+    double y1 = (d1 - L10 * y0) / L11;
+    double y2 = (d2 - (L20 * y0 + L21 * y1)) / L22;
+    double z2 = y2 / L22;
+    double z1 = (y1 - L21 * z2) / L11;
+    double z0 = (y0 - (L10 * z1 + L20 * z2)) / L00;
+    double r = sum3d(d0 * z0, d1 * z1, d2 * z2);
+    if (!(r >= 0.0)) return ODO_DBL_MAX;
+    return r;
+}
+
+// ---------------------------------------- glibc TYPE_3 random_r (A.12)
+struct Rng {
+    int32_t s[31];
+    int f, r;
+    ODO_INLINE void seed(uint32_t seedv) {
+        // __srandom_r: word is int32_t, Schrage's method, 310 discards
+        if (seedv == 0) seedv = 1;
+        s[0] = (int32_t)seedv;
+        int32_t word = (int32_t)seedv;
+        for (int i = 1; i < 31; ++i) {
+            long hi = word / 127773;
+            long lo = word % 127773;
+            long w2 = 16807 * lo - 2836 * hi;
+            if (w2 < 0) w2 += 2147483647;
+            word = (int32_t)w2;
+            s[i] = word;
+        }
+        f = 3;
+        r = 0;
+        for (int k = 0; k < 310; k++) next();
+    }
+    ODO_INLINE int32_t next() {
+        uint32_t val = (uint32_t)s[f] + (uint32_t)s[r];
+        s[f] = (int32_t)val;
+        int32_t out = (int32_t)(val >> 1);
+        ++f;
+        if (f >= 31) {
+            f = 0;
+            ++r;
+        } else {
+            ++r;
+            if (r >= 31) r = 0;
+        }
+        return out;
+    }
+};
+
+// Per-pair seed of the batched contract: splitmix64(seed ^ pair index), low
+// 32 bits (SURVEY.md §8d "Seeds").
+ODO_INLINE __host__ uint32_t pair_seed(uint64_t base, uint64_t pair) {
+    uint64_t z = (base ^ pair) + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z = z ^ (z >> 31);
+    return (uint32_t)z;
+}
+
+}  // namespace odo

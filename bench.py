@@ -1,0 +1,219 @@
+#!/usr/bin/env python3
+"""bench.py — frames/sec of the per-frame odometry hot path on MI355X.
+
+Metric (BASELINE.json): frames/sec (extract + match + RANSAC-PnP) at 640x480,
+2000 ORB keypoints. Workload = config 2 ("TUM fr1/desk proxy": 640x480, FR1
+intrinsics + distortion, 2000 kp, RANSAC 500 hypotheses) on a synthetic
+closed-loop RGB-D sequence (no datasets offline). One step = one batch of
+`--batch` frames through Tracking::Track's hot path (extract every frame,
+kNN-2 + ratio match against its predecessor, Ransac::Iterate, PnPSolver),
+inputs resident in HBM. Multi-GPU: one process per GPU, each tracking its
+own sequence (frames mode, weak scaling, no data-path collective).
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import importlib.util
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG_DIR = os.path.join(ROOT, "adaptive-rgbd-localization-mappig_amd")
+
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+INT_VALU_PEAK_TOPS = 78.6    # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (int32 VALU lane-ops)
+FP64_VALU_PEAK_TF = 78.6     # MI355X FP64 vector (FMA = 2 flops)
+
+
+def load_module(name, path, pkg_dir=None):
+    if name in sys.modules:
+        return sys.modules[name]
+    spec = importlib.util.spec_from_file_location(name, path, submodule_search_locations=pkg_dir)
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[name] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def load_pkg():
+    return load_module("arlm_amd", os.path.join(PKG_DIR, "__init__.py"), [PKG_DIR])
+
+
+def load_synth():
+    return load_module("arlm_amd_synth", os.path.join(PKG_DIR, "synth.py"))
+
+
+def shard_seed(rank: int) -> int:
+    """Each rank tracks its own sequence (independent scene seed)."""
+    return 0x5EED0002 + 7919 * rank
+
+
+def level_pixels(w, h, nlevels=8, scale=1.2):
+    s, tot, lv = 1.0, 0, []
+    for l in range(nlevels):
+        inv = np.float32(1.0) / np.float32(s)
+        lw, lh = int(np.rint(np.float32(w) * inv)), int(np.rint(np.float32(h) * inv))
+        lv.append((lw, lh))
+        tot += lw * lh
+        s = float(np.float32(np.float64(np.float32(s)) * np.float64(np.float32(scale))))
+    return tot, lv
+
+
+def stage_model(stage, ms, B, w, h, nkp_mean):
+    """Algorithmic work per launch of a stage -> (bound, achieved, peak, unit, work)."""
+    pyr_px, lv = level_pixels(w, h)
+    if stage == "gray+pyramid":
+        byts = B * (3 * w * h + w * h + sum(2 * a * b for a, b in lv[1:]) + sum(a * b for a, b in lv[:-1]))
+        return "hbm", byts / (ms * 1e-3) / 1e9, HBM_PEAK_GBS, "GB/s", byts
+    if stage == "blur":
+        byts = B * 2 * pyr_px
+        return "hbm", byts / (ms * 1e-3) / 1e9, HBM_PEAK_GBS, "GB/s", byts
+    if stage == "fast":
+        byts = B * pyr_px
+        return "hbm", byts / (ms * 1e-3) / 1e9, HBM_PEAK_GBS, "GB/s", byts
+    if stage == "knn2":
+        ops = B * 16.0 * nkp_mean * nkp_mean
+        return "valu-int", ops / (ms * 1e-3) / 1e12, INT_VALU_PEAK_TOPS, "Tops/s", ops
+    byts = B * (5 * w * h + 84 * nkp_mean)
+    return "hbm", byts / (ms * 1e-3) / 1e9, HBM_PEAK_GBS, "GB/s", byts
+
+
+def cpu_baseline(bgr, dep, nfeat, iters, n_frames):
+    """The C++ oracle (single thread) on the first n_frames frames of the same sequence."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    cal = O.fr1_calib()
+    p = O.orb_params(nfeat)
+    rp = O.ransac_params(iters)
+    pkg = load_pkg()
+    t0 = time.perf_counter()
+    prev = None
+    latch = float("nan")
+    for i in range(n_frames):
+        f = O.extract_frame(bgr[i], dep[i], p, cal)
+        if prev is not None:
+            _, _, _, latch = O.track_pair(prev, f, cal, rp, pkg.pair_seed(0x5EED0000, i), latch)
+        prev = f
+    dt = time.perf_counter() - t0
+    return n_frames / dt, dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=64, help="frames per step")
+    ap.add_argument("--nfeatures", type=int, default=2000)
+    ap.add_argument("--iters", type=int, default=500, help="RANSAC hypotheses (mIterations)")
+    ap.add_argument("--width", type=int, default=640)
+    ap.add_argument("--height", type=int, default=480)
+    ap.add_argument("--cpu-frames", type=int, default=48, help="oracle sample size (frames)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
+
+    pkg = load_pkg()
+    synth = load_synth()
+    B, W, H = args.batch, args.width, args.height
+    bgr, dep, _ = synth.make_sequence(B, W, H, seed=shard_seed(rank), closed_loop=True)
+    d_bgr = torch.from_numpy(bgr).to("cuda")
+    d_dep = torch.from_numpy(dep.view(np.int16)).to("cuda")
+    cfg = pkg.default_config(W, H, B, nfeatures=args.nfeatures, iterations=args.iters,
+                             seed=0x5EED0000 + 1000003 * rank)
+    odo = pkg.Odometry(cfg, device=local_rank)
+    torch.cuda.synchronize()
+
+    # untimed: one batch with results for the sanity summary
+    res = odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=True)
+    for _ in range(args.warmup):
+        odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=False)
+    odo.synchronize()
+    torch.cuda.synchronize()
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=False)
+    odo.synchronize()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    timings = odo.timings()  # HIP events on the library stream, last step
+    frames = B * args.steps * world
+    value = frames / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+
+    nkp_mean = float(np.mean([len(odo.frame(i)["kps"]) for i in range(min(B, 4))]))
+    kern = {k: v for k, v in timings.items() if v > 0}
+    dominant = max(kern, key=kern.get) if kern else None
+    roofline = None
+    if dominant:
+        bound, ach, peak, unit, work = stage_model(dominant, kern[dominant], B, W, H, nkp_mean)
+        roofline = {"bound": bound, "achieved": round(ach, 3), "peak": peak, "unit": unit,
+                    "frac": round(ach / peak, 5), "traffic": None, "kernel": dominant,
+                    "kernel_ms": round(kern[dominant], 4)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        nf = min(args.cpu_frames, B)
+        fps, dt = cpu_baseline(bgr, dep, args.nfeatures, args.iters, nf)
+        cpu = {"value": round(fps, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+               "sample": f"first {nf} frames of the rank-0 sequence, C++ oracle single-thread ({dt:.1f} s)"}
+
+    if rank == 0:
+        ok = res[1:]
+        out = {
+            "metric": "frames/sec (extract+match+RANSAC-PnP) @640x480, 2000 kp",
+            "value": round(value, 2),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8/i32 (extract, match), f32+f64 (ransac, pnp)",
+            "data": "synthetic (ray-cast textured room, closed-loop trajectory; no dataset offline)",
+            "config": {"workload": f"cfg2 fr1/desk proxy {W}x{H}, {args.nfeatures} kp, RANSAC {args.iters}",
+                       "frames_per_step": B, "global_batch": B * world, "parallelism": f"frames x{world}",
+                       "mean_keypoints": round(nkp_mean, 1),
+                       "mean_matches": round(float(np.mean(ok["n_matches"])), 1),
+                       "mean_ransac_inliers": round(float(np.mean(ok["n_inliers"])), 1),
+                       "mean_ransac_visited": round(float(np.mean(ok["visited"])), 1)},
+            "stage_ms": {k: round(v, 4) for k, v in timings.items()},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    odo.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,131 @@
+/*
+ * odo.h — C-ABI of the MI355X-native per-frame odometry hot path
+ * (ORB extraction + Hamming kNN matching + RANSAC-wrapped PnP), the drop-in
+ * boundary for ttwang0303/Adaptive-RGBD-Localization-Mappig.
+ *
+ * Implemented by libodo_hip.so (hand-written HIP for gfx950). Plain pointers
+ * and sizes only; every function returns an int status (ODO_OK = 0, < 0 on
+ * error, message via odo_last_error()). The library never falls back to a CPU
+ * implementation: without a usable gfx950 device odo_create() fails.
+ *
+ * Each entry point names the reference interface it replaces (file:line in
+ * the reference tree). INTEGRATION.md shows the reference-side bindings.
+ */
+#ifndef ODO_H
+#define ODO_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "odo_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ODO_OK 0
+#define ODO_ERR_ARG (-1)
+#define ODO_ERR_DEVICE (-2)
+#define ODO_ERR_CAPACITY (-3)
+#define ODO_ERR_STATE (-4)
+
+typedef struct odo_config {
+    int32_t width, height;      /* frame size (all frames of a context share it) */
+    int32_t max_batch;          /* frames per odo_track_batch() call */
+    odo_orb_params orb;         /* ORBextractor(nFeatures,1.2,8,20,7) extractor.cpp:86 */
+    odo_calib calib;            /* Utils/common.h Calibration */
+    float nn_ratio;             /* Matcher(0.9f) tracking.cpp:197 */
+    odo_ransac_params ransac;   /* Ransac(200,20,3.0,4) odometry.cpp:28 */
+    uint32_t seed;              /* per-pair RNG seed base (replaces srand(clock()), main.cpp:27) */
+} odo_config;
+
+typedef struct odo_ctx odo_ctx;
+
+/* Fill cfg with the reference's defaults (FR1 calibration, nfeatures=1000). */
+void odo_default_config(odo_config* cfg, int width, int height, int max_batch);
+
+/* Context: owns the HIP stream, HBM scratch and the cross-frame state the
+ * reference keeps in globals (previous frame, DepthCovariance latch). */
+odo_ctx* odo_create(const odo_config* cfg, int device);
+void odo_destroy(odo_ctx* ctx);
+const char* odo_last_error(void);
+void* odo_stream(odo_ctx* ctx);               /* hipStream_t, for callers that share streams */
+int odo_reset(odo_ctx* ctx);                  /* forget previous frame and latch */
+int odo_set_latch(odo_ctx* ctx, double cov);  /* NaN = unlatched */
+double odo_get_latch(odo_ctx* ctx);
+
+/* ---- Batched hot path: Tracking::Track for n frames (tracking.cpp:38-78 minus
+ * map bookkeeping): Frame::Frame + ExtractFeatures (frame.cpp:18,135), then for
+ * every frame t with a predecessor: UpdateLastFrame VO landmarks
+ * (tracking.cpp:136), Matcher::KnnMatch (matcher.cpp:55), Odometry::Compute
+ * ADAPTIVE_RBA = Ransac::Iterate + PnPSolver::Compute (odometry.cpp:105-116),
+ * with F1 pose = identity (DESIGN.md §3 batched contract).
+ * d_bgr: device [n][H][W][3] u8, d_depth: device [n][H][W] u16 (x5000).
+ * results[n] (host): results[i] is the pair (frame i-1 -> frame i); frame -1
+ * is the last frame of the previous call. When h_results is NULL the call is
+ * asynchronous on odo_stream(). */
+int odo_track_batch(odo_ctx* ctx, const uint8_t* d_bgr, const uint16_t* d_depth, int n,
+                    odo_pair_result* h_results);
+/* Same with host inputs (H2D copy included). */
+int odo_track_batch_host(odo_ctx* ctx, const uint8_t* bgr, const uint16_t* depth, int n,
+                         odo_pair_result* h_results);
+/* Extraction only (frames land in the batch slots; no pairs). Device inputs. */
+int odo_extract_batch(odo_ctx* ctx, const uint8_t* d_bgr, const uint16_t* d_depth, int n);
+int odo_synchronize(odo_ctx* ctx);
+
+/* Read back frame features of batch slot i (0 <= i < n of the last call). */
+int odo_get_frame(odo_ctx* ctx, int i, orb_kp* kps, uint8_t* desc, float* kps_un, float* xyz,
+                  float* u_right, int cap, int* n);
+/* Read back pair i's matches (KnnMatch output), RANSAC inlier mask over the
+ * sorted good matches, and PnP inlier mask over frame-i keypoints. */
+int odo_get_pair(odo_ctx* ctx, int i, odo_dmatch* matches, int match_cap, int* n_matches,
+                 odo_dmatch* good_sorted, int* n_good, uint8_t* ransac_inliers /* n_good */,
+                 uint8_t* pnp_inliers /* frame kps */, int32_t* f2_src);
+
+/* ---- Per-stage entry points (host buffers, synchronous) ---- */
+
+/* Extractor::Extract + Frame::ExtractFeatures (extractor.cpp:39, frame.cpp:135):
+ * BGR8 (or gray when channels==1) + optional depth16 -> keypoints,
+ * 32-byte descriptors, undistorted points, camera xyz and right coordinate. */
+int odo_extract(odo_ctx* ctx, const uint8_t* img, int channels, const uint16_t* depth,
+                orb_kp* kps, uint8_t* desc, float* kps_un, float* xyz, float* u_right, int cap,
+                int* n);
+
+/* cv::BFMatcher(NORM_HAMMING).knnMatch(k=2) as used by Matcher::KnnMatch
+ * (matcher.cpp:60). idx/dist: nq x 2 (trainIdx -1 / INT_MAX when absent). */
+int odo_knn2_hamming(odo_ctx* ctx, const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* idx,
+                     int32_t* dist);
+
+/* Ransac::Iterate(Frame*,Frame*,m12) (ransac.cpp:155). xyz1/xyz2: mvKeys3Dc of
+ * both frames (n1/n2 points). rng: in/out glibc rand() state; latch: in/out
+ * DepthCovariance static (NaN = unlatched). inliers: capacity n12. Returns the
+ * bool result (1/0) in *ok. */
+int odo_ransac(odo_ctx* ctx, const odo_dmatch* m12, int n12, const float* xyz1, int n1,
+               const float* xyz2, int n2, const odo_ransac_params* p, odo_rng* rng, double* latch,
+               float T12[16], float* rmse, odo_dmatch* inliers, int* n_inliers, int* ok);
+
+/* PnPSolver::Compute (pnpsolver.cpp:17): Xw n x 3 (world), obs n x 3 (u,v,uR;
+ * uR<0 = mono edge). outlier: out, per edge. Returns inliers in *n_inliers. */
+int odo_pnp_motion_ba(odo_ctx* ctx, const float* Xw, const float* obs, int n, const odo_calib* calib,
+                      const float Tcw_init[16], float Tcw_out[16], uint8_t* outlier, int* n_inliers);
+
+/* Kabsch::Compute (kabsch.cpp:14), host-side 3x3 SVD. A,B: n x 3. */
+int odo_kabsch(const float* A, const float* B, int n, float T[16]);
+
+/* glibc rand() stream helpers (srand/rand of main.cpp:27, ransac.cpp:275). */
+void odo_rng_seed(odo_rng* r, uint32_t seed);
+int32_t odo_rng_next(odo_rng* r);
+
+/* ---- Introspection for parity tests ---- */
+int odo_debug_pyramid(odo_ctx* ctx, int i, uint8_t* out, size_t cap);
+int odo_debug_fast(odo_ctx* ctx, int i, int level, orb_kp* out, int cap, int* n);
+int odo_debug_octree(odo_ctx* ctx, int i, int level, orb_kp* out, int cap, int* n);
+int odo_debug_blur(odo_ctx* ctx, int i, uint8_t* out, size_t cap);
+/* Per-kernel device time of the last odo_track_batch (ms), via HIP events. */
+int odo_last_timings(odo_ctx* ctx, float* ms, int cap, const char** names);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ODO_H */

@@ -1,0 +1,707 @@
+// ORACLE — TEST INFRASTRUCTURE ONLY (see oracle.h). CPU restatement of the
+// ORB-SLAM2 extractor used on the reference's hot path:
+//   Frame::Frame            Core/frame.cpp:18-45
+//   ORBextractor ctor       Features/orbextractor.cpp:346-404
+//   ComputePyramid          Features/orbextractor.cpp:833-857
+//   ComputeKeyPointsOctTree Features/orbextractor.cpp:665-746
+//   DistributeOctTree       Features/orbextractor.cpp:466-663
+//   IC_Angle                Features/orbextractor.cpp:14-39
+//   computeOrbDescriptor    Features/orbextractor.cpp:43-85
+//   operator()              Features/orbextractor.cpp:756-815
+// OpenCV internals (cvtColor, resize, FAST, GaussianBlur, fastAtan2, cvRound)
+// follow SURVEY.md Appendix A; choices the survey left open are recorded in
+// DESIGN.md §4 ("pinned choices").
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <list>
+#include <vector>
+#include <algorithm>
+#include <utility>
+
+#include "oracle.h"
+#include "../include/odo_orb_pattern.h"
+
+namespace {
+
+const int PATCH_SIZE = 31;
+const int HALF_PATCH_SIZE = 15;
+const int EDGE_THRESHOLD = 19;
+
+inline int cvRound(float v) { return (int)lrintf(v); }   // round half to even
+inline int cvRound(double v) { return (int)lrint(v); }
+inline int cvFloor(float v) { int i = (int)v; return i - (i > v); }
+inline int cvFloor(double v) { int i = (int)v; return i - (i > v); }
+inline int cvCeil(float v) { int i = (int)v; return i + (i < v); }
+inline short sat_short(float v) {
+    int r = cvRound(v);
+    return (short)std::min(std::max(r, -32768), 32767);
+}
+
+struct Img {
+    int w = 0, h = 0;
+    std::vector<uint8_t> px;
+    uint8_t at(int y, int x) const { return px[(size_t)y * w + x]; }
+};
+
+struct KP {
+    float x, y, size, angle, response;
+    int octave, class_id;
+};
+
+// ---------------------------------------------------------------- A.1
+void bgr2gray(const uint8_t* bgr, int w, int h, int stride, uint8_t* gray) {
+    for (int y = 0; y < h; ++y) {
+        const uint8_t* row = bgr + (size_t)y * stride;
+        for (int x = 0; x < w; ++x) {
+            int b = row[3 * x], g = row[3 * x + 1], r = row[3 * x + 2];
+            gray[(size_t)y * w + x] = (uint8_t)((b * 1868 + g * 9617 + r * 4899 + (1 << 13)) >> 14);
+        }
+    }
+}
+
+// ---------------------------------------------------------------- tables
+struct Tables {
+    int nlevels, nfeatures;
+    std::vector<float> scale, inv_scale, sigma2;
+    std::vector<int> quota;
+    std::vector<int> umax;
+};
+
+Tables make_tables(const odo_orb_params& p) {
+    // orbextractor.cpp:346-404. scaleFactor member is double (orbextractor.h)
+    Tables t;
+    t.nlevels = p.nlevels;
+    t.nfeatures = p.nfeatures;
+    const double scaleFactor = (double)p.scale_factor;
+    t.scale.resize(p.nlevels);
+    t.sigma2.resize(p.nlevels);
+    t.scale[0] = 1.0f;
+    t.sigma2[0] = 1.0f;
+    for (int i = 1; i < p.nlevels; i++) {
+        t.scale[i] = (float)((double)t.scale[i - 1] * scaleFactor);
+        t.sigma2[i] = t.scale[i] * t.scale[i];
+    }
+    t.inv_scale.resize(p.nlevels);
+    for (int i = 0; i < p.nlevels; i++) t.inv_scale[i] = 1.0f / t.scale[i];
+
+    t.quota.resize(p.nlevels);
+    float factor = (float)(1.0f / scaleFactor);
+    float nDesired = p.nfeatures * (1 - factor) / (1 - (float)pow((double)factor, (double)p.nlevels));
+    int sum = 0;
+    for (int level = 0; level < p.nlevels - 1; level++) {
+        t.quota[level] = cvRound(nDesired);
+        sum += t.quota[level];
+        nDesired *= factor;
+    }
+    t.quota[p.nlevels - 1] = std::max(p.nfeatures - sum, 0);
+
+    t.umax.resize(HALF_PATCH_SIZE + 1);
+    int v, v0, vmax = cvFloor(HALF_PATCH_SIZE * sqrtf(2.f) / 2 + 1);
+    int vmin = cvCeil(HALF_PATCH_SIZE * sqrtf(2.f) / 2);
+    const double hp2 = HALF_PATCH_SIZE * HALF_PATCH_SIZE;
+    for (v = 0; v <= vmax; ++v) t.umax[v] = cvRound(sqrt(hp2 - v * v));
+    for (v = HALF_PATCH_SIZE, v0 = 0; v >= vmin; --v) {
+        while (t.umax[v0] == t.umax[v0 + 1]) ++v0;
+        t.umax[v] = v0;
+        ++v0;
+    }
+    return t;
+}
+
+// ---------------------------------------------------------------- A.2
+// cv::resize(INTER_LINEAR) for 8U, generic fixed-point path; vertical pass
+// uses the scalar formula everywhere (App. A.2).
+void resize_linear(const Img& src, Img& dst, int dw, int dh) {
+    dst.w = dw;
+    dst.h = dh;
+    dst.px.assign((size_t)dw * dh, 0);
+    const double inv_scale_x = (double)dw / src.w, inv_scale_y = (double)dh / src.h;
+    const double scale_x = 1. / inv_scale_x, scale_y = 1. / inv_scale_y;
+    std::vector<int> xofs(dw);
+    std::vector<short> alpha(2 * dw);
+    int xmax = dw;
+    for (int dx = 0; dx < dw; dx++) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = cvFloor(fx);
+        fx -= sx;
+        if (sx < 0) { fx = 0; sx = 0; }
+        if (sx + 1 >= src.w) {
+            xmax = std::min(xmax, dx);
+            if (sx >= src.w - 1) { fx = 0; sx = src.w - 1; }
+        }
+        xofs[dx] = sx;
+        alpha[2 * dx] = sat_short((1.f - fx) * 2048);
+        alpha[2 * dx + 1] = sat_short(fx * 2048);
+    }
+    std::vector<int> row0(dw), row1(dw);
+    auto hresize = [&](int sy, std::vector<int>& out) {
+        const uint8_t* S = &src.px[(size_t)sy * src.w];
+        for (int dx = 0; dx < dw; dx++) {
+            int sx = xofs[dx];
+            if (dx < xmax) out[dx] = S[sx] * alpha[2 * dx] + S[sx + 1] * alpha[2 * dx + 1];
+            else out[dx] = S[sx] * 2048;
+        }
+    };
+    auto clip = [&](int y) { return y < 0 ? 0 : (y >= src.h ? src.h - 1 : y); };
+    for (int dy = 0; dy < dh; dy++) {
+        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+        int sy = cvFloor(fy);
+        fy -= sy;
+        int b0 = sat_short((1.f - fy) * 2048), b1 = sat_short(fy * 2048);
+        hresize(clip(sy), row0);
+        hresize(clip(sy + 1), row1);
+        for (int dx = 0; dx < dw; dx++) {
+            int v = (row0[dx] * b0 + row1[dx] * b1 + (1 << 21)) >> 22;
+            dst.px[(size_t)dy * dw + dx] = (uint8_t)std::min(std::max(v, 0), 255);
+        }
+    }
+}
+
+// ---------------------------------------------------------------- A.3 FAST
+const int kCircle[16][2] = {{0, 3}, {1, 3}, {2, 2}, {3, 1}, {3, 0}, {3, -1}, {2, -2}, {1, -3},
+                            {0, -3}, {-1, -3}, {-2, -2}, {-3, -1}, {-3, 0}, {-3, 1}, {-2, 2}, {-1, 3}};
+
+// cornerScore<16> (opencv fast_score.cpp), restated.
+int corner_score(const uint8_t* ptr, const int* pixel, int threshold) {
+    const int K = 8, N = K * 3 + 1;
+    int v = ptr[0];
+    short d[N];
+    for (int k = 0; k < N; k++) d[k] = (short)(v - ptr[pixel[k]]);
+    int a0 = threshold;
+    for (int k = 0; k < 16; k += 2) {
+        int a = std::min((int)d[k + 1], (int)d[k + 2]);
+        a = std::min(a, (int)d[k + 3]);
+        if (a <= a0) continue;
+        a = std::min(a, (int)d[k + 4]);
+        a = std::min(a, (int)d[k + 5]);
+        a = std::min(a, (int)d[k + 6]);
+        a = std::min(a, (int)d[k + 7]);
+        a = std::min(a, (int)d[k + 8]);
+        a0 = std::max(a0, std::min(a, (int)d[k]));
+        a0 = std::max(a0, std::min(a, (int)d[k + 9]));
+    }
+    int b0 = -a0;
+    for (int k = 0; k < 16; k += 2) {
+        int b = std::max((int)d[k + 1], (int)d[k + 2]);
+        b = std::max(b, (int)d[k + 3]);
+        b = std::max(b, (int)d[k + 4]);
+        b = std::max(b, (int)d[k + 5]);
+        if (b >= b0) continue;
+        b = std::max(b, (int)d[k + 6]);
+        b = std::max(b, (int)d[k + 7]);
+        b = std::max(b, (int)d[k + 8]);
+        b0 = std::min(b0, std::max(b, (int)d[k]));
+        b0 = std::min(b0, std::max(b, (int)d[k + 9]));
+    }
+    return -b0 - 1;
+}
+
+// cv::FAST(roi, kps, threshold, nonmax=true) TYPE_9_16 on an ROI given by
+// base pointer / stride / size: FAST_t<16> restated (scores stored as uchar,
+// NMS strictly greater than the 8 neighbours, row-major emission).
+void fast_roi(const uint8_t* base, int stride, int rows, int cols, int threshold,
+              std::vector<KP>& out) {
+    out.clear();
+    threshold = std::min(std::max(threshold, 0), 255);
+    int pixel[25];
+    for (int k = 0; k < 16; k++) pixel[k] = kCircle[k][0] + kCircle[k][1] * stride;
+    for (int k = 16; k < 25; k++) pixel[k] = pixel[k - 16];
+    std::vector<uint8_t> score((size_t)rows * cols, 0);
+    std::vector<uint8_t> is_corner((size_t)rows * cols, 0);
+    for (int i = 3; i < rows - 3; i++) {
+        for (int j = 3; j < cols - 3; j++) {
+            const uint8_t* ptr = base + (size_t)i * stride + j;
+            int v = ptr[0];
+            // darker run
+            bool corner = false;
+            {
+                int vt = v - threshold, count = 0;
+                for (int k = 0; k < 25; k++) {
+                    int x = ptr[pixel[k]];
+                    if (x < vt) {
+                        if (++count > 8) { corner = true; break; }
+                    } else count = 0;
+                }
+            }
+            if (!corner) {
+                int vt = v + threshold, count = 0;
+                for (int k = 0; k < 25; k++) {
+                    int x = ptr[pixel[k]];
+                    if (x > vt) {
+                        if (++count > 8) { corner = true; break; }
+                    } else count = 0;
+                }
+            }
+            if (corner) {
+                is_corner[(size_t)i * cols + j] = 1;
+                score[(size_t)i * cols + j] = (uint8_t)corner_score(ptr, pixel, threshold);
+            }
+        }
+    }
+    for (int i = 3; i < rows - 3; i++) {
+        for (int j = 3; j < cols - 3; j++) {
+            if (!is_corner[(size_t)i * cols + j]) continue;
+            int s = score[(size_t)i * cols + j];
+            bool keep = true;
+            for (int di = -1; di <= 1 && keep; di++)
+                for (int dj = -1; dj <= 1; dj++) {
+                    if (!di && !dj) continue;
+                    if (!(s > score[(size_t)(i + di) * cols + (j + dj)])) { keep = false; break; }
+                }
+            if (keep) out.push_back(KP{(float)j, (float)i, 7.f, -1.f, (float)s, 0, -1});
+        }
+    }
+}
+
+// ComputeKeyPointsOctTree FAST part (orbextractor.cpp:669-723).
+void fast_level(const Img& im, int iniTh, int minTh, std::vector<KP>& cands) {
+    const float W = 30;
+    const int minBorderX = EDGE_THRESHOLD - 3;
+    const int minBorderY = minBorderX;
+    const int maxBorderX = im.w - EDGE_THRESHOLD + 3;
+    const int maxBorderY = im.h - EDGE_THRESHOLD + 3;
+    cands.clear();
+    const float width = (maxBorderX - minBorderX);
+    const float height = (maxBorderY - minBorderY);
+    const int nCols = width / W;
+    const int nRows = height / W;
+    const int wCell = ceil(width / nCols);
+    const int hCell = ceil(height / nRows);
+    std::vector<KP> cell;
+    for (int i = 0; i < nRows; i++) {
+        const float iniY = minBorderY + i * hCell;
+        float maxY = iniY + hCell + 6;
+        if (iniY >= maxBorderY - 3) continue;
+        if (maxY > maxBorderY) maxY = maxBorderY;
+        for (int j = 0; j < nCols; j++) {
+            const float iniX = minBorderX + j * wCell;
+            float maxX = iniX + wCell + 6;
+            if (iniX >= maxBorderX - 6) continue;
+            if (maxX > maxBorderX) maxX = maxBorderX;
+            const int y0 = (int)iniY, y1 = (int)maxY, x0 = (int)iniX, x1 = (int)maxX;
+            const uint8_t* base = &im.px[(size_t)y0 * im.w + x0];
+            fast_roi(base, im.w, y1 - y0, x1 - x0, iniTh, cell);
+            if (cell.empty()) fast_roi(base, im.w, y1 - y0, x1 - x0, minTh, cell);
+            for (auto& k : cell) {
+                k.x += j * wCell;
+                k.y += i * hCell;
+                cands.push_back(k);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- octree
+struct Pt2i { int x, y; };
+struct Node {
+    std::vector<KP> vKeys;
+    Pt2i UL, UR, BL, BR;
+    std::list<Node>::iterator lit;
+    bool bNoMore = false;
+    long long seq = 0;  // creation order: pinned tie-break for (size, pointer) sort
+};
+
+void divide_node(const Node& n, Node& n1, Node& n2, Node& n3, Node& n4) {
+    const int halfX = ceil(static_cast<float>(n.UR.x - n.UL.x) / 2);
+    const int halfY = ceil(static_cast<float>(n.BR.y - n.UL.y) / 2);
+    n1.UL = n.UL;
+    n1.UR = Pt2i{n.UL.x + halfX, n.UL.y};
+    n1.BL = Pt2i{n.UL.x, n.UL.y + halfY};
+    n1.BR = Pt2i{n.UL.x + halfX, n.UL.y + halfY};
+    n2.UL = n1.UR;
+    n2.UR = n.UR;
+    n2.BL = n1.BR;
+    n2.BR = Pt2i{n.UR.x, n.UL.y + halfY};
+    n3.UL = n1.BL;
+    n3.UR = n1.BR;
+    n3.BL = n.BL;
+    n3.BR = Pt2i{n1.BR.x, n.BL.y};
+    n4.UL = n3.UR;
+    n4.UR = n2.BR;
+    n4.BL = n3.BR;
+    n4.BR = n.BR;
+    for (const KP& kp : n.vKeys) {
+        if (kp.x < n1.UR.x) {
+            if (kp.y < n1.BR.y) n1.vKeys.push_back(kp);
+            else n3.vKeys.push_back(kp);
+        } else if (kp.y < n1.BR.y) n2.vKeys.push_back(kp);
+        else n4.vKeys.push_back(kp);
+    }
+    if (n1.vKeys.size() == 1) n1.bNoMore = true;
+    if (n2.vKeys.size() == 1) n2.bNoMore = true;
+    if (n3.vKeys.size() == 1) n3.bNoMore = true;
+    if (n4.vKeys.size() == 1) n4.bNoMore = true;
+}
+
+struct SizePtr {
+    int size;
+    Node* node;
+    bool operator<(const SizePtr& o) const {
+        if (size != o.size) return size < o.size;
+        return node->seq < o.node->seq;
+    }
+};
+
+std::vector<KP> distribute_octree(const std::vector<KP>& keys, int minX, int maxX, int minY,
+                                  int maxY, int N) {
+    const int nIni = round(static_cast<float>(maxX - minX) / (maxY - minY));
+    const float hX = static_cast<float>(maxX - minX) / nIni;
+    std::list<Node> lNodes;
+    std::vector<Node*> ini(nIni);
+    long long seq = 0;
+    for (int i = 0; i < nIni; i++) {
+        Node ni;
+        ni.UL = Pt2i{(int)(hX * static_cast<float>(i)), 0};
+        ni.UR = Pt2i{(int)(hX * static_cast<float>(i + 1)), 0};
+        ni.BL = Pt2i{ni.UL.x, maxY - minY};
+        ni.BR = Pt2i{ni.UR.x, maxY - minY};
+        ni.seq = seq++;
+        lNodes.push_back(ni);
+        ini[i] = &lNodes.back();
+    }
+    for (const KP& kp : keys) ini[(size_t)(kp.x / hX)]->vKeys.push_back(kp);
+
+    auto lit = lNodes.begin();
+    while (lit != lNodes.end()) {
+        if (lit->vKeys.size() == 1) {
+            lit->bNoMore = true;
+            lit++;
+        } else if (lit->vKeys.empty()) lit = lNodes.erase(lit);
+        else lit++;
+    }
+
+    bool bFinish = false;
+    std::vector<SizePtr> vSizeAndPtr;
+    auto push_child = [&](Node& c, std::vector<SizePtr>& acc, int* nToExpand) {
+        if (c.vKeys.size() > 0) {
+            c.seq = seq++;
+            lNodes.push_front(c);
+            if (c.vKeys.size() > 1) {
+                if (nToExpand) (*nToExpand)++;
+                acc.push_back(SizePtr{(int)c.vKeys.size(), &lNodes.front()});
+                lNodes.front().lit = lNodes.begin();
+            }
+        }
+    };
+    while (!bFinish) {
+        int prevSize = lNodes.size();
+        lit = lNodes.begin();
+        int nToExpand = 0;
+        vSizeAndPtr.clear();
+        while (lit != lNodes.end()) {
+            if (lit->bNoMore) {
+                lit++;
+                continue;
+            }
+            Node n1, n2, n3, n4;
+            divide_node(*lit, n1, n2, n3, n4);
+            push_child(n1, vSizeAndPtr, &nToExpand);
+            push_child(n2, vSizeAndPtr, &nToExpand);
+            push_child(n3, vSizeAndPtr, &nToExpand);
+            push_child(n4, vSizeAndPtr, &nToExpand);
+            lit = lNodes.erase(lit);
+        }
+        if ((int)lNodes.size() >= N || (int)lNodes.size() == prevSize) {
+            bFinish = true;
+        } else if (((int)lNodes.size() + nToExpand * 3) > N) {
+            while (!bFinish) {
+                prevSize = lNodes.size();
+                std::vector<SizePtr> vPrev = vSizeAndPtr;
+                vSizeAndPtr.clear();
+                std::sort(vPrev.begin(), vPrev.end());
+                for (int j = (int)vPrev.size() - 1; j >= 0; j--) {
+                    Node n1, n2, n3, n4;
+                    divide_node(*vPrev[j].node, n1, n2, n3, n4);
+                    push_child(n1, vSizeAndPtr, nullptr);
+                    push_child(n2, vSizeAndPtr, nullptr);
+                    push_child(n3, vSizeAndPtr, nullptr);
+                    push_child(n4, vSizeAndPtr, nullptr);
+                    lNodes.erase(vPrev[j].node->lit);
+                    if ((int)lNodes.size() >= N) break;
+                }
+                if ((int)lNodes.size() >= N || (int)lNodes.size() == prevSize) bFinish = true;
+            }
+        }
+    }
+    std::vector<KP> res;
+    res.reserve(lNodes.size());
+    for (auto& n : lNodes) {
+        const KP* best = &n.vKeys[0];
+        float maxResponse = best->response;
+        for (size_t k = 1; k < n.vKeys.size(); k++)
+            if (n.vKeys[k].response > maxResponse) {
+                best = &n.vKeys[k];
+                maxResponse = n.vKeys[k].response;
+            }
+        res.push_back(*best);
+    }
+    return res;
+}
+
+// ---------------------------------------------------------------- A.5
+float fast_atan2(float y, float x) {
+    static const float p1 = 0.9997878412794807f * (float)(180 / M_PI);
+    static const float p3 = -0.3258083974640975f * (float)(180 / M_PI);
+    static const float p5 = 0.1555786518463281f * (float)(180 / M_PI);
+    static const float p7 = -0.04432655554792128f * (float)(180 / M_PI);
+    float ax = std::abs(x), ay = std::abs(y);
+    float a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = ax / (ay + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+float ic_angle(const Img& im, float px, float py, const std::vector<int>& umax) {
+    int m_01 = 0, m_10 = 0;
+    const int cy = cvRound(py), cx = cvRound(px);
+    for (int u = -HALF_PATCH_SIZE; u <= HALF_PATCH_SIZE; ++u) m_10 += u * im.at(cy, cx + u);
+    for (int v = 1; v <= HALF_PATCH_SIZE; ++v) {
+        int v_sum = 0;
+        int d = umax[v];
+        for (int u = -d; u <= d; ++u) {
+            int val_plus = im.at(cy + v, cx + u), val_minus = im.at(cy - v, cx + u);
+            v_sum += (val_plus - val_minus);
+            m_10 += u * (val_plus + val_minus);
+        }
+        m_01 += v * v_sum;
+    }
+    return fast_atan2((float)m_01, (float)m_10);
+}
+
+// ---------------------------------------------------------------- A.4
+const int kGauss[7] = {18, 34, 48, 56, 48, 34, 18};  // Q8, error-diffused, sum 256
+
+inline int reflect101(int i, int n) {
+    if (n == 1) return 0;
+    while (i < 0 || i >= n) {
+        if (i < 0) i = -i;
+        else i = 2 * n - 2 - i;
+    }
+    return i;
+}
+
+void gaussian_blur(const Img& src, Img& dst) {
+    dst.w = src.w;
+    dst.h = src.h;
+    dst.px.assign(src.px.size(), 0);
+    std::vector<uint32_t> H((size_t)src.w * src.h);
+    for (int y = 0; y < src.h; y++)
+        for (int x = 0; x < src.w; x++) {
+            uint32_t s = 0;
+            for (int j = -3; j <= 3; j++) s += kGauss[j + 3] * src.at(y, reflect101(x + j, src.w));
+            H[(size_t)y * src.w + x] = s;
+        }
+    for (int y = 0; y < src.h; y++)
+        for (int x = 0; x < src.w; x++) {
+            uint32_t s = 0;
+            for (int j = -3; j <= 3; j++) s += kGauss[j + 3] * H[(size_t)reflect101(y + j, src.h) * src.w + x];
+            dst.px[(size_t)y * src.w + x] = (uint8_t)((s + 32768) >> 16);
+        }
+}
+
+// computeOrbDescriptor (orbextractor.cpp:43-85); cos/sin of the float angle
+// are taken in double and rounded to float (App. A.5 note).
+void orb_descriptor(const KP& kpt, const Img& img, uint8_t* desc) {
+    const float factorPI = (float)(M_PI / 180.f);
+    float angle = (float)kpt.angle * factorPI;
+    float a = (float)cos((double)angle), b = (float)sin((double)angle);
+    const int cy = cvRound(kpt.y), cx = cvRound(kpt.x);
+    const int8_t* pattern = ODO_ORB_PATTERN;
+    auto value = [&](int idx) {
+        float px = (float)pattern[2 * idx], py = (float)pattern[2 * idx + 1];
+        int yy = cvRound(px * b + py * a);
+        int xx = cvRound(px * a - py * b);
+        return (int)img.at(cy + yy, cx + xx);
+    };
+    for (int i = 0; i < 32; ++i, pattern += 32) {
+        int val = 0;
+        for (int bit = 0; bit < 8; bit++) {
+            int t0 = value(2 * bit), t1 = value(2 * bit + 1);
+            val |= (t0 < t1) << bit;
+        }
+        desc[i] = (uint8_t)val;
+    }
+}
+
+// ---------------------------------------------------------------- extractor
+struct Extractor {
+    Tables t;
+    std::vector<Img> pyr;
+    explicit Extractor(const odo_orb_params& p) : t(make_tables(p)) {}
+
+    void compute_pyramid(const uint8_t* gray, int w, int h) {
+        pyr.assign(t.nlevels, Img());
+        for (int level = 0; level < t.nlevels; ++level) {
+            float s = t.inv_scale[level];
+            int sw = cvRound((float)w * s), sh = cvRound((float)h * s);
+            if (level == 0) {
+                pyr[0].w = w;
+                pyr[0].h = h;
+                pyr[0].px.assign(gray, gray + (size_t)w * h);
+            } else {
+                resize_linear(pyr[level - 1], pyr[level], sw, sh);
+            }
+        }
+    }
+
+    int run(const uint8_t* gray, int w, int h, std::vector<KP>& out, std::vector<uint8_t>& desc) {
+        out.clear();
+        desc.clear();
+        if (w <= 0 || h <= 0) return 0;
+        compute_pyramid(gray, w, h);
+        std::vector<std::vector<KP>> all(t.nlevels);
+        for (int level = 0; level < t.nlevels; ++level) {
+            const Img& im = pyr[level];
+            const int minBorderX = EDGE_THRESHOLD - 3, minBorderY = minBorderX;
+            const int maxBorderX = im.w - EDGE_THRESHOLD + 3, maxBorderY = im.h - EDGE_THRESHOLD + 3;
+            std::vector<KP> cands;
+            fast_level(im, ini_th, min_th, cands);
+            if (!cands.empty())
+                all[level] = distribute_octree(cands, minBorderX, maxBorderX, minBorderY, maxBorderY,
+                                               t.quota[level]);
+            const int scaledPatchSize = PATCH_SIZE * t.scale[level];
+            for (KP& k : all[level]) {
+                k.x += minBorderX;
+                k.y += minBorderY;
+                k.octave = level;
+                k.size = scaledPatchSize;
+            }
+        }
+        for (int level = 0; level < t.nlevels; ++level)
+            for (KP& k : all[level]) k.angle = ic_angle(pyr[level], k.x, k.y, t.umax);
+        int total = 0;
+        for (auto& v : all) total += (int)v.size();
+        desc.assign((size_t)total * 32, 0);
+        int offset = 0;
+        for (int level = 0; level < t.nlevels; ++level) {
+            std::vector<KP>& kps = all[level];
+            if (kps.empty()) continue;
+            Img blurred;
+            gaussian_blur(pyr[level], blurred);
+            for (size_t i = 0; i < kps.size(); i++) orb_descriptor(kps[i], blurred, &desc[(offset + i) * 32]);
+            offset += (int)kps.size();
+            if (level != 0) {
+                float scale = t.scale[level];
+                for (KP& k : kps) {
+                    k.x *= scale;
+                    k.y *= scale;
+                }
+            }
+            out.insert(out.end(), kps.begin(), kps.end());
+        }
+        return total;
+    }
+
+    int ini_th = 20, min_th = 7;
+};
+
+}  // namespace
+
+// ================================================================ C API
+extern "C" {
+
+void oracle_bgr2gray(const uint8_t* bgr, int w, int h, int stride, uint8_t* gray) {
+    bgr2gray(bgr, w, h, stride, gray);
+}
+
+void oracle_depth_to_f32(const uint16_t* d, int n, float factor, float* z) {
+    // Mat::convertTo(CV_32F, alpha): dst = (float)src * (float)alpha + 0.f
+    const float a = (float)(double)factor;
+    for (int i = 0; i < n; i++) z[i] = (float)d[i] * a + 0.0f;
+}
+
+int oracle_level_sizes(const odo_orb_params* p, int w, int h, int* lw, int* lh, float* scale,
+                       int* quota) {
+    Tables t = make_tables(*p);
+    for (int l = 0; l < p->nlevels; l++) {
+        lw[l] = cvRound((float)w * t.inv_scale[l]);
+        lh[l] = cvRound((float)h * t.inv_scale[l]);
+        if (scale) scale[l] = t.scale[l];
+        if (quota) quota[l] = t.quota[l];
+    }
+    return p->nlevels;
+}
+
+int oracle_umax(int* umax16) {
+    odo_orb_params p{1000, 1.2f, 8, 20, 7};
+    Tables t = make_tables(p);
+    for (int i = 0; i < 16; i++) umax16[i] = t.umax[i];
+    return 16;
+}
+
+int oracle_pyramid(const uint8_t* gray, int w, int h, const odo_orb_params* p, uint8_t* out) {
+    Extractor ex(*p);
+    ex.compute_pyramid(gray, w, h);
+    size_t off = 0;
+    for (auto& im : ex.pyr) {
+        memcpy(out + off, im.px.data(), im.px.size());
+        off += im.px.size();
+    }
+    return (int)off;
+}
+
+int oracle_fast_level(const uint8_t* img, int w, int h, int ini_th, int min_th, orb_kp* out, int cap) {
+    Img im;
+    im.w = w;
+    im.h = h;
+    im.px.assign(img, img + (size_t)w * h);
+    std::vector<KP> c;
+    fast_level(im, ini_th, min_th, c);
+    int n = std::min((int)c.size(), cap);
+    for (int i = 0; i < n; i++)
+        out[i] = orb_kp{c[i].x, c[i].y, c[i].size, c[i].angle, c[i].response, c[i].octave, c[i].class_id};
+    return (int)c.size();
+}
+
+int oracle_octree(const orb_kp* keys, int n, int minX, int maxX, int minY, int maxY, int N,
+                  orb_kp* out, int cap) {
+    std::vector<KP> k(n);
+    for (int i = 0; i < n; i++)
+        k[i] = KP{keys[i].x, keys[i].y, keys[i].size, keys[i].angle, keys[i].response, keys[i].octave,
+                  keys[i].class_id};
+    if (n == 0) return 0;
+    std::vector<KP> r = distribute_octree(k, minX, maxX, minY, maxY, N);
+    int m = std::min((int)r.size(), cap);
+    for (int i = 0; i < m; i++)
+        out[i] = orb_kp{r[i].x, r[i].y, r[i].size, r[i].angle, r[i].response, r[i].octave, r[i].class_id};
+    return (int)r.size();
+}
+
+void oracle_blur(const uint8_t* img, int w, int h, uint8_t* out) {
+    Img a, b;
+    a.w = w;
+    a.h = h;
+    a.px.assign(img, img + (size_t)w * h);
+    gaussian_blur(a, b);
+    memcpy(out, b.px.data(), b.px.size());
+}
+
+float oracle_fast_atan2(float y, float x) { return fast_atan2(y, x); }
+
+int oracle_orb_extract(const uint8_t* gray, int w, int h, const odo_orb_params* p, orb_kp* kps,
+                       uint8_t* desc, int cap) {
+    Extractor ex(*p);
+    ex.ini_th = p->ini_th_fast;
+    ex.min_th = p->min_th_fast;
+    std::vector<KP> out;
+    std::vector<uint8_t> d;
+    int n = ex.run(gray, w, h, out, d);
+    int m = std::min(n, cap);
+    for (int i = 0; i < m; i++)
+        kps[i] = orb_kp{out[i].x, out[i].y, out[i].size, out[i].angle, out[i].response, out[i].octave,
+                        out[i].class_id};
+    if (desc) memcpy(desc, d.data(), (size_t)m * 32);
+    return n;
+}
+
+}  // extern "C"

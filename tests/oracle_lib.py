@@ -1,0 +1,160 @@
+"""ctypes binding of the CPU oracle (oracle/liboracle.so) — TEST INFRASTRUCTURE.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(ROOT, "oracle", "liboracle.so")
+
+P = C.c_void_p
+
+
+class OrbKP(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("size", C.c_float), ("angle", C.c_float),
+                ("response", C.c_float), ("octave", C.c_int32), ("class_id", C.c_int32)]
+
+
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+DMATCH_DTYPE = np.dtype([("queryIdx", "<i4"), ("trainIdx", "<i4"), ("imgIdx", "<i4"), ("distance", "<f4")])
+
+
+class OrbParams(C.Structure):
+    _fields_ = [("nfeatures", C.c_int32), ("scale_factor", C.c_float), ("nlevels", C.c_int32),
+                ("ini_th_fast", C.c_int32), ("min_th_fast", C.c_int32)]
+
+
+class Calib(C.Structure):
+    _fields_ = [(n, C.c_float) for n in ("fx", "fy", "cx", "cy", "k1", "k2", "p1", "p2", "k3",
+                                         "depth_factor", "mbf", "th_depth")]
+
+
+class RansacParams(C.Structure):
+    _fields_ = [("iterations", C.c_int32), ("min_inlier_th", C.c_int32), ("max_mahalanobis", C.c_float),
+                ("sample_size", C.c_int32), ("check_depth", C.c_int32)]
+
+
+class Rng(C.Structure):
+    _fields_ = [("state", C.c_int32 * 31), ("fpos", C.c_int32), ("rpos", C.c_int32)]
+
+
+class PairResult(C.Structure):
+    _fields_ = [("T12", C.c_float * 16), ("Tcw", C.c_float * 16), ("rmse", C.c_float),
+                ("n_matches", C.c_int32), ("n_good", C.c_int32), ("n_inliers", C.c_int32),
+                ("ransac_ok", C.c_int32), ("pnp_inliers", C.c_int32), ("visited", C.c_int32),
+                ("pad", C.c_int32)]
+
+
+def fr1_calib() -> Calib:
+    # Utils/common.h:35-44, 67, 71-72
+    return Calib(517.3, 516.5, 318.6, 255.3, 0.262383, -0.953104, -0.005358, 0.002628, 1.163314,
+                 1.0 / 5000.0, 40.0, 40.0)
+
+
+def calib_from(fx, fy, cx, cy, dist=(0.262383, -0.953104, -0.005358, 0.002628, 1.163314)) -> Calib:
+    return Calib(fx, fy, cx, cy, *dist, 1.0 / 5000.0, 40.0, 40.0)
+
+
+def ptr(a: np.ndarray):
+    return a.ctypes.data_as(P)
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        L = C.CDLL(LIB_PATH)
+        sig = {
+            "oracle_bgr2gray": (None, [P, C.c_int, C.c_int, C.c_int, P]),
+            "oracle_depth_to_f32": (None, [P, C.c_int, C.c_float, P]),
+            "oracle_level_sizes": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P]),
+            "oracle_umax": (C.c_int, [P]),
+            "oracle_pyramid": (C.c_int, [P, C.c_int, C.c_int, P, P]),
+            "oracle_fast_level": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, P, C.c_int]),
+            "oracle_octree": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, C.c_int]),
+            "oracle_blur": (None, [P, C.c_int, C.c_int, P]),
+            "oracle_fast_atan2": (C.c_float, [C.c_float, C.c_float]),
+            "oracle_orb_extract": (C.c_int, [P, C.c_int, C.c_int, P, P, P, C.c_int]),
+            "oracle_frame_geometry": (None, [P, C.c_int, P, C.c_int, C.c_int, P, P, P, P]),
+            "oracle_extract_frame": (C.c_int, [P, P, C.c_int, C.c_int, P, P, P, P, P, P, P, C.c_int]),
+            "oracle_knn2": (None, [P, C.c_int, P, C.c_int, P, P]),
+            "oracle_knn_match": (C.c_int, [P, C.c_int, P, C.c_int, C.c_float, P, P, P, P, P, P, P, C.c_int]),
+            "oracle_vo_landmarks": (C.c_int, [P, C.c_int, C.c_float, P]),
+            "oracle_rng_seed": (None, [P, C.c_uint32]),
+            "oracle_rng_next": (C.c_int32, [P]),
+            "oracle_libc_rand_stream": (None, [C.c_uint32, C.c_int, P]),
+            "oracle_ransac": (C.c_int, [P, C.c_int, P, P, P, P, P, P, P, P, P, P, P]),
+            "oracle_tfc": (None, [P, P, P, C.c_int, P]),
+            "oracle_svd3": (None, [P, P, P, P]),
+            "oracle_pnp": (C.c_int, [P, P, C.c_int, P, P, P, P]),
+            "oracle_kabsch": (None, [P, P, C.c_int, P]),
+            "oracle_track_pair": (C.c_int, [P, P, P, C.c_int, P, P, P, P, P, C.c_int, P, C.c_float, P,
+                                            C.c_uint32, P, P, P, P, C.c_int]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def orb_params(nfeatures=2000, scale=1.2, nlevels=8, ini=20, mn=7) -> OrbParams:
+    return OrbParams(nfeatures, scale, nlevels, ini, mn)
+
+
+def ransac_params(iters=200, min_inl=20, max_mahal=3.0, sample=4, check_depth=1) -> RansacParams:
+    return RansacParams(iters, min_inl, max_mahal, sample, check_depth)
+
+
+def gray(bgr: np.ndarray) -> np.ndarray:
+    h, w = bgr.shape[:2]
+    out = np.empty((h, w), np.uint8)
+    lib().oracle_bgr2gray(ptr(np.ascontiguousarray(bgr)), w, h, 3 * w, ptr(out))
+    return out
+
+
+def extract_frame(bgr, depth, params: OrbParams, calib: Calib, cap=None):
+    h, w = bgr.shape[:2]
+    cap = cap or params.nfeatures + 8 * params.nlevels + 8
+    kps = np.zeros(cap, KP_DTYPE)
+    desc = np.zeros((cap, 32), np.uint8)
+    kun = np.zeros((cap, 2), np.float32)
+    xyz = np.zeros((cap, 3), np.float32)
+    ur = np.zeros(cap, np.float32)
+    n = lib().oracle_extract_frame(ptr(np.ascontiguousarray(bgr)), ptr(np.ascontiguousarray(depth)), w, h,
+                                   C.byref(params), C.byref(calib), ptr(kps), ptr(desc), ptr(kun),
+                                   ptr(xyz), ptr(ur), cap)
+    assert n <= cap
+    return dict(kps=kps[:n], desc=desc[:n], kun=kun[:n], xyz=xyz[:n], ur=ur[:n])
+
+
+def knn2(q: np.ndarray, t: np.ndarray):
+    nq = q.shape[0]
+    idx = np.zeros((nq, 2), np.int32)
+    dist = np.zeros((nq, 2), np.int32)
+    lib().oracle_knn2(ptr(np.ascontiguousarray(q)), nq, ptr(np.ascontiguousarray(t)), t.shape[0],
+                      ptr(idx), ptr(dist))
+    return idx, dist
+
+
+def track_pair(f1, f2, calib: Calib, rp: RansacParams, seed: int, latch=float("nan"), ratio=0.9):
+    n1, n2 = len(f1["kps"]), len(f2["kps"])
+    res = PairResult()
+    mask = np.zeros(max(n2, 1), np.uint8)
+    matches = np.zeros(max(n1, 1), DMATCH_DTYPE)
+    lat = C.c_double(latch)
+    L = lib()
+    nm = L.oracle_track_pair(ptr(f1["kps"]), ptr(f1["desc"]), ptr(f1["xyz"]), n1,
+                             ptr(f2["kps"]), ptr(f2["desc"]), ptr(f2["kun"]), ptr(f2["xyz"]), ptr(f2["ur"]), n2,
+                             C.byref(calib), ratio, C.byref(rp), seed, C.byref(lat), C.byref(res),
+                             ptr(mask), ptr(matches), max(n1, 1))
+    return res, mask[:n2], matches[:nm], lat.value

@@ -1,0 +1,233 @@
+"""CPU tests: pin the oracle (the parity checker) before trusting it.
+
+Known-answer tests against independent numpy restatements, the real glibc
+rand() stream, SURVEY.md §8 tables, and synthetic ground-truth poses. The
+reference ships no golden vectors, so these KATs plus
+tests/golden/ (oracle fixtures, see make_golden.py) are what pins it.
+"""
+import ctypes as C
+import math
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from conftest import sequence
+
+
+def test_level_tables_match_survey():
+    L = O.lib()
+    lw = (C.c_int * 8)(); lh = (C.c_int * 8)(); sc = (C.c_float * 8)(); q = (C.c_int * 8)()
+    L.oracle_level_sizes(C.byref(O.orb_params(1000)), 640, 480, lw, lh, sc, q)
+    assert list(lw) == [640, 533, 444, 370, 309, 257, 214, 179]
+    assert list(lh) == [480, 400, 333, 278, 231, 193, 161, 134]
+    assert list(q) == [217, 181, 151, 126, 105, 87, 73, 60]
+    L.oracle_level_sizes(C.byref(O.orb_params(2000)), 640, 480, lw, lh, sc, q)
+    assert list(q) == [434, 362, 302, 251, 209, 175, 145, 122]
+    assert abs(sc[7] - 3.5832) < 1e-3
+    u = (C.c_int * 16)()
+    L.oracle_umax(u)
+    assert list(u) == [15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3]
+
+
+def test_fast_atan2_kat():
+    f = O.lib().oracle_fast_atan2
+    assert f(0.0, 1.0) == 0.0
+    assert abs(f(1.0, 0.0) - 90.0) < 1e-4
+    assert abs(f(0.0, -1.0) - 180.0) < 1e-4
+    assert abs(f(-1.0, 0.0) - 270.0) < 1e-4
+    rng = np.random.default_rng(1)
+    for y, x in rng.normal(size=(2000, 2)) * 1000:
+        ref = math.degrees(math.atan2(y, x)) % 360.0
+        d = abs(f(y, x) - ref)
+        assert min(d, 360 - d) < 0.02  # polynomial error bound of cv::fastAtan2
+
+
+@pytest.mark.parametrize("seed", [0, 1, 1234, 0x5EED0000, 2**31 - 1, 2**31 + 5, 2**32 - 1])
+def test_rng_is_glibc(seed):
+    ref = np.zeros(400, np.int32)
+    O.lib().oracle_libc_rand_stream(seed, 400, O.ptr(ref))
+    r = O.Rng()
+    O.lib().oracle_rng_seed(C.byref(r), seed)
+    got = np.array([O.lib().oracle_rng_next(C.byref(r)) for _ in range(400)], np.int32)
+    assert np.array_equal(got, ref)
+
+
+def _fast_numpy(img, th):
+    """FAST-9/16 + score + 3x3 strict NMS written from the FAST definition."""
+    circ = [(0, 3), (1, 3), (2, 2), (3, 1), (3, 0), (3, -1), (2, -2), (1, -3), (0, -3), (-1, -3), (-2, -2),
+            (-3, -1), (-3, 0), (-3, 1), (-2, 2), (-1, 3)]
+    h, w = img.shape
+    score = np.zeros((h, w), np.int32)
+    corner = np.zeros((h, w), bool)
+    for i in range(3, h - 3):
+        for j in range(3, w - 3):
+            v = int(img[i, j])
+            d = np.array([v - int(img[i + dy, j + dx]) for dx, dy in circ])
+            dd = np.concatenate([d, d])
+            arcs_dark = max(dd[k:k + 9].min() for k in range(16))
+            arcs_bright = max((-dd[k:k + 9]).min() for k in range(16))
+            m = max(arcs_dark, arcs_bright)
+            if m > th:
+                corner[i, j] = True
+                score[i, j] = max(th, m) - 1
+    out = []
+    for i in range(3, h - 3):
+        for j in range(3, w - 3):
+            if corner[i, j]:
+                s = score[i, j]
+                nb = score[i - 1:i + 2, j - 1:j + 2].copy()
+                nb[1, 1] = -1
+                if (s > nb).all():
+                    out.append((j, i, s))
+    return out
+
+
+def test_fast_cell_kat():
+    rng = np.random.default_rng(3)
+    img = (rng.random((40, 46)) * 60 + 90).astype(np.uint8)
+    img[10:25, 12:30] = 230
+    img[28:33, 5:9] = 10
+    # one level whose single FAST cell ROI is the whole interior
+    cap = 4096
+    out = np.zeros(cap, O.KP_DTYPE)
+    n = O.lib().oracle_fast_level(O.ptr(np.ascontiguousarray(img)), 46, 40, 20, 7, O.ptr(out), cap)
+    # level geometry: border 16 -> width 14, height 8 -> nCols = 0: no cells at all
+    assert n == 0
+    big = (rng.random((96, 96)) * 40 + 100).astype(np.uint8)
+    big[30:60, 35:70] = 240
+    big[65:80, 20:30] = 5
+    n = O.lib().oracle_fast_level(O.ptr(np.ascontiguousarray(big)), 96, 96, 20, 7, O.ptr(out), cap)
+    got = [(int(k["x"]), int(k["y"]), int(k["response"])) for k in out[:n]]
+    # expected: per-cell FAST on the 30px grid (orbextractor.cpp:669-723)
+    exp = []
+    minb, maxb = 16, 96 - 16
+    width = height = float(maxb - minb)
+    ncols = int(width / 30)
+    nrows = int(height / 30)
+    wc = math.ceil(width / ncols)
+    hc = math.ceil(height / nrows)
+    for i in range(nrows):
+        y0 = minb + i * hc
+        y1 = min(y0 + hc + 6, maxb)
+        if y0 >= maxb - 3:
+            continue
+        for j in range(ncols):
+            x0 = minb + j * wc
+            x1 = min(x0 + wc + 6, maxb)
+            if x0 >= maxb - 6:
+                continue
+            cell = _fast_numpy(big[y0:y1, x0:x1], 20)
+            if not cell:
+                cell = _fast_numpy(big[y0:y1, x0:x1], 7)
+            exp += [(x + j * wc, y + i * hc, s) for x, y, s in cell]
+    assert got == exp and len(exp) > 0
+
+
+def test_blur_kat():
+    img = np.zeros((20, 24), np.uint8)
+    img[10, 12] = 255
+    out = np.zeros_like(img)
+    O.lib().oracle_blur(O.ptr(img), 24, 20, O.ptr(out))
+    taps = np.array([18, 34, 48, 56, 48, 34, 18])
+    assert taps.sum() == 256
+    exp = (np.outer(taps, taps) * 255 + 32768) >> 16
+    assert np.array_equal(out[7:14, 9:16], exp.astype(np.uint8))
+    const = np.full((20, 24), 77, np.uint8)
+    O.lib().oracle_blur(O.ptr(const), 24, 20, O.ptr(out))
+    assert (out == 77).all()
+
+
+def test_knn2_against_numpy():
+    rng = np.random.default_rng(5)
+    q = rng.integers(0, 256, (300, 32), dtype=np.uint8)
+    t = rng.integers(0, 256, (500, 32), dtype=np.uint8)
+    t[17] = t[3]
+    q[0] = t[3]
+    idx, dist = O.knn2(q, t)
+    bits = np.unpackbits(q[:, None, :] ^ t[None, :, :], axis=2).sum(2)
+    for i in range(300):
+        order = sorted(range(500), key=lambda j: (bits[i, j], j))[:2]
+        assert list(idx[i]) == order
+        assert list(dist[i]) == [bits[i, order[0]], bits[i, order[1]]]
+    assert list(idx[0]) == [3, 17] and list(dist[0]) == [0, 0]
+
+
+def _rand_rigid(rng):
+    a = rng.normal(size=3) * 0.05
+    th = np.linalg.norm(a)
+    k = a / th
+    K = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    R = np.eye(3) + math.sin(th) * K + (1 - math.cos(th)) * K @ K
+    t = rng.normal(size=3) * 0.05
+    return R, t
+
+
+def test_tfc_and_kabsch_recover_rigid_motion():
+    rng = np.random.default_rng(11)
+    R, t = _rand_rigid(rng)
+    src = (rng.random((200, 3)) * [2, 1.5, 2] + [-1, -0.7, 0.8]).astype(np.float32)
+    tgt = (src @ R.T + t).astype(np.float32)
+    w = (1.0 / (src[:, 2] * tgt[:, 2])).astype(np.float32)
+    T = np.zeros(16, np.float32)
+    O.lib().oracle_tfc(O.ptr(src), O.ptr(tgt), O.ptr(w), 200, O.ptr(T))
+    T = T.reshape(4, 4)
+    assert np.abs(T[:3, :3] - R).max() < 2e-5 and np.abs(T[:3, 3] - t).max() < 2e-5
+    K = np.zeros(16, np.float32)
+    O.lib().oracle_kabsch(O.ptr(src), O.ptr(tgt), 200, O.ptr(K))
+    K = K.reshape(4, 4)
+    assert np.abs(K[:3, :3] - R).max() < 2e-5 and np.abs(K[:3, 3] - t).max() < 2e-5
+
+
+def test_svd3_against_numpy():
+    rng = np.random.default_rng(2)
+    for _ in range(200):
+        A = rng.normal(size=(3, 3)).astype(np.float32)
+        U = np.zeros(9, np.float32); S = np.zeros(3, np.float32); V = np.zeros(9, np.float32)
+        O.lib().oracle_svd3(O.ptr(A), O.ptr(U), O.ptr(S), O.ptr(V))
+        U = U.reshape(3, 3); V = V.reshape(3, 3)
+        assert np.allclose(np.sort(S)[::-1], S)
+        assert np.allclose(S, np.linalg.svd(A.astype(np.float64), compute_uv=False), rtol=1e-4, atol=1e-5)
+        assert np.allclose(U @ np.diag(S) @ V.T, A, atol=1e-4)
+
+
+def _pnp_problem(rng, n=150, stereo_frac=0.5):
+    R, t = _rand_rigid(rng)
+    Xw = (rng.random((n, 3)) * [2, 1.5, 2] + [-1, -0.7, 1.0]).astype(np.float32)
+    Xc = Xw @ R.T + t
+    fx, fy, cx, cy, bf = 517.3, 516.5, 318.6, 255.3, 40.0
+    u = fx * Xc[:, 0] / Xc[:, 2] + cx
+    v = fy * Xc[:, 1] / Xc[:, 2] + cy
+    ur = np.where(rng.random(n) < stereo_frac, u - bf / Xc[:, 2], -1.0)
+    obs = np.stack([u, v, ur], 1).astype(np.float32)
+    return R, t, Xw, obs
+
+
+def test_pnp_oracle_recovers_pose():
+    rng = np.random.default_rng(21)
+    R, t, Xw, obs = _pnp_problem(rng)
+    obs[:10, 0] += 40  # gross outliers
+    Tinit = np.eye(4, dtype=np.float32)
+    Tout = np.zeros(16, np.float32)
+    out = np.zeros(len(Xw), np.uint8)
+    n = O.lib().oracle_pnp(O.ptr(Xw), O.ptr(obs), len(Xw), C.byref(O.fr1_calib()), O.ptr(Tinit.ravel()),
+                           O.ptr(Tout), O.ptr(out))
+    Tout = Tout.reshape(4, 4)
+    assert np.abs(Tout[:3, :3] - R).max() < 1e-4 and np.abs(Tout[:3, 3] - t).max() < 1e-4
+    assert out[:10].all() and not out[10:].any()
+    assert n == len(Xw) - 10
+
+
+def test_pair_pipeline_recovers_ground_truth():
+    bgr, dep, poses = sequence(3)
+    cal = O.fr1_calib()
+    fs = [O.extract_frame(bgr[i], dep[i], O.orb_params(1000), cal) for i in range(3)]
+    latch = float("nan")
+    for i in range(2):
+        r, mask, m, latch = O.track_pair(fs[i], fs[i + 1], cal, O.ransac_params(200), 100 + i, latch)
+        gt = np.linalg.inv(poses[i + 1]) @ poses[i]
+        T = np.array(r.Tcw).reshape(4, 4)
+        assert r.ransac_ok == 1 and r.n_matches >= 20
+        assert np.abs(T[:3, 3] - gt[:3, 3]).max() < 0.01
+        assert np.abs(T[:3, :3] - gt[:3, :3]).max() < 0.01
+    assert latch > 0
