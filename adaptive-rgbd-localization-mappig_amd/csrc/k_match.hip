@@ -250,13 +250,15 @@ __global__ void __launch_bounds__(PM_THREADS) k_pair_match(
     uint64_t* __restrict__ sort_scratch, int match_cap) {
     __shared__ int s_cnt[PM_THREADS];
     __shared__ int s_tot, s_total_valid, s_cle, s_K, s_nm;
+    extern __shared__ __attribute__((aligned(16))) uint64_t dyn_lds[];  // pw entries
     const int p = blockIdx.x;                  // pair index
     const int s1 = slot0 + p, s2 = slot0 + p + 1;
     const int n1 = nkp[s1], n2 = nkp[s2];
     const int t = threadIdx.x;
     const float* X1 = xyz + (size_t)s1 * kp_cap * 3;
     const float* X2 = xyz + (size_t)s2 * kp_cap * 3;
-    uint64_t* sk = sort_scratch + (size_t)p * kp_cap;
+    uint64_t* sk = dyn_lds;
+    (void)sort_scratch;
     int32_t* src = f2_src + (size_t)p * kp_cap;
     for (int i = t; i < n2; i += PM_THREADS) src[i] = -1;
     // ---- VO landmarks on F1 (UpdateLastFrame, tracking.cpp:146-190): the K smallest
@@ -387,11 +389,16 @@ __global__ void __launch_bounds__(PM_THREADS) k_pair_match(
         gbase += tot;
         __syncthreads();
     }
-    // ---- std::sort(vGoodMatches) by distance (one lane, exact libstdc++ algorithm)
+    // ---- std::sort(vGoodMatches) by distance (one lane, exact libstdc++ algorithm, in LDS)
+    SortEl* Gl = reinterpret_cast<SortEl*>(dyn_lds);
+    for (int i = t; i < gbase; i += PM_THREADS) Gl[i] = G[i];
+    __syncthreads();
     if (t == 0) {
         n_good[p] = gbase;
-        gnu_sort(G, gbase);
+        gnu_sort(Gl, gbase);
     }
+    __syncthreads();
+    for (int i = t; i < gbase; i += PM_THREADS) G[i] = Gl[i];
     (void)n2;
 }
 
@@ -438,7 +445,9 @@ void launch_pair_match(hipStream_t st, const int2* knn_idx, const int2* knn_dist
                        const int* nkp, int kp_cap, int slot0, float ratio, float th_depth_m, int check_depth,
                        odo_dmatch* matches, int* n_matches, void* good, int* n_good, int32_t* f2_src,
                        uint64_t* sort_scratch, int match_cap, int npairs) {
-    hipLaunchKernelGGL(k_pair_match, dim3(npairs), dim3(PM_THREADS), 0, st, knn_idx, knn_dist, knn_stride, xyz, nkp,
+    int pw = 1;
+    while (pw < kp_cap || pw < match_cap) pw <<= 1;
+    hipLaunchKernelGGL(k_pair_match, dim3(npairs), dim3(PM_THREADS), (size_t)pw * 8, st, knn_idx, knn_dist, knn_stride, xyz, nkp,
                        kp_cap, slot0, ratio, th_depth_m, check_depth, matches, n_matches, (SortEl*)good, n_good, f2_src,
                        sort_scratch, match_cap);
 }

@@ -38,6 +38,7 @@ ODO_INLINE Quat qmul(const Quat& a, const Quat& b) {
                 a.w * b.z + a.z * b.w + a.x * b.y - a.y * b.x, a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z};
 }
 ODO_INLINE Quat quat_from_R(const double m[3][3]) {
+    // Eigen quaternionbase_assign_impl<Matrix3>, branches written with static indices
     Quat q;
     double t = sum3d(m[0][0], m[1][1], m[2][2]);
     if (t > 0) {
@@ -50,18 +51,29 @@ ODO_INLINE Quat quat_from_R(const double m[3][3]) {
     } else {
         int i = 0;
         if (m[1][1] > m[0][0]) i = 1;
-        if (m[2][2] > m[i][i]) i = 2;
-        int j = (i + 1) % 3, k = (j + 1) % 3;
-        t = sqrt(m[i][i] - m[j][j] - m[k][k] + 1.0);
-        double c[3];
-        c[i] = 0.5 * t;
-        t = 0.5 / t;
-        q.w = (m[k][j] - m[j][k]) * t;
-        c[j] = (m[j][i] + m[i][j]) * t;
-        c[k] = (m[k][i] + m[i][k]) * t;
-        q.x = c[0];
-        q.y = c[1];
-        q.z = c[2];
+        if (m[2][2] > (i == 0 ? m[0][0] : m[1][1])) i = 2;
+        if (i == 0) {  // j=1, k=2
+            t = sqrt(m[0][0] - m[1][1] - m[2][2] + 1.0);
+            q.x = 0.5 * t;
+            t = 0.5 / t;
+            q.w = (m[2][1] - m[1][2]) * t;
+            q.y = (m[1][0] + m[0][1]) * t;
+            q.z = (m[2][0] + m[0][2]) * t;
+        } else if (i == 1) {  // j=2, k=0
+            t = sqrt(m[1][1] - m[2][2] - m[0][0] + 1.0);
+            q.y = 0.5 * t;
+            t = 0.5 / t;
+            q.w = (m[0][2] - m[2][0]) * t;
+            q.z = (m[2][1] + m[1][2]) * t;
+            q.x = (m[0][1] + m[1][0]) * t;
+        } else {  // j=0, k=1
+            t = sqrt(m[2][2] - m[0][0] - m[1][1] + 1.0);
+            q.z = 0.5 * t;
+            t = 0.5 / t;
+            q.w = (m[1][0] - m[0][1]) * t;
+            q.x = (m[0][2] + m[2][0]) * t;
+            q.y = (m[1][2] + m[2][1]) * t;
+        }
     }
     return q;
 }
@@ -119,7 +131,7 @@ ODO_INLINE SE3 se3_exp(const double u[6]) {
             }
     } else {
         double a = sin(theta) / theta, b = (1 - cos(theta)) / (theta * theta);
-        double c = (theta - sin(theta)) / (theta * theta * theta);
+        double c = (theta - sin(theta)) / pow(theta, 3);
         for (int i = 0; i < 3; i++)
             for (int j = 0; j < 3; j++) {
                 R[i][j] = ((i == j ? 1.0 : 0.0) + a * O[i][j]) + b * O2[i][j];
@@ -137,60 +149,77 @@ ODO_INLINE void se3_map(const SE3& T, const double p[3], double o[3]) {
     for (int i = 0; i < 3; i++) o[i] += T.t[i];
 }
 
-// Eigen LDLT with diagonal pivoting on a 6x6 (one thread).
+// Eigen LDLT with diagonal pivoting on a 6x6, every index static after
+// unrolling (the pivot swap is a select over the candidate rows), so the
+// matrix stays in registers.
 ODO_INLINE bool ldlt_solve6(const double Ain[6][6], const double b[6], double x[6]) {
-    const int n = 6;
     double m[6][6];
+#pragma unroll
     for (int i = 0; i < 6; i++)
+#pragma unroll
         for (int j = 0; j < 6; j++) m[i][j] = Ain[i][j];
     int tr[6];
     int sign = 0;
-    for (int k = 0; k < n; ++k) {
+    bool fail = false;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
         int big = k;
         double bv = fabs(m[k][k]);
-        for (int i = k + 1; i < n; i++)
+#pragma unroll
+        for (int i = k + 1; i < 6; i++)
             if (fabs(m[i][i]) > bv) {
                 bv = fabs(m[i][i]);
                 big = i;
             }
         tr[k] = big;
-        if (k != big) {
-            for (int j = 0; j < k; j++) {
-                double a = m[k][j];
-                m[k][j] = m[big][j];
-                m[big][j] = a;
-            }
-            for (int i = big + 1; i < n; i++) {
-                double a = m[i][k];
-                m[i][k] = m[i][big];
-                m[i][big] = a;
-            }
-            double a = m[k][k];
-            m[k][k] = m[big][big];
-            m[big][big] = a;
-            for (int i = k + 1; i < big; i++) {
-                double tmp = m[i][k];
-                m[i][k] = m[big][i];
-                m[big][i] = tmp;
+#pragma unroll
+        for (int q = k + 1; q < 6; q++) {
+            if (q == big) {
+#pragma unroll
+                for (int j = 0; j < k; j++) {
+                    double a = m[k][j];
+                    m[k][j] = m[q][j];
+                    m[q][j] = a;
+                }
+#pragma unroll
+                for (int i = q + 1; i < 6; i++) {
+                    double a = m[i][k];
+                    m[i][k] = m[i][q];
+                    m[i][q] = a;
+                }
+                double a = m[k][k];
+                m[k][k] = m[q][q];
+                m[q][q] = a;
+#pragma unroll
+                for (int i = k + 1; i < q; i++) {
+                    double tmp = m[i][k];
+                    m[i][k] = m[q][i];
+                    m[q][i] = tmp;
+                }
             }
         }
         double temp[6];
         if (k > 0) {
+#pragma unroll
             for (int j = 0; j < k; j++) temp[j] = m[j][j] * m[k][j];
             double s = 0;
+#pragma unroll
             for (int j = 0; j < k; j++) s += m[k][j] * temp[j];
             m[k][k] -= s;
-            for (int i = k + 1; i < n; i++) {
+#pragma unroll
+            for (int i = k + 1; i < 6; i++) {
                 double tt = 0;
+#pragma unroll
                 for (int j = 0; j < k; j++) tt += m[i][j] * temp[j];
                 m[i][k] -= tt;
             }
         }
-        double akk = m[k][k];
-        bool valid = fabs(akk) > 0;
-        if (k == 0 && !valid) return false;
+        const double akk = m[k][k];
+        const bool valid = fabs(akk) > 0;
+        if (k == 0 && !valid) fail = true;
         if (valid)
-            for (int i = k + 1; i < n; i++) m[i][k] /= akk;
+#pragma unroll
+            for (int i = k + 1; i < 6; i++) m[i][k] /= akk;
         if (sign == 1) {
             if (akk < 0) sign = 3;
         } else if (sign == 2) {
@@ -200,220 +229,256 @@ ODO_INLINE bool ldlt_solve6(const double Ain[6][6], const double b[6], double x[
             else if (akk < 0) sign = 2;
         }
     }
-    if (!(sign == 1 || sign == 0)) return false;
+    if (fail || !(sign == 1 || sign == 0)) return false;
     double y[6];
+#pragma unroll
     for (int i = 0; i < 6; i++) y[i] = b[i];
-    for (int k = 0; k < n; k++) {
-        double a = y[k];
-        y[k] = y[tr[k]];
-        y[tr[k]] = a;
-    }
-    for (int i = 0; i < n; i++) {
+#pragma unroll
+    for (int k = 0; k < 6; k++)
+#pragma unroll
+        for (int q = k + 1; q < 6; q++)
+            if (tr[k] == q) {
+                double a = y[k];
+                y[k] = y[q];
+                y[q] = a;
+            }
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
         double s = 0;
+#pragma unroll
         for (int j = 0; j < i; j++) s += m[i][j] * y[j];
         y[i] -= s;
     }
-    for (int i = 0; i < n; i++) {
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
         if (fabs(m[i][i]) > 2.2250738585072014e-308) y[i] /= m[i][i];
         else y[i] = 0;
     }
-    for (int i = n - 1; i >= 0; i--) {
+#pragma unroll
+    for (int i = 5; i >= 0; i--) {
         double s = 0;
-        for (int j = i + 1; j < n; j++) s += m[j][i] * y[j];
+#pragma unroll
+        for (int j = i + 1; j < 6; j++) s += m[j][i] * y[j];
         y[i] -= s;
     }
-    for (int k = n - 1; k >= 0; k--) {
-        double a = y[k];
-        y[k] = y[tr[k]];
-        y[tr[k]] = a;
-    }
+#pragma unroll
+    for (int k = 5; k >= 0; k--)
+#pragma unroll
+        for (int q = k + 1; q < 6; q++)
+            if (tr[k] == q) {
+                double a = y[k];
+                y[k] = y[q];
+                y[q] = a;
+            }
+#pragma unroll
     for (int i = 0; i < 6; i++) x[i] = y[i];
     return true;
 }
 
-struct PEdge {
-    double Xw[3];
-    double obs[3];
-    double info;
-    double delta;
-    double err[3];
-    int stereo;
-    int level;
-    int robust;
-    int idx;  // F2 keypoint index
+// Edge storage: SoA in HBM scratch, [pair][field][cap]. The reference keeps
+// Xw, observations and the information weight as float (cv::Mat / KeyPoint,
+// pnpsolver.cpp:74-125) and widens to double inside g2o; we store the floats.
+struct PEdgeSoA {
+    float* X;      // 3*cap
+    float* obs;    // 3*cap
+    float* info;   // cap
+    uint8_t* flags;  // cap: bit0 stereo, bit1 outlier (level 1), bit2 robust kernel on
+    double* chi;   // cap: chi2 of the stored _error (last computeActiveErrors / computeError)
+    int* idx;      // cap: F2 keypoint index
 };
 
-// ----- fixed-order block reduction of NV doubles (lane-serial, xor butterfly, waves in order)
-template <int NV>
-ODO_INLINE void block_reduce(double (&v)[NV], double* red /* 4*NV */) {
+#define PE_STEREO 1
+#define PE_OUT 2
+#define PE_ROBUST 4
+
+ODO_INLINE PEdgeSoA pedge_view(void* base, int cap, int p) {
+    char* b = (char*)base + (size_t)p * (size_t)cap * 48;
+    PEdgeSoA E;
+    E.chi = (double*)b;
+    E.X = (float*)(b + (size_t)cap * 8);
+    E.obs = E.X + 3 * cap;
+    E.info = E.obs + 3 * cap;
+    E.idx = (int*)(E.info + cap);
+    E.flags = (uint8_t*)(E.idx + cap);
+    return E;
+}
+
+ODO_INLINE double wave_sum(double x) {
 #pragma unroll
-    for (int k = 0; k < NV; k++) {
-        double x = v[k];
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
-        v[k] = x;
-    }
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    __syncthreads();
-    if (lane == 0)
-        for (int k = 0; k < NV; k++) red[wave * NV + k] = v[k];
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < NV; k++) v[k] = ((red[k] + red[NV + k]) + red[2 * NV + k]) + red[3 * NV + k];
-    __syncthreads();
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+    return x;
 }
 
 struct PnPCam {
     double fx, fy, cx, cy, bf;
 };
 
-ODO_INLINE void edge_error(PEdge& e, const SE3& T, const PnPCam& c) {
-    double Xc[3];
-    se3_map(T, e.Xw, Xc);
-    if (!e.stereo) {
+// EdgeSE3ProjectXYZOnlyPose / EdgeStereoSE3ProjectXYZOnlyPose::computeError (g2o types_six_dof_expmap)
+ODO_INLINE void edge_err(const double Xc[3], const double ob[3], bool stereo, const PnPCam& c, double e[3]) {
+    if (!stereo) {
         double px = Xc[0] / Xc[2], py = Xc[1] / Xc[2];
-        e.err[0] = e.obs[0] - (px * c.fx + c.cx);
-        e.err[1] = e.obs[1] - (py * c.fy + c.cy);
-        e.err[2] = 0;
+        e[0] = ob[0] - (px * c.fx + c.cx);
+        e[1] = ob[1] - (py * c.fy + c.cy);
+        e[2] = 0;
     } else {
         const float invz = (float)(1.0 / Xc[2]);
         const double iz = (double)invz;
         double r0 = Xc[0] * iz * c.fx + c.cx;
         double r1 = Xc[1] * iz * c.fy + c.cy;
         double r2 = r0 - c.bf * iz;
-        e.err[0] = e.obs[0] - r0;
-        e.err[1] = e.obs[1] - r1;
-        e.err[2] = e.obs[2] - r2;
+        e[0] = ob[0] - r0;
+        e[1] = ob[1] - r1;
+        e[2] = ob[2] - r2;
     }
 }
-ODO_INLINE double edge_chi2(const PEdge& e) {
-    if (!e.stereo) return e.err[0] * (e.info * e.err[0]) + e.err[1] * (e.info * e.err[1]);
-    return sum3d(e.err[0] * (e.info * e.err[0]), e.err[1] * (e.info * e.err[1]), e.err[2] * (e.info * e.err[2]));
+ODO_INLINE double chi2_of(const double e[3], double info, bool stereo) {
+    if (!stereo) return e[0] * (info * e[0]) + e[1] * (info * e[1]);
+    return sum3d(e[0] * (info * e[0]), e[1] * (info * e[1]), e[2] * (info * e[2]));
 }
-ODO_INLINE void huber(const PEdge& e, double chi, double rho[3]) {
-    double dsqr = e.delta * e.delta;
+ODO_INLINE void huber_rho(double delta, double chi, double rho[3]) {
+    double dsqr = delta * delta;
     if (chi <= dsqr) {
         rho[0] = chi;
         rho[1] = 1.;
         rho[2] = 0.;
     } else {
         double sq = sqrt(chi);
-        rho[0] = 2 * sq * e.delta - dsqr;
-        rho[1] = e.delta / sq;
+        rho[0] = 2 * sq * delta - dsqr;
+        rho[1] = delta / sq;
         rho[2] = -0.5 * rho[1] / chi;
     }
 }
 
-__global__ void __launch_bounds__(PNP_THREADS) k_pnp(const int32_t* __restrict__ f2_src, const float* __restrict__ xyz,
-                                                     const float* __restrict__ kun, const float* __restrict__ ur,
-                                                     const int* __restrict__ nkp, int kp_cap, int slot0,
-                                                     FrameCalib cal, const float* __restrict__ T12,
-                                                     const int* __restrict__ pair_valid, const int* __restrict__ n_matches,
-                                                     int min_matches,
-                                                     PEdge* __restrict__ edges_g, odo_pair_result* __restrict__ res,
-                                                     uint8_t* __restrict__ inlier_mask) {
+// One wave per frame pair. Every lane runs the (tiny) serial parts — LDLT,
+// exp map, LM bookkeeping — redundantly on identical values, so no lane ever
+// waits for a broadcast; per-edge work is split over lanes and combined with a
+// fixed xor-butterfly (deterministic).
+#define PNP_NW 4
+#define PNP_NT (64 * PNP_NW)
+
+// Sum of NV per-lane doubles over the workgroup: xor-butterfly per wave, then
+// waves added in index order (fixed order => deterministic).
+template <int NV>
+ODO_INLINE void wg_sum(double (&v)[NV], double* red) {
+#pragma unroll
+    for (int k = 0; k < NV; k++) v[k] = wave_sum(v[k]);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (PNP_NW == 1) return;
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < NV; k++) red[wave * NV + k] = v[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NV; k++) {
+        double a = red[k];
+        for (int w = 1; w < PNP_NW; w++) a += red[w * NV + k];
+        v[k] = a;
+    }
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(PNP_NT) k_pnp(const int32_t* __restrict__ f2_src, const float* __restrict__ xyz,
+                                            const float* __restrict__ kun, const float* __restrict__ ur,
+                                            const int* __restrict__ nkp, int kp_cap, int slot0, FrameCalib cal,
+                                            const float* __restrict__ T12, const int* __restrict__ pair_valid,
+                                            const int* __restrict__ n_matches, int min_matches, void* edges_g,
+                                            odo_pair_result* __restrict__ res, uint8_t* __restrict__ inlier_mask) {
     const int p = blockIdx.x;
-    const int t = threadIdx.x;
-    __shared__ double red[4 * 28];
-    __shared__ int s_scan[PNP_THREADS];
-    __shared__ SE3 s_T, s_backup, s_T0;
-    __shared__ double s_H[6][6], s_b[6], s_x[6];
-    __shared__ double s_lambda, s_ni, s_curChi, s_rho;
-    __shared__ int s_ok2, s_stop, s_qmax, s_nedges, s_accept;
+    const int lane = threadIdx.x;  // thread index within the workgroup
+    const int wlane = threadIdx.x & 63;
+    __shared__ double red[PNP_NW * 28];
+    __shared__ int s_ne[PNP_NW];
     odo_pair_result* R = res + p;
     const int s1 = slot0 + p, s2 = slot0 + p + 1;
     const int n2 = nkp[s2];
     uint8_t* mask = inlier_mask + (size_t)p * kp_cap;
-    for (int i = t; i < n2; i += PNP_THREADS) mask[i] = 0;
+    for (int i = lane; i < n2; i += PNP_NT) mask[i] = 0;
     const float* T0 = T12 + (size_t)p * 16;
-    if (t == 0) {
-        for (int i = 0; i < 16; i++) R->Tcw[i] = T0[i];
-        R->pnp_inliers = 0;
-    }
+    if (lane < 16) R->Tcw[lane] = T0[lane];
+    if (lane == 0) R->pnp_inliers = 0;
     if (!pair_valid[p] || n_matches[p] < min_matches) return;
     // ---- edges: F2 keypoints holding a landmark, index order (pnpsolver.cpp:57-135)
     const int32_t* src = f2_src + (size_t)p * kp_cap;
     const float* X1 = xyz + (size_t)s1 * kp_cap * 3;
     const float* K2 = kun + (size_t)s2 * kp_cap * 2;
     const float* U2 = ur + (size_t)s2 * kp_cap;
-    PEdge* E = edges_g + (size_t)p * kp_cap;
-    const float deltaMono = (float)sqrt(5.991), deltaStereo = (float)sqrt(7.815);  // pnpsolver.cpp:51-52
-    int base = 0;
-    for (int c0 = 0; c0 < n2; c0 += PNP_THREADS) {
-        const int i = c0 + t;
-        const int has = (i < n2 && src[i] >= 0) ? 1 : 0;
-        s_scan[t] = has;
+    PEdgeSoA E = pedge_view(edges_g, kp_cap, p);
+    int ne = 0;
+    for (int c0 = 0; c0 < n2; c0 += PNP_NT) {
+        const int i = c0 + lane;
+        const bool has = i < n2 && src[i] >= 0;
+        const uint64_t bal = __ballot(has);
+        if (wlane == 0) s_ne[lane >> 6] = __popcll(bal);
         __syncthreads();
-        for (int off = 1; off < PNP_THREADS; off <<= 1) {
-            int a = t >= off ? s_scan[t - off] : 0;
-            __syncthreads();
-            s_scan[t] += a;
-            __syncthreads();
+        int before = 0, tot = 0;
+        for (int w = 0; w < PNP_NW; w++) {
+            if (w < (lane >> 6)) before += s_ne[w];
+            tot += s_ne[w];
         }
-        const int incl = s_scan[t], tot = s_scan[PNP_THREADS - 1];
+        __syncthreads();
         if (has) {
-            PEdge e;
+            const int k = ne + before + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
             const int s = src[i];
-            for (int k = 0; k < 3; k++) e.Xw[k] = (double)X1[3 * s + k];
-            const float urv = U2[i];
-            e.stereo = !(urv < 0);
-            e.obs[0] = K2[2 * i];
-            e.obs[1] = K2[2 * i + 1];
-            e.obs[2] = e.stereo ? (double)urv : 0.0;
             const float zw = X1[3 * s + 2];
-            const float sigma = 1.0f / (zw * zw);
-            e.info = sigma;
-            e.delta = e.stereo ? (double)deltaStereo : (double)deltaMono;
-            e.level = 0;
-            e.robust = 1;
-            e.err[0] = e.err[1] = e.err[2] = 0;
-            e.idx = i;
-            E[base + incl - 1] = e;
+            E.X[3 * k] = X1[3 * s];
+            E.X[3 * k + 1] = X1[3 * s + 1];
+            E.X[3 * k + 2] = zw;
+            const float urv = U2[i];
+            const bool st = !(urv < 0);
+            E.obs[3 * k] = K2[2 * i];
+            E.obs[3 * k + 1] = K2[2 * i + 1];
+            E.obs[3 * k + 2] = st ? urv : 0.f;
+            E.info[k] = 1.0f / (zw * zw);
+            E.flags[k] = (uint8_t)((st ? PE_STEREO : 0) | PE_ROBUST);
+            E.chi[k] = 0.0;
+            E.idx[k] = i;
         }
-        base += tot;
-        __syncthreads();
+        ne += tot;
     }
-    const int ne = base;
+    __syncthreads();
     if (ne < 3) {
-        for (int k = t; k < ne; k += PNP_THREADS) mask[E[k].idx] = 1;  // set inlier at edge creation
+        for (int k = lane; k < ne; k += PNP_NT) mask[E.idx[k]] = 1;  // SetInlier at edge creation
         return;
     }
-    PnPCam cam{(double)cal.fx, (double)cal.fy, (double)cal.cx, (double)cal.cy, (double)cal.mbf};
-    if (t == 0) {
+    const PnPCam cam{(double)cal.fx, (double)cal.fy, (double)cal.cx, (double)cal.cy, (double)cal.mbf};
+    const double dMono = (double)(float)sqrt(5.991), dStereo = (double)(float)sqrt(7.815);  // pnpsolver.cpp:51-52
+    SE3 T0s;
+    {
         double R0[3][3], t0[3];
         for (int i = 0; i < 3; i++) {
             for (int j = 0; j < 3; j++) R0[i][j] = (double)T0[i * 4 + j];
             t0[i] = (double)T0[i * 4 + 3];
         }
-        s_T0.q = quat_from_R(R0);
-        for (int i = 0; i < 3; i++) s_T0.t[i] = t0[i];
-        normalize_rot(s_T0);
+        T0s.q = quat_from_R(R0);
+        for (int i = 0; i < 3; i++) T0s.t[i] = t0[i];
+        normalize_rot(T0s);
     }
-    __syncthreads();
     const float chi2Mono = 5.991f, chi2Stereo = 7.815f;
     int nBad = 0;
+    SE3 T = T0s;
     for (int it = 0; it < 4; it++) {
-        if (t == 0) s_T = s_T0;
-        __syncthreads();
-        // ---------------- optimize(10)
+        T = T0s;  // vSE3->setEstimate(pFrame->GetPose()) (pnpsolver.cpp:150)
+        double lambda = 0, ni = 2;
         for (int iter = 0; iter < 10; iter++) {
-            // computeActiveErrors + activeRobustChi2 + buildSystem at s_T
-            const SE3 T = s_T;
+            // computeActiveErrors + activeRobustChi2 + buildSystem at T
             double acc[28];
+#pragma unroll
             for (int k = 0; k < 28; k++) acc[k] = 0;
-            for (int k = t; k < ne; k += PNP_THREADS) {
-                PEdge e = E[k];
-                if (e.level != 0) continue;
-                edge_error(e, T, cam);
-                E[k].err[0] = e.err[0];
-                E[k].err[1] = e.err[1];
-                E[k].err[2] = e.err[2];
-                const double c2 = edge_chi2(e);
+            for (int k = lane; k < ne; k += PNP_NT) {
+                const uint8_t fl = E.flags[k];
+                if (fl & PE_OUT) continue;
+                const bool st = fl & PE_STEREO;
+                const double Xw[3] = {E.X[3 * k], E.X[3 * k + 1], E.X[3 * k + 2]};
+                const double ob[3] = {E.obs[3 * k], E.obs[3 * k + 1], E.obs[3 * k + 2]};
+                const double info = E.info[k];
+                double Xc[3], e[3];
+                se3_map(T, Xw, Xc);
+                edge_err(Xc, ob, st, cam, e);
+                const double c2 = chi2_of(e, info, st);
+                E.chi[k] = c2;
                 double rho[3] = {c2, 1.0, 0.0};
-                if (e.robust) huber(e, c2, rho);
+                if (fl & PE_ROBUST) huber_rho(st ? dStereo : dMono, c2, rho);
                 acc[27] += rho[0];
-                double Xc[3];
-                se3_map(T, e.Xw, Xc);
                 const double x = Xc[0], y = Xc[1], invz = 1.0 / Xc[2], invz_2 = invz * invz;
                 double J[3][6];
                 J[0][0] = x * y * invz_2 * cam.fx;
@@ -428,164 +493,176 @@ __global__ void __launch_bounds__(PNP_THREADS) k_pnp(const int32_t* __restrict__
                 J[1][3] = 0;
                 J[1][4] = -invz * cam.fy;
                 J[1][5] = y * invz_2 * cam.fy;
-                const int D = e.stereo ? 3 : 2;
-                if (e.stereo) {
-                    J[2][0] = J[0][0] - cam.bf * y * invz_2;
-                    J[2][1] = J[0][1] + cam.bf * x * invz_2;
-                    J[2][2] = J[0][2];
-                    J[2][3] = J[0][3];
-                    J[2][4] = 0;
-                    J[2][5] = J[0][5] - cam.bf * invz_2;
-                }
+                // mono edges: third row zero, so its terms add exactly +0
+                J[2][0] = st ? J[0][0] - cam.bf * y * invz_2 : 0.0;
+                J[2][1] = st ? J[0][1] + cam.bf * x * invz_2 : 0.0;
+                J[2][2] = st ? J[0][2] : 0.0;
+                J[2][3] = st ? J[0][3] : 0.0;
+                J[2][4] = 0;
+                J[2][5] = st ? J[0][5] - cam.bf * invz_2 : 0.0;
                 const double r1 = rho[1];
-                const double wo = r1 * e.info;
+                const double wo = r1 * info;
                 int h = 0;
+#pragma unroll
                 for (int a = 0; a < 6; a++) {
-                    double s = 0;
-                    for (int kk = 0; kk < D; kk++) s += J[kk][a] * (e.info * e.err[kk]);
-                    acc[21 + a] -= r1 * s;
-                    for (int c = a; c < 6; c++) {
+                    double sb = 0;
+#pragma unroll
+                    for (int kk = 0; kk < 3; kk++) sb += J[kk][a] * (info * e[kk]);
+                    acc[21 + a] -= r1 * sb;
+#pragma unroll
+                    for (int cc = a; cc < 6; cc++) {
                         double hh = 0;
-                        for (int kk = 0; kk < D; kk++) hh += J[kk][a] * wo * J[kk][c];
+#pragma unroll
+                        for (int kk = 0; kk < 3; kk++) hh += J[kk][a] * wo * J[kk][cc];
                         acc[h++] += hh;
                     }
                 }
             }
-            block_reduce<28>(acc, red);
-            if (t == 0) {
+            wg_sum<28>(acc, red);
+            double H[6][6], b[6];
+            {
                 int h = 0;
                 for (int a = 0; a < 6; a++)
-                    for (int c = a; c < 6; c++) {
-                        s_H[a][c] = acc[h];
-                        s_H[c][a] = acc[h];
+                    for (int cc = a; cc < 6; cc++) {
+                        H[a][cc] = acc[h];
+                        H[cc][a] = acc[h];
                         h++;
                     }
-                for (int a = 0; a < 6; a++) s_b[a] = acc[21 + a];
-                s_curChi = acc[27];
-                if (iter == 0) {
-                    double mx = 0;
-                    for (int j = 0; j < 6; j++) mx = fmax(fabs(s_H[j][j]), mx);
-                    s_lambda = 1e-5 * mx;
-                    s_ni = 2;
-                }
-                s_qmax = 0;
-                s_stop = 0;
+                for (int a = 0; a < 6; a++) b[a] = acc[21 + a];
             }
-            __syncthreads();
-            // LM trials (OptimizationAlgorithmLevenberg::solve)
-            while (true) {
-                if (t == 0) {
-                    s_backup = s_T;
-                    double Hl[6][6];
-                    for (int a = 0; a < 6; a++)
-                        for (int c = 0; c < 6; c++) Hl[a][c] = s_H[a][c];
-                    for (int j = 0; j < 6; j++) Hl[j][j] += s_lambda;
-                    double x[6] = {0, 0, 0, 0, 0, 0};
-                    s_ok2 = ldlt_solve6(Hl, s_b, x) ? 1 : 0;
-                    for (int j = 0; j < 6; j++) s_x[j] = x[j];
-                    s_T = se3_mul(se3_exp(x), s_T);
-                }
-                __syncthreads();
-                const SE3 Tn = s_T;
-                double chi[1] = {0};
-                for (int k = t; k < ne; k += PNP_THREADS) {
-                    PEdge e = E[k];
-                    if (e.level != 0) continue;
-                    edge_error(e, Tn, cam);
-                    E[k].err[0] = e.err[0];
-                    E[k].err[1] = e.err[1];
-                    E[k].err[2] = e.err[2];
-                    const double c2 = edge_chi2(e);
-                    if (e.robust) {
-                        double rho[3];
-                        huber(e, c2, rho);
-                        chi[0] += rho[0];
-                    } else chi[0] += c2;
-                }
-                block_reduce<1>(chi, red);
-                if (t == 0) {
-                    double tempChi = chi[0];
-                    if (!s_ok2) tempChi = 1.7976931348623157e308;
-                    double rho = s_curChi - tempChi;
-                    double scale = 0;
-                    for (int j = 0; j < 6; j++) scale += s_x[j] * (s_lambda * s_x[j] + s_b[j]);
-                    scale += 1e-3;
-                    rho /= scale;
-                    if (rho > 0 && isfinite(tempChi)) {
-                        double alpha = 1. - pow((2 * rho - 1), 3);
-                        alpha = fmin(alpha, 2. / 3.);
-                        double sf = fmax(1. / 3., alpha);
-                        s_lambda *= sf;
-                        s_ni = 2;
-                        s_curChi = tempChi;
-                    } else {
-                        s_lambda *= s_ni;
-                        s_ni *= 2;
-                        s_T = s_backup;
-                    }
-                    s_qmax++;
-                    s_rho = rho;
-                    s_accept = (rho < 0 && s_qmax < 10) ? 0 : 1;
-                    if (s_accept && (s_qmax == 10 || rho == 0)) s_stop = 1;
-                }
-                __syncthreads();
-                if (s_accept) break;
+            double curChi = acc[27];
+            if (iter == 0) {
+                double mx = 0;
+                for (int j = 0; j < 6; j++) mx = fmax(fabs(H[j][j]), mx);
+                lambda = 1e-5 * mx;
+                ni = 2;
             }
-            if (s_stop) break;
+            // OptimizationAlgorithmLevenberg::solve trial loop
+            double rho = 0;
+            int qmax = 0;
+            do {
+                const SE3 backup = T;
+                double Hl[6][6];
+                for (int a = 0; a < 6; a++)
+                    for (int cc = 0; cc < 6; cc++) Hl[a][cc] = H[a][cc];
+                for (int j = 0; j < 6; j++) Hl[j][j] += lambda;
+                double x[6] = {0, 0, 0, 0, 0, 0};
+                const bool ok2 = ldlt_solve6(Hl, b, x);
+                T = se3_mul(se3_exp(x), T);
+                double chi = 0;
+                for (int k = lane; k < ne; k += PNP_NT) {
+                    const uint8_t fl = E.flags[k];
+                    if (fl & PE_OUT) continue;
+                    const bool st = fl & PE_STEREO;
+                    const double Xw[3] = {E.X[3 * k], E.X[3 * k + 1], E.X[3 * k + 2]};
+                    const double ob[3] = {E.obs[3 * k], E.obs[3 * k + 1], E.obs[3 * k + 2]};
+                    double Xc[3], e[3];
+                    se3_map(T, Xw, Xc);
+                    edge_err(Xc, ob, st, cam, e);
+                    const double c2 = chi2_of(e, (double)E.info[k], st);
+                    E.chi[k] = c2;
+                    if (fl & PE_ROBUST) {
+                        double rr[3];
+                        huber_rho(st ? dStereo : dMono, c2, rr);
+                        chi += rr[0];
+                    } else chi += c2;
+                }
+                double chv[1] = {chi};
+                wg_sum<1>(chv, red);
+                double tempChi = chv[0];
+                if (!ok2) tempChi = 1.7976931348623157e308;
+                rho = curChi - tempChi;
+                double scale = 0;
+                for (int j = 0; j < 6; j++) scale += x[j] * (lambda * x[j] + b[j]);
+                scale += 1e-3;
+                rho /= scale;
+                if (rho > 0 && isfinite(tempChi)) {
+                    double alpha = 1. - pow((2 * rho - 1), 3);
+                    alpha = fmin(alpha, 2. / 3.);
+                    double sf = fmax(1. / 3., alpha);
+                    lambda *= sf;
+                    ni = 2;
+                    curChi = tempChi;
+                } else {
+                    lambda *= ni;
+                    ni *= 2;
+                    T = backup;
+                }
+                qmax++;
+            } while (rho < 0 && qmax < 10);
+            if (qmax == 10 || rho == 0) break;
         }
-        // ---------------- classification (pnpsolver.cpp:149-205)
-        const SE3 T = s_T;
-        double bad[1] = {0};
-        for (int k = t; k < ne; k += PNP_THREADS) {
-            PEdge e = E[k];
-            const int idx = e.idx;
-            if (mask[idx] == 2) {  // outlier from the previous round: recompute at current estimate
-                edge_error(e, T, cam);
-                E[k].err[0] = e.err[0];
-                E[k].err[1] = e.err[1];
-                E[k].err[2] = e.err[2];
+        // ---- classification (pnpsolver.cpp:157-201)
+        int bad = 0;
+        for (int k = lane; k < ne; k += PNP_NT) {
+            uint8_t fl = E.flags[k];
+            const bool st = fl & PE_STEREO;
+            double c2 = E.chi[k];
+            if (fl & PE_OUT) {  // IsOutlier: e->computeError() at the current estimate
+                const double Xw[3] = {E.X[3 * k], E.X[3 * k + 1], E.X[3 * k + 2]};
+                const double ob[3] = {E.obs[3 * k], E.obs[3 * k + 1], E.obs[3 * k + 2]};
+                double Xc[3], e[3];
+                se3_map(T, Xw, Xc);
+                edge_err(Xc, ob, st, cam, e);
+                c2 = chi2_of(e, (double)E.info[k], st);
+                E.chi[k] = c2;
             }
-            const float chi2 = (float)edge_chi2(e);
-            const float th = e.stereo ? chi2Stereo : chi2Mono;
-            if (chi2 > th) {
-                mask[idx] = 2;
-                E[k].level = 1;
-                bad[0] += 1;
+            const float chi2 = (float)c2;
+            if (chi2 > (st ? chi2Stereo : chi2Mono)) {
+                fl |= PE_OUT;
+                bad++;
             } else {
-                mask[idx] = 1;
-                E[k].level = 0;
+                fl &= ~PE_OUT;
             }
-            if (it == 2) E[k].robust = 0;
+            if (it == 2) fl &= ~PE_ROBUST;
+            E.flags[k] = fl;
         }
-        block_reduce<1>(bad, red);
-        nBad = (int)bad[0];
+        double bd[1] = {(double)bad};
+        wg_sum<1>(bd, red);
+        nBad = (int)bd[0];
         if (ne < 10) break;
     }
-    if (t == 0) {
+    if (lane == 0) {
         double Rm[3][3];
-        quat_to_R(s_T.q, Rm);
+        quat_to_R(T.q, Rm);
         for (int i = 0; i < 3; i++) {
             for (int j = 0; j < 3; j++) R->Tcw[i * 4 + j] = (float)Rm[i][j];
-            R->Tcw[i * 4 + 3] = (float)s_T.t[i];
+            R->Tcw[i * 4 + 3] = (float)T.t[i];
         }
         R->Tcw[12] = R->Tcw[13] = R->Tcw[14] = 0.f;
         R->Tcw[15] = 1.f;
         R->pnp_inliers = ne - nBad;
     }
-    __syncthreads();
-    for (int i = t; i < n2; i += PNP_THREADS) mask[i] = mask[i] == 1 ? 1 : 0;
+    for (int k = lane; k < ne; k += PNP_NT) mask[E.idx[k]] = (E.flags[k] & PE_OUT) ? 0 : 1;
 }
 
 }  // namespace odo
 
 namespace odo {
-size_t pnp_edge_bytes() { return sizeof(PEdge); }
+size_t pnp_edge_bytes() { return 48; }
 void launch_pnp(hipStream_t st, const int32_t* f2_src, const float* xyz, const float* kun, const float* ur,
                 const int* nkp, int kp_cap, int slot0, FrameCalib cal, const float* T12, const int* pair_valid,
                 const int* n_matches, int min_matches, void* edges, odo_pair_result* res, uint8_t* inlier_mask,
                 int npairs) {
-    hipLaunchKernelGGL(k_pnp, dim3(npairs), dim3(PNP_THREADS), 0, st, f2_src, xyz, kun, ur, nkp, kp_cap, slot0, cal,
-                       T12, pair_valid, n_matches, min_matches, (PEdge*)edges, res, inlier_mask);
+    hipLaunchKernelGGL(k_pnp, dim3(npairs), dim3(PNP_NT), 0, st, f2_src, xyz, kun, ur, nkp, kp_cap, slot0, cal, T12,
+                       pair_valid, n_matches, min_matches, edges, res, inlier_mask);
+}
+}  // namespace odo
+
+// fixed-order block reduction (4 waves) used by the Kabsch kernel
+namespace odo {
+template <int NV>
+ODO_INLINE void block_reduce(double (&v)[NV], double* red /* 4*NV */) {
+#pragma unroll
+    for (int k = 0; k < NV; k++) v[k] = wave_sum(v[k]);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __syncthreads();
+    if (lane == 0)
+        for (int k = 0; k < NV; k++) red[wave * NV + k] = v[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NV; k++) v[k] = ((red[k] + red[NV + k]) + red[2 * NV + k]) + red[3 * NV + k];
+    __syncthreads();
 }
 }  // namespace odo
 

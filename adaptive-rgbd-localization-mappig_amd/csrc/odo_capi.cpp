@@ -330,8 +330,7 @@ static int alloc_buffers(odo_ctx* c) {
     while (pw < c->kp_cap) pw <<= 1;
     if ((e = dalloc(&c->sort_scratch, B * std::max(pw, c->kp_cap)))) return e;
     if ((e = dalloc(&c->latch, 1))) return e;
-    if ((e = dalloc((uint8_t**)&c->gpts, B * c->match_cap * ransac_gpt_bytes()))) return e;
-    if ((e = dalloc(&c->masks, B * 2 * c->mask_words * 256))) return e;
+    if ((e = dalloc((uint8_t**)&c->gpts, ransac_scratch_bytes((int)B, c->match_cap, c->mask_words)))) return e;
     if ((e = dalloc(&c->best_mask, B * c->mask_words))) return e;
     if ((e = dalloc(&c->res, B))) return e;
     if ((e = dalloc(&c->T12, B * 16))) return e;
@@ -507,7 +506,7 @@ static int run_pairs(odo_ctx* c, int n) {
                  c->cfg.ransac.min_inlier_th, c->cfg.ransac.sample_size, c->cfg.ransac.iterations, c->pair_valid);
     hipEventRecord(c->ev[7], st);
     launch_ransac(st, c->good, c->n_good, c->n_matches, c->matches, c->xyz, c->kp_cap, 0, c->match_cap, c->rcfg,
-                  c->latch, (uint64_t)c->cfg.seed, c->pair_counter, c->pair_valid, 20, nullptr, c->gpts, c->masks,
+                  c->latch, (uint64_t)c->cfg.seed, c->pair_counter, c->pair_valid, 20, nullptr, c->gpts,
                   c->best_mask, c->mask_words, c->res, c->T12, n);
     hipEventRecord(c->ev[8], st);
     launch_pnp(st, c->f2_src, c->xyz, c->kun, c->ur, c->nkp, c->kp_cap, 0, c->cal, c->T12, c->pair_valid,
@@ -846,8 +845,7 @@ int odo_ransac(odo_ctx* c, const odo_dmatch* m12, int n12, const float* xyz1, in
     const int words = (ng + 31) / 32;
     DevBuf dxyz((size_t)2 * kc * 3 * sizeof(float)), dm((size_t)ng * sizeof(odo_dmatch)), dg((size_t)ng * 8);
     DevBuf dint(4 * sizeof(int)), dlatch(sizeof(double)), drng(sizeof(odo_rng)), dres(sizeof(odo_pair_result));
-    DevBuf dT(16 * sizeof(float)), dgp((size_t)ng * ransac_gpt_bytes()), dmask((size_t)2 * words * 256 * 4),
-        dbm((size_t)words * 4);
+    DevBuf dT(16 * sizeof(float)), dgp(ransac_scratch_bytes(1, ng, words)), dbm((size_t)words * 4);
     std::vector<uint64_t> gl(ng);
     for (int k = 0; k < ng; k++) {
         uint32_t bits;
@@ -867,8 +865,8 @@ int odo_ransac(odo_ctx* c, const odo_dmatch* m12, int n12, const float* xyz1, in
     RansacCfg cfg{p->iterations, p->min_inlier_th, p->max_mahalanobis, p->sample_size, p->check_depth, rsx * rsx,
                   rsy * rsy};
     launch_ransac(st, dg.p, dint.as<int>(), dint.as<int>() + 1, dm.as<odo_dmatch>(), dxyz.as<float>(), kc, 0, ng, cfg,
-                  dlatch.as<double>(), 0, 0, dint.as<int>() + 2, 0, drng.as<odo_rng>(), dgp.p, dmask.as<uint32_t>(),
-                  dbm.as<uint32_t>(), words, dres.as<odo_pair_result>(), dT.as<float>(), 1);
+                  dlatch.as<double>(), 0, 0, dint.as<int>() + 2, 0, drng.as<odo_rng>(), dgp.p, dbm.as<uint32_t>(),
+                  words, dres.as<odo_pair_result>(), dT.as<float>(), 1);
     HIPCHK(hipGetLastError());
     odo_pair_result r;
     std::vector<uint32_t> bm(words);

@@ -90,8 +90,8 @@ size_t ransac_gpt_bytes();
 void launch_ransac(hipStream_t st, const void* good, const int* n_good, const int* n_matches, const odo_dmatch* matches,
                    const float* xyz, int kp_cap, int slot0, int match_cap, RansacCfg cfg, const double* latch,
                    uint64_t seed_base, uint64_t pair_base, const int* pair_valid, int min_matches, odo_rng* rng_io,
-                   void* gpts, uint32_t* masks, uint32_t* best_mask, int mask_words_cap, odo_pair_result* res,
-                   float* T12, int npairs);
+                   void* scratch, uint32_t* best_mask, int mask_words, odo_pair_result* res, float* T12, int npairs);
+size_t ransac_scratch_bytes(int npairs, int match_cap, int mask_words);
 size_t pnp_edge_bytes();
 void launch_pnp(hipStream_t st, const int32_t* f2_src, const float* xyz, const float* kun, const float* ur,
                 const int* nkp, int kp_cap, int slot0, FrameCalib cal, const float* T12, const int* pair_valid,

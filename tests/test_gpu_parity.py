@@ -158,3 +158,112 @@ def test_knn2_entry_point(pkg):
     gd = np.zeros((777, 2), np.int32)
     pkg.check(lib.odo_knn2_hamming(odo.h, pkg.ptr(q), 777, pkg.ptr(t), 1025, pkg.ptr(gi), pkg.ptr(gd)))
     assert np.array_equal(gi, ri) and np.array_equal(gd, rd)
+
+
+def _frames_cfg1():
+    bgr, dep, _ = sequence(3, seed=0x5EED0001)
+    cal = O.fr1_calib()
+    return bgr, dep, cal, [O.extract_frame(bgr[i], dep[i], O.orb_params(1000), cal) for i in range(3)]
+
+
+def test_extract_entry_point_bgr_and_gray(pkg):
+    bgr, dep, cal, frames = _frames_cfg1()
+    odo, _ = make_odo(pkg, 640, 480, 1000, 200, 1)
+    lib = pkg.load()
+    cap = 1100
+    for channels in (3, 1):
+        img = np.ascontiguousarray(bgr[0] if channels == 3 else O.gray(bgr[0]))
+        kps = np.zeros(cap, pkg.KP_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        kun = np.zeros((cap, 2), np.float32)
+        xyz = np.zeros((cap, 3), np.float32)
+        ur = np.zeros(cap, np.float32)
+        n = O.C.c_int(0)
+        pkg.check(lib.odo_extract(odo.h, pkg.ptr(img), channels, pkg.ptr(np.ascontiguousarray(dep[0])), pkg.ptr(kps),
+                                  pkg.ptr(desc), pkg.ptr(kun), pkg.ptr(xyz), pkg.ptr(ur), cap, O.C.byref(n)))
+        ref = frames[0]
+        assert n.value == len(ref["kps"])
+        assert np.array_equal(kps[:n.value], ref["kps"]) and np.array_equal(desc[:n.value], ref["desc"])
+        assert np.array_equal(xyz[:n.value], ref["xyz"])
+
+
+@pytest.mark.parametrize("iters", [1, 200, 500])
+def test_ransac_entry_point_stream_and_latch(pkg, iters):
+    """odo_ransac == Ransac::Iterate: bit-exact T12/rmse/inliers, rand() stream
+    advanced by exactly the visited draws, latch set on first call."""
+    bgr, dep, cal, frames = _frames_cfg1()
+    f1, f2 = frames[0], frames[1]
+    n1, n2 = len(f1["kps"]), len(f2["kps"])
+    has = np.zeros(n1, np.uint8)
+    O.lib().oracle_vo_landmarks(O.ptr(f1["xyz"]), n1, 40 * 40 / 517.3, O.ptr(has))
+    obs2 = np.full(n2, -1, np.int32)
+    src2 = np.full(n2, -1, np.int32)
+    out2 = np.zeros(n2, np.uint8)
+    m = np.zeros(n1, O.DMATCH_DTYPE)
+    nm = O.lib().oracle_knn_match(O.ptr(f1["desc"]), n1, O.ptr(f2["desc"]), n2, 0.9, O.ptr(has),
+                                  O.ptr(np.zeros(n1, np.uint8)), O.ptr(np.zeros(n1, np.int32)), O.ptr(obs2),
+                                  O.ptr(src2), O.ptr(out2), O.ptr(m), n1)
+    m = m[:nm]
+    rp = O.ransac_params(iters)
+    odo, _ = make_odo(pkg, 640, 480, 1000, iters, 1)
+    lib = pkg.load()
+    for trial in range(2):
+        r_ref, r_gpu = O.Rng(), pkg.Rng()
+        O.lib().oracle_rng_seed(O.C.byref(r_ref), 777 + trial)
+        lib.odo_rng_seed(pkg.ptr(r_gpu), 777 + trial)
+        lat_ref = O.C.c_double(float("nan") if trial == 0 else 1e-3)
+        lat_gpu = O.C.c_double(lat_ref.value)
+        T_ref = np.zeros(16, np.float32)
+        rmse_ref = O.C.c_float(0)
+        inl_ref = np.zeros(nm, O.DMATCH_DTYPE)
+        ni_ref, vis, ng = O.C.c_int(0), O.C.c_int(0), O.C.c_int(0)
+        ok_ref = O.lib().oracle_ransac(O.ptr(m), nm, O.ptr(f1["xyz"]), O.ptr(f2["xyz"]), O.C.byref(rp),
+                                       O.C.byref(r_ref), O.C.byref(lat_ref), O.ptr(T_ref), O.C.byref(rmse_ref),
+                                       O.ptr(inl_ref), O.C.byref(ni_ref), O.C.byref(vis), O.C.byref(ng))
+        T = np.zeros(16, np.float32)
+        rmse = O.C.c_float(0)
+        inl = np.zeros(nm, O.DMATCH_DTYPE)
+        ni, ok = O.C.c_int(0), O.C.c_int(0)
+        rpg = pkg.RansacParams(iters, 20, 3.0, 4, 1)
+        pkg.check(lib.odo_ransac(odo.h, pkg.ptr(m), nm, pkg.ptr(f1["xyz"]), n1, pkg.ptr(f2["xyz"]), n2,
+                                 pkg.ptr(rpg), pkg.ptr(r_gpu), O.C.byref(lat_gpu), pkg.ptr(T), O.C.byref(rmse),
+                                 pkg.ptr(inl), O.C.byref(ni), O.C.byref(ok)))
+        assert ok.value == ok_ref and ni.value == ni_ref.value
+        assert np.array_equal(T, T_ref) and rmse.value == rmse_ref.value
+        assert np.array_equal(inl[:ni.value], inl_ref[:ni_ref.value])
+        assert lat_gpu.value == lat_ref.value
+        assert list(r_gpu.state) == list(r_ref.state) and (r_gpu.fpos, r_gpu.rpos) == (r_ref.fpos, r_ref.rpos)
+
+
+def test_pnp_entry_point(pkg):
+    rng = np.random.default_rng(5)
+    from test_oracle import _pnp_problem
+    R, t, Xw, obs = _pnp_problem(rng, n=300)
+    obs[:15, 1] += 30
+    Tinit = np.eye(4, dtype=np.float32)
+    Tinit[:3, 3] = t + 0.01
+    T_ref = np.zeros(16, np.float32)
+    out_ref = np.zeros(300, np.uint8)
+    n_ref = O.lib().oracle_pnp(O.ptr(Xw), O.ptr(obs), 300, O.C.byref(O.fr1_calib()), O.ptr(Tinit.ravel()),
+                               O.ptr(T_ref), O.ptr(out_ref))
+    odo, cfg = make_odo(pkg, 640, 480, 1000, 200, 1)
+    T = np.zeros(16, np.float32)
+    out = np.zeros(300, np.uint8)
+    n = O.C.c_int(0)
+    pkg.check(pkg.load().odo_pnp_motion_ba(odo.h, pkg.ptr(Xw), pkg.ptr(obs), 300, pkg.ptr(cfg.calib),
+                                           pkg.ptr(Tinit.ravel()), pkg.ptr(T), pkg.ptr(out), O.C.byref(n)))
+    assert np.abs(T - T_ref).max() < 1e-4
+    assert n.value == n_ref and np.array_equal(out, out_ref)
+    assert np.abs(T.reshape(4, 4)[:3, 3] - t).max() < 1e-4
+
+
+def test_kabsch_entry_point(pkg):
+    rng = np.random.default_rng(9)
+    from test_oracle import _rand_rigid
+    R, t = _rand_rigid(rng)
+    A = (rng.random((500, 3)) * 2 - 1).astype(np.float32)
+    B = (A @ R.T + t + rng.normal(size=(500, 3)) * 1e-3).astype(np.float32)
+    K_ref = np.zeros(16, np.float32)
+    O.lib().oracle_kabsch(O.ptr(A), O.ptr(B), 500, O.ptr(K_ref))
+    K = pkg.kabsch(A, B)
+    assert np.abs(K.ravel() - K_ref).max() < 1e-4
