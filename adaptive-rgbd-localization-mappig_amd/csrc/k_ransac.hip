@@ -1,21 +1,26 @@
 // Ransac::Iterate(Frame*,Frame*,m12) for gfx950 (Odometry/ransac.cpp:155-267).
 //
-// Visited iterations ("hypotheses") are evaluated speculatively in rounds of
-// growing size (16, 48, 448, 512, ... — most pairs stop after the first, see
-// ransac.cpp:246-247). One wave evaluates one hypothesis: the 64 lanes split
-// the Mahalanobis sweep over the sorted good matches (ErrorFunction2, double),
-// ballots build the ordered inlier bitmask, and lane 0 folds the meanError sum
-// sequentially in match order and runs the PCL TFC recurrence over the inlier
-// set (both order-dependent, so they stay serial and bit-identical to the
-// reference). Hypothesis v uses the v-th SampleMatches draw of the pair's
-// glibc rand() stream. Between rounds a one-wave scan replays the reference's
-// ordered running-best fold with its n+=10 skips and >80% break, keeps the
-// winner's mask and draws the next round's samples.
+// The reference visits iterations one after another: SampleMatches draws a
+// minimal set from the glibc rand() stream, the refinement loop re-fits PCL's
+// TransformationFromCorrespondences to the Mahalanobis inlier set, and a
+// running best with n+=10 skips / >80% break decides when to stop. Here:
 //
-//   k_ransac_prep   per pair: early-outs, GoodPt table, RNG seed, round-0 samples
-//   k_ransac_eval   per (pair, hypothesis): refinement loop (ransac.cpp:204-231)
-//   k_ransac_scan   per pair: ordered fold (ransac.cpp:233-249), next samples
-//   k_ransac_final  per pair: identity fallback (ransac.cpp:252-264), outputs
+//   k_ransac_raw    side stream, at batch start: each pair's rand() words are
+//                   data independent (seed only), generated while frames are
+//                   still being extracted
+//   k_ransac_prep   per pair: early-outs, GoodPt table, and the minimal sets of
+//                   ALL iterations at once (parallel mod, speculative sample
+//                   lengths, ballot scan over sample starts)
+//   k_ransac_eval   one launch, one wave per iteration (hypothesis); whichever
+//                   wave completes the prefix runs the reference's ordered fold
+//                   under a lock; once it breaks, in-flight hypotheses abort
+//   k_ransac_final  per pair: identity fallback (ransac.cpp:252-264), outputs,
+//                   the caller's rand() state after exactly the visited draws
+//
+// The TFC recurrence and the meanError sum are order-dependent float/double
+// folds; they run in match order, bit-identical to the reference.
+#include <algorithm>
+
 #include "odo_device.h"
 #include "odo_internal.h"
 
@@ -31,16 +36,15 @@ struct GoodPt {
 };
 
 #define MAX_SAMPLE 8
-#define RS_BMAX 512
+#define SREC (MAX_SAMPLE + 2)  // sample record: count, ids[MAX_SAMPLE], end (draw pairs consumed after it)
 
 struct RState {
-    int32_t rng_s[31];
-    int32_t rng_f, rng_r;
-    int32_t rng0_s[31];  // stream position at entry (for the in/out API)
+    int32_t rng0_s[31];  // rand() state at entry (written by k_ransac_raw)
     int32_t rng0_f, rng0_r;
-    int active, done, n, visited, valid, best_cnt, ng, S, round_base, round_count, words, pad;
+    int active, done, ng, S, words, H;
+    // ordered fold (ransac.cpp:233-249), updated under `lock`
+    int lock, fold_pos, n, visited, valid, best_cnt, best_h, pad;
     float rmse;
-    float bestT[12];
 };
 
 struct HypRes {
@@ -58,74 +62,73 @@ struct RansacBufs {
     const float* xyz;
     int kp_cap, slot0, match_cap;
     const double* latch;
-    uint64_t seed_base, pair_base;
     const int* pair_valid;
     int min_matches;
     odo_rng* rng_io;
-    GoodPt* gpts;
-    RState* st;
-    HypRes* hyp;      // [pair][RS_BMAX]
-    int* samples;     // [pair][RS_BMAX][MAX_SAMPLE+1] (count first)
-    uint32_t* masks;  // [pair][RS_BMAX][mask_words]
+    GoodPt* gpts;      // [pair][match_cap]
+    RState* st;        // [pair]
+    HypRes* hyp;       // [pair][hcap]
+    int* samples;      // [pair][hcap][SREC], by visited index
+    int* ready;        // [pair][hcap]
+    uint32_t* masks;   // [pair][hcap][mask_words]
+    uint32_t* raw;     // [pair][rawcap] full 32-bit generator words (rand() = word >> 1)
+    int hcap, rawcap;
     uint32_t* best_mask;
     int mask_words;
     odo_pair_result* res;
     float* T12;
 };
 
-// SampleMatches (ransac.cpp:269-293) for `count` consecutive visited
-// iterations, state in LDS (dynamic indexing), one lane.
-ODO_INLINE void draw_samples(Rng& r, int ng, int S, int count, int* out) {
-    for (int v = 0; v < count; v++) {
-        int cnt = 0;
-        int ids[MAX_SAMPLE];
-        int safety = 0;
-        while (cnt < S) {
-            int id1 = (int)((uint32_t)r.next() % (uint32_t)ng);
-            int id2 = (int)((uint32_t)r.next() % (uint32_t)ng);
-            if (id1 > id2) id1 = id2;
-            bool dup = false;
-            for (int q = 0; q < cnt; q++) dup |= ids[q] == id1;
-            if (!dup) {
-                int pos = cnt;  // std::set keeps them ascending
-                while (pos > 0 && ids[pos - 1] > id1) {
-                    ids[pos] = ids[pos - 1];
-                    pos--;
-                }
-                ids[pos] = id1;
-                cnt++;
-            }
-            if (++safety > 10000) break;
-        }
-        int* o = out + v * (MAX_SAMPLE + 1);
-        o[0] = cnt;
-        for (int q = 0; q < cnt; q++) o[1 + q] = ids[q];
+ODO_INLINE int ld_relaxed(const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+ODO_INLINE void st_relaxed(int* p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+// One std::set insertion (ascending order) with statically indexed registers.
+ODO_INLINE bool set_insert(int (&ids)[MAX_SAMPLE], int& cnt, int id1) {
+    bool dup = false;
+    int less = 0;
+#pragma unroll
+    for (int q = 0; q < MAX_SAMPLE; q++) {
+        const bool v = q < cnt;
+        dup |= v && ids[q] == id1;
+        less += (v && ids[q] < id1) ? 1 : 0;
     }
+    if (dup) return false;
+#pragma unroll
+    for (int q = MAX_SAMPLE - 1; q >= 1; q--) ids[q] = q > less ? ids[q - 1] : (q == less ? id1 : ids[q]);
+    if (less == 0) ids[0] = id1;
+    cnt++;
+    return true;
 }
 
-ODO_INLINE void rng_load(Rng& r, const int32_t* s, int f, int rr) {
-    for (int i = 0; i < 31; i++) r.s[i] = s[i];
-    r.f = f;
-    r.r = rr;
+// SampleMatches (ransac.cpp:269-293) for one visited iteration: pairs of
+// rand() draws reduced to min(rand()%M, rand()%M) until S distinct ids.
+ODO_INLINE int draw_one(Rng& r, int ng, int S, int (&ids)[MAX_SAMPLE], int& used) {
+#pragma unroll
+    for (int q = 0; q < MAX_SAMPLE; q++) ids[q] = 0;
+    int cnt = 0, safety = 0;
+    while (cnt < S) {
+        int id1 = (int)((uint32_t)r.next() % (uint32_t)ng);
+        const int id2 = (int)((uint32_t)r.next() % (uint32_t)ng);
+        if (id1 > id2) id1 = id2;
+        set_insert(ids, cnt, id1);
+        if (++safety > 10000) break;
+    }
+    used = safety > 10000 ? 10001 : safety;
+    return cnt;
 }
 
-// ---- fast SampleMatches for a whole round, one wave --------------------------
-// (1) the glibc TYPE_3 stream is generated with the 31-word ring held in
-//     registers (statically indexed after rotating to phase 0),
-// (2) all lanes reduce draws to min(rand()%ng, rand()%ng) in parallel,
-// (3) every draw position d speculatively forms "the sample that starts at d"
-//     (S distinct ids, ascending = std::set order) and its length in draws,
-// (4) lane 0 chases d -> d + len(d) for the round's visited iterations,
-// (5) the stream is re-advanced by exactly the draws consumed.
-// Bit-identical to draw_samples(); overflow of the LDS window falls back to it.
-#define DRAW_MAX 2816
 
-struct SampLds {
-    uint32_t raw[2 * DRAW_MAX];
-    uint16_t mval[DRAW_MAX];
-    uint16_t len[DRAW_MAX];
-    uint16_t ids[DRAW_MAX][MAX_SAMPLE];
-};
+ODO_INLINE void lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+ODO_INLINE void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 ODO_INLINE void gen_raw(int32_t* st, int32_t& f, int32_t& r, uint32_t* out, int n) {
     uint32_t reg[31];
@@ -140,7 +143,7 @@ ODO_INLINE void gen_raw(int32_t* st, int32_t& f, int32_t& r, uint32_t* out, int 
 #pragma unroll
         for (int j = 0; j < 31; j++) {
             reg[(j + 3) % 31] += reg[j];
-            if (out) out[produced + j] = reg[(j + 3) % 31] >> 1;
+            if (out) out[produced + j] = reg[(j + 3) % 31];
         }
         produced += 31;
     }
@@ -149,10 +152,8 @@ ODO_INLINE void gen_raw(int32_t* st, int32_t& f, int32_t& r, uint32_t* out, int 
     for (int j = 0; j < 31; j++)
         if (j < rem) {
             reg[(j + 3) % 31] += reg[j];
-            if (out) out[produced + j] = reg[(j + 3) % 31] >> 1;
+            if (out) out[produced + j] = reg[(j + 3) % 31];
         }
-    // physical index of logical j is (r + j) % 31; after rem extra steps the
-    // logical origin moved by rem
 #pragma unroll
     for (int j = 0; j < 31; j++) {
         int q = r + j;
@@ -163,95 +164,242 @@ ODO_INLINE void gen_raw(int32_t* st, int32_t& f, int32_t& r, uint32_t* out, int 
     f = (r + 3) % 31;
 }
 
-// state: 31 ints + f + r in LDS (st), shared by the wave; count <= RS_BMAX.
-ODO_INLINE void round_samples(int lane, int32_t* st, int32_t* fr, int ng, int S, int count, int* out, SampLds& L) {
-    if (count <= 0) return;
-    const int D = min(DRAW_MAX, 6 * count + 64);
-    __shared__ int32_t save[33];
-    __shared__ int s_pos, s_ok;
-    if (lane == 0) {
-        for (int i = 0; i < 31; i++) save[i] = st[i];
-        save[31] = fr[0];
-        save[32] = fr[1];
-        int32_t f = fr[0], r = fr[1];
-        gen_raw(st, f, r, L.raw, 2 * D);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    for (int d = lane; d < D; d += 64) {
-        uint32_t a = L.raw[2 * d] % (uint32_t)ng, b = L.raw[2 * d + 1] % (uint32_t)ng;
-        L.mval[d] = (uint16_t)(a > b ? b : a);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    for (int d = lane; d < D; d += 64) {
-        int ids[MAX_SAMPLE];
-        int cnt = 0, k = d;
-        while (cnt < S && k < D) {
-            const int id1 = L.mval[k++];
-            bool dup = false;
-            for (int q = 0; q < cnt; q++) dup |= ids[q] == id1;
-            if (!dup) {
-                int pos = cnt;
-                while (pos > 0 && ids[pos - 1] > id1) {
-                    ids[pos] = ids[pos - 1];
-                    pos--;
-                }
-                ids[pos] = id1;
-                cnt++;
-            }
-        }
-        L.len[d] = (uint16_t)(cnt == S ? k - d : 0);
-        for (int q = 0; q < S; q++) L.ids[d][q] = (uint16_t)(q < cnt ? ids[q] : 0);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    if (lane == 0) {
-        int pos = 0, ok = 1;
-        for (int v = 0; v < count; v++) {
-            if (pos >= D || L.len[pos] == 0) {
-                ok = 0;
-                break;
-            }
-            int* o = out + v * (MAX_SAMPLE + 1);
-            o[0] = S;
-            for (int q = 0; q < S; q++) o[1 + q] = L.ids[pos][q];
-            pos += L.len[pos];
-        }
-        // restore the round-start state and advance by exactly the consumed draws
-        for (int i = 0; i < 31; i++) st[i] = save[i];
-        int32_t f = save[31], r = save[32];
-        if (ok) {
-            gen_raw(st, f, r, nullptr, 2 * pos);
-        } else {
-            Rng rr;
-            rng_load(rr, st, f, r);
-            draw_samples(rr, ng, S, count, out);
-            for (int i = 0; i < 31; i++) st[i] = rr.s[i];
-            f = rr.f;
-            r = rr.r;
-        }
-        fr[0] = f;
-        fr[1] = r;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+// Sample starting at draw d of the window; returns its length in draw pairs
+// (0 if the window ends first).
+ODO_INLINE int form_sample(const uint16_t* mval, int d, int D, int S, int (&ids)[MAX_SAMPLE]) {
+#pragma unroll
+    for (int q = 0; q < MAX_SAMPLE; q++) ids[q] = 0;
+    int cnt = 0, k = d;
+    while (cnt < S && k < D) set_insert(ids, cnt, (int)mval[k++]);
+    return cnt == S ? k - d : 0;
 }
 
-__global__ void __launch_bounds__(256) k_ransac_prep(RansacBufs B, RansacCfg cfg, int round0) {
+// glibc __srandom_r into LDS: Schrage LCG fill, then 310 discards in registers.
+ODO_INLINE void seed_ring(uint32_t seedv, int32_t* st, int32_t* fr) {
+    if (seedv == 0) seedv = 1;
+    st[0] = (int32_t)seedv;
+    int32_t word = (int32_t)seedv;
+    for (int i = 1; i < 31; ++i) {
+        const long hi = word / 127773;
+        const long lo = word % 127773;
+        long w2 = 16807 * lo - 2836 * hi;
+        if (w2 < 0) w2 += 2147483647;
+        word = (int32_t)w2;
+        st[i] = word;
+    }
+    int32_t f = 3, r = 0;
+    gen_raw(st, f, r, nullptr, 310);
+    fr[0] = f;
+    fr[1] = r;
+}
+
+
+// rand() state after N generator words from the entry state (the ring holds
+// the last 31 words; the word of step k sits at logical slot (k+3)%31).
+ODO_INLINE void ring_at(const uint32_t* raw, const RState* S, int N, Rng& R) {
+    const int r0 = S->rng0_r;
+    for (int L = 0; L < 31; L++) {
+        const int k0 = (L + 28) % 31;
+        int32_t val = S->rng0_s[(r0 + L) % 31];
+        if (k0 < N) val = (int32_t)raw[k0 + 31 * ((N - 1 - k0) / 31)];
+        R.s[(r0 + L) % 31] = val;
+    }
+    R.r = (r0 + N) % 31;
+    R.f = (R.r + 3) % 31;
+}
+
+#define RAW_CHUNK 2048
+
+__global__ void __launch_bounds__(64) k_ransac_raw(RansacBufs B, uint64_t seed_base, uint64_t pair_base) {
+    const int p = blockIdx.x;
+    const int lane = threadIdx.x;
+    __shared__ int32_t s_st[31], s_fr[2];
+    __shared__ __align__(16) uint32_t s_buf[RAW_CHUNK];
+    if (lane == 0) {
+        if (B.rng_io) {
+            for (int i = 0; i < 31; i++) s_st[i] = B.rng_io->state[i];
+            s_fr[0] = B.rng_io->fpos;
+            s_fr[1] = B.rng_io->rpos;
+        } else {
+            seed_ring(pair_seed(seed_base, pair_base + (uint64_t)p), s_st, s_fr);
+        }
+    }
+    lds_sync();
+    RState* S = B.st + p;
+    if (lane < 31) S->rng0_s[lane] = s_st[lane];
+    if (lane == 0) {
+        S->rng0_f = s_fr[0];
+        S->rng0_r = s_fr[1];
+    }
+    uint32_t* out = B.raw + (size_t)p * B.rawcap;
+    int32_t f = s_fr[0], r = s_fr[1];
+    for (int o = 0; o < B.rawcap; o += RAW_CHUNK) {
+        const int n = min(RAW_CHUNK, B.rawcap - o);
+        if (lane == 0) gen_raw(s_st, f, r, s_buf, n);
+        lds_sync();
+        for (int i = lane * 4; i < n; i += 256)
+            *reinterpret_cast<uint4*>(out + o + i) = *reinterpret_cast<const uint4*>(s_buf + i);
+        lds_sync();
+    }
+}
+
+// ---------------------------------------------------------------- sampling
+// SampleMatches for every iteration of a pair (ransac.cpp:269-293): each draw
+// pair d reduces to mval[d] = min(rand()%ng, rand()%ng); the sample starting at
+// d takes S draw pairs unless an id repeats (rare), so lengths are formed
+// speculatively for every d and a ballot scan walks the chain of sample starts.
+#define SWIN 4096
+
+struct SampWin {
+    uint16_t mval[SWIN];
+    uint16_t len[SWIN];
+    uint16_t posv[SWIN];
+    int nv, e;
+};
+
+template <int S>
+ODO_INLINE int sample_len_fast(const uint16_t* mval, int d, int D) {
+    if (d + S > D) return -1;
+    int w[S];
+#pragma unroll
+    for (int q = 0; q < S; q++) w[q] = mval[d + q];
+    bool dup = false;
+#pragma unroll
+    for (int i = 0; i < S; i++)
+#pragma unroll
+        for (int j = i + 1; j < S; j++) dup |= w[i] == w[j];
+    return dup ? -1 : S;
+}
+
+ODO_INLINE int sample_len(const uint16_t* mval, int d, int D, int S) {
+    int l = -1;
+    if (S == 4) l = sample_len_fast<4>(mval, d, D);
+    else if (S == 3) l = sample_len_fast<3>(mval, d, D);
+    if (l > 0) return l;
+    int ids[MAX_SAMPLE];
+    return form_sample(mval, d, D, S, ids);
+}
+
+// ids of the sample at d (length ln): sorted window when duplicate-free.
+ODO_INLINE void sample_ids(const uint16_t* mval, int d, int D, int S, int ln, int (&ids)[MAX_SAMPLE]) {
+    if (ln == S) {
+#pragma unroll
+        for (int q = 0; q < MAX_SAMPLE; q++) ids[q] = q < S ? (int)mval[min(d + q, SWIN - 1)] : 0x7fffffff;
+#pragma unroll
+        for (int i = 0; i < MAX_SAMPLE; i++)
+#pragma unroll
+            for (int j = 0; j < MAX_SAMPLE - 1 - i; j++) {
+                const int a = ids[j], b = ids[j + 1];
+                ids[j] = a < b ? a : b;
+                ids[j + 1] = a < b ? b : a;
+            }
+    } else {
+        form_sample(mval, d, D, S, ids);
+    }
+}
+
+// One wave: chain of sample starts through the window (0, len[0], ...). Lane j
+// guesses "start of sample v+j" = base + S*j, valid up to the first irregular
+// sample; that one is resolved through its stored length.
+ODO_INLINE void chase_window(int lane, SampWin& L, int D, int S, int want) {
+    int v = 0, base = 0;
+    while (v < want) {
+        const int vv = v + lane;
+        const int pos = base + S * lane;
+        const bool inr = vv < want;
+        const int ln = (inr && pos < D) ? (int)L.len[pos] : 0;
+        const uint64_t irr = __ballot(inr && ln != S);
+        if (!irr) {
+            const int nin = __popcll(__ballot(inr));
+            if (inr) L.posv[vv] = (uint16_t)pos;
+            v += nin;
+            base += S * nin;
+            continue;
+        }
+        const int f = __builtin_ctzll(irr);
+        const int lnf = __shfl(ln, f);
+        if (lane < f || (lane == f && lnf > 0)) L.posv[vv] = (uint16_t)pos;
+        if (lnf == 0) {
+            v += f;
+            base += S * f;
+            break;
+        }
+        v += f + 1;
+        base += S * f + lnf;
+    }
+    if (lane == 0) {
+        L.nv = v;
+        L.e = base;
+    }
+}
+
+ODO_INLINE void write_rec(int* o, int cnt, const int (&ids)[MAX_SAMPLE], int end) {
+    o[0] = cnt;
+#pragma unroll
+    for (int q = 0; q < MAX_SAMPLE; q++)
+        if (q < cnt) o[1 + q] = ids[q];
+    o[SREC - 1] = end;
+}
+
+// All H samples of pair p (256 threads). Falls back to the serial draw when
+// the generated words run out (only with extreme duplicate rates).
+ODO_INLINE void pair_samples(const RansacBufs& B, int p, int ng, int S, int H, SampWin& L, Rng& R) {
+    const int t = threadIdx.x;
+    const uint32_t* raw = B.raw + (size_t)p * B.rawcap;
+    int* rec = B.samples + (size_t)p * B.hcap * SREC;
+    const int total = B.rawcap / 2;
+    int v = 0, pos = 0;
+    while (v < H) {
+        const int D = min(SWIN, total - pos);
+        if (D <= 0) break;
+        for (int d = t; d < D; d += blockDim.x) {
+            const uint2 w = *reinterpret_cast<const uint2*>(raw + 2 * (size_t)(pos + d));
+            const uint32_t a = (w.x >> 1) % (uint32_t)ng, b = (w.y >> 1) % (uint32_t)ng;
+            L.mval[d] = (uint16_t)(a > b ? b : a);
+        }
+        __syncthreads();
+        for (int d = t; d < D; d += blockDim.x) L.len[d] = (uint16_t)sample_len(L.mval, d, D, S);
+        __syncthreads();
+        if (t < 64) chase_window(t, L, D, S, H - v);
+        __syncthreads();
+        const int nv = L.nv, e = L.e;
+        for (int i = t; i < nv; i += blockDim.x) {
+            const int d = L.posv[i];
+            const int ln = L.len[d];
+            int ids[MAX_SAMPLE];
+            sample_ids(L.mval, d, D, S, ln, ids);
+            write_rec(rec + (size_t)(v + i) * SREC, S, ids, pos + d + ln);
+        }
+        __syncthreads();
+        const bool last = pos + D >= total;
+        v += nv;
+        pos += e;
+        if (last && v < H) break;
+    }
+    if (v < H && t == 0) {
+        // serial continuation from the generator state after 2*pos words
+        ring_at(raw, B.st + p, 2 * pos, R);
+        for (; v < H; v++) {
+            int ids[MAX_SAMPLE];
+            int used = 0;
+            const int cnt = draw_one(R, ng, S, ids, used);
+            pos += used;
+            write_rec(rec + (size_t)v * SREC, cnt, ids, pos);
+        }
+    }
+}
+
+
+__global__ void __launch_bounds__(256) k_ransac_prep(RansacBufs B, RansacCfg cfg) {
     const int p = blockIdx.x;
     const int t = threadIdx.x;
-    __shared__ Rng s_rng;
     RState* S = B.st + p;
     odo_pair_result* R = B.res + p;
     float* T12o = B.T12 + (size_t)p * 16;
     const int ng = B.n_good[p];
     const int nm = B.n_matches[p];
-    const int Ssz = cfg.sample_size < MAX_SAMPLE ? cfg.sample_size : MAX_SAMPLE;
+    const int Ssz = min(max(cfg.sample_size, 1), MAX_SAMPLE);
+    const int H = cfg.iterations;
     bool active = B.pair_valid[p] && nm >= B.min_matches && nm >= cfg.min_inlier_th;
     if (t == 0) {
         R->rmse = 1e6f;
@@ -263,6 +411,7 @@ __global__ void __launch_bounds__(256) k_ransac_prep(RansacBufs B, RansacCfg cfg
     }
     active = active && ng >= cfg.min_inlier_th;
     const int words = (ng + 31) >> 5;
+    const bool done = !active || H <= 0 || ng < Ssz;
     if (active) {
         const SortElR* G = B.good + (size_t)p * B.match_cap;
         const odo_dmatch* M = B.matches + (size_t)p * B.match_cap;
@@ -278,147 +427,331 @@ __global__ void __launch_bounds__(256) k_ransac_prep(RansacBufs B, RansacCfg cfg
             g.tx = X2[3 * m.trainIdx];
             g.ty = X2[3 * m.trainIdx + 1];
             g.tz = X2[3 * m.trainIdx + 2];
-            g.w = 1.0f / (g.sz * g.tz);
+            g.w = 1.0f / (g.sz * g.tz);  // ransac.cpp:305
             g.pad = 0.f;
             P[k] = g;
         }
         uint32_t* BM = B.best_mask + (size_t)p * B.mask_words;
         for (int w = t; w < words; w += 256) BM[w] = 0;
+        if (!done) {
+            int* rd = B.ready + (size_t)p * B.hcap;
+            for (int h = t; h < H; h += 256) rd[h] = 0;
+        }
     }
     if (t == 0) {
-        if (B.rng_io) {
-            for (int i = 0; i < 31; i++) s_rng.s[i] = B.rng_io->state[i];
-            s_rng.f = B.rng_io->fpos;
-            s_rng.r = B.rng_io->rpos;
-        } else {
-            s_rng.seed(pair_seed(B.seed_base, B.pair_base + (uint64_t)p));
-        }
-        for (int i = 0; i < 31; i++) S->rng0_s[i] = s_rng.s[i];
-        S->rng0_f = s_rng.f;
-        S->rng0_r = s_rng.r;
         S->active = active ? 1 : 0;
         S->ng = ng;
         S->S = Ssz;
         S->words = words;
+        S->H = H;
+        S->done = done ? 1 : 0;
+        S->lock = 0;
+        S->fold_pos = 0;
         S->n = 0;
         S->visited = 0;
         S->valid = 0;
         S->best_cnt = 0;
+        S->best_h = -1;
         S->rmse = 1e6f;
-        for (int i = 0; i < 12; i++) S->bestT[i] = (i % 5 == 0) ? 1.f : 0.f;
-        S->round_base = 0;
-        const int H = cfg.iterations;
-        S->done = (!active || H <= 0 || ng < Ssz) ? 1 : 0;
-        S->round_count = S->done ? 0 : min(round0, H);
     }
-    __syncthreads();
-    __shared__ SampLds s_L;
-    __shared__ int32_t s_st[31], s_fr[2];
-    const int cnt = S->round_count;
-    if (t < 64 && cnt > 0) {
-        if (t == 0) {
-            for (int i = 0; i < 31; i++) s_st[i] = s_rng.s[i];
-            s_fr[0] = s_rng.f;
-            s_fr[1] = s_rng.r;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        round_samples(t, s_st, s_fr, ng, Ssz, cnt, B.samples + (size_t)p * RS_BMAX * (MAX_SAMPLE + 1), s_L);
-        if (t == 0) {
-            for (int i = 0; i < 31; i++) S->rng_s[i] = s_st[i];
-            S->rng_f = s_fr[0];
-            S->rng_r = s_fr[1];
-        }
-    } else if (t == 0 && cnt == 0) {
-        for (int i = 0; i < 31; i++) S->rng_s[i] = s_rng.s[i];
-        S->rng_f = s_rng.f;
-        S->rng_r = s_rng.r;
-    }
+    if (done) return;
+    __shared__ SampWin s_win;
+    __shared__ Rng s_rng;
+    pair_samples(B, p, ng, Ssz, H, s_win, s_rng);
 }
 
 // ---------------------------------------------------------------- eval
 #define EV_WAVES 4
+#define EV_ROWS0 2
 
-ODO_INLINE void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+struct EvalLds {
+    uint32_t cur[256];  // current inlier set (refined), bit k = good match k
+    uint32_t nw[256];   // set produced by the sweep
+    // compacted TFC input chunk, SoA: sx sy sz tx ty tz w
+    __attribute__((aligned(16))) float pv[7][64];
+    __attribute__((aligned(16))) float acc[64];
+    __attribute__((aligned(16))) float alpha[64];
+    __attribute__((aligned(16))) float oma[64];
+    double dv[64];      // compacted Mahalanobis terms of one sweep chunk
+};
+
+ODO_INLINE bool tfc_point_ok(const GoodPt& g) {
+    return !__builtin_isnan(g.sz) && !__builtin_isnan(g.tz) && g.w != 0.0f;  // ransac.cpp:303, TFC::add
 }
 
-__global__ void __launch_bounds__(64 * EV_WAVES) k_ransac_eval(RansacBufs B, RansacCfg cfg) {
-    const int p = blockIdx.x;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    __shared__ uint32_t s_cur[EV_WAVES][256];   // current inlier set (refined), bit k = good match k
-    __shared__ uint32_t s_new[EV_WAVES][256];   // set produced by the sweep
-    __shared__ GoodPt s_pts[EV_WAVES][64];
-    __shared__ double s_d2[EV_WAVES][64];
-    const RState* S = B.st + p;
-    if (S->done) return;
-    const int count = S->round_count;
-    const int ng = S->ng, words = S->words;
-    const GoodPt* P = B.gpts + (size_t)p * B.match_cap;
+ODO_INLINE void stage_pt(EvalLds& L, int q, const GoodPt& g) {
+    L.pv[0][q] = g.sx;
+    L.pv[1][q] = g.sy;
+    L.pv[2][q] = g.sz;
+    L.pv[3][q] = g.tx;
+    L.pv[4][q] = g.ty;
+    L.pv[5][q] = g.tz;
+    L.pv[6][q] = g.w;
+}
+
+ODO_INLINE uint32_t lane_rank(uint64_t bal) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
+}
+
+// PCL TransformationFromCorrespondences::add over pts[0..nin), bit-identical
+// to the serial add(): lane 0 runs the accumulated-weight prefix, all lanes
+// form alpha = w/acc in parallel, then lane (i,j) < 9 runs three independent
+// chains per point — m1[j], m2[i] (recomputed redundantly, same operations)
+// and cov[i][j] — so the wave issues them interleaved instead of waiting on
+// one dependent chain.
+ODO_INLINE void tfc_fold(EvalLds& L, int nin, int lane, float& acc, float& m1, float& m2, float& c) {
+    if (nin <= 0) return;
+
+    if (lane == 0) {
+        float a = acc;
+        for (int q0 = 0; q0 < nin; q0 += 16) {
+            float wv[16];
+#pragma unroll
+            for (int u = 0; u < 16; u += 4) {
+                const float4 v = *reinterpret_cast<const float4*>(&L.pv[6][q0 + u]);
+                wv[u] = v.x;
+                wv[u + 1] = v.y;
+                wv[u + 2] = v.z;
+                wv[u + 3] = v.w;
+            }
+            if (q0 + 16 <= nin) {
+#pragma unroll
+                for (int u = 0; u < 16; u++) {
+                    a += wv[u];
+                    L.acc[q0 + u] = a;
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < 16; u++) {
+                    a = (q0 + u < nin) ? a + wv[u] : a;
+                    L.acc[q0 + u] = a;
+                }
+            }
+        }
+        acc = a;
+    }
+    wave_sync();
+    if (lane < nin) {
+        const float al = L.pv[6][lane] / L.acc[lane];
+        L.alpha[lane] = al;
+        L.oma[lane] = 1.0f - al;
+    }
+    wave_sync();
+    if (lane < 9) {
+        const int i = lane / 3, j = lane - 3 * (lane / 3);
+        const float* s1 = L.pv[j];
+        const float* s2 = L.pv[3 + i];
+        float a1 = m1, a2 = m2, cc = c;
+        for (int q0 = 0; q0 < nin; q0 += 16) {
+            float P1[16], P2[16], AL[16], OM[16];
+#pragma unroll
+            for (int u = 0; u < 16; u += 4) {
+                const float4 a = *reinterpret_cast<const float4*>(s1 + q0 + u);
+                const float4 b = *reinterpret_cast<const float4*>(s2 + q0 + u);
+                const float4 e = *reinterpret_cast<const float4*>(&L.alpha[q0 + u]);
+                const float4 o = *reinterpret_cast<const float4*>(&L.oma[q0 + u]);
+                P1[u] = a.x, P1[u + 1] = a.y, P1[u + 2] = a.z, P1[u + 3] = a.w;
+                P2[u] = b.x, P2[u + 1] = b.y, P2[u + 2] = b.z, P2[u + 3] = b.w;
+                AL[u] = e.x, AL[u + 1] = e.y, AL[u + 2] = e.z, AL[u + 3] = e.w;
+                OM[u] = o.x, OM[u + 1] = o.y, OM[u + 2] = o.z, OM[u + 3] = o.w;
+            }
+            if (q0 + 16 <= nin) {
+#pragma unroll
+                for (int u = 0; u < 16; u++) {
+                    const float d1 = P1[u] - a1;
+                    const float d2 = P2[u] - a2;
+                    const float ad2 = AL[u] * d2;
+                    cc = OM[u] * (cc + ad2 * d1);
+                    a1 = a1 + AL[u] * d1;
+                    a2 = a2 + ad2;
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < 16; u++) {
+                    const bool on = q0 + u < nin;
+                    const float d1 = P1[u] - a1;
+                    const float d2 = P2[u] - a2;
+                    const float ad2 = AL[u] * d2;
+                    cc = on ? OM[u] * (cc + ad2 * d1) : cc;
+                    a1 = on ? a1 + AL[u] * d1 : a1;
+                    a2 = on ? a2 + ad2 : a2;
+                }
+            }
+        }
+        m1 = a1;
+        m2 = a2;
+        c = cc;
+    }
+    wave_sync();
+}
+
+// Ordered sum of dv[0..nin) (lane 0), 16 loads ahead.
+ODO_INLINE double fold_dv(const EvalLds& L, int nin, double s) {
+    for (int q0 = 0; q0 < nin; q0 += 16) {
+        double v[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) v[u] = L.dv[q0 + u];
+        if (q0 + 16 <= nin) {
+#pragma unroll
+            for (int u = 0; u < 16; u++) s += v[u];
+        } else {
+#pragma unroll
+            for (int u = 0; u < 16; u++) s = (q0 + u < nin) ? s + v[u] : s;
+        }
+    }
+    return s;
+}
+
+
+// The pair's good-match table is staged in LDS (shared by the workgroup's
+// waves) when it fits; every refinement sweeps it twice.
+#define PCACHE 1024
+extern __shared__ __align__(16) uint8_t ev_dyn[];
+
+template <bool CACHED>
+ODO_INLINE GoodPt load_pt(const GoodPt* P, int k) {
+    if (CACHED) return reinterpret_cast<const GoodPt*>(ev_dyn)[k];
+    return P[k];
+}
+
+// Ordered fold of finished hypotheses (ransac.cpp:233-249), lane 0 only.
+// Whoever completes the visited prefix folds it; a wave that finds the lock
+// taken leaves, the holder re-checks after releasing it.
+ODO_INLINE void try_fold(const RansacBufs& B, const RansacCfg& cfg, int p) {
+    RState* S = B.st + p;
+    int* ready = B.ready + (size_t)p * B.hcap;
+    const HypRes* hyp = B.hyp + (size_t)p * B.hcap;
+    const unsigned minInl = (unsigned)cfg.min_inlier_th;
+    while (true) {
+        if (atomicCAS(&S->lock, 0, 1) != 0) return;
+        __threadfence();
+        const int H = S->H, ng = S->ng;
+        int pos = ld_relaxed(&S->fold_pos), n = ld_relaxed(&S->n), visited = ld_relaxed(&S->visited);
+        int valid = ld_relaxed(&S->valid), best = ld_relaxed(&S->best_cnt), best_h = ld_relaxed(&S->best_h);
+        float rmse = __int_as_float(ld_relaxed(reinterpret_cast<const int*>(&S->rmse)));
+        bool fin = n >= H;
+        while (!fin && pos < H) {
+            if (!__hip_atomic_load(&ready[pos], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) break;
+            const unsigned rc = (unsigned)ld_relaxed(&hyp[pos].cnt);
+            const double re = __longlong_as_double(__hip_atomic_load(
+                reinterpret_cast<const long long*>(&hyp[pos].err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            visited++;
+            bool brk = false;
+            if (rc > 0) {
+                valid++;
+                if (re <= (double)rmse && rc >= (unsigned)best && rc >= minInl) {
+                    rmse = (float)re;
+                    best = (int)rc;
+                    best_h = pos;
+                    if (rc > ng * 0.5) n += 10;
+                    if (rc > ng * 0.75) n += 10;
+                    if (rc > ng * 0.8) brk = true;
+                }
+            }
+            n++;
+            if (brk) n = H;
+            pos++;
+            fin = n >= H;
+        }
+        st_relaxed(&S->fold_pos, pos);
+        st_relaxed(&S->n, n);
+        st_relaxed(&S->visited, visited);
+        st_relaxed(&S->valid, valid);
+        st_relaxed(&S->best_cnt, best);
+        st_relaxed(&S->best_h, best_h);
+        st_relaxed(reinterpret_cast<int*>(&S->rmse), __float_as_int(rmse));
+        if (fin) st_relaxed(&S->done, 1);
+        __threadfence();
+        atomicExch(&S->lock, 0);
+        __threadfence();
+        if (fin) return;
+        if (!__hip_atomic_load(&ready[pos], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) return;
+    }
+}
+
+template <bool CACHED>
+ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int wave, int lane, EvalLds& L,
+                          const GoodPt* P, int ng, int words, int H, int y0) {
+    RState* S = B.st + p;
+    const int* smp0 = B.samples + (size_t)p * B.hcap * SREC;
     MahalConst K;
     K.raster_cov_x = cfg.raster_cov_x;
     K.raster_cov_y = cfg.raster_cov_y;
     K.depth_cov = *B.latch;
     const float th = cfg.max_mahal * cfg.max_mahal;
     const unsigned minInl = (unsigned)cfg.min_inlier_th;
-    uint32_t* cur = s_cur[wave];
-    uint32_t* nw = s_new[wave];
-    GoodPt* pts = s_pts[wave];
-    double* d2s = s_d2[wave];
-    for (int h = blockIdx.y * EV_WAVES + wave; h < count; h += gridDim.y * EV_WAVES) {
-        const int* smp = B.samples + ((size_t)p * RS_BMAX + h) * (MAX_SAMPLE + 1);
+    // this launch covers hypothesis rows [y0, y0 + gridDim.y)
+    const int hend = min(H, (y0 + (int)gridDim.y) * EV_WAVES);
+    for (int h = (y0 + blockIdx.y) * EV_WAVES + wave; h < hend; h += gridDim.y * EV_WAVES) {
+        const int* smp = smp0 + (size_t)h * SREC;
         double refinedError = 1e6;
         unsigned refinedCnt = 0;
         float refinedT[12];
         for (int i = 0; i < 12; i++) refinedT[i] = (i % 5 == 0) ? 1.f : 0.f;
-        bool useSample = true;
+        bool useSample = true, aborted = false;
+#ifdef ODO_RANSAC_PROFILE
+        // -DODO_RANSAC_PROFILE: per-hypothesis phase times (10 ns ticks) via printf
+        uint64_t t_tfc = 0, t_get = 0, t_sweep = 0, t0 = 0, t_start = wall_clock64();
+        int nref = 0;
+#define RP_T0() t0 = wall_clock64()
+#define RP_ACC(x) x += wall_clock64() - t0
+#else
+#define RP_T0()
+#define RP_ACC(x)
+#endif
         for (int refinements = 1; refinements < 20; refinements++) {
-            // ---- GetTransformFromMatches (ransac.cpp:295-313): lane 0, in set order
-            TFC tfc;
-            tfc.reset();
+            // ---- GetTransformFromMatches (ransac.cpp:295-313), in set order
+            float tacc = 0.f, tm1 = 0.f, tm2 = 0.f, tc = 0.f;
+            RP_T0();
             if (useSample) {
-                if (lane == 0) {
-                    const int ns = smp[0];
-                    for (int q = 0; q < ns; q++) {
-                        const GoodPt g = P[smp[1 + q]];
-                        if (__builtin_isnan(g.sz) || __builtin_isnan(g.tz)) continue;
-                        tfc.add(g.sx, g.sy, g.sz, g.tx, g.ty, g.tz, g.w);
-                    }
+                const int ns = smp[0];
+                bool in = false;
+                GoodPt g;
+                if (lane < ns) {
+                    g = load_pt<CACHED>(P, smp[1 + lane]);
+                    in = tfc_point_ok(g);
                 }
+                const uint64_t bal = __ballot(in);
+                if (in) stage_pt(L, lane_rank(bal), g);
+                wave_sync();
+                tfc_fold(L, __popcll(bal), lane, tacc, tm1, tm2, tc);
             } else {
                 for (int c0 = 0; c0 < ng; c0 += 64) {
                     const int k = c0 + lane;
-                    const bool in = k < ng && ((cur[k >> 5] >> (k & 31)) & 1);
+                    bool in = false;
+                    GoodPt g;
+                    if (k < ng && ((L.cur[k >> 5] >> (k & 31)) & 1)) {
+                        g = load_pt<CACHED>(P, k);
+                        in = tfc_point_ok(g);
+                    }
                     const uint64_t bal = __ballot(in);
-                    if (in) {
-                        const int pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
-                        pts[pos] = P[k];
-                    }
+                    if (in) stage_pt(L, lane_rank(bal), g);
                     wave_sync();
-                    if (lane == 0) {
-                        const int nin = __popcll(bal);
-                        for (int q = 0; q < nin; q++) {
-                            const GoodPt g = pts[q];
-                            if (__builtin_isnan(g.sz) || __builtin_isnan(g.tz)) continue;
-                            tfc.add(g.sx, g.sy, g.sz, g.tx, g.ty, g.tz, g.w);
-                        }
-                    }
-                    wave_sync();
+                    tfc_fold(L, __popcll(bal), lane, tacc, tm1, tm2, tc);
                 }
             }
-            float Tl[12];
-            for (int i = 0; i < 12; i++) Tl[i] = 0.f;
-            if (lane == 0) tfc.get(Tl);
-            float T[12];
+            RP_ACC(t_tfc);
+            RP_T0();
+            TFC tf;
+            tf.accW = __shfl(tacc, 0);
 #pragma unroll
-            for (int i = 0; i < 12; i++) T[i] = __shfl(Tl[i], 0);
+            for (int i = 0; i < 3; i++) {
+                tf.m1[i] = __shfl(tm1, i);
+                tf.m2[i] = __shfl(tm2, 3 * i);
+#pragma unroll
+                for (int j = 0; j < 3; j++) tf.cov[i][j] = __shfl(tc, 3 * i + j);
+            }
+            float T[12];
+            tf.get(T);
             double Td[12];
 #pragma unroll
             for (int i = 0; i < 12; i++) Td[i] = (double)T[i];
+            RP_ACC(t_get);
+            RP_T0();
+            // poll the fold's stop flag once per refinement: issued here, read
+            // after the sweep (one memory-coherent load per wave per refinement;
+            // polling per chunk hot-spots the flag's line)
+            const int dn = ld_relaxed(&S->done);
             // ---- ComputeInliersAndError (ransac.cpp:315-348)
             double meanError = 0.0;
             unsigned cnt = 0;
@@ -427,7 +760,7 @@ __global__ void __launch_bounds__(64 * EV_WAVES) k_ransac_eval(RansacBufs B, Ran
                 bool in = false;
                 double d = 0.0;
                 if (k < ng) {
-                    const GoodPt g = P[k];
+                    const GoodPt g = load_pt<CACHED>(P, k);
                     if (!(g.sz == 0.0f || g.tx == 0.0f)) {
                         const float x1[3] = {g.sx, g.sy, g.sz}, x2[3] = {g.tx, g.ty, g.tz};
                         d = error_function2(x1, x2, Td, K);
@@ -435,24 +768,27 @@ __global__ void __launch_bounds__(64 * EV_WAVES) k_ransac_eval(RansacBufs B, Ran
                     }
                 }
                 const uint64_t bal = __ballot(in);
-                d2s[lane] = d;
+                if (in) L.dv[lane_rank(bal)] = d;
                 if (lane == 0) {
-                    nw[c0 >> 5] = (uint32_t)bal;
-                    if (c0 + 32 < ng) nw[(c0 >> 5) + 1] = (uint32_t)(bal >> 32);
+                    L.nw[c0 >> 5] = (uint32_t)bal;
+                    if (c0 + 32 < ng) L.nw[(c0 >> 5) + 1] = (uint32_t)(bal >> 32);
                 }
                 wave_sync();
-                if (lane == 0) {
-                    uint64_t b = bal;
-                    while (b) {
-                        const int q = __builtin_ctzll(b);
-                        b &= b - 1;
-                        meanError += d2s[q];
-                    }
-                }
-                cnt += (unsigned)__popcll(bal);
+                const int nin = __popcll(bal);
+                if (lane == 0) meanError = fold_dv(L, nin, meanError);
+                cnt += (unsigned)nin;
                 wave_sync();
             }
             meanError = __shfl(meanError, 0);
+            RP_ACC(t_sweep);
+            // the fold already stopped before this hypothesis: nothing will read it
+            if (__builtin_amdgcn_readfirstlane(dn)) {
+                aborted = true;
+                break;
+            }
+#ifdef ODO_RANSAC_PROFILE
+            nref++;
+#endif
             if (cnt < 3) meanError = 1e9;
             else {
                 meanError /= (double)cnt;
@@ -465,13 +801,19 @@ __global__ void __launch_bounds__(64 * EV_WAVES) k_ransac_eval(RansacBufs B, Ran
                 for (int i = 0; i < 12; i++) refinedT[i] = T[i];
                 refinedError = meanError;
                 refinedCnt = cnt;
-                for (int w = lane; w < words; w += 64) cur[w] = nw[w];
+                for (int w = lane; w < words; w += 64) L.cur[w] = L.nw[w];
                 wave_sync();
                 useSample = false;
                 if (cnt == prev) break;
             } else break;
         }
-        HypRes* hr = B.hyp + (size_t)p * RS_BMAX + h;
+#ifdef ODO_RANSAC_PROFILE
+        if (lane == 0)
+            printf("HYP p %d h %d ng %d ab %d nref %d inl %u tfc %lu get %lu sweep %lu total %lu\n", p, h, ng,
+                   (int)aborted, nref, refinedCnt, t_tfc, t_get, t_sweep, wall_clock64() - t_start);
+#endif
+        if (aborted) continue;
+        HypRes* hr = B.hyp + (size_t)p * B.hcap + h;
         if (lane == 0) {
             hr->err = refinedError;
             hr->cnt = (int)refinedCnt;
@@ -483,98 +825,38 @@ __global__ void __launch_bounds__(64 * EV_WAVES) k_ransac_eval(RansacBufs B, Ran
                 if (lane == i) v = refinedT[i];
             hr->T[lane] = v;
         }
-        uint32_t* mo = B.masks + ((size_t)p * RS_BMAX + h) * B.mask_words;
+        uint32_t* mo = B.masks + ((size_t)p * B.hcap + h) * B.mask_words;
         if (refinedCnt > 0)
-            for (int w = lane; w < words; w += 64) mo[w] = cur[w];
+            for (int w = lane; w < words; w += 64) mo[w] = L.cur[w];
+        __threadfence();
+        if (lane == 0) {
+            __hip_atomic_store(B.ready + (size_t)p * B.hcap + h, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            try_fold(B, cfg, p);
+        }
         wave_sync();
     }
 }
 
-// ---------------------------------------------------------------- scan
-__global__ void __launch_bounds__(64) k_ransac_scan(RansacBufs B, RansacCfg cfg, int next_count) {
+__global__ void __launch_bounds__(64 * EV_WAVES) k_ransac_eval(RansacBufs B, RansacCfg cfg, int y0) {
     const int p = blockIdx.x;
-    const int lane = threadIdx.x;
-    __shared__ Rng s_rng;
-    __shared__ int s_copy_h;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __shared__ EvalLds s_w[EV_WAVES];
     RState* S = B.st + p;
-    if (S->done) return;
+    const int H = S->H;
+    if ((y0 + (int)blockIdx.y) * EV_WAVES >= H) return;
+    __shared__ int s_done;
+    if (threadIdx.x == 0) s_done = ld_relaxed(&S->done);
+    __syncthreads();
+    if (s_done) return;  // uniform over the workgroup
     const int ng = S->ng, words = S->words;
-    const int H = cfg.iterations;
-    const unsigned minInl = (unsigned)cfg.min_inlier_th;
-    __shared__ double s_err[RS_BMAX];
-    __shared__ int s_hc[RS_BMAX];
-    __shared__ int s_next;
-    const int count0 = S->round_count;
-    for (int v = lane; v < count0; v += 64) {
-        const HypRes* hr = B.hyp + (size_t)p * RS_BMAX + v;
-        s_err[v] = hr->err;
-        s_hc[v] = hr->cnt;
-    }
-    __syncthreads();
-    if (lane == 0) {
-        s_copy_h = -1;
-        s_next = 0;
-        int n = S->n;
-        const int count = S->round_count;
-        for (int v = 0; v < count && n < H; v++) {
-            S->visited++;
-            const HypRes* hr = B.hyp + (size_t)p * RS_BMAX + v;
-            const unsigned rc = (unsigned)s_hc[v];
-            const double re = s_err[v];
-            bool brk = false;
-            if (rc > 0) {
-                S->valid++;
-                if (re <= (double)S->rmse && rc >= (unsigned)S->best_cnt && rc >= minInl) {
-                    S->rmse = (float)re;
-                    S->best_cnt = (int)rc;
-                    for (int i = 0; i < 12; i++) S->bestT[i] = hr->T[i];
-                    s_copy_h = v;
-                    if (rc > ng * 0.5) n += 10;
-                    if (rc > ng * 0.75) n += 10;
-                    if (rc > ng * 0.8) brk = true;
-                }
-            }
-            n++;
-            if (brk) {
-                n = H;
-                break;
-            }
-        }
-        S->n = n;
-        S->round_base += count;
-        if (n >= H) S->done = 1;
-        if (!S->done && next_count > 0) {
-            const int cnt = min(next_count, H - n);
-            S->round_count = cnt;
-            s_next = cnt;
-        } else {
-            S->done = 1;
-            S->round_count = 0;
-        }
-    }
-    __syncthreads();
-    if (s_next > 0) {
-        __shared__ SampLds s_L;
-        __shared__ int32_t s_st[31], s_fr[2];
-        if (lane == 0) {
-            for (int i = 0; i < 31; i++) s_st[i] = S->rng_s[i];
-            s_fr[0] = S->rng_f;
-            s_fr[1] = S->rng_r;
-        }
+    const GoodPt* P = B.gpts + (size_t)p * B.match_cap;
+    if (ng <= PCACHE) {
+        GoodPt* pc = reinterpret_cast<GoodPt*>(ev_dyn);
+        for (int k = threadIdx.x; k < ng; k += 64 * EV_WAVES) pc[k] = P[k];
         __syncthreads();
-        round_samples(lane, s_st, s_fr, ng, S->S, s_next, B.samples + (size_t)p * RS_BMAX * (MAX_SAMPLE + 1), s_L);
-        if (lane == 0) {
-            for (int i = 0; i < 31; i++) S->rng_s[i] = s_st[i];
-            S->rng_f = s_fr[0];
-            S->rng_r = s_fr[1];
-        }
-    }
-    __syncthreads();
-    const int h = s_copy_h;
-    if (h >= 0) {
-        const uint32_t* src = B.masks + ((size_t)p * RS_BMAX + h) * B.mask_words;
-        uint32_t* BM = B.best_mask + (size_t)p * B.mask_words;
-        for (int w = lane; w < words; w += 64) BM[w] = src[w];
+        eval_hyps<true>(B, cfg, p, wave, lane, s_w[wave], P, ng, words, H, y0);
+    } else {
+        eval_hyps<false>(B, cfg, p, wave, lane, s_w[wave], P, ng, words, H, y0);
     }
 }
 
@@ -582,17 +864,24 @@ __global__ void __launch_bounds__(64) k_ransac_scan(RansacBufs B, RansacCfg cfg,
 __global__ void __launch_bounds__(64) k_ransac_final(RansacBufs B, RansacCfg cfg) {
     const int p = blockIdx.x;
     const int lane = threadIdx.x;
+
     __shared__ Rng s_rng;
     __shared__ double s_d2[64];
     __shared__ int s_ok;
     RState* S = B.st + p;
     odo_pair_result* R = B.res + p;
     float* T12o = B.T12 + (size_t)p * 16;
-    if (!S->active) return;
+    const bool active = S->active;
     const int ng = S->ng, words = S->words;
     const unsigned minInl = (unsigned)cfg.min_inlier_th;
-    if (S->valid == 0) {
-        // identity fallback: one sweep with T = I, same lane split as the eval kernel
+    uint32_t* BM = B.best_mask + (size_t)p * B.mask_words;
+    float bestT[12];
+    for (int i = 0; i < 12; i++) bestT[i] = (i % 5 == 0) ? 1.f : 0.f;
+    int best_cnt = S->best_cnt;
+    float rmse = S->rmse;
+    const int best_h = S->best_h;
+    if (active && S->valid == 0) {
+        // identity fallback (ransac.cpp:252-264): one sweep with T = I
         const GoodPt* P = B.gpts + (size_t)p * B.match_cap;
         MahalConst K;
         K.raster_cov_x = cfg.raster_cov_x;
@@ -600,7 +889,6 @@ __global__ void __launch_bounds__(64) k_ransac_final(RansacBufs B, RansacCfg cfg
         K.depth_cov = *B.latch;
         const float th = cfg.max_mahal * cfg.max_mahal;
         const double Td[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
-        uint32_t* BM = B.best_mask + (size_t)p * B.mask_words;
         double meanError = 0.0;
         unsigned cnt = 0;
         for (int c0 = 0; c0 < ng; c0 += 64) {
@@ -616,21 +904,16 @@ __global__ void __launch_bounds__(64) k_ransac_final(RansacBufs B, RansacCfg cfg
                 }
             }
             const uint64_t bal = __ballot(in);
-            s_d2[lane] = d;
+            if (in) s_d2[lane_rank(bal)] = d;
             if (lane == 0) {
                 BM[c0 >> 5] = (uint32_t)bal;
                 if (c0 + 32 < ng) BM[(c0 >> 5) + 1] = (uint32_t)(bal >> 32);
             }
             __syncthreads();
-            if (lane == 0) {
-                uint64_t b = bal;
-                while (b) {
-                    const int q = __builtin_ctzll(b);
-                    b &= b - 1;
-                    meanError += s_d2[q];
-                }
-            }
-            cnt += (unsigned)__popcll(bal);
+            const int nin = __popcll(bal);
+            if (lane == 0)
+                for (int q = 0; q < nin; q++) meanError += s_d2[q];
+            cnt += (unsigned)nin;
             __syncthreads();
         }
         if (lane == 0) {
@@ -640,66 +923,119 @@ __global__ void __launch_bounds__(64) k_ransac_final(RansacBufs B, RansacCfg cfg
                 meanError = sqrt(meanError);
             }
             s_ok = (cnt > minInl && meanError < (double)cfg.max_mahal) ? 1 : 0;
-            if (s_ok) {
-                S->best_cnt = (int)cnt;
-                S->rmse = (float)((double)S->rmse + meanError);
-                for (int i = 0; i < 12; i++) S->bestT[i] = (i % 5 == 0) ? 1.f : 0.f;
-            } else {
-                S->best_cnt = 0;
-            }
         }
         __syncthreads();
-        if (!s_ok)
+        if (s_ok) {
+            best_cnt = (int)cnt;
+            rmse = (float)((double)rmse + meanError);
+        } else {
+            best_cnt = 0;
             for (int w = lane; w < words; w += 64) BM[w] = 0;
+        }
+    } else if (active && best_h >= 0) {
+        const HypRes* hr = B.hyp + (size_t)p * B.hcap + best_h;
+        for (int i = 0; i < 12; i++) bestT[i] = hr->T[i];
+        const uint32_t* src = B.masks + ((size_t)p * B.hcap + best_h) * B.mask_words;
+        for (int w = lane; w < words; w += 64) BM[w] = src[w];
     }
-    if (lane == 0) {
-        R->rmse = S->rmse;
-        R->n_inliers = S->best_cnt;
-        R->ransac_ok = (unsigned)S->best_cnt >= minInl ? 1 : 0;
+    if (lane == 0 && active) {
+        R->rmse = rmse;
+        R->n_inliers = best_cnt;
+        R->ransac_ok = (unsigned)best_cnt >= minInl ? 1 : 0;
         R->visited = S->visited;
-        for (int i = 0; i < 12; i++) R->T12[i] = T12o[i] = S->bestT[i];
+        for (int i = 0; i < 12; i++) R->T12[i] = T12o[i] = bestT[i];
         R->T12[12] = R->T12[13] = R->T12[14] = 0.f;
         R->T12[15] = 1.f;
         T12o[12] = T12o[13] = T12o[14] = 0.f;
         T12o[15] = 1.f;
-        if (B.rng_io) {
-            // advance the caller's rand() stream by the visited iterations' draws only
-            rng_load(s_rng, S->rng0_s, S->rng0_f, S->rng0_r);
-            for (int v = 0; v < S->visited; v++) {
-                int cntv = 0, ids[MAX_SAMPLE], safety = 0;
-                while (cntv < S->S) {
-                    int id1 = (int)((uint32_t)s_rng.next() % (uint32_t)ng);
-                    int id2 = (int)((uint32_t)s_rng.next() % (uint32_t)ng);
-                    if (id1 > id2) id1 = id2;
-                    bool dup = false;
-                    for (int q = 0; q < cntv; q++) dup |= ids[q] == id1;
-                    if (!dup) ids[cntv++] = id1;
-                    if (++safety > 10000) break;
-                }
-            }
-            for (int i = 0; i < 31; i++) B.rng_io->state[i] = s_rng.s[i];
-            B.rng_io->fpos = s_rng.f;
-            B.rng_io->rpos = s_rng.r;
-        }
+    }
+    if (lane == 0 && B.rng_io) {
+        // the caller's rand() stream advances by the visited iterations' draws only
+        const int vis = active ? S->visited : 0;
+        const int pairs = vis > 0 ? B.samples[((size_t)p * B.hcap + vis - 1) * SREC + SREC - 1] : 0;
+        const uint32_t* raw = B.raw + (size_t)p * B.rawcap;
+        const int N = min(2 * pairs, B.rawcap);
+        ring_at(raw, S, N, s_rng);
+        for (int k = N; k < 2 * pairs; k++) s_rng.next();
+        for (int i = 0; i < 31; i++) B.rng_io->state[i] = s_rng.s[i];
+        B.rng_io->fpos = s_rng.f;
+        B.rng_io->rpos = s_rng.r;
     }
 }
 
 // ---------------------------------------------------------------- host side
 size_t ransac_gpt_bytes() { return sizeof(GoodPt); }
 
-size_t ransac_scratch_bytes(int npairs, int match_cap, int mask_words) {
-    size_t s = (size_t)npairs * match_cap * sizeof(GoodPt) + (size_t)npairs * sizeof(RState) + 16;
-    s += (size_t)npairs * RS_BMAX * sizeof(HypRes);
-    s += (size_t)npairs * RS_BMAX * (MAX_SAMPLE + 1) * sizeof(int) + 16;
-    s += (size_t)npairs * RS_BMAX * (size_t)mask_words * 4;
-    return s;
+static int ransac_hcap(const RansacCfg& cfg) { return std::max(cfg.iterations, 1); }
+
+// generator words per pair: twice the duplicate-free need, plus slack
+static int ransac_rawcap(const RansacCfg& cfg) {
+    const int S = std::min(std::max(cfg.sample_size, 1), MAX_SAMPLE);
+    const long w = 4L * S * ransac_hcap(cfg) + 512;
+    return (int)((w + 63) / 64 * 64);
 }
 
-void launch_ransac(hipStream_t st, const void* good, const int* n_good, const int* n_matches, const odo_dmatch* matches,
-                   const float* xyz, int kp_cap, int slot0, int match_cap, RansacCfg cfg, const double* latch,
-                   uint64_t seed_base, uint64_t pair_base, const int* pair_valid, int min_matches, odo_rng* rng_io,
-                   void* scratch, uint32_t* best_mask, int mask_words, odo_pair_result* res, float* T12, int npairs) {
-    RansacBufs B;
+struct Layout {
+    size_t gpts, st, hyp, samples, ready, masks, raw, total;
+};
+
+static Layout layout(int npairs, int match_cap, int mask_words, const RansacCfg& cfg) {
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t hc = ransac_hcap(cfg);
+    Layout L;
+    size_t o = 0;
+    L.gpts = o;
+    o = al(o + (size_t)npairs * match_cap * sizeof(GoodPt));
+    L.st = o;
+    o = al(o + (size_t)npairs * sizeof(RState));
+    L.hyp = o;
+    o = al(o + (size_t)npairs * hc * sizeof(HypRes));
+    L.samples = o;
+    o = al(o + (size_t)npairs * hc * SREC * sizeof(int));
+    L.ready = o;
+    o = al(o + (size_t)npairs * hc * sizeof(int));
+    L.masks = o;
+    o = al(o + (size_t)npairs * hc * mask_words * 4);
+    L.raw = o;
+    o = al(o + (size_t)npairs * ransac_rawcap(cfg) * 4);
+    L.total = o;
+    return L;
+}
+
+size_t ransac_scratch_bytes(int npairs, int match_cap, int mask_words, const RansacCfg& cfg) {
+    return layout(npairs, match_cap, mask_words, cfg).total;
+}
+
+static RansacBufs carve(void* scratch, int npairs, int match_cap, int mask_words, const RansacCfg& cfg) {
+    const Layout L = layout(npairs, match_cap, mask_words, cfg);
+    char* s = (char*)scratch;
+    RansacBufs B{};
+    B.gpts = (GoodPt*)(s + L.gpts);
+    B.st = (RState*)(s + L.st);
+    B.hyp = (HypRes*)(s + L.hyp);
+    B.samples = (int*)(s + L.samples);
+    B.ready = (int*)(s + L.ready);
+    B.masks = (uint32_t*)(s + L.masks);
+    B.raw = (uint32_t*)(s + L.raw);
+    B.hcap = ransac_hcap(cfg);
+    B.rawcap = ransac_rawcap(cfg);
+    B.match_cap = match_cap;
+    B.mask_words = mask_words;
+    return B;
+}
+
+void launch_ransac_raw(hipStream_t st, void* scratch, int npairs, int match_cap, int mask_words, RansacCfg cfg,
+                       uint64_t seed_base, uint64_t pair_base, odo_rng* rng_io) {
+    RansacBufs B = carve(scratch, npairs, match_cap, mask_words, cfg);
+    B.rng_io = rng_io;
+    hipLaunchKernelGGL(k_ransac_raw, dim3(npairs), dim3(64), 0, st, B, seed_base, pair_base);
+}
+
+void launch_ransac(hipStream_t st, const void* good, const int* n_good, const int* n_matches,
+                   const odo_dmatch* matches, const float* xyz, int kp_cap, int slot0, int match_cap, RansacCfg cfg,
+                   const double* latch, const int* pair_valid, int min_matches, odo_rng* rng_io, void* scratch,
+                   uint32_t* best_mask, int mask_words, odo_pair_result* res, float* T12, int npairs) {
+    RansacBufs B = carve(scratch, npairs, match_cap, mask_words, cfg);
     B.good = (const SortElR*)good;
     B.n_good = n_good;
     B.n_matches = n_matches;
@@ -707,49 +1043,27 @@ void launch_ransac(hipStream_t st, const void* good, const int* n_good, const in
     B.xyz = xyz;
     B.kp_cap = kp_cap;
     B.slot0 = slot0;
-    B.match_cap = match_cap;
     B.latch = latch;
-    B.seed_base = seed_base;
-    B.pair_base = pair_base;
     B.pair_valid = pair_valid;
     B.min_matches = min_matches;
     B.rng_io = rng_io;
-    B.mask_words = mask_words;
     B.best_mask = best_mask;
     B.res = res;
     B.T12 = T12;
-    // carve the per-call scratch: gpts | state | hyp | samples | masks
-    char* s = (char*)scratch;
-    B.gpts = (GoodPt*)s;
-    s += (size_t)npairs * match_cap * sizeof(GoodPt);
-    B.st = (RState*)s;
-    s += (size_t)npairs * sizeof(RState);
-    s = (char*)(((uintptr_t)s + 15) & ~(uintptr_t)15);
-    B.hyp = (HypRes*)s;
-    s += (size_t)npairs * RS_BMAX * sizeof(HypRes);
-    B.samples = (int*)s;
-    s += (size_t)npairs * RS_BMAX * (MAX_SAMPLE + 1) * sizeof(int);
-    s = (char*)(((uintptr_t)s + 15) & ~(uintptr_t)15);
-    B.masks = (uint32_t*)s;
-    // round schedule: 16, 48, 448, then 512 until H is covered
-    int sizes[64];
-    int nr = 0, cum = 0;
-    const int H = cfg.iterations;
-    const int sched[3] = {16, 48, 448};
-    while (cum < H && nr < 64) {
-        const int b = nr < 3 ? sched[nr] : RS_BMAX;
-        sizes[nr++] = b;
-        cum += b;
-    }
-    if (nr == 0) sizes[nr++] = 16;
-    hipLaunchKernelGGL(k_ransac_prep, dim3(npairs), dim3(256), 0, st, B, cfg, sizes[0]);
-    for (int r = 0; r < nr; r++) {
-        const int b = sizes[r];
-        dim3 g(npairs, (b + EV_WAVES - 1) / EV_WAVES);
-        hipLaunchKernelGGL(k_ransac_eval, g, dim3(64 * EV_WAVES), 0, st, B, cfg);
-        const int next = r + 1 < nr ? sizes[r + 1] : 0;
-        hipLaunchKernelGGL(k_ransac_scan, dim3(npairs), dim3(64), 0, st, B, cfg, next);
-    }
+    hipLaunchKernelGGL(k_ransac_prep, dim3(npairs), dim3(256), 0, st, B, cfg);
+    const int H = std::max(cfg.iterations, 0);
+    // Two launches: the first EV_ROWS0 rows of hypotheses for every pair (the
+    // >80% break usually ends a pair within them), then the rest, which only
+    // pairs still folding take up — so the speculative hypotheses of finished
+    // pairs do not compete with the long ones.
+    const int rows = (H + EV_WAVES - 1) / EV_WAVES;
+    const int r0 = std::min(rows, EV_ROWS0);
+    if (r0 > 0)
+        hipLaunchKernelGGL(k_ransac_eval, dim3(npairs, r0), dim3(64 * EV_WAVES), PCACHE * sizeof(GoodPt), st, B,
+                           cfg, 0);
+    if (rows > r0)
+        hipLaunchKernelGGL(k_ransac_eval, dim3(npairs, rows - r0), dim3(64 * EV_WAVES), PCACHE * sizeof(GoodPt), st,
+                           B, cfg, r0);
     hipLaunchKernelGGL(k_ransac_final, dim3(npairs), dim3(64), 0, st, B, cfg);
 }
 

@@ -111,6 +111,8 @@ struct odo_ctx {
     std::vector<int> valid_h;
     hipEvent_t ev[16];
     int nev = 0;
+    hipStream_t side = nullptr;        // RANSAC rand() words, overlapping extraction
+    hipEvent_t ev_go = nullptr, ev_raw = nullptr;
 };
 
 static void free_ctx(odo_ctx* c) {
@@ -123,6 +125,9 @@ static void free_ctx(odo_ctx* c) {
     for (void* p : ptrs)
         if (p) hipFree(p);
     for (int i = 0; i < c->nev; i++) hipEventDestroy(c->ev[i]);
+    if (c->ev_go) hipEventDestroy(c->ev_go);
+    if (c->ev_raw) hipEventDestroy(c->ev_raw);
+    if (c->side) hipStreamDestroy(c->side);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -330,7 +335,7 @@ static int alloc_buffers(odo_ctx* c) {
     while (pw < c->kp_cap) pw <<= 1;
     if ((e = dalloc(&c->sort_scratch, B * std::max(pw, c->kp_cap)))) return e;
     if ((e = dalloc(&c->latch, 1))) return e;
-    if ((e = dalloc((uint8_t**)&c->gpts, ransac_scratch_bytes((int)B, c->match_cap, c->mask_words)))) return e;
+    if ((e = dalloc((uint8_t**)&c->gpts, ransac_scratch_bytes((int)B, c->match_cap, c->mask_words, c->rcfg)))) return e;
     if ((e = dalloc(&c->best_mask, B * c->mask_words))) return e;
     if ((e = dalloc(&c->res, B))) return e;
     if ((e = dalloc(&c->T12, B * 16))) return e;
@@ -383,11 +388,19 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
     c->H = cfg->height;
     c->maxb = cfg->max_batch;
     c->slots = cfg->max_batch + 1;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_go, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_raw, hipEventDisableTiming) != hipSuccess) {
         fail(ODO_ERR_DEVICE, "hipStreamCreate failed");
         free_ctx(c);
         return nullptr;
     }
+    // ErrorFunction2 statics (ransac.cpp:352-359)
+    const double cam_angle_x = 58.0 / 180.0 * M_PI, cam_angle_y = 45.0 / 180.0 * M_PI;
+    const double rsx = 3 * tan(cam_angle_x / 640.0), rsy = 3 * tan(cam_angle_y / 480.0);
+    c->rcfg = RansacCfg{cfg->ransac.iterations, cfg->ransac.min_inlier_th, cfg->ransac.max_mahalanobis,
+                        cfg->ransac.sample_size, cfg->ransac.check_depth, rsx * rsx, rsy * rsy};
     if (build_geometry(c) != ODO_OK || alloc_buffers(c) != ODO_OK) {
         free_ctx(c);
         return nullptr;
@@ -396,11 +409,6 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
     const odo_calib& k = cfg->calib;
     c->cal = FrameCalib{k.fx, k.fy, k.cx, k.cy, k.k1, k.k2, k.p1, k.p2, k.k3, k.depth_factor, k.mbf,
                         1.0f / k.fx, 1.0f / k.fy};
-    // ErrorFunction2 statics (ransac.cpp:352-359)
-    const double cam_angle_x = 58.0 / 180.0 * M_PI, cam_angle_y = 45.0 / 180.0 * M_PI;
-    const double rsx = 3 * tan(cam_angle_x / 640.0), rsy = 3 * tan(cam_angle_y / 480.0);
-    c->rcfg = RansacCfg{cfg->ransac.iterations, cfg->ransac.min_inlier_th, cfg->ransac.max_mahalanobis,
-                        cfg->ransac.sample_size, cfg->ransac.check_depth, rsx * rsx, rsy * rsy};
     c->nev = 12;
     for (int i = 0; i < c->nev; i++) hipEventCreate(&c->ev[i]);
     return c;
@@ -505,8 +513,9 @@ static int run_pairs(odo_ctx* c, int n) {
     launch_latch(st, c->latch, c->good, c->n_good, c->n_matches, c->matches, c->xyz, c->kp_cap, 0, n, c->match_cap,
                  c->cfg.ransac.min_inlier_th, c->cfg.ransac.sample_size, c->cfg.ransac.iterations, c->pair_valid);
     hipEventRecord(c->ev[7], st);
+    HIPCHK(hipStreamWaitEvent(st, c->ev_raw, 0));
     launch_ransac(st, c->good, c->n_good, c->n_matches, c->matches, c->xyz, c->kp_cap, 0, c->match_cap, c->rcfg,
-                  c->latch, (uint64_t)c->cfg.seed, c->pair_counter, c->pair_valid, 20, nullptr, c->gpts,
+                  c->latch, c->pair_valid, 20, nullptr, c->gpts,
                   c->best_mask, c->mask_words, c->res, c->T12, n);
     hipEventRecord(c->ev[8], st);
     launch_pnp(st, c->f2_src, c->xyz, c->kun, c->ur, c->nkp, c->kp_cap, 0, c->cal, c->T12, c->pair_valid,
@@ -548,6 +557,13 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
     if (!c || !d_bgr || !d_depth || n <= 0 || n > c->maxb) return fail(ODO_ERR_ARG, "bad track args");
     int e;
     hipEventRecord(c->ev[0], c->stream);
+    // RANSAC's rand() words depend on the pair seeds only: drawn on the side
+    // stream while the frames are extracted (run_pairs waits for ev_raw)
+    HIPCHK(hipEventRecord(c->ev_go, c->stream));
+    HIPCHK(hipStreamWaitEvent(c->side, c->ev_go, 0));
+    launch_ransac_raw(c->side, c->gpts, n, c->match_cap, c->mask_words, c->rcfg, (uint64_t)c->cfg.seed,
+                      c->pair_counter, nullptr);
+    HIPCHK(hipEventRecord(c->ev_raw, c->side));
     if ((e = run_extract(c, d_bgr, d_depth, n, 1))) return e;
     if ((e = run_pairs(c, n))) return e;
     c->last_n = n;
@@ -845,7 +861,11 @@ int odo_ransac(odo_ctx* c, const odo_dmatch* m12, int n12, const float* xyz1, in
     const int words = (ng + 31) / 32;
     DevBuf dxyz((size_t)2 * kc * 3 * sizeof(float)), dm((size_t)ng * sizeof(odo_dmatch)), dg((size_t)ng * 8);
     DevBuf dint(4 * sizeof(int)), dlatch(sizeof(double)), drng(sizeof(odo_rng)), dres(sizeof(odo_pair_result));
-    DevBuf dT(16 * sizeof(float)), dgp(ransac_scratch_bytes(1, ng, words)), dbm((size_t)words * 4);
+    const double cam_angle_x = 58.0 / 180.0 * M_PI, cam_angle_y = 45.0 / 180.0 * M_PI;
+    const double rsx = 3 * tan(cam_angle_x / 640.0), rsy = 3 * tan(cam_angle_y / 480.0);
+    RansacCfg cfg{p->iterations, p->min_inlier_th, p->max_mahalanobis, p->sample_size, p->check_depth, rsx * rsx,
+                  rsy * rsy};
+    DevBuf dT(16 * sizeof(float)), dgp(ransac_scratch_bytes(1, ng, words, cfg)), dbm((size_t)words * 4);
     std::vector<uint64_t> gl(ng);
     for (int k = 0; k < ng; k++) {
         uint32_t bits;
@@ -860,12 +880,9 @@ int odo_ransac(odo_ctx* c, const odo_dmatch* m12, int n12, const float* xyz1, in
     HIPCHK(hipMemcpyAsync(dint.p, ints, sizeof(ints), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(dlatch.p, latch, sizeof(double), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(drng.p, rng, sizeof(odo_rng), hipMemcpyHostToDevice, st));
-    const double cam_angle_x = 58.0 / 180.0 * M_PI, cam_angle_y = 45.0 / 180.0 * M_PI;
-    const double rsx = 3 * tan(cam_angle_x / 640.0), rsy = 3 * tan(cam_angle_y / 480.0);
-    RansacCfg cfg{p->iterations, p->min_inlier_th, p->max_mahalanobis, p->sample_size, p->check_depth, rsx * rsx,
-                  rsy * rsy};
+    launch_ransac_raw(st, dgp.p, 1, ng, words, cfg, 0, 0, drng.as<odo_rng>());
     launch_ransac(st, dg.p, dint.as<int>(), dint.as<int>() + 1, dm.as<odo_dmatch>(), dxyz.as<float>(), kc, 0, ng, cfg,
-                  dlatch.as<double>(), 0, 0, dint.as<int>() + 2, 0, drng.as<odo_rng>(), dgp.p, dbm.as<uint32_t>(),
+                  dlatch.as<double>(), dint.as<int>() + 2, 0, drng.as<odo_rng>(), dgp.p, dbm.as<uint32_t>(),
                   words, dres.as<odo_pair_result>(), dT.as<float>(), 1);
     HIPCHK(hipGetLastError());
     odo_pair_result r;

@@ -87,11 +87,15 @@ void launch_latch(hipStream_t st, double* latch, const void* good, const int* n_
                   const odo_dmatch* matches, const float* xyz, int kp_cap, int slot0, int npairs, int match_cap,
                   int min_inl, int sample_size, int iterations, const int* pair_valid);
 size_t ransac_gpt_bytes();
-void launch_ransac(hipStream_t st, const void* good, const int* n_good, const int* n_matches, const odo_dmatch* matches,
-                   const float* xyz, int kp_cap, int slot0, int match_cap, RansacCfg cfg, const double* latch,
-                   uint64_t seed_base, uint64_t pair_base, const int* pair_valid, int min_matches, odo_rng* rng_io,
-                   void* scratch, uint32_t* best_mask, int mask_words, odo_pair_result* res, float* T12, int npairs);
-size_t ransac_scratch_bytes(int npairs, int match_cap, int mask_words);
+// rand() words for every pair (data independent): launched at batch start on
+// a side stream; launch_ransac's stream must wait for it.
+void launch_ransac_raw(hipStream_t st, void* scratch, int npairs, int match_cap, int mask_words, RansacCfg cfg,
+                       uint64_t seed_base, uint64_t pair_base, odo_rng* rng_io);
+void launch_ransac(hipStream_t st, const void* good, const int* n_good, const int* n_matches,
+                   const odo_dmatch* matches, const float* xyz, int kp_cap, int slot0, int match_cap, RansacCfg cfg,
+                   const double* latch, const int* pair_valid, int min_matches, odo_rng* rng_io, void* scratch,
+                   uint32_t* best_mask, int mask_words, odo_pair_result* res, float* T12, int npairs);
+size_t ransac_scratch_bytes(int npairs, int match_cap, int mask_words, const RansacCfg& cfg);
 size_t pnp_edge_bytes();
 void launch_pnp(hipStream_t st, const int32_t* f2_src, const float* xyz, const float* kun, const float* ur,
                 const int* nkp, int kp_cap, int slot0, FrameCalib cal, const float* T12, const int* pair_valid,

@@ -187,10 +187,14 @@ def test_extract_entry_point_bgr_and_gray(pkg):
         assert np.array_equal(xyz[:n.value], ref["xyz"])
 
 
-@pytest.mark.parametrize("iters", [1, 200, 500])
-def test_ransac_entry_point_stream_and_latch(pkg, iters):
+@pytest.mark.parametrize("iters,corrupt", [(1, 0.0), (200, 0.0), (500, 0.0), (500, 0.3), (500, 0.55),
+                                           (1200, 0.5), (40, 0.7)])
+def test_ransac_entry_point_stream_and_latch(pkg, iters, corrupt):
     """odo_ransac == Ransac::Iterate: bit-exact T12/rmse/inliers, rand() stream
-    advanced by exactly the visited draws, latch set on first call."""
+    advanced by exactly the visited draws, latch set on first call. `corrupt`
+    re-targets that fraction of the matches at random keypoints so the inlier
+    ratio stays under the 80% break and later rounds (side-stream samples,
+    several 512-hypothesis rounds) are exercised."""
     bgr, dep, cal, frames = _frames_cfg1()
     f1, f2 = frames[0], frames[1]
     n1, n2 = len(f1["kps"]), len(f2["kps"])
@@ -204,6 +208,10 @@ def test_ransac_entry_point_stream_and_latch(pkg, iters):
                                   O.ptr(np.zeros(n1, np.uint8)), O.ptr(np.zeros(n1, np.int32)), O.ptr(obs2),
                                   O.ptr(src2), O.ptr(out2), O.ptr(m), n1)
     m = m[:nm]
+    if corrupt > 0:
+        rs = np.random.default_rng(int(corrupt * 1000) + iters)
+        sel = rs.random(nm) < corrupt
+        m["trainIdx"][sel] = rs.integers(0, n2, int(sel.sum()))
     rp = O.ransac_params(iters)
     odo, _ = make_odo(pkg, 640, 480, 1000, iters, 1)
     lib = pkg.load()
@@ -228,6 +236,7 @@ def test_ransac_entry_point_stream_and_latch(pkg, iters):
         pkg.check(lib.odo_ransac(odo.h, pkg.ptr(m), nm, pkg.ptr(f1["xyz"]), n1, pkg.ptr(f2["xyz"]), n2,
                                  pkg.ptr(rpg), pkg.ptr(r_gpu), O.C.byref(lat_gpu), pkg.ptr(T), O.C.byref(rmse),
                                  pkg.ptr(inl), O.C.byref(ni), O.C.byref(ok)))
+        print(f"iters {iters} corrupt {corrupt}: good {ng.value} visited {vis.value} inliers {ni_ref.value}")
         assert ok.value == ok_ref and ni.value == ni_ref.value
         assert np.array_equal(T, T_ref) and rmse.value == rmse_ref.value
         assert np.array_equal(inl[:ni.value], inl_ref[:ni_ref.value])
