@@ -77,12 +77,14 @@ class Odometry:
                                        ptr(out) if want_results else None))
         return out
 
-    def track_batch_host(self, bgr: np.ndarray, depth: np.ndarray):
+    def track_batch_host(self, bgr: np.ndarray, depth: np.ndarray, want_results=True):
+        """Host inputs; without results the call returns once the frames are
+        staged and the batch is queued (its pair stages run asynchronously)."""
         bgr = np.ascontiguousarray(bgr, np.uint8)
         depth = np.ascontiguousarray(depth, np.uint16)
         n = bgr.shape[0]
-        out = np.zeros(n, PAIR_DTYPE)
-        check(self.lib.odo_track_batch_host(self.h, ptr(bgr), ptr(depth), n, ptr(out)))
+        out = np.zeros(n, PAIR_DTYPE) if want_results else None
+        check(self.lib.odo_track_batch_host(self.h, ptr(bgr), ptr(depth), n, ptr(out) if want_results else None))
         return out
 
     def synchronize(self):

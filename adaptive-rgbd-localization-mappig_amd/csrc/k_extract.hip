@@ -846,4 +846,50 @@ void launch_finalize(hipStream_t st, const uint8_t* pyr, const uint8_t* blur, si
     hipLaunchKernelGGL(k_finalize, g, dim3(256), 0, st, pyr, blur, pyr_stride, lv, nlevels, okp, ocnt, okp_stride,
                        depth, depth_stride, img_w, cal, kps, desc, kun, xyz, ur, nkp, kp_cap);
 }
+
+// Frame roll: the last frame of a batch becomes slot 0 (Tracking::mLastFrame)
+// of the next batch's frame set. One launch for all per-frame feature arrays
+// (16-byte moves; every array is kp_cap-sized, kp_cap a multiple of 64).
+struct FrameCopy {
+    const uint4* src[5];
+    uint4* dst[5];
+    int n16[5];
+    const int* nsrc;
+    int* ndst;
+};
+
+__global__ void __launch_bounds__(256) k_copy_frame(FrameCopy F) {
+    const int a = blockIdx.y;
+    const uint4* s = F.src[a];
+    uint4* d = F.dst[a];
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < F.n16[a]; i += gridDim.x * 256) d[i] = s[i];
+    if (a == 0 && blockIdx.x == 0 && threadIdx.x == 0) *F.ndst = *F.nsrc;
+}
+
+void launch_copy_frame(hipStream_t st, const orb_kp* kps_s, const uint8_t* desc_s, const float* kun_s,
+                       const float* xyz_s, const float* ur_s, const int* n_s, orb_kp* kps_d, uint8_t* desc_d,
+                       float* kun_d, float* xyz_d, float* ur_d, int* n_d, int kp_cap) {
+    FrameCopy F;
+    const size_t bytes[5] = {(size_t)kp_cap * sizeof(orb_kp), (size_t)kp_cap * 32, (size_t)kp_cap * 8,
+                             (size_t)kp_cap * 12, (size_t)kp_cap * 4};
+    const void* s[5] = {kps_s, desc_s, kun_s, xyz_s, ur_s};
+    void* d[5] = {kps_d, desc_d, kun_d, xyz_d, ur_d};
+    for (int i = 0; i < 5; i++) {
+        F.src[i] = (const uint4*)s[i];
+        F.dst[i] = (uint4*)d[i];
+        F.n16[i] = (int)(bytes[i] / 16);
+    }
+    F.nsrc = n_s;
+    F.ndst = n_d;
+    hipLaunchKernelGGL(k_copy_frame, dim3(8, 5), dim3(256), 0, st, F);
+}
+
+__global__ void k_pair_valid(int* pv, int n, int first_valid) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) pv[i] = (i > 0 || first_valid) ? 1 : 0;
+}
+
+void launch_pair_valid(hipStream_t st, int* pv, int n, int first_valid) {
+    hipLaunchKernelGGL(k_pair_valid, dim3((n + 255) / 256), dim3(256), 0, st, pv, n, first_valid);
+}
 }  // namespace odo

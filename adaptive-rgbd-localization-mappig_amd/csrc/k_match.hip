@@ -236,6 +236,234 @@ ODO_INLINE void gnu_sort(A a, int n) {
     } else st_insertion_sort(a, 0, n);
 }
 
+// ---- workgroup-parallel std::sort (identical permutation to gnu_sort) -------
+// Level-synchronous introsort: every range of a level is partitioned at once.
+// A Hoare partition (pivot key pk at `first`) swaps the k-th element from the
+// left with key >= pk against the k-th from the right with key <= pk for all
+// k < k*, k* = the first k where those stops cross, and cuts at the k*-th left
+// stop; ranks come from prefix counts over the level. Ranges are disjoint, so
+// the order libstdc++ recurses in does not matter. __final_insertion_sort never
+// moves an element across a cut (keys left of a cut are <= keys right of it),
+// so it equals a stable sort inside every final range, done one range per
+// thread.
+#define PS_MAXR 512
+
+struct PSortRanges {
+    int f[PS_MAXR], l[PS_MAXR], d[PS_MAXR], pk[PS_MAXR], ks[PS_MAXR];
+    int gs[PS_MAXR], ge[PS_MAXR], ls[PS_MAXR], le[PS_MAXR], cut[PS_MAXR];
+    int nf[2 * PS_MAXR], nd[2 * PS_MAXR];
+    int nr;
+    int ws[16][2];
+};
+
+static inline size_t psort_lds_bytes(int pw) {
+    return (size_t)pw * (8 + 2 + 2 + 2 + 1) + sizeof(PSortRanges) + 64;
+}
+
+// exclusive block scan of two per-thread counts
+ODO_INLINE int2 block_scan2(int a, int b, int (*ws)[2]) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int ia = a, ib = b;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int x = __shfl_up(ia, o), y = __shfl_up(ib, o);
+        if (lane >= o) {
+            ia += x;
+            ib += y;
+        }
+    }
+    if (lane == 63) {
+        ws[w][0] = ia;
+        ws[w][1] = ib;
+    }
+    __syncthreads();
+    int ba = 0, bb = 0;
+    for (int k = 0; k < w; k++) {
+        ba += ws[k][0];
+        bb += ws[k][1];
+    }
+    __syncthreads();
+    return make_int2(ba + ia - a, bb + ib - b);
+}
+
+// range of position j (j in [f+1, l) of an active range), or -1
+ODO_INLINE int psort_find(const PSortRanges& R, int nr, int j) {
+    int lo = 0, hi = nr - 1, r = -1;
+    while (lo <= hi) {
+        const int m = (lo + hi) >> 1;
+        if (R.f[m] < j) {
+            r = m;
+            lo = m + 1;
+        } else hi = m - 1;
+    }
+    if (r < 0 || j >= R.l[r] || R.d[r] < 0) return -1;
+    return r;
+}
+
+ODO_INLINE void block_gnu_sort(SortEl* A, int n, uint8_t* work, PSortRanges& R) {
+    const int t = threadIdx.x, T = blockDim.x;
+    if (n < 2) return;
+    uint16_t* rid = reinterpret_cast<uint16_t*>(work);
+    uint16_t* posL = rid + n;
+    uint16_t* posR = posL + n;
+    uint8_t* cutf = reinterpret_cast<uint8_t*>(posR + n);  // range boundaries
+    for (int j = t; j < n; j += T) cutf[j] = j == 0;
+    if (t == 0) {
+        R.nr = 0;
+        if (n > 16) {
+            R.f[0] = 0;
+            R.l[0] = n;
+            R.d[0] = 2 * (31 - __builtin_clz((unsigned)n));
+            R.nr = 1;
+        }
+    }
+    __syncthreads();
+    const int c = (n + T - 1) / T;
+    const int j0 = min(n, t * c), j1 = min(n, j0 + c);
+    while (R.nr > 0) {
+        const int nr = R.nr;
+        // pivot: median of three moved to `first`; depth 0 -> heap sort (range done)
+        for (int r = t; r < nr; r += T) {
+            const int f = R.f[r], l = R.l[r], d = R.d[r];
+            if (d == 0) {
+                st_heap_sort_range(A, f, l, l);
+                R.d[r] = -1;
+            } else {
+                R.d[r] = d - 1;
+                st_move_median_to_first(A, f, f + 1, f + (l - f) / 2, l - 1);
+                R.pk[r] = (int)A[f].key;
+                R.ks[r] = 0;
+            }
+        }
+        __syncthreads();
+        for (int j = t; j < n; j += T) {
+            const int r = psort_find(R, nr, j);
+            rid[j] = r < 0 ? 0xffff : (uint16_t)r;
+        }
+        __syncthreads();
+        // left stops: key >= pk, right stops: key <= pk (over [f+1, l))
+        int cg = 0, cl = 0;
+        for (int j = j0; j < j1; j++) {
+            const int r = rid[j];
+            if (r == 0xffff) continue;
+            const uint32_t k = A[j].key, pk = (uint32_t)R.pk[r];
+            cg += k >= pk;
+            cl += k <= pk;
+        }
+        const int2 base = block_scan2(cg, cl, R.ws);
+        int rg = base.x, rl = base.y;
+        for (int j = j0; j < j1; j++) {
+            const int r = rid[j];
+            if (r == 0xffff) continue;
+            if (j == R.f[r] + 1) {
+                R.gs[r] = rg;
+                R.ls[r] = rl;
+            }
+            const uint32_t k = A[j].key, pk = (uint32_t)R.pk[r];
+            rg += k >= pk;
+            rl += k <= pk;
+            if (j == R.l[r] - 1) {
+                R.ge[r] = rg;
+                R.le[r] = rl;
+            }
+        }
+        __syncthreads();
+        rg = base.x;
+        rl = base.y;
+        for (int j = j0; j < j1; j++) {
+            const int r = rid[j];
+            if (r == 0xffff) continue;
+            const uint32_t k = A[j].key, pk = (uint32_t)R.pk[r];
+            const int f = R.f[r];
+            if (k >= pk) posL[f + (rg - R.gs[r])] = (uint16_t)j;
+            rg += k >= pk;
+            rl += k <= pk;
+            if (k <= pk) posR[f + (R.le[r] - rl)] = (uint16_t)j;
+        }
+        __syncthreads();
+        // k* = #{k : posL[k] < posR[k]} (monotone in k)
+        for (int q = t; q + 1 < n; q += T) {
+            const int r = rid[q + 1];
+            if (r == 0xffff) continue;
+            const int k = q - R.f[r];
+            const int m = min(R.ge[r] - R.gs[r], R.le[r] - R.ls[r]);
+            if (k < m && posL[q] < posR[q]) atomicAdd(&R.ks[r], 1);
+        }
+        __syncthreads();
+        for (int q = t; q + 1 < n; q += T) {
+            const int r = rid[q + 1];
+            if (r == 0xffff) continue;
+            const int k = q - R.f[r];
+            if (k < R.ks[r]) {
+                const int a = posL[q], b = posR[q];
+                const SortEl x = A[a];
+                A[a] = A[b];
+                A[b] = x;
+            }
+        }
+        for (int r = t; r < nr; r += T) {
+            int f = -1, cut = -1, l = -1;
+            if (R.d[r] >= 0) {
+                // the left scan stops at the k*-th original left stop, or
+                // earlier at R[k*-1], which now holds a swapped-in key >= pk
+                f = R.f[r];
+                l = R.l[r];
+                const int ks = R.ks[r];
+                cut = l;
+                if (ks < R.ge[r] - R.gs[r]) cut = posL[f + ks];
+                if (ks > 0) cut = min(cut, (int)posR[f + ks - 1]);
+                cutf[cut] = 1;
+            }
+            // children with more than 16 elements continue at the next level
+            R.nf[2 * r] = (cut >= 0 && cut - f > 16) ? f : -1;
+            R.nf[2 * r + 1] = (cut >= 0 && l - cut > 16) ? cut : -1;
+            R.cut[r] = cut;
+        }
+        __syncthreads();
+        // compact the next level's ranges (in position order)
+        const int m2 = 2 * nr;
+        const int cc = (m2 + T - 1) / T;
+        const int q0 = min(m2, t * cc), q1 = min(m2, q0 + cc);
+        int cnt = 0;
+        for (int q = q0; q < q1; q++) cnt += R.nf[q] >= 0;
+        const int2 nb = block_scan2(cnt, 0, R.ws);
+        int o = nb.x;
+        int nf_[8], nl_[8], nd_[8], nq = 0;
+        for (int q = q0; q < q1; q++) {
+            if (R.nf[q] < 0) continue;
+            const int r = q >> 1;
+            nf_[nq & 7] = (q & 1) ? R.cut[r] : R.f[r];
+            nl_[nq & 7] = (q & 1) ? R.l[r] : R.cut[r];
+            nd_[nq & 7] = R.d[r];
+            nq++;
+        }
+        __syncthreads();
+        for (int i = 0; i < nq && i < 8; i++) {
+            R.f[o + i] = nf_[i];
+            R.l[o + i] = nl_[i];
+            R.d[o + i] = nd_[i];
+        }
+        if (t == T - 1) R.nr = o + nq;
+        __syncthreads();
+    }
+    // __final_insertion_sort == stable sort inside each final range
+    for (int j = t; j < n; j += T) {
+        if (!cutf[j]) continue;
+        int e = j + 1;
+        while (e < n && !cutf[e]) e++;
+        for (int i = j + 1; i < e; i++) {
+            const SortEl v = A[i];
+            int k = i;
+            while (k > j && v.key < A[k - 1].key) {
+                A[k] = A[k - 1];
+                k--;
+            }
+            A[k] = v;
+        }
+    }
+    __syncthreads();
+}
+
 // ============================================================ per-pair match stage
 // One workgroup (256 threads) per pair (F1 = previous frame, F2 = current).
 // Outputs: good matches sorted per std::sort (query/train/distance), counts,
@@ -389,15 +617,15 @@ __global__ void __launch_bounds__(PM_THREADS) k_pair_match(
         gbase += tot;
         __syncthreads();
     }
-    // ---- std::sort(vGoodMatches) by distance (one lane, exact libstdc++ algorithm, in LDS)
+    // ---- std::sort(vGoodMatches) by distance (ransac.cpp:199): exact
+    // libstdc++ permutation, workgroup-parallel, in LDS
     SortEl* Gl = reinterpret_cast<SortEl*>(dyn_lds);
     for (int i = t; i < gbase; i += PM_THREADS) Gl[i] = G[i];
+    if (t == 0) n_good[p] = gbase;
     __syncthreads();
-    if (t == 0) {
-        n_good[p] = gbase;
-        gnu_sort(Gl, gbase);
-    }
-    __syncthreads();
+    block_gnu_sort(Gl, gbase, reinterpret_cast<uint8_t*>(dyn_lds) + (size_t)pw * 8,
+                   *reinterpret_cast<PSortRanges*>(reinterpret_cast<uint8_t*>(dyn_lds) +
+                                                  (((size_t)pw * 15 + 63) & ~(size_t)63)));
     for (int i = t; i < gbase; i += PM_THREADS) G[i] = Gl[i];
     (void)n2;
 }
@@ -447,10 +675,34 @@ void launch_pair_match(hipStream_t st, const int2* knn_idx, const int2* knn_dist
                        uint64_t* sort_scratch, int match_cap, int npairs) {
     int pw = 1;
     while (pw < kp_cap || pw < match_cap) pw <<= 1;
-    hipLaunchKernelGGL(k_pair_match, dim3(npairs), dim3(PM_THREADS), (size_t)pw * 8, st, knn_idx, knn_dist, knn_stride, xyz, nkp,
+    const size_t lds = psort_lds_bytes(pw);
+    if (lds > 64 * 1024) hipFuncSetAttribute((const void*)k_pair_match, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_pair_match, dim3(npairs), dim3(PM_THREADS), lds, st, knn_idx, knn_dist, knn_stride, xyz, nkp,
                        kp_cap, slot0, ratio, th_depth_m, check_depth, matches, n_matches, (SortEl*)good, n_good, f2_src,
                        sort_scratch, match_cap);
 }
+// odo_debug_sort: the pair stage's std::sort on an arbitrary key array
+__global__ void __launch_bounds__(PM_THREADS) k_sort_dbg(SortEl* __restrict__ a, int n, int pw) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t dyn_lds[];
+    SortEl* A = reinterpret_cast<SortEl*>(dyn_lds);
+    for (int i = threadIdx.x; i < n; i += PM_THREADS) A[i] = a[i];
+    __syncthreads();
+    block_gnu_sort(A, n, reinterpret_cast<uint8_t*>(dyn_lds) + (size_t)pw * 8,
+                   *reinterpret_cast<PSortRanges*>(reinterpret_cast<uint8_t*>(dyn_lds) +
+                                                  (((size_t)pw * 15 + 63) & ~(size_t)63)));
+    for (int i = threadIdx.x; i < n; i += PM_THREADS) a[i] = A[i];
+}
+
+int launch_sort_dbg(hipStream_t st, void* a, int n) {
+    int pw = 1;
+    while (pw < n) pw <<= 1;
+    const size_t lds = psort_lds_bytes(pw);
+    if (lds > 160 * 1024) return -1;
+    if (lds > 64 * 1024) hipFuncSetAttribute((const void*)k_sort_dbg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_sort_dbg, dim3(1), dim3(PM_THREADS), lds, st, (SortEl*)a, n, pw);
+    return 0;
+}
+
 void launch_latch(hipStream_t st, double* latch, const void* good, const int* n_good, const int* n_matches,
                   const odo_dmatch* matches, const float* xyz, int kp_cap, int slot0, int npairs, int match_cap,
                   int min_inl, int sample_size, int iterations, const int* pair_valid) {

@@ -419,7 +419,14 @@ __global__ void __launch_bounds__(256) k_ransac_prep(RansacBufs B, RansacCfg cfg
         const float* X2 = B.xyz + (size_t)(B.slot0 + p + 1) * B.kp_cap * 3;
         GoodPt* P = B.gpts + (size_t)p * B.match_cap;
         for (int k = t; k < ng; k += 256) {
-            const odo_dmatch m = M[G[k].val];
+            // defensive: an index outside the match list (never produced by a
+            // correct sort) yields an excluded NaN point instead of a stray read
+            const uint32_t gi = G[k].val;
+            const odo_dmatch m = gi < (uint32_t)nm ? M[gi] : odo_dmatch{0, 0, 0, __builtin_nanf("")};
+            if (gi >= (uint32_t)nm) {
+                P[k] = GoodPt{0.f, 0.f, __builtin_nanf(""), 0.f, 0.f, __builtin_nanf(""), 0.f, 0.f};
+                continue;
+            }
             GoodPt g;
             g.sx = X1[3 * m.queryIdx];
             g.sy = X1[3 * m.queryIdx + 1];

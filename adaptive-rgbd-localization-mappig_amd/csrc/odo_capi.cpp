@@ -1,10 +1,17 @@
 // Host orchestration and C-ABI (include/odo.h) of the MI355X odometry path.
 //
-// A context owns one HIP stream, all HBM scratch sized for max_batch frames,
-// the per-image-size geometry tables (pyramid levels, FAST cells, resize
-// coefficients) and the cross-frame state the reference keeps in globals:
-// the previous frame (Tracking::mpLastFrame) and the DepthCovariance latch.
-// Frame slot 0 holds the previous frame, slots 1..n the current batch.
+// A context owns all HBM scratch sized for max_batch frames, the per-image-size
+// geometry tables (pyramid levels, FAST cells, resize coefficients) and the
+// cross-frame state the reference keeps in globals: the previous frame
+// (Tracking::mpLastFrame) and the DepthCovariance latch.
+//
+// Batches are pipelined over two streams. The extraction stream rolls the
+// previous batch's last frame into slot 0 of a frame set and extracts the new
+// frames into slots 1..n; the pair stream then matches, runs RANSAC and PnP on
+// that set. Frame sets (and the RANSAC scratch) alternate between batches, so
+// batch k+1's throughput-bound extraction overlaps batch k's latency-bound
+// pair stages; per-set events order the reuse (set s is rewritten only after
+// the pair stages of batch k-1 that read it have finished).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -60,7 +67,8 @@ uint32_t splitmix_host(uint64_t base, uint64_t pair) { return pair_seed(base, pa
 struct odo_ctx {
     odo_config cfg{};
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;   // extraction
+    hipStream_t pstream = nullptr;  // pair stages
     int W = 0, H = 0, maxb = 0, slots = 0, nlevels = 0;
     std::vector<LevelDesc> lv_h;
     std::vector<CellDesc> cells_h;
@@ -74,7 +82,7 @@ struct odo_ctx {
     size_t pyr_size = 0, keys_per_frame = 0;
     FrameCalib cal{};
     RansacCfg rcfg{};
-    // frame buffers ([slots])
+    // frame buffers ([2 sets][slots])
     uint8_t *pyr = nullptr, *blur = nullptr;
     uint32_t* cand = nullptr;
     int* cand_cnt = nullptr;
@@ -98,36 +106,52 @@ struct odo_ctx {
     int32_t* f2_src = nullptr;
     uint64_t* sort_scratch = nullptr;
     double* latch = nullptr;
-    void* gpts = nullptr;
+    void* rscr[2] = {nullptr, nullptr};  // RANSAC scratch per frame set
     uint32_t *masks = nullptr, *best_mask = nullptr;
     odo_pair_result* res = nullptr;
     float* T12 = nullptr;
     void* edges = nullptr;
     uint8_t* pnp_mask = nullptr;
-    // sequence state
+    // sequence state: the last tracked batch sits in frame set seq_set (its
+    // last frame at slot seq_n); getters read view_set / view_n
     bool has_prev = false;
     uint64_t pair_counter = 0;
-    int last_n = 0;
+    int seq_set = 1, seq_n = 0;
+    int view_set = 0, last_n = 0;
     std::vector<int> valid_h;
     hipEvent_t ev[16];
     int nev = 0;
-    hipStream_t side = nullptr;        // RANSAC rand() words, overlapping extraction
-    hipEvent_t ev_go = nullptr, ev_raw = nullptr;
+    hipStream_t side = nullptr;  // RANSAC rand() words, ahead of the pair stages
+    hipEvent_t ev_xdone[2] = {}, ev_pdone[2] = {}, ev_raw[2] = {};
+    bool pdone_rec[2] = {false, false};
 };
+
+static inline size_t fbase(const odo_ctx* c, int set) { return (size_t)set * c->slots; }
+
+static int sync_all(odo_ctx* c) {
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipStreamSynchronize(c->side));
+    HIPCHK(hipStreamSynchronize(c->pstream));
+    return ODO_OK;
+}
 
 static void free_ctx(odo_ctx* c) {
     if (!c) return;
     void* ptrs[] = {c->lv, c->cells, c->rx, c->ry, c->pyr, c->blur, c->cand, c->cand_cnt, c->keys, c->knode, c->kquad,
                     c->okp, c->ocnt, c->kps, c->desc, c->kun, c->xyz, c->ur, c->nkp, c->bgr_in, c->depth_in,
                     c->knn_idx, c->knn_dist, c->matches, c->n_matches, c->n_good, c->pair_valid, c->good, c->f2_src,
-                    c->sort_scratch, c->latch, c->gpts, c->masks, c->best_mask, c->res, c->T12, c->edges,
-                    c->pnp_mask};
+                    c->sort_scratch, c->latch, c->rscr[0], c->rscr[1], c->masks, c->best_mask, c->res, c->T12,
+                    c->edges, c->pnp_mask};
     for (void* p : ptrs)
         if (p) hipFree(p);
     for (int i = 0; i < c->nev; i++) hipEventDestroy(c->ev[i]);
-    if (c->ev_go) hipEventDestroy(c->ev_go);
-    if (c->ev_raw) hipEventDestroy(c->ev_raw);
+    for (int i = 0; i < 2; i++) {
+        if (c->ev_xdone[i]) hipEventDestroy(c->ev_xdone[i]);
+        if (c->ev_pdone[i]) hipEventDestroy(c->ev_pdone[i]);
+        if (c->ev_raw[i]) hipEventDestroy(c->ev_raw[i]);
+    }
     if (c->side) hipStreamDestroy(c->side);
+    if (c->pstream) hipStreamDestroy(c->pstream);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -304,7 +328,7 @@ static int build_geometry(odo_ctx* c) {
 }
 
 static int alloc_buffers(odo_ctx* c) {
-    const size_t S = (size_t)c->slots, B = (size_t)c->maxb;
+    const size_t S = 2 * (size_t)c->slots, B = (size_t)c->maxb;
     int e;
     if ((e = dalloc(&c->pyr, S * c->pyr_size))) return e;
     if ((e = dalloc(&c->blur, S * c->pyr_size))) return e;
@@ -335,7 +359,9 @@ static int alloc_buffers(odo_ctx* c) {
     while (pw < c->kp_cap) pw <<= 1;
     if ((e = dalloc(&c->sort_scratch, B * std::max(pw, c->kp_cap)))) return e;
     if ((e = dalloc(&c->latch, 1))) return e;
-    if ((e = dalloc((uint8_t**)&c->gpts, ransac_scratch_bytes((int)B, c->match_cap, c->mask_words, c->rcfg)))) return e;
+    for (int i = 0; i < 2; i++)
+        if ((e = dalloc((uint8_t**)&c->rscr[i], ransac_scratch_bytes((int)B, c->match_cap, c->mask_words, c->rcfg))))
+            return e;
     if ((e = dalloc(&c->best_mask, B * c->mask_words))) return e;
     if ((e = dalloc(&c->res, B))) return e;
     if ((e = dalloc(&c->T12, B * 16))) return e;
@@ -388,10 +414,14 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
     c->H = cfg->height;
     c->maxb = cfg->max_batch;
     c->slots = cfg->max_batch + 1;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_go, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_raw, hipEventDisableTiming) != hipSuccess) {
+    bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&c->pstream, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) == hipSuccess;
+    for (int i = 0; i < 2 && ok; i++)
+        ok = hipEventCreateWithFlags(&c->ev_xdone[i], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&c->ev_pdone[i], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&c->ev_raw[i], hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
         fail(ODO_ERR_DEVICE, "hipStreamCreate failed");
         free_ctx(c);
         return nullptr;
@@ -409,7 +439,7 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
     const odo_calib& k = cfg->calib;
     c->cal = FrameCalib{k.fx, k.fy, k.cx, k.cy, k.k1, k.k2, k.p1, k.p2, k.k3, k.depth_factor, k.mbf,
                         1.0f / k.fx, 1.0f / k.fy};
-    c->nev = 12;
+    c->nev = 11;
     for (int i = 0; i < c->nev; i++) hipEventCreate(&c->ev[i]);
     return c;
 }
@@ -420,38 +450,39 @@ void* odo_stream(odo_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 
 int odo_reset(odo_ctx* c) {
     if (!c) return fail(ODO_ERR_ARG, "null ctx");
+    int e;
+    if ((e = sync_all(c))) return e;
     c->has_prev = false;
     c->pair_counter = 0;
     const double nan = std::nan("");
-    HIPCHK(hipMemcpyAsync(c->latch, &nan, sizeof(double), hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipMemcpy(c->latch, &nan, sizeof(double), hipMemcpyHostToDevice));
     return ODO_OK;
 }
 
 int odo_set_latch(odo_ctx* c, double cov) {
     if (!c) return fail(ODO_ERR_ARG, "null ctx");
-    HIPCHK(hipMemcpyAsync(c->latch, &cov, sizeof(double), hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    int e;
+    if ((e = sync_all(c))) return e;
+    HIPCHK(hipMemcpy(c->latch, &cov, sizeof(double), hipMemcpyHostToDevice));
     return ODO_OK;
 }
 
 double odo_get_latch(odo_ctx* c) {
     double v = std::nan("");
-    if (!c) return v;
-    hipStreamSynchronize(c->stream);
+    if (!c || sync_all(c)) return v;
     hipMemcpy(&v, c->latch, sizeof(double), hipMemcpyDeviceToHost);
     return v;
 }
 
 int odo_synchronize(odo_ctx* c) {
     if (!c) return fail(ODO_ERR_ARG, "null ctx");
-    HIPCHK(hipStreamSynchronize(c->stream));
-    return ODO_OK;
+    return sync_all(c);
 }
 
-static int run_extract(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, int n, int slot) {
+static int run_extract(odo_ctx* c, int set, const uint8_t* d_bgr, const uint16_t* d_depth, int n, int slot0) {
     hipStream_t st = c->stream;
     const size_t P = c->pyr_size;
+    const size_t slot = fbase(c, set) + slot0;
     uint8_t* pyr = c->pyr + (size_t)slot * P;
     if (d_bgr) launch_gray(st, d_bgr, pyr, c->W * c->H, (size_t)c->W * c->H * 3, P, n);
     for (int l = 1; l < c->nlevels; l++) {
@@ -484,49 +515,56 @@ static int run_extract(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth
 }
 
 // Extraction when level 0 (the gray image) is already in the pyramid slot.
-static int run_extract_from_gray(odo_ctx* c, const uint16_t* d_depth, int n, int slot) {
-    return run_extract(c, nullptr, d_depth, n, slot);
+static int run_extract_from_gray(odo_ctx* c, int set, const uint16_t* d_depth, int n, int slot) {
+    return run_extract(c, set, nullptr, d_depth, n, slot);
 }
 
+// Extraction only (no pairs, no roll): frames land in the set the next
+// tracked batch will use, so the tracking sequence state is untouched.
 int odo_extract_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, int n) {
     if (!c || !d_bgr || !d_depth || n <= 0 || n > c->maxb) return fail(ODO_ERR_ARG, "bad extract args");
+    int e;
+    if ((e = sync_all(c))) return e;
+    const int set = c->seq_set ^ 1;
     hipEventRecord(c->ev[0], c->stream);
-    int e = run_extract(c, d_bgr, d_depth, n, 1);
+    if ((e = run_extract(c, set, d_bgr, d_depth, n, 1))) return e;
+    c->view_set = set;
     c->last_n = n;
-    return e;
+    return ODO_OK;
 }
 
-static int run_pairs(odo_ctx* c, int n) {
-    hipStream_t st = c->stream;
-    // pair p: F1 = slot p, F2 = slot p+1; pair 0 valid only with a previous frame
-    c->valid_h.assign(n, 1);
-    c->valid_h[0] = c->has_prev ? 1 : 0;
-    HIPCHK(hipMemcpyAsync(c->pair_valid, c->valid_h.data(), n * sizeof(int), hipMemcpyHostToDevice, st));
+// Pair stages of one batch on the pair stream, over frame set `set`:
+// pair p is (slot p, slot p+1); pair 0 is valid only with a previous frame.
+static int run_pairs(odo_ctx* c, int set, int n) {
+    hipStream_t st = c->pstream;
     const size_t KC = (size_t)c->kp_cap;
-    launch_knn2(st, c->desc, c->nkp, KC * 32, c->desc + KC * 32, c->nkp + 1, KC * 32, c->knn_idx, c->knn_dist, KC,
-                c->kp_cap, n);
+    const size_t b = fbase(c, set);
+    uint8_t* desc = c->desc + b * KC * 32;
+    int* nkp = c->nkp + b;
+    float* xyz = c->xyz + b * KC * 3;
+    hipEventRecord(c->ev[10], st);
+    launch_pair_valid(st, c->pair_valid, n, c->has_prev ? 1 : 0);
+    launch_knn2(st, desc, nkp, KC * 32, desc + KC * 32, nkp + 1, KC * 32, c->knn_idx, c->knn_dist, KC, c->kp_cap, n);
     hipEventRecord(c->ev[6], st);
     const float mThDepth = c->cfg.calib.mbf * c->cfg.calib.th_depth / c->cfg.calib.fx;
-    launch_pair_match(st, c->knn_idx, c->knn_dist, KC, c->xyz, c->nkp, c->kp_cap, 0, c->cfg.nn_ratio, mThDepth,
+    launch_pair_match(st, c->knn_idx, c->knn_dist, KC, xyz, nkp, c->kp_cap, 0, c->cfg.nn_ratio, mThDepth,
                       c->cfg.ransac.check_depth, c->matches, c->n_matches, c->good, c->n_good, c->f2_src,
                       c->sort_scratch, c->match_cap, n);
-    launch_latch(st, c->latch, c->good, c->n_good, c->n_matches, c->matches, c->xyz, c->kp_cap, 0, n, c->match_cap,
+    launch_latch(st, c->latch, c->good, c->n_good, c->n_matches, c->matches, xyz, c->kp_cap, 0, n, c->match_cap,
                  c->cfg.ransac.min_inlier_th, c->cfg.ransac.sample_size, c->cfg.ransac.iterations, c->pair_valid);
     hipEventRecord(c->ev[7], st);
-    HIPCHK(hipStreamWaitEvent(st, c->ev_raw, 0));
-    launch_ransac(st, c->good, c->n_good, c->n_matches, c->matches, c->xyz, c->kp_cap, 0, c->match_cap, c->rcfg,
-                  c->latch, c->pair_valid, 20, nullptr, c->gpts,
-                  c->best_mask, c->mask_words, c->res, c->T12, n);
+    launch_ransac(st, c->good, c->n_good, c->n_matches, c->matches, xyz, c->kp_cap, 0, c->match_cap, c->rcfg,
+                  c->latch, c->pair_valid, 20, nullptr, c->rscr[set], c->best_mask, c->mask_words, c->res, c->T12, n);
     hipEventRecord(c->ev[8], st);
-    launch_pnp(st, c->f2_src, c->xyz, c->kun, c->ur, c->nkp, c->kp_cap, 0, c->cal, c->T12, c->pair_valid,
-               c->n_matches, 20, c->edges, c->res, c->pnp_mask, n);
+    launch_pnp(st, c->f2_src, xyz, c->kun + b * KC * 2, c->ur + b * KC, nkp, c->kp_cap, 0, c->cal, c->T12,
+               c->pair_valid, c->n_matches, 20, c->edges, c->res, c->pnp_mask, n);
     hipEventRecord(c->ev[9], st);
     HIPCHK(hipGetLastError());
     return ODO_OK;
 }
 
 static int finish_batch(odo_ctx* c, int n, odo_pair_result* h_results) {
-    hipStream_t st = c->stream;
+    hipStream_t st = c->pstream;
     // n_matches/n_good into the result records
     if (h_results) {
         HIPCHK(hipMemcpyAsync(h_results, c->res, n * sizeof(odo_pair_result), hipMemcpyDeviceToHost, st));
@@ -540,54 +578,65 @@ static int finish_batch(odo_ctx* c, int n, odo_pair_result* h_results) {
     return ODO_OK;
 }
 
-// Copy slot n's features to slot 0 (it becomes the previous frame).
-static int roll_slots(odo_ctx* c, int n) {
-    hipStream_t st = c->stream;
-    const size_t KC = (size_t)c->kp_cap;
-    HIPCHK(hipMemcpyAsync(c->kps, c->kps + n * KC, KC * sizeof(orb_kp), hipMemcpyDeviceToDevice, st));
-    HIPCHK(hipMemcpyAsync(c->desc, c->desc + n * KC * 32, KC * 32, hipMemcpyDeviceToDevice, st));
-    HIPCHK(hipMemcpyAsync(c->kun, c->kun + n * KC * 2, KC * 2 * sizeof(float), hipMemcpyDeviceToDevice, st));
-    HIPCHK(hipMemcpyAsync(c->xyz, c->xyz + n * KC * 3, KC * 3 * sizeof(float), hipMemcpyDeviceToDevice, st));
-    HIPCHK(hipMemcpyAsync(c->ur, c->ur + n * KC, KC * sizeof(float), hipMemcpyDeviceToDevice, st));
-    HIPCHK(hipMemcpyAsync(c->nkp, c->nkp + n, sizeof(int), hipMemcpyDeviceToDevice, st));
-    return ODO_OK;
-}
-
 int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, int n, odo_pair_result* h_results) {
     if (!c || !d_bgr || !d_depth || n <= 0 || n > c->maxb) return fail(ODO_ERR_ARG, "bad track args");
     int e;
+    const int s = c->seq_set ^ 1;
+    const size_t KC = (size_t)c->kp_cap;
+    // ---- extraction stream: set s is free once the pair stages of the batch
+    // before the previous one (which read it) are done
+    if (c->pdone_rec[s]) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_pdone[s], 0));
     hipEventRecord(c->ev[0], c->stream);
-    // RANSAC's rand() words depend on the pair seeds only: drawn on the side
-    // stream while the frames are extracted (run_pairs waits for ev_raw)
-    HIPCHK(hipEventRecord(c->ev_go, c->stream));
-    HIPCHK(hipStreamWaitEvent(c->side, c->ev_go, 0));
-    launch_ransac_raw(c->side, c->gpts, n, c->match_cap, c->mask_words, c->rcfg, (uint64_t)c->cfg.seed,
+    if (c->has_prev) {
+        // the previous batch's last frame becomes slot 0 (Tracking::mLastFrame)
+        const size_t src = fbase(c, c->seq_set) + c->seq_n, dst = fbase(c, s);
+        launch_copy_frame(c->stream, c->kps + src * KC, c->desc + src * KC * 32, c->kun + src * KC * 2,
+                          c->xyz + src * KC * 3, c->ur + src * KC, c->nkp + src, c->kps + dst * KC,
+                          c->desc + dst * KC * 32, c->kun + dst * KC * 2, c->xyz + dst * KC * 3, c->ur + dst * KC,
+                          c->nkp + dst, c->kp_cap);
+    }
+    if ((e = run_extract(c, s, d_bgr, d_depth, n, 1))) return e;
+    HIPCHK(hipEventRecord(c->ev_xdone[s], c->stream));
+    // ---- side stream: RANSAC's rand() words depend on the pair seeds only
+    if (c->pdone_rec[s]) HIPCHK(hipStreamWaitEvent(c->side, c->ev_pdone[s], 0));
+    launch_ransac_raw(c->side, c->rscr[s], n, c->match_cap, c->mask_words, c->rcfg, (uint64_t)c->cfg.seed,
                       c->pair_counter, nullptr);
-    HIPCHK(hipEventRecord(c->ev_raw, c->side));
-    if ((e = run_extract(c, d_bgr, d_depth, n, 1))) return e;
-    if ((e = run_pairs(c, n))) return e;
+    HIPCHK(hipEventRecord(c->ev_raw[s], c->side));
+    // ---- pair stream
+    HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_xdone[s], 0));
+    HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_raw[s], 0));
+    c->valid_h.assign(n, 1);
+    c->valid_h[0] = c->has_prev ? 1 : 0;
+    if ((e = run_pairs(c, s, n))) return e;
+    HIPCHK(hipEventRecord(c->ev_pdone[s], c->pstream));
+    c->pdone_rec[s] = true;
+    c->seq_set = s;
+    c->seq_n = n;
+    c->view_set = s;
     c->last_n = n;
-    if ((e = finish_batch(c, n, h_results))) return e;
-    if ((e = roll_slots(c, n))) return e;
     c->has_prev = true;
     c->pair_counter += (uint64_t)n;
-    if (h_results) HIPCHK(hipStreamSynchronize(c->stream));
+    if ((e = finish_batch(c, n, h_results))) return e;
     return ODO_OK;
 }
 
 int odo_track_batch_host(odo_ctx* c, const uint8_t* bgr, const uint16_t* depth, int n, odo_pair_result* h_results) {
     if (!c || !bgr || !depth || n <= 0 || n > c->maxb) return fail(ODO_ERR_ARG, "bad track args");
-    HIPCHK(hipMemcpyAsync(c->bgr_in, bgr, (size_t)n * c->W * c->H * 3, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(c->depth_in, depth, (size_t)n * c->W * c->H * 2, hipMemcpyHostToDevice, c->stream));
+    // the staging buffers are read by the extraction stream of this batch:
+    // earlier extractions must have finished with them
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipMemcpy(c->bgr_in, bgr, (size_t)n * c->W * c->H * 3, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->depth_in, depth, (size_t)n * c->W * c->H * 2, hipMemcpyHostToDevice));
     return odo_track_batch(c, c->bgr_in, c->depth_in, n, h_results);
 }
 
 int odo_get_frame(odo_ctx* c, int i, orb_kp* kps, uint8_t* desc, float* kps_un, float* xyz, float* u_right, int cap,
                   int* n) {
     if (!c || i < 0 || i >= c->last_n) return fail(ODO_ERR_ARG, "bad frame index");
-    HIPCHK(hipStreamSynchronize(c->stream));
-    // after a track_batch the slots were rolled: slot i+1 still holds frame i
-    const int slot = i + 1;
+    int e;
+    if ((e = sync_all(c))) return e;
+    // frame i of the last batch: slot i+1 of its frame set
+    const size_t slot = fbase(c, c->view_set) + i + 1;
     int cnt = 0;
     HIPCHK(hipMemcpy(&cnt, c->nkp + slot, sizeof(int), hipMemcpyDeviceToHost));
     *n = cnt;
@@ -604,11 +653,12 @@ int odo_get_frame(odo_ctx* c, int i, orb_kp* kps, uint8_t* desc, float* kps_un, 
 int odo_get_pair(odo_ctx* c, int i, odo_dmatch* matches, int match_cap, int* n_matches, odo_dmatch* good_sorted,
                  int* n_good, uint8_t* ransac_inliers, uint8_t* pnp_inliers, int32_t* f2_src) {
     if (!c || i < 0 || i >= c->last_n) return fail(ODO_ERR_ARG, "bad pair index");
-    HIPCHK(hipStreamSynchronize(c->stream));
+    int e;
+    if ((e = sync_all(c))) return e;
     int nm = 0, ng = 0, n2 = 0;
     HIPCHK(hipMemcpy(&nm, c->n_matches + i, sizeof(int), hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(&ng, c->n_good + i, sizeof(int), hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(&n2, c->nkp + i + 1, sizeof(int), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&n2, c->nkp + fbase(c, c->view_set) + i + 1, sizeof(int), hipMemcpyDeviceToHost));
     if (n_matches) *n_matches = nm;
     if (n_good) *n_good = ng;
     std::vector<odo_dmatch> M(std::max(nm, 1));
@@ -634,10 +684,12 @@ int odo_get_pair(odo_ctx* c, int i, odo_dmatch* matches, int match_cap, int* n_m
 
 int odo_debug_pyramid(odo_ctx* c, int i, uint8_t* out, size_t cap) {
     if (!c || i < 0 || i >= c->last_n || cap < c->pyr_size) return fail(ODO_ERR_ARG, "bad args");
-    HIPCHK(hipStreamSynchronize(c->stream));
+    int e;
+    if ((e = sync_all(c))) return e;
     // compact levels back to back (device layout pads levels to 16 bytes)
     std::vector<uint8_t> buf(c->pyr_size);
-    HIPCHK(hipMemcpy(buf.data(), c->pyr + (size_t)(i + 1) * c->pyr_size, c->pyr_size, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(buf.data(), c->pyr + (fbase(c, c->view_set) + i + 1) * c->pyr_size, c->pyr_size,
+                     hipMemcpyDeviceToHost));
     size_t o = 0;
     for (auto& L : c->lv_h) {
         memcpy(out + o, buf.data() + L.off, (size_t)L.w * L.h);
@@ -648,15 +700,41 @@ int odo_debug_pyramid(odo_ctx* c, int i, uint8_t* out, size_t cap) {
 
 int odo_debug_blur(odo_ctx* c, int i, uint8_t* out, size_t cap) {
     if (!c || i < 0 || i >= c->last_n || cap < c->pyr_size) return fail(ODO_ERR_ARG, "bad args");
-    HIPCHK(hipStreamSynchronize(c->stream));
+    int e;
+    if ((e = sync_all(c))) return e;
     std::vector<uint8_t> buf(c->pyr_size);
-    HIPCHK(hipMemcpy(buf.data(), c->blur + (size_t)(i + 1) * c->pyr_size, c->pyr_size, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(buf.data(), c->blur + (fbase(c, c->view_set) + i + 1) * c->pyr_size, c->pyr_size,
+                     hipMemcpyDeviceToHost));
     size_t o = 0;
     for (auto& L : c->lv_h) {
         memcpy(out + o, buf.data() + L.off, (size_t)L.w * L.h);
         o += (size_t)L.w * L.h;
     }
     return (int)o;
+}
+
+int odo_debug_sort(odo_ctx* c, const odo_dmatch* in, int n, odo_dmatch* out) {
+    if (!c || n < 0 || (n && (!in || !out))) return fail(ODO_ERR_ARG, "bad sort args");
+    if (n > 8192) return fail(ODO_ERR_CAPACITY, "debug sort: at most 8192 elements");
+    if (n == 0) return ODO_OK;
+    std::vector<uint64_t> el(n);
+    for (int i = 0; i < n; i++) {
+        if (!(in[i].distance >= 0.f)) return fail(ODO_ERR_ARG, "debug sort: negative/NaN distance");
+        uint32_t bits;
+        memcpy(&bits, &in[i].distance, 4);
+        el[i] = ((uint64_t)(uint32_t)i << 32) | bits;  // SortEl{key = distance bits, val = index}
+    }
+    void* d = nullptr;
+    HIPCHK(hipMalloc(&d, (size_t)n * 8));
+    hipError_t e = hipMemcpy(d, el.data(), (size_t)n * 8, hipMemcpyHostToDevice);
+    if (e == hipSuccess && launch_sort_dbg(c->stream, d, n) != 0) e = hipErrorInvalidValue;
+    if (e == hipSuccess) e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) e = hipMemcpy(el.data(), d, (size_t)n * 8, hipMemcpyDeviceToHost);
+    hipFree(d);
+    if (e != hipSuccess) return fail(ODO_ERR_DEVICE, std::string("debug sort: ") + hipGetErrorString(e));
+    for (int i = 0; i < n; i++) out[i] = in[(uint32_t)(el[i] >> 32)];
+    return ODO_OK;
 }
 
 static orb_kp unpack_key(uint32_t k) {
@@ -673,8 +751,9 @@ static orb_kp unpack_key(uint32_t k) {
 
 int odo_debug_fast(odo_ctx* c, int i, int level, orb_kp* out, int cap, int* n) {
     if (!c || i < 0 || i >= c->last_n || level < 0 || level >= c->nlevels) return fail(ODO_ERR_ARG, "bad args");
-    HIPCHK(hipStreamSynchronize(c->stream));
-    const int slot = i + 1;
+    int e;
+    if ((e = sync_all(c))) return e;
+    const size_t slot = fbase(c, c->view_set) + i + 1;
     const LevelDesc& L = c->lv_h[level];
     const int nc = L.cell_end - L.cell_begin;
     std::vector<int> cnt(nc);
@@ -695,8 +774,9 @@ int odo_debug_fast(odo_ctx* c, int i, int level, orb_kp* out, int cap, int* n) {
 
 int odo_debug_octree(odo_ctx* c, int i, int level, orb_kp* out, int cap, int* n) {
     if (!c || i < 0 || i >= c->last_n || level < 0 || level >= c->nlevels) return fail(ODO_ERR_ARG, "bad args");
-    HIPCHK(hipStreamSynchronize(c->stream));
-    const int slot = i + 1;
+    int e;
+    if ((e = sync_all(c))) return e;
+    const size_t slot = fbase(c, c->view_set) + i + 1;
     int cnt = 0;
     HIPCHK(hipMemcpy(&cnt, c->ocnt + (size_t)slot * c->nlevels + level, sizeof(int), hipMemcpyDeviceToHost));
     std::vector<uint32_t> k(std::max(cnt, 1));
@@ -710,12 +790,15 @@ int odo_debug_octree(odo_ctx* c, int i, int level, orb_kp* out, int cap, int* n)
 int odo_last_timings(odo_ctx* c, float* ms, int cap, const char** names) {
     static const char* kNames[] = {"gray+pyramid", "fast", "octree", "blur", "finalize", "knn2", "match+sort",
                                    "ransac", "pnp"};
+    // stage i spans events (a[i], b[i]): extraction stream 0..5, pair stream 10,6..9
+    static const int a[9] = {0, 1, 2, 3, 4, 10, 6, 7, 8}, b[9] = {1, 2, 3, 4, 5, 6, 7, 8, 9};
     if (!c) return fail(ODO_ERR_ARG, "null ctx");
-    HIPCHK(hipStreamSynchronize(c->stream));
+    int e;
+    if ((e = sync_all(c))) return e;
     int m = 0;
     for (int i = 0; i < 9 && i < cap; i++) {
         float t = 0;
-        if (hipEventElapsedTime(&t, c->ev[i], c->ev[i + 1]) != hipSuccess) t = -1;
+        if (hipEventElapsedTime(&t, c->ev[a[i]], c->ev[b[i]]) != hipSuccess) t = -1;
         ms[i] = t;
         if (names) names[i] = kNames[i];
         m++;
@@ -773,24 +856,28 @@ extern "C" {
 int odo_extract(odo_ctx* c, const uint8_t* img, int channels, const uint16_t* depth, orb_kp* kps, uint8_t* desc,
                 float* kps_un, float* xyz, float* u_right, int cap, int* n) {
     if (!c || !img || (channels != 1 && channels != 3) || !n) return fail(ODO_ERR_ARG, "bad extract args");
+    int e0;
+    if ((e0 = sync_all(c))) return e0;
     hipStream_t st = c->stream;
     const size_t npix = (size_t)c->W * c->H;
+    const int set = c->seq_set ^ 1;
     const int slot = 1;
     if (depth) HIPCHK(hipMemcpyAsync(c->depth_in, depth, npix * 2, hipMemcpyHostToDevice, st));
     else HIPCHK(hipMemsetAsync(c->depth_in, 0, npix * 2, st));
     if (channels == 3) {
         HIPCHK(hipMemcpyAsync(c->bgr_in, img, npix * 3, hipMemcpyHostToDevice, st));
         hipEventRecord(c->ev[0], st);
-        int e = run_extract(c, c->bgr_in, c->depth_in, 1, slot);
+        int e = run_extract(c, set, c->bgr_in, c->depth_in, 1, slot);
         if (e) return e;
     } else {
         // ORBextractor::operator() on a gray image: level 0 = the image itself
-        HIPCHK(hipMemcpyAsync(c->pyr + (size_t)slot * c->pyr_size, img, npix, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(c->pyr + (fbase(c, set) + slot) * c->pyr_size, img, npix, hipMemcpyHostToDevice, st));
         hipEventRecord(c->ev[0], st);
-        int e = run_extract_from_gray(c, c->depth_in, 1, slot);
+        int e = run_extract_from_gray(c, set, c->depth_in, 1, slot);
         if (e) return e;
     }
-    c->last_n = std::max(c->last_n, 1);
+    c->view_set = set;
+    c->last_n = 1;
     return odo_get_frame(c, 0, kps, desc, kps_un, xyz, u_right, cap, n);
 }
 

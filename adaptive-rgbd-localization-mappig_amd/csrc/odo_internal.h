@@ -77,12 +77,17 @@ void launch_finalize(hipStream_t st, const uint8_t* pyr, const uint8_t* blur, si
                      int nlevels, const uint32_t* okp, const int* ocnt, int okp_stride, const uint16_t* depth,
                      size_t depth_stride, int img_w, FrameCalib cal, orb_kp* kps, uint8_t* desc, float* kun, float* xyz,
                      float* ur, int* nkp, int kp_cap, int nframes);
+void launch_pair_valid(hipStream_t st, int* pv, int n, int first_valid);
+void launch_copy_frame(hipStream_t st, const orb_kp* kps_s, const uint8_t* desc_s, const float* kun_s,
+                       const float* xyz_s, const float* ur_s, const int* n_s, orb_kp* kps_d, uint8_t* desc_d,
+                       float* kun_d, float* xyz_d, float* ur_d, int* n_d, int kp_cap);
 void launch_knn2(hipStream_t st, const uint8_t* q, const int* qn, size_t q_stride, const uint8_t* t, const int* tn,
                  size_t t_stride, int2* idx, int2* dist, size_t out_stride, int max_q, int npairs);
 void launch_pair_match(hipStream_t st, const int2* knn_idx, const int2* knn_dist, size_t knn_stride, const float* xyz,
                        const int* nkp, int kp_cap, int slot0, float ratio, float th_depth_m, int check_depth,
                        odo_dmatch* matches, int* n_matches, void* good, int* n_good, int32_t* f2_src,
                        uint64_t* sort_scratch, int match_cap, int npairs);
+int launch_sort_dbg(hipStream_t st, void* a, int n);
 void launch_latch(hipStream_t st, double* latch, const void* good, const int* n_good, const int* n_matches,
                   const odo_dmatch* matches, const float* xyz, int kp_cap, int slot0, int npairs, int match_cap,
                   int min_inl, int sample_size, int iterations, const int* pair_valid);

@@ -121,6 +121,10 @@ int odo_debug_pyramid(odo_ctx* ctx, int i, uint8_t* out, size_t cap);
 int odo_debug_fast(odo_ctx* ctx, int i, int level, orb_kp* out, int cap, int* n);
 int odo_debug_octree(odo_ctx* ctx, int i, int level, orb_kp* out, int cap, int* n);
 int odo_debug_blur(odo_ctx* ctx, int i, uint8_t* out, size_t cap);
+/* std::sort(vGoodMatches) of Ransac::Iterate (ransac.cpp:199) as the pair
+ * stage runs it on the GPU (workgroup-parallel introsort): in -> out sorted by
+ * distance in libstdc++'s exact (unstable) order; distances must be >= 0. */
+int odo_debug_sort(odo_ctx* ctx, const odo_dmatch* in, int n, odo_dmatch* out);
 /* Per-kernel device time of the last odo_track_batch (ms), via HIP events. */
 int odo_last_timings(odo_ctx* ctx, float* ms, int cap, const char** names);
 

@@ -950,6 +950,13 @@ int32_t rng_next(odo_rng* r) {
 // ================================================================ C API
 extern "C" {
 
+// std::sort(vector<cv::DMatch>) as in Ransac::Iterate (ransac.cpp:199):
+// libstdc++ introsort by distance (cv::DMatch::operator<), unstable.
+void oracle_sort_dmatch(void* v, int n) {
+    DM* a = static_cast<DM*>(v);
+    std::sort(a, a + n);
+}
+
 void oracle_frame_geometry(const orb_kp* kps, int n, const float* depth, int w, int h,
                            const odo_calib* c, float* kps_un, float* xyz, float* u_right) {
     (void)h;

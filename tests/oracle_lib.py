@@ -87,6 +87,7 @@ def lib():
             "oracle_extract_frame": (C.c_int, [P, P, C.c_int, C.c_int, P, P, P, P, P, P, P, C.c_int]),
             "oracle_knn2": (None, [P, C.c_int, P, C.c_int, P, P]),
             "oracle_knn_match": (C.c_int, [P, C.c_int, P, C.c_int, C.c_float, P, P, P, P, P, P, P, C.c_int]),
+            "oracle_sort_dmatch": (None, [P, C.c_int]),
             "oracle_vo_landmarks": (C.c_int, [P, C.c_int, C.c_float, P]),
             "oracle_rng_seed": (None, [P, C.c_uint32]),
             "oracle_rng_next": (C.c_int32, [P]),

@@ -145,6 +145,62 @@ def test_pairs_match_ransac_pnp(cfg2_run):
     assert abs(odo.latch - latch) == 0
 
 
+def test_pipelined_batches_roll_and_seeds():
+    """Batches queued back to back (extraction of one overlapping the pair
+    stages of the previous, alternating frame sets): the last batch's pair 0
+    links the previous batch's last frame, seeds follow the global pair index
+    and the latch from the first valid pair carries over."""
+    pkg = load_pkg()
+    bgr, dep, _ = sequence(8)
+    odo, cfg = make_odo(pkg, 640, 480, 1000, 300, 3)
+    cal = oracle_calib(cfg)
+    odo.track_batch_host(bgr[0:3], dep[0:3], want_results=False)
+    odo.track_batch_host(bgr[3:6], dep[3:6], want_results=False)
+    res = odo.track_batch_host(bgr[6:8], dep[6:8])
+    frames = [O.extract_frame(bgr[i], dep[i], O.orb_params(1000), cal) for i in range(8)]
+    for i in range(2):
+        got = odo.frame(i)
+        assert np.array_equal(got["desc"], frames[6 + i]["desc"]), f"frame {6 + i} descriptors"
+    rp = O.ransac_params(300)
+    latch = float("nan")
+    refs = {}
+    for f in range(1, 8):  # the oracle walks the whole sequence (latch set by pair 1)
+        refs[f] = O.track_pair(frames[f - 1], frames[f], cal, rp, pkg.pair_seed(cfg.seed, f), latch)
+        latch = refs[f][3]
+    for p, f in ((0, 6), (1, 7)):
+        r, mask, matches, _ = refs[f]
+        g = odo.pair(p)
+        assert np.array_equal(g["matches"], matches), f"frame {f}: match list differs"
+        assert res[p]["visited"] == r.visited and res[p]["n_inliers"] == r.n_inliers
+        assert np.array_equal(res[p]["T12"], np.array(r.T12, np.float32)), f"frame {f}: T12 not bit-exact"
+        T_gpu = res[p]["Tcw"].reshape(4, 4)
+        assert np.abs(T_gpu - np.array(r.Tcw, np.float32).reshape(4, 4)).max() < 1e-4
+    assert odo.latch == latch
+
+
+@pytest.mark.parametrize("n,levels", [(1, 3), (15, 4), (16, 3), (17, 5), (100, 2), (613, 40), (777, 256),
+                                      (2048, 30), (4099, 7), (8192, 200)])
+def test_good_match_sort_is_std_sort(pkg, n, levels):
+    """The pair stage's workgroup-parallel introsort returns exactly
+    libstdc++'s std::sort permutation (ties included: Hamming distances take
+    few values), against the oracle's std::sort on the same DMatch array."""
+    rng = np.random.default_rng(n * 31 + levels)
+    m = np.zeros(n, O.DMATCH_DTYPE)
+    m["queryIdx"] = np.arange(n)
+    m["trainIdx"] = rng.integers(0, 5000, n)
+    m["distance"] = rng.integers(0, levels, n).astype(np.float32)
+    if n > 100:  # presorted and reversed runs stress the median-of-3 / depth limit
+        k = n // 3
+        m["distance"][:k] = np.sort(m["distance"][:k])
+        m["distance"][k:2 * k] = np.sort(m["distance"][k:2 * k])[::-1]
+    ref = m.copy()
+    O.lib().oracle_sort_dmatch(O.ptr(ref), n)
+    got = np.zeros(n, O.DMATCH_DTYPE)
+    odo, _ = make_odo(pkg, 640, 480, 1000, 10, 1)
+    pkg.check(pkg.load().odo_debug_sort(odo.h, pkg.ptr(m), n, pkg.ptr(got)))
+    assert np.array_equal(got["queryIdx"], ref["queryIdx"]), "permutation differs from std::sort"
+
+
 def test_knn2_entry_point(pkg):
     rng = np.random.default_rng(7)
     q = rng.integers(0, 256, (777, 32), dtype=np.uint8)
