@@ -618,52 +618,103 @@ __global__ void __launch_bounds__(OT_THREADS) k_octree(const uint32_t* __restric
 }
 
 // ============================================================ blur
-// Separable 7-tap Q8 kernel {18,34,48,56,48,34,18}, REFLECT_101, exact integer.
-#define BLUR_TX 64
-#define BLUR_TY 16
+// Separable 7-tap Q8 kernel {18,34,48,56,48,34,18}, REFLECT_101, exact integer
+// (GaussianBlur 7x7 sigma 2 on 8U). One 128x32 output tile per workgroup over
+// a flattened (level, tile) grid; the 134x38 input window is staged in LDS
+// (reflection only on border tiles), the horizontal pass makes 4 outputs from
+// three aligned LDS dwords, the vertical pass 4x4 outputs per thread.
+#define BLUR_TX 128
+#define BLUR_TY 32
+#define BLUR_IW (BLUR_TX + 8)  // staged row stride (>= 134, multiple of 4)
+#define BLUR_IH (BLUR_TY + 6)
 ODO_INLINE int reflect101(int i, int n) {
     while (i < 0 || i >= n) i = i < 0 ? -i : 2 * n - 2 - i;
     return i;
 }
 
+struct BlurTiles {
+    int base[17];  // first tile of each level (prefix), base[nlevels] = total
+    int tx[16];    // tiles across
+};
+
 __global__ void __launch_bounds__(256) k_blur(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
-                                              size_t pyr_stride, const LevelDesc* __restrict__ lv) {
-    __shared__ uint8_t tile[(BLUR_TY + 6) * (BLUR_TX + 8)];
-    __shared__ uint16_t hrow[(BLUR_TY + 6) * BLUR_TX];
-    const int f = blockIdx.z;
-    const int l = blockIdx.y;
+                                              size_t pyr_stride, const LevelDesc* __restrict__ lv, BlurTiles TT,
+                                              int nlevels) {
+    __shared__ __attribute__((aligned(16))) uint8_t tile[BLUR_IH * BLUR_IW];
+    __shared__ __attribute__((aligned(16))) uint16_t hrow[BLUR_IH * BLUR_TX];
+    const int f = blockIdx.y;
+    const int tid = blockIdx.x;
+    int l = 0;
+    while (l + 1 < nlevels && tid >= TT.base[l + 1]) l++;
     const LevelDesc L = lv[l];
-    const int tilesX = (L.w + BLUR_TX - 1) / BLUR_TX;
-    const int tilesY = (L.h + BLUR_TY - 1) / BLUR_TY;
-    if ((int)blockIdx.x >= tilesX * tilesY) return;
-    const int tx0 = (blockIdx.x % tilesX) * BLUR_TX, ty0 = (blockIdx.x / tilesX) * BLUR_TY;
+    const int ti = tid - TT.base[l];
+    const int tx0 = (ti % TT.tx[l]) * BLUR_TX, ty0 = (ti / TT.tx[l]) * BLUR_TY;
     const uint8_t* src = pyr + (size_t)f * pyr_stride + L.off;
     uint8_t* dst = blur + (size_t)f * pyr_stride + L.off;
-    const int TW = BLUR_TX + 6, TH = BLUR_TY + 6;
-    for (int p = threadIdx.x; p < TW * TH; p += 256) {
-        const int r = p / TW, c = p % TW;
-        const int y = reflect101(ty0 + r - 3, L.h), x = reflect101(tx0 + c - 3, L.w);
-        tile[r * (BLUR_TX + 8) + c] = src[(size_t)y * L.w + x];
+    const int t = threadIdx.x;
+    const bool interior = tx0 >= 3 && ty0 >= 3 && tx0 + BLUR_TX + 3 <= L.w && ty0 + BLUR_TY + 3 <= L.h;
+    // stage rows ty0-3 .. ty0+34, columns tx0-3 .. tx0+130 (one wave per row pass)
+    const int TW = BLUR_TX + 6;
+    if (interior) {
+        for (int r = t >> 6; r < BLUR_IH; r += 4) {
+            const uint8_t* srow = src + (size_t)(ty0 + r - 3) * L.w + (tx0 - 3);
+            for (int c = t & 63; c < TW; c += 64) tile[r * BLUR_IW + c] = srow[c];
+        }
+    } else {
+        for (int r = t >> 6; r < BLUR_IH; r += 4) {
+            const uint8_t* srow = src + (size_t)reflect101(ty0 + r - 3, L.h) * L.w;
+            for (int c = t & 63; c < TW; c += 64) tile[r * BLUR_IW + c] = srow[reflect101(tx0 + c - 3, L.w)];
+        }
     }
     __syncthreads();
-    const int kq[7] = {18, 34, 48, 56, 48, 34, 18};
-    for (int p = threadIdx.x; p < TH * BLUR_TX; p += 256) {
-        const int r = p / BLUR_TX, c = p % BLUR_TX;
-        const uint8_t* s = &tile[r * (BLUR_TX + 8) + c];
-        uint32_t h = 0;
+    // horizontal: row r, outputs 4q..4q+3 need staged bytes 4q..4q+9
+    for (int it = t; it < BLUR_IH * (BLUR_TX / 4); it += 256) {
+        const int r = it / (BLUR_TX / 4), q = it % (BLUR_TX / 4);
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(&tile[r * BLUR_IW + 4 * q]);
+        const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+        uint32_t b[10];
 #pragma unroll
-        for (int j = 0; j < 7; j++) h += (uint32_t)kq[j] * s[j];
-        hrow[r * BLUR_TX + c] = (uint16_t)h;
+        for (int i = 0; i < 4; i++) {
+            b[i] = (w0 >> (8 * i)) & 0xff;
+            b[4 + i] = (w1 >> (8 * i)) & 0xff;
+        }
+        b[8] = w2 & 0xff;
+        b[9] = (w2 >> 8) & 0xff;
+        uint32_t h[4];
+#pragma unroll
+        for (int o = 0; o < 4; o++)
+            h[o] = 18u * b[o] + 34u * b[o + 1] + 48u * b[o + 2] + 56u * b[o + 3] + 48u * b[o + 4] + 34u * b[o + 5] +
+                   18u * b[o + 6];
+        uint2 pk;
+        pk.x = h[0] | (h[1] << 16);
+        pk.y = h[2] | (h[3] << 16);
+        *reinterpret_cast<uint2*>(&hrow[r * BLUR_TX + 4 * q]) = pk;
     }
     __syncthreads();
-    for (int p = threadIdx.x; p < BLUR_TY * BLUR_TX; p += 256) {
-        const int r = p / BLUR_TX, c = p % BLUR_TX;
-        const int y = ty0 + r, x = tx0 + c;
-        if (y < L.h && x < L.w) {
-            uint32_t v = 0;
+    // vertical: 4 columns x 4 rows per thread
+    {
+        const int q = t % (BLUR_TX / 4), rb = (t / (BLUR_TX / 4)) * 4;  // 32 x 8 threads
+        uint32_t v[10][4];
 #pragma unroll
-            for (int j = 0; j < 7; j++) v += (uint32_t)kq[j] * hrow[(r + j) * BLUR_TX + c];
-            dst[(size_t)y * L.w + x] = (uint8_t)((v + 32768u) >> 16);
+        for (int j = 0; j < 10; j++) {
+            const uint2 pk = *reinterpret_cast<const uint2*>(&hrow[(rb + j) * BLUR_TX + 4 * q]);
+            v[j][0] = pk.x & 0xffff;
+            v[j][1] = pk.x >> 16;
+            v[j][2] = pk.y & 0xffff;
+            v[j][3] = pk.y >> 16;
+        }
+#pragma unroll
+        for (int o = 0; o < 4; o++) {
+            const int y = ty0 + rb + o;
+            if (y >= L.h) break;
+            uint8_t* drow = dst + (size_t)y * L.w;
+#pragma unroll
+            for (int cI = 0; cI < 4; cI++) {
+                const int x = tx0 + 4 * q + cI;
+                const uint32_t s = 18u * v[o][cI] + 34u * v[o + 1][cI] + 48u * v[o + 2][cI] + 56u * v[o + 3][cI] +
+                                   48u * v[o + 4][cI] + 34u * v[o + 5][cI] + 18u * v[o + 6][cI];
+                if (x < L.w) drow[x] = (uint8_t)((s + 32768u) >> 16);
+            }
         }
     }
 }
@@ -833,10 +884,17 @@ void launch_octree(hipStream_t st, const uint32_t* cand, const int* cand_cnt, co
     hipLaunchKernelGGL(k_octree, g, dim3(OT_THREADS), octree_lds_bytes(node_cap), st, cand, cand_cnt, lv, ncells,
                        cell_cap, nlevels, keys, knode, kquad, keys_stride, okp, ocnt, okp_stride, node_cap);
 }
-void launch_blur(hipStream_t st, const uint8_t* pyr, uint8_t* blur, size_t pyr_stride, const LevelDesc* lv, int nlevels,
-                 int max_tiles, int nframes) {
-    dim3 g(max_tiles, nlevels, nframes);
-    hipLaunchKernelGGL(k_blur, g, dim3(256), 0, st, pyr, blur, pyr_stride, lv);
+void launch_blur(hipStream_t st, const uint8_t* pyr, uint8_t* blur, size_t pyr_stride, const LevelDesc* lv,
+                 const LevelDesc* lv_host, int nlevels, int nframes) {
+    BlurTiles T{};
+    int acc = 0;
+    for (int l = 0; l < nlevels; l++) {
+        T.base[l] = acc;
+        T.tx[l] = (lv_host[l].w + BLUR_TX - 1) / BLUR_TX;
+        acc += T.tx[l] * ((lv_host[l].h + BLUR_TY - 1) / BLUR_TY);
+    }
+    T.base[nlevels] = acc;
+    hipLaunchKernelGGL(k_blur, dim3(acc, nframes), dim3(256), 0, st, pyr, blur, pyr_stride, lv, T, nlevels);
 }
 void launch_finalize(hipStream_t st, const uint8_t* pyr, const uint8_t* blur, size_t pyr_stride, const LevelDesc* lv,
                      int nlevels, const uint32_t* okp, const int* ocnt, int okp_stride, const uint16_t* depth,

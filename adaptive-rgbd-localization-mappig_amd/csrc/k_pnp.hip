@@ -279,23 +279,24 @@ ODO_INLINE bool ldlt_solve6(const double Ain[6][6], const double b[6], double x[
 // Xw, observations and the information weight as float (cv::Mat / KeyPoint,
 // pnpsolver.cpp:74-125) and widens to double inside g2o; we store the floats.
 struct PEdgeSoA {
-    float* X;      // 3*cap
-    float* obs;    // 3*cap
-    float* info;   // cap
+    float* X;        // 3*cap
+    float* obs;      // 3*cap
+    float* info;     // cap
     uint8_t* flags;  // cap: bit0 stereo, bit1 outlier (level 1), bit2 robust kernel on
-    double* chi;   // cap: chi2 of the stored _error (last computeActiveErrors / computeError)
-    int* idx;      // cap: F2 keypoint index
+    double* chi4;    // 4*cap: chi2 of the stored _error per speculative trial slot
+    int* idx;        // cap: F2 keypoint index
 };
 
 #define PE_STEREO 1
 #define PE_OUT 2
 #define PE_ROBUST 4
+#define PE_BYTES 72
 
 ODO_INLINE PEdgeSoA pedge_view(void* base, int cap, int p) {
-    char* b = (char*)base + (size_t)p * (size_t)cap * 48;
+    char* b = (char*)base + (size_t)p * (size_t)cap * PE_BYTES;
     PEdgeSoA E;
-    E.chi = (double*)b;
-    E.X = (float*)(b + (size_t)cap * 8);
+    E.chi4 = (double*)b;
+    E.X = (float*)(b + (size_t)cap * 32);
     E.obs = E.X + 3 * cap;
     E.info = E.obs + 3 * cap;
     E.idx = (int*)(E.info + cap);
@@ -355,6 +356,7 @@ ODO_INLINE void huber_rho(double delta, double chi, double rho[3]) {
 // fixed xor-butterfly (deterministic).
 #define PNP_NW 4
 #define PNP_NT (64 * PNP_NW)
+#define PNP_K 4  // Levenberg trials evaluated per edge pass
 
 // Sum of NV per-lane doubles over the workgroup: xor-butterfly per wave, then
 // waves added in index order (fixed order => deterministic).
@@ -363,7 +365,6 @@ ODO_INLINE void wg_sum(double (&v)[NV], double* red) {
 #pragma unroll
     for (int k = 0; k < NV; k++) v[k] = wave_sum(v[k]);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (PNP_NW == 1) return;
     if (lane == 0)
 #pragma unroll
         for (int k = 0; k < NV; k++) red[wave * NV + k] = v[k];
@@ -377,16 +378,42 @@ ODO_INLINE void wg_sum(double (&v)[NV], double* red) {
     __syncthreads();
 }
 
+// robust (Huber) chi2 of one edge at pose T; c2 = plain chi2 of the stored error
+ODO_INLINE double edge_robust_chi(const SE3& T, const double Xw[3], const double ob[3], double info, uint8_t fl,
+                                  const PnPCam& cam, double dMono, double dStereo, double& c2) {
+    const bool st = fl & PE_STEREO;
+    double Xc[3], e[3];
+    se3_map(T, Xw, Xc);
+    edge_err(Xc, ob, st, cam, e);
+    c2 = chi2_of(e, info, st);
+    if (fl & PE_ROBUST) {
+        double rr[3];
+        huber_rho(st ? dStereo : dMono, c2, rr);
+        return rr[0];
+    }
+    return c2;
+}
+
+// One workgroup (4 waves) per pair. OptimizationAlgorithmLevenberg's trial
+// loop (reject -> lambda *= ni, ni *= 2) is run speculatively: the next
+// PNP_K lambdas of a rejection run are known in advance, so waves 0..K-1 each
+// solve one candidate step, a single edge pass sums chi2 for all candidates,
+// and the sequential accept/reject control flow is replayed over the results
+// (same decisions, same state as the one-trial-at-a-time loop).
 __global__ void __launch_bounds__(PNP_NT) k_pnp(const int32_t* __restrict__ f2_src, const float* __restrict__ xyz,
                                             const float* __restrict__ kun, const float* __restrict__ ur,
                                             const int* __restrict__ nkp, int kp_cap, int slot0, FrameCalib cal,
                                             const float* __restrict__ T12, const int* __restrict__ pair_valid,
                                             const int* __restrict__ n_matches, int min_matches, void* edges_g,
                                             odo_pair_result* __restrict__ res, uint8_t* __restrict__ inlier_mask) {
+    __builtin_amdgcn_s_setprio(3);  // latency-bound: issue ahead of co-resident extraction waves
     const int p = blockIdx.x;
     const int lane = threadIdx.x;  // thread index within the workgroup
-    const int wlane = threadIdx.x & 63;
+    const int wlane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     __shared__ double red[PNP_NW * 28];
+    __shared__ double s_acc[28];  // reduced H (upper, row-major), b, chi of the iteration
+    __shared__ double s_T[PNP_K][8];
+    __shared__ int s_ok[PNP_K];
     __shared__ int s_ne[PNP_NW];
     odo_pair_result* R = res + p;
     const int s1 = slot0 + p, s2 = slot0 + p + 1;
@@ -408,11 +435,11 @@ __global__ void __launch_bounds__(PNP_NT) k_pnp(const int32_t* __restrict__ f2_s
         const int i = c0 + lane;
         const bool has = i < n2 && src[i] >= 0;
         const uint64_t bal = __ballot(has);
-        if (wlane == 0) s_ne[lane >> 6] = __popcll(bal);
+        if (wlane == 0) s_ne[wave] = __popcll(bal);
         __syncthreads();
         int before = 0, tot = 0;
         for (int w = 0; w < PNP_NW; w++) {
-            if (w < (lane >> 6)) before += s_ne[w];
+            if (w < wave) before += s_ne[w];
             tot += s_ne[w];
         }
         __syncthreads();
@@ -430,7 +457,6 @@ __global__ void __launch_bounds__(PNP_NT) k_pnp(const int32_t* __restrict__ f2_s
             E.obs[3 * k + 2] = st ? urv : 0.f;
             E.info[k] = 1.0f / (zw * zw);
             E.flags[k] = (uint8_t)((st ? PE_STEREO : 0) | PE_ROBUST);
-            E.chi[k] = 0.0;
             E.idx[k] = i;
         }
         ne += tot;
@@ -456,11 +482,23 @@ __global__ void __launch_bounds__(PNP_NT) k_pnp(const int32_t* __restrict__ f2_s
     const float chi2Mono = 5.991f, chi2Stereo = 7.815f;
     int nBad = 0;
     SE3 T = T0s;
+#ifdef ODO_PNP_PROFILE
+    // -DODO_PNP_PROFILE: phase times (10 ns ticks) of one pair via printf
+    uint64_t tb = 0, tsol = 0, tchi = 0, tcls = 0, t0 = 0, tall = wall_clock64();
+    int nit = 0, ntr = 0;
+#define PP_T0() t0 = wall_clock64()
+#define PP_ACC(x) x += wall_clock64() - t0
+#else
+#define PP_T0()
+#define PP_ACC(x)
+#endif
+    int last_slot = 0;  // trial slot whose errors the edges store (last computeActiveErrors)
     for (int it = 0; it < 4; it++) {
         T = T0s;  // vSE3->setEstimate(pFrame->GetPose()) (pnpsolver.cpp:150)
         double lambda = 0, ni = 2;
         for (int iter = 0; iter < 10; iter++) {
             // computeActiveErrors + activeRobustChi2 + buildSystem at T
+            PP_T0();
             double acc[28];
 #pragma unroll
             for (int k = 0; k < 28; k++) acc[k] = 0;
@@ -475,7 +513,6 @@ __global__ void __launch_bounds__(PNP_NT) k_pnp(const int32_t* __restrict__ f2_s
                 se3_map(T, Xw, Xc);
                 edge_err(Xc, ob, st, cam, e);
                 const double c2 = chi2_of(e, info, st);
-                E.chi[k] = c2;
                 double rho[3] = {c2, 1.0, 0.0};
                 if (fl & PE_ROBUST) huber_rho(st ? dStereo : dMono, c2, rho);
                 acc[27] += rho[0];
@@ -519,85 +556,157 @@ __global__ void __launch_bounds__(PNP_NT) k_pnp(const int32_t* __restrict__ f2_s
                 }
             }
             wg_sum<28>(acc, red);
-            double H[6][6], b[6];
-            {
-                int h = 0;
-                for (int a = 0; a < 6; a++)
-                    for (int cc = a; cc < 6; cc++) {
-                        H[a][cc] = acc[h];
-                        H[cc][a] = acc[h];
-                        h++;
-                    }
-                for (int a = 0; a < 6; a++) b[a] = acc[21 + a];
-            }
+            PP_ACC(tb);
+#ifdef ODO_PNP_PROFILE
+            nit++;
+#endif
+            if (lane == 0)
+#pragma unroll
+                for (int k = 0; k < 28; k++) s_acc[k] = acc[k];
             double curChi = acc[27];
             if (iter == 0) {
+                // diagonal of the packed upper triangle: 0, 6, 11, 15, 18, 20
                 double mx = 0;
-                for (int j = 0; j < 6; j++) mx = fmax(fabs(H[j][j]), mx);
+                mx = fmax(fabs(acc[0]), mx);
+                mx = fmax(fabs(acc[6]), mx);
+                mx = fmax(fabs(acc[11]), mx);
+                mx = fmax(fabs(acc[15]), mx);
+                mx = fmax(fabs(acc[18]), mx);
+                mx = fmax(fabs(acc[20]), mx);
                 lambda = 1e-5 * mx;
                 ni = 2;
             }
-            // OptimizationAlgorithmLevenberg::solve trial loop
+            __syncthreads();
+            // ---- OptimizationAlgorithmLevenberg::solve trial loop, PNP_K trials per pass
             double rho = 0;
             int qmax = 0;
-            do {
-                const SE3 backup = T;
-                double Hl[6][6];
-                for (int a = 0; a < 6; a++)
-                    for (int cc = 0; cc < 6; cc++) Hl[a][cc] = H[a][cc];
-                for (int j = 0; j < 6; j++) Hl[j][j] += lambda;
-                double x[6] = {0, 0, 0, 0, 0, 0};
-                const bool ok2 = ldlt_solve6(Hl, b, x);
-                T = se3_mul(se3_exp(x), T);
-                double chi = 0;
-                for (int k = lane; k < ne; k += PNP_NT) {
-                    const uint8_t fl = E.flags[k];
+            bool trials_done = false;
+            while (!trials_done) {
+                const int K = min(PNP_K, 10 - qmax);
+                // lambdas of the next K trials if every one of them is rejected
+                double lam[PNP_K], nis[PNP_K];
+                {
+                    double l = lambda, n_ = ni;
+#pragma unroll
+                    for (int k = 0; k < PNP_K; k++) {
+                        lam[k] = l;
+                        nis[k] = n_;
+                        l *= n_;
+                        n_ *= 2;
+                    }
+                }
+                PP_T0();
+                if (wave < K) {
+                    double lw = lam[0];
+#pragma unroll
+                    for (int k = 1; k < PNP_K; k++)
+                        if (wave == k) lw = lam[k];
+                    double Hl[6][6], b[6];
+                    {
+                        int h = 0;
+#pragma unroll
+                        for (int a = 0; a < 6; a++)
+#pragma unroll
+                            for (int cc = a; cc < 6; cc++) {
+                                Hl[a][cc] = s_acc[h];
+                                Hl[cc][a] = s_acc[h];
+                                h++;
+                            }
+#pragma unroll
+                        for (int a = 0; a < 6; a++) b[a] = s_acc[21 + a];
+                    }
+                    for (int j = 0; j < 6; j++) Hl[j][j] += lw;
+                    double x[6] = {0, 0, 0, 0, 0, 0};
+                    const bool ok2 = ldlt_solve6(Hl, b, x);
+                    const SE3 Tk = se3_mul(se3_exp(x), T);
+                    double scale = 0;
+                    for (int j = 0; j < 6; j++) scale += x[j] * (lw * x[j] + b[j]);
+                    scale += 1e-3;
+                    if (wlane == 0) {
+                        s_T[wave][0] = Tk.q.x;
+                        s_T[wave][1] = Tk.q.y;
+                        s_T[wave][2] = Tk.q.z;
+                        s_T[wave][3] = Tk.q.w;
+                        s_T[wave][4] = Tk.t[0];
+                        s_T[wave][5] = Tk.t[1];
+                        s_T[wave][6] = Tk.t[2];
+                        s_T[wave][7] = scale;
+                        s_ok[wave] = ok2 ? 1 : 0;
+                    }
+                }
+                __syncthreads();
+                SE3 Tc[PNP_K];
+                double sc[PNP_K];
+                bool okc[PNP_K];
+#pragma unroll
+                for (int k = 0; k < PNP_K; k++) {
+                    Tc[k].q = Quat{s_T[k][0], s_T[k][1], s_T[k][2], s_T[k][3]};
+                    Tc[k].t[0] = s_T[k][4];
+                    Tc[k].t[1] = s_T[k][5];
+                    Tc[k].t[2] = s_T[k][6];
+                    sc[k] = s_T[k][7];
+                    okc[k] = s_ok[k] != 0;
+                }
+                PP_ACC(tsol);
+                PP_T0();
+                // computeActiveErrors + activeRobustChi2 at every candidate
+                double chi[PNP_K];
+#pragma unroll
+                for (int k = 0; k < PNP_K; k++) chi[k] = 0;
+                for (int e = lane; e < ne; e += PNP_NT) {
+                    const uint8_t fl = E.flags[e];
                     if (fl & PE_OUT) continue;
-                    const bool st = fl & PE_STEREO;
-                    const double Xw[3] = {E.X[3 * k], E.X[3 * k + 1], E.X[3 * k + 2]};
-                    const double ob[3] = {E.obs[3 * k], E.obs[3 * k + 1], E.obs[3 * k + 2]};
-                    double Xc[3], e[3];
-                    se3_map(T, Xw, Xc);
-                    edge_err(Xc, ob, st, cam, e);
-                    const double c2 = chi2_of(e, (double)E.info[k], st);
-                    E.chi[k] = c2;
-                    if (fl & PE_ROBUST) {
-                        double rr[3];
-                        huber_rho(st ? dStereo : dMono, c2, rr);
-                        chi += rr[0];
-                    } else chi += c2;
+                    const double Xw[3] = {E.X[3 * e], E.X[3 * e + 1], E.X[3 * e + 2]};
+                    const double ob[3] = {E.obs[3 * e], E.obs[3 * e + 1], E.obs[3 * e + 2]};
+                    const double info = E.info[e];
+#pragma unroll
+                    for (int k = 0; k < PNP_K; k++) {
+                        if (k >= K) break;
+                        double c2;
+                        chi[k] += edge_robust_chi(Tc[k], Xw, ob, info, fl, cam, dMono, dStereo, c2);
+                        E.chi4[4 * e + k] = c2;
+                    }
                 }
-                double chv[1] = {chi};
-                wg_sum<1>(chv, red);
-                double tempChi = chv[0];
-                if (!ok2) tempChi = 1.7976931348623157e308;
-                rho = curChi - tempChi;
-                double scale = 0;
-                for (int j = 0; j < 6; j++) scale += x[j] * (lambda * x[j] + b[j]);
-                scale += 1e-3;
-                rho /= scale;
-                if (rho > 0 && isfinite(tempChi)) {
-                    double alpha = 1. - pow((2 * rho - 1), 3);
-                    alpha = fmin(alpha, 2. / 3.);
-                    double sf = fmax(1. / 3., alpha);
-                    lambda *= sf;
-                    ni = 2;
-                    curChi = tempChi;
-                } else {
-                    lambda *= ni;
-                    ni *= 2;
-                    T = backup;
+                wg_sum<PNP_K>(chi, red);
+                PP_ACC(tchi);
+                // replay the trials in order
+#pragma unroll
+                for (int k = 0; k < PNP_K; k++) {
+                    if (k >= K || trials_done) break;
+#ifdef ODO_PNP_PROFILE
+                    ntr++;
+#endif
+                    double tempChi = chi[k];
+                    if (!okc[k]) tempChi = 1.7976931348623157e308;
+                    rho = curChi - tempChi;
+                    rho /= sc[k];
+                    last_slot = k;
+                    qmax++;
+                    if (rho > 0 && isfinite(tempChi)) {
+                        double alpha = 1. - pow((2 * rho - 1), 3);
+                        alpha = fmin(alpha, 2. / 3.);
+                        const double sf = fmax(1. / 3., alpha);
+                        lambda = lam[k] * sf;
+                        ni = 2;
+                        curChi = tempChi;
+                        T = Tc[k];
+                        trials_done = true;
+                    } else {
+                        lambda = lam[k] * nis[k];  // T stays at the backup
+                        ni = nis[k] * 2;
+                        if (!(rho < 0 && qmax < 10)) trials_done = true;
+                    }
                 }
-                qmax++;
-            } while (rho < 0 && qmax < 10);
+            }
             if (qmax == 10 || rho == 0) break;
         }
         // ---- classification (pnpsolver.cpp:157-201)
+        PP_T0();
         int bad = 0;
         for (int k = lane; k < ne; k += PNP_NT) {
             uint8_t fl = E.flags[k];
             const bool st = fl & PE_STEREO;
-            double c2 = E.chi[k];
+            double c2 = E.chi4[4 * k + last_slot];
             if (fl & PE_OUT) {  // IsOutlier: e->computeError() at the current estimate
                 const double Xw[3] = {E.X[3 * k], E.X[3 * k + 1], E.X[3 * k + 2]};
                 const double ob[3] = {E.obs[3 * k], E.obs[3 * k + 1], E.obs[3 * k + 2]};
@@ -605,7 +714,7 @@ __global__ void __launch_bounds__(PNP_NT) k_pnp(const int32_t* __restrict__ f2_s
                 se3_map(T, Xw, Xc);
                 edge_err(Xc, ob, st, cam, e);
                 c2 = chi2_of(e, (double)E.info[k], st);
-                E.chi[k] = c2;
+                E.chi4[4 * k + last_slot] = c2;
             }
             const float chi2 = (float)c2;
             if (chi2 > (st ? chi2Stereo : chi2Mono)) {
@@ -620,8 +729,14 @@ __global__ void __launch_bounds__(PNP_NT) k_pnp(const int32_t* __restrict__ f2_s
         double bd[1] = {(double)bad};
         wg_sum<1>(bd, red);
         nBad = (int)bd[0];
+        PP_ACC(tcls);
         if (ne < 10) break;
     }
+#ifdef ODO_PNP_PROFILE
+    if (lane == 0 && p < 3)
+        printf("PNP p %d ne %d iters %d trials %d: build %lu solve %lu chi %lu classify %lu total %lu (x10ns)\\n", p, ne,
+               nit, ntr, tb, tsol, tchi, tcls, wall_clock64() - tall);
+#endif
     if (lane == 0) {
         double Rm[3][3];
         quat_to_R(T.q, Rm);
@@ -639,7 +754,7 @@ __global__ void __launch_bounds__(PNP_NT) k_pnp(const int32_t* __restrict__ f2_s
 }  // namespace odo
 
 namespace odo {
-size_t pnp_edge_bytes() { return 48; }
+size_t pnp_edge_bytes() { return PE_BYTES; }
 void launch_pnp(hipStream_t st, const int32_t* f2_src, const float* xyz, const float* kun, const float* ur,
                 const int* nkp, int kp_cap, int slot0, FrameCalib cal, const float* T12, const int* pair_valid,
                 const int* n_matches, int min_matches, void* edges, odo_pair_result* res, uint8_t* inlier_mask,

@@ -99,7 +99,7 @@ struct odo_ctx {
     uint8_t* bgr_in = nullptr;
     uint16_t* depth_in = nullptr;
     // pair buffers ([maxb])
-    int2 *knn_idx = nullptr, *knn_dist = nullptr;
+    int2 *knn_idx[2] = {nullptr, nullptr}, *knn_dist[2] = {nullptr, nullptr};  // per frame set
     odo_dmatch* matches = nullptr;
     int *n_matches = nullptr, *n_good = nullptr, *pair_valid = nullptr;
     void* good = nullptr;  // SortEl
@@ -128,6 +128,14 @@ struct odo_ctx {
 
 static inline size_t fbase(const odo_ctx* c, int set) { return (size_t)set * c->slots; }
 
+// the pair stream's kernels are latency-bound: dispatch them ahead of the
+// extraction stream's throughput kernels
+static int pair_stream_priority() {
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return 0;
+    return greatest;
+}
+
 static int sync_all(odo_ctx* c) {
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipStreamSynchronize(c->side));
@@ -139,7 +147,7 @@ static void free_ctx(odo_ctx* c) {
     if (!c) return;
     void* ptrs[] = {c->lv, c->cells, c->rx, c->ry, c->pyr, c->blur, c->cand, c->cand_cnt, c->keys, c->knode, c->kquad,
                     c->okp, c->ocnt, c->kps, c->desc, c->kun, c->xyz, c->ur, c->nkp, c->bgr_in, c->depth_in,
-                    c->knn_idx, c->knn_dist, c->matches, c->n_matches, c->n_good, c->pair_valid, c->good, c->f2_src,
+                    c->knn_idx[0], c->knn_dist[0], c->knn_idx[1], c->knn_dist[1], c->matches, c->n_matches, c->n_good, c->pair_valid, c->good, c->f2_src,
                     c->sort_scratch, c->latch, c->rscr[0], c->rscr[1], c->masks, c->best_mask, c->res, c->T12,
                     c->edges, c->pnp_mask};
     for (void* p : ptrs)
@@ -347,8 +355,10 @@ static int alloc_buffers(odo_ctx* c) {
     if ((e = dalloc(&c->nkp, S))) return e;
     if ((e = dalloc(&c->bgr_in, B * c->W * c->H * 3))) return e;
     if ((e = dalloc(&c->depth_in, B * c->W * c->H))) return e;
-    if ((e = dalloc(&c->knn_idx, B * c->kp_cap))) return e;
-    if ((e = dalloc(&c->knn_dist, B * c->kp_cap))) return e;
+    for (int i = 0; i < 2; i++) {
+        if ((e = dalloc(&c->knn_idx[i], B * c->kp_cap))) return e;
+        if ((e = dalloc(&c->knn_dist[i], B * c->kp_cap))) return e;
+    }
     if ((e = dalloc(&c->matches, B * c->match_cap))) return e;
     if ((e = dalloc(&c->n_matches, B))) return e;
     if ((e = dalloc(&c->n_good, B))) return e;
@@ -415,7 +425,7 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
     c->maxb = cfg->max_batch;
     c->slots = cfg->max_batch + 1;
     bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
-              hipStreamCreateWithFlags(&c->pstream, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithPriority(&c->pstream, hipStreamNonBlocking, pair_stream_priority()) == hipSuccess &&
               hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) == hipSuccess;
     for (int i = 0; i < 2 && ok; i++)
         ok = hipEventCreateWithFlags(&c->ev_xdone[i], hipEventDisableTiming) == hipSuccess &&
@@ -501,7 +511,7 @@ static int run_extract(odo_ctx* c, int set, const uint8_t* d_bgr, const uint16_t
                   c->keys_per_frame, c->okp + (size_t)slot * c->nlevels * c->okp_stride,
                   c->ocnt + (size_t)slot * c->nlevels, c->okp_stride, c->node_cap, n);
     hipEventRecord(c->ev[3], st);
-    launch_blur(st, pyr, c->blur + (size_t)slot * P, P, c->lv, c->nlevels, c->max_blur_tiles, n);
+    launch_blur(st, pyr, c->blur + (size_t)slot * P, P, c->lv, c->lv_h.data(), c->nlevels, n);
     hipEventRecord(c->ev[4], st);
     launch_finalize(st, pyr, c->blur + (size_t)slot * P, P, c->lv, c->nlevels,
                     c->okp + (size_t)slot * c->nlevels * c->okp_stride, c->ocnt + (size_t)slot * c->nlevels,
@@ -542,12 +552,10 @@ static int run_pairs(odo_ctx* c, int set, int n) {
     uint8_t* desc = c->desc + b * KC * 32;
     int* nkp = c->nkp + b;
     float* xyz = c->xyz + b * KC * 3;
-    hipEventRecord(c->ev[10], st);
-    launch_pair_valid(st, c->pair_valid, n, c->has_prev ? 1 : 0);
-    launch_knn2(st, desc, nkp, KC * 32, desc + KC * 32, nkp + 1, KC * 32, c->knn_idx, c->knn_dist, KC, c->kp_cap, n);
     hipEventRecord(c->ev[6], st);
+    launch_pair_valid(st, c->pair_valid, n, c->has_prev ? 1 : 0);
     const float mThDepth = c->cfg.calib.mbf * c->cfg.calib.th_depth / c->cfg.calib.fx;
-    launch_pair_match(st, c->knn_idx, c->knn_dist, KC, xyz, nkp, c->kp_cap, 0, c->cfg.nn_ratio, mThDepth,
+    launch_pair_match(st, c->knn_idx[set], c->knn_dist[set], KC, xyz, nkp, c->kp_cap, 0, c->cfg.nn_ratio, mThDepth,
                       c->cfg.ransac.check_depth, c->matches, c->n_matches, c->good, c->n_good, c->f2_src,
                       c->sort_scratch, c->match_cap, n);
     launch_latch(st, c->latch, c->good, c->n_good, c->n_matches, c->matches, xyz, c->kp_cap, 0, n, c->match_cap,
@@ -596,6 +604,15 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
                           c->nkp + dst, c->kp_cap);
     }
     if ((e = run_extract(c, s, d_bgr, d_depth, n, 1))) return e;
+    // kNN-2 of every pair (throughput-bound) balances the two streams best here
+    {
+        const size_t b = fbase(c, s);
+        uint8_t* desc = c->desc + b * KC * 32;
+        int* nkp = c->nkp + b;
+        launch_knn2(c->stream, desc, nkp, KC * 32, desc + KC * 32, nkp + 1, KC * 32, c->knn_idx[s], c->knn_dist[s],
+                    KC, c->kp_cap, n);
+        hipEventRecord(c->ev[10], c->stream);
+    }
     HIPCHK(hipEventRecord(c->ev_xdone[s], c->stream));
     // ---- side stream: RANSAC's rand() words depend on the pair seeds only
     if (c->pdone_rec[s]) HIPCHK(hipStreamWaitEvent(c->side, c->ev_pdone[s], 0));
@@ -790,8 +807,8 @@ int odo_debug_octree(odo_ctx* c, int i, int level, orb_kp* out, int cap, int* n)
 int odo_last_timings(odo_ctx* c, float* ms, int cap, const char** names) {
     static const char* kNames[] = {"gray+pyramid", "fast", "octree", "blur", "finalize", "knn2", "match+sort",
                                    "ransac", "pnp"};
-    // stage i spans events (a[i], b[i]): extraction stream 0..5, pair stream 10,6..9
-    static const int a[9] = {0, 1, 2, 3, 4, 10, 6, 7, 8}, b[9] = {1, 2, 3, 4, 5, 6, 7, 8, 9};
+    // stage i spans events (a[i], b[i]): extraction stream 0..5,10; pair stream 6..9
+    static const int a[9] = {0, 1, 2, 3, 4, 5, 6, 7, 8}, b[9] = {1, 2, 3, 4, 5, 10, 7, 8, 9};
     if (!c) return fail(ODO_ERR_ARG, "null ctx");
     int e;
     if ((e = sync_all(c))) return e;

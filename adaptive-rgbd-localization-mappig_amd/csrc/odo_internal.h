@@ -71,8 +71,8 @@ size_t octree_lds_bytes(int node_cap);
 void launch_octree(hipStream_t st, const uint32_t* cand, const int* cand_cnt, const LevelDesc* lv, int ncells,
                    int cell_cap, int nlevels, uint32_t* keys, int32_t* knode, uint8_t* kquad, size_t keys_stride,
                    uint32_t* okp, int* ocnt, int okp_stride, int node_cap, int nframes);
-void launch_blur(hipStream_t st, const uint8_t* pyr, uint8_t* blur, size_t pyr_stride, const LevelDesc* lv, int nlevels,
-                 int max_tiles, int nframes);
+void launch_blur(hipStream_t st, const uint8_t* pyr, uint8_t* blur, size_t pyr_stride, const LevelDesc* lv,
+                 const LevelDesc* lv_host, int nlevels, int nframes);
 void launch_finalize(hipStream_t st, const uint8_t* pyr, const uint8_t* blur, size_t pyr_stride, const LevelDesc* lv,
                      int nlevels, const uint32_t* okp, const int* ocnt, int okp_stride, const uint16_t* depth,
                      size_t depth_stride, int img_w, FrameCalib cal, orb_kp* kps, uint8_t* desc, float* kun, float* xyz,
