@@ -87,6 +87,10 @@ class Odometry:
         check(self.lib.odo_track_batch_host(self.h, ptr(bgr), ptr(depth), n, ptr(out) if want_results else None))
         return out
 
+    def set_timing(self, enable: bool):
+        """Record per-stage HIP events in odo_track_batch (serialises queues a little)."""
+        check(self.lib.odo_set_timing(self.h, 1 if enable else 0))
+
     def synchronize(self):
         check(self.lib.odo_synchronize(self.h))
 

@@ -121,14 +121,21 @@ ODO_INLINE bool has_run9(uint32_t m16) {
 
 // One wave (64 lanes) per cell ROI. Candidates packed as (resp<<24)|(y<<12)|x
 // with x,y relative to the 16px border (vToDistributeKeys coordinates),
-// emitted in row-major order within the cell.
+// emitted in row-major order within the cell. Per threshold attempt:
+//   1. compass pre-filter over the detection region (pixels 0/4/8/12 of the
+//      circle: any 9-arc holds two adjacent compass points of its sign, so this
+//      is a necessary condition), survivors queued in row-major order,
+//   2. the full 16-pixel test + cornerScore on the queue, corners listed in
+//      order with their scores in an LDS map (0 elsewhere),
+//   3. NMS (strictly greater than the 8 neighbours) over the corner list.
 __global__ void __launch_bounds__(64) k_fast_cells(const uint8_t* __restrict__ pyr, size_t pyr_stride,
                                                    const CellDesc* __restrict__ cells, const LevelDesc* __restrict__ lv,
                                                    uint32_t* __restrict__ cand, int* __restrict__ cand_cnt,
                                                    int ncells, int cell_cap, int ini_th, int min_th) {
-    __shared__ uint8_t roi[FAST_ROI_MAX * FAST_ROI_MAX];
-    __shared__ uint8_t score[FAST_ROI_MAX * FAST_ROI_MAX];
-    __shared__ uint8_t isc[FAST_ROI_MAX * FAST_ROI_MAX];
+    __shared__ __attribute__((aligned(16))) uint8_t roi[FAST_ROI_MAX * FAST_ROI_MAX];
+    __shared__ __attribute__((aligned(16))) uint8_t score[FAST_ROI_MAX * FAST_ROI_MAX];
+    __shared__ uint16_t q1[(FAST_ROI_MAX - 6) * (FAST_ROI_MAX - 6)];
+    __shared__ uint16_t q2[(FAST_ROI_MAX - 6) * (FAST_ROI_MAX - 6)];
     const int f = blockIdx.y;
     const int ci = blockIdx.x;
     const int lane = threadIdx.x;
@@ -136,58 +143,85 @@ __global__ void __launch_bounds__(64) k_fast_cells(const uint8_t* __restrict__ p
     const LevelDesc L = lv[C.level];
     const uint8_t* img = pyr + (size_t)f * pyr_stride + L.off;
     const int rows = C.rows, cols = C.cols;
-    for (int p = lane; p < rows * cols; p += 64) {
-        int r = p / cols, c = p - r * cols;
-        roi[r * FAST_ROI_MAX + c] = img[(size_t)(C.y0 + r) * L.w + (C.x0 + c)];
+    constexpr int RS = FAST_ROI_MAX;
+    {
+        const uint32_t inv = ((1u << 20) + cols - 1) / cols;  // exact p / cols for p < 48*48
+        for (int p = lane; p < rows * cols; p += 64) {
+            const int r = (int)(((uint32_t)p * inv) >> 20), c = p - r * cols;
+            roi[r * RS + c] = img[(size_t)(C.y0 + r) * L.w + (C.x0 + c)];
+        }
     }
-    __syncthreads();
     uint32_t* out = cand + ((size_t)f * ncells + ci) * cell_cap;
     const int drows = rows - 6, dcols = cols - 6;
     const int nd = drows > 0 && dcols > 0 ? drows * dcols : 0;
+    const uint32_t dinv = dcols > 0 ? ((1u << 20) + dcols - 1) / dcols : 0;
+    uint32_t* score32 = reinterpret_cast<uint32_t*>(score);
     int count = 0;
     for (int attempt = 0; attempt < 2; attempt++) {
         const int th = attempt == 0 ? ini_th : min_th;
         const int thc = th < 0 ? 0 : (th > 255 ? 255 : th);
-        for (int p = lane; p < rows * FAST_ROI_MAX; p += 64) {
-            score[p] = 0;
-            isc[p] = 0;
-        }
+        for (int w = lane; w < rows * RS / 4; w += 64) score32[w] = 0;
         __syncthreads();
-        for (int p = lane; p < nd; p += 64) {
-            const int i = 3 + p / dcols, j = 3 + p % dcols;
-            const int v = roi[i * FAST_ROI_MAX + j];
-            int d[16];
-            uint32_t dark = 0, bright = 0;
-#pragma unroll
-            for (int k = 0; k < 16; k++) {
-                const int px = roi[(i + c_circle_dy[k]) * FAST_ROI_MAX + j + c_circle_dx[k]];
-                d[k] = v - px;
-                dark |= (uint32_t)(px < v - thc) << k;
-                bright |= (uint32_t)(px > v + thc) << k;
-            }
-            if (has_run9(dark) || has_run9(bright)) {
-                isc[i * FAST_ROI_MAX + j] = 1;
-                score[i * FAST_ROI_MAX + j] = (uint8_t)corner_score16(d, thc);
-            }
-        }
-        __syncthreads();
-        // NMS + ordered compaction, 64 pixels of the detection region per step
+        // 1. compass pre-filter
+        int n1 = 0;
         for (int base = 0; base < nd; base += 64) {
             const int p = base + lane;
+            bool sv = false;
+            int o = 0;
+            if (p < nd) {
+                const int ii = (int)(((uint32_t)p * dinv) >> 20);
+                o = (3 + ii) * RS + 3 + (p - ii * dcols);
+                const int v = roi[o];
+                const int a0 = roi[o + 3 * RS], a4 = roi[o + 3], a8 = roi[o - 3 * RS], a12 = roi[o - 3];
+                const bool d0 = a0 < v - thc, d4 = a4 < v - thc, d8 = a8 < v - thc, d12 = a12 < v - thc;
+                const bool b0 = a0 > v + thc, b4 = a4 > v + thc, b8 = a8 > v + thc, b12 = a12 > v + thc;
+                sv = (d0 & d4) | (d4 & d8) | (d8 & d12) | (d12 & d0) | (b0 & b4) | (b4 & b8) | (b8 & b12) | (b12 & b0);
+            }
+            const uint64_t bal = __ballot(sv);
+            if (sv) q1[n1 + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0))] = (uint16_t)o;
+            n1 += __popcll(bal);
+        }
+        __syncthreads();
+        // 2. full segment test + score on the survivors
+        int n2 = 0;
+        for (int base = 0; base < n1; base += 64) {
+            const int idx = base + lane;
+            bool corner = false;
+            int o = 0;
+            if (idx < n1) {
+                o = q1[idx];
+                const int v = roi[o];
+                int d[16];
+                uint32_t dark = 0, bright = 0;
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    const int px = roi[o + c_circle_dy[k] * RS + c_circle_dx[k]];
+                    d[k] = v - px;
+                    dark |= (uint32_t)(px < v - thc) << k;
+                    bright |= (uint32_t)(px > v + thc) << k;
+                }
+                if (has_run9(dark) || has_run9(bright)) {
+                    corner = true;
+                    score[o] = (uint8_t)corner_score16(d, thc);
+                }
+            }
+            const uint64_t bal = __ballot(corner);
+            if (corner) q2[n2 + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0))] = (uint16_t)o;
+            n2 += __popcll(bal);
+        }
+        __syncthreads();
+        // 3. NMS over the corner list (row-major), ordered compaction
+        for (int base = 0; base < n2; base += 64) {
+            const int idx = base + lane;
             bool keep = false;
             uint32_t packed = 0;
-            if (p < nd) {
-                const int i = 3 + p / dcols, j = 3 + p % dcols;
-                const int o = i * FAST_ROI_MAX + j;
-                if (isc[o]) {
-                    const int s = score[o];
-                    keep = s > score[o - FAST_ROI_MAX - 1] && s > score[o - FAST_ROI_MAX] &&
-                           s > score[o - FAST_ROI_MAX + 1] && s > score[o - 1] && s > score[o + 1] &&
-                           s > score[o + FAST_ROI_MAX - 1] && s > score[o + FAST_ROI_MAX] &&
-                           s > score[o + FAST_ROI_MAX + 1];
-                    const uint32_t x = (uint32_t)(j + C.offx), y = (uint32_t)(i + C.offy);
-                    packed = ((uint32_t)s << 24) | (y << 12) | x;
-                }
+            if (idx < n2) {
+                const int o = q2[idx];
+                const int sc = score[o];
+                keep = sc > score[o - RS - 1] && sc > score[o - RS] && sc > score[o - RS + 1] && sc > score[o - 1] &&
+                       sc > score[o + 1] && sc > score[o + RS - 1] && sc > score[o + RS] && sc > score[o + RS + 1];
+                const int i = o / RS, j = o - i * RS;
+                packed = ((uint32_t)sc << 24) | ((uint32_t)(i + C.offy) << 12) | (uint32_t)(j + C.offx);
             }
             const uint64_t m = __ballot(keep);
             if (keep) {
@@ -731,9 +765,22 @@ __global__ void __launch_bounds__(256) k_finalize(const uint8_t* __restrict__ py
                                                   orb_kp* __restrict__ kps, uint8_t* __restrict__ desc,
                                                   float* __restrict__ kun, float* __restrict__ xyz,
                                                   float* __restrict__ ur, int* __restrict__ nkp, int kp_cap) {
-    const int f = blockIdx.y;
+    // XCD-aware mapping: workgroups are dealt round-robin over the 8 XCDs, so
+    // hardware id h runs on XCD h%8; logical ids are assigned so that each XCD
+    // takes a contiguous run of (frame, keypoint-block) pairs and one frame's
+    // pyramid and blurred levels are fetched into one L2 instead of eight.
+    int bx = blockIdx.x, f = blockIdx.y;
+    {
+        const int total = gridDim.x * gridDim.y;
+        if ((total & 7) == 0) {
+            const int h = blockIdx.x + blockIdx.y * gridDim.x;
+            const int lid = (h & 7) * (total >> 3) + (h >> 3);
+            bx = lid % gridDim.x;
+            f = lid / gridDim.x;
+        }
+    }
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int idx = blockIdx.x * 4 + wave;
+    const int idx = bx * 4 + wave;
     // level lookup from per-level counts
     int lvl = -1, k = 0, acc = 0, total = 0;
     for (int i = 0; i < nlevels; i++) {
@@ -745,7 +792,7 @@ __global__ void __launch_bounds__(256) k_finalize(const uint8_t* __restrict__ py
         acc += c;
     }
     total = acc < kp_cap ? acc : kp_cap;
-    if (blockIdx.x == 0 && threadIdx.x == 0) nkp[f] = total;
+    if (bx == 0 && threadIdx.x == 0) nkp[f] = total;
     if (lvl < 0 || idx >= kp_cap) return;
     const LevelDesc L = lv[lvl];
     const uint32_t key = okp[((size_t)f * nlevels + lvl) * okp_stride + k];

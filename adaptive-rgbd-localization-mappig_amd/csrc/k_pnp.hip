@@ -405,9 +405,11 @@ __global__ void __launch_bounds__(PNP_NT) k_pnp(const int32_t* __restrict__ f2_s
                                             const int* __restrict__ nkp, int kp_cap, int slot0, FrameCalib cal,
                                             const float* __restrict__ T12, const int* __restrict__ pair_valid,
                                             const int* __restrict__ n_matches, int min_matches, void* edges_g,
-                                            odo_pair_result* __restrict__ res, uint8_t* __restrict__ inlier_mask) {
+                                            odo_pair_result* __restrict__ res, uint8_t* __restrict__ inlier_mask,
+                                            const int* __restrict__ sel, int sel_val) {
     __builtin_amdgcn_s_setprio(3);  // latency-bound: issue ahead of co-resident extraction waves
     const int p = blockIdx.x;
+    if (sel && sel[p] != sel_val) return;  // pair handled by the other PnP launch
     const int lane = threadIdx.x;  // thread index within the workgroup
     const int wlane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     __shared__ double red[PNP_NW * 28];
@@ -758,9 +760,9 @@ size_t pnp_edge_bytes() { return PE_BYTES; }
 void launch_pnp(hipStream_t st, const int32_t* f2_src, const float* xyz, const float* kun, const float* ur,
                 const int* nkp, int kp_cap, int slot0, FrameCalib cal, const float* T12, const int* pair_valid,
                 const int* n_matches, int min_matches, void* edges, odo_pair_result* res, uint8_t* inlier_mask,
-                int npairs) {
+                int npairs, const int* sel, int sel_val) {
     hipLaunchKernelGGL(k_pnp, dim3(npairs), dim3(PNP_NT), 0, st, f2_src, xyz, kun, ur, nkp, kp_cap, slot0, cal, T12,
-                       pair_valid, n_matches, min_matches, edges, res, inlier_mask);
+                       pair_valid, n_matches, min_matches, edges, res, inlier_mask, sel, sel_val);
 }
 }  // namespace odo
 

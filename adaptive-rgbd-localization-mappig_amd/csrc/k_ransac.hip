@@ -870,10 +870,19 @@ __global__ void __launch_bounds__(64 * EV_WAVES) k_ransac_eval(RansacBufs B, Ran
 }
 
 // ---------------------------------------------------------------- final
-__global__ void __launch_bounds__(64) k_ransac_final(RansacBufs B, RansacCfg cfg) {
+// mode 0: every pair. mode 1: after the first eval launch — record which pairs
+// are finished (phase[p] = 1) and finalize those. mode 2: finalize the others.
+__global__ void __launch_bounds__(64) k_ransac_final(RansacBufs B, RansacCfg cfg, int mode, int* phase) {
     __builtin_amdgcn_s_setprio(3);  // latency-bound: issue ahead of co-resident extraction waves
     const int p = blockIdx.x;
     const int lane = threadIdx.x;
+    if (mode == 1) {
+        const int dn = B.st[p].done;
+        if (lane == 0) phase[p] = dn ? 1 : 0;
+        if (!dn) return;
+    } else if (mode == 2 && phase[p] == 1) {
+        return;
+    }
 
     __shared__ Rng s_rng;
     __shared__ double s_d2[64];
@@ -1044,7 +1053,8 @@ void launch_ransac_raw(hipStream_t st, void* scratch, int npairs, int match_cap,
 void launch_ransac(hipStream_t st, const void* good, const int* n_good, const int* n_matches,
                    const odo_dmatch* matches, const float* xyz, int kp_cap, int slot0, int match_cap, RansacCfg cfg,
                    const double* latch, const int* pair_valid, int min_matches, odo_rng* rng_io, void* scratch,
-                   uint32_t* best_mask, int mask_words, odo_pair_result* res, float* T12, int npairs) {
+                   uint32_t* best_mask, int mask_words, odo_pair_result* res, float* T12, int npairs, int part,
+                   int* phase) {
     RansacBufs B = carve(scratch, npairs, match_cap, mask_words, cfg);
     B.good = (const SortElR*)good;
     B.n_good = n_good;
@@ -1060,21 +1070,28 @@ void launch_ransac(hipStream_t st, const void* good, const int* n_good, const in
     B.best_mask = best_mask;
     B.res = res;
     B.T12 = T12;
-    hipLaunchKernelGGL(k_ransac_prep, dim3(npairs), dim3(256), 0, st, B, cfg);
     const int H = std::max(cfg.iterations, 0);
-    // Two launches: the first EV_ROWS0 rows of hypotheses for every pair (the
-    // >80% break usually ends a pair within them), then the rest, which only
-    // pairs still folding take up — so the speculative hypotheses of finished
-    // pairs do not compete with the long ones.
+    // Two eval launches: the first EV_ROWS0 rows of hypotheses for every pair
+    // (the >80% break usually ends a pair within them), then the rest, which
+    // only pairs still folding take up — so the speculative hypotheses of
+    // finished pairs do not compete with the long ones. part 1 = prep, first
+    // launch and the finished pairs' outputs (phase[] marks them); part 2 = the
+    // rest; part 0 = both.
     const int rows = (H + EV_WAVES - 1) / EV_WAVES;
     const int r0 = std::min(rows, EV_ROWS0);
-    if (r0 > 0)
-        hipLaunchKernelGGL(k_ransac_eval, dim3(npairs, r0), dim3(64 * EV_WAVES), PCACHE * sizeof(GoodPt), st, B,
-                           cfg, 0);
-    if (rows > r0)
-        hipLaunchKernelGGL(k_ransac_eval, dim3(npairs, rows - r0), dim3(64 * EV_WAVES), PCACHE * sizeof(GoodPt), st,
-                           B, cfg, r0);
-    hipLaunchKernelGGL(k_ransac_final, dim3(npairs), dim3(64), 0, st, B, cfg);
+    if (part != 2) {
+        hipLaunchKernelGGL(k_ransac_prep, dim3(npairs), dim3(256), 0, st, B, cfg);
+        if (r0 > 0)
+            hipLaunchKernelGGL(k_ransac_eval, dim3(npairs, r0), dim3(64 * EV_WAVES), PCACHE * sizeof(GoodPt), st, B,
+                               cfg, 0);
+        if (part == 1) hipLaunchKernelGGL(k_ransac_final, dim3(npairs), dim3(64), 0, st, B, cfg, 1, phase);
+    }
+    if (part != 1) {
+        if (rows > r0)
+            hipLaunchKernelGGL(k_ransac_eval, dim3(npairs, rows - r0), dim3(64 * EV_WAVES), PCACHE * sizeof(GoodPt),
+                               st, B, cfg, r0);
+        hipLaunchKernelGGL(k_ransac_final, dim3(npairs), dim3(64), 0, st, B, cfg, part == 2 ? 2 : 0, phase);
+    }
 }
 
 }  // namespace odo

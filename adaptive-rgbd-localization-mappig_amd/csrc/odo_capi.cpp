@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -100,18 +101,24 @@ struct odo_ctx {
     uint16_t* depth_in = nullptr;
     // pair buffers ([maxb])
     int2 *knn_idx[2] = {nullptr, nullptr}, *knn_dist[2] = {nullptr, nullptr};  // per frame set
-    odo_dmatch* matches = nullptr;
-    int *n_matches = nullptr, *n_good = nullptr, *pair_valid = nullptr;
-    void* good = nullptr;  // SortEl
-    int32_t* f2_src = nullptr;
     uint64_t* sort_scratch = nullptr;
     double* latch = nullptr;
     void* rscr[2] = {nullptr, nullptr};  // RANSAC scratch per frame set
-    uint32_t *masks = nullptr, *best_mask = nullptr;
-    odo_pair_result* res = nullptr;
-    float* T12 = nullptr;
-    void* edges = nullptr;
-    uint8_t* pnp_mask = nullptr;
+    uint32_t* masks = nullptr;
+    // per frame set: the pair stages of batch k write set k%2 while the PnP
+    // launches of batch k-1 may still read set (k-1)%2
+    struct PairBufs {
+        odo_dmatch* matches = nullptr;
+        int *n_matches = nullptr, *n_good = nullptr, *pair_valid = nullptr;
+        void* good = nullptr;  // SortEl
+        int32_t* f2_src = nullptr;
+        uint32_t* best_mask = nullptr;
+        odo_pair_result* res = nullptr;
+        float* T12 = nullptr;
+        void* edges = nullptr;
+        uint8_t* pnp_mask = nullptr;
+        int* pair_phase = nullptr;  // per pair: finished by RANSAC part 1
+    } pb[2];
     // sequence state: the last tracked batch sits in frame set seq_set (its
     // last frame at slot seq_n); getters read view_set / view_n
     bool has_prev = false;
@@ -122,11 +129,24 @@ struct odo_ctx {
     hipEvent_t ev[16];
     int nev = 0;
     hipStream_t side = nullptr;  // RANSAC rand() words, ahead of the pair stages
-    hipEvent_t ev_xdone[2] = {}, ev_pdone[2] = {}, ev_raw[2] = {};
+    hipStream_t pnpa = nullptr;  // PnP of the pairs RANSAC part 1 finished
+    hipStream_t pnpb = nullptr;  // PnP of the pairs RANSAC part 2 finished
+    hipEvent_t ev_xdone[2] = {}, ev_raw[2] = {};
+    // per set: RANSAC part 1 / part 2 done, PnP A / PnP B done
+    hipEvent_t ev_ra[2] = {}, ev_rb[2] = {}, ev_pa[2] = {}, ev_pb[2] = {};
     bool pdone_rec[2] = {false, false};
+    bool serial = false;
+    bool timing = false;
 };
 
 static inline size_t fbase(const odo_ctx* c, int set) { return (size_t)set * c->slots; }
+
+// Stage-timing marks (odo_last_timings) are recorded only when enabled with
+// odo_set_timing: timing events serialise the queue they sit on, which costs
+// tens of microseconds per mark once several streams are busy.
+static inline void tmark(odo_ctx* c, int i, hipStream_t st) {
+    if (c->timing) hipEventRecord(c->ev[i], st);
+}
 
 // the pair stream's kernels are latency-bound: dispatch them ahead of the
 // extraction stream's throughput kernels
@@ -140,6 +160,8 @@ static int sync_all(odo_ctx* c) {
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipStreamSynchronize(c->side));
     HIPCHK(hipStreamSynchronize(c->pstream));
+    HIPCHK(hipStreamSynchronize(c->pnpa));
+    HIPCHK(hipStreamSynchronize(c->pnpb));
     return ODO_OK;
 }
 
@@ -147,19 +169,30 @@ static void free_ctx(odo_ctx* c) {
     if (!c) return;
     void* ptrs[] = {c->lv, c->cells, c->rx, c->ry, c->pyr, c->blur, c->cand, c->cand_cnt, c->keys, c->knode, c->kquad,
                     c->okp, c->ocnt, c->kps, c->desc, c->kun, c->xyz, c->ur, c->nkp, c->bgr_in, c->depth_in,
-                    c->knn_idx[0], c->knn_dist[0], c->knn_idx[1], c->knn_dist[1], c->matches, c->n_matches, c->n_good, c->pair_valid, c->good, c->f2_src,
-                    c->sort_scratch, c->latch, c->rscr[0], c->rscr[1], c->masks, c->best_mask, c->res, c->T12,
-                    c->edges, c->pnp_mask};
+                    c->knn_idx[0], c->knn_dist[0], c->knn_idx[1], c->knn_dist[1], c->sort_scratch, c->latch,
+                    c->rscr[0], c->rscr[1], c->masks};
     for (void* p : ptrs)
         if (p) hipFree(p);
+    for (auto& P : c->pb) {
+        void* pp[] = {P.matches, P.n_matches, P.n_good, P.pair_valid, P.good, P.f2_src, P.best_mask, P.res, P.T12,
+                      P.edges, P.pnp_mask, P.pair_phase};
+        for (void* q : pp)
+            if (q) hipFree(q);
+    }
     for (int i = 0; i < c->nev; i++) hipEventDestroy(c->ev[i]);
     for (int i = 0; i < 2; i++) {
+        hipEvent_t* evs[] = {&c->ev_ra[i], &c->ev_rb[i], &c->ev_pa[i], &c->ev_pb[i]};
+        for (hipEvent_t* e : evs)
+            if (*e) hipEventDestroy(*e);
         if (c->ev_xdone[i]) hipEventDestroy(c->ev_xdone[i]);
-        if (c->ev_pdone[i]) hipEventDestroy(c->ev_pdone[i]);
         if (c->ev_raw[i]) hipEventDestroy(c->ev_raw[i]);
     }
-    if (c->side) hipStreamDestroy(c->side);
-    if (c->pstream) hipStreamDestroy(c->pstream);
+    if (!c->serial) {
+        if (c->pnpa) hipStreamDestroy(c->pnpa);
+        if (c->pnpb) hipStreamDestroy(c->pnpb);
+        if (c->side) hipStreamDestroy(c->side);
+        if (c->pstream) hipStreamDestroy(c->pstream);
+    }
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -359,12 +392,20 @@ static int alloc_buffers(odo_ctx* c) {
         if ((e = dalloc(&c->knn_idx[i], B * c->kp_cap))) return e;
         if ((e = dalloc(&c->knn_dist[i], B * c->kp_cap))) return e;
     }
-    if ((e = dalloc(&c->matches, B * c->match_cap))) return e;
-    if ((e = dalloc(&c->n_matches, B))) return e;
-    if ((e = dalloc(&c->n_good, B))) return e;
-    if ((e = dalloc(&c->pair_valid, B))) return e;
-    if ((e = dalloc((uint64_t**)&c->good, B * c->match_cap))) return e;
-    if ((e = dalloc(&c->f2_src, B * c->kp_cap))) return e;
+    for (auto& P : c->pb) {
+        if ((e = dalloc(&P.matches, B * c->match_cap))) return e;
+        if ((e = dalloc(&P.n_matches, B))) return e;
+        if ((e = dalloc(&P.n_good, B))) return e;
+        if ((e = dalloc(&P.pair_valid, B))) return e;
+        if ((e = dalloc((uint64_t**)&P.good, B * c->match_cap))) return e;
+        if ((e = dalloc(&P.f2_src, B * c->kp_cap))) return e;
+        if ((e = dalloc(&P.best_mask, B * c->mask_words))) return e;
+        if ((e = dalloc(&P.res, B))) return e;
+        if ((e = dalloc(&P.T12, B * 16))) return e;
+        if ((e = dalloc((uint8_t**)&P.edges, B * c->kp_cap * pnp_edge_bytes()))) return e;
+        if ((e = dalloc(&P.pnp_mask, B * c->kp_cap))) return e;
+        if ((e = dalloc(&P.pair_phase, B))) return e;
+    }
     int pw = 1;
     while (pw < c->kp_cap) pw <<= 1;
     if ((e = dalloc(&c->sort_scratch, B * std::max(pw, c->kp_cap)))) return e;
@@ -372,11 +413,7 @@ static int alloc_buffers(odo_ctx* c) {
     for (int i = 0; i < 2; i++)
         if ((e = dalloc((uint8_t**)&c->rscr[i], ransac_scratch_bytes((int)B, c->match_cap, c->mask_words, c->rcfg))))
             return e;
-    if ((e = dalloc(&c->best_mask, B * c->mask_words))) return e;
-    if ((e = dalloc(&c->res, B))) return e;
-    if ((e = dalloc(&c->T12, B * 16))) return e;
-    if ((e = dalloc((uint8_t**)&c->edges, B * c->kp_cap * pnp_edge_bytes()))) return e;
-    if ((e = dalloc(&c->pnp_mask, B * c->kp_cap))) return e;
+
     HIPCHK(hipMemset(c->nkp, 0, S * sizeof(int)));
     const double nan = std::nan("");
     HIPCHK(hipMemcpy(c->latch, &nan, sizeof(double), hipMemcpyHostToDevice));
@@ -424,12 +461,31 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
     c->H = cfg->height;
     c->maxb = cfg->max_batch;
     c->slots = cfg->max_batch + 1;
+    // ODO_SERIAL_STREAMS=1 (profiling): every stage on one stream, no overlap,
+    // so per-kernel times are free of cross-stream contention
+    const char* ser = getenv("ODO_SERIAL_STREAMS");
+    c->serial = ser && ser[0] == '1';
     bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
-              hipStreamCreateWithPriority(&c->pstream, hipStreamNonBlocking, pair_stream_priority()) == hipSuccess &&
-              hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) == hipSuccess;
+              (c->serial || (hipStreamCreateWithPriority(&c->pstream, hipStreamNonBlocking, pair_stream_priority()) ==
+                                 hipSuccess &&
+                             hipStreamCreateWithPriority(&c->pnpa, hipStreamNonBlocking, pair_stream_priority()) ==
+                                 hipSuccess &&
+                             hipStreamCreateWithPriority(&c->pnpb, hipStreamNonBlocking, pair_stream_priority()) ==
+                                 hipSuccess &&
+                             hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) == hipSuccess));
+    if (ok && c->serial) {
+        c->pstream = c->stream;
+        c->side = c->stream;
+        c->pnpa = c->stream;
+        c->pnpb = c->stream;
+    }
+    for (int i = 0; i < 2 && ok; i++)
+        ok = hipEventCreateWithFlags(&c->ev_ra[i], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&c->ev_rb[i], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&c->ev_pa[i], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&c->ev_pb[i], hipEventDisableTiming) == hipSuccess;
     for (int i = 0; i < 2 && ok; i++)
         ok = hipEventCreateWithFlags(&c->ev_xdone[i], hipEventDisableTiming) == hipSuccess &&
-             hipEventCreateWithFlags(&c->ev_pdone[i], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&c->ev_raw[i], hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         fail(ODO_ERR_DEVICE, "hipStreamCreate failed");
@@ -484,6 +540,14 @@ double odo_get_latch(odo_ctx* c) {
     return v;
 }
 
+int odo_set_timing(odo_ctx* c, int enable) {
+    if (!c) return fail(ODO_ERR_ARG, "null ctx");
+    int e;
+    if ((e = sync_all(c))) return e;
+    c->timing = enable != 0;
+    return ODO_OK;
+}
+
 int odo_synchronize(odo_ctx* c) {
     if (!c) return fail(ODO_ERR_ARG, "null ctx");
     return sync_all(c);
@@ -500,26 +564,26 @@ static int run_extract(odo_ctx* c, int set, const uint8_t* d_bgr, const uint16_t
         const LevelDesc& D = c->lv_h[l];
         launch_resize(st, pyr, P, S.off, S.w, D.off, D.w, D.h, c->rx + c->rx_off[l], c->ry + c->ry_off[l], n);
     }
-    hipEventRecord(c->ev[1], st);
+    tmark(c, 1, st);
     launch_fast(st, pyr, P, c->cells, c->lv, c->cand + (size_t)slot * c->ncells * c->cell_cap,
                 c->cand_cnt + (size_t)slot * c->ncells, c->ncells, c->cell_cap, c->cfg.orb.ini_th_fast,
                 c->cfg.orb.min_th_fast, n);
-    hipEventRecord(c->ev[2], st);
+    tmark(c, 2, st);
     launch_octree(st, c->cand + (size_t)slot * c->ncells * c->cell_cap, c->cand_cnt + (size_t)slot * c->ncells, c->lv,
                   c->ncells, c->cell_cap, c->nlevels, c->keys + (size_t)slot * c->keys_per_frame,
                   c->knode + (size_t)slot * c->keys_per_frame, c->kquad + (size_t)slot * c->keys_per_frame,
                   c->keys_per_frame, c->okp + (size_t)slot * c->nlevels * c->okp_stride,
                   c->ocnt + (size_t)slot * c->nlevels, c->okp_stride, c->node_cap, n);
-    hipEventRecord(c->ev[3], st);
+    tmark(c, 3, st);
     launch_blur(st, pyr, c->blur + (size_t)slot * P, P, c->lv, c->lv_h.data(), c->nlevels, n);
-    hipEventRecord(c->ev[4], st);
+    tmark(c, 4, st);
     launch_finalize(st, pyr, c->blur + (size_t)slot * P, P, c->lv, c->nlevels,
                     c->okp + (size_t)slot * c->nlevels * c->okp_stride, c->ocnt + (size_t)slot * c->nlevels,
                     c->okp_stride, d_depth, (size_t)c->W * c->H, c->W, c->cal, c->kps + (size_t)slot * c->kp_cap,
                     c->desc + (size_t)slot * c->kp_cap * 32, c->kun + (size_t)slot * c->kp_cap * 2,
                     c->xyz + (size_t)slot * c->kp_cap * 3, c->ur + (size_t)slot * c->kp_cap, c->nkp + slot, c->kp_cap,
                     n);
-    hipEventRecord(c->ev[5], st);
+    tmark(c, 5, st);
     HIPCHK(hipGetLastError());
     return ODO_OK;
 }
@@ -536,7 +600,7 @@ int odo_extract_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth,
     int e;
     if ((e = sync_all(c))) return e;
     const int set = c->seq_set ^ 1;
-    hipEventRecord(c->ev[0], c->stream);
+    tmark(c, 0, c->stream);
     if ((e = run_extract(c, set, d_bgr, d_depth, n, 1))) return e;
     c->view_set = set;
     c->last_n = n;
@@ -547,42 +611,56 @@ int odo_extract_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth,
 // pair p is (slot p, slot p+1); pair 0 is valid only with a previous frame.
 static int run_pairs(odo_ctx* c, int set, int n) {
     hipStream_t st = c->pstream;
+    auto& P = c->pb[set];
     const size_t KC = (size_t)c->kp_cap;
     const size_t b = fbase(c, set);
     uint8_t* desc = c->desc + b * KC * 32;
     int* nkp = c->nkp + b;
     float* xyz = c->xyz + b * KC * 3;
-    hipEventRecord(c->ev[6], st);
-    launch_pair_valid(st, c->pair_valid, n, c->has_prev ? 1 : 0);
+    tmark(c, 6, st);
+    launch_pair_valid(st, P.pair_valid, n, c->has_prev ? 1 : 0);
     const float mThDepth = c->cfg.calib.mbf * c->cfg.calib.th_depth / c->cfg.calib.fx;
     launch_pair_match(st, c->knn_idx[set], c->knn_dist[set], KC, xyz, nkp, c->kp_cap, 0, c->cfg.nn_ratio, mThDepth,
-                      c->cfg.ransac.check_depth, c->matches, c->n_matches, c->good, c->n_good, c->f2_src,
+                      c->cfg.ransac.check_depth, P.matches, P.n_matches, P.good, P.n_good, P.f2_src,
                       c->sort_scratch, c->match_cap, n);
-    launch_latch(st, c->latch, c->good, c->n_good, c->n_matches, c->matches, xyz, c->kp_cap, 0, n, c->match_cap,
-                 c->cfg.ransac.min_inlier_th, c->cfg.ransac.sample_size, c->cfg.ransac.iterations, c->pair_valid);
-    hipEventRecord(c->ev[7], st);
-    launch_ransac(st, c->good, c->n_good, c->n_matches, c->matches, xyz, c->kp_cap, 0, c->match_cap, c->rcfg,
-                  c->latch, c->pair_valid, 20, nullptr, c->rscr[set], c->best_mask, c->mask_words, c->res, c->T12, n);
-    hipEventRecord(c->ev[8], st);
-    launch_pnp(st, c->f2_src, xyz, c->kun + b * KC * 2, c->ur + b * KC, nkp, c->kp_cap, 0, c->cal, c->T12,
-               c->pair_valid, c->n_matches, 20, c->edges, c->res, c->pnp_mask, n);
-    hipEventRecord(c->ev[9], st);
+    launch_latch(st, c->latch, P.good, P.n_good, P.n_matches, P.matches, xyz, c->kp_cap, 0, n, c->match_cap,
+                 c->cfg.ransac.min_inlier_th, c->cfg.ransac.sample_size, c->cfg.ransac.iterations, P.pair_valid);
+    tmark(c, 7, st);
+    // RANSAC part 1 (prep + first eval launch) finishes most pairs; their PnP
+    // starts on its own stream while part 2 evaluates the long pairs, whose
+    // PnP runs on a second stream so the pair stream moves on to the next batch
+    launch_ransac(st, P.good, P.n_good, P.n_matches, P.matches, xyz, c->kp_cap, 0, c->match_cap, c->rcfg, c->latch,
+                  P.pair_valid, 20, nullptr, c->rscr[set], P.best_mask, c->mask_words, P.res, P.T12, n, 1,
+                  P.pair_phase);
+    HIPCHK(hipEventRecord(c->ev_ra[set], st));
+    HIPCHK(hipStreamWaitEvent(c->pnpa, c->ev_ra[set], 0));
+    launch_pnp(c->pnpa, P.f2_src, xyz, c->kun + b * KC * 2, c->ur + b * KC, nkp, c->kp_cap, 0, c->cal, P.T12,
+               P.pair_valid, P.n_matches, 20, P.edges, P.res, P.pnp_mask, n, P.pair_phase, 1);
+    HIPCHK(hipEventRecord(c->ev_pa[set], c->pnpa));
+    launch_ransac(st, P.good, P.n_good, P.n_matches, P.matches, xyz, c->kp_cap, 0, c->match_cap, c->rcfg, c->latch,
+                  P.pair_valid, 20, nullptr, c->rscr[set], P.best_mask, c->mask_words, P.res, P.T12, n, 2,
+                  P.pair_phase);
+    tmark(c, 8, st);
+    HIPCHK(hipEventRecord(c->ev_rb[set], st));
+    HIPCHK(hipStreamWaitEvent(c->pnpb, c->ev_rb[set], 0));
+    launch_pnp(c->pnpb, P.f2_src, xyz, c->kun + b * KC * 2, c->ur + b * KC, nkp, c->kp_cap, 0, c->cal, P.T12,
+               P.pair_valid, P.n_matches, 20, P.edges, P.res, P.pnp_mask, n, P.pair_phase, 0);
+    tmark(c, 9, c->pnpb);
+    HIPCHK(hipEventRecord(c->ev_pb[set], c->pnpb));
     HIPCHK(hipGetLastError());
     return ODO_OK;
 }
 
-static int finish_batch(odo_ctx* c, int n, odo_pair_result* h_results) {
-    hipStream_t st = c->pstream;
-    // n_matches/n_good into the result records
-    if (h_results) {
-        HIPCHK(hipMemcpyAsync(h_results, c->res, n * sizeof(odo_pair_result), hipMemcpyDeviceToHost, st));
-        std::vector<int> nm(n);
-        HIPCHK(hipMemcpyAsync(nm.data(), c->n_matches, n * sizeof(int), hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
-        for (int i = 0; i < n; i++) {
-            h_results[i].n_matches = c->valid_h[i] ? nm[i] : 0;
-        }
-    }
+static int finish_batch(odo_ctx* c, int set, int n, odo_pair_result* h_results) {
+    if (!h_results) return ODO_OK;
+    int e;
+    if ((e = sync_all(c))) return e;
+    auto& P = c->pb[set];
+    HIPCHK(hipMemcpy(h_results, P.res, n * sizeof(odo_pair_result), hipMemcpyDeviceToHost));
+    std::vector<int> nm(n);
+    HIPCHK(hipMemcpy(nm.data(), P.n_matches, n * sizeof(int), hipMemcpyDeviceToHost));
+    // n_matches into the result records
+    for (int i = 0; i < n; i++) h_results[i].n_matches = c->valid_h[i] ? nm[i] : 0;
     return ODO_OK;
 }
 
@@ -593,8 +671,11 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
     const size_t KC = (size_t)c->kp_cap;
     // ---- extraction stream: set s is free once the pair stages of the batch
     // before the previous one (which read it) are done
-    if (c->pdone_rec[s]) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_pdone[s], 0));
-    hipEventRecord(c->ev[0], c->stream);
+    if (c->pdone_rec[s]) {
+        HIPCHK(hipStreamWaitEvent(c->stream, c->ev_pa[s], 0));
+        HIPCHK(hipStreamWaitEvent(c->stream, c->ev_pb[s], 0));
+    }
+    tmark(c, 0, c->stream);
     if (c->has_prev) {
         // the previous batch's last frame becomes slot 0 (Tracking::mLastFrame)
         const size_t src = fbase(c, c->seq_set) + c->seq_n, dst = fbase(c, s);
@@ -611,11 +692,11 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
         int* nkp = c->nkp + b;
         launch_knn2(c->stream, desc, nkp, KC * 32, desc + KC * 32, nkp + 1, KC * 32, c->knn_idx[s], c->knn_dist[s],
                     KC, c->kp_cap, n);
-        hipEventRecord(c->ev[10], c->stream);
+        tmark(c, 10, c->stream);
     }
     HIPCHK(hipEventRecord(c->ev_xdone[s], c->stream));
     // ---- side stream: RANSAC's rand() words depend on the pair seeds only
-    if (c->pdone_rec[s]) HIPCHK(hipStreamWaitEvent(c->side, c->ev_pdone[s], 0));
+    if (c->pdone_rec[s]) HIPCHK(hipStreamWaitEvent(c->side, c->ev_rb[s], 0));
     launch_ransac_raw(c->side, c->rscr[s], n, c->match_cap, c->mask_words, c->rcfg, (uint64_t)c->cfg.seed,
                       c->pair_counter, nullptr);
     HIPCHK(hipEventRecord(c->ev_raw[s], c->side));
@@ -625,7 +706,6 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
     c->valid_h.assign(n, 1);
     c->valid_h[0] = c->has_prev ? 1 : 0;
     if ((e = run_pairs(c, s, n))) return e;
-    HIPCHK(hipEventRecord(c->ev_pdone[s], c->pstream));
     c->pdone_rec[s] = true;
     c->seq_set = s;
     c->seq_n = n;
@@ -633,7 +713,7 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
     c->last_n = n;
     c->has_prev = true;
     c->pair_counter += (uint64_t)n;
-    if ((e = finish_batch(c, n, h_results))) return e;
+    if ((e = finish_batch(c, s, n, h_results))) return e;
     return ODO_OK;
 }
 
@@ -673,29 +753,30 @@ int odo_get_pair(odo_ctx* c, int i, odo_dmatch* matches, int match_cap, int* n_m
     int e;
     if ((e = sync_all(c))) return e;
     int nm = 0, ng = 0, n2 = 0;
-    HIPCHK(hipMemcpy(&nm, c->n_matches + i, sizeof(int), hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(&ng, c->n_good + i, sizeof(int), hipMemcpyDeviceToHost));
+    auto& P = c->pb[c->view_set];
+    HIPCHK(hipMemcpy(&nm, P.n_matches + i, sizeof(int), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&ng, P.n_good + i, sizeof(int), hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(&n2, c->nkp + fbase(c, c->view_set) + i + 1, sizeof(int), hipMemcpyDeviceToHost));
     if (n_matches) *n_matches = nm;
     if (n_good) *n_good = ng;
     std::vector<odo_dmatch> M(std::max(nm, 1));
-    HIPCHK(hipMemcpy(M.data(), c->matches + (size_t)i * c->match_cap, nm * sizeof(odo_dmatch), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(M.data(), P.matches + (size_t)i * c->match_cap, nm * sizeof(odo_dmatch), hipMemcpyDeviceToHost));
     if (matches) memcpy(matches, M.data(), std::min(nm, match_cap) * sizeof(odo_dmatch));
     if (good_sorted || ransac_inliers) {
         std::vector<uint64_t> G(std::max(ng, 1));
-        HIPCHK(hipMemcpy(G.data(), (uint64_t*)c->good + (size_t)i * c->match_cap, ng * sizeof(uint64_t),
+        HIPCHK(hipMemcpy(G.data(), (uint64_t*)P.good + (size_t)i * c->match_cap, ng * sizeof(uint64_t),
                          hipMemcpyDeviceToHost));
         if (good_sorted)
             for (int k = 0; k < ng && k < match_cap; k++) good_sorted[k] = M[(uint32_t)(G[k] >> 32)];
         if (ransac_inliers) {
             std::vector<uint32_t> bm(c->mask_words);
-            HIPCHK(hipMemcpy(bm.data(), c->best_mask + (size_t)i * c->mask_words, c->mask_words * 4,
+            HIPCHK(hipMemcpy(bm.data(), P.best_mask + (size_t)i * c->mask_words, c->mask_words * 4,
                              hipMemcpyDeviceToHost));
             for (int k = 0; k < ng && k < match_cap; k++) ransac_inliers[k] = (bm[k >> 5] >> (k & 31)) & 1;
         }
     }
-    if (pnp_inliers) HIPCHK(hipMemcpy(pnp_inliers, c->pnp_mask + (size_t)i * c->kp_cap, n2, hipMemcpyDeviceToHost));
-    if (f2_src) HIPCHK(hipMemcpy(f2_src, c->f2_src + (size_t)i * c->kp_cap, n2 * sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (pnp_inliers) HIPCHK(hipMemcpy(pnp_inliers, P.pnp_mask + (size_t)i * c->kp_cap, n2, hipMemcpyDeviceToHost));
+    if (f2_src) HIPCHK(hipMemcpy(f2_src, P.f2_src + (size_t)i * c->kp_cap, n2 * sizeof(int32_t), hipMemcpyDeviceToHost));
     return ODO_OK;
 }
 
@@ -810,6 +891,7 @@ int odo_last_timings(odo_ctx* c, float* ms, int cap, const char** names) {
     // stage i spans events (a[i], b[i]): extraction stream 0..5,10; pair stream 6..9
     static const int a[9] = {0, 1, 2, 3, 4, 5, 6, 7, 8}, b[9] = {1, 2, 3, 4, 5, 10, 7, 8, 9};
     if (!c) return fail(ODO_ERR_ARG, "null ctx");
+    if (!c->timing) return fail(ODO_ERR_ARG, "stage timing is off (odo_set_timing)");
     int e;
     if ((e = sync_all(c))) return e;
     int m = 0;
@@ -883,13 +965,13 @@ int odo_extract(odo_ctx* c, const uint8_t* img, int channels, const uint16_t* de
     else HIPCHK(hipMemsetAsync(c->depth_in, 0, npix * 2, st));
     if (channels == 3) {
         HIPCHK(hipMemcpyAsync(c->bgr_in, img, npix * 3, hipMemcpyHostToDevice, st));
-        hipEventRecord(c->ev[0], st);
+        tmark(c, 0, st);
         int e = run_extract(c, set, c->bgr_in, c->depth_in, 1, slot);
         if (e) return e;
     } else {
         // ORBextractor::operator() on a gray image: level 0 = the image itself
         HIPCHK(hipMemcpyAsync(c->pyr + (fbase(c, set) + slot) * c->pyr_size, img, npix, hipMemcpyHostToDevice, st));
-        hipEventRecord(c->ev[0], st);
+        tmark(c, 0, st);
         int e = run_extract_from_gray(c, set, c->depth_in, 1, slot);
         if (e) return e;
     }

@@ -99,13 +99,14 @@ void launch_ransac_raw(hipStream_t st, void* scratch, int npairs, int match_cap,
 void launch_ransac(hipStream_t st, const void* good, const int* n_good, const int* n_matches,
                    const odo_dmatch* matches, const float* xyz, int kp_cap, int slot0, int match_cap, RansacCfg cfg,
                    const double* latch, const int* pair_valid, int min_matches, odo_rng* rng_io, void* scratch,
-                   uint32_t* best_mask, int mask_words, odo_pair_result* res, float* T12, int npairs);
+                   uint32_t* best_mask, int mask_words, odo_pair_result* res, float* T12, int npairs, int part = 0,
+                   int* phase = nullptr);
 size_t ransac_scratch_bytes(int npairs, int match_cap, int mask_words, const RansacCfg& cfg);
 size_t pnp_edge_bytes();
 void launch_pnp(hipStream_t st, const int32_t* f2_src, const float* xyz, const float* kun, const float* ur,
                 const int* nkp, int kp_cap, int slot0, FrameCalib cal, const float* T12, const int* pair_valid,
                 const int* n_matches, int min_matches, void* edges, odo_pair_result* res, uint8_t* inlier_mask,
-                int npairs);
+                int npairs, const int* sel = nullptr, int sel_val = 0);
 void launch_kabsch(hipStream_t st, const float* A, const float* B, int n, float* T);
 
 }  // namespace odo

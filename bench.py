@@ -152,6 +152,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=False)
+    submit = time.perf_counter() - t0  # host time to queue the K steps (asynchronous)
     odo.synchronize()
     torch.cuda.synchronize()
     if world > 1:
@@ -162,7 +163,12 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    timings = odo.timings()  # HIP events on the library stream, last step
+    # per-stage times: one extra (untimed) step with the stage events on
+    odo.set_timing(True)
+    odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=False)
+    odo.synchronize()
+    timings = odo.timings()
+    odo.set_timing(False)
     frames = B * args.steps * world
     value = frames / elapsed
     ms_per_step = elapsed / args.steps * 1e3
@@ -206,6 +212,7 @@ def main():
                        "mean_ransac_inliers": round(float(np.mean(ok["n_inliers"])), 1),
                        "mean_ransac_visited": round(float(np.mean(ok["visited"])), 1)},
             "stage_ms": {k: round(v, 4) for k, v in timings.items()},
+            "host_submit_ms_per_step": round(submit / args.steps * 1e3, 3),
             "roofline": roofline,
             "cpu_baseline": cpu,
         }

@@ -125,7 +125,10 @@ int odo_debug_blur(odo_ctx* ctx, int i, uint8_t* out, size_t cap);
  * stage runs it on the GPU (workgroup-parallel introsort): in -> out sorted by
  * distance in libstdc++'s exact (unstable) order; distances must be >= 0. */
 int odo_debug_sort(odo_ctx* ctx, const odo_dmatch* in, int n, odo_dmatch* out);
-/* Per-kernel device time of the last odo_track_batch (ms), via HIP events. */
+/* Stage timing (off by default): when on, odo_track_batch records HIP events
+ * between stages; odo_last_timings then reports the last batch (ms). */
+int odo_set_timing(odo_ctx* ctx, int enable);
+/* Per-stage device time of the last odo_track_batch (ms), via HIP events. */
 int odo_last_timings(odo_ctx* ctx, float* ms, int cap, const char** names);
 
 #ifdef __cplusplus
