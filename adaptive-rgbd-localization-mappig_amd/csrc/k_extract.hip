@@ -19,15 +19,21 @@ __constant__ int8_t c_pattern[1024];
 __constant__ int c_umax[16];
 
 // ============================================================ gray
-// gray = (B*1868 + G*9617 + R*4899 + 8192) >> 14, 4 pixels per thread.
+// gray = (B*1868 + G*9617 + R*4899 + 8192) >> 14, 4 pixels per thread; level 0
+// rows are pitch-aligned (pitch = width rounded up to 16), so a quad never
+// crosses a row when the width is a multiple of 4 (the generic tail handles
+// the rest pixel by pixel).
 __global__ void __launch_bounds__(256) k_gray(const uint8_t* __restrict__ bgr, uint8_t* __restrict__ pyr,
-                                              int npix, size_t in_stride, size_t pyr_stride) {
+                                              int w, int h, int pitch, size_t in_stride, size_t pyr_stride) {
     const int f = blockIdx.y;
     const int q = blockIdx.x * blockDim.x + threadIdx.x;  // quad index
     const uint8_t* src = bgr + (size_t)f * in_stride;
     uint8_t* dst = pyr + (size_t)f * pyr_stride;
+    const int npix = w * h;
     const int p0 = q * 4;
-    if (p0 + 3 < npix) {
+    if (p0 >= npix) return;
+    const int y = p0 / w, x = p0 - y * w;
+    if ((w & 3) == 0) {
         const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src + (size_t)p0 * 3);
         uint32_t w0 = s32[0], w1 = s32[1], w2 = s32[2];
         uint8_t b[12];
@@ -44,36 +50,69 @@ __global__ void __launch_bounds__(256) k_gray(const uint8_t* __restrict__ bgr, u
                           8192u) >> 14;
             out |= g << (8 * i);
         }
-        *reinterpret_cast<uint32_t*>(dst + p0) = out;
+        *reinterpret_cast<uint32_t*>(dst + (size_t)y * pitch + x) = out;
     } else {
-        for (int p = p0; p < npix; p++) {
+        for (int p = p0; p < p0 + 4 && p < npix; p++) {
             const uint8_t* s = src + (size_t)p * 3;
-            dst[p] = (uint8_t)(((uint32_t)s[0] * 1868u + (uint32_t)s[1] * 9617u + (uint32_t)s[2] * 4899u + 8192u) >> 14);
+            const int yy = p / w, xx = p - yy * w;
+            dst[(size_t)yy * pitch + xx] =
+                (uint8_t)(((uint32_t)s[0] * 1868u + (uint32_t)s[1] * 9617u + (uint32_t)s[2] * 4899u + 8192u) >> 14);
         }
     }
 }
 
 // ============================================================ resize
-// One output pixel per thread; x/y tables precomputed on the host with the
-// OpenCV generic-path rules (xmax rule folded into a0=2048,a1=0).
+// One workgroup per band of RB output rows of one frame: the source rows the
+// band needs and the per-column x table are staged in LDS with 16-byte loads
+// (rows are pitch-aligned), then each thread makes 4 adjacent output pixels
+// from LDS byte reads and writes them as one aligned dword. Tables are
+// precomputed on the host with the OpenCV generic-path rules (xmax rule
+// folded into a0=2048, a1=0); bytes past the level width in the pitch are 0.
 __global__ void __launch_bounds__(256) k_resize(uint8_t* __restrict__ pyr, size_t pyr_stride, int src_off,
-                                                int sw, int dst_off, int dw, int dh,
+                                                int spitch, int dst_off, int dpitch, int dw, int dh, int rb,
                                                 const ResizeX* __restrict__ xt, const ResizeY* __restrict__ yt) {
-    const int f = blockIdx.z;
-    const int dx = blockIdx.x * blockDim.x + threadIdx.x;
-    const int dy = blockIdx.y;
-    if (dx >= dw) return;
+    extern __shared__ __attribute__((aligned(16))) uint8_t rz_lds[];
+    const int f = blockIdx.y;
+    const int y0 = blockIdx.x * rb;
+    const int nrow = min(rb, dh - y0);
+    const int t = threadIdx.x;
     uint8_t* base = pyr + (size_t)f * pyr_stride;
-    const uint8_t* S = base + src_off;
-    const ResizeX X = xt[dx];
-    const ResizeY Y = yt[dy];
-    const uint8_t* r0 = S + (size_t)Y.sy0 * sw;
-    const uint8_t* r1 = S + (size_t)Y.sy1 * sw;
-    int h0 = r0[X.sx0] * X.a0 + r0[X.sx1] * X.a1;
-    int h1 = r1[X.sx0] * X.a0 + r1[X.sx1] * X.a1;
-    int v = (h0 * Y.b0 + h1 * Y.b1 + (1 << 21)) >> 22;
-    v = v < 0 ? 0 : (v > 255 ? 255 : v);
-    base[dst_off + (size_t)dy * dw + dx] = (uint8_t)v;
+    const int sy_lo = yt[y0].sy0, sy_hi = yt[y0 + nrow - 1].sy1;
+    const int srows = sy_hi - sy_lo + 1;
+    const int nq = (dw + 3) >> 2;
+    ResizeX* xs = reinterpret_cast<ResizeX*>(rz_lds);
+    uint8_t* rows = rz_lds + (size_t)nq * 4 * sizeof(ResizeX);
+    for (int i = t; i < dw; i += 256) xs[i] = xt[i];
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(base + src_off + (size_t)sy_lo * spitch);
+        uint4* dstl = reinterpret_cast<uint4*>(rows);
+        const int n16 = srows * (spitch >> 4);
+        for (int i = t; i < n16; i += 256) dstl[i] = src[i];
+    }
+    __syncthreads();
+    const float inv_nq = 1.0f / (float)nq;
+    const int items = nrow * nq;
+    for (int it = t; it < items; it += 256) {
+        const int r = (int)(((float)it + 0.5f) * inv_nq);
+        const int q = it - r * nq;
+        const ResizeY Y = yt[y0 + r];
+        const uint8_t* r0 = rows + (size_t)(Y.sy0 - sy_lo) * spitch;
+        const uint8_t* r1 = rows + (size_t)(Y.sy1 - sy_lo) * spitch;
+        uint32_t packed = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int dx = 4 * q + j;
+            if (dx < dw) {
+                const ResizeX X = xs[dx];
+                const int h0 = r0[X.sx0] * X.a0 + r0[X.sx1] * X.a1;
+                const int h1 = r1[X.sx0] * X.a0 + r1[X.sx1] * X.a1;
+                int v = (h0 * Y.b0 + h1 * Y.b1 + (1 << 21)) >> 22;
+                v = v < 0 ? 0 : (v > 255 ? 255 : v);
+                packed |= (uint32_t)v << (8 * j);
+            }
+        }
+        *reinterpret_cast<uint32_t*>(base + dst_off + (size_t)(y0 + r) * dpitch + 4 * q) = packed;
+    }
 }
 
 // ============================================================ FAST per cell
@@ -148,7 +187,7 @@ __global__ void __launch_bounds__(64) k_fast_cells(const uint8_t* __restrict__ p
         const uint32_t inv = ((1u << 20) + cols - 1) / cols;  // exact p / cols for p < 48*48
         for (int p = lane; p < rows * cols; p += 64) {
             const int r = (int)(((uint32_t)p * inv) >> 20), c = p - r * cols;
-            roi[r * RS + c] = img[(size_t)(C.y0 + r) * L.w + (C.x0 + c)];
+            roi[r * RS + c] = img[(size_t)(C.y0 + r) * L.pitch + (C.x0 + c)];
         }
     }
     uint32_t* out = cand + ((size_t)f * ncells + ci) * cell_cap;
@@ -654,12 +693,15 @@ __global__ void __launch_bounds__(OT_THREADS) k_octree(const uint32_t* __restric
 // ============================================================ blur
 // Separable 7-tap Q8 kernel {18,34,48,56,48,34,18}, REFLECT_101, exact integer
 // (GaussianBlur 7x7 sigma 2 on 8U). One 128x32 output tile per workgroup over
-// a flattened (level, tile) grid; the 134x38 input window is staged in LDS
-// (reflection only on border tiles), the horizontal pass makes 4 outputs from
-// three aligned LDS dwords, the vertical pass 4x4 outputs per thread.
+// a flattened (level, tile) grid. The 136x38 input window (x from tx0-4) is
+// staged in LDS with aligned dword loads (rows are pitch-aligned; reflection
+// only on border tiles). Horizontal pass: 4 outputs from three LDS dwords,
+// two byte-aligned windows and two v_dot4_u32_u8 each. Vertical pass: 4x4
+// outputs per thread, row pairs packed with v_perm and summed with
+// v_dot2_u32_u16, one aligned dword store per output row.
 #define BLUR_TX 128
 #define BLUR_TY 32
-#define BLUR_IW (BLUR_TX + 8)  // staged row stride (>= 134, multiple of 4)
+#define BLUR_IW (BLUR_TX + 8)  // staged row stride: x in [tx0-4, tx0+132)
 #define BLUR_IH (BLUR_TY + 6)
 ODO_INLINE int reflect101(int i, int n) {
     while (i < 0 || i >= n) i = i < 0 ? -i : 2 * n - 2 - i;
@@ -670,6 +712,14 @@ struct BlurTiles {
     int base[17];  // first tile of each level (prefix), base[nlevels] = total
     int tx[16];    // tiles across
 };
+
+typedef unsigned short blur_us2 __attribute__((ext_vector_type(2)));
+ODO_INLINE uint32_t dot2u16(uint32_t a, uint32_t b, uint32_t c) {
+    blur_us2 x, y;
+    x.x = (unsigned short)(a & 0xffff), x.y = (unsigned short)(a >> 16);
+    y.x = (unsigned short)(b & 0xffff), y.y = (unsigned short)(b >> 16);
+    return __builtin_amdgcn_udot2(x, y, c, false);
+}
 
 __global__ void __launch_bounds__(256) k_blur(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
                                               size_t pyr_stride, const LevelDesc* __restrict__ lv, BlurTiles TT,
@@ -686,39 +736,39 @@ __global__ void __launch_bounds__(256) k_blur(const uint8_t* __restrict__ pyr, u
     const uint8_t* src = pyr + (size_t)f * pyr_stride + L.off;
     uint8_t* dst = blur + (size_t)f * pyr_stride + L.off;
     const int t = threadIdx.x;
-    const bool interior = tx0 >= 3 && ty0 >= 3 && tx0 + BLUR_TX + 3 <= L.w && ty0 + BLUR_TY + 3 <= L.h;
-    // stage rows ty0-3 .. ty0+34, columns tx0-3 .. tx0+130 (one wave per row pass)
-    const int TW = BLUR_TX + 6;
+    const bool interior = tx0 >= 4 && ty0 >= 3 && tx0 + BLUR_TX + 4 <= L.w && ty0 + BLUR_TY + 3 <= L.h;
     if (interior) {
-        for (int r = t >> 6; r < BLUR_IH; r += 4) {
-            const uint8_t* srow = src + (size_t)(ty0 + r - 3) * L.w + (tx0 - 3);
-            for (int c = t & 63; c < TW; c += 64) tile[r * BLUR_IW + c] = srow[c];
+        constexpr int NW = BLUR_IW / 4;  // dwords per staged row
+        for (int it = t; it < BLUR_IH * NW; it += 256) {
+            const int r = it / NW, c = it - r * NW;
+            const uint32_t* srow = reinterpret_cast<const uint32_t*>(src + (size_t)(ty0 + r - 3) * L.pitch + tx0 - 4);
+            reinterpret_cast<uint32_t*>(tile + r * BLUR_IW)[c] = srow[c];
         }
     } else {
         for (int r = t >> 6; r < BLUR_IH; r += 4) {
-            const uint8_t* srow = src + (size_t)reflect101(ty0 + r - 3, L.h) * L.w;
-            for (int c = t & 63; c < TW; c += 64) tile[r * BLUR_IW + c] = srow[reflect101(tx0 + c - 3, L.w)];
+            const uint8_t* srow = src + (size_t)reflect101(ty0 + r - 3, L.h) * L.pitch;
+            for (int c = t & 63; c < BLUR_IW; c += 64) tile[r * BLUR_IW + c] = srow[reflect101(tx0 + c - 4, L.w)];
         }
     }
     __syncthreads();
-    // horizontal: row r, outputs 4q..4q+3 need staged bytes 4q..4q+9
+    // horizontal: row r, outputs 4q+o take staged bytes 4q+1+o .. 4q+7+o
+    constexpr uint32_t C0 = 18u | (34u << 8) | (48u << 16) | (56u << 24);
+    constexpr uint32_t C1 = 48u | (34u << 8) | (18u << 16);
     for (int it = t; it < BLUR_IH * (BLUR_TX / 4); it += 256) {
         const int r = it / (BLUR_TX / 4), q = it % (BLUR_TX / 4);
         const uint32_t* w = reinterpret_cast<const uint32_t*>(&tile[r * BLUR_IW + 4 * q]);
         const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
-        uint32_t b[10];
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            b[i] = (w0 >> (8 * i)) & 0xff;
-            b[4 + i] = (w1 >> (8 * i)) & 0xff;
-        }
-        b[8] = w2 & 0xff;
-        b[9] = (w2 >> 8) & 0xff;
         uint32_t h[4];
-#pragma unroll
-        for (int o = 0; o < 4; o++)
-            h[o] = 18u * b[o] + 34u * b[o + 1] + 48u * b[o + 2] + 56u * b[o + 3] + 48u * b[o + 4] + 34u * b[o + 5] +
-                   18u * b[o + 6];
+        h[0] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 1), C1,
+                                      __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 1), C0, 0u, false),
+                                      false);
+        h[1] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 2), C1,
+                                      __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 2), C0, 0u, false),
+                                      false);
+        h[2] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 3), C1,
+                                      __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 3), C0, 0u, false),
+                                      false);
+        h[3] = __builtin_amdgcn_udot4(w2, C1, __builtin_amdgcn_udot4(w1, C0, 0u, false), false);
         uint2 pk;
         pk.x = h[0] | (h[1] << 16);
         pk.y = h[2] | (h[3] << 16);
@@ -728,26 +778,36 @@ __global__ void __launch_bounds__(256) k_blur(const uint8_t* __restrict__ pyr, u
     // vertical: 4 columns x 4 rows per thread
     {
         const int q = t % (BLUR_TX / 4), rb = (t / (BLUR_TX / 4)) * 4;  // 32 x 8 threads
-        uint32_t v[10][4];
+        uint2 pk[10];
 #pragma unroll
-        for (int j = 0; j < 10; j++) {
-            const uint2 pk = *reinterpret_cast<const uint2*>(&hrow[(rb + j) * BLUR_TX + 4 * q]);
-            v[j][0] = pk.x & 0xffff;
-            v[j][1] = pk.x >> 16;
-            v[j][2] = pk.y & 0xffff;
-            v[j][3] = pk.y >> 16;
+        for (int j = 0; j < 10; j++) pk[j] = *reinterpret_cast<const uint2*>(&hrow[(rb + j) * BLUR_TX + 4 * q]);
+        constexpr uint32_t K01 = 18u | (34u << 16), K23 = 48u | (56u << 16), K45 = 48u | (34u << 16), K6 = 18u;
+        uint32_t out[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int cI = 0; cI < 4; cI++) {
+            // P[j] = (row j, row j+1) of column cI; P[9] carries row 9 alone (its pair weight is 0)
+            uint32_t P[10];
+#pragma unroll
+            for (int j = 0; j < 9; j++) {
+                const uint32_t lo = (cI < 2) ? pk[j].x : pk[j].y, hi = (cI < 2) ? pk[j + 1].x : pk[j + 1].y;
+                P[j] = __builtin_amdgcn_perm(hi, lo, (cI & 1) ? 0x07060302u : 0x05040100u);
+            }
+            P[9] = (cI & 1) ? (((cI < 2) ? pk[9].x : pk[9].y) >> 16) : ((cI < 2) ? pk[9].x : pk[9].y);
+#pragma unroll
+            for (int o = 0; o < 4; o++) {
+                uint32_t sum = dot2u16(P[o], K01, 0u);
+                sum = dot2u16(P[o + 2], K23, sum);
+                sum = dot2u16(P[o + 4], K45, sum);
+                sum = dot2u16(P[o + 6], K6, sum);
+                out[o] |= ((sum + 32768u) >> 16) << (8 * cI);
+            }
         }
+        const int x = tx0 + 4 * q;
+        if (x < L.w) {
 #pragma unroll
-        for (int o = 0; o < 4; o++) {
-            const int y = ty0 + rb + o;
-            if (y >= L.h) break;
-            uint8_t* drow = dst + (size_t)y * L.w;
-#pragma unroll
-            for (int cI = 0; cI < 4; cI++) {
-                const int x = tx0 + 4 * q + cI;
-                const uint32_t s = 18u * v[o][cI] + 34u * v[o + 1][cI] + 48u * v[o + 2][cI] + 56u * v[o + 3][cI] +
-                                   48u * v[o + 4][cI] + 34u * v[o + 5][cI] + 18u * v[o + 6][cI];
-                if (x < L.w) drow[x] = (uint8_t)((s + 32768u) >> 16);
+            for (int o = 0; o < 4; o++) {
+                const int y = ty0 + rb + o;
+                if (y < L.h) *reinterpret_cast<uint32_t*>(dst + (size_t)y * L.pitch + x) = out[o];
             }
         }
     }
@@ -804,13 +864,21 @@ __global__ void __launch_bounds__(256) k_finalize(const uint8_t* __restrict__ py
     if (lane < 31) {
         const int u = lane - 15;
         const int au = u < 0 ? -u : u;
-        const uint8_t* col = img + (size_t)ky * L.w + kx + u;
+        const uint8_t* col = img + (size_t)ky * L.pitch + kx + u;
+        // rows ky-15..ky+15 lie inside the level (16 px border), so all 31
+        // loads are issued up front and the umax disk is applied as a mask
+        int vp[15], vm[15];
+#pragma unroll
+        for (int v = 1; v <= 15; v++) {
+            vp[v - 1] = col[(ptrdiff_t)v * L.pitch];
+            vm[v - 1] = col[-(ptrdiff_t)v * L.pitch];
+        }
         m10 += u * col[0];
+#pragma unroll
         for (int v = 1; v <= 15; v++) {
             if (au <= c_umax[v]) {
-                const int vp = col[(size_t)v * L.w], vm = col[-(ptrdiff_t)v * L.w];
-                m01 += v * (vp - vm);
-                m10 += u * (vp + vm);
+                m01 += v * (vp[v - 1] - vm[v - 1]);
+                m10 += u * (vp[v - 1] + vm[v - 1]);
             }
         }
     }
@@ -825,15 +893,15 @@ __global__ void __launch_bounds__(256) k_finalize(const uint8_t* __restrict__ py
     const float ang = angle * factorPI;
     const float a = (float)cos((double)ang), b = (float)sin((double)ang);
     const uint8_t* bl = blur + (size_t)f * pyr_stride + L.off;
-    const uint8_t* center = bl + (size_t)ky * L.w + kx;
+    const uint8_t* center = bl + (size_t)ky * L.pitch + kx;
     uint64_t words[4];
 #pragma unroll
     for (int w = 0; w < 4; w++) {
         const int bit = w * 64 + lane;  // pair index
         const float x0 = (float)c_pattern[4 * bit + 0], y0 = (float)c_pattern[4 * bit + 1];
         const float x1 = (float)c_pattern[4 * bit + 2], y1 = (float)c_pattern[4 * bit + 3];
-        const int t0 = center[cv_round(x0 * b + y0 * a) * L.w + cv_round(x0 * a - y0 * b)];
-        const int t1 = center[cv_round(x1 * b + y1 * a) * L.w + cv_round(x1 * a - y1 * b)];
+        const int t0 = center[cv_round(x0 * b + y0 * a) * L.pitch + cv_round(x0 * a - y0 * b)];
+        const int t1 = center[cv_round(x1 * b + y1 * a) * L.pitch + cv_round(x1 * a - y1 * b)];
         words[w] = __ballot(t0 < t1);
     }
     const int o = idx;
@@ -907,15 +975,20 @@ void upload_extract_constants() {
 
 // ============================================================ launch wrappers
 namespace odo {
-void launch_gray(hipStream_t st, const uint8_t* bgr, uint8_t* pyr, int npix, size_t in_stride, size_t pyr_stride,
-                 int nframes) {
-    dim3 g((npix / 4 + 255) / 256 + 1, nframes);
-    hipLaunchKernelGGL(k_gray, g, dim3(256), 0, st, bgr, pyr, npix, in_stride, pyr_stride);
+void launch_gray(hipStream_t st, const uint8_t* bgr, uint8_t* pyr, int w, int h, int pitch, size_t in_stride,
+                 size_t pyr_stride, int nframes) {
+    dim3 g((w * h / 4 + 255) / 256 + 1, nframes);
+    hipLaunchKernelGGL(k_gray, g, dim3(256), 0, st, bgr, pyr, w, h, pitch, in_stride, pyr_stride);
 }
-void launch_resize(hipStream_t st, uint8_t* pyr, size_t pyr_stride, int src_off, int sw, int dst_off, int dw, int dh,
-                   const ResizeX* xt, const ResizeY* yt, int nframes) {
-    dim3 g((dw + 255) / 256, dh, nframes);
-    hipLaunchKernelGGL(k_resize, g, dim3(256), 0, st, pyr, pyr_stride, src_off, sw, dst_off, dw, dh, xt, yt);
+size_t resize_lds_bytes(int spitch, int dw, int max_src_rows) {
+    return (size_t)((dw + 3) & ~3) * sizeof(ResizeX) + (size_t)max_src_rows * spitch;
+}
+void launch_resize(hipStream_t st, uint8_t* pyr, size_t pyr_stride, int src_off, int spitch, int dst_off, int dpitch,
+                   int dw, int dh, int rb, int max_src_rows, const ResizeX* xt, const ResizeY* yt, int nframes) {
+    dim3 g((dh + rb - 1) / rb, nframes);
+    const size_t lds = resize_lds_bytes(spitch, dw, max_src_rows);
+    hipLaunchKernelGGL(k_resize, g, dim3(256), lds, st, pyr, pyr_stride, src_off, spitch, dst_off, dpitch, dw, dh, rb,
+                       xt, yt);
 }
 void launch_fast(hipStream_t st, const uint8_t* pyr, size_t pyr_stride, const CellDesc* cells, const LevelDesc* lv,
                  uint32_t* cand, int* cand_cnt, int ncells, int cell_cap, int ini_th, int min_th, int nframes) {

@@ -19,6 +19,23 @@ namespace odo {
 #define KNN_Q 256
 #define KNN_T 256
 
+ODO_INLINE uint32_t bcnt_acc(uint32_t x, uint32_t acc) {
+    uint32_t r;
+    asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(acc));
+    return r;
+}
+// (dist << 20) | train index, the index wave-uniform (an SGPR operand)
+ODO_INLINE uint32_t key_of(uint32_t d, uint32_t idx) {
+    uint32_t r;
+    asm("v_lshl_or_b32 %0, %1, 20, %2" : "=v"(r) : "v"(d), "s"(idx));
+    return r;
+}
+ODO_INLINE uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 __global__ void __launch_bounds__(KNN_Q) k_knn2(const uint8_t* __restrict__ qdesc, const int* __restrict__ qn,
                                                 size_t q_stride, const uint8_t* __restrict__ tdesc,
                                                 const int* __restrict__ tn, size_t t_stride,
@@ -43,19 +60,44 @@ __global__ void __launch_bounds__(KNN_Q) k_knn2(const uint8_t* __restrict__ qdes
         for (int i = threadIdx.x; i < tcount * 2; i += KNN_Q)
             tile[i] = reinterpret_cast<const uint4*>(T + (size_t)t0 * 32)[i];
         __syncthreads();
-#pragma unroll 4
-        for (int j = 0; j < tcount; j++) {
+        // 8 xor + 8 accumulating bcnt, then key and the top-2 update as
+        // min + med3 (k0 <= k1 always holds): 19 VALU per comparison; four
+        // train descriptors interleaved so the bcnt chains overlap
+        int j = 0;
+        for (; j + 4 <= tcount; j += 4) {
+            uint32_t d[4], t[4][8];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint4 ta = tile[2 * (j + u)], tb = tile[2 * (j + u) + 1];
+                t[u][0] = ta.x, t[u][1] = ta.y, t[u][2] = ta.z, t[u][3] = ta.w;
+                t[u][4] = tb.x, t[u][5] = tb.y, t[u][6] = tb.z, t[u][7] = tb.w;
+                d[u] = 0u;
+            }
+            const uint32_t q[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
+#pragma unroll
+            for (int w = 0; w < 8; w++) {
+#pragma unroll
+                for (int u = 0; u < 4; u++) d[u] = bcnt_acc(q[w] ^ t[u][w], d[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t key = key_of(d[u], (uint32_t)(t0 + j + u));
+                k1 = med3_u32(k0, k1, key);
+                k0 = min(k0, key);
+            }
+        }
+        for (; j < tcount; j++) {
             const uint4 ta = tile[2 * j], tb = tile[2 * j + 1];
-            uint32_t d = __builtin_popcount(qa.x ^ ta.x);
-            d += __builtin_popcount(qa.y ^ ta.y);
-            d += __builtin_popcount(qa.z ^ ta.z);
-            d += __builtin_popcount(qa.w ^ ta.w);
-            d += __builtin_popcount(qb.x ^ tb.x);
-            d += __builtin_popcount(qb.y ^ tb.y);
-            d += __builtin_popcount(qb.z ^ tb.z);
-            d += __builtin_popcount(qb.w ^ tb.w);
+            uint32_t d = bcnt_acc(qa.x ^ ta.x, 0u);
+            d = bcnt_acc(qa.y ^ ta.y, d);
+            d = bcnt_acc(qa.z ^ ta.z, d);
+            d = bcnt_acc(qa.w ^ ta.w, d);
+            d = bcnt_acc(qb.x ^ tb.x, d);
+            d = bcnt_acc(qb.y ^ tb.y, d);
+            d = bcnt_acc(qb.z ^ tb.z, d);
+            d = bcnt_acc(qb.w ^ tb.w, d);
             const uint32_t key = (d << 20) | (uint32_t)(t0 + j);
-            k1 = min(k1, max(k0, key));
+            k1 = med3_u32(k0, k1, key);
             k0 = min(k0, key);
         }
     }

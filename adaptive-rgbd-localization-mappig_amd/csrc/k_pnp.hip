@@ -358,16 +358,49 @@ ODO_INLINE void huber_rho(double delta, double chi, double rho[3]) {
 #define PNP_NT (64 * PNP_NW)
 #define PNP_K 4  // Levenberg trials evaluated per edge pass
 
-// Sum of NV per-lane doubles over the workgroup: xor-butterfly per wave, then
-// waves added in index order (fixed order => deterministic).
+// Sum of NV per-lane doubles over the workgroup, the result in every lane.
+// Per wave a transposing xor-butterfly: at offset o the lane pair splits the
+// (padded) vector, each lane keeping one half and adding its partner's copy
+// of that half, so NP values need NP/2 + NP/4 + ... + 1 shuffles instead of
+// 6 per value; after log2(NP) halvings lane l holds value (l >> (6-log2 NP)),
+// reduced over the remaining offsets. Waves are then added in index order.
+// The tree is fixed, so the sum is deterministic.
+template <int NV>
+struct Pow2Pad {
+    static constexpr int v = NV <= 1 ? 1 : NV <= 2 ? 2 : NV <= 4 ? 4 : NV <= 8 ? 8 : NV <= 16 ? 16 : 32;
+    static constexpr int lg = NV <= 1 ? 0 : NV <= 2 ? 1 : NV <= 4 ? 2 : NV <= 8 ? 3 : NV <= 16 ? 4 : 5;
+};
+template <int NV>
+ODO_INLINE double wave_sum_transposed(const double (&v)[NV]) {
+    constexpr int NP = Pow2Pad<NV>::v, LG = Pow2Pad<NV>::lg;
+    static_assert(NP <= 32, "at most 32 values");
+    const int lane = threadIdx.x & 63;
+    double w[NP];
+#pragma unroll
+    for (int k = 0; k < NP; k++) w[k] = k < NV ? v[k] : 0.0;
+#pragma unroll
+    for (int s = 0; s < LG; s++) {
+        const int o = 32 >> s, n = NP >> s, h = n >> 1;
+        const bool hi = (lane & o) != 0;
+#pragma unroll
+        for (int i = 0; i < h; i++) {
+            const double send = hi ? w[i] : w[h + i];
+            const double keep = hi ? w[h + i] : w[i];
+            w[i] = keep + __shfl_xor(send, o);
+        }
+    }
+    double x = w[0];
+#pragma unroll
+    for (int o = 32 >> LG; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    return x;  // total of value (lane >> (6 - LG)) over the wave
+}
 template <int NV>
 ODO_INLINE void wg_sum(double (&v)[NV], double* red) {
-#pragma unroll
-    for (int k = 0; k < NV; k++) v[k] = wave_sum(v[k]);
+    constexpr int LG = Pow2Pad<NV>::lg;
+    const double x = wave_sum_transposed(v);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (lane == 0)
-#pragma unroll
-        for (int k = 0; k < NV; k++) red[wave * NV + k] = v[k];
+    const int j = lane >> (6 - LG);
+    if ((lane & ((1 << (6 - LG)) - 1)) == 0 && j < NV) red[wave * NV + j] = x;
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < NV; k++) {

@@ -65,6 +65,13 @@ uint32_t splitmix_host(uint64_t base, uint64_t pair) { return pair_seed(base, pa
 
 }  // namespace
 
+// Frame sets in flight: batch k extracts into set k%NSETS while the pair and
+// PnP stages of batches k-1 and k-2 still read theirs, so the extraction
+// stream never waits on the PnP latency of the batch just before it.
+constexpr int NSETS = 3;
+// output rows per resize workgroup
+constexpr int RZ_RB = 16;
+
 struct odo_ctx {
     odo_config cfg{};
     int device = 0;
@@ -73,7 +80,7 @@ struct odo_ctx {
     int W = 0, H = 0, maxb = 0, slots = 0, nlevels = 0;
     std::vector<LevelDesc> lv_h;
     std::vector<CellDesc> cells_h;
-    std::vector<int> rx_off, ry_off;
+    std::vector<int> rx_off, ry_off, rz_rows;
     LevelDesc* lv = nullptr;
     CellDesc* cells = nullptr;
     ResizeX* rx = nullptr;
@@ -100,13 +107,13 @@ struct odo_ctx {
     uint8_t* bgr_in = nullptr;
     uint16_t* depth_in = nullptr;
     // pair buffers ([maxb])
-    int2 *knn_idx[2] = {nullptr, nullptr}, *knn_dist[2] = {nullptr, nullptr};  // per frame set
+    int2 *knn_idx[NSETS] = {}, *knn_dist[NSETS] = {};  // per frame set
     uint64_t* sort_scratch = nullptr;
     double* latch = nullptr;
-    void* rscr[2] = {nullptr, nullptr};  // RANSAC scratch per frame set
+    void* rscr[NSETS] = {};  // RANSAC scratch per frame set
     uint32_t* masks = nullptr;
-    // per frame set: the pair stages of batch k write set k%2 while the PnP
-    // launches of batch k-1 may still read set (k-1)%2
+    // per frame set: the pair stages of batch k write set k%NSETS while the
+    // PnP launches of batches k-1, k-2 may still read their own sets
     struct PairBufs {
         odo_dmatch* matches = nullptr;
         int *n_matches = nullptr, *n_good = nullptr, *pair_valid = nullptr;
@@ -118,12 +125,12 @@ struct odo_ctx {
         void* edges = nullptr;
         uint8_t* pnp_mask = nullptr;
         int* pair_phase = nullptr;  // per pair: finished by RANSAC part 1
-    } pb[2];
+    } pb[NSETS];
     // sequence state: the last tracked batch sits in frame set seq_set (its
     // last frame at slot seq_n); getters read view_set / view_n
     bool has_prev = false;
     uint64_t pair_counter = 0;
-    int seq_set = 1, seq_n = 0;
+    int seq_set = NSETS - 1, seq_n = 0;
     int view_set = 0, last_n = 0;
     std::vector<int> valid_h;
     hipEvent_t ev[16];
@@ -131,15 +138,17 @@ struct odo_ctx {
     hipStream_t side = nullptr;  // RANSAC rand() words, ahead of the pair stages
     hipStream_t pnpa = nullptr;  // PnP of the pairs RANSAC part 1 finished
     hipStream_t pnpb = nullptr;  // PnP of the pairs RANSAC part 2 finished
-    hipEvent_t ev_xdone[2] = {}, ev_raw[2] = {};
+    hipEvent_t ev_xdone[NSETS] = {}, ev_raw[NSETS] = {};
     // per set: RANSAC part 1 / part 2 done, PnP A / PnP B done
-    hipEvent_t ev_ra[2] = {}, ev_rb[2] = {}, ev_pa[2] = {}, ev_pb[2] = {};
-    bool pdone_rec[2] = {false, false};
+    hipEvent_t ev_ra[NSETS] = {}, ev_rb[NSETS] = {}, ev_pa[NSETS] = {}, ev_pb[NSETS] = {};
+    bool pdone_rec[NSETS] = {};
     bool serial = false;
     bool timing = false;
 };
 
 static inline size_t fbase(const odo_ctx* c, int set) { return (size_t)set * c->slots; }
+// the set the next batch extracts into
+static inline int next_set(const odo_ctx* c) { return (c->seq_set + 1) % NSETS; }
 
 // Stage-timing marks (odo_last_timings) are recorded only when enabled with
 // odo_set_timing: timing events serialise the queue they sit on, which costs
@@ -180,7 +189,7 @@ static void free_ctx(odo_ctx* c) {
             if (q) hipFree(q);
     }
     for (int i = 0; i < c->nev; i++) hipEventDestroy(c->ev[i]);
-    for (int i = 0; i < 2; i++) {
+    for (int i = 0; i < NSETS; i++) {
         hipEvent_t* evs[] = {&c->ev_ra[i], &c->ev_rb[i], &c->ev_pa[i], &c->ev_pb[i]};
         for (hipEvent_t* e : evs)
             if (*e) hipEventDestroy(*e);
@@ -227,11 +236,11 @@ static int build_geometry(odo_ctx* c) {
         LevelDesc& L = c->lv_h[l];
         L.w = cvRoundH((float)W * inv[l]);
         L.h = cvRoundH((float)H * inv[l]);
+        L.pitch = (L.w + 15) & ~15;
         L.off = off;
         L.scale = scale[l];
         L.quota = quota[l];
-        off += L.w * L.h;
-        off = (off + 15) & ~15;
+        off += L.pitch * L.h;
         maxq = std::max(maxq, quota[l]);
         if (L.w < 40 || L.h < 40) return fail(ODO_ERR_ARG, "pyramid level too small (< 40 px)");
         // FAST cells (orbextractor.cpp:669-703)
@@ -285,7 +294,7 @@ static int build_geometry(odo_ctx* c) {
         koff += (size_t)(c->lv_h[l].cell_end - c->lv_h[l].cell_begin) * c->cell_cap;
     }
     c->keys_per_frame = koff;
-    c->pyr_size = (size_t)off;
+    c->pyr_size = (size_t)off + 64;  // tail: 16-byte staging loads may run past the last row
     c->max_blur_tiles = max_tiles;
     c->okp_stride = maxq + 8;
     int nc = 64;
@@ -301,6 +310,7 @@ static int build_geometry(odo_ctx* c) {
     std::vector<ResizeY> ry;
     c->rx_off.assign(p.nlevels, 0);
     c->ry_off.assign(p.nlevels, 0);
+    c->rz_rows.assign(p.nlevels, 0);
     for (int l = 1; l < p.nlevels; l++) {
         const LevelDesc& S = c->lv_h[l - 1];
         const LevelDesc& D = c->lv_h[l];
@@ -355,6 +365,14 @@ static int build_geometry(odo_ctx* c) {
             Y.sy1 = std::min(std::max(sy + 1, 0), S.h - 1);
             ry.push_back(Y);
         }
+        // source rows one band of RZ_RB output rows stages in LDS
+        int mr = 1;
+        for (int y0 = 0; y0 < D.h; y0 += RZ_RB) {
+            const int y1 = std::min(y0 + RZ_RB, D.h) - 1;
+            mr = std::max(mr, ry[c->ry_off[l] + y1].sy1 - ry[c->ry_off[l] + y0].sy0 + 1);
+        }
+        c->rz_rows[l] = mr;
+        if (resize_lds_bytes(S.pitch, D.w, mr) > 64 * 1024) return fail(ODO_ERR_ARG, "image too wide for the resize band");
     }
     int e;
     if ((e = dalloc(&c->lv, c->lv_h.size()))) return e;
@@ -369,7 +387,7 @@ static int build_geometry(odo_ctx* c) {
 }
 
 static int alloc_buffers(odo_ctx* c) {
-    const size_t S = 2 * (size_t)c->slots, B = (size_t)c->maxb;
+    const size_t S = NSETS * (size_t)c->slots, B = (size_t)c->maxb;
     int e;
     if ((e = dalloc(&c->pyr, S * c->pyr_size))) return e;
     if ((e = dalloc(&c->blur, S * c->pyr_size))) return e;
@@ -388,7 +406,7 @@ static int alloc_buffers(odo_ctx* c) {
     if ((e = dalloc(&c->nkp, S))) return e;
     if ((e = dalloc(&c->bgr_in, B * c->W * c->H * 3))) return e;
     if ((e = dalloc(&c->depth_in, B * c->W * c->H))) return e;
-    for (int i = 0; i < 2; i++) {
+    for (int i = 0; i < NSETS; i++) {
         if ((e = dalloc(&c->knn_idx[i], B * c->kp_cap))) return e;
         if ((e = dalloc(&c->knn_dist[i], B * c->kp_cap))) return e;
     }
@@ -410,7 +428,7 @@ static int alloc_buffers(odo_ctx* c) {
     while (pw < c->kp_cap) pw <<= 1;
     if ((e = dalloc(&c->sort_scratch, B * std::max(pw, c->kp_cap)))) return e;
     if ((e = dalloc(&c->latch, 1))) return e;
-    for (int i = 0; i < 2; i++)
+    for (int i = 0; i < NSETS; i++)
         if ((e = dalloc((uint8_t**)&c->rscr[i], ransac_scratch_bytes((int)B, c->match_cap, c->mask_words, c->rcfg))))
             return e;
 
@@ -479,12 +497,12 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
         c->pnpa = c->stream;
         c->pnpb = c->stream;
     }
-    for (int i = 0; i < 2 && ok; i++)
+    for (int i = 0; i < NSETS && ok; i++)
         ok = hipEventCreateWithFlags(&c->ev_ra[i], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&c->ev_rb[i], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&c->ev_pa[i], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&c->ev_pb[i], hipEventDisableTiming) == hipSuccess;
-    for (int i = 0; i < 2 && ok; i++)
+    for (int i = 0; i < NSETS && ok; i++)
         ok = hipEventCreateWithFlags(&c->ev_xdone[i], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&c->ev_raw[i], hipEventDisableTiming) == hipSuccess;
     if (!ok) {
@@ -558,11 +576,12 @@ static int run_extract(odo_ctx* c, int set, const uint8_t* d_bgr, const uint16_t
     const size_t P = c->pyr_size;
     const size_t slot = fbase(c, set) + slot0;
     uint8_t* pyr = c->pyr + (size_t)slot * P;
-    if (d_bgr) launch_gray(st, d_bgr, pyr, c->W * c->H, (size_t)c->W * c->H * 3, P, n);
+    if (d_bgr) launch_gray(st, d_bgr, pyr, c->W, c->H, c->lv_h[0].pitch, (size_t)c->W * c->H * 3, P, n);
     for (int l = 1; l < c->nlevels; l++) {
         const LevelDesc& S = c->lv_h[l - 1];
         const LevelDesc& D = c->lv_h[l];
-        launch_resize(st, pyr, P, S.off, S.w, D.off, D.w, D.h, c->rx + c->rx_off[l], c->ry + c->ry_off[l], n);
+        launch_resize(st, pyr, P, S.off, S.pitch, D.off, D.pitch, D.w, D.h, RZ_RB, c->rz_rows[l], c->rx + c->rx_off[l],
+                      c->ry + c->ry_off[l], n);
     }
     tmark(c, 1, st);
     launch_fast(st, pyr, P, c->cells, c->lv, c->cand + (size_t)slot * c->ncells * c->cell_cap,
@@ -599,7 +618,7 @@ int odo_extract_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth,
     if (!c || !d_bgr || !d_depth || n <= 0 || n > c->maxb) return fail(ODO_ERR_ARG, "bad extract args");
     int e;
     if ((e = sync_all(c))) return e;
-    const int set = c->seq_set ^ 1;
+    const int set = next_set(c);
     tmark(c, 0, c->stream);
     if ((e = run_extract(c, set, d_bgr, d_depth, n, 1))) return e;
     c->view_set = set;
@@ -667,7 +686,7 @@ static int finish_batch(odo_ctx* c, int set, int n, odo_pair_result* h_results) 
 int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, int n, odo_pair_result* h_results) {
     if (!c || !d_bgr || !d_depth || n <= 0 || n > c->maxb) return fail(ODO_ERR_ARG, "bad track args");
     int e;
-    const int s = c->seq_set ^ 1;
+    const int s = next_set(c);
     const size_t KC = (size_t)c->kp_cap;
     // ---- extraction stream: set s is free once the pair stages of the batch
     // before the previous one (which read it) are done
@@ -780,35 +799,31 @@ int odo_get_pair(odo_ctx* c, int i, odo_dmatch* matches, int match_cap, int* n_m
     return ODO_OK;
 }
 
-int odo_debug_pyramid(odo_ctx* c, int i, uint8_t* out, size_t cap) {
-    if (!c || i < 0 || i >= c->last_n || cap < c->pyr_size) return fail(ODO_ERR_ARG, "bad args");
-    int e;
-    if ((e = sync_all(c))) return e;
-    // compact levels back to back (device layout pads levels to 16 bytes)
+// levels back to back, rows compacted (the device layout pitches rows to 16 bytes)
+static int copy_levels(odo_ctx* c, const uint8_t* dev, uint8_t* out, size_t cap) {
+    size_t total = 0;
+    for (auto& L : c->lv_h) total += (size_t)L.w * L.h;
+    if (cap < total) return fail(ODO_ERR_ARG, "output buffer too small");
     std::vector<uint8_t> buf(c->pyr_size);
-    HIPCHK(hipMemcpy(buf.data(), c->pyr + (fbase(c, c->view_set) + i + 1) * c->pyr_size, c->pyr_size,
-                     hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(buf.data(), dev, c->pyr_size, hipMemcpyDeviceToHost));
     size_t o = 0;
-    for (auto& L : c->lv_h) {
-        memcpy(out + o, buf.data() + L.off, (size_t)L.w * L.h);
-        o += (size_t)L.w * L.h;
-    }
+    for (auto& L : c->lv_h)
+        for (int y = 0; y < L.h; y++, o += L.w) memcpy(out + o, buf.data() + L.off + (size_t)y * L.pitch, L.w);
     return (int)o;
 }
 
-int odo_debug_blur(odo_ctx* c, int i, uint8_t* out, size_t cap) {
-    if (!c || i < 0 || i >= c->last_n || cap < c->pyr_size) return fail(ODO_ERR_ARG, "bad args");
+int odo_debug_pyramid(odo_ctx* c, int i, uint8_t* out, size_t cap) {
+    if (!c || i < 0 || i >= c->last_n || !out) return fail(ODO_ERR_ARG, "bad args");
     int e;
     if ((e = sync_all(c))) return e;
-    std::vector<uint8_t> buf(c->pyr_size);
-    HIPCHK(hipMemcpy(buf.data(), c->blur + (fbase(c, c->view_set) + i + 1) * c->pyr_size, c->pyr_size,
-                     hipMemcpyDeviceToHost));
-    size_t o = 0;
-    for (auto& L : c->lv_h) {
-        memcpy(out + o, buf.data() + L.off, (size_t)L.w * L.h);
-        o += (size_t)L.w * L.h;
-    }
-    return (int)o;
+    return copy_levels(c, c->pyr + (fbase(c, c->view_set) + i + 1) * c->pyr_size, out, cap);
+}
+
+int odo_debug_blur(odo_ctx* c, int i, uint8_t* out, size_t cap) {
+    if (!c || i < 0 || i >= c->last_n || !out) return fail(ODO_ERR_ARG, "bad args");
+    int e;
+    if ((e = sync_all(c))) return e;
+    return copy_levels(c, c->blur + (fbase(c, c->view_set) + i + 1) * c->pyr_size, out, cap);
 }
 
 int odo_debug_sort(odo_ctx* c, const odo_dmatch* in, int n, odo_dmatch* out) {
@@ -959,7 +974,7 @@ int odo_extract(odo_ctx* c, const uint8_t* img, int channels, const uint16_t* de
     if ((e0 = sync_all(c))) return e0;
     hipStream_t st = c->stream;
     const size_t npix = (size_t)c->W * c->H;
-    const int set = c->seq_set ^ 1;
+    const int set = next_set(c);
     const int slot = 1;
     if (depth) HIPCHK(hipMemcpyAsync(c->depth_in, depth, npix * 2, hipMemcpyHostToDevice, st));
     else HIPCHK(hipMemsetAsync(c->depth_in, 0, npix * 2, st));
@@ -970,7 +985,8 @@ int odo_extract(odo_ctx* c, const uint8_t* img, int channels, const uint16_t* de
         if (e) return e;
     } else {
         // ORBextractor::operator() on a gray image: level 0 = the image itself
-        HIPCHK(hipMemcpyAsync(c->pyr + (fbase(c, set) + slot) * c->pyr_size, img, npix, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpy2DAsync(c->pyr + (fbase(c, set) + slot) * c->pyr_size, c->lv_h[0].pitch, img, c->W, c->W, c->H,
+                                hipMemcpyHostToDevice, st));
         tmark(c, 0, st);
         int e = run_extract_from_gray(c, set, c->depth_in, 1, slot);
         if (e) return e;

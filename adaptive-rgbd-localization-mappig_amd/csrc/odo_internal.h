@@ -16,6 +16,7 @@ namespace odo {
 struct LevelDesc {
     int off;          // byte offset of the level inside a frame's pyramid buffer
     int w, h;
+    int pitch;        // row stride in bytes (w rounded up to 16)
     float scale;      // mvScaleFactor[level] (float, orbextractor.cpp:358)
     int quota;        // mnFeaturesPerLevel[level]
     int cell_begin;   // range in the global cell table
@@ -61,10 +62,11 @@ struct RansacCfg {
 
 // ---- launch wrappers (defined next to their kernels)
 void upload_extract_constants();
-void launch_gray(hipStream_t st, const uint8_t* bgr, uint8_t* pyr, int npix, size_t in_stride, size_t pyr_stride,
-                 int nframes);
-void launch_resize(hipStream_t st, uint8_t* pyr, size_t pyr_stride, int src_off, int sw, int dst_off, int dw, int dh,
-                   const ResizeX* xt, const ResizeY* yt, int nframes);
+void launch_gray(hipStream_t st, const uint8_t* bgr, uint8_t* pyr, int w, int h, int pitch, size_t in_stride,
+                 size_t pyr_stride, int nframes);
+size_t resize_lds_bytes(int spitch, int dw, int max_src_rows);
+void launch_resize(hipStream_t st, uint8_t* pyr, size_t pyr_stride, int src_off, int spitch, int dst_off, int dpitch,
+                   int dw, int dh, int rb, int max_src_rows, const ResizeX* xt, const ResizeY* yt, int nframes);
 void launch_fast(hipStream_t st, const uint8_t* pyr, size_t pyr_stride, const CellDesc* cells, const LevelDesc* lv,
                  uint32_t* cand, int* cand_cnt, int ncells, int cell_cap, int ini_th, int min_th, int nframes);
 size_t octree_lds_bytes(int node_cap);

@@ -107,8 +107,8 @@ def cpu_baseline(bgr, dep, nfeat, iters, n_frames):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=64, help="frames per step")
     ap.add_argument("--nfeatures", type=int, default=2000)
     ap.add_argument("--iters", type=int, default=500, help="RANSAC hypotheses (mIterations)")

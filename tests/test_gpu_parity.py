@@ -146,28 +146,29 @@ def test_pairs_match_ransac_pnp(cfg2_run):
 
 
 def test_pipelined_batches_roll_and_seeds():
-    """Batches queued back to back (extraction of one overlapping the pair
-    stages of the previous, alternating frame sets): the last batch's pair 0
-    links the previous batch's last frame, seeds follow the global pair index
-    and the latch from the first valid pair carries over."""
+    """Batches queued back to back (extraction of one overlapping the pair and
+    PnP stages of the two before it, frame sets used round robin and wrapping):
+    the last batch's pair 0 links the previous batch's last frame, seeds follow
+    the global pair index and the latch from the first valid pair carries over."""
     pkg = load_pkg()
-    bgr, dep, _ = sequence(8)
+    bgr, dep, _ = sequence(11)
     odo, cfg = make_odo(pkg, 640, 480, 1000, 300, 3)
     cal = oracle_calib(cfg)
-    odo.track_batch_host(bgr[0:3], dep[0:3], want_results=False)
-    odo.track_batch_host(bgr[3:6], dep[3:6], want_results=False)
-    res = odo.track_batch_host(bgr[6:8], dep[6:8])
-    frames = [O.extract_frame(bgr[i], dep[i], O.orb_params(1000), cal) for i in range(8)]
+    cuts = [0, 3, 5, 7, 9, 11]
+    for a, b in zip(cuts[:-2], cuts[1:-1]):
+        odo.track_batch_host(bgr[a:b], dep[a:b], want_results=False)
+    res = odo.track_batch_host(bgr[9:11], dep[9:11])
+    frames = [O.extract_frame(bgr[i], dep[i], O.orb_params(1000), cal) for i in range(11)]
     for i in range(2):
         got = odo.frame(i)
-        assert np.array_equal(got["desc"], frames[6 + i]["desc"]), f"frame {6 + i} descriptors"
+        assert np.array_equal(got["desc"], frames[9 + i]["desc"]), f"frame {9 + i} descriptors"
     rp = O.ransac_params(300)
     latch = float("nan")
     refs = {}
-    for f in range(1, 8):  # the oracle walks the whole sequence (latch set by pair 1)
+    for f in range(1, 11):  # the oracle walks the whole sequence (latch set by pair 1)
         refs[f] = O.track_pair(frames[f - 1], frames[f], cal, rp, pkg.pair_seed(cfg.seed, f), latch)
         latch = refs[f][3]
-    for p, f in ((0, 6), (1, 7)):
+    for p, f in ((0, 9), (1, 10)):
         r, mask, matches, _ = refs[f]
         g = odo.pair(p)
         assert np.array_equal(g["matches"], matches), f"frame {f}: match list differs"
