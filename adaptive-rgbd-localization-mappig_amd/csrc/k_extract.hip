@@ -171,10 +171,15 @@ __global__ void __launch_bounds__(64) k_fast_cells(const uint8_t* __restrict__ p
                                                    const CellDesc* __restrict__ cells, const LevelDesc* __restrict__ lv,
                                                    uint32_t* __restrict__ cand, int* __restrict__ cand_cnt,
                                                    int ncells, int cell_cap, int ini_th, int min_th) {
-    __shared__ __attribute__((aligned(16))) uint8_t roi[FAST_ROI_MAX * FAST_ROI_MAX];
-    __shared__ __attribute__((aligned(16))) uint8_t score[FAST_ROI_MAX * FAST_ROI_MAX];
+    // ROI rows staged as whole aligned dwords: pixel (r, c) at byte r*RS + sh + c
+    constexpr int RS4 = (FAST_ROI_MAX + 3 + 3) / 4 + 1;  // dwords per staged row (>= (sh+cols+3)/4)
+    constexpr int RS = 4 * RS4;
+    __shared__ __attribute__((aligned(16))) uint32_t roi32[FAST_ROI_MAX * RS4];
+    __shared__ __attribute__((aligned(16))) uint32_t score32[FAST_ROI_MAX * RS4];
     __shared__ uint16_t q1[(FAST_ROI_MAX - 6) * (FAST_ROI_MAX - 6)];
     __shared__ uint16_t q2[(FAST_ROI_MAX - 6) * (FAST_ROI_MAX - 6)];
+    const uint8_t* roi = reinterpret_cast<const uint8_t*>(roi32);
+    uint8_t* score = reinterpret_cast<uint8_t*>(score32);
     const int f = blockIdx.y;
     const int ci = blockIdx.x;
     const int lane = threadIdx.x;
@@ -182,43 +187,101 @@ __global__ void __launch_bounds__(64) k_fast_cells(const uint8_t* __restrict__ p
     const LevelDesc L = lv[C.level];
     const uint8_t* img = pyr + (size_t)f * pyr_stride + L.off;
     const int rows = C.rows, cols = C.cols;
-    constexpr int RS = FAST_ROI_MAX;
+    const int sh = C.x0 & 3;
+    const int nwr = (sh + cols + 3) >> 2;  // dwords per ROI row
     {
-        const uint32_t inv = ((1u << 20) + cols - 1) / cols;  // exact p / cols for p < 48*48
-        for (int p = lane; p < rows * cols; p += 64) {
-            const int r = (int)(((uint32_t)p * inv) >> 20), c = p - r * cols;
-            roi[r * RS + c] = img[(size_t)(C.y0 + r) * L.pitch + (C.x0 + c)];
+        // rows are pitch-aligned: dword loads from the aligned column below x0
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(img + (size_t)C.y0 * L.pitch + (C.x0 & ~3));
+        const int p4 = L.pitch >> 2;
+        const float inv = 1.0f / (float)nwr;
+        for (int p = lane; p < rows * nwr; p += 64) {
+            const int r = (int)(((float)p + 0.5f) * inv), k = p - r * nwr;
+            roi32[r * RS4 + k] = src[r * p4 + k];
         }
     }
     uint32_t* out = cand + ((size_t)f * ncells + ci) * cell_cap;
-    const int drows = rows - 6, dcols = cols - 6;
-    const int nd = drows > 0 && dcols > 0 ? drows * dcols : 0;
-    const uint32_t dinv = dcols > 0 ? ((1u << 20) + dcols - 1) / dcols : 0;
-    uint32_t* score32 = reinterpret_cast<uint32_t*>(score);
+    const int drows = rows - 6;
+    // detection bytes [sh+3, sh+cols-3) of rows 3..rows-4, walked as aligned dwords
+    const int m0 = (sh + 3) >> 2, m1 = (sh + cols - 4) >> 2;
+    const int nq = cols > 6 ? m1 - m0 + 1 : 0;
+    const int nitems = drows > 0 ? drows * nq : 0;
+    const float qinv = nq > 0 ? 1.0f / (float)nq : 0.f;
+    typedef short s16x2 __attribute__((ext_vector_type(2)));
     int count = 0;
     for (int attempt = 0; attempt < 2; attempt++) {
         const int th = attempt == 0 ? ini_th : min_th;
         const int thc = th < 0 ? 0 : (th > 255 ? 255 : th);
-        for (int w = lane; w < rows * RS / 4; w += 64) score32[w] = 0;
+        for (int w = lane; w < rows * RS4; w += 64) score32[w] = 0;
         __syncthreads();
-        // 1. compass pre-filter
+        // 1. compass pre-filter, 4 pixels per lane in 16-bit pairs: dark_k iff
+        //    a_k - (v - th) < 0, bright_k iff (v + th) - a_k < 0 (sign bits)
         int n1 = 0;
-        for (int base = 0; base < nd; base += 64) {
-            const int p = base + lane;
-            bool sv = false;
-            int o = 0;
-            if (p < nd) {
-                const int ii = (int)(((uint32_t)p * dinv) >> 20);
-                o = (3 + ii) * RS + 3 + (p - ii * dcols);
-                const int v = roi[o];
-                const int a0 = roi[o + 3 * RS], a4 = roi[o + 3], a8 = roi[o - 3 * RS], a12 = roi[o - 3];
-                const bool d0 = a0 < v - thc, d4 = a4 < v - thc, d8 = a8 < v - thc, d12 = a12 < v - thc;
-                const bool b0 = a0 > v + thc, b4 = a4 > v + thc, b8 = a8 > v + thc, b12 = a12 > v + thc;
-                sv = (d0 & d4) | (d4 & d8) | (d8 & d12) | (d12 & d0) | (b0 & b4) | (b4 & b8) | (b8 & b12) | (b12 & b0);
+        const s16x2 thv = {(short)thc, (short)thc};
+        for (int base = 0; base < nitems; base += 64) {
+            const int it = base + lane;
+            uint32_t pass4 = 0;  // bit i: pixel 4m+i survives
+            int rowbase = 0, m = 0;
+            if (it < nitems) {
+                const int ii = (int)(((float)it + 0.5f) * qinv);
+                m = m0 + (it - ii * nq);
+                const int r = 3 + ii;
+                rowbase = r * RS;
+                const uint32_t* w = roi32 + r * RS4 + m;
+                const uint32_t Cw = w[0], Uw = w[-3 * RS4], Dw = w[3 * RS4];
+                const uint32_t Lw = __builtin_amdgcn_alignbyte(Cw, w[-1], 1);
+                const uint32_t Rw = __builtin_amdgcn_alignbyte(w[1], Cw, 3);
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const uint32_t sel = h ? 0x0c030c02u : 0x0c010c00u;
+                    s16x2 v, a0, a4, a8, a12;
+                    *reinterpret_cast<uint32_t*>(&v) = __builtin_amdgcn_perm(0u, Cw, sel);
+                    *reinterpret_cast<uint32_t*>(&a0) = __builtin_amdgcn_perm(0u, Dw, sel);   // circle 0: +3 rows
+                    *reinterpret_cast<uint32_t*>(&a4) = __builtin_amdgcn_perm(0u, Rw, sel);   // circle 4: +3 cols
+                    *reinterpret_cast<uint32_t*>(&a8) = __builtin_amdgcn_perm(0u, Uw, sel);   // circle 8: -3 rows
+                    *reinterpret_cast<uint32_t*>(&a12) = __builtin_amdgcn_perm(0u, Lw, sel);  // circle 12: -3 cols
+                    const s16x2 vm = v - thv, vp = v + thv;
+                    s16x2 t;
+                    t = a0 - vm;
+                    const uint32_t d0 = *reinterpret_cast<uint32_t*>(&t);
+                    t = a4 - vm;
+                    const uint32_t d4 = *reinterpret_cast<uint32_t*>(&t);
+                    t = a8 - vm;
+                    const uint32_t d8 = *reinterpret_cast<uint32_t*>(&t);
+                    t = a12 - vm;
+                    const uint32_t d12 = *reinterpret_cast<uint32_t*>(&t);
+                    t = vp - a0;
+                    const uint32_t b0 = *reinterpret_cast<uint32_t*>(&t);
+                    t = vp - a4;
+                    const uint32_t b4 = *reinterpret_cast<uint32_t*>(&t);
+                    t = vp - a8;
+                    const uint32_t b8 = *reinterpret_cast<uint32_t*>(&t);
+                    t = vp - a12;
+                    const uint32_t b12 = *reinterpret_cast<uint32_t*>(&t);
+                    const uint32_t pm = ((d0 & d4) | (d4 & d8) | (d8 & d12) | (d12 & d0) | (b0 & b4) | (b4 & b8) |
+                                         (b8 & b12) | (b12 & b0)) & 0x80008000u;
+                    pass4 |= ((pm >> 15) & 1u) << (2 * h);
+                    pass4 |= (pm >> 31) << (2 * h + 1);
+                }
+                // keep detection bytes only: sh+3 <= 4m+i < sh+cols-3
+                const int lo = sh + 3 - 4 * m, hi = sh + cols - 3 - 4 * m;  // valid i in [lo, hi)
+                const uint32_t vm = (lo <= 0 ? 0xFu : (0xFu << lo) & 0xFu) & (hi >= 4 ? 0xFu : ((1u << hi) - 1u));
+                pass4 &= vm;
             }
-            const uint64_t bal = __ballot(sv);
-            if (sv) q1[n1 + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0))] = (uint16_t)o;
-            n1 += __popcll(bal);
+            // ordered compaction: lane order, then pixel order within the lane
+            int before = 0;
+            uint64_t bi[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                bi[i] = __ballot((pass4 >> i) & 1u);
+                before += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bi[i] >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)bi[i], 0));
+            }
+            int k = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+                if ((pass4 >> i) & 1u) q1[n1 + before + k++] = (uint16_t)(rowbase + 4 * m + i);
+#pragma unroll
+            for (int i = 0; i < 4; i++) n1 += __popcll(bi[i]);
         }
         __syncthreads();
         // 2. full segment test + score on the survivors
@@ -259,7 +322,7 @@ __global__ void __launch_bounds__(64) k_fast_cells(const uint8_t* __restrict__ p
                 const int sc = score[o];
                 keep = sc > score[o - RS - 1] && sc > score[o - RS] && sc > score[o - RS + 1] && sc > score[o - 1] &&
                        sc > score[o + 1] && sc > score[o + RS - 1] && sc > score[o + RS] && sc > score[o + RS + 1];
-                const int i = o / RS, j = o - i * RS;
+                const int i = o / RS, j = o - i * RS - sh;
                 packed = ((uint32_t)sc << 24) | ((uint32_t)(i + C.offy) << 12) | (uint32_t)(j + C.offx);
             }
             const uint64_t m = __ballot(keep);
@@ -294,22 +357,29 @@ ODO_INLINE uint64_t ot_key(int cnt, int seq, int pos) {
     return ((uint64_t)(uint32_t)cnt << 40) | ((uint64_t)(uint32_t)(seq & 0xFFFFFF) << 16) | (uint64_t)(pos & 0xFFFF);
 }
 
+// Block-wide exclusive scan in threadIdx order: inclusive wave scans with
+// shuffles, then the wave totals (tmp: OT_THREADS/64 entries) in one LDS step.
 template <typename T>
 ODO_INLINE T block_exclusive_scan(T v, T* tmp, T* total) {
-    // tmp: OT_THREADS entries; returns exclusive prefix of v over threadIdx order
-    const int t = threadIdx.x;
-    tmp[t] = v;
-    __syncthreads();
-    for (int off = 1; off < OT_THREADS; off <<= 1) {
-        T a = t >= off ? tmp[t - off] : (T)0;
-        __syncthreads();
-        tmp[t] += a;
-        __syncthreads();
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    T x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const T y = __shfl_up(x, off);
+        if (lane >= off) x += y;
     }
-    T incl = tmp[t];
-    *total = tmp[OT_THREADS - 1];
+    if (lane == 63) tmp[wave] = x;
     __syncthreads();
-    return incl - v;
+    T base = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < OT_THREADS / 64; w++) {
+        const T sw = tmp[w];
+        if (w < wave) base += sw;
+        tot += sw;
+    }
+    *total = tot;
+    __syncthreads();
+    return base + x - v;
 }
 
 __global__ void __launch_bounds__(OT_THREADS) k_octree(const uint32_t* __restrict__ cand,
@@ -333,6 +403,8 @@ __global__ void __launch_bounds__(OT_THREADS) k_octree(const uint32_t* __restric
     int* scan = iscr + node_cap;                                   // OT_THREADS
     uint64_t* sortk = reinterpret_cast<uint64_t*>(scan + OT_THREADS + 2);  // node_cap (pow2) sort keys
     __shared__ __attribute__((aligned(16))) int s_vars[16];
+    __shared__ uint64_t s_scan64[OT_THREADS / 64];
+    int& s_J = s_vars[6];
     int& s_size = s_vars[0];
     int& s_prev = s_vars[1];
     int& s_seq = s_vars[2];
@@ -452,10 +524,12 @@ __global__ void __launch_bounds__(OT_THREADS) k_octree(const uint32_t* __restric
                         }
                     } else s = 1;
                 }
-                int te, tne, ts;
-                const int ex_e = block_exclusive_scan<int>(e, scan, &te);
-                const int ex_ne = block_exclusive_scan<int>(ne, scan, &tne);
-                const int ex_s = block_exclusive_scan<int>(s, scan, &ts);
+                // one scan of the three counts packed in 21-bit fields
+                uint64_t tp;
+                const uint64_t ex = block_exclusive_scan<uint64_t>(
+                    (uint64_t)e | ((uint64_t)ne << 21) | ((uint64_t)s << 42), s_scan64, &tp);
+                const int ex_e = (int)(ex & 0x1FFFFF), ex_ne = (int)((ex >> 21) & 0x1FFFFF), ex_s = (int)(ex >> 42);
+                const int te = (int)(tp & 0x1FFFFF), tne = (int)((tp >> 21) & 0x1FFFFF), ts = (int)(tp >> 42);
                 if (i < S) {
                     iscr[i] = childBase + ex_e;          // forward children prefix
                     npos[i * 4 + 0] = e;                 // stash e
@@ -578,85 +652,108 @@ __global__ void __launch_bounds__(OT_THREADS) k_octree(const uint32_t* __restric
                 }
             }
             __syncthreads();
-            // sequential part (one thread): break point, positions, seq numbers
-            if (t == 0) {
-                // processing list: proc[j] = node index
-                int* proc = npos;  // reuse: first vcount entries
-                for (int i = 0; i < S; i++)
-                    if (iscr[i] >= 0) proc[iscr[i]] = i;
-                int size = S, J = 0;
-                for (int j = 0; j < vcount; j++) {
-                    const int i = proc[j];
-                    int e = 0;
-                    for (int q = 0; q < 4; q++) e += cc[i * 4 + q] > 0;
-                    size += e - 1;
-                    J = j + 1;
-                    if (size >= N) break;
-                }
-                // children blocks in reverse processing order at the front
-                int pos = 0;
-                int seq = s_seq;
-                int nv = 0;
-                // seq numbers in processing order
-                int* childSeqBase = npos + vcount;  // J entries
-                for (int j = 0; j < J; j++) {
-                    const int i = proc[j];
-                    childSeqBase[j] = seq;
-                    for (int q = 0; q < 4; q++) seq += cc[i * 4 + q] > 0;
-                }
-                for (int j = J - 1; j >= 0; j--) {
-                    const int i = proc[j];
-                    const ONode P = cur[i];
-                    const int hx = (P.x1 - P.x0 + 1) >> 1, hy = (P.y1 - P.y0 + 1) >> 1;
-                    int e = 0;
-                    for (int q = 0; q < 4; q++) e += cc[i * 4 + q] > 0;
-                    int r = 0;
-                    int cpos[4];
-                    for (int q = 0; q < 4; q++) {
-                        const int c = cc[i * 4 + q];
-                        cpos[q] = -1;
-                        if (c > 0) {
-                            ONode C;
-                            const int qx = q & 1, qy = q >> 1;
-                            C.x0 = (int16_t)(qx ? P.x0 + hx : P.x0);
-                            C.x1 = (int16_t)(qx ? P.x1 : P.x0 + hx);
-                            C.y0 = (int16_t)(qy ? P.y0 + hy : P.y0);
-                            C.y1 = (int16_t)(qy ? P.y1 : P.y0 + hy);
-                            C.cnt = c;
-                            C.seq = childSeqBase[j] + r;
-                            const int p = pos + (e - 1 - r);
-                            nxt[p] = C;
-                            cpos[q] = p;
-                            r++;
+            // Node divisions in processing order j (largest first) until the
+            // list reaches N: with e_j the non-empty children of node proc[j],
+            // the list size after j is S + sum_{j'<=j}(e_j' - 1), so the break
+            // point J, the children's seq numbers, their (reverse processing
+            // order) block positions and the new vSizeAndPtr slots are all
+            // prefix sums over j; survivors keep their order after the blocks.
+            int* proc = npos;                  // [vcount] node of rank j
+            int* eincl = npos + node_cap;      // inclusive prefix of e_j
+            int* vexcl = npos + 2 * node_cap;  // exclusive prefix of #children with >1 keys
+            for (int i = t; i < S; i += OT_THREADS)
+                if (iscr[i] >= 0) proc[iscr[i]] = i;
+            if (t == 0) s_J = vcount;
+            __syncthreads();
+            {
+                int eb = 0, vb = 0;
+                for (int cb = 0; cb < vcount; cb += OT_THREADS) {
+                    const int j = cb + t;
+                    int e = 0, v = 0;
+                    if (j < vcount) {
+                        const int i = proc[j];
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            e += cc[i * 4 + q] > 0;
+                            v += cc[i * 4 + q] > 1;
                         }
                     }
-                    for (int q = 0; q < 4; q++) cc[i * 4 + q] = cpos[q];
-                    pos += e;
+                    int tot;
+                    const int ex = block_exclusive_scan<int>(e | (v << 16), scan, &tot);
+                    if (j < vcount) {
+                        const int ei = eb + (ex & 0xFFFF) + e;
+                        eincl[j] = ei;
+                        vexcl[j] = vb + (ex >> 16);
+                        if (S + ei - (j + 1) >= N) atomicMin(&s_J, j + 1);
+                    }
+                    eb += tot & 0xFFFF;
+                    vb += tot >> 16;
                 }
-                // new vSizeAndPtr: children with cnt>1 in processing order, n1..n4
-                for (int j = 0; j < J; j++) {
-                    const int i = proc[j];
-                    for (int q = 0; q < 4; q++) {
-                        const int p = cc[i * 4 + q];
-                        if (p >= 0 && nxt[p].cnt > 1) sortk[nv++] = ot_key(nxt[p].cnt, nxt[p].seq, p);
+            }
+            __syncthreads();
+            const int J = s_J;
+            const int EJ = J > 0 ? eincl[J - 1] : 0;
+            for (int j = t; j < J; j += OT_THREADS) {
+                const int i = proc[j];
+                const ONode P = cur[i];
+                const int hx = (P.x1 - P.x0 + 1) >> 1, hy = (P.y1 - P.y0 + 1) >> 1;
+                int e = 0;
+#pragma unroll
+                for (int q = 0; q < 4; q++) e += cc[i * 4 + q] > 0;
+                const int blockStart = EJ - eincl[j];
+                const int seqBase = s_seq + eincl[j] - e;
+                int r = 0, v = vexcl[j];
+                int cpos[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int c = cc[i * 4 + q];
+                    cpos[q] = -1;
+                    if (c > 0) {
+                        ONode C;
+                        const int qx = q & 1, qy = q >> 1;
+                        C.x0 = (int16_t)(qx ? P.x0 + hx : P.x0);
+                        C.x1 = (int16_t)(qx ? P.x1 : P.x0 + hx);
+                        C.y0 = (int16_t)(qy ? P.y0 + hy : P.y0);
+                        C.y1 = (int16_t)(qy ? P.y1 : P.y0 + hy);
+                        C.cnt = c;
+                        C.seq = seqBase + r;
+                        const int pp = blockStart + (e - 1 - r);
+                        nxt[pp] = C;
+                        cpos[q] = pp;
+                        if (c > 1) sortk[v++] = ot_key(c, C.seq, pp);
+                        r++;
                     }
                 }
-                // survivors: all nodes not processed (j >= J), original order
-                for (int i = 0; i < S; i++) {
+#pragma unroll
+                for (int q = 0; q < 4; q++) cc[i * 4 + q] = cpos[q];
+                if (j == J - 1) s_vcnt = v;  // vSizeAndPtr entries of the new list
+            }
+            // survivors: every node not processed (rank >= J or not listed), list order
+            int sb = 0;
+            for (int cb = 0; cb < S; cb += OT_THREADS) {
+                const int i = cb + t;
+                int sv = 0;
+                if (i < S) {
                     const int j = iscr[i];
-                    if (j >= 0 && j < J) continue;
-                    nxt[pos] = cur[i];
-                    cc[i * 4 + 0] = pos;
-                    iscr[i] = -2;  // survivor marker
-                    pos++;
+                    sv = !(j >= 0 && j < J);
                 }
-                for (int i = 0; i < S; i++)
-                    if (iscr[i] >= 0 && iscr[i] >= J) iscr[i] = -2;
+                int tot;
+                const int ex = block_exclusive_scan<int>(sv, scan, &tot);
+                if (sv) {
+                    const int pp = EJ + sb + ex;
+                    nxt[pp] = cur[i];
+                    cc[i * 4 + 0] = pp;
+                    iscr[i] = -2;
+                }
+                sb += tot;
+            }
+            if (t == 0) {
+                const int size = EJ + sb;
                 s_prev = S;
-                s_size = pos;
-                s_seq = seq;
-                s_vcnt = nv;
-                if (pos >= N || pos == S) s_finish = 1;
+                s_size = size;
+                s_seq += EJ;
+                if (J == 0) s_vcnt = 0;
+                if (size >= N || size == S) s_finish = 1;
             }
             __syncthreads();
             for (int k = t; k < n; k += OT_THREADS) {
@@ -814,9 +911,14 @@ __global__ void __launch_bounds__(256) k_blur(const uint8_t* __restrict__ pyr, u
 }
 
 // ============================================================ finalize
-// One wave per output keypoint (level-major order): IC angle on the raw
-// level, rBRIEF on the blurred level (4 bit-tests per lane, ballots pack the
-// bytes), coordinate scaling, cv::undistortPoints, depth back-projection.
+// Four keypoints per wave, 16 lanes each (level-major output order): IC angle
+// on the raw level (lane j owns columns j-15 and j+1, all 31-row loads issued
+// together), rBRIEF on the blurred level (16 bit-tests per lane; one ballot
+// per test group gives two descriptor bytes of each of the 4 keypoints),
+// coordinate scaling, cv::undistortPoints and depth back-projection on the
+// keypoint's first lane. 16 keypoints per 256-thread workgroup.
+#define FIN_KPW 4                  // keypoints per wave
+#define FIN_KPB (4 * FIN_KPW)      // keypoints per workgroup
 __global__ void __launch_bounds__(256) k_finalize(const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
                                                   size_t pyr_stride, const LevelDesc* __restrict__ lv, int nlevels,
                                                   const uint32_t* __restrict__ okp, const int* __restrict__ ocnt,
@@ -825,6 +927,7 @@ __global__ void __launch_bounds__(256) k_finalize(const uint8_t* __restrict__ py
                                                   orb_kp* __restrict__ kps, uint8_t* __restrict__ desc,
                                                   float* __restrict__ kun, float* __restrict__ xyz,
                                                   float* __restrict__ ur, int* __restrict__ nkp, int kp_cap) {
+    __shared__ uint64_t s_bal[4][16];
     // XCD-aware mapping: workgroups are dealt round-robin over the 8 XCDs, so
     // hardware id h runs on XCD h%8; logical ids are assigned so that each XCD
     // takes a contiguous run of (frame, keypoint-block) pairs and one frame's
@@ -840,9 +943,10 @@ __global__ void __launch_bounds__(256) k_finalize(const uint8_t* __restrict__ py
         }
     }
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int idx = bx * 4 + wave;
+    const int g = lane >> 4, sub = lane & 15;  // keypoint slot in the wave, lane within it
+    const int idx = bx * FIN_KPB + wave * FIN_KPW + g;
     // level lookup from per-level counts
-    int lvl = -1, k = 0, acc = 0, total = 0;
+    int lvl = -1, k = 0, acc = 0;
     for (int i = 0; i < nlevels; i++) {
         const int c = ocnt[f * nlevels + i];
         if (lvl < 0 && idx < acc + c) {
@@ -851,65 +955,83 @@ __global__ void __launch_bounds__(256) k_finalize(const uint8_t* __restrict__ py
         }
         acc += c;
     }
-    total = acc < kp_cap ? acc : kp_cap;
+    const int total = acc < kp_cap ? acc : kp_cap;
     if (bx == 0 && threadIdx.x == 0) nkp[f] = total;
-    if (lvl < 0 || idx >= kp_cap) return;
-    const LevelDesc L = lv[lvl];
-    const uint32_t key = okp[((size_t)f * nlevels + lvl) * okp_stride + k];
+    const bool valid = lvl >= 0 && idx < kp_cap;
+    // invalid slots run on a dummy in-level position and write nothing (no early
+    // exit: the ballots and the barrier below need every wave)
+    const LevelDesc L = lv[valid ? lvl : 0];
+    const uint32_t key = valid ? okp[((size_t)f * nlevels + lvl) * okp_stride + k] : (16u | (16u << 12));
     const int kx = (int)(key & 0xfff) + 16, ky = (int)((key >> 12) & 0xfff) + 16;
     const float resp = (float)(key >> 24);
     const uint8_t* img = pyr + (size_t)f * pyr_stride + L.off;
-    // ---- IC_Angle: lane u in [0,31) owns column offset u-15
+    // ---- IC_Angle: columns u0 = sub-15 (all 16 lanes) and u1 = sub+1 (lanes 0..14)
     int m10 = 0, m01 = 0;
-    if (lane < 31) {
-        const int u = lane - 15;
-        const int au = u < 0 ? -u : u;
-        const uint8_t* col = img + (size_t)ky * L.pitch + kx + u;
-        // rows ky-15..ky+15 lie inside the level (16 px border), so all 31
-        // loads are issued up front and the umax disk is applied as a mask
-        int vp[15], vm[15];
+    {
+        const int u0 = sub - 15, u1 = sub + 1;
+        const bool has1 = sub < 15;
+        const uint8_t* c0 = img + (size_t)ky * L.pitch + kx + u0;
+        const uint8_t* c1 = img + (size_t)ky * L.pitch + kx + (has1 ? u1 : 0);
+        // rows ky-15..ky+15 lie inside the level (16 px border): loads issued up front
+        int p0[15], n0[15], p1[15], n1[15];
 #pragma unroll
         for (int v = 1; v <= 15; v++) {
-            vp[v - 1] = col[(ptrdiff_t)v * L.pitch];
-            vm[v - 1] = col[-(ptrdiff_t)v * L.pitch];
+            p0[v - 1] = c0[(ptrdiff_t)v * L.pitch];
+            n0[v - 1] = c0[-(ptrdiff_t)v * L.pitch];
+            p1[v - 1] = c1[(ptrdiff_t)v * L.pitch];
+            n1[v - 1] = c1[-(ptrdiff_t)v * L.pitch];
         }
-        m10 += u * col[0];
+        const int a0 = u0 < 0 ? -u0 : u0;
+        m10 = u0 * c0[0] + (has1 ? u1 * c1[0] : 0);
 #pragma unroll
         for (int v = 1; v <= 15; v++) {
-            if (au <= c_umax[v]) {
-                m01 += v * (vp[v - 1] - vm[v - 1]);
-                m10 += u * (vp[v - 1] + vm[v - 1]);
+            const int um = c_umax[v];
+            if (a0 <= um) {
+                m01 += v * (p0[v - 1] - n0[v - 1]);
+                m10 += u0 * (p0[v - 1] + n0[v - 1]);
+            }
+            if (has1 && u1 <= um) {
+                m01 += v * (p1[v - 1] - n1[v - 1]);
+                m10 += u1 * (p1[v - 1] + n1[v - 1]);
             }
         }
     }
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
+    for (int off = 8; off > 0; off >>= 1) {
         m10 += __shfl_xor(m10, off);
         m01 += __shfl_xor(m01, off);
     }
     const float angle = fast_atan2((float)m01, (float)m10);
-    // ---- rBRIEF
+    // ---- rBRIEF: lane sub makes tests w*16+sub, w = 0..15
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
     const float ang = angle * factorPI;
     const float a = (float)cos((double)ang), b = (float)sin((double)ang);
     const uint8_t* bl = blur + (size_t)f * pyr_stride + L.off;
     const uint8_t* center = bl + (size_t)ky * L.pitch + kx;
-    uint64_t words[4];
+    int tv0[16], tv1[16];
 #pragma unroll
-    for (int w = 0; w < 4; w++) {
-        const int bit = w * 64 + lane;  // pair index
+    for (int w = 0; w < 16; w++) {
+        const int bit = w * 16 + sub;
         const float x0 = (float)c_pattern[4 * bit + 0], y0 = (float)c_pattern[4 * bit + 1];
         const float x1 = (float)c_pattern[4 * bit + 2], y1 = (float)c_pattern[4 * bit + 3];
-        const int t0 = center[cv_round(x0 * b + y0 * a) * L.pitch + cv_round(x0 * a - y0 * b)];
-        const int t1 = center[cv_round(x1 * b + y1 * a) * L.pitch + cv_round(x1 * a - y1 * b)];
-        words[w] = __ballot(t0 < t1);
+        tv0[w] = center[cv_round(x0 * b + y0 * a) * L.pitch + cv_round(x0 * a - y0 * b)];
+        tv1[w] = center[cv_round(x1 * b + y1 * a) * L.pitch + cv_round(x1 * a - y1 * b)];
     }
+#pragma unroll
+    for (int w = 0; w < 16; w++) {
+        const uint64_t bal = __ballot(tv0[w] < tv1[w]);
+        if (lane == 0) s_bal[wave][w] = bal;
+    }
+    __syncthreads();
     const int o = idx;
-    orb_kp* kp = kps + (size_t)f * kp_cap + o;
-    if (lane < 4) {
-        reinterpret_cast<uint64_t*>(desc + ((size_t)f * kp_cap + o) * 32)[lane] = words[lane];
+    if (valid && sub < 8) {
+        // descriptor dword sub = tests 32*sub .. 32*sub+31 = groups 2sub, 2sub+1
+        const uint32_t lo = (uint32_t)(s_bal[wave][2 * sub] >> (16 * g)) & 0xffffu;
+        const uint32_t hi = (uint32_t)(s_bal[wave][2 * sub + 1] >> (16 * g)) & 0xffffu;
+        reinterpret_cast<uint32_t*>(desc + ((size_t)f * kp_cap + o) * 32)[sub] = lo | (hi << 16);
     }
-    if (lane == 0) {
+    if (valid && sub == 0) {
+        orb_kp* kp = kps + (size_t)f * kp_cap + o;
         float px = (float)kx, py = (float)ky;
         if (lvl != 0) {
             px *= L.scale;
@@ -1020,7 +1142,7 @@ void launch_finalize(hipStream_t st, const uint8_t* pyr, const uint8_t* blur, si
                      int nlevels, const uint32_t* okp, const int* ocnt, int okp_stride, const uint16_t* depth,
                      size_t depth_stride, int img_w, FrameCalib cal, orb_kp* kps, uint8_t* desc, float* kun, float* xyz,
                      float* ur, int* nkp, int kp_cap, int nframes) {
-    dim3 g((kp_cap + 3) / 4, nframes);
+    dim3 g((kp_cap + FIN_KPB - 1) / FIN_KPB, nframes);
     hipLaunchKernelGGL(k_finalize, g, dim3(256), 0, st, pyr, blur, pyr_stride, lv, nlevels, okp, ocnt, okp_stride,
                        depth, depth_stride, img_w, cal, kps, desc, kun, xyz, ur, nkp, kp_cap);
 }
