@@ -100,11 +100,13 @@ SIGNATURES = {
 _lib = None
 
 
-def load(path: str = LIB_PATH):
-    """Load libodo_hip.so and bind every C-ABI symbol. Raises if it is missing."""
+def load(path: str = None):
+    """Load libodo_hip.so and bind every C-ABI symbol. Raises if it is missing.
+    ODO_LIB names an alternative build of the same library (A/B experiments)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = path or os.environ.get("ODO_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise RuntimeError(f"{path} not built: run __graft_entry__.build() (make -C adaptive-rgbd-localization-mappig_amd)")
     L = C.CDLL(path)

@@ -518,7 +518,7 @@ __global__ void __launch_bounds__(PM_THREADS) k_pair_match(
     float th_depth_m, int check_depth, odo_dmatch* __restrict__ matches, int* __restrict__ n_matches,
     SortEl* __restrict__ good, int* __restrict__ n_good, int32_t* __restrict__ f2_src,
     uint64_t* __restrict__ sort_scratch, int match_cap) {
-    __builtin_amdgcn_s_setprio(3);  // latency-bound: issue ahead of co-resident extraction waves
+    __builtin_amdgcn_s_setprio(ODO_WAVE_PRIO);  // latency-bound: issue ahead of co-resident extraction waves
     __shared__ int s_cnt[PM_THREADS];
     __shared__ int s_tot, s_total_valid, s_cle, s_K, s_nm;
     extern __shared__ __attribute__((aligned(16))) uint64_t dyn_lds[];  // pw entries

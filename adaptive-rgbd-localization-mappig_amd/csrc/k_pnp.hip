@@ -440,7 +440,7 @@ __global__ void __launch_bounds__(PNP_NT) k_pnp(const int32_t* __restrict__ f2_s
                                             const int* __restrict__ n_matches, int min_matches, void* edges_g,
                                             odo_pair_result* __restrict__ res, uint8_t* __restrict__ inlier_mask,
                                             const int* __restrict__ sel, int sel_val) {
-    __builtin_amdgcn_s_setprio(3);  // latency-bound: issue ahead of co-resident extraction waves
+    __builtin_amdgcn_s_setprio(ODO_WAVE_PRIO);  // latency-bound: issue ahead of co-resident extraction waves
     const int p = blockIdx.x;
     if (sel && sel[p] != sel_val) return;  // pair handled by the other PnP launch
     const int lane = threadIdx.x;  // thread index within the workgroup

@@ -391,7 +391,7 @@ ODO_INLINE void pair_samples(const RansacBufs& B, int p, int ng, int S, int H, S
 
 
 __global__ void __launch_bounds__(256) k_ransac_prep(RansacBufs B, RansacCfg cfg) {
-    __builtin_amdgcn_s_setprio(3);  // latency-bound: issue ahead of co-resident extraction waves
+    __builtin_amdgcn_s_setprio(ODO_WAVE_PRIO);  // latency-bound: issue ahead of co-resident extraction waves
     const int p = blockIdx.x;
     const int t = threadIdx.x;
     RState* S = B.st + p;
@@ -846,7 +846,7 @@ ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int 
 }
 
 __global__ void __launch_bounds__(64 * EV_WAVES) k_ransac_eval(RansacBufs B, RansacCfg cfg, int y0) {
-    __builtin_amdgcn_s_setprio(3);  // latency-bound: issue ahead of co-resident extraction waves
+    __builtin_amdgcn_s_setprio(ODO_WAVE_PRIO);  // latency-bound: issue ahead of co-resident extraction waves
     const int p = blockIdx.x;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     __shared__ EvalLds s_w[EV_WAVES];
@@ -873,7 +873,7 @@ __global__ void __launch_bounds__(64 * EV_WAVES) k_ransac_eval(RansacBufs B, Ran
 // mode 0: every pair. mode 1: after the first eval launch — record which pairs
 // are finished (phase[p] = 1) and finalize those. mode 2: finalize the others.
 __global__ void __launch_bounds__(64) k_ransac_final(RansacBufs B, RansacCfg cfg, int mode, int* phase) {
-    __builtin_amdgcn_s_setprio(3);  // latency-bound: issue ahead of co-resident extraction waves
+    __builtin_amdgcn_s_setprio(ODO_WAVE_PRIO);  // latency-bound: issue ahead of co-resident extraction waves
     const int p = blockIdx.x;
     const int lane = threadIdx.x;
     if (mode == 1) {

@@ -11,6 +11,12 @@
 
 #define ODO_INLINE __device__ __forceinline__
 
+// s_setprio level of the latency-bound kernels (pair match, RANSAC, PnP) so
+// their waves issue ahead of co-resident extraction waves
+#ifndef ODO_WAVE_PRIO
+#define ODO_WAVE_PRIO 3
+#endif
+
 namespace odo {
 
 // ----------------------------------------------------------------- rounding
