@@ -87,9 +87,19 @@ class Odometry:
         check(self.lib.odo_track_batch_host(self.h, ptr(bgr), ptr(depth), n, ptr(out) if want_results else None))
         return out
 
-    def set_timing(self, enable: bool):
-        """Record per-stage HIP events in odo_track_batch (serialises queues a little)."""
-        check(self.lib.odo_set_timing(self.h, 1 if enable else 0))
+    def set_timing(self, enable, mode: int = None):
+        """Timing mode: 0 off, 1 per-stage HIP events in odo_track_batch
+        (serialises the streams a little; see timings()), 2 an event pair around
+        the Hamming-match launch of every batch (see kernel_timing())."""
+        m = mode if mode is not None else (1 if enable else 0)
+        check(self.lib.odo_set_timing(self.h, m))
+
+    def kernel_timing(self):
+        """(mean Hamming-match launch duration in ms, launches) since mode 2 was set."""
+        avg = C.c_double(0)
+        n = C.c_long(0)
+        check(self.lib.odo_kernel_timing(self.h, C.byref(avg), C.byref(n)))
+        return avg.value, n.value
 
     def synchronize(self):
         check(self.lib.odo_synchronize(self.h))

@@ -93,6 +93,7 @@ SIGNATURES = {
     "odo_debug_octree": (C.c_int, [P, C.c_int, C.c_int, P, C.c_int, P]),
     "odo_debug_sort": (C.c_int, [P, P, C.c_int, P]),
     "odo_set_timing": (C.c_int, [P, C.c_int]),
+    "odo_kernel_timing": (C.c_int, [P, P, P]),
     "odo_debug_blur": (C.c_int, [P, C.c_int, P, C.c_size_t]),
     "odo_last_timings": (C.c_int, [P, P, C.c_int, P]),
 }

@@ -144,6 +144,14 @@ struct odo_ctx {
     bool pdone_rec[NSETS] = {};
     bool serial = false;
     bool timing = false;
+    // Hamming-match kernel timing (odo_set_timing mode 2): an event pair
+    // around the kNN-2 launch of every batch, read back and summed lazily
+    static constexpr int KT_RING = 256;
+    bool ktiming = false;
+    hipEvent_t kt0[KT_RING] = {}, kt1[KT_RING] = {};
+    int kt_next = 0, kt_pending = 0;
+    double kt_sum_ms = 0;
+    long kt_count = 0;
 };
 
 static inline size_t fbase(const odo_ctx* c, int set) { return (size_t)set * c->slots; }
@@ -157,8 +165,6 @@ static inline void tmark(odo_ctx* c, int i, hipStream_t st) {
     if (c->timing) hipEventRecord(c->ev[i], st);
 }
 
-// the pair stream's kernels are latency-bound: dispatch them ahead of the
-// extraction stream's throughput kernels
 // Every stream runs at the default priority: measured on MI355X, giving the
 // pair / PnP streams the highest priority starves the extraction stream and
 // costs 17% throughput (1.63 vs 1.35 ms per 64-frame step). ODO_STREAM_PRIO=1
@@ -195,6 +201,10 @@ static void free_ctx(odo_ctx* c) {
             if (q) hipFree(q);
     }
     for (int i = 0; i < c->nev; i++) hipEventDestroy(c->ev[i]);
+    for (int i = 0; i < odo_ctx::KT_RING; i++) {
+        if (c->kt0[i]) hipEventDestroy(c->kt0[i]);
+        if (c->kt1[i]) hipEventDestroy(c->kt1[i]);
+    }
     for (int i = 0; i < NSETS; i++) {
         hipEvent_t* evs[] = {&c->ev_ra[i], &c->ev_rb[i], &c->ev_pa[i], &c->ev_pb[i]};
         for (hipEvent_t* e : evs)
@@ -564,11 +574,47 @@ double odo_get_latch(odo_ctx* c) {
     return v;
 }
 
-int odo_set_timing(odo_ctx* c, int enable) {
-    if (!c) return fail(ODO_ERR_ARG, "null ctx");
+int odo_set_timing(odo_ctx* c, int mode) {
+    if (!c || mode < 0 || mode > 2) return fail(ODO_ERR_ARG, "bad timing mode");
     int e;
     if ((e = sync_all(c))) return e;
-    c->timing = enable != 0;
+    c->timing = mode == 1;
+    c->ktiming = mode == 2;
+    if (c->ktiming) {
+        if (!c->kt0[0])
+            for (int i = 0; i < odo_ctx::KT_RING; i++)
+                if (hipEventCreate(&c->kt0[i]) != hipSuccess || hipEventCreate(&c->kt1[i]) != hipSuccess)
+                    return fail(ODO_ERR_DEVICE, "hipEventCreate failed");
+        c->kt_next = c->kt_pending = 0;
+        c->kt_sum_ms = 0;
+        c->kt_count = 0;
+    }
+    return ODO_OK;
+}
+
+// fold the elapsed time of ring slot i into the running sum (waits for it)
+static int kt_collect(odo_ctx* c, int i) {
+    HIPCHK(hipEventSynchronize(c->kt1[i]));
+    float t = 0;
+    HIPCHK(hipEventElapsedTime(&t, c->kt0[i], c->kt1[i]));
+    c->kt_sum_ms += t;
+    c->kt_count++;
+    return ODO_OK;
+}
+
+int odo_kernel_timing(odo_ctx* c, double* avg_ms, long* launches) {
+    if (!c || !avg_ms || !launches) return fail(ODO_ERR_ARG, "null arg");
+    if (!c->ktiming) return fail(ODO_ERR_ARG, "kernel timing is off (odo_set_timing mode 2)");
+    int e;
+    if ((e = sync_all(c))) return e;
+    const int n = c->kt_pending;
+    for (int k = 0; k < n; k++) {
+        const int i = (c->kt_next - n + k + odo_ctx::KT_RING) % odo_ctx::KT_RING;
+        if ((e = kt_collect(c, i))) return e;
+    }
+    c->kt_pending = 0;
+    *launches = c->kt_count;
+    *avg_ms = c->kt_count ? c->kt_sum_ms / (double)c->kt_count : 0.0;
     return ODO_OK;
 }
 
@@ -715,8 +761,22 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
         const size_t b = fbase(c, s);
         uint8_t* desc = c->desc + b * KC * 32;
         int* nkp = c->nkp + b;
+        int kt = -1;
+        if (c->ktiming) {
+            kt = c->kt_next;
+            if (c->kt_pending == odo_ctx::KT_RING) {  // slot reused: fold its time first
+                if ((e = kt_collect(c, kt))) return e;
+                c->kt_pending--;
+            }
+            HIPCHK(hipEventRecord(c->kt0[kt], c->stream));
+        }
         launch_knn2(c->stream, desc, nkp, KC * 32, desc + KC * 32, nkp + 1, KC * 32, c->knn_idx[s], c->knn_dist[s],
                     KC, c->kp_cap, n);
+        if (kt >= 0) {
+            HIPCHK(hipEventRecord(c->kt1[kt], c->stream));
+            c->kt_next = (kt + 1) % odo_ctx::KT_RING;
+            c->kt_pending++;
+        }
         tmark(c, 10, c->stream);
     }
     HIPCHK(hipEventRecord(c->ev_xdone[s], c->stream));

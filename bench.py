@@ -27,8 +27,13 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG_DIR = os.path.join(ROOT, "adaptive-rgbd-localization-mappig_amd")
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-INT_VALU_PEAK_TOPS = 78.6    # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (int32 VALU lane-ops)
-FP64_VALU_PEAK_TF = 78.6     # MI355X FP64 vector (FMA = 2 flops)
+# int32 VALU lane-ops: 256 CU x 4 SIMD x 16 lanes/clk (a wave64 VALU op issues
+# every 4 clk, MI355X_MICROARCH.md cycle constants) x 2.4 GHz
+INT_VALU_PEAK_TOPS = 256 * 4 * 16 * 2.4e9 / 1e12
+# Hamming-match work per (query, train) comparison: 8 xor + 8 popcount over the
+# 256-bit descriptors, key formation, and the top-2 update (min + med3)
+KNN_OPS_PER_CMP = 19
+KNN_TRAFFIC = os.path.join(ROOT, "profiles", "r01_knn2_traffic.json")
 
 
 def load_module(name, path, pkg_dir=None):
@@ -52,6 +57,27 @@ def load_synth():
 def shard_seed(rank: int) -> int:
     """Each rank tracks its own sequence (independent scene seed)."""
     return 0x5EED0002 + 7919 * rank
+
+
+def rank_seeds(rank: int):
+    """(scene seed, RANSAC/pair seed base) of one rank: ranks shard the frames
+    (each tracks its own sequence), no data-path collective."""
+    return shard_seed(rank), 0x5EED0000 + 1000003 * rank
+
+
+def max_over_ranks(x: float, dist=None, world: int = 1, device: str = "cuda") -> float:
+    """Job time = the slowest rank's time (all_reduce MAX; RCCL on GPUs, gloo in tests)."""
+    if world <= 1:
+        return x
+    import torch
+    t = torch.tensor([x], device=device, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def job_throughput(frames_per_step: int, steps: int, world: int, elapsed_max: float) -> float:
+    """Whole-job frames/s: every rank tracks frames_per_step frames per step."""
+    return frames_per_step * steps * world / elapsed_max
 
 
 def level_pixels(w, h, nlevels=8, scale=1.2):
@@ -78,8 +104,8 @@ def stage_model(stage, ms, B, w, h, nkp_mean):
         byts = B * pyr_px
         return "hbm", byts / (ms * 1e-3) / 1e9, HBM_PEAK_GBS, "GB/s", byts
     if stage == "knn2":
-        ops = B * 16.0 * nkp_mean * nkp_mean
-        return "valu-int", ops / (ms * 1e-3) / 1e12, INT_VALU_PEAK_TOPS, "Tops/s", ops
+        ops = B * float(KNN_OPS_PER_CMP) * nkp_mean * nkp_mean
+        return "valu", ops / (ms * 1e-3) / 1e12, INT_VALU_PEAK_TOPS, "Top/s", ops
     byts = B * (5 * w * h + 84 * nkp_mean)
     return "hbm", byts / (ms * 1e-3) / 1e9, HBM_PEAK_GBS, "GB/s", byts
 
@@ -96,7 +122,7 @@ def cpu_baseline(bgr, dep, nfeat, iters, n_frames):
     prev = None
     latch = float("nan")
     for i in range(n_frames):
-        f = O.extract_frame(bgr[i], dep[i], p, cal)
+        f = O.extract_frame(bgr[i % len(bgr)], dep[i % len(dep)], p, cal)
         if prev is not None:
             _, _, _, latch = O.track_pair(prev, f, cal, rp, pkg.pair_seed(0x5EED0000, i), latch)
         prev = f
@@ -114,7 +140,8 @@ def main():
     ap.add_argument("--iters", type=int, default=500, help="RANSAC hypotheses (mIterations)")
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
-    ap.add_argument("--cpu-frames", type=int, default=48, help="oracle sample size (frames)")
+    ap.add_argument("--cpu-frames", type=int, default=192, help="oracle sample size (frames, ~10 s)")
+    ap.add_argument("--no-kernel-timing", action="store_true", help="no events around the kNN-2 launches")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -131,11 +158,11 @@ def main():
     pkg = load_pkg()
     synth = load_synth()
     B, W, H = args.batch, args.width, args.height
-    bgr, dep, _ = synth.make_sequence(B, W, H, seed=shard_seed(rank), closed_loop=True)
+    scene_seed, pair_seed = rank_seeds(rank)
+    bgr, dep, _ = synth.make_sequence(B, W, H, seed=scene_seed, closed_loop=True)
     d_bgr = torch.from_numpy(bgr).to("cuda")
     d_dep = torch.from_numpy(dep.view(np.int16)).to("cuda")
-    cfg = pkg.default_config(W, H, B, nfeatures=args.nfeatures, iterations=args.iters,
-                             seed=0x5EED0000 + 1000003 * rank)
+    cfg = pkg.default_config(W, H, B, nfeatures=args.nfeatures, iterations=args.iters, seed=pair_seed)
     odo = pkg.Odometry(cfg, device=local_rank)
     torch.cuda.synchronize()
 
@@ -148,6 +175,10 @@ def main():
 
     if world > 1:
         dist.barrier()
+    # Hamming-match (kNN-2) launches are bracketed by HIP events on their own
+    # (extraction) stream inside the timed region (odo timing mode 2)
+    if not args.no_kernel_timing:
+        odo.set_timing(None, mode=2)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -157,11 +188,8 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(time.perf_counter() - t0, dist, world)
+    knn_ms, knn_launches = odo.kernel_timing() if not args.no_kernel_timing else (None, 0)
 
     # per-stage times: one extra (untimed) step with the stage events on
     odo.set_timing(True)
@@ -169,26 +197,41 @@ def main():
     odo.synchronize()
     timings = odo.timings()
     odo.set_timing(False)
-    frames = B * args.steps * world
-    value = frames / elapsed
+    value = job_throughput(B, args.steps, world, elapsed)
     ms_per_step = elapsed / args.steps * 1e3
 
-    nkp_mean = float(np.mean([len(odo.frame(i)["kps"]) for i in range(min(B, 4))]))
-    kern = {k: v for k, v in timings.items() if v > 0}
-    dominant = max(kern, key=kern.get) if kern else None
+    nkp = [len(odo.frame(i)["kps"]) for i in range(B)]
+    nkp_mean = float(np.mean(nkp))
+    # Roofline of the Hamming-match kernel (k_knn2), the kernel the north star
+    # names. Brute-force kNN-2 re-reads each 32-byte descriptor ~2000 times from
+    # LDS, so it is bound by the integer VALU issue rate, not by HBM: achieved =
+    # algorithmic lane-ops of one launch / its live mean duration.
     roofline = None
-    if dominant:
-        bound, ach, peak, unit, work = stage_model(dominant, kern[dominant], B, W, H, nkp_mean)
-        roofline = {"bound": bound, "achieved": round(ach, 3), "peak": peak, "unit": unit,
-                    "frac": round(ach / peak, 5), "traffic": None, "kernel": dominant,
-                    "kernel_ms": round(kern[dominant], 4)}
+    if knn_ms:
+        # pair p = (slot p, slot p+1); slot 0 is the previous batch's last frame
+        # (the same sequence is tracked every step)
+        cmp = nkp[B - 1] * nkp[0] + sum(nkp[i] * nkp[i + 1] for i in range(B - 1))
+        ops = float(KNN_OPS_PER_CMP) * cmp
+        ach = ops / (knn_ms * 1e-3) / 1e12
+        traffic = None
+        if os.path.exists(KNN_TRAFFIC):
+            with open(KNN_TRAFFIC) as f:
+                traffic = json.load(f).get("hbm_bytes_per_launch")
+        roofline = {"bound": "valu", "achieved": round(ach, 3), "peak": round(INT_VALU_PEAK_TOPS, 2),
+                    "unit": "Top/s", "frac": round(ach / INT_VALU_PEAK_TOPS, 4), "traffic": traffic,
+                    "kernel": "k_knn2", "kernel_ms": round(knn_ms, 4), "launches": knn_launches,
+                    "work": f"{cmp} descriptor comparisons x {KNN_OPS_PER_CMP} int32 lane-ops",
+                    # algorithmic HBM bytes: every descriptor read once, 16 B of top-2 out per query
+                    "hbm_gbs": round(sum(2 * 32 * nkp[i] + 16 * nkp[i] for i in range(B)) /
+                                     (knn_ms * 1e-3) / 1e9, 1)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        nf = min(args.cpu_frames, B)
+        nf = args.cpu_frames
         fps, dt = cpu_baseline(bgr, dep, args.nfeatures, args.iters, nf)
         cpu = {"value": round(fps, 3), "unit": "frames/s", "cores": 1, "kind": "port",
-               "sample": f"first {nf} frames of the rank-0 sequence, C++ oracle single-thread ({dt:.1f} s)"}
+               "sample": f"{nf} frames (the rank-0 {B}-frame sequence, cycled) through the C++ oracle's "
+                         f"extract + match + RANSAC + PnP, single thread ({dt:.1f} s)"}
 
     if rank == 0:
         ok = res[1:]

@@ -125,9 +125,13 @@ int odo_debug_blur(odo_ctx* ctx, int i, uint8_t* out, size_t cap);
  * stage runs it on the GPU (workgroup-parallel introsort): in -> out sorted by
  * distance in libstdc++'s exact (unstable) order; distances must be >= 0. */
 int odo_debug_sort(odo_ctx* ctx, const odo_dmatch* in, int n, odo_dmatch* out);
-/* Stage timing (off by default): when on, odo_track_batch records HIP events
- * between stages; odo_last_timings then reports the last batch (ms). */
-int odo_set_timing(odo_ctx* ctx, int enable);
+/* Timing (off by default; mode 0). Mode 1: odo_track_batch records HIP events
+ * between stages and odo_last_timings reports the last batch (ms); these
+ * events serialise the streams they sit on. Mode 2: an event pair brackets the
+ * Hamming-match (kNN-2) launch of every batch on the extraction stream, and
+ * odo_kernel_timing reports the mean launch duration since the mode was set. */
+int odo_set_timing(odo_ctx* ctx, int mode);
+int odo_kernel_timing(odo_ctx* ctx, double* avg_ms, long* launches);
 /* Per-stage device time of the last odo_track_batch (ms), via HIP events. */
 int odo_last_timings(odo_ctx* ctx, float* ms, int cap, const char** names);
 
