@@ -63,7 +63,9 @@ double odo_get_latch(odo_ctx* ctx);
  * d_bgr: device [n][H][W][3] u8, d_depth: device [n][H][W] u16 (x5000).
  * results[n] (host): results[i] is the pair (frame i-1 -> frame i); frame -1
  * is the last frame of the previous call. When h_results is NULL the call is
- * asynchronous on odo_stream(). */
+ * asynchronous: the work runs on the library's streams (extraction =
+ * odo_stream(), plus pair / PnP / side streams), d_bgr and d_depth are read by
+ * the extraction stream, and odo_synchronize() waits for all of them. */
 int odo_track_batch(odo_ctx* ctx, const uint8_t* d_bgr, const uint16_t* d_depth, int n,
                     odo_pair_result* h_results);
 /* Same with host inputs (H2D copy included). */
