@@ -144,6 +144,9 @@ struct odo_ctx {
     bool pdone_rec[NSETS] = {};
     bool serial = false;
     bool timing = false;
+    // ODO_SKIP (measurement only; results are invalid when set): bit 0 skips
+    // the PnP launches, bit 1 RANSAC part 2, bit 2 every pair stage, bit 3 kNN-2
+    int skip = 0;
     // Hamming-match kernel timing (odo_set_timing mode 2): an event pair
     // around the kNN-2 launch of every batch, read back and summed lazily
     static constexpr int KT_RING = 256;
@@ -499,6 +502,7 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
     // so per-kernel times are free of cross-stream contention
     const char* ser = getenv("ODO_SERIAL_STREAMS");
     c->serial = ser && ser[0] == '1';
+    if (const char* sk = getenv("ODO_SKIP")) c->skip = atoi(sk);
     bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
               (c->serial || (hipStreamCreateWithPriority(&c->pstream, hipStreamNonBlocking, pair_stream_priority()) ==
                                  hipSuccess &&
@@ -705,15 +709,18 @@ static int run_pairs(odo_ctx* c, int set, int n) {
                   P.pair_phase);
     HIPCHK(hipEventRecord(c->ev_ra[set], st));
     HIPCHK(hipStreamWaitEvent(c->pnpa, c->ev_ra[set], 0));
+    if (!(c->skip & 1))
     launch_pnp(c->pnpa, P.f2_src, xyz, c->kun + b * KC * 2, c->ur + b * KC, nkp, c->kp_cap, 0, c->cal, P.T12,
                P.pair_valid, P.n_matches, 20, P.edges, P.res, P.pnp_mask, n, P.pair_phase, 1);
     HIPCHK(hipEventRecord(c->ev_pa[set], c->pnpa));
+    if (!(c->skip & 2))
     launch_ransac(st, P.good, P.n_good, P.n_matches, P.matches, xyz, c->kp_cap, 0, c->match_cap, c->rcfg, c->latch,
                   P.pair_valid, 20, nullptr, c->rscr[set], P.best_mask, c->mask_words, P.res, P.T12, n, 2,
                   P.pair_phase);
     tmark(c, 8, st);
     HIPCHK(hipEventRecord(c->ev_rb[set], st));
     HIPCHK(hipStreamWaitEvent(c->pnpb, c->ev_rb[set], 0));
+    if (!(c->skip & 1))
     launch_pnp(c->pnpb, P.f2_src, xyz, c->kun + b * KC * 2, c->ur + b * KC, nkp, c->kp_cap, 0, c->cal, P.T12,
                P.pair_valid, P.n_matches, 20, P.edges, P.res, P.pnp_mask, n, P.pair_phase, 0);
     tmark(c, 9, c->pnpb);
@@ -770,8 +777,9 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
             }
             HIPCHK(hipEventRecord(c->kt0[kt], c->stream));
         }
-        launch_knn2(c->stream, desc, nkp, KC * 32, desc + KC * 32, nkp + 1, KC * 32, c->knn_idx[s], c->knn_dist[s],
-                    KC, c->kp_cap, n);
+        if (!(c->skip & 8))
+            launch_knn2(c->stream, desc, nkp, KC * 32, desc + KC * 32, nkp + 1, KC * 32, c->knn_idx[s],
+                        c->knn_dist[s], KC, c->kp_cap, n);
         if (kt >= 0) {
             HIPCHK(hipEventRecord(c->kt1[kt], c->stream));
             c->kt_next = (kt + 1) % odo_ctx::KT_RING;
@@ -790,7 +798,7 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
     HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_raw[s], 0));
     c->valid_h.assign(n, 1);
     c->valid_h[0] = c->has_prev ? 1 : 0;
-    if ((e = run_pairs(c, s, n))) return e;
+    if (!(c->skip & 4) && (e = run_pairs(c, s, n))) return e;
     c->pdone_rec[s] = true;
     c->seq_set = s;
     c->seq_n = n;

@@ -136,6 +136,7 @@ def main():
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=64, help="frames per step")
+    ap.add_argument("--seq-len", type=int, default=64, help="frames in the closed-loop sequence (motion per frame)")
     ap.add_argument("--nfeatures", type=int, default=2000)
     ap.add_argument("--iters", type=int, default=500, help="RANSAC hypotheses (mIterations)")
     ap.add_argument("--width", type=int, default=640)
@@ -159,7 +160,15 @@ def main():
     synth = load_synth()
     B, W, H = args.batch, args.width, args.height
     scene_seed, pair_seed = rank_seeds(rank)
-    bgr, dep, _ = synth.make_sequence(B, W, H, seed=scene_seed, closed_loop=True)
+    # a closed loop of --seq-len distinct frames (fixed inter-frame motion);
+    # a batch of B frames walks it cyclically, so every pair is a genuine
+    # consecutive pair whatever B is
+    L = min(args.seq_len, B)
+    if B % L:
+        raise SystemExit(f"--batch {B} must be a multiple of --seq-len {L} (pair 0 links frame B-1 to frame 0)")
+    bgr, dep, _ = synth.make_sequence(L, W, H, seed=scene_seed, closed_loop=True)
+    if B != L:
+        bgr, dep = bgr[np.arange(B) % L], dep[np.arange(B) % L]
     d_bgr = torch.from_numpy(bgr).to("cuda")
     d_dep = torch.from_numpy(dep.view(np.int16)).to("cuda")
     cfg = pkg.default_config(W, H, B, nfeatures=args.nfeatures, iterations=args.iters, seed=pair_seed)
