@@ -3,7 +3,7 @@
 The compute path is libodo_hip.so (hand-written HIP for gfx950, C-ABI in
 include/odo.h). This package is a thin Python binding used by tests and
 bench.py; the reference-shaped C++ adapters (Extractor / Matcher / Ransac /
-PnPSolver / Kabsch) live in csrc/host/odo_reference_api.hpp.
+PnPSolver / Kabsch) are shown in INTEGRATION.md.
 """
 from __future__ import annotations
 

@@ -245,7 +245,8 @@ def test_extract_entry_point_bgr_and_gray(pkg):
 
 
 @pytest.mark.parametrize("iters,corrupt", [(1, 0.0), (200, 0.0), (500, 0.0), (500, 0.3), (500, 0.55),
-                                           (1200, 0.5), (40, 0.7)])
+                                           (1200, 0.5), (40, 0.7),
+                                           (4096, 0.6), (8192, 0.75)])
 def test_ransac_entry_point_stream_and_latch(pkg, iters, corrupt):
     """odo_ransac == Ransac::Iterate: bit-exact T12/rmse/inliers, rand() stream
     advanced by exactly the visited draws, latch set on first call. `corrupt`
