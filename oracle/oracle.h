@@ -61,6 +61,29 @@ float oracle_fast_atan2(float y, float x);
 int oracle_orb_extract(const uint8_t* gray, int w, int h, const odo_orb_params* p,
                        orb_kp* kps, uint8_t* desc, int cap);
 
+/* ---- Extractor(FAST, ORB, ADAPTIVE) (extractor.cpp:14-77, a10). thresh:
+ * in/out per-cell DetectorAdjuster thresholds (grid_rows*grid_cols doubles,
+ * start at init_thresh); t_used (optional): FAST threshold of each cell's last
+ * detect call. */
+void oracle_adaptive_default(odo_adaptive_params* p);
+/* VideoGridAdaptedFeatureDetector::detect (before retainBest). Returns N. */
+int oracle_adaptive_detect(const uint8_t* gray, int w, int h, const odo_adaptive_params* p,
+                           double* thresh, orb_kp* out, int cap, int* t_used);
+/* cv::FAST(roi, thr, nonmax) on an ROI given by pointer/stride/size. */
+int oracle_fast_roi(const uint8_t* gray, int stride, int rows, int cols, int threshold,
+                    orb_kp* out, int cap);
+/* Extractor::Extract: detect + retainBest(nFeatures) + cv::ORB::compute. */
+int oracle_adaptive_extract(const uint8_t* gray, int w, int h, const odo_adaptive_params* p,
+                            double* thresh, orb_kp* kps, uint8_t* desc, int cap, int* t_used);
+/* libstdc++ std::nth_element / retainBest on packed (score<<24|y<<12|x). */
+void oracle_nth_element_score(uint32_t* a, int n, int nth);
+int oracle_retain_best_score(uint32_t* a, int n, int n_points);
+/* Full Frame construction in ADAPTIVE mode. Returns N. */
+int oracle_extract_frame_adaptive(const uint8_t* bgr, const uint16_t* depth, int w, int h,
+                                  const odo_adaptive_params* p, double* thresh, const odo_calib* c,
+                                  orb_kp* kps, uint8_t* desc, float* kps_un, float* xyz,
+                                  float* u_right, int cap);
+
 /* Frame::ExtractFeatures tail + UndistortKeyPoints (frame.cpp:139-169, 286-313). */
 void oracle_frame_geometry(const orb_kp* kps, int n, const float* depth, int w, int h,
                            const odo_calib* c, float* kps_un, float* xyz, float* u_right);

@@ -605,6 +605,129 @@ struct Extractor {
     int ini_th = 20, min_th = 7;
 };
 
+
+// ---------------------------------------------------------------- ADAPTIVE
+// Extractor(FAST, ORB, ADAPTIVE) (extractor.cpp:14-77): a 3x3
+// VideoGridAdaptedFeatureDetector over VideoDynamicAdaptedFeatureDetector
+// cells, each owning a DetectorAdjuster(FAST, 20, 2, 10000, 1.3, 0.7) whose
+// threshold persists across frames; then KeyPointsFilter::retainBest and
+// cv::ORB::compute. The libstdc++ selection algorithms are the real ones.
+
+// keepStrongest / ResponseComparator (videogridadaptedfeaturedetector.cpp:17-31)
+void keep_strongest(int N, std::vector<KP>& kps) {
+    if ((int)kps.size() > N) {
+        std::nth_element(kps.begin(), kps.begin() + N, kps.end(),
+                         [](const KP& a, const KP& b) { return std::abs(a.response) > std::abs(b.response); });
+        kps.erase(kps.begin() + N, kps.end());
+    }
+}
+
+// cv::KeyPointsFilter::retainBest (OpenCV 3.4 keypoint.cpp): nth_element by
+// response (greater), then partition the tail keeping the boundary ties.
+void retain_best(std::vector<KP>& kps, int n_points) {
+    if (n_points >= 0 && kps.size() > (size_t)n_points) {
+        if (n_points == 0) {
+            kps.clear();
+            return;
+        }
+        std::nth_element(kps.begin(), kps.begin() + n_points, kps.end(),
+                         [](const KP& a, const KP& b) { return a.response > b.response; });
+        const float amb = kps[n_points - 1].response;
+        auto new_end = std::partition(kps.begin() + n_points, kps.end(),
+                                      [amb](const KP& k) { return k.response >= amb; });
+        kps.resize(new_end - kps.begin());
+    }
+}
+
+// One grid cell's stateful detector: VideoDynamicAdaptedFeatureDetector::detect
+// (videodynamicadaptedfeaturedetector.cpp:24-44) over DetectorAdjuster
+// (detectoradjuster.cpp:22-65) with the FAST inner detector: the double
+// threshold is passed to FastFeatureDetector::create(int) (truncation).
+int adaptive_cell_detect(const uint8_t* base, int stride, int rows, int cols, const odo_adaptive_params& p,
+                         double& thresh, std::vector<KP>& kps) {
+    int iterCount = p.escape_iters;
+    int t_used = 0;
+    do {
+        kps.clear();
+        t_used = (int)thresh;
+        fast_roi(base, stride, rows, cols, t_used, kps);
+        const int found = (int)kps.size();
+        if (found < p.cell_min) {
+            thresh *= p.decrease_factor;  // tooFew
+            if (thresh < p.min_thresh) thresh = p.min_thresh;
+        } else if (found > p.cell_max) {
+            thresh *= p.increase_factor;  // tooMany
+            if (thresh > p.max_thresh) thresh = p.max_thresh;
+            break;
+        } else
+            break;
+        iterCount--;
+    } while (iterCount > 0 && (thresh > p.min_thresh) && (thresh < p.max_thresh));
+    return std::min(std::max(t_used, 0), 255);
+}
+
+// VideoGridAdaptedFeatureDetector::detect (videogridadaptedfeaturedetector.cpp:52-84)
+void adaptive_grid_detect(const uint8_t* gray, int w, int h, const odo_adaptive_params& p, double* thresh,
+                          std::vector<KP>& out, int* t_used) {
+    const int R = p.grid_rows, C = p.grid_cols, E = p.edge_threshold;
+    const int maxPerCell = p.max_total_keypoints / (R * C);
+    std::vector<std::vector<KP>> sub(R * C);
+    for (int i = 0; i < R; ++i) {
+        const int rs = std::max((i * h) / R - E, 0), re = std::min(h, ((i + 1) * h) / R + E);
+        for (int j = 0; j < C; ++j) {
+            const int cs = std::max((j * w) / C - E, 0), ce = std::min(w, ((j + 1) * w) / C + E);
+            const int t = adaptive_cell_detect(gray + (size_t)rs * w + cs, w, re - rs, ce - cs, p, thresh[j + i * C],
+                                               sub[j + i * C]);
+            if (t_used) t_used[j + i * C] = t;
+            keep_strongest(maxPerCell, sub[j + i * C]);
+        }
+    }
+    out.clear();
+    for (int i = 0; i < R; ++i) {  // aggregateKeypointsPerGridCell (:33-50)
+        const int rs = std::max((i * h) / R - E, 0);
+        for (int j = 0; j < C; ++j) {
+            const int cs = std::max((j * w) / C - E, 0);
+            for (KP& k : sub[j + i * C]) {
+                k.x += cs;
+                k.y += rs;
+            }
+            out.insert(out.end(), sub[j + i * C].begin(), sub[j + i * C].end());
+        }
+    }
+}
+
+// cv::ORB::compute on provided keypoints (OpenCV 3.4 orb.cpp detectAndCompute,
+// useProvidedKeypoints): runByImageBorder(edgeThreshold 31), one pyramid level
+// (every FAST keypoint has octave 0), GaussianBlur 7x7 sigma 2 REFLECT_101 of
+// that level, rBRIEF at the keypoint's own angle (-1 for FAST keypoints: ORB
+// does not orient provided keypoints).
+void orb_compute_provided(const uint8_t* gray, int w, int h, std::vector<KP>& kps, std::vector<uint8_t>& desc) {
+    const int border = 31;
+    if (h <= 2 * border || w <= 2 * border) kps.clear();
+    else {
+        const float x0 = border, y0 = border, x1 = (float)(w - border), y1 = (float)(h - border);
+        kps.erase(std::remove_if(kps.begin(), kps.end(),
+                                 [&](const KP& k) { return !(x0 <= k.x && k.x < x1 && y0 <= k.y && k.y < y1); }),
+                  kps.end());
+    }
+    desc.assign(kps.size() * 32, 0);
+    if (kps.empty()) return;
+    Img im, blurred;
+    im.w = w;
+    im.h = h;
+    im.px.assign(gray, gray + (size_t)w * h);
+    gaussian_blur(im, blurred);
+    for (size_t i = 0; i < kps.size(); i++) orb_descriptor(kps[i], blurred, &desc[i * 32]);
+}
+
+int adaptive_extract(const uint8_t* gray, int w, int h, const odo_adaptive_params& p, double* thresh,
+                     std::vector<KP>& kps, std::vector<uint8_t>& desc, int* t_used) {
+    adaptive_grid_detect(gray, w, h, p, thresh, kps, t_used);
+    if ((int)kps.size() > p.retain_best) retain_best(kps, p.retain_best);  // extractor.cpp:45-46
+    orb_compute_provided(gray, w, h, kps, desc);
+    return (int)kps.size();
+}
+
 }  // namespace
 
 // ================================================================ C API
@@ -702,6 +825,62 @@ int oracle_orb_extract(const uint8_t* gray, int w, int h, const odo_orb_params* 
                         out[i].class_id};
     if (desc) memcpy(desc, d.data(), (size_t)m * 32);
     return n;
+}
+
+static void kp_out(const std::vector<KP>& v, orb_kp* out, int cap) {
+    const int m = std::min((int)v.size(), cap);
+    for (int i = 0; i < m; i++)
+        out[i] = orb_kp{v[i].x, v[i].y, v[i].size, v[i].angle, v[i].response, v[i].octave, v[i].class_id};
+}
+
+void oracle_adaptive_default(odo_adaptive_params* p) {
+    // Extractor::CreateAdaptiveDetector (extractor.cpp:55-77) + nFeatures (common.h:77)
+    const int minFeatures = 600;
+    const int maxFeatures = minFeatures * 1.7;
+    const int cells = 3 * 3;
+    *p = odo_adaptive_params{3, 3, 31, maxFeatures, (int)round(minFeatures / (float)cells),
+                             (int)round(maxFeatures / (float)cells), 5, 20, 2, 10000, 1.3, 0.7, 1000};
+}
+
+int oracle_adaptive_detect(const uint8_t* gray, int w, int h, const odo_adaptive_params* p, double* thresh,
+                           orb_kp* out, int cap, int* t_used) {
+    std::vector<KP> k;
+    adaptive_grid_detect(gray, w, h, *p, thresh, k, t_used);
+    kp_out(k, out, cap);
+    return (int)k.size();
+}
+
+int oracle_fast_roi(const uint8_t* gray, int stride, int rows, int cols, int threshold, orb_kp* out, int cap) {
+    std::vector<KP> k;
+    fast_roi(gray, stride, rows, cols, threshold, k);
+    kp_out(k, out, cap);
+    return (int)k.size();
+}
+
+int oracle_adaptive_extract(const uint8_t* gray, int w, int h, const odo_adaptive_params* p, double* thresh,
+                            orb_kp* kps, uint8_t* desc, int cap, int* t_used) {
+    std::vector<KP> k;
+    std::vector<uint8_t> d;
+    const int n = adaptive_extract(gray, w, h, *p, thresh, k, d, t_used);
+    kp_out(k, kps, cap);
+    if (desc) memcpy(desc, d.data(), (size_t)std::min(n, cap) * 32);
+    return n;
+}
+
+// std::nth_element / partition helpers on packed (score<<24 | y<<12 | x)
+// keys, compared by score only (the GPU selection's test hooks)
+void oracle_nth_element_score(uint32_t* a, int n, int nth) {
+    std::nth_element(a, a + nth, a + n, [](uint32_t x, uint32_t y) { return (x >> 24) > (y >> 24); });
+}
+
+int oracle_retain_best_score(uint32_t* a, int n, int n_points) {
+    std::vector<KP> k(n);
+    for (int i = 0; i < n; i++) k[i] = KP{(float)(a[i] & 0xfff), (float)((a[i] >> 12) & 0xfff), 7.f, -1.f,
+                                          (float)(a[i] >> 24), 0, -1};
+    retain_best(k, n_points);
+    for (size_t i = 0; i < k.size(); i++)
+        a[i] = ((uint32_t)k[i].response << 24) | ((uint32_t)k[i].y << 12) | (uint32_t)k[i].x;
+    return (int)k.size();
 }
 
 }  // extern "C"

@@ -994,6 +994,20 @@ int oracle_extract_frame(const uint8_t* bgr, const uint16_t* depth, int w, int h
     return n;
 }
 
+int oracle_extract_frame_adaptive(const uint8_t* bgr, const uint16_t* depth, int w, int h,
+                                  const odo_adaptive_params* p, double* thresh, const odo_calib* c,
+                                  orb_kp* kps, uint8_t* desc, float* kps_un, float* xyz, float* u_right,
+                                  int cap) {
+    std::vector<uint8_t> gray((size_t)w * h);
+    std::vector<float> z((size_t)w * h);
+    oracle_bgr2gray(bgr, w, h, 3 * w, gray.data());
+    oracle_depth_to_f32(depth, w * h, c->depth_factor, z.data());
+    int n = oracle_adaptive_extract(gray.data(), w, h, p, thresh, kps, desc, cap, nullptr);
+    int m = std::min(n, cap);
+    oracle_frame_geometry(kps, m, z.data(), w, h, c, kps_un, xyz, u_right);
+    return n;
+}
+
 void oracle_knn2(const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* idx, int32_t* dist) {
     for (int i = 0; i < nq; i++) {
         int nidx[2] = {-1, -1};

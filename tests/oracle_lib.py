@@ -40,6 +40,14 @@ class RansacParams(C.Structure):
                 ("sample_size", C.c_int32), ("check_depth", C.c_int32)]
 
 
+class AdaptiveParams(C.Structure):
+    _fields_ = [("grid_rows", C.c_int32), ("grid_cols", C.c_int32), ("edge_threshold", C.c_int32),
+                ("max_total_keypoints", C.c_int32), ("cell_min", C.c_int32), ("cell_max", C.c_int32),
+                ("escape_iters", C.c_int32), ("init_thresh", C.c_double), ("min_thresh", C.c_double),
+                ("max_thresh", C.c_double), ("increase_factor", C.c_double), ("decrease_factor", C.c_double),
+                ("retain_best", C.c_int32)]
+
+
 class Rng(C.Structure):
     _fields_ = [("state", C.c_int32 * 31), ("fpos", C.c_int32), ("rpos", C.c_int32)]
 
@@ -99,6 +107,13 @@ def lib():
             "oracle_kabsch": (None, [P, P, C.c_int, P]),
             "oracle_track_pair": (C.c_int, [P, P, P, C.c_int, P, P, P, P, P, C.c_int, P, C.c_float, P,
                                             C.c_uint32, P, P, P, P, C.c_int]),
+            "oracle_adaptive_default": (None, [P]),
+            "oracle_adaptive_detect": (C.c_int, [P, C.c_int, C.c_int, P, P, P, C.c_int, P]),
+            "oracle_fast_roi": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, P, C.c_int]),
+            "oracle_adaptive_extract": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, C.c_int, P]),
+            "oracle_nth_element_score": (None, [P, C.c_int, C.c_int]),
+            "oracle_retain_best_score": (C.c_int, [P, C.c_int, C.c_int]),
+            "oracle_extract_frame_adaptive": (C.c_int, [P, P, C.c_int, C.c_int, P, P, P, P, P, P, P, P, C.c_int]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -159,3 +174,39 @@ def track_pair(f1, f2, calib: Calib, rp: RansacParams, seed: int, latch=float("n
                              C.byref(calib), ratio, C.byref(rp), seed, C.byref(lat), C.byref(res),
                              ptr(mask), ptr(matches), max(n1, 1))
     return res, mask[:n2], matches[:nm], lat.value
+
+
+def adaptive_params() -> AdaptiveParams:
+    p = AdaptiveParams()
+    lib().oracle_adaptive_default(C.byref(p))
+    return p
+
+
+class AdaptiveExtractor:
+    """Extractor(FAST, ORB, ADAPTIVE): per-cell thresholds persist across calls."""
+
+    def __init__(self, params: AdaptiveParams = None):
+        self.p = params or adaptive_params()
+        self.thresh = np.full(self.p.grid_rows * self.p.grid_cols, self.p.init_thresh, np.float64)
+
+    def extract_frame(self, bgr, depth, calib: Calib, cap=1100):
+        h, w = bgr.shape[:2]
+        kps = np.zeros(cap, KP_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        kun = np.zeros((cap, 2), np.float32)
+        xyz = np.zeros((cap, 3), np.float32)
+        ur = np.zeros(cap, np.float32)
+        n = lib().oracle_extract_frame_adaptive(ptr(np.ascontiguousarray(bgr)), ptr(np.ascontiguousarray(depth)),
+                                                w, h, C.byref(self.p), ptr(self.thresh), C.byref(calib), ptr(kps),
+                                                ptr(desc), ptr(kun), ptr(xyz), ptr(ur), cap)
+        assert n <= cap
+        return dict(kps=kps[:n], desc=desc[:n], kun=kun[:n], xyz=xyz[:n], ur=ur[:n])
+
+    def extract_gray(self, gray, cap=1100):
+        h, w = gray.shape
+        kps = np.zeros(cap, KP_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        t_used = np.zeros(self.p.grid_rows * self.p.grid_cols, np.int32)
+        n = lib().oracle_adaptive_extract(ptr(np.ascontiguousarray(gray)), w, h, C.byref(self.p), ptr(self.thresh),
+                                          ptr(kps), ptr(desc), cap, ptr(t_used))
+        return kps[:n], desc[:n], t_used
