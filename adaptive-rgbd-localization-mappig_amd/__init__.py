@@ -12,18 +12,22 @@ import ctypes as C
 import numpy as np
 
 from . import _abi
-from ._abi import (Calib, Config, DMatch, DMATCH_DTYPE, KP_DTYPE, OrbParams, PAIR_DTYPE, PairResult,
-                   RansacParams, Rng, check, load, ptr)
+from ._abi import (DETECTOR_ADAPTIVE_FAST, DETECTOR_ORB_SLAM2, AdaptiveParams, Calib, Config, DMatch,
+                   DMATCH_DTYPE, KP_DTYPE, OrbParams, PAIR_DTYPE, PairResult, RansacParams, Rng, check, load, ptr)
 
 __all__ = ["Odometry", "default_config", "load", "KP_DTYPE", "DMATCH_DTYPE", "PAIR_DTYPE", "rng_stream",
-           "kabsch", "Calib", "OrbParams", "RansacParams", "Config"]
+           "kabsch", "Calib", "OrbParams", "RansacParams", "Config", "AdaptiveParams", "DETECTOR_ORB_SLAM2",
+           "DETECTOR_ADAPTIVE_FAST"]
 
 
 def default_config(width=640, height=480, max_batch=1, nfeatures=1000, iterations=200, seed=0x5EED0000,
-                   calib=None) -> Config:
-    """Reference defaults (extractor.cpp:86, odometry.cpp:28, common.h FR1)."""
+                   calib=None, detector=_abi.DETECTOR_ORB_SLAM2) -> Config:
+    """Reference defaults (extractor.cpp:86, odometry.cpp:28, common.h FR1).
+    detector: DETECTOR_ORB_SLAM2 (main.cpp:19-21) or DETECTOR_ADAPTIVE_FAST
+    (Extractor(FAST, ORB, ADAPTIVE), extractor.cpp:55-77)."""
     cfg = Config()
     load().odo_default_config(ptr(cfg), width, height, max_batch)
+    cfg.detector = detector
     cfg.orb.nfeatures = nfeatures
     cfg.ransac.iterations = iterations
     cfg.seed = seed
@@ -43,7 +47,8 @@ class Odometry:
         if not h:
             raise RuntimeError("odo_create failed: " + self.lib.odo_last_error().decode())
         self.h = h
-        self.kp_cap = cfg.orb.nfeatures + 4 * cfg.orb.nlevels + 64
+        self.kp_cap = max(cfg.orb.nfeatures + 4 * cfg.orb.nlevels + 64,
+                          cfg.adaptive.max_total_keypoints + 64)
 
     def close(self):
         if getattr(self, "h", None):
@@ -154,6 +159,29 @@ class Odometry:
         n = C.c_int(0)
         check(self.lib.odo_debug_octree(self.h, i, level, ptr(out), cap, C.byref(n)))
         return out[:n.value]
+
+    def adaptive_state(self, i: int = None):
+        """(FAST threshold per grid cell used for frame i of the last batch or
+        None, current per-cell DetectorAdjuster thresholds)."""
+        nc = self.cfg.adaptive.grid_rows * self.cfg.adaptive.grid_cols
+        t = np.zeros(nc, np.int32)
+        th = np.zeros(nc, np.float64)
+        rc = self.lib.odo_debug_adaptive(self.h, -1 if i is None else i, None if i is None else ptr(t), ptr(th))
+        if rc < 0:
+            check(rc)
+        return (None if i is None else t), th
+
+    def set_adaptive_thresholds(self, th):
+        th = np.ascontiguousarray(th, np.float64)
+        check(self.lib.odo_set_adaptive_thresholds(self.h, ptr(th), th.size))
+
+    def select(self, keys, nth: int, mode: int = 0):
+        """GPU std::nth_element (mode 0) / retainBest (mode 1) on packed keys."""
+        keys = np.ascontiguousarray(keys, np.uint32)
+        out = np.zeros_like(keys)
+        n = C.c_int(0)
+        check(self.lib.odo_debug_select(self.h, ptr(keys), keys.size, nth, mode, ptr(out), C.byref(n)))
+        return out, n.value
 
     def timings(self):
         ms = np.zeros(16, np.float32)

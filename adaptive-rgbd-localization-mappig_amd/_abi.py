@@ -41,6 +41,14 @@ class RansacParams(C.Structure):
                 ("sample_size", C.c_int32), ("check_depth", C.c_int32)]
 
 
+class AdaptiveParams(C.Structure):
+    _fields_ = [("grid_rows", C.c_int32), ("grid_cols", C.c_int32), ("edge_threshold", C.c_int32),
+                ("max_total_keypoints", C.c_int32), ("cell_min", C.c_int32), ("cell_max", C.c_int32),
+                ("escape_iters", C.c_int32), ("init_thresh", C.c_double), ("min_thresh", C.c_double),
+                ("max_thresh", C.c_double), ("increase_factor", C.c_double), ("decrease_factor", C.c_double),
+                ("retain_best", C.c_int32)]
+
+
 class Rng(C.Structure):
     _fields_ = [("state", C.c_int32 * 31), ("fpos", C.c_int32), ("rpos", C.c_int32)]
 
@@ -55,7 +63,12 @@ class PairResult(C.Structure):
 class Config(C.Structure):
     _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("max_batch", C.c_int32),
                 ("orb", OrbParams), ("calib", Calib), ("nn_ratio", C.c_float),
-                ("ransac", RansacParams), ("seed", C.c_uint32)]
+                ("ransac", RansacParams), ("seed", C.c_uint32), ("detector", C.c_int32),
+                ("adaptive", AdaptiveParams)]
+
+
+DETECTOR_ORB_SLAM2 = 0       # include/odo.h ODO_DETECTOR_ORB_SLAM2
+DETECTOR_ADAPTIVE_FAST = 1   # include/odo.h ODO_DETECTOR_ADAPTIVE_FAST
 
 
 KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
@@ -96,6 +109,9 @@ SIGNATURES = {
     "odo_kernel_timing": (C.c_int, [P, P, P]),
     "odo_debug_blur": (C.c_int, [P, C.c_int, P, C.c_size_t]),
     "odo_last_timings": (C.c_int, [P, P, C.c_int, P]),
+    "odo_debug_adaptive": (C.c_int, [P, C.c_int, P, P]),
+    "odo_set_adaptive_thresholds": (C.c_int, [P, P, C.c_int]),
+    "odo_debug_select": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, P, P]),
 }
 
 _lib = None

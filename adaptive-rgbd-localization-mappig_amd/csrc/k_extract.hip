@@ -1044,45 +1044,9 @@ __global__ void __launch_bounds__(256) k_finalize(const uint8_t* __restrict__ py
         kp->response = resp;
         kp->octave = lvl;
         kp->class_id = -1;
-        // UndistortKeyPoints: cv::undistortPoints, 5 iterations in double
-        float uu = px, vv = py;
-        float ux = uu, uy = vv;
-        if (cal.k1 != 0.0f) {
-            const double fx = cal.fx, fy = cal.fy, cx = cal.cx, cy = cal.cy;
-            const double ifx = 1. / fx, ify = 1. / fy;
-            const double k0 = cal.k1, k1 = cal.k2, k2 = cal.p1, k3 = cal.p2, k4 = cal.k3;
-            double x = uu, y = vv;
-            x = (x - cx) * ifx;
-            y = (y - cy) * ify;
-            const double x0 = x, y0 = y;
-            for (int j = 0; j < 5; j++) {
-                double r2 = x * x + y * y;
-                double icdist = 1 / (1 + ((k4 * r2 + k1) * r2 + k0) * r2);
-                double deltaX = 2 * k2 * x * y + k3 * (r2 + 2 * x * x);
-                double deltaY = k2 * (r2 + 2 * y * y) + 2 * k3 * x * y;
-                x = (x0 - deltaX) * icdist;
-                y = (y0 - deltaY) * icdist;
-            }
-            ux = (float)(fx * x + cx);
-            uy = (float)(fy * y + cy);
-        }
-        float* ku = kun + ((size_t)f * kp_cap + o) * 2;
-        ku[0] = ux;
-        ku[1] = uy;
-        float* p3 = xyz + ((size_t)f * kp_cap + o) * 3;
-        float urv = -1.f, X = 0.f, Y = 0.f, Z = 0.f;
-        const uint16_t d16 = depth[(size_t)f * depth_stride + (size_t)((int)vv) * img_w + (int)uu];
-        const float z = (float)d16 * cal.depth_factor + 0.0f;
-        if (z > 0) {
-            urv = ux - cal.mbf / z;
-            X = (ux - cal.cx) * z * cal.invfx;
-            Y = (uy - cal.cy) * z * cal.invfy;
-            Z = z;
-        }
-        p3[0] = X;
-        p3[1] = Y;
-        p3[2] = Z;
-        ur[(size_t)f * kp_cap + o] = urv;
+        // UndistortKeyPoints + depth back-projection (frame.cpp:139-164, 286-313)
+        kp_geometry(px, py, cal, depth + (size_t)f * depth_stride, img_w, kun + ((size_t)f * kp_cap + o) * 2,
+                    xyz + ((size_t)f * kp_cap + o) * 3, ur + (size_t)f * kp_cap + o);
     }
 }
 

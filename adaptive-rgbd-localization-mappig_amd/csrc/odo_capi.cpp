@@ -147,6 +147,21 @@ struct odo_ctx {
     // ODO_SKIP (measurement only; results are invalid when set): bit 0 skips
     // the PnP launches, bit 1 RANSAC part 2, bit 2 every pair stage, bit 3 kNN-2
     int skip = 0;
+    // ADAPTIVE grid extractor (ODO_DETECTOR_ADAPTIVE_FAST): cell / band
+    // tables and per-batch scratch (extraction stream only), plus the
+    // persistent per-cell DetectorAdjuster thresholds
+    bool adaptive = false;
+    int ad_ncells = 0, ad_nbands = 0, ad_mpc = 0;
+    std::vector<AdCell> adc_h;
+    std::vector<AdBand> adb_h;
+    AdCell* adc = nullptr;
+    AdBand* adb = nullptr;
+    uint8_t* smap = nullptr;
+    size_t smap_stride = 0, acand_stride = 0, abig_stride = 0;
+    uint32_t *acand = nullptr, *abig = nullptr, *acell = nullptr, *akp = nullptr;
+    int *aband_cnt = nullptr, *ahist = nullptr, *atsel = nullptr, *ansel = nullptr, *acell_cnt = nullptr;
+    double* athresh = nullptr;
+    float a_cos = 1.f, a_sin = 0.f;
     // Hamming-match kernel timing (odo_set_timing mode 2): an event pair
     // around the kNN-2 launch of every batch, read back and summed lazily
     static constexpr int KT_RING = 256;
@@ -193,10 +208,15 @@ static void free_ctx(odo_ctx* c) {
     if (!c) return;
     void* ptrs[] = {c->lv, c->cells, c->rx, c->ry, c->pyr, c->blur, c->cand, c->cand_cnt, c->keys, c->knode, c->kquad,
                     c->okp, c->ocnt, c->kps, c->desc, c->kun, c->xyz, c->ur, c->nkp, c->bgr_in, c->depth_in,
-                    c->knn_idx[0], c->knn_dist[0], c->knn_idx[1], c->knn_dist[1], c->sort_scratch, c->latch,
-                    c->rscr[0], c->rscr[1], c->masks};
+                    c->sort_scratch, c->latch, c->masks, c->adc, c->adb, c->smap, c->acand, c->abig, c->acell,
+                    c->akp, c->aband_cnt, c->ahist, c->atsel, c->ansel, c->acell_cnt, c->athresh};
     for (void* p : ptrs)
         if (p) hipFree(p);
+    for (int i = 0; i < NSETS; i++) {
+        void* pp[] = {c->knn_idx[i], c->knn_dist[i], c->rscr[i]};
+        for (void* q : pp)
+            if (q) hipFree(q);
+    }
     for (auto& P : c->pb) {
         void* pp[] = {P.matches, P.n_matches, P.n_good, P.pair_valid, P.good, P.f2_src, P.best_mask, P.res, P.T12,
                       P.edges, P.pnp_mask, P.pair_phase};
@@ -223,6 +243,73 @@ static void free_ctx(odo_ctx* c) {
     }
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
+}
+
+// ADAPTIVE grid (videogridadaptedfeaturedetector.cpp:62-71): cell ROIs,
+// FAST detection regions (ROI minus 3 px) and AD_BH-row bands with survivor
+// capacities (strict 3x3 maxima are never 8-adjacent: <= ceil(r/2)ceil(c/2)).
+static int build_adaptive_geometry(odo_ctx* c) {
+    const odo_adaptive_params& P = c->cfg.adaptive;
+    const int W = c->W, H = c->H, R = P.grid_rows, C = P.grid_cols, E = P.edge_threshold;
+    if (R <= 0 || C <= 0 || R * C > 64 || E < 0 || P.escape_iters < 1 || P.max_total_keypoints < R * C ||
+        !(P.min_thresh <= P.max_thresh))
+        return fail(ODO_ERR_ARG, "invalid adaptive params");
+    c->ad_ncells = R * C;
+    c->ad_mpc = P.max_total_keypoints / (R * C);
+    c->adc_h.clear();
+    c->adb_h.clear();
+    int off = 0, maxcap = 0;
+    for (int i = 0; i < R; i++)
+        for (int j = 0; j < C; j++) {
+            AdCell A{};
+            A.rs = std::max((i * H) / R - E, 0);
+            A.re = std::min(H, ((i + 1) * H) / R + E);
+            A.cs = std::max((j * W) / C - E, 0);
+            A.ce = std::min(W, ((j + 1) * W) / C + E);
+            A.r0 = A.rs + 3;
+            A.r1 = std::max(A.r0, A.re - 3);
+            A.c0 = A.cs + 3;
+            A.c1 = std::max(A.c0, A.ce - 3);
+            if (A.c1 - A.c0 > AD_MAXW) return fail(ODO_ERR_ARG, "adaptive cell wider than AD_MAXW");
+            A.band0 = (int)c->adb_h.size();
+            A.cand_cap = 0;
+            const int cw2 = (A.c1 - A.c0 + 1) / 2;
+            for (int y0 = A.r0; y0 < A.r1; y0 += AD_BH) {
+                AdBand B{(int)c->adc_h.size(), y0, std::min(y0 + AD_BH, A.r1), off};
+                const int cap = ((B.y1 - B.y0 + 1) / 2) * cw2;
+                off += (cap + 3) & ~3;
+                A.cand_cap += cap;
+                c->adb_h.push_back(B);
+            }
+            A.band1 = (int)c->adb_h.size();
+            maxcap = std::max(maxcap, A.cand_cap);
+            c->adc_h.push_back(A);
+        }
+    c->ad_nbands = (int)c->adb_h.size();
+    c->acand_stride = (size_t)std::max(off, 4);
+    c->abig_stride = (size_t)3 * std::max(maxcap, 1);
+    const int need = c->ad_ncells * c->ad_mpc;
+    if (adapt_assemble_lds_bytes(c->ad_ncells, c->ad_mpc) > 160 * 1024)
+        return fail(ODO_ERR_ARG, "adaptive grid keeps too many keypoints for one workgroup");
+    c->kp_cap = std::max(c->kp_cap, (need + 63) & ~63);
+    // ORB's rBRIEF at the FAST keypoints' angle -1 (orb.cpp computeOrbDescriptors)
+    const float ang = -1.f * (float)(M_PI / 180.f);
+    c->a_cos = (float)cos((double)ang);
+    c->a_sin = (float)sin((double)ang);
+    int e;
+    if ((e = dalloc(&c->adc, c->adc_h.size()))) return e;
+    if ((e = dalloc(&c->adb, std::max<size_t>(c->adb_h.size(), 1)))) return e;
+    HIPCHK(hipMemcpy(c->adc, c->adc_h.data(), c->adc_h.size() * sizeof(AdCell), hipMemcpyHostToDevice));
+    if (!c->adb_h.empty())
+        HIPCHK(hipMemcpy(c->adb, c->adb_h.data(), c->adb_h.size() * sizeof(AdBand), hipMemcpyHostToDevice));
+    return ODO_OK;
+}
+
+static int reset_adaptive(odo_ctx* c) {
+    if (!c->adaptive) return ODO_OK;
+    std::vector<double> t(c->ad_ncells, c->cfg.adaptive.init_thresh);
+    HIPCHK(hipMemcpy(c->athresh, t.data(), t.size() * sizeof(double), hipMemcpyHostToDevice));
+    return ODO_OK;
 }
 
 static int build_geometry(odo_ctx* c) {
@@ -322,6 +409,10 @@ static int build_geometry(odo_ctx* c) {
     if (octree_lds_bytes(nc) > 160 * 1024) return fail(ODO_ERR_ARG, "octree node capacity exceeds LDS");
     c->kp_cap = ((p.nfeatures + 4 * p.nlevels + 8) + 63) & ~63;
     if (c->kp_cap > 8192) return fail(ODO_ERR_ARG, "nfeatures too large (kp cap 8192)");
+    if (c->adaptive) {
+        int e;
+        if ((e = build_adaptive_geometry(c))) return e;
+    }
     c->match_cap = c->kp_cap;
     c->mask_words = (c->match_cap + 31) / 32;
     // resize tables (cv::resize generic INTER_LINEAR, App. A.2)
@@ -451,6 +542,22 @@ static int alloc_buffers(odo_ctx* c) {
         if ((e = dalloc((uint8_t**)&c->rscr[i], ransac_scratch_bytes((int)B, c->match_cap, c->mask_words, c->rcfg))))
             return e;
 
+    if (c->adaptive) {
+        const size_t nc = (size_t)c->ad_ncells;
+        c->smap_stride = (size_t)c->lv_h[0].pitch * c->H;
+        if ((e = dalloc(&c->smap, B * c->smap_stride))) return e;
+        if ((e = dalloc(&c->acand, B * c->acand_stride))) return e;
+        if ((e = dalloc(&c->aband_cnt, B * std::max(c->ad_nbands, 1)))) return e;
+        if ((e = dalloc(&c->ahist, B * nc * 256))) return e;
+        if ((e = dalloc(&c->atsel, B * nc))) return e;
+        if ((e = dalloc(&c->ansel, B * nc))) return e;
+        if ((e = dalloc(&c->abig, B * nc * c->abig_stride))) return e;
+        if ((e = dalloc(&c->acell, B * nc * c->ad_mpc))) return e;
+        if ((e = dalloc(&c->acell_cnt, B * nc))) return e;
+        if ((e = dalloc(&c->akp, B * c->kp_cap))) return e;
+        if ((e = dalloc(&c->athresh, nc))) return e;
+        if ((e = reset_adaptive(c))) return e;
+    }
     HIPCHK(hipMemset(c->nkp, 0, S * sizeof(int)));
     const double nan = std::nan("");
     HIPCHK(hipMemcpy(c->latch, &nan, sizeof(double), hipMemcpyHostToDevice));
@@ -472,6 +579,12 @@ void odo_default_config(odo_config* cfg, int width, int height, int max_batch) {
     cfg->nn_ratio = 0.9f;
     cfg->ransac = odo_ransac_params{200, 20, 3.0f, 4, 1};
     cfg->seed = 0x5EED0000u;
+    cfg->detector = ODO_DETECTOR_ORB_SLAM2;
+    // Extractor::CreateAdaptiveDetector (extractor.cpp:55-77): minFeatures 600,
+    // maxFeatures = 600 * 1.7 = 1020, 3x3 grid, gridMin = round(600/9.f) = 67,
+    // gridMax = round(1020/9.f) = 113, 5 iterations, edge 31; FAST adjuster
+    // (20, 2, 10000, 1.3, 0.7); Extract's retainBest(nFeatures = 1000)
+    cfg->adaptive = odo_adaptive_params{3, 3, 31, 1020, 67, 113, 5, 20.0, 2.0, 10000.0, 1.3, 0.7, 1000};
 }
 
 odo_ctx* odo_create(const odo_config* cfg, int device) {
@@ -498,6 +611,12 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
     c->H = cfg->height;
     c->maxb = cfg->max_batch;
     c->slots = cfg->max_batch + 1;
+    if (cfg->detector != ODO_DETECTOR_ORB_SLAM2 && cfg->detector != ODO_DETECTOR_ADAPTIVE_FAST) {
+        fail(ODO_ERR_ARG, "unsupported detector");  // extractor.cpp:26-27 terminates here
+        delete c;
+        return nullptr;
+    }
+    c->adaptive = cfg->detector == ODO_DETECTOR_ADAPTIVE_FAST;
     // ODO_SERIAL_STREAMS=1 (profiling): every stage on one stream, no overlap,
     // so per-kernel times are free of cross-stream contention
     const char* ser = getenv("ODO_SERIAL_STREAMS");
@@ -540,6 +659,7 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
         return nullptr;
     }
     upload_extract_constants();
+    upload_adaptive_constants();
     const odo_calib& k = cfg->calib;
     c->cal = FrameCalib{k.fx, k.fy, k.cx, k.cy, k.k1, k.k2, k.p1, k.p2, k.k3, k.depth_factor, k.mbf,
                         1.0f / k.fx, 1.0f / k.fy};
@@ -560,7 +680,7 @@ int odo_reset(odo_ctx* c) {
     c->pair_counter = 0;
     const double nan = std::nan("");
     HIPCHK(hipMemcpy(c->latch, &nan, sizeof(double), hipMemcpyHostToDevice));
-    return ODO_OK;
+    return reset_adaptive(c);
 }
 
 int odo_set_latch(odo_ctx* c, double cov) {
@@ -627,7 +747,45 @@ int odo_synchronize(odo_ctx* c) {
     return sync_all(c);
 }
 
+// Extractor(FAST, ORB, ADAPTIVE) for frames slot0.. of `set` (k_adaptive.hip):
+// threshold-free S map -> band survivors + S histograms -> the per-cell
+// threshold chain over the batch in frame order -> keepStrongest ->
+// retainBest + border filter -> rBRIEF / undistort / depth.
+static int run_extract_adaptive(odo_ctx* c, int set, const uint8_t* d_bgr, const uint16_t* d_depth, int n,
+                                int slot0) {
+    hipStream_t st = c->stream;
+    const size_t P = c->pyr_size;
+    const size_t slot = fbase(c, set) + slot0;
+    const LevelDesc& L0 = c->lv_h[0];
+    uint8_t* pyr = c->pyr + slot * P;
+    const size_t nc = (size_t)c->ad_ncells;
+    if (d_bgr) launch_gray(st, d_bgr, pyr, c->W, c->H, L0.pitch, (size_t)c->W * c->H * 3, P, n);
+    tmark(c, 1, st);
+    launch_adapt_smap(st, pyr, P, c->W, c->H, L0.pitch, c->smap, c->smap_stride, n);
+    HIPCHK(hipMemsetAsync(c->ahist, 0, (size_t)n * nc * 256 * sizeof(int), st));
+    if (c->ad_nbands > 0)
+        launch_adapt_cand(st, c->smap, c->smap_stride, L0.pitch, c->adb, c->ad_nbands, c->adc, c->ad_ncells, c->acand,
+                          c->acand_stride, c->aband_cnt, c->ahist, n);
+    tmark(c, 2, st);
+    launch_adapt_chain(st, c->ahist, c->ad_ncells, n, c->cfg.adaptive, c->athresh, c->atsel, c->ansel);
+    launch_adapt_select(st, c->acand, c->acand_stride, c->aband_cnt, c->ad_nbands, c->adb, c->adc, c->ad_ncells,
+                        c->atsel, c->ansel, c->ad_mpc, c->abig, c->abig_stride, c->acell, c->acell_cnt, n);
+    launch_adapt_assemble(st, c->acell, c->acell_cnt, c->ad_ncells, c->ad_mpc, c->cfg.adaptive.retain_best, c->W,
+                          c->H, c->akp, c->kp_cap, c->nkp + slot, c->kp_cap, n);
+    tmark(c, 3, st);
+    launch_blur(st, pyr, c->blur + slot * P, P, c->lv, c->lv_h.data(), 1, n);
+    tmark(c, 4, st);
+    launch_adapt_finalize(st, c->blur + slot * P, P, L0.pitch, c->akp, c->kp_cap, c->nkp + slot, c->a_cos, c->a_sin,
+                          d_depth, (size_t)c->W * c->H, c->W, c->cal, c->kps + slot * c->kp_cap,
+                          c->desc + slot * c->kp_cap * 32, c->kun + slot * c->kp_cap * 2, c->xyz + slot * c->kp_cap * 3,
+                          c->ur + slot * c->kp_cap, c->kp_cap, n);
+    tmark(c, 5, st);
+    HIPCHK(hipGetLastError());
+    return ODO_OK;
+}
+
 static int run_extract(odo_ctx* c, int set, const uint8_t* d_bgr, const uint16_t* d_depth, int n, int slot0) {
+    if (c->adaptive) return run_extract_adaptive(c, set, d_bgr, d_depth, n, slot0);
     hipStream_t st = c->stream;
     const size_t P = c->pyr_size;
     const size_t slot = fbase(c, set) + slot0;
@@ -898,6 +1056,58 @@ int odo_debug_blur(odo_ctx* c, int i, uint8_t* out, size_t cap) {
     int e;
     if ((e = sync_all(c))) return e;
     return copy_levels(c, c->blur + (fbase(c, c->view_set) + i + 1) * c->pyr_size, out, cap);
+}
+
+int odo_debug_adaptive(odo_ctx* c, int i, int32_t* t_used, double* thresh) {
+    if (!c) return fail(ODO_ERR_ARG, "null ctx");
+    if (!c->adaptive) return fail(ODO_ERR_STATE, "context is not in ADAPTIVE mode");
+    if (t_used && (i < 0 || i >= c->last_n)) return fail(ODO_ERR_ARG, "bad frame index");
+    int e;
+    if ((e = sync_all(c))) return e;
+    if (t_used)
+        HIPCHK(hipMemcpy(t_used, c->atsel + (size_t)i * c->ad_ncells, c->ad_ncells * sizeof(int),
+                         hipMemcpyDeviceToHost));
+    if (thresh) HIPCHK(hipMemcpy(thresh, c->athresh, c->ad_ncells * sizeof(double), hipMemcpyDeviceToHost));
+    return c->ad_ncells;
+}
+
+int odo_set_adaptive_thresholds(odo_ctx* c, const double* thresh, int n) {
+    if (!c || !thresh) return fail(ODO_ERR_ARG, "bad args");
+    if (!c->adaptive) return fail(ODO_ERR_STATE, "context is not in ADAPTIVE mode");
+    if (n != c->ad_ncells) return fail(ODO_ERR_ARG, "threshold count != grid cells");
+    int e;
+    if ((e = sync_all(c))) return e;
+    HIPCHK(hipMemcpy(c->athresh, thresh, n * sizeof(double), hipMemcpyHostToDevice));
+    return ODO_OK;
+}
+
+int odo_debug_select(odo_ctx* c, const uint32_t* in, int n, int nth, int mode, uint32_t* out, int* n_out) {
+    if (!c || n < 0 || (n && (!in || !out)) || !n_out || nth < 0 || (mode != 0 && mode != 1) || (mode == 1 && nth < 1))
+        return fail(ODO_ERR_ARG, "bad select args");
+    int e;
+    if ((e = sync_all(c))) return e;
+    if (n == 0) {
+        *n_out = 0;
+        return ODO_OK;
+    }
+    if (nth > n) nth = n;
+    void* d = nullptr;
+    const size_t bytes = (size_t)n * 12 + 16;
+    HIPCHK(hipMalloc(&d, bytes));
+    uint32_t* A = (uint32_t*)d;
+    int* posL = (int*)(A + n);
+    int* posR = posL + n;
+    int* dn = posR + n;
+    hipError_t er = hipMemcpy(A, in, (size_t)n * 4, hipMemcpyHostToDevice);
+    if (er == hipSuccess) {
+        launch_adapt_select_dbg(c->stream, A, n, nth, mode, posL, posR, dn);
+        er = hipStreamSynchronize(c->stream);
+    }
+    if (er == hipSuccess) er = hipMemcpy(out, A, (size_t)n * 4, hipMemcpyDeviceToHost);
+    if (er == hipSuccess) er = hipMemcpy(n_out, dn, sizeof(int), hipMemcpyDeviceToHost);
+    hipFree(d);
+    if (er != hipSuccess) return fail(ODO_ERR_DEVICE, hipGetErrorString(er));
+    return ODO_OK;
 }
 
 int odo_debug_sort(odo_ctx* c, const odo_dmatch* in, int n, odo_dmatch* out) {

@@ -50,6 +50,71 @@ struct FrameCalib {
     float invfx, invfy;
 };
 
+// Frame::ExtractFeatures tail for one keypoint (frame.cpp:139-164, 286-313):
+// cv::undistortPoints (5 iterations in double; skipped when k1 == 0,
+// frame.cpp:288), then the depth at the truncated distorted pixel and the
+// back-projection of the undistorted point.
+__device__ inline void kp_geometry(float uu, float vv, const FrameCalib& cal, const uint16_t* depth, int img_w,
+                                   float* ku, float* p3, float* urp) {
+    float ux = uu, uy = vv;
+    if (cal.k1 != 0.0f) {
+        const double fx = cal.fx, fy = cal.fy, cx = cal.cx, cy = cal.cy;
+        const double ifx = 1. / fx, ify = 1. / fy;
+        const double k0 = cal.k1, k1 = cal.k2, k2 = cal.p1, k3 = cal.p2, k4 = cal.k3;
+        double x = uu, y = vv;
+        x = (x - cx) * ifx;
+        y = (y - cy) * ify;
+        const double x0 = x, y0 = y;
+        for (int j = 0; j < 5; j++) {
+            double r2 = x * x + y * y;
+            double icdist = 1 / (1 + ((k4 * r2 + k1) * r2 + k0) * r2);
+            double deltaX = 2 * k2 * x * y + k3 * (r2 + 2 * x * x);
+            double deltaY = k2 * (r2 + 2 * y * y) + 2 * k3 * x * y;
+            x = (x0 - deltaX) * icdist;
+            y = (y0 - deltaY) * icdist;
+        }
+        ux = (float)(fx * x + cx);
+        uy = (float)(fy * y + cy);
+    }
+    ku[0] = ux;
+    ku[1] = uy;
+    float urv = -1.f, X = 0.f, Y = 0.f, Z = 0.f;
+    const uint16_t d16 = depth[(size_t)((int)vv) * img_w + (int)uu];
+    const float z = (float)d16 * cal.depth_factor + 0.0f;
+    if (z > 0) {
+        urv = ux - cal.mbf / z;
+        X = (ux - cal.cx) * z * cal.invfx;
+        Y = (uy - cal.cy) * z * cal.invfy;
+        Z = z;
+    }
+    p3[0] = X;
+    p3[1] = Y;
+    p3[2] = Z;
+    *urp = urv;
+}
+
+// ---- ADAPTIVE grid extractor (k_adaptive.hip)
+#define AD_BH 16          // rows per candidate band
+#define AD_MAXW 1024      // widest cell detection region (LDS staging)
+#define AD_SEL_LDS 4096   // survivors a cell selects in LDS (more: global scratch)
+using AdParams = odo_adaptive_params;
+
+// One grid cell of VideoGridAdaptedFeatureDetector (videogridadaptedfeature
+// detector.cpp:62-71): ROI [rs,re) x [cs,ce); FAST's detection region is the
+// ROI minus 3 pixels on every side: rows [r0,r1), cols [c0,c1).
+struct AdCell {
+    int rs, re, cs, ce;
+    int r0, r1, c0, c1;
+    int band0, band1;  // its bands in the band table
+    int cand_cap;      // survivor capacity over all its bands
+    int pad;
+};
+// AD_BH rows [y0,y1) of one cell's detection region; its survivors land at
+// cand_off of the frame's candidate buffer
+struct AdBand {
+    int cell, y0, y1, cand_off;
+};
+
 // RANSAC per-pair constants.
 struct RansacCfg {
     int iterations;
@@ -110,5 +175,28 @@ void launch_pnp(hipStream_t st, const int32_t* f2_src, const float* xyz, const f
                 const int* n_matches, int min_matches, void* edges, odo_pair_result* res, uint8_t* inlier_mask,
                 int npairs, const int* sel = nullptr, int sel_val = 0);
 void launch_kabsch(hipStream_t st, const float* A, const float* B, int n, float* T);
+void upload_adaptive_constants();
+void launch_adapt_smap(hipStream_t st, const uint8_t* pyr, size_t pyr_stride, int w, int h, int pitch, uint8_t* smap,
+                       size_t smap_stride, int nframes);
+void launch_adapt_cand(hipStream_t st, const uint8_t* smap, size_t smap_stride, int pitch, const AdBand* bands,
+                       int nbands, const AdCell* cells, int ncells, uint32_t* cand, size_t cand_stride, int* band_cnt,
+                       int* hist, int nframes);
+void launch_adapt_chain(hipStream_t st, const int* hist, int ncells, int nframes, AdParams P, double* thresh,
+                        int* tsel, int* nsel);
+size_t adapt_select_lds_bytes();
+void launch_adapt_select(hipStream_t st, const uint32_t* cand, size_t cand_stride, const int* band_cnt, int nbands,
+                         const AdBand* bands, const AdCell* cells, int ncells, const int* tsel, const int* nsel,
+                         int max_per_cell, uint32_t* big, size_t big_stride, uint32_t* cell_out, int* cell_cnt,
+                         int nframes);
+size_t adapt_assemble_lds_bytes(int ncells, int max_per_cell);
+void launch_adapt_assemble(hipStream_t st, const uint32_t* cell_out, const int* cell_cnt, int ncells, int max_per_cell,
+                           int retain, int w, int h, uint32_t* akp, int akp_stride, int* nkp, int kp_cap,
+                           int nframes);
+void launch_adapt_finalize(hipStream_t st, const uint8_t* blur, size_t pyr_stride, int pitch, const uint32_t* akp,
+                           int akp_stride, const int* nkp, float ca, float sb, const uint16_t* depth,
+                           size_t depth_stride, int img_w, FrameCalib cal, orb_kp* kps, uint8_t* desc, float* kun,
+                           float* xyz, float* ur, int kp_cap, int nframes);
+void launch_adapt_select_dbg(hipStream_t st, uint32_t* a, int n, int nth, int mode, int* posL, int* posR,
+                             int* n_out);
 
 }  // namespace odo

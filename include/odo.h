@@ -29,6 +29,10 @@ extern "C" {
 #define ODO_ERR_CAPACITY (-3)
 #define ODO_ERR_STATE (-4)
 
+/* odo_config.detector: Extractor(detector, descriptor, mode) (extractor.cpp:14) */
+#define ODO_DETECTOR_ORB_SLAM2 0      /* ORB_SLAM2 / ORB_SLAM2 / NORMAL (main.cpp:19-21, the reference default) */
+#define ODO_DETECTOR_ADAPTIVE_FAST 1  /* FAST / ORB / ADAPTIVE: 3x3 grid-adapted FAST + cv::ORB descriptor */
+
 typedef struct odo_config {
     int32_t width, height;      /* frame size (all frames of a context share it) */
     int32_t max_batch;          /* frames per odo_track_batch() call */
@@ -37,6 +41,8 @@ typedef struct odo_config {
     float nn_ratio;             /* Matcher(0.9f) tracking.cpp:197 */
     odo_ransac_params ransac;   /* Ransac(200,20,3.0,4) odometry.cpp:28 */
     uint32_t seed;              /* per-pair RNG seed base (replaces srand(clock()), main.cpp:27) */
+    int32_t detector;           /* ODO_DETECTOR_* */
+    odo_adaptive_params adaptive; /* ADAPTIVE grid (Extractor::CreateAdaptiveDetector, extractor.cpp:55-77) */
 } odo_config;
 
 typedef struct odo_ctx odo_ctx;
@@ -45,12 +51,13 @@ typedef struct odo_ctx odo_ctx;
 void odo_default_config(odo_config* cfg, int width, int height, int max_batch);
 
 /* Context: owns the HIP stream, HBM scratch and the cross-frame state the
- * reference keeps in globals (previous frame, DepthCovariance latch). */
+ * reference keeps in globals or detector objects (previous frame,
+ * DepthCovariance latch, the ADAPTIVE grid's per-cell FAST thresholds). */
 odo_ctx* odo_create(const odo_config* cfg, int device);
 void odo_destroy(odo_ctx* ctx);
 const char* odo_last_error(void);
 void* odo_stream(odo_ctx* ctx);               /* hipStream_t, for callers that share streams */
-int odo_reset(odo_ctx* ctx);                  /* forget previous frame and latch */
+int odo_reset(odo_ctx* ctx);                  /* forget previous frame, latch, adaptive thresholds */
 int odo_set_latch(odo_ctx* ctx, double cov);  /* NaN = unlatched */
 double odo_get_latch(odo_ctx* ctx);
 
@@ -88,7 +95,8 @@ int odo_get_pair(odo_ctx* ctx, int i, odo_dmatch* matches, int match_cap, int* n
 
 /* Extractor::Extract + Frame::ExtractFeatures (extractor.cpp:39, frame.cpp:135):
  * BGR8 (or gray when channels==1) + optional depth16 -> keypoints,
- * 32-byte descriptors, undistorted points, camera xyz and right coordinate. */
+ * 32-byte descriptors, undistorted points, camera xyz and right coordinate.
+ * With ODO_DETECTOR_ADAPTIVE_FAST every call advances the cell thresholds. */
 int odo_extract(odo_ctx* ctx, const uint8_t* img, int channels, const uint16_t* depth,
                 orb_kp* kps, uint8_t* desc, float* kps_un, float* xyz, float* u_right, int cap,
                 int* n);
@@ -127,6 +135,19 @@ int odo_debug_blur(odo_ctx* ctx, int i, uint8_t* out, size_t cap);
  * stage runs it on the GPU (workgroup-parallel introsort): in -> out sorted by
  * distance in libstdc++'s exact (unstable) order; distances must be >= 0. */
 int odo_debug_sort(odo_ctx* ctx, const odo_dmatch* in, int n, odo_dmatch* out);
+/* ADAPTIVE detector state. The per-cell DetectorAdjuster thresholds persist
+ * across frames and calls (detectoradjuster.cpp:52-65, App. B.13); they
+ * advance with every extracted frame, in frame order within a batch.
+ * odo_debug_adaptive: FAST threshold each cell used for frame i of the last
+ * batch (t_used, grid cells; NULL skips) and the current thresholds (thresh;
+ * NULL skips). Returns the number of grid cells (< 0 on error). */
+int odo_debug_adaptive(odo_ctx* ctx, int i, int32_t* t_used, double* thresh);
+int odo_set_adaptive_thresholds(odo_ctx* ctx, const double* thresh, int n);
+/* std::nth_element(a, a + nth, a + n) by score (mode 0; keepStrongest,
+ * videogridadaptedfeaturedetector.cpp:24-31) or KeyPointsFilter::retainBest
+ * (mode 1) exactly as the ADAPTIVE stages run them on the GPU, over packed
+ * keys (score << 24 | y << 12 | x). out: n keys, *n_out kept. */
+int odo_debug_select(odo_ctx* ctx, const uint32_t* in, int n, int nth, int mode, uint32_t* out, int* n_out);
 /* Timing (off by default; mode 0). Mode 1: odo_track_batch records HIP events
  * between stages and odo_last_timings reports the last batch (ms); these
  * events serialise the streams they sit on. Mode 2: an event pair brackets the

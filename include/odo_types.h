@@ -61,7 +61,8 @@ typedef struct odo_ransac_params {
 /* Grid-adapted detector (Extractor::ADAPTIVE with FAST inner detector),
  * extractor.cpp:52-77: DetectorAdjuster(FAST, 20, 2, 10000, 1.3, 0.7),
  * VideoDynamicAdaptedFeatureDetector(gridMin=67, gridMax=113, iters=5),
- * VideoGridAdaptedFeatureDetector(maxTotal=1020, 3x3, edge=31). */
+ * VideoGridAdaptedFeatureDetector(maxTotal=1020, 3x3, edge=31), then
+ * retainBest(nFeatures=1000) and cv::ORB::compute (extractor.cpp:39-50). */
 typedef struct odo_adaptive_params {
     int32_t grid_rows, grid_cols;
     int32_t edge_threshold;
