@@ -1185,8 +1185,12 @@ int odo_debug_octree(odo_ctx* c, int i, int level, orb_kp* out, int cap, int* n)
 }
 
 int odo_last_timings(odo_ctx* c, float* ms, int cap, const char** names) {
-    static const char* kNames[] = {"gray+pyramid", "fast", "octree", "blur", "finalize", "knn2", "match+sort",
-                                   "ransac", "pnp"};
+    static const char* kNamesOrb[] = {"gray+pyramid", "fast", "octree", "blur", "finalize", "knn2", "match+sort",
+                                      "ransac", "pnp"};
+    // ADAPTIVE marks: gray | S map + band survivors | chain + select + assemble | blur L0 | finalize
+    static const char* kNamesAd[] = {"gray", "smap+cand", "chain+select", "blur", "finalize", "knn2", "match+sort",
+                                     "ransac", "pnp"};
+    const char* const* kNames = c && c->adaptive ? kNamesAd : kNamesOrb;
     // stage i spans events (a[i], b[i]): extraction stream 0..5,10; pair stream 6..9
     static const int a[9] = {0, 1, 2, 3, 4, 5, 6, 7, 8}, b[9] = {1, 2, 3, 4, 5, 10, 7, 8, 9};
     if (!c) return fail(ODO_ERR_ARG, "null ctx");

@@ -110,7 +110,7 @@ def stage_model(stage, ms, B, w, h, nkp_mean):
     return "hbm", byts / (ms * 1e-3) / 1e9, HBM_PEAK_GBS, "GB/s", byts
 
 
-def cpu_baseline(bgr, dep, nfeat, iters, n_frames):
+def cpu_baseline(bgr, dep, nfeat, iters, n_frames, adaptive=False):
     """The C++ oracle (single thread) on the first n_frames frames of the same sequence."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
@@ -118,11 +118,15 @@ def cpu_baseline(bgr, dep, nfeat, iters, n_frames):
     p = O.orb_params(nfeat)
     rp = O.ransac_params(iters)
     pkg = load_pkg()
+    ex = O.AdaptiveExtractor() if adaptive else None
     t0 = time.perf_counter()
     prev = None
     latch = float("nan")
     for i in range(n_frames):
-        f = O.extract_frame(bgr[i % len(bgr)], dep[i % len(dep)], p, cal)
+        if ex is not None:
+            f = ex.extract_frame(bgr[i % len(bgr)], dep[i % len(dep)], cal)
+        else:
+            f = O.extract_frame(bgr[i % len(bgr)], dep[i % len(dep)], p, cal)
         if prev is not None:
             _, _, _, latch = O.track_pair(prev, f, cal, rp, pkg.pair_seed(0x5EED0000, i), latch)
         prev = f
@@ -144,6 +148,8 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=192, help="oracle sample size (frames, ~10 s)")
     ap.add_argument("--no-kernel-timing", action="store_true", help="no events around the kNN-2 launches")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--detector", choices=["orb_slam2", "adaptive"], default="orb_slam2",
+                    help="orb_slam2: ORBextractor (the metric's config); adaptive: Extractor(FAST, ORB, ADAPTIVE)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -171,7 +177,11 @@ def main():
         bgr, dep = bgr[np.arange(B) % L], dep[np.arange(B) % L]
     d_bgr = torch.from_numpy(bgr).to("cuda")
     d_dep = torch.from_numpy(dep.view(np.int16)).to("cuda")
-    cfg = pkg.default_config(W, H, B, nfeatures=args.nfeatures, iterations=args.iters, seed=pair_seed)
+    adaptive = args.detector == "adaptive"
+    if adaptive:
+        args.nfeatures = 1000  # Extract's retainBest(nFeatures), common.h:77
+    cfg = pkg.default_config(W, H, B, nfeatures=args.nfeatures, iterations=args.iters, seed=pair_seed,
+                             detector=pkg.DETECTOR_ADAPTIVE_FAST if adaptive else pkg.DETECTOR_ORB_SLAM2)
     odo = pkg.Odometry(cfg, device=local_rank)
     torch.cuda.synchronize()
 
@@ -237,7 +247,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         nf = args.cpu_frames
-        fps, dt = cpu_baseline(bgr, dep, args.nfeatures, args.iters, nf)
+        fps, dt = cpu_baseline(bgr, dep, args.nfeatures, args.iters, nf, adaptive)
         cpu = {"value": round(fps, 3), "unit": "frames/s", "cores": 1, "kind": "port",
                "sample": f"{nf} frames (the rank-0 {B}-frame sequence, cycled) through the C++ oracle's "
                          f"extract + match + RANSAC + PnP, single thread ({dt:.1f} s)"}
@@ -245,7 +255,8 @@ def main():
     if rank == 0:
         ok = res[1:]
         out = {
-            "metric": "frames/sec (extract+match+RANSAC-PnP) @640x480, 2000 kp",
+            "metric": "frames/sec (extract+match+RANSAC-PnP) @640x480, 2000 kp" if not adaptive else
+                      "frames/sec (ADAPTIVE FAST grid + ORB, match, RANSAC-PnP) @640x480, <=1000 kp",
             "value": round(value, 2),
             "unit": "frames/s",
             "n_gpus": world,
@@ -257,7 +268,10 @@ def main():
             "vs_baseline": None,
             "dtype": "u8/i32 (extract, match), f32+f64 (ransac, pnp)",
             "data": "synthetic (ray-cast textured room, closed-loop trajectory; no dataset offline)",
-            "config": {"workload": f"cfg2 fr1/desk proxy {W}x{H}, {args.nfeatures} kp, RANSAC {args.iters}",
+            "config": {"workload": (f"cfg2 fr1/desk proxy {W}x{H}, {args.nfeatures} kp, RANSAC {args.iters}"
+                                    if not adaptive else
+                                    f"fr1/desk proxy {W}x{H}, ADAPTIVE 3x3 FAST grid + ORB (<=1000 kp), "
+                                    f"RANSAC {args.iters}"),
                        "frames_per_step": B, "global_batch": B * world, "parallelism": f"frames x{world}",
                        "mean_keypoints": round(nkp_mean, 1),
                        "mean_matches": round(float(np.mean(ok["n_matches"])), 1),
