@@ -71,6 +71,12 @@ DETECTOR_ORB_SLAM2 = 0       # include/odo.h ODO_DETECTOR_ORB_SLAM2
 DETECTOR_ADAPTIVE_FAST = 1   # include/odo.h ODO_DETECTOR_ADAPTIVE_FAST
 
 
+class FoldResult(C.Structure):
+    _fields_ = [("best_h", C.c_int32), ("visited", C.c_int32), ("valid", C.c_int32), ("n_inliers", C.c_int32),
+                ("rmse", C.c_float), ("n_good", C.c_int32), ("pad", C.c_int32 * 2)]
+
+
+HYP_DTYPE = np.dtype([("err", "<f8"), ("cnt", "<i4"), ("pad", "<i4"), ("T", "<f4", 12)])  # odo_hyp_summary
 KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
                      ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
 DMATCH_DTYPE = np.dtype([("queryIdx", "<i4"), ("trainIdx", "<i4"), ("imgIdx", "<i4"), ("distance", "<f4")])
@@ -112,6 +118,9 @@ SIGNATURES = {
     "odo_debug_adaptive": (C.c_int, [P, C.c_int, P, P]),
     "odo_set_adaptive_thresholds": (C.c_int, [P, P, C.c_int]),
     "odo_debug_select": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, P, P]),
+    "odo_ransac_hyps": (C.c_int, [P, P, C.c_int, P, C.c_int, P, C.c_int, P, P, P, C.c_int, C.c_int, P, P]),
+    "odo_ransac_fold": (C.c_int, [P, C.c_int, C.c_int, P, P]),
+    "odo_ransac_hyps_finish": (C.c_int, [P, P, P, P, P, P, P, P, P]),
 }
 
 _lib = None

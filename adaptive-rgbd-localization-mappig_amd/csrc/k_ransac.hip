@@ -20,6 +20,7 @@
 // The TFC recurrence and the meanError sum are order-dependent float/double
 // folds; they run in match order, bit-identical to the reference.
 #include <algorithm>
+#include <vector>
 
 #include "odo_device.h"
 #include "odo_internal.h"
@@ -77,6 +78,8 @@ struct RansacBufs {
     int mask_words;
     odo_pair_result* res;
     float* T12;
+    // hypotheses mode: evaluate only [h_lo, h_hi), no fold
+    int h_lo, h_hi, no_fold;
 };
 
 ODO_INLINE int ld_relaxed(const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
@@ -691,6 +694,7 @@ ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int 
     // this launch covers hypothesis rows [y0, y0 + gridDim.y)
     const int hend = min(H, (y0 + (int)gridDim.y) * EV_WAVES);
     for (int h = (y0 + blockIdx.y) * EV_WAVES + wave; h < hend; h += gridDim.y * EV_WAVES) {
+        if (h < B.h_lo || h >= B.h_hi) continue;  // hypotheses mode: another rank's range
         const int* smp = smp0 + (size_t)h * SREC;
         double refinedError = 1e6;
         unsigned refinedCnt = 0;
@@ -839,7 +843,7 @@ ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int 
         __threadfence();
         if (lane == 0) {
             __hip_atomic_store(B.ready + (size_t)p * B.hcap + h, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            try_fold(B, cfg, p);
+            if (!B.no_fold) try_fold(B, cfg, p);
         }
         wave_sync();
     }
@@ -982,6 +986,18 @@ __global__ void __launch_bounds__(64) k_ransac_final(RansacBufs B, RansacCfg cfg
     }
 }
 
+// hypotheses mode: the ordered fold ran on the host over every rank's
+// summaries; install its outcome so k_ransac_final produces the outputs
+__global__ void k_ransac_install(RansacBufs B, int best_h, int visited, int valid, int best_cnt, float rmse) {
+    RState* S = B.st;
+    S->visited = visited;
+    S->valid = valid;
+    S->best_cnt = best_cnt;
+    S->best_h = best_h;
+    S->rmse = rmse;
+    S->done = 1;
+}
+
 // ---------------------------------------------------------------- host side
 size_t ransac_gpt_bytes() { return sizeof(GoodPt); }
 
@@ -1071,6 +1087,23 @@ void launch_ransac(hipStream_t st, const void* good, const int* n_good, const in
     B.res = res;
     B.T12 = T12;
     const int H = std::max(cfg.iterations, 0);
+    B.h_lo = 0;
+    B.h_hi = H;
+    B.no_fold = 0;
+    if (part == 3) {
+        // hypotheses mode, one pair: samples of all H, evaluation of [h0, h1)
+        // only (h0/h1 passed in phase[0..1]), no fold and no outputs
+        B.h_lo = std::max(0, phase[0]);
+        B.h_hi = std::min(H, phase[1]);
+        B.no_fold = 1;
+        hipLaunchKernelGGL(k_ransac_prep, dim3(npairs), dim3(256), 0, st, B, cfg);
+        if (B.h_hi > B.h_lo) {
+            const int ya = B.h_lo / EV_WAVES, yb = (B.h_hi + EV_WAVES - 1) / EV_WAVES;
+            hipLaunchKernelGGL(k_ransac_eval, dim3(npairs, yb - ya), dim3(64 * EV_WAVES), PCACHE * sizeof(GoodPt), st,
+                               B, cfg, ya);
+        }
+        return;
+    }
     // Two eval launches: the first EV_ROWS0 rows of hypotheses for every pair
     // (the >80% break usually ends a pair within them), then the rest, which
     // only pairs still folding take up — so the speculative hypotheses of
@@ -1092,6 +1125,38 @@ void launch_ransac(hipStream_t st, const void* good, const int* n_good, const in
                                st, B, cfg, r0);
         hipLaunchKernelGGL(k_ransac_final, dim3(npairs), dim3(64), 0, st, B, cfg, part == 2 ? 2 : 0, phase);
     }
+}
+
+// Hypotheses mode readback / finish over the scratch of a part-3 launch
+// (one pair): per-hypothesis (err, cnt, T) of [h0, h1), then the outputs of
+// the folded run (k_ransac_final mode 0: T12 / inlier mask of best_h when this
+// process evaluated it, identity fallback when nothing was valid, and the
+// caller's rand() state after exactly the visited draws).
+void ransac_read_hyps(hipStream_t st, void* scratch, int match_cap, int mask_words, RansacCfg cfg, int h0, int h1,
+                      double* err, int* cnt, float* T) {
+    RansacBufs B = carve(scratch, 1, match_cap, mask_words, cfg);
+    std::vector<HypRes> h(std::max(h1 - h0, 0));
+    if (h.empty()) return;
+    (void)hipMemcpyAsync(h.data(), B.hyp + h0, h.size() * sizeof(HypRes), hipMemcpyDeviceToHost, st);
+    (void)hipStreamSynchronize(st);
+    for (size_t i = 0; i < h.size(); i++) {
+        err[i] = h[i].err;
+        cnt[i] = h[i].cnt;
+        for (int k = 0; k < 12; k++) T[i * 12 + k] = h[i].T[k];
+    }
+}
+
+void launch_ransac_finish(hipStream_t st, void* scratch, int match_cap, int mask_words, RansacCfg cfg,
+                          const double* latch, odo_rng* rng_io, uint32_t* best_mask, odo_pair_result* res, float* T12,
+                          int best_h, int visited, int valid, int best_cnt, float rmse) {
+    RansacBufs B = carve(scratch, 1, match_cap, mask_words, cfg);
+    B.latch = latch;
+    B.rng_io = rng_io;
+    B.best_mask = best_mask;
+    B.res = res;
+    B.T12 = T12;
+    hipLaunchKernelGGL(k_ransac_install, dim3(1), dim3(1), 0, st, B, best_h, visited, valid, best_cnt, rmse);
+    hipLaunchKernelGGL(k_ransac_final, dim3(1), dim3(64), 0, st, B, cfg, 0, (int*)nullptr);
 }
 
 }  // namespace odo

@@ -72,8 +72,12 @@ constexpr int NSETS = 3;
 // output rows per resize workgroup
 constexpr int RZ_RB = 16;
 
+struct HypSession;  // hypotheses-mode RANSAC state (odo_ransac_hyps .. _finish)
+static void free_hyp_session(HypSession* h);
+
 struct odo_ctx {
     odo_config cfg{};
+    HypSession* hs = nullptr;
     int device = 0;
     hipStream_t stream = nullptr;   // extraction
     hipStream_t pstream = nullptr;  // pair stages
@@ -206,6 +210,7 @@ static int sync_all(odo_ctx* c) {
 
 static void free_ctx(odo_ctx* c) {
     if (!c) return;
+    free_hyp_session(c->hs);
     void* ptrs[] = {c->lv, c->cells, c->rx, c->ry, c->pyr, c->blur, c->cand, c->cand_cnt, c->keys, c->knode, c->kquad,
                     c->okp, c->ocnt, c->kps, c->desc, c->kun, c->xyz, c->ur, c->nkp, c->bgr_in, c->depth_in,
                     c->sort_scratch, c->latch, c->masks, c->adc, c->adb, c->smap, c->acand, c->abig, c->acell,
@@ -1251,7 +1256,70 @@ struct DevBuf {
         return (T*)p;
     }
 };
+
+// Ransac::Iterate's inputs after the depth filter, std::sort and the latch
+// (ransac.cpp:164-199), uploaded for the single-pair RANSAC kernels.
+struct PairRansacInput {
+    std::vector<odo_dmatch> good;
+    int ng = 0, words = 0, kc = 1;
+    RansacCfg cfg{};
+};
+
+// returns 0 when RANSAC does not run (too few matches / good matches)
+int prepare_pair_ransac(const odo_dmatch* m12, int n12, const float* xyz1, int n1, const float* xyz2, int n2,
+                        const odo_ransac_params* p, double* latch, PairRansacInput& in, int match_cap) {
+    if (n12 < p->min_inlier_th) return 0;
+    in.good.clear();
+    in.good.reserve(n12);
+    for (int i = 0; i < n12; i++) {
+        const odo_dmatch& m = m12[i];
+        if (m.queryIdx < 0 || m.queryIdx >= n1 || m.trainIdx < 0 || m.trainIdx >= n2)
+            return fail(ODO_ERR_ARG, "match index out of range");
+        const float zs = xyz1[3 * m.queryIdx + 2], zt = xyz2[3 * m.trainIdx + 2];
+        if (p->check_depth) {
+            if (std::isnan(zs) || std::isnan(zt)) continue;
+            if (zs <= 0 || zt <= 0) continue;
+        }
+        in.good.push_back(m);
+    }
+    if ((int)in.good.size() < p->min_inlier_th) return 0;
+    std::sort(in.good.begin(), in.good.end(),
+              [](const odo_dmatch& a, const odo_dmatch& b) { return a.distance < b.distance; });
+    in.ng = (int)in.good.size();
+    if (in.ng > match_cap * 64) return fail(ODO_ERR_CAPACITY, "too many matches");
+    if (std::isnan(*latch)) {  // DepthCovariance first-call latch (ransac.cpp:416-421)
+        for (const odo_dmatch& m : in.good) {
+            const float* o = &xyz1[3 * m.queryIdx];
+            const float* tg = &xyz2[3 * m.trainIdx];
+            if (o[2] == 0.0f || tg[0] == 0.0f) continue;
+            if (std::isnan(o[2]) || std::isnan(tg[2])) continue;
+            const double z = (double)o[2];
+            const double sd = 0.01 * z * z;
+            *latch = sd * sd;
+            break;
+        }
+    }
+    in.kc = std::max(std::max(n1, n2), 1);
+    in.words = (in.ng + 31) / 32;
+    const double cam_angle_x = 58.0 / 180.0 * M_PI, cam_angle_y = 45.0 / 180.0 * M_PI;
+    const double rsx = 3 * tan(cam_angle_x / 640.0), rsy = 3 * tan(cam_angle_y / 480.0);
+    in.cfg = RansacCfg{p->iterations, p->min_inlier_th, p->max_mahalanobis, p->sample_size, p->check_depth,
+                       rsx * rsx, rsy * rsy};
+    return 1;
+}
 }  // namespace
+
+struct HypSession {
+    PairRansacInput in;
+    int h0 = 0, h1 = 0, active = 0;
+    DevBuf *xyz = nullptr, *m = nullptr, *g = nullptr, *ints = nullptr, *latch = nullptr, *rng = nullptr,
+           *res = nullptr, *T = nullptr, *scr = nullptr, *bm = nullptr, *phase = nullptr;
+    ~HypSession() {
+        DevBuf* b[] = {xyz, m, g, ints, latch, rng, res, T, scr, bm, phase};
+        for (DevBuf* x : b) delete x;
+    }
+};
+static void free_hyp_session(HypSession* h) { delete h; }
 
 extern "C" {
 
@@ -1391,6 +1459,149 @@ int odo_ransac(odo_ctx* c, const odo_dmatch* m12, int n12, const float* xyz1, in
         }
     *n_inliers = k2;
     *ok = r.ransac_ok;
+    return ODO_OK;
+}
+
+int odo_ransac_hyps(odo_ctx* c, const odo_dmatch* m12, int n12, const float* xyz1, int n1, const float* xyz2, int n2,
+                    const odo_ransac_params* p, const odo_rng* rng, double* latch, int h0, int h1,
+                    odo_hyp_summary* out, int* n_good) {
+    if (!c || !p || !rng || !latch || !n_good || n12 < 0 || (n12 && !m12) || h0 < 0 || h1 < h0 ||
+        h1 > std::max(p->iterations, 0) || (h1 > h0 && !out))
+        return fail(ODO_ERR_ARG, "bad ransac_hyps args");
+    free_hyp_session(c->hs);
+    c->hs = new HypSession();
+    HypSession& S = *c->hs;
+    S.h0 = h0;
+    S.h1 = h1;
+    *n_good = 0;
+    for (int h = 0; h < h1 - h0; h++) out[h] = odo_hyp_summary{1e6, 0, 0, {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0}};
+    const int r = prepare_pair_ransac(m12, n12, xyz1, n1, xyz2, n2, p, latch, S.in, c->match_cap);
+    if (r < 0) return r;
+    if (r == 0) return ODO_OK;  // Iterate returns before the loop (too few matches)
+    S.active = 1;
+    PairRansacInput& in = S.in;
+    const int ng = in.ng, kc = in.kc;
+    *n_good = ng;
+    hipStream_t st = c->stream;
+    S.xyz = new DevBuf((size_t)2 * kc * 3 * sizeof(float));
+    S.m = new DevBuf((size_t)ng * sizeof(odo_dmatch));
+    S.g = new DevBuf((size_t)ng * 8);
+    S.ints = new DevBuf(4 * sizeof(int));
+    S.latch = new DevBuf(sizeof(double));
+    S.rng = new DevBuf(sizeof(odo_rng));
+    S.res = new DevBuf(sizeof(odo_pair_result));
+    S.T = new DevBuf(16 * sizeof(float));
+    S.scr = new DevBuf(ransac_scratch_bytes(1, ng, in.words, in.cfg));
+    S.bm = new DevBuf((size_t)in.words * 4);
+    S.phase = new DevBuf(2 * sizeof(int));
+    std::vector<uint64_t> gl(ng);
+    for (int k = 0; k < ng; k++) {
+        uint32_t bits;
+        memcpy(&bits, &in.good[k].distance, 4);
+        gl[k] = ((uint64_t)(uint32_t)k << 32) | bits;
+    }
+    const int ints[4] = {ng, ng, 1, 0};
+    const int range[2] = {h0, h1};
+    HIPCHK(hipMemcpyAsync(S.xyz->p, xyz1, (size_t)n1 * 12, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(S.xyz->as<float>() + (size_t)kc * 3, xyz2, (size_t)n2 * 12, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(S.m->p, in.good.data(), (size_t)ng * sizeof(odo_dmatch), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(S.g->p, gl.data(), (size_t)ng * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(S.ints->p, ints, sizeof(ints), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(S.latch->p, latch, sizeof(double), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(S.rng->p, rng, sizeof(odo_rng), hipMemcpyHostToDevice, st));
+    // the part-3 launch reads its range from host memory before returning
+    int* hrange = const_cast<int*>(range);
+    launch_ransac_raw(st, S.scr->p, 1, ng, in.words, in.cfg, 0, 0, S.rng->as<odo_rng>());
+    launch_ransac(st, S.g->p, S.ints->as<int>(), S.ints->as<int>() + 1, S.m->as<odo_dmatch>(), S.xyz->as<float>(),
+                  kc, 0, ng, in.cfg, S.latch->as<double>(), S.ints->as<int>() + 2, 0, S.rng->as<odo_rng>(), S.scr->p,
+                  S.bm->as<uint32_t>(), in.words, S.res->as<odo_pair_result>(), S.T->as<float>(), 1, 3, hrange);
+    HIPCHK(hipGetLastError());
+    if (h1 > h0) {
+        std::vector<double> err(h1 - h0);
+        std::vector<int> cnt(h1 - h0);
+        std::vector<float> T((size_t)(h1 - h0) * 12);
+        ransac_read_hyps(st, S.scr->p, ng, in.words, in.cfg, h0, h1, err.data(), cnt.data(), T.data());
+        HIPCHK(hipGetLastError());
+        for (int h = 0; h < h1 - h0; h++) {
+            out[h].err = err[h];
+            out[h].cnt = cnt[h];
+            memcpy(out[h].T, &T[(size_t)h * 12], 48);
+        }
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    return ODO_OK;
+}
+
+int odo_ransac_fold(const odo_hyp_summary* all, int H, int n_good, const odo_ransac_params* p,
+                    odo_ransac_fold_result* r) {
+    if (!p || !r || H < 0 || (H && !all)) return fail(ODO_ERR_ARG, "bad fold args");
+    // ransac.cpp:201-249: hypothesis j is the j-th visited iteration; n += 10
+    // skips do not consume samples, so the fold walks the summaries in order
+    *r = odo_ransac_fold_result{-1, 0, 0, 0, 1e6f, n_good, {0, 0}};
+    if (n_good < p->min_inlier_th || n_good < p->sample_size) return ODO_OK;
+    const unsigned minInl = (unsigned)p->min_inlier_th;
+    int n = 0, best = 0;
+    float rmse = 1e6f;
+    for (int pos = 0; pos < H && n < p->iterations; pos++) {
+        const unsigned rc = (unsigned)all[pos].cnt;
+        const double re = all[pos].err;
+        r->visited++;
+        bool brk = false;
+        if (rc > 0) {
+            r->valid++;
+            if (re <= (double)rmse && rc >= (unsigned)best && rc >= minInl) {
+                rmse = (float)re;
+                best = (int)rc;
+                r->best_h = pos;
+                if (rc > n_good * 0.5) n += 10;
+                if (rc > n_good * 0.75) n += 10;
+                if (rc > n_good * 0.8) brk = true;
+            }
+        }
+        n++;
+        if (brk) break;
+    }
+    r->rmse = rmse;
+    r->n_inliers = best;
+    return ODO_OK;
+}
+
+int odo_ransac_hyps_finish(odo_ctx* c, const odo_ransac_fold_result* r, odo_rng* rng, float T12[16], float* rmse,
+                           odo_dmatch* inliers, int* n_inliers, int* ok, int* owner) {
+    if (!c || !r || !rng || !T12 || !rmse || !n_inliers || !ok || !owner) return fail(ODO_ERR_ARG, "bad finish args");
+    if (!c->hs) return fail(ODO_ERR_STATE, "no odo_ransac_hyps call to finish");
+    HypSession& S = *c->hs;
+    for (int i = 0; i < 16; i++) T12[i] = (i % 5 == 0) ? 1.f : 0.f;
+    *rmse = 1e6f;
+    *n_inliers = 0;
+    *ok = 0;
+    *owner = 1;
+    if (!S.active) return ODO_OK;  // Iterate returned before sampling: rng untouched
+    PairRansacInput& in = S.in;
+    *owner = (r->best_h < 0 || (r->best_h >= S.h0 && r->best_h < S.h1)) ? 1 : 0;
+    hipStream_t st = c->stream;
+    HIPCHK(hipMemcpyAsync(S.rng->p, rng, sizeof(odo_rng), hipMemcpyHostToDevice, st));
+    launch_ransac_finish(st, S.scr->p, in.ng, in.words, in.cfg, S.latch->as<double>(), S.rng->as<odo_rng>(),
+                         S.bm->as<uint32_t>(), S.res->as<odo_pair_result>(), S.T->as<float>(), r->best_h, r->visited,
+                         r->valid, r->n_inliers, r->rmse);
+    HIPCHK(hipGetLastError());
+    odo_pair_result pr;
+    std::vector<uint32_t> bm(in.words);
+    HIPCHK(hipMemcpyAsync(&pr, S.res->p, sizeof(pr), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(bm.data(), S.bm->p, (size_t)in.words * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(rng, S.rng->p, sizeof(odo_rng), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (!*owner) return ODO_OK;
+    memcpy(T12, pr.T12, sizeof(pr.T12));
+    *rmse = pr.rmse;
+    int k2 = 0;
+    for (int k = 0; k < in.ng; k++)
+        if ((bm[k >> 5] >> (k & 31)) & 1) {
+            if (inliers) inliers[k2] = in.good[k];
+            k2++;
+        }
+    *n_inliers = k2;
+    *ok = pr.ransac_ok;
     return ODO_OK;
 }
 

@@ -169,6 +169,11 @@ void launch_ransac(hipStream_t st, const void* good, const int* n_good, const in
                    uint32_t* best_mask, int mask_words, odo_pair_result* res, float* T12, int npairs, int part = 0,
                    int* phase = nullptr);
 size_t ransac_scratch_bytes(int npairs, int match_cap, int mask_words, const RansacCfg& cfg);
+void ransac_read_hyps(hipStream_t st, void* scratch, int match_cap, int mask_words, RansacCfg cfg, int h0, int h1,
+                      double* err, int* cnt, float* T);
+void launch_ransac_finish(hipStream_t st, void* scratch, int match_cap, int mask_words, RansacCfg cfg,
+                          const double* latch, odo_rng* rng_io, uint32_t* best_mask, odo_pair_result* res, float* T12,
+                          int best_h, int visited, int valid, int best_cnt, float rmse);
 size_t pnp_edge_bytes();
 void launch_pnp(hipStream_t st, const int32_t* f2_src, const float* xyz, const float* kun, const float* ur,
                 const int* nkp, int kp_cap, int slot0, FrameCalib cal, const float* T12, const int* pair_valid,

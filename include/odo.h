@@ -114,6 +114,29 @@ int odo_ransac(odo_ctx* ctx, const odo_dmatch* m12, int n12, const float* xyz1, 
                const float* xyz2, int n2, const odo_ransac_params* p, odo_rng* rng, double* latch,
                float T12[16], float* rmse, odo_dmatch* inliers, int* n_inliers, int* ok);
 
+/* ---- Hypotheses mode of Ransac::Iterate: the
+ * hypotheses of one pair are sharded over ranks; each rank evaluates
+ * [h0, h1) from the same rand() stream, the per-hypothesis summaries are
+ * all-gathered (16..64 B each), every rank replays the ordered fold, and the
+ * rank that owns the winner supplies T12 and the inlier list.
+ * 1) odo_ransac_hyps: same inputs as odo_ransac (rng and latch are read, the
+ *    latch is set if unlatched, rng is NOT advanced); writes summaries of
+ *    [h0, h1) to out[0 .. h1-h0) and keeps the range's inlier masks in ctx. */
+int odo_ransac_hyps(odo_ctx* ctx, const odo_dmatch* m12, int n12, const float* xyz1, int n1,
+                    const float* xyz2, int n2, const odo_ransac_params* p, const odo_rng* rng,
+                    double* latch, int h0, int h1, odo_hyp_summary* out, int* n_good);
+/* 2) the ordered fold over all H = p->iterations summaries (host only, no
+ *    device needed): identical on every rank. */
+int odo_ransac_fold(const odo_hyp_summary* all, int H, int n_good, const odo_ransac_params* p,
+                    odo_ransac_fold_result* r);
+/* 3) outputs of the folded run from the last odo_ransac_hyps of this ctx:
+ *    rng advanced by exactly the visited draws (every rank); T12, rmse,
+ *    inliers and ok are valid when *owner = 1 (best_h in this rank's range,
+ *    or no valid hypothesis: identity fallback), otherwise they come from the
+ *    owner rank (broadcast). */
+int odo_ransac_hyps_finish(odo_ctx* ctx, const odo_ransac_fold_result* r, odo_rng* rng, float T12[16],
+                           float* rmse, odo_dmatch* inliers, int* n_inliers, int* ok, int* owner);
+
 /* PnPSolver::Compute (pnpsolver.cpp:17): Xw n x 3 (world), obs n x 3 (u,v,uR;
  * uR<0 = mono edge). outlier: out, per edge. Returns inliers in *n_inliers. */
 int odo_pnp_motion_ba(odo_ctx* ctx, const float* Xw, const float* obs, int n, const odo_calib* calib,

@@ -83,6 +83,27 @@ typedef struct odo_rng {
     int32_t rpos;   /* index of rptr into state */
 } odo_rng;
 
+/* Hypotheses mode: one evaluated RANSAC hypothesis (the
+ * visited iteration of that index: its sample, refinement loop and refined
+ * transform, ransac.cpp:201-231). cnt = |refined inliers| (0 = no valid
+ * refinement); err = refinedError; T = refined T12 rows 0..2. 64 bytes. */
+typedef struct odo_hyp_summary {
+    double err;
+    int32_t cnt;
+    int32_t pad;
+    float T[12];
+} odo_hyp_summary;
+
+/* Outcome of Ransac::Iterate's ordered running-best fold over all
+ * hypotheses (ransac.cpp:233-249): best_h = index of the accepted hypothesis
+ * (-1: none), visited = iterations run, valid = validIters. */
+typedef struct odo_ransac_fold_result {
+    int32_t best_h, visited, valid, n_inliers;
+    float rmse;
+    int32_t n_good;
+    int32_t pad[2];
+} odo_ransac_fold_result;
+
 /* Per-frame-pair odometry result. */
 typedef struct odo_pair_result {
     float T12[16];        /* RANSAC transform F1->F2 (row-major 4x4) */

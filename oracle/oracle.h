@@ -94,6 +94,12 @@ int oracle_extract_frame(const uint8_t* bgr, const uint16_t* depth, int w, int h
                          orb_kp* kps, uint8_t* desc, float* kps_un, float* xyz,
                          float* u_right, int cap);
 
+/* Hypotheses mode: per-hypothesis summaries of visited iterations [h0, h1)
+ * of Ransac::Iterate (no fold; rng_in is not advanced). Returns n_good. */
+int oracle_ransac_hyps(const odo_dmatch* m12, int n12, const float* xyz1, const float* xyz2,
+                       const odo_ransac_params* p, const odo_rng* rng_in, double* latch, int h0, int h1,
+                       odo_hyp_summary* out);
+
 /* BFMatcher(NORM_HAMMING).knnMatch(k=2) (App. A.6). */
 void oracle_knn2(const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* idx, int32_t* dist);
 

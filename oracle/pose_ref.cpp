@@ -1109,6 +1109,58 @@ int oracle_ransac(const odo_dmatch* m12, int n12, const float* xyz1, const float
     return ok ? 1 : 0;
 }
 
+// Hypotheses mode: the refinement loop of ransac.cpp:201-231
+// for visited iterations [h0, h1) only, from the same rand() stream (samples
+// of iterations < h0 are drawn and discarded); no fold. rng is not advanced.
+int oracle_ransac_hyps(const odo_dmatch* m12, int n12, const float* xyz1, const float* xyz2,
+                       const odo_ransac_params* p, const odo_rng* rng_in, double* latch, int h0, int h1,
+                       odo_hyp_summary* out) {
+    odo_rng rng = *rng_in;
+    RansacState S{xyz1, xyz2, *p, &rng, latch};
+    for (int h = h0; h < h1; h++) out[h - h0] = odo_hyp_summary{1e6, 0, 0, {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0}};
+    const size_t minInl = (size_t)p->min_inlier_th;
+    if ((size_t)n12 < minInl) return 0;
+    std::vector<DM> good;
+    for (int i = 0; i < n12; i++) {
+        const DM m{m12[i].queryIdx, m12[i].trainIdx, m12[i].imgIdx, m12[i].distance};
+        const float* s = &xyz1[3 * m.queryIdx];
+        const float* t = &xyz2[3 * m.trainIdx];
+        if (p->check_depth) {
+            if (std::isnan(s[2]) || std::isnan(t[2])) continue;
+            if (s[2] <= 0 || t[2] <= 0) continue;
+        }
+        good.push_back(m);
+    }
+    if (good.size() < minInl) return 0;
+    std::sort(good.begin(), good.end());
+    for (int h = 0; h < h1 && good.size() >= (size_t)p->sample_size; h++) {
+        std::vector<DM> inl = sample_matches(S, good);
+        if (h < h0) continue;
+        double refinedError = 1e6;
+        std::vector<DM> refined;
+        float refinedT[16];
+        for (int i = 0; i < 16; i++) refinedT[i] = (i % 5 == 0) ? 1.f : 0.f;
+        for (int refinements = 1; refinements < 20; refinements++) {
+            float T[16];
+            transform_from_matches(S, inl, T);
+            const double inlierError = compute_inliers_and_error(S, good, T, inl);
+            if (inl.size() < minInl || inlierError > p->max_mahalanobis) break;
+            if (inl.size() >= refined.size() && inlierError <= refinedError) {
+                const size_t prev = refined.size();
+                memcpy(refinedT, T, sizeof(T));
+                refined = inl;
+                refinedError = inlierError;
+                if (inl.size() == prev) break;
+            } else break;
+        }
+        odo_hyp_summary& o = out[h - h0];
+        o.err = refinedError;
+        o.cnt = (int)refined.size();
+        memcpy(o.T, refinedT, 48);
+    }
+    return (int)good.size();
+}
+
 void oracle_tfc(const float* src, const float* tgt, const float* w, int n, float* T) {
     TFC t;
     for (int i = 0; i < n; i++) t.add(&src[3 * i], &tgt[3 * i], w[i]);

@@ -20,6 +20,7 @@ class OrbKP(C.Structure):
                 ("response", C.c_float), ("octave", C.c_int32), ("class_id", C.c_int32)]
 
 
+HYP_DTYPE = np.dtype([("err", "<f8"), ("cnt", "<i4"), ("pad", "<i4"), ("T", "<f4", 12)])
 KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
                      ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
 DMATCH_DTYPE = np.dtype([("queryIdx", "<i4"), ("trainIdx", "<i4"), ("imgIdx", "<i4"), ("distance", "<f4")])
@@ -108,6 +109,7 @@ def lib():
             "oracle_track_pair": (C.c_int, [P, P, P, C.c_int, P, P, P, P, P, C.c_int, P, C.c_float, P,
                                             C.c_uint32, P, P, P, P, C.c_int]),
             "oracle_adaptive_default": (None, [P]),
+            "oracle_ransac_hyps": (C.c_int, [P, C.c_int, P, P, P, P, P, C.c_int, C.c_int, P]),
             "oracle_adaptive_detect": (C.c_int, [P, C.c_int, C.c_int, P, P, P, C.c_int, P]),
             "oracle_fast_roi": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, P, C.c_int]),
             "oracle_adaptive_extract": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, C.c_int, P]),
