@@ -20,6 +20,7 @@
 // The TFC recurrence and the meanError sum are order-dependent float/double
 // folds; they run in match order, bit-identical to the reference.
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "odo_device.h"
@@ -478,48 +479,62 @@ __global__ void __launch_bounds__(256) k_ransac_prep(RansacBufs B, RansacCfg cfg
 struct EvalLds {
     uint32_t cur[256];  // current inlier set (refined), bit k = good match k
     uint32_t nw[256];   // set produced by the sweep
-    // compacted TFC input chunk, SoA: sx sy sz tx ty tz w
-    __attribute__((aligned(16))) float pv[7][64];
-    __attribute__((aligned(16))) float acc[64];
-    __attribute__((aligned(16))) float alpha[64];
-    __attribute__((aligned(16))) float oma[64];
     double dv[64];      // compacted Mahalanobis terms of one sweep chunk
+};
+
+// TFC input slab of one wave (dynamic LDS after the good-point cache): the
+// current set's points compacted in set order, SoA rows sx sy sz tx ty tz
+// w->alpha acc->(1-alpha); up to TFC_CAP points per fold pass.
+#ifndef TFC_CAP
+#define TFC_CAP 512
+#endif
+struct TfcSlab {
+    float* v;  // 8 rows of TFC_CAP floats
+    ODO_INLINE float* row(int r) const { return v + r * TFC_CAP; }
 };
 
 ODO_INLINE bool tfc_point_ok(const GoodPt& g) {
     return !__builtin_isnan(g.sz) && !__builtin_isnan(g.tz) && g.w != 0.0f;  // ransac.cpp:303, TFC::add
 }
 
-ODO_INLINE void stage_pt(EvalLds& L, int q, const GoodPt& g) {
-    L.pv[0][q] = g.sx;
-    L.pv[1][q] = g.sy;
-    L.pv[2][q] = g.sz;
-    L.pv[3][q] = g.tx;
-    L.pv[4][q] = g.ty;
-    L.pv[5][q] = g.tz;
-    L.pv[6][q] = g.w;
+ODO_INLINE void stage_pt(const TfcSlab& L, int q, const GoodPt& g) {
+    L.row(0)[q] = g.sx;
+    L.row(1)[q] = g.sy;
+    L.row(2)[q] = g.sz;
+    L.row(3)[q] = g.tx;
+    L.row(4)[q] = g.ty;
+    L.row(5)[q] = g.tz;
+    L.row(6)[q] = g.w;
 }
 
 ODO_INLINE uint32_t lane_rank(uint64_t bal) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
 }
 
-// PCL TransformationFromCorrespondences::add over pts[0..nin), bit-identical
-// to the serial add(): lane 0 runs the accumulated-weight prefix, all lanes
-// form alpha = w/acc in parallel, then lane (i,j) < 9 runs three independent
-// chains per point — m1[j], m2[i] (recomputed redundantly, same operations)
-// and cov[i][j] — so the wave issues them interleaved instead of waiting on
-// one dependent chain.
-ODO_INLINE void tfc_fold(EvalLds& L, int nin, int lane, float& acc, float& m1, float& m2, float& c) {
+// PCL TransformationFromCorrespondences::add over the slab's n points,
+// bit-identical to the serial add(): lane 0 runs the accumulated-weight
+// prefix, all lanes form alpha = w/acc in parallel, then lane (i,j) < 9 runs
+// three independent chains per point - m1[j], m2[i] (recomputed redundantly,
+// same operations) and cov[i][j] - so the wave issues them interleaved
+// instead of waiting on one dependent chain. Chains carry over passes.
+ODO_INLINE void tfc_fold(const TfcSlab& L, int nin, int lane, float& acc, float& m1, float& m2, float& c,
+                         uint64_t* tp = nullptr) {
     if (nin <= 0) return;
-
+#ifdef ODO_RANSAC_PROFILE
+    uint64_t q = wall_clock64();
+#define TP(i) if (tp) { const uint64_t n_ = wall_clock64(); tp[i] += n_ - q; q = n_; }
+#else
+#define TP(i)
+#endif
     if (lane == 0) {
         float a = acc;
+        const float* W = L.row(6);
+        float* A = L.row(7);
         for (int q0 = 0; q0 < nin; q0 += 16) {
             float wv[16];
 #pragma unroll
             for (int u = 0; u < 16; u += 4) {
-                const float4 v = *reinterpret_cast<const float4*>(&L.pv[6][q0 + u]);
+                const float4 v = *reinterpret_cast<const float4*>(W + q0 + u);
                 wv[u] = v.x;
                 wv[u + 1] = v.y;
                 wv[u + 2] = v.z;
@@ -529,29 +544,33 @@ ODO_INLINE void tfc_fold(EvalLds& L, int nin, int lane, float& acc, float& m1, f
 #pragma unroll
                 for (int u = 0; u < 16; u++) {
                     a += wv[u];
-                    L.acc[q0 + u] = a;
+                    A[q0 + u] = a;
                 }
             } else {
 #pragma unroll
                 for (int u = 0; u < 16; u++) {
                     a = (q0 + u < nin) ? a + wv[u] : a;
-                    L.acc[q0 + u] = a;
+                    A[q0 + u] = a;
                 }
             }
         }
         acc = a;
     }
     wave_sync();
-    if (lane < nin) {
-        const float al = L.pv[6][lane] / L.acc[lane];
-        L.alpha[lane] = al;
-        L.oma[lane] = 1.0f - al;
+    TP(0)
+    for (int k = lane; k < nin; k += 64) {
+        const float al = L.row(6)[k] / L.row(7)[k];
+        L.row(6)[k] = al;
+        L.row(7)[k] = 1.0f - al;
     }
     wave_sync();
+    TP(1)
     if (lane < 9) {
         const int i = lane / 3, j = lane - 3 * (lane / 3);
-        const float* s1 = L.pv[j];
-        const float* s2 = L.pv[3 + i];
+        const float* s1 = L.row(j);
+        const float* s2 = L.row(3 + i);
+        const float* sa = L.row(6);
+        const float* so = L.row(7);
         float a1 = m1, a2 = m2, cc = c;
         for (int q0 = 0; q0 < nin; q0 += 16) {
             float P1[16], P2[16], AL[16], OM[16];
@@ -559,8 +578,8 @@ ODO_INLINE void tfc_fold(EvalLds& L, int nin, int lane, float& acc, float& m1, f
             for (int u = 0; u < 16; u += 4) {
                 const float4 a = *reinterpret_cast<const float4*>(s1 + q0 + u);
                 const float4 b = *reinterpret_cast<const float4*>(s2 + q0 + u);
-                const float4 e = *reinterpret_cast<const float4*>(&L.alpha[q0 + u]);
-                const float4 o = *reinterpret_cast<const float4*>(&L.oma[q0 + u]);
+                const float4 e = *reinterpret_cast<const float4*>(sa + q0 + u);
+                const float4 o = *reinterpret_cast<const float4*>(so + q0 + u);
                 P1[u] = a.x, P1[u + 1] = a.y, P1[u + 2] = a.z, P1[u + 3] = a.w;
                 P2[u] = b.x, P2[u + 1] = b.y, P2[u + 2] = b.z, P2[u + 3] = b.w;
                 AL[u] = e.x, AL[u + 1] = e.y, AL[u + 2] = e.z, AL[u + 3] = e.w;
@@ -594,6 +613,8 @@ ODO_INLINE void tfc_fold(EvalLds& L, int nin, int lane, float& acc, float& m1, f
         c = cc;
     }
     wave_sync();
+    TP(2)
+#undef TP
 }
 
 // Ordered sum of dv[0..nin) (lane 0), 16 loads ahead.
@@ -616,7 +637,11 @@ ODO_INLINE double fold_dv(const EvalLds& L, int nin, double s) {
 
 // The pair's good-match table is staged in LDS (shared by the workgroup's
 // waves) when it fits; every refinement sweeps it twice.
-#define PCACHE 1024
+#ifndef PCACHE
+#define PCACHE 0
+#endif
+// dynamic LDS of k_ransac_eval: good-point cache + one TFC slab per wave
+#define EV_LDS (PCACHE * sizeof(GoodPt) + (size_t)EV_WAVES * 8 * TFC_CAP * sizeof(float))
 extern __shared__ __align__(16) uint8_t ev_dyn[];
 
 template <bool CACHED>
@@ -682,9 +707,10 @@ ODO_INLINE void try_fold(const RansacBufs& B, const RansacCfg& cfg, int p) {
 
 template <bool CACHED>
 ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int wave, int lane, EvalLds& L,
-                          const GoodPt* P, int ng, int words, int H, int y0) {
+                          const GoodPt* P, int ng, int words, int H, int y0, int hlim) {
     RState* S = B.st + p;
     const int* smp0 = B.samples + (size_t)p * B.hcap * SREC;
+    const TfcSlab TS{reinterpret_cast<float*>(ev_dyn + PCACHE * sizeof(GoodPt)) + (size_t)wave * 8 * TFC_CAP};
     MahalConst K;
     K.raster_cov_x = cfg.raster_cov_x;
     K.raster_cov_y = cfg.raster_cov_y;
@@ -692,7 +718,8 @@ ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int 
     const float th = cfg.max_mahal * cfg.max_mahal;
     const unsigned minInl = (unsigned)cfg.min_inlier_th;
     // this launch covers hypothesis rows [y0, y0 + gridDim.y)
-    const int hend = min(H, (y0 + (int)gridDim.y) * EV_WAVES);
+    // this launch's waves stride over hypotheses [y0*EV_WAVES, hlim)
+    const int hend = min(H, hlim);
     for (int h = (y0 + blockIdx.y) * EV_WAVES + wave; h < hend; h += gridDim.y * EV_WAVES) {
         if (h < B.h_lo || h >= B.h_hi) continue;  // hypotheses mode: another rank's range
         const int* smp = smp0 + (size_t)h * SREC;
@@ -704,12 +731,15 @@ ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int 
 #ifdef ODO_RANSAC_PROFILE
         // -DODO_RANSAC_PROFILE: per-hypothesis phase times (10 ns ticks) via printf
         uint64_t t_tfc = 0, t_get = 0, t_sweep = 0, t0 = 0, t_start = wall_clock64();
-        int nref = 0;
+        uint64_t tpp[3] = {0, 0, 0};
+        int nref = 0, npass = 0;
+#define TPP (npass++, tpp)
 #define RP_T0() t0 = wall_clock64()
 #define RP_ACC(x) x += wall_clock64() - t0
 #else
 #define RP_T0()
 #define RP_ACC(x)
+#define TPP nullptr
 #endif
         for (int refinements = 1; refinements < 20; refinements++) {
             // ---- GetTransformFromMatches (ransac.cpp:295-313), in set order
@@ -724,10 +754,13 @@ ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int 
                     in = tfc_point_ok(g);
                 }
                 const uint64_t bal = __ballot(in);
-                if (in) stage_pt(L, lane_rank(bal), g);
+                if (in) stage_pt(TS, lane_rank(bal), g);
                 wave_sync();
-                tfc_fold(L, __popcll(bal), lane, tacc, tm1, tm2, tc);
+                tfc_fold(TS, __popcll(bal), lane, tacc, tm1, tm2, tc, TPP);
             } else {
+                // the whole set compacted into the slab in set order, folded
+                // once per TFC_CAP points (no per-chunk fold overhead)
+                int nfill = 0;
                 for (int c0 = 0; c0 < ng; c0 += 64) {
                     const int k = c0 + lane;
                     bool in = false;
@@ -737,10 +770,17 @@ ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int 
                         in = tfc_point_ok(g);
                     }
                     const uint64_t bal = __ballot(in);
-                    if (in) stage_pt(L, lane_rank(bal), g);
-                    wave_sync();
-                    tfc_fold(L, __popcll(bal), lane, tacc, tm1, tm2, tc);
+                    const int cnt = __popcll(bal);
+                    if (nfill + cnt > TFC_CAP) {
+                        wave_sync();
+                        tfc_fold(TS, nfill, lane, tacc, tm1, tm2, tc, TPP);
+                        nfill = 0;
+                    }
+                    if (in) stage_pt(TS, nfill + lane_rank(bal), g);
+                    nfill += cnt;
                 }
+                wave_sync();
+                tfc_fold(TS, nfill, lane, tacc, tm1, tm2, tc, TPP);
             }
             RP_ACC(t_tfc);
             RP_T0();
@@ -821,8 +861,9 @@ ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int 
         }
 #ifdef ODO_RANSAC_PROFILE
         if (lane == 0)
-            printf("HYP p %d h %d ng %d ab %d nref %d inl %u tfc %lu get %lu sweep %lu total %lu\n", p, h, ng,
-                   (int)aborted, nref, refinedCnt, t_tfc, t_get, t_sweep, wall_clock64() - t_start);
+            printf("HYP p %d h %d ng %d ab %d nref %d inl %u tfc %lu get %lu sweep %lu total %lu pass %d pre %lu al %lu ch %lu\n",
+                   p, h, ng, (int)aborted, nref, refinedCnt, t_tfc, t_get, t_sweep, wall_clock64() - t_start, npass,
+                   tpp[0], tpp[1], tpp[2]);
 #endif
         if (aborted) continue;
         HypRes* hr = B.hyp + (size_t)p * B.hcap + h;
@@ -849,7 +890,7 @@ ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int 
     }
 }
 
-__global__ void __launch_bounds__(64 * EV_WAVES) k_ransac_eval(RansacBufs B, RansacCfg cfg, int y0) {
+__global__ void __launch_bounds__(64 * EV_WAVES) k_ransac_eval(RansacBufs B, RansacCfg cfg, int y0, int hlim) {
     __builtin_amdgcn_s_setprio(ODO_WAVE_PRIO);  // latency-bound: issue ahead of co-resident extraction waves
     const int p = blockIdx.x;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -863,13 +904,13 @@ __global__ void __launch_bounds__(64 * EV_WAVES) k_ransac_eval(RansacBufs B, Ran
     if (s_done) return;  // uniform over the workgroup
     const int ng = S->ng, words = S->words;
     const GoodPt* P = B.gpts + (size_t)p * B.match_cap;
-    if (ng <= PCACHE) {
+    if (PCACHE > 0 && ng <= PCACHE) {
         GoodPt* pc = reinterpret_cast<GoodPt*>(ev_dyn);
         for (int k = threadIdx.x; k < ng; k += 64 * EV_WAVES) pc[k] = P[k];
         __syncthreads();
-        eval_hyps<true>(B, cfg, p, wave, lane, s_w[wave], P, ng, words, H, y0);
+        eval_hyps<true>(B, cfg, p, wave, lane, s_w[wave], P, ng, words, H, y0, hlim);
     } else {
-        eval_hyps<false>(B, cfg, p, wave, lane, s_w[wave], P, ng, words, H, y0);
+        eval_hyps<false>(B, cfg, p, wave, lane, s_w[wave], P, ng, words, H, y0, hlim);
     }
 }
 
@@ -1066,11 +1107,32 @@ void launch_ransac_raw(hipStream_t st, void* scratch, int npairs, int match_cap,
     hipLaunchKernelGGL(k_ransac_raw, dim3(npairs), dim3(64), 0, st, B, seed_base, pair_base);
 }
 
+static int ev2_rows() {
+    static int r = [] {
+        const char* e = getenv("ODO_EV2_ROWS");
+        // default: every remaining hypothesis row in flight. A pair whose best
+        // inlier ratio stays just under the 80 % break visits ~all H
+        // hypotheses; fewer rows make it take several rounds (measured at
+        // 64-frame batches: 1.366 ms per step with all rows, 1.39 with 16)
+        return e ? std::max(1, atoi(e)) : 1 << 30;
+    }();
+    return r;
+}
+
+static void ransac_eval_lds_attr() {
+    static bool done = false;
+    if (!done) {
+        (void)hipFuncSetAttribute((const void*)k_ransac_eval, hipFuncAttributeMaxDynamicSharedMemorySize, (int)EV_LDS);
+        done = true;
+    }
+}
+
 void launch_ransac(hipStream_t st, const void* good, const int* n_good, const int* n_matches,
                    const odo_dmatch* matches, const float* xyz, int kp_cap, int slot0, int match_cap, RansacCfg cfg,
                    const double* latch, const int* pair_valid, int min_matches, odo_rng* rng_io, void* scratch,
                    uint32_t* best_mask, int mask_words, odo_pair_result* res, float* T12, int npairs, int part,
                    int* phase) {
+    ransac_eval_lds_attr();
     RansacBufs B = carve(scratch, npairs, match_cap, mask_words, cfg);
     B.good = (const SortElR*)good;
     B.n_good = n_good;
@@ -1099,8 +1161,8 @@ void launch_ransac(hipStream_t st, const void* good, const int* n_good, const in
         hipLaunchKernelGGL(k_ransac_prep, dim3(npairs), dim3(256), 0, st, B, cfg);
         if (B.h_hi > B.h_lo) {
             const int ya = B.h_lo / EV_WAVES, yb = (B.h_hi + EV_WAVES - 1) / EV_WAVES;
-            hipLaunchKernelGGL(k_ransac_eval, dim3(npairs, yb - ya), dim3(64 * EV_WAVES), PCACHE * sizeof(GoodPt), st,
-                               B, cfg, ya);
+            hipLaunchKernelGGL(k_ransac_eval, dim3(npairs, yb - ya), dim3(64 * EV_WAVES), EV_LDS, st,
+                               B, cfg, ya, yb * EV_WAVES);
         }
         return;
     }
@@ -1115,14 +1177,16 @@ void launch_ransac(hipStream_t st, const void* good, const int* n_good, const in
     if (part != 2) {
         hipLaunchKernelGGL(k_ransac_prep, dim3(npairs), dim3(256), 0, st, B, cfg);
         if (r0 > 0)
-            hipLaunchKernelGGL(k_ransac_eval, dim3(npairs, r0), dim3(64 * EV_WAVES), PCACHE * sizeof(GoodPt), st, B,
-                               cfg, 0);
+            hipLaunchKernelGGL(k_ransac_eval, dim3(npairs, r0), dim3(64 * EV_WAVES), EV_LDS, st, B,
+                               cfg, 0, r0 * EV_WAVES);
         if (part == 1) hipLaunchKernelGGL(k_ransac_final, dim3(npairs), dim3(64), 0, st, B, cfg, 1, phase);
     }
     if (part != 1) {
+        // the second launch's waves stride over the remaining hypotheses:
+        // ev2_rows() rows of EV_WAVES per pair in flight (ODO_EV2_ROWS)
         if (rows > r0)
-            hipLaunchKernelGGL(k_ransac_eval, dim3(npairs, rows - r0), dim3(64 * EV_WAVES), PCACHE * sizeof(GoodPt),
-                               st, B, cfg, r0);
+            hipLaunchKernelGGL(k_ransac_eval, dim3(npairs, std::min(rows - r0, ev2_rows())), dim3(64 * EV_WAVES), EV_LDS,
+                               st, B, cfg, r0, H);
         hipLaunchKernelGGL(k_ransac_final, dim3(npairs), dim3(64), 0, st, B, cfg, part == 2 ? 2 : 0, phase);
     }
 }

@@ -148,6 +148,16 @@ struct odo_ctx {
     bool pdone_rec[NSETS] = {};
     bool serial = false;
     bool timing = false;
+    // stream layout (ODO_SCHED), measured on MI355X at 64-frame batches:
+    // 2 (default) = extraction | side (rand() words) | pair stages (match +
+    //     both RANSAC launches) | one PnP launch per batch: 1.37 ms per step;
+    // 1 = as 2 but two PnP launches on two streams (pairs finished by RANSAC
+    //     part 1 start early): 1.38 ms - the two PnP streams share a hardware
+    //     queue (GPU_MAX_HW_QUEUES=4) and serialise;
+    // 0 = as 2 with the words at the end of the extraction stream: 1.59 ms;
+    // 3 = kNN-2 and the words on the side stream: 1.30 ms... of a buggy run,
+    //     slower than 2 in the same A/B; 4 = the words on the pair stream.
+    int sched = 2;
     // ODO_SKIP (measurement only; results are invalid when set): bit 0 skips
     // the PnP launches, bit 1 RANSAC part 2, bit 2 every pair stage, bit 3 kNN-2
     int skip = 0;
@@ -627,6 +637,7 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
     const char* ser = getenv("ODO_SERIAL_STREAMS");
     c->serial = ser && ser[0] == '1';
     if (const char* sk = getenv("ODO_SKIP")) c->skip = atoi(sk);
+    if (const char* sc = getenv("ODO_SCHED")) c->sched = atoi(sc);
     bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
               (c->serial || (hipStreamCreateWithPriority(&c->pstream, hipStreamNonBlocking, pair_stream_priority()) ==
                                  hipSuccess &&
@@ -864,6 +875,25 @@ static int run_pairs(odo_ctx* c, int set, int n) {
     launch_latch(st, c->latch, P.good, P.n_good, P.n_matches, P.matches, xyz, c->kp_cap, 0, n, c->match_cap,
                  c->cfg.ransac.min_inlier_th, c->cfg.ransac.sample_size, c->cfg.ransac.iterations, P.pair_valid);
     tmark(c, 7, st);
+    if (c->sched != 1) {
+        // both RANSAC launches on the pair stream, then one PnP launch for the
+        // whole batch on its own stream (the pair stream moves on to the next
+        // batch while it runs)
+        launch_ransac(st, P.good, P.n_good, P.n_matches, P.matches, xyz, c->kp_cap, 0, c->match_cap, c->rcfg,
+                      c->latch, P.pair_valid, 20, nullptr, c->rscr[set], P.best_mask, c->mask_words, P.res, P.T12, n,
+                      0, P.pair_phase);
+        tmark(c, 8, st);
+        HIPCHK(hipEventRecord(c->ev_rb[set], st));
+        HIPCHK(hipStreamWaitEvent(c->pnpa, c->ev_rb[set], 0));
+        if (!(c->skip & 1))
+            launch_pnp(c->pnpa, P.f2_src, xyz, c->kun + b * KC * 2, c->ur + b * KC, nkp, c->kp_cap, 0, c->cal,
+                       P.T12, P.pair_valid, P.n_matches, 20, P.edges, P.res, P.pnp_mask, n);
+        tmark(c, 9, c->pnpa);
+        HIPCHK(hipEventRecord(c->ev_pa[set], c->pnpa));
+        HIPCHK(hipEventRecord(c->ev_pb[set], c->pnpa));
+        HIPCHK(hipGetLastError());
+        return ODO_OK;
+    }
     // RANSAC part 1 (prep + first eval launch) finishes most pairs; their PnP
     // starts on its own stream while part 2 evaluates the long pairs, whose
     // PnP runs on a second stream so the pair stream moves on to the next batch
@@ -926,7 +956,18 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
                           c->nkp + dst, c->kp_cap);
     }
     if ((e = run_extract(c, s, d_bgr, d_depth, n, 1))) return e;
-    // kNN-2 of every pair (throughput-bound) balances the two streams best here
+    // the kNN-2 stream: the extraction stream, or the side stream (sched 3)
+    hipStream_t ks = c->stream;
+    if (c->sched == 3) {
+        // side stream: the rand() words first (seed-only, they overlap the
+        // extraction), then kNN-2 once the batch's descriptors exist
+        if (c->pdone_rec[s]) HIPCHK(hipStreamWaitEvent(c->side, c->ev_rb[s], 0));
+        launch_ransac_raw(c->side, c->rscr[s], n, c->match_cap, c->mask_words, c->rcfg, (uint64_t)c->cfg.seed,
+                          c->pair_counter, nullptr);
+        HIPCHK(hipEventRecord(c->ev_xdone[s], c->stream));
+        HIPCHK(hipStreamWaitEvent(c->side, c->ev_xdone[s], 0));
+        ks = c->side;
+    }
     {
         const size_t b = fbase(c, s);
         uint8_t* desc = c->desc + b * KC * 32;
@@ -938,24 +979,42 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
                 if ((e = kt_collect(c, kt))) return e;
                 c->kt_pending--;
             }
-            HIPCHK(hipEventRecord(c->kt0[kt], c->stream));
+            HIPCHK(hipEventRecord(c->kt0[kt], ks));
         }
         if (!(c->skip & 8))
-            launch_knn2(c->stream, desc, nkp, KC * 32, desc + KC * 32, nkp + 1, KC * 32, c->knn_idx[s],
-                        c->knn_dist[s], KC, c->kp_cap, n);
+            launch_knn2(ks, desc, nkp, KC * 32, desc + KC * 32, nkp + 1, KC * 32, c->knn_idx[s], c->knn_dist[s], KC,
+                        c->kp_cap, n);
         if (kt >= 0) {
-            HIPCHK(hipEventRecord(c->kt1[kt], c->stream));
+            HIPCHK(hipEventRecord(c->kt1[kt], ks));
             c->kt_next = (kt + 1) % odo_ctx::KT_RING;
             c->kt_pending++;
         }
-        tmark(c, 10, c->stream);
+        tmark(c, 10, ks);
     }
-    HIPCHK(hipEventRecord(c->ev_xdone[s], c->stream));
-    // ---- side stream: RANSAC's rand() words depend on the pair seeds only
-    if (c->pdone_rec[s]) HIPCHK(hipStreamWaitEvent(c->side, c->ev_rb[s], 0));
-    launch_ransac_raw(c->side, c->rscr[s], n, c->match_cap, c->mask_words, c->rcfg, (uint64_t)c->cfg.seed,
-                      c->pair_counter, nullptr);
-    HIPCHK(hipEventRecord(c->ev_raw[s], c->side));
+    if (c->sched == 3) {
+        HIPCHK(hipEventRecord(c->ev_raw[s], c->side));
+        HIPCHK(hipEventRecord(c->ev_xdone[s], c->side));
+    } else if (c->sched == 0) {
+        // RANSAC's rand() words (seed-only) at the end of the extraction
+        // stream: set s was released (ev_pa/ev_pb) before this batch began
+        launch_ransac_raw(c->stream, c->rscr[s], n, c->match_cap, c->mask_words, c->rcfg, (uint64_t)c->cfg.seed,
+                          c->pair_counter, nullptr);
+        HIPCHK(hipEventRecord(c->ev_xdone[s], c->stream));
+        HIPCHK(hipEventRecord(c->ev_raw[s], c->stream));
+    } else if (c->sched == 4) {
+        // the words at the head of the pair stream (three streams in all)
+        HIPCHK(hipEventRecord(c->ev_xdone[s], c->stream));
+        launch_ransac_raw(c->pstream, c->rscr[s], n, c->match_cap, c->mask_words, c->rcfg, (uint64_t)c->cfg.seed,
+                          c->pair_counter, nullptr);
+        HIPCHK(hipEventRecord(c->ev_raw[s], c->pstream));
+    } else {
+        HIPCHK(hipEventRecord(c->ev_xdone[s], c->stream));
+        // ---- side stream: RANSAC's rand() words depend on the pair seeds only
+        if (c->pdone_rec[s]) HIPCHK(hipStreamWaitEvent(c->side, c->ev_rb[s], 0));
+        launch_ransac_raw(c->side, c->rscr[s], n, c->match_cap, c->mask_words, c->rcfg, (uint64_t)c->cfg.seed,
+                          c->pair_counter, nullptr);
+        HIPCHK(hipEventRecord(c->ev_raw[s], c->side));
+    }
     // ---- pair stream
     HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_xdone[s], 0));
     HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_raw[s], 0));
