@@ -81,6 +81,11 @@ struct odo_ctx {
     int device = 0;
     hipStream_t stream = nullptr;   // extraction
     hipStream_t pstream = nullptr;  // pair stages
+    hipStream_t pstream2 = nullptr;  // pair stages of odd batches (schedule 5)
+    hipStream_t cur_p = nullptr;     // pair stream of the batch being queued
+    hipEvent_t ev_latch = nullptr;   // after the last queued k_latch (schedule 5)
+    bool latch_rec = false;
+    uint64_t batch_counter = 0;
     int W = 0, H = 0, maxb = 0, slots = 0, nlevels = 0;
     std::vector<LevelDesc> lv_h;
     std::vector<CellDesc> cells_h;
@@ -155,8 +160,9 @@ struct odo_ctx {
     //     part 1 start early): 1.38 ms - the two PnP streams share a hardware
     //     queue (GPU_MAX_HW_QUEUES=4) and serialise;
     // 0 = as 2 with the words at the end of the extraction stream: 1.59 ms;
-    // 3 = kNN-2 and the words on the side stream: 1.30 ms... of a buggy run,
-    //     slower than 2 in the same A/B; 4 = the words on the pair stream.
+    // 3 = kNN-2 and the words on the side stream, 4 = the words at the head
+    //     of the pair stream, 5 = two pair streams alternating batches (each
+    //     with its batch's PnP): all slower than 2 in A/B runs (5: 1.99 ms).
     int sched = 2;
     // ODO_SKIP (measurement only; results are invalid when set): bit 0 skips
     // the PnP launches, bit 1 RANSAC part 2, bit 2 every pair stage, bit 3 kNN-2
@@ -213,6 +219,7 @@ static int sync_all(odo_ctx* c) {
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipStreamSynchronize(c->side));
     HIPCHK(hipStreamSynchronize(c->pstream));
+    if (c->pstream2) HIPCHK(hipStreamSynchronize(c->pstream2));
     HIPCHK(hipStreamSynchronize(c->pnpa));
     HIPCHK(hipStreamSynchronize(c->pnpb));
     return ODO_OK;
@@ -255,6 +262,8 @@ static void free_ctx(odo_ctx* c) {
         if (c->pnpb) hipStreamDestroy(c->pnpb);
         if (c->side) hipStreamDestroy(c->side);
         if (c->pstream) hipStreamDestroy(c->pstream);
+        if (c->pstream2) hipStreamDestroy(c->pstream2);
+        if (c->ev_latch) hipEventDestroy(c->ev_latch);
     }
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
@@ -648,6 +657,7 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
                              hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) == hipSuccess));
     if (ok && c->serial) {
         c->pstream = c->stream;
+        c->pstream2 = c->stream;
         c->side = c->stream;
         c->pnpa = c->stream;
         c->pnpb = c->stream;
@@ -660,6 +670,9 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
     for (int i = 0; i < NSETS && ok; i++)
         ok = hipEventCreateWithFlags(&c->ev_xdone[i], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&c->ev_raw[i], hipEventDisableTiming) == hipSuccess;
+    if (ok && !c->serial)
+        ok = hipStreamCreateWithFlags(&c->pstream2, hipStreamNonBlocking) == hipSuccess &&
+             hipEventCreateWithFlags(&c->ev_latch, hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         fail(ODO_ERR_DEVICE, "hipStreamCreate failed");
         free_ctx(c);
@@ -859,7 +872,7 @@ int odo_extract_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth,
 // Pair stages of one batch on the pair stream, over frame set `set`:
 // pair p is (slot p, slot p+1); pair 0 is valid only with a previous frame.
 static int run_pairs(odo_ctx* c, int set, int n) {
-    hipStream_t st = c->pstream;
+    hipStream_t st = c->cur_p ? c->cur_p : c->pstream;
     auto& P = c->pb[set];
     const size_t KC = (size_t)c->kp_cap;
     const size_t b = fbase(c, set);
@@ -872,8 +885,15 @@ static int run_pairs(odo_ctx* c, int set, int n) {
     launch_pair_match(st, c->knn_idx[set], c->knn_dist[set], KC, xyz, nkp, c->kp_cap, 0, c->cfg.nn_ratio, mThDepth,
                       c->cfg.ransac.check_depth, P.matches, P.n_matches, P.good, P.n_good, P.f2_src,
                       c->sort_scratch, c->match_cap, n);
+    // the DepthCovariance latch is taken from the first valid pair ever: with
+    // two pair streams, a batch's latch kernel runs after the previous one's
+    if (c->sched == 5 && c->latch_rec) HIPCHK(hipStreamWaitEvent(st, c->ev_latch, 0));
     launch_latch(st, c->latch, P.good, P.n_good, P.n_matches, P.matches, xyz, c->kp_cap, 0, n, c->match_cap,
                  c->cfg.ransac.min_inlier_th, c->cfg.ransac.sample_size, c->cfg.ransac.iterations, P.pair_valid);
+    if (c->sched == 5) {
+        HIPCHK(hipEventRecord(c->ev_latch, st));
+        c->latch_rec = true;
+    }
     tmark(c, 7, st);
     if (c->sched != 1) {
         // both RANSAC launches on the pair stream, then one PnP launch for the
@@ -884,13 +904,15 @@ static int run_pairs(odo_ctx* c, int set, int n) {
                       0, P.pair_phase);
         tmark(c, 8, st);
         HIPCHK(hipEventRecord(c->ev_rb[set], st));
-        HIPCHK(hipStreamWaitEvent(c->pnpa, c->ev_rb[set], 0));
+        // schedule 5: PnP follows RANSAC on the batch's own pair stream
+        hipStream_t ps = c->sched == 5 ? st : c->pnpa;
+        if (ps != st) HIPCHK(hipStreamWaitEvent(ps, c->ev_rb[set], 0));
         if (!(c->skip & 1))
-            launch_pnp(c->pnpa, P.f2_src, xyz, c->kun + b * KC * 2, c->ur + b * KC, nkp, c->kp_cap, 0, c->cal,
-                       P.T12, P.pair_valid, P.n_matches, 20, P.edges, P.res, P.pnp_mask, n);
-        tmark(c, 9, c->pnpa);
-        HIPCHK(hipEventRecord(c->ev_pa[set], c->pnpa));
-        HIPCHK(hipEventRecord(c->ev_pb[set], c->pnpa));
+            launch_pnp(ps, P.f2_src, xyz, c->kun + b * KC * 2, c->ur + b * KC, nkp, c->kp_cap, 0, c->cal, P.T12,
+                       P.pair_valid, P.n_matches, 20, P.edges, P.res, P.pnp_mask, n);
+        tmark(c, 9, ps);
+        HIPCHK(hipEventRecord(c->ev_pa[set], ps));
+        HIPCHK(hipEventRecord(c->ev_pb[set], ps));
         HIPCHK(hipGetLastError());
         return ODO_OK;
     }
@@ -1001,12 +1023,19 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
                           c->pair_counter, nullptr);
         HIPCHK(hipEventRecord(c->ev_xdone[s], c->stream));
         HIPCHK(hipEventRecord(c->ev_raw[s], c->stream));
-    } else if (c->sched == 4) {
-        // the words at the head of the pair stream (three streams in all)
+    } else if (c->sched == 4 || c->sched == 5) {
+        // the words at the head of the batch's pair stream; schedule 5
+        // alternates two pair streams (each also runs its batch's PnP), so one
+        // batch's long RANSAC / PnP overlaps the next batch's pair stages
+        c->cur_p = (c->sched == 5 && (c->batch_counter & 1)) ? c->pstream2 : c->pstream;
+        if (c->pdone_rec[s]) {
+            HIPCHK(hipStreamWaitEvent(c->cur_p, c->ev_pa[s], 0));
+            HIPCHK(hipStreamWaitEvent(c->cur_p, c->ev_pb[s], 0));
+        }
         HIPCHK(hipEventRecord(c->ev_xdone[s], c->stream));
-        launch_ransac_raw(c->pstream, c->rscr[s], n, c->match_cap, c->mask_words, c->rcfg, (uint64_t)c->cfg.seed,
+        launch_ransac_raw(c->cur_p, c->rscr[s], n, c->match_cap, c->mask_words, c->rcfg, (uint64_t)c->cfg.seed,
                           c->pair_counter, nullptr);
-        HIPCHK(hipEventRecord(c->ev_raw[s], c->pstream));
+        HIPCHK(hipEventRecord(c->ev_raw[s], c->cur_p));
     } else {
         HIPCHK(hipEventRecord(c->ev_xdone[s], c->stream));
         // ---- side stream: RANSAC's rand() words depend on the pair seeds only
@@ -1016,8 +1045,9 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
         HIPCHK(hipEventRecord(c->ev_raw[s], c->side));
     }
     // ---- pair stream
-    HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_xdone[s], 0));
-    HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_raw[s], 0));
+    if (c->sched != 4 && c->sched != 5) c->cur_p = c->pstream;
+    HIPCHK(hipStreamWaitEvent(c->cur_p, c->ev_xdone[s], 0));
+    HIPCHK(hipStreamWaitEvent(c->cur_p, c->ev_raw[s], 0));
     c->valid_h.assign(n, 1);
     c->valid_h[0] = c->has_prev ? 1 : 0;
     if (!(c->skip & 4) && (e = run_pairs(c, s, n))) return e;
@@ -1028,6 +1058,7 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
     c->last_n = n;
     c->has_prev = true;
     c->pair_counter += (uint64_t)n;
+    c->batch_counter++;
     if ((e = finish_batch(c, s, n, h_results))) return e;
     return ODO_OK;
 }
