@@ -77,6 +77,8 @@ class FoldResult(C.Structure):
 
 
 HYP_DTYPE = np.dtype([("err", "<f8"), ("cnt", "<i4"), ("pad", "<i4"), ("T", "<f4", 12)])  # odo_hyp_summary
+LANDMARK_DTYPE = np.dtype([("X", "<f4", 3), ("flags", "<i4"), ("desc", "u1", 32)])  # odo_landmark
+LM_BAD, LM_SEEN, LM_HAS_OBS = 1, 2, 4
 KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
                      ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
 DMATCH_DTYPE = np.dtype([("queryIdx", "<i4"), ("trainIdx", "<i4"), ("imgIdx", "<i4"), ("distance", "<f4")])
@@ -118,6 +120,8 @@ SIGNATURES = {
     "odo_debug_adaptive": (C.c_int, [P, C.c_int, P, P]),
     "odo_set_adaptive_thresholds": (C.c_int, [P, P, C.c_int]),
     "odo_debug_select": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, P, P]),
+    "odo_image_bounds": (C.c_int, [P, P]),
+    "odo_projection_match": (C.c_int, [P, P, P, C.c_int, P, P, P, C.c_int, P, C.c_float, C.c_float, P, P, P]),
     "odo_ransac_hyps": (C.c_int, [P, P, C.c_int, P, C.c_int, P, C.c_int, P, P, P, C.c_int, C.c_int, P, P]),
     "odo_ransac_fold": (C.c_int, [P, C.c_int, C.c_int, P, P]),
     "odo_ransac_hyps_finish": (C.c_int, [P, P, P, P, P, P, P, P, P]),

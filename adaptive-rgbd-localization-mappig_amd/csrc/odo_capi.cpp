@@ -1738,6 +1738,86 @@ int odo_pnp_motion_ba(odo_ctx* c, const float* Xw, const float* obs, int n, cons
     return ODO_OK;
 }
 
+// Frame::ComputeImageBounds: cv::undistortPoints of the four corners (5
+// iterations in double, App. A.10)
+static void undistort_host(float u, float v, const odo_calib& c, float* uo, float* vo) {
+    const double fx = c.fx, fy = c.fy, cx = c.cx, cy = c.cy;
+    const double ifx = 1. / fx, ify = 1. / fy;
+    const double k0 = c.k1, k1 = c.k2, k2 = c.p1, k3 = c.p2, k4 = c.k3;
+    double x = u, y = v;
+    x = (x - cx) * ifx;
+    y = (y - cy) * ify;
+    const double x0 = x, y0 = y;
+    for (int j = 0; j < 5; j++) {
+        double r2 = x * x + y * y;
+        double icdist = 1 / (1 + ((k4 * r2 + k1) * r2 + k0) * r2);
+        double deltaX = 2 * k2 * x * y + k3 * (r2 + 2 * x * x);
+        double deltaY = k2 * (r2 + 2 * y * y) + 2 * k3 * x * y;
+        x = (x0 - deltaX) * icdist;
+        y = (y0 - deltaY) * icdist;
+    }
+    *uo = (float)(fx * x + cx);
+    *vo = (float)(fy * y + cy);
+}
+
+int odo_image_bounds(odo_ctx* c, float b[4]) {
+    if (!c || !b) return fail(ODO_ERR_ARG, "bad bounds args");
+    const odo_calib& k = c->cfg.calib;
+    if (k.k1 != 0.0f) {
+        const float cu[4] = {0.f, (float)c->W, 0.f, (float)c->W}, cv_[4] = {0.f, 0.f, (float)c->H, (float)c->H};
+        float u[4], v[4];
+        for (int i = 0; i < 4; i++) undistort_host(cu[i], cv_[i], k, &u[i], &v[i]);
+        b[0] = std::min(u[0], u[2]);
+        b[1] = std::max(u[1], u[3]);
+        b[2] = std::min(v[0], v[1]);
+        b[3] = std::max(v[2], v[3]);
+    } else {
+        b[0] = 0.f;
+        b[1] = (float)c->W;
+        b[2] = 0.f;
+        b[3] = (float)c->H;
+    }
+    return ODO_OK;
+}
+
+int odo_projection_match(odo_ctx* c, const float Tcw[16], const odo_landmark* lms, int nL, const float* kun,
+                         const int32_t* octave, const uint8_t* desc, int n, const uint8_t* slot_taken, float th,
+                         float nn_ratio, int32_t* slot_lm, float* proj, int* n_matches) {
+    if (!c || !Tcw || nL < 0 || n < 0 || (nL && (!lms || !proj)) || (n && (!kun || !octave || !desc || !slot_lm)) ||
+        !n_matches)
+        return fail(ODO_ERR_ARG, "bad projection_match args");
+    if (n > 8191) return fail(ODO_ERR_CAPACITY, "more than 8191 keypoints");
+    *n_matches = 0;
+    hipStream_t st = c->stream;
+    float bounds[4];
+    odo_image_bounds(c, bounds);
+    const odo_calib& k = c->cfg.calib;
+    const float cal5[5] = {k.fx, k.fy, k.cx, k.cy, k.mbf};
+    const size_t nl = std::max(nL, 1), nn = std::max(n, 1);
+    DevBuf dT(64), dl(nl * sizeof(odo_landmark)), dk(nn * 8), doc(nn * 4), dd(nn * 32), dtk(nn), dproj(nl * 12),
+        din(nl), dcc(nl * 4), dcand(nl * projection_cand_cap() * 4), dsl(nn * 4), dnm(4);
+    HIPCHK(hipMemcpyAsync(dT.p, Tcw, 64, hipMemcpyHostToDevice, st));
+    if (nL) HIPCHK(hipMemcpyAsync(dl.p, lms, (size_t)nL * sizeof(odo_landmark), hipMemcpyHostToDevice, st));
+    if (n) {
+        HIPCHK(hipMemcpyAsync(dk.p, kun, (size_t)n * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(doc.p, octave, (size_t)n * 4, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(dd.p, desc, (size_t)n * 32, hipMemcpyHostToDevice, st));
+        if (slot_taken) HIPCHK(hipMemcpyAsync(dtk.p, slot_taken, (size_t)n, hipMemcpyHostToDevice, st));
+        else HIPCHK(hipMemsetAsync(dtk.p, 0, (size_t)n, st));
+    }
+    if (launch_projection_match(st, dT.as<float>(), dl.as<odo_landmark>(), nL, dk.as<float>(), doc.as<int32_t>(),
+                                dd.as<uint8_t>(), n, dtk.as<uint8_t>(), cal5, bounds, th, nn_ratio, dproj.as<float>(),
+                                din.as<uint8_t>(), dcc.as<int>(), dcand.as<uint32_t>(), dsl.as<int32_t>(),
+                                dnm.as<int>()) != 0)
+        return fail(ODO_ERR_CAPACITY, "projection match capacity");
+    HIPCHK(hipGetLastError());
+    if (nL) HIPCHK(hipMemcpyAsync(proj, dproj.p, (size_t)nL * 12, hipMemcpyDeviceToHost, st));
+    if (n) HIPCHK(hipMemcpyAsync(slot_lm, dsl.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(n_matches, dnm.p, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return ODO_OK;
+}
+
 int odo_kabsch(const float* A, const float* B, int n, float T[16]) {
     if (n < 0 || (n && (!A || !B)) || !T) return fail(ODO_ERR_ARG, "bad kabsch args");
     int ndev = 0;

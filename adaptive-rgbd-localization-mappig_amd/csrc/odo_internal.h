@@ -180,6 +180,11 @@ void launch_pnp(hipStream_t st, const int32_t* f2_src, const float* xyz, const f
                 const int* n_matches, int min_matches, void* edges, odo_pair_result* res, uint8_t* inlier_mask,
                 int npairs, const int* sel = nullptr, int sel_val = 0);
 void launch_kabsch(hipStream_t st, const float* A, const float* B, int n, float* T);
+int launch_projection_match(hipStream_t st, const float* Tcw, const odo_landmark* lms, int nL, const float* kun,
+                            const int32_t* octave, const uint8_t* desc, int n, const uint8_t* slot_taken,
+                            const float* calib5, const float* bounds, float th, float nnratio, float* proj,
+                            uint8_t* inview, int* ccount, uint32_t* cand, int32_t* slot_lm, int* nmatches);
+size_t projection_cand_cap();
 void upload_adaptive_constants();
 void launch_adapt_smap(hipStream_t st, const uint8_t* pyr, size_t pyr_stride, int w, int h, int pitch, uint8_t* smap,
                        size_t smap_stride, int nframes);

@@ -142,6 +142,26 @@ int odo_ransac_hyps_finish(odo_ctx* ctx, const odo_ransac_fold_result* r, odo_rn
 int odo_pnp_motion_ba(odo_ctx* ctx, const float* Xw, const float* obs, int n, const odo_calib* calib,
                       const float Tcw_init[16], float Tcw_out[16], uint8_t* outlier, int* n_inliers);
 
+/* Frame::ComputeImageBounds (frame.cpp:315-349) for the context's calibration
+ * and image size: undistorted corners -> minX, maxX, minY, maxY. Host only. */
+int odo_image_bounds(odo_ctx* ctx, float bounds[4]);
+
+/* Tracking::SearchLocalLMs (tracking.cpp:368-405): Frame::isInFrustum
+ * (frame.cpp:100-133) for every landmark neither ODO_LM_BAD nor ODO_LM_SEEN,
+ * then Matcher(nn_ratio)::ProjectionMatch(frame, landmarks, th)
+ * (matcher.cpp:90-145; the reference passes 0.8f and 8.0f). Frame: n
+ * undistorted keypoints (mvKeysUn), their octaves and descriptors;
+ * slot_taken[j] = slot j holds a landmark with Observations() > 0. Outputs:
+ * slot_lm[j] = index of the landmark AddLandmark put in slot j, or -1;
+ * proj[3*i..] = (mTrackProjX, mTrackProjY, mTrackProjXR) of in-view
+ * landmarks, NaN otherwise; *n_matches = ProjectionMatch's return. Then
+ * TrackLocalMap's second PnPSolver::Compute is odo_pnp_motion_ba over every
+ * slot holding a landmark. */
+int odo_projection_match(odo_ctx* ctx, const float Tcw[16], const odo_landmark* lms, int n_lms,
+                         const float* kps_un, const int32_t* octave, const uint8_t* desc, int n,
+                         const uint8_t* slot_taken, float th, float nn_ratio, int32_t* slot_lm, float* proj,
+                         int* n_matches);
+
 /* Kabsch::Compute (kabsch.cpp:14), host-side 3x3 SVD. A,B: n x 3. */
 int odo_kabsch(const float* A, const float* B, int n, float T[16]);
 

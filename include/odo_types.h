@@ -104,6 +104,18 @@ typedef struct odo_ransac_fold_result {
     int32_t pad[2];
 } odo_ransac_fold_result;
 
+/* One local-map landmark for Matcher::ProjectionMatch (matcher.cpp:90-145):
+ * world position (Landmark::GetWorldPos), distinctive descriptor
+ * (GetDescriptor) and state flags. 48 bytes. */
+#define ODO_LM_BAD 1       /* Landmark::isBad() */
+#define ODO_LM_SEEN 2      /* mnLastFrameSeen == current frame (already matched; SearchLocalLMs skips it) */
+#define ODO_LM_HAS_OBS 4   /* Observations() > 0 (a slot holding it is skipped by later landmarks) */
+typedef struct odo_landmark {
+    float X[3];
+    int32_t flags;
+    uint8_t desc[32];
+} odo_landmark;
+
 /* Per-frame-pair odometry result. */
 typedef struct odo_pair_result {
     float T12[16];        /* RANSAC transform F1->F2 (row-major 4x4) */

@@ -100,6 +100,15 @@ int oracle_ransac_hyps(const odo_dmatch* m12, int n12, const float* xyz1, const 
                        const odo_ransac_params* p, const odo_rng* rng_in, double* latch, int h0, int h1,
                        odo_hyp_summary* out);
 
+/* Frame::ComputeImageBounds (frame.cpp:315-349): minX maxX minY maxY. */
+void oracle_image_bounds(const odo_calib* c, int w, int h, float* bounds);
+/* SearchLocalLMs' isInFrustum + Matcher(0.8)::ProjectionMatch (tracking.cpp:368-405,
+ * matcher.cpp:90-145). Returns nmatches. */
+int oracle_projection_match(const float* Tcw, const odo_landmark* lms, int nL, const float* kun,
+                            const int32_t* octave, const uint8_t* desc, int n, const uint8_t* slot_taken,
+                            const odo_calib* c, const float* bounds, float th, float nnratio,
+                            int32_t* slot_lm, float* proj);
+
 /* BFMatcher(NORM_HAMMING).knnMatch(k=2) (App. A.6). */
 void oracle_knn2(const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* idx, int32_t* dist);
 

@@ -1008,6 +1008,99 @@ int oracle_extract_frame_adaptive(const uint8_t* bgr, const uint16_t* depth, int
     return n;
 }
 
+// Frame::ComputeImageBounds (frame.cpp:315-349): undistorted image corners.
+void oracle_image_bounds(const odo_calib* c, int w, int h, float* b) {
+    if (c->k1 != 0.0f) {
+        const float cu[4] = {0.f, (float)w, 0.f, (float)w}, cv_[4] = {0.f, 0.f, (float)h, (float)h};
+        float u[4], v[4];
+        for (int i = 0; i < 4; i++) undistort_point(cu[i], cv_[i], *c, &u[i], &v[i]);
+        b[0] = std::min(u[0], u[2]);
+        b[1] = std::max(u[1], u[3]);
+        b[2] = std::min(v[0], v[1]);
+        b[3] = std::max(v[2], v[3]);
+    } else {
+        b[0] = 0.f;
+        b[1] = (float)w;
+        b[2] = 0.f;
+        b[3] = (float)h;
+    }
+}
+
+// Tracking::SearchLocalLMs (tracking.cpp:368-405): Frame::isInFrustum
+// (frame.cpp:100-133) on every landmark neither bad nor already seen by the
+// frame, then Matcher(0.8f)::ProjectionMatch(frame, landmarks, th)
+// (matcher.cpp:90-145, TH_HIGH = 100, matcher.cpp:15-17) with
+// GetFeaturesInArea's linear scan (frame.cpp:258-274). mRcw * P + mtcw is one
+// folded cv::gemm (float data, double accumulation, one rounding). slot_taken:
+// the frame slot holds a landmark with Observations() > 0. Outputs: slot_lm =
+// landmark index added to the slot (AddLandmark) or -1; proj = (u, v, uR) of
+// in-view landmarks (mTrackProjX/Y/XR), NaN otherwise. Returns nmatches.
+int oracle_projection_match(const float* Tcw, const odo_landmark* lms, int nL, const float* kun,
+                            const int32_t* octave, const uint8_t* desc, int n, const uint8_t* slot_taken,
+                            const odo_calib* c, const float* bounds, float th, float nnratio, int32_t* slot_lm,
+                            float* proj) {
+    std::vector<uint8_t> taken(slot_taken, slot_taken + n);
+    for (int j = 0; j < n; j++) slot_lm[j] = -1;
+    std::vector<uint8_t> inview(nL, 0);
+    const float nan = std::numeric_limits<float>::quiet_NaN();
+    for (int i = 0; i < nL; i++) {
+        proj[3 * i] = proj[3 * i + 1] = proj[3 * i + 2] = nan;
+        const odo_landmark& L = lms[i];
+        if (L.flags & (ODO_LM_BAD | ODO_LM_SEEN)) continue;
+        float Pc[3];
+        for (int k = 0; k < 3; k++)
+            Pc[k] = (float)((((double)Tcw[4 * k] * L.X[0] + (double)Tcw[4 * k + 1] * L.X[1]) +
+                             (double)Tcw[4 * k + 2] * L.X[2]) + (double)Tcw[4 * k + 3]);
+        if (Pc[2] < 0.0f) continue;
+        const float invz = 1.0f / Pc[2];
+        const float u = c->fx * Pc[0] * invz + c->cx;
+        const float v = c->fy * Pc[1] * invz + c->cy;
+        if (u < bounds[0] || u > bounds[1]) continue;
+        if (v < bounds[2] || v > bounds[3]) continue;
+        inview[i] = 1;
+        proj[3 * i] = u;
+        proj[3 * i + 1] = v;
+        proj[3 * i + 2] = u - c->mbf * invz;
+    }
+    const double TH_HIGH = 100.0;
+    int nmatches = 0;
+    for (int i = 0; i < nL; i++) {
+        if (!inview[i]) continue;
+        const odo_landmark& L = lms[i];
+        if (L.flags & ODO_LM_BAD) continue;
+        const float x = proj[3 * i], y = proj[3 * i + 1];
+        std::vector<int> idx;
+        for (int j = 0; j < n; j++) {
+            const float distx = kun[2 * j] - x, disty = kun[2 * j + 1] - y;
+            if (fabsf(distx) < th && fabsf(disty) < th) idx.push_back(j);
+        }
+        if (idx.empty()) continue;
+        double best1 = std::numeric_limits<double>::max(), best2 = best1;
+        int lvl1 = -1, lvl2 = -1, bidx = -1;
+        for (int j : idx) {
+            if (taken[j]) continue;
+            const double d = (double)hamming32(L.desc, desc + 32 * (size_t)j);
+            if (d < best1) {
+                best2 = best1;
+                best1 = d;
+                lvl2 = lvl1;
+                lvl1 = octave[j];
+                bidx = j;
+            } else if (d < best2) {
+                lvl2 = octave[j];
+                best2 = d;
+            }
+        }
+        if (best1 <= TH_HIGH) {
+            if (lvl1 == lvl2 && best1 > nnratio * best2) continue;
+            slot_lm[bidx] = i;
+            taken[bidx] = (L.flags & ODO_LM_HAS_OBS) ? 1 : 0;
+            nmatches++;
+        }
+    }
+    return nmatches;
+}
+
 void oracle_knn2(const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* idx, int32_t* dist) {
     for (int i = 0; i < nq; i++) {
         int nidx[2] = {-1, -1};

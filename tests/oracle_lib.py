@@ -20,6 +20,7 @@ class OrbKP(C.Structure):
                 ("response", C.c_float), ("octave", C.c_int32), ("class_id", C.c_int32)]
 
 
+LANDMARK_DTYPE = np.dtype([("X", "<f4", 3), ("flags", "<i4"), ("desc", "u1", 32)])
 HYP_DTYPE = np.dtype([("err", "<f8"), ("cnt", "<i4"), ("pad", "<i4"), ("T", "<f4", 12)])
 KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
                      ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
@@ -109,6 +110,9 @@ def lib():
             "oracle_track_pair": (C.c_int, [P, P, P, C.c_int, P, P, P, P, P, C.c_int, P, C.c_float, P,
                                             C.c_uint32, P, P, P, P, C.c_int]),
             "oracle_adaptive_default": (None, [P]),
+            "oracle_image_bounds": (None, [P, C.c_int, C.c_int, P]),
+            "oracle_projection_match": (C.c_int, [P, P, C.c_int, P, P, P, C.c_int, P, P, P, C.c_float, C.c_float,
+                                                  P, P]),
             "oracle_ransac_hyps": (C.c_int, [P, C.c_int, P, P, P, P, P, C.c_int, C.c_int, P]),
             "oracle_adaptive_detect": (C.c_int, [P, C.c_int, C.c_int, P, P, P, C.c_int, P]),
             "oracle_fast_roi": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, P, C.c_int]),
