@@ -121,6 +121,8 @@ SIGNATURES = {
     "odo_set_adaptive_thresholds": (C.c_int, [P, P, C.c_int]),
     "odo_debug_select": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, P, P]),
     "odo_image_bounds": (C.c_int, [P, P]),
+    "odo_chain_poses": (C.c_int, [P, C.c_int, P, P]),
+    "odo_write_tum_trajectory": (C.c_int, [C.c_char_p, P, P, C.c_int, C.c_int]),
     "odo_projection_match": (C.c_int, [P, P, P, C.c_int, P, P, P, C.c_int, P, C.c_float, C.c_float, P, P, P]),
     "odo_ransac_hyps": (C.c_int, [P, P, C.c_int, P, C.c_int, P, C.c_int, P, P, P, C.c_int, C.c_int, P, P]),
     "odo_ransac_fold": (C.c_int, [P, C.c_int, C.c_int, P, P]),

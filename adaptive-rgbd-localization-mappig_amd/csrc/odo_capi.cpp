@@ -1818,6 +1818,73 @@ int odo_projection_match(odo_ctx* c, const float Tcw[16], const odo_landmark* lm
     return ODO_OK;
 }
 
+int odo_chain_poses(const odo_pair_result* res, int n, const float Tcw_prev[16], float* out) {
+    if (!res || n < 0 || !out) return fail(ODO_ERR_ARG, "bad chain args");
+    double T[16];
+    for (int k = 0; k < 16; k++) T[k] = Tcw_prev ? (double)Tcw_prev[k] : (k % 5 == 0 ? 1.0 : 0.0);
+    for (int i = 0; i < n; i++) {
+        if (!(i == 0 && res[i].n_matches == 0)) {
+            double R[16], M[16];
+            for (int k = 0; k < 16; k++) R[k] = (double)res[i].Tcw[k];
+            for (int r = 0; r < 4; r++)
+                for (int c2 = 0; c2 < 4; c2++)
+                    M[4 * r + c2] = ((R[4 * r] * T[c2] + R[4 * r + 1] * T[4 + c2]) + R[4 * r + 2] * T[8 + c2]) +
+                                    R[4 * r + 3] * T[12 + c2];
+            memcpy(T, M, sizeof(T));
+        }
+        for (int k = 0; k < 16; k++) out[16 * i + k] = (float)T[k];
+    }
+    return ODO_OK;
+}
+
+// Eigen::Quaterniond(Matrix3d) (quaternionbase_assign_impl), host restatement
+static void quat_from_rot(const double m[3][3], double q[4] /* x y z w */) {
+    double t = m[0][0] + m[1][1] + m[2][2];
+    if (t > 0) {
+        t = sqrt(t + 1.0);
+        q[3] = 0.5 * t;
+        t = 0.5 / t;
+        q[0] = (m[2][1] - m[1][2]) * t;
+        q[1] = (m[0][2] - m[2][0]) * t;
+        q[2] = (m[1][0] - m[0][1]) * t;
+    } else {
+        int i = 0;
+        if (m[1][1] > m[0][0]) i = 1;
+        if (m[2][2] > m[i][i]) i = 2;
+        const int j = (i + 1) % 3, k = (j + 1) % 3;
+        t = sqrt(m[i][i] - m[j][j] - m[k][k] + 1.0);
+        q[i] = 0.5 * t;
+        t = 0.5 / t;
+        q[3] = (m[k][j] - m[j][k]) * t;
+        q[j] = (m[j][i] + m[i][j]) * t;
+        q[k] = (m[k][i] + m[i][k]) * t;
+    }
+}
+
+int odo_write_tum_trajectory(const char* path, const double* ts, const float* Tcw, int n, int append) {
+    if (!path || n < 0 || (n && (!ts || !Tcw))) return fail(ODO_ERR_ARG, "bad trajectory args");
+    FILE* f = fopen(path, append ? "a" : "w");
+    if (!f) return fail(ODO_ERR_ARG, std::string("cannot open ") + path);
+    for (int i = 0; i < n; i++) {
+        const float* T = Tcw + 16 * i;
+        // Rwc = Rcw^T; twc = -Rwc * tcw (cv::Mat float, double accumulation)
+        float Rwc[3][3];
+        for (int r = 0; r < 3; r++)
+            for (int c2 = 0; c2 < 3; c2++) Rwc[r][c2] = T[4 * c2 + r];
+        float twc[3];
+        for (int r = 0; r < 3; r++)
+            twc[r] = (float)(((double)-Rwc[r][0] * T[3] + (double)-Rwc[r][1] * T[7]) + (double)-Rwc[r][2] * T[11]);
+        double m[3][3], q[4];
+        for (int r = 0; r < 3; r++)
+            for (int c2 = 0; c2 < 3; c2++) m[r][c2] = (double)Rwc[r][c2];
+        quat_from_rot(m, q);
+        fprintf(f, "%.6f %.9f %.9f %.9f %.9f %.9f %.9f %.9f\n", ts[i], twc[0], twc[1], twc[2], (float)q[0],
+                (float)q[1], (float)q[2], (float)q[3]);
+    }
+    fclose(f);
+    return ODO_OK;
+}
+
 int odo_kabsch(const float* A, const float* B, int n, float T[16]) {
     if (n < 0 || (n && (!A || !B)) || !T) return fail(ODO_ERR_ARG, "bad kabsch args");
     int ndev = 0;

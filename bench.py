@@ -172,7 +172,7 @@ def main():
     L = min(args.seq_len, B)
     if B % L:
         raise SystemExit(f"--batch {B} must be a multiple of --seq-len {L} (pair 0 links frame B-1 to frame 0)")
-    bgr, dep, _ = synth.make_sequence(L, W, H, seed=scene_seed, closed_loop=True)
+    bgr, dep, gt_poses = synth.make_sequence(L, W, H, seed=scene_seed, closed_loop=True)
     if B != L:
         bgr, dep = bgr[np.arange(B) % L], dep[np.arange(B) % L]
     d_bgr = torch.from_numpy(bgr).to("cuda")
@@ -220,6 +220,12 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
 
     nkp = [len(odo.frame(i)["kps"]) for i in range(B)]
+    # quality sanity: the untimed first batch's chained poses against the
+    # sequence's ground truth (absolute trajectory error, TUM definition)
+    from importlib import import_module
+    tj = import_module("arlm_amd.trajectory")
+    Tcw = tj.chain_poses(res[:L], np.linalg.inv(gt_poses[0]).astype(np.float32))
+    ate_mm = 1000.0 * tj.ate_rmse(tj.camera_centres(Tcw), gt_poses[:L, :3, 3])
     nkp_mean = float(np.mean(nkp))
     # Roofline of the Hamming-match kernel (k_knn2), the kernel the north star
     # names. Brute-force kNN-2 re-reads each 32-byte descriptor ~2000 times from
@@ -276,7 +282,8 @@ def main():
                        "mean_keypoints": round(nkp_mean, 1),
                        "mean_matches": round(float(np.mean(ok["n_matches"])), 1),
                        "mean_ransac_inliers": round(float(np.mean(ok["n_inliers"])), 1),
-                       "mean_ransac_visited": round(float(np.mean(ok["visited"])), 1)},
+                       "mean_ransac_visited": round(float(np.mean(ok["visited"])), 1),
+                       "ate_mm": round(ate_mm, 3)},
             "stage_ms": {k: round(v, 4) for k, v in timings.items()},
             "host_submit_ms_per_step": round(submit / args.steps * 1e3, 3),
             "roofline": roofline,

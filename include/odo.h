@@ -142,6 +142,21 @@ int odo_ransac_hyps_finish(odo_ctx* ctx, const odo_ransac_fold_result* r, odo_rn
 int odo_pnp_motion_ba(odo_ctx* ctx, const float* Xw, const float* obs, int n, const odo_calib* calib,
                       const float Tcw_init[16], float Tcw_out[16], uint8_t* outlier, int* n_inliers);
 
+/* ---- Trajectory (host only) ----
+ * Relative-pose chain of the batched contract: results[i].Tcw is frame i's
+ * pose in frame i-1's camera coordinates, so Tcw(i) = Tcw_rel(i) * Tcw(i-1)
+ * (Odometry::Compute's Tcw2 = T12 * Tcw1, odometry.cpp:110-112), starting
+ * from Tcw_prev (the last pose of the previous batch; identity for a new
+ * sequence). Pairs without a predecessor (n_matches == 0 at i == 0 of a
+ * sequence) keep Tcw_prev. 4x4 row-major floats; products in double. */
+int odo_chain_poses(const odo_pair_result* results, int n, const float Tcw_prev[16], float* Tcw_out);
+/* Tracking::SaveTrajectory's line format (tracking.cpp:544-582): "timestamp
+ * tx ty tz qx qy qz qw" of the camera centre twc = -Rcw^T tcw and
+ * Converter::toQuaternion(Rwc) (Eigen Quaterniond from the double matrix,
+ * converter.cpp:149-161), std::fixed with 6 / 9 decimals. append: 0 = new
+ * file. */
+int odo_write_tum_trajectory(const char* path, const double* timestamps, const float* Tcw, int n, int append);
+
 /* Frame::ComputeImageBounds (frame.cpp:315-349) for the context's calibration
  * and image size: undistorted corners -> minX, maxX, minY, maxY. Host only. */
 int odo_image_bounds(odo_ctx* ctx, float bounds[4]);
