@@ -20,6 +20,8 @@
 // The TFC recurrence and the meanError sum are order-dependent float/double
 // folds; they run in match order, bit-identical to the reference.
 #include <algorithm>
+#include <map>
+#include <mutex>
 #include <cstdlib>
 #include <vector>
 
@@ -212,39 +214,113 @@ ODO_INLINE void ring_at(const uint32_t* raw, const RState* S, int N, Rng& R) {
     R.f = (R.r + 3) % 31;
 }
 
-#define RAW_CHUNK 2048
+// The generator words x_n = x_{n-31} + x_{n-3} (mod 2^32) are a linear map of
+// the 31-word state, so instead of one lane producing all rawcap words in
+// sequence, lane k jumps to word k*L with a host-built matrix A^(kL) and
+// produces its own L words (the 310 seeding discards jump too: A^310).
+// Same words, bit for bit; ~150 us of serial generation becomes a 31x31
+// matrix-vector product plus L steps per lane.
+#define RAW_LANES 64
 
-__global__ void __launch_bounds__(64) k_ransac_raw(RansacBufs B, uint64_t seed_base, uint64_t pair_base) {
+// state vector, oldest word first, from / to the ring (slot r = x_{n-3})
+ODO_INLINE void ring_to_vec(const int32_t* st, int r, uint32_t* v) {
+    for (int m = 0; m < 28; m++) v[m] = (uint32_t)st[(r + 3 + m) % 31];
+    for (int m = 0; m < 3; m++) v[28 + m] = (uint32_t)st[(r + m) % 31];
+}
+ODO_INLINE void vec_to_ring(const uint32_t* v, int r, int32_t* st) {
+    for (int m = 0; m < 28; m++) st[(r + 3 + m) % 31] = (int32_t)v[m];
+    for (int m = 0; m < 3; m++) st[(r + m) % 31] = (int32_t)v[28 + m];
+}
+
+// jump: [RAW_LANES][31][31] stored as [i][j][lane] (lane k: A^(k*L)), then
+// A^310 as [31][31]
+__global__ void __launch_bounds__(64) k_ransac_raw(RansacBufs B, uint64_t seed_base, uint64_t pair_base,
+                                                   const uint32_t* __restrict__ jump, int L) {
     const int p = blockIdx.x;
     const int lane = threadIdx.x;
     __shared__ int32_t s_st[31], s_fr[2];
-    __shared__ __align__(16) uint32_t s_buf[RAW_CHUNK];
+    __shared__ uint32_t s_v[31], s_w[31];
     if (lane == 0) {
         if (B.rng_io) {
             for (int i = 0; i < 31; i++) s_st[i] = B.rng_io->state[i];
             s_fr[0] = B.rng_io->fpos;
             s_fr[1] = B.rng_io->rpos;
         } else {
-            seed_ring(pair_seed(seed_base, pair_base + (uint64_t)p), s_st, s_fr);
+            // __srandom_r: Schrage fill (f = 3, r = 0), discards below
+            uint32_t seedv = pair_seed(seed_base, pair_base + (uint64_t)p);
+            if (seedv == 0) seedv = 1;
+            s_st[0] = (int32_t)seedv;
+            int32_t word = (int32_t)seedv;
+            for (int i = 1; i < 31; ++i) {
+                const long hi = word / 127773;
+                const long lo = word % 127773;
+                long w2 = 16807 * lo - 2836 * hi;
+                if (w2 < 0) w2 += 2147483647;
+                word = (int32_t)w2;
+                s_st[i] = word;
+            }
+            s_fr[0] = 3;
+            s_fr[1] = 0;
         }
+        ring_to_vec(s_st, s_fr[1], s_v);
     }
     lds_sync();
+    if (!B.rng_io) {
+        // 310 discards: v <- A^310 v (row `lane` per lane); r advances 310 % 31 = 0
+        const uint32_t* D = jump + (size_t)RAW_LANES * 31 * 31;
+        if (lane < 31) {
+            uint32_t a = 0;
+            for (int j = 0; j < 31; j++) a += D[lane * 31 + j] * s_v[j];
+            s_w[lane] = a;
+        }
+        lds_sync();
+        if (lane < 31) s_v[lane] = s_w[lane];
+        lds_sync();
+        if (lane == 0) vec_to_ring(s_v, s_fr[1], s_st);
+        lds_sync();
+    }
     RState* S = B.st + p;
     if (lane < 31) S->rng0_s[lane] = s_st[lane];
     if (lane == 0) {
         S->rng0_f = s_fr[0];
         S->rng0_r = s_fr[1];
     }
-    uint32_t* out = B.raw + (size_t)p * B.rawcap;
-    int32_t f = s_fr[0], r = s_fr[1];
-    for (int o = 0; o < B.rawcap; o += RAW_CHUNK) {
-        const int n = min(RAW_CHUNK, B.rawcap - o);
-        if (lane == 0) gen_raw(s_st, f, r, s_buf, n);
-        lds_sync();
-        for (int i = lane * 4; i < n; i += 256)
-            *reinterpret_cast<uint4*>(out + o + i) = *reinterpret_cast<const uint4*>(s_buf + i);
-        lds_sync();
+    // lane k: state at word k*L, then words [kL, kL + L)
+    uint32_t reg[31];
+    {
+        uint32_t v[31];
+#pragma unroll
+        for (int i = 0; i < 31; i++) {
+            uint32_t a = 0;
+            if (lane == 0) a = s_v[i];
+            else
+                for (int j = 0; j < 31; j++) a += jump[((size_t)i * 31 + j) * RAW_LANES + lane] * s_v[j];
+            v[i] = a;
+        }
+        // ring registers as gen_raw holds them: reg[0..2] = x_{n-3..n-1}, reg[3..30] = x_{n-31..n-4}
+#pragma unroll
+        for (int m = 0; m < 28; m++) reg[3 + m] = v[m];
+#pragma unroll
+        for (int m = 0; m < 3; m++) reg[m] = v[28 + m];
     }
+    uint32_t* out = B.raw + (size_t)p * B.rawcap;
+    const int k0 = lane * L;
+    const int n = max(0, min(L, B.rawcap - k0));
+    int produced = 0;
+    while (produced + 31 <= n) {
+#pragma unroll
+        for (int j = 0; j < 31; j++) {
+            reg[(j + 3) % 31] += reg[j];
+            out[k0 + produced + j] = reg[(j + 3) % 31];
+        }
+        produced += 31;
+    }
+#pragma unroll
+    for (int j = 0; j < 31; j++)
+        if (produced + j < n) {
+            reg[(j + 3) % 31] += reg[j];
+            out[k0 + produced + j] = reg[(j + 3) % 31];
+        }
 }
 
 // ---------------------------------------------------------------- sampling
@@ -1100,11 +1176,65 @@ static RansacBufs carve(void* scratch, int npairs, int match_cap, int mask_words
     return B;
 }
 
+// A^k of the generator's 31x31 transition (mod 2^32), host side
+typedef std::vector<uint32_t> Mat31;
+static Mat31 mat_mul31(const Mat31& X, const Mat31& Y) {
+    Mat31 Z(31 * 31, 0);
+    for (int i = 0; i < 31; i++)
+        for (int k = 0; k < 31; k++) {
+            const uint32_t x = X[i * 31 + k];
+            if (!x) continue;
+            for (int j = 0; j < 31; j++) Z[i * 31 + j] += x * Y[k * 31 + j];
+        }
+    return Z;
+}
+static Mat31 mat_pow31(long e) {
+    Mat31 A(31 * 31, 0), R(31 * 31, 0);
+    for (int i = 0; i < 30; i++) A[i * 31 + i + 1] = 1;  // shift
+    A[30 * 31 + 0] = 1;                                  // x_n = x_{n-31} + x_{n-3}
+    A[30 * 31 + 28] = 1;
+    for (int i = 0; i < 31; i++) R[i * 31 + i] = 1;
+    while (e > 0) {
+        if (e & 1) R = mat_mul31(R, A);
+        A = mat_mul31(A, A);
+        e >>= 1;
+    }
+    return R;
+}
+
+// device jump tables per (device, L): [i][j][lane] A^(lane*L), then A^310
+static const uint32_t* raw_jump_tables(int L) {
+    static std::mutex mu;
+    static std::map<std::pair<int, int>, uint32_t*> cache;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find({dev, L});
+    if (it != cache.end()) return it->second;
+    std::vector<uint32_t> h((size_t)RAW_LANES * 961 + 961);
+    const Mat31 AL = mat_pow31(L);
+    Mat31 M(31 * 31, 0);
+    for (int i = 0; i < 31; i++) M[i * 31 + i] = 1;
+    for (int k = 0; k < RAW_LANES; k++) {
+        for (int i = 0; i < 31; i++)
+            for (int j = 0; j < 31; j++) h[((size_t)i * 31 + j) * RAW_LANES + k] = M[i * 31 + j];
+        M = mat_mul31(AL, M);
+    }
+    const Mat31 D = mat_pow31(310);
+    std::copy(D.begin(), D.end(), h.begin() + (size_t)RAW_LANES * 961);
+    uint32_t* d = nullptr;
+    if (hipMalloc(&d, h.size() * 4) != hipSuccess) return nullptr;
+    (void)hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice);
+    cache[{dev, L}] = d;
+    return d;
+}
+
 void launch_ransac_raw(hipStream_t st, void* scratch, int npairs, int match_cap, int mask_words, RansacCfg cfg,
                        uint64_t seed_base, uint64_t pair_base, odo_rng* rng_io) {
     RansacBufs B = carve(scratch, npairs, match_cap, mask_words, cfg);
     B.rng_io = rng_io;
-    hipLaunchKernelGGL(k_ransac_raw, dim3(npairs), dim3(64), 0, st, B, seed_base, pair_base);
+    const int L = (B.rawcap + RAW_LANES - 1) / RAW_LANES;
+    hipLaunchKernelGGL(k_ransac_raw, dim3(npairs), dim3(64), 0, st, B, seed_base, pair_base, raw_jump_tables(L), L);
 }
 
 static int ev2_rows() {

@@ -165,7 +165,8 @@ struct odo_ctx {
     //     with its batch's PnP): all slower than 2 in A/B runs (5: 1.99 ms).
     int sched = 2;
     // ODO_SKIP (measurement only; results are invalid when set): bit 0 skips
-    // the PnP launches, bit 1 RANSAC part 2, bit 2 every pair stage, bit 3 kNN-2
+    // the PnP launches, bit 1 RANSAC part 2, bit 2 every pair stage, bit 3 kNN-2,
+    // bit 4 RANSAC (schedule 2)
     int skip = 0;
     // ADAPTIVE grid extractor (ODO_DETECTOR_ADAPTIVE_FAST): cell / band
     // tables and per-batch scratch (extraction stream only), plus the
@@ -899,6 +900,7 @@ static int run_pairs(odo_ctx* c, int set, int n) {
         // both RANSAC launches on the pair stream, then one PnP launch for the
         // whole batch on its own stream (the pair stream moves on to the next
         // batch while it runs)
+        if (!(c->skip & 16))
         launch_ransac(st, P.good, P.n_good, P.n_matches, P.matches, xyz, c->kp_cap, 0, c->match_cap, c->rcfg,
                       c->latch, P.pair_valid, 20, nullptr, c->rscr[set], P.best_mask, c->mask_words, P.res, P.T12, n,
                       0, P.pair_phase);
