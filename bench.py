@@ -242,7 +242,11 @@ def main():
         traffic = None
         if os.path.exists(KNN_TRAFFIC):
             with open(KNN_TRAFFIC) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
+                tr = json.load(f)
+            # PMC-measured HBM bytes (FETCH_SIZE x2 + WRITE_SIZE) per launch;
+            # scaled per pair when this run's batch differs from the profiled one
+            traffic = tr.get("hbm_bytes_per_launch") if tr.get("batch") == B else \
+                (tr["hbm_bytes_per_pair"] * B if "hbm_bytes_per_pair" in tr else None)
         roofline = {"bound": "valu", "achieved": round(ach, 3), "peak": round(INT_VALU_PEAK_TOPS, 2),
                     "unit": "Top/s", "frac": round(ach / INT_VALU_PEAK_TOPS, 4), "traffic": traffic,
                     "kernel": "k_knn2", "kernel_ms": round(knn_ms, 4), "launches": knn_launches,
