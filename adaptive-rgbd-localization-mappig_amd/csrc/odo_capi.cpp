@@ -83,6 +83,7 @@ struct odo_ctx {
     hipStream_t pstream = nullptr;  // pair stages
     hipStream_t pstream2 = nullptr;  // pair stages of odd batches (schedule 5)
     hipStream_t cur_p = nullptr;     // pair stream of the batch being queued
+    std::vector<hipStream_t> owned;  // streams created (the rest alias them)
     hipEvent_t ev_latch = nullptr;   // after the last queued k_latch (schedule 5)
     bool latch_rec = false;
     uint64_t batch_counter = 0;
@@ -153,17 +154,19 @@ struct odo_ctx {
     bool pdone_rec[NSETS] = {};
     bool serial = false;
     bool timing = false;
-    // stream layout (ODO_SCHED), measured on MI355X at 64-frame batches:
-    // 2 (default) = extraction | side (rand() words) | pair stages (match +
-    //     both RANSAC launches) | one PnP launch per batch: 1.37 ms per step;
-    // 1 = as 2 but two PnP launches on two streams (pairs finished by RANSAC
-    //     part 1 start early): 1.38 ms - the two PnP streams share a hardware
-    //     queue (GPU_MAX_HW_QUEUES=4) and serialise;
-    // 0 = as 2 with the words at the end of the extraction stream: 1.59 ms;
-    // 3 = kNN-2 and the words on the side stream, 4 = the words at the head
-    //     of the pair stream, 5 = two pair streams alternating batches (each
-    //     with its batch's PnP): all slower than 2 in A/B runs (5: 1.99 ms).
-    int sched = 2;
+    // stream layout (ODO_SCHED). Only the streams a schedule uses are created:
+    // every stream beyond the process's GPU_MAX_HW_QUEUES (4) hardware queues
+    // shares one with another stream and serialises behind it.
+    // 5 (default) = extraction (+ kNN-2) | two pair streams taking alternate
+    //     batches, each running its batch's rand() words, match, RANSAC and
+    //     PnP, so one batch's long RANSAC/PnP overlaps the next batch's pair
+    //     stages (the DepthCovariance latch kernels are ordered by an event):
+    //     52.9k frames/s at 128-frame batches;
+    // 2 = extraction | side (words) | pair stages | one PnP stream: 42.1k;
+    // 1 = as 2 with two PnP launches on two streams: 41.9k;
+    // 0 = words on the extraction stream; 3 = kNN-2 + words on the side
+    //     stream; 4 = words at the head of the pair stream.
+    int sched = 5;
     // ODO_SKIP (measurement only; results are invalid when set): bit 0 skips
     // the PnP launches, bit 1 RANSAC part 2, bit 2 every pair stage, bit 3 kNN-2,
     // bit 4 RANSAC (schedule 2)
@@ -217,12 +220,7 @@ static int pair_stream_priority() {
 }
 
 static int sync_all(odo_ctx* c) {
-    HIPCHK(hipStreamSynchronize(c->stream));
-    HIPCHK(hipStreamSynchronize(c->side));
-    HIPCHK(hipStreamSynchronize(c->pstream));
-    if (c->pstream2) HIPCHK(hipStreamSynchronize(c->pstream2));
-    HIPCHK(hipStreamSynchronize(c->pnpa));
-    HIPCHK(hipStreamSynchronize(c->pnpb));
+    for (hipStream_t st : c->owned) HIPCHK(hipStreamSynchronize(st));
     return ODO_OK;
 }
 
@@ -258,15 +256,8 @@ static void free_ctx(odo_ctx* c) {
         if (c->ev_xdone[i]) hipEventDestroy(c->ev_xdone[i]);
         if (c->ev_raw[i]) hipEventDestroy(c->ev_raw[i]);
     }
-    if (!c->serial) {
-        if (c->pnpa) hipStreamDestroy(c->pnpa);
-        if (c->pnpb) hipStreamDestroy(c->pnpb);
-        if (c->side) hipStreamDestroy(c->side);
-        if (c->pstream) hipStreamDestroy(c->pstream);
-        if (c->pstream2) hipStreamDestroy(c->pstream2);
-        if (c->ev_latch) hipEventDestroy(c->ev_latch);
-    }
-    if (c->stream) hipStreamDestroy(c->stream);
+    if (c->ev_latch) hipEventDestroy(c->ev_latch);
+    for (hipStream_t st : c->owned) hipStreamDestroy(st);
     delete c;
 }
 
@@ -648,20 +639,27 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
     c->serial = ser && ser[0] == '1';
     if (const char* sk = getenv("ODO_SKIP")) c->skip = atoi(sk);
     if (const char* sc = getenv("ODO_SCHED")) c->sched = atoi(sc);
-    bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
-              (c->serial || (hipStreamCreateWithPriority(&c->pstream, hipStreamNonBlocking, pair_stream_priority()) ==
-                                 hipSuccess &&
-                             hipStreamCreateWithPriority(&c->pnpa, hipStreamNonBlocking, pair_stream_priority()) ==
-                                 hipSuccess &&
-                             hipStreamCreateWithPriority(&c->pnpb, hipStreamNonBlocking, pair_stream_priority()) ==
-                                 hipSuccess &&
-                             hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) == hipSuccess));
+    // only the streams the schedule uses (each extra stream shares one of the
+    // process's GPU_MAX_HW_QUEUES hardware queues with another and serialises
+    // against it); the others alias
+    auto mk = [&](hipStream_t* s, bool prio) {
+        const bool r = prio ? hipStreamCreateWithPriority(s, hipStreamNonBlocking, pair_stream_priority()) == hipSuccess
+                            : hipStreamCreateWithFlags(s, hipStreamNonBlocking) == hipSuccess;
+        if (r) c->owned.push_back(*s);
+        return r;
+    };
+    bool ok = mk(&c->stream, false);
     if (ok && c->serial) {
-        c->pstream = c->stream;
-        c->pstream2 = c->stream;
-        c->side = c->stream;
-        c->pnpa = c->stream;
-        c->pnpb = c->stream;
+        c->pstream = c->pstream2 = c->side = c->pnpa = c->pnpb = c->stream;
+    } else if (ok && c->sched == 5) {
+        ok = mk(&c->pstream, true) && mk(&c->pstream2, true);
+        c->side = c->pnpa = c->pnpb = c->pstream;
+    } else if (ok) {
+        ok = mk(&c->pstream, true) && mk(&c->pnpa, true) && (c->sched == 0 || mk(&c->side, false)) &&
+             (c->sched != 1 || mk(&c->pnpb, true));
+        if (c->sched == 0) c->side = c->stream;
+        if (c->sched != 1) c->pnpb = c->pnpa;
+        c->pstream2 = c->pstream;
     }
     for (int i = 0; i < NSETS && ok; i++)
         ok = hipEventCreateWithFlags(&c->ev_ra[i], hipEventDisableTiming) == hipSuccess &&
@@ -671,9 +669,7 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
     for (int i = 0; i < NSETS && ok; i++)
         ok = hipEventCreateWithFlags(&c->ev_xdone[i], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&c->ev_raw[i], hipEventDisableTiming) == hipSuccess;
-    if (ok && !c->serial)
-        ok = hipStreamCreateWithFlags(&c->pstream2, hipStreamNonBlocking) == hipSuccess &&
-             hipEventCreateWithFlags(&c->ev_latch, hipEventDisableTiming) == hipSuccess;
+    if (ok) ok = hipEventCreateWithFlags(&c->ev_latch, hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         fail(ODO_ERR_DEVICE, "hipStreamCreate failed");
         free_ctx(c);
