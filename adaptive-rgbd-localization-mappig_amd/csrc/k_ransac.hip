@@ -83,6 +83,8 @@ struct RansacBufs {
     float* T12;
     // hypotheses mode: evaluate only [h_lo, h_hi), no fold
     int h_lo, h_hi, no_fold;
+    int* open_list;  // [pair] pairs still folding after the first launch
+    int* open_cnt;   // [0] their count, [1] the second launch's work counter
 };
 
 ODO_INLINE int ld_relaxed(const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
@@ -783,7 +785,7 @@ ODO_INLINE void try_fold(const RansacBufs& B, const RansacCfg& cfg, int p) {
 
 template <bool CACHED>
 ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int wave, int lane, EvalLds& L,
-                          const GoodPt* P, int ng, int words, int H, int y0, int hlim) {
+                          const GoodPt* P, int ng, int words, int H, int y0, int hlim, int yrow, int ystride) {
     RState* S = B.st + p;
     const int* smp0 = B.samples + (size_t)p * B.hcap * SREC;
     const TfcSlab TS{reinterpret_cast<float*>(ev_dyn + PCACHE * sizeof(GoodPt)) + (size_t)wave * 8 * TFC_CAP};
@@ -796,7 +798,7 @@ ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int 
     // this launch covers hypothesis rows [y0, y0 + gridDim.y)
     // this launch's waves stride over hypotheses [y0*EV_WAVES, hlim)
     const int hend = min(H, hlim);
-    for (int h = (y0 + blockIdx.y) * EV_WAVES + wave; h < hend; h += gridDim.y * EV_WAVES) {
+    for (int h = (y0 + yrow) * EV_WAVES + wave; h < hend; h += ystride * EV_WAVES) {
         if (h < B.h_lo || h >= B.h_hi) continue;  // hypotheses mode: another rank's range
         const int* smp = smp0 + (size_t)h * SREC;
         double refinedError = 1e6;
@@ -987,9 +989,66 @@ __global__ void __launch_bounds__(64 * EV_WAVES, EV_MIN_BLOCKS) k_ransac_eval(Ra
         GoodPt* pc = reinterpret_cast<GoodPt*>(ev_dyn);
         for (int k = threadIdx.x; k < ng; k += 64 * EV_WAVES) pc[k] = P[k];
         __syncthreads();
-        eval_hyps<true>(B, cfg, p, wave, lane, s_w[wave], P, ng, words, H, y0, hlim);
+        eval_hyps<true>(B, cfg, p, wave, lane, s_w[wave], P, ng, words, H, y0, hlim, blockIdx.y, gridDim.y);
     } else {
-        eval_hyps<false>(B, cfg, p, wave, lane, s_w[wave], P, ng, words, H, y0, hlim);
+        eval_hyps<false>(B, cfg, p, wave, lane, s_w[wave], P, ng, words, H, y0, hlim, blockIdx.y, gridDim.y);
+    }
+}
+
+// The pairs still folding after the first launch, in pair order, and a work
+// counter for the second launch (one workgroup).
+__global__ void __launch_bounds__(256) k_ransac_open(RansacBufs B, int npairs) {
+    __shared__ int s_base;
+    if (threadIdx.x == 0) s_base = 0;
+    __syncthreads();
+    for (int p0 = 0; p0 < npairs; p0 += 256) {
+        const int p = p0 + (int)threadIdx.x;
+        const bool open = p < npairs && !ld_relaxed(&B.st[p].done);
+        const uint64_t bal = __ballot(open);
+        __shared__ int s_cnt[4];
+        if ((threadIdx.x & 63) == 0) s_cnt[threadIdx.x >> 6] = __popcll(bal);
+        __syncthreads();
+        int before = 0, tot = 0;
+        for (int w = 0; w < 4; w++) {
+            if (w < (int)(threadIdx.x >> 6)) before += s_cnt[w];
+            tot += s_cnt[w];
+        }
+        if (open) B.open_list[s_base + before + (int)lane_rank(bal)] = p;
+        __syncthreads();
+        if (threadIdx.x == 0) s_base += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        B.open_cnt[0] = s_base;
+        B.open_cnt[1] = 0;  // work counter
+    }
+}
+
+// Second launch as a work list: a fixed grid of workgroups takes (row, open
+// pair) items in row-major order (lower hypotheses first) from an atomic
+// counter, 4 hypotheses per item - no launch-sized crowd of early-exit
+// workgroups for the pairs that already broke.
+__global__ void __launch_bounds__(64 * EV_WAVES, EV_MIN_BLOCKS) k_ransac_eval_list(RansacBufs B, RansacCfg cfg, int y0,
+                                                                                   int rows) {
+    __builtin_amdgcn_s_setprio(ODO_WAVE_PRIO);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __shared__ EvalLds s_w[EV_WAVES];
+    __shared__ int s_item;
+    const int cnt = B.open_cnt[0];
+    const int total = cnt * rows;
+    while (true) {
+        __syncthreads();
+        if (threadIdx.x == 0) s_item = atomicAdd(&B.open_cnt[1], 1);
+        __syncthreads();
+        const int item = s_item;
+        if (item >= total) break;
+        const int row = item / cnt, p = B.open_list[item - row * cnt];
+        RState* S = B.st + p;
+        const int H = S->H;
+        if ((y0 + row) * EV_WAVES >= H || ld_relaxed(&S->done)) continue;  // uniform per item
+        const GoodPt* P = B.gpts + (size_t)p * B.match_cap;
+        eval_hyps<false>(B, cfg, p, wave, lane, s_w[wave], P, S->ng, S->words, H, y0 + row,
+                         (y0 + row + 1) * EV_WAVES, 0, 1);
     }
 }
 
@@ -1131,7 +1190,7 @@ static int ransac_rawcap(const RansacCfg& cfg) {
 }
 
 struct Layout {
-    size_t gpts, st, hyp, samples, ready, masks, raw, total;
+    size_t gpts, st, hyp, samples, ready, masks, raw, open, total;
 };
 
 static Layout layout(int npairs, int match_cap, int mask_words, const RansacCfg& cfg) {
@@ -1153,6 +1212,8 @@ static Layout layout(int npairs, int match_cap, int mask_words, const RansacCfg&
     o = al(o + (size_t)npairs * hc * mask_words * 4);
     L.raw = o;
     o = al(o + (size_t)npairs * ransac_rawcap(cfg) * 4);
+    L.open = o;
+    o = al(o + (size_t)(npairs + 2) * 4);
     L.total = o;
     return L;
 }
@@ -1171,6 +1232,8 @@ static RansacBufs carve(void* scratch, int npairs, int match_cap, int mask_words
     B.samples = (int*)(s + L.samples);
     B.ready = (int*)(s + L.ready);
     B.masks = (uint32_t*)(s + L.masks);
+    B.open_list = (int*)(s + L.open);
+    B.open_cnt = B.open_list + npairs;
     B.raw = (uint32_t*)(s + L.raw);
     B.hcap = ransac_hcap(cfg);
     B.rawcap = ransac_rawcap(cfg);
@@ -1252,10 +1315,22 @@ static int ev2_rows() {
     return r;
 }
 
+// workgroups of the work-list second launch (ODO_EV2_LIST; 0 = the
+// (pairs x rows) grid instead)
+static int ev2_list() {
+    static int r = [] {
+        const char* e = getenv("ODO_EV2_LIST");
+        return e ? std::max(0, atoi(e)) : 512;
+    }();
+    return r;
+}
+
 static void ransac_eval_lds_attr() {
     static bool done = false;
     if (!done) {
         (void)hipFuncSetAttribute((const void*)k_ransac_eval, hipFuncAttributeMaxDynamicSharedMemorySize, (int)EV_LDS);
+        (void)hipFuncSetAttribute((const void*)k_ransac_eval_list, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)EV_LDS);
         done = true;
     }
 }
@@ -1317,9 +1392,16 @@ void launch_ransac(hipStream_t st, const void* good, const int* n_good, const in
     if (part != 1) {
         // the second launch's waves stride over the remaining hypotheses:
         // ev2_rows() rows of EV_WAVES per pair in flight (ODO_EV2_ROWS)
-        if (rows > r0)
-            hipLaunchKernelGGL(k_ransac_eval, dim3(npairs, std::min(rows - r0, ev2_rows())), dim3(64 * EV_WAVES), EV_LDS,
-                               st, B, cfg, r0, H);
+        if (rows > r0) {
+            if (ev2_list()) {
+                hipLaunchKernelGGL(k_ransac_open, dim3(1), dim3(256), 0, st, B, npairs);
+                hipLaunchKernelGGL(k_ransac_eval_list, dim3(ev2_list()), dim3(64 * EV_WAVES), EV_LDS, st, B, cfg, r0,
+                                   rows - r0);
+            } else {
+                hipLaunchKernelGGL(k_ransac_eval, dim3(npairs, std::min(rows - r0, ev2_rows())), dim3(64 * EV_WAVES),
+                                   EV_LDS, st, B, cfg, r0, H);
+            }
+        }
         hipLaunchKernelGGL(k_ransac_final, dim3(npairs), dim3(64), 0, st, B, cfg, part == 2 ? 2 : 0, phase);
     }
 }
