@@ -261,7 +261,7 @@ def main():
         nf = args.cpu_frames
         fps, dt = cpu_baseline(bgr, dep, args.nfeatures, args.iters, nf, adaptive)
         cpu = {"value": round(fps, 3), "unit": "frames/s", "cores": 1, "kind": "port",
-               "sample": f"{nf} frames (the rank-0 {B}-frame sequence, cycled) through the C++ oracle's "
+               "sample": f"{nf} frames (the rank-0 {L}-frame closed loop, cycled) through the C++ oracle's "
                          f"extract + match + RANSAC + PnP, single thread ({dt:.1f} s)"}
 
     if rank == 0:
