@@ -575,16 +575,15 @@ __global__ void __launch_bounds__(256) k_adapt_assemble(const uint32_t* __restri
 // ============================================================ finalize
 // Four keypoints per wave, 16 lanes each: rBRIEF (16 tests per lane, one
 // ballot per test group) at the fixed angle -1 deg (cos/sin precomputed on the
-// host in the reference's float arithmetic), then undistort + depth.
+// host in the reference's float arithmetic); undistort + depth follow in
+// k_kp_geometry (k_finalize.hip).
 #define AF_KPW 4
 #define AF_KPB (4 * AF_KPW)
 __global__ void __launch_bounds__(256) k_adapt_finalize(const uint8_t* __restrict__ blur, size_t pyr_stride, int pitch,
                                                         const uint32_t* __restrict__ akp, int akp_stride,
                                                         const int* __restrict__ nkp, float ca, float sb,
-                                                        const uint16_t* __restrict__ depth, size_t depth_stride,
-                                                        int img_w, FrameCalib cal, orb_kp* __restrict__ kps,
-                                                        uint8_t* __restrict__ desc, float* __restrict__ kun,
-                                                        float* __restrict__ xyz, float* __restrict__ ur, int kp_cap) {
+                                                        orb_kp* __restrict__ kps, uint8_t* __restrict__ desc,
+                                                        int kp_cap) {
     __shared__ uint64_t s_bal[4][16];
     const int f = blockIdx.y;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -627,8 +626,6 @@ __global__ void __launch_bounds__(256) k_adapt_finalize(const uint8_t* __restric
         kp->response = (float)((int)(key >> 24) - 1);  // cornerScore = S - 1
         kp->octave = 0;
         kp->class_id = -1;
-        kp_geometry(px, py, cal, depth + (size_t)f * depth_stride, img_w, kun + ((size_t)f * kp_cap + idx) * 2,
-                    xyz + ((size_t)f * kp_cap + idx) * 3, ur + (size_t)f * kp_cap + idx);
     }
 }
 
@@ -711,7 +708,8 @@ void launch_adapt_finalize(hipStream_t st, const uint8_t* blur, size_t pyr_strid
                            float* xyz, float* ur, int kp_cap, int nframes) {
     dim3 g((kp_cap + AF_KPB - 1) / AF_KPB, nframes);
     hipLaunchKernelGGL(k_adapt_finalize, g, dim3(256), 0, st, blur, pyr_stride, pitch, akp, akp_stride, nkp, ca, sb,
-                       depth, depth_stride, img_w, cal, kps, desc, kun, xyz, ur, kp_cap);
+                       kps, desc, kp_cap);
+    launch_kp_geometry(st, kps, nkp, depth, depth_stride, img_w, cal, kun, xyz, ur, kp_cap, nframes);
 }
 
 void launch_adapt_select_dbg(hipStream_t st, uint32_t* a, int n, int nth, int mode, int* posL, int* posR,

@@ -7,16 +7,12 @@
 //   k_fast_cells  FAST-9/16 + NMS per 30px cell       orbextractor.cpp:669-723
 //   k_octree      DistributeOctTree                   orbextractor.cpp:466-663
 //   k_blur        GaussianBlur 7x7 s=2 REFLECT_101    orbextractor.cpp:795-796
-//   k_finalize    IC_Angle + rBRIEF + scale + undistort + depth back-projection
+//   k_finalize    (k_finalize.hip) IC_Angle + rBRIEF + scale; k_kp_geometry undistort + depth
 //                 orbextractor.cpp:14-85,805-811; frame.cpp:139-164,286-313
 #include "odo_device.h"
 #include "odo_internal.h"
-#include "../../include/odo_orb_pattern.h"
 
 namespace odo {
-
-__constant__ int8_t c_pattern[1024];
-__constant__ int c_umax[16];
 
 // ============================================================ gray
 // gray = (B*1868 + G*9617 + R*4899 + 8192) >> 14, 4 pixels per thread; level 0
@@ -910,152 +906,8 @@ __global__ void __launch_bounds__(256) k_blur(const uint8_t* __restrict__ pyr, u
     }
 }
 
-// ============================================================ finalize
-// Four keypoints per wave, 16 lanes each (level-major output order): IC angle
-// on the raw level (lane j owns columns j-15 and j+1, all 31-row loads issued
-// together), rBRIEF on the blurred level (16 bit-tests per lane; one ballot
-// per test group gives two descriptor bytes of each of the 4 keypoints),
-// coordinate scaling, cv::undistortPoints and depth back-projection on the
-// keypoint's first lane. 16 keypoints per 256-thread workgroup.
-#define FIN_KPW 4                  // keypoints per wave
-#define FIN_KPB (4 * FIN_KPW)      // keypoints per workgroup
-__global__ void __launch_bounds__(256) k_finalize(const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
-                                                  size_t pyr_stride, const LevelDesc* __restrict__ lv, int nlevels,
-                                                  const uint32_t* __restrict__ okp, const int* __restrict__ ocnt,
-                                                  int okp_stride, const uint16_t* __restrict__ depth,
-                                                  size_t depth_stride, int img_w, FrameCalib cal,
-                                                  orb_kp* __restrict__ kps, uint8_t* __restrict__ desc,
-                                                  float* __restrict__ kun, float* __restrict__ xyz,
-                                                  float* __restrict__ ur, int* __restrict__ nkp, int kp_cap) {
-    __shared__ uint64_t s_bal[4][16];
-    // XCD-aware mapping: workgroups are dealt round-robin over the 8 XCDs, so
-    // hardware id h runs on XCD h%8; logical ids are assigned so that each XCD
-    // takes a contiguous run of (frame, keypoint-block) pairs and one frame's
-    // pyramid and blurred levels are fetched into one L2 instead of eight.
-    int bx = blockIdx.x, f = blockIdx.y;
-    {
-        const int total = gridDim.x * gridDim.y;
-        if ((total & 7) == 0) {
-            const int h = blockIdx.x + blockIdx.y * gridDim.x;
-            const int lid = (h & 7) * (total >> 3) + (h >> 3);
-            bx = lid % gridDim.x;
-            f = lid / gridDim.x;
-        }
-    }
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int g = lane >> 4, sub = lane & 15;  // keypoint slot in the wave, lane within it
-    const int idx = bx * FIN_KPB + wave * FIN_KPW + g;
-    // level lookup from per-level counts
-    int lvl = -1, k = 0, acc = 0;
-    for (int i = 0; i < nlevels; i++) {
-        const int c = ocnt[f * nlevels + i];
-        if (lvl < 0 && idx < acc + c) {
-            lvl = i;
-            k = idx - acc;
-        }
-        acc += c;
-    }
-    const int total = acc < kp_cap ? acc : kp_cap;
-    if (bx == 0 && threadIdx.x == 0) nkp[f] = total;
-    const bool valid = lvl >= 0 && idx < kp_cap;
-    // invalid slots run on a dummy in-level position and write nothing (no early
-    // exit: the ballots and the barrier below need every wave)
-    const LevelDesc L = lv[valid ? lvl : 0];
-    const uint32_t key = valid ? okp[((size_t)f * nlevels + lvl) * okp_stride + k] : (16u | (16u << 12));
-    const int kx = (int)(key & 0xfff) + 16, ky = (int)((key >> 12) & 0xfff) + 16;
-    const float resp = (float)(key >> 24);
-    const uint8_t* img = pyr + (size_t)f * pyr_stride + L.off;
-    // ---- IC_Angle: columns u0 = sub-15 (all 16 lanes) and u1 = sub+1 (lanes 0..14)
-    int m10 = 0, m01 = 0;
-    {
-        const int u0 = sub - 15, u1 = sub + 1;
-        const bool has1 = sub < 15;
-        const uint8_t* c0 = img + (size_t)ky * L.pitch + kx + u0;
-        const uint8_t* c1 = img + (size_t)ky * L.pitch + kx + (has1 ? u1 : 0);
-        // rows ky-15..ky+15 lie inside the level (16 px border): loads issued up front
-        int p0[15], n0[15], p1[15], n1[15];
-#pragma unroll
-        for (int v = 1; v <= 15; v++) {
-            p0[v - 1] = c0[(ptrdiff_t)v * L.pitch];
-            n0[v - 1] = c0[-(ptrdiff_t)v * L.pitch];
-            p1[v - 1] = c1[(ptrdiff_t)v * L.pitch];
-            n1[v - 1] = c1[-(ptrdiff_t)v * L.pitch];
-        }
-        const int a0 = u0 < 0 ? -u0 : u0;
-        m10 = u0 * c0[0] + (has1 ? u1 * c1[0] : 0);
-#pragma unroll
-        for (int v = 1; v <= 15; v++) {
-            const int um = c_umax[v];
-            if (a0 <= um) {
-                m01 += v * (p0[v - 1] - n0[v - 1]);
-                m10 += u0 * (p0[v - 1] + n0[v - 1]);
-            }
-            if (has1 && u1 <= um) {
-                m01 += v * (p1[v - 1] - n1[v - 1]);
-                m10 += u1 * (p1[v - 1] + n1[v - 1]);
-            }
-        }
-    }
-#pragma unroll
-    for (int off = 8; off > 0; off >>= 1) {
-        m10 += __shfl_xor(m10, off);
-        m01 += __shfl_xor(m01, off);
-    }
-    const float angle = fast_atan2((float)m01, (float)m10);
-    // ---- rBRIEF: lane sub makes tests w*16+sub, w = 0..15
-    const float factorPI = (float)(3.14159265358979323846 / 180.f);
-    const float ang = angle * factorPI;
-    const float a = (float)cos((double)ang), b = (float)sin((double)ang);
-    const uint8_t* bl = blur + (size_t)f * pyr_stride + L.off;
-    const uint8_t* center = bl + (size_t)ky * L.pitch + kx;
-    int tv0[16], tv1[16];
-#pragma unroll
-    for (int w = 0; w < 16; w++) {
-        const int bit = w * 16 + sub;
-        const float x0 = (float)c_pattern[4 * bit + 0], y0 = (float)c_pattern[4 * bit + 1];
-        const float x1 = (float)c_pattern[4 * bit + 2], y1 = (float)c_pattern[4 * bit + 3];
-        tv0[w] = center[cv_round(x0 * b + y0 * a) * L.pitch + cv_round(x0 * a - y0 * b)];
-        tv1[w] = center[cv_round(x1 * b + y1 * a) * L.pitch + cv_round(x1 * a - y1 * b)];
-    }
-#pragma unroll
-    for (int w = 0; w < 16; w++) {
-        const uint64_t bal = __ballot(tv0[w] < tv1[w]);
-        if (lane == 0) s_bal[wave][w] = bal;
-    }
-    __syncthreads();
-    const int o = idx;
-    if (valid && sub < 8) {
-        // descriptor dword sub = tests 32*sub .. 32*sub+31 = groups 2sub, 2sub+1
-        const uint32_t lo = (uint32_t)(s_bal[wave][2 * sub] >> (16 * g)) & 0xffffu;
-        const uint32_t hi = (uint32_t)(s_bal[wave][2 * sub + 1] >> (16 * g)) & 0xffffu;
-        reinterpret_cast<uint32_t*>(desc + ((size_t)f * kp_cap + o) * 32)[sub] = lo | (hi << 16);
-    }
-    if (valid && sub == 0) {
-        orb_kp* kp = kps + (size_t)f * kp_cap + o;
-        float px = (float)kx, py = (float)ky;
-        if (lvl != 0) {
-            px *= L.scale;
-            py *= L.scale;
-        }
-        kp->x = px;
-        kp->y = py;
-        kp->size = (float)(int)(31 * L.scale);
-        kp->angle = angle;
-        kp->response = resp;
-        kp->octave = lvl;
-        kp->class_id = -1;
-        // UndistortKeyPoints + depth back-projection (frame.cpp:139-164, 286-313)
-        kp_geometry(px, py, cal, depth + (size_t)f * depth_stride, img_w, kun + ((size_t)f * kp_cap + o) * 2,
-                    xyz + ((size_t)f * kp_cap + o) * 3, ur + (size_t)f * kp_cap + o);
-    }
-}
-
 // ============================================================ host-side launch helpers
-void upload_extract_constants() {
-    hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), ODO_ORB_PATTERN, sizeof(ODO_ORB_PATTERN));
-    const int umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
-    hipMemcpyToSymbol(HIP_SYMBOL(c_umax), umax, sizeof(umax));
-}
+void upload_extract_constants() { upload_finalize_constants(); }
 
 }  // namespace odo
 
@@ -1102,15 +954,6 @@ void launch_blur(hipStream_t st, const uint8_t* pyr, uint8_t* blur, size_t pyr_s
     T.base[nlevels] = acc;
     hipLaunchKernelGGL(k_blur, dim3(acc, nframes), dim3(256), 0, st, pyr, blur, pyr_stride, lv, T, nlevels);
 }
-void launch_finalize(hipStream_t st, const uint8_t* pyr, const uint8_t* blur, size_t pyr_stride, const LevelDesc* lv,
-                     int nlevels, const uint32_t* okp, const int* ocnt, int okp_stride, const uint16_t* depth,
-                     size_t depth_stride, int img_w, FrameCalib cal, orb_kp* kps, uint8_t* desc, float* kun, float* xyz,
-                     float* ur, int* nkp, int kp_cap, int nframes) {
-    dim3 g((kp_cap + FIN_KPB - 1) / FIN_KPB, nframes);
-    hipLaunchKernelGGL(k_finalize, g, dim3(256), 0, st, pyr, blur, pyr_stride, lv, nlevels, okp, ocnt, okp_stride,
-                       depth, depth_stride, img_w, cal, kps, desc, kun, xyz, ur, nkp, kp_cap);
-}
-
 // Frame roll: the last frame of a batch becomes slot 0 (Tracking::mLastFrame)
 // of the next batch's frame set. One launch for all per-frame feature arrays
 // (16-byte moves; every array is kp_cap-sized, kp_cap a multiple of 64).

@@ -1,0 +1,234 @@
+// Keypoint finalisation for gfx950: ORBextractor::operator()'s tail
+// (Features/orbextractor.cpp:756-815) — IC_Angle (:14-39), computeOrbDescriptor
+// (:43-85) on the Gaussian-blurred level, the level-0 scaling of the
+// coordinates (:805-811) — and Frame::ExtractFeatures' per-keypoint geometry
+// (Core/frame.cpp:139-164 UndistortKeyPoints / depth back-projection,
+// :286-313).
+//
+//   k_finalize      16 lanes per keypoint, 4 keypoints per wave:
+//                   IC angle from 9 aligned dwords per disc row (two rows per
+//                   lane), realigned with alignbyte, bytes outside the disc
+//                   masked, and the moments by udot4 (exact integers);
+//                   rBRIEF with the rotation in packed fp32 and cvRound by the
+//                   1.5*2^23 magic add, 32-bit gather offsets off the frame
+//                   base, one ballot per test group
+//   k_kp_geometry   one keypoint per lane: undistortion (5 double iterations)
+//                   and the depth back-projection, shared with the ADAPTIVE
+//                   extractor's finalisation (k_adaptive.hip)
+#include "odo_device.h"
+#include "odo_internal.h"
+#include "../../include/odo_orb_pattern.h"
+
+namespace odo {
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__constant__ float4 c_patf[256];  // ORB_SLAM2 pattern test t: (x0, y0, x1, y1)
+__constant__ int c_umax16[16];    // IC_Angle disc half-widths per |v|
+
+// 1.5 * 2^23: for |x| < 2^22, the float sum x + RND_MAGIC is x rounded half to
+// even (cvRound) plus the magic, so its low mantissa bits are the integer.
+#define RND_MAGIC 12582912.0f
+#define RND_BITS 0x4B400000u
+
+#define FIN_KPW 4              // keypoints per wave
+#define FIN_KPB (4 * FIN_KPW)  // keypoints per workgroup
+__global__ void __launch_bounds__(256) k_finalize(const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
+                                                  size_t pyr_stride, const LevelDesc* __restrict__ lv, int nlevels,
+                                                  const uint32_t* __restrict__ okp, const int* __restrict__ ocnt,
+                                                  int okp_stride, orb_kp* __restrict__ kps, uint8_t* __restrict__ desc,
+                                                  int* __restrict__ nkp, int kp_cap) {
+    __shared__ uint64_t s_bal[4][16];
+    __shared__ __attribute__((aligned(16))) uint32_t s_disc[16][8];  // byte masks of the disc rows |v| = 0..15
+    if (threadIdx.x < 128) {
+        const int av = threadIdx.x >> 3, i = threadIdx.x & 7;
+        const int um = c_umax16[av];
+        uint32_t m = 0;
+#pragma unroll
+        for (int bb = 0; bb < 4; bb++) {
+            const int u = 4 * i + bb - 15;  // dword i covers columns -15+4i .. -12+4i
+            if (u >= -um && u <= um) m |= 0xffu << (8 * bb);
+        }
+        s_disc[av][i] = m;
+    }
+    // XCD-aware mapping: workgroups are dealt round-robin over the 8 XCDs, so
+    // hardware id h runs on XCD h%8; logical ids are assigned so that each XCD
+    // takes a contiguous run of (frame, keypoint-block) pairs and one frame's
+    // pyramid and blurred levels are fetched into one L2 instead of eight.
+    int bx = blockIdx.x, f = blockIdx.y;
+    {
+        const int total = gridDim.x * gridDim.y;
+        if ((total & 7) == 0) {
+            const int h = blockIdx.x + blockIdx.y * gridDim.x;
+            const int lid = (h & 7) * (total >> 3) + (h >> 3);
+            bx = lid % gridDim.x;
+            f = lid / gridDim.x;
+        }
+    }
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int g = lane >> 4, sub = lane & 15;  // keypoint slot in the wave, lane within it
+    const int idx = bx * FIN_KPB + wave * FIN_KPW + g;
+    // level lookup from per-level counts
+    int lvl = -1, k = 0, acc = 0;
+    for (int i = 0; i < nlevels; i++) {
+        const int c = ocnt[f * nlevels + i];
+        if (lvl < 0 && idx < acc + c) {
+            lvl = i;
+            k = idx - acc;
+        }
+        acc += c;
+    }
+    const int total = acc < kp_cap ? acc : kp_cap;
+    if (bx == 0 && threadIdx.x == 0) nkp[f] = total;
+    const bool valid = lvl >= 0 && idx < kp_cap;
+    // invalid slots run on a dummy in-level position and write nothing (no early
+    // exit: the ballots and the barriers below need every wave)
+    const LevelDesc L = lv[valid ? lvl : 0];
+    const uint32_t key = valid ? okp[((size_t)f * nlevels + lvl) * okp_stride + k] : (16u | (16u << 12));
+    const int kx = (int)(key & 0xfff) + 16, ky = (int)((key >> 12) & 0xfff) + 16;
+    const float resp = (float)(key >> 24);
+    // ---- IC_Angle: lane sub sums disc rows v0 = sub-15 and v1 = sub+1 (lanes
+    // 0..14; lane 15's second row is masked to zero). Columns -15..16 of a row
+    // are 8 dwords realigned from the 9 aligned dwords holding them (rows are
+    // 16-byte aligned, a row's loads stay inside the pitch-padded level or the
+    // pyramid's 64-byte tail). m10 = sum (u+16) I - 16 sum I, m01 = sum v I.
+    int m10, m01;
+    {
+        const uint8_t* img = pyr + (size_t)f * pyr_stride + L.off;
+        const bool has1 = sub < 15;
+        const int v0 = sub - 15, v1 = has1 ? sub + 1 : 0;
+        const int sh = (kx - 15) & 3;
+        const uint32_t* r0 = reinterpret_cast<const uint32_t*>(img + (size_t)(ky + v0) * L.pitch + (kx - 15 - sh));
+        const uint32_t* r1 = reinterpret_cast<const uint32_t*>(img + (size_t)(ky + v1) * L.pitch + (kx - 15 - sh));
+        uint32_t w0[9], w1[9];
+#pragma unroll
+        for (int i = 0; i < 9; i++) {
+            w0[i] = r0[i];
+            w1[i] = r1[i];
+        }
+        __syncthreads();  // s_disc
+        const uint4* M0 = reinterpret_cast<const uint4*>(s_disc[-v0]);
+        const uint4* M1 = reinterpret_cast<const uint4*>(s_disc[v1]);
+        const uint4 a0 = M0[0], a1 = M0[1], b0 = M1[0], b1 = M1[1];
+        const uint32_t z = has1 ? 0xffffffffu : 0u;
+        const uint32_t mk0[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        const uint32_t mk1[8] = {b0.x & z, b0.y & z, b0.z & z, b0.w & z, b1.x & z, b1.y & z, b1.z & z, b1.w & z};
+        uint32_t s0 = 0, s1 = 0, t = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const uint32_t U = (uint32_t)(4 * i + 1) | ((uint32_t)(4 * i + 2) << 8) | ((uint32_t)(4 * i + 3) << 16) |
+                               ((uint32_t)(4 * i + 4) << 24);
+            const uint32_t d0 = __builtin_amdgcn_alignbyte(w0[i + 1], w0[i], sh) & mk0[i];
+            const uint32_t d1 = __builtin_amdgcn_alignbyte(w1[i + 1], w1[i], sh) & mk1[i];
+            s0 = __builtin_amdgcn_udot4(d0, 0x01010101u, s0, false);
+            s1 = __builtin_amdgcn_udot4(d1, 0x01010101u, s1, false);
+            t = __builtin_amdgcn_udot4(d0, U, t, false);
+            t = __builtin_amdgcn_udot4(d1, U, t, false);
+        }
+        m10 = (int)t - 16 * (int)(s0 + s1);
+        m01 = v0 * (int)s0 + v1 * (int)s1;
+    }
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1) {
+        m10 += __shfl_xor(m10, off);
+        m01 += __shfl_xor(m01, off);
+    }
+    const float angle = fast_atan2((float)m01, (float)m10);
+    // ---- rBRIEF: lane sub makes tests w*16+sub, w = 0..15. Per point
+    // (x*b + y*a, x*a + (-y)*b) in packed fp32 — the reference's two products
+    // and one sum per coordinate, each rounded once — then cvRound by the magic
+    // add; offset = iy*pitch + ix in 32 bits with the magic folded into cofs.
+    const float factorPI = (float)(3.14159265358979323846 / 180.f);
+    const float ang = angle * factorPI;
+    double sd, cd;
+    sincos((double)ang, &sd, &cd);
+    const float a = (float)cd, b = (float)sd;
+    const f32x2 BA = {b, a}, AB = {a, b}, MAG = {RND_MAGIC, RND_MAGIC};
+    const uint8_t* fb = blur + (size_t)f * pyr_stride;
+    const uint32_t pitch = (uint32_t)L.pitch;
+    // iy's low 24 bits are 0x400000 + dy (mul_u24), ix is RND_BITS + dx
+    const uint32_t cofs = (uint32_t)L.off + (uint32_t)ky * pitch + (uint32_t)kx - 0x400000u * pitch - RND_BITS;
+    int tv0[16], tv1[16];
+#pragma unroll
+    for (int w = 0; w < 16; w++) {
+        const float4 P = c_patf[w * 16 + sub];
+        f32x2 q0 = (f32x2){P.x, P.x} * BA + (f32x2){P.y, -P.y} * AB;
+        f32x2 q1 = (f32x2){P.z, P.z} * BA + (f32x2){P.w, -P.w} * AB;
+        q0 = q0 + MAG;
+        q1 = q1 + MAG;
+        const uint32_t o0 = __umul24(__float_as_uint(q0.x), pitch) + __float_as_uint(q0.y) + cofs;
+        const uint32_t o1 = __umul24(__float_as_uint(q1.x), pitch) + __float_as_uint(q1.y) + cofs;
+        tv0[w] = fb[o0];
+        tv1[w] = fb[o1];
+    }
+#pragma unroll
+    for (int w = 0; w < 16; w++) {
+        const uint64_t bal = __ballot(tv0[w] < tv1[w]);
+        if (lane == 0) s_bal[wave][w] = bal;
+    }
+    __syncthreads();
+    const int o = idx;
+    if (valid && sub < 8) {
+        // descriptor dword sub = tests 32*sub .. 32*sub+31 = groups 2sub, 2sub+1
+        const uint32_t lo = (uint32_t)(s_bal[wave][2 * sub] >> (16 * g)) & 0xffffu;
+        const uint32_t hi = (uint32_t)(s_bal[wave][2 * sub + 1] >> (16 * g)) & 0xffffu;
+        reinterpret_cast<uint32_t*>(desc + ((size_t)f * kp_cap + o) * 32)[sub] = lo | (hi << 16);
+    }
+    if (valid && sub == 0) {
+        orb_kp* kp = kps + (size_t)f * kp_cap + o;
+        float px = (float)kx, py = (float)ky;
+        if (lvl != 0) {
+            px *= L.scale;
+            py *= L.scale;
+        }
+        kp->x = px;
+        kp->y = py;
+        kp->size = (float)(int)(31 * L.scale);
+        kp->angle = angle;
+        kp->response = resp;
+        kp->octave = lvl;
+        kp->class_id = -1;
+    }
+}
+
+// UndistortKeyPoints + depth back-projection (frame.cpp:139-164, 286-313) of
+// every finalised keypoint, one per lane.
+__global__ void __launch_bounds__(256) k_kp_geometry(const orb_kp* __restrict__ kps, const int* __restrict__ nkp,
+                                                     const uint16_t* __restrict__ depth, size_t depth_stride, int img_w,
+                                                     FrameCalib cal, float* __restrict__ kun, float* __restrict__ xyz,
+                                                     float* __restrict__ ur, int kp_cap) {
+    const int f = blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nkp[f]) return;
+    const size_t o = (size_t)f * kp_cap + i;
+    const float2 p = *reinterpret_cast<const float2*>(&kps[o].x);
+    kp_geometry(p.x, p.y, cal, depth + (size_t)f * depth_stride, img_w, kun + o * 2, xyz + o * 3, ur + o);
+}
+
+void upload_finalize_constants() {
+    float4 pat[256];
+    for (int t = 0; t < 256; t++)
+        pat[t] = make_float4((float)ODO_ORB_PATTERN[4 * t], (float)ODO_ORB_PATTERN[4 * t + 1],
+                             (float)ODO_ORB_PATTERN[4 * t + 2], (float)ODO_ORB_PATTERN[4 * t + 3]);
+    hipMemcpyToSymbol(HIP_SYMBOL(c_patf), pat, sizeof(pat));
+    const int umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
+    hipMemcpyToSymbol(HIP_SYMBOL(c_umax16), umax, sizeof(umax));
+}
+
+void launch_kp_geometry(hipStream_t st, const orb_kp* kps, const int* nkp, const uint16_t* depth, size_t depth_stride,
+                        int img_w, FrameCalib cal, float* kun, float* xyz, float* ur, int kp_cap, int nframes) {
+    dim3 g((kp_cap + 255) / 256, nframes);
+    hipLaunchKernelGGL(k_kp_geometry, g, dim3(256), 0, st, kps, nkp, depth, depth_stride, img_w, cal, kun, xyz, ur,
+                       kp_cap);
+}
+
+void launch_finalize(hipStream_t st, const uint8_t* pyr, const uint8_t* blur, size_t pyr_stride, const LevelDesc* lv,
+                     int nlevels, const uint32_t* okp, const int* ocnt, int okp_stride, const uint16_t* depth,
+                     size_t depth_stride, int img_w, FrameCalib cal, orb_kp* kps, uint8_t* desc, float* kun, float* xyz,
+                     float* ur, int* nkp, int kp_cap, int nframes) {
+    dim3 g((kp_cap + FIN_KPB - 1) / FIN_KPB, nframes);
+    hipLaunchKernelGGL(k_finalize, g, dim3(256), 0, st, pyr, blur, pyr_stride, lv, nlevels, okp, ocnt, okp_stride, kps,
+                       desc, nkp, kp_cap);
+    launch_kp_geometry(st, kps, nkp, depth, depth_stride, img_w, cal, kun, xyz, ur, kp_cap, nframes);
+}
+
+}  // namespace odo

@@ -127,6 +127,9 @@ struct RansacCfg {
 
 // ---- launch wrappers (defined next to their kernels)
 void upload_extract_constants();
+void upload_finalize_constants();
+void launch_kp_geometry(hipStream_t st, const orb_kp* kps, const int* nkp, const uint16_t* depth, size_t depth_stride,
+                        int img_w, FrameCalib cal, float* kun, float* xyz, float* ur, int kp_cap, int nframes);
 void launch_gray(hipStream_t st, const uint8_t* bgr, uint8_t* pyr, int w, int h, int pitch, size_t in_stride,
                  size_t pyr_stride, int nframes);
 size_t resize_lds_bytes(int spitch, int dw, int max_src_rows);
