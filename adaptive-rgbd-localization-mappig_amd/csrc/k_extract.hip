@@ -838,9 +838,22 @@ __global__ void __launch_bounds__(256) k_blur(const uint8_t* __restrict__ pyr, u
             reinterpret_cast<uint32_t*>(tile + r * BLUR_IW)[c] = srow[c];
         }
     } else {
-        for (int r = t >> 6; r < BLUR_IH; r += 4) {
+        // border tile: rows reflected once per dword, in-row dwords loaded whole,
+        // only the dwords straddling a left/right edge assembled bytewise
+        constexpr int NW = BLUR_IW / 4;
+        for (int it = t; it < BLUR_IH * NW; it += 256) {
+            const int r = it / NW, c = it - r * NW;
             const uint8_t* srow = src + (size_t)reflect101(ty0 + r - 3, L.h) * L.pitch;
-            for (int c = t & 63; c < BLUR_IW; c += 64) tile[r * BLUR_IW + c] = srow[reflect101(tx0 + c - 4, L.w)];
+            const int x = tx0 - 4 + 4 * c;
+            uint32_t v;
+            if (x >= 0 && x + 3 < L.w) {
+                v = *reinterpret_cast<const uint32_t*>(srow + x);
+            } else {
+                v = 0;
+#pragma unroll
+                for (int b = 0; b < 4; b++) v |= (uint32_t)srow[reflect101(x + b, L.w)] << (8 * b);
+            }
+            reinterpret_cast<uint32_t*>(tile + r * BLUR_IW)[c] = v;
         }
     }
     __syncthreads();
