@@ -115,37 +115,6 @@ __global__ void __launch_bounds__(256) k_resize(uint8_t* __restrict__ pyr, size_
 __constant__ int c_circle_dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
 __constant__ int c_circle_dy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
 
-// cornerScore<16> restated (min/max over arcs), d[k] = v - p[k].
-ODO_INLINE int corner_score16(const int* d, int threshold) {
-    int a0 = threshold;
-#pragma unroll
-    for (int k = 0; k < 16; k += 2) {
-        int a = min(d[(k + 1) & 15], d[(k + 2) & 15]);
-        a = min(a, d[(k + 3) & 15]);
-        a = min(a, d[(k + 4) & 15]);
-        a = min(a, d[(k + 5) & 15]);
-        a = min(a, d[(k + 6) & 15]);
-        a = min(a, d[(k + 7) & 15]);
-        a = min(a, d[(k + 8) & 15]);
-        a0 = max(a0, min(a, d[k]));
-        a0 = max(a0, min(a, d[(k + 9) & 15]));
-    }
-    int b0 = -a0;
-#pragma unroll
-    for (int k = 0; k < 16; k += 2) {
-        int b = max(d[(k + 1) & 15], d[(k + 2) & 15]);
-        b = max(b, d[(k + 3) & 15]);
-        b = max(b, d[(k + 4) & 15]);
-        b = max(b, d[(k + 5) & 15]);
-        b = max(b, d[(k + 6) & 15]);
-        b = max(b, d[(k + 7) & 15]);
-        b = max(b, d[(k + 8) & 15]);
-        b0 = min(b0, max(b, d[k]));
-        b0 = min(b0, max(b, d[(k + 9) & 15]));
-    }
-    return -b0 - 1;
-}
-
 ODO_INLINE bool has_run9(uint32_t m16) {
     uint32_t x = m16 | (m16 << 16);
     uint32_t a = x & (x >> 1);
@@ -163,17 +132,22 @@ ODO_INLINE bool has_run9(uint32_t m16) {
 //   2. the full 16-pixel test + cornerScore on the queue, corners listed in
 //      order with their scores in an LDS map (0 elsewhere),
 //   3. NMS (strictly greater than the 8 neighbours) over the corner list.
+template <int ROI_MAX>
 __global__ void __launch_bounds__(64) k_fast_cells(const uint8_t* __restrict__ pyr, size_t pyr_stride,
                                                    const CellDesc* __restrict__ cells, const LevelDesc* __restrict__ lv,
                                                    uint32_t* __restrict__ cand, int* __restrict__ cand_cnt,
                                                    int ncells, int cell_cap, int ini_th, int min_th) {
     // ROI rows staged as whole aligned dwords: pixel (r, c) at byte r*RS + sh + c
-    constexpr int RS4 = (FAST_ROI_MAX + 3 + 3) / 4 + 1;  // dwords per staged row (>= (sh+cols+3)/4)
+    constexpr int RS4 = (ROI_MAX + 3 + 3) / 4 + 1;  // dwords per staged row (>= (sh+cols+3)/4)
     constexpr int RS = 4 * RS4;
-    __shared__ __attribute__((aligned(16))) uint32_t roi32[FAST_ROI_MAX * RS4];
-    __shared__ __attribute__((aligned(16))) uint32_t score32[FAST_ROI_MAX * RS4];
-    __shared__ uint16_t q1[(FAST_ROI_MAX - 6) * (FAST_ROI_MAX - 6)];
-    __shared__ uint16_t q2[(FAST_ROI_MAX - 6) * (FAST_ROI_MAX - 6)];
+    __shared__ __attribute__((aligned(16))) uint32_t roi32[ROI_MAX * RS4];
+    __shared__ __attribute__((aligned(16))) uint32_t score32[ROI_MAX * RS4];
+    // survivor queue; the corner list is compacted into it in place (a wave
+    // writes entry n2 + rank <= base + lane only after reading entries
+    // base..base+63, so unread entries are never overwritten): 8.9 KB of LDS
+    // per single-wave workgroup, 4 waves per SIMD
+    __shared__ uint16_t q1[(ROI_MAX - 6) * (ROI_MAX - 6)];
+    uint16_t* const q2 = q1;
     const uint8_t* roi = reinterpret_cast<const uint8_t*>(roi32);
     uint8_t* score = reinterpret_cast<uint8_t*>(score32);
     const int f = blockIdx.y;
@@ -280,7 +254,7 @@ __global__ void __launch_bounds__(64) k_fast_cells(const uint8_t* __restrict__ p
             for (int i = 0; i < 4; i++) n1 += __popcll(bi[i]);
         }
         __syncthreads();
-        // 2. full segment test + score on the survivors
+        // 2a. full segment test on the survivors; corners listed in order
         int n2 = 0;
         for (int base = 0; base < n1; base += 64) {
             const int idx = base + lane;
@@ -289,23 +263,60 @@ __global__ void __launch_bounds__(64) k_fast_cells(const uint8_t* __restrict__ p
             if (idx < n1) {
                 o = q1[idx];
                 const int v = roi[o];
-                int d[16];
                 uint32_t dark = 0, bright = 0;
 #pragma unroll
                 for (int k = 0; k < 16; k++) {
                     const int px = roi[o + c_circle_dy[k] * RS + c_circle_dx[k]];
-                    d[k] = v - px;
                     dark |= (uint32_t)(px < v - thc) << k;
                     bright |= (uint32_t)(px > v + thc) << k;
                 }
-                if (has_run9(dark) || has_run9(bright)) {
-                    corner = true;
-                    score[o] = (uint8_t)corner_score16(d, thc);
-                }
+                corner = has_run9(dark) || has_run9(bright);
             }
             const uint64_t bal = __ballot(corner);
             if (corner) q2[n2 + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0))] = (uint16_t)o;
             n2 += __popcll(bal);
+        }
+        __syncthreads();
+        // 2b. cornerScore<16> of the corners, two per lane in packed 16-bit
+        //     lanes: d = v - p, S = max(best 9-arc min of d, -(best 9-arc max));
+        //     a corner at th has S > th, so cornerScore = max(th, S) - 1 = S - 1
+        for (int base = 0; base < n2; base += 128) {
+            const int i0 = base + 2 * lane, i1 = i0 + 1;
+            if (i0 < n2) {
+                const int o0 = q2[i0], o1 = i1 < n2 ? q2[i1] : o0;
+                const int v0 = roi[o0], v1 = roi[o1];
+                s16x2 d[16];
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    const int off = c_circle_dy[k] * RS + c_circle_dx[k];
+                    d[k] = s16x2{(short)(v0 - (int)roi[o0 + off]), (short)(v1 - (int)roi[o1 + off])};
+                }
+                s16x2 mn[16], mx[16];
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    mn[k] = __builtin_elementwise_min(d[k], d[(k + 1) & 15]);
+                    mx[k] = __builtin_elementwise_max(d[k], d[(k + 1) & 15]);
+                }
+                s16x2 mn4[16], mx4[16];
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    mn4[k] = __builtin_elementwise_min(mn[k], mn[(k + 2) & 15]);
+                    mx4[k] = __builtin_elementwise_max(mx[k], mx[(k + 2) & 15]);
+                }
+                s16x2 dk = s16x2{-32768, -32768}, br = s16x2{32767, 32767};
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    const s16x2 a9 = __builtin_elementwise_min(__builtin_elementwise_min(mn4[k], mn4[(k + 4) & 15]),
+                                                               d[(k + 8) & 15]);
+                    const s16x2 b9 = __builtin_elementwise_max(__builtin_elementwise_max(mx4[k], mx4[(k + 4) & 15]),
+                                                               d[(k + 8) & 15]);
+                    dk = __builtin_elementwise_max(dk, a9);
+                    br = __builtin_elementwise_min(br, b9);
+                }
+                const s16x2 sc = __builtin_elementwise_max(dk, -br);
+                score[o0] = (uint8_t)(sc.x - 1);
+                if (i1 < n2) score[o1] = (uint8_t)(sc.y - 1);
+            }
         }
         __syncthreads();
         // 3. NMS over the corner list (row-major), ordered compaction
@@ -942,10 +953,20 @@ void launch_resize(hipStream_t st, uint8_t* pyr, size_t pyr_stride, int src_off,
                        xt, yt);
 }
 void launch_fast(hipStream_t st, const uint8_t* pyr, size_t pyr_stride, const CellDesc* cells, const LevelDesc* lv,
-                 uint32_t* cand, int* cand_cnt, int ncells, int cell_cap, int ini_th, int min_th, int nframes) {
+                 uint32_t* cand, int* cand_cnt, int ncells, int cell_cap, int ini_th, int min_th, int roi_max,
+                 int nframes) {
+    // LDS sized for the largest cell ROI of the context: the kernel is
+    // occupancy-bound (one wave per workgroup), 7.5 KB at 44 px vs 8.9 KB at 48
     dim3 g(ncells, nframes);
-    hipLaunchKernelGGL(k_fast_cells, g, dim3(64), 0, st, pyr, pyr_stride, cells, lv, cand, cand_cnt, ncells, cell_cap,
-                       ini_th, min_th);
+    if (roi_max <= 40)
+        hipLaunchKernelGGL(k_fast_cells<40>, g, dim3(64), 0, st, pyr, pyr_stride, cells, lv, cand, cand_cnt, ncells,
+                           cell_cap, ini_th, min_th);
+    else if (roi_max <= 44)
+        hipLaunchKernelGGL(k_fast_cells<44>, g, dim3(64), 0, st, pyr, pyr_stride, cells, lv, cand, cand_cnt, ncells,
+                           cell_cap, ini_th, min_th);
+    else
+        hipLaunchKernelGGL(k_fast_cells<FAST_ROI_MAX>, g, dim3(64), 0, st, pyr, pyr_stride, cells, lv, cand, cand_cnt,
+                           ncells, cell_cap, ini_th, min_th);
 }
 size_t octree_lds_bytes(int node_cap) { return (size_t)76 * node_cap + 1032; }
 void launch_octree(hipStream_t st, const uint32_t* cand, const int* cand_cnt, const LevelDesc* lv, int ncells,

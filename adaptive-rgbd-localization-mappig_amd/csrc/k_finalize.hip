@@ -31,9 +31,12 @@ __constant__ int c_umax16[16];    // IC_Angle disc half-widths per |v|
 #define RND_MAGIC 12582912.0f
 #define RND_BITS 0x4B400000u
 
+#ifndef FIN_WAVES_PER_EU
+#define FIN_WAVES_PER_EU 1  // occupancy floor (launch bounds); 1 = compiler's choice
+#endif
 #define FIN_KPW 4              // keypoints per wave
 #define FIN_KPB (4 * FIN_KPW)  // keypoints per workgroup
-__global__ void __launch_bounds__(256) k_finalize(const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
+__global__ void __launch_bounds__(256, FIN_WAVES_PER_EU) k_finalize(const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
                                                   size_t pyr_stride, const LevelDesc* __restrict__ lv, int nlevels,
                                                   const uint32_t* __restrict__ okp, const int* __restrict__ ocnt,
                                                   int okp_stride, orb_kp* __restrict__ kps, uint8_t* __restrict__ desc,

@@ -103,6 +103,7 @@ struct odo_ctx {
     ResizeY* ry = nullptr;
     int ncells = 0, cell_cap = 0, kp_cap = 0, okp_stride = 0, node_cap = 0, match_cap = 0, mask_words = 0;
     int max_blur_tiles = 0;
+    int fast_roi = 0;  // largest FAST cell ROI side (sizes the kernel's LDS)
     size_t pyr_size = 0, keys_per_frame = 0;
     FrameCalib cal{};
     RansacCfg rcfg{};
@@ -408,6 +409,7 @@ static int build_geometry(odo_ctx* c) {
                 C.pad = 0;
                 if (C.rows > FAST_ROI_MAX || C.cols > FAST_ROI_MAX) return fail(ODO_ERR_ARG, "FAST cell exceeds ROI max");
                 c->cells_h.push_back(C);
+                c->fast_roi = std::max(c->fast_roi, (int)std::max(C.rows, C.cols));
                 c->cell_cap = std::max(c->cell_cap, ((C.rows - 6 + 1) / 2) * ((C.cols - 6 + 1) / 2) + 1);
             }
         }
@@ -867,7 +869,7 @@ static int run_extract(odo_ctx* c, int set, const uint8_t* d_bgr, const uint16_t
     }
     launch_fast(st, pyr, P, c->cells, c->lv, c->cand + (size_t)slot * c->ncells * c->cell_cap,
                 c->cand_cnt + (size_t)slot * c->ncells, c->ncells, c->cell_cap, c->cfg.orb.ini_th_fast,
-                c->cfg.orb.min_th_fast, n);
+                c->cfg.orb.min_th_fast, c->fast_roi, n);
     tmark(c, 2, st);
     launch_octree(st, c->cand + (size_t)slot * c->ncells * c->cell_cap, c->cand_cnt + (size_t)slot * c->ncells, c->lv,
                   c->ncells, c->cell_cap, c->nlevels, c->keys + (size_t)slot * c->keys_per_frame,

@@ -136,7 +136,8 @@ size_t resize_lds_bytes(int spitch, int dw, int max_src_rows);
 void launch_resize(hipStream_t st, uint8_t* pyr, size_t pyr_stride, int src_off, int spitch, int dst_off, int dpitch,
                    int dw, int dh, int rb, int max_src_rows, const ResizeX* xt, const ResizeY* yt, int nframes);
 void launch_fast(hipStream_t st, const uint8_t* pyr, size_t pyr_stride, const CellDesc* cells, const LevelDesc* lv,
-                 uint32_t* cand, int* cand_cnt, int ncells, int cell_cap, int ini_th, int min_th, int nframes);
+                 uint32_t* cand, int* cand_cnt, int ncells, int cell_cap, int ini_th, int min_th, int roi_max,
+                 int nframes);
 size_t octree_lds_bytes(int node_cap);
 void launch_octree(hipStream_t st, const uint32_t* cand, const int* cand_cnt, const LevelDesc* lv, int ncells,
                    int cell_cap, int nlevels, uint32_t* keys, int32_t* knode, uint8_t* kquad, size_t keys_stride,
