@@ -433,7 +433,10 @@ ODO_INLINE double edge_robust_chi(const SE3& T, const double Xw[3], const double
 // solve one candidate step, a single edge pass sums chi2 for all candidates,
 // and the sequential accept/reject control flow is replayed over the results
 // (same decisions, same state as the one-trial-at-a-time loop).
-__global__ void __launch_bounds__(PNP_NT) k_pnp(const int32_t* __restrict__ f2_src, const float* __restrict__ xyz,
+#ifndef PNP_WAVES_PER_EU
+#define PNP_WAVES_PER_EU 1  // occupancy floor (launch bounds); 1 = compiler's choice
+#endif
+__global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t* __restrict__ f2_src, const float* __restrict__ xyz,
                                             const float* __restrict__ kun, const float* __restrict__ ur,
                                             const int* __restrict__ nkp, int kp_cap, int slot0, FrameCalib cal,
                                             const float* __restrict__ T12, const int* __restrict__ pair_valid,
