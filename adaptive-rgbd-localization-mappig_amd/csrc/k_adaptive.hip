@@ -66,22 +66,34 @@ __global__ void __launch_bounds__(256) k_adapt_smap(const uint8_t* __restrict__ 
     const int r = threadIdx.x >> 5, q = threadIdx.x & 31;
     const int y = ty0 + r, x = tx0 + 4 * q;
     if (y >= h || x >= pitch) return;
-    const uint8_t* L = reinterpret_cast<const uint8_t*>(lds);
-    const int ly = r + 3, lx = 4 * q + 4;
+    // the 7 rows x 12 columns (x-4 .. x+7) the 4 pixels' circles touch: three
+    // aligned dwords per row; a circle pixel pair (columns c, c+1 of a row) is
+    // one v_perm into the two 16-bit halves
+    const int ly = r + 3;
+    uint32_t W[7][3];
+#pragma unroll
+    for (int dy = 0; dy < 7; dy++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) W[dy][j] = lds[(ly - 3 + dy) * (SM_LW / 4) + q + j];
+    // bytes i, i+1 (i = 0..10 over the row's 12 bytes) -> 16-bit lanes (lo, hi)
+    auto pair16 = [&](int dy, int i) -> short2v {
+        const uint32_t lo = W[dy][i >> 2], hi = W[dy][(i >> 2) + 1 < 3 ? (i >> 2) + 1 : 2];
+        const int o = i & 3;  // byte offset within lo; o + 1 may spill into hi
+        const uint32_t sel = (uint32_t)o | 0x0c00u | ((uint32_t)(o + 1) << 16) | 0x0c000000u;
+        const uint32_t v = __builtin_amdgcn_perm(hi, lo, sel);
+        return *reinterpret_cast<const short2v*>(&v);
+    };
     // circle offsets (x, y) of FAST_t<16> (App. A.3)
-    const int cxo[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
-    const int cyo[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
+    constexpr int cxo[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+    constexpr int cyo[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
     uint32_t out = 0;
 #pragma unroll
     for (int pp = 0; pp < 4; pp += 2) {
         // two pixels per packed 16-bit lane pair
         short2v d[16];
-        const int v0 = L[ly * SM_LW + lx + pp], v1 = L[ly * SM_LW + lx + pp + 1];
+        const short2v v = pair16(3, 4 + pp);
 #pragma unroll
-        for (int k = 0; k < 16; k++) {
-            const int o = (ly + cyo[k]) * SM_LW + lx + pp + cxo[k];
-            d[k] = short2v{(short)(v0 - (int)L[o]), (short)(v1 - (int)L[o + 1])};
-        }
+        for (int k = 0; k < 16; k++) d[k] = v - pair16(3 + cyo[k], 4 + pp + cxo[k]);
         short2v mn[16], mx[16];
 #pragma unroll
         for (int k = 0; k < 16; k++) {
