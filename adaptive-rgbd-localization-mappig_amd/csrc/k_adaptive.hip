@@ -196,19 +196,25 @@ __global__ void __launch_bounds__(256) k_adapt_cand(const uint8_t* __restrict__ 
     const int rows = B.y1 - B.y0;
     const uint8_t* S = smap + (size_t)f * smap_stride;
     sh[threadIdx.x] = 0;
-    for (int i = threadIdx.x; i < (rows + 2) * lw; i += 256) {
-        const int r = i / lw, q = i % lw;
-        const int y = B.y0 - 1 + r, x = C.c0 - 1 + q;
-        const bool in = y >= C.r0 && y < C.r1 && x >= C.c0 && x < C.c1;
-        s[i] = in ? S[(size_t)y * pitch + x] : 0;
+    // rows outer, columns across the threads: no division per staged byte
+    for (int r = 0; r < rows + 2; r++) {
+        const int y = B.y0 - 1 + r;
+        const bool yin = y >= C.r0 && y < C.r1;
+        for (int q = threadIdx.x; q < lw; q += 256) {
+            const int x = C.c0 - 1 + q;
+            s[r * lw + q] = (yin && x >= C.c0 && x < C.c1) ? S[(size_t)y * pitch + x] : 0;
+        }
     }
     __syncthreads();
+    // each thread a contiguous run of the band's pixels (row-major order is
+    // kept by the scan below); (row, col) stepped, not divided, per pixel;
+    // survivors of the first pass remembered in a bit mask (runs <= 32 px)
     const int npx = rows * cw;
     const int chunk = (npx + 255) / 256;
     const int i0 = min(npx, (int)threadIdx.x * chunk), i1 = min(npx, i0 + chunk);
-    auto survivor = [&](int i, int* sv) -> bool {
-        const int r = i / cw + 1, q = i % cw + 1;
-        const uint8_t* p = s + r * lw + q;
+    const int r0 = cw > 0 ? i0 / cw : 0, q0 = i0 - r0 * cw;
+    auto survivor = [&](int r, int q, int* sv) -> bool {
+        const uint8_t* p = s + (r + 1) * lw + (q + 1);
         const int v = p[0];
         *sv = v;
         if (v < 2) return false;
@@ -217,22 +223,36 @@ __global__ void __launch_bounds__(256) k_adapt_cand(const uint8_t* __restrict__ 
         return v > m;
     };
     int cnt = 0;
-    for (int i = i0; i < i1; i++) {
-        int sv;
-        if (survivor(i, &sv)) {
-            cnt++;
-            atomicAdd(&sh[sv], 1);
+    uint32_t smask = 0;
+    {
+        int r = r0, q = q0;
+        for (int i = i0; i < i1; i++) {
+            int sv;
+            if (survivor(r, q, &sv)) {
+                cnt++;
+                atomicAdd(&sh[sv], 1);
+                if (i - i0 < 32) smask |= 1u << (i - i0);
+            }
+            if (++q == cw) {
+                q = 0;
+                r++;
+            }
         }
     }
     int2 tot;
     const int2 base = block_scan2i(cnt, 0, reinterpret_cast<int(*)[2]>(ws), &tot);
     uint32_t* out = cand + (size_t)f * cand_stride + B.cand_off;
     int o = base.x;
-    for (int i = i0; i < i1; i++) {
-        int sv;
-        if (survivor(i, &sv)) {
-            const int y = B.y0 + i / cw, x = C.c0 + i % cw;
-            out[o++] = ((uint32_t)sv << 24) | ((uint32_t)y << 12) | (uint32_t)x;
+    {
+        int r = r0, q = q0;
+        for (int i = i0; i < i1; i++) {
+            int sv = s[(r + 1) * lw + (q + 1)];
+            const bool keep = (i - i0 < 32) ? ((smask >> (i - i0)) & 1u) != 0 : survivor(r, q, &sv);
+            if (keep) out[o++] = ((uint32_t)sv << 24) | ((uint32_t)(B.y0 + r) << 12) | (uint32_t)(C.c0 + q);
+            if (++q == cw) {
+                q = 0;
+                r++;
+            }
         }
     }
     if (threadIdx.x == 0) band_cnt[(size_t)f * nbands + blockIdx.x] = tot.x;
