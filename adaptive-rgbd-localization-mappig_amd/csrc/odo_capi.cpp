@@ -87,7 +87,7 @@ struct odo_ctx {
     hipStream_t pstream2 = nullptr;  // pair stages of odd batches (schedule 5)
     hipStream_t pstream3 = nullptr;  // third pair stream (schedule 5, ODO_PSTREAMS=3)
     int npstreams = 2;
-    bool knn_pair = false;  // schedule 5, ODO_KNN_PAIR=1: kNN-2 at the head of the pair stream (measured +1.8%, within noise; kNN roofline 0.82 vs 0.92)
+    bool knn_pair = true;  // schedule 5 (ODO_KNN_PAIR=0: on the extraction stream): kNN-2 at the head of the pair stream, 88.2k vs 86.5k frames/s (kNN roofline 0.85 vs 0.90)
     hipStream_t cur_p = nullptr;     // pair stream of the batch being queued
     std::vector<hipStream_t> owned;  // streams created (the rest alias them)
     hipEvent_t ev_latch = nullptr;   // after the last queued k_latch (schedule 5)
