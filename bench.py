@@ -196,8 +196,9 @@ def main():
 
     if world > 1:
         dist.barrier()
-    # Hamming-match (kNN-2) launches are bracketed by HIP events on their own
-    # (extraction) stream inside the timed region (odo timing mode 2)
+    # Hamming-match (kNN-2) launches are bracketed by HIP events on the stream
+    # that runs them (a pair stream by default) inside the timed region (odo
+    # timing mode 2)
     if not args.no_kernel_timing:
         odo.set_timing(None, mode=2)
     torch.cuda.synchronize()
