@@ -117,6 +117,16 @@ inline odo_ctx* shared_ctx() {
     if (!g.ctx) g.ctx = make_ctx(default_config(640, 480), g.device);
     return g.ctx.get();
 }
+// ProjectionMatch needs the frame's image bounds: one context per image size.
+inline odo_ctx* geometry_ctx(int width, int height) {
+    Globals& g = G();
+    std::lock_guard<std::mutex> lk(g.mu);
+    static std::vector<std::pair<std::pair<int, int>, std::shared_ptr<odo_ctx>>> by_size;
+    for (auto& e : by_size)
+        if (e.first.first == width && e.first.second == height) return e.second.get();
+    by_size.emplace_back(std::make_pair(width, height), make_ctx(default_config(width, height), g.device));
+    return by_size.back().second.get();
+}
 }  // namespace detail
 
 // srand(seed) for the stream Ransac::SampleMatches draws from (main.cpp:27).
@@ -141,6 +151,9 @@ struct Landmark {
     int nObs = 0;  // Observations(): 0 for visual-odometry temporal points
     bool mbBad = false;
     uint8_t mDescriptor[32] = {};
+    // set by Matcher::ProjectionMatch's isInFrustum (frame.cpp:100-133)
+    bool mbTrackInView = false;
+    float mTrackProjX = 0, mTrackProjY = 0, mTrackProjXR = 0;
     int Observations() const { return nObs; }
     bool isBad() const { return mbBad; }
 };
@@ -259,6 +272,8 @@ public:
         mvbOutlier.assign(N, false);
     }
 
+    int Width() const { return mW; }
+    int Height() const { return mH; }
     void SetPose(const Pose& Tcw) { mTcw = Tcw; }
     Pose GetPose() const { return mTcw; }
 
@@ -360,6 +375,56 @@ public:
             vMatches12.push_back(DMatch{(int32_t)i1, (int32_t)i2, 0, d0});
         }
         return vMatches12.size();
+    }
+
+    // Tracking::SearchLocalLMs + Matcher::ProjectionMatch(pFrame, vpLandmarks, th)
+    // (tracking.cpp:368-405, matcher.cpp:90-145): landmarks already in the
+    // frame's slots are skipped (mnLastFrameSeen), the rest get isInFrustum at
+    // the frame's pose (frame.cpp:100-133; mbTrackInView / mTrackProj* set),
+    // then the windowed best / second-best search with the same-level ratio
+    // test in landmark order on the GPU. Matches go into the frame's slots
+    // (AddLandmark); returns their number.
+    size_t ProjectionMatch(Frame* pFrame, const std::vector<LandmarkPtr>& vpLandmarks, const float th = 3.0f) {
+        const int n = (int)pFrame->N, nL = (int)vpLandmarks.size();
+        std::vector<odo_landmark> lms(std::max(nL, 1));
+        for (int i = 0; i < nL; i++) {
+            const Landmark& L = *vpLandmarks[i];
+            odo_landmark& o = lms[i];
+            std::memcpy(o.X, L.mWorldPos, sizeof(o.X));
+            std::memcpy(o.desc, L.mDescriptor, 32);
+            o.flags = (L.isBad() ? ODO_LM_BAD : 0) | (L.Observations() > 0 ? ODO_LM_HAS_OBS : 0);
+            for (size_t j = 0; j < pFrame->N && !(o.flags & ODO_LM_SEEN); j++)
+                if (pFrame->mvpLandmarks[j].get() == vpLandmarks[i].get()) o.flags |= ODO_LM_SEEN;
+        }
+        std::vector<float> kun(2 * (size_t)std::max(n, 1));
+        std::vector<int32_t> oct(std::max(n, 1)), slot_lm(std::max(n, 1));
+        std::vector<uint8_t> taken(std::max(n, 1));
+        for (int j = 0; j < n; j++) {
+            kun[2 * j] = pFrame->mvKeysUn[j].x;
+            kun[2 * j + 1] = pFrame->mvKeysUn[j].y;
+            oct[j] = pFrame->mvKeysUn[j].octave;
+            const LandmarkPtr& lm = pFrame->mvpLandmarks[j];
+            taken[j] = lm && lm->Observations() > 0;
+        }
+        std::vector<float> proj(3 * (size_t)std::max(nL, 1));
+        int nm = 0;
+        Check(odo_projection_match(detail::geometry_ctx(pFrame->Width(), pFrame->Height()), pFrame->mTcw.data(),
+                                   lms.data(), nL, kun.data(), oct.data(), pFrame->mDescriptors.data(), n,
+                                   taken.data(), th, mfNNratio, slot_lm.data(), proj.data(), &nm),
+              "Matcher::ProjectionMatch");
+        for (int i = 0; i < nL; i++) {
+            Landmark& L = *vpLandmarks[i];
+            if (lms[i].flags & ODO_LM_SEEN) continue;
+            L.mbTrackInView = !std::isnan(proj[3 * i]);
+            if (L.mbTrackInView) {
+                L.mTrackProjX = proj[3 * i];
+                L.mTrackProjY = proj[3 * i + 1];
+                L.mTrackProjXR = proj[3 * i + 2];
+            }
+        }
+        for (int j = 0; j < n; j++)
+            if (slot_lm[j] >= 0) pFrame->AddLandmark(vpLandmarks[slot_lm[j]], j);
+        return (size_t)nm;
     }
 
     // Matcher::DescriptorDistance (matcher.cpp:20-38): bit-count Hamming.

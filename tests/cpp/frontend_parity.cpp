@@ -45,6 +45,63 @@ struct OracleFrame {
 
 static int run(int argc, char** argv);
 
+// Tracking::SearchLocalLMs' ProjectionMatch on the current frame at its PnP
+// pose against the previous frame's landmarks (some with observations, some
+// bad, the ones already matched into the frame skipped), through the mirror
+// and through the oracle on the same inputs. Returns the match count.
+static int check_projection(odo_hip::Frame& last, odo_hip::Frame& cur, const OracleFrame& o, const odo_calib& cal,
+                            int W, int H) {
+    std::vector<odo_hip::LandmarkPtr> lms;
+    for (size_t i = 0; i < last.N; i++)
+        if (last.mvpLandmarks[i]) lms.push_back(last.mvpLandmarks[i]);
+    for (size_t i = 0; i < lms.size(); i++) {
+        lms[i]->nObs = (i % 3 == 0) ? 1 : 0;
+        lms[i]->mbBad = (i % 17 == 5);
+    }
+    const int n = (int)cur.N, nL = (int)lms.size();
+    // oracle inputs from the frame state before the call
+    std::vector<odo_landmark> ol(std::max(nL, 1));
+    for (int i = 0; i < nL; i++) {
+        memcpy(ol[i].X, lms[i]->mWorldPos, 12);
+        memcpy(ol[i].desc, lms[i]->mDescriptor, 32);
+        ol[i].flags = (lms[i]->mbBad ? ODO_LM_BAD : 0) | (lms[i]->nObs > 0 ? ODO_LM_HAS_OBS : 0);
+        for (int j = 0; j < n; j++)
+            if (cur.mvpLandmarks[j] == lms[i]) ol[i].flags |= ODO_LM_SEEN;
+    }
+    std::vector<uint8_t> taken(std::max(n, 1));
+    std::vector<int32_t> oct(std::max(n, 1)), slot_lm(std::max(n, 1));
+    for (int j = 0; j < n; j++) {
+        taken[j] = cur.mvpLandmarks[j] && cur.mvpLandmarks[j]->nObs > 0;
+        oct[j] = o.kps[j].octave;
+    }
+    std::vector<odo_hip::LandmarkPtr> before = cur.mvpLandmarks;
+    float bounds[4];
+    oracle_image_bounds(&cal, W, H, bounds);
+    std::vector<float> proj(3 * (size_t)std::max(nL, 1));
+    const int onm = oracle_projection_match(cur.mTcw.data(), ol.data(), nL, o.kun.data(), oct.data(), o.desc.data(), n,
+                                            taken.data(), &cal, bounds, 8.0f, 0.8f, slot_lm.data(), proj.data());
+    odo_hip::Matcher matcher(0.8f);
+    const int nm = (int)matcher.ProjectionMatch(&cur, lms, 8.0f);
+    EXPECT(nm == onm, "ProjectionMatch: %d matches vs oracle %d", nm, onm);
+    int slot_diff = 0, view_diff = 0;
+    for (int j = 0; j < n; j++) {
+        const odo_hip::LandmarkPtr want = slot_lm[j] >= 0 ? lms[slot_lm[j]] : before[j];
+        slot_diff += cur.mvpLandmarks[j] != want;
+    }
+    for (int i = 0; i < nL; i++) {
+        if (ol[i].flags & ODO_LM_SEEN) continue;
+        const bool in = !std::isnan(proj[3 * i]);
+        view_diff += in != lms[i]->mbTrackInView;
+        if (in && lms[i]->mbTrackInView)
+            view_diff += memcmp(&proj[3 * i], &lms[i]->mTrackProjX, 4) != 0 ||
+                         memcmp(&proj[3 * i + 1], &lms[i]->mTrackProjY, 4) != 0 ||
+                         memcmp(&proj[3 * i + 2], &lms[i]->mTrackProjXR, 4) != 0;
+    }
+    EXPECT(slot_diff == 0, "ProjectionMatch: %d frame slots differ", slot_diff);
+    EXPECT(view_diff == 0, "ProjectionMatch: %d landmarks' isInFrustum projections differ", view_diff);
+    return nm;
+}
+
 int main(int argc, char** argv) {
     // the library never falls back to the CPU: without a gfx950 device the
     // first call that needs one throws odo_hip::Error
@@ -106,6 +163,7 @@ static int run(int argc, char** argv) {
     std::unique_ptr<odo_hip::Frame> last;
     OracleFrame olast;
     long total_matches = 0, total_inliers = 0, total_pnp = 0;
+    int proj_checked = -1;
     double max_dT = 0;
     for (int t = 0; t < F; t++) {
         auto cur = std::make_unique<odo_hip::Frame>(&bgr[npx * 3 * t], &dep[npx * t], W, H, 0.033 * t);
@@ -190,6 +248,7 @@ static int run(int argc, char** argv) {
                 EXPECT(flag_diff == 0, "pair %d: %d PnP outlier flags differ", t, flag_diff);
                 total_inliers += r.n_inliers;
                 total_pnp += pnp;
+                if (t == F - 1) proj_checked = check_projection(*last, *cur, o, cal, W, H);
             }
         }
         last = std::move(cur);
@@ -215,7 +274,9 @@ static int run(int argc, char** argv) {
         EXPECT(d < 1e-4, "Kabsch::Compute vs oracle: %g", d);
     }
 
-    printf("frontend_parity %s frames=%d matches=%ld ransac_inliers=%ld pnp_inliers=%ld max_dT=%.3g failures=%d\n",
-           adaptive ? "adaptive" : "orb_slam2", F, total_matches, total_inliers, total_pnp, max_dT, g_fail);
+    printf("frontend_parity %s frames=%d matches=%ld ransac_inliers=%ld pnp_inliers=%ld max_dT=%.3g "
+           "projection_matches=%d failures=%d\n",
+           adaptive ? "adaptive" : "orb_slam2", F, total_matches, total_inliers, total_pnp, max_dT, proj_checked,
+           g_fail);
     return g_fail ? 1 : 0;
 }

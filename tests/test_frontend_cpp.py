@@ -4,7 +4,9 @@ for Features/extractor.h, Core/frame.h, Features/matcher.h, Odometry/ransac.h,
 Odometry/pnpsolver.h, Odometry/kabsch.h) driven by tests/cpp/frontend_parity.cpp
 in the reference's Tracking::TrackFrame call pattern and checked against the
 oracle inside that program (bit-exact features / matches / RANSAC, PnP pose
-within 1e-4). The binary is built by build() (tests/cpp/Makefile) and links
+within 1e-4), then Matcher::ProjectionMatch of the last frame at its PnP pose
+against the previous frame's landmarks (slots and isInFrustum projections
+bit-exact). The binary is built by build() (tests/cpp/Makefile) and links
 libodo_hip.so + liboracle.so through relative rpaths."""
 import os
 import subprocess
@@ -62,3 +64,4 @@ def test_frontend_parity(tmp_path, mode):
     assert "failures=0" in r.stdout
     stats = dict(kv.split("=") for kv in r.stdout.split()[2:])
     assert int(stats["matches"]) > 100 and int(stats["pnp_inliers"]) > 50
+    assert int(stats["projection_matches"]) > 0
