@@ -957,6 +957,7 @@ void launch_fast(hipStream_t st, const uint8_t* pyr, size_t pyr_stride, const Ce
                  int nframes) {
     // LDS sized for the largest cell ROI of the context: the kernel is
     // occupancy-bound (one wave per workgroup), 7.5 KB at 44 px vs 8.9 KB at 48
+    // (20 KB at 72, only for small images)
     dim3 g(ncells, nframes);
     if (roi_max <= 40)
         hipLaunchKernelGGL(k_fast_cells<40>, g, dim3(64), 0, st, pyr, pyr_stride, cells, lv, cand, cand_cnt, ncells,
@@ -964,7 +965,10 @@ void launch_fast(hipStream_t st, const uint8_t* pyr, size_t pyr_stride, const Ce
     else if (roi_max <= 44)
         hipLaunchKernelGGL(k_fast_cells<44>, g, dim3(64), 0, st, pyr, pyr_stride, cells, lv, cand, cand_cnt, ncells,
                            cell_cap, ini_th, min_th);
-    else
+    else if (roi_max <= 48)
+        hipLaunchKernelGGL(k_fast_cells<48>, g, dim3(64), 0, st, pyr, pyr_stride, cells, lv, cand, cand_cnt, ncells,
+                           cell_cap, ini_th, min_th);
+    else  // small images: levels narrower than two 30-px cells
         hipLaunchKernelGGL(k_fast_cells<FAST_ROI_MAX>, g, dim3(64), 0, st, pyr, pyr_stride, cells, lv, cand, cand_cnt,
                            ncells, cell_cap, ini_th, min_th);
 }

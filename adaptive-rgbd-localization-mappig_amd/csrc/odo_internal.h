@@ -10,7 +10,7 @@
 
 namespace odo {
 
-#define FAST_ROI_MAX 48
+#define FAST_ROI_MAX 72  // largest FAST cell ROI side (a level narrower than 2 cells: up to 65)
 
 // One pyramid level of one frame (all frames share the geometry).
 struct LevelDesc {

@@ -1,0 +1,40 @@
+"""Frame sizes other than 640x480 (ORBextractor accepts any image): widths
+that are not a multiple of 4 (k_gray's per-pixel path, unaligned pitches),
+and small images whose upper pyramid levels are narrower than two 30-px FAST
+cells (cell ROIs up to 65 px, orbextractor.cpp:688-711). The batched GPU path
+against the oracle: keypoints, descriptors, geometry, matches and RANSAC
+bit-exact, PnP pose within 1e-4."""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from conftest import load_pkg, sequence
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,h", [(320, 240), (330, 250), (354, 286), (642, 482)])
+def test_gpu_frame_sizes(w, h):
+    pkg = load_pkg()
+    nf, iters, seed = 800, 200, 0x5EED0040
+    bgr, dep, _ = sequence(3, w, h, seed=seed)
+    cal = O.fr1_calib()
+    fr = [O.extract_frame(bgr[i], dep[i], O.orb_params(nf), cal) for i in range(3)]
+    cfg = pkg.default_config(w, h, 3, nfeatures=nf, iterations=iters)
+    odo = pkg.Odometry(cfg)
+    res = odo.track_batch_host(bgr, dep)
+    for i in range(3):
+        g = odo.frame(i)
+        assert len(g["kps"]) == len(fr[i]["kps"]) > 50, f"{w}x{h} frame {i}: N"
+        assert np.array_equal(g["kps"], fr[i]["kps"]), f"{w}x{h} frame {i}: keypoints"
+        assert np.array_equal(g["desc"], fr[i]["desc"]), f"{w}x{h} frame {i}: descriptors"
+        assert np.array_equal(g["kun"], fr[i]["kun"]) and np.array_equal(g["xyz"], fr[i]["xyz"])
+    latch = float("nan")
+    for p in range(1, 3):
+        r, _, matches, latch = O.track_pair(fr[p - 1], fr[p], cal, O.ransac_params(iters),
+                                            pkg.pair_seed(cfg.seed, p), latch)
+        assert np.array_equal(odo.pair(p)["matches"], matches), f"{w}x{h} pair {p}: matches"
+        assert (res[p]["n_matches"], res[p]["n_inliers"], res[p]["visited"]) == \
+            (r.n_matches, r.n_inliers, r.visited), f"{w}x{h} pair {p}: counts"
+        assert np.array_equal(res[p]["T12"], np.array(r.T12, np.float32)), f"{w}x{h} pair {p}: T12"
+        assert np.abs(res[p]["Tcw"] - np.array(r.Tcw, np.float32)).max() < 1e-4, f"{w}x{h} pair {p}: Tcw"
+    odo.close()
