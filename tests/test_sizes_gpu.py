@@ -38,3 +38,29 @@ def test_gpu_frame_sizes(w, h):
         assert np.array_equal(res[p]["T12"], np.array(r.T12, np.float32)), f"{w}x{h} pair {p}: T12"
         assert np.abs(res[p]["Tcw"] - np.array(r.Tcw, np.float32)).max() < 1e-4, f"{w}x{h} pair {p}: Tcw"
     odo.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,h", [(330, 250), (642, 482)])
+def test_gpu_adaptive_frame_sizes(w, h):
+    """Extractor(FAST, ORB, ADAPTIVE) at other sizes: the 3x3 grid's cells and
+    edge bands follow the image (videogridadaptedfeaturedetector.cpp:62-71)."""
+    pkg = load_pkg()
+    bgr, dep, _ = sequence(4, w, h, seed=0x5EED0041)
+    cfg = pkg.default_config(w, h, 4, nfeatures=1000, iterations=200, detector=pkg.DETECTOR_ADAPTIVE_FAST)
+    odo = pkg.Odometry(cfg)
+    cal = O.fr1_calib()
+    ex = O.AdaptiveExtractor()
+    ref = [ex.extract_frame(bgr[i], dep[i], cal) for i in range(4)]
+    res = odo.track_batch_host(bgr, dep)
+    for i in range(4):
+        g = odo.frame(i)
+        assert len(g["kps"]) == len(ref[i]["kps"]) > 20, f"{w}x{h} frame {i}: N"
+        assert np.array_equal(g["kps"], ref[i]["kps"]) and np.array_equal(g["desc"], ref[i]["desc"]), \
+            f"{w}x{h} frame {i}: keypoints / descriptors"
+    latch = float("nan")
+    for p in range(1, 4):
+        r, _, _, latch = O.track_pair(ref[p - 1], ref[p], cal, O.ransac_params(200), pkg.pair_seed(cfg.seed, p), latch)
+        assert np.array_equal(res[p]["T12"], np.array(r.T12, np.float32)), f"{w}x{h} pair {p}: T12"
+        assert np.abs(res[p]["Tcw"] - np.array(r.Tcw, np.float32)).max() < 1e-4, f"{w}x{h} pair {p}: Tcw"
+    odo.close()
