@@ -40,26 +40,41 @@ __global__ void __launch_bounds__(KNN_Q) k_knn2(const uint8_t* __restrict__ qdes
                                                 size_t q_stride, const uint8_t* __restrict__ tdesc,
                                                 const int* __restrict__ tn, size_t t_stride,
                                                 int2* __restrict__ out_idx, int2* __restrict__ out_dist,
-                                                size_t out_stride) {
+                                                size_t out_stride, const int32_t* __restrict__ qlist,
+                                                const int* __restrict__ qcnt, size_t ql_stride,
+                                                size_t split_stride, int npairs, int qblocks, int nsplit) {
 #ifndef ODO_KNN_PRIO
 #define ODO_KNN_PRIO 2  // co-runs with the previous batch's PnP: issue first (+0.07 roofline, same step time)
 #endif
     __builtin_amdgcn_s_setprio(ODO_KNN_PRIO);
     __shared__ uint4 tile[KNN_T * 2];
-    const int p = blockIdx.y;
-    const int nq = qn[p], nt = tn[p];
-    const int qi = blockIdx.x * KNN_Q + threadIdx.x;
-    if ((int)(blockIdx.x * KNN_Q) >= nq) return;
+    // A fixed grid (one round of resident workgroups) strides over the items
+    // (pair, block of KNN_Q queries, train split): with the landmark query
+    // lists, pairs have fewer and uneven query blocks, and a grid of one
+    // workgroup per item would leave a partial second round.
+    const int nitems = npairs * qblocks * nsplit;
+    for (int item = blockIdx.x; item < nitems; item += gridDim.x) {
+    const int h = item % nsplit, rq = item / nsplit;
+    const int qbk = rq % qblocks, p = rq / qblocks;
+    // with a query list (the batched path: F1 keypoints holding a landmark),
+    // position k of the list is query qlist[k]; without, every query
+    const int nq = qlist ? qcnt[p] : qn[p], nt = tn[p];
+    if (qbk * KNN_Q >= nq) continue;  // uniform over the workgroup
+    const int qpos = qbk * KNN_Q + threadIdx.x;
+    const int qi = qpos < nq ? (qlist ? qlist[(size_t)p * ql_stride + qpos] : qpos) : -1;
     const uint8_t* Q = qdesc + (size_t)p * q_stride;
     const uint8_t* T = tdesc + (size_t)p * t_stride;
     uint4 qa = make_uint4(0, 0, 0, 0), qb = make_uint4(0, 0, 0, 0);
-    if (qi < nq) {
+    if (qi >= 0) {
         qa = reinterpret_cast<const uint4*>(Q + (size_t)qi * 32)[0];
         qb = reinterpret_cast<const uint4*>(Q + (size_t)qi * 32)[1];
     }
+    // train split h: the splits' top-2 lists are merged by the consumer (k_pair_match)
+    const int S = nsplit;
+    const int tb = (int)((long)nt * h / S), te = (int)((long)nt * (h + 1) / S);
     uint32_t k0 = 0xFFFFFFFFu, k1 = 0xFFFFFFFFu;
-    for (int t0 = 0; t0 < nt; t0 += KNN_T) {
-        const int tcount = min(KNN_T, nt - t0);
+    for (int t0 = tb; t0 < te; t0 += KNN_T) {
+        const int tcount = min(KNN_T, te - t0);
         __syncthreads();
         for (int i = threadIdx.x; i < tcount * 2; i += KNN_Q)
             tile[i] = reinterpret_cast<const uint4*>(T + (size_t)t0 * 32)[i];
@@ -105,14 +120,15 @@ __global__ void __launch_bounds__(KNN_Q) k_knn2(const uint8_t* __restrict__ qdes
             k0 = min(k0, key);
         }
     }
-    if (qi < nq) {
+    if (qi >= 0) {
         int2 I, D;
         I.x = k0 == 0xFFFFFFFFu ? -1 : (int)(k0 & 0xFFFFF);
         D.x = k0 == 0xFFFFFFFFu ? 0x7FFFFFFF : (int)(k0 >> 20);
         I.y = k1 == 0xFFFFFFFFu ? -1 : (int)(k1 & 0xFFFFF);
         D.y = k1 == 0xFFFFFFFFu ? 0x7FFFFFFF : (int)(k1 >> 20);
-        out_idx[(size_t)p * out_stride + qi] = I;
-        out_dist[(size_t)p * out_stride + qi] = D;
+        out_idx[(size_t)h * split_stride + (size_t)p * out_stride + qi] = I;
+        out_dist[(size_t)h * split_stride + (size_t)p * out_stride + qi] = D;
+    }
     }
 }
 
@@ -510,34 +526,28 @@ ODO_INLINE void block_gnu_sort(SortEl* A, int n, uint8_t* work, PSortRanges& R) 
     __syncthreads();
 }
 
-// ============================================================ per-pair match stage
-// One workgroup (256 threads) per pair (F1 = previous frame, F2 = current).
-// Outputs: good matches sorted per std::sort (query/train/distance), counts,
-// f2_src[i2] = F1 index whose landmark sits in F2 slot i2 (-1 if none).
 #define PM_THREADS 256
 
-__global__ void __launch_bounds__(PM_THREADS) k_pair_match(
-    const int2* __restrict__ knn_idx, const int2* __restrict__ knn_dist, size_t knn_stride,
-    const float* __restrict__ xyz, const int* __restrict__ nkp, int kp_cap, int slot0, float ratio,
-    float th_depth_m, int check_depth, odo_dmatch* __restrict__ matches, int* __restrict__ n_matches,
-    SortEl* __restrict__ good, int* __restrict__ n_good, int32_t* __restrict__ f2_src,
-    uint64_t* __restrict__ sort_scratch, int match_cap) {
-    __builtin_amdgcn_s_setprio(ODO_WAVE_PRIO);  // latency-bound: issue ahead of co-resident extraction waves
-    __shared__ int s_cnt[PM_THREADS];
-    __shared__ int s_tot, s_total_valid, s_cle, s_K, s_nm;
-    extern __shared__ __attribute__((aligned(16))) uint64_t dyn_lds[];  // pw entries
-    const int p = blockIdx.x;                  // pair index
-    const int s1 = slot0 + p, s2 = slot0 + p + 1;
-    const int n1 = nkp[s1], n2 = nkp[s2];
-    const int t = threadIdx.x;
+// ============================================================ VO landmarks
+// Tracking::UpdateLastFrame's visual-odometry landmarks of every query frame
+// (F1 of pair p, tracking.cpp:146-190): the K smallest (z, index) pairs among
+// z > 0, K = min(valid, max(#(z <= th) + 1, 101)): with #(z <= th) >= 100 the
+// points within th plus the nearest one beyond, else a bitonic sort in LDS.
+// Outputs the landmark bit set and the landmark keypoints in index order.
+// Matcher::KnnMatch drops every query without a landmark (matcher.cpp:70-72),
+// so kNN-2 runs on this list alone; its matches are unchanged.
+__global__ void __launch_bounds__(PM_THREADS) k_vo_lm(const float* __restrict__ xyz, const int* __restrict__ nkp,
+                                                      int kp_cap, int slot0, float th_depth_m,
+                                                      uint32_t* __restrict__ lm_g, int lm_words,
+                                                      int32_t* __restrict__ qlist, int* __restrict__ qcnt) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t sk[];  // pw entries
+    __shared__ int s_total_valid, s_cle, s_w[PM_THREADS / 64];
+    __shared__ unsigned long long s_min;
+    __shared__ uint32_t bits[(8192 + 31) / 32];
+    const int p = blockIdx.x, t = threadIdx.x;
+    const int s1 = slot0 + p;
+    const int n1 = nkp[s1];
     const float* X1 = xyz + (size_t)s1 * kp_cap * 3;
-    const float* X2 = xyz + (size_t)s2 * kp_cap * 3;
-    uint64_t* sk = dyn_lds;
-    (void)sort_scratch;
-    int32_t* src = f2_src + (size_t)p * kp_cap;
-    for (int i = t; i < n2; i += PM_THREADS) src[i] = -1;
-    // ---- VO landmarks on F1 (UpdateLastFrame, tracking.cpp:146-190): the K smallest
-    // (z, index) pairs among z>0, K = min(valid, max(#(z<=th)+1, 101)).
     int cv = 0, cle = 0;
     for (int i = t; i < n1; i += PM_THREADS) {
         const float z = X1[3 * i + 2];
@@ -550,6 +560,7 @@ __global__ void __launch_bounds__(PM_THREADS) k_pair_match(
         s_total_valid = 0;
         s_cle = 0;
     }
+    for (int i = t; i < lm_words; i += PM_THREADS) bits[i] = 0;
     __syncthreads();
     atomicAdd(&s_total_valid, cv);
     atomicAdd(&s_cle, cle);
@@ -557,7 +568,32 @@ __global__ void __launch_bounds__(PM_THREADS) k_pair_match(
     const int valid = s_total_valid;
     int K = s_cle + 1 > 101 ? s_cle + 1 : 101;
     if (K > valid) K = valid;
-    // rank selection: sort (z_bits<<32 | i) ascending with a bitonic sort in global scratch
+    if (s_cle >= 100) {
+        // the common case, K = #(z <= th) + 1 (or all valid): every point with
+        // z <= th plus the smallest (z, index) beyond th — no sort needed
+        if (t == 0) s_min = ~0ull;
+        __syncthreads();
+        uint64_t mk = ~0ull;
+        for (int i = t; i < n1; i += PM_THREADS) {
+            const float z = X1[3 * i + 2];
+            if (z > 0) {
+                if (z <= th_depth_m)
+                    atomicOr(&bits[i >> 5], 1u << (i & 31));
+                else {
+                    const uint64_t key = ((uint64_t)__float_as_uint(z) << 32) | (uint32_t)i;
+                    mk = key < mk ? key : mk;
+                }
+            }
+        }
+        atomicMin(&s_min, mk);
+        __syncthreads();
+        if (t == 0 && K > s_cle && s_min != ~0ull) {
+            const int i = (int)(uint32_t)s_min;
+            bits[i >> 5] |= 1u << (i & 31);
+        }
+        __syncthreads();
+    } else {
+    // rank selection: sort (z_bits << 32 | i) ascending (z > 0: the float bits order as integers)
     int pw = 1;
     while (pw < n1) pw <<= 1;
     for (int i = t; i < pw; i += PM_THREADS) {
@@ -584,15 +620,66 @@ __global__ void __launch_bounds__(PM_THREADS) k_pair_match(
             }
             __syncthreads();
         }
-    // has_lm flag for F1 index i: stored in the low bit field of a second pass over sk
-    // (reuse sk[pw + ..] is not available; mark via s2 knn output? use a bitmap in LDS)
-    __shared__ uint32_t lm_bits[(8192 + 31) / 32];
-    for (int i = t; i < (kp_cap + 31) / 32 && i < (8192 + 31) / 32; i += PM_THREADS) lm_bits[i] = 0;
-    __syncthreads();
     for (int r = t; r < K; r += PM_THREADS) {
         const int i = (int)(uint32_t)sk[r];
-        atomicOr(&lm_bits[i >> 5], 1u << (i & 31));
+        atomicOr(&bits[i >> 5], 1u << (i & 31));
     }
+    __syncthreads();
+    }
+    for (int i = t; i < lm_words; i += PM_THREADS) lm_g[(size_t)p * lm_words + i] = bits[i];
+    // the landmark keypoints in index order
+    const int wave = t >> 6, lane = t & 63;
+    int base = 0;
+    for (int c0 = 0; c0 < n1; c0 += PM_THREADS) {
+        const int i = c0 + t;
+        const bool keep = i < n1 && ((bits[i >> 5] >> (i & 31)) & 1u);
+        const uint64_t bal = __ballot(keep);
+        if (lane == 0) s_w[wave] = __popcll(bal);
+        __syncthreads();
+        int before = 0, tot = 0;
+        for (int w = 0; w < PM_THREADS / 64; w++) {
+            if (w < wave) before += s_w[w];
+            tot += s_w[w];
+        }
+        if (keep)
+            qlist[(size_t)p * kp_cap + base + before +
+                  __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0))] = i;
+        base += tot;
+        __syncthreads();
+    }
+    if (t == 0) qcnt[p] = base;
+}
+
+// ============================================================ per-pair match stage
+// One workgroup (256 threads) per pair (F1 = previous frame, F2 = current).
+// Outputs: good matches sorted per std::sort (query/train/distance), counts,
+// f2_src[i2] = F1 index whose landmark sits in F2 slot i2 (-1 if none).
+__global__ void __launch_bounds__(PM_THREADS) k_pair_match(
+    const int2* __restrict__ knn_idx, const int2* __restrict__ knn_dist, size_t knn_stride,
+    const float* __restrict__ xyz, const int* __restrict__ nkp, int kp_cap, int slot0, float ratio,
+    const uint32_t* __restrict__ lm_g, int lm_words, int nsplit, size_t split_stride, int check_depth,
+    odo_dmatch* __restrict__ matches,
+    int* __restrict__ n_matches,
+    SortEl* __restrict__ good, int* __restrict__ n_good, int32_t* __restrict__ f2_src,
+    uint64_t* __restrict__ sort_scratch, int match_cap) {
+    __builtin_amdgcn_s_setprio(ODO_WAVE_PRIO);  // latency-bound: issue ahead of co-resident extraction waves
+    __shared__ int s_cnt[PM_THREADS];
+    extern __shared__ __attribute__((aligned(16))) uint64_t dyn_lds[];  // pw entries
+    const int p = blockIdx.x;                  // pair index
+    const int s1 = slot0 + p, s2 = slot0 + p + 1;
+    const int n1 = nkp[s1], n2 = nkp[s2];
+    const int t = threadIdx.x;
+    const float* X1 = xyz + (size_t)s1 * kp_cap * 3;
+    const float* X2 = xyz + (size_t)s2 * kp_cap * 3;
+    (void)sort_scratch;
+    int32_t* src = f2_src + (size_t)p * kp_cap;
+    for (int i = t; i < n2; i += PM_THREADS) src[i] = -1;
+    // ---- VO landmarks on F1 (UpdateLastFrame, tracking.cpp:146-190): the bit
+    // set k_vo_lm computed before kNN-2 (queries without one have no kNN-2 output)
+    int pw = 1;
+    while (pw < n1) pw <<= 1;
+    __shared__ uint32_t lm_bits[(8192 + 31) / 32];
+    for (int i = t; i < lm_words; i += PM_THREADS) lm_bits[i] = lm_g[(size_t)p * lm_words + i];
     __syncthreads();
     // ---- ratio test + bookkeeping in query order (all F1 landmarks are fresh
     // VO landmarks with 0 observations and F2 starts empty, so no match is
@@ -605,12 +692,22 @@ __global__ void __launch_bounds__(PM_THREADS) k_pair_match(
         const int i = c0 + t;
         bool acc = false;
         int2 I = make_int2(-1, -1), D = make_int2(0, 0);
-        if (i < n1) {
-            I = KI[i];
-            D = KD[i];
+        if (i < n1 && ((lm_bits[i >> 5] >> (i & 31)) & 1)) {  // kNN-2 ran on landmark queries only
+            // the train splits' top-2 lists merged: the two smallest (distance, index) keys
+            uint32_t k0 = 0xFFFFFFFFu, k1 = 0xFFFFFFFFu;
+            for (int h = 0; h < nsplit; h++) {
+                const int2 Ih = KI[(size_t)h * split_stride + i], Dh = KD[(size_t)h * split_stride + i];
+                const uint32_t a = Ih.x >= 0 ? ((uint32_t)Dh.x << 20) | (uint32_t)Ih.x : 0xFFFFFFFFu;
+                const uint32_t b = Ih.y >= 0 ? ((uint32_t)Dh.y << 20) | (uint32_t)Ih.y : 0xFFFFFFFFu;
+                // two sorted pairs: second smallest = min(max(k0, a), k1, b)
+                k1 = min(max(k0, a), min(k1, b));
+                k0 = min(k0, a);
+            }
+            I = make_int2(k0 == 0xFFFFFFFFu ? -1 : (int)(k0 & 0xFFFFF), k1 == 0xFFFFFFFFu ? -1 : (int)(k1 & 0xFFFFF));
+            D = make_int2(k0 == 0xFFFFFFFFu ? 0x7FFFFFFF : (int)(k0 >> 20), k1 == 0xFFFFFFFFu ? 0x7FFFFFFF : (int)(k1 >> 20));
             if (I.x >= 0) {
                 const float d0 = (float)D.x, d1 = (float)D.y;
-                acc = (d0 < ratio * d1) && ((lm_bits[i >> 5] >> (i & 31)) & 1);
+                acc = d0 < ratio * d1;
             }
         }
         s_cnt[t] = acc;
@@ -712,12 +809,34 @@ __global__ void k_latch(double* __restrict__ latch, const SortEl* __restrict__ g
 
 namespace odo {
 void launch_knn2(hipStream_t st, const uint8_t* q, const int* qn, size_t q_stride, const uint8_t* t, const int* tn,
-                 size_t t_stride, int2* idx, int2* dist, size_t out_stride, int max_q, int npairs) {
-    dim3 g((max_q + KNN_Q - 1) / KNN_Q, npairs);
-    hipLaunchKernelGGL(k_knn2, g, dim3(KNN_Q), 0, st, q, qn, q_stride, t, tn, t_stride, idx, dist, out_stride);
+                 size_t t_stride, int2* idx, int2* dist, size_t out_stride, int max_q, int npairs,
+                 const int32_t* qlist, const int* qcnt, size_t ql_stride, int nsplit, size_t split_stride) {
+    static int resident = 0;  // workgroups of one full round: 8 four-wave workgroups per CU
+    if (!resident) {
+        int dev = 0, cus = 256;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        resident = 8 * cus;
+    }
+    const int qblocks = (max_q + KNN_Q - 1) / KNN_Q;
+    const int nitems = qblocks * npairs * nsplit;
+    if (nitems <= 0) return;
+    dim3 g(std::min(nitems, resident));
+    hipLaunchKernelGGL(k_knn2, g, dim3(KNN_Q), 0, st, q, qn, q_stride, t, tn, t_stride, idx, dist, out_stride, qlist,
+                       qcnt, ql_stride, split_stride, npairs, qblocks, nsplit);
+}
+void launch_vo_lm(hipStream_t st, const float* xyz, const int* nkp, int kp_cap, int slot0, float th_depth_m,
+                  uint32_t* lm_bits, int lm_words, int32_t* qlist, int* qcnt, int npairs) {
+    int pw = 1;
+    while (pw < kp_cap) pw <<= 1;
+    const size_t lds = (size_t)pw * 8;
+    if (lds > 64 * 1024) hipFuncSetAttribute((const void*)k_vo_lm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_vo_lm, dim3(npairs), dim3(PM_THREADS), lds, st, xyz, nkp, kp_cap, slot0, th_depth_m, lm_bits,
+                       lm_words, qlist, qcnt);
 }
 void launch_pair_match(hipStream_t st, const int2* knn_idx, const int2* knn_dist, size_t knn_stride, const float* xyz,
-                       const int* nkp, int kp_cap, int slot0, float ratio, float th_depth_m, int check_depth,
+                       const int* nkp, int kp_cap, int slot0, float ratio, const uint32_t* lm_bits, int lm_words,
+                       int nsplit, size_t split_stride, int check_depth,
                        odo_dmatch* matches, int* n_matches, void* good, int* n_good, int32_t* f2_src,
                        uint64_t* sort_scratch, int match_cap, int npairs) {
     int pw = 1;
@@ -725,7 +844,9 @@ void launch_pair_match(hipStream_t st, const int2* knn_idx, const int2* knn_dist
     const size_t lds = psort_lds_bytes(pw);
     if (lds > 64 * 1024) hipFuncSetAttribute((const void*)k_pair_match, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(k_pair_match, dim3(npairs), dim3(PM_THREADS), lds, st, knn_idx, knn_dist, knn_stride, xyz, nkp,
-                       kp_cap, slot0, ratio, th_depth_m, check_depth, matches, n_matches, (SortEl*)good, n_good, f2_src,
+                       kp_cap, slot0, ratio, lm_bits, lm_words, nsplit, split_stride, check_depth, matches, n_matches,
+                       (SortEl*)good, n_good,
+                       f2_src,
                        sort_scratch, match_cap);
 }
 // odo_debug_sort: the pair stage's std::sort on an arbitrary key array

@@ -125,6 +125,12 @@ struct odo_ctx {
     uint16_t* depth_in = nullptr;
     // pair buffers ([maxb])
     int2 *knn_idx[NSETS] = {}, *knn_dist[NSETS] = {};  // per frame set
+    // per frame set: the query frames' VO-landmark bits and kNN-2 query lists
+    uint32_t* lm_bits[NSETS] = {};
+    int32_t* qlist[NSETS] = {};
+    int* qcnt[NSETS] = {};
+    int lm_words = 0;
+    int knn_split = 8;  // kNN-2 train splits per query block (ODO_KNN_SPLIT): more waves for short query lists
     uint64_t* sort_scratch = nullptr;
     double* latch = nullptr;
     void* rscr[NSETS] = {};  // RANSAC scratch per frame set
@@ -247,7 +253,7 @@ static void free_ctx(odo_ctx* c) {
     for (void* p : ptrs)
         if (p) hipFree(p);
     for (int i = 0; i < NSETS; i++) {
-        void* pp[] = {c->knn_idx[i], c->knn_dist[i], c->rscr[i]};
+        void* pp[] = {c->knn_idx[i], c->knn_dist[i], c->rscr[i], c->lm_bits[i], c->qlist[i], c->qcnt[i]};
         for (void* q : pp)
             if (q) hipFree(q);
     }
@@ -548,9 +554,14 @@ static int alloc_buffers(odo_ctx* c) {
     if ((e = dalloc(&c->nkp, S))) return e;
     if ((e = dalloc(&c->bgr_in, B * c->W * c->H * 3))) return e;
     if ((e = dalloc(&c->depth_in, B * c->W * c->H))) return e;
+    c->lm_words = (c->kp_cap + 31) / 32;
+    if (const char* ks = getenv("ODO_KNN_SPLIT")) c->knn_split = std::min(8, std::max(1, atoi(ks)));
     for (int i = 0; i < NSETS; i++) {
-        if ((e = dalloc(&c->knn_idx[i], B * c->kp_cap))) return e;
-        if ((e = dalloc(&c->knn_dist[i], B * c->kp_cap))) return e;
+        if ((e = dalloc(&c->knn_idx[i], (size_t)c->knn_split * B * c->kp_cap))) return e;
+        if ((e = dalloc(&c->knn_dist[i], (size_t)c->knn_split * B * c->kp_cap))) return e;
+        if ((e = dalloc(&c->lm_bits[i], B * c->lm_words))) return e;
+        if ((e = dalloc(&c->qlist[i], B * c->kp_cap))) return e;
+        if ((e = dalloc(&c->qcnt[i], B))) return e;
     }
     for (auto& P : c->pb) {
         if ((e = dalloc(&P.matches, B * c->match_cap))) return e;
@@ -924,9 +935,8 @@ static int run_pairs(odo_ctx* c, int set, int n) {
     float* xyz = c->xyz + b * KC * 3;
     tmark(c, 6, st);
     launch_pair_valid(st, P.pair_valid, n, c->has_prev ? 1 : 0);
-    const float mThDepth = c->cfg.calib.mbf * c->cfg.calib.th_depth / c->cfg.calib.fx;
-    launch_pair_match(st, c->knn_idx[set], c->knn_dist[set], KC, xyz, nkp, c->kp_cap, 0, c->cfg.nn_ratio, mThDepth,
-                      c->cfg.ransac.check_depth, P.matches, P.n_matches, P.good, P.n_good, P.f2_src,
+    launch_pair_match(st, c->knn_idx[set], c->knn_dist[set], KC, xyz, nkp, c->kp_cap, 0, c->cfg.nn_ratio,
+                      c->lm_bits[set], c->lm_words, c->knn_split, (size_t)c->maxb * KC, c->cfg.ransac.check_depth, P.matches, P.n_matches, P.good, P.n_good, P.f2_src,
                       c->sort_scratch, c->match_cap, n);
     // the DepthCovariance latch is taken from the first valid pair ever: with
     // two pair streams, a batch's latch kernel runs after the previous one's
@@ -996,8 +1006,13 @@ static int finish_batch(odo_ctx* c, int set, int n, odo_pair_result* h_results) 
     HIPCHK(hipMemcpy(h_results, P.res, n * sizeof(odo_pair_result), hipMemcpyDeviceToHost));
     std::vector<int> nm(n);
     HIPCHK(hipMemcpy(nm.data(), P.n_matches, n * sizeof(int), hipMemcpyDeviceToHost));
-    // n_matches into the result records
-    for (int i = 0; i < n; i++) h_results[i].n_matches = c->valid_h[i] ? nm[i] : 0;
+    std::vector<int> nq(n);
+    HIPCHK(hipMemcpy(nq.data(), c->qcnt[set], n * sizeof(int), hipMemcpyDeviceToHost));
+    // n_matches and the kNN-2 query counts into the result records
+    for (int i = 0; i < n; i++) {
+        h_results[i].n_matches = c->valid_h[i] ? nm[i] : 0;
+        h_results[i].n_queries = c->valid_h[i] ? nq[i] : 0;
+    }
     return ODO_OK;
 }
 
@@ -1039,6 +1054,10 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
         const size_t b = fbase(c, s);
         uint8_t* desc = c->desc + b * KC * 32;
         int* nkp = c->nkp + b;
+        // the query frames' VO landmarks first: kNN-2 runs on their keypoints only
+        const float mThDepth = c->cfg.calib.mbf * c->cfg.calib.th_depth / c->cfg.calib.fx;
+        launch_vo_lm(kst, c->xyz + b * KC * 3, nkp, c->kp_cap, 0, mThDepth, c->lm_bits[s], c->lm_words, c->qlist[s],
+                     c->qcnt[s], n);
         int kt = -1;
         if (c->ktiming) {
             kt = c->kt_next;
@@ -1051,7 +1070,7 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
         }
         if (!(c->skip & 8))
             launch_knn2(kst, desc, nkp, KC * 32, desc + KC * 32, nkp + 1, KC * 32, c->knn_idx[s], c->knn_dist[s], KC,
-                        c->kp_cap, n);
+                        c->kp_cap, n, c->qlist[s], c->qcnt[s], KC, c->knn_split, (size_t)c->maxb * KC);
         if (kt >= 0) {
             HIPCHK(hipEventRecord(c->kt1[kt], kst));
             c->kt_next = (kt + 1) % odo_ctx::KT_RING;

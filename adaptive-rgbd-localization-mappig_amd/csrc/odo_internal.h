@@ -153,9 +153,14 @@ void launch_copy_frame(hipStream_t st, const orb_kp* kps_s, const uint8_t* desc_
                        const float* xyz_s, const float* ur_s, const int* n_s, orb_kp* kps_d, uint8_t* desc_d,
                        float* kun_d, float* xyz_d, float* ur_d, int* n_d, int kp_cap);
 void launch_knn2(hipStream_t st, const uint8_t* q, const int* qn, size_t q_stride, const uint8_t* t, const int* tn,
-                 size_t t_stride, int2* idx, int2* dist, size_t out_stride, int max_q, int npairs);
+                 size_t t_stride, int2* idx, int2* dist, size_t out_stride, int max_q, int npairs,
+                 const int32_t* qlist = nullptr, const int* qcnt = nullptr, size_t ql_stride = 0, int nsplit = 1,
+                 size_t split_stride = 0);
+void launch_vo_lm(hipStream_t st, const float* xyz, const int* nkp, int kp_cap, int slot0, float th_depth_m,
+                  uint32_t* lm_bits, int lm_words, int32_t* qlist, int* qcnt, int npairs);
 void launch_pair_match(hipStream_t st, const int2* knn_idx, const int2* knn_dist, size_t knn_stride, const float* xyz,
-                       const int* nkp, int kp_cap, int slot0, float ratio, float th_depth_m, int check_depth,
+                       const int* nkp, int kp_cap, int slot0, float ratio, const uint32_t* lm_bits, int lm_words,
+                       int nsplit, size_t split_stride, int check_depth,
                        odo_dmatch* matches, int* n_matches, void* good, int* n_good, int32_t* f2_src,
                        uint64_t* sort_scratch, int match_cap, int npairs);
 int launch_sort_dbg(hipStream_t st, void* a, int n);

@@ -191,6 +191,9 @@ def main():
     res = odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=True)
     for _ in range(args.warmup):
         odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=False)
+    # untimed: a batch whose pair 0 links to the previous batch, as in the timed
+    # steps, for the kNN-2 query counts (F1 keypoints holding a VO landmark)
+    res_q = odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=True)
     odo.synchronize()
     torch.cuda.synchronize()
 
@@ -236,9 +239,12 @@ def main():
     # algorithmic lane-ops of one launch / its live mean duration.
     roofline = None
     if knn_ms:
-        # pair p = (slot p, slot p+1); slot 0 is the previous batch's last frame
-        # (the same sequence is tracked every step)
-        cmp = nkp[B - 1] * nkp[0] + sum(nkp[i] * nkp[i + 1] for i in range(B - 1))
+        # result i = pair (frame i-1, frame i); frame -1 is the previous batch's
+        # last frame (the same sequence is tracked every step). kNN-2 compares
+        # the query frame's landmark keypoints (n_queries) with every keypoint
+        # of frame i: Matcher::KnnMatch drops the other queries' matches
+        nq = res_q["n_queries"]
+        cmp = int(sum(int(nq[i]) * nkp[i] for i in range(B)))
         ops = float(KNN_OPS_PER_CMP) * cmp
         ach = ops / (knn_ms * 1e-3) / 1e12
         traffic = None
@@ -254,7 +260,7 @@ def main():
                     "kernel": "k_knn2", "kernel_ms": round(knn_ms, 4), "launches": knn_launches,
                     "work": f"{cmp} descriptor comparisons x {KNN_OPS_PER_CMP} int32 lane-ops",
                     # algorithmic HBM bytes: every descriptor read once, 16 B of top-2 out per query
-                    "hbm_gbs": round(sum(2 * 32 * nkp[i] + 16 * nkp[i] for i in range(B)) /
+                    "hbm_gbs": round(sum(32 * int(nq[i]) + 32 * nkp[i] + 16 * int(nq[i]) for i in range(B)) /
                                      (knn_ms * 1e-3) / 1e9, 1)}
 
     cpu = None
@@ -287,6 +293,7 @@ def main():
                                     f"RANSAC {args.iters}"),
                        "frames_per_step": B, "global_batch": B * world, "parallelism": f"frames x{world}",
                        "mean_keypoints": round(nkp_mean, 1),
+                       "mean_knn_queries": round(float(np.mean(res_q["n_queries"])), 1),
                        "mean_matches": round(float(np.mean(ok["n_matches"])), 1),
                        "mean_ransac_inliers": round(float(np.mean(ok["n_inliers"])), 1),
                        "mean_ransac_visited": round(float(np.mean(ok["visited"])), 1),

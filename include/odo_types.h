@@ -127,7 +127,7 @@ typedef struct odo_pair_result {
     int32_t ransac_ok;    /* Ransac::Iterate return */
     int32_t pnp_inliers;  /* PnPSolver::Compute return */
     int32_t visited;      /* RANSAC iterations actually run (realIters) */
-    int32_t pad;
+    int32_t n_queries;    /* kNN-2 queries: F1 keypoints holding a VO landmark (the only ones KnnMatch keeps) */
 } odo_pair_result;
 
 #ifdef __cplusplus

@@ -1325,7 +1325,7 @@ int oracle_track_pair(const orb_kp* k1, const uint8_t* d1, const float* xyz1, in
     std::vector<uint8_t> has_lm(n1), out1(n1, 0);
     std::vector<int32_t> obs1(n1, 0);
     const float mThDepth = c->mbf * c->th_depth / c->fx;
-    oracle_vo_landmarks(xyz1, n1, mThDepth, has_lm.data());
+    res->n_queries = oracle_vo_landmarks(xyz1, n1, mThDepth, has_lm.data());
     std::vector<int32_t> lm_obs2(n2, -1), lm_src2(n2, -1);
     std::vector<uint8_t> out2(n2, 0);
     std::vector<odo_dmatch> m(std::max(n1, 1));

@@ -58,7 +58,7 @@ class PairResult(C.Structure):
     _fields_ = [("T12", C.c_float * 16), ("Tcw", C.c_float * 16), ("rmse", C.c_float),
                 ("n_matches", C.c_int32), ("n_good", C.c_int32), ("n_inliers", C.c_int32),
                 ("ransac_ok", C.c_int32), ("pnp_inliers", C.c_int32), ("visited", C.c_int32),
-                ("pad", C.c_int32)]
+                ("n_queries", C.c_int32)]
 
 
 def fr1_calib() -> Calib:
