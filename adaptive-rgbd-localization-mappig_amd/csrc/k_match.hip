@@ -16,7 +16,9 @@ namespace odo {
 // as packed keys (dist<<20 | trainIdx): the BFMatcher insertion rule (ties keep
 // the lower train index, equal-to-second does not replace) is exactly "the two
 // smallest (dist, idx) pairs", so min/max updates reproduce it.
-#define KNN_Q 256
+#ifndef KNN_Q
+#define KNN_Q 256  // queries (threads) per workgroup
+#endif
 #define KNN_T 256
 
 ODO_INLINE uint32_t bcnt_acc(uint32_t x, uint32_t acc) {
@@ -811,12 +813,13 @@ namespace odo {
 void launch_knn2(hipStream_t st, const uint8_t* q, const int* qn, size_t q_stride, const uint8_t* t, const int* tn,
                  size_t t_stride, int2* idx, int2* dist, size_t out_stride, int max_q, int npairs,
                  const int32_t* qlist, const int* qcnt, size_t ql_stride, int nsplit, size_t split_stride) {
-    static int resident = 0;  // workgroups of one full round: 8 four-wave workgroups per CU
+    static int resident = 0;  // workgroups of one full round (occupancy x CUs)
     if (!resident) {
-        int dev = 0, cus = 256;
+        int dev = 0, cus = 256, per_cu = 0;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        resident = 8 * cus;
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_knn2, KNN_Q, 0);
+        resident = std::max(1, per_cu) * cus;
     }
     const int qblocks = (max_q + KNN_Q - 1) / KNN_Q;
     const int nitems = qblocks * npairs * nsplit;
