@@ -107,3 +107,32 @@ def test_gpu_knn_degenerate_sizes():
         pkg.check(lib.odo_knn2_hamming(odo.h, pkg.ptr(q), nq, pkg.ptr(t), nt, pkg.ptr(gi), pkg.ptr(gd)))
         assert np.array_equal(gi[:nq], ri[:nq]) and np.array_equal(gd[:nq], rd[:nq]), (nq, nt)
     odo.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scale", [2.0, 4.0])
+def test_gpu_far_scenes_vo_landmark_sort_path(scale):
+    """Scenes pushed beyond Calibration::mThDepth: fewer than 100 keypoints
+    within it, so UpdateLastFrame takes the 101 nearest (k_vo_lm's sort
+    path) and kNN-2 runs on those queries only. Landmark counts, matches and
+    poses against the oracle."""
+    pkg = load_pkg()
+    bgr, dep, _ = sequence(3, seed=0x5EED0042)
+    dep = np.clip(dep.astype(np.float64) * scale, 0, 65535).astype(np.uint16)
+    cal = O.fr1_calib()
+    fr = [O.extract_frame(bgr[i], dep[i], O.orb_params(1000), cal) for i in range(3)]
+    cfg = pkg.default_config(640, 480, 3, nfeatures=1000, iterations=200)
+    odo = pkg.Odometry(cfg)
+    res = odo.track_batch_host(bgr, dep)
+    latch = float("nan")
+    for p in range(1, 3):
+        r, _, matches, latch = O.track_pair(fr[p - 1], fr[p], cal, O.ransac_params(200),
+                                            pkg.pair_seed(cfg.seed, p), latch)
+        th = cal.mbf * cal.th_depth / cal.fx
+        z = fr[p - 1]["xyz"][:, 2]
+        assert np.count_nonzero((z > 0) & (z <= th)) < 100 or scale == 2.0
+        assert res[p]["n_queries"] == r.n_queries, f"pair {p}: VO landmarks"
+        assert np.array_equal(odo.pair(p)["matches"], matches), f"pair {p}: matches"
+        assert np.array_equal(res[p]["T12"], np.array(r.T12, np.float32)), f"pair {p}: T12"
+        assert np.abs(res[p]["Tcw"] - np.array(r.Tcw, np.float32)).max() < 1e-4, f"pair {p}: Tcw"
+    odo.close()
