@@ -53,34 +53,73 @@ __global__ void __launch_bounds__(KNN_Q) k_knn2(const uint8_t* __restrict__ qdes
     // A fixed grid (one round of resident workgroups) strides over the items
     // (pair, block of KNN_Q queries, train split): with the landmark query
     // lists, pairs have fewer and uneven query blocks, and a grid of one
-    // workgroup per item would leave a partial second round.
+    // workgroup per item would leave a partial second round. The next train
+    // chunk (the next item's first chunk at the end of an item) is loaded into
+    // registers while the current chunk is compared.
     const int nitems = npairs * qblocks * nsplit;
-    for (int item = blockIdx.x; item < nitems; item += gridDim.x) {
+    const int tid = threadIdx.x;
+    auto next_valid = [&](int it) -> int {  // first item >= it of this workgroup's stride with queries
+        for (; it < nitems; it += gridDim.x) {
+            const int rq = it / nsplit, p = rq / qblocks;
+            const int nq = qlist ? qcnt[p] : qn[p];
+            if ((rq % qblocks) * KNN_Q < nq) return it;
+        }
+        return nitems;
+    };
+    auto split_range = [&](int it, int& p, int& tb, int& te) {
+        const int h = it % nsplit;
+        p = (it / nsplit) / qblocks;
+        const int nt = tn[p];
+        tb = (int)((long)nt * h / nsplit);
+        te = (int)((long)nt * (h + 1) / nsplit);
+    };
+    uint4 r0 = make_uint4(0, 0, 0, 0), r1 = make_uint4(0, 0, 0, 0);  // prefetched train chunk
+    auto load_chunk = [&](int p, int t0, int te) {
+        const int cnt = min(KNN_T, te - t0);
+        const uint4* src = reinterpret_cast<const uint4*>(tdesc + (size_t)p * t_stride + (size_t)t0 * 32);
+        if (tid < 2 * cnt) r0 = src[tid];
+        if (tid + KNN_Q < 2 * cnt) r1 = src[tid + KNN_Q];
+    };
+    int item = next_valid(blockIdx.x);
+    if (item < nitems) {
+        int p, tb, te;
+        split_range(item, p, tb, te);
+        if (te > tb) load_chunk(p, tb, te);
+    }
+    while (item < nitems) {
     const int h = item % nsplit, rq = item / nsplit;
     const int qbk = rq % qblocks, p = rq / qblocks;
-    // with a query list (the batched path: F1 keypoints holding a landmark),
-    // position k of the list is query qlist[k]; without, every query
     const int nq = qlist ? qcnt[p] : qn[p], nt = tn[p];
-    if (qbk * KNN_Q >= nq) continue;  // uniform over the workgroup
-    const int qpos = qbk * KNN_Q + threadIdx.x;
+    const int qpos = qbk * KNN_Q + tid;
     const int qi = qpos < nq ? (qlist ? qlist[(size_t)p * ql_stride + qpos] : qpos) : -1;
     const uint8_t* Q = qdesc + (size_t)p * q_stride;
-    const uint8_t* T = tdesc + (size_t)p * t_stride;
     uint4 qa = make_uint4(0, 0, 0, 0), qb = make_uint4(0, 0, 0, 0);
     if (qi >= 0) {
         qa = reinterpret_cast<const uint4*>(Q + (size_t)qi * 32)[0];
         qb = reinterpret_cast<const uint4*>(Q + (size_t)qi * 32)[1];
     }
     // train split h: the splits' top-2 lists are merged by the consumer (k_pair_match)
-    const int S = nsplit;
-    const int tb = (int)((long)nt * h / S), te = (int)((long)nt * (h + 1) / S);
+    const int tb = (int)((long)nt * h / nsplit), te = (int)((long)nt * (h + 1) / nsplit);
+    const int next = next_valid(item + gridDim.x);
     uint32_t k0 = 0xFFFFFFFFu, k1 = 0xFFFFFFFFu;
+    if (te <= tb && next < nitems) {  // empty split: the next item's first chunk now
+        int np, ntb, nte;
+        split_range(next, np, ntb, nte);
+        if (nte > ntb) load_chunk(np, ntb, nte);
+    }
     for (int t0 = tb; t0 < te; t0 += KNN_T) {
         const int tcount = min(KNN_T, te - t0);
         __syncthreads();
-        for (int i = threadIdx.x; i < tcount * 2; i += KNN_Q)
-            tile[i] = reinterpret_cast<const uint4*>(T + (size_t)t0 * 32)[i];
+        tile[tid] = r0;
+        tile[tid + KNN_Q] = r1;
         __syncthreads();
+        if (t0 + KNN_T < te) {
+            load_chunk(p, t0 + KNN_T, te);
+        } else if (next < nitems) {
+            int np, ntb, nte;
+            split_range(next, np, ntb, nte);
+            if (nte > ntb) load_chunk(np, ntb, nte);
+        }
         // 8 xor + 8 accumulating bcnt, then key and the top-2 update as
         // min + med3 (k0 <= k1 always holds): 19 VALU per comparison; four
         // train descriptors interleaved so the bcnt chains overlap
@@ -131,6 +170,7 @@ __global__ void __launch_bounds__(KNN_Q) k_knn2(const uint8_t* __restrict__ qdes
         out_idx[(size_t)h * split_stride + (size_t)p * out_stride + qi] = I;
         out_dist[(size_t)h * split_stride + (size_t)p * out_stride + qi] = D;
     }
+    item = next;
     }
 }
 
@@ -819,6 +859,8 @@ void launch_knn2(hipStream_t st, const uint8_t* q, const int* qn, size_t q_strid
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_knn2, KNN_Q, 0);
+        // ODO_KNN_WG_PER_CU < occupancy leaves wave slots to co-running kernels
+        if (const char* e = getenv("ODO_KNN_WG_PER_CU")) per_cu = std::min(std::max(1, atoi(e)), std::max(1, per_cu));
         resident = std::max(1, per_cu) * cus;
     }
     const int qblocks = (max_q + KNN_Q - 1) / KNN_Q;
