@@ -38,13 +38,18 @@ ODO_INLINE uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c) {
     return r;
 }
 
-__global__ void __launch_bounds__(KNN_Q) k_knn2(const uint8_t* __restrict__ qdesc, const int* __restrict__ qn,
-                                                size_t q_stride, const uint8_t* __restrict__ tdesc,
-                                                const int* __restrict__ tn, size_t t_stride,
-                                                int2* __restrict__ out_idx, int2* __restrict__ out_dist,
-                                                size_t out_stride, const int32_t* __restrict__ qlist,
-                                                const int* __restrict__ qcnt, size_t ql_stride,
-                                                size_t split_stride, int npairs, int qblocks, int nsplit) {
+#ifndef KNN_QPL
+#define KNN_QPL 1  // queries per lane (more independent popcount chains per wave)
+#endif
+#define KNN_TH (KNN_Q / KNN_QPL)      // threads per workgroup
+#define KNN_PF (2 * KNN_T / KNN_TH)   // uint4 of a staged train chunk per thread
+__global__ void __launch_bounds__(KNN_TH) k_knn2(const uint8_t* __restrict__ qdesc, const int* __restrict__ qn,
+                                                 size_t q_stride, const uint8_t* __restrict__ tdesc,
+                                                 const int* __restrict__ tn, size_t t_stride,
+                                                 int2* __restrict__ out_idx, int2* __restrict__ out_dist,
+                                                 size_t out_stride, const int32_t* __restrict__ qlist,
+                                                 const int* __restrict__ qcnt, size_t ql_stride,
+                                                 size_t split_stride, int npairs, int qblocks, int nsplit) {
 #ifndef ODO_KNN_PRIO
 #define ODO_KNN_PRIO 2  // co-runs with the previous batch's PnP: issue first (+0.07 roofline, same step time)
 #endif
@@ -73,12 +78,15 @@ __global__ void __launch_bounds__(KNN_Q) k_knn2(const uint8_t* __restrict__ qdes
         tb = (int)((long)nt * h / nsplit);
         te = (int)((long)nt * (h + 1) / nsplit);
     };
-    uint4 r0 = make_uint4(0, 0, 0, 0), r1 = make_uint4(0, 0, 0, 0);  // prefetched train chunk
+    uint4 r[KNN_PF];  // prefetched train chunk
+#pragma unroll
+    for (int k = 0; k < KNN_PF; k++) r[k] = make_uint4(0, 0, 0, 0);
     auto load_chunk = [&](int p, int t0, int te) {
         const int cnt = min(KNN_T, te - t0);
         const uint4* src = reinterpret_cast<const uint4*>(tdesc + (size_t)p * t_stride + (size_t)t0 * 32);
-        if (tid < 2 * cnt) r0 = src[tid];
-        if (tid + KNN_Q < 2 * cnt) r1 = src[tid + KNN_Q];
+#pragma unroll
+        for (int k = 0; k < KNN_PF; k++)
+            if (tid + k * KNN_TH < 2 * cnt) r[k] = src[tid + k * KNN_TH];
     };
     int item = next_valid(blockIdx.x);
     if (item < nitems) {
@@ -87,90 +95,103 @@ __global__ void __launch_bounds__(KNN_Q) k_knn2(const uint8_t* __restrict__ qdes
         if (te > tb) load_chunk(p, tb, te);
     }
     while (item < nitems) {
-    const int h = item % nsplit, rq = item / nsplit;
-    const int qbk = rq % qblocks, p = rq / qblocks;
-    const int nq = qlist ? qcnt[p] : qn[p], nt = tn[p];
-    const int qpos = qbk * KNN_Q + tid;
-    const int qi = qpos < nq ? (qlist ? qlist[(size_t)p * ql_stride + qpos] : qpos) : -1;
-    const uint8_t* Q = qdesc + (size_t)p * q_stride;
-    uint4 qa = make_uint4(0, 0, 0, 0), qb = make_uint4(0, 0, 0, 0);
-    if (qi >= 0) {
-        qa = reinterpret_cast<const uint4*>(Q + (size_t)qi * 32)[0];
-        qb = reinterpret_cast<const uint4*>(Q + (size_t)qi * 32)[1];
-    }
-    // train split h: the splits' top-2 lists are merged by the consumer (k_pair_match)
-    const int tb = (int)((long)nt * h / nsplit), te = (int)((long)nt * (h + 1) / nsplit);
-    const int next = next_valid(item + gridDim.x);
-    uint32_t k0 = 0xFFFFFFFFu, k1 = 0xFFFFFFFFu;
-    if (te <= tb && next < nitems) {  // empty split: the next item's first chunk now
-        int np, ntb, nte;
-        split_range(next, np, ntb, nte);
-        if (nte > ntb) load_chunk(np, ntb, nte);
-    }
-    for (int t0 = tb; t0 < te; t0 += KNN_T) {
-        const int tcount = min(KNN_T, te - t0);
-        __syncthreads();
-        tile[tid] = r0;
-        tile[tid + KNN_Q] = r1;
-        __syncthreads();
-        if (t0 + KNN_T < te) {
-            load_chunk(p, t0 + KNN_T, te);
-        } else if (next < nitems) {
+        const int h = item % nsplit, rq = item / nsplit;
+        const int qbk = rq % qblocks, p = rq / qblocks;
+        const int nq = qlist ? qcnt[p] : qn[p], nt = tn[p];
+        const uint8_t* Q = qdesc + (size_t)p * q_stride;
+        int qi[KNN_QPL];
+        uint32_t q[KNN_QPL][8], k0[KNN_QPL], k1[KNN_QPL];
+#pragma unroll
+        for (int s = 0; s < KNN_QPL; s++) {
+            const int qpos = qbk * KNN_Q + s * KNN_TH + tid;
+            qi[s] = qpos < nq ? (qlist ? qlist[(size_t)p * ql_stride + qpos] : qpos) : -1;
+            uint4 qa = make_uint4(0, 0, 0, 0), qb = make_uint4(0, 0, 0, 0);
+            if (qi[s] >= 0) {
+                qa = reinterpret_cast<const uint4*>(Q + (size_t)qi[s] * 32)[0];
+                qb = reinterpret_cast<const uint4*>(Q + (size_t)qi[s] * 32)[1];
+            }
+            q[s][0] = qa.x, q[s][1] = qa.y, q[s][2] = qa.z, q[s][3] = qa.w;
+            q[s][4] = qb.x, q[s][5] = qb.y, q[s][6] = qb.z, q[s][7] = qb.w;
+            k0[s] = 0xFFFFFFFFu;
+            k1[s] = 0xFFFFFFFFu;
+        }
+        // train split h: the splits' top-2 lists are merged by the consumer (k_pair_match)
+        const int tb = (int)((long)nt * h / nsplit), te = (int)((long)nt * (h + 1) / nsplit);
+        const int next = next_valid(item + gridDim.x);
+        if (te <= tb && next < nitems) {  // empty split: the next item's first chunk now
             int np, ntb, nte;
             split_range(next, np, ntb, nte);
             if (nte > ntb) load_chunk(np, ntb, nte);
         }
-        // 8 xor + 8 accumulating bcnt, then key and the top-2 update as
-        // min + med3 (k0 <= k1 always holds): 19 VALU per comparison; four
-        // train descriptors interleaved so the bcnt chains overlap
-        int j = 0;
-        for (; j + 4 <= tcount; j += 4) {
-            uint32_t d[4], t[4][8];
+        for (int t0 = tb; t0 < te; t0 += KNN_T) {
+            const int tcount = min(KNN_T, te - t0);
+            __syncthreads();
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const uint4 ta = tile[2 * (j + u)], tb = tile[2 * (j + u) + 1];
-                t[u][0] = ta.x, t[u][1] = ta.y, t[u][2] = ta.z, t[u][3] = ta.w;
-                t[u][4] = tb.x, t[u][5] = tb.y, t[u][6] = tb.z, t[u][7] = tb.w;
-                d[u] = 0u;
+            for (int k = 0; k < KNN_PF; k++) tile[tid + k * KNN_TH] = r[k];
+            __syncthreads();
+            if (t0 + KNN_T < te) {
+                load_chunk(p, t0 + KNN_T, te);
+            } else if (next < nitems) {
+                int np, ntb, nte;
+                split_range(next, np, ntb, nte);
+                if (nte > ntb) load_chunk(np, ntb, nte);
             }
-            const uint32_t q[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
+            // 8 xor + 8 accumulating bcnt, then key and the top-2 update as
+            // min + med3 (k0 <= k1 always holds): 19 VALU per comparison; four
+            // train descriptors interleaved so the bcnt chains overlap
+            int j = 0;
+            for (; j + 4 <= tcount; j += 4) {
+                uint32_t d[KNN_QPL][4], t[4][8];
 #pragma unroll
-            for (int w = 0; w < 8; w++) {
+                for (int u = 0; u < 4; u++) {
+                    const uint4 ta = tile[2 * (j + u)], tb2 = tile[2 * (j + u) + 1];
+                    t[u][0] = ta.x, t[u][1] = ta.y, t[u][2] = ta.z, t[u][3] = ta.w;
+                    t[u][4] = tb2.x, t[u][5] = tb2.y, t[u][6] = tb2.z, t[u][7] = tb2.w;
 #pragma unroll
-                for (int u = 0; u < 4; u++) d[u] = bcnt_acc(q[w] ^ t[u][w], d[u]);
+                    for (int s = 0; s < KNN_QPL; s++) d[s][u] = 0u;
+                }
+#pragma unroll
+                for (int w = 0; w < 8; w++)
+#pragma unroll
+                    for (int s = 0; s < KNN_QPL; s++)
+#pragma unroll
+                        for (int u = 0; u < 4; u++) d[s][u] = bcnt_acc(q[s][w] ^ t[u][w], d[s][u]);
+#pragma unroll
+                for (int s = 0; s < KNN_QPL; s++)
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const uint32_t key = key_of(d[s][u], (uint32_t)(t0 + j + u));
+                        k1[s] = med3_u32(k0[s], k1[s], key);
+                        k0[s] = min(k0[s], key);
+                    }
             }
+            for (; j < tcount; j++) {
+                const uint4 ta = tile[2 * j], tb2 = tile[2 * j + 1];
+                const uint32_t tw[8] = {ta.x, ta.y, ta.z, ta.w, tb2.x, tb2.y, tb2.z, tb2.w};
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const uint32_t key = key_of(d[u], (uint32_t)(t0 + j + u));
-                k1 = med3_u32(k0, k1, key);
-                k0 = min(k0, key);
+                for (int s = 0; s < KNN_QPL; s++) {
+                    uint32_t d = 0u;
+#pragma unroll
+                    for (int w = 0; w < 8; w++) d = bcnt_acc(q[s][w] ^ tw[w], d);
+                    const uint32_t key = (d << 20) | (uint32_t)(t0 + j);
+                    k1[s] = med3_u32(k0[s], k1[s], key);
+                    k0[s] = min(k0[s], key);
+                }
             }
         }
-        for (; j < tcount; j++) {
-            const uint4 ta = tile[2 * j], tb = tile[2 * j + 1];
-            uint32_t d = bcnt_acc(qa.x ^ ta.x, 0u);
-            d = bcnt_acc(qa.y ^ ta.y, d);
-            d = bcnt_acc(qa.z ^ ta.z, d);
-            d = bcnt_acc(qa.w ^ ta.w, d);
-            d = bcnt_acc(qb.x ^ tb.x, d);
-            d = bcnt_acc(qb.y ^ tb.y, d);
-            d = bcnt_acc(qb.z ^ tb.z, d);
-            d = bcnt_acc(qb.w ^ tb.w, d);
-            const uint32_t key = (d << 20) | (uint32_t)(t0 + j);
-            k1 = med3_u32(k0, k1, key);
-            k0 = min(k0, key);
+#pragma unroll
+        for (int s = 0; s < KNN_QPL; s++) {
+            if (qi[s] >= 0) {
+                int2 I, D;
+                I.x = k0[s] == 0xFFFFFFFFu ? -1 : (int)(k0[s] & 0xFFFFF);
+                D.x = k0[s] == 0xFFFFFFFFu ? 0x7FFFFFFF : (int)(k0[s] >> 20);
+                I.y = k1[s] == 0xFFFFFFFFu ? -1 : (int)(k1[s] & 0xFFFFF);
+                D.y = k1[s] == 0xFFFFFFFFu ? 0x7FFFFFFF : (int)(k1[s] >> 20);
+                out_idx[(size_t)h * split_stride + (size_t)p * out_stride + qi[s]] = I;
+                out_dist[(size_t)h * split_stride + (size_t)p * out_stride + qi[s]] = D;
+            }
         }
-    }
-    if (qi >= 0) {
-        int2 I, D;
-        I.x = k0 == 0xFFFFFFFFu ? -1 : (int)(k0 & 0xFFFFF);
-        D.x = k0 == 0xFFFFFFFFu ? 0x7FFFFFFF : (int)(k0 >> 20);
-        I.y = k1 == 0xFFFFFFFFu ? -1 : (int)(k1 & 0xFFFFF);
-        D.y = k1 == 0xFFFFFFFFu ? 0x7FFFFFFF : (int)(k1 >> 20);
-        out_idx[(size_t)h * split_stride + (size_t)p * out_stride + qi] = I;
-        out_dist[(size_t)h * split_stride + (size_t)p * out_stride + qi] = D;
-    }
-    item = next;
+        item = next;
     }
 }
 
@@ -858,7 +879,7 @@ void launch_knn2(hipStream_t st, const uint8_t* q, const int* qn, size_t q_strid
         int dev = 0, cus = 256, per_cu = 0;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_knn2, KNN_Q, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_knn2, KNN_TH, 0);
         // ODO_KNN_WG_PER_CU < occupancy leaves wave slots to co-running kernels
         if (const char* e = getenv("ODO_KNN_WG_PER_CU")) per_cu = std::min(std::max(1, atoi(e)), std::max(1, per_cu));
         resident = std::max(1, per_cu) * cus;
@@ -867,7 +888,7 @@ void launch_knn2(hipStream_t st, const uint8_t* q, const int* qn, size_t q_strid
     const int nitems = qblocks * npairs * nsplit;
     if (nitems <= 0) return;
     dim3 g(std::min(nitems, resident));
-    hipLaunchKernelGGL(k_knn2, g, dim3(KNN_Q), 0, st, q, qn, q_stride, t, tn, t_stride, idx, dist, out_stride, qlist,
+    hipLaunchKernelGGL(k_knn2, g, dim3(KNN_TH), 0, st, q, qn, q_stride, t, tn, t_stride, idx, dist, out_stride, qlist,
                        qcnt, ql_stride, split_stride, npairs, qblocks, nsplit);
 }
 void launch_vo_lm(hipStream_t st, const float* xyz, const int* nkp, int kp_cap, int slot0, float th_depth_m,
