@@ -43,6 +43,7 @@ ODO_INLINE uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c) {
 #endif
 #define KNN_TH (KNN_Q / KNN_QPL)      // threads per workgroup
 #define KNN_PF (2 * KNN_T / KNN_TH)   // uint4 of a staged train chunk per thread
+#define KNN_MAXP 1024                 // pairs per launch (the item prefix lives in LDS)
 __global__ void __launch_bounds__(KNN_TH) k_knn2(const uint8_t* __restrict__ qdesc, const int* __restrict__ qn,
                                                  size_t q_stride, const uint8_t* __restrict__ tdesc,
                                                  const int* __restrict__ tn, size_t t_stride,
@@ -55,28 +56,45 @@ __global__ void __launch_bounds__(KNN_TH) k_knn2(const uint8_t* __restrict__ qde
 #endif
     __builtin_amdgcn_s_setprio(ODO_KNN_PRIO);
     __shared__ uint4 tile[KNN_T * 2];
-    // A fixed grid (one round of resident workgroups) strides over the items
-    // (pair, block of KNN_Q queries, train split): with the landmark query
-    // lists, pairs have fewer and uneven query blocks, and a grid of one
-    // workgroup per item would leave a partial second round. The next train
-    // chunk (the next item's first chunk at the end of an item) is loaded into
-    // registers while the current chunk is compared.
-    const int nitems = npairs * qblocks * nsplit;
+    // A fixed grid (one round of resident workgroups) shares out the active
+    // items (pair, block of KNN_Q queries, train split) in contiguous equal
+    // runs: the items of one query block are consecutive, so a run reloads
+    // its queries and writes its top-2 only when the block changes (the
+    // block's other split slots it covered get an empty entry; the consumer
+    // merges the splits). The next train chunk is loaded into registers while
+    // the current chunk is compared.
+    __shared__ int s_pre[KNN_MAXP + 1];
     const int tid = threadIdx.x;
-    auto next_valid = [&](int it) -> int {  // first item >= it of this workgroup's stride with queries
-        for (; it < nitems; it += gridDim.x) {
-            const int rq = it / nsplit, p = rq / qblocks;
-            const int nq = qlist ? qcnt[p] : qn[p];
-            if ((rq % qblocks) * KNN_Q < nq) return it;
-        }
-        return nitems;
+    // exclusive prefix of the pairs' active item counts
+    for (int i = tid; i < npairs; i += KNN_TH) {
+        const int nq = qlist ? qcnt[i] : qn[i];
+        s_pre[i + 1] = ((nq + KNN_Q - 1) / KNN_Q) * nsplit;
+    }
+    if (tid == 0) s_pre[0] = 0;
+    __syncthreads();
+    if (tid == 0)
+        for (int i = 1; i <= npairs; i++) s_pre[i] += s_pre[i - 1];
+    __syncthreads();
+    const int nact = s_pre[npairs];
+    const int g0 = (int)((long)nact * blockIdx.x / gridDim.x), g1 = (int)((long)nact * (blockIdx.x + 1) / gridDim.x);
+    struct Item {
+        int p, qbk, h, tb, te;
     };
-    auto split_range = [&](int it, int& p, int& tb, int& te) {
-        const int h = it % nsplit;
-        p = (it / nsplit) / qblocks;
-        const int nt = tn[p];
-        tb = (int)((long)nt * h / nsplit);
-        te = (int)((long)nt * (h + 1) / nsplit);
+    auto decode = [&](int g) -> Item {
+        int lo = 0, hi = npairs;  // last pair with s_pre[p] <= g
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (s_pre[mid] <= g) lo = mid; else hi = mid;
+        }
+        Item I;
+        I.p = lo;
+        const int local = g - s_pre[lo];
+        I.qbk = local / nsplit;
+        I.h = local - I.qbk * nsplit;
+        const int nt = tn[I.p];
+        I.tb = (int)((long)nt * I.h / nsplit);
+        I.te = (int)((long)nt * (I.h + 1) / nsplit);
+        return I;
     };
     uint4 r[KNN_PF];  // prefetched train chunk
 #pragma unroll
@@ -88,53 +106,73 @@ __global__ void __launch_bounds__(KNN_TH) k_knn2(const uint8_t* __restrict__ qde
         for (int k = 0; k < KNN_PF; k++)
             if (tid + k * KNN_TH < 2 * cnt) r[k] = src[tid + k * KNN_TH];
     };
-    int item = next_valid(blockIdx.x);
-    if (item < nitems) {
-        int p, tb, te;
-        split_range(item, p, tb, te);
-        if (te > tb) load_chunk(p, tb, te);
-    }
-    while (item < nitems) {
-        const int h = item % nsplit, rq = item / nsplit;
-        const int qbk = rq % qblocks, p = rq / qblocks;
-        const int nq = qlist ? qcnt[p] : qn[p], nt = tn[p];
-        const uint8_t* Q = qdesc + (size_t)p * q_stride;
-        int qi[KNN_QPL];
-        uint32_t q[KNN_QPL][8], k0[KNN_QPL], k1[KNN_QPL];
+    int cur_p = -1, cur_qbk = -1, h_first = 0, h_last = 0;
+    int qi[KNN_QPL];
+    uint32_t q[KNN_QPL][8], k0[KNN_QPL], k1[KNN_QPL];
+    auto flush = [&]() {  // the run's top-2 into split slot h_first, empties into the others it covered
+        if (cur_p < 0) return;
 #pragma unroll
         for (int s = 0; s < KNN_QPL; s++) {
-            const int qpos = qbk * KNN_Q + s * KNN_TH + tid;
-            qi[s] = qpos < nq ? (qlist ? qlist[(size_t)p * ql_stride + qpos] : qpos) : -1;
-            uint4 qa = make_uint4(0, 0, 0, 0), qb = make_uint4(0, 0, 0, 0);
-            if (qi[s] >= 0) {
-                qa = reinterpret_cast<const uint4*>(Q + (size_t)qi[s] * 32)[0];
-                qb = reinterpret_cast<const uint4*>(Q + (size_t)qi[s] * 32)[1];
+            if (qi[s] < 0) continue;
+            int2 I, D;
+            I.x = k0[s] == 0xFFFFFFFFu ? -1 : (int)(k0[s] & 0xFFFFF);
+            D.x = k0[s] == 0xFFFFFFFFu ? 0x7FFFFFFF : (int)(k0[s] >> 20);
+            I.y = k1[s] == 0xFFFFFFFFu ? -1 : (int)(k1[s] & 0xFFFFF);
+            D.y = k1[s] == 0xFFFFFFFFu ? 0x7FFFFFFF : (int)(k1[s] >> 20);
+            const size_t o = (size_t)cur_p * out_stride + qi[s];
+            out_idx[(size_t)h_first * split_stride + o] = I;
+            out_dist[(size_t)h_first * split_stride + o] = D;
+            for (int hh = h_first + 1; hh <= h_last; hh++) {
+                out_idx[(size_t)hh * split_stride + o] = make_int2(-1, -1);
+                out_dist[(size_t)hh * split_stride + o] = make_int2(0x7FFFFFFF, 0x7FFFFFFF);
             }
-            q[s][0] = qa.x, q[s][1] = qa.y, q[s][2] = qa.z, q[s][3] = qa.w;
-            q[s][4] = qb.x, q[s][5] = qb.y, q[s][6] = qb.z, q[s][7] = qb.w;
-            k0[s] = 0xFFFFFFFFu;
-            k1[s] = 0xFFFFFFFFu;
         }
-        // train split h: the splits' top-2 lists are merged by the consumer (k_pair_match)
-        const int tb = (int)((long)nt * h / nsplit), te = (int)((long)nt * (h + 1) / nsplit);
-        const int next = next_valid(item + gridDim.x);
-        if (te <= tb && next < nitems) {  // empty split: the next item's first chunk now
-            int np, ntb, nte;
-            split_range(next, np, ntb, nte);
-            if (nte > ntb) load_chunk(np, ntb, nte);
+    };
+    if (g0 < g1) {
+        const Item I = decode(g0);
+        if (I.te > I.tb) load_chunk(I.p, I.tb, I.te);
+    }
+    for (int g = g0; g < g1; g++) {
+        const Item I = decode(g);
+        if (I.p != cur_p || I.qbk != cur_qbk) {
+            flush();
+            cur_p = I.p;
+            cur_qbk = I.qbk;
+            h_first = I.h;
+            const int nq = qlist ? qcnt[I.p] : qn[I.p];
+            const uint8_t* Q = qdesc + (size_t)I.p * q_stride;
+#pragma unroll
+            for (int s = 0; s < KNN_QPL; s++) {
+                const int qpos = I.qbk * KNN_Q + s * KNN_TH + tid;
+                qi[s] = qpos < nq ? (qlist ? qlist[(size_t)I.p * ql_stride + qpos] : qpos) : -1;
+                uint4 qa = make_uint4(0, 0, 0, 0), qb = make_uint4(0, 0, 0, 0);
+                if (qi[s] >= 0) {
+                    qa = reinterpret_cast<const uint4*>(Q + (size_t)qi[s] * 32)[0];
+                    qb = reinterpret_cast<const uint4*>(Q + (size_t)qi[s] * 32)[1];
+                }
+                q[s][0] = qa.x, q[s][1] = qa.y, q[s][2] = qa.z, q[s][3] = qa.w;
+                q[s][4] = qb.x, q[s][5] = qb.y, q[s][6] = qb.z, q[s][7] = qb.w;
+                k0[s] = 0xFFFFFFFFu;
+                k1[s] = 0xFFFFFFFFu;
+            }
         }
-        for (int t0 = tb; t0 < te; t0 += KNN_T) {
-            const int tcount = min(KNN_T, te - t0);
+        h_last = I.h;
+        const bool more = g + 1 < g1;
+        if (I.te <= I.tb && more) {  // empty split: the next item's first chunk now
+            const Item N = decode(g + 1);
+            if (N.te > N.tb) load_chunk(N.p, N.tb, N.te);
+        }
+        for (int t0 = I.tb; t0 < I.te; t0 += KNN_T) {
+            const int tcount = min(KNN_T, I.te - t0);
             __syncthreads();
 #pragma unroll
             for (int k = 0; k < KNN_PF; k++) tile[tid + k * KNN_TH] = r[k];
             __syncthreads();
-            if (t0 + KNN_T < te) {
-                load_chunk(p, t0 + KNN_T, te);
-            } else if (next < nitems) {
-                int np, ntb, nte;
-                split_range(next, np, ntb, nte);
-                if (nte > ntb) load_chunk(np, ntb, nte);
+            if (t0 + KNN_T < I.te) {
+                load_chunk(I.p, t0 + KNN_T, I.te);
+            } else if (more) {
+                const Item N = decode(g + 1);
+                if (N.te > N.tb) load_chunk(N.p, N.tb, N.te);
             }
             // 8 xor + 8 accumulating bcnt, then key and the top-2 update as
             // min + med3 (k0 <= k1 always holds): 19 VALU per comparison; four
@@ -179,20 +217,8 @@ __global__ void __launch_bounds__(KNN_TH) k_knn2(const uint8_t* __restrict__ qde
                 }
             }
         }
-#pragma unroll
-        for (int s = 0; s < KNN_QPL; s++) {
-            if (qi[s] >= 0) {
-                int2 I, D;
-                I.x = k0[s] == 0xFFFFFFFFu ? -1 : (int)(k0[s] & 0xFFFFF);
-                D.x = k0[s] == 0xFFFFFFFFu ? 0x7FFFFFFF : (int)(k0[s] >> 20);
-                I.y = k1[s] == 0xFFFFFFFFu ? -1 : (int)(k1[s] & 0xFFFFF);
-                D.y = k1[s] == 0xFFFFFFFFu ? 0x7FFFFFFF : (int)(k1[s] >> 20);
-                out_idx[(size_t)h * split_stride + (size_t)p * out_stride + qi[s]] = I;
-                out_dist[(size_t)h * split_stride + (size_t)p * out_stride + qi[s]] = D;
-            }
-        }
-        item = next;
     }
+    flush();
 }
 
 // ============================================================ libstdc++ std::sort emulation
@@ -887,6 +913,15 @@ void launch_knn2(hipStream_t st, const uint8_t* q, const int* qn, size_t q_strid
     const int qblocks = (max_q + KNN_Q - 1) / KNN_Q;
     const int nitems = qblocks * npairs * nsplit;
     if (nitems <= 0) return;
+    if (npairs > KNN_MAXP) {  // the item prefix is per launch: split larger batches
+        launch_knn2(st, q, qn, q_stride, t, tn, t_stride, idx, dist, out_stride, max_q, KNN_MAXP, qlist, qcnt,
+                    ql_stride, nsplit, split_stride);
+        launch_knn2(st, q + KNN_MAXP * q_stride, qn + KNN_MAXP, q_stride, t + KNN_MAXP * t_stride, tn + KNN_MAXP,
+                    t_stride, idx + KNN_MAXP * out_stride, dist + KNN_MAXP * out_stride, out_stride, max_q,
+                    npairs - KNN_MAXP, qlist ? qlist + KNN_MAXP * ql_stride : nullptr, qcnt ? qcnt + KNN_MAXP : nullptr,
+                    ql_stride, nsplit, split_stride);
+        return;
+    }
     dim3 g(std::min(nitems, resident));
     hipLaunchKernelGGL(k_knn2, g, dim3(KNN_TH), 0, st, q, qn, q_stride, t, tn, t_stride, idx, dist, out_stride, qlist,
                        qcnt, ql_stride, split_stride, npairs, qblocks, nsplit);

@@ -130,7 +130,7 @@ struct odo_ctx {
     int32_t* qlist[NSETS] = {};
     int* qcnt[NSETS] = {};
     int lm_words = 0;
-    int knn_split = 8;  // kNN-2 train splits per query block (ODO_KNN_SPLIT): more waves for short query lists
+    int knn_split = 2;  // kNN-2 train splits per query block (ODO_KNN_SPLIT): more waves for short query lists
     uint64_t* sort_scratch = nullptr;
     double* latch = nullptr;
     void* rscr[NSETS] = {};  // RANSAC scratch per frame set
