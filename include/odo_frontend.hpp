@@ -351,24 +351,30 @@ public:
     explicit Matcher(float nnratio = 0.6f) : mfNNratio(nnratio) {}
 
     // Matcher::KnnMatch(Frame&, Frame&, vMatches12) (matcher.cpp:55-88): the
-    // k=2 Hamming brute force on the GPU, then the ratio test and the
-    // landmark hand-over in query order on the host.
+    // k=2 Hamming brute force on the GPU for the queries that can match, then
+    // the ratio test and the landmark hand-over in query order on the host.
     size_t KnnMatch(Frame& F1, Frame& F2, std::vector<DMatch>& vMatches12) {
         vMatches12.clear();
-        const int n1 = (int)F1.N, n2 = (int)F2.N;
-        std::vector<int32_t> idx(2 * (size_t)std::max(n1, 1)), dist(2 * (size_t)std::max(n1, 1));
-        Check(odo_knn2_hamming(detail::shared_ctx(), F1.mDescriptors.data(), n1, F2.mDescriptors.data(), n2,
-                               idx.data(), dist.data()),
+        const int n2 = (int)F2.N;
+        // only queries holding a landmark that is not an outlier can yield a
+        // match (matcher.cpp:70-74): kNN-2 runs on those, in query order
+        std::vector<int> qi;
+        for (size_t i = 0; i < F1.N; i++)
+            if (F1.GetLandmark(i) && !F1.IsOutlier(i)) qi.push_back((int)i);
+        const int nq = (int)qi.size();
+        std::vector<uint8_t> qd(32 * (size_t)std::max(nq, 1));
+        for (int k = 0; k < nq; k++) std::memcpy(&qd[32 * (size_t)k], &F1.mDescriptors[32 * (size_t)qi[k]], 32);
+        std::vector<int32_t> idx(2 * (size_t)std::max(nq, 1)), dist(2 * (size_t)std::max(nq, 1));
+        Check(odo_knn2_hamming(detail::shared_ctx(), qd.data(), nq, F2.mDescriptors.data(), n2, idx.data(),
+                               dist.data()),
               "Matcher::KnnMatch");
-        for (int i = 0; i < n1; i++) {
+        for (int k = 0; k < nq; k++) {
             // a missing second neighbour counts as distance INT_MAX
-            if (idx[2 * i] < 0) continue;
-            const float d0 = (float)dist[2 * i], d1 = (float)dist[2 * i + 1];
+            if (idx[2 * k] < 0) continue;
+            const float d0 = (float)dist[2 * k], d1 = (float)dist[2 * k + 1];
             if (!(d0 < mfNNratio * d1)) continue;
-            const size_t i1 = i, i2 = idx[2 * i];
+            const size_t i1 = qi[k], i2 = idx[2 * k];
             LandmarkPtr lm = F1.GetLandmark(i1);
-            if (!lm) continue;
-            if (F1.IsOutlier(i1)) continue;
             if (F2.GetLandmark(i2) && F2.GetLandmark(i2)->Observations() > 0) continue;
             F2.AddLandmark(lm, i2);
             F2.SetOutlier(i2);
