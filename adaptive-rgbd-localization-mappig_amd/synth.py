@@ -15,6 +15,8 @@ from __future__ import annotations
 
 import dataclasses
 import math
+import os
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
@@ -184,13 +186,14 @@ def make_sequence(n_frames: int, w: int = 640, h: int = 480, intrinsics=None, se
     bgr = np.empty((n_frames, h, w, 3), np.uint8)
     dep = np.empty((n_frames, h, w), np.uint16)
     poses = np.empty((n_frames, 4, 4))
+    renders = []
     for f in range(n_frames):
         if closed_loop:
             R, t = _loop_pose(f, n_frames, seed)
         R_render = R
         if intr["fy"] < 0:  # ICL: negative fy flips the image rows
             R_render = R @ np.diag([1.0, -1.0, -1.0]) @ np.diag([1.0, -1.0, -1.0])
-        bgr[f], dep[f] = scene.render(cam, R_render, t, f)
+        renders.append((f, R_render, t))
         T = np.eye(4)
         T[:3, :3] = R
         T[:3, 3] = t
@@ -200,6 +203,20 @@ def make_sequence(n_frames: int, w: int = 640, h: int = 480, intrinsics=None, se
         step = rng.random(3) * 2 - 1
         step *= max_step_m / max(1e-9, np.linalg.norm(step)) * rng.random()
         t = np.clip(t + step, [-0.8, -0.5, -0.6], [0.8, 0.5, 0.3])
+
+    def render(job):
+        f, Rr, tr = job
+        bgr[f], dep[f] = scene.render(cam, Rr, tr, f)
+
+    # frames are independent once the poses are drawn; numpy releases the GIL
+    # in its array loops, so a thread pool renders them concurrently
+    workers = max(1, min(16, os.cpu_count() or 1, n_frames))
+    if workers > 1:
+        with ThreadPoolExecutor(workers) as ex:
+            list(ex.map(render, renders))
+    else:
+        for job in renders:
+            render(job)
     return bgr, dep, poses
 
 

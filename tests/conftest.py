@@ -42,10 +42,11 @@ def load_synth():
 _SEQ_CACHE = {}
 
 
-def sequence(n, w=640, h=480, intrinsics=None, seed=0x5EED0002):
-    key = (n, w, h, tuple(sorted((intrinsics or {}).items())), seed)
+def sequence(n, w=640, h=480, intrinsics=None, seed=0x5EED0002, closed_loop=False):
+    key = (n, w, h, tuple(sorted((intrinsics or {}).items())), seed, closed_loop)
     if key not in _SEQ_CACHE:
-        _SEQ_CACHE[key] = load_synth().make_sequence(n, w, h, intrinsics=intrinsics, seed=seed)
+        _SEQ_CACHE[key] = load_synth().make_sequence(n, w, h, intrinsics=intrinsics, seed=seed,
+                                                     closed_loop=closed_loop)
     return _SEQ_CACHE[key]
 
 
