@@ -15,7 +15,7 @@ from . import _abi
 from ._abi import (DETECTOR_ADAPTIVE_FAST, DETECTOR_ORB_SLAM2, AdaptiveParams, Calib, Config, DMatch,
                    DMATCH_DTYPE, KP_DTYPE, OrbParams, PAIR_DTYPE, PairResult, RansacParams, Rng, check, load, ptr)
 
-__all__ = ["Odometry", "default_config", "load", "KP_DTYPE", "DMATCH_DTYPE", "PAIR_DTYPE", "rng_stream",
+__all__ = ["Odometry", "HostFrames", "default_config", "load", "KP_DTYPE", "DMATCH_DTYPE", "PAIR_DTYPE", "rng_stream",
            "kabsch", "Calib", "OrbParams", "RansacParams", "Config", "AdaptiveParams", "DETECTOR_ORB_SLAM2",
            "DETECTOR_ADAPTIVE_FAST"]
 
@@ -35,6 +35,38 @@ def default_config(width=640, height=480, max_batch=1, nfeatures=1000, iteration
         for k, v in calib.items():
             setattr(cfg.calib, k, v)
     return cfg
+
+
+class HostFrames:
+    """Page-locked host buffers for n frames of BGR8 + depth16 (odo_host_alloc):
+    decode into `bgr` / `depth` (numpy views) and pass the object to
+    Odometry.track_batch_host; the DMA engines read it without a staging copy."""
+
+    def __init__(self, n: int, width: int, height: int):
+        self.lib = load()
+        self.n, self.w, self.h = n, width, height
+        nb, nd = n * height * width * 3, n * height * width * 2
+        self._pb = self.lib.odo_host_alloc(nb)
+        self._pd = self.lib.odo_host_alloc(nd)
+        if not self._pb or not self._pd:
+            self.close()
+            raise MemoryError("odo_host_alloc failed: " + self.lib.odo_last_error().decode())
+        self.bgr = np.ctypeslib.as_array(C.cast(self._pb, C.POINTER(C.c_uint8)), (n, height, width, 3))
+        self.depth = np.ctypeslib.as_array(C.cast(self._pd, C.POINTER(C.c_uint16)), (n, height, width))
+
+    def close(self):
+        for a in ("_pb", "_pd"):
+            p = getattr(self, a, None)
+            if p:
+                self.lib.odo_host_free(p)
+                setattr(self, a, None)
+        self.bgr = self.depth = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Odometry:
@@ -82,14 +114,22 @@ class Odometry:
                                        ptr(out) if want_results else None))
         return out
 
-    def track_batch_host(self, bgr: np.ndarray, depth: np.ndarray, want_results=True):
-        """Host inputs; without results the call returns once the frames are
-        staged and the batch is queued (its pair stages run asynchronously)."""
-        bgr = np.ascontiguousarray(bgr, np.uint8)
-        depth = np.ascontiguousarray(depth, np.uint16)
-        n = bgr.shape[0]
+    def track_batch_host(self, bgr, depth=None, want_results=True, n=None):
+        """Host inputs: numpy arrays (pageable) or a HostFrames (pinned; then
+        `n` frames of it, default all). Without results the call returns once
+        the host buffers are consumed and the batch is queued (the upload
+        overlaps the compute of earlier batches; the batch runs asynchronously)."""
+        if isinstance(bgr, HostFrames):
+            hf = bgr
+            n = hf.n if n is None else n
+            pb, pd = hf._pb, hf._pd
+        else:
+            bgr = np.ascontiguousarray(bgr, np.uint8)
+            depth = np.ascontiguousarray(depth, np.uint16)
+            n = bgr.shape[0]
+            pb, pd = ptr(bgr), ptr(depth)
         out = np.zeros(n, PAIR_DTYPE) if want_results else None
-        check(self.lib.odo_track_batch_host(self.h, ptr(bgr), ptr(depth), n, ptr(out) if want_results else None))
+        check(self.lib.odo_track_batch_host(self.h, pb, pd, n, ptr(out) if want_results else None))
         return out
 
     def set_timing(self, enable, mode: int = None):

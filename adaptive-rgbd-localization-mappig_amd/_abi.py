@@ -57,7 +57,7 @@ class PairResult(C.Structure):
     _fields_ = [("T12", C.c_float * 16), ("Tcw", C.c_float * 16), ("rmse", C.c_float),
                 ("n_matches", C.c_int32), ("n_good", C.c_int32), ("n_inliers", C.c_int32),
                 ("ransac_ok", C.c_int32), ("pnp_inliers", C.c_int32), ("visited", C.c_int32),
-                ("n_queries", C.c_int32)]
+                ("n_queries", C.c_int32), ("n_sweeps", C.c_int32), ("n_fit_points", C.c_int32)]
 
 
 class Config(C.Structure):
@@ -84,7 +84,7 @@ KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4
 DMATCH_DTYPE = np.dtype([("queryIdx", "<i4"), ("trainIdx", "<i4"), ("imgIdx", "<i4"), ("distance", "<f4")])
 PAIR_DTYPE = np.dtype([("T12", "<f4", 16), ("Tcw", "<f4", 16), ("rmse", "<f4"), ("n_matches", "<i4"),
                        ("n_good", "<i4"), ("n_inliers", "<i4"), ("ransac_ok", "<i4"), ("pnp_inliers", "<i4"),
-                       ("visited", "<i4"), ("n_queries", "<i4")])
+                       ("visited", "<i4"), ("n_queries", "<i4"), ("n_sweeps", "<i4"), ("n_fit_points", "<i4")])
 
 # Every symbol include/odo.h declares, with its ctypes signature.
 SIGNATURES = {
@@ -98,6 +98,8 @@ SIGNATURES = {
     "odo_get_latch": (C.c_double, [P]),
     "odo_track_batch": (C.c_int, [P, P, P, C.c_int, P]),
     "odo_track_batch_host": (C.c_int, [P, P, P, C.c_int, P]),
+    "odo_host_alloc": (P, [C.c_size_t]),
+    "odo_host_free": (C.c_int, [P]),
     "odo_extract_batch": (C.c_int, [P, P, P, C.c_int]),
     "odo_synchronize": (C.c_int, [P]),
     "odo_get_frame": (C.c_int, [P, C.c_int, P, P, P, P, P, C.c_int, P]),

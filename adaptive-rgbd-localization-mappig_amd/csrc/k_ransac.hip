@@ -49,12 +49,13 @@ struct RState {
     // ordered fold (ransac.cpp:233-249), updated under `lock`
     int lock, fold_pos, n, visited, valid, best_cnt, best_h, pad;
     float rmse;
+    int sweeps, fitpts;  // work of the visited prefix (odo_pair_result.n_sweeps / n_fit_points)
 };
 
 struct HypRes {
     double err;
     int cnt;
-    int pad;
+    int pad;  // work: ComputeInliersAndError sweeps | TFC points added << 5
     float T[12];
 };
 
@@ -490,6 +491,8 @@ __global__ void __launch_bounds__(256) k_ransac_prep(RansacBufs B, RansacCfg cfg
         R->n_inliers = 0;
         R->ransac_ok = 0;
         R->visited = 0;
+        R->n_sweeps = 0;
+        R->n_fit_points = 0;
         for (int i = 0; i < 16; i++) R->T12[i] = T12o[i] = (i % 5 == 0) ? 1.f : 0.f;
     }
     active = active && ng >= cfg.min_inlier_th;
@@ -543,6 +546,8 @@ __global__ void __launch_bounds__(256) k_ransac_prep(RansacBufs B, RansacCfg cfg
         S->best_cnt = 0;
         S->best_h = -1;
         S->rmse = 1e6f;
+        S->sweeps = 0;
+        S->fitpts = 0;
     }
     if (done) return;
     __shared__ SampWin s_win;
@@ -745,6 +750,7 @@ ODO_INLINE void try_fold(const RansacBufs& B, const RansacCfg& cfg, int p) {
         int pos = ld_relaxed(&S->fold_pos), n = ld_relaxed(&S->n), visited = ld_relaxed(&S->visited);
         int valid = ld_relaxed(&S->valid), best = ld_relaxed(&S->best_cnt), best_h = ld_relaxed(&S->best_h);
         float rmse = __int_as_float(ld_relaxed(reinterpret_cast<const int*>(&S->rmse)));
+        int sweeps = ld_relaxed(&S->sweeps), fitpts = ld_relaxed(&S->fitpts);
         bool fin = n >= H;
         while (!fin && pos < H) {
             if (!__hip_atomic_load(&ready[pos], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) break;
@@ -752,6 +758,9 @@ ODO_INLINE void try_fold(const RansacBufs& B, const RansacCfg& cfg, int p) {
             const double re = __longlong_as_double(__hip_atomic_load(
                 reinterpret_cast<const long long*>(&hyp[pos].err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
             visited++;
+            const int work = ld_relaxed(&hyp[pos].pad);
+            sweeps += work & 31;
+            fitpts += work >> 5;
             bool brk = false;
             if (rc > 0) {
                 valid++;
@@ -772,6 +781,8 @@ ODO_INLINE void try_fold(const RansacBufs& B, const RansacCfg& cfg, int p) {
         st_relaxed(&S->fold_pos, pos);
         st_relaxed(&S->n, n);
         st_relaxed(&S->visited, visited);
+        st_relaxed(&S->sweeps, sweeps);
+        st_relaxed(&S->fitpts, fitpts);
         st_relaxed(&S->valid, valid);
         st_relaxed(&S->best_cnt, best);
         st_relaxed(&S->best_h, best_h);
@@ -808,6 +819,7 @@ ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int 
         float refinedT[12];
         for (int i = 0; i < 12; i++) refinedT[i] = (i % 5 == 0) ? 1.f : 0.f;
         bool useSample = true, aborted = false;
+        int nsweep = 0, nfit = 0;  // algorithmic work of this hypothesis
 #ifdef ODO_RANSAC_PROFILE
         // -DODO_RANSAC_PROFILE: per-hypothesis phase times (10 ns ticks) via printf
         uint64_t t_tfc = 0, t_get = 0, t_sweep = 0, t0 = 0, t_start = wall_clock64();
@@ -836,6 +848,7 @@ ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int 
                 const uint64_t bal = __ballot(in);
                 if (in) stage_pt(TS, lane_rank(bal), g);
                 wave_sync();
+                nfit += __popcll(bal);
                 tfc_fold(TS, __popcll(bal), lane, tacc, tm1, tm2, tc, TPP);
             } else {
                 // the whole set compacted into the slab in set order, folded
@@ -851,6 +864,7 @@ ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int 
                     }
                     const uint64_t bal = __ballot(in);
                     const int cnt = __popcll(bal);
+                    nfit += cnt;
                     if (nfill + cnt > TFC_CAP) {
                         wave_sync();
                         tfc_fold(TS, nfill, lane, tacc, tm1, tm2, tc, TPP);
@@ -918,6 +932,7 @@ ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int 
                 aborted = true;
                 break;
             }
+            nsweep++;
 #ifdef ODO_RANSAC_PROFILE
             nref++;
 #endif
@@ -950,6 +965,7 @@ ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int 
         if (lane == 0) {
             hr->err = refinedError;
             hr->cnt = (int)refinedCnt;
+            hr->pad = nsweep | (nfit << 5);
         }
         if (lane < 12) {
             float v = refinedT[0];
@@ -1147,6 +1163,8 @@ __global__ void __launch_bounds__(64) k_ransac_final(RansacBufs B, RansacCfg cfg
         R->n_inliers = best_cnt;
         R->ransac_ok = (unsigned)best_cnt >= minInl ? 1 : 0;
         R->visited = S->visited;
+        R->n_sweeps = S->sweeps + (S->valid == 0 ? 1 : 0);  // + the identity fallback's sweep
+        R->n_fit_points = S->fitpts;
         for (int i = 0; i < 12; i++) R->T12[i] = T12o[i] = bestT[i];
         R->T12[12] = R->T12[13] = R->T12[14] = 0.f;
         R->T12[15] = 1.f;

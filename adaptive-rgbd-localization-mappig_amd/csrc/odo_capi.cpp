@@ -120,9 +120,15 @@ struct odo_ctx {
     uint8_t* desc = nullptr;
     float *kun = nullptr, *xyz = nullptr, *ur = nullptr;
     int* nkp = nullptr;
-    // staging for host inputs
-    uint8_t* bgr_in = nullptr;
-    uint16_t* depth_in = nullptr;
+    // staging for host inputs: two device buffers of max_batch frames each,
+    // filled on the copy stream (odo_track_batch_host) while the extraction
+    // stream reads the other one
+    uint8_t* bgr_in[2] = {};
+    uint16_t* depth_in[2] = {};
+    hipStream_t cstream = nullptr;                      // H2D copies of host inputs
+    hipEvent_t ev_in_copied[2] = {}, ev_in_free[2] = {};
+    bool in_used[2] = {};
+    int in_next = 0;
     // pair buffers ([maxb])
     int2 *knn_idx[NSETS] = {}, *knn_dist[NSETS] = {};  // per frame set
     // per frame set: the query frames' VO-landmark bits and kNN-2 query lists
@@ -247,7 +253,8 @@ static void free_ctx(odo_ctx* c) {
     if (!c) return;
     free_hyp_session(c->hs);
     void* ptrs[] = {c->lv, c->cells, c->rx, c->ry, c->pyr, c->blur, c->cand, c->cand_cnt, c->keys, c->knode, c->kquad,
-                    c->okp, c->ocnt, c->kps, c->desc, c->kun, c->xyz, c->ur, c->nkp, c->bgr_in, c->depth_in,
+                    c->okp, c->ocnt, c->kps, c->desc, c->kun, c->xyz, c->ur, c->nkp, c->bgr_in[0], c->depth_in[0],
+                    c->bgr_in[1], c->depth_in[1],
                     c->sort_scratch, c->latch, c->masks, c->adc, c->adb, c->smap, c->acand, c->abig, c->acell,
                     c->akp, c->aband_cnt, c->ahist, c->atsel, c->ansel, c->acell_cnt, c->athresh};
     for (void* p : ptrs)
@@ -276,6 +283,10 @@ static void free_ctx(odo_ctx* c) {
         if (c->ev_raw[i]) hipEventDestroy(c->ev_raw[i]);
         if (c->ev_pyr[i]) hipEventDestroy(c->ev_pyr[i]);
         if (c->ev_blur[i]) hipEventDestroy(c->ev_blur[i]);
+    }
+    for (int i = 0; i < 2; i++) {
+        if (c->ev_in_copied[i]) hipEventDestroy(c->ev_in_copied[i]);
+        if (c->ev_in_free[i]) hipEventDestroy(c->ev_in_free[i]);
     }
     if (c->ev_latch) hipEventDestroy(c->ev_latch);
     for (hipStream_t st : c->owned) hipStreamDestroy(st);
@@ -552,8 +563,10 @@ static int alloc_buffers(odo_ctx* c) {
     if ((e = dalloc(&c->xyz, S * c->kp_cap * 3))) return e;
     if ((e = dalloc(&c->ur, S * c->kp_cap))) return e;
     if ((e = dalloc(&c->nkp, S))) return e;
-    if ((e = dalloc(&c->bgr_in, B * c->W * c->H * 3))) return e;
-    if ((e = dalloc(&c->depth_in, B * c->W * c->H))) return e;
+    for (int i = 0; i < 2; i++) {
+        if ((e = dalloc(&c->bgr_in[i], B * c->W * c->H * 3))) return e;
+        if ((e = dalloc(&c->depth_in[i], B * c->W * c->H))) return e;
+    }
     c->lm_words = (c->kp_cap + 31) / 32;
     if (const char* ks = getenv("ODO_KNN_SPLIT")) c->knn_split = std::min(8, std::max(1, atoi(ks)));
     for (int i = 0; i < NSETS; i++) {
@@ -707,6 +720,12 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
              hipEventCreateWithFlags(&c->ev_blur[i], hipEventDisableTiming) == hipSuccess;
     if (!c->bstream) c->bstream = c->stream;
     if (ok) ok = hipEventCreateWithFlags(&c->ev_latch, hipEventDisableTiming) == hipSuccess;
+    // host-input uploads run on their own stream (the DMA engines), ordered
+    // against the extraction stream by events only
+    if (ok) ok = mk(&c->cstream, false);
+    for (int i = 0; i < 2 && ok; i++)
+        ok = hipEventCreateWithFlags(&c->ev_in_copied[i], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&c->ev_in_free[i], hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         fail(ODO_ERR_DEVICE, "hipStreamCreate failed");
         free_ctx(c);
@@ -1139,14 +1158,46 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
     return ODO_OK;
 }
 
+// Host inputs (main.cpp:93-102 hands Track() images in host memory): the
+// upload of this batch goes to staging buffer k on the copy stream and the
+// extraction stream waits for it, so it overlaps the compute of the batches
+// already queued. Buffer k is rewritten only after the extraction that last
+// read it (two batches earlier) is done. The call returns once the host
+// buffers have been consumed (the caller may refill them); with pinned
+// buffers (odo_host_alloc, or hipHostRegister'ed) the DMA engines read them
+// directly, pageable ones are staged by the runtime.
 int odo_track_batch_host(odo_ctx* c, const uint8_t* bgr, const uint16_t* depth, int n, odo_pair_result* h_results) {
     if (!c || !bgr || !depth || n <= 0 || n > c->maxb) return fail(ODO_ERR_ARG, "bad track args");
-    // the staging buffers are read by the extraction stream of this batch:
-    // earlier extractions must have finished with them
-    HIPCHK(hipStreamSynchronize(c->stream));
-    HIPCHK(hipMemcpy(c->bgr_in, bgr, (size_t)n * c->W * c->H * 3, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->depth_in, depth, (size_t)n * c->W * c->H * 2, hipMemcpyHostToDevice));
-    return odo_track_batch(c, c->bgr_in, c->depth_in, n, h_results);
+    const int k = c->in_next;
+    c->in_next ^= 1;
+    if (c->in_used[k]) HIPCHK(hipStreamWaitEvent(c->cstream, c->ev_in_free[k], 0));
+    const size_t px = (size_t)n * c->W * c->H;
+    HIPCHK(hipMemcpyAsync(c->bgr_in[k], bgr, px * 3, hipMemcpyHostToDevice, c->cstream));
+    HIPCHK(hipMemcpyAsync(c->depth_in[k], depth, px * 2, hipMemcpyHostToDevice, c->cstream));
+    HIPCHK(hipEventRecord(c->ev_in_copied[k], c->cstream));
+    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_in_copied[k], 0));
+    int e;
+    if ((e = odo_track_batch(c, c->bgr_in[k], c->depth_in[k], n, nullptr))) return e;
+    // everything that reads staging buffer k is queued on the extraction stream
+    HIPCHK(hipEventRecord(c->ev_in_free[k], c->stream));
+    c->in_used[k] = true;
+    // the host buffers are free once their copy has landed
+    HIPCHK(hipEventSynchronize(c->ev_in_copied[k]));
+    return finish_batch(c, c->view_set, n, h_results);
+}
+
+void* odo_host_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (bytes == 0 || hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) {
+        fail(ODO_ERR_DEVICE, "hipHostMalloc failed");
+        return nullptr;
+    }
+    return p;
+}
+
+int odo_host_free(void* p) {
+    if (p) HIPCHK(hipHostFree(p));
+    return ODO_OK;
 }
 
 int odo_get_frame(odo_ctx* c, int i, orb_kp* kps, uint8_t* desc, float* kps_un, float* xyz, float* u_right, int cap,
@@ -1498,19 +1549,19 @@ int odo_extract(odo_ctx* c, const uint8_t* img, int channels, const uint16_t* de
     const size_t npix = (size_t)c->W * c->H;
     const int set = next_set(c);
     const int slot = 1;
-    if (depth) HIPCHK(hipMemcpyAsync(c->depth_in, depth, npix * 2, hipMemcpyHostToDevice, st));
-    else HIPCHK(hipMemsetAsync(c->depth_in, 0, npix * 2, st));
+    if (depth) HIPCHK(hipMemcpyAsync(c->depth_in[0], depth, npix * 2, hipMemcpyHostToDevice, st));
+    else HIPCHK(hipMemsetAsync(c->depth_in[0], 0, npix * 2, st));
     if (channels == 3) {
-        HIPCHK(hipMemcpyAsync(c->bgr_in, img, npix * 3, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(c->bgr_in[0], img, npix * 3, hipMemcpyHostToDevice, st));
         tmark(c, 0, st);
-        int e = run_extract(c, set, c->bgr_in, c->depth_in, 1, slot);
+        int e = run_extract(c, set, c->bgr_in[0], c->depth_in[0], 1, slot);
         if (e) return e;
     } else {
         // ORBextractor::operator() on a gray image: level 0 = the image itself
         HIPCHK(hipMemcpy2DAsync(c->pyr + (fbase(c, set) + slot) * c->pyr_size, c->lv_h[0].pitch, img, c->W, c->W, c->H,
                                 hipMemcpyHostToDevice, st));
         tmark(c, 0, st);
-        int e = run_extract_from_gray(c, set, c->depth_in, 1, slot);
+        int e = run_extract_from_gray(c, set, c->depth_in[0], 1, slot);
         if (e) return e;
     }
     c->view_set = set;

@@ -27,13 +27,43 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG_DIR = os.path.join(ROOT, "adaptive-rgbd-localization-mappig_amd")
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# int32 VALU lane-ops: 256 CU x 4 SIMD x 16 lanes/clk (a wave64 VALU op issues
-# every 4 clk, MI355X_MICROARCH.md cycle constants) x 2.4 GHz
-INT_VALU_PEAK_TOPS = 256 * 4 * 16 * 2.4e9 / 1e12
-# Hamming-match work per (query, train) comparison: 8 xor + 8 popcount over the
-# 256-bit descriptors, key formation, and the top-2 update (min + med3)
-KNN_OPS_PER_CMP = 19
+FP64_PEAK_TFLOPS = 78.6      # MI355X_MICROARCH.md: FP64 vector spec
+# the algorithmic Hamming work is 16 int32 lane-ops per (query,
+# train) comparison (8 v_xor_b32 + 8 v_bcnt_u32_b32 over the 256-bit
+# descriptors; the top-2 update is excluded). k_knn2 issues 19 (+ key, min, med3).
+KNN_OPS_PER_CMP = 16
+KNN_ISSUED_OPS_PER_CMP = 19
+# SURVEY §8(d) RANSAC work: ~120 FP64 flops per non-shortcut ErrorFunction2
+# evaluation (E = sweeps x good matches) and ~40 FP32 flops per point added to
+# a TransformationFromCorrespondences fit (F)
+RANSAC_FLOPS_PER_EVAL = 120
+RANSAC_FLOPS_PER_FIT_POINT = 40
 KNN_TRAFFIC = os.path.join(ROOT, "profiles", "r01_knn2_traffic.json")
+# on-box peak microbenchmarks (tools/ubench_peak.hip); the fallbacks are the
+# r02 measurements
+UBENCH = os.path.join(ROOT, "profiles", "r02_ubench_peak.jsonl")
+UBENCH_FALLBACK = {"valu_xor_bcnt": 50.213, "fp64_fma": 61.22, "hbm_read": 6946.7, "hbm_copy": 4867.8,
+                   "mfma_i32_16x16x64_i8": 3484.73}
+
+
+def measured_peaks(path=UBENCH):
+    """Best rate of each instruction mix / access pattern in the committed
+    microbenchmark output (Top/s, TFLOP/s or GB/s)."""
+    peaks = dict(UBENCH_FALLBACK)
+    if os.path.exists(path):
+        best = {}
+        with open(path) as f:
+            for line in f:
+                try:
+                    r = json.loads(line)
+                except ValueError:
+                    continue
+                b = r.get("bench")
+                v = r.get("tops", r.get("tflops", r.get("gbs")))
+                if b and v is not None:
+                    best[b] = max(best.get(b, 0.0), float(v))
+        peaks.update(best)
+    return peaks
 
 
 def load_module(name, path, pkg_dir=None):
@@ -80,58 +110,133 @@ def job_throughput(frames_per_step: int, steps: int, world: int, elapsed_max: fl
     return frames_per_step * steps * world / elapsed_max
 
 
-def level_pixels(w, h, nlevels=8, scale=1.2):
-    s, tot, lv = 1.0, 0, []
-    for l in range(nlevels):
-        inv = np.float32(1.0) / np.float32(s)
-        lw, lh = int(np.rint(np.float32(w) * inv)), int(np.rint(np.float32(h) * inv))
-        lv.append((lw, lh))
-        tot += lw * lh
-        s = float(np.float32(np.float64(np.float32(s)) * np.float64(np.float32(scale))))
-    return tot, lv
+def host_info():
+    """nproc, usable cores and CPU model of this host (the GPU box's when run there)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "usable_cores": len(os.sched_getaffinity(0)), "model": model}
 
 
-def stage_model(stage, ms, B, w, h, nkp_mean):
-    """Algorithmic work per launch of a stage -> (bound, achieved, peak, unit, work)."""
-    pyr_px, lv = level_pixels(w, h)
-    if stage == "gray+pyramid":
-        byts = B * (3 * w * h + w * h + sum(2 * a * b for a, b in lv[1:]) + sum(a * b for a, b in lv[:-1]))
-        return "hbm", byts / (ms * 1e-3) / 1e9, HBM_PEAK_GBS, "GB/s", byts
-    if stage == "blur":
-        byts = B * 2 * pyr_px
-        return "hbm", byts / (ms * 1e-3) / 1e9, HBM_PEAK_GBS, "GB/s", byts
-    if stage == "fast":
-        byts = B * pyr_px
-        return "hbm", byts / (ms * 1e-3) / 1e9, HBM_PEAK_GBS, "GB/s", byts
-    if stage == "knn2":
-        ops = B * float(KNN_OPS_PER_CMP) * nkp_mean * nkp_mean
-        return "valu", ops / (ms * 1e-3) / 1e12, INT_VALU_PEAK_TOPS, "Top/s", ops
-    byts = B * (5 * w * h + 84 * nkp_mean)
-    return "hbm", byts / (ms * 1e-3) / 1e9, HBM_PEAK_GBS, "GB/s", byts
+def cpu_baseline(bgr, dep, nfeat, iters, n_frames, reps, adaptive=False, threads=16):
+    """The C++ oracle on the first n_frames frames of the same sequence.
 
-
-def cpu_baseline(bgr, dep, nfeat, iters, n_frames, adaptive=False):
-    """The C++ oracle (single thread) on the first n_frames frames of the same sequence."""
+    Single thread: this thread pinned to one core (taskset -c equivalent),
+    one warm-up pass, then `reps` timed passes; per-stage medians (extraction
+    per frame, match + RANSAC + PnP per pair). All cores: the same frames with
+    a thread pool (ctypes releases the GIL inside the oracle) extracting frames
+    and tracking pairs in parallel, the latch taken from pair 1 as in the
+    batched contract (ADAPTIVE extraction stays sequential: its thresholds
+    carry from frame to frame)."""
+    from concurrent.futures import ThreadPoolExecutor
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
     cal = O.fr1_calib()
     p = O.orb_params(nfeat)
     rp = O.ransac_params(iters)
     pkg = load_pkg()
-    ex = O.AdaptiveExtractor() if adaptive else None
+    n = len(bgr)
+
+    def extract(ex, i):
+        return ex.extract_frame(bgr[i % n], dep[i % n], cal) if ex is not None else \
+            O.extract_frame(bgr[i % n], dep[i % n], p, cal)
+
+    def run_pass():
+        ex = O.AdaptiveExtractor() if adaptive else None
+        te = tt = 0.0
+        prev, latch = None, float("nan")
+        for i in range(n_frames):
+            t0 = time.perf_counter()
+            f = extract(ex, i)
+            t1 = time.perf_counter()
+            if prev is not None:
+                _, _, _, latch = O.track_pair(prev, f, cal, rp, pkg.pair_seed(0x5EED0000, i), latch)
+            tt += time.perf_counter() - t1
+            te += t1 - t0
+            prev = f
+        return te, tt
+
+    aff = os.sched_getaffinity(0)
+    core = min(aff)
+    os.sched_setaffinity(0, {core})
+    try:
+        run_pass()  # warm-up
+        passes = [run_pass() for _ in range(reps)]
+    finally:
+        os.sched_setaffinity(0, aff)
+    tot = sorted(te + tt for te, tt in passes)
+    med = tot[len(tot) // 2]
+    ext_ms = sorted(te for te, _ in passes)[len(passes) // 2] / n_frames * 1e3
+    trk_ms = sorted(tt for _, tt in passes)[len(passes) // 2] / max(1, n_frames - 1) * 1e3
+
+    nthr = max(1, min(threads, len(aff)))
+    nf_all = n_frames * 4
+
+    def all_cores_pass():
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(nthr) as pool:
+            if adaptive:
+                ex = O.AdaptiveExtractor()
+                frames = [extract(ex, i) for i in range(nf_all)]
+            else:
+                frames = list(pool.map(lambda i: extract(None, i), range(nf_all)))
+            _, _, _, latch = O.track_pair(frames[0], frames[1], cal, rp, pkg.pair_seed(0x5EED0000, 1))
+            list(pool.map(lambda i: O.track_pair(frames[i - 1], frames[i], cal, rp,
+                                                 pkg.pair_seed(0x5EED0000, i), latch), range(2, nf_all)))
+        return time.perf_counter() - t0
+
+    all_cores_pass()
+    ta = sorted(all_cores_pass() for _ in range(3))[1]
+    return {"fps": n_frames / med, "seconds": med, "reps": reps, "core": core,
+            "stage_ms": {"extract_per_frame": round(ext_ms, 3), "match_ransac_pnp_per_pair": round(trk_ms, 3)},
+            "all_cores": {"fps": nf_all / ta, "threads": nthr, "frames": nf_all}}
+
+
+def host_leg(pkg, odo, bgr_b, dep_b, B, W, H, steps, warmup, world, dist):
+    """Frames/s from BGR8 + depth16 in (pinned) host memory (SURVEY §8(d) unit):
+    odo_track_batch_host uploads each batch on the copy stream into a staging
+    buffer while the compute of the previous batches runs."""
+    import torch
+    hf = pkg.HostFrames(B, W, H)
+    hf.bgr[:] = bgr_b
+    hf.depth[:] = dep_b
+    for _ in range(warmup):
+        odo.track_batch_host(hf, want_results=False)
+    odo.synchronize()
+    if world > 1:
+        dist.barrier()
     t0 = time.perf_counter()
-    prev = None
-    latch = float("nan")
-    for i in range(n_frames):
-        if ex is not None:
-            f = ex.extract_frame(bgr[i % len(bgr)], dep[i % len(dep)], cal)
-        else:
-            f = O.extract_frame(bgr[i % len(bgr)], dep[i % len(dep)], p, cal)
-        if prev is not None:
-            _, _, _, latch = O.track_pair(prev, f, cal, rp, pkg.pair_seed(0x5EED0000, i), latch)
-        prev = f
-    dt = time.perf_counter() - t0
-    return n_frames / dt, dt
+    for _ in range(steps):
+        odo.track_batch_host(hf, want_results=False)
+    odo.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = max_over_ranks(time.perf_counter() - t0, dist, world)
+    nbytes = hf.bgr.nbytes + hf.depth.nbytes
+    hf.close()
+    # raw pinned host -> HBM rate of the same bytes, no compute (the PCIe bound)
+    hsrc = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    ddst = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    ddst.copy_(hsrc, non_blocking=True)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(3):
+        ddst.copy_(hsrc, non_blocking=True)
+    torch.cuda.synchronize()
+    raw = 3 * nbytes / (time.perf_counter() - t1) / 1e9
+    del hsrc, ddst
+    fps = job_throughput(B, steps, world, dt)
+    return {"value": round(fps, 2), "unit": "frames/s", "ms_per_step": round(dt / steps * 1e3, 3), "steps": steps,
+            "bytes_per_frame": nbytes // B, "h2d_gbs": round(fps / world * nbytes / B / 1e9, 2),
+            "raw_pinned_h2d_gbs": round(raw, 2),
+            "pcie_bound_fps_per_gpu": round(raw * 1e9 / (nbytes / B), 1),
+            "inputs": "pinned host buffers (odo_host_alloc), one upload per batch on the copy stream"}
 
 
 def main():
@@ -140,14 +245,15 @@ def main():
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=256,
-                    help="frames per step (MI355X: 45.7k / 52.9k / 56.8k / 57.0k frames/s at 64 / 128 / 192 / 256: "
-                         "the latency-bound pair stages see more pairs per launch)")
+                    help="frames per step (the latency-bound pair stages see more pairs per launch at larger batches)")
     ap.add_argument("--seq-len", type=int, default=64, help="frames in the closed-loop sequence (motion per frame)")
     ap.add_argument("--nfeatures", type=int, default=2000)
     ap.add_argument("--iters", type=int, default=500, help="RANSAC hypotheses (mIterations)")
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
-    ap.add_argument("--cpu-frames", type=int, default=192, help="oracle sample size (frames, ~10 s)")
+    ap.add_argument("--cpu-frames", type=int, default=24, help="oracle sample (frames per timed pass)")
+    ap.add_argument("--cpu-reps", type=int, default=5, help="timed oracle passes (median reported)")
+    ap.add_argument("--host-steps", type=int, default=10, help="steps of the from-host leg (0: skip it)")
     ap.add_argument("--no-kernel-timing", action="store_true", help="no events around the kNN-2 launches")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--detector", choices=["orb_slam2", "adaptive"], default="orb_slam2",
@@ -233,20 +339,24 @@ def main():
     Tcw = tj.chain_poses(res[:L], np.linalg.inv(gt_poses[0]).astype(np.float32))
     ate_mm = 1000.0 * tj.ate_rmse(tj.camera_centres(Tcw), gt_poses[:L, :3, 3])
     nkp_mean = float(np.mean(nkp))
+    peaks = measured_peaks()
     # Roofline of the Hamming-match kernel (k_knn2), the kernel the north star
     # names. Brute-force kNN-2 re-reads each 32-byte descriptor ~2000 times from
     # LDS, so it is bound by the integer VALU issue rate, not by HBM: achieved =
-    # algorithmic lane-ops of one launch / its live mean duration.
+    # SURVEY §8(d)'s algorithmic 16 lane-ops per comparison x the launch's
+    # comparisons / its live mean duration; peak = the measured on-box rate of
+    # the same v_xor_b32 + v_bcnt_u32_b32 mix (profiles/r02_ubench_peak.jsonl).
     roofline = None
+    nq = res_q["n_queries"]
     if knn_ms:
         # result i = pair (frame i-1, frame i); frame -1 is the previous batch's
         # last frame (the same sequence is tracked every step). kNN-2 compares
         # the query frame's landmark keypoints (n_queries) with every keypoint
         # of frame i: Matcher::KnnMatch drops the other queries' matches
-        nq = res_q["n_queries"]
         cmp = int(sum(int(nq[i]) * nkp[i] for i in range(B)))
         ops = float(KNN_OPS_PER_CMP) * cmp
         ach = ops / (knn_ms * 1e-3) / 1e12
+        peak = peaks["valu_xor_bcnt"]
         traffic = None
         if os.path.exists(KNN_TRAFFIC):
             with open(KNN_TRAFFIC) as f:
@@ -255,21 +365,61 @@ def main():
             # scaled per pair when this run's batch differs from the profiled one
             traffic = tr.get("hbm_bytes_per_launch") if tr.get("batch") == B else \
                 (tr["hbm_bytes_per_pair"] * B if "hbm_bytes_per_pair" in tr else None)
-        roofline = {"bound": "valu", "achieved": round(ach, 3), "peak": round(INT_VALU_PEAK_TOPS, 2),
-                    "unit": "Top/s", "frac": round(ach / INT_VALU_PEAK_TOPS, 4), "traffic": traffic,
+        roofline = {"bound": "valu", "achieved": round(ach, 3), "peak": round(peak, 2),
+                    "unit": "Top/s", "frac": round(ach / peak, 4), "traffic": traffic,
                     "kernel": "k_knn2", "kernel_ms": round(knn_ms, 4), "launches": knn_launches,
-                    "work": f"{cmp} descriptor comparisons x {KNN_OPS_PER_CMP} int32 lane-ops",
+                    "work": f"{cmp} descriptor comparisons x {KNN_OPS_PER_CMP} int32 lane-ops (SURVEY 8(d))",
+                    "peak_source": "measured v_xor_b32 + v_bcnt_u32_b32 rate, profiles/r02_ubench_peak.jsonl",
+                    "issued_ops_per_cmp": KNN_ISSUED_OPS_PER_CMP,
                     # algorithmic HBM bytes: every descriptor read once, 16 B of top-2 out per query
                     "hbm_gbs": round(sum(32 * int(nq[i]) + 32 * nkp[i] + 16 * int(nq[i]) for i in range(B)) /
                                      (knn_ms * 1e-3) / 1e9, 1)}
 
+    # the other SURVEY §8(d) legs, from the per-stage (one stream, events
+    # between stages) times of the untimed timing step
+    ext_stages = [k for k in ("gray+pyramid", "gray", "smap+cand", "fast", "octree", "chain+select", "blur", "finalize")
+                  if k in timings]
+    ext_ms = sum(timings[k] for k in ext_stages)
+    comp_bytes = B * (5 * W * H + 84 * nkp_mean)  # compulsory I/O per frame: 5WH + 84N
+    legs = {"extraction": {"bound": "hbm", "achieved": round(comp_bytes / (ext_ms * 1e-3) / 1e9, 1),
+                           "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": round(comp_bytes / (ext_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                           "measured_peak_read": peaks["hbm_read"], "ms": round(ext_ms, 4),
+                           "work": f"compulsory bytes 5WH + 84N per frame x {B} frames", "stages": ext_stages}}
+    ok_res = res_q[1:] if len(res_q) > 1 else res_q
+    E = float(sum(int(r["n_sweeps"]) * int(r["n_good"]) for r in res_q))
+    F = float(sum(int(r["n_fit_points"]) for r in res_q))
+    if "ransac" in timings and timings["ransac"] > 0:
+        t = timings["ransac"] * 1e-3
+        legs["ransac"] = {"bound": "fp64", "achieved": round(E * RANSAC_FLOPS_PER_EVAL / t / 1e12, 4),
+                          "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                          "frac": round(E * RANSAC_FLOPS_PER_EVAL / t / 1e12 / FP64_PEAK_TFLOPS, 5),
+                          "measured_peak_fma": peaks["fp64_fma"], "ms": round(timings["ransac"], 4),
+                          "evaluations": int(E), "fit_points": int(F),
+                          "fp32_fit_tflops": round(F * RANSAC_FLOPS_PER_FIT_POINT / t / 1e12, 5),
+                          "mean_sweeps_per_pair": round(float(np.mean(ok_res["n_sweeps"])), 2),
+                          "work": f"E = sum(n_sweeps x n_good) x {RANSAC_FLOPS_PER_EVAL} FP64 flops"}
+    if "pnp" in timings:
+        legs["pnp"] = {"bound": "latency", "ms": round(timings["pnp"], 4)}
+
+    from_host = None
+    if args.host_steps > 0:
+        from_host = host_leg(pkg, odo, bgr, dep, B, W, H, args.host_steps, 2, world, dist)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         nf = args.cpu_frames
-        fps, dt = cpu_baseline(bgr, dep, args.nfeatures, args.iters, nf, adaptive)
-        cpu = {"value": round(fps, 3), "unit": "frames/s", "cores": 1, "kind": "port",
-               "sample": f"{nf} frames (the rank-0 {L}-frame closed loop, cycled) through the C++ oracle's "
-                         f"extract + match + RANSAC + PnP, single thread ({dt:.1f} s)"}
+        cb = cpu_baseline(bgr, dep, args.nfeatures, args.iters, nf, args.cpu_reps, adaptive)
+        hi = host_info()
+        cpu = {"value": round(cb["fps"], 3), "unit": "frames/s", "cores": 1, "kind": "port",
+               "sample": f"{nf} frames of the rank-0 {L}-frame closed loop through the C++ oracle's extract + "
+                         f"match + RANSAC + PnP, one thread pinned to core {cb['core']}, median of {cb['reps']} "
+                         f"passes after a warm-up ({cb['seconds']:.2f} s per pass)",
+               "stage_ms": cb["stage_ms"], "host": hi,
+               "all_cores": {"value": round(cb["all_cores"]["fps"], 2), "unit": "frames/s",
+                             "cores": cb["all_cores"]["threads"],
+                             "sample": f"{cb['all_cores']['frames']} frames, frames-parallel thread pool "
+                                       f"(extraction and pairs), median of 3 passes"}}
 
     if rank == 0:
         ok = res[1:]
@@ -300,7 +450,9 @@ def main():
                        "ate_mm": round(ate_mm, 3)},
             "stage_ms": {k: round(v, 4) for k, v in timings.items()},
             "host_submit_ms_per_step": round(submit / args.steps * 1e3, 3),
+            "from_host": from_host,
             "roofline": roofline,
+            "roofline_legs": legs,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

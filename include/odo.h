@@ -75,9 +75,19 @@ double odo_get_latch(odo_ctx* ctx);
  * the extraction stream, and odo_synchronize() waits for all of them. */
 int odo_track_batch(odo_ctx* ctx, const uint8_t* d_bgr, const uint16_t* d_depth, int n,
                     odo_pair_result* h_results);
-/* Same with host inputs (H2D copy included). */
+/* Same with host inputs, as Tracking::Track receives them (main.cpp:93-102).
+ * The H2D upload runs on the context's copy stream into one of two device
+ * staging buffers and overlaps the compute of the batches already queued; the
+ * call returns once the host buffers have been consumed (the caller may refill
+ * them) and the batch is queued. Pinned buffers (odo_host_alloc) are read by
+ * the DMA engines directly; pageable ones are staged by the HIP runtime. With
+ * h_results non-null it waits for the batch and fills the results. */
 int odo_track_batch_host(odo_ctx* ctx, const uint8_t* bgr, const uint16_t* depth, int n,
                          odo_pair_result* h_results);
+/* Page-locked host memory for input frames (decode straight into it so the
+ * upload needs no extra host copy). NULL on failure; free with odo_host_free. */
+void* odo_host_alloc(size_t bytes);
+int odo_host_free(void* p);
 /* Extraction only (frames land in the batch slots; no pairs). Device inputs. */
 int odo_extract_batch(odo_ctx* ctx, const uint8_t* d_bgr, const uint16_t* d_depth, int n);
 int odo_synchronize(odo_ctx* ctx);

@@ -128,6 +128,9 @@ typedef struct odo_pair_result {
     int32_t pnp_inliers;  /* PnPSolver::Compute return */
     int32_t visited;      /* RANSAC iterations actually run (realIters) */
     int32_t n_queries;    /* kNN-2 queries: F1 keypoints holding a VO landmark (the only ones KnnMatch keeps) */
+    int32_t n_sweeps;     /* ComputeInliersAndError calls in the visited iterations (+1 for the identity
+                             fallback): the RANSAC work E of SURVEY §8(d) is n_sweeps * n_good evaluations */
+    int32_t n_fit_points; /* points added to TransformationFromCorrespondences fits (F of SURVEY §8(d)) */
 } odo_pair_result;
 
 #ifdef __cplusplus

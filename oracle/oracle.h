@@ -134,6 +134,7 @@ void oracle_libc_rand_stream(uint32_t seed, int n, int32_t* out);
  * mvKeys3Dc of both frames. inlier_idx receives mvInliers as indices into
  * m12 order? No: as DMatch copies. latch: in/out DepthCovariance static
  * (NaN = not yet latched). */
+void oracle_last_ransac_work(int* sweeps, int* fit_points);
 int oracle_ransac(const odo_dmatch* m12, int n12, const float* xyz1, const float* xyz2,
                   const odo_ransac_params* p, odo_rng* rng, double* latch,
                   float* T12, float* rmse, odo_dmatch* inliers, int* n_inliers,

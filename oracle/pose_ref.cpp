@@ -258,6 +258,9 @@ struct RansacState {
     odo_ransac_params p;
     odo_rng* rng;
     double* latch;
+    // algorithmic work of the visited iterations
+    int n_sweeps = 0;      // ComputeInliersAndError calls
+    int n_fit_points = 0;  // points added to TransformationFromCorrespondences
 };
 
 int32_t rng_next(odo_rng* r);
@@ -362,6 +365,7 @@ double compute_inliers_and_error(RansacState& S, const std::vector<DM>& m12, con
     for (int i = 0; i < 4; i++)
         for (int j = 0; j < 4; j++) Td[i][j] = (double)T[i * 4 + j];
     const float th = S.p.max_mahalanobis * S.p.max_mahalanobis;
+    S.n_sweeps++;
     for (const DM& m : m12) {
         const float* o = &S.xyz1[3 * m.queryIdx];
         const float* t = &S.xyz2[3 * m.trainIdx];
@@ -389,6 +393,7 @@ void transform_from_matches(RansacState& S, const std::vector<DM>& v, float T[16
         if (std::isnan(f[2]) || std::isnan(t[2])) continue;
         float weight = 1.0f / (f[2] * t[2]);
         tfc.add(f, t, weight);
+        S.n_fit_points++;
     }
     tfc.get(T);
 }
@@ -1188,6 +1193,14 @@ void oracle_libc_rand_stream(uint32_t seed, int n, int32_t* out) {
     for (int i = 0; i < n; i++) out[i] = rand();
 }
 
+// work counters of the calling thread's last oracle_ransac (measurement only)
+static thread_local int g_last_sweeps = 0, g_last_fit_points = 0;
+
+void oracle_last_ransac_work(int* sweeps, int* fit_points) {
+    *sweeps = g_last_sweeps;
+    *fit_points = g_last_fit_points;
+}
+
 int oracle_ransac(const odo_dmatch* m12, int n12, const float* xyz1, const float* xyz2,
                   const odo_ransac_params* p, odo_rng* rng, double* latch, float* T12, float* rmse,
                   odo_dmatch* inliers, int* n_inliers, int* visited, int* n_good) {
@@ -1196,6 +1209,8 @@ int oracle_ransac(const odo_dmatch* m12, int n12, const float* xyz1, const float
     for (int i = 0; i < n12; i++) m[i] = DM{m12[i].queryIdx, m12[i].trainIdx, m12[i].imgIdx, m12[i].distance};
     std::vector<DM> inl;
     bool ok = ransac_iterate(S, m, T12, rmse, inl, visited, n_good);
+    g_last_sweeps = S.n_sweeps;
+    g_last_fit_points = S.n_fit_points;
     for (size_t i = 0; i < inl.size(); i++)
         inliers[i] = odo_dmatch{inl[i].queryIdx, inl[i].trainIdx, inl[i].imgIdx, inl[i].distance};
     *n_inliers = (int)inl.size();
@@ -1349,6 +1364,8 @@ int oracle_track_pair(const orb_kp* k1, const uint8_t* d1, const float* xyz1, in
     res->n_inliers = ninl;
     res->visited = visited;
     res->n_good = ngood;
+    res->n_sweeps = g_last_sweeps;
+    res->n_fit_points = g_last_fit_points;
     // Odometry::Compute ADAPTIVE_RBA: Tcw2 = T12 * Tcw1 (= T12), then PnP on F2
     std::vector<float> Xw, ob;
     std::vector<int> eidx;

@@ -58,7 +58,7 @@ class PairResult(C.Structure):
     _fields_ = [("T12", C.c_float * 16), ("Tcw", C.c_float * 16), ("rmse", C.c_float),
                 ("n_matches", C.c_int32), ("n_good", C.c_int32), ("n_inliers", C.c_int32),
                 ("ransac_ok", C.c_int32), ("pnp_inliers", C.c_int32), ("visited", C.c_int32),
-                ("n_queries", C.c_int32)]
+                ("n_queries", C.c_int32), ("n_sweeps", C.c_int32), ("n_fit_points", C.c_int32)]
 
 
 def fr1_calib() -> Calib:
@@ -104,6 +104,7 @@ def lib():
             "oracle_libc_rand_stream": (None, [C.c_uint32, C.c_int, P]),
             "oracle_ransac": (C.c_int, [P, C.c_int, P, P, P, P, P, P, P, P, P, P, P]),
             "oracle_tfc": (None, [P, P, P, C.c_int, P]),
+            "oracle_last_ransac_work": (None, [P, P]),
             "oracle_svd3": (None, [P, P, P, P]),
             "oracle_pnp": (C.c_int, [P, P, C.c_int, P, P, P, P]),
             "oracle_kabsch": (None, [P, P, C.c_int, P]),

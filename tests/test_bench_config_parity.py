@@ -11,7 +11,8 @@ ransac.cpp:155-267; PnPSolver::Compute pnpsolver.cpp:17-214):
 
 * every frame's keypoints, descriptors, kun, xyz, uR: bit-exact;
 * every pair's match list, n_queries, n_good, visited, n_inliers, ok, T12, rmse,
-  RANSAC inlier mask: bit-exact; the DepthCovariance latch: exact;
+  RANSAC inlier mask, RANSAC work (sweeps, fit points): bit-exact; the
+  DepthCovariance latch: exact;
 * PnP pose within 1e-4; PnP inlier flags equal except on edges whose chi2 at
   the oracle's pose lies within 2 % of the threshold (5.991 mono, 7.815 stereo).
 
@@ -171,6 +172,8 @@ def _compare(name, c, odo, res, oracle, full=True):
         assert (res[p]["n_matches"], res[p]["n_good"], res[p]["visited"], res[p]["n_inliers"],
                 res[p]["ransac_ok"]) == (r.n_matches, r.n_good, r.visited, r.n_inliers, r.ransac_ok), \
             f"{tag}: RANSAC counts"
+        assert (res[p]["n_sweeps"], res[p]["n_fit_points"]) == (r.n_sweeps, r.n_fit_points), \
+            f"{tag}: RANSAC work counts (sweeps, fit points)"
         assert np.array_equal(res[p]["T12"], np.array(r.T12, np.float32)), f"{tag}: T12"
         assert res[p]["rmse"] == np.float32(r.rmse), f"{tag}: rmse"
         ni = int(r.n_inliers)

@@ -64,6 +64,7 @@ def test_config_path_parity(name):
             (r.n_good, r.visited, r.n_inliers, r.ransac_ok), f"{name} pair {p}: RANSAC counts"
         assert np.array_equal(res[p]["T12"], np.array(r.T12, np.float32)), f"{name} pair {p}: T12"
         assert res[p]["rmse"] == np.float32(r.rmse)
+        assert (res[p]["n_sweeps"], res[p]["n_fit_points"]) == (r.n_sweeps, r.n_fit_points), f"{name} pair {p}: work"
         dT = np.abs(res[p]["Tcw"] - np.array(r.Tcw, np.float32)).max()
         assert dT < 1e-4, f"{name} pair {p}: PnP pose differs by {dT}"
         assert abs(int(res[p]["pnp_inliers"]) - r.pnp_inliers) <= 2

@@ -134,6 +134,7 @@ def test_pairs_match_ransac_pnp(cfg2_run):
         assert res[p]["visited"] == r.visited, f"pair {p}: visited {res[p]['visited']} vs {r.visited}"
         assert res[p]["n_inliers"] == r.n_inliers
         assert res[p]["ransac_ok"] == r.ransac_ok
+        assert (res[p]["n_sweeps"], res[p]["n_fit_points"]) == (r.n_sweeps, r.n_fit_points), f"pair {p}: work"
         assert np.array_equal(res[p]["T12"], np.array(r.T12, np.float32)), f"pair {p}: T12 not bit-exact"
         assert res[p]["rmse"] == np.float32(r.rmse)
         T_gpu = res[p]["Tcw"].reshape(4, 4)
