@@ -253,7 +253,7 @@ def main():
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--cpu-frames", type=int, default=24, help="oracle sample (frames per timed pass)")
     ap.add_argument("--cpu-reps", type=int, default=5, help="timed oracle passes (median reported)")
-    ap.add_argument("--host-steps", type=int, default=10, help="steps of the from-host leg (0: skip it)")
+    ap.add_argument("--host-steps", type=int, default=20, help="steps of the from-host leg (0: skip it)")
     ap.add_argument("--no-kernel-timing", action="store_true", help="no events around the kNN-2 launches")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--detector", choices=["orb_slam2", "adaptive"], default="orb_slam2",

@@ -1177,7 +1177,7 @@ int oracle_vo_landmarks(const float* xyz, int n, float th_depth_m, uint8_t* has_
 }
 
 void oracle_rng_seed(odo_rng* r, uint32_t seed) {
-    static char statebuf[128];
+    char statebuf[128];  // per call: the oracle is called from several threads at once
     struct random_data rd;
     memset(&rd, 0, sizeof(rd));
     initstate_r(seed, statebuf, sizeof(statebuf), &rd);  // TYPE_3, seeded via srandom_r
