@@ -221,6 +221,194 @@ __global__ void __launch_bounds__(KNN_TH) k_knn2(const uint8_t* __restrict__ qde
     flush();
 }
 
+// ============================================================ kNN-2 Hamming on the matrix cores
+// Exact integer reformulation of the same comparison. With s(b) = +1 / -1 for a
+// descriptor bit 0 / 1, the dot product of two descriptors' sign vectors is
+// 256 - 2H (H = Hamming distance). k_knn2_mx feeds the train signs scaled by +64
+// and the query signs scaled by -64 to v_mfma_i32_16x16x64_i8, so a 256-bit
+// comparison is four k-steps whose i32 sum is -4096 (256 - 2H) = 8192 H - 2^20.
+// The accumulator starts at the train index, so the MFMA result is already the
+// packed key 8192 H + idx - 2^20 (idx < 8192), ordered exactly as (H, idx): the
+// BFMatcher top-2 is min + med3 on signed keys, two VALU ops per comparison
+// instead of k_knn2's 19.
+//
+// Layout: a workgroup item is (pair, block of 256 queries); each of its 4 waves
+// holds 64 queries as the MFMA B operand (4 query tiles x 4 k-steps x 16 signed
+// bytes per lane = 64 VGPRs, expanded once per item). Trains stream through LDS
+// in chunks of 64: each thread expands 4 of a chunk's 1024 (train, 16-bit unit)
+// pieces into 16 signed bytes (double-buffered, one barrier per chunk); the
+// 16-byte pieces of a train are XOR-swizzled by the train index so the A-operand
+// ds_read_b128 of 16 consecutive trains hits distinct banks. The output
+// D[train][query] puts 4 trains of one query in each lane; the 4 lane groups
+// holding a query are merged with two xor-shuffles at the end of the item.
+#define KMX_Q 256       // queries per item (4 waves x 64)
+#define KMX_T 64        // trains per LDS chunk
+#define KMX_EMPTY 0x7FFFFFFF
+#define KMX_BIG 0x3FFFFFFF  // accumulator start of a train slot past the end (never a top-2 key)
+typedef int kmx_v4i __attribute__((ext_vector_type(4)));
+
+// 16 descriptor bits -> 16 bytes: bit 0 -> +64 (0x40), bit 1 -> -64 (0xC0)
+ODO_INLINE kmx_v4i kmx_expand16(uint32_t h) {
+    kmx_v4i r;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t nib = __builtin_amdgcn_ubfe(h, 4 * j, 4);
+        const uint32_t v = __umul24(nib, 0x204081u) & 0x01010101u;  // bit i -> byte i
+        r[j] = (int)((v << 7) | 0x40404040u);
+    }
+    return r;
+}
+ODO_INLINE int med3_i32(int a, int b, int c) {
+    int r;
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+__global__ void __launch_bounds__(256) k_knn2_mx(const uint8_t* __restrict__ qdesc, const int* __restrict__ qn,
+                                                 size_t q_stride, const uint8_t* __restrict__ tdesc,
+                                                 const int* __restrict__ tn, size_t t_stride,
+                                                 int2* __restrict__ out_idx, int2* __restrict__ out_dist,
+                                                 size_t out_stride, const int32_t* __restrict__ qlist,
+                                                 const int* __restrict__ qcnt, size_t ql_stride, int npairs) {
+    __builtin_amdgcn_s_setprio(ODO_KNN_PRIO);
+    __shared__ __attribute__((aligned(16))) uint8_t s_tr[2][KMX_T * 256];
+    __shared__ int s_pre[KNN_MAXP + 1];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int grp = lane >> 4, col = lane & 15;
+    for (int i = tid; i < npairs; i += 256) {
+        const int nq = qlist ? qcnt[i] : qn[i];
+        s_pre[i + 1] = (nq + KMX_Q - 1) / KMX_Q;
+    }
+    if (tid == 0) s_pre[0] = 0;
+    __syncthreads();
+    if (tid == 0)
+        for (int i = 1; i <= npairs; i++) s_pre[i] += s_pre[i - 1];
+    __syncthreads();
+    const int nact = s_pre[npairs];
+    // staging role of this thread: train st_t of a chunk, 16-bit units 4 st_q .. 4 st_q + 3
+    const int st_t = tid >> 2, st_q = tid & 3;
+    for (int g = blockIdx.x; g < nact; g += gridDim.x) {
+        int lo = 0, hi = npairs;  // last pair with s_pre[p] <= g
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (s_pre[mid] <= g) lo = mid; else hi = mid;
+        }
+        const int p = lo, qb = g - s_pre[p];
+        const int nq = qlist ? qcnt[p] : qn[p];
+        const int nt = tn[p];
+        const uint8_t* Q = qdesc + (size_t)p * q_stride;
+        const uint8_t* T = tdesc + (size_t)p * t_stride;
+        const int qbase = qb * KMX_Q + wave * 64;
+        // ---- B operand: this wave's 64 queries, sign bytes scaled by -64 (the
+        // complemented bits expanded as trains are)
+        kmx_v4i B[4][4];
+#pragma unroll
+        for (int qt = 0; qt < 4; qt++) {
+            const int qpos = qbase + qt * 16 + col;
+            uint4 a = make_uint4(0, 0, 0, 0), b = make_uint4(0, 0, 0, 0);
+            if (qpos < nq) {
+                const int qi = qlist ? qlist[(size_t)p * ql_stride + qpos] : qpos;
+                a = reinterpret_cast<const uint4*>(Q + (size_t)qi * 32)[0];
+                b = reinterpret_cast<const uint4*>(Q + (size_t)qi * 32)[1];
+            }
+            const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const int u = 4 * c + grp;  // 16-bit unit of k-step c, lane group grp
+                uint32_t h = 0;
+#pragma unroll
+                for (int k = 0; k < 16; k++)
+                    if (k == u) h = (k & 1) ? (w[k >> 1] >> 16) : (w[k >> 1] & 0xFFFFu);
+                B[qt][c] = kmx_expand16(~h & 0xFFFFu);
+            }
+        }
+        int k0[4], k1[4];
+#pragma unroll
+        for (int qt = 0; qt < 4; qt++) k0[qt] = k1[qt] = KMX_EMPTY;
+        const int nch = (nt + KMX_T - 1) / KMX_T;
+        uint2 pf = make_uint2(0, 0);
+        auto fetch = [&](int ch) {
+            const int t = ch * KMX_T + st_t;
+            pf = t < nt ? *reinterpret_cast<const uint2*>(T + (size_t)t * 32 + 8 * st_q) : make_uint2(0, 0);
+        };
+        auto stage = [&](int buf) {
+            uint8_t* dst = s_tr[buf] + st_t * 256;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t h = (k < 2 ? pf.x : pf.y) >> (16 * (k & 1)) & 0xFFFFu;
+                const int u = 4 * st_q + k;
+                *reinterpret_cast<kmx_v4i*>(dst + ((u ^ (st_t & 15)) << 4)) = kmx_expand16(h);
+            }
+        };
+        __syncthreads();  // the previous item's last chunk is no longer read
+        if (nch > 0) {
+            fetch(0);
+            stage(0);
+        }
+        __syncthreads();
+        const bool live = qbase < nq;  // wave-uniform: this wave holds queries
+        for (int ch = 0; ch < nch; ch++) {
+            const int buf = ch & 1;
+            if (ch + 1 < nch) fetch(ch + 1);
+            if (live) {
+                const uint8_t* src = s_tr[buf];
+#pragma unroll
+                for (int tt = 0; tt < KMX_T / 16; tt++) {
+                    const int r = tt * 16 + col;  // train row of this lane's A operand
+                    kmx_v4i C;
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const int idx = ch * KMX_T + tt * 16 + 4 * grp + i;
+                        C[i] = idx < nt ? idx : KMX_BIG;
+                    }
+                    kmx_v4i acc[4];
+#pragma unroll
+                    for (int c = 0; c < 4; c++) {
+                        const int u = 4 * c + grp;
+                        const kmx_v4i A = *reinterpret_cast<const kmx_v4i*>(src + r * 256 + ((u ^ col) << 4));
+#pragma unroll
+                        for (int qt = 0; qt < 4; qt++)
+                            acc[qt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B[qt][c], c == 0 ? C : acc[qt], 0, 0, 0);
+                    }
+#pragma unroll
+                    for (int qt = 0; qt < 4; qt++)
+#pragma unroll
+                        for (int i = 0; i < 4; i++) {
+                            k1[qt] = med3_i32(k0[qt], k1[qt], acc[qt][i]);
+                            k0[qt] = min(k0[qt], acc[qt][i]);
+                        }
+                }
+            }
+            if (ch + 1 < nch) stage(buf ^ 1);
+            __syncthreads();
+        }
+        if (!live) continue;
+        // ---- merge the 4 lane groups holding each query, then lane l writes query qbase + l
+#pragma unroll
+        for (int m = 16; m <= 32; m <<= 1)
+#pragma unroll
+            for (int qt = 0; qt < 4; qt++) {
+                const int p0 = __shfl_xor(k0[qt], m), p1 = __shfl_xor(k1[qt], m);
+                const int n1 = min(max(k0[qt], p0), min(k1[qt], p1));
+                k0[qt] = min(k0[qt], p0);
+                k1[qt] = n1;
+            }
+        int a0 = k0[0], a1 = k1[0];
+#pragma unroll
+        for (int qt = 1; qt < 4; qt++)
+            if (grp == qt) a0 = k0[qt], a1 = k1[qt];
+        const int qpos = qbase + lane;
+        if (qpos < nq) {
+            const int qi = qlist ? qlist[(size_t)p * ql_stride + qpos] : qpos;
+            const bool e0 = a0 > (1 << 21), e1 = a1 > (1 << 21);  // no train in the slot
+            const int u0 = a0 + (1 << 20), u1 = a1 + (1 << 20);
+            const size_t o = (size_t)p * out_stride + qi;
+            out_idx[o] = make_int2(e0 ? -1 : (u0 & 8191), e1 ? -1 : (u1 & 8191));
+            out_dist[o] = make_int2(e0 ? 0x7FFFFFFF : (u0 >> 13), e1 ? 0x7FFFFFFF : (u1 >> 13));
+        }
+    }
+}
+
 // ============================================================ libstdc++ std::sort emulation
 // Exactly the GNU introsort (std::__introsort_loop + __final_insertion_sort,
 // threshold 16, median-of-3 pivot, unguarded Hoare partition, heap fallback) on
@@ -925,6 +1113,31 @@ void launch_knn2(hipStream_t st, const uint8_t* q, const int* qn, size_t q_strid
     dim3 g(std::min(nitems, resident));
     hipLaunchKernelGGL(k_knn2, g, dim3(KNN_TH), 0, st, q, qn, q_stride, t, tn, t_stride, idx, dist, out_stride, qlist,
                        qcnt, ql_stride, split_stride, npairs, qblocks, nsplit);
+}
+void launch_knn2_mx(hipStream_t st, const uint8_t* q, const int* qn, size_t q_stride, const uint8_t* t, const int* tn,
+                    size_t t_stride, int2* idx, int2* dist, size_t out_stride, int max_q, int npairs,
+                    const int32_t* qlist, const int* qcnt, size_t ql_stride) {
+    static int resident = 0;  // workgroups of one full round (occupancy x CUs)
+    if (!resident) {
+        int dev = 0, cus = 256, per_cu = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_knn2_mx, 256, 0);
+        resident = std::max(1, per_cu) * cus;
+    }
+    if (npairs <= 0 || max_q <= 0) return;
+    if (npairs > KNN_MAXP) {  // the item prefix is per launch: split larger batches
+        launch_knn2_mx(st, q, qn, q_stride, t, tn, t_stride, idx, dist, out_stride, max_q, KNN_MAXP, qlist, qcnt,
+                       ql_stride);
+        launch_knn2_mx(st, q + KNN_MAXP * q_stride, qn + KNN_MAXP, q_stride, t + KNN_MAXP * t_stride, tn + KNN_MAXP,
+                       t_stride, idx + KNN_MAXP * out_stride, dist + KNN_MAXP * out_stride, out_stride, max_q,
+                       npairs - KNN_MAXP, qlist ? qlist + KNN_MAXP * ql_stride : nullptr,
+                       qcnt ? qcnt + KNN_MAXP : nullptr, ql_stride);
+        return;
+    }
+    const int items = npairs * ((max_q + KMX_Q - 1) / KMX_Q);  // upper bound; the kernel counts the real ones
+    hipLaunchKernelGGL(k_knn2_mx, dim3(std::min(items, resident)), dim3(256), 0, st, q, qn, q_stride, t, tn, t_stride,
+                       idx, dist, out_stride, qlist, qcnt, ql_stride, npairs);
 }
 void launch_vo_lm(hipStream_t st, const float* xyz, const int* nkp, int kp_cap, int slot0, float th_depth_m,
                   uint32_t* lm_bits, int lm_words, int32_t* qlist, int* qcnt, int npairs) {

@@ -137,6 +137,9 @@ struct odo_ctx {
     int* qcnt[NSETS] = {};
     int lm_words = 0;
     int knn_split = 2;  // kNN-2 train splits per query block (ODO_KNN_SPLIT): more waves for short query lists
+    // kNN-2 on the matrix cores (k_knn2_mx, exact int8 sign-vector products;
+    // ODO_KNN_MFMA=0 selects the VALU xor/popcount kernel k_knn2)
+    bool knn_mx = true;
     uint64_t* sort_scratch = nullptr;
     double* latch = nullptr;
     void* rscr[NSETS] = {};  // RANSAC scratch per frame set
@@ -461,6 +464,10 @@ static int build_geometry(odo_ctx* c) {
     if (c->adaptive) {
         int e;
         if ((e = build_adaptive_geometry(c))) return e;
+        // the ADAPTIVE keypoint capacity (cells x per-cell maximum) may exceed
+        // the cap checked above: the LDS landmark bit sets of k_vo_lm /
+        // k_pair_match and the 13-bit train index of the kNN-2 keys hold 8192
+        if (c->kp_cap > 8192) return fail(ODO_ERR_ARG, "ADAPTIVE max_total_keypoints too large (kp cap 8192)");
     }
     c->match_cap = c->kp_cap;
     c->mask_words = (c->match_cap + 31) / 32;
@@ -569,6 +576,8 @@ static int alloc_buffers(odo_ctx* c) {
     }
     c->lm_words = (c->kp_cap + 31) / 32;
     if (const char* ks = getenv("ODO_KNN_SPLIT")) c->knn_split = std::min(8, std::max(1, atoi(ks)));
+    if (const char* km = getenv("ODO_KNN_MFMA")) c->knn_mx = atoi(km) != 0;
+    if (c->knn_mx) c->knn_split = 1;  // one top-2 slot per query
     for (int i = 0; i < NSETS; i++) {
         if ((e = dalloc(&c->knn_idx[i], (size_t)c->knn_split * B * c->kp_cap))) return e;
         if ((e = dalloc(&c->knn_dist[i], (size_t)c->knn_split * B * c->kp_cap))) return e;
@@ -1087,9 +1096,14 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
             }
             HIPCHK(hipEventRecord(c->kt0[kt], kst));
         }
-        if (!(c->skip & 8))
-            launch_knn2(kst, desc, nkp, KC * 32, desc + KC * 32, nkp + 1, KC * 32, c->knn_idx[s], c->knn_dist[s], KC,
-                        c->kp_cap, n, c->qlist[s], c->qcnt[s], KC, c->knn_split, (size_t)c->maxb * KC);
+        if (!(c->skip & 8)) {
+            if (c->knn_mx)
+                launch_knn2_mx(kst, desc, nkp, KC * 32, desc + KC * 32, nkp + 1, KC * 32, c->knn_idx[s], c->knn_dist[s],
+                               KC, c->kp_cap, n, c->qlist[s], c->qcnt[s], KC);
+            else
+                launch_knn2(kst, desc, nkp, KC * 32, desc + KC * 32, nkp + 1, KC * 32, c->knn_idx[s], c->knn_dist[s],
+                            KC, c->kp_cap, n, c->qlist[s], c->qcnt[s], KC, c->knn_split, (size_t)c->maxb * KC);
+        }
         if (kt >= 0) {
             HIPCHK(hipEventRecord(c->kt1[kt], kst));
             c->kt_next = (kt + 1) % odo_ctx::KT_RING;
@@ -1580,8 +1594,12 @@ int odo_knn2_hamming(odo_ctx* c, const uint8_t* q, int nq, const uint8_t* t, int
     HIPCHK(hipMemcpyAsync(dq.p, q, (size_t)nq * 32, hipMemcpyHostToDevice, st));
     if (nt) HIPCHK(hipMemcpyAsync(dt.p, t, (size_t)nt * 32, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(dn.p, cnt, sizeof(cnt), hipMemcpyHostToDevice, st));
-    launch_knn2(st, dq.as<uint8_t>(), dn.as<int>(), 0, dt.as<uint8_t>(), dn.as<int>() + 1, 0, di.as<int2>(),
-                dd.as<int2>(), 0, nq, 1);
+    if (c->knn_mx && nt <= 8192)  // the packed key holds a 13-bit train index
+        launch_knn2_mx(st, dq.as<uint8_t>(), dn.as<int>(), 0, dt.as<uint8_t>(), dn.as<int>() + 1, 0, di.as<int2>(),
+                       dd.as<int2>(), 0, nq, 1);
+    else
+        launch_knn2(st, dq.as<uint8_t>(), dn.as<int>(), 0, dt.as<uint8_t>(), dn.as<int>() + 1, 0, di.as<int2>(),
+                    dd.as<int2>(), 0, nq, 1);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(idx, di.p, (size_t)nq * 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(dist, dd.p, (size_t)nq * 8, hipMemcpyDeviceToHost, st));

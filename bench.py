@@ -28,6 +28,7 @@ PKG_DIR = os.path.join(ROOT, "adaptive-rgbd-localization-mappig_amd")
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP64_PEAK_TFLOPS = 78.6      # MI355X_MICROARCH.md: FP64 vector spec
+I8_MFMA_PEAK_TOPS = 5033.2   # dense I8 MFMA: 2x the BF16 rate per clock (MI355X_MICROARCH.md), 256 CU x 2.4 GHz
 # the algorithmic Hamming work is 16 int32 lane-ops per (query,
 # train) comparison (8 v_xor_b32 + 8 v_bcnt_u32_b32 over the 256-bit
 # descriptors; the top-2 update is excluded). k_knn2 issues 19 (+ key, min, med3).
@@ -365,15 +366,32 @@ def main():
             # scaled per pair when this run's batch differs from the profiled one
             traffic = tr.get("hbm_bytes_per_launch") if tr.get("batch") == B else \
                 (tr["hbm_bytes_per_pair"] * B if "hbm_bytes_per_pair" in tr else None)
-        roofline = {"bound": "valu", "achieved": round(ach, 3), "peak": round(peak, 2),
-                    "unit": "Top/s", "frac": round(ach / peak, 4), "traffic": traffic,
-                    "kernel": "k_knn2", "kernel_ms": round(knn_ms, 4), "launches": knn_launches,
-                    "work": f"{cmp} descriptor comparisons x {KNN_OPS_PER_CMP} int32 lane-ops (SURVEY 8(d))",
-                    "peak_source": "measured v_xor_b32 + v_bcnt_u32_b32 rate, profiles/r02_ubench_peak.jsonl",
-                    "issued_ops_per_cmp": KNN_ISSUED_OPS_PER_CMP,
-                    # algorithmic HBM bytes: every descriptor read once, 16 B of top-2 out per query
-                    "hbm_gbs": round(sum(32 * int(nq[i]) + 32 * nkp[i] + 16 * int(nq[i]) for i in range(B)) /
-                                     (knn_ms * 1e-3) / 1e9, 1)}
+        hbm_alg = sum(32 * int(nq[i]) + 32 * nkp[i] + 16 * int(nq[i]) for i in range(B))
+        if os.environ.get("ODO_KNN_MFMA", "1") != "0":
+            # k_knn2_mx: the exact int8 sign-vector formulation on the matrix
+            # cores, 256 MACs = 512 int8 ops per comparison, against the dense
+            # I8 MFMA peak (2x BF16 per clock, MI355X_MICROARCH.md)
+            mops = 512.0 * cmp
+            mach = mops / (knn_ms * 1e-3) / 1e12
+            roofline = {"bound": "mfma", "achieved": round(mach, 2), "peak": I8_MFMA_PEAK_TOPS, "unit": "Top/s",
+                        "frac": round(mach / I8_MFMA_PEAK_TOPS, 4), "traffic": None,
+                        "kernel": "k_knn2_mx", "kernel_ms": round(knn_ms, 4), "launches": knn_launches,
+                        "work": f"{cmp} descriptor comparisons x 512 int8 ops (v_mfma_i32_16x16x64_i8, K = 256)",
+                        "measured_peak": round(peaks["mfma_i32_16x16x64_i8"], 1),
+                        "equiv_valu_16op": {"achieved": round(ach, 3), "peak": round(peak, 2), "unit": "Top/s",
+                                            "frac": round(ach / peak, 4),
+                                            "note": "SURVEY 8(d) 16 lane-ops per comparison vs the measured "
+                                                    "xor+bcnt VALU rate"},
+                        "hbm_gbs": round(hbm_alg / (knn_ms * 1e-3) / 1e9, 1)}
+        else:
+            roofline = {"bound": "valu", "achieved": round(ach, 3), "peak": round(peak, 2),
+                        "unit": "Top/s", "frac": round(ach / peak, 4), "traffic": traffic,
+                        "kernel": "k_knn2", "kernel_ms": round(knn_ms, 4), "launches": knn_launches,
+                        "work": f"{cmp} descriptor comparisons x {KNN_OPS_PER_CMP} int32 lane-ops (SURVEY 8(d))",
+                        "peak_source": "measured v_xor_b32 + v_bcnt_u32_b32 rate, profiles/r02_ubench_peak.jsonl",
+                        "issued_ops_per_cmp": KNN_ISSUED_OPS_PER_CMP,
+                        # algorithmic HBM bytes: every descriptor read once, 16 B of top-2 out per query
+                        "hbm_gbs": round(hbm_alg / (knn_ms * 1e-3) / 1e9, 1)}
 
     # the other SURVEY §8(d) legs, from the per-stage (one stream, events
     # between stages) times of the untimed timing step
