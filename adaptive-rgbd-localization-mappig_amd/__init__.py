@@ -15,7 +15,7 @@ from . import _abi
 from ._abi import (DETECTOR_ADAPTIVE_FAST, DETECTOR_ORB_SLAM2, AdaptiveParams, Calib, Config, DMatch,
                    DMATCH_DTYPE, KP_DTYPE, OrbParams, PAIR_DTYPE, PairResult, RansacParams, Rng, check, load, ptr)
 
-__all__ = ["Odometry", "HostFrames", "default_config", "load", "KP_DTYPE", "DMATCH_DTYPE", "PAIR_DTYPE", "rng_stream",
+__all__ = ["Odometry", "HostFrames", "PinnedResults", "default_config", "load", "KP_DTYPE", "DMATCH_DTYPE", "PAIR_DTYPE", "rng_stream",
            "kabsch", "Calib", "OrbParams", "RansacParams", "Config", "AdaptiveParams", "DETECTOR_ORB_SLAM2",
            "DETECTOR_ADAPTIVE_FAST"]
 
@@ -69,6 +69,35 @@ class HostFrames:
             pass
 
 
+class PinnedResults:
+    """Page-locked ring of result records for Odometry.track_batch_async:
+    `rows` batches of `n` records each (a numpy PAIR_DTYPE view per row)."""
+
+    def __init__(self, rows: int, n: int):
+        self.lib = load()
+        self.rows, self.n = rows, n
+        self._p = self.lib.odo_host_alloc(rows * n * PAIR_DTYPE.itemsize)
+        if not self._p:
+            raise MemoryError("odo_host_alloc failed: " + self.lib.odo_last_error().decode())
+        raw = np.ctypeslib.as_array(C.cast(self._p, C.POINTER(C.c_uint8)), (rows * n * PAIR_DTYPE.itemsize,))
+        self.all = raw.view(PAIR_DTYPE).reshape(rows, n)
+
+    def row_ptr(self, r: int) -> int:
+        return self._p + (r % self.rows) * self.n * PAIR_DTYPE.itemsize
+
+    def close(self):
+        if getattr(self, "_p", None):
+            self.lib.odo_host_free(self._p)
+            self._p = None
+        self.all = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Odometry:
     """One context = one HIP stream + HBM scratch + previous-frame/latch state."""
 
@@ -113,6 +142,17 @@ class Odometry:
         check(self.lib.odo_track_batch(self.h, C.c_void_p(bgr_ptr), C.c_void_p(depth_ptr), n,
                                        ptr(out) if want_results else None))
         return out
+
+    def track_batch_async(self, bgr_ptr: int, depth_ptr: int, n: int, results: PinnedResults, row: int):
+        """Device-resident inputs; the n result records land in results.all[row]
+        after the next synchronize() (no host sync here)."""
+        check(self.lib.odo_track_batch_async(self.h, C.c_void_p(bgr_ptr), C.c_void_p(depth_ptr), n,
+                                             C.c_void_p(results.row_ptr(row))))
+
+    def seek(self, pair_index: int, keep_prev: bool = False):
+        """Next batch's pair p gets global pair index pair_index + p; without
+        keep_prev its first frame starts a segment (a halo frame, no pair)."""
+        check(self.lib.odo_seek(self.h, int(pair_index), 1 if keep_prev else 0))
 
     def track_batch_host(self, bgr, depth=None, want_results=True, n=None):
         """Host inputs: numpy arrays (pageable) or a HostFrames (pinned; then

@@ -1026,6 +1026,17 @@ static int run_pairs(odo_ctx* c, int set, int n) {
     return ODO_OK;
 }
 
+// n_matches / n_queries of the batch's result records (0 for a pair without a
+// previous frame), on the device so the records can be copied out asynchronously
+__global__ void k_res_patch(odo_pair_result* __restrict__ res, const int* __restrict__ n_matches,
+                            const int* __restrict__ qcnt, int n, int first_valid) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const bool v = i > 0 || first_valid;
+    res[i].n_matches = v ? n_matches[i] : 0;
+    res[i].n_queries = v ? qcnt[i] : 0;
+}
+
 static int finish_batch(odo_ctx* c, int set, int n, odo_pair_result* h_results) {
     if (!h_results) return ODO_OK;
     int e;
@@ -1169,6 +1180,41 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
     c->pair_counter += (uint64_t)n;
     c->batch_counter++;
     if ((e = finish_batch(c, s, n, h_results))) return e;
+    return ODO_OK;
+}
+
+// odo_track_batch with the result records copied into page-locked host memory
+// asynchronously (on the batch's pair stream, after its PnP): no host sync, so
+// batches keep streaming; the records are valid after odo_synchronize().
+int odo_track_batch_async(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, int n, odo_pair_result* h_results) {
+    if (!h_results) return fail(ODO_ERR_ARG, "null results");
+    const int first_valid = c && c->has_prev ? 1 : 0;
+    int e;
+    if ((e = odo_track_batch(c, d_bgr, d_depth, n, nullptr))) return e;
+    const int s = c->view_set;
+    auto& P = c->pb[s];
+    hipStream_t st = c->cur_p ? c->cur_p : c->pstream;  // the batch's pair stream (its PnP ran there last)
+    HIPCHK(hipStreamWaitEvent(st, c->ev_pa[s], 0));
+    HIPCHK(hipStreamWaitEvent(st, c->ev_pb[s], 0));
+    hipLaunchKernelGGL(k_res_patch, dim3((n + 255) / 256), dim3(256), 0, st, P.res, P.n_matches, c->qcnt[s], n,
+                       first_valid);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(h_results, P.res, (size_t)n * sizeof(odo_pair_result), hipMemcpyDeviceToHost, st));
+    // the batch that next reuses set s waits for these events: include the copy
+    HIPCHK(hipEventRecord(c->ev_pa[s], st));
+    HIPCHK(hipEventRecord(c->ev_pb[s], st));
+    return ODO_OK;
+}
+
+// Position the sequence (SURVEY §8(e) frames mode): the next batch's pair p
+// gets the global pair index pair_index + p (its per-pair RANSAC seed); with
+// keep_prev = 0 the next batch's first frame starts a sequence segment (no
+// pair with the previous call's last frame: a rank's halo frame). The latch
+// and the ADAPTIVE thresholds are kept.
+int odo_seek(odo_ctx* c, uint64_t pair_index, int keep_prev) {
+    if (!c) return fail(ODO_ERR_ARG, "null ctx");
+    c->pair_counter = pair_index;
+    if (!keep_prev) c->has_prev = false;
     return ODO_OK;
 }
 

@@ -257,6 +257,9 @@ def main():
     ap.add_argument("--host-steps", type=int, default=20, help="steps of the from-host leg (0: skip it)")
     ap.add_argument("--no-kernel-timing", action="store_true", help="no events around the kNN-2 launches")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--shard", choices=["sequence", "independent"], default="sequence",
+                    help="N > 1: 'sequence' = SURVEY 8(e) frames mode (one sequence, per-rank chunks + 1-frame "
+                         "halo, latch broadcast, pose stitch); 'independent' = one sequence per rank")
     ap.add_argument("--detector", choices=["orb_slam2", "adaptive"], default="orb_slam2",
                     help="orb_slam2: ORBextractor (the metric's config); adaptive: Extractor(FAST, ORB, ADAPTIVE)")
     args = ap.parse_args()
@@ -274,71 +277,133 @@ def main():
     pkg = load_pkg()
     synth = load_synth()
     B, W, H = args.batch, args.width, args.height
-    scene_seed, pair_seed = rank_seeds(rank)
+    # N > 1: SURVEY §8(e) frames mode by default: ONE sequence, each step's
+    # B x N frames split into per-rank chunks with a one-frame halo, the latch
+    # broadcast from rank 0, the poses stitched with an all_gather ("sequence");
+    # "independent" gives every rank its own sequence (no exchange at all)
+    seq_mode = world > 1 and args.shard == "sequence"
+    scene_seed, pair_seed = rank_seeds(0 if seq_mode else rank)
     # a closed loop of --seq-len distinct frames (fixed inter-frame motion);
     # a batch of B frames walks it cyclically, so every pair is a genuine
     # consecutive pair whatever B is
     L = min(args.seq_len, B)
     if B % L:
         raise SystemExit(f"--batch {B} must be a multiple of --seq-len {L} (pair 0 links frame B-1 to frame 0)")
-    bgr, dep, gt_poses = synth.make_sequence(L, W, H, seed=scene_seed, closed_loop=True)
-    if B != L:
-        bgr, dep = bgr[np.arange(B) % L], dep[np.arange(B) % L]
-    d_bgr = torch.from_numpy(bgr).to("cuda")
-    d_dep = torch.from_numpy(dep.view(np.int16)).to("cuda")
+    bgr_loop, dep_loop, gt_poses = synth.make_sequence(L, W, H, seed=scene_seed, closed_loop=True)
+    bgr, dep = bgr_loop[np.arange(B) % L], dep_loop[np.arange(B) % L]
     adaptive = args.detector == "adaptive"
     if adaptive:
         args.nfeatures = 1000  # Extract's retainBest(nFeatures), common.h:77
-    cfg = pkg.default_config(W, H, B, nfeatures=args.nfeatures, iterations=args.iters, seed=pair_seed,
+        if seq_mode:
+            raise SystemExit("ADAPTIVE thresholds carry from frame to frame: not frame-shardable (--shard independent)")
+    fb = (W * H * 3, W * H * 2)
+    if seq_mode:
+        # every chunk starts at a multiple of L: its halo is loop frame L - 1
+        hb = np.concatenate([bgr_loop[L - 1:], bgr])
+        hd = np.concatenate([dep_loop[L - 1:], dep])
+        d_bgr = torch.from_numpy(hb).to("cuda")
+        d_dep = torch.from_numpy(hd.view(np.int16)).to("cuda")
+    else:
+        d_bgr = torch.from_numpy(bgr).to("cuda")
+        d_dep = torch.from_numpy(dep.view(np.int16)).to("cuda")
+    cfg = pkg.default_config(W, H, B + 1 if seq_mode else B, nfeatures=args.nfeatures, iterations=args.iters,
+                             seed=pair_seed,
                              detector=pkg.DETECTOR_ADAPTIVE_FAST if adaptive else pkg.DETECTOR_ORB_SLAM2)
     odo = pkg.Odometry(cfg, device=local_rank)
     torch.cuda.synchronize()
+    from importlib import import_module
+    tj = import_module("arlm_amd.trajectory")
 
-    # untimed: one batch with results for the sanity summary
-    res = odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=True)
-    for _ in range(args.warmup):
-        odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=False)
-    # untimed: a batch whose pair 0 links to the previous batch, as in the timed
-    # steps, for the kNN-2 query counts (F1 keypoints holding a VO landmark)
-    res_q = odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=True)
-    odo.synchronize()
-    torch.cuda.synchronize()
+    if seq_mode:
+        fsm = import_module("arlm_amd.frames_shard")
+        shard = fsm.FramesShard(odo, dist, rank, world, B * world)
+        # the DepthCovariance latch of global pair 1 (loop frames 0, 1), broadcast
+        shard.prime_latch(d_bgr.data_ptr() + fb[0], d_dep.data_ptr() + fb[1])
+        nun = args.warmup + 2
+        ring = pkg.PinnedResults(max(args.steps, nun), B + 1)
 
-    if world > 1:
+        def run_step(k, row=None):
+            return shard.track_step(k, d_bgr.data_ptr(), d_dep.data_ptr(), fb,
+                                    results=ring if row is not None else None, row=row or 0)
+
+        for k in range(nun):  # untimed: step 0, warm-up, one more for the statistics
+            run_step(k, k)
+        odo.synchronize()
+        recs = [ring.all[k][:fsm.batch_of(k, B * world, rank, world)[1]].copy() for k in range(nun)]
+        G = shard.stitch(recs, list(range(nun)), G_start=np.linalg.inv(gt_poses[0]))
+        # ATE over rank 0's first loop (global frames 0 .. L-1 of step 0)
+        ate_mm = 1000.0 * tj.ate_rmse(tj.camera_centres(G[0][:L]), gt_poses[:L, :3, 3]) if rank == 0 else None
+        res_q = recs[-1][1:]  # a halo step: B genuine pairs, record p+1 = pair (frame p, frame p+1)
+        pair_frame0 = 1       # batch frame of record 0 of res_q
+        torch.cuda.synchronize()
         dist.barrier()
-    # Hamming-match (kNN-2) launches are bracketed by HIP events on the stream
-    # that runs them (a pair stream by default) inside the timed region (odo
-    # timing mode 2)
-    if not args.no_kernel_timing:
-        odo.set_timing(None, mode=2)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=False)
-    submit = time.perf_counter() - t0  # host time to queue the K steps (asynchronous)
-    odo.synchronize()
-    torch.cuda.synchronize()
-    if world > 1:
+        if not args.no_kernel_timing:
+            odo.set_timing(None, mode=2)
+        t0 = time.perf_counter()
+        for s_ in range(args.steps):
+            run_step(nun + s_, s_)
+        submit = time.perf_counter() - t0
+        odo.synchronize()
+        # the cross-rank pose chain of the timed steps (one all_gather)
+        shard.stitch([ring.all[s_][:fsm.batch_of(nun + s_, B * world, rank, world)[1]] for s_ in range(args.steps)],
+                     [nun + s_ for s_ in range(args.steps)])
+        torch.cuda.synchronize()
         dist.barrier()
-    elapsed = max_over_ranks(time.perf_counter() - t0, dist, world)
-    knn_ms, knn_launches = odo.kernel_timing() if not args.no_kernel_timing else (None, 0)
+        elapsed = max_over_ranks(time.perf_counter() - t0, dist, world)
+        knn_ms, knn_launches = odo.kernel_timing() if not args.no_kernel_timing else (None, 0)
+        odo.set_timing(True)
+        run_step(nun + args.steps)
+        odo.synchronize()
+        timings = odo.timings()
+        odo.set_timing(False)
+        ring.close()
+    else:
+        # untimed: one batch with results for the sanity summary
+        res = odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=True)
+        for _ in range(args.warmup):
+            odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=False)
+        # untimed: a batch whose pair 0 links to the previous batch, as in the timed
+        # steps, for the kNN-2 query counts (F1 keypoints holding a VO landmark)
+        res_q = odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=True)
+        pair_frame0 = 0
+        odo.synchronize()
+        torch.cuda.synchronize()
+        # quality sanity: the untimed first batch's chained poses against the
+        # sequence's ground truth (absolute trajectory error, TUM definition)
+        Tcw = tj.chain_poses(res[:L], np.linalg.inv(gt_poses[0]).astype(np.float32))
+        ate_mm = 1000.0 * tj.ate_rmse(tj.camera_centres(Tcw), gt_poses[:L, :3, 3])
 
-    # per-stage times: one extra (untimed) step with the stage events on
-    odo.set_timing(True)
-    odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=False)
-    odo.synchronize()
-    timings = odo.timings()
-    odo.set_timing(False)
+        if world > 1:
+            dist.barrier()
+        # Hamming-match (kNN-2) launches are bracketed by HIP events on the stream
+        # that runs them (a pair stream by default) inside the timed region (odo
+        # timing mode 2)
+        if not args.no_kernel_timing:
+            odo.set_timing(None, mode=2)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=False)
+        submit = time.perf_counter() - t0  # host time to queue the K steps (asynchronous)
+        odo.synchronize()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = max_over_ranks(time.perf_counter() - t0, dist, world)
+        knn_ms, knn_launches = odo.kernel_timing() if not args.no_kernel_timing else (None, 0)
+
+        # per-stage times: one extra (untimed) step with the stage events on
+        odo.set_timing(True)
+        odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=False)
+        odo.synchronize()
+        timings = odo.timings()
+        odo.set_timing(False)
     value = job_throughput(B, args.steps, world, elapsed)
     ms_per_step = elapsed / args.steps * 1e3
 
-    nkp = [len(odo.frame(i)["kps"]) for i in range(B)]
-    # quality sanity: the untimed first batch's chained poses against the
-    # sequence's ground truth (absolute trajectory error, TUM definition)
-    from importlib import import_module
-    tj = import_module("arlm_amd.trajectory")
-    Tcw = tj.chain_poses(res[:L], np.linalg.inv(gt_poses[0]).astype(np.float32))
-    ate_mm = 1000.0 * tj.ate_rmse(tj.camera_centres(Tcw), gt_poses[:L, :3, 3])
+    # keypoints of the frames the statistics' pairs match against (every batch
+    # holds the same cycled frames): pair record i's train frame
+    nkp = [len(odo.frame(pair_frame0 + i)["kps"]) for i in range(B)]
     nkp_mean = float(np.mean(nkp))
     peaks = measured_peaks()
     # Roofline of the Hamming-match kernel (k_knn2), the kernel the north star
@@ -421,7 +486,7 @@ def main():
         legs["pnp"] = {"bound": "latency", "ms": round(timings["pnp"], 4)}
 
     from_host = None
-    if args.host_steps > 0:
+    if args.host_steps > 0 and not seq_mode:
         from_host = host_leg(pkg, odo, bgr, dep, B, W, H, args.host_steps, 2, world, dist)
 
     cpu = None
@@ -440,7 +505,7 @@ def main():
                                        f"(extraction and pairs), median of 3 passes"}}
 
     if rank == 0:
-        ok = res[1:]
+        ok = res_q
         out = {
             "metric": "frames/sec (extract+match+RANSAC-PnP) @640x480, 2000 kp" if not adaptive else
                       "frames/sec (ADAPTIVE FAST grid + ORB, match, RANSAC-PnP) @640x480, <=1000 kp",
@@ -459,7 +524,8 @@ def main():
                                     if not adaptive else
                                     f"fr1/desk proxy {W}x{H}, ADAPTIVE 3x3 FAST grid + ORB (<=1000 kp), "
                                     f"RANSAC {args.iters}"),
-                       "frames_per_step": B, "global_batch": B * world, "parallelism": f"frames x{world}",
+                       "frames_per_step": B, "global_batch": B * world, "parallelism": (f"sequence chunks x{world} (+1-frame halo, latch broadcast, pose stitch)"
+                                       if seq_mode else f"frames x{world}"),
                        "mean_keypoints": round(nkp_mean, 1),
                        "mean_knn_queries": round(float(np.mean(res_q["n_queries"])), 1),
                        "mean_matches": round(float(np.mean(ok["n_matches"])), 1),

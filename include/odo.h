@@ -84,6 +84,17 @@ int odo_track_batch(odo_ctx* ctx, const uint8_t* d_bgr, const uint16_t* d_depth,
  * h_results non-null it waits for the batch and fills the results. */
 int odo_track_batch_host(odo_ctx* ctx, const uint8_t* bgr, const uint16_t* depth, int n,
                          odo_pair_result* h_results);
+/* odo_track_batch with the n result records copied into PAGE-LOCKED host memory
+ * (odo_host_alloc) asynchronously after the batch's PnP: no host sync, the
+ * records are valid after odo_synchronize(). Used to stream results. */
+int odo_track_batch_async(odo_ctx* ctx, const uint8_t* d_bgr, const uint16_t* d_depth, int n,
+                          odo_pair_result* h_results);
+/* Sequence position (SURVEY §8(e) frames mode, replaces the implicit global
+ * frame counter of Tracking): the next batch's pair p uses global pair index
+ * pair_index + p for its RANSAC seed; keep_prev = 0 makes the next batch's
+ * first frame a segment start (a rank's halo frame: extracted, no pair with
+ * the previous call). The DepthCovariance latch and ADAPTIVE thresholds stay. */
+int odo_seek(odo_ctx* ctx, uint64_t pair_index, int keep_prev);
 /* Page-locked host memory for input frames (decode straight into it so the
  * upload needs no extra host copy). NULL on failure; free with odo_host_free. */
 void* odo_host_alloc(size_t bytes);
