@@ -199,7 +199,7 @@ def cpu_baseline(bgr, dep, nfeat, iters, n_frames, reps, adaptive=False, threads
             "all_cores": {"fps": nf_all / ta, "threads": nthr, "frames": nf_all}}
 
 
-def host_leg(pkg, odo, bgr_b, dep_b, B, W, H, steps, warmup, world, dist):
+def host_leg(pkg, odo, bgr_b, dep_b, B, W, H, steps, warmup, world, dist, coll_dev="cuda"):
     """Frames/s from BGR8 + depth16 in (pinned) host memory (SURVEY §8(d) unit):
     odo_track_batch_host uploads each batch on the copy stream into a staging
     buffer while the compute of the previous batches runs."""
@@ -218,7 +218,7 @@ def host_leg(pkg, odo, bgr_b, dep_b, B, W, H, steps, warmup, world, dist):
     odo.synchronize()
     if world > 1:
         dist.barrier()
-    dt = max_over_ranks(time.perf_counter() - t0, dist, world)
+    dt = max_over_ranks(time.perf_counter() - t0, dist, world, device=coll_dev)
     nbytes = hf.bgr.nbytes + hf.depth.nbytes
     hf.close()
     # raw pinned host -> HBM rate of the same bytes, no compute (the PCIe bound)
@@ -240,6 +240,77 @@ def host_leg(pkg, odo, bgr_b, dep_b, B, W, H, steps, warmup, world, dist):
             "inputs": "pinned host buffers (odo_host_alloc), one upload per batch on the copy stream"}
 
 
+class LocalExchange:
+    """hyp_shard.Exchange for a single rank (no process group)."""
+    world, rank = 1, 0
+
+    def all_gather(self, local, block):
+        buf = np.zeros(block, np.uint8)
+        raw = np.frombuffer(np.ascontiguousarray(local).tobytes(), np.uint8)
+        buf[:raw.size] = raw
+        return [buf]
+
+    def broadcast(self, buf, src):
+        return np.ascontiguousarray(buf).view(np.uint8).copy()
+
+
+def hyp_mode(args, rank, world, local_rank, dist):
+    """SURVEY §8(e) hypotheses mode on config 3: one hard pair's RANSAC
+    (H = 4096) with its hypotheses sharded over the ranks (hyp_shard.py:
+    per-rank odo_ransac_hyps, all_gather of the 64-B summaries, the ordered
+    fold, broadcast of the winner). A latency metric: ms per pair."""
+    import torch
+    pkg = load_pkg()
+    synth = load_synth()
+    from importlib import import_module
+    hs = import_module("arlm_amd.hyp_shard")
+    fr2 = dict(fx=520.9, fy=521.0, cx=325.1, cy=249.7)  # common.h:47-50 (FR1 distortion kept, App. B.16)
+    bgr, dep, _ = synth.make_sequence(2, 640, 480, intrinsics=fr2, seed=0x5EED0003)
+    H_ = args.iters if args.iters != 500 else 4096
+    cfg = pkg.default_config(640, 480, 2, nfeatures=4000, iterations=H_, seed=0x5EED0003, calib=fr2)
+    odo = pkg.Odometry(cfg, device=local_rank % max(1, torch.cuda.device_count()))
+    odo.track_batch_host(bgr, dep)
+    m = odo.pair(1)["matches"].copy()
+    x1, x2 = odo.frame(0)["xyz"], odo.frame(1)["xyz"]
+    # a hard pair: half the matches re-targeted at random keypoints, so the
+    # > 80 % early exit never fires and RANSAC visits many hypotheses
+    rs = np.random.default_rng(3)
+    sel = rs.random(m.size) < args.hyp_outliers
+    m["trainIdx"][sel] = rs.integers(0, x2.shape[0], int(sel.sum()))
+    params = pkg.RansacParams(H_, 20, 3.0, 4, 1)
+    backend = dist.get_backend() if world > 1 else None
+    ex = hs.Exchange(dist, world, rank, device="cuda" if backend == "nccl" else "cpu") if world > 1 else LocalExchange()
+
+    def once():
+        rng = pkg.Rng()
+        pkg.load().odo_rng_seed(pkg.ptr(rng), 12345)
+        return hs.sharded_ransac(odo, ex, m, x1, x2, params, rng, float("nan"))
+
+    for _ in range(2):
+        out = once()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = once()
+    if world > 1:
+        dist.barrier()
+    dt = max_over_ranks(time.perf_counter() - t0, dist, world, device="cuda" if backend == "nccl" else "cpu")
+    T, rmse, inl, ok, visited, _ = out
+    if rank == 0:
+        print(json.dumps({
+            "metric": f"RANSAC latency of one hard pair, hypotheses sharded (cfg3 fr2/desk proxy, H={H_})",
+            "value": round(dt / args.steps * 1e3, 4), "unit": "ms/pair", "n_gpus": world, "steps": args.steps,
+            "higher_is_better": False, "scaling": "strong",
+            "config": {"workload": f"cfg3 640x480 FR2 K + FR1 distortion, 4000 kp, H={H_}, "
+                                   f"{int(100 * args.hyp_outliers)}% of the matches re-targeted",
+                       "n_matches": int(m.size), "visited": int(visited), "n_inliers": int(len(inl)),
+                       "ok": int(ok), "backend": backend or "single rank",
+                       "exchange": "all_gather of 64-B hypothesis summaries + ordered fold + owner broadcast"}}),
+              flush=True)
+    odo.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -257,6 +328,11 @@ def main():
     ap.add_argument("--host-steps", type=int, default=20, help="steps of the from-host leg (0: skip it)")
     ap.add_argument("--no-kernel-timing", action="store_true", help="no events around the kNN-2 launches")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mode", choices=["track", "hyp"], default="track",
+                    help="track: the frames/s metric; hyp: SURVEY 8(e) hypotheses mode latency (cfg3, H=4096)")
+    ap.add_argument("--hyp-outliers", type=float, default=0.5, help="hyp mode: fraction of matches re-targeted")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="process group backend for N > 1 (gloo: several ranks sharing one GPU)")
     ap.add_argument("--shard", choices=["sequence", "independent"], default="sequence",
                     help="N > 1: 'sequence' = SURVEY 8(e) frames mode (one sequence, per-rank chunks + 1-frame "
                          "halo, latch broadcast, pose stitch); 'independent' = one sequence per rank")
@@ -269,10 +345,18 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
-    torch.cuda.set_device(local_rank)
+    torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+    if args.mode == "hyp":
+        hyp_mode(args, rank, world, local_rank, dist)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     pkg = load_pkg()
     synth = load_synth()
@@ -309,14 +393,15 @@ def main():
     cfg = pkg.default_config(W, H, B + 1 if seq_mode else B, nfeatures=args.nfeatures, iterations=args.iters,
                              seed=pair_seed,
                              detector=pkg.DETECTOR_ADAPTIVE_FAST if adaptive else pkg.DETECTOR_ORB_SLAM2)
-    odo = pkg.Odometry(cfg, device=local_rank)
+    odo = pkg.Odometry(cfg, device=local_rank % max(1, torch.cuda.device_count()))
     torch.cuda.synchronize()
+    coll_dev = "cuda" if args.backend == "nccl" else "cpu"  # where the exchanges' tensors live
     from importlib import import_module
     tj = import_module("arlm_amd.trajectory")
 
     if seq_mode:
         fsm = import_module("arlm_amd.frames_shard")
-        shard = fsm.FramesShard(odo, dist, rank, world, B * world)
+        shard = fsm.FramesShard(odo, dist, rank, world, B * world, device=coll_dev)
         # the DepthCovariance latch of global pair 1 (loop frames 0, 1), broadcast
         shard.prime_latch(d_bgr.data_ptr() + fb[0], d_dep.data_ptr() + fb[1])
         nun = args.warmup + 2
@@ -349,7 +434,7 @@ def main():
                      [nun + s_ for s_ in range(args.steps)])
         torch.cuda.synchronize()
         dist.barrier()
-        elapsed = max_over_ranks(time.perf_counter() - t0, dist, world)
+        elapsed = max_over_ranks(time.perf_counter() - t0, dist, world, device=coll_dev)
         knn_ms, knn_launches = odo.kernel_timing() if not args.no_kernel_timing else (None, 0)
         odo.set_timing(True)
         run_step(nun + args.steps)
@@ -389,7 +474,7 @@ def main():
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
-        elapsed = max_over_ranks(time.perf_counter() - t0, dist, world)
+        elapsed = max_over_ranks(time.perf_counter() - t0, dist, world, device=coll_dev)
         knn_ms, knn_launches = odo.kernel_timing() if not args.no_kernel_timing else (None, 0)
 
         # per-stage times: one extra (untimed) step with the stage events on
@@ -487,7 +572,7 @@ def main():
 
     from_host = None
     if args.host_steps > 0 and not seq_mode:
-        from_host = host_leg(pkg, odo, bgr, dep, B, W, H, args.host_steps, 2, world, dist)
+        from_host = host_leg(pkg, odo, bgr, dep, B, W, H, args.host_steps, 2, world, dist, coll_dev)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
