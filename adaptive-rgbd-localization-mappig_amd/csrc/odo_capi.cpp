@@ -21,6 +21,7 @@
 #include <string>
 #include <vector>
 #include <algorithm>
+#include <mutex>
 
 #include "../../include/odo.h"
 #include "odo_device.h"
@@ -64,6 +65,53 @@ int dalloc(T** p, size_t count) {
 uint32_t splitmix_host(uint64_t base, uint64_t pair) { return pair_seed(base, pair); }
 
 }  // namespace
+
+// Device scratch of the per-stage entry points (odo_extract ... odo_kabsch):
+// owned by a context, bump-allocated per call, grown on demand and never freed
+// per call. A call that outgrows the block takes an extra block; the next call
+// replaces the blocks by one of their total size. Every allocation is checked
+// (a failed one sets `failed`, which the entry point turns into
+// ODO_ERR_DEVICE). The entry points are synchronous, so no kernel of an
+// earlier call still uses the blocks when begin() replaces them.
+struct DevArena {
+    std::vector<std::pair<uint8_t*, size_t>> blocks;
+    size_t used = 0;
+    bool failed = false;
+    ~DevArena() { release(); }
+    void release() {
+        for (auto& b : blocks) (void)hipFree(b.first);
+        blocks.clear();
+        used = 0;
+    }
+    void begin() {
+        failed = false;
+        if (blocks.size() > 1) {
+            size_t tot = 0;
+            for (auto& b : blocks) tot += b.second;
+            release();
+            grow(tot);
+        }
+        used = 0;
+    }
+    bool grow(size_t bytes) {
+        uint8_t* p = nullptr;
+        if (hipMalloc((void**)&p, bytes) != hipSuccess) {
+            failed = true;
+            return false;
+        }
+        blocks.push_back({p, bytes});
+        used = 0;
+        return true;
+    }
+    void* take(size_t bytes) {
+        bytes = std::max<size_t>((bytes + 255) & ~(size_t)255, 256);
+        if (blocks.empty() || used + bytes > blocks.back().second)
+            if (!grow(std::max(bytes, blocks.empty() ? (size_t)16 << 20 : blocks.back().second))) return nullptr;
+        void* r = blocks.back().first + used;
+        used += bytes;
+        return r;
+    }
+};
 
 // Frame sets in flight (4): batch k extracts into set k%NSETS while the pair and
 // PnP stages of batches k-1 and k-2 still read theirs, so the extraction
@@ -214,6 +262,7 @@ struct odo_ctx {
     int *aband_cnt = nullptr, *ahist = nullptr, *atsel = nullptr, *ansel = nullptr, *acell_cnt = nullptr;
     double* athresh = nullptr;
     float a_cos = 1.f, a_sin = 0.f;
+    DevArena arena;  // per-stage entry points' device scratch
     // Hamming-match kernel timing (odo_set_timing mode 2): an event pair
     // around the kNN-2 launch of every batch, read back and summed lazily
     static constexpr int KT_RING = 256;
@@ -1522,17 +1571,17 @@ int32_t odo_rng_next(odo_rng* r) {
 
 // ====================================================================== per-stage entry points
 namespace {
+// a carve of the calling entry point's arena (no free: the arena owns it)
 struct DevBuf {
     void* p = nullptr;
-    explicit DevBuf(size_t bytes) { hipMalloc(&p, bytes ? bytes : 1); }
-    ~DevBuf() {
-        if (p) hipFree(p);
-    }
+    DevBuf(DevArena& a, size_t bytes) : p(a.take(bytes)) {}
     template <typename T>
     T* as() {
         return (T*)p;
     }
 };
+#define ARENA_CHECK(a) \
+    if ((a).failed) return fail(ODO_ERR_DEVICE, "device scratch allocation failed")
 
 // Ransac::Iterate's inputs after the depth filter, std::sort and the latch
 // (ransac.cpp:164-199), uploaded for the single-pair RANSAC kernels.
@@ -1589,6 +1638,7 @@ int prepare_pair_ransac(const odo_dmatch* m12, int n12, const float* xyz1, int n
 struct HypSession {
     PairRansacInput in;
     int h0 = 0, h1 = 0, active = 0;
+    DevArena arena;  // lives from odo_ransac_hyps to odo_ransac_hyps_finish
     DevBuf *xyz = nullptr, *m = nullptr, *g = nullptr, *ints = nullptr, *latch = nullptr, *rng = nullptr,
            *res = nullptr, *T = nullptr, *scr = nullptr, *bm = nullptr, *phase = nullptr;
     ~HypSession() {
@@ -1634,8 +1684,11 @@ int odo_knn2_hamming(odo_ctx* c, const uint8_t* q, int nq, const uint8_t* t, int
     if (nq == 0) return ODO_OK;
     if (nq > (1 << 20) || nt > (1 << 20)) return fail(ODO_ERR_CAPACITY, "knn2: at most 2^20 descriptors");
     hipStream_t st = c->stream;
-    DevBuf dq((size_t)nq * 32), dt((size_t)std::max(nt, 1) * 32), dn(2 * sizeof(int));
-    DevBuf di((size_t)nq * sizeof(int2)), dd((size_t)nq * sizeof(int2));
+    DevArena& A = c->arena;
+    A.begin();
+    DevBuf dq(A, (size_t)nq * 32), dt(A, (size_t)std::max(nt, 1) * 32), dn(A, 2 * sizeof(int));
+    DevBuf di(A, (size_t)nq * sizeof(int2)), dd(A, (size_t)nq * sizeof(int2));
+    ARENA_CHECK(A);
     const int cnt[2] = {nq, nt};
     HIPCHK(hipMemcpyAsync(dq.p, q, (size_t)nq * 32, hipMemcpyHostToDevice, st));
     if (nt) HIPCHK(hipMemcpyAsync(dt.p, t, (size_t)nt * 32, hipMemcpyHostToDevice, st));
@@ -1698,13 +1751,17 @@ int odo_ransac(odo_ctx* c, const odo_dmatch* m12, int n12, const float* xyz1, in
     hipStream_t st = c->stream;
     const int kc = std::max(std::max(n1, n2), 1);
     const int words = (ng + 31) / 32;
-    DevBuf dxyz((size_t)2 * kc * 3 * sizeof(float)), dm((size_t)ng * sizeof(odo_dmatch)), dg((size_t)ng * 8);
-    DevBuf dint(4 * sizeof(int)), dlatch(sizeof(double)), drng(sizeof(odo_rng)), dres(sizeof(odo_pair_result));
+    DevArena& A = c->arena;
+    A.begin();
+    DevBuf dxyz(A, (size_t)2 * kc * 3 * sizeof(float)), dm(A, (size_t)ng * sizeof(odo_dmatch)), dg(A, (size_t)ng * 8);
+    DevBuf dint(A, 4 * sizeof(int)), dlatch(A, sizeof(double)), drng(A, sizeof(odo_rng)),
+        dres(A, sizeof(odo_pair_result));
     const double cam_angle_x = 58.0 / 180.0 * M_PI, cam_angle_y = 45.0 / 180.0 * M_PI;
     const double rsx = 3 * tan(cam_angle_x / 640.0), rsy = 3 * tan(cam_angle_y / 480.0);
     RansacCfg cfg{p->iterations, p->min_inlier_th, p->max_mahalanobis, p->sample_size, p->check_depth, rsx * rsx,
                   rsy * rsy};
-    DevBuf dT(16 * sizeof(float)), dgp(ransac_scratch_bytes(1, ng, words, cfg)), dbm((size_t)words * 4);
+    DevBuf dT(A, 16 * sizeof(float)), dgp(A, ransac_scratch_bytes(1, ng, words, cfg)), dbm(A, (size_t)words * 4);
+    ARENA_CHECK(A);
     std::vector<uint64_t> gl(ng);
     for (int k = 0; k < ng; k++) {
         uint32_t bits;
@@ -1764,17 +1821,20 @@ int odo_ransac_hyps(odo_ctx* c, const odo_dmatch* m12, int n12, const float* xyz
     const int ng = in.ng, kc = in.kc;
     *n_good = ng;
     hipStream_t st = c->stream;
-    S.xyz = new DevBuf((size_t)2 * kc * 3 * sizeof(float));
-    S.m = new DevBuf((size_t)ng * sizeof(odo_dmatch));
-    S.g = new DevBuf((size_t)ng * 8);
-    S.ints = new DevBuf(4 * sizeof(int));
-    S.latch = new DevBuf(sizeof(double));
-    S.rng = new DevBuf(sizeof(odo_rng));
-    S.res = new DevBuf(sizeof(odo_pair_result));
-    S.T = new DevBuf(16 * sizeof(float));
-    S.scr = new DevBuf(ransac_scratch_bytes(1, ng, in.words, in.cfg));
-    S.bm = new DevBuf((size_t)in.words * 4);
-    S.phase = new DevBuf(2 * sizeof(int));
+    DevArena& A = S.arena;
+    A.begin();
+    S.xyz = new DevBuf(A, (size_t)2 * kc * 3 * sizeof(float));
+    S.m = new DevBuf(A, (size_t)ng * sizeof(odo_dmatch));
+    S.g = new DevBuf(A, (size_t)ng * 8);
+    S.ints = new DevBuf(A, 4 * sizeof(int));
+    S.latch = new DevBuf(A, sizeof(double));
+    S.rng = new DevBuf(A, sizeof(odo_rng));
+    S.res = new DevBuf(A, sizeof(odo_pair_result));
+    S.T = new DevBuf(A, 16 * sizeof(float));
+    S.scr = new DevBuf(A, ransac_scratch_bytes(1, ng, in.words, in.cfg));
+    S.bm = new DevBuf(A, (size_t)in.words * 4);
+    S.phase = new DevBuf(A, 2 * sizeof(int));
+    ARENA_CHECK(A);
     std::vector<uint64_t> gl(ng);
     for (int k = 0; k < ng; k++) {
         uint32_t bits;
@@ -1891,9 +1951,12 @@ int odo_pnp_motion_ba(odo_ctx* c, const float* Xw, const float* obs, int n, cons
     if (!c || n < 0 || (n && (!Xw || !obs)) || !Tcw_init || !Tcw_out || !n_inliers) return fail(ODO_ERR_ARG, "bad pnp args");
     hipStream_t st = c->stream;
     const int kc = std::max(n, 1);
-    DevBuf dx((size_t)kc * 12), dkun((size_t)2 * kc * 8), dur((size_t)2 * kc * 4), dsrc((size_t)kc * 4);
-    DevBuf dint(4 * sizeof(int)), dT(16 * 4), dres(sizeof(odo_pair_result)), dedges((size_t)kc * pnp_edge_bytes()),
-        dmask((size_t)kc);
+    DevArena& A = c->arena;
+    A.begin();
+    DevBuf dx(A, (size_t)kc * 12), dkun(A, (size_t)2 * kc * 8), dur(A, (size_t)2 * kc * 4), dsrc(A, (size_t)kc * 4);
+    DevBuf dint(A, 4 * sizeof(int)), dT(A, 16 * 4), dres(A, sizeof(odo_pair_result)),
+        dedges(A, (size_t)kc * pnp_edge_bytes()), dmask(A, (size_t)kc);
+    ARENA_CHECK(A);
     std::vector<float> kun(2 * kc), ur(kc);
     std::vector<int32_t> src(kc);
     for (int i = 0; i < n; i++) {
@@ -1985,8 +2048,12 @@ int odo_projection_match(odo_ctx* c, const float Tcw[16], const odo_landmark* lm
     const odo_calib& k = c->cfg.calib;
     const float cal5[5] = {k.fx, k.fy, k.cx, k.cy, k.mbf};
     const size_t nl = std::max(nL, 1), nn = std::max(n, 1);
-    DevBuf dT(64), dl(nl * sizeof(odo_landmark)), dk(nn * 8), doc(nn * 4), dd(nn * 32), dtk(nn), dproj(nl * 12),
-        din(nl), dcc(nl * 4), dcand(nl * projection_cand_cap() * 4), dsl(nn * 4), dnm(4);
+    DevArena& A = c->arena;
+    A.begin();
+    DevBuf dT(A, 64), dl(A, nl * sizeof(odo_landmark)), dk(A, nn * 8), doc(A, nn * 4), dd(A, nn * 32), dtk(A, nn),
+        dproj(A, nl * 12), din(A, nl), dcc(A, nl * 4), dcand(A, nl * projection_cand_cap() * 4), dsl(A, nn * 4),
+        dnm(A, 4);
+    ARENA_CHECK(A);
     HIPCHK(hipMemcpyAsync(dT.p, Tcw, 64, hipMemcpyHostToDevice, st));
     if (nL) HIPCHK(hipMemcpyAsync(dl.p, lms, (size_t)nL * sizeof(odo_landmark), hipMemcpyHostToDevice, st));
     if (n) {
@@ -2081,7 +2148,13 @@ int odo_kabsch(const float* A, const float* B, int n, float T[16]) {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(ODO_ERR_DEVICE, "no HIP device");
     const int kc = std::max(n, 1);
-    DevBuf da((size_t)kc * 12), db((size_t)kc * 12), dT(64);
+    // Kabsch::Compute takes no context: one process-wide arena, one caller at a time
+    static std::mutex mu;
+    static DevArena KA;
+    std::lock_guard<std::mutex> lock(mu);
+    KA.begin();
+    DevBuf da(KA, (size_t)kc * 12), db(KA, (size_t)kc * 12), dT(KA, 64);
+    ARENA_CHECK(KA);
     if (n) {
         HIPCHK(hipMemcpy(da.p, A, (size_t)n * 12, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(db.p, B, (size_t)n * 12, hipMemcpyHostToDevice));

@@ -311,6 +311,39 @@ def hyp_mode(args, rank, world, local_rank, dist):
     odo.close()
 
 
+def latency_mode(args):
+    """Per-frame latency of the drop-in path: tools/build/frontend_latency runs
+    one Tracking::Track frame at a time through include/odo_frontend.hpp
+    (Extract -> KnnMatch -> Ransac::Iterate -> PnPSolver::Compute, each a
+    synchronous C-ABI call) on the cfg2 sequence; p50 / p99 ms per frame."""
+    import subprocess
+    import tempfile
+    synth = load_synth()
+    W, H = args.width, args.height
+    nf = max(args.steps, 16) + 8
+    bgr, dep, _ = synth.make_sequence(64, W, H, seed=0x5EED0002, closed_loop=True)
+    idx = np.arange(nf) % 64
+    exe = os.path.join(ROOT, "tools", "build", "frontend_latency")
+    if not os.path.exists(exe):
+        raise SystemExit("tools/build/frontend_latency missing: run make -C tools (done by __graft_entry__.build)")
+    with tempfile.NamedTemporaryFile(suffix=".bin", dir=os.environ.get("TMPDIR", "/tmp")) as f:
+        f.write(np.ascontiguousarray(bgr[idx]).tobytes())
+        f.write(np.ascontiguousarray(dep[idx]).tobytes())
+        f.flush()
+        out = subprocess.run([exe, f.name, str(W), str(H), str(nf), str(args.iters), "8"], check=True,
+                             capture_output=True, text=True).stdout
+    r = json.loads(out.strip().splitlines()[-1])
+    print(json.dumps({"metric": "per-frame latency of the drop-in path (Tracking::Track order, one frame at a time)",
+                      "value": r["p50_ms"], "unit": "ms/frame (p50)", "n_gpus": 1, "steps": r["frames"],
+                      "warmup": r["warmup"], "higher_is_better": False, "p99_ms": r["p99_ms"], "p90_ms": r["p90_ms"],
+                      "mean_ms": r["mean_ms"], "max_ms": r["max_ms"], "stage_median_ms": r["stage_median_ms"],
+                      "config": {"workload": f"fr1/desk proxy {W}x{H}, 1000 kp (the reference's nFeatures, "
+                                             f"common.h:77, as odo_frontend.hpp's Extractor uses it), "
+                                             f"RANSAC {args.iters}",
+                                 "mean_matches": r["mean_matches"], "mean_ransac_inliers": r["mean_ransac_inliers"],
+                                 "path": "include/odo_frontend.hpp classes over the per-stage C-ABI"}}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -328,8 +361,9 @@ def main():
     ap.add_argument("--host-steps", type=int, default=20, help="steps of the from-host leg (0: skip it)")
     ap.add_argument("--no-kernel-timing", action="store_true", help="no events around the kNN-2 launches")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mode", choices=["track", "hyp"], default="track",
-                    help="track: the frames/s metric; hyp: SURVEY 8(e) hypotheses mode latency (cfg3, H=4096)")
+    ap.add_argument("--mode", choices=["track", "hyp", "latency"], default="track",
+                    help="track: the frames/s metric; hyp: SURVEY 8(e) hypotheses mode latency (cfg3, H=4096); "
+                         "latency: per-frame ms of the drop-in path through include/odo_frontend.hpp")
     ap.add_argument("--hyp-outliers", type=float, default=0.5, help="hyp mode: fraction of matches re-targeted")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="process group backend for N > 1 (gloo: several ranks sharing one GPU)")
@@ -340,6 +374,9 @@ def main():
                     help="orb_slam2: ORBextractor (the metric's config); adaptive: Extractor(FAST, ORB, ADAPTIVE)")
     args = ap.parse_args()
 
+    if args.mode == "latency":
+        latency_mode(args)
+        return
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
