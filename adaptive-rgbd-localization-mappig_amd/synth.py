@@ -97,11 +97,17 @@ def _rot(ax, ay, az):
 
 
 class Scene:
-    """Desk-sized room [-1.7,1.7]x[-1.2,1.2]x[-1.0,3.0] with cuboid obstacles."""
+    """Desk-sized room [-1.7,1.7]x[-1.2,1.2]x[-1.0,3.0] with cuboid obstacles.
 
-    def __init__(self, seed: int):
+    hard=True (the "hard" workload): two extra cuboids move on their own
+    periodic paths (dynamic outliers for RANSAC), the floor and ceiling carry an
+    exactly periodic tile pattern (repeated texture: ambiguous descriptors),
+    and the renderer adds image noise and depth noise."""
+
+    def __init__(self, seed: int, hard: bool = False, period: int = 64):
         rng = np.random.default_rng(seed)
         self.seed = int(seed) & 0x7FFFFFFF
+        self.hard, self.period = hard, period
         self.room_lo = np.array([-1.7, -1.2, -1.0])
         self.room_hi = np.array([1.7, 1.2, 3.0])
         boxes = []
@@ -110,6 +116,22 @@ class Scene:
             s = np.array([rng.uniform(0.1, 0.35), rng.uniform(0.1, 0.4), rng.uniform(0.1, 0.35)])
             boxes.append((c - s, c + s))
         self.boxes = boxes
+        # movers: (centre, half size, motion amplitude, phase), periodic in `period` frames
+        self.movers = []
+        if hard:
+            for k in range(2):
+                c = np.array([(-0.45 if k == 0 else 0.5), rng.uniform(-0.3, 0.3), rng.uniform(1.0, 1.5)])
+                hs = np.array([0.36, 0.34, 0.22])
+                amp = np.array([0.35, 0.15, 0.20]) * (1 if k == 0 else -1)
+                self.movers.append((c, hs, amp, rng.uniform(0, 2 * math.pi)))
+
+    def mover_boxes(self, frame: int):
+        out = []
+        for c, hs, amp, ph in self.movers:
+            th = 2 * math.pi * (frame % self.period) / self.period * 3 + ph
+            cc = c + amp * np.array([math.sin(th), math.cos(th), math.sin(2 * th)])
+            out.append((cc - hs, cc + hs))
+        return out
 
     def render(self, cam: Camera, Rwc: np.ndarray, twc: np.ndarray, frame_seed: int):
         """Return (bgr uint8 HxWx3, depth uint16 HxW) for camera pose (Rwc, twc)."""
@@ -126,7 +148,7 @@ class Scene:
             best = tfar.copy()
             axis = np.argmin(np.maximum(t1, t2), -1)
             sid = axis * 2 + (np.take_along_axis(dw, axis[..., None], -1)[..., 0] > 0)
-            for bi, (lo, hi) in enumerate(self.boxes):
+            for bi, (lo, hi) in enumerate(self.boxes + self.mover_boxes(frame_seed)):
                 a1 = (lo - o) * inv
                 a2 = (hi - o) * inv
                 tmin3 = np.minimum(a1, a2)
@@ -146,11 +168,23 @@ class Scene:
         r = _texture(ua + 0.37, va - 0.11, sidc + 50, self.seed)
         b = _texture(ua - 0.21, va + 0.53, sidc + 90, self.seed)
         col = np.stack([0.7 * b + 0.3 * g, g, 0.7 * r + 0.3 * g], -1)
+        if self.hard:
+            # floor and ceiling (faces of the y axis: sid 2, 3): an exactly
+            # periodic 4 x 4 block of hashed tiles, repeated every 0.32 m
+            rep = (sid == 2) | (sid == 3)
+            tu = np.floor(ua / 0.08).astype(np.int64) & 3
+            tv = np.floor(va / 0.08).astype(np.int64) & 3
+            pat = _hash(tu, tv, sidc + 7) * 0.8 + 0.1 * (np.sin(ua * 40.0) > 0)
+            col = np.where(rep[..., None], np.stack([pat, pat, pat], -1), col)
+        rs = np.random.default_rng((self.seed * 1000003 + frame_seed) & 0xFFFFFFFF)
+        if self.hard:
+            col = col + rs.normal(0.0, 3.0 / 255.0, col.shape)  # sensor noise, sigma 3 grey levels
         bgr = np.clip(np.round(col * 255.0), 0, 255).astype(np.uint8)
         z = (p - o) @ Rwc[:, 2]
+        if self.hard:
+            z = z + rs.normal(0.0, 1.0, z.shape) * 1.425e-3 * z * z  # Kinect-like sigma_z = 1.425e-3 z^2
         d = np.round(z * 5000.0)
         d = np.where((z > 0.3) & (z < 10.0), d, 0).astype(np.uint16)
-        rs = np.random.default_rng((self.seed * 1000003 + frame_seed) & 0xFFFFFFFF)
         drop = rs.random(d.shape) < 0.03
         d[drop] = 0
         hy, hx = rs.integers(0, cam.h), rs.integers(0, cam.w)
@@ -160,9 +194,10 @@ class Scene:
         return np.ascontiguousarray(bgr), np.ascontiguousarray(d)
 
 
-def _loop_pose(f: int, n: int, seed: int):
-    """Closed periodic trajectory: frame n-1 -> frame 0 is an ordinary step."""
-    th = 2 * math.pi * f / n
+def _loop_pose(f: int, n: int, seed: int, speed: int = 1):
+    """Closed periodic trajectory: frame n-1 -> frame 0 is an ordinary step
+    (`speed` laps of the path per n frames: larger inter-frame motion)."""
+    th = 2 * math.pi * f * speed / n
     ph = (seed % 997) / 997.0 * 2 * math.pi
     t = np.array([0.30 * math.sin(th + ph), 0.12 * math.sin(2 * th), -0.25 + 0.20 * math.cos(th)])
     R = _rot(0.05 + 0.10 * math.sin(th), -0.08 + 0.12 * math.cos(th + ph), 0.02 + 0.08 * math.sin(2 * th))
@@ -170,16 +205,20 @@ def _loop_pose(f: int, n: int, seed: int):
 
 
 def make_sequence(n_frames: int, w: int = 640, h: int = 480, intrinsics=None, seed: int = 0x5EED0002,
-                  max_step_m: float = 0.03, max_step_deg: float = 1.5, closed_loop: bool = False):
+                  max_step_m: float = 0.03, max_step_deg: float = 1.5, closed_loop: bool = False,
+                  hard: bool = False):
     """Render n_frames consecutive frames. Returns (bgr [F,H,W,3] u8, depth [F,H,W] u16, poses [F,4,4] Twc).
 
     closed_loop: poses follow a periodic path so the sequence can be replayed
     back to back (bench steps) without a jump between its last and first frame.
+    hard: the harder workload: image noise, depth noise
+    sigma ~ z^2, two independently moving cuboids, repeated texture on the
+    floor and ceiling, and twice the inter-frame motion.
     """
     intr = dict(FR1 if intrinsics is None else intrinsics)
     sx = w / 640.0
     cam = Camera(w, h, intr["fx"] * sx, intr["fy"] * sx, intr["cx"] * sx, intr["cy"] * sx)
-    scene = Scene(seed)
+    scene = Scene(seed, hard=hard, period=n_frames)
     rng = np.random.default_rng(seed ^ 0xABCDEF)
     R = _rot(0.05, -0.08, 0.02)
     t = np.array([0.1, 0.05, -0.3])
@@ -189,7 +228,7 @@ def make_sequence(n_frames: int, w: int = 640, h: int = 480, intrinsics=None, se
     renders = []
     for f in range(n_frames):
         if closed_loop:
-            R, t = _loop_pose(f, n_frames, seed)
+            R, t = _loop_pose(f, n_frames, seed, speed=2 if hard else 1)
         R_render = R
         if intr["fy"] < 0:  # ICL: negative fy flips the image rows
             R_render = R @ np.diag([1.0, -1.0, -1.0]) @ np.diag([1.0, -1.0, -1.0])

@@ -311,6 +311,48 @@ def hyp_mode(args, rank, world, local_rank, dist):
     odo.close()
 
 
+def hard_leg(pkg, synth, args, B, W, H, device):
+    """The hard workload (synth.make_sequence(hard=True): image noise, depth
+    noise ~ z^2, two independently moving cuboids, repeated texture, twice the
+    inter-frame motion), same batched path and contract as the headline: the
+    RANSAC of every pair runs most of its hypotheses."""
+    import torch
+    from importlib import import_module
+    tj = import_module("arlm_amd.trajectory")
+    L = min(args.seq_len, B)
+    bgr, dep, gt = synth.make_sequence(L, W, H, seed=shard_seed(0), closed_loop=True, hard=True)
+    idx = np.arange(B) % L
+    d_bgr = torch.from_numpy(np.ascontiguousarray(bgr[idx])).to("cuda")
+    d_dep = torch.from_numpy(np.ascontiguousarray(dep[idx]).view(np.int16)).to("cuda")
+    cfg = pkg.default_config(W, H, B, nfeatures=args.nfeatures, iterations=args.iters, seed=rank_seeds(0)[1])
+    odo = pkg.Odometry(cfg, device=device)
+    torch.cuda.synchronize()
+    res = odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=True)
+    for _ in range(2):
+        odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=False)
+    res_q = odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=True)
+    odo.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.hard_steps):
+        odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=False)
+    odo.synchronize()
+    dt = time.perf_counter() - t0
+    Tcw = tj.chain_poses(res[:L], np.linalg.inv(gt[0]).astype(np.float32))
+    ate = 1000.0 * tj.ate_rmse(tj.camera_centres(Tcw), gt[:L, :3, 3])
+    odo.close()
+    ratio = res_q["n_inliers"] / np.maximum(res_q["n_good"], 1)
+    return {"value": round(B * args.hard_steps / dt, 2), "unit": "frames/s",
+            "ms_per_step": round(dt / args.hard_steps * 1e3, 3), "steps": args.hard_steps,
+            "workload": f"cfg2 {W}x{H}, {args.nfeatures} kp, RANSAC {args.iters}; image noise sigma 3, depth noise "
+                        "1.425e-3 z^2, 2 moving cuboids, repeated floor/ceiling texture, 2x motion",
+            "mean_matches": round(float(np.mean(res_q["n_matches"])), 1),
+            "mean_inlier_ratio": round(float(np.mean(ratio)), 3),
+            "mean_ransac_visited": round(float(np.mean(res_q["visited"])), 1),
+            "mean_ransac_sweeps": round(float(np.mean(res_q["n_sweeps"])), 1),
+            "mean_pnp_inliers": round(float(np.mean(res_q["pnp_inliers"])), 1),
+            "ate_mm": round(ate, 3)}
+
+
 def latency_mode(args):
     """Per-frame latency of the drop-in path: tools/build/frontend_latency runs
     one Tracking::Track frame at a time through include/odo_frontend.hpp
@@ -359,6 +401,7 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=24, help="oracle sample (frames per timed pass)")
     ap.add_argument("--cpu-reps", type=int, default=5, help="timed oracle passes (median reported)")
     ap.add_argument("--host-steps", type=int, default=20, help="steps of the from-host leg (0: skip it)")
+    ap.add_argument("--hard-steps", type=int, default=20, help="steps of the hard-workload leg (0: skip it)")
     ap.add_argument("--no-kernel-timing", action="store_true", help="no events around the kNN-2 launches")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", choices=["track", "hyp", "latency"], default="track",
@@ -611,6 +654,10 @@ def main():
     if args.host_steps > 0 and not seq_mode:
         from_host = host_leg(pkg, odo, bgr, dep, B, W, H, args.host_steps, 2, world, dist, coll_dev)
 
+    hard = None
+    if args.hard_steps > 0 and world == 1 and not adaptive:
+        hard = hard_leg(pkg, synth, args, B, W, H, local_rank % max(1, torch.cuda.device_count()))
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         nf = args.cpu_frames
@@ -657,6 +704,7 @@ def main():
             "stage_ms": {k: round(v, 4) for k, v in timings.items()},
             "host_submit_ms_per_step": round(submit / args.steps * 1e3, 3),
             "from_host": from_host,
+            "hard_workload": hard,
             "roofline": roofline,
             "roofline_legs": legs,
             "cpu_baseline": cpu,

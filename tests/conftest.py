@@ -42,11 +42,11 @@ def load_synth():
 _SEQ_CACHE = {}
 
 
-def sequence(n, w=640, h=480, intrinsics=None, seed=0x5EED0002, closed_loop=False):
-    key = (n, w, h, tuple(sorted((intrinsics or {}).items())), seed, closed_loop)
+def sequence(n, w=640, h=480, intrinsics=None, seed=0x5EED0002, closed_loop=False, hard=False):
+    key = (n, w, h, tuple(sorted((intrinsics or {}).items())), seed, closed_loop, hard)
     if key not in _SEQ_CACHE:
         _SEQ_CACHE[key] = load_synth().make_sequence(n, w, h, intrinsics=intrinsics, seed=seed,
-                                                     closed_loop=closed_loop)
+                                                     closed_loop=closed_loop, hard=hard)
     return _SEQ_CACHE[key]
 
 

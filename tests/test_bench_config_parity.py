@@ -16,6 +16,10 @@ ransac.cpp:155-267; PnPSolver::Compute pnpsolver.cpp:17-214):
 * PnP pose within 1e-4; PnP inlier flags equal except on edges whose chi2 at
   the oracle's pose lies within 2 % of the threshold (5.991 mono, 7.815 stereo).
 
+cfg2_hard_b64 runs the hard workload (synth.make_sequence(hard=True): image and
+depth noise, two moving cuboids, repeated texture, twice the motion), where
+the inlier ratio is ~64 % and RANSAC visits ~450 of its 500 hypotheses.
+
 cfg2 also runs with ODO_KNN_SPLIT = 1, 2 and 8 (match lists and query counts
 bit-exact each time): 256 pairs give more active kNN-2 items than resident
 workgroups, so runs covering several items, split flushes and query-block
@@ -48,6 +52,10 @@ CONFIGS = {
     "cfg5_1280_b32": dict(w=1280, h=960, nf=8000, iters=8192, B=32, L=32, intr=FR1,
                           calib=dict(fx=2 * FR1["fx"], fy=2 * FR1["fy"], cx=2 * FR1["cx"], cy=2 * FR1["cy"],
                                      **NODIST), scene=0x5EED0005, seed=0x5EED0005),
+    # the hard workload (bench.py's hard_workload leg): noise, movers, repeated
+    # texture, 2x motion; RANSAC visits ~450 of 500 hypotheses per pair
+    "cfg2_hard_b64": dict(w=640, h=480, nf=2000, iters=500, B=64, L=64, intr=None, calib=None,
+                          scene=0x5EED0002, seed=0x5EED0000, hard=True),
 }
 
 
@@ -191,7 +199,8 @@ def _compare(name, c, odo, res, oracle, full=True):
 def test_bench_configuration_full_batch(name):
     c = CONFIGS[name]
     pkg = load_pkg()
-    bgr, dep, _ = sequence(c["L"], c["w"], c["h"], intrinsics=c["intr"], seed=c["scene"], closed_loop=True)
+    bgr, dep, _ = sequence(c["L"], c["w"], c["h"], intrinsics=c["intr"], seed=c["scene"], closed_loop=True,
+                           hard=c.get("hard", False))
     odo, cfg, res = _run_gpu(pkg, c, bgr, dep)
     oracle = _oracle_cached(name, pkg, c, cfg, bgr, dep)
     r = oracle[2]
