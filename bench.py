@@ -402,6 +402,8 @@ def main():
     ap.add_argument("--cpu-reps", type=int, default=5, help="timed oracle passes (median reported)")
     ap.add_argument("--host-steps", type=int, default=20, help="steps of the from-host leg (0: skip it)")
     ap.add_argument("--hard-steps", type=int, default=20, help="steps of the hard-workload leg (0: skip it)")
+    ap.add_argument("--workload", choices=["default", "hard"], default="default",
+                    help="main leg's sequence: the cfg2 proxy or the hard variant (synth hard=True)")
     ap.add_argument("--no-kernel-timing", action="store_true", help="no events around the kNN-2 launches")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", choices=["track", "hyp", "latency"], default="track",
@@ -453,7 +455,8 @@ def main():
     L = min(args.seq_len, B)
     if B % L:
         raise SystemExit(f"--batch {B} must be a multiple of --seq-len {L} (pair 0 links frame B-1 to frame 0)")
-    bgr_loop, dep_loop, gt_poses = synth.make_sequence(L, W, H, seed=scene_seed, closed_loop=True)
+    bgr_loop, dep_loop, gt_poses = synth.make_sequence(L, W, H, seed=scene_seed, closed_loop=True,
+                                                       hard=args.workload == "hard")
     bgr, dep = bgr_loop[np.arange(B) % L], dep_loop[np.arange(B) % L]
     adaptive = args.detector == "adaptive"
     if adaptive:
@@ -690,6 +693,7 @@ def main():
             "dtype": "u8/i32 (extract, match), f32+f64 (ransac, pnp)",
             "data": "synthetic (ray-cast textured room, closed-loop trajectory; no dataset offline)",
             "config": {"workload": (f"cfg2 fr1/desk proxy {W}x{H}, {args.nfeatures} kp, RANSAC {args.iters}"
+                                    + (" (hard variant)" if args.workload == "hard" else "")
                                     if not adaptive else
                                     f"fr1/desk proxy {W}x{H}, ADAPTIVE 3x3 FAST grid + ORB (<=1000 kp), "
                                     f"RANSAC {args.iters}"),
