@@ -39,6 +39,10 @@ struct GoodPt {
     float sx, sy, sz, tx, ty, tz, w, pad;
 };
 
+#define EV_WAVES_C 4   // waves per k_ransac_eval workgroup (EV_WAVES below)
+#ifndef EV_ROWS0
+#define EV_ROWS0 1  // 4 hypotheses per pair in the first launch (most pairs break at the first); 75.7k vs 74.8k at 2
+#endif
 #define MAX_SAMPLE 8
 #define SREC (MAX_SAMPLE + 2)  // sample record: count, ids[MAX_SAMPLE], end (draw pairs consumed after it)
 
@@ -50,6 +54,7 @@ struct RState {
     int lock, fold_pos, n, visited, valid, best_cnt, best_h, pad;
     float rmse;
     int sweeps, fitpts;  // work of the visited prefix (odo_pair_result.n_sweeps / n_fit_points)
+    int nexth;           // k_ransac_lanes: the next hypothesis a lane takes up
 };
 
 struct HypRes {
@@ -86,6 +91,7 @@ struct RansacBufs {
     int h_lo, h_hi, no_fold;
     int* open_list;  // [pair] pairs still folding after the first launch
     int* open_cnt;   // [0] their count, [1] the second launch's work counter
+    uint32_t* lslab;  // k_ransac_lanes: [wave][2][mask_words][64] inlier sets
 };
 
 ODO_INLINE int ld_relaxed(const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
@@ -548,6 +554,7 @@ __global__ void __launch_bounds__(256) k_ransac_prep(RansacBufs B, RansacCfg cfg
         S->rmse = 1e6f;
         S->sweeps = 0;
         S->fitpts = 0;
+        S->nexth = EV_ROWS0 * EV_WAVES_C;  // the first eval launch covers [0, EV_ROWS0 * EV_WAVES)
     }
     if (done) return;
     __shared__ SampWin s_win;
@@ -556,10 +563,7 @@ __global__ void __launch_bounds__(256) k_ransac_prep(RansacBufs B, RansacCfg cfg
 }
 
 // ---------------------------------------------------------------- eval
-#define EV_WAVES 4
-#ifndef EV_ROWS0
-#define EV_ROWS0 1  // 4 hypotheses per pair in the first launch (most pairs break at the first); 75.7k vs 74.8k at 2
-#endif
+#define EV_WAVES EV_WAVES_C
 
 struct EvalLds {
     uint32_t cur[256];  // current inlier set (refined), bit k = good match k
@@ -1047,12 +1051,13 @@ __global__ void __launch_bounds__(256) k_ransac_open(RansacBufs B, int npairs) {
 // counter, 4 hypotheses per item - no launch-sized crowd of early-exit
 // workgroups for the pairs that already broke.
 __global__ void __launch_bounds__(64 * EV_WAVES, EV_MIN_BLOCKS) k_ransac_eval_list(RansacBufs B, RansacCfg cfg, int y0,
-                                                                                   int rows) {
+                                                                                   int rows, int max_open) {
     __builtin_amdgcn_s_setprio(ODO_WAVE_PRIO);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     __shared__ EvalLds s_w[EV_WAVES];
     __shared__ int s_item;
     const int cnt = B.open_cnt[0];
+    if (cnt > max_open) return;  // many open pairs: k_ransac_lanes takes them
     const int total = cnt * rows;
     while (true) {
         __syncthreads();
@@ -1067,6 +1072,231 @@ __global__ void __launch_bounds__(64 * EV_WAVES, EV_MIN_BLOCKS) k_ransac_eval_li
         const GoodPt* P = B.gpts + (size_t)p * B.match_cap;
         eval_hyps<false>(B, cfg, p, wave, lane, s_w[wave], P, S->ng, S->words, H, y0 + row,
                          (y0 + row + 1) * EV_WAVES, 0, 1);
+    }
+}
+
+// ---------------------------------------------------------------- lanes
+// The hypotheses after the first launch, one per LANE (the throughput form;
+// k_ransac_eval keeps one per wave for the latency of the first rows).
+// Ransac::Iterate's inner loop (ransac.cpp:201-231) is sequential per
+// hypothesis: PCL's TFC recurrence over the inlier set in set order, then
+// ComputeInliersAndError's ordered double sum. With a hypothesis per lane both
+// run in their natural order in that lane, with no cross-lane folds, and the
+// wave-uniform good points (one 32-B record per step) are shared by all 64
+// lanes. A round is one refinement of every lane's hypothesis: pass A (the TFC
+// over the lane's current inlier set; a fresh hypothesis fits its minimal
+// sample instead), the SVD, pass B (the Mahalanobis sweep over all good
+// points: new inlier set, mean error). A lane whose hypothesis ends writes its
+// result, marks it ready, runs the ordered fold and takes the next hypothesis
+// of the pair from the pair's counter, so lanes never idle while the pair has
+// hypotheses left. Inlier sets live in a per-wave global slab ([2][words][64],
+// coalesced), swapped on accept.
+#define LN_WAVES 4
+__global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B, RansacCfg cfg, uint32_t* lane_slab,
+                                                                   int waves_total, int min_open) {
+    __builtin_amdgcn_s_setprio(ODO_WAVE_PRIO);
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int gw = (int)blockIdx.x * LN_WAVES + wv;
+    // the good points stream through a per-wave LDS chunk: one coalesced load
+    // per lane, then wave-uniform broadcast reads in point order
+    __shared__ GoodPt s_pts[LN_WAVES][64];
+    GoodPt* lp = s_pts[wv];
+    // the sweep's parked Mahalanobis terms: [active slot][32 points], and the
+    // active lanes in slot order
+    __shared__ double s_res[LN_WAVES][64 * 32];
+    __shared__ int s_la[LN_WAVES][64];
+    double* lres = s_res[wv];
+    int* la = s_la[wv];
+    auto stage = [&](const GoodPt* P, int c0, int ng) {
+        wave_sync();  // the previous chunk has been read
+        if (c0 + lane < ng) lp[lane] = P[c0 + lane];
+        wave_sync();
+    };
+    const int cnt = B.open_cnt[0];
+    if (cnt < min_open || cnt <= 0) return;  // few open pairs: latency matters, k_ransac_eval_list takes them
+    uint32_t* slab = lane_slab + (size_t)gw * 2 * B.mask_words * 64;
+    MahalConst K;
+    K.raster_cov_x = cfg.raster_cov_x;
+    K.raster_cov_y = cfg.raster_cov_y;
+    K.depth_cov = *B.latch;
+    const float th = cfg.max_mahal * cfg.max_mahal;
+    const unsigned minInl = (unsigned)cfg.min_inlier_th;
+    // waves_total >= open pairs: several waves per pair share its counter;
+    // fewer: each wave walks its pairs in turn
+    const int iters = cnt > waves_total ? (cnt + waves_total - 1) / waves_total : 1;
+    for (int it = 0; it < iters; it++) {
+        const int slot = gw + it * waves_total;
+        if (cnt > waves_total && slot >= cnt) break;
+        const int p = __builtin_amdgcn_readfirstlane(B.open_list[slot % cnt]);
+        RState* S = B.st + p;
+        const int H = S->H, ng = S->ng, words = S->words;
+        const GoodPt* P = B.gpts + (size_t)p * B.match_cap;
+        const int* smp0 = B.samples + (size_t)p * B.hcap * SREC;
+        // lane state: hypothesis h (-1 idle), inlier set buffer, refinement bookkeeping
+        int h = -1, cur = 0, nref = 0, nsweep = 0, nfit = 0;
+        bool sample = false, exhausted = false;
+        unsigned refinedCnt = 0;
+        double refinedError = 1e6;
+        float refinedT[12];
+        while (true) {
+            if (h < 0 && !exhausted) {
+                const int nh = atomicAdd(&S->nexth, 1);
+                if (nh < H) {
+                    h = nh;
+                    sample = true;
+                    nref = nsweep = nfit = 0;
+                    refinedCnt = 0;
+                    refinedError = 1e6;
+#pragma unroll
+                    for (int i = 0; i < 12; i++) refinedT[i] = (i % 5 == 0) ? 1.f : 0.f;
+                } else {
+                    exhausted = true;
+                }
+            }
+            if (__ballot(h >= 0) == 0) break;
+            if (ld_relaxed(&S->done)) break;  // the fold has stopped: nothing will read these
+            const bool act = h >= 0;
+            // ---- GetTransformFromMatches (ransac.cpp:295-313) in set order
+            TFC tf;
+            tf.reset();
+            if (act && sample) {
+                const int* smp = smp0 + (size_t)h * SREC;
+                const int ns = smp[0];
+#pragma unroll
+                for (int j = 0; j < MAX_SAMPLE; j++) {
+                    if (j < ns) {
+                        const GoodPt g = P[smp[1 + j]];
+                        if (tfc_point_ok(g)) {
+                            tf.add(g.sx, g.sy, g.sz, g.tx, g.ty, g.tz, g.w);
+                            nfit++;
+                        }
+                    }
+                }
+            }
+            const bool inset = act && !sample;
+            if (__ballot(inset) != 0) {
+                const uint32_t* cw = slab + (size_t)cur * B.mask_words * 64;
+                for (int c0 = 0; c0 < ng; c0 += 64) {
+                    stage(P, c0, ng);
+                    const int w0 = c0 >> 5;
+                    const uint32_t b0 = inset ? cw[(size_t)w0 * 64 + lane] : 0u;
+                    const uint32_t b1 = inset && c0 + 32 < ng ? cw[(size_t)(w0 + 1) * 64 + lane] : 0u;
+                    const int n = min(64, ng - c0);
+                    for (int j = 0; j < n; j++) {
+                        const GoodPt g = lp[j];
+                        if (!tfc_point_ok(g)) continue;  // uniform
+                        if ((((j < 32) ? b0 : b1) >> (j & 31)) & 1u) {
+                            tf.add(g.sx, g.sy, g.sz, g.tx, g.ty, g.tz, g.w);
+                            nfit++;
+                        }
+                    }
+                }
+            }
+            float T[12];
+            tf.get(T);
+            double Td[12];
+#pragma unroll
+            for (int i = 0; i < 12; i++) Td[i] = (double)T[i];
+            // ---- ComputeInliersAndError (ransac.cpp:315-348): the new set into the other buffer
+            // Evaluations are spread over the lanes, not over the hypotheses:
+            // per 32-point chunk, lanes (point j, half hf) evaluate point j for
+            // the active hypotheses 2i + hf, i = 0.. (T broadcast by readlane),
+            // and park d in LDS; then every active lane sums its own 32 values
+            // in point order (the reference's sequential double sum) and forms
+            // the chunk's inlier word. Work is proportional to the active
+            // hypotheses, so lanes whose hypothesis already ended cost nothing.
+            uint32_t* nw = slab + (size_t)(cur ^ 1) * B.mask_words * 64;
+            const uint64_t actm = __ballot(act);
+            const int nact = __popcll(actm);
+            const int rank = (int)lane_rank(actm);  // this lane's slot among the active ones
+            if (act) la[rank] = lane;
+            wave_sync();
+            double meanError = 0.0;
+            unsigned c = 0;
+            const int pj = lane & 31, hf = lane >> 5;
+            for (int c0 = 0; c0 < ng; c0 += 32) {
+                const int k = c0 + pj;
+                GoodPt g;
+                bool skip = true;
+                if (k < ng) {
+                    g = P[k];
+                    skip = g.sz == 0.0f || g.tx == 0.0f;  // sic: target.x (ransac.cpp:326)
+                }
+                const float x1[3] = {g.sx, g.sy, g.sz}, x2[3] = {g.tx, g.ty, g.tz};
+                for (int i = 0; i < nact; i += 2) {
+                    const int a = i + hf;  // this half's hypothesis slot
+                    const int src0 = la[i], src1 = la[min(i + 1, nact - 1)];
+                    double Ta[12];
+#pragma unroll
+                    for (int q = 0; q < 12; q++) {
+                        const double t0 = __shfl(Td[q], src0), t1 = __shfl(Td[q], src1);
+                        Ta[q] = hf ? t1 : t0;
+                    }
+                    double d = -1.0;  // not an inlier
+                    if (a < nact && !skip) {
+                        const double e = error_function2(x1, x2, Ta, K);
+                        if (!(e > th) && (e >= 0.0)) d = e;
+                    }
+                    if (a < nact) lres[a * 32 + pj] = d;
+                }
+                wave_sync();
+                uint32_t word = 0;
+                if (act) {
+                    const int nj = min(32, ng - c0);
+                    for (int j = 0; j < nj; j++) {
+                        const double v = lres[rank * 32 + j];
+                        if (v >= 0.0) {
+                            meanError += v;
+                            c++;
+                            word |= 1u << j;
+                        }
+                    }
+                    nw[(size_t)(c0 >> 5) * 64 + lane] = word;
+                }
+                wave_sync();
+            }
+            if (!act) continue;
+            nsweep++;
+            nref++;
+            if (c < 3) meanError = 1e9;
+            else {
+                meanError /= (double)c;
+                meanError = sqrt(meanError);
+            }
+            bool fin;
+            if (c < minInl || meanError > (double)cfg.max_mahal) {
+                fin = true;
+            } else if (c >= refinedCnt && meanError <= refinedError) {
+                const unsigned prev = refinedCnt;
+#pragma unroll
+                for (int i = 0; i < 12; i++) refinedT[i] = T[i];
+                refinedError = meanError;
+                refinedCnt = c;
+                cur ^= 1;  // the new set becomes the current one
+                sample = false;
+                fin = c == prev || nref >= 19;
+            } else {
+                fin = true;
+            }
+            if (fin) {
+                HypRes* hr = B.hyp + (size_t)p * B.hcap + h;
+                hr->err = refinedError;
+                hr->cnt = (int)refinedCnt;
+                hr->pad = nsweep | (nfit << 5);
+#pragma unroll
+                for (int i = 0; i < 12; i++) hr->T[i] = refinedT[i];
+                uint32_t* mo = B.masks + ((size_t)p * B.hcap + h) * B.mask_words;
+                if (refinedCnt > 0) {
+                    const uint32_t* cw = slab + (size_t)cur * B.mask_words * 64;
+                    for (int w = 0; w < words; w++) mo[w] = cw[(size_t)w * 64 + lane];
+                }
+                __threadfence();
+                __hip_atomic_store(B.ready + (size_t)p * B.hcap + h, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                try_fold(B, cfg, p);
+                h = -1;
+            }
+        }
     }
 }
 
@@ -1210,8 +1440,29 @@ static int ransac_rawcap(const RansacCfg& cfg) {
 }
 
 struct Layout {
-    size_t gpts, st, hyp, samples, ready, masks, raw, open, total;
+    size_t gpts, st, hyp, samples, ready, masks, raw, open, lslab, total;
 };
+
+// k_ransac_lanes grid: workgroups of LN_WAVES waves (ODO_RANSAC_LANES, 0 = the
+// wave-per-hypothesis work list k_ransac_eval_list instead)
+static int ln_groups() {
+    static int r = [] {
+        const char* e = getenv("ODO_RANSAC_LANES");
+        return e ? std::max(0, atoi(e)) : 512;
+    }();
+    return r;
+}
+// Open pairs from which the second RANSAC launch switches from the
+// wave-per-hypothesis work list (latency: a few long pairs, as in the default
+// workload) to k_ransac_lanes (throughput: most pairs run most of their
+// hypotheses, as in the hard workload). Both are launched; the other exits.
+static int ln_min_open() {
+    static int r = [] {
+        const char* e = getenv("ODO_LANES_MIN_OPEN");
+        return e ? std::max(1, atoi(e)) : 32;
+    }();
+    return r;
+}
 
 static Layout layout(int npairs, int match_cap, int mask_words, const RansacCfg& cfg) {
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
@@ -1234,6 +1485,8 @@ static Layout layout(int npairs, int match_cap, int mask_words, const RansacCfg&
     o = al(o + (size_t)npairs * ransac_rawcap(cfg) * 4);
     L.open = o;
     o = al(o + (size_t)(npairs + 2) * 4);
+    L.lslab = o;  // per-wave inlier-set buffers of k_ransac_lanes
+    o = al(o + (size_t)ln_groups() * LN_WAVES * 2 * mask_words * 64 * 4);
     L.total = o;
     return L;
 }
@@ -1254,6 +1507,7 @@ static RansacBufs carve(void* scratch, int npairs, int match_cap, int mask_words
     B.masks = (uint32_t*)(s + L.masks);
     B.open_list = (int*)(s + L.open);
     B.open_cnt = B.open_list + npairs;
+    B.lslab = (uint32_t*)(s + L.lslab);
     B.raw = (uint32_t*)(s + L.raw);
     B.hcap = ransac_hcap(cfg);
     B.rawcap = ransac_rawcap(cfg);
@@ -1359,7 +1613,7 @@ void launch_ransac(hipStream_t st, const void* good, const int* n_good, const in
                    const odo_dmatch* matches, const float* xyz, int kp_cap, int slot0, int match_cap, RansacCfg cfg,
                    const double* latch, const int* pair_valid, int min_matches, odo_rng* rng_io, void* scratch,
                    uint32_t* best_mask, int mask_words, odo_pair_result* res, float* T12, int npairs, int part,
-                   int* phase) {
+                   int* phase, int* open_hint) {
     ransac_eval_lds_attr();
     RansacBufs B = carve(scratch, npairs, match_cap, mask_words, cfg);
     B.good = (const SortElR*)good;
@@ -1415,8 +1669,20 @@ void launch_ransac(hipStream_t st, const void* good, const int* n_good, const in
         if (rows > r0) {
             if (ev2_list()) {
                 hipLaunchKernelGGL(k_ransac_open, dim3(1), dim3(256), 0, st, B, npairs);
-                hipLaunchKernelGGL(k_ransac_eval_list, dim3(ev2_list()), dim3(64 * EV_WAVES), EV_LDS, st, B, cfg, r0,
-                                   rows - r0);
+                // which of the two kernels takes the open pairs: decided on the
+                // host from the previous batch's open count on this frame set
+                // (open_hint, page-locked, copied back asynchronously), so
+                // only one of them is launched; both give the same results
+                const int lanes = ln_groups();
+                const bool use_lanes =
+                    lanes && open_hint && *reinterpret_cast<volatile int*>(open_hint) >= ln_min_open();
+                if (use_lanes)
+                    hipLaunchKernelGGL(k_ransac_lanes, dim3(lanes), dim3(64 * LN_WAVES), 0, st, B, cfg, B.lslab,
+                                       lanes * LN_WAVES, 1);
+                else
+                    hipLaunchKernelGGL(k_ransac_eval_list, dim3(ev2_list()), dim3(64 * EV_WAVES), EV_LDS, st, B, cfg,
+                                       r0, rows - r0, 1 << 30);
+                if (open_hint) (void)hipMemcpyAsync(open_hint, B.open_cnt, sizeof(int), hipMemcpyDeviceToHost, st);
             } else {
                 hipLaunchKernelGGL(k_ransac_eval, dim3(npairs, std::min(rows - r0, ev2_rows())), dim3(64 * EV_WAVES),
                                    EV_LDS, st, B, cfg, r0, H);

@@ -263,6 +263,7 @@ struct odo_ctx {
     double* athresh = nullptr;
     float a_cos = 1.f, a_sin = 0.f;
     DevArena arena;  // per-stage entry points' device scratch
+    int* h_open = nullptr;  // page-locked [NSETS]: RANSAC open pairs of the last batch per set (launch hint)
     // Hamming-match kernel timing (odo_set_timing mode 2): an event pair
     // around the kNN-2 launch of every batch, read back and summed lazily
     static constexpr int KT_RING = 256;
@@ -342,6 +343,7 @@ static void free_ctx(odo_ctx* c) {
     }
     if (c->ev_latch) hipEventDestroy(c->ev_latch);
     for (hipStream_t st : c->owned) hipStreamDestroy(st);
+    if (c->h_open) (void)hipHostFree(c->h_open);
     delete c;
 }
 
@@ -672,6 +674,8 @@ static int alloc_buffers(odo_ctx* c) {
         if ((e = dalloc(&c->athresh, nc))) return e;
         if ((e = reset_adaptive(c))) return e;
     }
+    HIPCHK(hipHostMalloc((void**)&c->h_open, NSETS * sizeof(int), hipHostMallocDefault));
+    for (int i = 0; i < NSETS; i++) c->h_open[i] = 0;
     HIPCHK(hipMemset(c->nkp, 0, S * sizeof(int)));
     const double nan = std::nan("");
     HIPCHK(hipMemcpy(c->latch, &nan, sizeof(double), hipMemcpyHostToDevice));
@@ -1032,7 +1036,7 @@ static int run_pairs(odo_ctx* c, int set, int n) {
         if (!(c->skip & 16))
         launch_ransac(st, P.good, P.n_good, P.n_matches, P.matches, xyz, c->kp_cap, 0, c->match_cap, c->rcfg,
                       c->latch, P.pair_valid, 20, nullptr, c->rscr[set], P.best_mask, c->mask_words, P.res, P.T12, n,
-                      0, P.pair_phase);
+                      0, P.pair_phase, c->h_open + set);
         tmark(c, 8, st);
         HIPCHK(hipEventRecord(c->ev_rb[set], st));
         // schedule 5: PnP follows RANSAC on the batch's own pair stream
@@ -1062,7 +1066,7 @@ static int run_pairs(odo_ctx* c, int set, int n) {
     if (!(c->skip & 2))
     launch_ransac(st, P.good, P.n_good, P.n_matches, P.matches, xyz, c->kp_cap, 0, c->match_cap, c->rcfg, c->latch,
                   P.pair_valid, 20, nullptr, c->rscr[set], P.best_mask, c->mask_words, P.res, P.T12, n, 2,
-                  P.pair_phase);
+                  P.pair_phase, c->h_open + set);
     tmark(c, 8, st);
     HIPCHK(hipEventRecord(c->ev_rb[set], st));
     HIPCHK(hipStreamWaitEvent(c->pnpb, c->ev_rb[set], 0));

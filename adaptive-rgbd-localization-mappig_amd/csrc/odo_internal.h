@@ -181,7 +181,7 @@ void launch_ransac(hipStream_t st, const void* good, const int* n_good, const in
                    const odo_dmatch* matches, const float* xyz, int kp_cap, int slot0, int match_cap, RansacCfg cfg,
                    const double* latch, const int* pair_valid, int min_matches, odo_rng* rng_io, void* scratch,
                    uint32_t* best_mask, int mask_words, odo_pair_result* res, float* T12, int npairs, int part = 0,
-                   int* phase = nullptr);
+                   int* phase = nullptr, int* open_hint = nullptr);
 size_t ransac_scratch_bytes(int npairs, int match_cap, int mask_words, const RansacCfg& cfg);
 void ransac_read_hyps(hipStream_t st, void* scratch, int match_cap, int mask_words, RansacCfg cfg, int h0, int h1,
                       double* err, int* cnt, float* T);

@@ -226,3 +226,20 @@ def test_bench_configuration_knn_splits(split):
         _compare(name + f" split {split}", c, odo, res, oracle, full=False)
     finally:
         odo.close()
+
+
+@pytest.mark.parametrize("name", ["cfg2_bench", "cfg4_icl_b256"])
+def test_bench_configuration_ransac_lanes(name):
+    """The second RANSAC launch on the lane-per-hypothesis kernel
+    (k_ransac_lanes) whatever the open-pair count (ODO_LANES_MIN_OPEN=1: from
+    the fifth batch on, a set whose previous batch left a pair open takes it):
+    every pair of the last batch bit-exact against the oracle."""
+    c = CONFIGS[name]
+    pkg = load_pkg()
+    bgr, dep, _ = sequence(c["L"], c["w"], c["h"], intrinsics=c["intr"], seed=c["scene"], closed_loop=True)
+    odo, cfg, res = _run_gpu(pkg, c, bgr, dep, env={"ODO_LANES_MIN_OPEN": "1"})
+    oracle = _oracle_cached(name, pkg, c, cfg, bgr, dep)
+    try:
+        _compare(name + " lanes", c, odo, res, oracle)
+    finally:
+        odo.close()
