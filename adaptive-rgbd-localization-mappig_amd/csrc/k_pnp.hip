@@ -792,14 +792,360 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
     for (int k = lane; k < ne; k += PNP_NT) mask[E.idx[k]] = (E.flags[k] & PE_OUT) ? 0 : 1;
 }
 
+
+// ---------------------------------------------------------------- one wave per pair
+// The same PnPSolver::Compute with ONE wave per pair: the batched path runs
+// 256 pairs at once beside the next batch's extraction, so what matters is
+// the PnP's footprint on the CUs, not one pair's latency. A wave needs no
+// barriers: edge sums are xor-butterflies, the normal equations are read
+// into scalar registers, and the PNP_K speculative Levenberg trials are
+// solved by the wave's four 16-lane groups at once (each group runs the LDLT,
+// exp map and composition of its lambda; the candidates are broadcast from
+// lanes 0/16/32/48). Edges are an AoS record per edge (two float4 + index)
+// in the pair's scratch, streamed each pass.
+struct PEdge1 {
+    float4* a;     // X.x X.y X.z info
+    float4* b;     // obs u v uR(0 mono) | flags (int bits)
+    int* idx;      // F2 keypoint index
+    double* chi4;  // chi2 of the stored _error per trial slot
+};
+ODO_INLINE PEdge1 pedge1_view(void* base, int cap, int p) {
+    char* bp = (char*)base + (size_t)p * (size_t)cap * PE_BYTES;
+    PEdge1 E;
+    E.chi4 = (double*)bp;
+    E.a = (float4*)(bp + (size_t)cap * 32);
+    E.b = E.a + cap;
+    E.idx = (int*)(E.b + cap);
+    return E;
+}
+
+// sum of v over the wave, the result in every lane (fixed butterfly)
+template <int NV>
+ODO_INLINE void wave_allsum(double (&v)[NV]) {
+    constexpr int LG = Pow2Pad<NV>::lg;
+    const double x = wave_sum_transposed(v);  // lane l: total of value l >> (6 - LG)
+#pragma unroll
+    for (int k = 0; k < NV; k++) v[k] = __shfl(x, k << (6 - LG));
+}
+
+__global__ void __launch_bounds__(64) k_pnp1(const int32_t* __restrict__ f2_src, const float* __restrict__ xyz,
+                                             const float* __restrict__ kun, const float* __restrict__ ur,
+                                             const int* __restrict__ nkp, int kp_cap, int slot0, FrameCalib cal,
+                                             const float* __restrict__ T12, const int* __restrict__ pair_valid,
+                                             const int* __restrict__ n_matches, int min_matches, void* edges_g,
+                                             odo_pair_result* __restrict__ res, uint8_t* __restrict__ inlier_mask,
+                                             const int* __restrict__ sel, int sel_val) {
+    __builtin_amdgcn_s_setprio(ODO_PNP_PRIO);
+    const int p = blockIdx.x;
+    if (sel && sel[p] != sel_val) return;
+    const int lane = threadIdx.x;
+    odo_pair_result* R = res + p;
+    const int s1 = slot0 + p, s2 = slot0 + p + 1;
+    const int n2 = nkp[s2];
+    uint8_t* mask = inlier_mask + (size_t)p * kp_cap;
+    for (int i = lane; i < n2; i += 64) mask[i] = 0;
+    const float* T0 = T12 + (size_t)p * 16;
+    if (lane < 16) R->Tcw[lane] = T0[lane];
+    if (lane == 0) R->pnp_inliers = 0;
+    if (!pair_valid[p] || n_matches[p] < min_matches) return;
+    // ---- edges: F2 keypoints holding a landmark, index order (pnpsolver.cpp:57-135)
+    const int32_t* src = f2_src + (size_t)p * kp_cap;
+    const float* X1 = xyz + (size_t)s1 * kp_cap * 3;
+    const float* K2 = kun + (size_t)s2 * kp_cap * 2;
+    const float* U2 = ur + (size_t)s2 * kp_cap;
+    PEdge1 E = pedge1_view(edges_g, kp_cap, p);
+    int ne = 0;
+    for (int c0 = 0; c0 < n2; c0 += 64) {
+        const int i = c0 + lane;
+        const bool has = i < n2 && src[i] >= 0;
+        const uint64_t bal = __ballot(has);
+        if (has) {
+            const int k = ne + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
+            const int s = src[i];
+            const float zw = X1[3 * s + 2];
+            const float urv = U2[i];
+            const bool st = !(urv < 0);
+            E.a[k] = make_float4(X1[3 * s], X1[3 * s + 1], zw, 1.0f / (zw * zw));
+            E.b[k] = make_float4(K2[2 * i], K2[2 * i + 1], st ? urv : 0.f,
+                                 __int_as_float((st ? PE_STEREO : 0) | PE_ROBUST));
+            E.idx[k] = i;
+        }
+        ne += __popcll(bal);
+    }
+    if (ne < 3) {
+        for (int k = lane; k < ne; k += 64) mask[E.idx[k]] = 1;  // SetInlier at edge creation
+        return;
+    }
+    const PnPCam cam{(double)cal.fx, (double)cal.fy, (double)cal.cx, (double)cal.cy, (double)cal.mbf};
+    const double dMono = (double)(float)sqrt(5.991), dStereo = (double)(float)sqrt(7.815);  // pnpsolver.cpp:51-52
+    SE3 T0s;
+    {
+        double R0[3][3], t0[3];
+        for (int i = 0; i < 3; i++) {
+            for (int j = 0; j < 3; j++) R0[i][j] = (double)T0[i * 4 + j];
+            t0[i] = (double)T0[i * 4 + 3];
+        }
+        T0s.q = quat_from_R(R0);
+        for (int i = 0; i < 3; i++) T0s.t[i] = t0[i];
+        normalize_rot(T0s);
+    }
+    const float chi2Mono = 5.991f, chi2Stereo = 7.815f;
+    int nBad = 0;
+    SE3 T = T0s;
+    int last_slot = 0;
+    const int grp = lane >> 4;  // Levenberg trial of this lane group
+    for (int it = 0; it < 4; it++) {
+        T = T0s;  // vSE3->setEstimate(pFrame->GetPose()) (pnpsolver.cpp:150)
+        double lambda = 0, ni = 2;
+        for (int iter = 0; iter < 10; iter++) {
+            // computeActiveErrors + activeRobustChi2 + buildSystem at T
+            double acc[28];
+#pragma unroll
+            for (int k = 0; k < 28; k++) acc[k] = 0;
+            for (int k = lane; k < ne; k += 64) {
+                const float4 ea = E.a[k], eb = E.b[k];
+                const uint8_t fl = (uint8_t)__float_as_int(eb.w);
+                if (fl & PE_OUT) continue;
+                const bool st = fl & PE_STEREO;
+                const double Xw[3] = {ea.x, ea.y, ea.z};
+                const double ob[3] = {eb.x, eb.y, eb.z};
+                const double info = ea.w;
+                double Xc[3], e[3];
+                se3_map(T, Xw, Xc);
+                edge_err(Xc, ob, st, cam, e);
+                const double c2 = chi2_of(e, info, st);
+                double rho[3] = {c2, 1.0, 0.0};
+                if (fl & PE_ROBUST) huber_rho(st ? dStereo : dMono, c2, rho);
+                acc[27] += rho[0];
+                const double x = Xc[0], y = Xc[1], invz = 1.0 / Xc[2], invz_2 = invz * invz;
+                double J[3][6];
+                J[0][0] = x * y * invz_2 * cam.fx;
+                J[0][1] = -(1 + (x * x * invz_2)) * cam.fx;
+                J[0][2] = y * invz * cam.fx;
+                J[0][3] = -invz * cam.fx;
+                J[0][4] = 0;
+                J[0][5] = x * invz_2 * cam.fx;
+                J[1][0] = (1 + y * y * invz_2) * cam.fy;
+                J[1][1] = -x * y * invz_2 * cam.fy;
+                J[1][2] = -x * invz * cam.fy;
+                J[1][3] = 0;
+                J[1][4] = -invz * cam.fy;
+                J[1][5] = y * invz_2 * cam.fy;
+                J[2][0] = st ? J[0][0] - cam.bf * y * invz_2 : 0.0;
+                J[2][1] = st ? J[0][1] + cam.bf * x * invz_2 : 0.0;
+                J[2][2] = st ? J[0][2] : 0.0;
+                J[2][3] = st ? J[0][3] : 0.0;
+                J[2][4] = 0;
+                J[2][5] = st ? J[0][5] - cam.bf * invz_2 : 0.0;
+                const double r1 = rho[1];
+                const double wo = r1 * info;
+                int h = 0;
+#pragma unroll
+                for (int a = 0; a < 6; a++) {
+                    double sb = 0;
+#pragma unroll
+                    for (int kk = 0; kk < 3; kk++) sb += J[kk][a] * (info * e[kk]);
+                    acc[21 + a] -= r1 * sb;
+#pragma unroll
+                    for (int cc = a; cc < 6; cc++) {
+                        double hh = 0;
+#pragma unroll
+                        for (int kk = 0; kk < 3; kk++) hh += J[kk][a] * wo * J[kk][cc];
+                        acc[h++] += hh;
+                    }
+                }
+            }
+            wave_allsum<28>(acc);
+            double curChi = acc[27];
+            if (iter == 0) {
+                double mx = 0;  // diagonal of the packed upper triangle: 0, 6, 11, 15, 18, 20
+                mx = fmax(fabs(acc[0]), mx);
+                mx = fmax(fabs(acc[6]), mx);
+                mx = fmax(fabs(acc[11]), mx);
+                mx = fmax(fabs(acc[15]), mx);
+                mx = fmax(fabs(acc[18]), mx);
+                mx = fmax(fabs(acc[20]), mx);
+                lambda = 1e-5 * mx;
+                ni = 2;
+            }
+            // ---- OptimizationAlgorithmLevenberg::solve trial loop, PNP_K trials per pass
+            double rho = 0;
+            int qmax = 0;
+            bool trials_done = false;
+            while (!trials_done) {
+                const int K = min(PNP_K, 10 - qmax);
+                double lam[PNP_K], nis[PNP_K];
+                {
+                    double l = lambda, n_ = ni;
+#pragma unroll
+                    for (int k = 0; k < PNP_K; k++) {
+                        lam[k] = l;
+                        nis[k] = n_;
+                        l *= n_;
+                        n_ *= 2;
+                    }
+                }
+                // lane group grp solves trial grp
+                double lw = lam[0];
+#pragma unroll
+                for (int k = 1; k < PNP_K; k++)
+                    if (grp == k) lw = lam[k];
+                double Hl[6][6], b[6];
+                {
+                    int h = 0;
+#pragma unroll
+                    for (int a = 0; a < 6; a++)
+#pragma unroll
+                        for (int cc = a; cc < 6; cc++) {
+                            Hl[a][cc] = acc[h];
+                            Hl[cc][a] = acc[h];
+                            h++;
+                        }
+#pragma unroll
+                    for (int a = 0; a < 6; a++) b[a] = acc[21 + a];
+                }
+#pragma unroll
+                for (int j = 0; j < 6; j++) Hl[j][j] += lw;
+                double x[6] = {0, 0, 0, 0, 0, 0};
+                const bool ok2 = ldlt_solve6(Hl, b, x);
+                const SE3 Tk = se3_mul(se3_exp(x), T);
+                double scale = 0;
+                for (int j = 0; j < 6; j++) scale += x[j] * (lw * x[j] + b[j]);
+                scale += 1e-3;
+                SE3 Tc[PNP_K];
+                double sc[PNP_K];
+                bool okc[PNP_K];
+#pragma unroll
+                for (int k = 0; k < PNP_K; k++) {
+                    const int sl = 16 * k;
+                    Tc[k].q = Quat{__shfl(Tk.q.x, sl), __shfl(Tk.q.y, sl), __shfl(Tk.q.z, sl), __shfl(Tk.q.w, sl)};
+                    Tc[k].t[0] = __shfl(Tk.t[0], sl);
+                    Tc[k].t[1] = __shfl(Tk.t[1], sl);
+                    Tc[k].t[2] = __shfl(Tk.t[2], sl);
+                    sc[k] = __shfl(scale, sl);
+                    okc[k] = __shfl(ok2 ? 1 : 0, sl) != 0;
+                }
+                // computeActiveErrors + activeRobustChi2 at every candidate
+                double chi[PNP_K];
+#pragma unroll
+                for (int k = 0; k < PNP_K; k++) chi[k] = 0;
+                for (int e = lane; e < ne; e += 64) {
+                    const float4 ea = E.a[e], eb = E.b[e];
+                    const uint8_t fl = (uint8_t)__float_as_int(eb.w);
+                    if (fl & PE_OUT) continue;
+                    const double Xw[3] = {ea.x, ea.y, ea.z};
+                    const double ob[3] = {eb.x, eb.y, eb.z};
+                    const double info = ea.w;
+#pragma unroll
+                    for (int k = 0; k < PNP_K; k++) {
+                        if (k >= K) break;
+                        double c2;
+                        chi[k] += edge_robust_chi(Tc[k], Xw, ob, info, fl, cam, dMono, dStereo, c2);
+                        E.chi4[4 * e + k] = c2;
+                    }
+                }
+                wave_allsum<PNP_K>(chi);
+                // replay the trials in order
+#pragma unroll
+                for (int k = 0; k < PNP_K; k++) {
+                    if (k >= K || trials_done) break;
+                    double tempChi = chi[k];
+                    if (!okc[k]) tempChi = 1.7976931348623157e308;
+                    rho = curChi - tempChi;
+                    rho /= sc[k];
+                    last_slot = k;
+                    qmax++;
+                    if (rho > 0 && isfinite(tempChi)) {
+                        double alpha = 1. - pow((2 * rho - 1), 3);
+                        alpha = fmin(alpha, 2. / 3.);
+                        const double sf = fmax(1. / 3., alpha);
+                        lambda = lam[k] * sf;
+                        ni = 2;
+                        curChi = tempChi;
+                        T = Tc[k];
+                        trials_done = true;
+                    } else {
+                        lambda = lam[k] * nis[k];  // T stays at the backup
+                        ni = nis[k] * 2;
+                        if (!(rho < 0 && qmax < 10)) trials_done = true;
+                    }
+                }
+            }
+            if (qmax == 10 || rho == 0) break;
+        }
+        // ---- classification (pnpsolver.cpp:157-201)
+        int bad = 0;
+        for (int k = lane; k < ne; k += 64) {
+            float4 eb = E.b[k];
+            uint8_t fl = (uint8_t)__float_as_int(eb.w);
+            const bool st = fl & PE_STEREO;
+            double c2 = E.chi4[4 * k + last_slot];
+            if (fl & PE_OUT) {  // IsOutlier: e->computeError() at the current estimate
+                const float4 ea = E.a[k];
+                const double Xw[3] = {ea.x, ea.y, ea.z};
+                const double ob[3] = {eb.x, eb.y, eb.z};
+                double Xc[3], e[3];
+                se3_map(T, Xw, Xc);
+                edge_err(Xc, ob, st, cam, e);
+                c2 = chi2_of(e, (double)ea.w, st);
+                E.chi4[4 * k + last_slot] = c2;
+            }
+            const float chi2 = (float)c2;
+            if (chi2 > (st ? chi2Stereo : chi2Mono)) {
+                fl |= PE_OUT;
+                bad++;
+            } else {
+                fl &= ~PE_OUT;
+            }
+            if (it == 2) fl &= ~PE_ROBUST;
+            eb.w = __int_as_float((int)fl);
+            E.b[k] = eb;
+        }
+        double bd[1] = {(double)bad};
+        wave_allsum<1>(bd);
+        nBad = (int)bd[0];
+        if (ne < 10) break;
+    }
+    if (lane == 0) {
+        double Rm[3][3];
+        quat_to_R(T.q, Rm);
+        for (int i = 0; i < 3; i++) {
+            for (int j = 0; j < 3; j++) R->Tcw[i * 4 + j] = (float)Rm[i][j];
+            R->Tcw[i * 4 + 3] = (float)T.t[i];
+        }
+        R->Tcw[12] = R->Tcw[13] = R->Tcw[14] = 0.f;
+        R->Tcw[15] = 1.f;
+        R->pnp_inliers = ne - nBad;
+    }
+    for (int k = lane; k < ne; k += 64)
+        mask[E.idx[k]] = ((uint8_t)__float_as_int(E.b[k].w) & PE_OUT) ? 0 : 1;
+}
+
 }  // namespace odo
 
 namespace odo {
 size_t pnp_edge_bytes() { return PE_BYTES; }
+// The 4-wave workgroup per pair (k_pnp) by default. ODO_PNP_WAVES=1 selects
+// k_pnp1 (one wave per pair: a quarter of the SIMDs occupied), measured
+// slower: PnP 1.66 vs 0.72 ms alone per 256 pairs, step 2.61 vs 2.50 ms, one
+// frame 0.65 vs 0.49 ms — the solver is latency-bound per pair, and the freed
+// SIMDs do not buy back the 4x longer edge passes.
+static int pnp_waves() {
+    static int r = [] {
+        const char* e = getenv("ODO_PNP_WAVES");
+        return e && atoi(e) == 1 ? 1 : 4;
+    }();
+    return r;
+}
 void launch_pnp(hipStream_t st, const int32_t* f2_src, const float* xyz, const float* kun, const float* ur,
                 const int* nkp, int kp_cap, int slot0, FrameCalib cal, const float* T12, const int* pair_valid,
                 const int* n_matches, int min_matches, void* edges, odo_pair_result* res, uint8_t* inlier_mask,
                 int npairs, const int* sel, int sel_val) {
+    if (pnp_waves() == 1) {
+        hipLaunchKernelGGL(k_pnp1, dim3(npairs), dim3(64), 0, st, f2_src, xyz, kun, ur, nkp, kp_cap, slot0, cal, T12,
+                           pair_valid, n_matches, min_matches, edges, res, inlier_mask, sel, sel_val);
+        return;
+    }
     hipLaunchKernelGGL(k_pnp, dim3(npairs), dim3(PNP_NT), 0, st, f2_src, xyz, kun, ur, nkp, kp_cap, slot0, cal, T12,
                        pair_valid, n_matches, min_matches, edges, res, inlier_mask, sel, sel_val);
 }
