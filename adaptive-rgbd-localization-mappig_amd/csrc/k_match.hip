@@ -5,6 +5,8 @@
 //                 ratio test + landmark bookkeeping (matcher.cpp:62-85),
 //                 Ransac good-match filter + std::sort (ransac.cpp:175-199)
 //   k_latch       Ransac::DepthCovariance first-call latch (ransac.cpp:416-421)
+#include <type_traits>
+
 #include "odo_device.h"
 #include "odo_internal.h"
 
@@ -253,18 +255,22 @@ ODO_INLINE kmx_v4i kmx_expand16(uint32_t h) {
 #pragma unroll
     for (int j = 0; j < 4; j++) {
         const uint32_t nib = __builtin_amdgcn_ubfe(h, 4 * j, 4);
-        const uint32_t v = __umul24(nib, 0x204081u) & 0x01010101u;  // bit i -> byte i
-        r[j] = (int)((v << 7) | 0x40404040u);
+        // asm: left to itself the compiler folds the << 7 into the constant
+        // (v_mul_lo_u32, quarter rate) or splits the shift-or in two
+        uint32_t m, b;
+        asm("v_mul_u32_u24 %0, %1, %2" : "=v"(m) : "v"(nib), "v"(0x204081u));
+        asm("v_lshl_or_b32 %0, %1, 7, %2" : "=v"(b) : "v"(m & 0x01010101u), "s"(0x40404040u));  // bit i -> byte i
+        r[j] = (int)b;
     }
     return r;
 }
-ODO_INLINE int med3_i32(int a, int b, int c) {
-    int r;
-    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
+// v_med3_i32 by pattern (not inline asm: its operands come straight from MFMA
+// results, and the hazard recognizer inserts the MFMA-to-VALU wait states only
+// for instructions it sees)
+ODO_INLINE int med3_i32(int a, int b, int c) { return max(min(a, b), min(max(a, b), c)); }
 
-__global__ void __launch_bounds__(256) k_knn2_mx(const uint8_t* __restrict__ qdesc, const int* __restrict__ qn,
+// (256, 3): 168 VGPRs, three workgroups per CU (measured 137 us vs 144 us at two)
+__global__ void __launch_bounds__(256, 3) k_knn2_mx(const uint8_t* __restrict__ qdesc, const int* __restrict__ qn,
                                                  size_t q_stride, const uint8_t* __restrict__ tdesc,
                                                  const int* __restrict__ tn, size_t t_stride,
                                                  int2* __restrict__ out_idx, int2* __restrict__ out_dist,
@@ -347,37 +353,54 @@ __global__ void __launch_bounds__(256) k_knn2_mx(const uint8_t* __restrict__ qde
         }
         __syncthreads();
         const bool live = qbase < nq;  // wave-uniform: this wave holds queries
+        // One chunk of 64 trains against the wave's 64 queries: 4 tiles of 16
+        // trains, each 4 k-steps x 4 query tiles = 16 MFMAs. The 4 A reads of
+        // tile tt + 1 are issued before tile tt's MFMAs, so the LDS latency
+        // hides behind them. A full chunk starts each accumulator at its train
+        // index; only the last, partial chunk selects KMX_BIG for the pad rows.
+        auto chunk = [&](const uint8_t* src, int cbase, auto full_tag) {
+            constexpr bool full = decltype(full_tag)::value;
+            kmx_v4i A[2][4];
+#pragma unroll
+            for (int c = 0; c < 4; c++)
+                A[0][c] = *reinterpret_cast<const kmx_v4i*>(src + col * 256 + (((4 * c + grp) ^ col) << 4));
+#pragma unroll
+            for (int tt = 0; tt < KMX_T / 16; tt++) {
+                const int cur = tt & 1;
+                if (tt + 1 < KMX_T / 16) {
+                    const int r = (tt + 1) * 16 + col;  // train row of this lane's next A operand
+#pragma unroll
+                    for (int c = 0; c < 4; c++)
+                        A[cur ^ 1][c] = *reinterpret_cast<const kmx_v4i*>(src + r * 256 + (((4 * c + grp) ^ col) << 4));
+                }
+                kmx_v4i C;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const int idx = cbase + tt * 16 + i;  // cbase = chunk start + 4 grp
+                    C[i] = full ? idx : (idx < nt ? idx : KMX_BIG);
+                }
+                kmx_v4i acc[4];
+#pragma unroll
+                for (int c = 0; c < 4; c++)
+#pragma unroll
+                    for (int qt = 0; qt < 4; qt++)
+                        acc[qt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[cur][c], B[qt][c], c == 0 ? C : acc[qt], 0, 0, 0);
+#pragma unroll
+                for (int qt = 0; qt < 4; qt++)
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        k1[qt] = med3_i32(k0[qt], k1[qt], acc[qt][i]);
+                        k0[qt] = min(k0[qt], acc[qt][i]);
+                    }
+            }
+        };
         for (int ch = 0; ch < nch; ch++) {
             const int buf = ch & 1;
             if (ch + 1 < nch) fetch(ch + 1);
             if (live) {
-                const uint8_t* src = s_tr[buf];
-#pragma unroll
-                for (int tt = 0; tt < KMX_T / 16; tt++) {
-                    const int r = tt * 16 + col;  // train row of this lane's A operand
-                    kmx_v4i C;
-#pragma unroll
-                    for (int i = 0; i < 4; i++) {
-                        const int idx = ch * KMX_T + tt * 16 + 4 * grp + i;
-                        C[i] = idx < nt ? idx : KMX_BIG;
-                    }
-                    kmx_v4i acc[4];
-#pragma unroll
-                    for (int c = 0; c < 4; c++) {
-                        const int u = 4 * c + grp;
-                        const kmx_v4i A = *reinterpret_cast<const kmx_v4i*>(src + r * 256 + ((u ^ col) << 4));
-#pragma unroll
-                        for (int qt = 0; qt < 4; qt++)
-                            acc[qt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B[qt][c], c == 0 ? C : acc[qt], 0, 0, 0);
-                    }
-#pragma unroll
-                    for (int qt = 0; qt < 4; qt++)
-#pragma unroll
-                        for (int i = 0; i < 4; i++) {
-                            k1[qt] = med3_i32(k0[qt], k1[qt], acc[qt][i]);
-                            k0[qt] = min(k0[qt], acc[qt][i]);
-                        }
-                }
+                const int cbase = ch * KMX_T + 4 * grp;
+                if ((ch + 1) * KMX_T <= nt) chunk(s_tr[buf], cbase, std::true_type{});
+                else chunk(s_tr[buf], cbase, std::false_type{});
             }
             if (ch + 1 < nch) stage(buf ^ 1);
             __syncthreads();
@@ -405,6 +428,207 @@ __global__ void __launch_bounds__(256) k_knn2_mx(const uint8_t* __restrict__ qde
             const size_t o = (size_t)p * out_stride + qi;
             out_idx[o] = make_int2(e0 ? -1 : (u0 & 8191), e1 ? -1 : (u1 & 8191));
             out_dist[o] = make_int2(e0 ? 0x7FFFFFFF : (u0 >> 13), e1 ? 0x7FFFFFFF : (u1 >> 13));
+        }
+    }
+}
+
+// ------------------------------------------------------------ FP4 form
+// The same sign-vector product on v_mfma_scale_f32_16x16x128_f8f6f4 with e2m1
+// operands: +1.0 (nibble 0x2) for a 0 bit, -1.0 (0xA) for a 1 bit, the query
+// signs negated, unit scales. A 256-bit comparison is two k-steps of 128; the
+// f32 sum is 2H - 256, exact, and the accumulator starts at 256 + idx / 8192, so
+// the result is the key 2H + idx / 8192 (22 significant bits, exact in f32, every
+// partial sum too), ordered as (H, idx). The keys are non-negative, so their bit
+// patterns order as unsigned integers: top-2 is v_min_u32 + v_med3_u32 on the
+// raw accumulator (no NaN canonicalisation), and the accumulator start is an
+// integer add (the bits of 256 + idx / 8192 are 0x43800000 + 4 idx). Half the MFMAs of the
+// int8 form, and a cheap expansion: the sign bit of nibble m of output dword j
+// is descriptor bit j + 4m of the 32-bit word, so one word becomes its four
+// dwords with one and + one shift-or each (A and B use the same permutation of
+// the 256 bits, which leaves the dot product unchanged).
+#define KF_T 128         // trains per LDS chunk (128 B per expanded train)
+#define KF_PAD 0x45800000u    // 4096.0f: accumulator start of a train slot past the end
+#define KF_EMPTY 0x46000000u  // 8192.0f
+#define KF_BASE 0x43800000u   // 256.0f
+#define KF_NONE 0x44800000u   // 1024.0f: keys at or above are no train
+typedef float kf_v4f __attribute__((ext_vector_type(4)));
+typedef int kf_v8i __attribute__((ext_vector_type(8)));
+
+// one 32-bit descriptor word -> 32 e2m1 signs in 4 dwords
+ODO_INLINE kmx_v4i kf_expand32(uint32_t w) {
+    kmx_v4i r;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        uint32_t b;
+        asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(b) : "v"(w & (0x11111111u << j)), "i"(3 - j), "s"(0x22222222u));
+        r[j] = (int)b;
+    }
+    return r;
+}
+ODO_INLINE kf_v8i kf_op(kmx_v4i v) {
+    kf_v8i r;
+    r[0] = v[0], r[1] = v[1], r[2] = v[2], r[3] = v[3];
+    r[4] = r[5] = r[6] = r[7] = 0;
+    return r;
+}
+
+__global__ void __launch_bounds__(256, 3) k_knn2_f4(const uint8_t* __restrict__ qdesc, const int* __restrict__ qn,
+                                                    size_t q_stride, const uint8_t* __restrict__ tdesc,
+                                                    const int* __restrict__ tn, size_t t_stride,
+                                                    int2* __restrict__ out_idx, int2* __restrict__ out_dist,
+                                                    size_t out_stride, const int32_t* __restrict__ qlist,
+                                                    const int* __restrict__ qcnt, size_t ql_stride, int npairs) {
+    __builtin_amdgcn_s_setprio(ODO_KNN_PRIO);
+    __shared__ __attribute__((aligned(16))) uint8_t s_tr[2][KF_T * 128];
+    __shared__ int s_pre[KNN_MAXP + 1];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int grp = lane >> 4, col = lane & 15;
+    for (int i = tid; i < npairs; i += 256) {
+        const int nq = qlist ? qcnt[i] : qn[i];
+        s_pre[i + 1] = (nq + KMX_Q - 1) / KMX_Q;
+    }
+    if (tid == 0) s_pre[0] = 0;
+    __syncthreads();
+    if (tid == 0)
+        for (int i = 1; i <= npairs; i++) s_pre[i] += s_pre[i - 1];
+    __syncthreads();
+    const int nact = s_pre[npairs];
+    // staging role of this thread: train st_t of a chunk, words 4 st_h .. 4 st_h + 3
+    const int st_t = tid >> 1, st_h = tid & 1;
+    for (int g = blockIdx.x; g < nact; g += gridDim.x) {
+        int lo = 0, hi = npairs;  // last pair with s_pre[p] <= g
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (s_pre[mid] <= g) lo = mid; else hi = mid;
+        }
+        const int p = lo, qb = g - s_pre[p];
+        const int nq = qlist ? qcnt[p] : qn[p];
+        const int nt = tn[p];
+        const uint8_t* Q = qdesc + (size_t)p * q_stride;
+        const uint8_t* T = tdesc + (size_t)p * t_stride;
+        const int qbase = qb * KMX_Q + wave * 64;
+        // ---- B operand: this wave's 64 queries, negated signs
+        kmx_v4i B[4][2];
+#pragma unroll
+        for (int qt = 0; qt < 4; qt++) {
+            const int qpos = qbase + qt * 16 + col;
+            uint4 a = make_uint4(0, 0, 0, 0), b = make_uint4(0, 0, 0, 0);
+            if (qpos < nq) {
+                const int qi = qlist ? qlist[(size_t)p * ql_stride + qpos] : qpos;
+                a = reinterpret_cast<const uint4*>(Q + (size_t)qi * 32)[0];
+                b = reinterpret_cast<const uint4*>(Q + (size_t)qi * 32)[1];
+            }
+            const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+            for (int c = 0; c < 2; c++) {
+                uint32_t h = 0;  // word 4 c + grp of k-step c, lane group grp
+#pragma unroll
+                for (int k = 0; k < 8; k++)
+                    if (k == 4 * c + grp) h = w[k];
+                B[qt][c] = kf_expand32(~h);
+            }
+        }
+        uint32_t k0[4], k1[4];
+#pragma unroll
+        for (int qt = 0; qt < 4; qt++) k0[qt] = k1[qt] = KF_EMPTY;
+        const int nch = (nt + KF_T - 1) / KF_T;
+        uint4 pf = make_uint4(0, 0, 0, 0);
+        auto fetch = [&](int ch) {
+            const int t = ch * KF_T + st_t;
+            pf = t < nt ? *reinterpret_cast<const uint4*>(T + (size_t)t * 32 + 16 * st_h) : make_uint4(0, 0, 0, 0);
+        };
+        auto stage = [&](int buf) {
+            uint8_t* dst = s_tr[buf] + st_t * 128;
+            const uint32_t w[4] = {pf.x, pf.y, pf.z, pf.w};
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int u = 4 * st_h + k;
+                *reinterpret_cast<kmx_v4i*>(dst + ((u ^ (st_t & 7)) << 4)) = kf_expand32(w[k]);
+            }
+        };
+        __syncthreads();  // the previous item's last chunk is no longer read
+        if (nch > 0) {
+            fetch(0);
+            stage(0);
+        }
+        __syncthreads();
+        const bool live = qbase < nq;  // wave-uniform: this wave holds queries
+        // one chunk of 128 trains: 8 tiles of 16 trains x 2 k-steps x 4 query tiles
+        auto chunk = [&](const uint8_t* src, int cbase, auto full_tag) {
+            constexpr bool full = decltype(full_tag)::value;
+            kmx_v4i A[2][2];
+#pragma unroll
+            for (int c = 0; c < 2; c++)
+                A[0][c] = *reinterpret_cast<const kmx_v4i*>(src + col * 128 + (((4 * c + grp) ^ (col & 7)) << 4));
+#pragma unroll
+            for (int tt = 0; tt < KF_T / 16; tt++) {
+                const int cur = tt & 1;
+                if (tt + 1 < KF_T / 16) {
+                    const int r = (tt + 1) * 16 + col;  // train row of this lane's next A operand
+#pragma unroll
+                    for (int c = 0; c < 2; c++)
+                        A[cur ^ 1][c] = *reinterpret_cast<const kmx_v4i*>(src + r * 128 + (((4 * c + grp) ^ (col & 7)) << 4));
+                }
+                kmx_v4i Cb;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const int idx = cbase + tt * 16 + i;  // cbase = chunk start + 4 grp
+                    Cb[i] = (full || idx < nt) ? (int)(KF_BASE + 4u * (uint32_t)idx) : (int)KF_PAD;
+                }
+                const kf_v4f C = __builtin_bit_cast(kf_v4f, Cb);
+                kf_v4f acc[4];
+#pragma unroll
+                for (int c = 0; c < 2; c++)
+#pragma unroll
+                    for (int qt = 0; qt < 4; qt++)
+                        acc[qt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+                            kf_op(A[cur][c]), kf_op(B[qt][c]), c == 0 ? C : acc[qt], 4, 4, 0, 127, 0, 127);
+#pragma unroll
+                for (int qt = 0; qt < 4; qt++)
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const float xf = acc[qt][i];
+                        const uint32_t x = __float_as_uint(xf);
+                        k1[qt] = max(min(k0[qt], k1[qt]), min(max(k0[qt], k1[qt]), x));  // v_med3_u32
+                        k0[qt] = min(k0[qt], x);
+                    }
+            }
+        };
+        for (int ch = 0; ch < nch; ch++) {
+            const int buf = ch & 1;
+            if (ch + 1 < nch) fetch(ch + 1);
+            if (live) {
+                const int cbase = ch * KF_T + 4 * grp;
+                if ((ch + 1) * KF_T <= nt) chunk(s_tr[buf], cbase, std::true_type{});
+                else chunk(s_tr[buf], cbase, std::false_type{});
+            }
+            if (ch + 1 < nch) stage(buf ^ 1);
+            __syncthreads();
+        }
+        if (!live) continue;
+        // ---- merge the 4 lane groups holding each query, then lane l writes query qbase + l
+#pragma unroll
+        for (int m = 16; m <= 32; m <<= 1)
+#pragma unroll
+            for (int qt = 0; qt < 4; qt++) {
+                const uint32_t p0 = __shfl_xor(k0[qt], m), p1 = __shfl_xor(k1[qt], m);
+                const uint32_t n1 = min(max(k0[qt], p0), min(k1[qt], p1));
+                k0[qt] = min(k0[qt], p0);
+                k1[qt] = n1;
+            }
+        uint32_t a0 = k0[0], a1 = k1[0];
+#pragma unroll
+        for (int qt = 1; qt < 4; qt++)
+            if (grp == qt) a0 = k0[qt], a1 = k1[qt];
+        const int qpos = qbase + lane;
+        if (qpos < nq) {
+            const int qi = qlist ? qlist[(size_t)p * ql_stride + qpos] : qpos;
+            // no train in the slot: a pad row's key is 4096 + (2H - 256), real keys are < 513
+            const bool e0 = a0 >= KF_NONE, e1 = a1 >= KF_NONE;
+            const int u0 = (int)(__uint_as_float(a0) * 8192.0f), u1 = (int)(__uint_as_float(a1) * 8192.0f);  // 16384 H + idx
+            const size_t o = (size_t)p * out_stride + qi;
+            out_idx[o] = make_int2(e0 ? -1 : (u0 & 8191), e1 ? -1 : (u1 & 8191));
+            out_dist[o] = make_int2(e0 ? 0x7FFFFFFF : (u0 >> 14), e1 ? 0x7FFFFFFF : (u1 >> 14));
         }
     }
 }
@@ -1116,28 +1340,35 @@ void launch_knn2(hipStream_t st, const uint8_t* q, const int* qn, size_t q_strid
 }
 void launch_knn2_mx(hipStream_t st, const uint8_t* q, const int* qn, size_t q_stride, const uint8_t* t, const int* tn,
                     size_t t_stride, int2* idx, int2* dist, size_t out_stride, int max_q, int npairs,
-                    const int32_t* qlist, const int* qcnt, size_t ql_stride) {
-    static int resident = 0;  // workgroups of one full round (occupancy x CUs)
-    if (!resident) {
+                    const int32_t* qlist, const int* qcnt, size_t ql_stride, int fmt) {
+    const bool f4 = fmt == KNN_FMT_F4;
+    static int resident[2] = {0, 0};  // workgroups of one full round (occupancy x CUs), per kernel
+    if (!resident[f4]) {
         int dev = 0, cus = 256, per_cu = 0;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_knn2_mx, 256, 0);
-        resident = std::max(1, per_cu) * cus;
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f4 ? (const void*)k_knn2_f4 : (const void*)k_knn2_mx,
+                                                           256, 0);
+        resident[f4] = std::max(1, per_cu) * cus;
     }
     if (npairs <= 0 || max_q <= 0) return;
     if (npairs > KNN_MAXP) {  // the item prefix is per launch: split larger batches
         launch_knn2_mx(st, q, qn, q_stride, t, tn, t_stride, idx, dist, out_stride, max_q, KNN_MAXP, qlist, qcnt,
-                       ql_stride);
+                       ql_stride, fmt);
         launch_knn2_mx(st, q + KNN_MAXP * q_stride, qn + KNN_MAXP, q_stride, t + KNN_MAXP * t_stride, tn + KNN_MAXP,
                        t_stride, idx + KNN_MAXP * out_stride, dist + KNN_MAXP * out_stride, out_stride, max_q,
                        npairs - KNN_MAXP, qlist ? qlist + KNN_MAXP * ql_stride : nullptr,
-                       qcnt ? qcnt + KNN_MAXP : nullptr, ql_stride);
+                       qcnt ? qcnt + KNN_MAXP : nullptr, ql_stride, fmt);
         return;
     }
     const int items = npairs * ((max_q + KMX_Q - 1) / KMX_Q);  // upper bound; the kernel counts the real ones
-    hipLaunchKernelGGL(k_knn2_mx, dim3(std::min(items, resident)), dim3(256), 0, st, q, qn, q_stride, t, tn, t_stride,
-                       idx, dist, out_stride, qlist, qcnt, ql_stride, npairs);
+    const dim3 grid(std::min(items, resident[f4]));
+    if (f4)
+        hipLaunchKernelGGL(k_knn2_f4, grid, dim3(256), 0, st, q, qn, q_stride, t, tn, t_stride, idx, dist, out_stride,
+                           qlist, qcnt, ql_stride, npairs);
+    else
+        hipLaunchKernelGGL(k_knn2_mx, grid, dim3(256), 0, st, q, qn, q_stride, t, tn, t_stride, idx, dist, out_stride,
+                           qlist, qcnt, ql_stride, npairs);
 }
 void launch_vo_lm(hipStream_t st, const float* xyz, const int* nkp, int kp_cap, int slot0, float th_depth_m,
                   uint32_t* lm_bits, int lm_words, int32_t* qlist, int* qcnt, int npairs) {

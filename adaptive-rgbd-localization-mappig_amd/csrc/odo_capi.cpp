@@ -185,9 +185,11 @@ struct odo_ctx {
     int* qcnt[NSETS] = {};
     int lm_words = 0;
     int knn_split = 2;  // kNN-2 train splits per query block (ODO_KNN_SPLIT): more waves for short query lists
-    // kNN-2 on the matrix cores (k_knn2_mx, exact int8 sign-vector products;
-    // ODO_KNN_MFMA=0 selects the VALU xor/popcount kernel k_knn2)
-    bool knn_mx = true;
+    // kNN-2 form (ODO_KNN_MFMA): 0 the VALU xor/popcount kernel k_knn2, 1 exact
+    // int8 sign-vector products on the matrix cores (k_knn2_mx), 2 the same on
+    // FP4 (e2m1 +-1) operands (k_knn2_f4, the default: 97 us vs 137-150 us for
+    // the 256-pair bench launch alone)
+    int knn_mx = KNN_FMT_F4;
     uint64_t* sort_scratch = nullptr;
     double* latch = nullptr;
     void* rscr[NSETS] = {};  // RANSAC scratch per frame set
@@ -627,7 +629,7 @@ static int alloc_buffers(odo_ctx* c) {
     }
     c->lm_words = (c->kp_cap + 31) / 32;
     if (const char* ks = getenv("ODO_KNN_SPLIT")) c->knn_split = std::min(8, std::max(1, atoi(ks)));
-    if (const char* km = getenv("ODO_KNN_MFMA")) c->knn_mx = atoi(km) != 0;
+    if (const char* km = getenv("ODO_KNN_MFMA")) c->knn_mx = std::min(2, std::max(0, atoi(km)));
     if (c->knn_mx) c->knn_split = 1;  // one top-2 slot per query
     for (int i = 0; i < NSETS; i++) {
         if ((e = dalloc(&c->knn_idx[i], (size_t)c->knn_split * B * c->kp_cap))) return e;
@@ -1163,7 +1165,7 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
         if (!(c->skip & 8)) {
             if (c->knn_mx)
                 launch_knn2_mx(kst, desc, nkp, KC * 32, desc + KC * 32, nkp + 1, KC * 32, c->knn_idx[s], c->knn_dist[s],
-                               KC, c->kp_cap, n, c->qlist[s], c->qcnt[s], KC);
+                               KC, c->kp_cap, n, c->qlist[s], c->qcnt[s], KC, c->knn_mx);
             else
                 launch_knn2(kst, desc, nkp, KC * 32, desc + KC * 32, nkp + 1, KC * 32, c->knn_idx[s], c->knn_dist[s],
                             KC, c->kp_cap, n, c->qlist[s], c->qcnt[s], KC, c->knn_split, (size_t)c->maxb * KC);
@@ -1699,7 +1701,7 @@ int odo_knn2_hamming(odo_ctx* c, const uint8_t* q, int nq, const uint8_t* t, int
     HIPCHK(hipMemcpyAsync(dn.p, cnt, sizeof(cnt), hipMemcpyHostToDevice, st));
     if (c->knn_mx && nt <= 8192)  // the packed key holds a 13-bit train index
         launch_knn2_mx(st, dq.as<uint8_t>(), dn.as<int>(), 0, dt.as<uint8_t>(), dn.as<int>() + 1, 0, di.as<int2>(),
-                       dd.as<int2>(), 0, nq, 1);
+                       dd.as<int2>(), 0, nq, 1, nullptr, nullptr, 0, c->knn_mx);
     else
         launch_knn2(st, dq.as<uint8_t>(), dn.as<int>(), 0, dt.as<uint8_t>(), dn.as<int>() + 1, 0, di.as<int2>(),
                     dd.as<int2>(), 0, nq, 1);

@@ -158,9 +158,12 @@ void launch_knn2(hipStream_t st, const uint8_t* q, const int* qn, size_t q_strid
                  size_t split_stride = 0);
 // the same top-2 on the matrix cores (exact int8 sign-vector formulation); one
 // split slot, all trains (k_knn2_mx)
+// kNN-2 kernel forms (ODO_KNN_MFMA): VALU xor/popcount, int8 MFMA, FP4 MFMA
+enum { KNN_FMT_VALU = 0, KNN_FMT_I8 = 1, KNN_FMT_F4 = 2 };
 void launch_knn2_mx(hipStream_t st, const uint8_t* q, const int* qn, size_t q_stride, const uint8_t* t, const int* tn,
                     size_t t_stride, int2* idx, int2* dist, size_t out_stride, int max_q, int npairs,
-                    const int32_t* qlist = nullptr, const int* qcnt = nullptr, size_t ql_stride = 0);
+                    const int32_t* qlist = nullptr, const int* qcnt = nullptr, size_t ql_stride = 0,
+                    int fmt = KNN_FMT_I8);
 void launch_vo_lm(hipStream_t st, const float* xyz, const int* nkp, int kp_cap, int slot0, float th_depth_m,
                   uint32_t* lm_bits, int lm_words, int32_t* qlist, int* qcnt, int npairs);
 void launch_pair_match(hipStream_t st, const int2* knn_idx, const int2* knn_dist, size_t knn_stride, const float* xyz,

@@ -29,6 +29,7 @@ PKG_DIR = os.path.join(ROOT, "adaptive-rgbd-localization-mappig_amd")
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP64_PEAK_TFLOPS = 78.6      # MI355X_MICROARCH.md: FP64 vector spec
 I8_MFMA_PEAK_TOPS = 5033.2   # dense I8 MFMA: 2x the BF16 rate per clock (MI355X_MICROARCH.md), 256 CU x 2.4 GHz
+F4_MFMA_PEAK_TOPS = 10066.3  # dense FP4 (block-scaled f8f6f4, e2m1): 4x the BF16 rate per clock
 # the algorithmic Hamming work is 16 int32 lane-ops per (query,
 # train) comparison (8 v_xor_b32 + 8 v_bcnt_u32_b32 over the 256-bit
 # descriptors; the top-2 update is excluded). k_knn2 issues 19 (+ key, min, med3).
@@ -44,7 +45,7 @@ KNN_TRAFFIC = os.path.join(ROOT, "profiles", "r01_knn2_traffic.json")
 # r02 measurements
 UBENCH = os.path.join(ROOT, "profiles", "r02_ubench_peak.jsonl")
 UBENCH_FALLBACK = {"valu_xor_bcnt": 50.213, "fp64_fma": 61.22, "hbm_read": 6946.7, "hbm_copy": 4867.8,
-                   "mfma_i32_16x16x64_i8": 3484.73}
+                   "mfma_i32_16x16x64_i8": 3484.73, "mfma_scale_f32_16x16x128_f4": 6073.79, "knn_f4_mix": 3930.16}
 
 
 def measured_peaks(path=UBENCH):
@@ -600,22 +601,41 @@ def main():
             traffic = tr.get("hbm_bytes_per_launch") if tr.get("batch") == B else \
                 (tr["hbm_bytes_per_pair"] * B if "hbm_bytes_per_pair" in tr else None)
         hbm_alg = sum(32 * int(nq[i]) + 32 * nkp[i] + 16 * int(nq[i]) for i in range(B))
-        if os.environ.get("ODO_KNN_MFMA", "1") != "0":
-            # k_knn2_mx: the exact int8 sign-vector formulation on the matrix
-            # cores, 256 MACs = 512 int8 ops per comparison, against the dense
-            # I8 MFMA peak (2x BF16 per clock, MI355X_MICROARCH.md)
+        form = os.environ.get("ODO_KNN_MFMA", "2")
+        if form != "0":
+            # the exact sign-vector formulation on the matrix cores: 256 MACs =
+            # 512 ops per comparison, against the dense MFMA peak of the operand
+            # type (MI355X_MICROARCH.md: I8 2x, FP4 4x the BF16 rate per clock).
+            # kernel_ms is the live mean inside the timed region, where the
+            # launch shares the CUs with the next batch's extraction; alone_ms
+            # is the same launch in the one-stream stage-timing step.
+            f4 = form == "2"
+            mpk = F4_MFMA_PEAK_TOPS if f4 else I8_MFMA_PEAK_TOPS
             mops = 512.0 * cmp
             mach = mops / (knn_ms * 1e-3) / 1e12
-            roofline = {"bound": "mfma", "achieved": round(mach, 2), "peak": I8_MFMA_PEAK_TOPS, "unit": "Top/s",
-                        "frac": round(mach / I8_MFMA_PEAK_TOPS, 4), "traffic": None,
-                        "kernel": "k_knn2_mx", "kernel_ms": round(knn_ms, 4), "launches": knn_launches,
-                        "work": f"{cmp} descriptor comparisons x 512 int8 ops (v_mfma_i32_16x16x64_i8, K = 256)",
-                        "measured_peak": round(peaks["mfma_i32_16x16x64_i8"], 1),
+            alone = timings.get("knn2")
+            roofline = {"bound": "mfma", "achieved": round(mach, 2), "peak": mpk, "unit": "Top/s",
+                        "frac": round(mach / mpk, 4), "traffic": None,
+                        "kernel": "k_knn2_f4" if f4 else "k_knn2_mx", "kernel_ms": round(knn_ms, 4),
+                        "launches": knn_launches,
+                        "work": f"{cmp} descriptor comparisons x 512 ops (" +
+                                ("v_mfma_scale_f32_16x16x128_f8f6f4, e2m1 operands" if f4 else
+                                 "v_mfma_i32_16x16x64_i8") + ", K = 256)",
+                        "measured_peak": round(peaks["mfma_scale_f32_16x16x128_f4" if f4 else
+                                                     "mfma_i32_16x16x64_i8"], 1),
                         "equiv_valu_16op": {"achieved": round(ach, 3), "peak": round(peak, 2), "unit": "Top/s",
                                             "frac": round(ach / peak, 4),
                                             "note": "SURVEY 8(d) 16 lane-ops per comparison vs the measured "
                                                     "xor+bcnt VALU rate"},
                         "hbm_gbs": round(hbm_alg / (knn_ms * 1e-3) / 1e9, 1)}
+            if alone:
+                aach = mops / (alone * 1e-3) / 1e12
+                roofline["alone"] = {"ms": round(alone, 4), "achieved": round(aach, 2), "frac": round(aach / mpk, 4)}
+                if f4 and "knn_f4_mix" in peaks:
+                    # the kernel's irreducible per-tile instruction mix (2 MFMAs +
+                    # 8 top-2 VALU ops per 256 comparisons) issued from registers
+                    roofline["alone"]["issue_ceiling"] = round(peaks["knn_f4_mix"], 1)
+                    roofline["alone"]["frac_of_issue_ceiling"] = round(aach / peaks["knn_f4_mix"], 4)
         else:
             roofline = {"bound": "valu", "achieved": round(ach, 3), "peak": round(peak, 2),
                         "unit": "Top/s", "frac": round(ach / peak, 4), "traffic": traffic,

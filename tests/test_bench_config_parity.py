@@ -20,7 +20,7 @@ cfg2_hard_b64 runs the hard workload (synth.make_sequence(hard=True): image and
 depth noise, two moving cuboids, repeated texture, twice the motion), where
 the inlier ratio is ~64 % and RANSAC visits ~450 of its 500 hypotheses.
 
-cfg2 also runs with ODO_KNN_SPLIT = 1, 2 and 8 (match lists and query counts
+cfg2 also runs with every kNN-2 kernel form and ODO_KNN_SPLIT = 1, 2 and 8 (match lists and query counts
 bit-exact each time): 256 pairs give more active kNN-2 items than resident
 workgroups, so runs covering several items, split flushes and query-block
 switches inside one workgroup are all exercised. cfg4 (ICL, fy < 0) runs at
@@ -212,18 +212,20 @@ def test_bench_configuration_full_batch(name):
         odo.close()
 
 
-@pytest.mark.parametrize("split", ["1", "2", "8"])
-def test_bench_configuration_knn_splits(split):
-    """kNN-2 train splits 1 / 2 / 8 with more active items than resident
-    workgroups: match lists and query counts of all 256 pairs bit-exact."""
+@pytest.mark.parametrize("form,split", [("0", "1"), ("0", "2"), ("0", "8"), ("1", "1"), ("2", "1")])
+def test_bench_configuration_knn_forms(form, split):
+    """Every kNN-2 kernel form (ODO_KNN_MFMA): the VALU xor/popcount kernel with
+    train splits 1 / 2 / 8 and more active items than resident workgroups, the
+    int8 MFMA kernel and the FP4 MFMA kernel (the default): match lists and
+    query counts of all 256 pairs bit-exact."""
     name = "cfg2_bench"
     c = CONFIGS[name]
     pkg = load_pkg()
     bgr, dep, _ = sequence(c["L"], c["w"], c["h"], intrinsics=c["intr"], seed=c["scene"], closed_loop=True)
-    odo, cfg, res = _run_gpu(pkg, c, bgr, dep, env={"ODO_KNN_SPLIT": split})
+    odo, cfg, res = _run_gpu(pkg, c, bgr, dep, env={"ODO_KNN_MFMA": form, "ODO_KNN_SPLIT": split})
     oracle = _oracle_cached(name, pkg, c, cfg, bgr, dep)
     try:
-        _compare(name + f" split {split}", c, odo, res, oracle, full=False)
+        _compare(name + f" kNN form {form} split {split}", c, odo, res, oracle, full=False)
     finally:
         odo.close()
 

@@ -6,6 +6,9 @@
 //          1, 2, 4 and 8 waves per SIMD. Exact instruction counts via inline asm.
 //   mfma   v_mfma_i32_16x16x64_i8 back to back (independent accumulators),
 //          1 and 2 waves per SIMD: the int8 matrix peak.
+//   mfma_f4  v_mfma_scale_f32_16x16x128_f8f6f4 on e2m1 operands, likewise.
+//   knn_f4_mix  k_knn2_f4's per-tile MFMA + top-2 instruction mix with the
+//          operands in registers: the issue-bound ceiling of that kernel.
 //   fp64   v_fma_f64 chains (the RANSAC ErrorFunction2 arithmetic).
 //   hbm    streaming copy (dwordx4 loads and stores, 2 x 2 GiB) and a
 //          read-only reduction over 4 GiB: achievable HBM bandwidth.
@@ -72,6 +75,71 @@ __global__ __launch_bounds__(256) void k_mfma_i8(int* out, int seed, int iters) 
   int s = 0;
 #pragma unroll
   for (int c = 0; c < NACC; ++c) s += acc[c][0] + acc[c][1] + acc[c][2] + acc[c][3];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+// ---- FP4 (e2m1) scaled MFMA, and the kNN-2 inner-loop mix on it ----------------
+typedef int v8i_t __attribute__((ext_vector_type(8)));
+typedef float v4f_t __attribute__((ext_vector_type(4)));
+template <int NACC>
+__global__ __launch_bounds__(256) void k_mfma_f4(float* out, int seed, int iters) {
+  v8i_t a = {seed, seed + 1, seed + 2, (int)threadIdx.x, 0, 0, 0, 0};
+  v8i_t b = {seed ^ 5, seed ^ 9, (int)threadIdx.x, seed, 0, 0, 0, 0};
+  v4f_t acc[NACC];
+#pragma unroll
+  for (int c = 0; c < NACC; ++c) acc[c] = v4f_t{0.f, 0.f, 0.f, (float)c};
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int c = 0; c < NACC; ++c)
+      acc[c] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, acc[c], 4, 4, 0, 127, 0, 127);
+  }
+  float s = 0;
+#pragma unroll
+  for (int c = 0; c < NACC; ++c) s += acc[c][0] + acc[c][1] + acc[c][2] + acc[c][3];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+// k_knn2_f4's irreducible per-tile work with operands in registers (no LDS, no
+// staging): 4 query tiles x 2 k-steps of FP4 MFMA from an accumulator start
+// advanced by integer adds, then v_min_u32 + v_med3_u32 per key. 1024 (query,
+// train) comparisons per wave per iteration.
+__global__ __launch_bounds__(256) void k_knn_mix(uint32_t* out, int seed, int iters) {
+  v8i_t a0 = {seed, seed + 1, seed + 2, (int)threadIdx.x, 0, 0, 0, 0};
+  v8i_t a1 = {seed ^ 3, seed + 7, (int)threadIdx.x, seed, 0, 0, 0, 0};
+  v8i_t b[4][2];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    b[q][0] = v8i_t{seed ^ q, seed ^ 9, (int)threadIdx.x + q, seed, 0, 0, 0, 0};
+    b[q][1] = v8i_t{seed + q, seed ^ 11, (int)threadIdx.x, seed - q, 0, 0, 0, 0};
+  }
+  typedef int v4i_t __attribute__((ext_vector_type(4)));
+  v4i_t cb = {0x43800000 + 4 * (int)(threadIdx.x & 15), 0x43800004, 0x43800008, 0x4380000c};
+  uint32_t k0[4], k1[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) k0[q] = k1[q] = 0x46000000u;
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cb[j] += 64;
+    const v4f_t C = __builtin_bit_cast(v4f_t, cb);
+    v4f_t acc[4];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        acc[q] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(c ? a1 : a0, b[q][c], c ? acc[q] : C, 4, 4, 0,
+                                                                   127, 0, 127);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float xf = acc[q][e];
+        const uint32_t x = __float_as_uint(xf);
+        k1[q] = max(min(k0[q], k1[q]), min(max(k0[q], k1[q]), x));
+        k0[q] = min(k0[q], x);
+      }
+  }
+  uint32_t s = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) s += k0[q] ^ k1[q];
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
@@ -163,6 +231,31 @@ static void run_mfma(int ncu, int* out) {
   }
 }
 
+template <int NACC>
+static void run_mfma_f4(int ncu, float* out) {
+  const int iters = 2048;
+  for (int wps : {1, 2}) {
+    const int grid = ncu * wps;
+    float ms = time_ms([&] { k_mfma_f4<NACC><<<grid, 256>>>(out, 3, iters); }, 5);
+    CHECK(hipGetLastError());
+    const double ops = (double)grid * 4 * iters * NACC * (16.0 * 16 * 128 * 2);
+    printf("{\"bench\": \"mfma_scale_f32_16x16x128_f4\", \"accumulators\": %d, \"waves_per_simd\": %d, "
+           "\"ms\": %.4f, \"tops\": %.2f}\n", NACC, wps, ms, ops / (ms * 1e-3) / 1e12);
+  }
+}
+
+static void run_knn_mix(int ncu, uint32_t* out) {
+  const int iters = 2048;
+  for (int wps : {1, 2, 3}) {
+    const int grid = ncu * wps;
+    float ms = time_ms([&] { k_knn_mix<<<grid, 256>>>(out, 3, iters); }, 5);
+    CHECK(hipGetLastError());
+    const double cmp = (double)grid * 4 * iters * 1024;
+    printf("{\"bench\": \"knn_f4_mix\", \"waves_per_simd\": %d, \"ms\": %.4f, \"gcmp_s\": %.1f, "
+           "\"tops\": %.2f}\n", wps, ms, cmp / (ms * 1e-3) / 1e9, cmp * 512 / (ms * 1e-3) / 1e12);
+  }
+}
+
 template <int NCH>
 static void run_fp64(int ncu, double* out) {
   const int iters = 1024;
@@ -195,6 +288,10 @@ int main(int argc, char** argv) {
   fflush(stdout);
   run_mfma<1>(ncu, (int*)out32);
   run_mfma<4>(ncu, (int*)out32);
+  fflush(stdout);
+  run_mfma_f4<1>(ncu, (float*)out32);
+  run_mfma_f4<4>(ncu, (float*)out32);
+  run_knn_mix(ncu, out32);
   fflush(stdout);
   run_fp64<1>(ncu, (double*)out32);
   run_fp64<4>(ncu, (double*)out32);
