@@ -145,6 +145,15 @@ def load(path: str = None):
     path = path or os.environ.get("ODO_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise RuntimeError(f"{path} not built: run __graft_entry__.build() (make -C adaptive-rgbd-localization-mappig_amd)")
+    # One HIP runtime per process: torch bundles its own libamdhip64.so.7 /
+    # libhsa-runtime64.so.1 under the same SONAMEs as /opt/rocm's. Loaded
+    # first, this library would pull in /opt/rocm's copies and torch would then
+    # bind to them and find no GPU; with torch imported first, the dynamic
+    # linker resolves this library's HIP dependency to torch's copy.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         f = getattr(L, name)

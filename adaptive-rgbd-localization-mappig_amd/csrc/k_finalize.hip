@@ -83,6 +83,9 @@ __global__ void __launch_bounds__(256, FIN_WAVES_PER_EU) k_finalize(const uint8_
     }
     const int total = acc < kp_cap ? acc : kp_cap;
     if (bx == 0 && threadIdx.x == 0) nkp[f] = total;
+    // a workgroup past the frame's last keypoint has nothing to do (the test is
+    // uniform over the workgroup, so no barrier below is left waiting)
+    if (bx * FIN_KPB >= total) return;
     const bool valid = lvl >= 0 && idx < kp_cap;
     // invalid slots run on a dummy in-level position and write nothing (no early
     // exit: the ballots and the barriers below need every wave)

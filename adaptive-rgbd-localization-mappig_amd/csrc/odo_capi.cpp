@@ -149,6 +149,13 @@ struct odo_ctx {
     CellDesc* cells = nullptr;
     ResizeX* rx = nullptr;
     ResizeY* ry = nullptr;
+    // fused gray + pyramid (k_pyramid; ODO_PYR_FUSED=0: k_gray + one k_resize per level)
+    uint2* rxp = nullptr;  // packed x taps (sx0 | sx1 << 16, a0 | a1 << 16)
+    int* pyr_band_tab = nullptr;  // per band: needed / owned rows and LDS offsets of every level
+    int pyr_bands = 0;     // 0: the fused kernel is off
+    size_t pyr_lds = 0;
+    int pyr_ymax = 0;
+    bool pyr_gray = false;  // gray conversion inside k_pyramid (ODO_PYR_FUSED=2) or k_gray first (1)
     int ncells = 0, cell_cap = 0, kp_cap = 0, okp_stride = 0, node_cap = 0, match_cap = 0, mask_words = 0;
     int max_blur_tiles = 0;
     int fast_roi = 0;  // largest FAST cell ROI side (sizes the kernel's LDS)
@@ -307,7 +314,7 @@ static int sync_all(odo_ctx* c) {
 static void free_ctx(odo_ctx* c) {
     if (!c) return;
     free_hyp_session(c->hs);
-    void* ptrs[] = {c->lv, c->cells, c->rx, c->ry, c->pyr, c->blur, c->cand, c->cand_cnt, c->keys, c->knode, c->kquad,
+    void* ptrs[] = {c->lv, c->cells, c->rx, c->ry, c->rxp, c->pyr_band_tab, c->pyr, c->blur, c->cand, c->cand_cnt, c->keys, c->knode, c->kquad,
                     c->okp, c->ocnt, c->kps, c->desc, c->kun, c->xyz, c->ur, c->nkp, c->bgr_in[0], c->depth_in[0],
                     c->bgr_in[1], c->depth_in[1],
                     c->sort_scratch, c->latch, c->masks, c->adc, c->adb, c->smap, c->acand, c->abig, c->acell,
@@ -602,6 +609,33 @@ static int build_geometry(odo_ctx* c) {
     HIPCHK(hipMemcpy(c->cells, c->cells_h.data(), c->cells_h.size() * sizeof(CellDesc), hipMemcpyHostToDevice));
     if (!rx.empty()) HIPCHK(hipMemcpy(c->rx, rx.data(), rx.size() * sizeof(ResizeX), hipMemcpyHostToDevice));
     if (!ry.empty()) HIPCHK(hipMemcpy(c->ry, ry.data(), ry.size() * sizeof(ResizeY), hipMemcpyHostToDevice));
+    // the fused pyramid: 16-pixel BGR items need W % 16 == 0; bands sized for
+    // two workgroups per CU
+    c->pyr_bands = 0;
+    const char* pf = getenv("ODO_PYR_FUSED");
+    const int pmode = pf ? atoi(pf) : 0;
+    const char* pr = getenv("ODO_PYR_ROWS");  // level-0 rows per band (at most)
+    const char* pb = getenv("ODO_PYR_LDS_KB");
+    if (p.nlevels > 1 && c->W % 16 == 0 && pmode > 0) {
+        int nb = 0, ym = 0;
+        size_t lds = 0;
+        std::vector<int> tab;
+        if (pyramid_plan(c->lv_h.data(), p.nlevels, ry.data(), c->ry_off.data(), (pb ? atoi(pb) : 76) * 1024,
+                         pr ? atoi(pr) : 48, &nb, &lds, &ym, &tab) == 0) {
+            if ((e = dalloc(&c->pyr_band_tab, tab.size()))) return e;
+            HIPCHK(hipMemcpy(c->pyr_band_tab, tab.data(), tab.size() * sizeof(int), hipMemcpyHostToDevice));
+            std::vector<uint2> rp(rx.size());
+            for (size_t i = 0; i < rx.size(); i++)
+                rp[i] = make_uint2((uint32_t)rx[i].sx0 | ((uint32_t)rx[i].sx1 << 16),
+                                   (uint32_t)rx[i].a0 | ((uint32_t)rx[i].a1 << 16));
+            if ((e = dalloc(&c->rxp, rp.size()))) return e;
+            HIPCHK(hipMemcpy(c->rxp, rp.data(), rp.size() * sizeof(uint2), hipMemcpyHostToDevice));
+            c->pyr_bands = nb;
+            c->pyr_lds = lds;
+            c->pyr_ymax = ym;
+            c->pyr_gray = pmode == 2;
+        }
+    }
     return ODO_OK;
 }
 
@@ -946,12 +980,18 @@ static int run_extract(odo_ctx* c, int set, const uint8_t* d_bgr, const uint16_t
     const size_t P = c->pyr_size;
     const size_t slot = fbase(c, set) + slot0;
     uint8_t* pyr = c->pyr + (size_t)slot * P;
-    if (d_bgr) launch_gray(st, d_bgr, pyr, c->W, c->H, c->lv_h[0].pitch, (size_t)c->W * c->H * 3, P, n);
-    for (int l = 1; l < c->nlevels; l++) {
-        const LevelDesc& S = c->lv_h[l - 1];
-        const LevelDesc& D = c->lv_h[l];
-        launch_resize(st, pyr, P, S.off, S.pitch, D.off, D.pitch, D.w, D.h, RZ_RB, c->rz_rows[l], c->rx + c->rx_off[l],
-                      c->ry + c->ry_off[l], n);
+    if (c->pyr_bands > 0) {
+        if (d_bgr && !c->pyr_gray) launch_gray(st, d_bgr, pyr, c->W, c->H, c->lv_h[0].pitch, (size_t)c->W * c->H * 3, P, n);
+        launch_pyramid(st, c->pyr_gray ? d_bgr : nullptr, (size_t)c->W * c->H * 3, pyr, P, c->lv_h.data(), c->nlevels,
+                       c->rx_off.data(), c->ry_off.data(), c->rxp, c->ry, c->pyr_band_tab, c->pyr_bands, c->pyr_lds, c->pyr_ymax, n);
+    } else {
+        if (d_bgr) launch_gray(st, d_bgr, pyr, c->W, c->H, c->lv_h[0].pitch, (size_t)c->W * c->H * 3, P, n);
+        for (int l = 1; l < c->nlevels; l++) {
+            const LevelDesc& S = c->lv_h[l - 1];
+            const LevelDesc& D = c->lv_h[l];
+            launch_resize(st, pyr, P, S.off, S.pitch, D.off, D.pitch, D.w, D.h, RZ_RB, c->rz_rows[l],
+                          c->rx + c->rx_off[l], c->ry + c->ry_off[l], n);
+        }
     }
     tmark(c, 1, st);
     const bool split = c->bstream != st;  // blur beside FAST + octree

@@ -1,0 +1,12 @@
+# GPU tests, the default bench line and a serial-stream kernel trace, in one call.
+# Usage: tools/gpu_check.sh OUTDIR_NAME   (results under gpurun_out/OUTDIR_NAME)
+set -e
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/${1:-check}; mkdir -p $O
+cd $R
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
+echo pytest ok
+timeout -k 10 600 python bench.py --no-cpu-baseline --host-steps 0 --hard-steps 0 > $O/bench.json 2> $O/bench.err
+echo bench ok
+cd /tmp && export TMPDIR=/tmp
+ODO_SERIAL_STREAMS=1 timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --host-steps 0 --hard-steps 0 > $O/kt.log 2>&1
+echo kt ok
