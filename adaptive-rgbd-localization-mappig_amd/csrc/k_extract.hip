@@ -123,22 +123,24 @@ __global__ void __launch_bounds__(256) k_resize(uint8_t* __restrict__ pyr, size_
 // three 16-byte loads) or copied from the pyramid when the gray image is
 // already there; every level is built in LDS from the level below and its own
 // rows are stored with aligned dword writes (zero bytes past the width, as the
-// FAST loads expect). The resize arithmetic and tables are k_resize's: the
-// horizontal taps per output column come from a packed (sx0 | sx1 << 16,
-// a0 | a1 << 16) table staged in LDS one level ahead.
+// FAST loads expect). The resize arithmetic and tables are k_resize's; the
+// horizontal taps of every level are staged in LDS at the start, one dword per
+// output column: sx0 (bits 0-10), a0 (11-22), a1 - (2048 - a0) + 1 (23-24) and
+// sx1 == sx0 (bit 25), so the level phases touch global memory only to store.
 #define PYR_TH 256
 #define PYR_MAXL 16
 struct PyrDesc {
     int nlevels;
     int off[PYR_MAXL], w[PYR_MAXL], h[PYR_MAXL], pitch[PYR_MAXL];
     int rx_off[PYR_MAXL], ry_off[PYR_MAXL];
-    int xt_max;  // widest level >= 1 (entries of one staged x table)
-    int y_max;   // most y-tap entries one band stages (all levels)
+    int xt_off[PYR_MAXL];  // level's first entry in the packed x table (all levels)
+    int xt_total;          // entries of the packed x table
+    int y_max;             // most y-tap entries one band stages (all levels)
 };
 
 __global__ void __launch_bounds__(PYR_TH) k_pyramid(const uint8_t* __restrict__ bgr, size_t in_stride,
                                                     uint8_t* __restrict__ pyr, size_t pyr_stride, PyrDesc D,
-                                                    const uint2* __restrict__ xt, const ResizeY* __restrict__ yt,
+                                                    const uint32_t* __restrict__ xt, const ResizeY* __restrict__ yt,
                                                     const int* __restrict__ bands) {
     extern __shared__ __attribute__((aligned(16))) uint8_t pz_lds[];
     __shared__ int s_lo[PYR_MAXL], s_hi[PYR_MAXL], s_own_lo[PYR_MAXL], s_own_hi[PYR_MAXL], s_base[PYR_MAXL],
@@ -146,10 +148,11 @@ __global__ void __launch_bounds__(PYR_TH) k_pyramid(const uint8_t* __restrict__ 
     const int f = blockIdx.y, b = blockIdx.x, t = threadIdx.x;
     const int L = D.nlevels;
     uint8_t* base = pyr + (size_t)f * pyr_stride;
-    // LDS: two staged x tables | the needed rows' y taps of every level | rows
-    uint2* xs = reinterpret_cast<uint2*>(pz_lds);
-    ResizeY* ys = reinterpret_cast<ResizeY*>(pz_lds + (size_t)2 * D.xt_max * sizeof(uint2));
-    uint8_t* rows = pz_lds + (size_t)2 * D.xt_max * sizeof(uint2) + (size_t)D.y_max * sizeof(ResizeY);
+    // LDS: x taps of every level | the needed rows' y taps of every level | rows
+    uint32_t* xs = reinterpret_cast<uint32_t*>(pz_lds);
+    const size_t xbytes = ((size_t)D.xt_total * 4 + 15) & ~(size_t)15;
+    ResizeY* ys = reinterpret_cast<ResizeY*>(pz_lds + xbytes);
+    uint8_t* rows = pz_lds + xbytes + (size_t)D.y_max * sizeof(ResizeY);
     // this band's row ranges (built on the host: the same for every frame)
     if (t < 6 * PYR_MAXL) {
         const int v = bands[(size_t)b * 6 * PYR_MAXL + t];
@@ -160,8 +163,7 @@ __global__ void __launch_bounds__(PYR_TH) k_pyramid(const uint8_t* __restrict__ 
     // ---- y taps of every level, the level-1 x table, level 0
     for (int l = 1; l < L; l++)
         for (int i = t; i < s_hi[l] - s_lo[l]; i += PYR_TH) ys[s_ybase[l] + i] = yt[D.ry_off[l] + s_lo[l] + i];
-    if (L > 1)
-        for (int i = t; i < D.w[1]; i += PYR_TH) xs[i] = xt[D.rx_off[1] + i];
+    for (int i = t; i < D.xt_total; i += PYR_TH) xs[i] = xt[i];
     {
         const int lo = s_lo[0], nr = s_hi[0] - lo, pitch = D.pitch[0], w = D.w[0];
         uint8_t* lrow = rows + s_base[0];
@@ -225,11 +227,7 @@ __global__ void __launch_bounds__(PYR_TH) k_pyramid(const uint8_t* __restrict__ 
     __syncthreads();
     // ---- levels 1 .. L-1
     for (int l = 1; l < L; l++) {
-        const uint2* X = xs + (size_t)((l - 1) & 1) * D.xt_max;
-        if (l + 1 < L) {
-            uint2* Xn = xs + (size_t)(l & 1) * D.xt_max;
-            for (int i = t; i < D.w[l + 1]; i += PYR_TH) Xn[i] = xt[D.rx_off[l + 1] + i];
-        }
+        const uint32_t* X = xs + D.xt_off[l];
         const int lo = s_lo[l], nr = s_hi[l] - lo, pitch = D.pitch[l], w = D.w[l];
         const int slo = s_lo[l - 1], spitch = D.pitch[l - 1];
         const uint8_t* srows = rows + s_base[l - 1];
@@ -250,9 +248,10 @@ __global__ void __launch_bounds__(PYR_TH) k_pyramid(const uint8_t* __restrict__ 
             for (int j = 0; j < 4; j++) {
                 const int dx = 4 * q + j;
                 if (dx < w) {
-                    const uint2 E = X[dx];
-                    const int sx0 = (int)(E.x & 0xffffu), sx1 = (int)(E.x >> 16);
-                    const int a0 = (int)(E.y & 0xffffu), a1 = (int)(E.y >> 16);
+                    const uint32_t E = X[dx];
+                    const int sx0 = (int)(E & 0x7ffu), a0 = (int)((E >> 11) & 0xfffu);
+                    const int a1 = 2048 - a0 + (int)((E >> 23) & 3u) - 1;
+                    const int sx1 = sx0 + 1 - (int)((E >> 25) & 1u);
                     const int h0 = r0[sx0] * a0 + r0[sx1] * a1;
                     const int h1 = r1[sx0] * a0 + r1[sx1] * a1;
                     int v = (h0 * Y.b0 + h1 * Y.b1 + (1 << 21)) >> 22;
@@ -1106,8 +1105,8 @@ void launch_gray(hipStream_t st, const uint8_t* bgr, uint8_t* pyr, int w, int h,
 int pyramid_plan(const LevelDesc* lv, int nlevels, const ResizeY* ry_host, const int* ry_off, int lds_budget,
                  int min_rows, int* nbands, size_t* lds_bytes, int* y_max, std::vector<int>* table) {
     if (nlevels > PYR_MAXL || nlevels < 2) return -1;
-    int xt_max = 1;
-    for (int l = 1; l < nlevels; l++) xt_max = std::max(xt_max, lv[l].w);
+    int xt_total = 0;
+    for (int l = 1; l < nlevels; l++) xt_total += lv[l].w;
     for (int nb = std::max(1, lv[0].h / std::max(1, min_rows)); nb <= lv[0].h; nb++) {
         std::vector<int> T((size_t)nb * 6 * PYR_MAXL, 0);
         size_t worst = 0;
@@ -1144,7 +1143,7 @@ int pyramid_plan(const LevelDesc* lv, int nlevels, const ResizeY* ry_host, const
             worst = std::max(worst, acc);
             ymax = std::max(ymax, ya);
         }
-        const size_t bytes = (size_t)2 * xt_max * sizeof(uint2) + (size_t)ymax * sizeof(ResizeY) + worst + 16;
+        const size_t bytes = (((size_t)xt_total * 4 + 15) & ~(size_t)15) + (size_t)ymax * sizeof(ResizeY) + worst + 16;
         if (bytes <= (size_t)lds_budget) {
             *nbands = nb;
             *lds_bytes = bytes;
@@ -1156,16 +1155,17 @@ int pyramid_plan(const LevelDesc* lv, int nlevels, const ResizeY* ry_host, const
     return -1;
 }
 void launch_pyramid(hipStream_t st, const uint8_t* bgr, size_t in_stride, uint8_t* pyr, size_t pyr_stride,
-                    const LevelDesc* lv, int nlevels, const int* rx_off, const int* ry_off, const uint2* xt,
+                    const LevelDesc* lv, int nlevels, const int* rx_off, const int* ry_off, const uint32_t* xt,
                     const ResizeY* yt, const int* bands, int nbands, size_t lds_bytes, int y_max, int nframes) {
     PyrDesc D{};
     D.nlevels = nlevels;
     D.y_max = y_max;
-    D.xt_max = 1;
+    D.xt_total = 0;
     for (int l = 0; l < nlevels; l++) {
         D.off[l] = lv[l].off, D.w[l] = lv[l].w, D.h[l] = lv[l].h, D.pitch[l] = lv[l].pitch;
         D.rx_off[l] = rx_off[l], D.ry_off[l] = ry_off[l];
-        if (l >= 1) D.xt_max = std::max(D.xt_max, lv[l].w);
+        D.xt_off[l] = D.xt_total;
+        if (l >= 1) D.xt_total += lv[l].w;
     }
     if (lds_bytes > 64 * 1024)
         (void)hipFuncSetAttribute((const void*)k_pyramid, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);

@@ -197,6 +197,187 @@ __global__ void __launch_bounds__(256, FIN_WAVES_PER_EU) k_finalize(const uint8_
     }
 }
 
+// k_finalize_lds: the same finalisation with each keypoint's two patches
+// staged in LDS by its 16 lanes with row-contiguous dword loads (the IC disc,
+// rows ky-15..ky+15 of the level, 9 dwords each; the rBRIEF window, rows
+// ky-18..ky+18 of the blurred level, 10 dwords each: rotated pattern points
+// round into [-18, 18]). k_finalize's per-lane loads put the 16 lanes of a
+// keypoint on 16 different rows, 64 cache lines per wave instruction through
+// the texture path; staged, a wave instruction touches about two rows per
+// keypoint, and the 512 rBRIEF samples become LDS byte reads.
+#define FL_IC_W 9                    // dwords per staged IC row
+#define FL_IC_N (31 * FL_IC_W)       // 279
+#define FL_BR_W 10                   // dwords per staged rBRIEF row
+#define FL_BR_N (37 * FL_BR_W)       // 370
+#define FL_KP_DW (FL_IC_N + FL_BR_N)  // dwords of LDS per keypoint
+__global__ void __launch_bounds__(256) k_finalize_lds(const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
+                                                      size_t pyr_stride, const LevelDesc* __restrict__ lv, int nlevels,
+                                                      const uint32_t* __restrict__ okp, const int* __restrict__ ocnt,
+                                                      int okp_stride, orb_kp* __restrict__ kps, uint8_t* __restrict__ desc,
+                                                      int* __restrict__ nkp, int kp_cap) {
+    __shared__ uint64_t s_bal[4][16];
+    __shared__ __attribute__((aligned(16))) uint32_t s_disc[16][8];
+    __shared__ __attribute__((aligned(16))) uint32_t s_patch[FIN_KPB][FL_KP_DW];
+    if (threadIdx.x < 128) {
+        const int av = threadIdx.x >> 3, i = threadIdx.x & 7;
+        const int um = c_umax16[av];
+        uint32_t m = 0;
+#pragma unroll
+        for (int bb = 0; bb < 4; bb++) {
+            const int u = 4 * i + bb - 15;
+            if (u >= -um && u <= um) m |= 0xffu << (8 * bb);
+        }
+        s_disc[av][i] = m;
+    }
+    int bx = blockIdx.x, f = blockIdx.y;
+    {
+        const int total = gridDim.x * gridDim.y;
+        if ((total & 7) == 0) {
+            const int h = blockIdx.x + blockIdx.y * gridDim.x;
+            const int lid = (h & 7) * (total >> 3) + (h >> 3);
+            bx = lid % gridDim.x;
+            f = lid / gridDim.x;
+        }
+    }
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int g = lane >> 4, sub = lane & 15;
+    const int kslot = wave * FIN_KPW + g;  // keypoint slot in the workgroup
+    const int idx = bx * FIN_KPB + kslot;
+    int lvl = -1, k = 0, acc = 0;
+    for (int i = 0; i < nlevels; i++) {
+        const int c = ocnt[f * nlevels + i];
+        if (lvl < 0 && idx < acc + c) {
+            lvl = i;
+            k = idx - acc;
+        }
+        acc += c;
+    }
+    const int total = acc < kp_cap ? acc : kp_cap;
+    if (bx == 0 && threadIdx.x == 0) nkp[f] = total;
+    if (bx * FIN_KPB >= total) return;  // uniform over the workgroup
+    const bool valid = lvl >= 0 && idx < kp_cap;
+    const LevelDesc L = lv[valid ? lvl : 0];
+    // an invalid slot stages and reads a dummy in-level patch and writes nothing
+    const uint32_t key = valid ? okp[((size_t)f * nlevels + lvl) * okp_stride + k] : (16u | (16u << 12));
+    const int kx = (int)(key & 0xfff) + 16, ky = (int)((key >> 12) & 0xfff) + 16;
+    const float resp = (float)(key >> 24);
+    uint32_t* P = s_patch[kslot];
+    const int sh = (kx - 15) & 3, sh2 = (kx - 18) & 3;
+    {
+        const uint8_t* img = pyr + (size_t)f * pyr_stride + L.off + (size_t)(ky - 15) * L.pitch + (kx - 15 - sh);
+        const uint8_t* bim = blur + (size_t)f * pyr_stride + L.off + (size_t)(ky - 18) * L.pitch + (kx - 18 - sh2);
+        uint32_t v[18 + 24];
+#pragma unroll
+        for (int j = 0; j < 18; j++) {
+            const int i = min(sub + 16 * j, FL_IC_N - 1);
+            const int r = i / FL_IC_W, c = i - r * FL_IC_W;
+            v[j] = *reinterpret_cast<const uint32_t*>(img + (size_t)r * L.pitch + 4 * c);
+        }
+#pragma unroll
+        for (int j = 0; j < 24; j++) {
+            const int i = min(sub + 16 * j, FL_BR_N - 1);
+            const int r = i / FL_BR_W, c = i - r * FL_BR_W;
+            v[18 + j] = *reinterpret_cast<const uint32_t*>(bim + (size_t)r * L.pitch + 4 * c);
+        }
+#pragma unroll
+        for (int j = 0; j < 18; j++)
+            if (sub + 16 * j < FL_IC_N) P[sub + 16 * j] = v[j];
+#pragma unroll
+        for (int j = 0; j < 24; j++)
+            if (sub + 16 * j < FL_BR_N) P[FL_IC_N + sub + 16 * j] = v[18 + j];
+    }
+    __syncthreads();  // s_disc, the patches
+    int m10, m01;
+    {
+        const bool has1 = sub < 15;
+        const int v0 = sub - 15, v1 = has1 ? sub + 1 : 0;
+        const uint32_t* r0 = P + (v0 + 15) * FL_IC_W;
+        const uint32_t* r1 = P + (v1 + 15) * FL_IC_W;
+        uint32_t w0[9], w1[9];
+#pragma unroll
+        for (int i = 0; i < 9; i++) {
+            w0[i] = r0[i];
+            w1[i] = r1[i];
+        }
+        const uint4* M0 = reinterpret_cast<const uint4*>(s_disc[-v0]);
+        const uint4* M1 = reinterpret_cast<const uint4*>(s_disc[v1]);
+        const uint4 a0 = M0[0], a1 = M0[1], b0 = M1[0], b1 = M1[1];
+        const uint32_t z = has1 ? 0xffffffffu : 0u;
+        const uint32_t mk0[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        const uint32_t mk1[8] = {b0.x & z, b0.y & z, b0.z & z, b0.w & z, b1.x & z, b1.y & z, b1.z & z, b1.w & z};
+        uint32_t s0 = 0, s1 = 0, t = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const uint32_t U = (uint32_t)(4 * i + 1) | ((uint32_t)(4 * i + 2) << 8) | ((uint32_t)(4 * i + 3) << 16) |
+                               ((uint32_t)(4 * i + 4) << 24);
+            const uint32_t d0 = __builtin_amdgcn_alignbyte(w0[i + 1], w0[i], sh) & mk0[i];
+            const uint32_t d1 = __builtin_amdgcn_alignbyte(w1[i + 1], w1[i], sh) & mk1[i];
+            s0 = __builtin_amdgcn_udot4(d0, 0x01010101u, s0, false);
+            s1 = __builtin_amdgcn_udot4(d1, 0x01010101u, s1, false);
+            t = __builtin_amdgcn_udot4(d0, U, t, false);
+            t = __builtin_amdgcn_udot4(d1, U, t, false);
+        }
+        m10 = (int)t - 16 * (int)(s0 + s1);
+        m01 = v0 * (int)s0 + v1 * (int)s1;
+    }
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1) {
+        m10 += __shfl_xor(m10, off);
+        m01 += __shfl_xor(m01, off);
+    }
+    const float angle = fast_atan2((float)m01, (float)m10);
+    const float factorPI = (float)(3.14159265358979323846 / 180.f);
+    const float ang = angle * factorPI;
+    double sd, cd;
+    sincos((double)ang, &sd, &cd);
+    const float a = (float)cd, b = (float)sd;
+    const f32x2 BA = {b, a}, AB = {a, b}, MAG = {RND_MAGIC, RND_MAGIC};
+    // staged byte of rotated offset (iy, ix): (iy + 18) * 40 + ix + 18 + sh2; the
+    // magic-rounded floats carry RND_BITS + offset in their bits
+    const uint8_t* PB = reinterpret_cast<const uint8_t*>(P + FL_IC_N);
+    const uint32_t cofs = (uint32_t)(18 * 4 * FL_BR_W + 18 + sh2) - RND_BITS * (uint32_t)(4 * FL_BR_W + 1);  // mod 2^32
+    int tv0[16], tv1[16];
+#pragma unroll
+    for (int w = 0; w < 16; w++) {
+        const float4 Pt = c_patf[w * 16 + sub];
+        f32x2 q0 = (f32x2){Pt.x, Pt.x} * BA + (f32x2){Pt.y, -Pt.y} * AB;
+        f32x2 q1 = (f32x2){Pt.z, Pt.z} * BA + (f32x2){Pt.w, -Pt.w} * AB;
+        q0 = q0 + MAG;
+        q1 = q1 + MAG;
+        const uint32_t o0 = __float_as_uint(q0.x) * (uint32_t)(4 * FL_BR_W) + __float_as_uint(q0.y) + cofs;
+        const uint32_t o1 = __float_as_uint(q1.x) * (uint32_t)(4 * FL_BR_W) + __float_as_uint(q1.y) + cofs;
+        tv0[w] = PB[o0];
+        tv1[w] = PB[o1];
+    }
+#pragma unroll
+    for (int w = 0; w < 16; w++) {
+        const uint64_t bal = __ballot(tv0[w] < tv1[w]);
+        if (lane == 0) s_bal[wave][w] = bal;
+    }
+    __syncthreads();
+    const int o = idx;
+    if (valid && sub < 8) {
+        const uint32_t lo = (uint32_t)(s_bal[wave][2 * sub] >> (16 * g)) & 0xffffu;
+        const uint32_t hi = (uint32_t)(s_bal[wave][2 * sub + 1] >> (16 * g)) & 0xffffu;
+        reinterpret_cast<uint32_t*>(desc + ((size_t)f * kp_cap + o) * 32)[sub] = lo | (hi << 16);
+    }
+    if (valid && sub == 0) {
+        orb_kp* kp = kps + (size_t)f * kp_cap + o;
+        float px = (float)kx, py = (float)ky;
+        if (lvl != 0) {
+            px *= L.scale;
+            py *= L.scale;
+        }
+        kp->x = px;
+        kp->y = py;
+        kp->size = (float)(int)(31 * L.scale);
+        kp->angle = angle;
+        kp->response = resp;
+        kp->octave = lvl;
+        kp->class_id = -1;
+    }
+}
+
 // UndistortKeyPoints + depth back-projection (frame.cpp:139-164, 286-313) of
 // every finalised keypoint, one per lane.
 __global__ void __launch_bounds__(256) k_kp_geometry(const orb_kp* __restrict__ kps, const int* __restrict__ nkp,
@@ -232,8 +413,17 @@ void launch_finalize(hipStream_t st, const uint8_t* pyr, const uint8_t* blur, si
                      size_t depth_stride, int img_w, FrameCalib cal, orb_kp* kps, uint8_t* desc, float* kun, float* xyz,
                      float* ur, int* nkp, int kp_cap, int nframes) {
     dim3 g((kp_cap + FIN_KPB - 1) / FIN_KPB, nframes);
-    hipLaunchKernelGGL(k_finalize, g, dim3(256), 0, st, pyr, blur, pyr_stride, lv, nlevels, okp, ocnt, okp_stride, kps,
-                       desc, nkp, kp_cap);
+    // ODO_FIN_LDS=0: the per-lane-gather k_finalize
+    static const bool staged = [] {
+        const char* e = getenv("ODO_FIN_LDS");
+        return !(e && e[0] == '0');
+    }();
+    if (staged)
+        hipLaunchKernelGGL(k_finalize_lds, g, dim3(256), 0, st, pyr, blur, pyr_stride, lv, nlevels, okp, ocnt,
+                           okp_stride, kps, desc, nkp, kp_cap);
+    else
+        hipLaunchKernelGGL(k_finalize, g, dim3(256), 0, st, pyr, blur, pyr_stride, lv, nlevels, okp, ocnt, okp_stride,
+                           kps, desc, nkp, kp_cap);
     launch_kp_geometry(st, kps, nkp, depth, depth_stride, img_w, cal, kun, xyz, ur, kp_cap, nframes);
 }
 

@@ -150,7 +150,7 @@ struct odo_ctx {
     ResizeX* rx = nullptr;
     ResizeY* ry = nullptr;
     // fused gray + pyramid (k_pyramid; ODO_PYR_FUSED=0: k_gray + one k_resize per level)
-    uint2* rxp = nullptr;  // packed x taps (sx0 | sx1 << 16, a0 | a1 << 16)
+    uint32_t* rxp = nullptr;  // packed x taps of levels 1.. (k_pyramid's format)
     int* pyr_band_tab = nullptr;  // per band: needed / owned rows and LDS offsets of every level
     int pyr_bands = 0;     // 0: the fused kernel is off
     size_t pyr_lds = 0;
@@ -624,12 +624,20 @@ static int build_geometry(odo_ctx* c) {
                          pr ? atoi(pr) : 48, &nb, &lds, &ym, &tab) == 0) {
             if ((e = dalloc(&c->pyr_band_tab, tab.size()))) return e;
             HIPCHK(hipMemcpy(c->pyr_band_tab, tab.data(), tab.size() * sizeof(int), hipMemcpyHostToDevice));
-            std::vector<uint2> rp(rx.size());
-            for (size_t i = 0; i < rx.size(); i++)
-                rp[i] = make_uint2((uint32_t)rx[i].sx0 | ((uint32_t)rx[i].sx1 << 16),
-                                   (uint32_t)rx[i].a0 | ((uint32_t)rx[i].a1 << 16));
-            if ((e = dalloc(&c->rxp, rp.size()))) return e;
-            HIPCHK(hipMemcpy(c->rxp, rp.data(), rp.size() * sizeof(uint2), hipMemcpyHostToDevice));
+            // one dword per column: sx0 | a0 << 11 | (a1 - (2048 - a0) + 1) << 23 | (sx1 == sx0) << 25
+            std::vector<uint32_t> rp(rx.size());
+            bool packable = true;
+            for (size_t i = 0; i < rx.size(); i++) {
+                const ResizeX& X = rx[i];
+                const int d = X.a1 - (2048 - X.a0) + 1;
+                packable &= X.sx0 >= 0 && X.sx0 < 2048 && X.a0 >= 0 && X.a0 <= 4095 && d >= 0 && d <= 3 &&
+                            (X.sx1 == X.sx0 || X.sx1 == X.sx0 + 1);
+                rp[i] = (uint32_t)X.sx0 | ((uint32_t)X.a0 << 11) | ((uint32_t)(d & 3) << 23) |
+                        ((uint32_t)(X.sx1 == X.sx0) << 25);
+            }
+            if (!packable) nb = 0;
+            if (nb && (e = dalloc(&c->rxp, rp.size()))) return e;
+            if (nb) HIPCHK(hipMemcpy(c->rxp, rp.data(), rp.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
             c->pyr_bands = nb;
             c->pyr_lds = lds;
             c->pyr_ymax = ym;

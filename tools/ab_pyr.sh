@@ -3,7 +3,7 @@
 set -e
 R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/ab_pyr; mkdir -p $O
 cd $R
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
+ODO_PYR_FUSED=1 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
 echo pytest ok
 ODO_PYR_FUSED=2 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_bench_config_parity.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_fused_gray.log 2>&1
 echo pytest2 ok
