@@ -179,6 +179,12 @@ class Odometry:
         m = mode if mode is not None else (1 if enable else 0)
         check(self.lib.odo_set_timing(self.h, m))
 
+    def knn_replay_ms(self, reps: int = 20) -> float:
+        """Mean duration of the last batch's kNN-2 launch re-run alone (measurement)."""
+        ms = C.c_float(0)
+        check(self.lib.odo_knn_replay_time(self.h, reps, C.byref(ms)))
+        return float(ms.value)
+
     def kernel_timing(self):
         """(mean Hamming-match launch duration in ms, launches) since mode 2 was set."""
         avg = C.c_double(0)

@@ -117,6 +117,7 @@ SIGNATURES = {
     "odo_debug_fast": (C.c_int, [P, C.c_int, C.c_int, P, C.c_int, P]),
     "odo_debug_octree": (C.c_int, [P, C.c_int, C.c_int, P, C.c_int, P]),
     "odo_debug_sort": (C.c_int, [P, P, C.c_int, P]),
+    "odo_knn_replay_time": (C.c_int, [P, C.c_int, C.POINTER(C.c_float)]),
     "odo_set_timing": (C.c_int, [P, C.c_int]),
     "odo_kernel_timing": (C.c_int, [P, P, P]),
     "odo_debug_blur": (C.c_int, [P, C.c_int, P, C.c_size_t]),

@@ -9,8 +9,6 @@
 //   k_blur        GaussianBlur 7x7 s=2 REFLECT_101    orbextractor.cpp:795-796
 //   k_finalize    (k_finalize.hip) IC_Angle + rBRIEF + scale; k_kp_geometry undistort + depth
 //                 orbextractor.cpp:14-85,805-811; frame.cpp:139-164,286-313
-#include <vector>
-
 #include "odo_device.h"
 #include "odo_internal.h"
 
@@ -110,159 +108,6 @@ __global__ void __launch_bounds__(256) k_resize(uint8_t* __restrict__ pyr, size_
             }
         }
         *reinterpret_cast<uint32_t*>(base + dst_off + (size_t)(y0 + r) * dpitch + 4 * q) = packed;
-    }
-}
-
-// ============================================================ fused gray + pyramid
-// ComputePyramid in one launch (frame.cpp:23 + orbextractor.cpp:833-857): a
-// workgroup owns a band of rows of every level (level l rows [b H_l / nb,
-// (b+1) H_l / nb)) and computes, top-down from the last level, the rows each
-// level needs from the one below (its own rows plus the one- or two-row halo
-// the bilinear taps reach into the neighbouring bands, recomputed here rather
-// than exchanged). Level 0 is converted from BGR (16 pixels per thread from
-// three 16-byte loads) or copied from the pyramid when the gray image is
-// already there; every level is built in LDS from the level below and its own
-// rows are stored with aligned dword writes (zero bytes past the width, as the
-// FAST loads expect). The resize arithmetic and tables are k_resize's; the
-// horizontal taps of every level are staged in LDS at the start, one dword per
-// output column: sx0 (bits 0-10), a0 (11-22), a1 - (2048 - a0) + 1 (23-24) and
-// sx1 == sx0 (bit 25), so the level phases touch global memory only to store.
-#define PYR_TH 256
-#define PYR_MAXL 16
-struct PyrDesc {
-    int nlevels;
-    int off[PYR_MAXL], w[PYR_MAXL], h[PYR_MAXL], pitch[PYR_MAXL];
-    int rx_off[PYR_MAXL], ry_off[PYR_MAXL];
-    int xt_off[PYR_MAXL];  // level's first entry in the packed x table (all levels)
-    int xt_total;          // entries of the packed x table
-    int y_max;             // most y-tap entries one band stages (all levels)
-};
-
-__global__ void __launch_bounds__(PYR_TH) k_pyramid(const uint8_t* __restrict__ bgr, size_t in_stride,
-                                                    uint8_t* __restrict__ pyr, size_t pyr_stride, PyrDesc D,
-                                                    const uint32_t* __restrict__ xt, const ResizeY* __restrict__ yt,
-                                                    const int* __restrict__ bands) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t pz_lds[];
-    __shared__ int s_lo[PYR_MAXL], s_hi[PYR_MAXL], s_own_lo[PYR_MAXL], s_own_hi[PYR_MAXL], s_base[PYR_MAXL],
-        s_ybase[PYR_MAXL];
-    const int f = blockIdx.y, b = blockIdx.x, t = threadIdx.x;
-    const int L = D.nlevels;
-    uint8_t* base = pyr + (size_t)f * pyr_stride;
-    // LDS: x taps of every level | the needed rows' y taps of every level | rows
-    uint32_t* xs = reinterpret_cast<uint32_t*>(pz_lds);
-    const size_t xbytes = ((size_t)D.xt_total * 4 + 15) & ~(size_t)15;
-    ResizeY* ys = reinterpret_cast<ResizeY*>(pz_lds + xbytes);
-    uint8_t* rows = pz_lds + xbytes + (size_t)D.y_max * sizeof(ResizeY);
-    // this band's row ranges (built on the host: the same for every frame)
-    if (t < 6 * PYR_MAXL) {
-        const int v = bands[(size_t)b * 6 * PYR_MAXL + t];
-        int* dst[6] = {s_lo, s_hi, s_own_lo, s_own_hi, s_base, s_ybase};
-        dst[t / PYR_MAXL][t % PYR_MAXL] = v;
-    }
-    __syncthreads();
-    // ---- y taps of every level, the level-1 x table, level 0
-    for (int l = 1; l < L; l++)
-        for (int i = t; i < s_hi[l] - s_lo[l]; i += PYR_TH) ys[s_ybase[l] + i] = yt[D.ry_off[l] + s_lo[l] + i];
-    for (int i = t; i < D.xt_total; i += PYR_TH) xs[i] = xt[i];
-    {
-        const int lo = s_lo[0], nr = s_hi[0] - lo, pitch = D.pitch[0], w = D.w[0];
-        uint8_t* lrow = rows + s_base[0];
-        const bool own_all = s_own_lo[0] <= lo && s_hi[0] <= s_own_hi[0];
-        if (bgr) {
-            // 16 pixels per item from three 16-byte loads; 4 items' loads in flight per thread
-            const uint8_t* src = bgr + (size_t)f * in_stride;
-            const int n16 = w >> 4;  // w % 16 == 0 checked on the host
-            const int items = nr * n16;
-            for (int it0 = t; it0 < items; it0 += 4 * PYR_TH) {
-                uint4 v[4][3];
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const int it = min(it0 + u * PYR_TH, items - 1);
-                    const int r = it / n16, q = it - r * n16;
-                    const uint4* s4 = reinterpret_cast<const uint4*>(src + ((size_t)(lo + r) * w + 16 * q) * 3);
-                    v[u][0] = s4[0], v[u][1] = s4[1], v[u][2] = s4[2];
-                }
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const int it = it0 + u * PYR_TH;
-                    if (it >= items) continue;
-                    const int r = it / n16, q = it - r * n16;
-                    const int y = lo + r;
-                    const uint32_t wd[12] = {v[u][0].x, v[u][0].y, v[u][0].z, v[u][0].w, v[u][1].x, v[u][1].y,
-                                             v[u][1].z, v[u][1].w, v[u][2].x, v[u][2].y, v[u][2].z, v[u][2].w};
-                    uint32_t o[4];
-#pragma unroll
-                    for (int k = 0; k < 4; k++) {
-                        uint32_t out = 0;
-#pragma unroll
-                        for (int i = 0; i < 4; i++) {
-                            const int px = 4 * k + i;  // bytes 3px .. 3px+2 of the 48
-                            const uint32_t B0 = (wd[(3 * px) >> 2] >> (8 * ((3 * px) & 3))) & 0xffu;
-                            const uint32_t G0 = (wd[(3 * px + 1) >> 2] >> (8 * ((3 * px + 1) & 3))) & 0xffu;
-                            const uint32_t R0 = (wd[(3 * px + 2) >> 2] >> (8 * ((3 * px + 2) & 3))) & 0xffu;
-                            out |= ((B0 * 1868u + G0 * 9617u + R0 * 4899u + 8192u) >> 14) << (8 * i);
-                        }
-                        o[k] = out;
-                    }
-                    const uint4 g = make_uint4(o[0], o[1], o[2], o[3]);
-                    *reinterpret_cast<uint4*>(lrow + (size_t)r * pitch + 16 * q) = g;
-                    if (own_all || (y >= s_own_lo[0] && y < s_own_hi[0]))
-                        *reinterpret_cast<uint4*>(base + D.off[0] + (size_t)y * pitch + 16 * q) = g;
-                }
-            }
-        } else {
-            const int n16 = pitch >> 4, items = nr * n16;
-            const uint4* src = reinterpret_cast<const uint4*>(base + D.off[0] + (size_t)lo * pitch);
-            uint4* dst = reinterpret_cast<uint4*>(lrow);
-            for (int it0 = t; it0 < items; it0 += 8 * PYR_TH) {
-                uint4 v[8];
-#pragma unroll
-                for (int u = 0; u < 8; u++) v[u] = src[min(it0 + u * PYR_TH, items - 1)];  // rows are contiguous (pitch)
-#pragma unroll
-                for (int u = 0; u < 8; u++)
-                    if (it0 + u * PYR_TH < items) dst[it0 + u * PYR_TH] = v[u];
-            }
-        }
-    }
-    __syncthreads();
-    // ---- levels 1 .. L-1
-    for (int l = 1; l < L; l++) {
-        const uint32_t* X = xs + D.xt_off[l];
-        const int lo = s_lo[l], nr = s_hi[l] - lo, pitch = D.pitch[l], w = D.w[l];
-        const int slo = s_lo[l - 1], spitch = D.pitch[l - 1];
-        const uint8_t* srows = rows + s_base[l - 1];
-        uint8_t* lrow = rows + s_base[l];
-        const ResizeY* Ys = ys + s_ybase[l];
-        const int own_lo = s_own_lo[l], own_hi = s_own_hi[l];
-        const int nq = pitch >> 2;
-        const float inv_nq = 1.0f / (float)nq;
-        for (int it = t; it < nr * nq; it += PYR_TH) {
-            const int r = (int)(((float)it + 0.5f) * inv_nq);
-            const int q = it - r * nq;
-            const int y = lo + r;
-            const ResizeY Y = Ys[r];
-            const uint8_t* r0 = srows + (size_t)(Y.sy0 - slo) * spitch;
-            const uint8_t* r1 = srows + (size_t)(Y.sy1 - slo) * spitch;
-            uint32_t packed = 0;
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int dx = 4 * q + j;
-                if (dx < w) {
-                    const uint32_t E = X[dx];
-                    const int sx0 = (int)(E & 0x7ffu), a0 = (int)((E >> 11) & 0xfffu);
-                    const int a1 = 2048 - a0 + (int)((E >> 23) & 3u) - 1;
-                    const int sx1 = sx0 + 1 - (int)((E >> 25) & 1u);
-                    const int h0 = r0[sx0] * a0 + r0[sx1] * a1;
-                    const int h1 = r1[sx0] * a0 + r1[sx1] * a1;
-                    int v = (h0 * Y.b0 + h1 * Y.b1 + (1 << 21)) >> 22;
-                    v = v < 0 ? 0 : (v > 255 ? 255 : v);
-                    packed |= (uint32_t)v << (8 * j);
-                }
-            }
-            if (l + 1 < L) *reinterpret_cast<uint32_t*>(lrow + (size_t)r * pitch + 4 * q) = packed;
-            if (y >= own_lo && y < own_hi) *reinterpret_cast<uint32_t*>(base + D.off[l] + (size_t)y * pitch + 4 * q) = packed;
-        }
-        __syncthreads();
     }
 }
 
@@ -1096,81 +941,6 @@ void launch_gray(hipStream_t st, const uint8_t* bgr, uint8_t* pyr, int w, int h,
                  size_t pyr_stride, int nframes) {
     dim3 g((w * h / 4 + 255) / 256 + 1, nframes);
     hipLaunchKernelGGL(k_gray, g, dim3(256), 0, st, bgr, pyr, w, h, pitch, in_stride, pyr_stride);
-}
-// k_pyramid: host-side band plan. Band b owns level-l rows [b H_l / nb,
-// (b+1) H_l / nb); the rows it needs are found top-down from the last level.
-// The band table holds, per band, 6 x PYR_MAXL ints: needed lo, hi, owned lo,
-// hi, the LDS byte offset of the level's rows and of its y taps. nb is the
-// smallest count at or above H_0 / min_rows whose LDS fits the budget.
-int pyramid_plan(const LevelDesc* lv, int nlevels, const ResizeY* ry_host, const int* ry_off, int lds_budget,
-                 int min_rows, int* nbands, size_t* lds_bytes, int* y_max, std::vector<int>* table) {
-    if (nlevels > PYR_MAXL || nlevels < 2) return -1;
-    int xt_total = 0;
-    for (int l = 1; l < nlevels; l++) xt_total += lv[l].w;
-    for (int nb = std::max(1, lv[0].h / std::max(1, min_rows)); nb <= lv[0].h; nb++) {
-        std::vector<int> T((size_t)nb * 6 * PYR_MAXL, 0);
-        size_t worst = 0;
-        int ymax = 1;
-        for (int b = 0; b < nb; b++) {
-            int* E = T.data() + (size_t)b * 6 * PYR_MAXL;
-            int *lo_ = E, *hi_ = E + PYR_MAXL, *olo = E + 2 * PYR_MAXL, *ohi = E + 3 * PYR_MAXL,
-                *bs = E + 4 * PYR_MAXL, *yb = E + 5 * PYR_MAXL;
-            for (int l = 0; l < nlevels; l++) {
-                olo[l] = (int)((long)b * lv[l].h / nb);
-                ohi[l] = (int)((long)(b + 1) * lv[l].h / nb);
-            }
-            int lo = olo[nlevels - 1], hi = ohi[nlevels - 1];
-            for (int l = nlevels - 1; l >= 1; l--) {
-                lo_[l] = lo, hi_[l] = hi;
-                int slo = 1 << 30, shi = -1;
-                if (hi > lo) {
-                    slo = ry_host[ry_off[l] + lo].sy0;
-                    shi = ry_host[ry_off[l] + hi - 1].sy1 + 1;
-                }
-                lo = std::min(olo[l - 1], slo);
-                hi = std::max(ohi[l - 1], shi);
-                if (hi <= lo) lo = hi = 0;
-            }
-            lo_[0] = lo, hi_[0] = hi;
-            size_t acc = 0;
-            int ya = 0;
-            for (int l = 0; l < nlevels; l++) {
-                bs[l] = (int)acc;
-                acc += (size_t)(hi_[l] - lo_[l]) * lv[l].pitch;
-                yb[l] = ya;
-                if (l >= 1) ya += hi_[l] - lo_[l];
-            }
-            worst = std::max(worst, acc);
-            ymax = std::max(ymax, ya);
-        }
-        const size_t bytes = (((size_t)xt_total * 4 + 15) & ~(size_t)15) + (size_t)ymax * sizeof(ResizeY) + worst + 16;
-        if (bytes <= (size_t)lds_budget) {
-            *nbands = nb;
-            *lds_bytes = bytes;
-            *y_max = ymax;
-            *table = std::move(T);
-            return 0;
-        }
-    }
-    return -1;
-}
-void launch_pyramid(hipStream_t st, const uint8_t* bgr, size_t in_stride, uint8_t* pyr, size_t pyr_stride,
-                    const LevelDesc* lv, int nlevels, const int* rx_off, const int* ry_off, const uint32_t* xt,
-                    const ResizeY* yt, const int* bands, int nbands, size_t lds_bytes, int y_max, int nframes) {
-    PyrDesc D{};
-    D.nlevels = nlevels;
-    D.y_max = y_max;
-    D.xt_total = 0;
-    for (int l = 0; l < nlevels; l++) {
-        D.off[l] = lv[l].off, D.w[l] = lv[l].w, D.h[l] = lv[l].h, D.pitch[l] = lv[l].pitch;
-        D.rx_off[l] = rx_off[l], D.ry_off[l] = ry_off[l];
-        D.xt_off[l] = D.xt_total;
-        if (l >= 1) D.xt_total += lv[l].w;
-    }
-    if (lds_bytes > 64 * 1024)
-        (void)hipFuncSetAttribute((const void*)k_pyramid, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
-    hipLaunchKernelGGL(k_pyramid, dim3(nbands, nframes), dim3(PYR_TH), lds_bytes, st, bgr, in_stride, pyr, pyr_stride,
-                       D, xt, yt, bands);
 }
 size_t resize_lds_bytes(int spitch, int dw, int max_src_rows) {
     return (size_t)((dw + 3) & ~3) * sizeof(ResizeX) + (size_t)max_src_rows * spitch;

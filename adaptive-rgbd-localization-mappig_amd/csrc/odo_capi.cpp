@@ -149,13 +149,6 @@ struct odo_ctx {
     CellDesc* cells = nullptr;
     ResizeX* rx = nullptr;
     ResizeY* ry = nullptr;
-    // fused gray + pyramid (k_pyramid; ODO_PYR_FUSED=0: k_gray + one k_resize per level)
-    uint32_t* rxp = nullptr;  // packed x taps of levels 1.. (k_pyramid's format)
-    int* pyr_band_tab = nullptr;  // per band: needed / owned rows and LDS offsets of every level
-    int pyr_bands = 0;     // 0: the fused kernel is off
-    size_t pyr_lds = 0;
-    int pyr_ymax = 0;
-    bool pyr_gray = false;  // gray conversion inside k_pyramid (ODO_PYR_FUSED=2) or k_gray first (1)
     int ncells = 0, cell_cap = 0, kp_cap = 0, okp_stride = 0, node_cap = 0, match_cap = 0, mask_words = 0;
     int max_blur_tiles = 0;
     int fast_roi = 0;  // largest FAST cell ROI side (sizes the kernel's LDS)
@@ -197,6 +190,7 @@ struct odo_ctx {
     // FP4 (e2m1 +-1) operands (k_knn2_f4, the default: 97 us vs 137-150 us for
     // the 256-pair bench launch alone)
     int knn_mx = KNN_FMT_F4;
+    int last_knn_set = -1, last_knn_n = 0;  // the most recent batch's kNN-2 launch (odo_knn_replay_time)
     uint64_t* sort_scratch = nullptr;
     double* latch = nullptr;
     void* rscr[NSETS] = {};  // RANSAC scratch per frame set
@@ -314,7 +308,7 @@ static int sync_all(odo_ctx* c) {
 static void free_ctx(odo_ctx* c) {
     if (!c) return;
     free_hyp_session(c->hs);
-    void* ptrs[] = {c->lv, c->cells, c->rx, c->ry, c->rxp, c->pyr_band_tab, c->pyr, c->blur, c->cand, c->cand_cnt, c->keys, c->knode, c->kquad,
+    void* ptrs[] = {c->lv, c->cells, c->rx, c->ry, c->pyr, c->blur, c->cand, c->cand_cnt, c->keys, c->knode, c->kquad,
                     c->okp, c->ocnt, c->kps, c->desc, c->kun, c->xyz, c->ur, c->nkp, c->bgr_in[0], c->depth_in[0],
                     c->bgr_in[1], c->depth_in[1],
                     c->sort_scratch, c->latch, c->masks, c->adc, c->adb, c->smap, c->acand, c->abig, c->acell,
@@ -609,41 +603,6 @@ static int build_geometry(odo_ctx* c) {
     HIPCHK(hipMemcpy(c->cells, c->cells_h.data(), c->cells_h.size() * sizeof(CellDesc), hipMemcpyHostToDevice));
     if (!rx.empty()) HIPCHK(hipMemcpy(c->rx, rx.data(), rx.size() * sizeof(ResizeX), hipMemcpyHostToDevice));
     if (!ry.empty()) HIPCHK(hipMemcpy(c->ry, ry.data(), ry.size() * sizeof(ResizeY), hipMemcpyHostToDevice));
-    // the fused pyramid: 16-pixel BGR items need W % 16 == 0; bands sized for
-    // two workgroups per CU
-    c->pyr_bands = 0;
-    const char* pf = getenv("ODO_PYR_FUSED");
-    const int pmode = pf ? atoi(pf) : 0;
-    const char* pr = getenv("ODO_PYR_ROWS");  // level-0 rows per band (at most)
-    const char* pb = getenv("ODO_PYR_LDS_KB");
-    if (p.nlevels > 1 && c->W % 16 == 0 && pmode > 0) {
-        int nb = 0, ym = 0;
-        size_t lds = 0;
-        std::vector<int> tab;
-        if (pyramid_plan(c->lv_h.data(), p.nlevels, ry.data(), c->ry_off.data(), (pb ? atoi(pb) : 76) * 1024,
-                         pr ? atoi(pr) : 48, &nb, &lds, &ym, &tab) == 0) {
-            if ((e = dalloc(&c->pyr_band_tab, tab.size()))) return e;
-            HIPCHK(hipMemcpy(c->pyr_band_tab, tab.data(), tab.size() * sizeof(int), hipMemcpyHostToDevice));
-            // one dword per column: sx0 | a0 << 11 | (a1 - (2048 - a0) + 1) << 23 | (sx1 == sx0) << 25
-            std::vector<uint32_t> rp(rx.size());
-            bool packable = true;
-            for (size_t i = 0; i < rx.size(); i++) {
-                const ResizeX& X = rx[i];
-                const int d = X.a1 - (2048 - X.a0) + 1;
-                packable &= X.sx0 >= 0 && X.sx0 < 2048 && X.a0 >= 0 && X.a0 <= 4095 && d >= 0 && d <= 3 &&
-                            (X.sx1 == X.sx0 || X.sx1 == X.sx0 + 1);
-                rp[i] = (uint32_t)X.sx0 | ((uint32_t)X.a0 << 11) | ((uint32_t)(d & 3) << 23) |
-                        ((uint32_t)(X.sx1 == X.sx0) << 25);
-            }
-            if (!packable) nb = 0;
-            if (nb && (e = dalloc(&c->rxp, rp.size()))) return e;
-            if (nb) HIPCHK(hipMemcpy(c->rxp, rp.data(), rp.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-            c->pyr_bands = nb;
-            c->pyr_lds = lds;
-            c->pyr_ymax = ym;
-            c->pyr_gray = pmode == 2;
-        }
-    }
     return ODO_OK;
 }
 
@@ -988,18 +947,12 @@ static int run_extract(odo_ctx* c, int set, const uint8_t* d_bgr, const uint16_t
     const size_t P = c->pyr_size;
     const size_t slot = fbase(c, set) + slot0;
     uint8_t* pyr = c->pyr + (size_t)slot * P;
-    if (c->pyr_bands > 0) {
-        if (d_bgr && !c->pyr_gray) launch_gray(st, d_bgr, pyr, c->W, c->H, c->lv_h[0].pitch, (size_t)c->W * c->H * 3, P, n);
-        launch_pyramid(st, c->pyr_gray ? d_bgr : nullptr, (size_t)c->W * c->H * 3, pyr, P, c->lv_h.data(), c->nlevels,
-                       c->rx_off.data(), c->ry_off.data(), c->rxp, c->ry, c->pyr_band_tab, c->pyr_bands, c->pyr_lds, c->pyr_ymax, n);
-    } else {
-        if (d_bgr) launch_gray(st, d_bgr, pyr, c->W, c->H, c->lv_h[0].pitch, (size_t)c->W * c->H * 3, P, n);
-        for (int l = 1; l < c->nlevels; l++) {
-            const LevelDesc& S = c->lv_h[l - 1];
-            const LevelDesc& D = c->lv_h[l];
-            launch_resize(st, pyr, P, S.off, S.pitch, D.off, D.pitch, D.w, D.h, RZ_RB, c->rz_rows[l],
-                          c->rx + c->rx_off[l], c->ry + c->ry_off[l], n);
-        }
+    if (d_bgr) launch_gray(st, d_bgr, pyr, c->W, c->H, c->lv_h[0].pitch, (size_t)c->W * c->H * 3, P, n);
+    for (int l = 1; l < c->nlevels; l++) {
+        const LevelDesc& S = c->lv_h[l - 1];
+        const LevelDesc& D = c->lv_h[l];
+        launch_resize(st, pyr, P, S.off, S.pitch, D.off, D.pitch, D.w, D.h, RZ_RB, c->rz_rows[l],
+                      c->rx + c->rx_off[l], c->ry + c->ry_off[l], n);
     }
     tmark(c, 1, st);
     const bool split = c->bstream != st;  // blur beside FAST + octree
@@ -1210,6 +1163,8 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
             }
             HIPCHK(hipEventRecord(c->kt0[kt], kst));
         }
+        c->last_knn_set = s;  // odo_knn_replay_time
+        c->last_knn_n = n;
         if (!(c->skip & 8)) {
             if (c->knn_mx)
                 launch_knn2_mx(kst, desc, nkp, KC * 32, desc + KC * 32, nkp + 1, KC * 32, c->knn_idx[s], c->knn_dist[s],
@@ -1492,6 +1447,44 @@ int odo_debug_select(odo_ctx* c, const uint32_t* in, int n, int nth, int mode, u
     if (er == hipSuccess) er = hipMemcpy(n_out, dn, sizeof(int), hipMemcpyDeviceToHost);
     hipFree(d);
     if (er != hipSuccess) return fail(ODO_ERR_DEVICE, hipGetErrorString(er));
+    return ODO_OK;
+}
+
+// Measurement: re-run the most recent batch's kNN-2 launch `reps` times on one
+// stream of an otherwise idle device (all streams drained first; same inputs,
+// same outputs rewritten) and return the mean launch time from HIP events.
+int odo_knn_replay_time(odo_ctx* c, int reps, float* avg_ms) {
+    if (!c || !avg_ms || reps <= 0) return fail(ODO_ERR_ARG, "knn_replay_time: bad arguments");
+    if (c->last_knn_set < 0) return fail(ODO_ERR_ARG, "knn_replay_time: no batch tracked yet");
+    int e;
+    if ((e = sync_all(c))) return e;
+    const int s = c->last_knn_set, n = c->last_knn_n;
+    const size_t b = fbase(c, s), KC = (size_t)c->kp_cap;
+    uint8_t* desc = c->desc + b * KC * 32;
+    int* nkp = c->nkp + b;
+    hipStream_t st = c->stream;
+    auto launch = [&]() {
+        if (c->knn_mx)
+            launch_knn2_mx(st, desc, nkp, KC * 32, desc + KC * 32, nkp + 1, KC * 32, c->knn_idx[s], c->knn_dist[s], KC,
+                           c->kp_cap, n, c->qlist[s], c->qcnt[s], KC, c->knn_mx);
+        else
+            launch_knn2(st, desc, nkp, KC * 32, desc + KC * 32, nkp + 1, KC * 32, c->knn_idx[s], c->knn_dist[s], KC,
+                        c->kp_cap, n, c->qlist[s], c->qcnt[s], KC, c->knn_split, (size_t)c->maxb * KC);
+    };
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    launch();  // warm
+    HIPCHK(hipEventRecord(e0, st));
+    for (int r = 0; r < reps; r++) launch();
+    HIPCHK(hipEventRecord(e1, st));
+    HIPCHK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    HIPCHK(hipEventDestroy(e0));
+    HIPCHK(hipEventDestroy(e1));
+    HIPCHK(hipGetLastError());
+    *avg_ms = ms / (float)reps;
     return ODO_OK;
 }
 

@@ -6,8 +6,6 @@
 #include <stddef.h>
 #include <stdint.h>
 
-#include <vector>
-
 #include "../../include/odo_types.h"
 
 namespace odo {
@@ -135,12 +133,6 @@ void launch_kp_geometry(hipStream_t st, const orb_kp* kps, const int* nkp, const
 void launch_gray(hipStream_t st, const uint8_t* bgr, uint8_t* pyr, int w, int h, int pitch, size_t in_stride,
                  size_t pyr_stride, int nframes);
 size_t resize_lds_bytes(int spitch, int dw, int max_src_rows);
-// fused gray + pyramid (k_pyramid): bands per frame whose LDS fits the budget
-int pyramid_plan(const LevelDesc* lv, int nlevels, const ResizeY* ry_host, const int* ry_off, int lds_budget,
-                 int min_rows, int* nbands, size_t* lds_bytes, int* y_max, std::vector<int>* table);
-void launch_pyramid(hipStream_t st, const uint8_t* bgr, size_t in_stride, uint8_t* pyr, size_t pyr_stride,
-                    const LevelDesc* lv, int nlevels, const int* rx_off, const int* ry_off, const uint32_t* xt,
-                    const ResizeY* yt, const int* bands, int nbands, size_t lds_bytes, int y_max, int nframes);
 void launch_resize(hipStream_t st, uint8_t* pyr, size_t pyr_stride, int src_off, int spitch, int dst_off, int dpitch,
                    int dw, int dh, int rb, int max_src_rows, const ResizeX* xt, const ResizeY* yt, int nframes);
 void launch_fast(hipStream_t st, const uint8_t* pyr, size_t pyr_stride, const CellDesc* cells, const LevelDesc* lv,

@@ -214,6 +214,11 @@ int odo_debug_blur(odo_ctx* ctx, int i, uint8_t* out, size_t cap);
  * stage runs it on the GPU (workgroup-parallel introsort): in -> out sorted by
  * distance in libstdc++'s exact (unstable) order; distances must be >= 0. */
 int odo_debug_sort(odo_ctx* ctx, const odo_dmatch* in, int n, odo_dmatch* out);
+
+/* Measurement only (no reference counterpart): re-runs the most recent
+ * batch's kNN-2 launch `reps` times on an idle device and returns its mean
+ * duration in ms (HIP events). The bench's roofline "alone" figure. */
+int odo_knn_replay_time(odo_ctx* ctx, int reps, float* avg_ms);
 /* ADAPTIVE detector state. The per-cell DetectorAdjuster thresholds persist
  * across frames and calls (detectoradjuster.cpp:52-65, App. B.13); they
  * advance with every extracted frame, in frame order within a batch.
