@@ -41,6 +41,7 @@ KNN_ISSUED_OPS_PER_CMP = 19
 RANSAC_FLOPS_PER_EVAL = 120
 RANSAC_FLOPS_PER_FIT_POINT = 40
 KNN_TRAFFIC = os.path.join(ROOT, "profiles", "r01_knn2_traffic.json")
+KNN_F4_TRAFFIC = os.path.join(ROOT, "profiles", "r02_knn2_f4_traffic.json")
 # on-box peak microbenchmarks (tools/ubench_peak.hip); the fallbacks are the
 # r02 measurements
 UBENCH = os.path.join(ROOT, "profiles", "r02_ubench_peak.jsonl")
@@ -615,8 +616,15 @@ def main():
             mach = mops / (knn_ms * 1e-3) / 1e12
             # the last batch's kNN-2 launch re-run alone (HIP events, idle device)
             alone = odo.knn_replay_ms(20) if hasattr(odo, "knn_replay_ms") else timings.get("knn2")
+            ftraffic = None
+            if f4 and os.path.exists(KNN_F4_TRAFFIC):
+                with open(KNN_F4_TRAFFIC) as fh:
+                    tr4 = json.load(fh)
+                # PMC HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, gfx950
+                # correction), scaled per pair when the batch differs
+                ftraffic = tr4["hbm_bytes_per_launch"] if tr4.get("batch") == B else tr4["hbm_bytes_per_pair"] * B
             roofline = {"bound": "mfma", "achieved": round(mach, 2), "peak": mpk, "unit": "Top/s",
-                        "frac": round(mach / mpk, 4), "traffic": None,
+                        "frac": round(mach / mpk, 4), "traffic": ftraffic,
                         "kernel": "k_knn2_f4" if f4 else "k_knn2_mx", "kernel_ms": round(knn_ms, 4),
                         "launches": knn_launches,
                         "work": f"{cmp} descriptor comparisons x 512 ops (" +
