@@ -210,16 +210,17 @@ __global__ void __launch_bounds__(256, FIN_WAVES_PER_EU) k_finalize(const uint8_
 #define FL_BR_W 10                   // dwords per staged rBRIEF row
 #define FL_BR_N (37 * FL_BR_W)       // 370
 #define FL_KP_DW (FL_IC_N + FL_BR_N)  // dwords of LDS per keypoint
-__global__ void __launch_bounds__(256) k_finalize_lds(const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
+template <int NW>  // waves (of 4 keypoints) per workgroup
+__global__ void __launch_bounds__(64 * NW) k_finalize_lds(const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
                                                       size_t pyr_stride, const LevelDesc* __restrict__ lv, int nlevels,
                                                       const uint32_t* __restrict__ okp, const int* __restrict__ ocnt,
                                                       int okp_stride, orb_kp* __restrict__ kps, uint8_t* __restrict__ desc,
                                                       int* __restrict__ nkp, int kp_cap) {
-    __shared__ uint64_t s_bal[4][16];
+    __shared__ uint64_t s_bal[NW][16];
     __shared__ __attribute__((aligned(16))) uint32_t s_disc[16][8];
-    __shared__ __attribute__((aligned(16))) uint32_t s_patch[FIN_KPB][FL_KP_DW];
-    if (threadIdx.x < 128) {
-        const int av = threadIdx.x >> 3, i = threadIdx.x & 7;
+    __shared__ __attribute__((aligned(16))) uint32_t s_patch[NW * FIN_KPW][FL_KP_DW];
+    for (int d = threadIdx.x; d < 128; d += 64 * NW) {
+        const int av = d >> 3, i = d & 7;
         const int um = c_umax16[av];
         uint32_t m = 0;
 #pragma unroll
@@ -242,7 +243,7 @@ __global__ void __launch_bounds__(256) k_finalize_lds(const uint8_t* __restrict_
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int g = lane >> 4, sub = lane & 15;
     const int kslot = wave * FIN_KPW + g;  // keypoint slot in the workgroup
-    const int idx = bx * FIN_KPB + kslot;
+    const int idx = bx * (NW * FIN_KPW) + kslot;
     int lvl = -1, k = 0, acc = 0;
     for (int i = 0; i < nlevels; i++) {
         const int c = ocnt[f * nlevels + i];
@@ -254,7 +255,7 @@ __global__ void __launch_bounds__(256) k_finalize_lds(const uint8_t* __restrict_
     }
     const int total = acc < kp_cap ? acc : kp_cap;
     if (bx == 0 && threadIdx.x == 0) nkp[f] = total;
-    if (bx * FIN_KPB >= total) return;  // uniform over the workgroup
+    if (bx * (NW * FIN_KPW) >= total) return;  // uniform over the workgroup
     const bool valid = lvl >= 0 && idx < kp_cap;
     const LevelDesc L = lv[valid ? lvl : 0];
     // an invalid slot stages and reads a dummy in-level patch and writes nothing
@@ -413,13 +414,18 @@ void launch_finalize(hipStream_t st, const uint8_t* pyr, const uint8_t* blur, si
                      size_t depth_stride, int img_w, FrameCalib cal, orb_kp* kps, uint8_t* desc, float* kun, float* xyz,
                      float* ur, int* nkp, int kp_cap, int nframes) {
     dim3 g((kp_cap + FIN_KPB - 1) / FIN_KPB, nframes);
-    // ODO_FIN_LDS=0: the per-lane-gather k_finalize
-    static const bool staged = [] {
+    // ODO_FIN_LDS: 0 the per-lane-gather k_finalize; 1 the staged kernel at 4
+    // waves (16 keypoints, 42.5 KB LDS) per workgroup; 2 (default) at 2 waves
+    // (8 keypoints, 21 KB: more workgroups resident per CU)
+    static const int staged = [] {
         const char* e = getenv("ODO_FIN_LDS");
-        return !(e && e[0] == '0');
+        return e ? atoi(e) : 2;
     }();
-    if (staged)
-        hipLaunchKernelGGL(k_finalize_lds, g, dim3(256), 0, st, pyr, blur, pyr_stride, lv, nlevels, okp, ocnt,
+    if (staged == 2)
+        hipLaunchKernelGGL(k_finalize_lds<2>, dim3((kp_cap + 7) / 8, nframes), dim3(128), 0, st, pyr, blur, pyr_stride,
+                           lv, nlevels, okp, ocnt, okp_stride, kps, desc, nkp, kp_cap);
+    else if (staged)
+        hipLaunchKernelGGL(k_finalize_lds<4>, g, dim3(256), 0, st, pyr, blur, pyr_stride, lv, nlevels, okp, ocnt,
                            okp_stride, kps, desc, nkp, kp_cap);
     else
         hipLaunchKernelGGL(k_finalize, g, dim3(256), 0, st, pyr, blur, pyr_stride, lv, nlevels, okp, ocnt, okp_stride,

@@ -7,7 +7,7 @@ echo pytest ok
 timeout -k 10 600 python bench.py --no-cpu-baseline --host-steps 0 --hard-steps 0 > $O/bench.json 2> $O/bench.err
 echo bench ok
 cd /tmp && export TMPDIR=/tmp
-for m in 1 0; do
+for m in 2 1; do
   ODO_FIN_LDS=$m ODO_SERIAL_STREAMS=1 timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d $O/kt$m -o run --output-format csv -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --host-steps 0 --hard-steps 0 > $O/kt$m.log 2>&1
   echo kt$m ok
 done
