@@ -411,6 +411,58 @@ ODO_INLINE void wg_sum(double (&v)[NV], double* red) {
     __syncthreads();
 }
 
+// computeActiveErrors + activeRobustChi2 + buildSystem contribution of one edge
+// at pose T into acc (H upper triangle row-major 0..20, b 21..26, robust chi 27)
+ODO_INLINE void edge_build(const SE3& T, const double Xw[3], const double ob[3], double info, uint8_t fl,
+                           const PnPCam& cam, double dMono, double dStereo, double (&acc)[28]) {
+    const bool st = fl & PE_STEREO;
+    double Xc[3], e[3];
+    se3_map(T, Xw, Xc);
+    edge_err(Xc, ob, st, cam, e);
+    const double c2 = chi2_of(e, info, st);
+    double rho[3] = {c2, 1.0, 0.0};
+    if (fl & PE_ROBUST) huber_rho(st ? dStereo : dMono, c2, rho);
+    acc[27] += rho[0];
+    const double x = Xc[0], y = Xc[1], invz = 1.0 / Xc[2], invz_2 = invz * invz;
+    double J[3][6];
+    J[0][0] = x * y * invz_2 * cam.fx;
+    J[0][1] = -(1 + (x * x * invz_2)) * cam.fx;
+    J[0][2] = y * invz * cam.fx;
+    J[0][3] = -invz * cam.fx;
+    J[0][4] = 0;
+    J[0][5] = x * invz_2 * cam.fx;
+    J[1][0] = (1 + y * y * invz_2) * cam.fy;
+    J[1][1] = -x * y * invz_2 * cam.fy;
+    J[1][2] = -x * invz * cam.fy;
+    J[1][3] = 0;
+    J[1][4] = -invz * cam.fy;
+    J[1][5] = y * invz_2 * cam.fy;
+    // mono edges: third row zero, so its terms add exactly +0
+    J[2][0] = st ? J[0][0] - cam.bf * y * invz_2 : 0.0;
+    J[2][1] = st ? J[0][1] + cam.bf * x * invz_2 : 0.0;
+    J[2][2] = st ? J[0][2] : 0.0;
+    J[2][3] = st ? J[0][3] : 0.0;
+    J[2][4] = 0;
+    J[2][5] = st ? J[0][5] - cam.bf * invz_2 : 0.0;
+    const double r1 = rho[1];
+    const double wo = r1 * info;
+    int h = 0;
+#pragma unroll
+    for (int a = 0; a < 6; a++) {
+        double sb = 0;
+#pragma unroll
+        for (int kk = 0; kk < 3; kk++) sb += J[kk][a] * (info * e[kk]);
+        acc[21 + a] -= r1 * sb;
+#pragma unroll
+        for (int cc = a; cc < 6; cc++) {
+            double hh = 0;
+#pragma unroll
+            for (int kk = 0; kk < 3; kk++) hh += J[kk][a] * wo * J[kk][cc];
+            acc[h++] += hh;
+        }
+    }
+}
+
 // robust (Huber) chi2 of one edge at pose T; c2 = plain chi2 of the stored error
 ODO_INLINE double edge_robust_chi(const SE3& T, const double Xw[3], const double ob[3], double info, uint8_t fl,
                                   const PnPCam& cam, double dMono, double dStereo, double& c2) {
@@ -546,55 +598,9 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
             for (int k = lane; k < ne; k += PNP_NT) {
                 const uint8_t fl = E.flags[k];
                 if (fl & PE_OUT) continue;
-                const bool st = fl & PE_STEREO;
                 const double Xw[3] = {E.X[3 * k], E.X[3 * k + 1], E.X[3 * k + 2]};
                 const double ob[3] = {E.obs[3 * k], E.obs[3 * k + 1], E.obs[3 * k + 2]};
-                const double info = E.info[k];
-                double Xc[3], e[3];
-                se3_map(T, Xw, Xc);
-                edge_err(Xc, ob, st, cam, e);
-                const double c2 = chi2_of(e, info, st);
-                double rho[3] = {c2, 1.0, 0.0};
-                if (fl & PE_ROBUST) huber_rho(st ? dStereo : dMono, c2, rho);
-                acc[27] += rho[0];
-                const double x = Xc[0], y = Xc[1], invz = 1.0 / Xc[2], invz_2 = invz * invz;
-                double J[3][6];
-                J[0][0] = x * y * invz_2 * cam.fx;
-                J[0][1] = -(1 + (x * x * invz_2)) * cam.fx;
-                J[0][2] = y * invz * cam.fx;
-                J[0][3] = -invz * cam.fx;
-                J[0][4] = 0;
-                J[0][5] = x * invz_2 * cam.fx;
-                J[1][0] = (1 + y * y * invz_2) * cam.fy;
-                J[1][1] = -x * y * invz_2 * cam.fy;
-                J[1][2] = -x * invz * cam.fy;
-                J[1][3] = 0;
-                J[1][4] = -invz * cam.fy;
-                J[1][5] = y * invz_2 * cam.fy;
-                // mono edges: third row zero, so its terms add exactly +0
-                J[2][0] = st ? J[0][0] - cam.bf * y * invz_2 : 0.0;
-                J[2][1] = st ? J[0][1] + cam.bf * x * invz_2 : 0.0;
-                J[2][2] = st ? J[0][2] : 0.0;
-                J[2][3] = st ? J[0][3] : 0.0;
-                J[2][4] = 0;
-                J[2][5] = st ? J[0][5] - cam.bf * invz_2 : 0.0;
-                const double r1 = rho[1];
-                const double wo = r1 * info;
-                int h = 0;
-#pragma unroll
-                for (int a = 0; a < 6; a++) {
-                    double sb = 0;
-#pragma unroll
-                    for (int kk = 0; kk < 3; kk++) sb += J[kk][a] * (info * e[kk]);
-                    acc[21 + a] -= r1 * sb;
-#pragma unroll
-                    for (int cc = a; cc < 6; cc++) {
-                        double hh = 0;
-#pragma unroll
-                        for (int kk = 0; kk < 3; kk++) hh += J[kk][a] * wo * J[kk][cc];
-                        acc[h++] += hh;
-                    }
-                }
+                edge_build(T, Xw, ob, (double)E.info[k], fl, cam, dMono, dStereo, acc);
             }
             wg_sum<28>(acc, red);
             PP_ACC(tb);
