@@ -198,7 +198,8 @@ int odo_projection_match(odo_ctx* ctx, const float Tcw[16], const odo_landmark* 
                          const uint8_t* slot_taken, float th, float nn_ratio, int32_t* slot_lm, float* proj,
                          int* n_matches);
 
-/* Kabsch::Compute (kabsch.cpp:14), host-side 3x3 SVD. A,B: n x 3. */
+/* Kabsch::Compute (kabsch.cpp:14): one GPU workgroup (k_kabsch: centroids, A^T B
+ * with a fixed-order block reduction, 3x3 Jacobi SVD). A,B: n x 3 host arrays. */
 int odo_kabsch(const float* A, const float* B, int n, float T[16]);
 
 /* glibc rand() stream helpers (srand/rand of main.cpp:27, ransac.cpp:275). */

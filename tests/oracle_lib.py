@@ -217,3 +217,40 @@ class AdaptiveExtractor:
         n = lib().oracle_adaptive_extract(ptr(np.ascontiguousarray(gray)), w, h, C.byref(self.p), ptr(self.thresh),
                                           ptr(kps), ptr(desc), cap, ptr(t_used))
         return kps[:n], desc[:n], t_used
+
+
+def pnp_chi2(Tcw, Xw, ob, cal):
+    """g2o edge chi2 at pose Tcw (EdgeSE3ProjectXYZOnlyPose / StereoOnlyPose,
+    information 1/Xw.z^2), as the oracle's PnPProblem::compute_error."""
+    R = Tcw[:3, :3].astype(np.float64)
+    t = Tcw[:3, 3].astype(np.float64)
+    Xc = Xw.astype(np.float64) @ R.T + t
+    info = (1.0 / (Xw[:, 2].astype(np.float32) * Xw[:, 2].astype(np.float32))).astype(np.float64)
+    stereo = ~(ob[:, 2] < 0)
+    invz32 = (np.float32(1.0) / Xc[:, 2].astype(np.float32)).astype(np.float64)
+    invz = np.where(stereo, invz32, 1.0 / Xc[:, 2])
+    u = Xc[:, 0] * invz * cal.fx + cal.cx
+    v = Xc[:, 1] * invz * cal.fy + cal.cy
+    ur = u - float(np.float32(cal.mbf)) * invz
+    e0, e1 = ob[:, 0] - u, ob[:, 1] - v
+    e2 = np.where(stereo, ob[:, 2] - ur, 0.0)
+    return info * (e0 * e0 + e1 * e1 + e2 * e2), stereo
+
+
+def check_pnp_flags(got_flags, ref_flags, f1, f2, f2_src, Tcw_ref, cal, tag):
+    """PnP inlier flags must agree except within a 2 % chi2 margin of the
+    classification threshold (SURVEY §7 hard part 6); returns the number of
+    (marginal) flags that differ."""
+    bad = np.nonzero(got_flags != ref_flags)[0]
+    if bad.size == 0:
+        return 0
+    src = f2_src[bad]
+    assert (src >= 0).all(), f"{tag}: PnP flag differs on a keypoint without a landmark"
+    Xw = f1["xyz"][src]
+    ob = np.stack([f2["kun"][bad, 0], f2["kun"][bad, 1], f2["ur"][bad]], 1).astype(np.float64)
+    chi, stereo = pnp_chi2(Tcw_ref, Xw, ob, cal)
+    th = np.where(stereo, 7.815, 5.991)
+    far = np.abs(chi - th) > 0.02 * th
+    assert not far.any(), (f"{tag}: PnP inlier flags differ away from the chi2 threshold at keypoints "
+                           f"{bad[far][:8]} (chi2 {chi[far][:8]})")
+    return int(bad.size)

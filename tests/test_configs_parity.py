@@ -67,6 +67,9 @@ def test_config_path_parity(name):
         assert (res[p]["n_sweeps"], res[p]["n_fit_points"]) == (r.n_sweeps, r.n_fit_points), f"{name} pair {p}: work"
         dT = np.abs(res[p]["Tcw"] - np.array(r.Tcw, np.float32)).max()
         assert dT < 1e-4, f"{name} pair {p}: PnP pose differs by {dT}"
-        assert abs(int(res[p]["pnp_inliers"]) - r.pnp_inliers) <= 2
+        n2 = len(frames[p]["kps"])
+        nb = O.check_pnp_flags(g["pnp_inliers"][:n2], mask, frames[p - 1], frames[p], g["f2_src"][:n2],
+                               np.array(r.Tcw, np.float32).reshape(4, 4), cal, f"{name} pair {p}")
+        assert abs(int(res[p]["pnp_inliers"]) - r.pnp_inliers) <= nb, f"{name} pair {p}: PnP inlier count"
     assert odo.latch == latch
     odo.close()

@@ -101,9 +101,12 @@ def test_hip_reproduces_frame_and_pair_fixtures(inputs):
     assert np.array_equal(res[1]["T12"], g["T12"]), "T12 not bit-exact"
     assert res[1]["rmse"] == g["rmse"][0]
     assert np.abs(res[1]["Tcw"] - g["Tcw"]).max() < 1e-4, "PnP pose"
-    # PnP inlier flags: g2o accumulation order is not reproducible (SURVEY §7 hard part 6)
+    # PnP inlier flags: g2o accumulation order is not reproducible (SURVEY §7 hard
+    # part 6), so a flag may differ only within the chi2 margin of its threshold
     n2 = len(g["pnp_inlier_mask"])
-    assert (p["pnp_inliers"][:n2] != g["pnp_inlier_mask"]).sum() <= 2
+    fr = [{k: gold[f"f{i}_{k}"] for k in ("kps", "desc", "kun", "xyz", "ur")} for i in range(2)]
+    O.check_pnp_flags(p["pnp_inliers"][:n2], g["pnp_inlier_mask"], fr[0], fr[1], p["f2_src"][:n2],
+                      g["Tcw"].reshape(4, 4), O.fr1_calib(), "golden pair")
     c = g["counts"]
     assert (res[1]["n_matches"], res[1]["n_good"], res[1]["n_inliers"], res[1]["visited"]) == (c[0], c[1], c[2], c[5])
     assert odo.latch == g["latch"][0]

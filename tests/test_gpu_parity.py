@@ -4,7 +4,9 @@ Bit-exact for integer/byte/index work (pyramid, FAST candidates, octree,
 blurred levels, keypoints, descriptors, kNN indices and distances, match
 lists, std::sort order, RANSAC inlier masks) and for the float/double RANSAC
 fit (same operation order); PnP pose within 1e-4 (SURVEY §8 contract) with
-inlier flags compared outside a small chi2 margin.
+inlier flags compared outside a small chi2 margin (oracle_lib.check_pnp_flags:
+a flag may differ only where the edge's chi2 at the oracle pose is within 2 %
+of the 5.991 / 7.815 threshold).
 """
 import numpy as np
 import pytest
@@ -140,9 +142,10 @@ def test_pairs_match_ransac_pnp(cfg2_run):
         T_gpu = res[p]["Tcw"].reshape(4, 4)
         T_ref = np.array(r.Tcw, np.float32).reshape(4, 4)
         assert np.abs(T_gpu - T_ref).max() < 1e-4, f"pair {p}: PnP pose differs {np.abs(T_gpu - T_ref).max()}"
-        assert abs(int(res[p]["pnp_inliers"]) - r.pnp_inliers) <= 2
         n2 = len(frames[p]["kps"])
-        assert (g["pnp_inliers"][:n2] != mask).sum() <= 2
+        nb = O.check_pnp_flags(g["pnp_inliers"][:n2], mask, frames[p - 1], frames[p], g["f2_src"][:n2], T_ref, cal,
+                               f"pair {p}")
+        assert abs(int(res[p]["pnp_inliers"]) - r.pnp_inliers) <= nb, f"pair {p}: PnP inlier count"
     assert abs(odo.latch - latch) == 0
 
 
