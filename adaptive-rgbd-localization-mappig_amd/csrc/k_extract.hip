@@ -434,8 +434,24 @@ __global__ void __launch_bounds__(OT_THREADS) k_octree(const uint32_t* __restric
         int tot;
         const int ex = block_exclusive_scan<int>(cnt, scan, &tot);
         if (c < nc) {
-            const uint32_t* src = cand + ((size_t)f * ncells + c0 + c) * cell_cap;
-            for (int k = 0; k < cnt; k++) keys[n + ex + k] = src[k];
+            // 32 candidates in flight per batch (cell rows are 16-byte aligned):
+            // a load-then-store loop would wait out one memory latency per 4 keys
+            const uint4* src = reinterpret_cast<const uint4*>(cand + ((size_t)f * ncells + c0 + c) * cell_cap);
+            uint32_t* dst = keys + n + ex;
+            for (int k0 = 0; k0 < cnt; k0 += 32) {
+                uint4 v[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++)
+                    if (k0 + 4 * u < cnt) v[u] = src[(k0 >> 2) + u];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const int k = k0 + 4 * u;
+                    if (k < cnt) dst[k] = v[u].x;
+                    if (k + 1 < cnt) dst[k + 1] = v[u].y;
+                    if (k + 2 < cnt) dst[k + 2] = v[u].z;
+                    if (k + 3 < cnt) dst[k + 3] = v[u].w;
+                }
+            }
         }
         n += tot;
     }

@@ -554,7 +554,7 @@ __global__ void __launch_bounds__(256) k_ransac_prep(RansacBufs B, RansacCfg cfg
         S->rmse = 1e6f;
         S->sweeps = 0;
         S->fitpts = 0;
-        S->nexth = EV_ROWS0 * EV_WAVES_C;  // the first eval launch covers [0, EV_ROWS0 * EV_WAVES)
+        S->nexth = cfg.rows0 * EV_WAVES_C;  // the first eval launch covers [0, rows0 * EV_WAVES)
     }
     if (done) return;
     __shared__ SampWin s_win;
@@ -1615,6 +1615,7 @@ void launch_ransac(hipStream_t st, const void* good, const int* n_good, const in
                    uint32_t* best_mask, int mask_words, odo_pair_result* res, float* T12, int npairs, int part,
                    int* phase, int* open_hint) {
     ransac_eval_lds_attr();
+    cfg.rows0 = EV_ROWS0;
     RansacBufs B = carve(scratch, npairs, match_cap, mask_words, cfg);
     B.good = (const SortElR*)good;
     B.n_good = n_good;
@@ -1655,7 +1656,13 @@ void launch_ransac(hipStream_t st, const void* good, const int* n_good, const in
     // launch and the finished pairs' outputs (phase[] marks them); part 2 = the
     // rest; part 0 = both.
     const int rows = (H + EV_WAVES - 1) / EV_WAVES;
-    const int r0 = std::min(rows, EV_ROWS0);
+    // ODO_EV_ROWS0: rows of the first launch (default EV_ROWS0)
+    static const int rows0 = [] {
+        const char* e = getenv("ODO_EV_ROWS0");
+        return e ? std::max(1, atoi(e)) : EV_ROWS0;
+    }();
+    const int r0 = std::min(rows, rows0);
+    cfg.rows0 = r0;
     if (part != 2) {
         hipLaunchKernelGGL(k_ransac_prep, dim3(npairs), dim3(256), 0, st, B, cfg);
         if (r0 > 0)

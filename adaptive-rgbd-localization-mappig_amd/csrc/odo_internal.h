@@ -123,6 +123,7 @@ struct RansacCfg {
     int sample_size;
     int check_depth;
     double raster_cov_x, raster_cov_y;
+    int rows0;  // hypothesis rows (of EV_WAVES) of the first eval launch; set by launch_ransac
 };
 
 // ---- launch wrappers (defined next to their kernels)
