@@ -92,19 +92,23 @@ __global__ void __launch_bounds__(256) k_resize(uint8_t* __restrict__ pyr, size_
         const int r = (int)(((float)it + 0.5f) * inv_nq);
         const int q = it - r * nq;
         const ResizeY Y = yt[y0 + r];
-        const uint8_t* r0 = rows + (size_t)(Y.sy0 - sy_lo) * spitch;
-        const uint8_t* r1 = rows + (size_t)(Y.sy1 - sy_lo) * spitch;
+        // 32-bit LDS offsets and 24-bit multiplies (pixels <= 255, taps <= 2048,
+        // h <= 522240): left to size_t / int the compiler emits quarter-rate
+        // v_mad_u64_u32 / v_mul_lo_u32 for every tap
+        const uint8_t* r0 = rows + (uint32_t)__umul24((uint32_t)(Y.sy0 - sy_lo), (uint32_t)spitch);
+        const uint8_t* r1 = rows + (uint32_t)__umul24((uint32_t)(Y.sy1 - sy_lo), (uint32_t)spitch);
+        const uint32_t b0 = (uint32_t)Y.b0, b1 = (uint32_t)Y.b1;
         uint32_t packed = 0;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const int dx = 4 * q + j;
             if (dx < dw) {
                 const ResizeX X = xs[dx];
-                const int h0 = r0[X.sx0] * X.a0 + r0[X.sx1] * X.a1;
-                const int h1 = r1[X.sx0] * X.a0 + r1[X.sx1] * X.a1;
-                int v = (h0 * Y.b0 + h1 * Y.b1 + (1 << 21)) >> 22;
-                v = v < 0 ? 0 : (v > 255 ? 255 : v);
-                packed |= (uint32_t)v << (8 * j);
+                const uint32_t a0 = (uint32_t)X.a0, a1 = (uint32_t)X.a1;
+                const uint32_t h0 = __umul24(r0[X.sx0], a0) + __umul24(r0[X.sx1], a1);
+                const uint32_t h1 = __umul24(r1[X.sx0], a0) + __umul24(r1[X.sx1], a1);
+                const uint32_t v = (__umul24(h0, b0) + __umul24(h1, b1) + (1u << 21)) >> 22;
+                packed |= min(v, 255u) << (8 * j);
             }
         }
         *reinterpret_cast<uint32_t*>(base + dst_off + (size_t)(y0 + r) * dpitch + 4 * q) = packed;
