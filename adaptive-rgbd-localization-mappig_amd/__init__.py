@@ -12,19 +12,21 @@ import ctypes as C
 import numpy as np
 
 from . import _abi
-from ._abi import (DETECTOR_ADAPTIVE_FAST, DETECTOR_ORB_SLAM2, AdaptiveParams, Calib, Config, DMatch,
+from ._abi import (DETECTOR_ADAPTIVE_FAST, DETECTOR_ADAPTIVE_ORB, DETECTOR_ORB_SLAM2, AdaptiveParams, Calib, Config, DMatch,
                    DMATCH_DTYPE, KP_DTYPE, OrbParams, PAIR_DTYPE, PairResult, RansacParams, Rng, check, load, ptr)
 
 __all__ = ["Odometry", "HostFrames", "PinnedResults", "default_config", "load", "KP_DTYPE", "DMATCH_DTYPE", "PAIR_DTYPE", "rng_stream",
            "kabsch", "Calib", "OrbParams", "RansacParams", "Config", "AdaptiveParams", "DETECTOR_ORB_SLAM2",
-           "DETECTOR_ADAPTIVE_FAST"]
+           "DETECTOR_ADAPTIVE_FAST", "DETECTOR_ADAPTIVE_ORB"]
 
 
 def default_config(width=640, height=480, max_batch=1, nfeatures=1000, iterations=200, seed=0x5EED0000,
                    calib=None, detector=_abi.DETECTOR_ORB_SLAM2) -> Config:
     """Reference defaults (extractor.cpp:86, odometry.cpp:28, common.h FR1).
-    detector: DETECTOR_ORB_SLAM2 (main.cpp:19-21) or DETECTOR_ADAPTIVE_FAST
-    (Extractor(FAST, ORB, ADAPTIVE), extractor.cpp:55-77)."""
+    detector: DETECTOR_ORB_SLAM2 (main.cpp:19-21), DETECTOR_ADAPTIVE_FAST
+    (Extractor(FAST, ORB, ADAPTIVE), extractor.cpp:55-77) or
+    DETECTOR_ADAPTIVE_ORB (Extractor(ORB, ORB, ADAPTIVE): the cv::ORB cell
+    detector of detectoradjuster.cpp:29)."""
     cfg = Config()
     load().odo_default_config(ptr(cfg), width, height, max_batch)
     cfg.detector = detector

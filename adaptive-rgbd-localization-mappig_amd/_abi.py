@@ -69,6 +69,7 @@ class Config(C.Structure):
 
 DETECTOR_ORB_SLAM2 = 0       # include/odo.h ODO_DETECTOR_ORB_SLAM2
 DETECTOR_ADAPTIVE_FAST = 1   # include/odo.h ODO_DETECTOR_ADAPTIVE_FAST
+DETECTOR_ADAPTIVE_ORB = 2    # include/odo.h ODO_DETECTOR_ADAPTIVE_ORB
 
 
 class FoldResult(C.Structure):

@@ -26,6 +26,7 @@
 //                   keypoints) on the blurred image, undistort, depth.
 #include "odo_device.h"
 #include "odo_internal.h"
+#include "odo_select.h"
 #include "../../include/odo_orb_pattern.h"
 
 namespace odo {
@@ -33,148 +34,14 @@ namespace odo {
 __constant__ int8_t c_apattern[1024];
 
 // ============================================================ S map
-// Tile: 128 x 8 output pixels, 4 per thread; input window staged in LDS with
-// dword loads of the pitched level 0 (columns tx0-4 .. tx0+131, rows ty0-3 ..
-// ty0+10). Pixels within 3 of the image border get S = 0 (FAST never tests
-// them), so out-of-image words are clamped reads whose values are unused.
-#define SM_TW 128
-#define SM_TH 8
-#define SM_LW (SM_TW + 8)            // bytes per LDS row
-#define SM_LR (SM_TH + 6)            // LDS rows
-
-typedef short short2v __attribute__((ext_vector_type(2)));
-
-ODO_INLINE short2v pk_min(short2v a, short2v b) { return __builtin_elementwise_min(a, b); }
-ODO_INLINE short2v pk_max(short2v a, short2v b) { return __builtin_elementwise_max(a, b); }
-
+// Tile: 128 x 8 output pixels of the pitched level 0 (smap_tile, odo_select.h).
 __global__ void __launch_bounds__(256) k_adapt_smap(const uint8_t* __restrict__ pyr, size_t pyr_stride, int w, int h,
                                                     int pitch, int tiles_x, uint8_t* __restrict__ smap,
                                                     size_t smap_stride) {
     __shared__ uint32_t lds[SM_LR * SM_LW / 4];
     const int f = blockIdx.y;
     const int tx0 = (blockIdx.x % tiles_x) * SM_TW, ty0 = (blockIdx.x / tiles_x) * SM_TH;
-    const uint8_t* img = pyr + (size_t)f * pyr_stride;
-    for (int i = threadIdx.x; i < SM_LR * (SM_LW / 4); i += 256) {
-        const int r = i / (SM_LW / 4), q = i % (SM_LW / 4);
-        int gy = ty0 - 3 + r;
-        gy = gy < 0 ? 0 : (gy >= h ? h - 1 : gy);
-        int gx = tx0 - 4 + 4 * q;
-        gx = gx < 0 ? 0 : (gx + 4 > pitch ? pitch - 4 : gx);
-        lds[i] = *reinterpret_cast<const uint32_t*>(img + (size_t)gy * pitch + gx);
-    }
-    __syncthreads();
-    const int r = threadIdx.x >> 5, q = threadIdx.x & 31;
-    const int y = ty0 + r, x = tx0 + 4 * q;
-    if (y >= h || x >= pitch) return;
-    // the 7 rows x 12 columns (x-4 .. x+7) the 4 pixels' circles touch: three
-    // aligned dwords per row; a circle pixel pair (columns c, c+1 of a row) is
-    // one v_perm into the two 16-bit halves
-    const int ly = r + 3;
-    uint32_t W[7][3];
-#pragma unroll
-    for (int dy = 0; dy < 7; dy++)
-#pragma unroll
-        for (int j = 0; j < 3; j++) W[dy][j] = lds[(ly - 3 + dy) * (SM_LW / 4) + q + j];
-    // bytes i, i+1 (i = 0..10 over the row's 12 bytes) -> 16-bit lanes (lo, hi)
-    auto pair16 = [&](int dy, int i) -> short2v {
-        const uint32_t lo = W[dy][i >> 2], hi = W[dy][(i >> 2) + 1 < 3 ? (i >> 2) + 1 : 2];
-        const int o = i & 3;  // byte offset within lo; o + 1 may spill into hi
-        const uint32_t sel = (uint32_t)o | 0x0c00u | ((uint32_t)(o + 1) << 16) | 0x0c000000u;
-        const uint32_t v = __builtin_amdgcn_perm(hi, lo, sel);
-        return *reinterpret_cast<const short2v*>(&v);
-    };
-    // circle offsets (x, y) of FAST_t<16> (App. A.3)
-    constexpr int cxo[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
-    constexpr int cyo[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
-    uint32_t out = 0;
-#pragma unroll
-    for (int pp = 0; pp < 4; pp += 2) {
-        // two pixels per packed 16-bit lane pair
-        short2v d[16];
-        const short2v v = pair16(3, 4 + pp);
-#pragma unroll
-        for (int k = 0; k < 16; k++) d[k] = v - pair16(3 + cyo[k], 4 + pp + cxo[k]);
-        short2v mn[16], mx[16];
-#pragma unroll
-        for (int k = 0; k < 16; k++) {
-            mn[k] = pk_min(d[k], d[(k + 1) & 15]);
-            mx[k] = pk_max(d[k], d[(k + 1) & 15]);
-        }
-        short2v mn4[16], mx4[16];
-#pragma unroll
-        for (int k = 0; k < 16; k++) {
-            mn4[k] = pk_min(mn[k], mn[(k + 2) & 15]);
-            mx4[k] = pk_max(mx[k], mx[(k + 2) & 15]);
-        }
-        short2v dark = short2v{0, 0}, bright = short2v{0, 0};  // max(arc min), min(arc max)
-#pragma unroll
-        for (int k = 0; k < 16; k++) {
-            const short2v a = pk_min(pk_min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]);
-            const short2v b = pk_max(pk_max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]);
-            dark = pk_max(dark, a);
-            bright = pk_min(bright, b);
-        }
-        const short2v s = pk_max(dark, -bright);
-#pragma unroll
-        for (int e = 0; e < 2; e++) {
-            const int xx = x + pp + e;
-            const int sv = e ? s.y : s.x;
-            const bool in = xx >= 3 && xx < w - 3 && y >= 3 && y < h - 3;
-            out |= (uint32_t)(in ? sv : 0) << (8 * (pp + e));
-        }
-    }
-    *reinterpret_cast<uint32_t*>(smap + (size_t)f * smap_stride + (size_t)y * pitch + x) = out;
-}
-
-// ============================================================ block helpers
-// ordered rank of `keep` among the workgroup's threads (thread order) and the
-// total; ws: >= 16 ints of LDS
-ODO_INLINE int block_rank(bool keep, int* ws, int* total) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
-    const uint64_t b = __ballot(keep);
-    const int in_wave = __popcll(b & ((1ull << lane) - 1ull));
-    if (lane == 0) ws[wv] = __popcll(b);
-    __syncthreads();
-    int base = 0, tot = 0;
-    for (int k = 0; k < nw; k++) {
-        const int c = ws[k];
-        if (k < wv) base += c;
-        tot += c;
-    }
-    __syncthreads();
-    *total = tot;
-    return base + in_wave;
-}
-
-// exclusive scan of two per-thread counts over the workgroup
-ODO_INLINE int2 block_scan2i(int a, int b, int (*ws)[2], int2* total) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
-    int ia = a, ib = b;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int x = __shfl_up(ia, o), y = __shfl_up(ib, o);
-        if (lane >= o) {
-            ia += x;
-            ib += y;
-        }
-    }
-    if (lane == 63) {
-        ws[wv][0] = ia;
-        ws[wv][1] = ib;
-    }
-    __syncthreads();
-    int ba = 0, bb = 0, ta = 0, tb = 0;
-    for (int k = 0; k < nw; k++) {
-        if (k < wv) {
-            ba += ws[k][0];
-            bb += ws[k][1];
-        }
-        ta += ws[k][0];
-        tb += ws[k][1];
-    }
-    __syncthreads();
-    *total = make_int2(ta, tb);
-    return make_int2(ba + ia - a, bb + ib - b);
+    smap_tile(pyr + (size_t)f * pyr_stride, w, h, pitch, tx0, ty0, smap + (size_t)f * smap_stride, lds);
 }
 
 // ============================================================ candidates
@@ -320,165 +187,6 @@ __global__ void __launch_bounds__(256) k_adapt_chain(const int* __restrict__ his
     if (threadIdx.x == 0) thresh[c] = th;
 }
 
-// ============================================================ std::nth_element
-// libstdc++ __introselect on packed keypoints (score << 24 | y << 12 | x),
-// comp(a, b) = score(a) > score(b) (ResponseComparator /
-// KeypointResponseGreater): key = 255 - score ascending. Every partition runs
-// on the whole workgroup: the Hoare scan pairs the k-th left stop (key >= pk)
-// with the k-th right stop (key <= pk) while they have not crossed (k < k*),
-// and cuts at min(L[k*], R[k*-1]) (the model checked against the real
-// std::nth_element in tests/test_adaptive_model.py).
-ODO_INLINE uint32_t sel_key(uint32_t e) { return 255u - (e >> 24); }
-
-struct SelState {
-    int first, last, depth, pk, ks, nl, nr, done;
-    int ws[16][2];
-};
-
-ODO_INLINE void sel_swap(uint32_t* A, int i, int j) {
-    const uint32_t t = A[i];
-    A[i] = A[j];
-    A[j] = t;
-}
-
-ODO_INLINE void sel_adjust_heap(uint32_t* A, int first, int hole, int len, uint32_t value) {
-    const int top = hole;
-    int child = hole;
-    while (child < (len - 1) / 2) {
-        child = 2 * (child + 1);
-        if (sel_key(A[first + child]) < sel_key(A[first + child - 1])) child--;
-        A[first + hole] = A[first + child];
-        hole = child;
-    }
-    if ((len & 1) == 0 && child == (len - 2) / 2) {
-        child = 2 * (child + 1);
-        A[first + hole] = A[first + child - 1];
-        hole = child - 1;
-    }
-    int parent = (hole - 1) / 2;
-    while (hole > top && sel_key(A[first + parent]) < sel_key(value)) {
-        A[first + hole] = A[first + parent];
-        hole = parent;
-        parent = (hole - 1) / 2;
-    }
-    A[first + hole] = value;
-}
-
-// std::__heap_select(first, middle, last) (depth-limit fallback; one lane)
-ODO_INLINE void sel_heap_select(uint32_t* A, int first, int middle, int last) {
-    const int len = middle - first;
-    if (len >= 2)
-        for (int parent = (len - 2) / 2;; parent--) {
-            sel_adjust_heap(A, first, parent, len, A[first + parent]);
-            if (parent == 0) break;
-        }
-    for (int i = middle; i < last; ++i)
-        if (sel_key(A[i]) < sel_key(A[first])) {  // __pop_heap(first, middle, i)
-            const uint32_t v = A[i];
-            A[i] = A[first];
-            sel_adjust_heap(A, first, 0, len, v);
-        }
-}
-
-ODO_INLINE void sel_insertion_sort(uint32_t* A, int first, int last) {
-    if (first == last) return;
-    for (int i = first + 1; i != last; ++i) {
-        const uint32_t v = A[i];
-        if (sel_key(v) < sel_key(A[first])) {
-            for (int k = i; k > first; --k) A[k] = A[k - 1];
-            A[first] = v;
-        } else {
-            int cur = i, next = i - 1;
-            while (sel_key(v) < sel_key(A[next])) {
-                A[cur] = A[next];
-                cur = next;
-                --next;
-            }
-            A[cur] = v;
-        }
-    }
-}
-
-// A: n elements (LDS or global); posL/posR: n ints of scratch; every thread of
-// the workgroup calls this.
-ODO_INLINE void block_nth_element(uint32_t* A, int n, int nth, int* posL, int* posR, SelState& S) {
-    if (n <= 0 || nth >= n) return;
-    const int t = threadIdx.x, T = blockDim.x;
-    if (t == 0) {
-        S.first = 0;
-        S.last = n;
-        S.depth = 2 * (31 - __builtin_clz((unsigned)n));
-        S.done = 0;
-    }
-    __syncthreads();
-    while (S.last - S.first > 3 && !S.done) {
-        const int first = S.first, last = S.last;
-        if (S.depth == 0) {
-            if (t == 0) {
-                sel_heap_select(A, first, nth + 1, last);
-                sel_swap(A, first, nth);
-                S.done = 1;
-            }
-            __syncthreads();
-            break;
-        }
-        if (t == 0) {
-            S.depth--;
-            // __move_median_to_first(first, first + 1, mid, last - 1)
-            const int a = first + 1, b = first + (last - first) / 2, c = last - 1;
-            const uint32_t ka = sel_key(A[a]), kb = sel_key(A[b]), kc = sel_key(A[c]);
-            int m;
-            if (ka < kb) m = kb < kc ? b : (ka < kc ? c : a);
-            else m = ka < kc ? a : (kb < kc ? c : b);
-            sel_swap(A, first, m);
-            S.pk = (int)sel_key(A[first]);
-        }
-        __syncthreads();
-        const uint32_t pk = (uint32_t)S.pk;
-        const int m = last - first - 1;
-        const int chunk = (m + T - 1) / T;
-        const int j0 = first + 1 + min(m, t * chunk), j1 = first + 1 + min(m, t * chunk + chunk);
-        int cg = 0, cl = 0;
-        for (int j = j0; j < j1; j++) {
-            const uint32_t k = sel_key(A[j]);
-            cg += k >= pk;
-            cl += k <= pk;
-        }
-        int2 tot;
-        const int2 base = block_scan2i(cg, cl, S.ws, &tot);
-        int rg = base.x, rl = base.y;
-        for (int j = j0; j < j1; j++) {
-            const uint32_t k = sel_key(A[j]);
-            if (k >= pk) posL[rg++] = j;
-            if (k <= pk) posR[tot.y - 1 - rl++] = j;  // posR[0] = the rightmost right stop
-        }
-        __syncthreads();
-        if (t == 0) {
-            // k* = #{k < min(nL, nR) : posL[k] < posR[k]} (monotone in k)
-            int lo = 0, hi = min(tot.x, tot.y);
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (posL[mid] < posR[mid]) lo = mid + 1;
-                else hi = mid;
-            }
-            S.ks = lo;
-        }
-        __syncthreads();
-        const int ks = S.ks;
-        for (int k = t; k < ks; k += T) sel_swap(A, posL[k], posR[k]);
-        __syncthreads();
-        if (t == 0) {
-            int cut = ks < tot.x ? posL[ks] : last;
-            if (ks > 0) cut = min(cut, posR[ks - 1]);
-            if (cut <= nth) S.first = cut;
-            else S.last = cut;
-        }
-        __syncthreads();
-    }
-    if (t == 0 && !S.done) sel_insertion_sort(A, S.first, S.last);
-    __syncthreads();
-}
-
 // ============================================================ per-cell select
 // One workgroup per (cell, frame): gather the survivors with S > t* from the
 // cell's bands in order (= cv::FAST's row-major emission), keepStrongest.
@@ -518,7 +226,7 @@ __global__ void __launch_bounds__(256) k_adapt_select(const uint32_t* __restrict
     }
     const int m = min(pos, n);
     __syncthreads();
-    if (m > max_per_cell) block_nth_element(A, m, max_per_cell, posL, posR, S);
+    if (m > max_per_cell) block_nth_element<uint32_t, ScoreKey>(A, m, max_per_cell, posL, posR, S);
     const int k = min(m, max_per_cell);
     uint32_t* out = cell_out + ((size_t)f * ncells + c) * max_per_cell;
     for (int i = threadIdx.x; i < k; i += blockDim.x) out[i] = A[i];
@@ -562,7 +270,7 @@ __global__ void __launch_bounds__(256) k_adapt_assemble(const uint32_t* __restri
     if (retain >= 0 && n > retain) {
         if (retain == 0) n = 0;
         else {
-            block_nth_element(A, n, retain, posL, posR, S);
+            block_nth_element<uint32_t, ScoreKey>(A, n, retain, posL, posR, S);
             if (threadIdx.x == 0) {
                 // std::partition(begin + n_points, end, response >= ambiguous)
                 // (libstdc++ bidirectional __partition)
@@ -666,7 +374,7 @@ __global__ void __launch_bounds__(256) k_adapt_finalize(const uint8_t* __restric
 __global__ void __launch_bounds__(256) k_adapt_select_dbg(uint32_t* A, int n, int nth, int mode, int* posL, int* posR,
                                                           int* n_out) {
     __shared__ SelState S;
-    block_nth_element(A, n, nth, posL, posR, S);
+    block_nth_element<uint32_t, ScoreKey>(A, n, nth, posL, posR, S);
     if (threadIdx.x == 0) {
         int m = n;
         if (mode == 1 && n > nth) {

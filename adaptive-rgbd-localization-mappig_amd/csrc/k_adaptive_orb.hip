@@ -1,0 +1,631 @@
+// Extractor(ORB, ORB, ADAPTIVE) for gfx950: the
+// grid-adapted detector of k_adaptive.hip with the cv::ORB inner detector of
+// Features/detectoradjuster.cpp:29 - cv::ORB::create(10000, 1.2f, 8, 15, 0,
+// 2, HARRIS_SCORE, 31, (int)thresh)->detect(cell sub-image) - then
+// Extractor::Extract's retainBest(1000) and cv::ORB::compute on the kept
+// keypoints, which carry the detector's octaves (extractor.cpp:39-50).
+// OpenCV 3.4 orb.cpp is restated in oracle/orb_ref.cpp (orbcv_detect,
+// orb_compute_provided_levels); DESIGN.md §4 "ADAPTIVE, cv::ORB inner".
+//
+// As in the FAST-inner path, the threshold never touches the pixels: FAST at
+// threshold t on a cell level keeps p iff S(p) > t and p passes the
+// threshold-free NMS, so one S map per cell level gives the candidates of
+// every threshold. Each level then keeps retainBest(2 * quota) by FAST score
+// and retainBest(quota) by Harris response; quota >= 606 > gridMax 113, so a
+// level that binds makes the cell's count exceed gridMax whatever the exact
+// count is, and the DetectorAdjuster chain runs on sum_l min(count_l, quota_l)
+// (the host checks the quota bound).
+//
+//   k_oa_pyr       per (frame, cell): the cell's 8-level pyramid (INTER_LINEAR,
+//                  App. A.2), levels ping-ponged in LDS, written to HBM
+//   k_oa_smap      S map of every cell level (smap_tile)
+//   k_oa_cand      per (frame, band): NMS survivors in [15, w-15) x [15, h-15)
+//                  in row-major order + per-level S histogram
+//   k_oa_count     per (frame, cell): the chain's count table for every t
+//   (k_adapt_chain) the tooFew/tooMany/good chain over the batch, in frame order
+//   k_oa_select    per (frame, cell): survivors with S > t*, retainBest by FAST
+//                  score, Harris responses, retainBest by Harris, keepStrongest
+//                  by |response| (libstdc++ introselect, odo_select.h)
+//   k_oa_assemble  per frame: cells in grid order, retainBest(1000),
+//                  runByImageBorder(31), stable regroup by octave
+//   k_oa_finalize  IC angle on the cell level, rBRIEF on the blurred level of
+//                  the frame pyramid (samples past the level edge read the
+//                  unblurred REFLECT_101 border), keypoint record
+#include "odo_device.h"
+#include "odo_internal.h"
+#include "odo_select.h"
+#include "../../include/odo_orb_pattern.h"
+
+namespace odo {
+
+static_assert(OA_TILE_W == SM_TW && OA_TILE_H == SM_TH, "S-map tile table and smap_tile disagree");
+
+__constant__ int8_t c_opattern[1024];
+
+// ============================================================ cell pyramids
+// One workgroup per (frame, cell). Level 0 = the cell's ROI of the frame's
+// gray level 0; level l = cv::resize(level l-1, INTER_LINEAR) to the getScale
+// size (host). Source and destination levels alternate between two LDS
+// buffers; every level is also written to the frame's cell-pyramid buffer
+// (pitched rows, zero padding). Resize tables are made in LDS with the
+// generic-path rules of App. A.2 (the host rules of odo_capi.cpp
+// build_geometry).
+__global__ void __launch_bounds__(512) k_oa_pyr(const uint8_t* __restrict__ pyr, size_t pyr_stride, int gpitch,
+                                                const OaCell* __restrict__ cells, const OaImg* __restrict__ imgs,
+                                                int buf0, uint8_t* __restrict__ cpyr, size_t cp_stride) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t op_lds[];
+    __shared__ ResizeX xt[1024];
+    __shared__ ResizeY yt[1024];
+    const int c = blockIdx.x, f = blockIdx.y;
+    const OaCell C = cells[c];
+    uint8_t* buf[2] = {op_lds, op_lds + buf0};
+    uint8_t* out = cpyr + (size_t)f * cp_stride;
+    {
+        const OaImg I = imgs[C.img0];
+        const uint8_t* g = pyr + (size_t)f * pyr_stride + (size_t)C.rs * gpitch + C.cs;
+        const int nq = I.pitch >> 2;
+        for (int i = threadIdx.x; i < I.h * nq; i += blockDim.x) {
+            const int r = i / nq, q = i - r * nq;
+            uint32_t v = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if (4 * q + j < I.w) v |= (uint32_t)g[(size_t)r * gpitch + 4 * q + j] << (8 * j);
+            reinterpret_cast<uint32_t*>(buf[0])[i] = v;
+            reinterpret_cast<uint32_t*>(out + I.off)[i] = v;
+        }
+    }
+    for (int l = 1; l < OA_NLEV; l++) {
+        const OaImg S = imgs[C.img0 + l - 1], D = imgs[C.img0 + l];
+        const uint8_t* src = buf[(l - 1) & 1];
+        uint8_t* dst = buf[l & 1];
+        const double scale_x = 1. / ((double)D.w / S.w), scale_y = 1. / ((double)D.h / S.h);
+        for (int dx = threadIdx.x; dx < D.w; dx += blockDim.x) {
+            float fx = (float)((dx + 0.5) * scale_x - 0.5);
+            int sx = cv_floor(fx);
+            fx -= sx;
+            if (sx < 0) {
+                fx = 0;
+                sx = 0;
+            }
+            ResizeX X;
+            if (sx + 1 >= S.w) {  // past xmax: S[w-1] * 2048
+                X.sx0 = X.sx1 = S.w - 1;
+                X.a0 = 2048;
+                X.a1 = 0;
+            } else {
+                X.sx0 = sx;
+                X.sx1 = sx + 1;
+                X.a0 = cv_round((1.f - fx) * 2048);
+                X.a1 = cv_round(fx * 2048);
+            }
+            xt[dx] = X;
+        }
+        for (int dy = threadIdx.x; dy < D.h; dy += blockDim.x) {
+            float fy = (float)((dy + 0.5) * scale_y - 0.5);
+            const int sy = cv_floor(fy);
+            fy -= sy;
+            ResizeY Y;
+            Y.b0 = cv_round((1.f - fy) * 2048);
+            Y.b1 = cv_round(fy * 2048);
+            Y.sy0 = min(max(sy, 0), S.h - 1);
+            Y.sy1 = min(max(sy + 1, 0), S.h - 1);
+            yt[dy] = Y;
+        }
+        __syncthreads();
+        const int nq = D.pitch >> 2;
+        for (int i = threadIdx.x; i < D.h * nq; i += blockDim.x) {
+            const int r = i / nq, q = i - r * nq;
+            const ResizeY Y = yt[r];
+            const uint8_t* r0 = src + Y.sy0 * S.pitch;
+            const uint8_t* r1 = src + Y.sy1 * S.pitch;
+            uint32_t packed = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int dx = 4 * q + j;
+                if (dx < D.w) {
+                    const ResizeX X = xt[dx];
+                    const int h0 = r0[X.sx0] * X.a0 + r0[X.sx1] * X.a1;
+                    const int h1 = r1[X.sx0] * X.a0 + r1[X.sx1] * X.a1;
+                    int v = (h0 * Y.b0 + h1 * Y.b1 + (1 << 21)) >> 22;
+                    v = v < 0 ? 0 : (v > 255 ? 255 : v);
+                    packed |= (uint32_t)v << (8 * j);
+                }
+            }
+            reinterpret_cast<uint32_t*>(dst)[i] = packed;
+            reinterpret_cast<uint32_t*>(out + D.off)[i] = packed;
+        }
+        __syncthreads();
+    }
+}
+
+// ============================================================ S maps
+__global__ void __launch_bounds__(256) k_oa_smap(const uint8_t* __restrict__ cpyr, size_t cp_stride,
+                                                 const OaImg* __restrict__ imgs, const OaTile* __restrict__ tiles,
+                                                 uint8_t* __restrict__ csmap) {
+    __shared__ uint32_t lds[SM_LR * SM_LW / 4];
+    const int f = blockIdx.y;
+    const OaTile T = tiles[blockIdx.x];
+    const OaImg I = imgs[T.img];
+    smap_tile(cpyr + (size_t)f * cp_stride + I.off, I.w, I.h, I.pitch, T.tx0, T.ty0,
+              csmap + (size_t)f * cp_stride + I.off, lds);
+}
+
+// ============================================================ candidates
+// One workgroup per (band, frame): the band's S rows with one row / column of
+// halo (real S values: the halo lies inside FAST's detection region [3, h-3),
+// where NMS sees it; S is 0 outside it) staged in LDS; survivors of the
+// threshold-free NMS (S >= 2, S > all 8 neighbours) inside runByImageBorder's
+// [15, w-15) x [15, h-15), in row-major order, + the level's S histogram.
+#define OA_MAXW 1024
+__global__ void __launch_bounds__(256) k_oa_cand(const uint8_t* __restrict__ csmap, size_t cp_stride,
+                                                 const OaImg* __restrict__ imgs, const OaBand* __restrict__ bands,
+                                                 int nimgs, uint32_t* __restrict__ cand, size_t cand_stride,
+                                                 int* __restrict__ band_cnt, int nbands, int* __restrict__ hist) {
+    __shared__ uint8_t s[(AD_BH + 2) * (OA_MAXW + 2)];
+    __shared__ int sh[256];
+    __shared__ int ws[16];
+    const int f = blockIdx.y;
+    const OaBand B = bands[blockIdx.x];
+    const OaImg I = imgs[B.img];
+    const int c0 = OA_EDGE, c1 = I.w - OA_EDGE;
+    const int cw = c1 - c0, lw = cw + 2;
+    const int rows = B.y1 - B.y0;
+    const uint8_t* S = csmap + (size_t)f * cp_stride + I.off;
+    sh[threadIdx.x] = 0;
+    for (int r = 0; r < rows + 2; r++) {
+        const uint8_t* srow = S + (size_t)(B.y0 - 1 + r) * I.pitch + (c0 - 1);
+        for (int q = threadIdx.x; q < lw; q += 256) s[r * lw + q] = srow[q];
+    }
+    __syncthreads();
+    const int npx = rows * cw;
+    const int chunk = (npx + 255) / 256;
+    const int i0 = min(npx, (int)threadIdx.x * chunk), i1 = min(npx, i0 + chunk);
+    const int r0 = cw > 0 ? i0 / cw : 0, q0 = i0 - r0 * cw;
+    auto survivor = [&](int r, int q, int* sv) -> bool {
+        const uint8_t* p = s + (r + 1) * lw + (q + 1);
+        const int v = p[0];
+        *sv = v;
+        if (v < 2) return false;
+        int m = max(max(p[-lw - 1], p[-lw]), max(p[-lw + 1], p[-1]));
+        m = max(m, max(max(p[1], p[lw - 1]), max(p[lw], p[lw + 1])));
+        return v > m;
+    };
+    int cnt = 0;
+    uint32_t smask = 0;
+    {
+        int r = r0, q = q0;
+        for (int i = i0; i < i1; i++) {
+            int sv;
+            if (survivor(r, q, &sv)) {
+                cnt++;
+                atomicAdd(&sh[sv], 1);
+                if (i - i0 < 32) smask |= 1u << (i - i0);
+            }
+            if (++q == cw) {
+                q = 0;
+                r++;
+            }
+        }
+    }
+    int2 tot;
+    const int2 base = block_scan2i(cnt, 0, reinterpret_cast<int(*)[2]>(ws), &tot);
+    uint32_t* out = cand + (size_t)f * cand_stride + B.cand_off;
+    int o = base.x;
+    {
+        int r = r0, q = q0;
+        for (int i = i0; i < i1; i++) {
+            int sv = s[(r + 1) * lw + (q + 1)];
+            const bool keep = (i - i0 < 32) ? ((smask >> (i - i0)) & 1u) != 0 : survivor(r, q, &sv);
+            if (keep) out[o++] = ((uint32_t)sv << 24) | ((uint32_t)(B.y0 + r) << 12) | (uint32_t)(c0 + q);
+            if (++q == cw) {
+                q = 0;
+                r++;
+            }
+        }
+    }
+    if (threadIdx.x == 0) band_cnt[(size_t)f * nbands + blockIdx.x] = tot.x;
+    __syncthreads();
+    const int hv = sh[threadIdx.x];
+    if (hv) atomicAdd(&hist[((size_t)f * nimgs + B.img) * 256 + threadIdx.x], hv);
+}
+
+// ============================================================ count tables
+// Per (frame, cell): n(t) = sum_l min(#{S_l > t}, quota_l), written as a
+// pseudo-histogram ph[t] = n(t-1) - n(t) (ph[0] = 0), so k_adapt_chain's
+// suffix sums give back n(t) (n(255) = 0).
+__global__ void __launch_bounds__(256) k_oa_count(const int* __restrict__ hist, const OaCell* __restrict__ cells,
+                                                  const OaImg* __restrict__ imgs, int nimgs, int ncells,
+                                                  int* __restrict__ phist) {
+    __shared__ int hv[OA_NLEV][256];
+    __shared__ int nt[256];
+    const int c = blockIdx.x, f = blockIdx.y, t = threadIdx.x;
+    const OaCell C = cells[c];
+    for (int l = 0; l < OA_NLEV; l++) hv[l][t] = hist[((size_t)f * nimgs + C.img0 + l) * 256 + t];
+    __syncthreads();
+    int n = 0;
+    for (int l = 0; l < OA_NLEV; l++) {
+        int above = 0;
+        for (int s2 = t + 1; s2 < 256; s2++) above += hv[l][s2];
+        n += min(above, imgs[C.img0 + l].quota);
+    }
+    nt[t] = n;
+    __syncthreads();
+    phist[((size_t)f * ncells + c) * 256 + t] = t ? nt[t - 1] - n : 0;
+}
+
+// ============================================================ per-cell select
+// Float responses as ascending 32-bit keys: comp(a, b) = a.response >
+// b.response is key(a) < key(b) for key = ~ord(response), ord the
+// order-preserving map of IEEE floats (no response is -0 or NaN).
+ODO_INLINE uint32_t f_ord(float v) {
+    const uint32_t u = __float_as_uint(v);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+ODO_INLINE float f_unord(uint32_t o) { return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o); }
+ODO_INLINE uint32_t key_greater(float r) { return ~f_ord(r); }
+ODO_INLINE float resp_of_key(uint32_t k) { return f_unord(~k); }
+
+struct HiKey {  // 64-bit elements ordered by their high word
+    static ODO_INLINE uint32_t key(uint64_t e) { return (uint32_t)(e >> 32); }
+};
+
+// HarrisResponses (orb.cpp): 7x7 block of the 3x3 Sobel-like gradients around
+// (x0, y0), integer sums, float response (-ffp-contract=off keeps the order).
+ODO_INLINE float harris_at(const uint8_t* img, int pitch, int x0, int y0) {
+    int a = 0, b = 0, c = 0;
+    for (int i = 0; i < 7; i++) {
+        const uint8_t* r0 = img + (y0 - 4 + i) * pitch;
+        const uint8_t* r1 = r0 + pitch;
+        const uint8_t* r2 = r1 + pitch;
+#pragma unroll
+        for (int j = 0; j < 7; j++) {
+            const int x = x0 - 3 + j;
+            const int Ix = (r1[x + 1] - r1[x - 1]) * 2 + (r0[x + 1] - r0[x - 1]) + (r2[x + 1] - r2[x - 1]);
+            const int Iy = (r2[x] - r0[x]) * 2 + (r2[x - 1] - r0[x - 1]) + (r2[x + 1] - r0[x + 1]);
+            a += Ix * Ix;
+            b += Iy * Iy;
+            c += Ix * Iy;
+        }
+    }
+    const float scale = 1.f / ((1 << 2) * 7 * 255.f);
+    const float scale_sq_sq = scale * scale * scale * scale;
+    const float fa = (float)a, fb = (float)b, fc = (float)c;
+    return (fa * fb - fc * fc - 0.04f * (fa + fb) * (fa + fb)) * scale_sq_sq;
+}
+
+// One workgroup per (cell, frame); its arrays live in a global scratch slice
+// (sizes up to the cell's candidate capacity): A32 (level survivors), posL /
+// posR (selection scratch), A64 (Harris-keyed level list, then the
+// keepStrongest list), rec (the cell's keypoints, level-major). Record =
+// key_greater(response) << 32 | level << 24 | y << 12 | x (level coords).
+__global__ void __launch_bounds__(256) k_oa_select(const uint32_t* __restrict__ cand, size_t cand_stride,
+                                                   const int* __restrict__ band_cnt, int nbands,
+                                                   const OaBand* __restrict__ bands, const OaImg* __restrict__ imgs,
+                                                   const OaCell* __restrict__ cells, int ncells,
+                                                   const int* __restrict__ tsel, const uint8_t* __restrict__ cpyr,
+                                                   size_t cp_stride, int max_per_cell, uint8_t* __restrict__ scr,
+                                                   size_t scr_stride, int ncap, uint64_t* __restrict__ cell_out,
+                                                   int* __restrict__ cell_cnt) {
+    __shared__ SelState S;
+    __shared__ int ws[16];
+    __shared__ int s_n;
+    const int c = blockIdx.x, f = blockIdx.y;
+    const OaCell C = cells[c];
+    const int ts = tsel[(size_t)f * ncells + c];
+    uint8_t* base = scr + ((size_t)f * ncells + c) * scr_stride;
+    uint64_t* A64 = reinterpret_cast<uint64_t*>(base);
+    uint64_t* rec = A64 + ncap;
+    uint32_t* A32 = reinterpret_cast<uint32_t*>(rec + ncap);
+    int* posL = reinterpret_cast<int*>(A32 + ncap);
+    int* posR = posL + ncap;
+    const uint32_t* fc = cand + (size_t)f * cand_stride;
+    const uint8_t* fp = cpyr + (size_t)f * cp_stride;
+    int cnt = 0;
+    for (int l = 0; l < OA_NLEV; l++) {
+        const OaImg I = imgs[C.img0 + l];
+        // FAST(t*) + runByImageBorder: the level's survivors with S > t*, in order
+        int m = 0;
+        for (int b = I.band0; b < I.band1; b++) {
+            const int bc = band_cnt[(size_t)f * nbands + b];
+            const uint32_t* src = fc + bands[b].cand_off;
+            for (int i0 = 0; i0 < bc; i0 += blockDim.x) {
+                const int i = i0 + threadIdx.x;
+                const uint32_t e = i < bc ? src[i] : 0u;
+                const bool keep = i < bc && (int)(e >> 24) > ts;
+                int tot;
+                const int r = block_rank(keep, ws, &tot);
+                if (keep) A32[m + r] = e;
+                m += tot;
+            }
+        }
+        __syncthreads();
+        // retainBest(2 * quota) by FAST score
+        if (m > 2 * I.quota) {
+            block_nth_element<uint32_t, ScoreKey>(A32, m, 2 * I.quota, posL, posR, S);
+            if (threadIdx.x == 0)
+                s_n = sel_partition_le<uint32_t, ScoreKey>(A32, 2 * I.quota, m, ScoreKey::key(A32[2 * I.quota - 1]));
+            __syncthreads();
+            m = s_n;
+        }
+        // Harris responses on the unblurred cell level
+        const uint8_t* img = fp + I.off;
+        for (int i = threadIdx.x; i < m; i += blockDim.x) {
+            const uint32_t e = A32[i];
+            const int x = (int)(e & 0xfff), y = (int)((e >> 12) & 0xfff);
+            const float h = harris_at(img, I.pitch, x, y);
+            A64[i] = ((uint64_t)key_greater(h) << 32) | ((uint32_t)l << 24) | (e & 0xffffffu);
+        }
+        __syncthreads();
+        // retainBest(quota) by Harris response
+        if (m > I.quota) {
+            block_nth_element<uint64_t, HiKey>(A64, m, I.quota, posL, posR, S);
+            if (threadIdx.x == 0) s_n = sel_partition_le<uint64_t, HiKey>(A64, I.quota, m, HiKey::key(A64[I.quota - 1]));
+            __syncthreads();
+            m = s_n;
+        }
+        for (int i = threadIdx.x; i < m; i += blockDim.x) rec[cnt + i] = A64[i];
+        cnt += m;
+        __syncthreads();
+    }
+    uint64_t* out = cell_out + ((size_t)f * ncells + c) * max_per_cell;
+    if (cnt > max_per_cell) {
+        // keepStrongest: nth_element at begin + N by |response|, erase the tail
+        for (int i = threadIdx.x; i < cnt; i += blockDim.x)
+            A64[i] = ((uint64_t)key_greater(fabsf(resp_of_key((uint32_t)(rec[i] >> 32)))) << 32) | (uint32_t)i;
+        __syncthreads();
+        block_nth_element<uint64_t, HiKey>(A64, cnt, max_per_cell, posL, posR, S);
+        for (int i = threadIdx.x; i < max_per_cell; i += blockDim.x) out[i] = rec[(uint32_t)A64[i]];
+    } else {
+        for (int i = threadIdx.x; i < cnt; i += blockDim.x) out[i] = rec[i];
+    }
+    if (threadIdx.x == 0) cell_cnt[(size_t)f * ncells + c] = min(cnt, max_per_cell);
+}
+
+// ============================================================ per-frame assemble
+// aggregateKeypointsPerGridCell, retainBest(retain) by response, cv::ORB::
+// compute's runByImageBorder(31) and its stable regroup by octave. Output per
+// keypoint: key_greater(response) << 32 | cell << 27 | level << 24 | y << 12 | x.
+__global__ void __launch_bounds__(256) k_oa_assemble(const uint64_t* __restrict__ cell_out,
+                                                     const int* __restrict__ cell_cnt, const OaCell* __restrict__ cells,
+                                                     int ncells, int max_per_cell, int retain, int w, int h,
+                                                     OaScales sc, uint64_t* __restrict__ akp, int akp_stride,
+                                                     int* __restrict__ nkp, int kp_cap) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t oa_dyn[];
+    __shared__ SelState S;
+    __shared__ int ws[16];
+    __shared__ int s_off[65];
+    __shared__ int s_n;
+    const int f = blockIdx.x;
+    const int cap = ncells * max_per_cell;
+    uint64_t* rec = oa_dyn;
+    uint64_t* A = rec + cap;
+    int* posL = reinterpret_cast<int*>(A + cap);
+    int* posR = posL + cap;
+    if (threadIdx.x == 0) {
+        int acc = 0;
+        for (int c = 0; c < ncells; c++) {
+            s_off[c] = acc;
+            acc += cell_cnt[(size_t)f * ncells + c];
+        }
+        s_off[ncells] = acc;
+    }
+    __syncthreads();
+    int n = s_off[ncells];
+    for (int c = 0; c < ncells; c++) {
+        const int cnt = s_off[c + 1] - s_off[c];
+        const uint64_t* src = cell_out + ((size_t)f * ncells + c) * max_per_cell;
+        for (int i = threadIdx.x; i < cnt; i += blockDim.x) {
+            rec[s_off[c] + i] = src[i] | ((uint64_t)c << 27);
+            A[s_off[c] + i] = (src[i] & 0xffffffff00000000ull) | (uint32_t)(s_off[c] + i);
+        }
+    }
+    __syncthreads();
+    if (retain >= 0 && n > retain) {
+        if (retain == 0) n = 0;
+        else {
+            block_nth_element<uint64_t, HiKey>(A, n, retain, posL, posR, S);
+            if (threadIdx.x == 0) s_n = sel_partition_le<uint64_t, HiKey>(A, retain, n, HiKey::key(A[retain - 1]));
+            __syncthreads();
+            n = s_n;
+        }
+    }
+    // runByImageBorder(31) on the image coordinates, then octave-major (stable)
+    const float B = 31.f;
+    const bool ok_img = h > 62 && w > 62;
+    int o = 0;
+    for (int lv = 0; lv < OA_NLEV; lv++) {
+        for (int i0 = 0; i0 < n; i0 += blockDim.x) {
+            const int i = i0 + threadIdx.x;
+            bool keep = false;
+            uint64_t e = 0;
+            if (i < n && ok_img) {
+                e = rec[(uint32_t)A[i]];
+                const int l = (int)((e >> 24) & 7), cc = (int)((e >> 27) & 15);
+                if (l == lv) {
+                    const OaCell C = cells[cc];
+                    const float x = (float)(int)(e & 0xfff) * sc.s[l] + (float)C.cs;
+                    const float y = (float)(int)((e >> 12) & 0xfff) * sc.s[l] + (float)C.rs;
+                    keep = x >= B && x < (float)(w - 31) && y >= B && y < (float)(h - 31);
+                }
+            }
+            int tot;
+            const int r = block_rank(keep, ws, &tot);
+            if (keep && o + r < kp_cap) akp[(size_t)f * akp_stride + o + r] = e;
+            o += tot;
+        }
+    }
+    if (threadIdx.x == 0) nkp[f] = min(o, kp_cap);
+}
+
+// ============================================================ finalize
+// Four keypoints per wave, 16 lanes each. IC angle (ICAngles, orb.cpp) on the
+// keypoint's cell level: lane v sums disc row pair +-v (lane 0 the centre
+// row), then a 16-lane butterfly. rBRIEF (computeOrbDescriptors): centre
+// cvRound(pt / scale) on the frame pyramid's level; 16 tests per lane; a
+// sample inside the level reads the blurred level, one outside reads the
+// unblurred level at the REFLECT_101 position (the bordered pyramid's border,
+// which the in-place ROI blur leaves untouched).
+__constant__ int c_oumax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
+
+ODO_INLINE int refl101(int i, int n) {
+    while (i < 0 || i >= n) i = i < 0 ? -i : 2 * n - 2 - i;
+    return i;
+}
+
+#define OF_KPW 4
+#define OF_KPB (4 * OF_KPW)
+__global__ void __launch_bounds__(256) k_oa_finalize(const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
+                                                     size_t pyr_stride, const LevelDesc* __restrict__ lv,
+                                                     const uint8_t* __restrict__ cpyr, size_t cp_stride,
+                                                     const OaImg* __restrict__ imgs, const OaCell* __restrict__ cells,
+                                                     OaScales sc, const uint64_t* __restrict__ akp, int akp_stride,
+                                                     const int* __restrict__ nkp, orb_kp* __restrict__ kps,
+                                                     uint8_t* __restrict__ desc, int kp_cap) {
+    __shared__ uint64_t s_bal[4][16];
+    const int f = blockIdx.y;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int g = lane >> 4, sub = lane & 15;
+    const int n = nkp[f];
+    if (blockIdx.x * OF_KPB >= n) return;  // whole workgroup idle
+    const int idx = blockIdx.x * OF_KPB + wave * OF_KPW + g;
+    const bool valid = idx < n;
+    const uint64_t e = valid ? akp[(size_t)f * akp_stride + idx] : 0ull;
+    const int cc = (int)((e >> 27) & 15), l = (int)((e >> 24) & 7);
+    const int kx = (int)(e & 0xfff), ky = (int)((e >> 12) & 0xfff);
+    const OaCell C = cells[cc];
+    const float s = sc.s[l];
+    const float px = (float)kx * s + (float)C.cs, py = (float)ky * s + (float)C.rs;
+    // IC angle
+    int m10 = 0, m01 = 0;
+    if (valid) {
+        const OaImg I = imgs[C.img0 + l];
+        const uint8_t* ctr = cpyr + (size_t)f * cp_stride + I.off + (size_t)ky * I.pitch + kx;
+        const int v = sub, d = c_oumax[v];
+        if (v == 0) {
+            for (int u = -15; u <= 15; u++) m10 += u * ctr[u];
+        } else {
+            int vs = 0;
+            for (int u = -d; u <= d; u++) {
+                const int vp = ctr[u + v * I.pitch], vm = ctr[u - v * I.pitch];
+                vs += vp - vm;
+                m10 += u * (vp + vm);
+            }
+            m01 = v * vs;
+        }
+    }
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) {
+        m10 += __shfl_xor(m10, o, 16);
+        m01 += __shfl_xor(m01, o, 16);
+    }
+    const float angle = fast_atan2((float)m01, (float)m10);
+    const float ang = angle * (float)(3.14159265358979323846 / 180.f);
+    double sd, cd;
+    sincos((double)ang, &sd, &cd);
+    const float a = (float)cd, b = (float)sd;
+    // rBRIEF
+    const LevelDesc L = lv[l];
+    const float inv = 1.f / s;
+    const int cy = cv_round(py * inv), cx = cv_round(px * inv);
+    const uint8_t* bl = blur + (size_t)f * pyr_stride + L.off;
+    const uint8_t* un = pyr + (size_t)f * pyr_stride + L.off;
+    auto sample = [&](float x, float y) -> int {
+        const int yy = cy + cv_round(x * b + y * a), xx = cx + cv_round(x * a - y * b);
+        if (yy >= 0 && yy < L.h && xx >= 0 && xx < L.w) return bl[yy * L.pitch + xx];
+        return un[refl101(yy, L.h) * L.pitch + refl101(xx, L.w)];
+    };
+    int tv0[16], tv1[16];
+#pragma unroll
+    for (int w = 0; w < 16; w++) {
+        const int bit = w * 16 + sub;
+        tv0[w] = valid ? sample((float)c_opattern[4 * bit + 0], (float)c_opattern[4 * bit + 1]) : 0;
+        tv1[w] = valid ? sample((float)c_opattern[4 * bit + 2], (float)c_opattern[4 * bit + 3]) : 0;
+    }
+#pragma unroll
+    for (int w = 0; w < 16; w++) {
+        const uint64_t bal = __ballot(tv0[w] < tv1[w]);
+        if (lane == 0) s_bal[wave][w] = bal;
+    }
+    __syncthreads();
+    if (valid && sub < 8) {
+        const uint32_t lo = (uint32_t)(s_bal[wave][2 * sub] >> (16 * g)) & 0xffffu;
+        const uint32_t hi = (uint32_t)(s_bal[wave][2 * sub + 1] >> (16 * g)) & 0xffffu;
+        reinterpret_cast<uint32_t*>(desc + ((size_t)f * kp_cap + idx) * 32)[sub] = lo | (hi << 16);
+    }
+    if (valid && sub == 0) {
+        orb_kp* kp = kps + (size_t)f * kp_cap + idx;
+        kp->x = px;
+        kp->y = py;
+        kp->size = (float)OA_PATCH * s;
+        kp->angle = angle;
+        kp->response = resp_of_key((uint32_t)(e >> 32));
+        kp->octave = l;
+        kp->class_id = -1;
+    }
+}
+
+// ============================================================ launch wrappers
+void upload_adaptive_orb_constants() {
+    hipMemcpyToSymbol(HIP_SYMBOL(c_opattern), ODO_ORB_PATTERN, sizeof(ODO_ORB_PATTERN));
+}
+
+void launch_oa_pyr(hipStream_t st, const uint8_t* pyr, size_t pyr_stride, int gpitch, const OaCell* cells, int ncells,
+                   const OaImg* imgs, int buf0, int buf1, uint8_t* cpyr, size_t cp_stride, int nframes) {
+    const size_t lds = (size_t)buf0 + buf1;
+    hipFuncSetAttribute((const void*)k_oa_pyr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_oa_pyr, dim3(ncells, nframes), dim3(512), lds, st, pyr, pyr_stride, gpitch, cells, imgs, buf0,
+                       cpyr, cp_stride);
+}
+
+void launch_oa_smap(hipStream_t st, const uint8_t* cpyr, size_t cp_stride, const OaImg* imgs, const OaTile* tiles,
+                    int ntiles, uint8_t* csmap, int nframes) {
+    hipLaunchKernelGGL(k_oa_smap, dim3(ntiles, nframes), dim3(256), 0, st, cpyr, cp_stride, imgs, tiles, csmap);
+}
+
+void launch_oa_cand(hipStream_t st, const uint8_t* csmap, size_t cp_stride, const OaImg* imgs, int nimgs,
+                    const OaBand* bands, int nbands, uint32_t* cand, size_t cand_stride, int* band_cnt, int* hist,
+                    int nframes) {
+    hipLaunchKernelGGL(k_oa_cand, dim3(nbands, nframes), dim3(256), 0, st, csmap, cp_stride, imgs, bands, nimgs, cand,
+                       cand_stride, band_cnt, nbands, hist);
+}
+
+void launch_oa_count(hipStream_t st, const int* hist, const OaCell* cells, const OaImg* imgs, int nimgs, int ncells,
+                     int* phist, int nframes) {
+    hipLaunchKernelGGL(k_oa_count, dim3(ncells, nframes), dim3(256), 0, st, hist, cells, imgs, nimgs, ncells, phist);
+}
+
+size_t oa_select_scratch_bytes(int ncap) { return (size_t)ncap * (8 + 8 + 4 + 4 + 4); }
+
+void launch_oa_select(hipStream_t st, const uint32_t* cand, size_t cand_stride, const int* band_cnt, int nbands,
+                      const OaBand* bands, const OaImg* imgs, const OaCell* cells, int ncells, const int* tsel,
+                      const uint8_t* cpyr, size_t cp_stride, int max_per_cell, uint8_t* scr, size_t scr_stride,
+                      int ncap, uint64_t* cell_out, int* cell_cnt, int nframes) {
+    hipLaunchKernelGGL(k_oa_select, dim3(ncells, nframes), dim3(256), 0, st, cand, cand_stride, band_cnt, nbands, bands,
+                       imgs, cells, ncells, tsel, cpyr, cp_stride, max_per_cell, scr, scr_stride, ncap, cell_out,
+                       cell_cnt);
+}
+
+size_t oa_assemble_lds_bytes(int ncells, int max_per_cell) { return (size_t)ncells * max_per_cell * 24; }
+
+void launch_oa_assemble(hipStream_t st, const uint64_t* cell_out, const int* cell_cnt, const OaCell* cells,
+                        int ncells, int max_per_cell, int retain, int w, int h, OaScales sc, uint64_t* akp,
+                        int akp_stride, int* nkp, int kp_cap, int nframes) {
+    const size_t lds = oa_assemble_lds_bytes(ncells, max_per_cell);
+    if (lds > 64 * 1024)
+        hipFuncSetAttribute((const void*)k_oa_assemble, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_oa_assemble, dim3(nframes), dim3(256), lds, st, cell_out, cell_cnt, cells, ncells,
+                       max_per_cell, retain, w, h, sc, akp, akp_stride, nkp, kp_cap);
+}
+
+void launch_oa_finalize(hipStream_t st, const uint8_t* pyr, const uint8_t* blur, size_t pyr_stride,
+                        const LevelDesc* lv, const uint8_t* cpyr, size_t cp_stride, const OaImg* imgs,
+                        const OaCell* cells, OaScales sc, const uint64_t* akp, int akp_stride, const int* nkp,
+                        const uint16_t* depth, size_t depth_stride, int img_w, FrameCalib cal, orb_kp* kps,
+                        uint8_t* desc, float* kun, float* xyz, float* ur, int kp_cap, int nframes) {
+    dim3 g((kp_cap + OF_KPB - 1) / OF_KPB, nframes);
+    hipLaunchKernelGGL(k_oa_finalize, g, dim3(256), 0, st, pyr, blur, pyr_stride, lv, cpyr, cp_stride, imgs, cells, sc,
+                       akp, akp_stride, nkp, kps, desc, kp_cap);
+    launch_kp_geometry(st, kps, nkp, depth, depth_stride, img_w, cal, kun, xyz, ur, kp_cap, nframes);
+}
+
+}  // namespace odo

@@ -265,6 +265,26 @@ struct odo_ctx {
     int *aband_cnt = nullptr, *ahist = nullptr, *atsel = nullptr, *ansel = nullptr, *acell_cnt = nullptr;
     double* athresh = nullptr;
     float a_cos = 1.f, a_sin = 0.f;
+    // ODO_DETECTOR_ADAPTIVE_ORB (k_adaptive_orb.hip): cell-level images, bands,
+    // S-map tiles; per-batch cell pyramids / S maps / survivors / selection
+    // scratch (extraction stream only); the frame pyramid and its blur come
+    // from pyr / blur
+    bool adaptive_orb = false;
+    std::vector<OaImg> oai_h;
+    std::vector<OaCell> oac_h;
+    std::vector<OaBand> oab_h;
+    std::vector<OaTile> oat_h;
+    OaImg* oai = nullptr;
+    OaCell* oac = nullptr;
+    OaBand* oab = nullptr;
+    OaTile* oat = nullptr;
+    OaScales osc{};
+    int oa_ncap = 0, oa_buf0 = 0, oa_buf1 = 0;
+    size_t cp_stride = 0, ocand_stride = 0, oscr_stride = 0;
+    uint8_t *cpyr = nullptr, *csmap = nullptr, *oscr = nullptr;
+    uint32_t* ocand = nullptr;
+    int *oband_cnt = nullptr, *ohist = nullptr, *ophist = nullptr;
+    uint64_t *ocell = nullptr, *oakp = nullptr;
     DevArena arena;  // per-stage entry points' device scratch
     int* h_open = nullptr;  // page-locked [NSETS]: RANSAC open pairs of the last batch per set (launch hint)
     // Hamming-match kernel timing (odo_set_timing mode 2): an event pair
@@ -312,7 +332,9 @@ static void free_ctx(odo_ctx* c) {
                     c->okp, c->ocnt, c->kps, c->desc, c->kun, c->xyz, c->ur, c->nkp, c->bgr_in[0], c->depth_in[0],
                     c->bgr_in[1], c->depth_in[1],
                     c->sort_scratch, c->latch, c->masks, c->adc, c->adb, c->smap, c->acand, c->abig, c->acell,
-                    c->akp, c->aband_cnt, c->ahist, c->atsel, c->ansel, c->acell_cnt, c->athresh};
+                    c->akp, c->aband_cnt, c->ahist, c->atsel, c->ansel, c->acell_cnt, c->athresh, c->oai, c->oac,
+                    c->oab, c->oat, c->cpyr, c->csmap, c->oscr, c->ocand, c->oband_cnt, c->ohist, c->ophist,
+                    c->ocell, c->oakp};
     for (void* p : ptrs)
         if (p) hipFree(p);
     for (int i = 0; i < NSETS; i++) {
@@ -348,6 +370,111 @@ static void free_ctx(odo_ctx* c) {
     for (hipStream_t st : c->owned) hipStreamDestroy(st);
     if (c->h_open) (void)hipHostFree(c->h_open);
     delete c;
+}
+
+// ADAPTIVE with the cv::ORB inner detector: per grid cell the 8 levels of
+// cv::ORB's pyramid of the cell sub-image (getScale sizes, orb.cpp), their
+// candidate bands (rows [15, h-15) in AD_BH-row bands; strict 3x3 maxima are
+// never 8-adjacent: <= ceil(r/2)ceil(c/2) survivors), S-map tiles; the frame
+// pyramid (pyr / blur, built by build_geometry) must have cv::ORB's level
+// sizes, since cv::ORB::compute samples it.
+static int build_adaptive_orb_geometry(odo_ctx* c) {
+    const odo_adaptive_params& P = c->cfg.adaptive;
+    float scale[OA_NLEV];
+    int quota[OA_NLEV];
+    {
+        const double sf = (double)1.2f;
+        const float factor = (float)(1.0 / sf);
+        float nd = 10000 * (1 - factor) / (1 - (float)pow((double)factor, (double)OA_NLEV));
+        int sum = 0;
+        for (int l = 0; l < OA_NLEV; l++) {
+            scale[l] = (float)pow(sf, (double)l);
+            c->osc.s[l] = scale[l];
+            if (l < OA_NLEV - 1) {
+                quota[l] = cvRoundH(nd);
+                sum += quota[l];
+                nd *= factor;
+            } else
+                quota[l] = std::max(10000 - sum, 0);
+        }
+    }
+    // the DetectorAdjuster chain runs on sum_l min(count_l, quota_l): exact
+    // decisions need every quota above gridMax (k_adaptive_orb.hip)
+    for (int l = 0; l < OA_NLEV; l++)
+        if (quota[l] <= P.cell_max) return fail(ODO_ERR_ARG, "ADAPTIVE ORB: a level quota <= cell_max");
+    if (c->nlevels < OA_NLEV) return fail(ODO_ERR_ARG, "ADAPTIVE ORB needs orb.nlevels >= 8 (frame pyramid)");
+    for (int l = 0; l < OA_NLEV; l++) {
+        const float inv = 1.0f / scale[l];
+        if (cvRoundH((float)c->W * inv) != c->lv_h[l].w || cvRoundH((float)c->H * inv) != c->lv_h[l].h)
+            return fail(ODO_ERR_ARG, "ADAPTIVE ORB: cv::ORB level size differs from the frame pyramid's");
+    }
+    c->oai_h.clear();
+    c->oac_h.clear();
+    c->oab_h.clear();
+    c->oat_h.clear();
+    int off = 0, coff = 0, buf0 = 0, buf1 = 0;
+    c->oa_ncap = 1;
+    for (const AdCell& A : c->adc_h) {
+        OaCell C{};
+        C.rs = A.rs;
+        C.cs = A.cs;
+        C.cw = A.ce - A.cs;
+        C.ch = A.re - A.rs;
+        C.img0 = (int)c->oai_h.size();
+        int ncap = 0;
+        for (int l = 0; l < OA_NLEV; l++) {
+            OaImg I{};
+            const float inv = 1.0f / scale[l];
+            I.w = cvRoundH((float)C.cw * inv);
+            I.h = cvRoundH((float)C.ch * inv);
+            if (I.w > 1024 || I.h > 1024) return fail(ODO_ERR_ARG, "ADAPTIVE ORB: cell wider than 1024");
+            if (I.w < 1 || I.h < 1) return fail(ODO_ERR_ARG, "ADAPTIVE ORB: empty cell level");
+            I.pitch = (I.w + 15) & ~15;
+            I.off = off;
+            off += I.pitch * I.h;
+            I.quota = quota[l];
+            (l & 1 ? buf1 : buf0) = std::max(l & 1 ? buf1 : buf0, I.pitch * I.h);
+            const int img = (int)c->oai_h.size();
+            I.band0 = (int)c->oab_h.size();
+            I.cand_cap = 0;
+            const int cw = I.w - 2 * OA_EDGE;
+            if (cw > 0)
+                for (int y0 = OA_EDGE; y0 < I.h - OA_EDGE; y0 += AD_BH) {
+                    OaBand B{img, y0, std::min(y0 + AD_BH, I.h - OA_EDGE), coff};
+                    const int cap = ((B.y1 - B.y0 + 1) / 2) * ((cw + 1) / 2);
+                    coff += (cap + 3) & ~3;
+                    I.cand_cap += cap;
+                    c->oab_h.push_back(B);
+                }
+            I.band1 = (int)c->oab_h.size();
+            ncap += I.cand_cap;
+            for (int ty = 0; ty < I.h; ty += OA_TILE_H)
+                for (int tx = 0; tx < I.pitch; tx += OA_TILE_W) c->oat_h.push_back(OaTile{img, tx, ty, 0});
+            c->oai_h.push_back(I);
+        }
+        c->oa_ncap = std::max(c->oa_ncap, ncap);
+        c->oac_h.push_back(C);
+    }
+    c->cp_stride = (size_t)off + 64;
+    c->ocand_stride = (size_t)std::max(coff, 4);
+    c->oa_buf0 = buf0;
+    c->oa_buf1 = buf1;
+    if ((size_t)buf0 + buf1 + 32 * 1024 > 160 * 1024) return fail(ODO_ERR_ARG, "ADAPTIVE ORB: cell pyramid exceeds LDS");
+    c->oscr_stride = (oa_select_scratch_bytes(c->oa_ncap) + 255) & ~(size_t)255;
+    if (oa_assemble_lds_bytes(c->ad_ncells, c->ad_mpc) > 160 * 1024)
+        return fail(ODO_ERR_ARG, "ADAPTIVE ORB grid keeps too many keypoints for one workgroup");
+    if (c->ad_ncells > 15) return fail(ODO_ERR_ARG, "ADAPTIVE ORB: more than 15 grid cells");
+    int e;
+    if ((e = dalloc(&c->oai, c->oai_h.size()))) return e;
+    if ((e = dalloc(&c->oac, c->oac_h.size()))) return e;
+    if ((e = dalloc(&c->oab, std::max<size_t>(c->oab_h.size(), 1)))) return e;
+    if ((e = dalloc(&c->oat, std::max<size_t>(c->oat_h.size(), 1)))) return e;
+    HIPCHK(hipMemcpy(c->oai, c->oai_h.data(), c->oai_h.size() * sizeof(OaImg), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->oac, c->oac_h.data(), c->oac_h.size() * sizeof(OaCell), hipMemcpyHostToDevice));
+    if (!c->oab_h.empty())
+        HIPCHK(hipMemcpy(c->oab, c->oab_h.data(), c->oab_h.size() * sizeof(OaBand), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->oat, c->oat_h.data(), c->oat_h.size() * sizeof(OaTile), hipMemcpyHostToDevice));
+    return ODO_OK;
 }
 
 // ADAPTIVE grid (videogridadaptedfeaturedetector.cpp:62-71): cell ROIs,
@@ -397,6 +524,10 @@ static int build_adaptive_geometry(odo_ctx* c) {
     if (adapt_assemble_lds_bytes(c->ad_ncells, c->ad_mpc) > 160 * 1024)
         return fail(ODO_ERR_ARG, "adaptive grid keeps too many keypoints for one workgroup");
     c->kp_cap = std::max(c->kp_cap, (need + 63) & ~63);
+    if (c->adaptive_orb) {
+        int e;
+        if ((e = build_adaptive_orb_geometry(c))) return e;
+    }
     // ORB's rBRIEF at the FAST keypoints' angle -1 (orb.cpp computeOrbDescriptors)
     const float ang = -1.f * (float)(M_PI / 180.f);
     c->a_cos = (float)cos((double)ang);
@@ -663,18 +794,31 @@ static int alloc_buffers(odo_ctx* c) {
 
     if (c->adaptive) {
         const size_t nc = (size_t)c->ad_ncells;
-        c->smap_stride = (size_t)c->lv_h[0].pitch * c->H;
-        if ((e = dalloc(&c->smap, B * c->smap_stride))) return e;
-        if ((e = dalloc(&c->acand, B * c->acand_stride))) return e;
-        if ((e = dalloc(&c->aband_cnt, B * std::max(c->ad_nbands, 1)))) return e;
-        if ((e = dalloc(&c->ahist, B * nc * 256))) return e;
         if ((e = dalloc(&c->atsel, B * nc))) return e;
         if ((e = dalloc(&c->ansel, B * nc))) return e;
-        if ((e = dalloc(&c->abig, B * nc * c->abig_stride))) return e;
-        if ((e = dalloc(&c->acell, B * nc * c->ad_mpc))) return e;
         if ((e = dalloc(&c->acell_cnt, B * nc))) return e;
-        if ((e = dalloc(&c->akp, B * c->kp_cap))) return e;
         if ((e = dalloc(&c->athresh, nc))) return e;
+        if (!c->adaptive_orb) {
+            c->smap_stride = (size_t)c->lv_h[0].pitch * c->H;
+            if ((e = dalloc(&c->smap, B * c->smap_stride))) return e;
+            if ((e = dalloc(&c->acand, B * c->acand_stride))) return e;
+            if ((e = dalloc(&c->aband_cnt, B * std::max(c->ad_nbands, 1)))) return e;
+            if ((e = dalloc(&c->ahist, B * nc * 256))) return e;
+            if ((e = dalloc(&c->abig, B * nc * c->abig_stride))) return e;
+            if ((e = dalloc(&c->acell, B * nc * c->ad_mpc))) return e;
+            if ((e = dalloc(&c->akp, B * c->kp_cap))) return e;
+        } else {
+            const size_t ni = c->oai_h.size();
+            if ((e = dalloc(&c->cpyr, B * c->cp_stride))) return e;
+            if ((e = dalloc(&c->csmap, B * c->cp_stride))) return e;
+            if ((e = dalloc(&c->ocand, B * c->ocand_stride))) return e;
+            if ((e = dalloc(&c->oband_cnt, B * std::max<size_t>(c->oab_h.size(), 1)))) return e;
+            if ((e = dalloc(&c->ohist, B * ni * 256))) return e;
+            if ((e = dalloc(&c->ophist, B * nc * 256))) return e;
+            if ((e = dalloc(&c->oscr, B * nc * c->oscr_stride))) return e;
+            if ((e = dalloc(&c->ocell, B * nc * c->ad_mpc))) return e;
+            if ((e = dalloc(&c->oakp, B * c->kp_cap))) return e;
+        }
         if ((e = reset_adaptive(c))) return e;
     }
     HIPCHK(hipHostMalloc((void**)&c->h_open, NSETS * sizeof(int), hipHostMallocDefault));
@@ -732,12 +876,14 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
     c->H = cfg->height;
     c->maxb = cfg->max_batch;
     c->slots = cfg->max_batch + 1;
-    if (cfg->detector != ODO_DETECTOR_ORB_SLAM2 && cfg->detector != ODO_DETECTOR_ADAPTIVE_FAST) {
+    if (cfg->detector != ODO_DETECTOR_ORB_SLAM2 && cfg->detector != ODO_DETECTOR_ADAPTIVE_FAST &&
+        cfg->detector != ODO_DETECTOR_ADAPTIVE_ORB) {
         fail(ODO_ERR_ARG, "unsupported detector");  // extractor.cpp:26-27 terminates here
         delete c;
         return nullptr;
     }
-    c->adaptive = cfg->detector == ODO_DETECTOR_ADAPTIVE_FAST;
+    c->adaptive = cfg->detector == ODO_DETECTOR_ADAPTIVE_FAST || cfg->detector == ODO_DETECTOR_ADAPTIVE_ORB;
+    c->adaptive_orb = cfg->detector == ODO_DETECTOR_ADAPTIVE_ORB;
     // ODO_SERIAL_STREAMS=1 (profiling): every stage on one stream, no overlap,
     // so per-kernel times are free of cross-stream contention
     const char* ser = getenv("ODO_SERIAL_STREAMS");
@@ -807,6 +953,7 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
     }
     upload_extract_constants();
     upload_adaptive_constants();
+    upload_adaptive_orb_constants();
     const odo_calib& k = cfg->calib;
     c->cal = FrameCalib{k.fx, k.fy, k.cx, k.cy, k.k1, k.k2, k.p1, k.p2, k.k3, k.depth_factor, k.mbf,
                         1.0f / k.fx, 1.0f / k.fy};
@@ -941,7 +1088,53 @@ static int run_extract_adaptive(odo_ctx* c, int set, const uint8_t* d_bgr, const
     return ODO_OK;
 }
 
+// Extractor(ORB, ORB, ADAPTIVE) for frames slot0.. of `set`
+// (k_adaptive_orb.hip): the frame pyramid + blur (cv::ORB::compute's levels)
+// -> cell pyramids -> S maps -> band survivors + S histograms -> count tables
+// -> the per-cell threshold chain -> per-cell select -> assemble ->
+// IC angle / rBRIEF / undistort / depth.
+static int run_extract_adaptive_orb(odo_ctx* c, int set, const uint8_t* d_bgr, const uint16_t* d_depth, int n,
+                                    int slot0) {
+    hipStream_t st = c->stream;
+    const size_t P = c->pyr_size;
+    const size_t slot = fbase(c, set) + slot0;
+    uint8_t* pyr = c->pyr + slot * P;
+    const int nc = c->ad_ncells, ni = (int)c->oai_h.size(), nb = (int)c->oab_h.size();
+    if (d_bgr) launch_gray(st, d_bgr, pyr, c->W, c->H, c->lv_h[0].pitch, (size_t)c->W * c->H * 3, P, n);
+    for (int l = 1; l < c->nlevels; l++) {
+        const LevelDesc& S = c->lv_h[l - 1];
+        const LevelDesc& D = c->lv_h[l];
+        launch_resize(st, pyr, P, S.off, S.pitch, D.off, D.pitch, D.w, D.h, RZ_RB, c->rz_rows[l],
+                      c->rx + c->rx_off[l], c->ry + c->ry_off[l], n);
+    }
+    tmark(c, 1, st);
+    launch_oa_pyr(st, pyr, P, c->lv_h[0].pitch, c->oac, nc, c->oai, c->oa_buf0, c->oa_buf1, c->cpyr, c->cp_stride, n);
+    launch_oa_smap(st, c->cpyr, c->cp_stride, c->oai, c->oat, (int)c->oat_h.size(), c->csmap, n);
+    HIPCHK(hipMemsetAsync(c->ohist, 0, (size_t)n * ni * 256 * sizeof(int), st));
+    if (nb > 0)
+        launch_oa_cand(st, c->csmap, c->cp_stride, c->oai, ni, c->oab, nb, c->ocand, c->ocand_stride, c->oband_cnt,
+                       c->ohist, n);
+    launch_oa_count(st, c->ohist, c->oac, c->oai, ni, nc, c->ophist, n);
+    tmark(c, 2, st);
+    launch_adapt_chain(st, c->ophist, nc, n, c->cfg.adaptive, c->athresh, c->atsel, c->ansel);
+    launch_oa_select(st, c->ocand, c->ocand_stride, c->oband_cnt, nb, c->oab, c->oai, c->oac, nc, c->atsel, c->cpyr,
+                     c->cp_stride, c->ad_mpc, c->oscr, c->oscr_stride, c->oa_ncap, c->ocell, c->acell_cnt, n);
+    launch_oa_assemble(st, c->ocell, c->acell_cnt, c->oac, nc, c->ad_mpc, c->cfg.adaptive.retain_best, c->W, c->H,
+                       c->osc, c->oakp, c->kp_cap, c->nkp + slot, c->kp_cap, n);
+    tmark(c, 3, st);
+    launch_blur(st, pyr, c->blur + slot * P, P, c->lv, c->lv_h.data(), OA_NLEV, n);
+    tmark(c, 4, st);
+    launch_oa_finalize(st, pyr, c->blur + slot * P, P, c->lv, c->cpyr, c->cp_stride, c->oai, c->oac, c->osc, c->oakp,
+                       c->kp_cap, c->nkp + slot, d_depth, (size_t)c->W * c->H, c->W, c->cal,
+                       c->kps + slot * c->kp_cap, c->desc + slot * c->kp_cap * 32, c->kun + slot * c->kp_cap * 2,
+                       c->xyz + slot * c->kp_cap * 3, c->ur + slot * c->kp_cap, c->kp_cap, n);
+    tmark(c, 5, st);
+    HIPCHK(hipGetLastError());
+    return ODO_OK;
+}
+
 static int run_extract(odo_ctx* c, int set, const uint8_t* d_bgr, const uint16_t* d_depth, int n, int slot0) {
+    if (c->adaptive_orb) return run_extract_adaptive_orb(c, set, d_bgr, d_depth, n, slot0);
     if (c->adaptive) return run_extract_adaptive(c, set, d_bgr, d_depth, n, slot0);
     hipStream_t st = c->stream;
     const size_t P = c->pyr_size;

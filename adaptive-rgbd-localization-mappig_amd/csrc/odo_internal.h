@@ -115,6 +115,37 @@ struct AdBand {
     int cell, y0, y1, cand_off;
 };
 
+// ---- ADAPTIVE grid with the cv::ORB inner detector (k_adaptive_orb.hip):
+// cv::ORB::create(10000, 1.2f, 8, 15, 0, 2, HARRIS_SCORE, 31, t) per grid
+// cell (detectoradjuster.cpp:29)
+#define OA_NLEV 8     // nlevels
+#define OA_EDGE 15    // edgeThreshold (runByImageBorder of each level)
+#define OA_PATCH 31   // patchSize
+// one pyramid level of one grid cell, inside a frame's cell-pyramid buffer
+struct OaImg {
+    int off, w, h, pitch;
+    int quota;         // nfeaturesPerLevel[level] of nfeatures 10000
+    int band0, band1;  // its candidate bands (rows [15, h-15))
+    int cand_cap;      // survivors over its bands
+};
+// one grid cell: ROI origin / size in the frame, its 8 level images
+struct OaCell {
+    int rs, cs, cw, ch;
+    int img0;
+    int pad[3];
+};
+struct OaBand {
+    int img, y0, y1, cand_off;
+};
+struct OaTile {
+    int img, tx0, ty0, pad;
+};
+#define OA_TILE_W 128  // S-map tile (smap_tile, odo_select.h)
+#define OA_TILE_H 8
+struct OaScales {
+    float s[OA_NLEV];  // getScale(level) = (float)pow((double)1.2f, level)
+};
+
 // RANSAC per-pair constants.
 struct RansacCfg {
     int iterations;
@@ -224,6 +255,30 @@ void launch_adapt_finalize(hipStream_t st, const uint8_t* blur, size_t pyr_strid
                            int akp_stride, const int* nkp, float ca, float sb, const uint16_t* depth,
                            size_t depth_stride, int img_w, FrameCalib cal, orb_kp* kps, uint8_t* desc, float* kun,
                            float* xyz, float* ur, int kp_cap, int nframes);
+void upload_adaptive_orb_constants();
+void launch_oa_pyr(hipStream_t st, const uint8_t* pyr, size_t pyr_stride, int gpitch, const OaCell* cells, int ncells,
+                   const OaImg* imgs, int buf0, int buf1, uint8_t* cpyr, size_t cp_stride, int nframes);
+void launch_oa_smap(hipStream_t st, const uint8_t* cpyr, size_t cp_stride, const OaImg* imgs, const OaTile* tiles,
+                    int ntiles, uint8_t* csmap, int nframes);
+void launch_oa_cand(hipStream_t st, const uint8_t* csmap, size_t cp_stride, const OaImg* imgs, int nimgs,
+                    const OaBand* bands, int nbands, uint32_t* cand, size_t cand_stride, int* band_cnt, int* hist,
+                    int nframes);
+void launch_oa_count(hipStream_t st, const int* hist, const OaCell* cells, const OaImg* imgs, int nimgs, int ncells,
+                     int* phist, int nframes);
+size_t oa_select_scratch_bytes(int ncap);
+void launch_oa_select(hipStream_t st, const uint32_t* cand, size_t cand_stride, const int* band_cnt, int nbands,
+                      const OaBand* bands, const OaImg* imgs, const OaCell* cells, int ncells, const int* tsel,
+                      const uint8_t* cpyr, size_t cp_stride, int max_per_cell, uint8_t* scr, size_t scr_stride,
+                      int ncap, uint64_t* cell_out, int* cell_cnt, int nframes);
+size_t oa_assemble_lds_bytes(int ncells, int max_per_cell);
+void launch_oa_assemble(hipStream_t st, const uint64_t* cell_out, const int* cell_cnt, const OaCell* cells,
+                        int ncells, int max_per_cell, int retain, int w, int h, OaScales sc, uint64_t* akp,
+                        int akp_stride, int* nkp, int kp_cap, int nframes);
+void launch_oa_finalize(hipStream_t st, const uint8_t* pyr, const uint8_t* blur, size_t pyr_stride,
+                        const LevelDesc* lv, const uint8_t* cpyr, size_t cp_stride, const OaImg* imgs,
+                        const OaCell* cells, OaScales sc, const uint64_t* akp, int akp_stride, const int* nkp,
+                        const uint16_t* depth, size_t depth_stride, int img_w, FrameCalib cal, orb_kp* kps,
+                        uint8_t* desc, float* kun, float* xyz, float* ur, int kp_cap, int nframes);
 void launch_adapt_select_dbg(hipStream_t st, uint32_t* a, int n, int nth, int mode, int* posL, int* posR,
                              int* n_out);
 

@@ -32,6 +32,8 @@ extern "C" {
 /* odo_config.detector: Extractor(detector, descriptor, mode) (extractor.cpp:14) */
 #define ODO_DETECTOR_ORB_SLAM2 0      /* ORB_SLAM2 / ORB_SLAM2 / NORMAL (main.cpp:19-21, the reference default) */
 #define ODO_DETECTOR_ADAPTIVE_FAST 1  /* FAST / ORB / ADAPTIVE: 3x3 grid-adapted FAST + cv::ORB descriptor */
+#define ODO_DETECTOR_ADAPTIVE_ORB 2   /* ORB / ORB / ADAPTIVE: 3x3 grid-adapted cv::ORB detector (Harris,
+                                         8 levels; detectoradjuster.cpp:29) + cv::ORB descriptor */
 
 typedef struct odo_config {
     int32_t width, height;      /* frame size (all frames of a context share it) */
@@ -117,7 +119,7 @@ int odo_get_pair(odo_ctx* ctx, int i, odo_dmatch* matches, int match_cap, int* n
 /* Extractor::Extract + Frame::ExtractFeatures (extractor.cpp:39, frame.cpp:135):
  * BGR8 (or gray when channels==1) + optional depth16 -> keypoints,
  * 32-byte descriptors, undistorted points, camera xyz and right coordinate.
- * With ODO_DETECTOR_ADAPTIVE_FAST every call advances the cell thresholds. */
+ * With ODO_DETECTOR_ADAPTIVE_FAST / _ORB every call advances the cell thresholds. */
 int odo_extract(odo_ctx* ctx, const uint8_t* img, int channels, const uint16_t* depth,
                 orb_kp* kps, uint8_t* desc, float* kps_un, float* xyz, float* u_right, int cap,
                 int* n);

@@ -161,10 +161,12 @@ using LandmarkPtr = std::shared_ptr<Landmark>;
 
 class Frame;
 
-// Features/extractor.h:6-42. Only the two configurations of the hot path run
-// on the GPU: (ORB_SLAM2, ORB_SLAM2, NORMAL), the reference default
-// (main.cpp:19-21), and (FAST, ORB, ADAPTIVE), the grid-adapted detector
-// (extractor.cpp:52-77). Any other combination throws std::invalid_argument.
+// Features/extractor.h:6-42. The configurations of the hot path run on the
+// GPU: (ORB_SLAM2, ORB_SLAM2, NORMAL), the reference default (main.cpp:19-21),
+// and the grid-adapted detector (extractor.cpp:52-77) with the FAST inner
+// detector, (FAST, ORB, ADAPTIVE), or the cv::ORB one, (ORB, ORB, ADAPTIVE)
+// (detectoradjuster.cpp:29). Any other combination throws
+// std::invalid_argument.
 class Extractor {
 public:
     enum eAlgorithm { ORB = 0, ORB_SLAM2, FAST, GFTT, STAR, BRISK, FREAK, BRIEF, LATCH, SURF, SIFT };
@@ -182,9 +184,11 @@ public:
             mDetector = ODO_DETECTOR_ORB_SLAM2;
         else if (detector == FAST && descriptor == ORB && mode == ADAPTIVE)
             mDetector = ODO_DETECTOR_ADAPTIVE_FAST;
+        else if (detector == ORB && descriptor == ORB && mode == ADAPTIVE)
+            mDetector = ODO_DETECTOR_ADAPTIVE_ORB;
         else
-            throw std::invalid_argument("odo_hip::Extractor: only (ORB_SLAM2, ORB_SLAM2, NORMAL) and "
-                                        "(FAST, ORB, ADAPTIVE) run on the MI355X path");
+            throw std::invalid_argument("odo_hip::Extractor: only (ORB_SLAM2, ORB_SLAM2, NORMAL), "
+                                        "(FAST, ORB, ADAPTIVE) and (ORB, ORB, ADAPTIVE) run on the MI355X path");
     }
 
     // Extractor::Extract(image, mask, keypoints, descriptors) (extractor.cpp:39-50):

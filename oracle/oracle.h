@@ -84,6 +84,25 @@ int oracle_extract_frame_adaptive(const uint8_t* bgr, const uint16_t* depth, int
                                   orb_kp* kps, uint8_t* desc, float* kps_un, float* xyz,
                                   float* u_right, int cap);
 
+/* ---- Extractor(ORB, ORB, ADAPTIVE): the same grid / threshold chain with
+ * the cv::ORB inner detector of detectoradjuster.cpp:29 (SURVEY §8(f) rank 2;
+ * OpenCV 3.4 orb.cpp restated). */
+int oracle_adaptive_orb_extract(const uint8_t* gray, int w, int h, const odo_adaptive_params* p,
+                                double* thresh, orb_kp* kps, uint8_t* desc, int cap, int* t_used);
+int oracle_adaptive_orb_detect(const uint8_t* gray, int w, int h, const odo_adaptive_params* p,
+                               double* thresh, orb_kp* out, int cap, int* t_used);
+/* cv::ORB(10000, 1.2, 8, 15, 0, 2, HARRIS, 31, threshold)::detect on one image. */
+int oracle_orbcv_detect(const uint8_t* img, int stride, int rows, int cols, int threshold,
+                        orb_kp* out, int cap);
+/* HarrisResponses (blockSize 7, k 0.04) at (x, y) of a w x h image. */
+float oracle_harris(const uint8_t* img, int w, int h, int x, int y);
+/* cv::ORB pyramid sizes / getScale / nfeaturesPerLevel for nfeatures 10000. */
+int oracle_orbcv_levels(int w, int h, int* lw, int* lh, float* scale, int* quota);
+int oracle_extract_frame_adaptive_orb(const uint8_t* bgr, const uint16_t* depth, int w, int h,
+                                      const odo_adaptive_params* p, double* thresh, const odo_calib* c,
+                                      orb_kp* kps, uint8_t* desc, float* kps_un, float* xyz,
+                                      float* u_right, int cap);
+
 /* Frame::ExtractFeatures tail + UndistortKeyPoints (frame.cpp:139-169, 286-313). */
 void oracle_frame_geometry(const orb_kp* kps, int n, const float* depth, int w, int h,
                            const odo_calib* c, float* kps_un, float* xyz, float* u_right);

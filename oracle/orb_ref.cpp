@@ -728,6 +728,224 @@ int adaptive_extract(const uint8_t* gray, int w, int h, const odo_adaptive_param
     return (int)kps.size();
 }
 
+// ---------------------------------------------------------------- ADAPTIVE, cv::ORB inner
+// Extractor(ORB, ORB, ADAPTIVE) (extractor.cpp:52-77 with the ORB adjuster
+// DetectorAdjuster(ORB, 20, 2, 10000, 1.3, 0.7)): every cell's detect() is
+// cv::ORB::create(10000, 1.2f, 8, 15, 0, 2, HARRIS_SCORE, 31, (int)mThresh)
+// ->detect(sub_image) (detectoradjuster.cpp:29), restated from OpenCV 3.4
+// orb.cpp (detectAndCompute with do_keypoints, computeKeyPoints,
+// HarrisResponses, ICAngles). Pinned choices (DESIGN.md §4 "ADAPTIVE, cv::ORB
+// inner"): the pyramid uses the INTER_LINEAR resize of App. A.2 (OpenCV
+// 3.4.0/3.4.1; later 3.4.x switched orb.cpp to INTER_LINEAR_EXACT).
+const int OCV_NFEATURES = 10000, OCV_NLEVELS = 8, OCV_EDGE = 15, OCV_PATCH = 31, OCV_HARRIS_BLOCK = 7;
+const float OCV_SCALE_FACTOR = 1.2f, OCV_HARRIS_K = 0.04f;
+
+// ORB_Impl::getScale: (float)pow(scaleFactor, level) with the double member
+// scaleFactor = (double)1.2f (not the cumulative float product of ORB-SLAM2).
+float orbcv_scale(int level) { return (float)std::pow((double)OCV_SCALE_FACTOR, (double)level); }
+
+// computeKeyPoints: nfeaturesPerLevel (geometric, cvRound, last = remainder)
+std::vector<int> orbcv_quotas(int nfeatures, int nlevels) {
+    std::vector<int> q(nlevels);
+    const float factor = (float)(1.0 / (double)OCV_SCALE_FACTOR);
+    float nd = nfeatures * (1 - factor) / (1 - (float)std::pow((double)factor, (double)nlevels));
+    int sum = 0;
+    for (int l = 0; l < nlevels - 1; l++) {
+        q[l] = cvRound(nd);
+        sum += q[l];
+        nd *= factor;
+    }
+    q[nlevels - 1] = std::max(nfeatures - sum, 0);
+    return q;
+}
+
+// KeyPointsFilter::runByImageBorder (keypoint.cpp): keep Rect(b, b, w-2b, h-2b)
+// .contains(pt) in order; everything goes when the image is too small.
+void run_by_image_border(std::vector<KP>& kps, int w, int h, int b) {
+    if (b <= 0) return;
+    if (h <= 2 * b || w <= 2 * b) {
+        kps.clear();
+        return;
+    }
+    const float x0 = (float)b, y0 = (float)b, x1 = (float)(w - b), y1 = (float)(h - b);
+    kps.erase(std::remove_if(kps.begin(), kps.end(),
+                             [&](const KP& k) { return !(x0 <= k.x && k.x < x1 && y0 <= k.y && k.y < y1); }),
+              kps.end());
+}
+
+// HarrisResponses (orb.cpp): 7x7 block of Sobel-like gradients around
+// (cvRound(x), cvRound(y)) of the level, integer sums, float response.
+float harris_response(const Img& im, int x0, int y0) {
+    const int r = OCV_HARRIS_BLOCK / 2;
+    const float scale = 1.f / ((1 << 2) * OCV_HARRIS_BLOCK * 255.f);
+    const float scale_sq_sq = scale * scale * scale * scale;
+    int a = 0, b = 0, c = 0;
+    for (int i = 0; i < OCV_HARRIS_BLOCK; i++)
+        for (int j = 0; j < OCV_HARRIS_BLOCK; j++) {
+            const int y = y0 - r + i, x = x0 - r + j;
+            const int Ix = (im.at(y, x + 1) - im.at(y, x - 1)) * 2 + (im.at(y - 1, x + 1) - im.at(y - 1, x - 1)) +
+                           (im.at(y + 1, x + 1) - im.at(y + 1, x - 1));
+            const int Iy = (im.at(y + 1, x) - im.at(y - 1, x)) * 2 + (im.at(y + 1, x - 1) - im.at(y - 1, x - 1)) +
+                           (im.at(y + 1, x + 1) - im.at(y - 1, x + 1));
+            a += Ix * Ix;
+            b += Iy * Iy;
+            c += Ix * Iy;
+        }
+    return ((float)a * b - (float)c * c - OCV_HARRIS_K * ((float)a + b) * ((float)a + b)) * scale_sq_sq;
+}
+
+// cv::ORB::detect on one image (a grid cell's sub-image): pyramid (level 0 =
+// the image, level l = resize of level l-1 to cvRound(size / scale_l)), per
+// level FAST(fastThreshold, nonmax) -> runByImageBorder(edgeThreshold) ->
+// retainBest(2 * quota) with octave / size set; Harris responses; per level
+// retainBest(quota) on them; ICAngles (unblurred level, umax of half patch
+// 15); pt *= scale. Keypoint order: level-major, retainBest's permutation.
+void orbcv_detect(const uint8_t* base, int stride, int rows, int cols, int threshold, std::vector<KP>& out,
+                  const std::vector<int>& umax) {
+    out.clear();
+    if (rows <= 0 || cols <= 0) return;
+    const std::vector<int> quota = orbcv_quotas(OCV_NFEATURES, OCV_NLEVELS);
+    std::vector<Img> pyr(OCV_NLEVELS);
+    pyr[0].w = cols;
+    pyr[0].h = rows;
+    pyr[0].px.resize((size_t)rows * cols);
+    for (int y = 0; y < rows; y++) memcpy(&pyr[0].px[(size_t)y * cols], base + (size_t)y * stride, cols);
+    for (int l = 1; l < OCV_NLEVELS; l++) {
+        const float inv = 1.0f / orbcv_scale(l);
+        resize_linear(pyr[l - 1], pyr[l], cvRound((float)cols * inv), cvRound((float)rows * inv));
+    }
+    std::vector<std::vector<KP>> lv(OCV_NLEVELS);
+    for (int l = 0; l < OCV_NLEVELS; l++) {
+        const Img& im = pyr[l];
+        fast_roi(im.px.data(), im.w, im.h, im.w, threshold, lv[l]);
+        run_by_image_border(lv[l], im.w, im.h, OCV_EDGE);
+        retain_best(lv[l], 2 * quota[l]);
+        const float sf = orbcv_scale(l);
+        for (KP& k : lv[l]) {
+            k.octave = l;
+            k.size = OCV_PATCH * sf;
+        }
+    }
+    for (int l = 0; l < OCV_NLEVELS; l++) {
+        for (KP& k : lv[l]) k.response = harris_response(pyr[l], cvRound(k.x), cvRound(k.y));
+        retain_best(lv[l], quota[l]);
+        for (KP& k : lv[l]) k.angle = ic_angle(pyr[l], k.x, k.y, umax);
+        const float sf = orbcv_scale(l);
+        for (KP& k : lv[l]) {
+            k.x *= sf;
+            k.y *= sf;
+        }
+        out.insert(out.end(), lv[l].begin(), lv[l].end());
+    }
+}
+
+int adaptive_orb_cell_detect(const uint8_t* base, int stride, int rows, int cols, const odo_adaptive_params& p,
+                             double& thresh, std::vector<KP>& kps, const std::vector<int>& umax) {
+    int iterCount = p.escape_iters;
+    int t_used = 0;
+    do {  // VideoDynamicAdaptedFeatureDetector::detect (videodynamicadaptedfeaturedetector.cpp:24-44)
+        kps.clear();
+        t_used = (int)thresh;  // static_cast<int>(mThresh) (detectoradjuster.cpp:29)
+        orbcv_detect(base, stride, rows, cols, t_used, kps, umax);
+        const int found = (int)kps.size();
+        if (found < p.cell_min) {
+            thresh *= p.decrease_factor;
+            if (thresh < p.min_thresh) thresh = p.min_thresh;
+        } else if (found > p.cell_max) {
+            thresh *= p.increase_factor;
+            if (thresh > p.max_thresh) thresh = p.max_thresh;
+            break;
+        } else
+            break;
+        iterCount--;
+    } while (iterCount > 0 && (thresh > p.min_thresh) && (thresh < p.max_thresh));
+    return std::min(std::max(t_used, 0), 255);
+}
+
+void adaptive_orb_grid_detect(const uint8_t* gray, int w, int h, const odo_adaptive_params& p, double* thresh,
+                              std::vector<KP>& out, int* t_used) {
+    const int R = p.grid_rows, C = p.grid_cols, E = p.edge_threshold;
+    const int maxPerCell = p.max_total_keypoints / (R * C);
+    const std::vector<int> umax = make_tables(odo_orb_params{1000, 1.2f, 8, 20, 7}).umax;  // same 15-radius table
+    std::vector<std::vector<KP>> sub(R * C);
+    for (int i = 0; i < R; ++i) {
+        const int rs = std::max((i * h) / R - E, 0), re = std::min(h, ((i + 1) * h) / R + E);
+        for (int j = 0; j < C; ++j) {
+            const int cs = std::max((j * w) / C - E, 0), ce = std::min(w, ((j + 1) * w) / C + E);
+            const int t = adaptive_orb_cell_detect(gray + (size_t)rs * w + cs, w, re - rs, ce - cs, p,
+                                                   thresh[j + i * C], sub[j + i * C], umax);
+            if (t_used) t_used[j + i * C] = t;
+            keep_strongest(maxPerCell, sub[j + i * C]);
+        }
+    }
+    out.clear();
+    for (int i = 0; i < R; ++i) {
+        const int rs = std::max((i * h) / R - E, 0);
+        for (int j = 0; j < C; ++j) {
+            const int cs = std::max((j * w) / C - E, 0);
+            for (KP& k : sub[j + i * C]) {
+                k.x += cs;
+                k.y += rs;
+            }
+            out.insert(out.end(), sub[j + i * C].begin(), sub[j + i * C].end());
+        }
+    }
+}
+
+// cv::ORB::compute on keypoints with octaves (orb.cpp, !do_keypoints):
+// runByImageBorder(31) on the image; keypoints grouped by octave (stable, the
+// !sortedByLevel regrouping); pyramid of the whole image with the getScale
+// sizes; each level blurred in place inside the bordered pyramid (GaussianBlur
+// 7x7 REFLECT_101 on the level ROI), so a pattern sample that falls outside
+// the level reads the unblurred REFLECT_101 border; centre =
+// cvRound(pt / layerScale) (computeOrbDescriptors).
+void orb_compute_provided_levels(const uint8_t* gray, int w, int h, std::vector<KP>& kps,
+                                 std::vector<uint8_t>& desc) {
+    run_by_image_border(kps, w, h, 31);
+    std::stable_sort(kps.begin(), kps.end(), [](const KP& a, const KP& b) { return a.octave < b.octave; });
+    desc.assign(kps.size() * 32, 0);
+    if (kps.empty()) return;
+    int nlev = 0;
+    for (const KP& k : kps) nlev = std::max(nlev, k.octave + 1);
+    std::vector<Img> pyr(nlev), blr(nlev);
+    pyr[0].w = w;
+    pyr[0].h = h;
+    pyr[0].px.assign(gray, gray + (size_t)w * h);
+    for (int l = 1; l < nlev; l++) {
+        const float inv = 1.0f / orbcv_scale(l);
+        resize_linear(pyr[l - 1], pyr[l], cvRound((float)w * inv), cvRound((float)h * inv));
+    }
+    for (int l = 0; l < nlev; l++) gaussian_blur(pyr[l], blr[l]);
+    for (size_t i = 0; i < kps.size(); i++) {
+        const KP& k = kps[i];
+        const Img &B = blr[k.octave], &U = pyr[k.octave];
+        const float sc = 1.f / orbcv_scale(k.octave);
+        const int cy = cvRound(k.y * sc), cx = cvRound(k.x * sc);
+        const float ang = k.angle * (float)(M_PI / 180.f);
+        const float a = (float)cos((double)ang), b = (float)sin((double)ang);
+        const int8_t* pattern = ODO_ORB_PATTERN;
+        auto value = [&](int idx) {
+            const float px = (float)pattern[2 * idx], py = (float)pattern[2 * idx + 1];
+            const int yy = cy + cvRound(px * b + py * a), xx = cx + cvRound(px * a - py * b);
+            if (yy >= 0 && yy < B.h && xx >= 0 && xx < B.w) return (int)B.at(yy, xx);
+            return (int)U.at(reflect101(yy, U.h), reflect101(xx, U.w));
+        };
+        for (int j = 0; j < 32; ++j, pattern += 32) {
+            int val = 0;
+            for (int bit = 0; bit < 8; bit++) val |= (value(2 * bit) < value(2 * bit + 1)) << bit;
+            desc[i * 32 + j] = (uint8_t)val;
+        }
+    }
+}
+
+int adaptive_orb_extract(const uint8_t* gray, int w, int h, const odo_adaptive_params& p, double* thresh,
+                         std::vector<KP>& kps, std::vector<uint8_t>& desc, int* t_used) {
+    adaptive_orb_grid_detect(gray, w, h, p, thresh, kps, t_used);
+    if ((int)kps.size() > p.retain_best) retain_best(kps, p.retain_best);  // extractor.cpp:45-46
+    orb_compute_provided_levels(gray, w, h, kps, desc);
+    return (int)kps.size();
+}
+
 }  // namespace
 
 // ================================================================ C API
@@ -865,6 +1083,52 @@ int oracle_adaptive_extract(const uint8_t* gray, int w, int h, const odo_adaptiv
     kp_out(k, kps, cap);
     if (desc) memcpy(desc, d.data(), (size_t)std::min(n, cap) * 32);
     return n;
+}
+
+int oracle_adaptive_orb_extract(const uint8_t* gray, int w, int h, const odo_adaptive_params* p, double* thresh,
+                                orb_kp* kps, uint8_t* desc, int cap, int* t_used) {
+    std::vector<KP> k;
+    std::vector<uint8_t> d;
+    const int n = adaptive_orb_extract(gray, w, h, *p, thresh, k, d, t_used);
+    kp_out(k, kps, cap);
+    if (desc) memcpy(desc, d.data(), (size_t)std::min(n, cap) * 32);
+    return n;
+}
+
+int oracle_adaptive_orb_detect(const uint8_t* gray, int w, int h, const odo_adaptive_params* p, double* thresh,
+                               orb_kp* out, int cap, int* t_used) {
+    std::vector<KP> k;
+    adaptive_orb_grid_detect(gray, w, h, *p, thresh, k, t_used);
+    kp_out(k, out, cap);
+    return (int)k.size();
+}
+
+int oracle_orbcv_detect(const uint8_t* img, int stride, int rows, int cols, int threshold, orb_kp* out, int cap) {
+    std::vector<KP> k;
+    const std::vector<int> umax = make_tables(odo_orb_params{1000, 1.2f, 8, 20, 7}).umax;
+    orbcv_detect(img, stride, rows, cols, threshold, k, umax);
+    kp_out(k, out, cap);
+    return (int)k.size();
+}
+
+float oracle_harris(const uint8_t* img, int w, int h, int x, int y) {
+    Img im;
+    im.w = w;
+    im.h = h;
+    im.px.assign(img, img + (size_t)w * h);
+    return harris_response(im, x, y);
+}
+
+int oracle_orbcv_levels(int w, int h, int* lw, int* lh, float* scale, int* quota) {
+    const std::vector<int> q = orbcv_quotas(OCV_NFEATURES, OCV_NLEVELS);
+    for (int l = 0; l < OCV_NLEVELS; l++) {
+        const float inv = 1.0f / orbcv_scale(l);
+        lw[l] = cvRound((float)w * inv);
+        lh[l] = cvRound((float)h * inv);
+        scale[l] = orbcv_scale(l);
+        quota[l] = q[l];
+    }
+    return OCV_NLEVELS;
 }
 
 // std::nth_element / partition helpers on packed (score<<24 | y<<12 | x)

@@ -1013,6 +1013,21 @@ int oracle_extract_frame_adaptive(const uint8_t* bgr, const uint16_t* depth, int
     return n;
 }
 
+// The same with the cv::ORB inner detector (Extractor(ORB, ORB, ADAPTIVE)).
+int oracle_extract_frame_adaptive_orb(const uint8_t* bgr, const uint16_t* depth, int w, int h,
+                                      const odo_adaptive_params* p, double* thresh, const odo_calib* c,
+                                      orb_kp* kps, uint8_t* desc, float* kps_un, float* xyz, float* u_right,
+                                      int cap) {
+    std::vector<uint8_t> gray((size_t)w * h);
+    std::vector<float> z((size_t)w * h);
+    oracle_bgr2gray(bgr, w, h, 3 * w, gray.data());
+    oracle_depth_to_f32(depth, w * h, c->depth_factor, z.data());
+    int n = oracle_adaptive_orb_extract(gray.data(), w, h, p, thresh, kps, desc, cap, nullptr);
+    int m = std::min(n, cap);
+    oracle_frame_geometry(kps, m, z.data(), w, h, c, kps_un, xyz, u_right);
+    return n;
+}
+
 // Frame::ComputeImageBounds (frame.cpp:315-349): undistorted image corners.
 void oracle_image_bounds(const odo_calib* c, int w, int h, float* b) {
     if (c->k1 != 0.0f) {

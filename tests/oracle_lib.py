@@ -121,6 +121,13 @@ def lib():
             "oracle_nth_element_score": (None, [P, C.c_int, C.c_int]),
             "oracle_retain_best_score": (C.c_int, [P, C.c_int, C.c_int]),
             "oracle_extract_frame_adaptive": (C.c_int, [P, P, C.c_int, C.c_int, P, P, P, P, P, P, P, P, C.c_int]),
+            "oracle_adaptive_orb_extract": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, C.c_int, P]),
+            "oracle_adaptive_orb_detect": (C.c_int, [P, C.c_int, C.c_int, P, P, P, C.c_int, P]),
+            "oracle_orbcv_detect": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, P, C.c_int]),
+            "oracle_harris": (C.c_float, [P, C.c_int, C.c_int, C.c_int, C.c_int]),
+            "oracle_orbcv_levels": (C.c_int, [C.c_int, C.c_int, P, P, P, P]),
+            "oracle_extract_frame_adaptive_orb": (C.c_int, [P, P, C.c_int, C.c_int, P, P, P, P, P, P, P, P,
+                                                            C.c_int]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -190,9 +197,13 @@ def adaptive_params() -> AdaptiveParams:
 
 
 class AdaptiveExtractor:
-    """Extractor(FAST, ORB, ADAPTIVE): per-cell thresholds persist across calls."""
+    """Extractor(FAST, ORB, ADAPTIVE) (inner="fast") or Extractor(ORB, ORB,
+    ADAPTIVE) (inner="orb", the cv::ORB cell detector): per-cell thresholds
+    persist across calls."""
 
-    def __init__(self, params: AdaptiveParams = None):
+    def __init__(self, params: AdaptiveParams = None, inner: str = "fast"):
+        assert inner in ("fast", "orb")
+        self.inner = inner
         self.p = params or adaptive_params()
         self.thresh = np.full(self.p.grid_rows * self.p.grid_cols, self.p.init_thresh, np.float64)
 
@@ -203,7 +214,8 @@ class AdaptiveExtractor:
         kun = np.zeros((cap, 2), np.float32)
         xyz = np.zeros((cap, 3), np.float32)
         ur = np.zeros(cap, np.float32)
-        n = lib().oracle_extract_frame_adaptive(ptr(np.ascontiguousarray(bgr)), ptr(np.ascontiguousarray(depth)),
+        fn = lib().oracle_extract_frame_adaptive if self.inner == "fast" else lib().oracle_extract_frame_adaptive_orb
+        n = fn(ptr(np.ascontiguousarray(bgr)), ptr(np.ascontiguousarray(depth)),
                                                 w, h, C.byref(self.p), ptr(self.thresh), C.byref(calib), ptr(kps),
                                                 ptr(desc), ptr(kun), ptr(xyz), ptr(ur), cap)
         assert n <= cap
@@ -214,7 +226,8 @@ class AdaptiveExtractor:
         kps = np.zeros(cap, KP_DTYPE)
         desc = np.zeros((cap, 32), np.uint8)
         t_used = np.zeros(self.p.grid_rows * self.p.grid_cols, np.int32)
-        n = lib().oracle_adaptive_extract(ptr(np.ascontiguousarray(gray)), w, h, C.byref(self.p), ptr(self.thresh),
+        fn = lib().oracle_adaptive_extract if self.inner == "fast" else lib().oracle_adaptive_orb_extract
+        n = fn(ptr(np.ascontiguousarray(gray)), w, h, C.byref(self.p), ptr(self.thresh),
                                           ptr(kps), ptr(desc), cap, ptr(t_used))
         return kps[:n], desc[:n], t_used
 
