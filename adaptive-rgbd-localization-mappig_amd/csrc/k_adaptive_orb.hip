@@ -18,9 +18,9 @@
 //
 //   k_oa_pyr       per (frame, cell): the cell's 8-level pyramid (INTER_LINEAR,
 //                  App. A.2), levels ping-ponged in LDS, written to HBM
-//   k_oa_smap      S map of every cell level (smap_tile)
-//   k_oa_cand      per (frame, band): NMS survivors in [15, w-15) x [15, h-15)
-//                  in row-major order + per-level S histogram
+//   k_oa_scand     per (frame, band of a cell level): S (smap4) of the band
+//                  in LDS, NMS survivors in [15, w-15) x [15, h-15) in
+//                  row-major order + per-level S histogram
 //   k_oa_count     per (frame, cell): the chain's count table for every t
 //   (k_adapt_chain) the tooFew/tooMany/good chain over the batch, in frame order
 //   k_oa_select    per (frame, cell): survivors with S > t*, retainBest by FAST
@@ -37,8 +37,6 @@
 #include "../../include/odo_orb_pattern.h"
 
 namespace odo {
-
-static_assert(OA_TILE_W == SM_TW && OA_TILE_H == SM_TH, "S-map tile table and smap_tile disagree");
 
 __constant__ int8_t c_opattern[1024];
 
@@ -138,51 +136,57 @@ __global__ void __launch_bounds__(512) k_oa_pyr(const uint8_t* __restrict__ pyr,
     }
 }
 
-// ============================================================ S maps
-__global__ void __launch_bounds__(256) k_oa_smap(const uint8_t* __restrict__ cpyr, size_t cp_stride,
-                                                 const OaImg* __restrict__ imgs, const OaTile* __restrict__ tiles,
-                                                 uint8_t* __restrict__ csmap) {
-    __shared__ uint32_t lds[SM_LR * SM_LW / 4];
-    const int f = blockIdx.y;
-    const OaTile T = tiles[blockIdx.x];
-    const OaImg I = imgs[T.img];
-    smap_tile(cpyr + (size_t)f * cp_stride + I.off, I.w, I.h, I.pitch, T.tx0, T.ty0,
-              csmap + (size_t)f * cp_stride + I.off, lds);
-}
-
-// ============================================================ candidates
-// One workgroup per (band, frame): the band's S rows with one row / column of
-// halo (real S values: the halo lies inside FAST's detection region [3, h-3),
-// where NMS sees it; S is 0 outside it) staged in LDS; survivors of the
-// threshold-free NMS (S >= 2, S > all 8 neighbours) inside runByImageBorder's
-// [15, w-15) x [15, h-15), in row-major order, + the level's S histogram.
+// ============================================================ S + candidates
+// One workgroup per (band, frame). The band's image rows y0-4 .. y1+3 are
+// staged in LDS (aligned dwords); S (smap4) is computed for the band's rows
+// and one halo row / column on each side (rows y0-1 .. y1, columns 12 ..
+// w-14: inside FAST's detection region [3, h-3), so every value is the real
+// S), kept in LDS; then the survivors of the threshold-free NMS (S >= 2,
+// S > all 8 neighbours) inside runByImageBorder's [15, w-15) x [15, h-15),
+// in row-major order, + the level's S histogram. The S map never goes to HBM.
 #define OA_MAXW 1024
-__global__ void __launch_bounds__(256) k_oa_cand(const uint8_t* __restrict__ csmap, size_t cp_stride,
-                                                 const OaImg* __restrict__ imgs, const OaBand* __restrict__ bands,
-                                                 int nimgs, uint32_t* __restrict__ cand, size_t cand_stride,
-                                                 int* __restrict__ band_cnt, int nbands, int* __restrict__ hist) {
-    __shared__ uint8_t s[(AD_BH + 2) * (OA_MAXW + 2)];
+#define OA_X0 12  // first S column (dword aligned, <= 15 - 1)
+__global__ void __launch_bounds__(256) k_oa_scand(const uint8_t* __restrict__ cpyr, size_t cp_stride,
+                                                  const OaImg* __restrict__ imgs, const OaBand* __restrict__ bands,
+                                                  int nimgs, uint32_t* __restrict__ cand, size_t cand_stride,
+                                                  int* __restrict__ band_cnt, int nbands, int* __restrict__ hist) {
+    __shared__ uint32_t img_l[(AD_BH + 8) * (OA_MAXW / 4)];
+    __shared__ __attribute__((aligned(4))) uint8_t s[(AD_BH + 2) * OA_MAXW];
     __shared__ int sh[256];
     __shared__ int ws[16];
     const int f = blockIdx.y;
     const OaBand B = bands[blockIdx.x];
     const OaImg I = imgs[B.img];
     const int c0 = OA_EDGE, c1 = I.w - OA_EDGE;
-    const int cw = c1 - c0, lw = cw + 2;
+    const int cw = c1 - c0;
     const int rows = B.y1 - B.y0;
-    const uint8_t* S = csmap + (size_t)f * cp_stride + I.off;
+    const int pq = I.pitch >> 2;                       // dwords per image row
+    const int nq = (c1 + 1 - OA_X0 + 3) >> 2;          // S dwords per row (columns OA_X0 .. c1)
+    const int lw = nq * 4;                             // S bytes per LDS row
     sh[threadIdx.x] = 0;
-    for (int r = 0; r < rows + 2; r++) {
-        const uint8_t* srow = S + (size_t)(B.y0 - 1 + r) * I.pitch + (c0 - 1);
-        for (int q = threadIdx.x; q < lw; q += 256) s[r * lw + q] = srow[q];
+    {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(cpyr + (size_t)f * cp_stride + I.off +
+                                                                (size_t)(B.y0 - 4) * I.pitch);
+        for (int i = threadIdx.x; i < (rows + 8) * pq; i += 256) img_l[i] = src[i];
+    }
+    __syncthreads();
+    for (int it = threadIdx.x; it < (rows + 2) * nq; it += 256) {
+        const int r = it / nq, q = it - r * nq;         // S row y0-1+r, columns OA_X0 + 4q ..
+        const int k = (OA_X0 >> 2) + q;                 // image dword of the 4 pixels
+        uint32_t W[7][3];
+#pragma unroll
+        for (int dy = 0; dy < 7; dy++)
+#pragma unroll
+            for (int j = 0; j < 3; j++) W[dy][j] = img_l[(r + dy) * pq + min(k - 1 + j, pq - 1)];
+        reinterpret_cast<uint32_t*>(s)[r * nq + q] = smap4(W);
     }
     __syncthreads();
     const int npx = rows * cw;
     const int chunk = (npx + 255) / 256;
     const int i0 = min(npx, (int)threadIdx.x * chunk), i1 = min(npx, i0 + chunk);
     const int r0 = cw > 0 ? i0 / cw : 0, q0 = i0 - r0 * cw;
-    auto survivor = [&](int r, int q, int* sv) -> bool {
-        const uint8_t* p = s + (r + 1) * lw + (q + 1);
+    auto survivor = [&](int r, int q, int* sv) -> bool {  // band row r, candidate column c0 + q
+        const uint8_t* p = s + (r + 1) * lw + (c0 - OA_X0 + q);
         const int v = p[0];
         *sv = v;
         if (v < 2) return false;
@@ -214,7 +218,7 @@ __global__ void __launch_bounds__(256) k_oa_cand(const uint8_t* __restrict__ csm
     {
         int r = r0, q = q0;
         for (int i = i0; i < i1; i++) {
-            int sv = s[(r + 1) * lw + (q + 1)];
+            int sv = s[(r + 1) * lw + (c0 - OA_X0 + q)];
             const bool keep = (i - i0 < 32) ? ((smask >> (i - i0)) & 1u) != 0 : survivor(r, q, &sv);
             if (keep) out[o++] = ((uint32_t)sv << 24) | ((uint32_t)(B.y0 + r) << 12) | (uint32_t)(c0 + q);
             if (++q == cw) {
@@ -577,15 +581,10 @@ void launch_oa_pyr(hipStream_t st, const uint8_t* pyr, size_t pyr_stride, int gp
                        cpyr, cp_stride);
 }
 
-void launch_oa_smap(hipStream_t st, const uint8_t* cpyr, size_t cp_stride, const OaImg* imgs, const OaTile* tiles,
-                    int ntiles, uint8_t* csmap, int nframes) {
-    hipLaunchKernelGGL(k_oa_smap, dim3(ntiles, nframes), dim3(256), 0, st, cpyr, cp_stride, imgs, tiles, csmap);
-}
-
-void launch_oa_cand(hipStream_t st, const uint8_t* csmap, size_t cp_stride, const OaImg* imgs, int nimgs,
-                    const OaBand* bands, int nbands, uint32_t* cand, size_t cand_stride, int* band_cnt, int* hist,
-                    int nframes) {
-    hipLaunchKernelGGL(k_oa_cand, dim3(nbands, nframes), dim3(256), 0, st, csmap, cp_stride, imgs, bands, nimgs, cand,
+void launch_oa_scand(hipStream_t st, const uint8_t* cpyr, size_t cp_stride, const OaImg* imgs, int nimgs,
+                     const OaBand* bands, int nbands, uint32_t* cand, size_t cand_stride, int* band_cnt, int* hist,
+                     int nframes) {
+    hipLaunchKernelGGL(k_oa_scand, dim3(nbands, nframes), dim3(256), 0, st, cpyr, cp_stride, imgs, bands, nimgs, cand,
                        cand_stride, band_cnt, nbands, hist);
 }
 

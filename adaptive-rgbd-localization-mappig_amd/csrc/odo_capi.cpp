@@ -273,15 +273,13 @@ struct odo_ctx {
     std::vector<OaImg> oai_h;
     std::vector<OaCell> oac_h;
     std::vector<OaBand> oab_h;
-    std::vector<OaTile> oat_h;
     OaImg* oai = nullptr;
     OaCell* oac = nullptr;
     OaBand* oab = nullptr;
-    OaTile* oat = nullptr;
     OaScales osc{};
     int oa_ncap = 0, oa_buf0 = 0, oa_buf1 = 0;
     size_t cp_stride = 0, ocand_stride = 0, oscr_stride = 0;
-    uint8_t *cpyr = nullptr, *csmap = nullptr, *oscr = nullptr;
+    uint8_t *cpyr = nullptr, *oscr = nullptr;
     uint32_t* ocand = nullptr;
     int *oband_cnt = nullptr, *ohist = nullptr, *ophist = nullptr;
     uint64_t *ocell = nullptr, *oakp = nullptr;
@@ -333,7 +331,7 @@ static void free_ctx(odo_ctx* c) {
                     c->bgr_in[1], c->depth_in[1],
                     c->sort_scratch, c->latch, c->masks, c->adc, c->adb, c->smap, c->acand, c->abig, c->acell,
                     c->akp, c->aband_cnt, c->ahist, c->atsel, c->ansel, c->acell_cnt, c->athresh, c->oai, c->oac,
-                    c->oab, c->oat, c->cpyr, c->csmap, c->oscr, c->ocand, c->oband_cnt, c->ohist, c->ophist,
+                    c->oab, c->cpyr, c->oscr, c->ocand, c->oband_cnt, c->ohist, c->ophist,
                     c->ocell, c->oakp};
     for (void* p : ptrs)
         if (p) hipFree(p);
@@ -375,7 +373,7 @@ static void free_ctx(odo_ctx* c) {
 // ADAPTIVE with the cv::ORB inner detector: per grid cell the 8 levels of
 // cv::ORB's pyramid of the cell sub-image (getScale sizes, orb.cpp), their
 // candidate bands (rows [15, h-15) in AD_BH-row bands; strict 3x3 maxima are
-// never 8-adjacent: <= ceil(r/2)ceil(c/2) survivors), S-map tiles; the frame
+// never 8-adjacent: <= ceil(r/2)ceil(c/2) survivors); the frame
 // pyramid (pyr / blur, built by build_geometry) must have cv::ORB's level
 // sizes, since cv::ORB::compute samples it.
 static int build_adaptive_orb_geometry(odo_ctx* c) {
@@ -411,7 +409,6 @@ static int build_adaptive_orb_geometry(odo_ctx* c) {
     c->oai_h.clear();
     c->oac_h.clear();
     c->oab_h.clear();
-    c->oat_h.clear();
     int off = 0, coff = 0, buf0 = 0, buf1 = 0;
     c->oa_ncap = 1;
     for (const AdCell& A : c->adc_h) {
@@ -448,8 +445,6 @@ static int build_adaptive_orb_geometry(odo_ctx* c) {
                 }
             I.band1 = (int)c->oab_h.size();
             ncap += I.cand_cap;
-            for (int ty = 0; ty < I.h; ty += OA_TILE_H)
-                for (int tx = 0; tx < I.pitch; tx += OA_TILE_W) c->oat_h.push_back(OaTile{img, tx, ty, 0});
             c->oai_h.push_back(I);
         }
         c->oa_ncap = std::max(c->oa_ncap, ncap);
@@ -468,12 +463,10 @@ static int build_adaptive_orb_geometry(odo_ctx* c) {
     if ((e = dalloc(&c->oai, c->oai_h.size()))) return e;
     if ((e = dalloc(&c->oac, c->oac_h.size()))) return e;
     if ((e = dalloc(&c->oab, std::max<size_t>(c->oab_h.size(), 1)))) return e;
-    if ((e = dalloc(&c->oat, std::max<size_t>(c->oat_h.size(), 1)))) return e;
     HIPCHK(hipMemcpy(c->oai, c->oai_h.data(), c->oai_h.size() * sizeof(OaImg), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c->oac, c->oac_h.data(), c->oac_h.size() * sizeof(OaCell), hipMemcpyHostToDevice));
     if (!c->oab_h.empty())
         HIPCHK(hipMemcpy(c->oab, c->oab_h.data(), c->oab_h.size() * sizeof(OaBand), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->oat, c->oat_h.data(), c->oat_h.size() * sizeof(OaTile), hipMemcpyHostToDevice));
     return ODO_OK;
 }
 
@@ -810,7 +803,6 @@ static int alloc_buffers(odo_ctx* c) {
         } else {
             const size_t ni = c->oai_h.size();
             if ((e = dalloc(&c->cpyr, B * c->cp_stride))) return e;
-            if ((e = dalloc(&c->csmap, B * c->cp_stride))) return e;
             if ((e = dalloc(&c->ocand, B * c->ocand_stride))) return e;
             if ((e = dalloc(&c->oband_cnt, B * std::max<size_t>(c->oab_h.size(), 1)))) return e;
             if ((e = dalloc(&c->ohist, B * ni * 256))) return e;
@@ -1109,11 +1101,10 @@ static int run_extract_adaptive_orb(odo_ctx* c, int set, const uint8_t* d_bgr, c
     }
     tmark(c, 1, st);
     launch_oa_pyr(st, pyr, P, c->lv_h[0].pitch, c->oac, nc, c->oai, c->oa_buf0, c->oa_buf1, c->cpyr, c->cp_stride, n);
-    launch_oa_smap(st, c->cpyr, c->cp_stride, c->oai, c->oat, (int)c->oat_h.size(), c->csmap, n);
     HIPCHK(hipMemsetAsync(c->ohist, 0, (size_t)n * ni * 256 * sizeof(int), st));
     if (nb > 0)
-        launch_oa_cand(st, c->csmap, c->cp_stride, c->oai, ni, c->oab, nb, c->ocand, c->ocand_stride, c->oband_cnt,
-                       c->ohist, n);
+        launch_oa_scand(st, c->cpyr, c->cp_stride, c->oai, ni, c->oab, nb, c->ocand, c->ocand_stride, c->oband_cnt,
+                        c->ohist, n);
     launch_oa_count(st, c->ohist, c->oac, c->oai, ni, nc, c->ophist, n);
     tmark(c, 2, st);
     launch_adapt_chain(st, c->ophist, nc, n, c->cfg.adaptive, c->athresh, c->atsel, c->ansel);

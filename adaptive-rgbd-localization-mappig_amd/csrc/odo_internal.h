@@ -137,11 +137,6 @@ struct OaCell {
 struct OaBand {
     int img, y0, y1, cand_off;
 };
-struct OaTile {
-    int img, tx0, ty0, pad;
-};
-#define OA_TILE_W 128  // S-map tile (smap_tile, odo_select.h)
-#define OA_TILE_H 8
 struct OaScales {
     float s[OA_NLEV];  // getScale(level) = (float)pow((double)1.2f, level)
 };
@@ -258,11 +253,9 @@ void launch_adapt_finalize(hipStream_t st, const uint8_t* blur, size_t pyr_strid
 void upload_adaptive_orb_constants();
 void launch_oa_pyr(hipStream_t st, const uint8_t* pyr, size_t pyr_stride, int gpitch, const OaCell* cells, int ncells,
                    const OaImg* imgs, int buf0, int buf1, uint8_t* cpyr, size_t cp_stride, int nframes);
-void launch_oa_smap(hipStream_t st, const uint8_t* cpyr, size_t cp_stride, const OaImg* imgs, const OaTile* tiles,
-                    int ntiles, uint8_t* csmap, int nframes);
-void launch_oa_cand(hipStream_t st, const uint8_t* csmap, size_t cp_stride, const OaImg* imgs, int nimgs,
-                    const OaBand* bands, int nbands, uint32_t* cand, size_t cand_stride, int* band_cnt, int* hist,
-                    int nframes);
+void launch_oa_scand(hipStream_t st, const uint8_t* cpyr, size_t cp_stride, const OaImg* imgs, int nimgs,
+                     const OaBand* bands, int nbands, uint32_t* cand, size_t cand_stride, int* band_cnt, int* hist,
+                     int nframes);
 void launch_oa_count(hipStream_t st, const int* hist, const OaCell* cells, const OaImg* imgs, int nimgs, int ncells,
                      int* phist, int nframes);
 size_t oa_select_scratch_bytes(int ncap);

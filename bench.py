@@ -127,7 +127,7 @@ def host_info():
     return {"nproc": os.cpu_count(), "usable_cores": len(os.sched_getaffinity(0)), "model": model}
 
 
-def cpu_baseline(bgr, dep, nfeat, iters, n_frames, reps, adaptive=False, threads=16):
+def cpu_baseline(bgr, dep, nfeat, iters, n_frames, reps, adaptive=False, threads=16, inner="fast"):
     """The C++ oracle on the first n_frames frames of the same sequence.
 
     Single thread: this thread pinned to one core (taskset -c equivalent),
@@ -151,7 +151,7 @@ def cpu_baseline(bgr, dep, nfeat, iters, n_frames, reps, adaptive=False, threads
             O.extract_frame(bgr[i % n], dep[i % n], p, cal)
 
     def run_pass():
-        ex = O.AdaptiveExtractor() if adaptive else None
+        ex = O.AdaptiveExtractor(inner=inner) if adaptive else None
         te = tt = 0.0
         prev, latch = None, float("nan")
         for i in range(n_frames):
@@ -185,7 +185,7 @@ def cpu_baseline(bgr, dep, nfeat, iters, n_frames, reps, adaptive=False, threads
         t0 = time.perf_counter()
         with ThreadPoolExecutor(nthr) as pool:
             if adaptive:
-                ex = O.AdaptiveExtractor()
+                ex = O.AdaptiveExtractor(inner=inner)
                 frames = [extract(ex, i) for i in range(nf_all)]
             else:
                 frames = list(pool.map(lambda i: extract(None, i), range(nf_all)))
@@ -417,8 +417,9 @@ def main():
     ap.add_argument("--shard", choices=["sequence", "independent"], default="sequence",
                     help="N > 1: 'sequence' = SURVEY 8(e) frames mode (one sequence, per-rank chunks + 1-frame "
                          "halo, latch broadcast, pose stitch); 'independent' = one sequence per rank")
-    ap.add_argument("--detector", choices=["orb_slam2", "adaptive"], default="orb_slam2",
-                    help="orb_slam2: ORBextractor (the metric's config); adaptive: Extractor(FAST, ORB, ADAPTIVE)")
+    ap.add_argument("--detector", choices=["orb_slam2", "adaptive", "adaptive-orb"], default="orb_slam2",
+                    help="orb_slam2: ORBextractor (the metric's config); adaptive: Extractor(FAST, ORB, ADAPTIVE); "
+                         "adaptive-orb: Extractor(ORB, ORB, ADAPTIVE) (cv::ORB cell detector)")
     args = ap.parse_args()
 
     if args.mode == "latency":
@@ -460,7 +461,8 @@ def main():
     bgr_loop, dep_loop, gt_poses = synth.make_sequence(L, W, H, seed=scene_seed, closed_loop=True,
                                                        hard=args.workload == "hard")
     bgr, dep = bgr_loop[np.arange(B) % L], dep_loop[np.arange(B) % L]
-    adaptive = args.detector == "adaptive"
+    adaptive = args.detector in ("adaptive", "adaptive-orb")
+    inner = "orb" if args.detector == "adaptive-orb" else "fast"
     if adaptive:
         args.nfeatures = 1000  # Extract's retainBest(nFeatures), common.h:77
         if seq_mode:
@@ -477,7 +479,8 @@ def main():
         d_dep = torch.from_numpy(dep.view(np.int16)).to("cuda")
     cfg = pkg.default_config(W, H, B + 1 if seq_mode else B, nfeatures=args.nfeatures, iterations=args.iters,
                              seed=pair_seed,
-                             detector=pkg.DETECTOR_ADAPTIVE_FAST if adaptive else pkg.DETECTOR_ORB_SLAM2)
+                             detector=(pkg.DETECTOR_ORB_SLAM2 if not adaptive else
+                                       pkg.DETECTOR_ADAPTIVE_ORB if inner == "orb" else pkg.DETECTOR_ADAPTIVE_FAST))
     odo = pkg.Odometry(cfg, device=local_rank % max(1, torch.cuda.device_count()))
     torch.cuda.synchronize()
     coll_dev = "cuda" if args.backend == "nccl" else "cpu"  # where the exchanges' tensors live
@@ -693,7 +696,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         nf = args.cpu_frames
-        cb = cpu_baseline(bgr, dep, args.nfeatures, args.iters, nf, args.cpu_reps, adaptive)
+        cb = cpu_baseline(bgr, dep, args.nfeatures, args.iters, nf, args.cpu_reps, adaptive, inner=inner)
         hi = host_info()
         cpu = {"value": round(cb["fps"], 3), "unit": "frames/s", "cores": 1, "kind": "port",
                "sample": f"{nf} frames of the rank-0 {L}-frame closed loop through the C++ oracle's extract + "
@@ -709,7 +712,8 @@ def main():
         ok = res_q
         out = {
             "metric": "frames/sec (extract+match+RANSAC-PnP) @640x480, 2000 kp" if not adaptive else
-                      "frames/sec (ADAPTIVE FAST grid + ORB, match, RANSAC-PnP) @640x480, <=1000 kp",
+                      f"frames/sec (ADAPTIVE {'cv::ORB' if inner == 'orb' else 'FAST'} grid + ORB, match, "
+                      f"RANSAC-PnP) @640x480, <=1000 kp",
             "value": round(value, 2),
             "unit": "frames/s",
             "n_gpus": world,
@@ -724,7 +728,8 @@ def main():
             "config": {"workload": (f"cfg2 fr1/desk proxy {W}x{H}, {args.nfeatures} kp, RANSAC {args.iters}"
                                     + (" (hard variant)" if args.workload == "hard" else "")
                                     if not adaptive else
-                                    f"fr1/desk proxy {W}x{H}, ADAPTIVE 3x3 FAST grid + ORB (<=1000 kp), "
+                                    f"fr1/desk proxy {W}x{H}, ADAPTIVE 3x3 {'cv::ORB' if inner == 'orb' else 'FAST'} "
+                                    f"grid + ORB (<=1000 kp), "
                                     f"RANSAC {args.iters}"),
                        "frames_per_step": B, "global_batch": B * world, "parallelism": (f"sequence chunks x{world} (+1-frame halo, latch broadcast, pose stitch)"
                                        if seq_mode else f"frames x{world}"),
