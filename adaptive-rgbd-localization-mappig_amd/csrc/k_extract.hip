@@ -295,27 +295,30 @@ __global__ void __launch_bounds__(64) k_fast_cells(const uint8_t* __restrict__ p
                     const int off = c_circle_dy[k] * RS + c_circle_dx[k];
                     d[k] = s16x2{(short)(v0 - (int)roi[o0 + off]), (short)(v1 - (int)roi[o1 + off])};
                 }
-                s16x2 mn[16], mx[16];
+                // best 9-arc min / max: arcs k, k+1 (k even) share the run
+                // d[k+1 .. k+8] (odd 2-, 4-, 8-runs; the smap4 lattice form)
+                s16x2 mn2[8], mx2[8], mn4[8], mx4[8];
 #pragma unroll
-                for (int k = 0; k < 16; k++) {
-                    mn[k] = __builtin_elementwise_min(d[k], d[(k + 1) & 15]);
-                    mx[k] = __builtin_elementwise_max(d[k], d[(k + 1) & 15]);
+                for (int i = 0; i < 8; i++) {
+                    const int j = 2 * i + 1;
+                    mn2[i] = __builtin_elementwise_min(d[j], d[(j + 1) & 15]);
+                    mx2[i] = __builtin_elementwise_max(d[j], d[(j + 1) & 15]);
                 }
-                s16x2 mn4[16], mx4[16];
 #pragma unroll
-                for (int k = 0; k < 16; k++) {
-                    mn4[k] = __builtin_elementwise_min(mn[k], mn[(k + 2) & 15]);
-                    mx4[k] = __builtin_elementwise_max(mx[k], mx[(k + 2) & 15]);
+                for (int i = 0; i < 8; i++) {
+                    mn4[i] = __builtin_elementwise_min(mn2[i], mn2[(i + 1) & 7]);
+                    mx4[i] = __builtin_elementwise_max(mx2[i], mx2[(i + 1) & 7]);
                 }
                 s16x2 dk = s16x2{-32768, -32768}, br = s16x2{32767, 32767};
 #pragma unroll
-                for (int k = 0; k < 16; k++) {
-                    const s16x2 a9 = __builtin_elementwise_min(__builtin_elementwise_min(mn4[k], mn4[(k + 4) & 15]),
-                                                               d[(k + 8) & 15]);
-                    const s16x2 b9 = __builtin_elementwise_max(__builtin_elementwise_max(mx4[k], mx4[(k + 4) & 15]),
-                                                               d[(k + 8) & 15]);
-                    dk = __builtin_elementwise_max(dk, a9);
-                    br = __builtin_elementwise_min(br, b9);
+                for (int i = 0; i < 8; i++) {
+                    const int k = 2 * i;
+                    const s16x2 m8 = __builtin_elementwise_min(mn4[i], mn4[(i + 2) & 7]);
+                    const s16x2 x8 = __builtin_elementwise_max(mx4[i], mx4[(i + 2) & 7]);
+                    dk = __builtin_elementwise_max(
+                        dk, __builtin_elementwise_min(m8, __builtin_elementwise_max(d[k], d[(k + 9) & 15])));
+                    br = __builtin_elementwise_min(
+                        br, __builtin_elementwise_max(x8, __builtin_elementwise_min(d[k], d[(k + 9) & 15])));
                 }
                 const s16x2 sc = __builtin_elementwise_max(dk, -br);
                 score[o0] = (uint8_t)(sc.x - 1);
