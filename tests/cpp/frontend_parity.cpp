@@ -12,7 +12,7 @@
 //   Ransac mT12, inliers, rmse     bit-exact
 //   PnPSolver pose                 |dT| < 1e-4, inlier count and outlier flags equal
 //
-// usage: frontend_parity FRAMES.bin W H F SEED [adaptive]
+// usage: frontend_parity FRAMES.bin W H F SEED [adaptive|adaptive_orb]
 //   FRAMES.bin = F x H x W x 3 BGR8, then F x H x W depth16 (x5000)
 // Prints one summary line; exit 0 = parity.
 #include <cmath>
@@ -115,12 +115,13 @@ int main(int argc, char** argv) {
 
 static int run(int argc, char** argv) {
     if (argc < 6) {
-        fprintf(stderr, "usage: %s FRAMES.bin W H F SEED [adaptive]\n", argv[0]);
+        fprintf(stderr, "usage: %s FRAMES.bin W H F SEED [adaptive|adaptive_orb]\n", argv[0]);
         return 2;
     }
     const int W = atoi(argv[2]), H = atoi(argv[3]), F = atoi(argv[4]);
     const uint32_t seed = (uint32_t)strtoul(argv[5], nullptr, 0);
-    const bool adaptive = argc > 6 && strcmp(argv[6], "adaptive") == 0;
+    const bool adaptive_orb = argc > 6 && strcmp(argv[6], "adaptive_orb") == 0;
+    const bool adaptive = adaptive_orb || (argc > 6 && strcmp(argv[6], "adaptive") == 0);
     const size_t npx = (size_t)W * H;
     vector<uint8_t> bgr(npx * 3 * F);
     vector<uint16_t> dep(npx * F);
@@ -142,8 +143,9 @@ static int run(int argc, char** argv) {
     EXPECT(threw, "Extractor(SURF, BRIEF, ADAPTIVE) must throw");
 
     odo_hip::Extractor extractor =
-        adaptive ? odo_hip::Extractor(odo_hip::Extractor::FAST, odo_hip::Extractor::ORB, odo_hip::Extractor::ADAPTIVE)
-                 : odo_hip::Extractor(odo_hip::Extractor::ORB_SLAM2, odo_hip::Extractor::ORB_SLAM2,
+        adaptive_orb ? odo_hip::Extractor(odo_hip::Extractor::ORB, odo_hip::Extractor::ORB, odo_hip::Extractor::ADAPTIVE)
+        : adaptive   ? odo_hip::Extractor(odo_hip::Extractor::FAST, odo_hip::Extractor::ORB, odo_hip::Extractor::ADAPTIVE)
+                     : odo_hip::Extractor(odo_hip::Extractor::ORB_SLAM2, odo_hip::Extractor::ORB_SLAM2,
                                       odo_hip::Extractor::NORMAL);
     const odo_calib cal = odo_hip::Calibration();
     odo_orb_params orb;
@@ -175,7 +177,11 @@ static int run(int argc, char** argv) {
         o.kun.resize(2 * cap);
         o.xyz.resize(3 * cap);
         o.ur.resize(cap);
-        const int n = adaptive ? oracle_extract_frame_adaptive(&bgr[npx * 3 * t], &dep[npx * t], W, H, &ap,
+        const int n = adaptive_orb
+                          ? oracle_extract_frame_adaptive_orb(&bgr[npx * 3 * t], &dep[npx * t], W, H, &ap,
+                                                              thresh.data(), &cal, o.kps.data(), o.desc.data(),
+                                                              o.kun.data(), o.xyz.data(), o.ur.data(), cap)
+                      : adaptive ? oracle_extract_frame_adaptive(&bgr[npx * 3 * t], &dep[npx * t], W, H, &ap,
                                                                thresh.data(), &cal, o.kps.data(), o.desc.data(),
                                                                o.kun.data(), o.xyz.data(), o.ur.data(), cap)
                                : oracle_extract_frame(&bgr[npx * 3 * t], &dep[npx * t], W, H, &orb, &cal,
@@ -276,7 +282,7 @@ static int run(int argc, char** argv) {
 
     printf("frontend_parity %s frames=%d matches=%ld ransac_inliers=%ld pnp_inliers=%ld max_dT=%.3g "
            "projection_matches=%d failures=%d\n",
-           adaptive ? "adaptive" : "orb_slam2", F, total_matches, total_inliers, total_pnp, max_dT, proj_checked,
+           adaptive_orb ? "adaptive_orb" : adaptive ? "adaptive" : "orb_slam2", F, total_matches, total_inliers, total_pnp, max_dT, proj_checked,
            g_fail);
     return g_fail ? 1 : 0;
 }

@@ -52,12 +52,12 @@ def test_fails_loudly_without_device(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["orb_slam2", "adaptive"])
+@pytest.mark.parametrize("mode", ["orb_slam2", "adaptive", "adaptive_orb"])
 def test_frontend_parity(tmp_path, mode):
     bgr, dep, _ = sequence(5, seed=0x5EED0032)
     p = tmp_path / "f.bin"
     _write_frames(p, bgr, dep)
-    args = [_binary(), str(p), "640", "480", "5", "0x1234"] + (["adaptive"] if mode == "adaptive" else [])
+    args = [_binary(), str(p), "640", "480", "5", "0x1234"] + ([mode] if mode != "orb_slam2" else [])
     r = subprocess.run(args, capture_output=True, text=True, timeout=110)
     print(r.stdout, r.stderr)
     assert r.returncode == 0, r.stderr[-4000:]
