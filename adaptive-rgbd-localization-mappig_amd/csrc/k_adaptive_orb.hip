@@ -38,17 +38,15 @@
 
 namespace odo {
 
-__constant__ int8_t c_opattern[1024];
-
 // ============================================================ cell pyramids
-// One workgroup per (frame, cell). Level 0 = the cell's ROI of the frame's
+// One 1024-thread workgroup per (frame, cell). Level 0 = the cell's ROI of the frame's
 // gray level 0; level l = cv::resize(level l-1, INTER_LINEAR) to the getScale
 // size (host). Source and destination levels alternate between two LDS
 // buffers; every level is also written to the frame's cell-pyramid buffer
 // (pitched rows, zero padding). Resize tables are made in LDS with the
 // generic-path rules of App. A.2 (the host rules of odo_capi.cpp
 // build_geometry).
-__global__ void __launch_bounds__(512) k_oa_pyr(const uint8_t* __restrict__ pyr, size_t pyr_stride, int gpitch,
+__global__ void __launch_bounds__(1024) k_oa_pyr(const uint8_t* __restrict__ pyr, size_t pyr_stride, int gpitch,
                                                 const OaCell* __restrict__ cells, const OaImg* __restrict__ imgs,
                                                 int buf0, uint8_t* __restrict__ cpyr, size_t cp_stride) {
     extern __shared__ __attribute__((aligned(16))) uint8_t op_lds[];
@@ -59,15 +57,19 @@ __global__ void __launch_bounds__(512) k_oa_pyr(const uint8_t* __restrict__ pyr,
     uint8_t* buf[2] = {op_lds, op_lds + buf0};
     uint8_t* out = cpyr + (size_t)f * cp_stride;
     {
+        // level 0: aligned dword pairs of the frame row realigned to the cell's
+        // first column (rows are pitch-aligned), bytes past the cell width zeroed
         const OaImg I = imgs[C.img0];
-        const uint8_t* g = pyr + (size_t)f * pyr_stride + (size_t)C.rs * gpitch + C.cs;
+        const uint32_t* g = reinterpret_cast<const uint32_t*>(pyr + (size_t)f * pyr_stride + (size_t)C.rs * gpitch +
+                                                              (C.cs & ~3));
+        const int sh = C.cs & 3, gq = gpitch >> 2;
         const int nq = I.pitch >> 2;
         for (int i = threadIdx.x; i < I.h * nq; i += blockDim.x) {
             const int r = i / nq, q = i - r * nq;
-            uint32_t v = 0;
-#pragma unroll
-            for (int j = 0; j < 4; j++)
-                if (4 * q + j < I.w) v |= (uint32_t)g[(size_t)r * gpitch + 4 * q + j] << (8 * j);
+            const uint32_t* row = g + (size_t)r * gq + q;
+            uint32_t v = __builtin_amdgcn_alignbyte(row[1], row[0], sh);
+            const int valid = I.w - 4 * q;  // bytes of this dword inside the cell
+            if (valid < 4) v = valid <= 0 ? 0u : v & ((1u << (8 * valid)) - 1u);
             reinterpret_cast<uint32_t*>(buf[0])[i] = v;
             reinterpret_cast<uint32_t*>(out + I.off)[i] = v;
         }
@@ -144,14 +146,16 @@ __global__ void __launch_bounds__(512) k_oa_pyr(const uint8_t* __restrict__ pyr,
 // S), kept in LDS; then the survivors of the threshold-free NMS (S >= 2,
 // S > all 8 neighbours) inside runByImageBorder's [15, w-15) x [15, h-15),
 // in row-major order, + the level's S histogram. The S map never goes to HBM.
-#define OA_MAXW 1024
 #define OA_X0 12  // first S column (dword aligned, <= 15 - 1)
 __global__ void __launch_bounds__(256) k_oa_scand(const uint8_t* __restrict__ cpyr, size_t cp_stride,
                                                   const OaImg* __restrict__ imgs, const OaBand* __restrict__ bands,
                                                   int nimgs, uint32_t* __restrict__ cand, size_t cand_stride,
-                                                  int* __restrict__ band_cnt, int nbands, int* __restrict__ hist) {
-    __shared__ uint32_t img_l[(AD_BH + 8) * (OA_MAXW / 4)];
-    __shared__ __attribute__((aligned(4))) uint8_t s[(AD_BH + 2) * OA_MAXW];
+                                                  int* __restrict__ band_cnt, int nbands, int* __restrict__ hist,
+                                                  int maxpitch) {
+    // dynamic LDS sized for the widest cell level (maxpitch): the image rows,
+    // then the S rows
+    extern __shared__ __attribute__((aligned(16))) uint32_t img_l[];
+    uint8_t* s = reinterpret_cast<uint8_t*>(img_l + (AD_BH + 8) * (maxpitch >> 2));
     __shared__ int sh[256];
     __shared__ int ws[16];
     const int f = blockIdx.y;
@@ -462,88 +466,181 @@ __global__ void __launch_bounds__(256) k_oa_assemble(const uint64_t* __restrict_
 }
 
 // ============================================================ finalize
-// Four keypoints per wave, 16 lanes each. IC angle (ICAngles, orb.cpp) on the
-// keypoint's cell level: lane v sums disc row pair +-v (lane 0 the centre
-// row), then a 16-lane butterfly. rBRIEF (computeOrbDescriptors): centre
-// cvRound(pt / scale) on the frame pyramid's level; 16 tests per lane; a
-// sample inside the level reads the blurred level, one outside reads the
-// unblurred level at the REFLECT_101 position (the bordered pyramid's border,
-// which the in-place ROI blur leaves untouched).
+// Four keypoints per wave, 16 lanes each, OF_NW waves per workgroup (the
+// k_finalize_lds scheme, k_finalize.hip): each keypoint's two patches are
+// staged in LDS by its 16 lanes with row-contiguous dword loads -
+//   the IC disc, rows y-15..y+15 of the keypoint's cell level (always inside:
+//   runByImageBorder(15)), 9 dwords each;
+//   the rBRIEF window, rows cy-18..cy+18 of the frame pyramid's blurred level
+//   around the centre cvRound(pt / scale), 10 dwords each. A window that
+//   leaves the level is staged byte by byte with computeOrbDescriptors'
+//   border: the unblurred level at the REFLECT_101 position (the bordered
+//   pyramid's border, which the in-place ROI blur leaves untouched).
+// IC angle (ICAngles, orb.cpp): lane s sums disc rows s-15 and s+1 with
+// v_dot4 against the column weights and the |v| masks; 16-lane butterfly.
+// rBRIEF (computeOrbDescriptors): 16 tests per lane read as LDS bytes at the
+// magic-rounded offsets (cvRound half to even), one ballot per test group.
 __constant__ int c_oumax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
+__constant__ float4 c_opatf[256];  // pattern test t: (x0, y0, x1, y1)
 
 ODO_INLINE int refl101(int i, int n) {
     while (i < 0 || i >= n) i = i < 0 ? -i : 2 * n - 2 - i;
     return i;
 }
 
-#define OF_KPW 4
-#define OF_KPB (4 * OF_KPW)
-__global__ void __launch_bounds__(256) k_oa_finalize(const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
-                                                     size_t pyr_stride, const LevelDesc* __restrict__ lv,
-                                                     const uint8_t* __restrict__ cpyr, size_t cp_stride,
-                                                     const OaImg* __restrict__ imgs, const OaCell* __restrict__ cells,
-                                                     OaScales sc, const uint64_t* __restrict__ akp, int akp_stride,
-                                                     const int* __restrict__ nkp, orb_kp* __restrict__ kps,
-                                                     uint8_t* __restrict__ desc, int kp_cap) {
-    __shared__ uint64_t s_bal[4][16];
+typedef float f32x2o __attribute__((ext_vector_type(2)));
+#define OF_RND_MAGIC 12582912.0f  // 1.5 * 2^23
+#define OF_RND_BITS 0x4B400000u
+#define OF_IC_W 9
+#define OF_IC_N (31 * OF_IC_W)
+#define OF_BR_W 10
+#define OF_BR_N (37 * OF_BR_W)
+#define OF_KP_DW (OF_IC_N + OF_BR_N)
+#define OF_NW 2
+#define OF_KPB (4 * OF_NW)
+__global__ void __launch_bounds__(64 * OF_NW) k_oa_finalize(const uint8_t* __restrict__ pyr,
+                                                            const uint8_t* __restrict__ blur, size_t pyr_stride,
+                                                            const LevelDesc* __restrict__ lv,
+                                                            const uint8_t* __restrict__ cpyr, size_t cp_stride,
+                                                            const OaImg* __restrict__ imgs,
+                                                            const OaCell* __restrict__ cells, OaScales sc,
+                                                            const uint64_t* __restrict__ akp, int akp_stride,
+                                                            const int* __restrict__ nkp, orb_kp* __restrict__ kps,
+                                                            uint8_t* __restrict__ desc, int kp_cap) {
+    __shared__ uint64_t s_bal[OF_NW][16];
+    __shared__ __attribute__((aligned(16))) uint32_t s_disc[16][8];
+    __shared__ __attribute__((aligned(16))) uint32_t s_patch[OF_NW * 4][OF_KP_DW];
+    for (int d = threadIdx.x; d < 128; d += 64 * OF_NW) {
+        const int av = d >> 3, i = d & 7;
+        const int um = c_oumax[av];
+        uint32_t m = 0;
+#pragma unroll
+        for (int bb = 0; bb < 4; bb++) {
+            const int u = 4 * i + bb - 15;
+            if (u >= -um && u <= um) m |= 0xffu << (8 * bb);
+        }
+        s_disc[av][i] = m;
+    }
     const int f = blockIdx.y;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int g = lane >> 4, sub = lane & 15;
     const int n = nkp[f];
-    if (blockIdx.x * OF_KPB >= n) return;  // whole workgroup idle
-    const int idx = blockIdx.x * OF_KPB + wave * OF_KPW + g;
+    if (blockIdx.x * OF_KPB >= n) return;  // uniform over the workgroup
+    const int kslot = wave * 4 + g;
+    const int idx = blockIdx.x * OF_KPB + kslot;
     const bool valid = idx < n;
-    const uint64_t e = valid ? akp[(size_t)f * akp_stride + idx] : 0ull;
+    // an invalid slot stages a dummy in-level patch (keypoint 0) and writes nothing
+    const uint64_t e = akp[(size_t)f * akp_stride + (valid ? idx : 0)];
     const int cc = (int)((e >> 27) & 15), l = (int)((e >> 24) & 7);
     const int kx = (int)(e & 0xfff), ky = (int)((e >> 12) & 0xfff);
     const OaCell C = cells[cc];
+    const OaImg I = imgs[C.img0 + l];
+    const LevelDesc L = lv[l];
     const float s = sc.s[l];
     const float px = (float)kx * s + (float)C.cs, py = (float)ky * s + (float)C.rs;
-    // IC angle
-    int m10 = 0, m01 = 0;
-    if (valid) {
-        const OaImg I = imgs[C.img0 + l];
-        const uint8_t* ctr = cpyr + (size_t)f * cp_stride + I.off + (size_t)ky * I.pitch + kx;
-        const int v = sub, d = c_oumax[v];
-        if (v == 0) {
-            for (int u = -15; u <= 15; u++) m10 += u * ctr[u];
-        } else {
-            int vs = 0;
-            for (int u = -d; u <= d; u++) {
-                const int vp = ctr[u + v * I.pitch], vm = ctr[u - v * I.pitch];
-                vs += vp - vm;
-                m10 += u * (vp + vm);
+    const float inv = 1.f / s;
+    const int cy = cv_round(py * inv), cx = cv_round(px * inv);
+    uint32_t* P = s_patch[kslot];
+    const int sh = (kx - 15) & 3, sh2 = (cx - 18) & 3;
+    const bool inside = cy >= 18 && cy + 18 < L.h && cx >= 18 && cx + 18 < L.w;  // uniform per keypoint
+    {
+        const uint8_t* img = cpyr + (size_t)f * cp_stride + I.off + (size_t)(ky - 15) * I.pitch + (kx - 15 - sh);
+        uint32_t v[18];
+#pragma unroll
+        for (int j = 0; j < 18; j++) {
+            const int i = min(sub + 16 * j, OF_IC_N - 1);
+            const int r = i / OF_IC_W, c = i - r * OF_IC_W;
+            v[j] = *reinterpret_cast<const uint32_t*>(img + (size_t)r * I.pitch + 4 * c);
+        }
+#pragma unroll
+        for (int j = 0; j < 18; j++)
+            if (sub + 16 * j < OF_IC_N) P[sub + 16 * j] = v[j];
+    }
+    {
+        const uint8_t* bim = blur + (size_t)f * pyr_stride + L.off;
+        if (inside) {
+            const uint8_t* b0 = bim + (size_t)(cy - 18) * L.pitch + (cx - 18 - sh2);
+            uint32_t v[24];
+#pragma unroll
+            for (int j = 0; j < 24; j++) {
+                const int i = min(sub + 16 * j, OF_BR_N - 1);
+                const int r = i / OF_BR_W, c = i - r * OF_BR_W;
+                v[j] = *reinterpret_cast<const uint32_t*>(b0 + (size_t)r * L.pitch + 4 * c);
             }
-            m01 = v * vs;
+#pragma unroll
+            for (int j = 0; j < 24; j++)
+                if (sub + 16 * j < OF_BR_N) P[OF_IC_N + sub + 16 * j] = v[j];
+        } else {
+            const uint8_t* un = pyr + (size_t)f * pyr_stride + L.off;
+            uint8_t* PB = reinterpret_cast<uint8_t*>(P + OF_IC_N);
+            for (int i = sub; i < 4 * OF_BR_N; i += 16) {
+                const int r = i / (4 * OF_BR_W), c = i - r * (4 * OF_BR_W);
+                const int yy = cy - 18 + r, xx = cx - 18 - sh2 + c;
+                PB[i] = (yy >= 0 && yy < L.h && xx >= 0 && xx < L.w)
+                            ? bim[(size_t)yy * L.pitch + xx]
+                            : un[(size_t)refl101(yy, L.h) * L.pitch + refl101(xx, L.w)];
+            }
         }
     }
+    __syncthreads();  // s_disc, the patches
+    int m10, m01;
+    {
+        const bool has1 = sub < 15;
+        const int v0 = sub - 15, v1 = has1 ? sub + 1 : 0;
+        const uint32_t* r0 = P + (v0 + 15) * OF_IC_W;
+        const uint32_t* r1 = P + (v1 + 15) * OF_IC_W;
+        uint32_t w0[9], w1[9];
 #pragma unroll
-    for (int o = 8; o >= 1; o >>= 1) {
-        m10 += __shfl_xor(m10, o, 16);
-        m01 += __shfl_xor(m01, o, 16);
+        for (int i = 0; i < 9; i++) {
+            w0[i] = r0[i];
+            w1[i] = r1[i];
+        }
+        const uint4* M0 = reinterpret_cast<const uint4*>(s_disc[-v0]);
+        const uint4* M1 = reinterpret_cast<const uint4*>(s_disc[v1]);
+        const uint4 a0 = M0[0], a1 = M0[1], b0 = M1[0], b1 = M1[1];
+        const uint32_t z = has1 ? 0xffffffffu : 0u;
+        const uint32_t mk0[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        const uint32_t mk1[8] = {b0.x & z, b0.y & z, b0.z & z, b0.w & z, b1.x & z, b1.y & z, b1.z & z, b1.w & z};
+        uint32_t s0 = 0, s1 = 0, t = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const uint32_t U = (uint32_t)(4 * i + 1) | ((uint32_t)(4 * i + 2) << 8) | ((uint32_t)(4 * i + 3) << 16) |
+                               ((uint32_t)(4 * i + 4) << 24);
+            const uint32_t d0 = __builtin_amdgcn_alignbyte(w0[i + 1], w0[i], sh) & mk0[i];
+            const uint32_t d1 = __builtin_amdgcn_alignbyte(w1[i + 1], w1[i], sh) & mk1[i];
+            s0 = __builtin_amdgcn_udot4(d0, 0x01010101u, s0, false);
+            s1 = __builtin_amdgcn_udot4(d1, 0x01010101u, s1, false);
+            t = __builtin_amdgcn_udot4(d0, U, t, false);
+            t = __builtin_amdgcn_udot4(d1, U, t, false);
+        }
+        m10 = (int)t - 16 * (int)(s0 + s1);
+        m01 = v0 * (int)s0 + v1 * (int)s1;
+    }
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1) {
+        m10 += __shfl_xor(m10, off);
+        m01 += __shfl_xor(m01, off);
     }
     const float angle = fast_atan2((float)m01, (float)m10);
     const float ang = angle * (float)(3.14159265358979323846 / 180.f);
     double sd, cd;
     sincos((double)ang, &sd, &cd);
     const float a = (float)cd, b = (float)sd;
-    // rBRIEF
-    const LevelDesc L = lv[l];
-    const float inv = 1.f / s;
-    const int cy = cv_round(py * inv), cx = cv_round(px * inv);
-    const uint8_t* bl = blur + (size_t)f * pyr_stride + L.off;
-    const uint8_t* un = pyr + (size_t)f * pyr_stride + L.off;
-    auto sample = [&](float x, float y) -> int {
-        const int yy = cy + cv_round(x * b + y * a), xx = cx + cv_round(x * a - y * b);
-        if (yy >= 0 && yy < L.h && xx >= 0 && xx < L.w) return bl[yy * L.pitch + xx];
-        return un[refl101(yy, L.h) * L.pitch + refl101(xx, L.w)];
-    };
+    const f32x2o BA = {b, a}, AB = {a, b}, MAG = {OF_RND_MAGIC, OF_RND_MAGIC};
+    const uint8_t* PB = reinterpret_cast<const uint8_t*>(P + OF_IC_N);
+    const uint32_t cofs = (uint32_t)(18 * 4 * OF_BR_W + 18 + sh2) - OF_RND_BITS * (uint32_t)(4 * OF_BR_W + 1);
     int tv0[16], tv1[16];
 #pragma unroll
     for (int w = 0; w < 16; w++) {
-        const int bit = w * 16 + sub;
-        tv0[w] = valid ? sample((float)c_opattern[4 * bit + 0], (float)c_opattern[4 * bit + 1]) : 0;
-        tv1[w] = valid ? sample((float)c_opattern[4 * bit + 2], (float)c_opattern[4 * bit + 3]) : 0;
+        const float4 Pt = c_opatf[w * 16 + sub];
+        f32x2o q0 = (f32x2o){Pt.x, Pt.x} * BA + (f32x2o){Pt.y, -Pt.y} * AB;
+        f32x2o q1 = (f32x2o){Pt.z, Pt.z} * BA + (f32x2o){Pt.w, -Pt.w} * AB;
+        q0 = q0 + MAG;
+        q1 = q1 + MAG;
+        const uint32_t o0 = __float_as_uint(q0.x) * (uint32_t)(4 * OF_BR_W) + __float_as_uint(q0.y) + cofs;
+        const uint32_t o1 = __float_as_uint(q1.x) * (uint32_t)(4 * OF_BR_W) + __float_as_uint(q1.y) + cofs;
+        tv0[w] = PB[o0];
+        tv1[w] = PB[o1];
     }
 #pragma unroll
     for (int w = 0; w < 16; w++) {
@@ -570,22 +667,28 @@ __global__ void __launch_bounds__(256) k_oa_finalize(const uint8_t* __restrict__
 
 // ============================================================ launch wrappers
 void upload_adaptive_orb_constants() {
-    hipMemcpyToSymbol(HIP_SYMBOL(c_opattern), ODO_ORB_PATTERN, sizeof(ODO_ORB_PATTERN));
+    float4 pat[256];
+    for (int t = 0; t < 256; t++)
+        pat[t] = make_float4((float)ODO_ORB_PATTERN[4 * t], (float)ODO_ORB_PATTERN[4 * t + 1],
+                             (float)ODO_ORB_PATTERN[4 * t + 2], (float)ODO_ORB_PATTERN[4 * t + 3]);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_opatf), pat, sizeof(pat));
 }
 
 void launch_oa_pyr(hipStream_t st, const uint8_t* pyr, size_t pyr_stride, int gpitch, const OaCell* cells, int ncells,
                    const OaImg* imgs, int buf0, int buf1, uint8_t* cpyr, size_t cp_stride, int nframes) {
     const size_t lds = (size_t)buf0 + buf1;
     hipFuncSetAttribute((const void*)k_oa_pyr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(k_oa_pyr, dim3(ncells, nframes), dim3(512), lds, st, pyr, pyr_stride, gpitch, cells, imgs, buf0,
+    hipLaunchKernelGGL(k_oa_pyr, dim3(ncells, nframes), dim3(1024), lds, st, pyr, pyr_stride, gpitch, cells, imgs, buf0,
                        cpyr, cp_stride);
 }
 
+size_t oa_scand_lds_bytes(int maxpitch) { return (size_t)(AD_BH + 8) * maxpitch + (size_t)(AD_BH + 2) * maxpitch; }
+
 void launch_oa_scand(hipStream_t st, const uint8_t* cpyr, size_t cp_stride, const OaImg* imgs, int nimgs,
                      const OaBand* bands, int nbands, uint32_t* cand, size_t cand_stride, int* band_cnt, int* hist,
-                     int nframes) {
-    hipLaunchKernelGGL(k_oa_scand, dim3(nbands, nframes), dim3(256), 0, st, cpyr, cp_stride, imgs, bands, nimgs, cand,
-                       cand_stride, band_cnt, nbands, hist);
+                     int maxpitch, int nframes) {
+    hipLaunchKernelGGL(k_oa_scand, dim3(nbands, nframes), dim3(256), oa_scand_lds_bytes(maxpitch), st, cpyr,
+                       cp_stride, imgs, bands, nimgs, cand, cand_stride, band_cnt, nbands, hist, maxpitch);
 }
 
 void launch_oa_count(hipStream_t st, const int* hist, const OaCell* cells, const OaImg* imgs, int nimgs, int ncells,
@@ -622,7 +725,7 @@ void launch_oa_finalize(hipStream_t st, const uint8_t* pyr, const uint8_t* blur,
                         const uint16_t* depth, size_t depth_stride, int img_w, FrameCalib cal, orb_kp* kps,
                         uint8_t* desc, float* kun, float* xyz, float* ur, int kp_cap, int nframes) {
     dim3 g((kp_cap + OF_KPB - 1) / OF_KPB, nframes);
-    hipLaunchKernelGGL(k_oa_finalize, g, dim3(256), 0, st, pyr, blur, pyr_stride, lv, cpyr, cp_stride, imgs, cells, sc,
+    hipLaunchKernelGGL(k_oa_finalize, g, dim3(64 * OF_NW), 0, st, pyr, blur, pyr_stride, lv, cpyr, cp_stride, imgs, cells, sc,
                        akp, akp_stride, nkp, kps, desc, kp_cap);
     launch_kp_geometry(st, kps, nkp, depth, depth_stride, img_w, cal, kun, xyz, ur, kp_cap, nframes);
 }

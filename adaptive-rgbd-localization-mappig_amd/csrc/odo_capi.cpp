@@ -277,7 +277,7 @@ struct odo_ctx {
     OaCell* oac = nullptr;
     OaBand* oab = nullptr;
     OaScales osc{};
-    int oa_ncap = 0, oa_buf0 = 0, oa_buf1 = 0;
+    int oa_ncap = 0, oa_buf0 = 0, oa_buf1 = 0, oa_maxpitch = 16;
     size_t cp_stride = 0, ocand_stride = 0, oscr_stride = 0;
     uint8_t *cpyr = nullptr, *oscr = nullptr;
     uint32_t* ocand = nullptr;
@@ -427,6 +427,7 @@ static int build_adaptive_orb_geometry(odo_ctx* c) {
             if (I.w > 1024 || I.h > 1024) return fail(ODO_ERR_ARG, "ADAPTIVE ORB: cell wider than 1024");
             if (I.w < 1 || I.h < 1) return fail(ODO_ERR_ARG, "ADAPTIVE ORB: empty cell level");
             I.pitch = (I.w + 15) & ~15;
+            c->oa_maxpitch = std::max(c->oa_maxpitch, I.pitch);
             I.off = off;
             off += I.pitch * I.h;
             I.quota = quota[l];
@@ -456,6 +457,7 @@ static int build_adaptive_orb_geometry(odo_ctx* c) {
     c->oa_buf1 = buf1;
     if ((size_t)buf0 + buf1 + 32 * 1024 > 160 * 1024) return fail(ODO_ERR_ARG, "ADAPTIVE ORB: cell pyramid exceeds LDS");
     c->oscr_stride = (oa_select_scratch_bytes(c->oa_ncap) + 255) & ~(size_t)255;
+    if (oa_scand_lds_bytes(c->oa_maxpitch) > 64 * 1024) return fail(ODO_ERR_ARG, "ADAPTIVE ORB: cell too wide for the S band");
     if (oa_assemble_lds_bytes(c->ad_ncells, c->ad_mpc) > 160 * 1024)
         return fail(ODO_ERR_ARG, "ADAPTIVE ORB grid keeps too many keypoints for one workgroup");
     if (c->ad_ncells > 15) return fail(ODO_ERR_ARG, "ADAPTIVE ORB: more than 15 grid cells");
@@ -1104,7 +1106,7 @@ static int run_extract_adaptive_orb(odo_ctx* c, int set, const uint8_t* d_bgr, c
     HIPCHK(hipMemsetAsync(c->ohist, 0, (size_t)n * ni * 256 * sizeof(int), st));
     if (nb > 0)
         launch_oa_scand(st, c->cpyr, c->cp_stride, c->oai, ni, c->oab, nb, c->ocand, c->ocand_stride, c->oband_cnt,
-                        c->ohist, n);
+                        c->ohist, c->oa_maxpitch, n);
     launch_oa_count(st, c->ohist, c->oac, c->oai, ni, nc, c->ophist, n);
     tmark(c, 2, st);
     launch_adapt_chain(st, c->ophist, nc, n, c->cfg.adaptive, c->athresh, c->atsel, c->ansel);

@@ -253,9 +253,10 @@ void launch_adapt_finalize(hipStream_t st, const uint8_t* blur, size_t pyr_strid
 void upload_adaptive_orb_constants();
 void launch_oa_pyr(hipStream_t st, const uint8_t* pyr, size_t pyr_stride, int gpitch, const OaCell* cells, int ncells,
                    const OaImg* imgs, int buf0, int buf1, uint8_t* cpyr, size_t cp_stride, int nframes);
+size_t oa_scand_lds_bytes(int maxpitch);
 void launch_oa_scand(hipStream_t st, const uint8_t* cpyr, size_t cp_stride, const OaImg* imgs, int nimgs,
                      const OaBand* bands, int nbands, uint32_t* cand, size_t cand_stride, int* band_cnt, int* hist,
-                     int nframes);
+                     int maxpitch, int nframes);
 void launch_oa_count(hipStream_t st, const int* hist, const OaCell* cells, const OaImg* imgs, int nimgs, int ncells,
                      int* phist, int nframes);
 size_t oa_select_scratch_bytes(int ncap);
