@@ -404,8 +404,16 @@ __global__ void __launch_bounds__(OT_THREADS) k_octree(const uint32_t* __restric
                                                        uint32_t* __restrict__ okp, int* __restrict__ ocnt, int okp_stride,
                                                        int node_cap) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int f = blockIdx.y;
-    const int l = blockIdx.x;
+    // ODO_OCTREE_LPT=1: grid (frames, levels), so every frame's level 0 (the
+    // longest workgroups) is dispatched first (longest-first): 129 vs 190-206
+    // us alone, but the step is slower (110.8 k vs 113.5 k frames/s, two A/B
+    // runs each, profiles/r02_octree_ab/): the 256 level-0 workgroups at once
+    // crowd out the co-running pair stages. Default: grid (levels, frames).
+#ifndef ODO_OCTREE_LPT
+#define ODO_OCTREE_LPT 0
+#endif
+    const int f = ODO_OCTREE_LPT ? blockIdx.x : blockIdx.y;
+    const int l = ODO_OCTREE_LPT ? blockIdx.y : blockIdx.x;
     const int t = threadIdx.x;
     const LevelDesc L = lv[l];
     // carve LDS
@@ -999,7 +1007,7 @@ size_t octree_lds_bytes(int node_cap) { return (size_t)76 * node_cap + 1032; }
 void launch_octree(hipStream_t st, const uint32_t* cand, const int* cand_cnt, const LevelDesc* lv, int ncells,
                    int cell_cap, int nlevels, uint32_t* keys, int32_t* knode, uint8_t* kquad, size_t keys_stride,
                    uint32_t* okp, int* ocnt, int okp_stride, int node_cap, int nframes) {
-    dim3 g(nlevels, nframes);
+    const dim3 g = ODO_OCTREE_LPT ? dim3(nframes, nlevels) : dim3(nlevels, nframes);
     hipLaunchKernelGGL(k_octree, g, dim3(OT_THREADS), octree_lds_bytes(node_cap), st, cand, cand_cnt, lv, ncells,
                        cell_cap, nlevels, keys, knode, kquad, keys_stride, okp, ocnt, okp_stride, node_cap);
 }

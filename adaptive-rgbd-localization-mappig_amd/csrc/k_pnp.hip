@@ -356,7 +356,8 @@ ODO_INLINE void huber_rho(double delta, double chi, double rho[3]) {
 // fixed xor-butterfly (deterministic).
 #define PNP_NW 4
 #define PNP_NT (64 * PNP_NW)
-#define PNP_K 4  // Levenberg trials evaluated per edge pass
+#define PNP_K 4  // Levenberg trials evaluated per edge pass (one per 16-lane group of wave 0)
+static_assert(PNP_K <= 4, "the trial solves run on the four 16-lane groups of one wave");
 
 // Sum of NV per-lane doubles over the workgroup, the result in every lane.
 // Per wave a transposing xor-butterfly: at offset o the lane pair splits the
@@ -643,11 +644,18 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                     }
                 }
                 PP_T0();
-                if (wave < K) {
+                // the K trial solves on wave 0's four 16-lane groups (group g =
+                // trial g): the same per-lane arithmetic as one wave per trial,
+                // a quarter of the issued FP64 instructions
+#ifndef ODO_PNP_GROUP_TRIALS
+#define ODO_PNP_GROUP_TRIALS 1  // 0: one wave per trial (A/B)
+#endif
+                const int tg = ODO_PNP_GROUP_TRIALS ? wlane >> 4 : wave;
+                if ((ODO_PNP_GROUP_TRIALS ? wave == 0 : true) && tg < K) {
                     double lw = lam[0];
 #pragma unroll
                     for (int k = 1; k < PNP_K; k++)
-                        if (wave == k) lw = lam[k];
+                        if (tg == k) lw = lam[k];
                     double Hl[6][6], b[6];
                     {
                         int h = 0;
@@ -669,16 +677,16 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                     double scale = 0;
                     for (int j = 0; j < 6; j++) scale += x[j] * (lw * x[j] + b[j]);
                     scale += 1e-3;
-                    if (wlane == 0) {
-                        s_T[wave][0] = Tk.q.x;
-                        s_T[wave][1] = Tk.q.y;
-                        s_T[wave][2] = Tk.q.z;
-                        s_T[wave][3] = Tk.q.w;
-                        s_T[wave][4] = Tk.t[0];
-                        s_T[wave][5] = Tk.t[1];
-                        s_T[wave][6] = Tk.t[2];
-                        s_T[wave][7] = scale;
-                        s_ok[wave] = ok2 ? 1 : 0;
+                    if ((wlane & (ODO_PNP_GROUP_TRIALS ? 15 : 63)) == 0) {
+                        s_T[tg][0] = Tk.q.x;
+                        s_T[tg][1] = Tk.q.y;
+                        s_T[tg][2] = Tk.q.z;
+                        s_T[tg][3] = Tk.q.w;
+                        s_T[tg][4] = Tk.t[0];
+                        s_T[tg][5] = Tk.t[1];
+                        s_T[tg][6] = Tk.t[2];
+                        s_T[tg][7] = scale;
+                        s_ok[tg] = ok2 ? 1 : 0;
                     }
                 }
                 __syncthreads();
