@@ -119,22 +119,15 @@ __global__ void __launch_bounds__(256) k_resize(uint8_t* __restrict__ pyr, size_
 __constant__ int c_circle_dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
 __constant__ int c_circle_dy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
 
-ODO_INLINE bool has_run9(uint32_t m16) {
-    uint32_t x = m16 | (m16 << 16);
-    uint32_t a = x & (x >> 1);
-    uint32_t b = a & (a >> 2);
-    uint32_t c = b & (b >> 4);
-    return (c & (x >> 8)) != 0;
-}
-
 // One wave (64 lanes) per cell ROI. Candidates packed as (resp<<24)|(y<<12)|x
 // with x,y relative to the 16px border (vToDistributeKeys coordinates),
 // emitted in row-major order within the cell. Per threshold attempt:
 //   1. compass pre-filter over the detection region (pixels 0/4/8/12 of the
 //      circle: any 9-arc holds two adjacent compass points of its sign, so this
 //      is a necessary condition), survivors queued in row-major order,
-//   2. the full 16-pixel test + cornerScore on the queue, corners listed in
-//      order with their scores in an LDS map (0 elsewhere),
+//   2. the 16-pixel test and cornerScore in one pass on the queue (corner iff
+//      the threshold-free S exceeds th), corners listed in order with their
+//      scores in an LDS map (0 elsewhere),
 //   3. NMS (strictly greater than the 8 neighbours) over the corner list.
 template <int ROI_MAX>
 __global__ void __launch_bounds__(64) k_fast_cells(const uint8_t* __restrict__ pyr, size_t pyr_stride,
@@ -231,8 +224,9 @@ __global__ void __launch_bounds__(64) k_fast_cells(const uint8_t* __restrict__ p
                     const uint32_t b8 = *reinterpret_cast<uint32_t*>(&t);
                     t = vp - a12;
                     const uint32_t b12 = *reinterpret_cast<uint32_t*>(&t);
-                    const uint32_t pm = ((d0 & d4) | (d4 & d8) | (d8 & d12) | (d12 & d0) | (b0 & b4) | (b4 & b8) |
-                                         (b8 & b12) | (b12 & b0)) & 0x80008000u;
+                    // two adjacent compass points of one sign: (d0&d4)|(d4&d8)|(d8&d12)|(d12&d0)
+                    // = (d0|d8)&(d4|d12), on the sign bits
+                    const uint32_t pm = (((d0 | d8) & (d4 | d12)) | ((b0 | b8) & (b4 | b12))) & 0x80008000u;
                     pass4 |= ((pm >> 15) & 1u) << (2 * h);
                     pass4 |= (pm >> 31) << (2 * h + 1);
                 }
@@ -258,36 +252,21 @@ __global__ void __launch_bounds__(64) k_fast_cells(const uint8_t* __restrict__ p
             for (int i = 0; i < 4; i++) n1 += __popcll(bi[i]);
         }
         __syncthreads();
-        // 2a. full segment test on the survivors; corners listed in order
+        // 2. segment test + cornerScore<16> of the survivors, two per lane in
+        //    packed 16-bit lanes: d = v - p, S = max(best 9-arc min of d,
+        //    -(best 9-arc max)). p is a corner at th iff S > th (a 9-arc whose
+        //    every d lies beyond th), and its cornerScore is max(th, S) - 1 =
+        //    S - 1 (the segment test and the score were two passes until round 2).
+        //    Corners listed in order, in place over the survivor queue (every
+        //    lane reads its two entries before any lane writes).
         int n2 = 0;
-        for (int base = 0; base < n1; base += 64) {
-            const int idx = base + lane;
-            bool corner = false;
-            int o = 0;
-            if (idx < n1) {
-                o = q1[idx];
-                const int v = roi[o];
-                uint32_t dark = 0, bright = 0;
-#pragma unroll
-                for (int k = 0; k < 16; k++) {
-                    const int px = roi[o + c_circle_dy[k] * RS + c_circle_dx[k]];
-                    dark |= (uint32_t)(px < v - thc) << k;
-                    bright |= (uint32_t)(px > v + thc) << k;
-                }
-                corner = has_run9(dark) || has_run9(bright);
-            }
-            const uint64_t bal = __ballot(corner);
-            if (corner) q2[n2 + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0))] = (uint16_t)o;
-            n2 += __popcll(bal);
-        }
-        __syncthreads();
-        // 2b. cornerScore<16> of the corners, two per lane in packed 16-bit
-        //     lanes: d = v - p, S = max(best 9-arc min of d, -(best 9-arc max));
-        //     a corner at th has S > th, so cornerScore = max(th, S) - 1 = S - 1
-        for (int base = 0; base < n2; base += 128) {
+        for (int base = 0; base < n1; base += 128) {
             const int i0 = base + 2 * lane, i1 = i0 + 1;
-            if (i0 < n2) {
-                const int o0 = q2[i0], o1 = i1 < n2 ? q2[i1] : o0;
+            bool c0 = false, c1 = false;
+            int o0 = 0, o1 = 0;
+            if (i0 < n1) {
+                o0 = q1[i0];
+                o1 = i1 < n1 ? q1[i1] : o0;
                 const int v0 = roi[o0], v1 = roi[o1];
                 s16x2 d[16];
 #pragma unroll
@@ -321,9 +300,17 @@ __global__ void __launch_bounds__(64) k_fast_cells(const uint8_t* __restrict__ p
                         br, __builtin_elementwise_max(x8, __builtin_elementwise_min(d[k], d[(k + 9) & 15])));
                 }
                 const s16x2 sc = __builtin_elementwise_max(dk, -br);
-                score[o0] = (uint8_t)(sc.x - 1);
-                if (i1 < n2) score[o1] = (uint8_t)(sc.y - 1);
+                c0 = sc.x > thc;
+                c1 = i1 < n1 && sc.y > thc;
+                if (c0) score[o0] = (uint8_t)(sc.x - 1);
+                if (c1) score[o1] = (uint8_t)(sc.y - 1);
             }
+            const uint64_t b0 = __ballot(c0), b1 = __ballot(c1);
+            const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b0, 0)) +
+                            (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b1, 0));
+            if (c0) q2[n2 + pre] = (uint16_t)o0;
+            if (c1) q2[n2 + pre + (c0 ? 1 : 0)] = (uint16_t)o1;
+            n2 += __popcll(b0) + __popcll(b1);
         }
         __syncthreads();
         // 3. NMS over the corner list (row-major), ordered compaction
