@@ -818,9 +818,11 @@ __global__ void __launch_bounds__(OT_THREADS) k_octree(const uint32_t* __restric
 // a flattened (level, tile) grid. The 136x38 input window (x from tx0-4) is
 // staged in LDS with aligned dword loads (rows are pitch-aligned; reflection
 // only on border tiles). Horizontal pass: 4 outputs from three LDS dwords,
-// two byte-aligned windows and two v_dot4_u32_u8 each. Vertical pass: 4x4
-// outputs per thread, row pairs packed with v_perm and summed with
-// v_dot2_u32_u16, one aligned dword store per output row.
+// two byte-aligned windows and two v_dot4_u32_u8 each, two rows per item,
+// stored as (row 2i, row 2i+1) u16 pairs per column. Vertical pass: 4x4
+// outputs per thread, odd row pairs formed with one v_perm, summed with
+// v_dot2_u32_u16 (the rounding term as the first accumulator), output bytes
+// gathered with v_perm, one aligned dword store per output row.
 #define BLUR_TX 128
 #define BLUR_TY 32
 #define BLUR_IW (BLUR_TX + 8)  // staged row stride: x in [tx0-4, tx0+132)
@@ -847,7 +849,7 @@ __global__ void __launch_bounds__(256) k_blur(const uint8_t* __restrict__ pyr, u
                                               size_t pyr_stride, const LevelDesc* __restrict__ lv, BlurTiles TT,
                                               int nlevels) {
     __shared__ __attribute__((aligned(16))) uint8_t tile[BLUR_IH * BLUR_IW];
-    __shared__ __attribute__((aligned(16))) uint16_t hrow[BLUR_IH * BLUR_TX];
+    __shared__ __attribute__((aligned(16))) uint32_t hrow[(BLUR_IH / 2) * BLUR_TX];
     const int f = blockIdx.y;
     const int tid = blockIdx.x;
     int l = 0;
@@ -886,56 +888,74 @@ __global__ void __launch_bounds__(256) k_blur(const uint8_t* __restrict__ pyr, u
         }
     }
     __syncthreads();
-    // horizontal: row r, outputs 4q+o take staged bytes 4q+1+o .. 4q+7+o
+    // horizontal: row r, outputs 4q+o take staged bytes 4q+1+o .. 4q+7+o. An
+    // item is two rows (2rp, 2rp+1) x 4 columns; hrow holds per (row pair,
+    // column) the dword (h[2rp], h[2rp+1]), the vertical pass's even row pairs
     constexpr uint32_t C0 = 18u | (34u << 8) | (48u << 16) | (56u << 24);
     constexpr uint32_t C1 = 48u | (34u << 8) | (18u << 16);
-    for (int it = t; it < BLUR_IH * (BLUR_TX / 4); it += 256) {
-        const int r = it / (BLUR_TX / 4), q = it % (BLUR_TX / 4);
-        const uint32_t* w = reinterpret_cast<const uint32_t*>(&tile[r * BLUR_IW + 4 * q]);
-        const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
-        uint32_t h[4];
-        h[0] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 1), C1,
-                                      __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 1), C0, 0u, false),
-                                      false);
-        h[1] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 2), C1,
-                                      __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 2), C0, 0u, false),
-                                      false);
-        h[2] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 3), C1,
-                                      __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 3), C0, 0u, false),
-                                      false);
-        h[3] = __builtin_amdgcn_udot4(w2, C1, __builtin_amdgcn_udot4(w1, C0, 0u, false), false);
-        uint2 pk;
-        pk.x = h[0] | (h[1] << 16);
-        pk.y = h[2] | (h[3] << 16);
-        *reinterpret_cast<uint2*>(&hrow[r * BLUR_TX + 4 * q]) = pk;
+    for (int it = t; it < (BLUR_IH / 2) * (BLUR_TX / 4); it += 256) {
+        const int rp = it / (BLUR_TX / 4), q = it % (BLUR_TX / 4);
+        uint32_t h[2][4];
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(&tile[(2 * rp + e) * BLUR_IW + 4 * q]);
+            const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+            h[e][0] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 1), C1,
+                                             __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 1), C0, 0u, false),
+                                             false);
+            h[e][1] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 2), C1,
+                                             __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 2), C0, 0u, false),
+                                             false);
+            h[e][2] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 3), C1,
+                                             __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 3), C0, 0u, false),
+                                             false);
+            h[e][3] = __builtin_amdgcn_udot4(w2, C1, __builtin_amdgcn_udot4(w1, C0, 0u, false), false);
+        }
+        uint4 pk;
+        pk.x = h[0][0] | (h[1][0] << 16);
+        pk.y = h[0][1] | (h[1][1] << 16);
+        pk.z = h[0][2] | (h[1][2] << 16);
+        pk.w = h[0][3] | (h[1][3] << 16);
+        *reinterpret_cast<uint4*>(&hrow[rp * BLUR_TX + 4 * q]) = pk;
     }
     __syncthreads();
     // vertical: 4 columns x 4 rows per thread
     {
         const int q = t % (BLUR_TX / 4), rb = (t / (BLUR_TX / 4)) * 4;  // 32 x 8 threads
-        uint2 pk[10];
+        uint4 pk[5];  // row pairs (rb + 2i, rb + 2i + 1), columns 4q .. 4q+3
 #pragma unroll
-        for (int j = 0; j < 10; j++) pk[j] = *reinterpret_cast<const uint2*>(&hrow[(rb + j) * BLUR_TX + 4 * q]);
+        for (int i = 0; i < 5; i++) pk[i] = *reinterpret_cast<const uint4*>(&hrow[(rb / 2 + i) * BLUR_TX + 4 * q]);
         constexpr uint32_t K01 = 18u | (34u << 16), K23 = 48u | (56u << 16), K45 = 48u | (34u << 16), K6 = 18u;
-        uint32_t out[4] = {0u, 0u, 0u, 0u};
+        // sums start at the rounding term 32768: (S + 32768) >> 16 is then byte 2
+        // of the sum (S < 2^24), gathered four columns at a time with v_perm
+        uint32_t sum4[4][4];  // [output row][column]
 #pragma unroll
         for (int cI = 0; cI < 4; cI++) {
-            // P[j] = (row j, row j+1) of column cI; P[9] carries row 9 alone (its pair weight is 0)
+            uint32_t E[5];
+#pragma unroll
+            for (int i = 0; i < 5; i++) E[i] = cI == 0 ? pk[i].x : cI == 1 ? pk[i].y : cI == 2 ? pk[i].z : pk[i].w;
+            // P[j] = (row j, row j+1): even j straight from hrow, odd j = (high
+            // half of pair j-1, low half of pair j+1); P[9] = row 9 alone
             uint32_t P[10];
 #pragma unroll
-            for (int j = 0; j < 9; j++) {
-                const uint32_t lo = (cI < 2) ? pk[j].x : pk[j].y, hi = (cI < 2) ? pk[j + 1].x : pk[j + 1].y;
-                P[j] = __builtin_amdgcn_perm(hi, lo, (cI & 1) ? 0x07060302u : 0x05040100u);
-            }
-            P[9] = (cI & 1) ? (((cI < 2) ? pk[9].x : pk[9].y) >> 16) : ((cI < 2) ? pk[9].x : pk[9].y);
+            for (int j = 0; j < 9; j++)
+                P[j] = (j & 1) ? __builtin_amdgcn_perm(E[(j + 1) / 2], E[(j - 1) / 2], 0x05040302u) : E[j / 2];
+            P[9] = E[4] >> 16;
 #pragma unroll
             for (int o = 0; o < 4; o++) {
-                uint32_t sum = dot2u16(P[o], K01, 0u);
+                uint32_t sum = dot2u16(P[o], K01, 32768u);
                 sum = dot2u16(P[o + 2], K23, sum);
                 sum = dot2u16(P[o + 4], K45, sum);
-                sum = dot2u16(P[o + 6], K6, sum);
-                out[o] |= ((sum + 32768u) >> 16) << (8 * cI);
+                sum4[o][cI] = dot2u16(P[o + 6], K6, sum);
             }
+        }
+        uint32_t out[4];
+#pragma unroll
+        for (int o = 0; o < 4; o++) {
+            // bytes 2 of columns (0, 1) and (2, 3) into the low / high halves
+            const uint32_t lo = __builtin_amdgcn_perm(sum4[o][1], sum4[o][0], 0x0c0c0602u);
+            const uint32_t hi = __builtin_amdgcn_perm(sum4[o][3], sum4[o][2], 0x06020c0cu);
+            out[o] = lo | hi;
         }
         const int x = tx0 + 4 * q;
         if (x < L.w) {
