@@ -1,7 +1,7 @@
 # Round-end evidence: GPU tests, the default bench line (all legs), the
 # rocprofv3 kernel stats of the same bench command, and smoke().
 set -e
-R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/final; mkdir -p $O
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/${1:-final}; mkdir -p $O
 cd $R
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
 echo pytest ok
