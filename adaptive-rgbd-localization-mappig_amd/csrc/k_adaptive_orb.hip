@@ -46,6 +46,10 @@ namespace odo {
 // (pitched rows, zero padding). Resize tables are made in LDS with the
 // generic-path rules of App. A.2 (the host rules of odo_capi.cpp
 // build_geometry).
+// LDS = false (cells too large for the two LDS level buffers, e.g. 1280x960
+// frames): every level reads its source level back from the cell-pyramid
+// buffer the same workgroup wrote (L2), through the same code.
+template <bool LDS>
 __global__ void __launch_bounds__(1024) k_oa_pyr(const uint8_t* __restrict__ pyr, size_t pyr_stride, int gpitch,
                                                 const OaCell* __restrict__ cells, const OaImg* __restrict__ imgs,
                                                 int buf0, uint8_t* __restrict__ cpyr, size_t cp_stride) {
@@ -70,13 +74,13 @@ __global__ void __launch_bounds__(1024) k_oa_pyr(const uint8_t* __restrict__ pyr
             uint32_t v = __builtin_amdgcn_alignbyte(row[1], row[0], sh);
             const int valid = I.w - 4 * q;  // bytes of this dword inside the cell
             if (valid < 4) v = valid <= 0 ? 0u : v & ((1u << (8 * valid)) - 1u);
-            reinterpret_cast<uint32_t*>(buf[0])[i] = v;
+            if (LDS) reinterpret_cast<uint32_t*>(buf[0])[i] = v;
             reinterpret_cast<uint32_t*>(out + I.off)[i] = v;
         }
     }
     for (int l = 1; l < OA_NLEV; l++) {
         const OaImg S = imgs[C.img0 + l - 1], D = imgs[C.img0 + l];
-        const uint8_t* src = buf[(l - 1) & 1];
+        const uint8_t* src = LDS ? buf[(l - 1) & 1] : out + S.off;
         uint8_t* dst = buf[l & 1];
         const double scale_x = 1. / ((double)D.w / S.w), scale_y = 1. / ((double)D.h / S.h);
         for (int dx = threadIdx.x; dx < D.w; dx += blockDim.x) {
@@ -131,7 +135,7 @@ __global__ void __launch_bounds__(1024) k_oa_pyr(const uint8_t* __restrict__ pyr
                     packed |= (uint32_t)v << (8 * j);
                 }
             }
-            reinterpret_cast<uint32_t*>(dst)[i] = packed;
+            if (LDS) reinterpret_cast<uint32_t*>(dst)[i] = packed;
             reinterpret_cast<uint32_t*>(out + D.off)[i] = packed;
         }
         __syncthreads();
@@ -677,9 +681,14 @@ void upload_adaptive_orb_constants() {
 void launch_oa_pyr(hipStream_t st, const uint8_t* pyr, size_t pyr_stride, int gpitch, const OaCell* cells, int ncells,
                    const OaImg* imgs, int buf0, int buf1, uint8_t* cpyr, size_t cp_stride, int nframes) {
     const size_t lds = (size_t)buf0 + buf1;
-    hipFuncSetAttribute((const void*)k_oa_pyr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(k_oa_pyr, dim3(ncells, nframes), dim3(1024), lds, st, pyr, pyr_stride, gpitch, cells, imgs, buf0,
-                       cpyr, cp_stride);
+    if (lds + 32 * 1024 <= 160 * 1024) {
+        hipFuncSetAttribute((const void*)k_oa_pyr<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(k_oa_pyr<true>, dim3(ncells, nframes), dim3(1024), lds, st, pyr, pyr_stride, gpitch, cells,
+                           imgs, buf0, cpyr, cp_stride);
+    } else {
+        hipLaunchKernelGGL(k_oa_pyr<false>, dim3(ncells, nframes), dim3(1024), 0, st, pyr, pyr_stride, gpitch, cells,
+                           imgs, 0, cpyr, cp_stride);
+    }
 }
 
 size_t oa_scand_lds_bytes(int maxpitch) { return (size_t)(AD_BH + 8) * maxpitch + (size_t)(AD_BH + 2) * maxpitch; }

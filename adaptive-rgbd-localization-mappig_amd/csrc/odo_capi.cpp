@@ -455,7 +455,6 @@ static int build_adaptive_orb_geometry(odo_ctx* c) {
     c->ocand_stride = (size_t)std::max(coff, 4);
     c->oa_buf0 = buf0;
     c->oa_buf1 = buf1;
-    if ((size_t)buf0 + buf1 + 32 * 1024 > 160 * 1024) return fail(ODO_ERR_ARG, "ADAPTIVE ORB: cell pyramid exceeds LDS");
     c->oscr_stride = (oa_select_scratch_bytes(c->oa_ncap) + 255) & ~(size_t)255;
     if (oa_scand_lds_bytes(c->oa_maxpitch) > 64 * 1024) return fail(ODO_ERR_ARG, "ADAPTIVE ORB: cell too wide for the S band");
     if (oa_assemble_lds_bytes(c->ad_ncells, c->ad_mpc) > 160 * 1024)

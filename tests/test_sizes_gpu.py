@@ -41,16 +41,21 @@ def test_gpu_frame_sizes(w, h):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("w,h", [(330, 250), (642, 482)])
-def test_gpu_adaptive_frame_sizes(w, h):
-    """Extractor(FAST, ORB, ADAPTIVE) at other sizes: the 3x3 grid's cells and
-    edge bands follow the image (videogridadaptedfeaturedetector.cpp:62-71)."""
+@pytest.mark.parametrize("w,h,inner", [(330, 250, "fast"), (642, 482, "fast"), (330, 250, "orb"), (642, 482, "orb"),
+                                        (1280, 960, "orb")])
+def test_gpu_adaptive_frame_sizes(w, h, inner):
+    """Extractor(FAST | ORB, ORB, ADAPTIVE) at other sizes: the 3x3 grid's
+    cells and edge bands follow the image (videogridadaptedfeaturedetector.cpp:
+    62-71); with the cv::ORB inner detector every cell level's size follows
+    the cell (odd widths, unaligned cell origins; 1280x960 cells of up to
+    489 x 382 px, too large for the LDS cell pyramid, take its L2 variant)."""
     pkg = load_pkg()
     bgr, dep, _ = sequence(4, w, h, seed=0x5EED0041)
-    cfg = pkg.default_config(w, h, 4, nfeatures=1000, iterations=200, detector=pkg.DETECTOR_ADAPTIVE_FAST)
+    det = pkg.DETECTOR_ADAPTIVE_ORB if inner == "orb" else pkg.DETECTOR_ADAPTIVE_FAST
+    cfg = pkg.default_config(w, h, 4, nfeatures=1000, iterations=200, detector=det)
     odo = pkg.Odometry(cfg)
     cal = O.fr1_calib()
-    ex = O.AdaptiveExtractor()
+    ex = O.AdaptiveExtractor(inner=inner)
     ref = [ex.extract_frame(bgr[i], dep[i], cal) for i in range(4)]
     res = odo.track_batch_host(bgr, dep)
     for i in range(4):
