@@ -209,7 +209,14 @@ __global__ void __launch_bounds__(256, FIN_WAVES_PER_EU) k_finalize(const uint8_
 #define FL_IC_N (31 * FL_IC_W)       // 279
 #define FL_BR_W 10                   // dwords per staged rBRIEF row
 #define FL_BR_N (37 * FL_BR_W)       // 370
-#define FL_KP_DW (FL_IC_N + FL_BR_N)  // dwords of LDS per keypoint
+// FIN_OVERLAY=1: the rBRIEF window overwrites the IC disc once the angle is
+// known (its loads are in flight since the start), so a keypoint holds 370
+// dwords of LDS instead of 649 and more workgroups fit a CU
+#ifndef FIN_OVERLAY
+#define FIN_OVERLAY 1
+#endif
+#define FL_KP_DW (FIN_OVERLAY ? FL_BR_N : FL_IC_N + FL_BR_N)  // dwords of LDS per keypoint
+#define FL_BR_AT (FIN_OVERLAY ? 0 : FL_IC_N)                  // first dword of the rBRIEF window
 template <int NW>  // waves (of 4 keypoints) per workgroup
 __global__ void __launch_bounds__(64 * NW) k_finalize_lds(const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
                                                       size_t pyr_stride, const LevelDesc* __restrict__ lv, int nlevels,
@@ -262,6 +269,7 @@ __global__ void __launch_bounds__(64 * NW) k_finalize_lds(const uint8_t* __restr
     const uint32_t key = valid ? okp[((size_t)f * nlevels + lvl) * okp_stride + k] : (16u | (16u << 12));
     const int kx = (int)(key & 0xfff) + 16, ky = (int)((key >> 12) & 0xfff) + 16;
     const float resp = (float)(key >> 24);
+    uint32_t vbr[24];  // the rBRIEF window's dwords (in flight during the IC angle)
     uint32_t* P = s_patch[kslot];
     const int sh = (kx - 15) & 3, sh2 = (kx - 18) & 3;
     {
@@ -283,9 +291,13 @@ __global__ void __launch_bounds__(64 * NW) k_finalize_lds(const uint8_t* __restr
 #pragma unroll
         for (int j = 0; j < 18; j++)
             if (sub + 16 * j < FL_IC_N) P[sub + 16 * j] = v[j];
+        if (!FIN_OVERLAY) {
 #pragma unroll
-        for (int j = 0; j < 24; j++)
-            if (sub + 16 * j < FL_BR_N) P[FL_IC_N + sub + 16 * j] = v[18 + j];
+            for (int j = 0; j < 24; j++)
+                if (sub + 16 * j < FL_BR_N) P[FL_BR_AT + sub + 16 * j] = v[18 + j];
+        }
+#pragma unroll
+        for (int j = 0; j < 24; j++) vbr[j] = v[18 + j];
     }
     __syncthreads();  // s_disc, the patches
     int m10, m01;
@@ -335,7 +347,14 @@ __global__ void __launch_bounds__(64 * NW) k_finalize_lds(const uint8_t* __restr
     const f32x2 BA = {b, a}, AB = {a, b}, MAG = {RND_MAGIC, RND_MAGIC};
     // staged byte of rotated offset (iy, ix): (iy + 18) * 40 + ix + 18 + sh2; the
     // magic-rounded floats carry RND_BITS + offset in their bits
-    const uint8_t* PB = reinterpret_cast<const uint8_t*>(P + FL_IC_N);
+    if (FIN_OVERLAY) {
+        __syncthreads();  // every IC disc read
+#pragma unroll
+        for (int j = 0; j < 24; j++)
+            if (sub + 16 * j < FL_BR_N) P[sub + 16 * j] = vbr[j];
+        __syncthreads();
+    }
+    const uint8_t* PB = reinterpret_cast<const uint8_t*>(P + FL_BR_AT);
     const uint32_t cofs = (uint32_t)(18 * 4 * FL_BR_W + 18 + sh2) - RND_BITS * (uint32_t)(4 * FL_BR_W + 1);  // mod 2^32
     int tv0[16], tv1[16];
 #pragma unroll
