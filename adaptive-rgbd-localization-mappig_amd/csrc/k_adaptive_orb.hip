@@ -476,7 +476,8 @@ __global__ void __launch_bounds__(256) k_oa_assemble(const uint64_t* __restrict_
 //   the IC disc, rows y-15..y+15 of the keypoint's cell level (always inside:
 //   runByImageBorder(15)), 9 dwords each;
 //   the rBRIEF window, rows cy-18..cy+18 of the frame pyramid's blurred level
-//   around the centre cvRound(pt / scale), 10 dwords each. A window that
+//   around the centre cvRound(pt / scale), 10 dwords each, written over the
+//   disc once the angle is known (its loads in flight meanwhile). A window that
 //   leaves the level is staged byte by byte with computeOrbDescriptors'
 //   border: the unblurred level at the REFLECT_101 position (the bordered
 //   pyramid's border, which the in-place ROI blur leaves untouched).
@@ -499,7 +500,7 @@ typedef float f32x2o __attribute__((ext_vector_type(2)));
 #define OF_IC_N (31 * OF_IC_W)
 #define OF_BR_W 10
 #define OF_BR_N (37 * OF_BR_W)
-#define OF_KP_DW (OF_IC_N + OF_BR_N)
+#define OF_KP_DW OF_BR_N  // the rBRIEF window overlays the IC disc
 #define OF_NW 2
 #define OF_KPB (4 * OF_NW)
 __global__ void __launch_bounds__(64 * OF_NW) k_oa_finalize(const uint8_t* __restrict__ pyr,
@@ -560,30 +561,18 @@ __global__ void __launch_bounds__(64 * OF_NW) k_oa_finalize(const uint8_t* __res
         for (int j = 0; j < 18; j++)
             if (sub + 16 * j < OF_IC_N) P[sub + 16 * j] = v[j];
     }
-    {
-        const uint8_t* bim = blur + (size_t)f * pyr_stride + L.off;
-        if (inside) {
-            const uint8_t* b0 = bim + (size_t)(cy - 18) * L.pitch + (cx - 18 - sh2);
-            uint32_t v[24];
+    // the rBRIEF window overlays the IC disc once the angle is known (the
+    // k_finalize_lds FIN_OVERLAY scheme): its in-level dwords are loaded now and
+    // held in registers, a window past the level edge is staged afterwards
+    const uint8_t* bim = blur + (size_t)f * pyr_stride + L.off;
+    uint32_t vbr[24];
+    if (inside) {
+        const uint8_t* b0 = bim + (size_t)(cy - 18) * L.pitch + (cx - 18 - sh2);
 #pragma unroll
-            for (int j = 0; j < 24; j++) {
-                const int i = min(sub + 16 * j, OF_BR_N - 1);
-                const int r = i / OF_BR_W, c = i - r * OF_BR_W;
-                v[j] = *reinterpret_cast<const uint32_t*>(b0 + (size_t)r * L.pitch + 4 * c);
-            }
-#pragma unroll
-            for (int j = 0; j < 24; j++)
-                if (sub + 16 * j < OF_BR_N) P[OF_IC_N + sub + 16 * j] = v[j];
-        } else {
-            const uint8_t* un = pyr + (size_t)f * pyr_stride + L.off;
-            uint8_t* PB = reinterpret_cast<uint8_t*>(P + OF_IC_N);
-            for (int i = sub; i < 4 * OF_BR_N; i += 16) {
-                const int r = i / (4 * OF_BR_W), c = i - r * (4 * OF_BR_W);
-                const int yy = cy - 18 + r, xx = cx - 18 - sh2 + c;
-                PB[i] = (yy >= 0 && yy < L.h && xx >= 0 && xx < L.w)
-                            ? bim[(size_t)yy * L.pitch + xx]
-                            : un[(size_t)refl101(yy, L.h) * L.pitch + refl101(xx, L.w)];
-            }
+        for (int j = 0; j < 24; j++) {
+            const int i = min(sub + 16 * j, OF_BR_N - 1);
+            const int r = i / OF_BR_W, c = i - r * OF_BR_W;
+            vbr[j] = *reinterpret_cast<const uint32_t*>(b0 + (size_t)r * L.pitch + 4 * c);
         }
     }
     __syncthreads();  // s_disc, the patches
@@ -626,12 +615,29 @@ __global__ void __launch_bounds__(64 * OF_NW) k_oa_finalize(const uint8_t* __res
         m01 += __shfl_xor(m01, off);
     }
     const float angle = fast_atan2((float)m01, (float)m10);
+    __syncthreads();  // every IC disc read
+    if (inside) {
+#pragma unroll
+        for (int j = 0; j < 24; j++)
+            if (sub + 16 * j < OF_BR_N) P[sub + 16 * j] = vbr[j];
+    } else {
+        const uint8_t* un = pyr + (size_t)f * pyr_stride + L.off;
+        uint8_t* PBw = reinterpret_cast<uint8_t*>(P);
+        for (int i = sub; i < 4 * OF_BR_N; i += 16) {
+            const int r = i / (4 * OF_BR_W), c = i - r * (4 * OF_BR_W);
+            const int yy = cy - 18 + r, xx = cx - 18 - sh2 + c;
+            PBw[i] = (yy >= 0 && yy < L.h && xx >= 0 && xx < L.w)
+                         ? bim[(size_t)yy * L.pitch + xx]
+                         : un[(size_t)refl101(yy, L.h) * L.pitch + refl101(xx, L.w)];
+        }
+    }
+    __syncthreads();
     const float ang = angle * (float)(3.14159265358979323846 / 180.f);
     double sd, cd;
     sincos((double)ang, &sd, &cd);
     const float a = (float)cd, b = (float)sd;
     const f32x2o BA = {b, a}, AB = {a, b}, MAG = {OF_RND_MAGIC, OF_RND_MAGIC};
-    const uint8_t* PB = reinterpret_cast<const uint8_t*>(P + OF_IC_N);
+    const uint8_t* PB = reinterpret_cast<const uint8_t*>(P);
     const uint32_t cofs = (uint32_t)(18 * 4 * OF_BR_W + 18 + sh2) - OF_RND_BITS * (uint32_t)(4 * OF_BR_W + 1);
     int tv0[16], tv1[16];
 #pragma unroll
