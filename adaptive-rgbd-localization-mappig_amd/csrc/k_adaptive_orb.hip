@@ -189,32 +189,69 @@ __global__ void __launch_bounds__(256) k_oa_scand(const uint8_t* __restrict__ cp
         reinterpret_cast<uint32_t*>(s)[r * nq + q] = smap4(W);
     }
     __syncthreads();
-    const int npx = rows * cw;
-    const int chunk = (npx + 255) / 256;
-    const int i0 = min(npx, (int)threadIdx.x * chunk), i1 = min(npx, i0 + chunk);
-    const int r0 = cw > 0 ? i0 / cw : 0, q0 = i0 - r0 * cw;
-    auto survivor = [&](int r, int q, int* sv) -> bool {  // band row r, candidate column c0 + q
-        const uint8_t* p = s + (r + 1) * lw + (c0 - OA_X0 + q);
-        const int v = p[0];
-        *sv = v;
-        if (v < 2) return false;
-        int m = max(max(p[-lw - 1], p[-lw]), max(p[-lw + 1], p[-1]));
-        m = max(m, max(max(p[1], p[lw - 1]), max(p[lw], p[lw + 1])));
-        return v > m;
+#ifdef OA_SCAND_NO_NMS  // measurement only (wrong results): the S part alone
+    if (threadIdx.x == 0) band_cnt[(size_t)f * nbands + blockIdx.x] = s[threadIdx.x] & 0;
+    return;
+#endif
+    // NMS four pixels at a time: item (r, k) = the S dword of band row r at
+    // columns OA_X0 + 4k .. +3. The 3x3 neighbourhood max of its four bytes
+    // comes from byte-shifted dwords (v_alignbyte) split into (b0, b2) / (b1,
+    // b3) u16 pairs and packed max; survivors are bytes with S >= 2, S > max,
+    // inside [c0, c1). Contiguous runs of items per thread keep row-major order.
+    const int nitem = rows * nq;
+    const int chunk = (nitem + 255) / 256;
+    const int i0 = min(nitem, (int)threadIdx.x * chunk), i1 = min(nitem, i0 + chunk);
+    const uint32_t* s32 = reinterpret_cast<const uint32_t*>(s);
+    auto lo16 = [](uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x0c020c00u); };  // (b0, b2)
+    auto hi16 = [](uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x0c030c01u); };  // (b1, b3)
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    auto pmax = [](uint32_t x, uint32_t y) -> uint32_t {
+        const u16x2 r = __builtin_elementwise_max(*reinterpret_cast<const u16x2*>(&x), *reinterpret_cast<const u16x2*>(&y));
+        return *reinterpret_cast<const uint32_t*>(&r);
+    };
+    // survivor mask (bit e = byte e) of item (r, k)
+    auto survivors = [&](int r, int k) -> uint32_t {
+        const int km = max(k - 1, 0), kp = min(k + 1, nq - 1);
+        uint32_t L[3], C[3], R[3];
+#pragma unroll
+        for (int d = 0; d < 3; d++) {  // S rows r-1, r, r+1 = LDS rows r .. r+2
+            const uint32_t* row = s32 + (r + d) * nq;
+            const uint32_t a0 = row[km], a1 = row[k], a2 = row[kp];
+            C[d] = a1;
+            L[d] = __builtin_amdgcn_alignbyte(a1, a0, 3);  // bytes x-1 .. x+2
+            R[d] = __builtin_amdgcn_alignbyte(a2, a1, 1);  // bytes x+1 .. x+4
+        }
+        const uint32_t mL = pmax(pmax(lo16(L[0]), lo16(L[2])), pmax(lo16(C[0]), lo16(C[2])));
+        const uint32_t mlo = pmax(pmax(mL, pmax(lo16(R[0]), lo16(R[2]))), pmax(lo16(L[1]), lo16(R[1])));
+        const uint32_t mH = pmax(pmax(hi16(L[0]), hi16(L[2])), pmax(hi16(C[0]), hi16(C[2])));
+        const uint32_t mhi = pmax(pmax(mH, pmax(hi16(R[0]), hi16(R[2]))), pmax(hi16(L[1]), hi16(R[1])));
+        const uint32_t v = C[1];
+        uint32_t m = 0;
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const uint32_t ve = (v >> (8 * e)) & 0xffu;
+            const uint32_t me = ((e & 1 ? mhi : mlo) >> (16 * (e >> 1))) & 0xffffu;
+            const int x = OA_X0 + 4 * k + e;
+            m |= (uint32_t)(ve >= 2u && ve > me && x >= c0 && x < c1) << e;
+        }
+        return m;
     };
     int cnt = 0;
-    uint32_t smask = 0;
+    uint32_t smask = 0;  // 4 bits per item, first 8 items of the run
     {
-        int r = r0, q = q0;
+        int r = i0 / max(nq, 1), k = i0 - r * nq;
         for (int i = i0; i < i1; i++) {
-            int sv;
-            if (survivor(r, q, &sv)) {
-                cnt++;
-                atomicAdd(&sh[sv], 1);
-                if (i - i0 < 32) smask |= 1u << (i - i0);
+            const uint32_t m = survivors(r, k);
+            if (m) {
+                cnt += __popc(m);
+                const uint32_t v = s32[(r + 1) * nq + k];
+#pragma unroll
+                for (int e = 0; e < 4; e++)
+                    if ((m >> e) & 1u) atomicAdd(&sh[(v >> (8 * e)) & 0xffu], 1);
             }
-            if (++q == cw) {
-                q = 0;
+            if (i - i0 < 8) smask |= m << (4 * (i - i0));
+            if (++k == nq) {
+                k = 0;
                 r++;
             }
         }
@@ -224,13 +261,19 @@ __global__ void __launch_bounds__(256) k_oa_scand(const uint8_t* __restrict__ cp
     uint32_t* out = cand + (size_t)f * cand_stride + B.cand_off;
     int o = base.x;
     {
-        int r = r0, q = q0;
+        int r = i0 / max(nq, 1), k = i0 - r * nq;
         for (int i = i0; i < i1; i++) {
-            int sv = s[(r + 1) * lw + (c0 - OA_X0 + q)];
-            const bool keep = (i - i0 < 32) ? ((smask >> (i - i0)) & 1u) != 0 : survivor(r, q, &sv);
-            if (keep) out[o++] = ((uint32_t)sv << 24) | ((uint32_t)(B.y0 + r) << 12) | (uint32_t)(c0 + q);
-            if (++q == cw) {
-                q = 0;
+            const uint32_t m = (i - i0 < 8) ? (smask >> (4 * (i - i0))) & 0xfu : survivors(r, k);
+            if (m) {
+                const uint32_t v = s32[(r + 1) * nq + k];
+#pragma unroll
+                for (int e = 0; e < 4; e++)
+                    if ((m >> e) & 1u)
+                        out[o++] = (((v >> (8 * e)) & 0xffu) << 24) | ((uint32_t)(B.y0 + r) << 12) |
+                                   (uint32_t)(OA_X0 + 4 * k + e);
+            }
+            if (++k == nq) {
+                k = 0;
                 r++;
             }
         }
