@@ -159,7 +159,7 @@ __global__ void __launch_bounds__(256) k_oa_scand(const uint8_t* __restrict__ cp
     // dynamic LDS sized for the widest cell level (maxpitch): the image rows,
     // then the S rows
     extern __shared__ __attribute__((aligned(16))) uint32_t img_l[];
-    uint8_t* s = reinterpret_cast<uint8_t*>(img_l + (AD_BH + 8) * (maxpitch >> 2));
+    uint8_t* s = reinterpret_cast<uint8_t*>(img_l + (OA_BH + 8) * (maxpitch >> 2));
     __shared__ int sh[256];
     __shared__ int ws[16];
     const int f = blockIdx.y;
@@ -740,12 +740,15 @@ void launch_oa_pyr(hipStream_t st, const uint8_t* pyr, size_t pyr_stride, int gp
     }
 }
 
-size_t oa_scand_lds_bytes(int maxpitch) { return (size_t)(AD_BH + 8) * maxpitch + (size_t)(AD_BH + 2) * maxpitch; }
+size_t oa_scand_lds_bytes(int maxpitch) { return (size_t)(OA_BH + 8) * maxpitch + (size_t)(OA_BH + 2) * maxpitch; }
 
 void launch_oa_scand(hipStream_t st, const uint8_t* cpyr, size_t cp_stride, const OaImg* imgs, int nimgs,
                      const OaBand* bands, int nbands, uint32_t* cand, size_t cand_stride, int* band_cnt, int* hist,
                      int maxpitch, int nframes) {
-    hipLaunchKernelGGL(k_oa_scand, dim3(nbands, nframes), dim3(256), oa_scand_lds_bytes(maxpitch), st, cpyr,
+    const size_t lds = oa_scand_lds_bytes(maxpitch);
+    if (lds > 64 * 1024)
+        hipFuncSetAttribute((const void*)k_oa_scand, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_oa_scand, dim3(nbands, nframes), dim3(256), lds, st, cpyr,
                        cp_stride, imgs, bands, nimgs, cand, cand_stride, band_cnt, nbands, hist, maxpitch);
 }
 

@@ -372,7 +372,7 @@ static void free_ctx(odo_ctx* c) {
 
 // ADAPTIVE with the cv::ORB inner detector: per grid cell the 8 levels of
 // cv::ORB's pyramid of the cell sub-image (getScale sizes, orb.cpp), their
-// candidate bands (rows [15, h-15) in AD_BH-row bands; strict 3x3 maxima are
+// candidate bands (rows [15, h-15) in OA_BH-row bands; strict 3x3 maxima are
 // never 8-adjacent: <= ceil(r/2)ceil(c/2) survivors); the frame
 // pyramid (pyr / blur, built by build_geometry) must have cv::ORB's level
 // sizes, since cv::ORB::compute samples it.
@@ -437,8 +437,8 @@ static int build_adaptive_orb_geometry(odo_ctx* c) {
             I.cand_cap = 0;
             const int cw = I.w - 2 * OA_EDGE;
             if (cw > 0)
-                for (int y0 = OA_EDGE; y0 < I.h - OA_EDGE; y0 += AD_BH) {
-                    OaBand B{img, y0, std::min(y0 + AD_BH, I.h - OA_EDGE), coff};
+                for (int y0 = OA_EDGE; y0 < I.h - OA_EDGE; y0 += OA_BH) {
+                    OaBand B{img, y0, std::min(y0 + OA_BH, I.h - OA_EDGE), coff};
                     const int cap = ((B.y1 - B.y0 + 1) / 2) * ((cw + 1) / 2);
                     coff += (cap + 3) & ~3;
                     I.cand_cap += cap;
@@ -456,7 +456,7 @@ static int build_adaptive_orb_geometry(odo_ctx* c) {
     c->oa_buf0 = buf0;
     c->oa_buf1 = buf1;
     c->oscr_stride = (oa_select_scratch_bytes(c->oa_ncap) + 255) & ~(size_t)255;
-    if (oa_scand_lds_bytes(c->oa_maxpitch) > 64 * 1024) return fail(ODO_ERR_ARG, "ADAPTIVE ORB: cell too wide for the S band");
+    if (oa_scand_lds_bytes(c->oa_maxpitch) > 160 * 1024) return fail(ODO_ERR_ARG, "ADAPTIVE ORB: cell too wide for the S band");
     if (oa_assemble_lds_bytes(c->ad_ncells, c->ad_mpc) > 160 * 1024)
         return fail(ODO_ERR_ARG, "ADAPTIVE ORB grid keeps too many keypoints for one workgroup");
     if (c->ad_ncells > 15) return fail(ODO_ERR_ARG, "ADAPTIVE ORB: more than 15 grid cells");

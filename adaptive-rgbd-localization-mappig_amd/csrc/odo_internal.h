@@ -121,6 +121,7 @@ struct AdBand {
 #define OA_NLEV 8     // nlevels
 #define OA_EDGE 15    // edgeThreshold (runByImageBorder of each level)
 #define OA_PATCH 31   // patchSize
+#define OA_BH 32      // rows per candidate band of a cell level (k_oa_scand)
 // one pyramid level of one grid cell, inside a frame's cell-pyramid buffer
 struct OaImg {
     int off, w, h, pitch;
