@@ -237,7 +237,7 @@ __global__ void __launch_bounds__(256) k_oa_scand(const uint8_t* __restrict__ cp
         return m;
     };
     int cnt = 0;
-    uint32_t smask = 0;  // 4 bits per item, first 8 items of the run
+    uint64_t smask = 0;  // 4 bits per item, first 16 items of the run
     {
         int r = i0 / max(nq, 1), k = i0 - r * nq;
         for (int i = i0; i < i1; i++) {
@@ -249,7 +249,7 @@ __global__ void __launch_bounds__(256) k_oa_scand(const uint8_t* __restrict__ cp
                 for (int e = 0; e < 4; e++)
                     if ((m >> e) & 1u) atomicAdd(&sh[(v >> (8 * e)) & 0xffu], 1);
             }
-            if (i - i0 < 8) smask |= m << (4 * (i - i0));
+            if (i - i0 < 16) smask |= (uint64_t)m << (4 * (i - i0));
             if (++k == nq) {
                 k = 0;
                 r++;
@@ -263,7 +263,7 @@ __global__ void __launch_bounds__(256) k_oa_scand(const uint8_t* __restrict__ cp
     {
         int r = i0 / max(nq, 1), k = i0 - r * nq;
         for (int i = i0; i < i1; i++) {
-            const uint32_t m = (i - i0 < 8) ? (smask >> (4 * (i - i0))) & 0xfu : survivors(r, k);
+            const uint32_t m = (i - i0 < 16) ? (uint32_t)(smask >> (4 * (i - i0))) & 0xfu : survivors(r, k);
             if (m) {
                 const uint32_t v = s32[(r + 1) * nq + k];
 #pragma unroll

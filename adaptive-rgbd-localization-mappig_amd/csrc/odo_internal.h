@@ -121,7 +121,9 @@ struct AdBand {
 #define OA_NLEV 8     // nlevels
 #define OA_EDGE 15    // edgeThreshold (runByImageBorder of each level)
 #define OA_PATCH 31   // patchSize
-#define OA_BH 32      // rows per candidate band of a cell level (k_oa_scand)
+#ifndef OA_BH
+#define OA_BH 64      // rows per candidate band of a cell level (k_oa_scand; 32: -1 %, profiles/r02_oa_bands_ab)
+#endif
 // one pyramid level of one grid cell, inside a frame's cell-pyramid buffer
 struct OaImg {
     int off, w, h, pitch;
