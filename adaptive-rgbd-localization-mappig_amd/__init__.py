@@ -12,7 +12,7 @@ import ctypes as C
 import numpy as np
 
 from . import _abi
-from ._abi import (DETECTOR_ADAPTIVE_FAST, DETECTOR_ADAPTIVE_ORB, DETECTOR_ORB_SLAM2, AdaptiveParams, Calib, Config, DMatch,
+from ._abi import (DETECTOR_ADAPTIVE_FAST, DETECTOR_ADAPTIVE_ORB, DETECTOR_ORB_SLAM2, AdaptiveParams, Calib, Config, DMatch, PnPRansacResult,
                    DMATCH_DTYPE, KP_DTYPE, OrbParams, PAIR_DTYPE, PairResult, RansacParams, Rng, check, load, ptr)
 
 __all__ = ["Odometry", "HostFrames", "PinnedResults", "default_config", "load", "KP_DTYPE", "DMATCH_DTYPE", "PAIR_DTYPE", "rng_stream",
@@ -270,6 +270,22 @@ class Odometry:
         n = C.c_int(0)
         check(self.lib.odo_debug_select(self.h, ptr(keys), keys.size, nth, mode, ptr(out), C.byref(n)))
         return out, n.value
+
+    def pnp_ransac(self, Xw, uv, calib=None, iterations: int = 500, reproj_err: float = 3.0,
+                   confidence: float = 0.85):
+        """PnPRansac::Compute (pnpransac.cpp:11-51) on the GPU: cv::solvePnPRansac
+        over n landmark observations. Returns (result, inlier mask, per-hypothesis
+        inlier counts)."""
+        Xw = np.ascontiguousarray(Xw, np.float32).reshape(-1, 3)
+        uv = np.ascontiguousarray(uv, np.float32).reshape(-1, 2)
+        n = Xw.shape[0]
+        res = PnPRansacResult()
+        mask = np.zeros(max(n, 1), np.uint8)
+        good = np.zeros(max(iterations, 1), np.int32)
+        cal = calib if calib is not None else self.cfg.calib
+        check(self.lib.odo_pnp_ransac(self.h, ptr(Xw), ptr(uv), n, ptr(cal), iterations, reproj_err, confidence,
+                                      ptr(res), ptr(mask), ptr(good)))
+        return res, mask[:n].astype(bool), good
 
     def timings(self):
         ms = np.zeros(16, np.float32)

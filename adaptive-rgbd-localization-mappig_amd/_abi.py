@@ -36,6 +36,13 @@ class OrbParams(C.Structure):
                 ("ini_th_fast", C.c_int32), ("min_th_fast", C.c_int32)]
 
 
+class PnPRansacResult(C.Structure):
+    """odo_pnp_ransac_result (include/odo_types.h)."""
+    _fields_ = [("rvec", C.c_double * 3), ("tvec", C.c_double * 3), ("model_rvec", C.c_double * 3),
+                ("model_tvec", C.c_double * 3), ("Tcw", C.c_float * 16), ("ok", C.c_int32),
+                ("n_inliers", C.c_int32), ("best_iter", C.c_int32), ("iterations_visited", C.c_int32)]
+
+
 class RansacParams(C.Structure):
     _fields_ = [("iterations", C.c_int32), ("min_inlier_th", C.c_int32), ("max_mahalanobis", C.c_float),
                 ("sample_size", C.c_int32), ("check_depth", C.c_int32)]
@@ -112,6 +119,7 @@ SIGNATURES = {
     "odo_ransac": (C.c_int, [P, P, C.c_int, P, C.c_int, P, C.c_int, P, P, P, P, P, P, P, P]),
     "odo_pnp_motion_ba": (C.c_int, [P, P, P, C.c_int, P, P, P, P, P]),
     "odo_kabsch": (C.c_int, [P, P, C.c_int, P]),
+    "odo_pnp_ransac": (C.c_int, [P, P, P, C.c_int, P, C.c_int, C.c_float, C.c_double, P, P, P]),
     "odo_rng_seed": (None, [P, C.c_uint32]),
     "odo_rng_next": (C.c_int32, [P]),
     "odo_debug_pyramid": (C.c_int, [P, C.c_int, P, C.c_size_t]),

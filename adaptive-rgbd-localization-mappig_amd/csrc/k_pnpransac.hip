@@ -1,0 +1,837 @@
+// PnPRansac::Compute (Odometry/pnpransac.cpp:11-51): cv::solvePnPRansac(v3D,
+// v2D, mK, noDist, r, t, false, 500, 3.0f, 0.85, inliers) on the GPU
+// (SURVEY §8(f) rank 4). OpenCV 3.4's RANSACPointSetRegistrator::run is a
+// sequential loop whose only cross-iteration state is (maxGoodCount, niters);
+// the minimal sets come from cv::RNG independently of the models. So:
+//   k_pr_subsets  one lane draws every hypothesis' 5 distinct indices
+//                 (cv::RNG(-1).uniform(0, n), getSubset's retry rule);
+//   k_pr_epnp     one lane per hypothesis: EPnP on its 5 points (epnp.cpp:
+//                 control points, barycentrics, 12x12 M^T M eigenvectors, the
+//                 three beta approximations + 5 Gauss-Newton steps, best
+//                 reprojection), Rodrigues -> (rvec, tvec) and the rotation
+//                 projectPoints rebuilds from rvec;
+//   k_pr_count    one workgroup per hypothesis: computeError (projectPoints in
+//                 double, stored as float, L2SQR in float) and findInliers
+//                 (err <= 9) for every point -> inlier bytes + count;
+//   k_pr_fold     one lane replays run()'s loop over the counts in order:
+//                 goodCount > max(maxGoodCount, 4) -> best, niters =
+//                 RANSACUpdateNumIters(0.85, outlier ratio, 5, niters);
+//   k_pr_refine   one workgroup: solvePnP(ITERATIVE, extrinsic guess) on the
+//                 best model's inliers = CvLevMarq (20 iterations, FLT_EPSILON)
+//                 over cvProjectPoints2 residuals and Jacobians; J^T J, J^T e
+//                 and |e| reduced in a fixed wave-then-workgroup order.
+// All hypotheses up to `iterations` are evaluated (the fold decides how many
+// were visited), like the Ransac::Iterate kernels. The per-hypothesis math is
+// double precision IEEE +,-,*,/,sqrt in the oracle's operation order
+// (-ffp-contract=off), so the models agree with oracle/pnpransac_ref.cpp up to
+// the device libm's cos/sin/acos.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+
+#include "odo_internal.h"
+
+namespace odo {
+namespace {
+
+constexpr int PR_MODEL_POINTS = 5;
+constexpr int PR_COUNT_THREADS = 256;
+constexpr int PR_REFINE_THREADS = 256;
+
+struct PrK {
+    double fx, fy, cx, cy;
+};
+
+// ------------------------------------------- one-sided Jacobi SVD (double)
+// A (m x n, m >= n, row-major) = U diag(w) V^T, w descending (first maximum
+// first); U m x n, V n x n by columns.
+__device__ void svdj(int m, int n, const double* A, double* w, double* U, double* V) {
+    double a[144], v[144];
+    for (int i = 0; i < m * n; i++) a[i] = A[i];
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) v[i * n + j] = i == j ? 1.0 : 0.0;
+    for (int sweep = 0; sweep < 60; sweep++) {
+        int changed = 0;
+        for (int p = 0; p < n - 1; p++)
+            for (int q = p + 1; q < n; q++) {
+                double alpha = 0, beta = 0, gamma = 0;
+                for (int i = 0; i < m; i++) {
+                    const double ap = a[i * n + p], aq = a[i * n + q];
+                    alpha += ap * ap;
+                    beta += aq * aq;
+                    gamma += ap * aq;
+                }
+                if (gamma == 0.0 || fabs(gamma) <= DBL_EPSILON * sqrt(alpha * beta)) continue;
+                changed = 1;
+                const double zeta = (beta - alpha) / (2.0 * gamma);
+                const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+                const double c = 1.0 / sqrt(1.0 + t * t), s = c * t;
+                for (int i = 0; i < m; i++) {
+                    const double ap = a[i * n + p], aq = a[i * n + q];
+                    a[i * n + p] = c * ap - s * aq;
+                    a[i * n + q] = s * ap + c * aq;
+                }
+                for (int i = 0; i < n; i++) {
+                    const double vp = v[i * n + p], vq = v[i * n + q];
+                    v[i * n + p] = c * vp - s * vq;
+                    v[i * n + q] = s * vp + c * vq;
+                }
+            }
+        if (!changed) break;
+    }
+    double ww[12];
+    int ord[12];
+    for (int j = 0; j < n; j++) {
+        double s = 0;
+        for (int i = 0; i < m; i++) s += a[i * n + j] * a[i * n + j];
+        ww[j] = sqrt(s);
+        ord[j] = j;
+    }
+    for (int j = 0; j < n; j++) {
+        int b = j;
+        for (int k = j + 1; k < n; k++)
+            if (ww[ord[k]] > ww[ord[b]]) b = k;
+        const int t = ord[j];
+        ord[j] = ord[b];
+        ord[b] = t;
+    }
+    for (int j = 0; j < n; j++) {
+        const int c = ord[j];
+        w[j] = ww[c];
+        const double inv = ww[c] > 0 ? 1.0 / ww[c] : 0.0;
+        if (U)
+            for (int i = 0; i < m; i++) U[i * n + j] = a[i * n + c] * inv;
+        for (int i = 0; i < n; i++) V[i * n + j] = v[i * n + c];
+    }
+}
+
+// cvSolve(A, b, x, CV_SVD): least squares over w > n * DBL_EPSILON * w[0]
+__device__ void svd_solve(int m, int n, const double* A, const double* b, double* x) {
+    double w[12], U[72], V[36];
+    svdj(m, n, A, w, U, V);
+    const double thr = n * DBL_EPSILON * w[0];
+    double y[6];
+    for (int j = 0; j < n; j++) {
+        double s = 0;
+        for (int i = 0; i < m; i++) s += U[i * n + j] * b[i];
+        y[j] = w[j] > thr ? s / w[j] : 0.0;
+    }
+    for (int i = 0; i < n; i++) {
+        double s = 0;
+        for (int j = 0; j < n; j++) s += V[i * n + j] * y[j];
+        x[i] = s;
+    }
+}
+
+__device__ __forceinline__ double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+
+// cvRodrigues2 vector -> matrix (+ dRdr[i*9+k] = dR_k/dr_i)
+__device__ void rod_v2m(const double* r, double* R, double* J) {
+    const double theta = sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
+    if (theta < DBL_EPSILON) {
+        for (int k = 0; k < 9; k++) R[k] = k % 4 == 0 ? 1.0 : 0.0;
+        if (J) {
+            for (int k = 0; k < 27; k++) J[k] = 0.0;
+            J[5] = 1;
+            J[7] = -1;
+            J[11] = -1;
+            J[15] = 1;
+            J[19] = 1;
+            J[21] = -1;
+        }
+        return;
+    }
+    const double c = cos(theta), s = sin(theta), c1 = 1. - c;
+    const double itheta = theta ? 1. / theta : 0.;
+    const double rx = r[0] * itheta, ry = r[1] * itheta, rz = r[2] * itheta;
+    const double rrt[9] = {rx * rx, rx * ry, rx * rz, rx * ry, ry * ry, ry * rz, rx * rz, ry * rz, rz * rz};
+    const double rx_[9] = {0, -rz, ry, rz, 0, -rx, -ry, rx, 0};
+    const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    for (int k = 0; k < 9; k++) R[k] = c * I[k] + c1 * rrt[k] + s * rx_[k];
+    if (J) {
+        const double drrt[27] = {rx + rx, ry, rz, ry, 0, 0, rz, 0, 0, 0, rx, 0, rx, ry + ry, rz, 0, rz, 0,
+                                 0, 0, rx, 0, 0, ry, rx, ry, rz + rz};
+        const double drx_[27] = {0, 0, 0, 0, 0, -1, 0, 1, 0, 0, 0, 1, 0, 0, 0, -1, 0, 0,
+                                 0, -1, 0, 1, 0, 0, 0, 0, 0};
+        for (int i = 0; i < 3; i++) {
+            const double ri = i == 0 ? rx : i == 1 ? ry : rz;
+            const double a0 = -s * ri, a1 = (s - 2 * c1 * itheta) * ri, a2 = c1 * itheta;
+            const double a3 = (c - s * itheta) * ri, a4 = s * itheta;
+            for (int k = 0; k < 9; k++)
+                J[i * 9 + k] = a0 * I[k] + a1 * rrt[k] + a2 * drrt[i * 9 + k] + a3 * rx_[k] + a4 * drx_[i * 9 + k];
+        }
+    }
+}
+
+// cvRodrigues2 matrix -> vector (R := U V^T first)
+__device__ void rod_m2v(const double* Rin, double* r) {
+    double w[3], U[9], V[9], R[9];
+    svdj(3, 3, Rin, w, U, V);
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) R[i * 3 + j] = U[i * 3 + 0] * V[j * 3 + 0] + U[i * 3 + 1] * V[j * 3 + 1] + U[i * 3 + 2] * V[j * 3 + 2];
+    double rx = R[7] - R[5], ry = R[2] - R[6], rz = R[3] - R[1];
+    const double s = sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
+    double c = (R[0] + R[4] + R[8] - 1) * 0.5;
+    c = c > 1. ? 1. : c < -1. ? -1. : c;
+    double theta = acos(c);
+    if (s < 1e-5) {
+        if (c > 0) {
+            rx = ry = rz = 0;
+        } else {
+            double t = (R[0] + 1) * 0.5;
+            rx = sqrt(t > 0 ? t : 0.);
+            t = (R[4] + 1) * 0.5;
+            ry = sqrt(t > 0 ? t : 0.) * (R[1] < 0 ? -1. : 1.);
+            t = (R[8] + 1) * 0.5;
+            rz = sqrt(t > 0 ? t : 0.) * (R[2] < 0 ? -1. : 1.);
+            if (fabs(rx) < fabs(ry) && fabs(rx) < fabs(rz) && (R[5] > 0) != (ry * rz > 0)) rz = -rz;
+            theta /= sqrt(rx * rx + ry * ry + rz * rz);
+            rx *= theta;
+            ry *= theta;
+            rz *= theta;
+        }
+    } else {
+        double vth = 1 / (2 * s);
+        vth *= theta;
+        rx *= vth;
+        ry *= vth;
+        rz *= vth;
+    }
+    r[0] = rx;
+    r[1] = ry;
+    r[2] = rz;
+}
+
+// cvProjectPoints2 of one point without distortion (+ Jacobian rows)
+__device__ __forceinline__ void project_pt(const double* R, const double* dRdr, const double* t, const PrK& K,
+                                           double X, double Y, double Z, double* u, double* v, double* Ju,
+                                           double* Jv) {
+    double x = R[0] * X + R[1] * Y + R[2] * Z + t[0];
+    double y = R[3] * X + R[4] * Y + R[5] * Z + t[1];
+    double z = R[6] * X + R[7] * Y + R[8] * Z + t[2];
+    z = z ? 1. / z : 1;
+    x *= z;
+    y *= z;
+    *u = x * K.fx + K.cx;
+    *v = y * K.fy + K.cy;
+    if (Ju) {
+        Ju[3] = K.fx * z;
+        Ju[4] = K.fx * 0.0;
+        Ju[5] = K.fx * (-x * z);
+        Jv[3] = K.fy * 0.0;
+        Jv[4] = K.fy * z;
+        Jv[5] = K.fy * (-y * z);
+        for (int j = 0; j < 3; j++) {
+            const double* d = dRdr + 9 * j;
+            const double dx0 = X * d[0] + Y * d[1] + Z * d[2];
+            const double dy0 = X * d[3] + Y * d[4] + Z * d[5];
+            const double dz0 = X * d[6] + Y * d[7] + Z * d[8];
+            Ju[j] = K.fx * (z * (dx0 - x * dz0));
+            Jv[j] = K.fy * (z * (dy0 - y * dz0));
+        }
+    }
+}
+
+// ------------------------------------------------ EPnP on the 5 points (epnp.cpp)
+struct Epnp5 {
+    double pws[15], us[10];
+    double alphas[20], pcs[15];
+    double cws[4][3], ccs[4][3];
+    double fu, fv, uc, vc;
+
+    __device__ void choose_control_points() {
+        cws[0][0] = cws[0][1] = cws[0][2] = 0;
+        for (int i = 0; i < PR_MODEL_POINTS; i++)
+            for (int j = 0; j < 3; j++) cws[0][j] += pws[3 * i + j];
+        for (int j = 0; j < 3; j++) cws[0][j] /= PR_MODEL_POINTS;
+        double PtP[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        for (int i = 0; i < PR_MODEL_POINTS; i++) {
+            double d[3];
+            for (int j = 0; j < 3; j++) d[j] = pws[3 * i + j] - cws[0][j];
+            for (int a = 0; a < 3; a++)
+                for (int b = 0; b < 3; b++) PtP[a * 3 + b] += d[a] * d[b];
+        }
+        double dc[3], V[9];
+        svdj(3, 3, PtP, dc, nullptr, V);
+        for (int i = 1; i < 4; i++) {
+            const double k = sqrt(dc[i - 1] / PR_MODEL_POINTS);
+            for (int j = 0; j < 3; j++) cws[i][j] = cws[0][j] + k * V[j * 3 + (i - 1)];
+        }
+    }
+    __device__ void compute_barycentric_coordinates() {
+        double cc[9], w[3], U[9], V[9], ci[9];
+        for (int i = 0; i < 3; i++)
+            for (int j = 1; j < 4; j++) cc[3 * i + j - 1] = cws[j][i] - cws[0][i];
+        svdj(3, 3, cc, w, U, V);
+        const double thr = 3 * DBL_EPSILON * w[0];
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) {
+                double s = 0;
+                for (int k = 0; k < 3; k++) s += V[i * 3 + k] * (w[k] > thr ? 1.0 / w[k] : 0.0) * U[j * 3 + k];
+                ci[i * 3 + j] = s;
+            }
+        for (int i = 0; i < PR_MODEL_POINTS; i++) {
+            const double* pi = pws + 3 * i;
+            double* a = alphas + 4 * i;
+            for (int j = 0; j < 3; j++)
+                a[1 + j] = ci[3 * j] * (pi[0] - cws[0][0]) + ci[3 * j + 1] * (pi[1] - cws[0][1]) +
+                           ci[3 * j + 2] * (pi[2] - cws[0][2]);
+            a[0] = 1.0f - a[1] - a[2] - a[3];
+        }
+    }
+    __device__ double compute_R_and_t(const double* ut, const double* betas, double R[3][3], double t[3]) {
+        for (int i = 0; i < 4; i++) ccs[i][0] = ccs[i][1] = ccs[i][2] = 0.0f;
+        for (int i = 0; i < 4; i++) {
+            const double* v = ut + 12 * (11 - i);
+            for (int j = 0; j < 4; j++)
+                for (int k = 0; k < 3; k++) ccs[j][k] += betas[i] * v[3 * j + k];
+        }
+        for (int i = 0; i < PR_MODEL_POINTS; i++) {
+            const double* a = alphas + 4 * i;
+            for (int j = 0; j < 3; j++)
+                pcs[3 * i + j] = a[0] * ccs[0][j] + a[1] * ccs[1][j] + a[2] * ccs[2][j] + a[3] * ccs[3][j];
+        }
+        if (pcs[2] < 0.0) {  // solve_for_sign
+            for (int i = 0; i < 4; i++)
+                for (int j = 0; j < 3; j++) ccs[i][j] = -ccs[i][j];
+            for (int i = 0; i < 3 * PR_MODEL_POINTS; i++) pcs[i] = -pcs[i];
+        }
+        // estimate_R_and_t
+        double pc0[3] = {0, 0, 0}, pw0[3] = {0, 0, 0};
+        for (int i = 0; i < PR_MODEL_POINTS; i++)
+            for (int j = 0; j < 3; j++) {
+                pc0[j] += pcs[3 * i + j];
+                pw0[j] += pws[3 * i + j];
+            }
+        for (int j = 0; j < 3; j++) {
+            pc0[j] /= PR_MODEL_POINTS;
+            pw0[j] /= PR_MODEL_POINTS;
+        }
+        double abt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        for (int i = 0; i < PR_MODEL_POINTS; i++) {
+            const double* pc = pcs + 3 * i;
+            const double* pw = pws + 3 * i;
+            for (int j = 0; j < 3; j++) {
+                abt[3 * j] += (pc[j] - pc0[j]) * (pw[0] - pw0[0]);
+                abt[3 * j + 1] += (pc[j] - pc0[j]) * (pw[1] - pw0[1]);
+                abt[3 * j + 2] += (pc[j] - pc0[j]) * (pw[2] - pw0[2]);
+            }
+        }
+        double d[3], u[9], v[9];
+        svdj(3, 3, abt, d, u, v);
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) R[i][j] = dot3(u + 3 * i, v + 3 * j);
+        const double det = R[0][0] * R[1][1] * R[2][2] + R[0][1] * R[1][2] * R[2][0] + R[0][2] * R[1][0] * R[2][1] -
+                           R[0][2] * R[1][1] * R[2][0] - R[0][1] * R[1][0] * R[2][2] - R[0][0] * R[1][2] * R[2][1];
+        if (det < 0) {
+            R[2][0] = -R[2][0];
+            R[2][1] = -R[2][1];
+            R[2][2] = -R[2][2];
+        }
+        t[0] = pc0[0] - dot3(R[0], pw0);
+        t[1] = pc0[1] - dot3(R[1], pw0);
+        t[2] = pc0[2] - dot3(R[2], pw0);
+        // reprojection_error
+        double sum2 = 0.0;
+        for (int i = 0; i < PR_MODEL_POINTS; i++) {
+            const double* pw = pws + 3 * i;
+            const double Xc = dot3(R[0], pw) + t[0], Yc = dot3(R[1], pw) + t[1];
+            const double inv_Zc = 1.0 / (dot3(R[2], pw) + t[2]);
+            const double ue = uc + fu * Xc * inv_Zc, ve = vc + fv * Yc * inv_Zc;
+            const double uu = us[2 * i], vv = us[2 * i + 1];
+            sum2 += sqrt((uu - ue) * (uu - ue) + (vv - ve) * (vv - ve));
+        }
+        return sum2 / PR_MODEL_POINTS;
+    }
+};
+
+__device__ void compute_L_6x10(const double* ut, double* l) {
+    const double* v[4] = {ut + 12 * 11, ut + 12 * 10, ut + 12 * 9, ut + 12 * 8};
+    double dv[4][6][3];
+    for (int i = 0; i < 4; i++) {
+        int a = 0, b = 1;
+        for (int j = 0; j < 6; j++) {
+            for (int k = 0; k < 3; k++) dv[i][j][k] = v[i][3 * a + k] - v[i][3 * b + k];
+            b++;
+            if (b > 3) {
+                a++;
+                b = a + 1;
+            }
+        }
+    }
+    for (int i = 0; i < 6; i++) {
+        double* row = l + 10 * i;
+        row[0] = dot3(dv[0][i], dv[0][i]);
+        row[1] = 2.0f * dot3(dv[0][i], dv[1][i]);
+        row[2] = dot3(dv[1][i], dv[1][i]);
+        row[3] = 2.0f * dot3(dv[0][i], dv[2][i]);
+        row[4] = 2.0f * dot3(dv[1][i], dv[2][i]);
+        row[5] = dot3(dv[2][i], dv[2][i]);
+        row[6] = 2.0f * dot3(dv[0][i], dv[3][i]);
+        row[7] = 2.0f * dot3(dv[1][i], dv[3][i]);
+        row[8] = 2.0f * dot3(dv[2][i], dv[3][i]);
+        row[9] = dot3(dv[3][i], dv[3][i]);
+    }
+}
+
+__device__ __forceinline__ double dist2(const double* a, const double* b) {
+    return (a[0] - b[0]) * (a[0] - b[0]) + (a[1] - b[1]) * (a[1] - b[1]) + (a[2] - b[2]) * (a[2] - b[2]);
+}
+
+__device__ void betas_approx(const double* l, const double* rho, int which, double* betas) {
+    const int nc = which == 1 ? 4 : which == 2 ? 3 : 5;
+    int cols[5] = {0, 1, 2, 3, 4};
+    if (which == 1) {
+        cols[2] = 3;
+        cols[3] = 6;
+    }
+    double L[30], b[5];
+    for (int i = 0; i < 6; i++)
+        for (int j = 0; j < nc; j++) L[i * nc + j] = l[10 * i + cols[j]];
+    svd_solve(6, nc, L, rho, b);
+    if (which == 1) {
+        if (b[0] < 0) {
+            betas[0] = sqrt(-b[0]);
+            betas[1] = -b[1] / betas[0];
+            betas[2] = -b[2] / betas[0];
+            betas[3] = -b[3] / betas[0];
+        } else {
+            betas[0] = sqrt(b[0]);
+            betas[1] = b[1] / betas[0];
+            betas[2] = b[2] / betas[0];
+            betas[3] = b[3] / betas[0];
+        }
+        return;
+    }
+    if (b[0] < 0) {
+        betas[0] = sqrt(-b[0]);
+        betas[1] = (b[2] < 0) ? sqrt(-b[2]) : 0.0;
+    } else {
+        betas[0] = sqrt(b[0]);
+        betas[1] = (b[2] > 0) ? sqrt(b[2]) : 0.0;
+    }
+    if (b[1] < 0) betas[0] = -betas[0];
+    betas[2] = which == 3 ? b[3] / betas[0] : 0.0;
+    betas[3] = 0.0;
+}
+
+// epnp.cpp qr_solve (6 x 4 Householder), with its column scan as written
+__device__ void qr_solve(double* A, double* b, double* X) {
+    const int nr = 6, nc = 4;
+    double A1[4], A2[4];
+    for (int k = 0; k < nc; k++) {
+        double* ppAkk = A + k * (nc + 1);
+        double* ppAik = ppAkk;
+        double eta = fabs(*ppAik);
+        for (int i = k + 1; i < nr; i++) {
+            const double elt = fabs(*ppAik);
+            if (eta < elt) eta = elt;
+            ppAik += nc;
+        }
+        if (eta == 0) {
+            A1[k] = A2[k] = 0.0;
+            return;
+        }
+        double sum = 0.0;
+        const double inv_eta = 1. / eta;
+        ppAik = ppAkk;
+        for (int i = k; i < nr; i++) {
+            *ppAik *= inv_eta;
+            sum += *ppAik * *ppAik;
+            ppAik += nc;
+        }
+        double sigma = sqrt(sum);
+        if (*ppAkk < 0) sigma = -sigma;
+        *ppAkk += sigma;
+        A1[k] = sigma * *ppAkk;
+        A2[k] = -eta * sigma;
+        for (int j = k + 1; j < nc; j++) {
+            double* p = ppAkk;
+            double s = 0;
+            for (int i = k; i < nr; i++) {
+                s += *p * p[j - k];
+                p += nc;
+            }
+            const double tau = s / A1[k];
+            p = ppAkk;
+            for (int i = k; i < nr; i++) {
+                p[j - k] -= tau * *p;
+                p += nc;
+            }
+        }
+    }
+    for (int j = 0; j < nc; j++) {
+        double* p = A + j * (nc + 1);
+        double tau = 0;
+        for (int i = j; i < nr; i++) {
+            tau += *p * b[i];
+            p += nc;
+        }
+        tau /= A1[j];
+        p = A + j * (nc + 1);
+        for (int i = j; i < nr; i++) {
+            b[i] -= tau * *p;
+            p += nc;
+        }
+    }
+    X[nc - 1] = b[nc - 1] / A2[nc - 1];
+    for (int i = nc - 2; i >= 0; i--) {
+        const double* p = A + i * nc + (i + 1);
+        double s = 0;
+        for (int j = i + 1; j < nc; j++) {
+            s += *p * X[j];
+            p++;
+        }
+        X[i] = (b[i] - s) / A2[i];
+    }
+}
+
+__device__ void gauss_newton(const double* l, const double* rho, double* betas) {
+    for (int k = 0; k < 5; k++) {
+        double A[24], b[6], x[4] = {0, 0, 0, 0};
+        for (int i = 0; i < 6; i++) {
+            const double* r = l + i * 10;
+            double* a = A + i * 4;
+            a[0] = 2 * r[0] * betas[0] + r[1] * betas[1] + r[3] * betas[2] + r[6] * betas[3];
+            a[1] = r[1] * betas[0] + 2 * r[2] * betas[1] + r[4] * betas[2] + r[7] * betas[3];
+            a[2] = r[3] * betas[0] + r[4] * betas[1] + 2 * r[5] * betas[2] + r[8] * betas[3];
+            a[3] = r[6] * betas[0] + r[7] * betas[1] + r[8] * betas[2] + 2 * r[9] * betas[3];
+            b[i] = rho[i] - (r[0] * betas[0] * betas[0] + r[1] * betas[0] * betas[1] + r[2] * betas[1] * betas[1] +
+                             r[3] * betas[0] * betas[2] + r[4] * betas[1] * betas[2] + r[5] * betas[2] * betas[2] +
+                             r[6] * betas[0] * betas[3] + r[7] * betas[1] * betas[3] + r[8] * betas[2] * betas[3] +
+                             r[9] * betas[3] * betas[3]);
+        }
+        qr_solve(A, b, x);
+        for (int i = 0; i < 4; i++) betas[i] += x[i];
+    }
+}
+
+// ------------------------------------------------------------------ kernels
+__global__ void k_pr_subsets(int n, int H, int* __restrict__ idx) {
+    if (threadIdx.x != 0) return;
+    uint64_t state = ~(uint64_t)0;  // RNG rng((uint64)-1), ptsetreg.cpp run()
+    for (int h = 0; h < H; h++) {
+        int s[PR_MODEL_POINTS];
+        for (int i = 0; i < PR_MODEL_POINTS; i++) {
+            for (;;) {
+                state = (uint64_t)(unsigned)state * 4164903690U + (unsigned)(state >> 32);
+                s[i] = (int)((unsigned)state % (unsigned)n);
+                int j;
+                for (j = 0; j < i; j++)
+                    if (s[i] == s[j]) break;
+                if (j == i) break;
+            }
+            idx[h * PR_MODEL_POINTS + i] = s[i];
+        }
+    }
+}
+
+__global__ __launch_bounds__(64) void k_pr_epnp(const float* __restrict__ Xw, const float* __restrict__ uv,
+                                                const int* __restrict__ idx, int H, PrK K,
+                                                double* __restrict__ model, double* __restrict__ Rproj) {
+    const int h = blockIdx.x * blockDim.x + threadIdx.x;
+    if (h >= H) return;
+    Epnp5 e;
+    e.fu = K.fx;
+    e.fv = K.fy;
+    e.uc = K.cx;
+    e.vc = K.cy;
+    for (int i = 0; i < PR_MODEL_POINTS; i++) {
+        const int p = idx[h * PR_MODEL_POINTS + i];
+        for (int k = 0; k < 3; k++) e.pws[3 * i + k] = (double)Xw[3 * p + k];
+        e.us[2 * i] = (double)uv[2 * p];
+        e.us[2 * i + 1] = (double)uv[2 * p + 1];
+    }
+    e.choose_control_points();
+    e.compute_barycentric_coordinates();
+    double mtm[144];
+    for (int k = 0; k < 144; k++) mtm[k] = 0.0;
+    for (int i = 0; i < PR_MODEL_POINTS; i++) {  // fill_M rows 2i, 2i+1 and M^T M in row order
+        const double* as = e.alphas + 4 * i;
+        double M1[12], M2[12];
+        const double uu = e.us[2 * i], vv = e.us[2 * i + 1];
+        for (int j = 0; j < 4; j++) {
+            M1[3 * j] = as[j] * e.fu;
+            M1[3 * j + 1] = 0.0;
+            M1[3 * j + 2] = as[j] * (e.uc - uu);
+            M2[3 * j] = 0.0;
+            M2[3 * j + 1] = as[j] * e.fv;
+            M2[3 * j + 2] = as[j] * (e.vc - vv);
+        }
+        for (int a = 0; a < 12; a++)
+            for (int b = 0; b < 12; b++) mtm[a * 12 + b] += M1[a] * M1[b];
+        for (int a = 0; a < 12; a++)
+            for (int b = 0; b < 12; b++) mtm[a * 12 + b] += M2[a] * M2[b];
+    }
+    double d[12], V[144], ut[144];
+    svdj(12, 12, mtm, d, nullptr, V);
+    for (int i = 0; i < 12; i++)
+        for (int j = 0; j < 12; j++) ut[i * 12 + j] = V[j * 12 + i];
+    double l[60], rho[6];
+    compute_L_6x10(ut, l);
+    rho[0] = dist2(e.cws[0], e.cws[1]);
+    rho[1] = dist2(e.cws[0], e.cws[2]);
+    rho[2] = dist2(e.cws[0], e.cws[3]);
+    rho[3] = dist2(e.cws[1], e.cws[2]);
+    rho[4] = dist2(e.cws[1], e.cws[3]);
+    rho[5] = dist2(e.cws[2], e.cws[3]);
+    double bestR[3][3], bestt[3], bestErr = 0;
+    for (int w = 1; w <= 3; w++) {
+        double betas[4], R[3][3], t[3];
+        betas_approx(l, rho, w, betas);
+        gauss_newton(l, rho, betas);
+        const double err = e.compute_R_and_t(ut, betas, R, t);
+        if (w == 1 || err < bestErr) {  // N = 1; rep[2] < rep[1] -> 2; rep[3] < rep[N] -> 3
+            bestErr = err;
+            for (int a = 0; a < 3; a++) {
+                bestt[a] = t[a];
+                for (int b = 0; b < 3; b++) bestR[a][b] = R[a][b];
+            }
+        }
+    }
+    double r[3], Rp[9];
+    rod_m2v(&bestR[0][0], r);
+    rod_v2m(r, Rp, nullptr);
+    double* mo = model + 6 * h;
+    mo[0] = r[0];
+    mo[1] = r[1];
+    mo[2] = r[2];
+    mo[3] = bestt[0];
+    mo[4] = bestt[1];
+    mo[5] = bestt[2];
+    for (int k = 0; k < 9; k++) Rproj[9 * h + k] = Rp[k];
+}
+
+__global__ __launch_bounds__(PR_COUNT_THREADS) void k_pr_count(const float* __restrict__ Xw,
+                                                               const float* __restrict__ uv, int n, PrK K,
+                                                               float thr, const double* __restrict__ model,
+                                                               const double* __restrict__ Rproj,
+                                                               uint8_t* __restrict__ mask, int* __restrict__ good) {
+    const int h = blockIdx.x;
+    __shared__ int wsum[PR_COUNT_THREADS / 64];
+    double R[9], t[3];
+    for (int k = 0; k < 9; k++) R[k] = Rproj[9 * h + k];
+    for (int k = 0; k < 3; k++) t[k] = model[6 * h + 3 + k];
+    uint8_t* mrow = mask + (size_t)h * n;
+    int cnt = 0;
+    for (int i = threadIdx.x; i < n; i += PR_COUNT_THREADS) {
+        double u, v;
+        project_pt(R, nullptr, t, K, (double)Xw[3 * i], (double)Xw[3 * i + 1], (double)Xw[3 * i + 2], &u, &v,
+                   nullptr, nullptr);
+        const float dx = uv[2 * i] - (float)u, dy = uv[2 * i + 1] - (float)v;
+        const float e2 = dx * dx + dy * dy;
+        const int f = e2 <= thr;
+        mrow[i] = (uint8_t)f;
+        cnt += f;
+    }
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_down(cnt, o, 64);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int s = 0;
+        for (int w = 0; w < PR_COUNT_THREADS / 64; w++) s += wsum[w];
+        good[h] = s;
+    }
+}
+
+__device__ int update_num_iters(double p, double ep, int modelPoints, int maxIters) {
+    p = p > 0. ? p : 0.;
+    p = p < 1. ? p : 1.;
+    ep = ep > 0. ? ep : 0.;
+    ep = ep < 1. ? ep : 1.;
+    double num = 1. - p > DBL_MIN ? 1. - p : DBL_MIN;
+    double denom = 1. - pow(1. - ep, (double)modelPoints);
+    if (denom < DBL_MIN) return 0;
+    num = log(num);
+    denom = log(denom);
+    return denom >= 0 || -num >= maxIters * (-denom) ? maxIters : (int)rint(num / denom);
+}
+
+// state[0] = best hypothesis (-1: none), [1] = iterations visited, [2] = maxGoodCount
+__global__ void k_pr_fold(const int* __restrict__ good, int n, int H, double confidence, int* __restrict__ state) {
+    if (threadIdx.x != 0) return;
+    int niters = H > 1 ? H : 1, maxGood = 0, best = -1, iter;
+    for (iter = 0; iter < niters; iter++) {
+        const int g = good[iter];
+        if (g > (maxGood > PR_MODEL_POINTS - 1 ? maxGood : PR_MODEL_POINTS - 1)) {
+            best = iter;
+            maxGood = g;
+            niters = update_num_iters(confidence, (double)(n - g) / n, PR_MODEL_POINTS, niters);
+        }
+    }
+    state[0] = best;
+    state[1] = iter;
+    state[2] = maxGood;
+}
+
+// fixed-order workgroup sum of NV doubles per thread (wave shuffles, then waves in order)
+template <int NV>
+__device__ void block_sum(double* v, double (*wred)[NV], double* out) {
+    for (int k = 0; k < NV; k++)
+        for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_down(v[k], o, 64);
+    if ((threadIdx.x & 63) == 0)
+        for (int k = 0; k < NV; k++) wred[threadIdx.x >> 6][k] = v[k];
+    __syncthreads();
+    if (threadIdx.x < NV) {
+        double s = wred[0][threadIdx.x];
+        for (int w = 1; w < PR_REFINE_THREADS / 64; w++) s += wred[w][threadIdx.x];
+        out[threadIdx.x] = s;
+    }
+    __syncthreads();
+}
+
+// residual pass over the inliers: with J -> red[0..35] = J^T J, [36..41] = J^T e, [42] = |e|^2
+__device__ void lm_pass(const float* __restrict__ Xw, const float* __restrict__ uv, const uint8_t* __restrict__ m,
+                        int n, const PrK& K, const double* p, bool withJ, double (*wred)[43], double* red) {
+    double R[9], dRdr[27];
+    rod_v2m(p, R, withJ ? dRdr : nullptr);
+    double acc[43];
+    for (int k = 0; k < 43; k++) acc[k] = 0.0;
+    for (int i = threadIdx.x; i < n; i += PR_REFINE_THREADS) {
+        if (!m[i]) continue;
+        double u, v, Ju[6], Jv[6];
+        project_pt(R, dRdr, p + 3, K, (double)Xw[3 * i], (double)Xw[3 * i + 1], (double)Xw[3 * i + 2], &u, &v,
+                   withJ ? Ju : nullptr, withJ ? Jv : nullptr);
+        const double eu = u - (double)uv[2 * i], ev = v - (double)uv[2 * i + 1];
+        acc[42] += eu * eu;
+        acc[42] += ev * ev;
+        if (withJ)
+            for (int a = 0; a < 6; a++) {
+                for (int b = 0; b < 6; b++) {
+                    acc[a * 6 + b] += Ju[a] * Ju[b];
+                    acc[a * 6 + b] += Jv[a] * Jv[b];
+                }
+                acc[36 + a] += Ju[a] * eu;
+                acc[36 + a] += Jv[a] * ev;
+            }
+    }
+    if (withJ) {
+        block_sum<43>(acc, wred, red);
+    } else {
+        // only |e|^2: reuse the 43-wide path for slot 42 alone
+        double one[1] = {acc[42]};
+        for (int o = 32; o > 0; o >>= 1) one[0] += __shfl_down(one[0], o, 64);
+        if ((threadIdx.x & 63) == 0) wred[threadIdx.x >> 6][42] = one[0];
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double s = wred[0][42];
+            for (int w = 1; w < PR_REFINE_THREADS / 64; w++) s += wred[w][42];
+            red[42] = s;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(PR_REFINE_THREADS) void k_pr_refine(const float* __restrict__ Xw,
+                                                                 const float* __restrict__ uv, int n, PrK K,
+                                                                 const uint8_t* __restrict__ mask,
+                                                                 const double* __restrict__ model,
+                                                                 const int* __restrict__ state,
+                                                                 odo_pnp_ransac_result* __restrict__ res,
+                                                                 uint8_t* __restrict__ mask_out) {
+    __shared__ double wred[PR_REFINE_THREADS / 64][43];
+    __shared__ double red[43];
+    __shared__ double sp[6], sprev[6];
+    const int best = state[0];
+    if (best < 0 || state[2] <= 0) {
+        if (threadIdx.x == 0) {
+            res->ok = 0;
+            res->n_inliers = 0;
+            res->best_iter = best;
+            res->iterations_visited = state[1];
+        }
+        for (int i = threadIdx.x; i < n; i += PR_REFINE_THREADS) mask_out[i] = 0;
+        return;
+    }
+    const uint8_t* m = mask + (size_t)best * n;
+    for (int i = threadIdx.x; i < n; i += PR_REFINE_THREADS) mask_out[i] = m[i];
+    if (threadIdx.x < 6) sp[threadIdx.x] = model[6 * best + threadIdx.x];
+    __syncthreads();
+    double lambdaLg10 = -3, prevErrNorm = DBL_MAX;
+    double JtJ[36], JtErr[6];
+    int iters = 0;
+    for (;;) {
+        double p[6];
+        for (int k = 0; k < 6; k++) p[k] = sp[k];
+        lm_pass(Xw, uv, m, n, K, p, true, wred, red);
+        const double e0 = sqrt(red[42]);
+        for (int k = 0; k < 36; k++) JtJ[k] = red[k];
+        for (int k = 0; k < 6; k++) JtErr[k] = red[36 + k];
+        for (int k = 0; k < 6; k++) p[k] = sp[k];  // prevParam
+        // step(): param = prev - solve((JtJ with diag * (1 + lambda)), JtErr)
+        auto step = [&]() {
+            if (threadIdx.x == 0) {
+                const double lambda = exp(lambdaLg10 * log(10.));
+                double A[36], x[6];
+                for (int k = 0; k < 36; k++) A[k] = JtJ[k];
+                for (int i = 0; i < 6; i++) A[i * 7] *= 1. + lambda;
+                svd_solve(6, 6, A, JtErr, x);
+                for (int i = 0; i < 6; i++) sp[i] = p[i] - x[i];
+            }
+            __syncthreads();
+        };
+        if (threadIdx.x < 6) sprev[threadIdx.x] = p[threadIdx.x];
+        step();
+        if (iters == 0) prevErrNorm = e0;
+        double q[6];
+        for (int k = 0; k < 6; k++) q[k] = sp[k];
+        lm_pass(Xw, uv, m, n, K, q, false, wred, red);
+        double errNorm = sqrt(red[42]);
+        while (errNorm > prevErrNorm && ++lambdaLg10 <= 16) {
+            step();
+            for (int k = 0; k < 6; k++) q[k] = sp[k];
+            lm_pass(Xw, uv, m, n, K, q, false, wred, red);
+            errNorm = sqrt(red[42]);
+        }
+        lambdaLg10 = lambdaLg10 - 1 > -16 ? lambdaLg10 - 1 : -16;
+        double dn = 0, pn = 0;
+        for (int i = 0; i < 6; i++) {
+            dn += (sp[i] - sprev[i]) * (sp[i] - sprev[i]);
+            pn += sprev[i] * sprev[i];
+        }
+        if (++iters >= 20 || sqrt(dn) / (sqrt(pn) + DBL_EPSILON) < FLT_EPSILON) break;
+        prevErrNorm = errNorm;
+    }
+    if (threadIdx.x == 0) {
+        double R[9];
+        double p[6];
+        for (int k = 0; k < 6; k++) p[k] = sp[k];
+        rod_v2m(p, R, nullptr);
+        for (int k = 0; k < 3; k++) {
+            res->rvec[k] = p[k];
+            res->tvec[k] = p[3 + k];
+            res->model_rvec[k] = model[6 * best + k];
+            res->model_tvec[k] = model[6 * best + 3 + k];
+        }
+        for (int r = 0; r < 3; r++) {
+            for (int k = 0; k < 3; k++) res->Tcw[4 * r + k] = (float)R[3 * r + k];
+            res->Tcw[4 * r + 3] = (float)p[3 + r];
+        }
+        res->Tcw[12] = res->Tcw[13] = res->Tcw[14] = 0.f;
+        res->Tcw[15] = 1.f;
+        res->ok = 1;
+        res->n_inliers = state[2];
+        res->best_iter = best;
+        res->iterations_visited = state[1];
+    }
+}
+
+}  // namespace
+
+int pnp_ransac_max_points() { return 1 << 16; }
+
+void launch_pnp_ransac(hipStream_t st, const float* Xw, const float* uv, int n, const float K4[4], int H,
+                       float reproj_err, double confidence, int* idx, double* model, double* Rproj, uint8_t* mask,
+                       int* good, int* state, odo_pnp_ransac_result* res, uint8_t* mask_out) {
+    const PrK K{(double)K4[0], (double)K4[1], (double)K4[2], (double)K4[3]};
+    const float thr = (float)((double)reproj_err * (double)reproj_err);
+    hipLaunchKernelGGL(k_pr_subsets, dim3(1), dim3(64), 0, st, n, H, idx);
+    hipLaunchKernelGGL(k_pr_epnp, dim3((H + 63) / 64), dim3(64), 0, st, Xw, uv, idx, H, K, model, Rproj);
+    hipLaunchKernelGGL(k_pr_count, dim3(H), dim3(PR_COUNT_THREADS), 0, st, Xw, uv, n, K, thr, model, Rproj, mask,
+                       good);
+    hipLaunchKernelGGL(k_pr_fold, dim3(1), dim3(64), 0, st, good, n, H, confidence, state);
+    hipLaunchKernelGGL(k_pr_refine, dim3(1), dim3(PR_REFINE_THREADS), 0, st, Xw, uv, n, K, mask, model, state, res,
+                       mask_out);
+}
+
+}  // namespace odo

@@ -227,6 +227,11 @@ void launch_pnp(hipStream_t st, const int32_t* f2_src, const float* xyz, const f
                 const int* n_matches, int min_matches, void* edges, odo_pair_result* res, uint8_t* inlier_mask,
                 int npairs, const int* sel = nullptr, int sel_val = 0);
 void launch_kabsch(hipStream_t st, const float* A, const float* B, int n, float* T);
+// PnPRansac (k_pnpransac.hip): idx H*5, model H*6, Rproj H*9, mask H*n, good H, state 3
+int pnp_ransac_max_points();
+void launch_pnp_ransac(hipStream_t st, const float* Xw, const float* uv, int n, const float K4[4], int H,
+                       float reproj_err, double confidence, int* idx, double* model, double* Rproj, uint8_t* mask,
+                       int* good, int* state, odo_pnp_ransac_result* res, uint8_t* mask_out);
 int launch_projection_match(hipStream_t st, const float* Tcw, const odo_landmark* lms, int nL, const float* kun,
                             const int32_t* octave, const uint8_t* desc, int n, const uint8_t* slot_taken,
                             const float* calib5, const float* bounds, float th, float nnratio, float* proj,

@@ -165,6 +165,20 @@ int odo_ransac_hyps_finish(odo_ctx* ctx, const odo_ransac_fold_result* r, odo_rn
 int odo_pnp_motion_ba(odo_ctx* ctx, const float* Xw, const float* obs, int n, const odo_calib* calib,
                       const float Tcw_init[16], float Tcw_out[16], uint8_t* outlier, int* n_inliers);
 
+/* PnPRansac::Compute (pnpransac.cpp:11-51), the RANSAC
+ * PnP back-end: cv::solvePnPRansac(v3D, v2D, mK, noDist, r, t, false,
+ * iterations = 500, reproj_err = 3.0f, confidence = 0.85, inliers) over the
+ * frame's landmark observations. Xw: n x 3 world points (Landmark::GetWorldPos),
+ * uv: n x 2 undistorted keypoints (mvKeysUn), in index order. n < 10 returns
+ * res->ok = 0 without running (pnpransac.cpp:30). inlier_mask (n, optional):
+ * the RANSAC inliers (Frame::SetInlier); good_counts (iterations, optional):
+ * inliers of every hypothesis, of which the first res->iterations_visited are
+ * the ones RANSAC visited. Hypotheses, EPnP, counts, the ordered fold and the
+ * Levenberg-Marquardt refinement all run on the GPU (k_pnpransac.hip). */
+int odo_pnp_ransac(odo_ctx* ctx, const float* Xw, const float* uv, int n, const odo_calib* calib, int iterations,
+                   float reproj_err, double confidence, odo_pnp_ransac_result* res, uint8_t* inlier_mask,
+                   int32_t* good_counts);
+
 /* ---- Trajectory (host only) ----
  * Relative-pose chain of the batched contract: results[i].Tcw is frame i's
  * pose in frame i-1's camera coordinates, so Tcw(i) = Tcw_rel(i) * Tcw(i-1)

@@ -104,6 +104,18 @@ typedef struct odo_ransac_fold_result {
     int32_t pad[2];
 } odo_ransac_fold_result;
 
+/* Result of PnPRansac::Compute's cv::solvePnPRansac (pnpransac.cpp:34-50):
+ * (rvec, tvec) refined by solvePnP(ITERATIVE) on the RANSAC inliers, the best
+ * RANSAC model, T = Converter::toHomogeneous(r, t) (row-major float), bOK,
+ * inliers.rows, the index of the winning hypothesis and the RANSAC
+ * iterations run (niters after RANSACUpdateNumIters). 176 bytes. */
+typedef struct odo_pnp_ransac_result {
+    double rvec[3], tvec[3];
+    double model_rvec[3], model_tvec[3];
+    float Tcw[16];
+    int32_t ok, n_inliers, best_iter, iterations_visited;
+} odo_pnp_ransac_result;
+
 /* One local-map landmark for Matcher::ProjectionMatch (matcher.cpp:90-145):
  * world position (Landmark::GetWorldPos), distinctive descriptor
  * (GetDescriptor) and state flags. 48 bytes. */

@@ -169,6 +169,26 @@ void oracle_svd3(const float* A, float* U, float* S, float* V);
 int oracle_pnp(const float* Xw, const float* obs, int n, const odo_calib* c,
                const float* Tcw_init, float* Tcw_out, uint8_t* outlier);
 
+/* ---- PnPRansac::Compute (pnpransac.cpp:11-51):
+ * cv::solvePnPRansac(v3D, v2D, K, noDist, r, t, false, iterations, reproj_err,
+ * confidence, inliers) of OpenCV 3.4 restated in pnpransac_ref.cpp. Xw n x 3,
+ * uv n x 2 (mvKeysUn). model_out: best RANSAC model (rvec, tvec); rt_out: the
+ * refined (rvec, tvec); Tcw: Converter::toHomogeneous(r, t); mask: RANSAC
+ * inlier mask (n); good_counts (optional, >= iterations): inliers of every
+ * visited hypothesis. Returns 1 (bOK), 0 when n < 10 or no model. */
+int oracle_pnp_ransac(const float* Xw, const float* uv, int n, const odo_calib* c, int iterations, float reproj_err,
+                      double confidence, double model_out[6], double rt_out[6], float* Tcw, uint8_t* mask,
+                      int* n_inliers, int* best_iter, int* niters_out, int* good_counts);
+/* Pieces of it, for known-answer tests: cv::RNG(state).uniform(a, b) x n,
+ * RANSACUpdateNumIters, cvRodrigues2 both ways (dRdr 3x9, optional), the EPnP
+ * model of n points, the LM refinement from param (in/out). */
+void oracle_cvrng_stream(uint64_t state, int a, int b, int n, int32_t* out);
+int oracle_ransac_update_num_iters(double p, double ep, int model_points, int max_iters);
+void oracle_rodrigues(const double r[3], double R[9], double* dRdr);
+void oracle_rodrigues_inv(const double R[9], double r[3]);
+void oracle_epnp(const double* pw, const double* uv, int n, const double K[4], double model[6]);
+void oracle_pnp_refine(const double* M, const double* m, int n, const double K[4], double param[6]);
+
 /* Kabsch::Compute (kabsch.cpp:14-57). */
 void oracle_kabsch(const float* A, const float* B, int n, float* T);
 

@@ -128,6 +128,14 @@ def lib():
             "oracle_orbcv_levels": (C.c_int, [C.c_int, C.c_int, P, P, P, P]),
             "oracle_extract_frame_adaptive_orb": (C.c_int, [P, P, C.c_int, C.c_int, P, P, P, P, P, P, P, P,
                                                             C.c_int]),
+            "oracle_pnp_ransac": (C.c_int, [P, P, C.c_int, P, C.c_int, C.c_float, C.c_double, P, P, P, P, P, P, P,
+                                            P]),
+            "oracle_cvrng_stream": (None, [C.c_uint64, C.c_int, C.c_int, C.c_int, P]),
+            "oracle_ransac_update_num_iters": (C.c_int, [C.c_double, C.c_double, C.c_int, C.c_int]),
+            "oracle_rodrigues": (None, [P, P, P]),
+            "oracle_rodrigues_inv": (None, [P, P]),
+            "oracle_epnp": (None, [P, P, C.c_int, P, P]),
+            "oracle_pnp_refine": (None, [P, P, C.c_int, P, P]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -267,3 +275,20 @@ def check_pnp_flags(got_flags, ref_flags, f1, f2, f2_src, Tcw_ref, cal, tag):
     assert not far.any(), (f"{tag}: PnP inlier flags differ away from the chi2 threshold at keypoints "
                            f"{bad[far][:8]} (chi2 {chi[far][:8]})")
     return int(bad.size)
+
+
+def pnp_ransac(Xw, uv, calib: Calib, iterations=500, reproj=3.0, confidence=0.85):
+    """PnPRansac::Compute's cv::solvePnPRansac (pnpransac.cpp:34) on the oracle."""
+    Xw = np.ascontiguousarray(Xw, np.float32)
+    uv = np.ascontiguousarray(uv, np.float32)
+    n = len(Xw)
+    model = np.zeros(6)
+    rt = np.zeros(6)
+    T = np.zeros(16, np.float32)
+    mask = np.zeros(max(n, 1), np.uint8)
+    good = np.zeros(max(iterations, 1), np.int32)
+    ni, bi, nit = C.c_int(), C.c_int(), C.c_int()
+    ok = lib().oracle_pnp_ransac(ptr(Xw), ptr(uv), n, C.byref(calib), iterations, reproj, confidence, ptr(model),
+                                 ptr(rt), ptr(T), ptr(mask), C.byref(ni), C.byref(bi), C.byref(nit), ptr(good))
+    return dict(ok=ok, model=model, rt=rt, T=T.reshape(4, 4), mask=mask[:n].astype(bool), n_inliers=ni.value,
+                best_iter=bi.value, niters=nit.value, good=good[:nit.value])
