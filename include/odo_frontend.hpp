@@ -543,6 +543,40 @@ public:
     }
 };
 
+// Odometry/pnpransac.h: cv::solvePnPRansac over the frame's landmark
+// observations (pnpransac.cpp:11-51): fewer than 10 returns 0; on success the
+// pose is set and the RANSAC inliers are marked; a failed solve, where the
+// reference prints "PnPRansac fail" and calls terminate(), throws.
+class PnPRansac {
+public:
+    int Compute(Frame& frame) {
+        std::vector<float> v3D, v2D;
+        std::vector<size_t> vnIndex;
+        for (size_t i = 0; i < frame.N; ++i) {
+            LandmarkPtr lm = frame.GetLandmark(i);
+            if (!lm) continue;
+            v3D.insert(v3D.end(), {lm->mWorldPos[0], lm->mWorldPos[1], lm->mWorldPos[2]});
+            v2D.insert(v2D.end(), {frame.mvKeysUn[i].x, frame.mvKeysUn[i].y});
+            vnIndex.push_back(i);
+        }
+        const int n = (int)vnIndex.size();
+        if (n < 10) return 0;
+        const odo_calib cal = Calibration();
+        odo_pnp_ransac_result r;
+        std::vector<uint8_t> inl(n, 0);
+        Check(odo_pnp_ransac(detail::shared_ctx(), v3D.data(), v2D.data(), n, &cal, 500, 3.0f, 0.85, &r, inl.data(),
+                             nullptr),
+              "PnPRansac::Compute");
+        if (!r.ok) throw std::runtime_error("PnPRansac fail");
+        Pose T;
+        std::copy(r.Tcw, r.Tcw + 16, T.begin());
+        frame.SetPose(T);
+        for (int k = 0; k < n; ++k)
+            if (inl[k]) frame.SetInlier(vnIndex[k]);
+        return r.n_inliers;
+    }
+};
+
 // Odometry/kabsch.h: Compute(setA, setB) for n x 3 row-major point sets.
 class Kabsch {
 public:
