@@ -355,6 +355,63 @@ def hard_leg(pkg, synth, args, B, W, H, device):
             "ate_mm": round(ate, 3)}
 
 
+def pnpransac_mode(args):
+    """SURVEY 8(f) rank 4: PnPRansac::Compute (pnpransac.cpp:11-51), the
+    cv::solvePnPRansac back-end, on one cfg2 pair: landmarks = frame 0's camera
+    points of the KnnMatch matches, observations = frame 1's undistorted
+    keypoints (a third of them re-targeted at random keypoints as outliers),
+    500 iterations, 3 px, confidence 0.85. A latency metric: ms per call of
+    odo_pnp_ransac (host arrays in and out); per-kernel times come from
+    rocprofv3 of the same command."""
+    import torch
+    pkg = load_pkg()
+    synth = load_synth()
+    bgr, dep, _ = synth.make_sequence(2, args.width, args.height, seed=0x5EED0002)
+    cfg = pkg.default_config(args.width, args.height, 2, nfeatures=args.nfeatures, iterations=200,
+                             seed=0x5EED0002)
+    odo = pkg.Odometry(cfg)
+    odo.track_batch_host(bgr, dep)
+    m = odo.pair(1)["matches"]
+    f0, f1 = odo.frame(0), odo.frame(1)
+    ok = f0["xyz"][m["queryIdx"], 2] > 0
+    m = m[ok]
+    Xw = np.ascontiguousarray(f0["xyz"][m["queryIdx"]])
+    uv = np.ascontiguousarray(f1["kun"][m["trainIdx"]])
+    rs = np.random.default_rng(5)
+    sel = rs.random(len(uv)) < 1.0 / 3.0
+    uv[sel] = f1["kun"][rs.integers(0, len(f1["kun"]), int(sel.sum()))]
+    for _ in range(3):
+        res, mask, _ = odo.pnp_ransac(Xw, uv, None, args.iters)
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(max(args.steps, 5)):
+        t0 = time.perf_counter()
+        res, mask, _ = odo.pnp_ransac(Xw, uv, None, args.iters)
+        ts.append((time.perf_counter() - t0) * 1e3)
+    odo.close()
+    out = {"metric": "PnPRansac::Compute latency (cv::solvePnPRansac on the GPU, one call)",
+           "value": round(float(np.median(ts)), 4), "unit": "ms/call (p50)", "n_gpus": 1, "steps": len(ts),
+           "higher_is_better": False, "p90_ms": round(float(np.percentile(ts, 90)), 4),
+           "observations": int(len(Xw)), "outliers_injected": int(sel.sum()), "ok": int(res.ok),
+           "n_inliers": int(res.n_inliers), "iterations_visited": int(res.iterations_visited),
+           "best_iter": int(res.best_iter),
+           "config": {"workload": f"cfg2 pair {args.width}x{args.height}, {args.nfeatures} kp, "
+                                  f"iterations {args.iters}, 3 px, confidence 0.85"}}
+    if not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib as O
+        c = cfg.calib
+        cal = O.Calib(c.fx, c.fy, c.cx, c.cy, c.k1, c.k2, c.p1, c.p2, c.k3, c.depth_factor, c.mbf, c.th_depth)
+        cts = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            O.pnp_ransac(Xw, uv, cal, args.iters)
+            cts.append((time.perf_counter() - t0) * 1e3)
+        out["cpu_baseline"] = {"value": round(float(np.median(cts)), 3), "unit": "ms/call (median of 5)", "cores": 1,
+                               "kind": "port", "sample": "the same call on oracle/pnpransac_ref.cpp"}
+    print(json.dumps(out), flush=True)
+
+
 def latency_mode(args):
     """Per-frame latency of the drop-in path: tools/build/frontend_latency runs
     one Tracking::Track frame at a time through include/odo_frontend.hpp
@@ -408,9 +465,10 @@ def main():
                     help="main leg's sequence: the cfg2 proxy or the hard variant (synth hard=True)")
     ap.add_argument("--no-kernel-timing", action="store_true", help="no events around the kNN-2 launches")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mode", choices=["track", "hyp", "latency"], default="track",
+    ap.add_argument("--mode", choices=["track", "hyp", "latency", "pnpransac"], default="track",
                     help="track: the frames/s metric; hyp: SURVEY 8(e) hypotheses mode latency (cfg3, H=4096); "
-                         "latency: per-frame ms of the drop-in path through include/odo_frontend.hpp")
+                         "latency: per-frame ms of the drop-in path through include/odo_frontend.hpp; "
+                         "pnpransac: SURVEY 8(f) rank 4 PnPRansac latency on a cfg2 pair")
     ap.add_argument("--hyp-outliers", type=float, default=0.5, help="hyp mode: fraction of matches re-targeted")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="process group backend for N > 1 (gloo: several ranks sharing one GPU)")
@@ -424,6 +482,9 @@ def main():
 
     if args.mode == "latency":
         latency_mode(args)
+        return
+    if args.mode == "pnpransac":
+        pnpransac_mode(args)
         return
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
