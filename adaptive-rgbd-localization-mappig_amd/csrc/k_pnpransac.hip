@@ -5,7 +5,8 @@
 // the minimal sets come from cv::RNG independently of the models. So:
 //   k_pr_subsets  one lane draws every hypothesis' 5 distinct indices
 //                 (cv::RNG(-1).uniform(0, n), getSubset's retry rule);
-//   k_pr_epnp     one lane per hypothesis: EPnP on its 5 points (epnp.cpp:
+//   k_pr_epnp     16 lanes per hypothesis (row-parallel 12x12 Jacobi, the rest
+//                 replicated on the group): EPnP on its 5 points (epnp.cpp:
 //                 control points, barycentrics, 12x12 M^T M eigenvectors, the
 //                 three beta approximations + 5 Gauss-Newton steps, best
 //                 reprojection), Rodrigues -> (rvec, tvec) and the rotation
@@ -16,10 +17,10 @@
 //   k_pr_fold     one lane replays run()'s loop over the counts in order:
 //                 goodCount > max(maxGoodCount, 4) -> best, niters =
 //                 RANSACUpdateNumIters(0.85, outlier ratio, 5, niters);
-//   k_pr_refine   one workgroup: solvePnP(ITERATIVE, extrinsic guess) on the
+//   k_pr_refine   one wave: solvePnP(ITERATIVE, extrinsic guess) on the
 //                 best model's inliers = CvLevMarq (20 iterations, FLT_EPSILON)
 //                 over cvProjectPoints2 residuals and Jacobians; J^T J, J^T e
-//                 and |e| reduced in a fixed wave-then-workgroup order.
+//                 and |e| reduced in a fixed lane-shuffle order.
 // All hypotheses up to `iterations` are evaluated (the fold decides how many
 // were visited), like the Ransac::Iterate kernels. The per-hypothesis math is
 // double precision IEEE +,-,*,/,sqrt in the oracle's operation order
@@ -36,27 +37,35 @@ namespace {
 
 constexpr int PR_MODEL_POINTS = 5;
 constexpr int PR_COUNT_THREADS = 256;
-constexpr int PR_REFINE_THREADS = 256;
+constexpr int PR_REFINE_THREADS = 64;  // one wave: the LM reductions need no LDS round
 
 struct PrK {
     double fx, fy, cx, cy;
 };
 
 // ------------------------------------------- one-sided Jacobi SVD (double)
-// A (m x n, m >= n, row-major) = U diag(w) V^T, w descending (first maximum
-// first); U m x n, V n x n by columns.
-__device__ void svdj(int m, int n, const double* A, double* w, double* U, double* V) {
-    double a[144], v[144];
-    for (int i = 0; i < m * n; i++) a[i] = A[i];
-    for (int i = 0; i < n; i++)
-        for (int j = 0; j < n; j++) v[i * n + j] = i == j ? 1.0 : 0.0;
+// A (M x N, M >= N, row-major) = U diag(w) V^T, w descending (first maximum
+// first); U M x N, V N x N by columns. Sizes are template parameters so the
+// small systems (3x3, 6xN) live in registers.
+template <int M, int N>
+__device__ void svdj(const double* A, double* w, double* U, double* V) {
+    double a[M * N], v[N * N];
+#pragma unroll
+    for (int i = 0; i < M * N; i++) a[i] = A[i];
+#pragma unroll
+    for (int i = 0; i < N; i++)
+#pragma unroll
+        for (int j = 0; j < N; j++) v[i * N + j] = i == j ? 1.0 : 0.0;
     for (int sweep = 0; sweep < 60; sweep++) {
         int changed = 0;
-        for (int p = 0; p < n - 1; p++)
-            for (int q = p + 1; q < n; q++) {
+#pragma unroll
+        for (int p = 0; p < N - 1; p++)
+#pragma unroll
+            for (int q = p + 1; q < N; q++) {
                 double alpha = 0, beta = 0, gamma = 0;
-                for (int i = 0; i < m; i++) {
-                    const double ap = a[i * n + p], aq = a[i * n + q];
+#pragma unroll
+                for (int i = 0; i < M; i++) {
+                    const double ap = a[i * N + p], aq = a[i * N + q];
                     alpha += ap * ap;
                     beta += aq * aq;
                     gamma += ap * aq;
@@ -66,59 +75,158 @@ __device__ void svdj(int m, int n, const double* A, double* w, double* U, double
                 const double zeta = (beta - alpha) / (2.0 * gamma);
                 const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
                 const double c = 1.0 / sqrt(1.0 + t * t), s = c * t;
-                for (int i = 0; i < m; i++) {
-                    const double ap = a[i * n + p], aq = a[i * n + q];
-                    a[i * n + p] = c * ap - s * aq;
-                    a[i * n + q] = s * ap + c * aq;
+#pragma unroll
+                for (int i = 0; i < M; i++) {
+                    const double ap = a[i * N + p], aq = a[i * N + q];
+                    a[i * N + p] = c * ap - s * aq;
+                    a[i * N + q] = s * ap + c * aq;
                 }
-                for (int i = 0; i < n; i++) {
-                    const double vp = v[i * n + p], vq = v[i * n + q];
-                    v[i * n + p] = c * vp - s * vq;
-                    v[i * n + q] = s * vp + c * vq;
+#pragma unroll
+                for (int i = 0; i < N; i++) {
+                    const double vp = v[i * N + p], vq = v[i * N + q];
+                    v[i * N + p] = c * vp - s * vq;
+                    v[i * N + q] = s * vp + c * vq;
                 }
             }
         if (!changed) break;
     }
-    double ww[12];
-    int ord[12];
-    for (int j = 0; j < n; j++) {
+    double ww[N];
+    int ord[N];
+#pragma unroll
+    for (int j = 0; j < N; j++) {
         double s = 0;
-        for (int i = 0; i < m; i++) s += a[i * n + j] * a[i * n + j];
+#pragma unroll
+        for (int i = 0; i < M; i++) s += a[i * N + j] * a[i * N + j];
         ww[j] = sqrt(s);
         ord[j] = j;
     }
-    for (int j = 0; j < n; j++) {
+    // selection sort (descending, first maximum wins) on the values, ord follows
+#pragma unroll
+    for (int j = 0; j < N; j++) {
         int b = j;
-        for (int k = j + 1; k < n; k++)
-            if (ww[ord[k]] > ww[ord[b]]) b = k;
-        const int t = ord[j];
-        ord[j] = ord[b];
-        ord[b] = t;
+        double wb = ww[j];
+#pragma unroll
+        for (int k = j + 1; k < N; k++)
+            if (ww[k] > wb) {
+                b = k;
+                wb = ww[k];
+            }
+#pragma unroll
+        for (int k = j + 1; k < N; k++)
+            if (k == b) {
+                const double tw = ww[j];
+                ww[j] = ww[k];
+                ww[k] = tw;
+                const int to = ord[j];
+                ord[j] = ord[k];
+                ord[k] = to;
+            }
     }
-    for (int j = 0; j < n; j++) {
-        const int c = ord[j];
-        w[j] = ww[c];
-        const double inv = ww[c] > 0 ? 1.0 / ww[c] : 0.0;
-        if (U)
-            for (int i = 0; i < m; i++) U[i * n + j] = a[i * n + c] * inv;
-        for (int i = 0; i < n; i++) V[i * n + j] = v[i * n + c];
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+        w[j] = ww[j];
+        const double inv = ww[j] > 0 ? 1.0 / ww[j] : 0.0;
+#pragma unroll
+        for (int c = 0; c < N; c++)
+            if (ord[j] == c) {
+                if (U)
+#pragma unroll
+                    for (int i = 0; i < M; i++) U[i * N + j] = a[i * N + c] * inv;
+#pragma unroll
+                for (int i = 0; i < N; i++) V[i * N + j] = v[i * N + c];
+            }
+    }
+}
+
+// The 12 x 12 M^T M of EPnP, row-parallel: a group of 16 lanes per
+// hypothesis, lane r < 12 holding row r of A and of V (lanes 12..15 hold
+// zeros). The column dot products of a rotation are xor-butterfly sums over the
+// group taken from its first lane (tree16 in oracle/pnpransac_ref.cpp follows
+// the same association); the rotations are lane-local, in svdj's order.
+constexpr int PR_EPNP_GROUP = 16;
+constexpr int PR_EPNP_THREADS = 64;
+__device__ __forceinline__ double group_sum16(double x) {
+    x += __shfl_xor(x, 8, PR_EPNP_GROUP);
+    x += __shfl_xor(x, 4, PR_EPNP_GROUP);
+    x += __shfl_xor(x, 2, PR_EPNP_GROUP);
+    x += __shfl_xor(x, 1, PR_EPNP_GROUP);
+    return __shfl(x, 0, PR_EPNP_GROUP);
+}
+
+__device__ void svdj12_rows(double* arow, double* vrow, int r, int* ord) {
+#pragma unroll
+    for (int j = 0; j < 12; j++) vrow[j] = (r == j) ? 1.0 : 0.0;
+    for (int sweep = 0; sweep < 60; sweep++) {
+        int changed = 0;
+#pragma unroll
+        for (int p = 0; p < 11; p++)
+#pragma unroll
+            for (int q = p + 1; q < 12; q++) {
+                const double ap0 = arow[p], aq0 = arow[q];
+                const double alpha = group_sum16(ap0 * ap0);
+                const double beta = group_sum16(aq0 * aq0);
+                const double gamma = group_sum16(ap0 * aq0);
+                if (gamma == 0.0 || fabs(gamma) <= DBL_EPSILON * sqrt(alpha * beta)) continue;
+                changed = 1;
+                const double zeta = (beta - alpha) / (2.0 * gamma);
+                const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+                const double c = 1.0 / sqrt(1.0 + t * t), s = c * t;
+                arow[p] = c * ap0 - s * aq0;
+                arow[q] = s * ap0 + c * aq0;
+                const double vp = vrow[p], vq = vrow[q];
+                vrow[p] = c * vp - s * vq;
+                vrow[q] = s * vp + c * vq;
+            }
+        if (!changed) break;
+    }
+    double ww[12];
+#pragma unroll
+    for (int j = 0; j < 12; j++) {
+        ww[j] = sqrt(group_sum16(arow[j] * arow[j]));
+        ord[j] = j;
+    }
+#pragma unroll
+    for (int j = 0; j < 12; j++) {
+        int b = j;
+        double wb = ww[j];
+#pragma unroll
+        for (int k = j + 1; k < 12; k++)
+            if (ww[k] > wb) {
+                b = k;
+                wb = ww[k];
+            }
+#pragma unroll
+        for (int k = j + 1; k < 12; k++)
+            if (k == b) {
+                const double tw = ww[j];
+                ww[j] = ww[k];
+                ww[k] = tw;
+                const int to = ord[j];
+                ord[j] = ord[k];
+                ord[k] = to;
+            }
     }
 }
 
 // cvSolve(A, b, x, CV_SVD): least squares over w > n * DBL_EPSILON * w[0]
-__device__ void svd_solve(int m, int n, const double* A, const double* b, double* x) {
-    double w[12], U[72], V[36];
-    svdj(m, n, A, w, U, V);
-    const double thr = n * DBL_EPSILON * w[0];
-    double y[6];
-    for (int j = 0; j < n; j++) {
+template <int M, int N>
+__device__ void svd_solve(const double* A, const double* b, double* x) {
+    double w[N], U[M * N], V[N * N];
+    svdj<M, N>(A, w, U, V);
+    const double thr = N * DBL_EPSILON * w[0];
+    double y[N];
+#pragma unroll
+    for (int j = 0; j < N; j++) {
         double s = 0;
-        for (int i = 0; i < m; i++) s += U[i * n + j] * b[i];
+#pragma unroll
+        for (int i = 0; i < M; i++) s += U[i * N + j] * b[i];
         y[j] = w[j] > thr ? s / w[j] : 0.0;
     }
-    for (int i = 0; i < n; i++) {
+#pragma unroll
+    for (int i = 0; i < N; i++) {
         double s = 0;
-        for (int j = 0; j < n; j++) s += V[i * n + j] * y[j];
+#pragma unroll
+        for (int j = 0; j < N; j++) s += V[i * N + j] * y[j];
         x[i] = s;
     }
 }
@@ -166,7 +274,7 @@ __device__ void rod_v2m(const double* r, double* R, double* J) {
 // cvRodrigues2 matrix -> vector (R := U V^T first)
 __device__ void rod_m2v(const double* Rin, double* r) {
     double w[3], U[9], V[9], R[9];
-    svdj(3, 3, Rin, w, U, V);
+    svdj<3, 3>(Rin, w, U, V);
     for (int i = 0; i < 3; i++)
         for (int j = 0; j < 3; j++) R[i * 3 + j] = U[i * 3 + 0] * V[j * 3 + 0] + U[i * 3 + 1] * V[j * 3 + 1] + U[i * 3 + 2] * V[j * 3 + 2];
     double rx = R[7] - R[5], ry = R[2] - R[6], rz = R[3] - R[1];
@@ -252,7 +360,7 @@ struct Epnp5 {
                 for (int b = 0; b < 3; b++) PtP[a * 3 + b] += d[a] * d[b];
         }
         double dc[3], V[9];
-        svdj(3, 3, PtP, dc, nullptr, V);
+        svdj<3, 3>(PtP, dc, nullptr, V);
         for (int i = 1; i < 4; i++) {
             const double k = sqrt(dc[i - 1] / PR_MODEL_POINTS);
             for (int j = 0; j < 3; j++) cws[i][j] = cws[0][j] + k * V[j * 3 + (i - 1)];
@@ -262,7 +370,7 @@ struct Epnp5 {
         double cc[9], w[3], U[9], V[9], ci[9];
         for (int i = 0; i < 3; i++)
             for (int j = 1; j < 4; j++) cc[3 * i + j - 1] = cws[j][i] - cws[0][i];
-        svdj(3, 3, cc, w, U, V);
+        svdj<3, 3>(cc, w, U, V);
         const double thr = 3 * DBL_EPSILON * w[0];
         for (int i = 0; i < 3; i++)
             for (int j = 0; j < 3; j++) {
@@ -282,7 +390,7 @@ struct Epnp5 {
     __device__ double compute_R_and_t(const double* ut, const double* betas, double R[3][3], double t[3]) {
         for (int i = 0; i < 4; i++) ccs[i][0] = ccs[i][1] = ccs[i][2] = 0.0f;
         for (int i = 0; i < 4; i++) {
-            const double* v = ut + 12 * (11 - i);
+            const double* v = ut + 12 * (3 - i);  // ut4 row 11 - i
             for (int j = 0; j < 4; j++)
                 for (int k = 0; k < 3; k++) ccs[j][k] += betas[i] * v[3 * j + k];
         }
@@ -318,7 +426,7 @@ struct Epnp5 {
             }
         }
         double d[3], u[9], v[9];
-        svdj(3, 3, abt, d, u, v);
+        svdj<3, 3>(abt, d, u, v);
         for (int i = 0; i < 3; i++)
             for (int j = 0; j < 3; j++) R[i][j] = dot3(u + 3 * i, v + 3 * j);
         const double det = R[0][0] * R[1][1] * R[2][2] + R[0][1] * R[1][2] * R[2][0] + R[0][2] * R[1][0] * R[2][1] -
@@ -345,8 +453,9 @@ struct Epnp5 {
     }
 };
 
-__device__ void compute_L_6x10(const double* ut, double* l) {
-    const double* v[4] = {ut + 12 * 11, ut + 12 * 10, ut + 12 * 9, ut + 12 * 8};
+// ut4 = rows 8..11 of epnp.cpp's ut (the four smallest singular vectors)
+__device__ void compute_L_6x10(const double* ut4, double* l) {
+    const double* v[4] = {ut4 + 12 * 3, ut4 + 12 * 2, ut4 + 12 * 1, ut4};
     double dv[4][6][3];
     for (int i = 0; i < 4; i++) {
         int a = 0, b = 1;
@@ -388,7 +497,12 @@ __device__ void betas_approx(const double* l, const double* rho, int which, doub
     double L[30], b[5];
     for (int i = 0; i < 6; i++)
         for (int j = 0; j < nc; j++) L[i * nc + j] = l[10 * i + cols[j]];
-    svd_solve(6, nc, L, rho, b);
+    if (which == 1)
+        svd_solve<6, 4>(L, rho, b);
+    else if (which == 2)
+        svd_solve<6, 3>(L, rho, b);
+    else
+        svd_solve<6, 5>(L, rho, b);
     if (which == 1) {
         if (b[0] < 0) {
             betas[0] = sqrt(-b[0]);
@@ -507,30 +621,48 @@ __device__ void gauss_newton(const double* l, const double* rho, double* betas) 
 }
 
 // ------------------------------------------------------------------ kernels
-__global__ void k_pr_subsets(int n, int H, int* __restrict__ idx) {
+// cv::RNG draws on one lane: the multiply-with-carry step, x % n through a
+// double reciprocal with one correction (exact for x < 2^32), getSubset's
+// rule (a draw equal to an earlier index of the same subset is drawn again).
+constexpr int PR_RNG_THREADS = 64;
+__global__ __launch_bounds__(PR_RNG_THREADS) void k_pr_subsets(int n, int H, int* __restrict__ idx) {
     if (threadIdx.x != 0) return;
+    const double inv = 1.0 / (double)n;
     uint64_t state = ~(uint64_t)0;  // RNG rng((uint64)-1), ptsetreg.cpp run()
     for (int h = 0; h < H; h++) {
-        int s[PR_MODEL_POINTS];
+        int sub[PR_MODEL_POINTS];
+#pragma unroll
         for (int i = 0; i < PR_MODEL_POINTS; i++) {
+            int v;
             for (;;) {
                 state = (uint64_t)(unsigned)state * 4164903690U + (unsigned)(state >> 32);
-                s[i] = (int)((unsigned)state % (unsigned)n);
-                int j;
-                for (j = 0; j < i; j++)
-                    if (s[i] == s[j]) break;
-                if (j == i) break;
+                const uint32_t x = (uint32_t)state;
+                int64_t q = (int64_t)((double)x * inv);
+                int64_t rem = (int64_t)x - q * n;
+                if (rem < 0) rem += n;
+                if (rem >= n) rem -= n;
+                v = (int)rem;
+                bool dup = false;
+#pragma unroll
+                for (int j = 0; j < i; j++) dup |= sub[j] == v;
+                if (!dup) break;
             }
-            idx[h * PR_MODEL_POINTS + i] = s[i];
+            sub[i] = v;
         }
+#pragma unroll
+        for (int i = 0; i < PR_MODEL_POINTS; i++) idx[h * PR_MODEL_POINTS + i] = sub[i];
     }
 }
 
-__global__ __launch_bounds__(64) void k_pr_epnp(const float* __restrict__ Xw, const float* __restrict__ uv,
-                                                const int* __restrict__ idx, int H, PrK K,
-                                                double* __restrict__ model, double* __restrict__ Rproj) {
-    const int h = blockIdx.x * blockDim.x + threadIdx.x;
-    if (h >= H) return;
+__global__ __launch_bounds__(PR_EPNP_THREADS) void k_pr_epnp(const float* __restrict__ Xw,
+                                                             const float* __restrict__ uv,
+                                                             const int* __restrict__ idx, int H, PrK K,
+                                                             double* __restrict__ model, double* __restrict__ Rproj) {
+    const int r = threadIdx.x & (PR_EPNP_GROUP - 1);
+    const int h = blockIdx.x * (PR_EPNP_THREADS / PR_EPNP_GROUP) + (threadIdx.x >> 4);
+    if (h >= H) return;  // whole 16-lane groups leave together
+    // every lane of the group runs the small steps redundantly (identical
+    // arithmetic), lane r < 12 owns row r of the 12 x 12 eigenproblem
     Epnp5 e;
     e.fu = K.fx;
     e.fv = K.fy;
@@ -544,12 +676,15 @@ __global__ __launch_bounds__(64) void k_pr_epnp(const float* __restrict__ Xw, co
     }
     e.choose_control_points();
     e.compute_barycentric_coordinates();
-    double mtm[144];
-    for (int k = 0; k < 144; k++) mtm[k] = 0.0;
-    for (int i = 0; i < PR_MODEL_POINTS; i++) {  // fill_M rows 2i, 2i+1 and M^T M in row order
+    // row r of M^T M: sum over the M rows 2i, 2i+1 in order (fill_M)
+    double arow[12], vrow[12];
+#pragma unroll
+    for (int j = 0; j < 12; j++) arow[j] = 0.0;
+    for (int i = 0; i < PR_MODEL_POINTS; i++) {
         const double* as = e.alphas + 4 * i;
         double M1[12], M2[12];
         const double uu = e.us[2 * i], vv = e.us[2 * i + 1];
+#pragma unroll
         for (int j = 0; j < 4; j++) {
             M1[3 * j] = as[j] * e.fu;
             M1[3 * j + 1] = 0.0;
@@ -558,15 +693,35 @@ __global__ __launch_bounds__(64) void k_pr_epnp(const float* __restrict__ Xw, co
             M2[3 * j + 1] = as[j] * e.fv;
             M2[3 * j + 2] = as[j] * (e.vc - vv);
         }
-        for (int a = 0; a < 12; a++)
-            for (int b = 0; b < 12; b++) mtm[a * 12 + b] += M1[a] * M1[b];
-        for (int a = 0; a < 12; a++)
-            for (int b = 0; b < 12; b++) mtm[a * 12 + b] += M2[a] * M2[b];
+        double m1r = 0.0, m2r = 0.0;
+#pragma unroll
+        for (int j = 0; j < 12; j++)
+            if (j == r) {
+                m1r = M1[j];
+                m2r = M2[j];
+            }
+#pragma unroll
+        for (int j = 0; j < 12; j++) {
+            arow[j] += m1r * M1[j];
+            arow[j] += m2r * M2[j];
+        }
     }
-    double d[12], V[144], ut[144];
-    svdj(12, 12, mtm, d, nullptr, V);
-    for (int i = 0; i < 12; i++)
-        for (int j = 0; j < 12; j++) ut[i * 12 + j] = V[j * 12 + i];
+    if (r >= 12)
+#pragma unroll
+        for (int j = 0; j < 12; j++) arow[j] = 0.0;
+    int ord[12];
+    svdj12_rows(arow, vrow, r, ord);
+    // ut rows 8..11 (the four smallest singular vectors) = V columns ord[8..11]
+    double ut[48];  // ut4[(k) * 12 + j] = V(j, ord[8 + k]), V row j on lane j
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        double mine = 0.0;
+#pragma unroll
+        for (int c = 0; c < 12; c++)
+            if (c == ord[8 + k]) mine = vrow[c];
+#pragma unroll
+        for (int j = 0; j < 12; j++) ut[k * 12 + j] = __shfl(mine, j, PR_EPNP_GROUP);
+    }
     double l[60], rho[6];
     compute_L_6x10(ut, l);
     rho[0] = dist2(e.cws[0], e.cws[1]);
@@ -589,13 +744,14 @@ __global__ __launch_bounds__(64) void k_pr_epnp(const float* __restrict__ Xw, co
             }
         }
     }
-    double r[3], Rp[9];
-    rod_m2v(&bestR[0][0], r);
-    rod_v2m(r, Rp, nullptr);
+    double rv[3], Rp[9];
+    rod_m2v(&bestR[0][0], rv);
+    rod_v2m(rv, Rp, nullptr);
+    if (r != 0) return;
     double* mo = model + 6 * h;
-    mo[0] = r[0];
-    mo[1] = r[1];
-    mo[2] = r[2];
+    mo[0] = rv[0];
+    mo[1] = rv[1];
+    mo[2] = rv[2];
     mo[3] = bestt[0];
     mo[4] = bestt[1];
     mo[5] = bestt[2];
@@ -765,7 +921,7 @@ __global__ __launch_bounds__(PR_REFINE_THREADS) void k_pr_refine(const float* __
                 double A[36], x[6];
                 for (int k = 0; k < 36; k++) A[k] = JtJ[k];
                 for (int i = 0; i < 6; i++) A[i * 7] *= 1. + lambda;
-                svd_solve(6, 6, A, JtErr, x);
+                svd_solve<6, 6>(A, JtErr, x);
                 for (int i = 0; i < 6; i++) sp[i] = p[i] - x[i];
             }
             __syncthreads();
@@ -825,8 +981,10 @@ void launch_pnp_ransac(hipStream_t st, const float* Xw, const float* uv, int n, 
                        int* good, int* state, odo_pnp_ransac_result* res, uint8_t* mask_out) {
     const PrK K{(double)K4[0], (double)K4[1], (double)K4[2], (double)K4[3]};
     const float thr = (float)((double)reproj_err * (double)reproj_err);
-    hipLaunchKernelGGL(k_pr_subsets, dim3(1), dim3(64), 0, st, n, H, idx);
-    hipLaunchKernelGGL(k_pr_epnp, dim3((H + 63) / 64), dim3(64), 0, st, Xw, uv, idx, H, K, model, Rproj);
+    hipLaunchKernelGGL(k_pr_subsets, dim3(1), dim3(PR_RNG_THREADS), 0, st, n, H, idx);
+    const int hyp_per_block = PR_EPNP_THREADS / PR_EPNP_GROUP;
+    hipLaunchKernelGGL(k_pr_epnp, dim3((H + hyp_per_block - 1) / hyp_per_block), dim3(PR_EPNP_THREADS), 0, st, Xw,
+                       uv, idx, H, K, model, Rproj);
     hipLaunchKernelGGL(k_pr_count, dim3(H), dim3(PR_COUNT_THREADS), 0, st, Xw, uv, n, K, thr, model, Rproj, mask,
                        good);
     hipLaunchKernelGGL(k_pr_fold, dim3(1), dim3(64), 0, st, good, n, H, confidence, state);

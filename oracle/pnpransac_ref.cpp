@@ -95,6 +95,78 @@ void svdj(int m, int n, const double* A, double* w, double* U, double* V) {
     }
 }
 
+// The sum of 12 row values as the GPU's 16-lane xor butterfly forms it on its
+// first lane (rows 12..15 are zero): ((x0+x8)+(x4+x12)) + ((x2+x10)+(x6+x14))
+// + ... — the summation order of the 12 x 12 EPnP eigenproblem (pinned choice).
+double tree16(const double* x) {
+    double y[16];
+    for (int i = 0; i < 16; i++) y[i] = i < 12 ? x[i] : 0.0;
+    for (int o = 8; o >= 1; o >>= 1) {
+        double z[16];
+        for (int i = 0; i < 16; i++) z[i] = y[i] + y[i ^ o];
+        memcpy(y, z, sizeof(y));
+    }
+    return y[0];
+}
+
+// svdj for the 12 x 12 M^T M with tree16 column sums; V only.
+void svdj12(const double* A, double* w, double* V) {
+    double a[144], v[144];
+    memcpy(a, A, sizeof(a));
+    for (int i = 0; i < 12; i++)
+        for (int j = 0; j < 12; j++) v[i * 12 + j] = i == j ? 1.0 : 0.0;
+    for (int sweep = 0; sweep < 60; sweep++) {
+        int changed = 0;
+        for (int p = 0; p < 11; p++)
+            for (int q = p + 1; q < 12; q++) {
+                double pp[12], qq[12], pq[12];
+                for (int i = 0; i < 12; i++) {
+                    const double ap = a[i * 12 + p], aq = a[i * 12 + q];
+                    pp[i] = ap * ap;
+                    qq[i] = aq * aq;
+                    pq[i] = ap * aq;
+                }
+                const double alpha = tree16(pp), beta = tree16(qq), gamma = tree16(pq);
+                if (gamma == 0.0 || std::fabs(gamma) <= DBL_EPSILON * std::sqrt(alpha * beta)) continue;
+                changed = 1;
+                const double zeta = (beta - alpha) / (2.0 * gamma);
+                const double t = (zeta >= 0 ? 1.0 : -1.0) / (std::fabs(zeta) + std::sqrt(1.0 + zeta * zeta));
+                const double c = 1.0 / std::sqrt(1.0 + t * t), s = c * t;
+                for (int i = 0; i < 12; i++) {
+                    const double ap = a[i * 12 + p], aq = a[i * 12 + q];
+                    a[i * 12 + p] = c * ap - s * aq;
+                    a[i * 12 + q] = s * ap + c * aq;
+                }
+                for (int i = 0; i < 12; i++) {
+                    const double vp = v[i * 12 + p], vq = v[i * 12 + q];
+                    v[i * 12 + p] = c * vp - s * vq;
+                    v[i * 12 + q] = s * vp + c * vq;
+                }
+            }
+        if (!changed) break;
+    }
+    double ww[12];
+    for (int j = 0; j < 12; j++) {
+        double sq[12];
+        for (int i = 0; i < 12; i++) sq[i] = a[i * 12 + j] * a[i * 12 + j];
+        ww[j] = std::sqrt(tree16(sq));
+    }
+    int ord[12];
+    for (int j = 0; j < 12; j++) ord[j] = j;
+    for (int j = 0; j < 12; j++) {
+        int b = j;
+        for (int k = j + 1; k < 12; k++)
+            if (ww[ord[k]] > ww[ord[b]]) b = k;
+        const int t = ord[j];
+        ord[j] = ord[b];
+        ord[b] = t;
+    }
+    for (int j = 0; j < 12; j++) {
+        w[j] = ww[ord[j]];
+        for (int i = 0; i < 12; i++) V[i * 12 + j] = v[i * 12 + ord[j]];
+    }
+}
+
 // cvSolve(A, b, x, CV_SVD) for m x n (m >= n): x = V diag(1/w) U^T b over
 // singular values above n * DBL_EPSILON * w[0].
 void svd_solve(int m, int n, const double* A, const double* b, double* x) {
@@ -533,8 +605,8 @@ struct Epnp {
         for (int r = 0; r < 2 * n; r++)  // cvMulTransposed(M, MtM, 1)
             for (int a = 0; a < 12; a++)
                 for (int b = 0; b < 12; b++) mtm[a * 12 + b] += M[(size_t)r * 12 + a] * M[(size_t)r * 12 + b];
-        double d[12], U[144], V[144], ut[144];
-        svdj(12, 12, mtm, d, U, V);
+        double d[12], V[144], ut[144];
+        svdj12(mtm, d, V);
         for (int i = 0; i < 12; i++)
             for (int j = 0; j < 12; j++) ut[i * 12 + j] = V[j * 12 + i];  // symmetric PSD: U = V
         double l[60], rho[6];
