@@ -287,6 +287,19 @@ class Odometry:
                                       ptr(res), ptr(mask), ptr(good)))
         return res, mask[:n].astype(bool), good
 
+    def gicp(self, src, tgt, guess=None, max_iterations: int = 10, max_corr_dist: float = 0.07):
+        """GeneralizedICP(max_iterations, max_corr_dist)::Compute(source, target,
+        guess) (generalizedicp.cpp:30-39, 65-89) on the GPU. Returns
+        (T12 4x4, converged, iterations, n_corr)."""
+        src = np.ascontiguousarray(src, np.float32).reshape(-1, 3)
+        tgt = np.ascontiguousarray(tgt, np.float32).reshape(-1, 3)
+        g = np.ascontiguousarray(np.eye(4, dtype=np.float32) if guess is None else guess, np.float32)
+        T = np.zeros(16, np.float32)
+        conv, it, nc = C.c_int(), C.c_int(), C.c_int()
+        check(self.lib.odo_gicp(self.h, ptr(src), src.shape[0], ptr(tgt), tgt.shape[0], ptr(g), max_iterations,
+                                max_corr_dist, ptr(T), C.byref(conv), C.byref(it), C.byref(nc)))
+        return T.reshape(4, 4), conv.value, it.value, nc.value
+
     def timings(self):
         ms = np.zeros(16, np.float32)
         names = (C.c_char_p * 16)()

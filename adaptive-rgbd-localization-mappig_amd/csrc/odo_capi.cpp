@@ -2261,6 +2261,43 @@ int odo_pnp_ransac(odo_ctx* c, const float* Xw, const float* uv, int n, const od
     return ODO_OK;
 }
 
+int odo_gicp(odo_ctx* c, const float* src, int ns, const float* tgt, int nt, const float guess[16], int max_iterations,
+             double max_corr_dist, float T12[16], int* converged, int* iterations, int* n_corr) {
+    if (!c || ns < 0 || nt < 0 || (ns && !src) || (nt && !tgt) || !T12 || !converged || !iterations || !n_corr)
+        return fail(ODO_ERR_ARG, "bad gicp args");
+    *converged = 0;
+    *iterations = 0;
+    *n_corr = 0;
+    for (int i = 0; i < 16; i++) T12[i] = i % 5 == 0 ? 1.f : 0.f;
+    if (ns < 20 || nt < 20) return ODO_OK;  // generalizedicp.cpp:33
+    if (ns > 65536 || nt > 65536) return fail(ODO_ERR_CAPACITY, "gicp: more than 65536 points");
+    GicpArgs args{};
+    for (int i = 0; i < 16; i++) args.guess[i] = guess ? guess[i] : (i % 5 == 0 ? 1.f : 0.f);
+    args.max_corr_dist = max_corr_dist;
+    args.max_iterations = max_iterations;
+    args.max_inner = 20;  // PCL's max_inner_iterations_
+    hipStream_t st = c->stream;
+    DevArena& A = c->arena;
+    A.begin();
+    DevBuf ds(A, (size_t)ns * 12), dt(A, (size_t)nt * 12), dCs(A, (size_t)ns * 72), dCt(A, (size_t)nt * 72),
+        dout(A, (size_t)ns * 12), dM(A, (size_t)ns * 72), dis(A, (size_t)ns * 4), dit(A, (size_t)ns * 4), dT(A, 64),
+        dio(A, 16);
+    ARENA_CHECK(A);
+    HIPCHK(hipMemcpyAsync(ds.p, src, (size_t)ns * 12, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(dt.p, tgt, (size_t)nt * 12, hipMemcpyHostToDevice, st));
+    launch_gicp(st, ds.as<float>(), ns, dt.as<float>(), nt, dCs.as<double>(), dCt.as<double>(), dout.as<float>(),
+                dM.as<double>(), dis.as<int>(), dit.as<int>(), args, dT.as<float>(), dio.as<int>());
+    HIPCHK(hipGetLastError());
+    int io[4];
+    HIPCHK(hipMemcpyAsync(T12, dT.p, 64, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(io, dio.p, 16, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    *converged = io[0];
+    *iterations = io[1];
+    *n_corr = io[2];
+    return ODO_OK;
+}
+
 // Frame::ComputeImageBounds: cv::undistortPoints of the four corners (5
 // iterations in double, App. A.10)
 static void undistort_host(float u, float v, const odo_calib& c, float* uo, float* vo) {

@@ -227,6 +227,15 @@ void launch_pnp(hipStream_t st, const int32_t* f2_src, const float* xyz, const f
                 const int* n_matches, int min_matches, void* edges, odo_pair_result* res, uint8_t* inlier_mask,
                 int npairs, const int* sel = nullptr, int sel_val = 0);
 void launch_kabsch(hipStream_t st, const float* A, const float* B, int n, float* T);
+// GICP (k_gicp.hip): Cs ns*9, Ct nt*9, outp ns*3, Mah ns*9, is / it ns; outi 4
+struct GicpArgs {
+    float guess[16];
+    double max_corr_dist;
+    int max_iterations;
+    int max_inner;
+};
+void launch_gicp(hipStream_t st, const float* src, int ns, const float* tgt, int nt, double* Cs, double* Ct,
+                 float* outp, double* Mah, int* is, int* it, GicpArgs args, float* T12, int* outi);
 // PnPRansac (k_pnpransac.hip): idx H*5, model H*6, Rproj H*9, mask H*n, good H, state 3
 int pnp_ransac_max_points();
 void launch_pnp_ransac(hipStream_t st, const float* Xw, const float* uv, int n, const float K4[4], int H,

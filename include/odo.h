@@ -179,6 +179,19 @@ int odo_pnp_ransac(odo_ctx* ctx, const float* Xw, const float* uv, int n, const 
                    float reproj_err, double confidence, odo_pnp_ransac_result* res, uint8_t* inlier_mask,
                    int32_t* good_counts);
 
+/* GeneralizedICP(max_iterations, max_corr_dist)::Compute(source, target, guess)
+ * (generalizedicp.cpp:11-22, 30-39, 65-89): the PCL
+ * GICP refinement Odometry::Compute's ADAPTIVE_RICP mode runs on RANSAC's
+ * matched clouds (odometry.cpp:46-78; the reference builds it with 10
+ * iterations and 0.07 m). src/tgt: n x 3 (Ransac::mpSourceCloud /
+ * mpTargetCloud). Fewer than 20 points in either cloud: *converged = 0 without
+ * running (generalizedicp.cpp:33). T12 = the final transformation when
+ * converged, identity otherwise (generalizedicp.cpp:76-88); iterations = ICP
+ * iterations run, n_corr = correspondences of the last one. Covariances,
+ * correspondences and the BFGS all run on the GPU (k_gicp.hip). */
+int odo_gicp(odo_ctx* ctx, const float* src, int ns, const float* tgt, int nt, const float guess[16],
+             int max_iterations, double max_corr_dist, float T12[16], int* converged, int* iterations, int* n_corr);
+
 /* ---- Trajectory (host only) ----
  * Relative-pose chain of the batched contract: results[i].Tcw is frame i's
  * pose in frame i-1's camera coordinates, so Tcw(i) = Tcw_rel(i) * Tcw(i-1)

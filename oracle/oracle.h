@@ -189,6 +189,17 @@ void oracle_rodrigues_inv(const double R[9], double r[3]);
 void oracle_epnp(const double* pw, const double* uv, int n, const double K[4], double model[6]);
 void oracle_pnp_refine(const double* M, const double* m, int n, const double K[4], double param[6]);
 
+/* ---- GeneralizedICP::Compute(source, target, guess) (generalizedicp.cpp:30-39,
+ * 65-89; SURVEY §8(f) rank 4, the ADAPTIVE_RICP fallback of odometry.cpp:46-78):
+ * PCL 1.8 GICP restated in gicp_ref.cpp. src/tgt: n x 3. Returns 1 when
+ * hasConverged (T12 = final transformation), 0 otherwise (T12 = identity,
+ * generalizedicp.cpp:84-87). iterations: outer ICP iterations run; n_corr:
+ * correspondences of the last one. */
+int oracle_gicp(const float* src, int ns, const float* tgt, int nt, const float* guess, int max_iterations,
+                double max_corr_dist, float* T12, int* converged, int* iterations, int* n_corr);
+/* computeCovariances (k 20, epsilon 1e-3): n x 9 doubles. */
+void oracle_gicp_covariances(const float* P, int n, double* C);
+
 /* Kabsch::Compute (kabsch.cpp:14-57). */
 void oracle_kabsch(const float* A, const float* B, int n, float* T);
 

@@ -136,6 +136,8 @@ def lib():
             "oracle_rodrigues_inv": (None, [P, P]),
             "oracle_epnp": (None, [P, P, C.c_int, P, P]),
             "oracle_pnp_refine": (None, [P, P, C.c_int, P, P]),
+            "oracle_gicp": (C.c_int, [P, C.c_int, P, C.c_int, P, C.c_int, C.c_double, P, P, P, P]),
+            "oracle_gicp_covariances": (None, [P, C.c_int, P]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -292,3 +294,15 @@ def pnp_ransac(Xw, uv, calib: Calib, iterations=500, reproj=3.0, confidence=0.85
                                  ptr(rt), ptr(T), ptr(mask), C.byref(ni), C.byref(bi), C.byref(nit), ptr(good))
     return dict(ok=ok, model=model, rt=rt, T=T.reshape(4, 4), mask=mask[:n].astype(bool), n_inliers=ni.value,
                 best_iter=bi.value, niters=nit.value, good=good[:nit.value])
+
+
+def gicp(src, tgt, guess=None, max_iterations=10, max_corr_dist=0.07):
+    """GeneralizedICP(iters, dist)::Compute(source, target, guess) on the oracle."""
+    src = np.ascontiguousarray(src, np.float32)
+    tgt = np.ascontiguousarray(tgt, np.float32)
+    g = np.ascontiguousarray(np.eye(4, dtype=np.float32) if guess is None else guess, np.float32)
+    T = np.zeros(16, np.float32)
+    conv, it, nc = C.c_int(), C.c_int(), C.c_int()
+    ok = lib().oracle_gicp(ptr(src), len(src), ptr(tgt), len(tgt), ptr(g), max_iterations, max_corr_dist, ptr(T),
+                           C.byref(conv), C.byref(it), C.byref(nc))
+    return dict(ok=ok, T=T.reshape(4, 4), converged=conv.value, iterations=it.value, n_corr=nc.value)
