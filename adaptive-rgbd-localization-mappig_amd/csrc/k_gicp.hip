@@ -46,25 +46,32 @@ __global__ __launch_bounds__(64) void k_gicp_cov(const float* __restrict__ P, in
                                                  double* __restrict__ C) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= n) return;
+    // the sorted top 20 in registers: +inf padding stands for "fewer than 20
+    // so far", a candidate is inserted after equal distances (ties to the lower
+    // index, as the scan is in index order)
     float nd[GI_K];
     int nn[GI_K];
+#pragma unroll
+    for (int j = 0; j < GI_K; j++) {
+        nd[j] = __builtin_inff();
+        nn[j] = 0;
+    }
     const float pq[3] = {P[3 * q], P[3 * q + 1], P[3 * q + 2]};
-    int cnt = 0;
     for (int i = 0; i < n; i++) {
         const float pi[3] = {P[3 * i], P[3 * i + 1], P[3 * i + 2]};
         const float d = dist2f(pq, pi);
-        if (cnt == GI_K && !(d < nd[GI_K - 1])) continue;
-        int pos = cnt < GI_K ? cnt : GI_K - 1;
-        while (pos > 0 && d < nd[pos - 1]) {
-            if (pos < GI_K) {
-                nd[pos] = nd[pos - 1];
-                nn[pos] = nn[pos - 1];
-            }
-            pos--;
+        if (!(d < nd[GI_K - 1])) continue;
+#pragma unroll
+        for (int j = GI_K - 1; j > 0; j--) {
+            const bool up = d < nd[j - 1];
+            const bool here = !up && d < nd[j];
+            nd[j] = up ? nd[j - 1] : (here ? d : nd[j]);
+            nn[j] = up ? nn[j - 1] : (here ? i : nn[j]);
         }
-        nd[pos] = d;
-        nn[pos] = i;
-        if (cnt < GI_K) cnt++;
+        if (d < nd[0]) {
+            nd[0] = d;
+            nn[0] = i;
+        }
     }
     double mean[3] = {0, 0, 0}, cov[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (int j = 0; j < GI_K; j++) {

@@ -412,6 +412,55 @@ def pnpransac_mode(args):
     print(json.dumps(out), flush=True)
 
 
+def gicp_mode(args):
+    """SURVEY 8(f) rank 4: GeneralizedICP(10, 0.07)::Compute(source, target,
+    T12) of Odometry::Compute's ADAPTIVE_RICP mode (odometry.cpp:46-78) on one
+    cfg2 pair: Ransac::Iterate's matched clouds (depth-valid KnnMatch pairs,
+    ransac.cpp:175-189) and the RANSAC T12 as the guess (odometry.cpp:61). A
+    latency metric: ms per odo_gicp call (host clouds in, T12 out)."""
+    import torch
+    pkg = load_pkg()
+    synth = load_synth()
+    bgr, dep, _ = synth.make_sequence(2, args.width, args.height, seed=0x5EED0002)
+    cfg = pkg.default_config(args.width, args.height, 2, nfeatures=args.nfeatures, iterations=200,
+                             seed=0x5EED0002)
+    odo = pkg.Odometry(cfg)
+    res = odo.track_batch_host(bgr, dep)
+    m = odo.pair(1)["matches"]
+    f0, f1 = odo.frame(0), odo.frame(1)
+    src, tgt = f0["xyz"][m["queryIdx"]], f1["xyz"][m["trainIdx"]]
+    ok = (src[:, 2] > 0) & (tgt[:, 2] > 0)
+    src, tgt = np.ascontiguousarray(src[ok]), np.ascontiguousarray(tgt[ok])
+    guess = np.ascontiguousarray(np.asarray(res[1]["T12"], np.float32).reshape(4, 4))
+    for _ in range(2):
+        T, conv, it, nc = odo.gicp(src, tgt, guess, 10, 0.07)
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(max(args.steps, 5)):
+        t0 = time.perf_counter()
+        T, conv, it, nc = odo.gicp(src, tgt, guess, 10, 0.07)
+        ts.append((time.perf_counter() - t0) * 1e3)
+    odo.close()
+    out = {"metric": "GeneralizedICP::Compute latency (PCL GICP on the GPU, one call)",
+           "value": round(float(np.median(ts)), 4), "unit": "ms/call (p50)", "n_gpus": 1, "steps": len(ts),
+           "higher_is_better": False, "p90_ms": round(float(np.percentile(ts, 90)), 4),
+           "points": [int(len(src)), int(len(tgt))], "converged": int(conv), "iterations": int(it),
+           "correspondences": int(nc),
+           "config": {"workload": f"cfg2 pair {args.width}x{args.height}, {args.nfeatures} kp: RANSAC's matched "
+                                  "clouds, guess = RANSAC T12, GeneralizedICP(10, 0.07)"}}
+    if not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib as O
+        cts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            O.gicp(src, tgt, guess, 10, 0.07)
+            cts.append((time.perf_counter() - t0) * 1e3)
+        out["cpu_baseline"] = {"value": round(float(np.median(cts)), 3), "unit": "ms/call (median of 3)", "cores": 1,
+                               "kind": "port", "sample": "the same call on oracle/gicp_ref.cpp"}
+    print(json.dumps(out), flush=True)
+
+
 def latency_mode(args):
     """Per-frame latency of the drop-in path: tools/build/frontend_latency runs
     one Tracking::Track frame at a time through include/odo_frontend.hpp
@@ -465,10 +514,10 @@ def main():
                     help="main leg's sequence: the cfg2 proxy or the hard variant (synth hard=True)")
     ap.add_argument("--no-kernel-timing", action="store_true", help="no events around the kNN-2 launches")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mode", choices=["track", "hyp", "latency", "pnpransac"], default="track",
+    ap.add_argument("--mode", choices=["track", "hyp", "latency", "pnpransac", "gicp"], default="track",
                     help="track: the frames/s metric; hyp: SURVEY 8(e) hypotheses mode latency (cfg3, H=4096); "
                          "latency: per-frame ms of the drop-in path through include/odo_frontend.hpp; "
-                         "pnpransac: SURVEY 8(f) rank 4 PnPRansac latency on a cfg2 pair")
+                         "pnpransac / gicp: SURVEY 8(f) rank 4 back-end latency on a cfg2 pair")
     ap.add_argument("--hyp-outliers", type=float, default=0.5, help="hyp mode: fraction of matches re-targeted")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="process group backend for N > 1 (gloo: several ranks sharing one GPU)")
@@ -485,6 +534,9 @@ def main():
         return
     if args.mode == "pnpransac":
         pnpransac_mode(args)
+        return
+    if args.mode == "gicp":
+        gicp_mode(args)
         return
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
