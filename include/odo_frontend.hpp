@@ -472,6 +472,18 @@ public:
     // from the process rand() stream (advanced by exactly the draws made),
     // evaluated on the GPU; sets rmse, mvInliers, mT12.
     bool Iterate(Frame* pF1, Frame* pF2, const std::vector<DMatch>& m12) {
+        // mpSourceCloud / mpTargetCloud (ransac.cpp:161-189): the depth-valid
+        // matched points, kept for the GICP refinement of ADAPTIVE_RICP
+        mvSourceCloud.clear();
+        mvTargetCloud.clear();
+        if (m12.size() >= (size_t)mP.min_inlier_th)
+            for (const DMatch& m : m12) {
+                const Point3f& s = pF1->mvKeys3Dc[m.queryIdx];
+                const Point3f& t = pF2->mvKeys3Dc[m.trainIdx];
+                if (mP.check_depth && (std::isnan(s.z) || std::isnan(t.z) || s.z <= 0 || t.z <= 0)) continue;
+                mvSourceCloud.insert(mvSourceCloud.end(), {s.x, s.y, s.z});
+                mvTargetCloud.insert(mvTargetCloud.end(), {t.x, t.y, t.z});
+            }
         std::vector<float> x1 = xyz(*pF1), x2 = xyz(*pF2);
         std::vector<DMatch> inl(std::max<size_t>(m12.size(), 1));
         int ninl = 0, ok = 0;
@@ -489,6 +501,7 @@ public:
     float rmse = 0.f;
     std::vector<DMatch> mvInliers;
     Pose mT12 = Identity();
+    std::vector<float> mvSourceCloud, mvTargetCloud;  // n x 3
 
 private:
     static std::vector<float> xyz(const Frame& F) {
@@ -575,6 +588,32 @@ public:
             if (inl[k]) frame.SetInlier(vnIndex[k]);
         return r.n_inliers;
     }
+};
+
+// Odometry/generalizedicp.h: GeneralizedICP(iters, maxCorrespondenceDist)
+// (generalizedicp.cpp:11-22; Odometry builds it with (10, 0.07)) and
+// Compute(source, target, guess) (generalizedicp.cpp:30-39, 65-89) over n x 3
+// clouds: mT12 = the final transformation when converged, identity otherwise.
+class GeneralizedICP {
+public:
+    GeneralizedICP() : GeneralizedICP(15, 0.05) {}
+    GeneralizedICP(int iters, double maxCorrespondenceDist) : mIters(iters), mDist(maxCorrespondenceDist) {}
+    bool Compute(const std::vector<float>& source, const std::vector<float>& target, const Pose& guess) {
+        if (source.size() % 3 || target.size() % 3) throw std::invalid_argument("GeneralizedICP::Compute: sizes");
+        int converged = 0, iters = 0, ncorr = 0;
+        Check(odo_gicp(detail::shared_ctx(), source.data(), (int)(source.size() / 3), target.data(),
+                       (int)(target.size() / 3), guess.data(), mIters, mDist, mT12.data(), &converged, &iters, &ncorr),
+              "GeneralizedICP::Compute");
+        return converged != 0;
+    }
+    void SetMaximumIterations(int iters) { mIters = iters; }
+    void SetMaxCorrespondenceDistance(double dist) { mDist = dist; }
+
+    Pose mT12 = Identity();
+
+private:
+    int mIters;
+    double mDist;
 };
 
 // Odometry/kabsch.h: Compute(setA, setB) for n x 3 row-major point sets.
