@@ -5,15 +5,16 @@
 //               (brute force, float squared distances, ties to the lower
 //               index), mean / covariance in double, eigenvalues replaced by
 //               (1, 1, 1e-3) (computeCovariances);
-//   k_gicp      one wave runs computeTransformation: per ICP iteration the
+//   k_gicp      one 4-wave workgroup runs computeTransformation: per ICP iteration the
 //               nearest target point of every transformed source point
 //               (lane-strided brute force), the Mahalanobis matrices
 //               (R C1 R^T + C2)^-1 of the pairs within the distance threshold,
 //               compaction in source order (ballot prefix), then
 //               estimateRigidTransformationBFGS: BFGS2 + Fletcher's line search
 //               with identical control flow on all lanes, the cost and gradient
-//               as lane-strided partial sums + an xor butterfly read on lane 0
-//               (oracle/gicp_ref.cpp's sum64), and the convergence test.
+//               as thread-strided partial sums, the four waves' partials of a
+//               lane position added in order, an xor butterfly read on lane 0
+//               (oracle/gicp_ref.cpp's sum256), and the convergence test.
 // The restatement, its pinned choices and the oracle are in oracle/gicp_ref.cpp
 // (PCL is absent: parity with the library is unpinned).
 #include <hip/hip_runtime.h>
@@ -28,6 +29,9 @@ namespace {
 
 constexpr int GI_K = 20;
 constexpr int GI_LANES = 64;
+constexpr int GI_THREADS = 256;  // the ICP / BFGS workgroup: 4 waves share every pass over the correspondences
+constexpr int GI_WAVES = GI_THREADS / GI_LANES;
+constexpr int GI_NV = 12;        // values reduced per gradient evaluation
 
 __device__ __forceinline__ double s3(double a, double b, double c) { return a + (b + c); }
 
@@ -42,9 +46,15 @@ __device__ __forceinline__ float dist2f(const float* a, const float* b) {
     return r;
 }
 
-__global__ __launch_bounds__(64) void k_gicp_cov(const float* __restrict__ P, int n, double eps,
-                                                 double* __restrict__ C) {
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+// blocks [0, nb_a) cover cloud A, the rest cloud B (both clouds in one launch)
+__global__ __launch_bounds__(64) void k_gicp_cov(const float* __restrict__ PA, int na, double* __restrict__ CA,
+                                                 const float* __restrict__ PB, int nb, double* __restrict__ CB,
+                                                 int nb_a, double eps) {
+    const bool first = (int)blockIdx.x < nb_a;
+    const float* __restrict__ P = first ? PA : PB;
+    double* __restrict__ C = first ? CA : CB;
+    const int n = first ? na : nb;
+    const int q = (first ? blockIdx.x : blockIdx.x - nb_a) * blockDim.x + threadIdx.x;
     if (q >= n) return;
     // the sorted top 20 in registers: +inf padding stands for "fewer than 20
     // so far", a candidate is inserted after equal distances (ties to the lower
@@ -170,11 +180,25 @@ __device__ void apply_state(const double* x, float* T) {
     T[15] = 1.f;
 }
 
-// lane-strided partial sums are formed by the caller; this is the butterfly
-__device__ __forceinline__ double wave_sum(double v) {
+// oracle/gicp_ref.cpp's sum256: thread t's partial over k = t, t + 256, ...;
+// lane l of wave 0 adds the four waves' partials of position l in wave order,
+// then an xor butterfly read on lane 0; the NV results are broadcast via LDS.
+template <int NV>
+__device__ void block_sum256(double* v, double (*red)[GI_THREADS], double* out) {
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, GI_LANES);
-    return __shfl(v, 0, GI_LANES);
+    for (int k = 0; k < NV; k++) red[k][threadIdx.x] = v[k];
+    __syncthreads();
+    if (threadIdx.x < GI_LANES) {
+#pragma unroll
+        for (int k = 0; k < NV; k++) {
+            double z = ((red[k][threadIdx.x] + red[k][threadIdx.x + 64]) + red[k][threadIdx.x + 128]) +
+                       red[k][threadIdx.x + 192];
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) z += __shfl_xor(z, o, GI_LANES);
+            if (threadIdx.x == 0) out[k] = z;
+        }
+    }
+    __syncthreads();
 }
 
 struct GiProblem {
@@ -184,13 +208,15 @@ struct GiProblem {
     const int* it;
     const double* M;
     int m;
+    double (*red)[GI_THREADS];  // LDS [GI_NV][GI_THREADS]
+    double* bc;                 // LDS [GI_NV]
 };
 
 __device__ double gi_cost(const GiProblem& P, const double* x) {
     float T[16];
     apply_state(x, T);
     double part = 0.0;
-    for (int k = threadIdx.x; k < P.m; k += GI_LANES) {
+    for (int k = threadIdx.x; k < P.m; k += GI_THREADS) {
         const int si = P.is[k];
         const float ps[3] = {P.src[3 * si], P.src[3 * si + 1], P.src[3 * si + 2]};
         float pp[3];
@@ -203,7 +229,8 @@ __device__ double gi_cost(const GiProblem& P, const double* x) {
         for (int i = 0; i < 3; i++) t[i] = s3(M[3 * i] * r[0], M[3 * i + 1] * r[1], M[3 * i + 2] * r[2]);
         part += s3(r[0] * t[0], r[1] * t[1], r[2] * t[2]);
     }
-    return wave_sum(part) / P.m;
+    block_sum256<1>(&part, P.red, P.bc);
+    return P.bc[0] / P.m;
 }
 
 __device__ void gi_grad(const GiProblem& P, const double* x, double* g) {
@@ -212,7 +239,7 @@ __device__ void gi_grad(const GiProblem& P, const double* x, double* g) {
     double part[12];
 #pragma unroll
     for (int i = 0; i < 12; i++) part[i] = 0.0;
-    for (int k = threadIdx.x; k < P.m; k += GI_LANES) {
+    for (int k = threadIdx.x; k < P.m; k += GI_THREADS) {
         const int si = P.is[k];
         const float ps[3] = {P.src[3 * si], P.src[3 * si + 1], P.src[3 * si + 2]};
         float pp[3];
@@ -231,10 +258,11 @@ __device__ void gi_grad(const GiProblem& P, const double* x, double* g) {
             for (int b = 0; b < 3; b++) part[3 + 3 * a + b] += (double)ps[a] * t[b];
     }
     double Rm[9];
+    block_sum256<GI_NV>(part, P.red, P.bc);
 #pragma unroll
-    for (int i = 0; i < 3; i++) g[i] = wave_sum(part[i]) * (2.0 / P.m);
+    for (int i = 0; i < 3; i++) g[i] = P.bc[i] * (2.0 / P.m);
 #pragma unroll
-    for (int i = 0; i < 9; i++) Rm[i] = wave_sum(part[3 + i]) * (2.0 / P.m);
+    for (int i = 0; i < 9; i++) Rm[i] = P.bc[3 + i] * (2.0 / P.m);
     const double phi = x[3], theta = x[4], psi = x[5];
     const double cphi = cos(phi), sphi = sin(phi), ctheta = cos(theta), stheta = sin(theta), cpsi = cos(psi),
                  spsi = sin(psi);
@@ -554,14 +582,17 @@ struct GiBfgs {
 };
 
 // out[4]: converged, iterations, n_corr, (pad); T12[16]
-__global__ __launch_bounds__(GI_LANES) void k_gicp(const float* __restrict__ src, int ns, const float* __restrict__ tgt,
+__global__ __launch_bounds__(GI_THREADS) void k_gicp(const float* __restrict__ src, int ns, const float* __restrict__ tgt,
                                                    int nt, const double* __restrict__ Cs, const double* __restrict__ Ct,
                                                    float* __restrict__ outp, double* __restrict__ Mah,
                                                    int* __restrict__ is, int* __restrict__ it, GicpArgs A,
                                                    float* __restrict__ T12, int* __restrict__ outi) {
-    const int lane = threadIdx.x;
+    __shared__ double red[GI_NV][GI_THREADS];
+    __shared__ double bc[GI_NV];
+    __shared__ int wcnt[GI_WAVES];
+    const int lane = threadIdx.x & (GI_LANES - 1), wave = threadIdx.x / GI_LANES;
     const float* guess = A.guess;
-    for (int i = lane; i < ns; i += GI_LANES) {  // transformPointCloud(output, output, guess)
+    for (int i = threadIdx.x; i < ns; i += GI_THREADS) {  // transformPointCloud(output, output, guess)
         const float p0 = src[3 * i], p1 = src[3 * i + 1], p2 = src[3 * i + 2];
 #pragma unroll
         for (int r = 0; r < 3; r++)
@@ -585,8 +616,8 @@ __global__ __launch_bounds__(GI_LANES) void k_gicp(const float* __restrict__ src
                 R[3 * i + j] = s;
             }
         int base = 0;
-        for (int i0 = 0; i0 < ns; i0 += GI_LANES) {
-            const int i = i0 + lane;
+        for (int i0 = 0; i0 < ns; i0 += GI_THREADS) {
+            const int i = i0 + threadIdx.x;
             bool hit = false;
             int best = 0;
             if (i < ns) {
@@ -625,16 +656,26 @@ __global__ __launch_bounds__(GI_LANES) void k_gicp(const float* __restrict__ src
                     for (int k = 0; k < 9; k++) Mah[9 * i + k] = Mi[k];
                 }
             }
+            // compaction in source order: ballot within the wave, wave counts in order
             const uint64_t bal = __ballot(hit);
-            const int pos = base + __popcll(bal & ((1ull << lane) - 1ull));
+            if (lane == 0) wcnt[wave] = __popcll(bal);
+            __syncthreads();
+            int pre = base, tot = 0;
+#pragma unroll
+            for (int w = 0; w < GI_WAVES; w++) {
+                if (w < wave) pre += wcnt[w];
+                tot += wcnt[w];
+            }
+            const int pos = pre + __popcll(bal & ((1ull << lane) - 1ull));
             if (hit) {
                 is[pos] = i;
                 it[pos] = best;
             }
-            base += __popcll(bal);
+            base += tot;
+            __syncthreads();
         }
-        __syncthreads();
         __threadfence_block();
+        __syncthreads();
         ncorr = base;
 #pragma unroll
         for (int i = 0; i < 16; i++) Tprev[i] = Tcur[i];
@@ -642,7 +683,7 @@ __global__ __launch_bounds__(GI_LANES) void k_gicp(const float* __restrict__ src
         double x[6] = {Tcur[3], Tcur[7], Tcur[11], (double)(float)atan2((double)Tcur[9], (double)Tcur[10]), (double)(float)asin(-(double)Tcur[8]),
                        (double)(float)atan2((double)Tcur[4], (double)Tcur[0])};
         GiBfgs bf;
-        bf.P = GiProblem{outp, tgt, is, it, Mah, base};
+        bf.P = GiProblem{outp, tgt, is, it, Mah, base, red, bc};
         bf.minimizeInit(x);
         int inner = 0, result;
         do {
@@ -672,7 +713,7 @@ __global__ __launch_bounds__(GI_LANES) void k_gicp(const float* __restrict__ src
             for (int i = 0; i < 16; i++) Tprev[i] = Tcur[i];
         }
     }
-    if (lane == 0) {
+    if (threadIdx.x == 0) {
         outi[0] = conv;
         outi[1] = nr_iterations;
         outi[2] = ncorr;
@@ -688,9 +729,9 @@ __global__ __launch_bounds__(GI_LANES) void k_gicp(const float* __restrict__ src
 
 void launch_gicp(hipStream_t st, const float* src, int ns, const float* tgt, int nt, double* Cs, double* Ct,
                  float* outp, double* Mah, int* is, int* it, GicpArgs args, float* T12, int* outi) {
-    hipLaunchKernelGGL(k_gicp_cov, dim3((nt + 63) / 64), dim3(64), 0, st, tgt, nt, 1e-3, Ct);
-    hipLaunchKernelGGL(k_gicp_cov, dim3((ns + 63) / 64), dim3(64), 0, st, src, ns, 1e-3, Cs);
-    hipLaunchKernelGGL(k_gicp, dim3(1), dim3(GI_LANES), 0, st, src, ns, tgt, nt, Cs, Ct, outp, Mah, is, it, args, T12,
+    const int nb_t = (nt + 63) / 64, nb_s = (ns + 63) / 64;
+    hipLaunchKernelGGL(k_gicp_cov, dim3(nb_t + nb_s), dim3(64), 0, st, tgt, nt, Ct, src, ns, Cs, nb_t, 1e-3);
+    hipLaunchKernelGGL(k_gicp, dim3(1), dim3(GI_THREADS), 0, st, src, ns, tgt, nt, Cs, Ct, outp, Mah, is, it, args, T12,
                        outi);
 }
 

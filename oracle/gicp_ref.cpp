@@ -16,9 +16,10 @@
 //     accumulates column by column; AngleAxisf products via quaternions;
 //   * float cos / sin / atan2 / asin (AngleAxisf, the initial Euler angles) are
 //     the double functions rounded to float;
-//   * every sum over correspondences (cost, gradient) is the 64-lane form of the
-//     GPU: lane l sums k = l, l + 64, ... in order, then an xor butterfly
-//     32 .. 1 read on lane 0 (sum64 below).
+//   * every sum over correspondences (cost, gradient) is the 256-thread form of
+//     the GPU: thread t sums k = t, t + 256, ... in order, lane position l adds
+//     the partials of threads l, l + 64, l + 128, l + 192 in that order, then an
+//     xor butterfly 32 .. 1 read on lane 0 (sum256 below).
 #include <cfloat>
 #include <cmath>
 #include <cstring>
@@ -199,14 +200,15 @@ void apply_state(const double* x, float* T) {
     T[15] = 1.f;
 }
 
-// the GPU's 64-lane sum of values v[0..m) (see the header)
-double sum64(const std::vector<double>& v) {
-    double y[64];
-    for (int l = 0; l < 64; l++) {
+// the GPU's 256-thread sum of values v[0..m) (see the header)
+double sum256(const std::vector<double>& v) {
+    double t256[256], y[64];
+    for (int t = 0; t < 256; t++) {
         double s = 0.0;
-        for (size_t k = l; k < v.size(); k += 64) s += v[k];
-        y[l] = s;
+        for (size_t k = t; k < v.size(); k += 256) s += v[k];
+        t256[t] = s;
     }
+    for (int l = 0; l < 64; l++) y[l] = ((t256[l] + t256[l + 64]) + t256[l + 128]) + t256[l + 192];
     for (int o = 32; o >= 1; o >>= 1) {
         double z[64];
         for (int i = 0; i < 64; i++) z[i] = y[i] + y[i ^ o];
@@ -238,7 +240,7 @@ double cost(const Problem& P, const double* x) {
         for (int i = 0; i < 3; i++) t[i] = s3(M[3 * i] * r[0], M[3 * i + 1] * r[1], M[3 * i + 2] * r[2]);
         v[k] = s3(r[0] * t[0], r[1] * t[1], r[2] * t[2]);
     }
-    return sum64(v) / P.m;
+    return sum256(v) / P.m;
 }
 
 void grad(const Problem& P, const double* x, double* g) {
@@ -260,8 +262,8 @@ void grad(const Problem& P, const double* x, double* g) {
             for (int b = 0; b < 3; b++) v[3 + 3 * a + b][k] = (double)ps[a] * t[b];
     }
     double Rm[9];
-    for (int i = 0; i < 3; i++) g[i] = sum64(v[i]) * (2.0 / P.m);
-    for (int i = 0; i < 9; i++) Rm[i] = sum64(v[3 + i]) * (2.0 / P.m);
+    for (int i = 0; i < 3; i++) g[i] = sum256(v[i]) * (2.0 / P.m);
+    for (int i = 0; i < 9; i++) Rm[i] = sum256(v[3 + i]) * (2.0 / P.m);
     // computeRDerivative
     const double phi = x[3], theta = x[4], psi = x[5];
     const double cphi = cos(phi), sphi = sin(phi), ctheta = cos(theta), stheta = sin(theta), cpsi = cos(psi),
