@@ -616,6 +616,59 @@ private:
     double mDist;
 };
 
+// Odometry/odometry.h: the pose back-end dispatcher (odometry.cpp:10-117).
+// ADAPTIVE_RBA is the reference's (System/tracking.cpp); ADAPTIVE_RICP refines
+// a weak RANSAC with GICP on RANSAC's matched clouds; ICP is "not implemented
+// yet" in the reference and does nothing here either.
+class Odometry {
+public:
+    enum eAlgorithm { RANSAC = 0, ICP, MOTION_ONLY_BA, ADAPTIVE_RICP, ADAPTIVE_RBA };
+
+    explicit Odometry(eAlgorithm algorithm)
+        : mRansac(200, 20, 3.0f, 4), mGicp(10, 0.07), mOdometryAlgorithm(algorithm) {}
+
+    void Compute(Frame* pF1, Frame* pF2, const std::vector<DMatch>& vMatches12) {
+        switch (mOdometryAlgorithm) {
+        case ADAPTIVE_RICP: {  // odometry.cpp:46-78
+            mRansac.Iterate(pF1, pF2, vMatches12);
+            Pose T12 = mRansac.mT12;
+            if (mRansac.mvInliers.size() < 20 || mRansac.rmse * 10.0f >= 7.0f) {
+                if (mRansac.rmse * 10.0f >= 20)
+                    T12 = mGicp.Compute(mRansac.mvSourceCloud, mRansac.mvTargetCloud, Identity()) ? mGicp.mT12
+                                                                                                 : Identity();
+                else
+                    T12 = mGicp.Compute(mRansac.mvSourceCloud, mRansac.mvTargetCloud, mRansac.mT12) ? mGicp.mT12
+                                                                                                   : mRansac.mT12;
+            }
+            pF2->SetPose(Mul(T12, pF1->GetPose()));
+            for (const DMatch& m : mRansac.mvInliers) pF2->SetInlier((size_t)m.trainIdx);
+            break;
+        }
+        case RANSAC:  // odometry.cpp:81-92
+            mRansac.Iterate(pF1, pF2, vMatches12);
+            pF2->SetPose(Mul(mRansac.mT12, pF1->GetPose()));
+            for (const DMatch& m : mRansac.mvInliers) pF2->SetInlier((size_t)m.trainIdx);
+            break;
+        case ICP:  // odometry.cpp:95-97
+            break;
+        case MOTION_ONLY_BA:  // odometry.cpp:100-102
+            PnPSolver::Compute(pF2);
+            break;
+        case ADAPTIVE_RBA:  // odometry.cpp:105-116
+            mRansac.Iterate(pF1, pF2, vMatches12);
+            pF2->SetPose(Mul(mRansac.mT12, pF1->GetPose()));
+            PnPSolver::Compute(pF2);
+            break;
+        }
+    }
+
+    Ransac mRansac;
+    GeneralizedICP mGicp;
+
+private:
+    eAlgorithm mOdometryAlgorithm;
+};
+
 // Odometry/kabsch.h: Compute(setA, setB) for n x 3 row-major point sets.
 class Kabsch {
 public:

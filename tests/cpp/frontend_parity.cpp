@@ -11,6 +11,8 @@
 //   KnnMatch list                  bit-exact   (oracle_track_pair)
 //   Ransac mT12, inliers, rmse     bit-exact
 //   PnPSolver pose                 |dT| < 1e-4, inlier count and outlier flags equal
+//   GeneralizedICP on RANSAC's clouds from T12 (ADAPTIVE_RICP)   converged, |dT| < 1e-5
+//   PnPRansac on the frame's landmarks                           inlier count, |dT| < 1e-5
 //
 // usage: frontend_parity FRAMES.bin W H F SEED [adaptive|adaptive_orb]
 //   FRAMES.bin = F x H x W x 3 BGR8, then F x H x W depth16 (x5000)
@@ -165,7 +167,7 @@ static int run(int argc, char** argv) {
     std::unique_ptr<odo_hip::Frame> last;
     OracleFrame olast;
     long total_matches = 0, total_inliers = 0, total_pnp = 0;
-    int proj_checked = -1;
+    int proj_checked = -1, gicp_checked = 0, pnpransac_checked = 0;
     double max_dT = 0;
     for (int t = 0; t < F; t++) {
         auto cur = std::make_unique<odo_hip::Frame>(&bgr[npx * 3 * t], &dep[npx * t], W, H, 0.033 * t);
@@ -254,6 +256,49 @@ static int run(int argc, char** argv) {
                 EXPECT(flag_diff == 0, "pair %d: %d PnP outlier flags differ", t, flag_diff);
                 total_inliers += r.n_inliers;
                 total_pnp += pnp;
+                // GeneralizedICP(10, 0.07) on RANSAC's matched clouds from T12
+                // (ADAPTIVE_RICP, odometry.cpp:61) vs the oracle on the same clouds
+                {
+                    odo_hip::GeneralizedICP gicp(10, 0.07);
+                    const bool gok = gicp.Compute(ransac.mvSourceCloud, ransac.mvTargetCloud, T12);
+                    float Tg[16];
+                    int conv = 0, it = 0, nc = 0;
+                    oracle_gicp(ransac.mvSourceCloud.data(), (int)(ransac.mvSourceCloud.size() / 3),
+                                ransac.mvTargetCloud.data(), (int)(ransac.mvTargetCloud.size() / 3), T12.data(), 10,
+                                0.07, Tg, &conv, &it, &nc);
+                    EXPECT(gok == (conv != 0), "pair %d: GICP converged %d vs %d", t, (int)gok, conv);
+                    double dg = 0;
+                    for (int k = 0; k < 16; k++) dg = std::max(dg, (double)fabsf(gicp.mT12[k] - Tg[k]));
+                    EXPECT(dg < 1e-5, "pair %d: GICP |dT| = %g", t, dg);
+                    gicp_checked++;
+                }
+                // PnPRansac::Compute on the frame's landmarks (a copy of the frame)
+                {
+                    odo_hip::Frame fr = *cur;
+                    odo_hip::PnPRansac pr;
+                    vector<float> Xw, uv;
+                    for (size_t i = 0; i < fr.N; i++)
+                        if (fr.GetLandmark(i)) {
+                            const odo_hip::LandmarkPtr lm = fr.GetLandmark(i);
+                            Xw.insert(Xw.end(), {lm->mWorldPos[0], lm->mWorldPos[1], lm->mWorldPos[2]});
+                            uv.insert(uv.end(), {fr.mvKeysUn[i].x, fr.mvKeysUn[i].y});
+                        }
+                    const int nobs = (int)(uv.size() / 2);
+                    if (nobs >= 10) {
+                        const int ninl = pr.Compute(fr);
+                        double model[6], rt[6];
+                        float To[16];
+                        vector<uint8_t> om2(nobs);
+                        int oinl = 0, best = 0, nit = 0;
+                        const int ook = oracle_pnp_ransac(Xw.data(), uv.data(), nobs, &cal, 500, 3.0f, 0.85, model, rt,
+                                                          To, om2.data(), &oinl, &best, &nit, nullptr);
+                        EXPECT(ook == 1 && ninl == oinl, "pair %d: PnPRansac inliers %d vs %d", t, ninl, oinl);
+                        double dp = 0;
+                        for (int k = 0; k < 16; k++) dp = std::max(dp, (double)fabsf(fr.mTcw[k] - To[k]));
+                        EXPECT(dp < 1e-5, "pair %d: PnPRansac |dT| = %g", t, dp);
+                        pnpransac_checked++;
+                    }
+                }
                 if (t == F - 1) proj_checked = check_projection(*last, *cur, o, cal, W, H);
             }
         }
@@ -281,8 +326,8 @@ static int run(int argc, char** argv) {
     }
 
     printf("frontend_parity %s frames=%d matches=%ld ransac_inliers=%ld pnp_inliers=%ld max_dT=%.3g "
-           "projection_matches=%d failures=%d\n",
+           "projection_matches=%d gicp_checked=%d pnpransac_checked=%d failures=%d\n",
            adaptive_orb ? "adaptive_orb" : adaptive ? "adaptive" : "orb_slam2", F, total_matches, total_inliers, total_pnp, max_dT, proj_checked,
-           g_fail);
+           gicp_checked, pnpransac_checked, g_fail);
     return g_fail ? 1 : 0;
 }
