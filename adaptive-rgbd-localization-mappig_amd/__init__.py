@@ -287,6 +287,25 @@ class Odometry:
                                       ptr(res), ptr(mask), ptr(good)))
         return res, mask[:n].astype(bool), good
 
+    def pnp_ransac_batch(self, problems, calib=None, iterations: int = 500, reproj_err: float = 3.0,
+                         confidence: float = 0.85):
+        """PnPRansac::Compute for a list of (Xw n x 3, uv n x 2) problems in one
+        launch chain. Returns (results[nprob], list of inlier masks)."""
+        sizes = [len(x) for x, _ in problems]
+        offs = np.zeros(len(problems) + 1, np.int32)
+        offs[1:] = np.cumsum(sizes)
+        Xw = np.ascontiguousarray(np.concatenate([np.asarray(x, np.float32).reshape(-1, 3) for x, _ in problems])
+                                  if problems else np.zeros((0, 3), np.float32))
+        uv = np.ascontiguousarray(np.concatenate([np.asarray(u, np.float32).reshape(-1, 2) for _, u in problems])
+                                  if problems else np.zeros((0, 2), np.float32))
+        res = (PnPRansacResult * max(len(problems), 1))()
+        mask = np.zeros(max(int(offs[-1]), 1), np.uint8)
+        cal = calib if calib is not None else self.cfg.calib
+        check(self.lib.odo_pnp_ransac_batch(self.h, ptr(Xw), ptr(uv), ptr(offs), len(problems), ptr(cal), iterations,
+                                            reproj_err, confidence, C.cast(res, C.c_void_p), ptr(mask)))
+        return [res[i] for i in range(len(problems))], [mask[offs[i]:offs[i + 1]].astype(bool)
+                                                         for i in range(len(problems))]
+
     def gicp(self, src, tgt, guess=None, max_iterations: int = 10, max_corr_dist: float = 0.07):
         """GeneralizedICP(max_iterations, max_corr_dist)::Compute(source, target,
         guess) (generalizedicp.cpp:30-39, 65-89) on the GPU. Returns

@@ -531,8 +531,15 @@ __device__ void gauss_newton(const double* l, const double* rho, double* betas) 
 // double reciprocal with one correction (exact for x < 2^32), getSubset's
 // rule (a draw equal to an earlier index of the same subset is drawn again).
 constexpr int PR_RNG_THREADS = 64;
-__global__ __launch_bounds__(PR_RNG_THREADS) void k_pr_subsets(int n, int H, int* __restrict__ idx) {
-    if (threadIdx.x != 0) return;
+// Problems of a batch: problem p owns points [offs[p], offs[p + 1]); problems
+// with fewer than 10 points are skipped (pnpransac.cpp:30).
+__global__ __launch_bounds__(PR_RNG_THREADS) void k_pr_subsets(const int* __restrict__ offs, int nprob, int H,
+                                                               int* __restrict__ idx) {
+    const int pb = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pb >= nprob) return;
+    const int n = offs[pb + 1] - offs[pb];
+    if (n < 10) return;
+    idx += (size_t)pb * H * PR_MODEL_POINTS;
     const double inv = 1.0 / (double)n;
     uint64_t state = ~(uint64_t)0;  // RNG rng((uint64)-1), ptsetreg.cpp run()
     for (int h = 0; h < H; h++) {
@@ -562,11 +569,18 @@ __global__ __launch_bounds__(PR_RNG_THREADS) void k_pr_subsets(int n, int H, int
 
 __global__ __launch_bounds__(PR_EPNP_THREADS) void k_pr_epnp(const float* __restrict__ Xw,
                                                              const float* __restrict__ uv,
-                                                             const int* __restrict__ idx, int H, PrK K,
-                                                             double* __restrict__ model, double* __restrict__ Rproj) {
+                                                             const int* __restrict__ offs, const int* __restrict__ idx,
+                                                             int H, PrK K, double* __restrict__ model,
+                                                             double* __restrict__ Rproj) {
     const int r = threadIdx.x & (PR_EPNP_GROUP - 1);
     const int h = blockIdx.x * (PR_EPNP_THREADS / PR_EPNP_GROUP) + (threadIdx.x >> 4);
-    if (h >= H) return;  // whole 16-lane groups leave together
+    const int pb = blockIdx.y;
+    if (h >= H || offs[pb + 1] - offs[pb] < 10) return;  // whole 16-lane groups leave together
+    Xw += 3 * (size_t)offs[pb];
+    uv += 2 * (size_t)offs[pb];
+    idx += (size_t)pb * H * PR_MODEL_POINTS;
+    model += (size_t)pb * H * 6;
+    Rproj += (size_t)pb * H * 9;
     // every lane of the group runs the small steps redundantly (identical
     // arithmetic), lane r < 12 owns row r of the 12 x 12 eigenproblem
     Epnp5 e;
@@ -665,11 +679,20 @@ __global__ __launch_bounds__(PR_EPNP_THREADS) void k_pr_epnp(const float* __rest
 }
 
 __global__ __launch_bounds__(PR_COUNT_THREADS) void k_pr_count(const float* __restrict__ Xw,
-                                                               const float* __restrict__ uv, int n, PrK K,
+                                                               const float* __restrict__ uv,
+                                                               const int* __restrict__ offs, int H, PrK K,
                                                                float thr, const double* __restrict__ model,
                                                                const double* __restrict__ Rproj,
                                                                uint8_t* __restrict__ mask, int* __restrict__ good) {
-    const int h = blockIdx.x;
+    const int h = blockIdx.x, pb = blockIdx.y;
+    const int n = offs[pb + 1] - offs[pb];
+    if (n < 10) return;
+    Xw += 3 * (size_t)offs[pb];
+    uv += 2 * (size_t)offs[pb];
+    model += (size_t)pb * H * 6;
+    Rproj += (size_t)pb * H * 9;
+    mask += (size_t)H * offs[pb];
+    good += (size_t)pb * H;
     __shared__ int wsum[PR_COUNT_THREADS / 64];
     double R[9], t[3];
     for (int k = 0; k < 9; k++) R[k] = Rproj[9 * h + k];
@@ -710,8 +733,19 @@ __device__ int update_num_iters(double p, double ep, int modelPoints, int maxIte
 }
 
 // state[0] = best hypothesis (-1: none), [1] = iterations visited, [2] = maxGoodCount
-__global__ void k_pr_fold(const int* __restrict__ good, int n, int H, double confidence, int* __restrict__ state) {
-    if (threadIdx.x != 0) return;
+__global__ void k_pr_fold(const int* __restrict__ good, const int* __restrict__ offs, int nprob, int H,
+                          double confidence, int* __restrict__ state) {
+    const int pb = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pb >= nprob) return;
+    const int n = offs[pb + 1] - offs[pb];
+    good += (size_t)pb * H;
+    state += 4 * pb;
+    if (n < 10) {
+        state[0] = -1;
+        state[1] = 0;
+        state[2] = 0;
+        return;
+    }
     int niters = H > 1 ? H : 1, maxGood = 0, best = -1, iter;
     for (iter = 0; iter < niters; iter++) {
         const int g = good[iter];
@@ -785,7 +819,8 @@ __device__ void lm_pass(const float* __restrict__ Xw, const float* __restrict__ 
 }
 
 __global__ __launch_bounds__(PR_REFINE_THREADS) void k_pr_refine(const float* __restrict__ Xw,
-                                                                 const float* __restrict__ uv, int n, PrK K,
+                                                                 const float* __restrict__ uv,
+                                                                 const int* __restrict__ offs, int H, PrK K,
                                                                  const uint8_t* __restrict__ mask,
                                                                  const double* __restrict__ model,
                                                                  const int* __restrict__ state,
@@ -794,9 +829,20 @@ __global__ __launch_bounds__(PR_REFINE_THREADS) void k_pr_refine(const float* __
     __shared__ double wred[PR_REFINE_THREADS / 64][43];
     __shared__ double red[43];
     __shared__ double sp[6], sprev[6];
+    const int pb = blockIdx.x;
+    const int n = offs[pb + 1] - offs[pb];
+    Xw += 3 * (size_t)offs[pb];
+    uv += 2 * (size_t)offs[pb];
+    mask += (size_t)H * offs[pb];
+    model += (size_t)pb * H * 6;
+    state += 4 * pb;
+    res += pb;
+    mask_out += offs[pb];
     const int best = state[0];
     if (best < 0 || state[2] <= 0) {
         if (threadIdx.x == 0) {
+            for (int k = 0; k < 3; k++) res->rvec[k] = res->tvec[k] = res->model_rvec[k] = res->model_tvec[k] = 0.0;
+            for (int k = 0; k < 16; k++) res->Tcw[k] = 0.f;
             res->ok = 0;
             res->n_inliers = 0;
             res->best_iter = best;
@@ -882,20 +928,22 @@ __global__ __launch_bounds__(PR_REFINE_THREADS) void k_pr_refine(const float* __
 
 int pnp_ransac_max_points() { return 1 << 16; }
 
-void launch_pnp_ransac(hipStream_t st, const float* Xw, const float* uv, int n, const float K4[4], int H,
-                       float reproj_err, double confidence, int* idx, double* model, double* Rproj, uint8_t* mask,
-                       int* good, int* state, odo_pnp_ransac_result* res, uint8_t* mask_out) {
+void launch_pnp_ransac(hipStream_t st, const float* Xw, const float* uv, const int* offs, int nprob,
+                       const float K4[4], int H, float reproj_err, double confidence, int* idx, double* model,
+                       double* Rproj, uint8_t* mask, int* good, int* state, odo_pnp_ransac_result* res,
+                       uint8_t* mask_out) {
     const PrK K{(double)K4[0], (double)K4[1], (double)K4[2], (double)K4[3]};
     const float thr = (float)((double)reproj_err * (double)reproj_err);
-    hipLaunchKernelGGL(k_pr_subsets, dim3(1), dim3(PR_RNG_THREADS), 0, st, n, H, idx);
+    const int pblocks = (nprob + 63) / 64;
+    hipLaunchKernelGGL(k_pr_subsets, dim3(pblocks), dim3(PR_RNG_THREADS), 0, st, offs, nprob, H, idx);
     const int hyp_per_block = PR_EPNP_THREADS / PR_EPNP_GROUP;
-    hipLaunchKernelGGL(k_pr_epnp, dim3((H + hyp_per_block - 1) / hyp_per_block), dim3(PR_EPNP_THREADS), 0, st, Xw,
-                       uv, idx, H, K, model, Rproj);
-    hipLaunchKernelGGL(k_pr_count, dim3(H), dim3(PR_COUNT_THREADS), 0, st, Xw, uv, n, K, thr, model, Rproj, mask,
-                       good);
-    hipLaunchKernelGGL(k_pr_fold, dim3(1), dim3(64), 0, st, good, n, H, confidence, state);
-    hipLaunchKernelGGL(k_pr_refine, dim3(1), dim3(PR_REFINE_THREADS), 0, st, Xw, uv, n, K, mask, model, state, res,
-                       mask_out);
+    hipLaunchKernelGGL(k_pr_epnp, dim3((H + hyp_per_block - 1) / hyp_per_block, nprob), dim3(PR_EPNP_THREADS), 0, st,
+                       Xw, uv, offs, idx, H, K, model, Rproj);
+    hipLaunchKernelGGL(k_pr_count, dim3(H, nprob), dim3(PR_COUNT_THREADS), 0, st, Xw, uv, offs, H, K, thr, model,
+                       Rproj, mask, good);
+    hipLaunchKernelGGL(k_pr_fold, dim3(pblocks), dim3(64), 0, st, good, offs, nprob, H, confidence, state);
+    hipLaunchKernelGGL(k_pr_refine, dim3(nprob), dim3(PR_REFINE_THREADS), 0, st, Xw, uv, offs, H, K, mask, model,
+                       state, res, mask_out);
 }
 
 }  // namespace odo

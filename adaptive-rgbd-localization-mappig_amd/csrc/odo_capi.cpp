@@ -2224,41 +2224,73 @@ int odo_pnp_motion_ba(odo_ctx* c, const float* Xw, const float* obs, int n, cons
     return ODO_OK;
 }
 
+// PnPRansac::Compute over nprob problems (problem p = points [offs[p], offs[p+1])),
+// one launch chain for the whole batch.
+static int pnp_ransac_run(odo_ctx* c, const float* Xw, const float* uv, const int32_t* offs, int nprob,
+                          const odo_calib* calib, int iterations, float reproj_err, double confidence,
+                          odo_pnp_ransac_result* res, uint8_t* inlier_mask, int32_t* good_counts) {
+    // ptsetreg.cpp run(): CV_Assert(confidence > 0 && confidence < 1); niters = MAX(maxIters, 1)
+    if (!(confidence > 0.0 && confidence < 1.0)) return fail(ODO_ERR_ARG, "confidence must be in (0, 1)");
+    const int H = std::max(iterations, 1);
+    if (offs[0] != 0) return fail(ODO_ERR_ARG, "pnp_ransac: offs[0] must be 0");
+    for (int p = 0; p < nprob; p++) {
+        const int n = offs[p + 1] - offs[p];
+        if (n < 0) return fail(ODO_ERR_ARG, "pnp_ransac: offsets must not decrease");
+        if (n > pnp_ransac_max_points()) return fail(ODO_ERR_CAPACITY, "pnp_ransac: too many points");
+    }
+    const int total = offs[nprob];
+    if ((size_t)H * (size_t)std::max(total, 1) > ((size_t)1 << 28))
+        return fail(ODO_ERR_CAPACITY, "pnp_ransac: iterations x points");
+    hipStream_t st = c->stream;
+    DevArena& A = c->arena;
+    A.begin();
+    const size_t tn = (size_t)std::max(total, 1), P = (size_t)nprob;
+    DevBuf dx(A, tn * 12), duv(A, tn * 8), doffs(A, (P + 1) * 4), didx(A, P * H * 5 * 4), dmodel(A, P * H * 6 * 8),
+        dR(A, P * H * 9 * 8), dmask(A, (size_t)H * tn), dgood(A, P * H * 4), dstate(A, P * 4 * 4),
+        dres(A, P * sizeof(odo_pnp_ransac_result)), dmo(A, tn);
+    ARENA_CHECK(A);
+    if (total) {
+        HIPCHK(hipMemcpyAsync(dx.p, Xw, (size_t)total * 12, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(duv.p, uv, (size_t)total * 8, hipMemcpyHostToDevice, st));
+    }
+    HIPCHK(hipMemcpyAsync(doffs.p, offs, (P + 1) * 4, hipMemcpyHostToDevice, st));
+    const odo_calib& k = calib ? *calib : c->cfg.calib;
+    const float K4[4] = {k.fx, k.fy, k.cx, k.cy};
+    launch_pnp_ransac(st, dx.as<float>(), duv.as<float>(), doffs.as<int>(), nprob, K4, H, reproj_err, confidence,
+                      didx.as<int>(), dmodel.as<double>(), dR.as<double>(), dmask.as<uint8_t>(), dgood.as<int>(),
+                      dstate.as<int>(), dres.as<odo_pnp_ransac_result>(), dmo.as<uint8_t>());
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(res, dres.p, P * sizeof(odo_pnp_ransac_result), hipMemcpyDeviceToHost, st));
+    if (inlier_mask && total) HIPCHK(hipMemcpyAsync(inlier_mask, dmo.p, (size_t)total, hipMemcpyDeviceToHost, st));
+    if (good_counts) HIPCHK(hipMemcpyAsync(good_counts, dgood.p, P * H * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return ODO_OK;
+}
+
 int odo_pnp_ransac(odo_ctx* c, const float* Xw, const float* uv, int n, const odo_calib* calib, int iterations,
                    float reproj_err, double confidence, odo_pnp_ransac_result* res, uint8_t* inlier_mask,
                    int32_t* good_counts) {
     if (!c || n < 0 || (n && (!Xw || !uv)) || !res) return fail(ODO_ERR_ARG, "bad pnp_ransac args");
-    // ptsetreg.cpp run(): CV_Assert(confidence > 0 && confidence < 1); niters = MAX(maxIters, 1)
     if (!(confidence > 0.0 && confidence < 1.0)) return fail(ODO_ERR_ARG, "confidence must be in (0, 1)");
-    const int H = std::max(iterations, 1);
     memset(res, 0, sizeof(*res));
     res->best_iter = -1;
     if (n < 10) {  // pnpransac.cpp:30: return 0 before solvePnPRansac
         if (inlier_mask && n) memset(inlier_mask, 0, (size_t)n);
         return ODO_OK;
     }
-    if (n > pnp_ransac_max_points()) return fail(ODO_ERR_CAPACITY, "pnp_ransac: too many points");
-    if ((size_t)H * (size_t)n > ((size_t)1 << 28)) return fail(ODO_ERR_CAPACITY, "pnp_ransac: iterations x points");
-    hipStream_t st = c->stream;
-    DevArena& A = c->arena;
-    A.begin();
-    DevBuf dx(A, (size_t)n * 12), duv(A, (size_t)n * 8), didx(A, (size_t)H * 5 * 4), dmodel(A, (size_t)H * 6 * 8),
-        dR(A, (size_t)H * 9 * 8), dmask(A, (size_t)H * n), dgood(A, (size_t)H * 4), dstate(A, 4 * 4),
-        dres(A, sizeof(odo_pnp_ransac_result)), dmo(A, (size_t)n);
-    ARENA_CHECK(A);
-    HIPCHK(hipMemcpyAsync(dx.p, Xw, (size_t)n * 12, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(duv.p, uv, (size_t)n * 8, hipMemcpyHostToDevice, st));
-    const odo_calib& k = calib ? *calib : c->cfg.calib;
-    const float K4[4] = {k.fx, k.fy, k.cx, k.cy};
-    launch_pnp_ransac(st, dx.as<float>(), duv.as<float>(), n, K4, H, reproj_err, confidence, didx.as<int>(),
-                      dmodel.as<double>(), dR.as<double>(), dmask.as<uint8_t>(), dgood.as<int>(), dstate.as<int>(),
-                      dres.as<odo_pnp_ransac_result>(), dmo.as<uint8_t>());
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(res, dres.p, sizeof(*res), hipMemcpyDeviceToHost, st));
-    if (inlier_mask) HIPCHK(hipMemcpyAsync(inlier_mask, dmo.p, (size_t)n, hipMemcpyDeviceToHost, st));
-    if (good_counts) HIPCHK(hipMemcpyAsync(good_counts, dgood.p, (size_t)H * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    return ODO_OK;
+    const int32_t offs[2] = {0, n};
+    return pnp_ransac_run(c, Xw, uv, offs, 1, calib, iterations, reproj_err, confidence, res, inlier_mask,
+                          good_counts);
+}
+
+int odo_pnp_ransac_batch(odo_ctx* c, const float* Xw, const float* uv, const int32_t* offs, int nprob,
+                         const odo_calib* calib, int iterations, float reproj_err, double confidence,
+                         odo_pnp_ransac_result* res, uint8_t* inlier_mask) {
+    if (!c || nprob < 0 || !offs || (nprob && !res)) return fail(ODO_ERR_ARG, "bad pnp_ransac_batch args");
+    if (nprob == 0) return ODO_OK;
+    if (offs[nprob] > 0 && (!Xw || !uv)) return fail(ODO_ERR_ARG, "bad pnp_ransac_batch args");
+    return pnp_ransac_run(c, Xw, uv, offs, nprob, calib, iterations, reproj_err, confidence, res, inlier_mask,
+                          nullptr);
 }
 
 int odo_gicp(odo_ctx* c, const float* src, int ns, const float* tgt, int nt, const float guess[16], int max_iterations,

@@ -236,11 +236,13 @@ struct GicpArgs {
 };
 void launch_gicp(hipStream_t st, const float* src, int ns, const float* tgt, int nt, double* Cs, double* Ct,
                  float* outp, double* Mah, int* is, int* it, GicpArgs args, float* T12, int* outi);
-// PnPRansac (k_pnpransac.hip): idx H*5, model H*6, Rproj H*9, mask H*n, good H, state 3
+// PnPRansac (k_pnpransac.hip), nprob problems, problem p = points [offs[p], offs[p+1]):
+// idx P*H*5, model P*H*6, Rproj P*H*9, mask H*sum(n), good P*H, state P*4, res P, mask_out sum(n)
 int pnp_ransac_max_points();
-void launch_pnp_ransac(hipStream_t st, const float* Xw, const float* uv, int n, const float K4[4], int H,
-                       float reproj_err, double confidence, int* idx, double* model, double* Rproj, uint8_t* mask,
-                       int* good, int* state, odo_pnp_ransac_result* res, uint8_t* mask_out);
+void launch_pnp_ransac(hipStream_t st, const float* Xw, const float* uv, const int* offs, int nprob,
+                       const float K4[4], int H, float reproj_err, double confidence, int* idx, double* model,
+                       double* Rproj, uint8_t* mask, int* good, int* state, odo_pnp_ransac_result* res,
+                       uint8_t* mask_out);
 int launch_projection_match(hipStream_t st, const float* Tcw, const odo_landmark* lms, int nL, const float* kun,
                             const int32_t* octave, const uint8_t* desc, int n, const uint8_t* slot_taken,
                             const float* calib5, const float* bounds, float th, float nnratio, float* proj,

@@ -388,6 +388,23 @@ def pnpransac_mode(args):
         t0 = time.perf_counter()
         res, mask, _ = odo.pnp_ransac(Xw, uv, None, args.iters)
         ts.append((time.perf_counter() - t0) * 1e3)
+    # the batched contract: B such problems (the same observations, outliers
+    # re-drawn per problem) in one odo_pnp_ransac_batch launch chain
+    B = 256
+    probs = []
+    for b in range(B):
+        u2 = np.ascontiguousarray(f1["kun"][m["trainIdx"]])
+        s2 = np.random.default_rng(100 + b).random(len(u2)) < 1.0 / 3.0
+        u2[s2] = f1["kun"][np.random.default_rng(200 + b).integers(0, len(f1["kun"]), int(s2.sum()))]
+        probs.append((Xw, u2))
+    odo.pnp_ransac_batch(probs, None, args.iters)
+    torch.cuda.synchronize()
+    tb = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        bres, _ = odo.pnp_ransac_batch(probs, None, args.iters)
+        tb.append((time.perf_counter() - t0) * 1e3)
+    bok = sum(int(r.ok) for r in bres)
     odo.close()
     out = {"metric": "PnPRansac::Compute latency (cv::solvePnPRansac on the GPU, one call)",
            "value": round(float(np.median(ts)), 4), "unit": "ms/call (p50)", "n_gpus": 1, "steps": len(ts),
@@ -395,6 +412,9 @@ def pnpransac_mode(args):
            "observations": int(len(Xw)), "outliers_injected": int(sel.sum()), "ok": int(res.ok),
            "n_inliers": int(res.n_inliers), "iterations_visited": int(res.iterations_visited),
            "best_iter": int(res.best_iter),
+           "batch": {"problems": B, "ms_per_batch": round(float(np.median(tb)), 3),
+                     "problems_per_s": round(B / (float(np.median(tb)) / 1e3), 1), "ok": bok,
+                     "api": "odo_pnp_ransac_batch (host arrays in and out)"},
            "config": {"workload": f"cfg2 pair {args.width}x{args.height}, {args.nfeatures} kp, "
                                   f"iterations {args.iters}, 3 px, confidence 0.85"}}
     if not args.no_cpu_baseline:

@@ -179,6 +179,15 @@ int odo_pnp_ransac(odo_ctx* ctx, const float* Xw, const float* uv, int n, const 
                    float reproj_err, double confidence, odo_pnp_ransac_result* res, uint8_t* inlier_mask,
                    int32_t* good_counts);
 
+/* PnPRansac::Compute for a batch of frames in one launch chain (the batched
+ * contract of odo_track_batch): problem p = observations [offs[p], offs[p+1])
+ * of Xw / uv (offs[0] = 0, nprob + 1 entries); res[p] as odo_pnp_ransac
+ * (problems with fewer than 10 observations: ok = 0, best_iter = -1);
+ * inlier_mask (optional) over all offs[nprob] observations. */
+int odo_pnp_ransac_batch(odo_ctx* ctx, const float* Xw, const float* uv, const int32_t* offs, int nprob,
+                         const odo_calib* calib, int iterations, float reproj_err, double confidence,
+                         odo_pnp_ransac_result* res, uint8_t* inlier_mask);
+
 /* GeneralizedICP(max_iterations, max_corr_dist)::Compute(source, target, guess)
  * (generalizedicp.cpp:11-22, 30-39, 65-89): the PCL
  * GICP refinement Odometry::Compute's ADAPTIVE_RICP mode runs on RANSAC's

@@ -238,3 +238,36 @@ def test_gpu_edge_cases(odo):
     with pytest.raises(RuntimeError):
         odo.pnp_ransac(Xw, uv, None, 500, 3.0, 1.0)
     assert pkg is not None
+
+
+@pytest.mark.gpu
+def test_gpu_batch_matches_oracle(odo):
+    """odo_pnp_ransac_batch: every problem of a ragged batch (incl. < 10
+    observations, pure noise, large) equals the oracle and the one-call API."""
+    probs = []
+    for seed, n, outl in [(21, 400, 0.4), (22, 9, 0.0), (23, 1200, 0.6), (24, 60, 0.0), (25, 0, 0.0),
+                          (26, 800, 0.75), (27, 30, 0.2)]:
+        Xw, uv, cal, *_ = _problem(seed, max(n, 1), outl)
+        probs.append((Xw[:n], uv[:n]))
+    rng = np.random.default_rng(28)
+    probs.append((rng.uniform(-2, 2, (200, 3)).astype(np.float32) + np.float32([0, 0, 4]),
+                  rng.uniform(0, 640, (200, 2)).astype(np.float32)))
+    probs.append(_frames_problem())
+    cal = O.fr1_calib()
+    res, masks = odo.pnp_ransac_batch([(x, u) for x, u, *_ in probs])
+    for (Xw, uv, *_), r, m in zip(probs, res, masks):
+        ref = O.pnp_ransac(Xw, uv, cal)
+        one, mask1, _ = odo.pnp_ransac(Xw, uv)
+        assert r.ok == ref["ok"] == one.ok
+        if len(Xw) < 10:
+            assert r.best_iter == -1 and not m.any()
+            continue
+        assert r.iterations_visited == ref["niters"] == one.iterations_visited
+        assert r.best_iter == ref["best_iter"]
+        if not ref["ok"]:
+            continue
+        assert r.n_inliers == ref["n_inliers"]
+        np.testing.assert_array_equal(m, ref["mask"])
+        np.testing.assert_array_equal(m, mask1)
+        np.testing.assert_allclose(np.r_[r.rvec[:], r.tvec[:]], ref["rt"], rtol=0, atol=1e-7)
+        assert np.array_equal(np.array(r.Tcw[:]), np.array(one.Tcw[:]))
