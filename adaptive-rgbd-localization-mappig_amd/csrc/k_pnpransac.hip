@@ -570,12 +570,15 @@ __global__ __launch_bounds__(PR_RNG_THREADS) void k_pr_subsets(const int* __rest
 __global__ __launch_bounds__(PR_EPNP_THREADS) void k_pr_epnp(const float* __restrict__ Xw,
                                                              const float* __restrict__ uv,
                                                              const int* __restrict__ offs, const int* __restrict__ idx,
-                                                             int H, PrK K, double* __restrict__ model,
+                                                             int H, int h0, int h1, const int* __restrict__ fstate,
+                                                             PrK K, double* __restrict__ model,
                                                              double* __restrict__ Rproj) {
     const int r = threadIdx.x & (PR_EPNP_GROUP - 1);
-    const int h = blockIdx.x * (PR_EPNP_THREADS / PR_EPNP_GROUP) + (threadIdx.x >> 4);
+    const int h = h0 + blockIdx.x * (PR_EPNP_THREADS / PR_EPNP_GROUP) + (threadIdx.x >> 4);
     const int pb = blockIdx.y;
-    if (h >= H || offs[pb + 1] - offs[pb] < 10) return;  // whole 16-lane groups leave together
+    // whole 16-lane groups leave together; with a fold state, hypotheses at or
+    // past the problem's current niters are never visited (niters only shrinks)
+    if (h >= h1 || offs[pb + 1] - offs[pb] < 10 || (fstate && h >= fstate[4 * pb + 3])) return;
     Xw += 3 * (size_t)offs[pb];
     uv += 2 * (size_t)offs[pb];
     idx += (size_t)pb * H * PR_MODEL_POINTS;
@@ -680,13 +683,14 @@ __global__ __launch_bounds__(PR_EPNP_THREADS) void k_pr_epnp(const float* __rest
 
 __global__ __launch_bounds__(PR_COUNT_THREADS) void k_pr_count(const float* __restrict__ Xw,
                                                                const float* __restrict__ uv,
-                                                               const int* __restrict__ offs, int H, PrK K,
-                                                               float thr, const double* __restrict__ model,
+                                                               const int* __restrict__ offs, int H, int h0,
+                                                               const int* __restrict__ fstate, PrK K, float thr,
+                                                               const double* __restrict__ model,
                                                                const double* __restrict__ Rproj,
                                                                uint8_t* __restrict__ mask, int* __restrict__ good) {
-    const int h = blockIdx.x, pb = blockIdx.y;
+    const int h = h0 + blockIdx.x, pb = blockIdx.y;
     const int n = offs[pb + 1] - offs[pb];
-    if (n < 10) return;
+    if (n < 10 || (fstate && h >= fstate[4 * pb + 3])) return;
     Xw += 3 * (size_t)offs[pb];
     uv += 2 * (size_t)offs[pb];
     model += (size_t)pb * H * 6;
@@ -732,9 +736,11 @@ __device__ int update_num_iters(double p, double ep, int modelPoints, int maxIte
     return denom >= 0 || -num >= maxIters * (-denom) ? maxIters : (int)rint(num / denom);
 }
 
-// state[0] = best hypothesis (-1: none), [1] = iterations visited, [2] = maxGoodCount
-__global__ void k_pr_fold(const int* __restrict__ good, const int* __restrict__ offs, int nprob, int H,
-                          double confidence, int* __restrict__ state) {
+// state[4p]: [0] = best hypothesis (-1: none), [1] = iterations visited so
+// far, [2] = maxGoodCount, [3] = niters. Folds hypotheses [h0, h1) in order,
+// continuing the state of earlier chunks (h0 = 0 starts it).
+__global__ void k_pr_fold(const int* __restrict__ good, const int* __restrict__ offs, int nprob, int H, int h0,
+                          int h1, double confidence, int* __restrict__ state) {
     const int pb = blockIdx.x * blockDim.x + threadIdx.x;
     if (pb >= nprob) return;
     const int n = offs[pb + 1] - offs[pb];
@@ -744,10 +750,23 @@ __global__ void k_pr_fold(const int* __restrict__ good, const int* __restrict__ 
         state[0] = -1;
         state[1] = 0;
         state[2] = 0;
+        state[3] = 0;
         return;
     }
-    int niters = H > 1 ? H : 1, maxGood = 0, best = -1, iter;
-    for (iter = 0; iter < niters; iter++) {
+    int niters, maxGood, best, iter;
+    if (h0 == 0) {
+        niters = H > 1 ? H : 1;
+        maxGood = 0;
+        best = -1;
+        iter = 0;
+    } else {
+        best = state[0];
+        iter = state[1];
+        maxGood = state[2];
+        niters = state[3];
+        if (iter < h0) return;  // the fold ended in an earlier chunk
+    }
+    for (; iter < niters && iter < h1; iter++) {
         const int g = good[iter];
         if (g > (maxGood > PR_MODEL_POINTS - 1 ? maxGood : PR_MODEL_POINTS - 1)) {
             best = iter;
@@ -758,6 +777,7 @@ __global__ void k_pr_fold(const int* __restrict__ good, const int* __restrict__ 
     state[0] = best;
     state[1] = iter;
     state[2] = maxGood;
+    state[3] = niters;
 }
 
 // fixed-order workgroup sum of NV doubles per thread (wave shuffles, then waves in order)
@@ -928,6 +948,11 @@ __global__ __launch_bounds__(PR_REFINE_THREADS) void k_pr_refine(const float* __
 
 int pnp_ransac_max_points() { return 1 << 16; }
 
+// One problem: every hypothesis at once (the per-hypothesis chains are the
+// latency). A batch: chunks of PR_CHUNK hypotheses, each chunk's EPnP and
+// counts skipping the problems whose fold has already stopped, so the work
+// follows the visited hypotheses (typically a fraction of `iterations`).
+constexpr int PR_CHUNK = 64;
 void launch_pnp_ransac(hipStream_t st, const float* Xw, const float* uv, const int* offs, int nprob,
                        const float K4[4], int H, float reproj_err, double confidence, int* idx, double* model,
                        double* Rproj, uint8_t* mask, int* good, int* state, odo_pnp_ransac_result* res,
@@ -937,11 +962,17 @@ void launch_pnp_ransac(hipStream_t st, const float* Xw, const float* uv, const i
     const int pblocks = (nprob + 63) / 64;
     hipLaunchKernelGGL(k_pr_subsets, dim3(pblocks), dim3(PR_RNG_THREADS), 0, st, offs, nprob, H, idx);
     const int hyp_per_block = PR_EPNP_THREADS / PR_EPNP_GROUP;
-    hipLaunchKernelGGL(k_pr_epnp, dim3((H + hyp_per_block - 1) / hyp_per_block, nprob), dim3(PR_EPNP_THREADS), 0, st,
-                       Xw, uv, offs, idx, H, K, model, Rproj);
-    hipLaunchKernelGGL(k_pr_count, dim3(H, nprob), dim3(PR_COUNT_THREADS), 0, st, Xw, uv, offs, H, K, thr, model,
-                       Rproj, mask, good);
-    hipLaunchKernelGGL(k_pr_fold, dim3(pblocks), dim3(64), 0, st, good, offs, nprob, H, confidence, state);
+    const int chunk = nprob > 1 ? PR_CHUNK : H;
+    for (int h0 = 0; h0 < H; h0 += chunk) {
+        const int h1 = h0 + chunk < H ? h0 + chunk : H;
+        const int* fs = h0 == 0 ? nullptr : state;
+        hipLaunchKernelGGL(k_pr_epnp, dim3((h1 - h0 + hyp_per_block - 1) / hyp_per_block, nprob),
+                           dim3(PR_EPNP_THREADS), 0, st, Xw, uv, offs, idx, H, h0, h1, fs, K, model, Rproj);
+        hipLaunchKernelGGL(k_pr_count, dim3(h1 - h0, nprob), dim3(PR_COUNT_THREADS), 0, st, Xw, uv, offs, H, h0, fs,
+                           K, thr, model, Rproj, mask, good);
+        hipLaunchKernelGGL(k_pr_fold, dim3(pblocks), dim3(64), 0, st, good, offs, nprob, H, h0, h1, confidence,
+                           state);
+    }
     hipLaunchKernelGGL(k_pr_refine, dim3(nprob), dim3(PR_REFINE_THREADS), 0, st, Xw, uv, offs, H, K, mask, model,
                        state, res, mask_out);
 }
