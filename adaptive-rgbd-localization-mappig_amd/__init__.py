@@ -319,6 +319,26 @@ class Odometry:
                                 max_corr_dist, ptr(T), C.byref(conv), C.byref(it), C.byref(nc)))
         return T.reshape(4, 4), conv.value, it.value, nc.value
 
+    def gicp_batch(self, pairs, max_iterations: int = 10, max_corr_dist: float = 0.07):
+        """GeneralizedICP::Compute for a list of (src n x 3, tgt m x 3, guess 4x4 or
+        None) in one launch chain. Returns a list of (T12, converged, iterations,
+        n_corr)."""
+        P = len(pairs)
+        so = np.zeros(P + 1, np.int32)
+        to = np.zeros(P + 1, np.int32)
+        so[1:] = np.cumsum([len(s) for s, _, _ in pairs])
+        to[1:] = np.cumsum([len(t) for _, t, _ in pairs])
+        cat = lambda xs: np.ascontiguousarray(np.concatenate([np.asarray(x, np.float32).reshape(-1, 3) for x in xs])
+                                              if xs else np.zeros((0, 3), np.float32))
+        src, tgt = cat([s for s, _, _ in pairs]), cat([t for _, t, _ in pairs])
+        g = np.ascontiguousarray(np.stack([np.eye(4, dtype=np.float32) if q is None else np.asarray(q, np.float32)
+                                           for _, _, q in pairs]) if P else np.zeros((1, 4, 4), np.float32))
+        T = np.zeros((max(P, 1), 16), np.float32)
+        conv, it, nc = (np.zeros(max(P, 1), np.int32) for _ in range(3))
+        check(self.lib.odo_gicp_batch(self.h, ptr(src), ptr(so), ptr(tgt), ptr(to), ptr(g), P, max_iterations,
+                                      max_corr_dist, ptr(T), ptr(conv), ptr(it), ptr(nc)))
+        return [(T[p].reshape(4, 4), int(conv[p]), int(it[p]), int(nc[p])) for p in range(P)]
+
     def timings(self):
         ms = np.zeros(16, np.float32)
         names = (C.c_char_p * 16)()

@@ -121,6 +121,7 @@ SIGNATURES = {
     "odo_kabsch": (C.c_int, [P, P, C.c_int, P]),
     "odo_pnp_ransac": (C.c_int, [P, P, P, C.c_int, P, C.c_int, C.c_float, C.c_double, P, P, P]),
     "odo_pnp_ransac_batch": (C.c_int, [P, P, P, P, C.c_int, P, C.c_int, C.c_float, C.c_double, P, P]),
+    "odo_gicp_batch": (C.c_int, [P, P, P, P, P, P, C.c_int, C.c_int, C.c_double, P, P, P, P]),
     "odo_gicp": (C.c_int, [P, P, C.c_int, P, C.c_int, P, C.c_int, C.c_double, P, P, P, P]),
     "odo_rng_seed": (None, [P, C.c_uint32]),
     "odo_rng_next": (C.c_int32, [P]),

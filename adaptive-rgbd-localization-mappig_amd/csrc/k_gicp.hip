@@ -19,6 +19,7 @@
 // (PCL is absent: parity with the library is unpinned).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cfloat>
 
 #include "odo_internal.h"
@@ -46,16 +47,17 @@ __device__ __forceinline__ float dist2f(const float* a, const float* b) {
     return r;
 }
 
-// blocks [0, nb_a) cover cloud A, the rest cloud B (both clouds in one launch)
-__global__ __launch_bounds__(64) void k_gicp_cov(const float* __restrict__ PA, int na, double* __restrict__ CA,
-                                                 const float* __restrict__ PB, int nb, double* __restrict__ CB,
-                                                 int nb_a, double eps) {
-    const bool first = (int)blockIdx.x < nb_a;
-    const float* __restrict__ P = first ? PA : PB;
-    double* __restrict__ C = first ? CA : CB;
-    const int n = first ? na : nb;
-    const int q = (first ? blockIdx.x : blockIdx.x - nb_a) * blockDim.x + threadIdx.x;
-    if (q >= n) return;
+// grid (point blocks, problems, 2): z = 0 the target clouds, z = 1 the sources
+__global__ __launch_bounds__(64) void k_gicp_cov(const float* __restrict__ src, const int* __restrict__ soffs,
+                                                 double* __restrict__ Cs, const float* __restrict__ tgt,
+                                                 const int* __restrict__ toffs, double* __restrict__ Ct, double eps) {
+    const int pb = blockIdx.y;
+    const int* offs = blockIdx.z ? soffs : toffs;
+    const int n = offs[pb + 1] - offs[pb];
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n || soffs[pb + 1] - soffs[pb] < 20 || toffs[pb + 1] - toffs[pb] < 20) return;
+    const float* __restrict__ P = (blockIdx.z ? src : tgt) + 3 * (size_t)offs[pb];
+    double* __restrict__ C = (blockIdx.z ? Cs : Ct) + 9 * (size_t)offs[pb];
     // the sorted top 20 in registers: +inf padding stands for "fewer than 20
     // so far", a candidate is inserted after equal distances (ties to the lower
     // index, as the scan is in index order)
@@ -582,8 +584,9 @@ struct GiBfgs {
 };
 
 // out[4]: converged, iterations, n_corr, (pad); T12[16]
-__global__ __launch_bounds__(GI_THREADS) void k_gicp(const float* __restrict__ src, int ns, const float* __restrict__ tgt,
-                                                   int nt, const double* __restrict__ Cs, const double* __restrict__ Ct,
+// one workgroup per problem of the batch
+__global__ __launch_bounds__(GI_THREADS) void k_gicp(const float* __restrict__ src, const float* __restrict__ tgt,
+                                                   const double* __restrict__ Cs, const double* __restrict__ Ct,
                                                    float* __restrict__ outp, double* __restrict__ Mah,
                                                    int* __restrict__ is, int* __restrict__ it, GicpArgs A,
                                                    float* __restrict__ T12, int* __restrict__ outi) {
@@ -591,7 +594,25 @@ __global__ __launch_bounds__(GI_THREADS) void k_gicp(const float* __restrict__ s
     __shared__ double bc[GI_NV];
     __shared__ int wcnt[GI_WAVES];
     const int lane = threadIdx.x & (GI_LANES - 1), wave = threadIdx.x / GI_LANES;
-    const float* guess = A.guess;
+    const int pb = blockIdx.x;
+    const int s0 = A.soffs[pb], t0 = A.toffs[pb];
+    const int ns = A.soffs[pb + 1] - s0, nt = A.toffs[pb + 1] - t0;
+    const float* guess = A.guess + 16 * pb;
+    T12 += 16 * pb;
+    outi += 4 * pb;
+    if (ns < 20 || nt < 20) {  // generalizedicp.cpp:33
+        if (threadIdx.x < 16) T12[threadIdx.x] = threadIdx.x % 5 == 0 ? 1.f : 0.f;
+        if (threadIdx.x < 4) outi[threadIdx.x] = 0;
+        return;
+    }
+    src += 3 * (size_t)s0;
+    outp += 3 * (size_t)s0;
+    Cs += 9 * (size_t)s0;
+    Mah += 9 * (size_t)s0;
+    is += s0;
+    it += s0;
+    tgt += 3 * (size_t)t0;
+    Ct += 9 * (size_t)t0;
     for (int i = threadIdx.x; i < ns; i += GI_THREADS) {  // transformPointCloud(output, output, guess)
         const float p0 = src[3 * i], p1 = src[3 * i + 1], p2 = src[3 * i + 2];
 #pragma unroll
@@ -727,11 +748,12 @@ __global__ __launch_bounds__(GI_THREADS) void k_gicp(const float* __restrict__ s
 
 }  // namespace
 
-void launch_gicp(hipStream_t st, const float* src, int ns, const float* tgt, int nt, double* Cs, double* Ct,
-                 float* outp, double* Mah, int* is, int* it, GicpArgs args, float* T12, int* outi) {
-    const int nb_t = (nt + 63) / 64, nb_s = (ns + 63) / 64;
-    hipLaunchKernelGGL(k_gicp_cov, dim3(nb_t + nb_s), dim3(64), 0, st, tgt, nt, Ct, src, ns, Cs, nb_t, 1e-3);
-    hipLaunchKernelGGL(k_gicp, dim3(1), dim3(GI_THREADS), 0, st, src, ns, tgt, nt, Cs, Ct, outp, Mah, is, it, args, T12,
+void launch_gicp(hipStream_t st, const float* src, const float* tgt, int nprob, int max_ns, int max_nt, double* Cs,
+                 double* Ct, float* outp, double* Mah, int* is, int* it, GicpArgs args, float* T12, int* outi) {
+    const int nbx = (std::max(max_ns, max_nt) + 63) / 64;
+    hipLaunchKernelGGL(k_gicp_cov, dim3(nbx, nprob, 2), dim3(64), 0, st, src, args.soffs, Cs, tgt, args.toffs, Ct,
+                       1e-3);
+    hipLaunchKernelGGL(k_gicp, dim3(nprob), dim3(GI_THREADS), 0, st, src, tgt, Cs, Ct, outp, Mah, is, it, args, T12,
                        outi);
 }
 

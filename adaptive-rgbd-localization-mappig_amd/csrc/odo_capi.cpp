@@ -2293,6 +2293,49 @@ int odo_pnp_ransac_batch(odo_ctx* c, const float* Xw, const float* uv, const int
                           nullptr);
 }
 
+static int gicp_run(odo_ctx* c, const float* src, const int32_t* soffs, const float* tgt, const int32_t* toffs,
+                    const float* guesses, int nprob, int max_iterations, double max_corr_dist, float* T12,
+                    int32_t* converged, int32_t* iterations, int32_t* n_corr) {
+    if (soffs[0] != 0 || toffs[0] != 0) return fail(ODO_ERR_ARG, "gicp: offsets must start at 0");
+    int max_ns = 0, max_nt = 0;
+    for (int p = 0; p < nprob; p++) {
+        const int ns = soffs[p + 1] - soffs[p], nt = toffs[p + 1] - toffs[p];
+        if (ns < 0 || nt < 0) return fail(ODO_ERR_ARG, "gicp: offsets must not decrease");
+        if (ns > 65536 || nt > 65536) return fail(ODO_ERR_CAPACITY, "gicp: more than 65536 points");
+        max_ns = std::max(max_ns, ns);
+        max_nt = std::max(max_nt, nt);
+    }
+    const size_t S = (size_t)std::max(soffs[nprob], 1), T = (size_t)std::max(toffs[nprob], 1), P = (size_t)nprob;
+    hipStream_t st = c->stream;
+    DevArena& A = c->arena;
+    A.begin();
+    DevBuf ds(A, S * 12), dt(A, T * 12), dCs(A, S * 72), dCt(A, T * 72), dout(A, S * 12), dM(A, S * 72), dis(A, S * 4),
+        dit(A, S * 4), dT(A, P * 64), dio(A, P * 16), dg(A, P * 64), dso(A, (P + 1) * 4), dto(A, (P + 1) * 4);
+    ARENA_CHECK(A);
+    if (soffs[nprob]) HIPCHK(hipMemcpyAsync(ds.p, src, (size_t)soffs[nprob] * 12, hipMemcpyHostToDevice, st));
+    if (toffs[nprob]) HIPCHK(hipMemcpyAsync(dt.p, tgt, (size_t)toffs[nprob] * 12, hipMemcpyHostToDevice, st));
+    std::vector<float> g(16 * P);
+    for (size_t p = 0; p < P; p++)
+        for (int i = 0; i < 16; i++) g[16 * p + i] = guesses ? guesses[16 * p + i] : (i % 5 == 0 ? 1.f : 0.f);
+    HIPCHK(hipMemcpyAsync(dg.p, g.data(), P * 64, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(dso.p, soffs, (P + 1) * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(dto.p, toffs, (P + 1) * 4, hipMemcpyHostToDevice, st));
+    GicpArgs args{dg.as<float>(), dso.as<int>(), dto.as<int>(), max_corr_dist, max_iterations, 20 /* PCL inner */};
+    launch_gicp(st, ds.as<float>(), dt.as<float>(), nprob, max_ns, max_nt, dCs.as<double>(), dCt.as<double>(),
+                dout.as<float>(), dM.as<double>(), dis.as<int>(), dit.as<int>(), args, dT.as<float>(), dio.as<int>());
+    HIPCHK(hipGetLastError());
+    std::vector<int> io(4 * P);
+    HIPCHK(hipMemcpyAsync(T12, dT.p, P * 64, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(io.data(), dio.p, P * 16, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    for (size_t p = 0; p < P; p++) {
+        converged[p] = io[4 * p];
+        iterations[p] = io[4 * p + 1];
+        n_corr[p] = io[4 * p + 2];
+    }
+    return ODO_OK;
+}
+
 int odo_gicp(odo_ctx* c, const float* src, int ns, const float* tgt, int nt, const float guess[16], int max_iterations,
              double max_corr_dist, float T12[16], int* converged, int* iterations, int* n_corr) {
     if (!c || ns < 0 || nt < 0 || (ns && !src) || (nt && !tgt) || !T12 || !converged || !iterations || !n_corr)
@@ -2302,32 +2345,19 @@ int odo_gicp(odo_ctx* c, const float* src, int ns, const float* tgt, int nt, con
     *n_corr = 0;
     for (int i = 0; i < 16; i++) T12[i] = i % 5 == 0 ? 1.f : 0.f;
     if (ns < 20 || nt < 20) return ODO_OK;  // generalizedicp.cpp:33
-    if (ns > 65536 || nt > 65536) return fail(ODO_ERR_CAPACITY, "gicp: more than 65536 points");
-    GicpArgs args{};
-    for (int i = 0; i < 16; i++) args.guess[i] = guess ? guess[i] : (i % 5 == 0 ? 1.f : 0.f);
-    args.max_corr_dist = max_corr_dist;
-    args.max_iterations = max_iterations;
-    args.max_inner = 20;  // PCL's max_inner_iterations_
-    hipStream_t st = c->stream;
-    DevArena& A = c->arena;
-    A.begin();
-    DevBuf ds(A, (size_t)ns * 12), dt(A, (size_t)nt * 12), dCs(A, (size_t)ns * 72), dCt(A, (size_t)nt * 72),
-        dout(A, (size_t)ns * 12), dM(A, (size_t)ns * 72), dis(A, (size_t)ns * 4), dit(A, (size_t)ns * 4), dT(A, 64),
-        dio(A, 16);
-    ARENA_CHECK(A);
-    HIPCHK(hipMemcpyAsync(ds.p, src, (size_t)ns * 12, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(dt.p, tgt, (size_t)nt * 12, hipMemcpyHostToDevice, st));
-    launch_gicp(st, ds.as<float>(), ns, dt.as<float>(), nt, dCs.as<double>(), dCt.as<double>(), dout.as<float>(),
-                dM.as<double>(), dis.as<int>(), dit.as<int>(), args, dT.as<float>(), dio.as<int>());
-    HIPCHK(hipGetLastError());
-    int io[4];
-    HIPCHK(hipMemcpyAsync(T12, dT.p, 64, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(io, dio.p, 16, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    *converged = io[0];
-    *iterations = io[1];
-    *n_corr = io[2];
-    return ODO_OK;
+    const int32_t so[2] = {0, ns}, to[2] = {0, nt};
+    return gicp_run(c, src, so, tgt, to, guess, 1, max_iterations, max_corr_dist, T12, converged, iterations, n_corr);
+}
+
+int odo_gicp_batch(odo_ctx* c, const float* src, const int32_t* soffs, const float* tgt, const int32_t* toffs,
+                   const float* guesses, int nprob, int max_iterations, double max_corr_dist, float* T12,
+                   int32_t* converged, int32_t* iterations, int32_t* n_corr) {
+    if (!c || nprob < 0 || !soffs || !toffs || (nprob && (!T12 || !converged || !iterations || !n_corr)))
+        return fail(ODO_ERR_ARG, "bad gicp_batch args");
+    if (nprob == 0) return ODO_OK;
+    if ((soffs[nprob] > 0 && !src) || (toffs[nprob] > 0 && !tgt)) return fail(ODO_ERR_ARG, "bad gicp_batch args");
+    return gicp_run(c, src, soffs, tgt, toffs, guesses, nprob, max_iterations, max_corr_dist, T12, converged,
+                    iterations, n_corr);
 }
 
 // Frame::ComputeImageBounds: cv::undistortPoints of the four corners (5

@@ -227,15 +227,19 @@ void launch_pnp(hipStream_t st, const int32_t* f2_src, const float* xyz, const f
                 const int* n_matches, int min_matches, void* edges, odo_pair_result* res, uint8_t* inlier_mask,
                 int npairs, const int* sel = nullptr, int sel_val = 0);
 void launch_kabsch(hipStream_t st, const float* A, const float* B, int n, float* T);
-// GICP (k_gicp.hip): Cs ns*9, Ct nt*9, outp ns*3, Mah ns*9, is / it ns; outi 4
+// GICP (k_gicp.hip), nprob problems: source p = points [soffs[p], soffs[p+1]) of
+// src, target p = [toffs[p], toffs[p+1]) of tgt. Cs sum(ns)*9, Ct sum(nt)*9,
+// outp sum(ns)*3, Mah sum(ns)*9, is / it sum(ns); T12 16 and outi 4 per problem.
 struct GicpArgs {
-    float guess[16];
+    const float* guess;  // 16 per problem (device)
+    const int* soffs;    // nprob + 1 (device)
+    const int* toffs;
     double max_corr_dist;
     int max_iterations;
     int max_inner;
 };
-void launch_gicp(hipStream_t st, const float* src, int ns, const float* tgt, int nt, double* Cs, double* Ct,
-                 float* outp, double* Mah, int* is, int* it, GicpArgs args, float* T12, int* outi);
+void launch_gicp(hipStream_t st, const float* src, const float* tgt, int nprob, int max_ns, int max_nt, double* Cs,
+                 double* Ct, float* outp, double* Mah, int* is, int* it, GicpArgs args, float* T12, int* outi);
 // PnPRansac (k_pnpransac.hip), nprob problems, problem p = points [offs[p], offs[p+1]):
 // idx P*H*5, model P*H*6, Rproj P*H*9, mask H*sum(n), good P*H, state P*4, res P, mask_out sum(n)
 int pnp_ransac_max_points();

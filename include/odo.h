@@ -201,6 +201,15 @@ int odo_pnp_ransac_batch(odo_ctx* ctx, const float* Xw, const float* uv, const i
 int odo_gicp(odo_ctx* ctx, const float* src, int ns, const float* tgt, int nt, const float guess[16],
              int max_iterations, double max_corr_dist, float T12[16], int* converged, int* iterations, int* n_corr);
 
+/* GeneralizedICP::Compute for a batch of pairs in one launch chain: pair p =
+ * source points [soffs[p], soffs[p+1]) of src, target points [toffs[p],
+ * toffs[p+1]) of tgt (offsets start at 0, nprob + 1 entries), guesses 16 per
+ * pair (NULL: identity); T12 16 per pair, converged / iterations / n_corr one
+ * per pair, as odo_gicp. */
+int odo_gicp_batch(odo_ctx* ctx, const float* src, const int32_t* soffs, const float* tgt, const int32_t* toffs,
+                   const float* guesses, int nprob, int max_iterations, double max_corr_dist, float* T12,
+                   int32_t* converged, int32_t* iterations, int32_t* n_corr);
+
 /* ---- Trajectory (host only) ----
  * Relative-pose chain of the batched contract: results[i].Tcw is frame i's
  * pose in frame i-1's camera coordinates, so Tcw(i) = Tcw_rel(i) * Tcw(i-1)

@@ -143,3 +143,29 @@ def test_gpu_edge_cases(odo):
     P, Q, _ = _scene(6, n=100, t=(3.0, 0.0, 0.0))
     ref = _check(odo, P, Q)
     assert ref["converged"] == 0
+
+
+@pytest.mark.gpu
+def test_gpu_batch_matches_oracle(odo):
+    """odo_gicp_batch: every pair of a ragged batch (incl. < 20 points and no
+    correspondences) equals the oracle and the one-call API."""
+    pairs = []
+    for seed, n, outl, t in [(31, 400, 0.0, (0.02, -0.01, 0.03)), (32, 19, 0.0, (0.0, 0.0, 0.0)),
+                             (33, 1500, 0.1, (0.02, -0.01, 0.03)), (34, 100, 0.0, (3.0, 0.0, 0.0)),
+                             (35, 60, 0.3, (0.02, -0.01, 0.03))]:
+        P, Q, _ = _scene(seed, n=n, outl=outl, t=t)
+        pairs.append((P, Q, None))
+    P, Q, T = _scene(36, t=(0.08, -0.05, 0.1))
+    guess = T.astype(np.float32).copy()
+    guess[:3, 3] += np.float32([0.01, -0.01, 0.005])
+    pairs.append((P, Q, guess))
+    pairs.append((*_frames_clouds(), None))
+    out = odo.gicp_batch(pairs)
+    for (P, Q, g), (T, conv, it, nc) in zip(pairs, out):
+        ref = O.gicp(P, Q, g)
+        T1, conv1, it1, nc1 = odo.gicp(P, Q, g)
+        assert conv == ref["converged"] == conv1
+        assert it == ref["iterations"] == it1
+        assert nc == ref["n_corr"] == nc1
+        np.testing.assert_allclose(T, ref["T"], rtol=0, atol=1e-5)
+        assert np.array_equal(T, T1)
