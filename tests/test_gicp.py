@@ -11,7 +11,7 @@ library is UNPINNED.
 GPU: odo_gicp (k_gicp.hip) against the oracle on the same clouds: converged
 flag, ICP iterations and correspondence count exactly; T12 within 1e-5 (the
 device's double cos / sin in the gradient are the only non-IEEE steps; every
-sum over correspondences uses the same 64-lane association on both sides).
+sum over correspondences uses the same 256-thread association on both sides).
 """
 import numpy as np
 import pytest
