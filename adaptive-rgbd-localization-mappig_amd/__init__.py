@@ -174,6 +174,14 @@ class Odometry:
         check(self.lib.odo_track_batch_host(self.h, pb, pd, n, ptr(out) if want_results else None))
         return out
 
+    def track_batch_host_sparse_depth(self, hf: "HostFrames", want_results=True, n=None):
+        """odo_track_batch_host_sparse_depth: BGR uploaded, depth read in place
+        from the pinned HostFrames (keep it unchanged until synchronize())."""
+        n = hf.n if n is None else n
+        out = np.zeros(n, PAIR_DTYPE) if want_results else None
+        check(self.lib.odo_track_batch_host_sparse_depth(self.h, hf._pb, hf._pd, n, ptr(out) if want_results else None))
+        return out
+
     def set_timing(self, enable, mode: int = None):
         """Timing mode: 0 off, 1 per-stage HIP events in odo_track_batch
         (serialises the streams a little; see timings()), 2 an event pair around

@@ -108,6 +108,7 @@ SIGNATURES = {
     "odo_track_batch_host": (C.c_int, [P, P, P, C.c_int, P]),
     "odo_host_alloc": (P, [C.c_size_t]),
     "odo_track_batch_async": (C.c_int, [P, P, P, C.c_int, P]),
+    "odo_track_batch_host_sparse_depth": (C.c_int, [P, P, P, C.c_int, P]),
     "odo_seek": (C.c_int, [P, C.c_uint64, C.c_int]),
     "odo_host_free": (C.c_int, [P]),
     "odo_extract_batch": (C.c_int, [P, P, P, C.c_int]),

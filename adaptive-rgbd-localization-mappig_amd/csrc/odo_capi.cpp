@@ -1489,6 +1489,29 @@ int odo_track_batch_host(odo_ctx* c, const uint8_t* bgr, const uint16_t* depth, 
     return finish_batch(c, c->view_set, n, h_results);
 }
 
+int odo_track_batch_host_sparse_depth(odo_ctx* c, const uint8_t* bgr, const uint16_t* depth, int n,
+                                      odo_pair_result* h_results) {
+    if (!c || !bgr || !depth || n <= 0 || n > c->maxb) return fail(ODO_ERR_ARG, "bad track args");
+    // the depth frames stay in page-locked host memory: the keypoint geometry
+    // kernel reads each keypoint's pixel through the mapped pointer over PCIe
+    void* dmap = nullptr;
+    if (hipHostGetDevicePointer(&dmap, (void*)depth, 0) != hipSuccess || !dmap)
+        return fail(ODO_ERR_ARG, "sparse depth: depth must be page-locked host memory (odo_host_alloc)");
+    const int k = c->in_next;
+    c->in_next ^= 1;
+    if (c->in_used[k]) HIPCHK(hipStreamWaitEvent(c->cstream, c->ev_in_free[k], 0));
+    const size_t px = (size_t)n * c->W * c->H;
+    HIPCHK(hipMemcpyAsync(c->bgr_in[k], bgr, px * 3, hipMemcpyHostToDevice, c->cstream));
+    HIPCHK(hipEventRecord(c->ev_in_copied[k], c->cstream));
+    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_in_copied[k], 0));
+    int e;
+    if ((e = odo_track_batch(c, c->bgr_in[k], (const uint16_t*)dmap, n, nullptr))) return e;
+    HIPCHK(hipEventRecord(c->ev_in_free[k], c->stream));
+    c->in_used[k] = true;
+    HIPCHK(hipEventSynchronize(c->ev_in_copied[k]));  // the BGR frames may be refilled
+    return finish_batch(c, c->view_set, n, h_results);
+}
+
 void* odo_host_alloc(size_t bytes) {
     void* p = nullptr;
     if (bytes == 0 || hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) {

@@ -221,6 +221,19 @@ def host_leg(pkg, odo, bgr_b, dep_b, B, W, H, steps, warmup, world, dist, coll_d
     if world > 1:
         dist.barrier()
     dt = max_over_ranks(time.perf_counter() - t0, dist, world, device=coll_dev)
+    # the same with the depth frames read in place (only keypoint pixels cross PCIe)
+    for _ in range(warmup):
+        odo.track_batch_host_sparse_depth(hf, want_results=False)
+    odo.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        odo.track_batch_host_sparse_depth(hf, want_results=False)
+    odo.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt_sd = max_over_ranks(time.perf_counter() - t0, dist, world, device=coll_dev)
     nbytes = hf.bgr.nbytes + hf.depth.nbytes
     hf.close()
     # raw pinned host -> HBM rate of the same bytes, no compute (the PCIe bound)
@@ -239,7 +252,11 @@ def host_leg(pkg, odo, bgr_b, dep_b, B, W, H, steps, warmup, world, dist, coll_d
             "bytes_per_frame": nbytes // B, "h2d_gbs": round(fps / world * nbytes / B / 1e9, 2),
             "raw_pinned_h2d_gbs": round(raw, 2),
             "pcie_bound_fps_per_gpu": round(raw * 1e9 / (nbytes / B), 1),
-            "inputs": "pinned host buffers (odo_host_alloc), one upload per batch on the copy stream"}
+            "inputs": "pinned host buffers (odo_host_alloc), one upload per batch on the copy stream",
+            "sparse_depth": {"value": round(job_throughput(B, steps, world, dt_sd), 2), "unit": "frames/s",
+                             "ms_per_step": round(dt_sd / steps * 1e3, 3),
+                             "api": "odo_track_batch_host_sparse_depth: BGR uploaded, depth read in place "
+                                    "(keypoint pixels only) from the pinned host frames"}}
 
 
 class LocalExchange:

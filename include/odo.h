@@ -86,6 +86,15 @@ int odo_track_batch(odo_ctx* ctx, const uint8_t* d_bgr, const uint16_t* d_depth,
  * h_results non-null it waits for the batch and fills the results. */
 int odo_track_batch_host(odo_ctx* ctx, const uint8_t* bgr, const uint16_t* depth, int n,
                          odo_pair_result* h_results);
+/* odo_track_batch_host with the depth frames read in place: depth must be
+ * page-locked host memory from odo_host_alloc (else ODO_ERR_ARG). Only the BGR
+ * frames are uploaded; the keypoint geometry kernel reads each keypoint's depth
+ * pixel through the mapped pointer, so about 2000 small reads per frame cross
+ * PCIe instead of the 614 kB depth image. The BGR buffer is consumed when the
+ * call returns; the DEPTH buffer must stay valid and unchanged until the batch
+ * has finished (odo_synchronize(), or the call itself when h_results is set). */
+int odo_track_batch_host_sparse_depth(odo_ctx* ctx, const uint8_t* bgr, const uint16_t* depth, int n,
+                                      odo_pair_result* h_results);
 /* odo_track_batch with the n result records copied into PAGE-LOCKED host memory
  * (odo_host_alloc) asynchronously after the batch's PnP: no host sync, the
  * records are valid after odo_synchronize(). Used to stream results. */

@@ -115,3 +115,30 @@ def test_partial_batches_from_pinned_buffer():
         odo.close()
         ref_odo.close()
         hf.close()
+
+
+def test_sparse_depth_batches_equal_device_path():
+    """odo_track_batch_host_sparse_depth: BGR uploaded, depth read in place
+    from pinned memory (keypoint pixels only). The depth buffer must stay
+    unchanged until the batch finishes, so each batch gets its own pinned
+    buffer here; the BGR buffer is refilled right after each call."""
+    pkg = load_pkg()
+    batches = _batches()
+    ref = _device_reference(pkg, batches)
+    hfs = [pkg.HostFrames(B, 640, 480) for _ in batches]
+    odo = pkg.Odometry(_cfg(pkg))
+    try:
+        res = None
+        for k, (b, d) in enumerate(batches):
+            hfs[k].bgr[:] = b
+            hfs[k].depth[:] = d
+            res = odo.track_batch_host_sparse_depth(hfs[k], want_results=(k == NB - 1))
+        _check(odo, res, ref)
+        # pageable depth is refused (it cannot be read in place)
+        dep = np.ascontiguousarray(batches[0][1])
+        rc = pkg.load().odo_track_batch_host_sparse_depth(odo.h, hfs[0]._pb, pkg.ptr(dep), B, None)
+        assert rc != 0
+    finally:
+        odo.close()
+        for h in hfs:
+            h.close()
