@@ -1494,9 +1494,15 @@ int odo_track_batch_host_sparse_depth(odo_ctx* c, const uint8_t* bgr, const uint
     if (!c || !bgr || !depth || n <= 0 || n > c->maxb) return fail(ODO_ERR_ARG, "bad track args");
     // the depth frames stay in page-locked host memory: the keypoint geometry
     // kernel reads each keypoint's pixel through the mapped pointer over PCIe
+    // only HIP page-locked host memory may be read by a kernel (pageable memory
+    // would fault): check the allocation type before taking its device pointer
+    hipPointerAttribute_t attr{};
     void* dmap = nullptr;
-    if (hipHostGetDevicePointer(&dmap, (void*)depth, 0) != hipSuccess || !dmap)
+    if (hipPointerGetAttributes(&attr, depth) != hipSuccess || attr.type != hipMemoryTypeHost ||
+        hipHostGetDevicePointer(&dmap, (void*)depth, 0) != hipSuccess || !dmap) {
+        (void)hipGetLastError();
         return fail(ODO_ERR_ARG, "sparse depth: depth must be page-locked host memory (odo_host_alloc)");
+    }
     const int k = c->in_next;
     c->in_next ^= 1;
     if (c->in_used[k]) HIPCHK(hipStreamWaitEvent(c->cstream, c->ev_in_free[k], 0));

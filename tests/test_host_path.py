@@ -134,10 +134,6 @@ def test_sparse_depth_batches_equal_device_path():
             hfs[k].depth[:] = d
             res = odo.track_batch_host_sparse_depth(hfs[k], want_results=(k == NB - 1))
         _check(odo, res, ref)
-        # pageable depth is refused (it cannot be read in place)
-        dep = np.ascontiguousarray(batches[0][1])
-        rc = pkg.load().odo_track_batch_host_sparse_depth(odo.h, hfs[0]._pb, pkg.ptr(dep), B, None)
-        assert rc != 0
     finally:
         odo.close()
         for h in hfs:
