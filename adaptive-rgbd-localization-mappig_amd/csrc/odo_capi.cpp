@@ -2262,6 +2262,7 @@ static int pnp_ransac_run(odo_ctx* c, const float* Xw, const float* uv, const in
     if (!(confidence > 0.0 && confidence < 1.0)) return fail(ODO_ERR_ARG, "confidence must be in (0, 1)");
     const int H = std::max(iterations, 1);
     if (offs[0] != 0) return fail(ODO_ERR_ARG, "pnp_ransac: offs[0] must be 0");
+    if (nprob > 65535) return fail(ODO_ERR_CAPACITY, "pnp_ransac: more than 65535 problems per call");
     for (int p = 0; p < nprob; p++) {
         const int n = offs[p + 1] - offs[p];
         if (n < 0) return fail(ODO_ERR_ARG, "pnp_ransac: offsets must not decrease");
@@ -2326,11 +2327,13 @@ static int gicp_run(odo_ctx* c, const float* src, const int32_t* soffs, const fl
                     const float* guesses, int nprob, int max_iterations, double max_corr_dist, float* T12,
                     int32_t* converged, int32_t* iterations, int32_t* n_corr) {
     if (soffs[0] != 0 || toffs[0] != 0) return fail(ODO_ERR_ARG, "gicp: offsets must start at 0");
+    if (nprob > 65535) return fail(ODO_ERR_CAPACITY, "gicp: more than 65535 pairs per call");
     int max_ns = 0, max_nt = 0;
     for (int p = 0; p < nprob; p++) {
         const int ns = soffs[p + 1] - soffs[p], nt = toffs[p + 1] - toffs[p];
         if (ns < 0 || nt < 0) return fail(ODO_ERR_ARG, "gicp: offsets must not decrease");
-        if (ns > 65536 || nt > 65536) return fail(ODO_ERR_CAPACITY, "gicp: more than 65536 points");
+        // brute-force neighbour searches: O(ns * nt) per ICP iteration in one workgroup
+        if (ns > 16384 || nt > 16384) return fail(ODO_ERR_CAPACITY, "gicp: more than 16384 points in a cloud");
         max_ns = std::max(max_ns, ns);
         max_nt = std::max(max_nt, nt);
     }

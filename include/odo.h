@@ -206,7 +206,9 @@ int odo_pnp_ransac_batch(odo_ctx* ctx, const float* Xw, const float* uv, const i
  * running (generalizedicp.cpp:33). T12 = the final transformation when
  * converged, identity otherwise (generalizedicp.cpp:76-88); iterations = ICP
  * iterations run, n_corr = correspondences of the last one. Covariances,
- * correspondences and the BFGS all run on the GPU (k_gicp.hip). */
+ * correspondences and the BFGS all run on the GPU (k_gicp.hip); neighbour
+ * searches are brute force, so clouds hold at most 16384 points
+ * (ODO_ERR_CAPACITY; RANSAC's matched clouds are a few hundred). */
 int odo_gicp(odo_ctx* ctx, const float* src, int ns, const float* tgt, int nt, const float guess[16],
              int max_iterations, double max_corr_dist, float T12[16], int* converged, int* iterations, int* n_corr);
 
