@@ -33,6 +33,7 @@ constexpr int GI_LANES = 64;
 constexpr int GI_THREADS = 256;  // the ICP / BFGS workgroup: 4 waves share every pass over the correspondences
 constexpr int GI_WAVES = GI_THREADS / GI_LANES;
 constexpr int GI_NV = 12;        // values reduced per gradient evaluation
+constexpr int GI_STAGE = 4096;   // clouds up to this many points are staged in LDS (48 KB)
 
 __device__ __forceinline__ double s3(double a, double b, double c) { return a + (b + c); }
 
@@ -47,17 +48,9 @@ __device__ __forceinline__ float dist2f(const float* a, const float* b) {
     return r;
 }
 
-// grid (point blocks, problems, 2): z = 0 the target clouds, z = 1 the sources
-__global__ __launch_bounds__(64) void k_gicp_cov(const float* __restrict__ src, const int* __restrict__ soffs,
-                                                 double* __restrict__ Cs, const float* __restrict__ tgt,
-                                                 const int* __restrict__ toffs, double* __restrict__ Ct, double eps) {
-    const int pb = blockIdx.y;
-    const int* offs = blockIdx.z ? soffs : toffs;
-    const int n = offs[pb + 1] - offs[pb];
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= n || soffs[pb + 1] - soffs[pb] < 20 || toffs[pb + 1] - toffs[pb] < 20) return;
-    const float* __restrict__ P = (blockIdx.z ? src : tgt) + 3 * (size_t)offs[pb];
-    double* __restrict__ C = (blockIdx.z ? Cs : Ct) + 9 * (size_t)offs[pb];
+// computeCovariances for point q of a cloud P of n points (LDS or global)
+__device__ __forceinline__ void cov_point(const float* __restrict__ P, int n, int q, double eps,
+                                          double* __restrict__ C) {
     // the sorted top 20 in registers: +inf padding stands for "fewer than 20
     // so far", a candidate is inserted after equal distances (ties to the lower
     // index, as the scan is in index order)
@@ -122,6 +115,28 @@ __global__ __launch_bounds__(64) void k_gicp_cov(const float* __restrict__ src, 
     }
 #pragma unroll
     for (int k = 0; k < 9; k++) C[9 * q + k] = out[k];
+}
+
+// grid (point blocks, problems, 2): z = 0 the target clouds, z = 1 the sources
+__global__ __launch_bounds__(64) void k_gicp_cov(const float* __restrict__ src, const int* __restrict__ soffs,
+                                                 double* __restrict__ Cs, const float* __restrict__ tgt,
+                                                 const int* __restrict__ toffs, double* __restrict__ Ct, double eps) {
+    const int pb = blockIdx.y;
+    const int* offs = blockIdx.z ? soffs : toffs;
+    const int n = offs[pb + 1] - offs[pb];
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    // whole blocks leave together (the staging below needs every thread)
+    if ((int)(blockIdx.x * blockDim.x) >= n || soffs[pb + 1] - soffs[pb] < 20 || toffs[pb + 1] - toffs[pb] < 20) return;
+    const float* __restrict__ Pg = (blockIdx.z ? src : tgt) + 3 * (size_t)offs[pb];
+    double* __restrict__ C = (blockIdx.z ? Cs : Ct) + 9 * (size_t)offs[pb];
+    if (n <= GI_STAGE) {  // the whole cloud in LDS: the scan reads it with uniform addresses
+        __shared__ float cst[3 * GI_STAGE];
+        for (int i = threadIdx.x; i < 3 * n; i += blockDim.x) cst[i] = Pg[i];
+        __syncthreads();
+        if (q < n) cov_point(cst, n, q, eps, C);
+    } else if (q < n) {
+        cov_point(Pg, n, q, eps, C);
+    }
 }
 
 __device__ void inv3(const double* m, double* r) {
@@ -584,6 +599,22 @@ struct GiBfgs {
 };
 
 // out[4]: converged, iterations, n_corr, (pad); T12[16]
+// nearest point of T (n points, LDS or global) to q: strict <, ties to the lower index
+__device__ __forceinline__ int nn_search(const float* __restrict__ T, int n, const float* q, float* bdo) {
+    float bd = dist2f(q, T);
+    int best = 0;
+    for (int j = 1; j < n; j++) {
+        const float tj[3] = {T[3 * j], T[3 * j + 1], T[3 * j + 2]};
+        const float d = dist2f(q, tj);
+        if (d < bd) {
+            bd = d;
+            best = j;
+        }
+    }
+    *bdo = bd;
+    return best;
+}
+
 // one workgroup per problem of the batch
 __global__ __launch_bounds__(GI_THREADS) void k_gicp(const float* __restrict__ src, const float* __restrict__ tgt,
                                                    const double* __restrict__ Cs, const double* __restrict__ Ct,
@@ -645,15 +676,8 @@ __global__ __launch_bounds__(GI_THREADS) void k_gicp(const float* __restrict__ s
                 const float pi[3] = {outp[3 * i], outp[3 * i + 1], outp[3 * i + 2]};
                 float q[3];
                 xform4f(Tcur, pi, q);
-                float bd = dist2f(q, tgt);
-                for (int j = 1; j < nt; j++) {
-                    const float tj[3] = {tgt[3 * j], tgt[3 * j + 1], tgt[3 * j + 2]};
-                    const float d = dist2f(q, tj);
-                    if (d < bd) {
-                        bd = d;
-                        best = j;
-                    }
-                }
+                float bd;
+                best = nn_search(tgt, nt, q, &bd);  // (an LDS-staged target measured no faster)
                 if ((double)bd < dist_threshold) {
                     hit = true;
                     const double* C1 = Cs + 9 * i;
