@@ -549,12 +549,16 @@ __global__ __launch_bounds__(PR_RNG_THREADS) void k_pr_subsets(const int* __rest
             int v;
             for (;;) {
                 state = (uint64_t)(unsigned)state * 4164903690U + (unsigned)(state >> 32);
+                // x % n: the double quotient is floor(x / n) or one off, the
+                // 32-bit remainder (mod 2^32) is corrected once either way
                 const uint32_t x = (uint32_t)state;
-                int64_t q = (int64_t)((double)x * inv);
-                int64_t rem = (int64_t)x - q * n;
-                if (rem < 0) rem += n;
-                if (rem >= n) rem -= n;
-                v = (int)rem;
+                const uint32_t q = (uint32_t)((double)x * inv);
+                int rem = (int)(x - q * (uint32_t)n);
+                if (rem < 0)
+                    rem += n;
+                else if (rem >= n)
+                    rem -= n;
+                v = rem;
                 bool dup = false;
 #pragma unroll
                 for (int j = 0; j < i; j++) dup |= sub[j] == v;
