@@ -12,21 +12,23 @@ import ctypes as C
 import numpy as np
 
 from . import _abi
-from ._abi import (DETECTOR_ADAPTIVE_FAST, DETECTOR_ADAPTIVE_ORB, DETECTOR_ORB_SLAM2, AdaptiveParams, Calib, Config, DMatch, PnPRansacResult,
+from ._abi import (DETECTOR_ADAPTIVE_FAST, DETECTOR_ADAPTIVE_ORB, DETECTOR_ORB_SLAM2, KNN_FORM_FP4, KNN_FORM_VALU,
+                   AdaptiveParams, Calib, Config, DMatch, PnPRansacResult,
                    DMATCH_DTYPE, KP_DTYPE, OrbParams, PAIR_DTYPE, PairResult, RansacParams, Rng, check, load, ptr)
 
 __all__ = ["Odometry", "HostFrames", "PinnedResults", "default_config", "load", "KP_DTYPE", "DMATCH_DTYPE", "PAIR_DTYPE", "rng_stream",
            "kabsch", "Calib", "OrbParams", "RansacParams", "Config", "AdaptiveParams", "DETECTOR_ORB_SLAM2",
-           "DETECTOR_ADAPTIVE_FAST", "DETECTOR_ADAPTIVE_ORB"]
+           "DETECTOR_ADAPTIVE_FAST", "DETECTOR_ADAPTIVE_ORB", "KNN_FORM_FP4", "KNN_FORM_VALU"]
 
 
 def default_config(width=640, height=480, max_batch=1, nfeatures=1000, iterations=200, seed=0x5EED0000,
-                   calib=None, detector=_abi.DETECTOR_ORB_SLAM2) -> Config:
+                   calib=None, detector=_abi.DETECTOR_ORB_SLAM2, forms=None) -> Config:
     """Reference defaults (extractor.cpp:86, odometry.cpp:28, common.h FR1).
     detector: DETECTOR_ORB_SLAM2 (main.cpp:19-21), DETECTOR_ADAPTIVE_FAST
     (Extractor(FAST, ORB, ADAPTIVE), extractor.cpp:55-77) or
     DETECTOR_ADAPTIVE_ORB (Extractor(ORB, ORB, ADAPTIVE): the cv::ORB cell
-    detector of detectoradjuster.cpp:29)."""
+    detector of detectoradjuster.cpp:29). forms: odo_kernel_forms fields
+    (knn = KNN_FORM_FP4 / KNN_FORM_VALU, knn_split, ransac_lanes_min_open)."""
     cfg = Config()
     load().odo_default_config(ptr(cfg), width, height, max_batch)
     cfg.detector = detector
@@ -36,6 +38,8 @@ def default_config(width=640, height=480, max_batch=1, nfeatures=1000, iteration
     if calib is not None:
         for k, v in calib.items():
             setattr(cfg.calib, k, v)
+    for k, v in (forms or {}).items():  # odo_kernel_forms: bit-identical kernel alternatives
+        setattr(cfg.forms, k, v)
     return cfg
 
 
@@ -156,31 +160,86 @@ class Odometry:
         keep_prev its first frame starts a segment (a halo frame, no pair)."""
         check(self.lib.odo_seek(self.h, int(pair_index), 1 if keep_prev else 0))
 
+    def _host_frames(self, hf: "HostFrames", n):
+        """(n, bgr pointer, depth pointer) of a HostFrames after checking that it
+        holds n frames of this context's size: the C-ABI trusts n * W * H."""
+        n = hf.n if n is None else int(n)
+        if not 0 < n <= hf.n:
+            raise ValueError(f"n = {n} frames requested from a HostFrames of {hf.n}")
+        if (hf.w, hf.h) != (self.cfg.width, self.cfg.height):
+            raise ValueError(f"HostFrames are {hf.w}x{hf.h}, the context tracks "
+                             f"{self.cfg.width}x{self.cfg.height}")
+        if hf._pb is None:
+            raise ValueError("HostFrames closed")
+        return n, hf._pb, hf._pd
+
     def track_batch_host(self, bgr, depth=None, want_results=True, n=None):
         """Host inputs: numpy arrays (pageable) or a HostFrames (pinned; then
         `n` frames of it, default all). Without results the call returns once
         the host buffers are consumed and the batch is queued (the upload
         overlaps the compute of earlier batches; the batch runs asynchronously)."""
         if isinstance(bgr, HostFrames):
-            hf = bgr
-            n = hf.n if n is None else n
-            pb, pd = hf._pb, hf._pd
+            n, pb, pd = self._host_frames(bgr, n)
         else:
             bgr = np.ascontiguousarray(bgr, np.uint8)
             depth = np.ascontiguousarray(depth, np.uint16)
+            W, H = self.cfg.width, self.cfg.height
             n = bgr.shape[0]
+            if bgr.shape != (n, H, W, 3) or depth.shape != (n, H, W):
+                raise ValueError(f"frames must be (n, {H}, {W}, 3) u8 and (n, {H}, {W}) u16, got "
+                                 f"{bgr.shape} and {depth.shape}")
             pb, pd = ptr(bgr), ptr(depth)
         out = np.zeros(n, PAIR_DTYPE) if want_results else None
         check(self.lib.odo_track_batch_host(self.h, pb, pd, n, ptr(out) if want_results else None))
         return out
 
+    def track_batch_host_async(self, hf: "HostFrames", results: "PinnedResults", row: int, n=None, first: int = 0):
+        """odo_track_batch_host_async: frames [first, first + n) of a HostFrames
+        uploaded and tracked, the records streamed into results.all[row] (valid
+        after synchronize(); the host frames are consumed on return)."""
+        n = (hf.n - first) if n is None else int(n)
+        if first < 0 or not 0 < n <= hf.n - first or n > results.n:
+            raise ValueError(f"frames [{first}, {first + n}) of {hf.n}, result rows of {results.n}")
+        self._host_frames(hf, first + n)
+        fb, fd = hf.w * hf.h * 3, hf.w * hf.h * 2
+        check(self.lib.odo_track_batch_host_async(self.h, C.c_void_p(hf._pb + first * fb),
+                                                  C.c_void_p(hf._pd + first * fd), n,
+                                                  C.c_void_p(results.row_ptr(row))))
+
     def track_batch_host_sparse_depth(self, hf: "HostFrames", want_results=True, n=None):
         """odo_track_batch_host_sparse_depth: BGR uploaded, depth read in place
-        from the pinned HostFrames (keep it unchanged until synchronize())."""
-        n = hf.n if n is None else n
+        from the pinned HostFrames. Until the batch has read it the depth view
+        is made read-only (numpy raises on a refill): depth_wait(),
+        depth_busy() == False or synchronize() release it."""
+        n, pb, pd = self._host_frames(hf, n)
         out = np.zeros(n, PAIR_DTYPE) if want_results else None
-        check(self.lib.odo_track_batch_host_sparse_depth(self.h, hf._pb, hf._pd, n, ptr(out) if want_results else None))
+        check(self.lib.odo_track_batch_host_sparse_depth(self.h, pb, pd, n, ptr(out) if want_results else None))
+        if not want_results:
+            hf.depth.flags.writeable = False
+            self._depth_hold = getattr(self, "_depth_hold", []) + [hf]
         return out
+
+    def _release_depth(self):
+        # the event covers the last sparse batch; earlier ones ran before it
+        # on the same stream
+        for hf in getattr(self, "_depth_hold", []):
+            if hf.depth is not None:
+                hf.depth.flags.writeable = True
+        self._depth_hold = []
+
+    def depth_busy(self) -> bool:
+        """odo_host_depth_query: the last sparse-depth batch may still read its depth frames."""
+        r = self.lib.odo_host_depth_query(self.h)
+        if r < 0:
+            check(r)
+        if r == 0:
+            self._release_depth()
+        return r == 1
+
+    def depth_wait(self):
+        """odo_host_depth_wait: block until the sparse-depth frames are released."""
+        check(self.lib.odo_host_depth_wait(self.h))
+        self._release_depth()
 
     def set_timing(self, enable, mode: int = None):
         """Timing mode: 0 off, 1 per-stage HIP events in odo_track_batch
@@ -204,6 +263,7 @@ class Odometry:
 
     def synchronize(self):
         check(self.lib.odo_synchronize(self.h))
+        self._release_depth()
 
     def frame(self, i: int):
         cap = self.kp_cap

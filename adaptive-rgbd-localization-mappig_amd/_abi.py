@@ -67,11 +67,21 @@ class PairResult(C.Structure):
                 ("n_queries", C.c_int32), ("n_sweeps", C.c_int32), ("n_fit_points", C.c_int32)]
 
 
+class KernelForms(C.Structure):
+    """odo_kernel_forms (include/odo.h): bit-identical kernel alternatives."""
+    _fields_ = [("knn", C.c_int32), ("knn_split", C.c_int32), ("ransac_lanes_min_open", C.c_int32),
+                ("reserved", C.c_int32)]
+
+
 class Config(C.Structure):
     _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("max_batch", C.c_int32),
                 ("orb", OrbParams), ("calib", Calib), ("nn_ratio", C.c_float),
                 ("ransac", RansacParams), ("seed", C.c_uint32), ("detector", C.c_int32),
-                ("adaptive", AdaptiveParams)]
+                ("adaptive", AdaptiveParams), ("forms", KernelForms)]
+
+
+KNN_FORM_FP4 = 0   # include/odo.h ODO_KNN_FORM_FP4
+KNN_FORM_VALU = 1  # include/odo.h ODO_KNN_FORM_VALU
 
 
 DETECTOR_ORB_SLAM2 = 0       # include/odo.h ODO_DETECTOR_ORB_SLAM2
@@ -109,6 +119,9 @@ SIGNATURES = {
     "odo_host_alloc": (P, [C.c_size_t]),
     "odo_track_batch_async": (C.c_int, [P, P, P, C.c_int, P]),
     "odo_track_batch_host_sparse_depth": (C.c_int, [P, P, P, C.c_int, P]),
+    "odo_track_batch_host_async": (C.c_int, [P, P, P, C.c_int, P]),
+    "odo_host_depth_query": (C.c_int, [P]),
+    "odo_host_depth_wait": (C.c_int, [P]),
     "odo_seek": (C.c_int, [P, C.c_uint64, C.c_int]),
     "odo_host_free": (C.c_int, [P]),
     "odo_extract_batch": (C.c_int, [P, P, P, C.c_int]),

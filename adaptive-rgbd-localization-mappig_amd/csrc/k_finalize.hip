@@ -36,6 +36,7 @@ __constant__ int c_umax16[16];    // IC_Angle disc half-widths per |v|
 #endif
 #define FIN_KPW 4              // keypoints per wave
 #define FIN_KPB (4 * FIN_KPW)  // keypoints per workgroup
+#ifdef ODO_TUNING  // retired per-lane-gather form (A/B only: the tuning build)
 __global__ void __launch_bounds__(256, FIN_WAVES_PER_EU) k_finalize(const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
                                                   size_t pyr_stride, const LevelDesc* __restrict__ lv, int nlevels,
                                                   const uint32_t* __restrict__ okp, const int* __restrict__ ocnt,
@@ -196,6 +197,7 @@ __global__ void __launch_bounds__(256, FIN_WAVES_PER_EU) k_finalize(const uint8_
         kp->class_id = -1;
     }
 }
+#endif  // ODO_TUNING
 
 // k_finalize_lds: the same finalisation with each keypoint's two patches
 // staged in LDS by its 16 lanes with row-contiguous dword loads (the IC disc,
@@ -437,18 +439,20 @@ void launch_finalize(hipStream_t st, const uint8_t* pyr, const uint8_t* blur, si
     // waves (16 keypoints, 42.5 KB LDS) per workgroup; 2 (default) at 2 waves
     // (8 keypoints, 21 KB: more workgroups resident per CU)
     static const int staged = [] {
-        const char* e = getenv("ODO_FIN_LDS");
+        const char* e = odo_knob("ODO_FIN_LDS");
         return e ? atoi(e) : 2;
     }();
-    if (staged == 2)
-        hipLaunchKernelGGL(k_finalize_lds<2>, dim3((kp_cap + 7) / 8, nframes), dim3(128), 0, st, pyr, blur, pyr_stride,
-                           lv, nlevels, okp, ocnt, okp_stride, kps, desc, nkp, kp_cap);
-    else if (staged)
+#ifdef ODO_TUNING
+    if (staged == 1)
         hipLaunchKernelGGL(k_finalize_lds<4>, g, dim3(256), 0, st, pyr, blur, pyr_stride, lv, nlevels, okp, ocnt,
                            okp_stride, kps, desc, nkp, kp_cap);
-    else
+    else if (staged == 0)
         hipLaunchKernelGGL(k_finalize, g, dim3(256), 0, st, pyr, blur, pyr_stride, lv, nlevels, okp, ocnt, okp_stride,
                            kps, desc, nkp, kp_cap);
+    else
+#endif
+        hipLaunchKernelGGL(k_finalize_lds<2>, dim3((kp_cap + 7) / 8, nframes), dim3(128), 0, st, pyr, blur, pyr_stride,
+                           lv, nlevels, okp, ocnt, okp_stride, kps, desc, nkp, kp_cap);
     launch_kp_geometry(st, kps, nkp, depth, depth_stride, img_w, cal, kun, xyz, ur, kp_cap, nframes);
 }
 

@@ -269,6 +269,7 @@ ODO_INLINE kmx_v4i kmx_expand16(uint32_t h) {
 // for instructions it sees)
 ODO_INLINE int med3_i32(int a, int b, int c) { return max(min(a, b), min(max(a, b), c)); }
 
+#ifdef ODO_TUNING  // retired int8 form (A/B only: the tuning build)
 // (256, 3): 168 VGPRs, three workgroups per CU (measured 137 us vs 144 us at two)
 __global__ void __launch_bounds__(256, 3) k_knn2_mx(const uint8_t* __restrict__ qdesc, const int* __restrict__ qn,
                                                  size_t q_stride, const uint8_t* __restrict__ tdesc,
@@ -431,6 +432,7 @@ __global__ void __launch_bounds__(256, 3) k_knn2_mx(const uint8_t* __restrict__ 
         }
     }
 }
+#endif  // ODO_TUNING
 
 // ------------------------------------------------------------ FP4 form
 // The same sign-vector product on v_mfma_scale_f32_16x16x128_f8f6f4 with e2m1
@@ -495,7 +497,20 @@ __global__ void __launch_bounds__(256, 3) k_knn2_f4(const uint8_t* __restrict__ 
     const int nact = s_pre[npairs];
     // staging role of this thread: train st_t of a chunk, words 4 st_h .. 4 st_h + 3
     const int st_t = tid >> 1, st_h = tid & 1;
-    for (int g = blockIdx.x; g < nact; g += gridDim.x) {
+    // XCD-aware item order: workgroups are dispatched round robin over the 8
+    // XCDs (blockIdx % 8), so XCD x takes the contiguous item range
+    // [x nact / 8, (x + 1) nact / 8) and strides its own workgroups over it. A
+    // pair's query blocks (consecutive items) then stream the pair's train
+    // descriptors through one XCD's L2 instead of up to five.
+    int g_lo = 0, g_hi = nact, g_first = blockIdx.x, g_step = gridDim.x;
+    if (gridDim.x >= 8) {
+        const int x = blockIdx.x & 7;
+        g_lo = (int)((long)nact * x / 8);
+        g_hi = (int)((long)nact * (x + 1) / 8);
+        g_first = g_lo + (blockIdx.x >> 3);
+        g_step = (gridDim.x - x + 7) >> 3;  // workgroups on XCD x
+    }
+    for (int g = g_first; g < g_hi; g += g_step) {
         int lo = 0, hi = npairs;  // last pair with s_pre[p] <= g
         while (hi - lo > 1) {
             const int mid = (lo + hi) >> 1;
@@ -583,14 +598,23 @@ __global__ void __launch_bounds__(256, 3) k_knn2_f4(const uint8_t* __restrict__ 
                     for (int qt = 0; qt < 4; qt++)
                         acc[qt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
                             kf_op(A[cur][c]), kf_op(B[qt][c]), c == 0 ? C : acc[qt], 4, 4, 0, 127, 0, 127);
+                // top-2 over two new keys at a time (k0 <= k1 holds throughout):
+                // the second smallest of {k0, k1, x0, x1} is min(k1, med3(k0, x0, x1))
+                // and the smallest min3(k0, x0, x1): 3 ops per 2 keys instead of 4
 #pragma unroll
                 for (int qt = 0; qt < 4; qt++)
 #pragma unroll
-                    for (int i = 0; i < 4; i++) {
-                        const float xf = acc[qt][i];
-                        const uint32_t x = __float_as_uint(xf);
-                        k1[qt] = max(min(k0[qt], k1[qt]), min(max(k0[qt], k1[qt]), x));  // v_med3_u32
-                        k0[qt] = min(k0[qt], x);
+                    for (int i = 0; i < 4; i += 2) {
+                        const uint32_t x0 = __float_as_uint(acc[qt][i]), x1 = __float_as_uint(acc[qt][i + 1]);
+                        const uint32_t m = max(min(k0[qt], x0), min(max(k0[qt], x0), x1));  // v_med3_u32
+                        k1[qt] = min(k1[qt], m);
+                        // v_min3_u32 as inline asm (the optimiser would share
+                        // min(k0, x0) with the med3 and issue two v_min_u32). m is
+                        // a dependency only: the asm follows the med3, which
+                        // already read x0 / x1 past the MFMA's result hazard.
+                        uint32_t n0;
+                        asm("v_min3_u32 %0, %1, %2, %3" : "=v"(n0) : "v"(k0[qt]), "v"(x0), "v"(x1), "v"(m));
+                        k0[qt] = n0;
                     }
             }
         };
@@ -1319,7 +1343,7 @@ void launch_knn2(hipStream_t st, const uint8_t* q, const int* qn, size_t q_strid
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_knn2, KNN_TH, 0);
         // ODO_KNN_WG_PER_CU < occupancy leaves wave slots to co-running kernels
-        if (const char* e = getenv("ODO_KNN_WG_PER_CU")) per_cu = std::min(std::max(1, atoi(e)), std::max(1, per_cu));
+        if (const char* e = odo_knob("ODO_KNN_WG_PER_CU")) per_cu = std::min(std::max(1, atoi(e)), std::max(1, per_cu));
         resident = std::max(1, per_cu) * cus;
     }
     const int qblocks = (max_q + KNN_Q - 1) / KNN_Q;
@@ -1347,8 +1371,12 @@ void launch_knn2_mx(hipStream_t st, const uint8_t* q, const int* qn, size_t q_st
         int dev = 0, cus = 256, per_cu = 0;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f4 ? (const void*)k_knn2_f4 : (const void*)k_knn2_mx,
-                                                           256, 0);
+#ifdef ODO_TUNING
+        const void* kf = f4 ? (const void*)k_knn2_f4 : (const void*)k_knn2_mx;
+#else
+        const void* kf = (const void*)k_knn2_f4;
+#endif
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kf, 256, 0);
         resident[f4] = std::max(1, per_cu) * cus;
     }
     if (npairs <= 0 || max_q <= 0) return;
@@ -1363,12 +1391,15 @@ void launch_knn2_mx(hipStream_t st, const uint8_t* q, const int* qn, size_t q_st
     }
     const int items = npairs * ((max_q + KMX_Q - 1) / KMX_Q);  // upper bound; the kernel counts the real ones
     const dim3 grid(std::min(items, resident[f4]));
-    if (f4)
-        hipLaunchKernelGGL(k_knn2_f4, grid, dim3(256), 0, st, q, qn, q_stride, t, tn, t_stride, idx, dist, out_stride,
-                           qlist, qcnt, ql_stride, npairs);
-    else
+#ifdef ODO_TUNING
+    if (!f4) {
         hipLaunchKernelGGL(k_knn2_mx, grid, dim3(256), 0, st, q, qn, q_stride, t, tn, t_stride, idx, dist, out_stride,
                            qlist, qcnt, ql_stride, npairs);
+        return;
+    }
+#endif
+    hipLaunchKernelGGL(k_knn2_f4, grid, dim3(256), 0, st, q, qn, q_stride, t, tn, t_stride, idx, dist, out_stride,
+                       qlist, qcnt, ql_stride, npairs);
 }
 void launch_vo_lm(hipStream_t st, const float* xyz, const int* nkp, int kp_cap, int slot0, float th_depth_m,
                   uint32_t* lm_bits, int lm_words, int32_t* qlist, int* qcnt, int npairs) {

@@ -842,6 +842,7 @@ ODO_INLINE void wave_allsum(double (&v)[NV]) {
     for (int k = 0; k < NV; k++) v[k] = __shfl(x, k << (6 - LG));
 }
 
+#ifdef ODO_TUNING  // retired one-wave-per-pair form (A/B only: the tuning build)
 __global__ void __launch_bounds__(64) k_pnp1(const int32_t* __restrict__ f2_src, const float* __restrict__ xyz,
                                              const float* __restrict__ kun, const float* __restrict__ ur,
                                              const int* __restrict__ nkp, int kp_cap, int slot0, FrameCalib cal,
@@ -1134,6 +1135,7 @@ __global__ void __launch_bounds__(64) k_pnp1(const int32_t* __restrict__ f2_src,
     for (int k = lane; k < ne; k += 64)
         mask[E.idx[k]] = ((uint8_t)__float_as_int(E.b[k].w) & PE_OUT) ? 0 : 1;
 }
+#endif  // ODO_TUNING
 
 }  // namespace odo
 
@@ -1146,7 +1148,7 @@ size_t pnp_edge_bytes() { return PE_BYTES; }
 // SIMDs do not buy back the 4x longer edge passes.
 static int pnp_waves() {
     static int r = [] {
-        const char* e = getenv("ODO_PNP_WAVES");
+        const char* e = odo_knob("ODO_PNP_WAVES");
         return e && atoi(e) == 1 ? 1 : 4;
     }();
     return r;
@@ -1155,11 +1157,13 @@ void launch_pnp(hipStream_t st, const int32_t* f2_src, const float* xyz, const f
                 const int* nkp, int kp_cap, int slot0, FrameCalib cal, const float* T12, const int* pair_valid,
                 const int* n_matches, int min_matches, void* edges, odo_pair_result* res, uint8_t* inlier_mask,
                 int npairs, const int* sel, int sel_val) {
+#ifdef ODO_TUNING
     if (pnp_waves() == 1) {
         hipLaunchKernelGGL(k_pnp1, dim3(npairs), dim3(64), 0, st, f2_src, xyz, kun, ur, nkp, kp_cap, slot0, cal, T12,
                            pair_valid, n_matches, min_matches, edges, res, inlier_mask, sel, sel_val);
         return;
     }
+#endif
     hipLaunchKernelGGL(k_pnp, dim3(npairs), dim3(PNP_NT), 0, st, f2_src, xyz, kun, ur, nkp, kp_cap, slot0, cal, T12,
                        pair_valid, n_matches, min_matches, edges, res, inlier_mask, sel, sel_val);
 }

@@ -1447,7 +1447,7 @@ struct Layout {
 // wave-per-hypothesis work list k_ransac_eval_list instead)
 static int ln_groups() {
     static int r = [] {
-        const char* e = getenv("ODO_RANSAC_LANES");
+        const char* e = odo_knob("ODO_RANSAC_LANES");
         return e ? std::max(0, atoi(e)) : 512;
     }();
     return r;
@@ -1458,7 +1458,7 @@ static int ln_groups() {
 // hypotheses, as in the hard workload). Both are launched; the other exits.
 static int ln_min_open() {
     static int r = [] {
-        const char* e = getenv("ODO_LANES_MIN_OPEN");
+        const char* e = odo_knob("ODO_LANES_MIN_OPEN");
         return e ? std::max(1, atoi(e)) : 32;
     }();
     return r;
@@ -1579,7 +1579,7 @@ void launch_ransac_raw(hipStream_t st, void* scratch, int npairs, int match_cap,
 
 static int ev2_rows() {
     static int r = [] {
-        const char* e = getenv("ODO_EV2_ROWS");
+        const char* e = odo_knob("ODO_EV2_ROWS");
         // default: every remaining hypothesis row in flight. A pair whose best
         // inlier ratio stays just under the 80 % break visits ~all H
         // hypotheses; fewer rows make it take several rounds (measured at
@@ -1593,7 +1593,7 @@ static int ev2_rows() {
 // (pairs x rows) grid instead)
 static int ev2_list() {
     static int r = [] {
-        const char* e = getenv("ODO_EV2_LIST");
+        const char* e = odo_knob("ODO_EV2_LIST");
         return e ? std::max(0, atoi(e)) : 512;
     }();
     return r;
@@ -1658,7 +1658,7 @@ void launch_ransac(hipStream_t st, const void* good, const int* n_good, const in
     const int rows = (H + EV_WAVES - 1) / EV_WAVES;
     // ODO_EV_ROWS0: rows of the first launch (default EV_ROWS0)
     static const int rows0 = [] {
-        const char* e = getenv("ODO_EV_ROWS0");
+        const char* e = odo_knob("ODO_EV_ROWS0");
         return e ? std::max(1, atoi(e)) : EV_ROWS0;
     }();
     const int r0 = std::min(rows, rows0);
@@ -1682,7 +1682,8 @@ void launch_ransac(hipStream_t st, const void* good, const int* n_good, const in
                 // only one of them is launched; both give the same results
                 const int lanes = ln_groups();
                 const bool use_lanes =
-                    lanes && open_hint && *reinterpret_cast<volatile int*>(open_hint) >= ln_min_open();
+                    lanes && open_hint &&
+                    *reinterpret_cast<volatile int*>(open_hint) >= (cfg.lanes_min_open > 0 ? cfg.lanes_min_open : ln_min_open());
                 if (use_lanes)
                     hipLaunchKernelGGL(k_ransac_lanes, dim3(lanes), dim3(64 * LN_WAVES), 0, st, B, cfg, B.lslab,
                                        lanes * LN_WAVES, 1);

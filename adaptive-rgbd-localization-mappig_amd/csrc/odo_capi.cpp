@@ -176,6 +176,10 @@ struct odo_ctx {
     hipStream_t cstream = nullptr;                      // H2D copies of host inputs
     hipEvent_t ev_in_copied[2] = {}, ev_in_free[2] = {};
     bool in_used[2] = {};
+    // the last odo_track_batch_host_sparse_depth batch's depth reads (extraction
+    // stream): the caller's depth buffer is in use until this event
+    hipEvent_t ev_depth_done = nullptr;
+    bool depth_busy = false;
     int in_next = 0;
     // pair buffers ([maxb])
     int2 *knn_idx[NSETS] = {}, *knn_dist[NSETS] = {};  // per frame set
@@ -311,7 +315,7 @@ static inline void tmark(odo_ctx* c, int i, hipStream_t st) {
 // costs 17% throughput (1.63 vs 1.35 ms per 64-frame step). ODO_STREAM_PRIO=1
 // restores the high priority for experiments.
 static int pair_stream_priority() {
-    const char* e = getenv("ODO_STREAM_PRIO");
+    const char* e = odo_knob("ODO_STREAM_PRIO");
     if (!(e && e[0] == '1')) return 0;
     int least = 0, greatest = 0;
     if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return 0;
@@ -320,6 +324,7 @@ static int pair_stream_priority() {
 
 static int sync_all(odo_ctx* c) {
     for (hipStream_t st : c->owned) HIPCHK(hipStreamSynchronize(st));
+    c->depth_busy = false;
     return ODO_OK;
 }
 
@@ -365,6 +370,7 @@ static void free_ctx(odo_ctx* c) {
         if (c->ev_in_free[i]) hipEventDestroy(c->ev_in_free[i]);
     }
     if (c->ev_latch) hipEventDestroy(c->ev_latch);
+    if (c->ev_depth_done) hipEventDestroy(c->ev_depth_done);
     for (hipStream_t st : c->owned) hipStreamDestroy(st);
     if (c->h_open) (void)hipHostFree(c->h_open);
     delete c;
@@ -754,8 +760,11 @@ static int alloc_buffers(odo_ctx* c) {
         if ((e = dalloc(&c->depth_in[i], B * c->W * c->H))) return e;
     }
     c->lm_words = (c->kp_cap + 31) / 32;
-    if (const char* ks = getenv("ODO_KNN_SPLIT")) c->knn_split = std::min(8, std::max(1, atoi(ks)));
-    if (const char* km = getenv("ODO_KNN_MFMA")) c->knn_mx = std::min(2, std::max(0, atoi(km)));
+    // kernel forms (odo_config.forms; all bit-identical)
+    if (c->cfg.forms.knn_split > 0) c->knn_split = std::min(8, c->cfg.forms.knn_split);
+    c->knn_mx = c->cfg.forms.knn == ODO_KNN_FORM_VALU ? KNN_FMT_VALU : KNN_FMT_F4;
+    if (const char* ks = odo_knob("ODO_KNN_SPLIT")) c->knn_split = std::min(8, std::max(1, atoi(ks)));
+    if (const char* km = odo_knob("ODO_KNN_MFMA")) c->knn_mx = std::min(2, std::max(0, atoi(km)));
     if (c->knn_mx) c->knn_split = 1;  // one top-2 slot per query
     for (int i = 0; i < NSETS; i++) {
         if ((e = dalloc(&c->knn_idx[i], (size_t)c->knn_split * B * c->kp_cap))) return e;
@@ -869,6 +878,11 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
     c->H = cfg->height;
     c->maxb = cfg->max_batch;
     c->slots = cfg->max_batch + 1;
+    if (cfg->forms.knn != ODO_KNN_FORM_FP4 && cfg->forms.knn != ODO_KNN_FORM_VALU) {
+        fail(ODO_ERR_ARG, "unknown kNN-2 kernel form");
+        delete c;
+        return nullptr;
+    }
     if (cfg->detector != ODO_DETECTOR_ORB_SLAM2 && cfg->detector != ODO_DETECTOR_ADAPTIVE_FAST &&
         cfg->detector != ODO_DETECTOR_ADAPTIVE_ORB) {
         fail(ODO_ERR_ARG, "unsupported detector");  // extractor.cpp:26-27 terminates here
@@ -879,10 +893,10 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
     c->adaptive_orb = cfg->detector == ODO_DETECTOR_ADAPTIVE_ORB;
     // ODO_SERIAL_STREAMS=1 (profiling): every stage on one stream, no overlap,
     // so per-kernel times are free of cross-stream contention
-    const char* ser = getenv("ODO_SERIAL_STREAMS");
+    const char* ser = odo_knob("ODO_SERIAL_STREAMS");
     c->serial = ser && ser[0] == '1';
-    if (const char* sk = getenv("ODO_SKIP")) c->skip = atoi(sk);
-    if (const char* sc = getenv("ODO_SCHED")) c->sched = atoi(sc);
+    if (const char* sk = odo_knob("ODO_SKIP")) c->skip = atoi(sk);
+    if (const char* sc = odo_knob("ODO_SCHED")) c->sched = atoi(sc);
     // only the streams the schedule uses (each extra stream shares one of the
     // process's GPU_MAX_HW_QUEUES hardware queues with another and serialises
     // against it); the others alias
@@ -896,14 +910,14 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
     if (ok && c->serial) {
         c->pstream = c->pstream2 = c->side = c->pnpa = c->pnpb = c->stream;
     } else if (ok && c->sched == 5) {
-        if (const char* np = getenv("ODO_PSTREAMS")) c->npstreams = std::min(3, std::max(1, atoi(np)));
-        if (const char* kp = getenv("ODO_KNN_PAIR")) c->knn_pair = atoi(kp) != 0;
+        if (const char* np = odo_knob("ODO_PSTREAMS")) c->npstreams = std::min(3, std::max(1, atoi(np)));
+        if (const char* kp = odo_knob("ODO_KNN_PAIR")) c->knn_pair = atoi(kp) != 0;
         ok = mk(&c->pstream, true) && (c->npstreams < 2 || mk(&c->pstream2, true)) &&
              (c->npstreams < 3 || mk(&c->pstream3, true));
         if (c->npstreams < 2) c->pstream2 = c->pstream;
         if (c->npstreams < 3) c->pstream3 = c->pstream;
         c->side = c->pnpa = c->pnpb = c->pstream;
-        const char* bs = getenv("ODO_BLUR_STREAM");
+        const char* bs = odo_knob("ODO_BLUR_STREAM");
         if (ok && bs && atoi(bs) != 0) ok = mk(&c->bstream, false);
     } else if (ok) {
         ok = mk(&c->pstream, true) && mk(&c->pnpa, true) && (c->sched == 0 || mk(&c->side, false)) &&
@@ -924,6 +938,7 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
              hipEventCreateWithFlags(&c->ev_blur[i], hipEventDisableTiming) == hipSuccess;
     if (!c->bstream) c->bstream = c->stream;
     if (ok) ok = hipEventCreateWithFlags(&c->ev_latch, hipEventDisableTiming) == hipSuccess;
+    if (ok) ok = hipEventCreateWithFlags(&c->ev_depth_done, hipEventDisableTiming) == hipSuccess;
     // host-input uploads run on their own stream (the DMA engines), ordered
     // against the extraction stream by events only
     if (ok) ok = mk(&c->cstream, false);
@@ -939,7 +954,8 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
     const double cam_angle_x = 58.0 / 180.0 * M_PI, cam_angle_y = 45.0 / 180.0 * M_PI;
     const double rsx = 3 * tan(cam_angle_x / 640.0), rsy = 3 * tan(cam_angle_y / 480.0);
     c->rcfg = RansacCfg{cfg->ransac.iterations, cfg->ransac.min_inlier_th, cfg->ransac.max_mahalanobis,
-                        cfg->ransac.sample_size, cfg->ransac.check_depth, rsx * rsx, rsy * rsy};
+                        cfg->ransac.sample_size, cfg->ransac.check_depth, rsx * rsx, rsy * rsy, 0,
+                        cfg->forms.ransac_lanes_min_open};
     if (build_geometry(c) != ODO_OK || alloc_buffers(c) != ODO_OK) {
         free_ctx(c);
         return nullptr;
@@ -1466,56 +1482,92 @@ int odo_seek(odo_ctx* c, uint64_t pair_index, int keep_prev) {
 // extraction stream waits for it, so it overlaps the compute of the batches
 // already queued. Buffer k is rewritten only after the extraction that last
 // read it (two batches earlier) is done. The call returns once the host
-// buffers have been consumed (the caller may refill them); with pinned
-// buffers (odo_host_alloc, or hipHostRegister'ed) the DMA engines read them
-// directly, pageable ones are staged by the runtime.
-int odo_track_batch_host(odo_ctx* c, const uint8_t* bgr, const uint16_t* depth, int n, odo_pair_result* h_results) {
+// buffers have been consumed (the caller may refill them), on the error path
+// too; with pinned buffers (odo_host_alloc, or hipHostRegister'ed) the DMA
+// engines read them directly, pageable ones are staged by the runtime.
+// sparse: only the BGR frames are uploaded and the extraction reads the
+// keypoints' depth pixels in place through the mapped pointer (the depth
+// buffer stays in use until ev_depth_done, odo_host_depth_query / _wait).
+// async_res: the result records stream to page-locked memory as in
+// odo_track_batch_async (no host sync).
+static int track_host(odo_ctx* c, const uint8_t* bgr, const uint16_t* depth, int n, bool sparse,
+                      odo_pair_result* h_results, odo_pair_result* async_res) {
     if (!c || !bgr || !depth || n <= 0 || n > c->maxb) return fail(ODO_ERR_ARG, "bad track args");
-    const int k = c->in_next;
-    c->in_next ^= 1;
-    if (c->in_used[k]) HIPCHK(hipStreamWaitEvent(c->cstream, c->ev_in_free[k], 0));
-    const size_t px = (size_t)n * c->W * c->H;
-    HIPCHK(hipMemcpyAsync(c->bgr_in[k], bgr, px * 3, hipMemcpyHostToDevice, c->cstream));
-    HIPCHK(hipMemcpyAsync(c->depth_in[k], depth, px * 2, hipMemcpyHostToDevice, c->cstream));
-    HIPCHK(hipEventRecord(c->ev_in_copied[k], c->cstream));
-    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_in_copied[k], 0));
-    int e;
-    if ((e = odo_track_batch(c, c->bgr_in[k], c->depth_in[k], n, nullptr))) return e;
-    // everything that reads staging buffer k is queued on the extraction stream
-    HIPCHK(hipEventRecord(c->ev_in_free[k], c->stream));
-    c->in_used[k] = true;
-    // the host buffers are free once their copy has landed
-    HIPCHK(hipEventSynchronize(c->ev_in_copied[k]));
-    return finish_batch(c, c->view_set, n, h_results);
-}
-
-int odo_track_batch_host_sparse_depth(odo_ctx* c, const uint8_t* bgr, const uint16_t* depth, int n,
-                                      odo_pair_result* h_results) {
-    if (!c || !bgr || !depth || n <= 0 || n > c->maxb) return fail(ODO_ERR_ARG, "bad track args");
-    // the depth frames stay in page-locked host memory: the keypoint geometry
-    // kernel reads each keypoint's pixel through the mapped pointer over PCIe
-    // only HIP page-locked host memory may be read by a kernel (pageable memory
-    // would fault): check the allocation type before taking its device pointer
-    hipPointerAttribute_t attr{};
     void* dmap = nullptr;
-    if (hipPointerGetAttributes(&attr, depth) != hipSuccess || attr.type != hipMemoryTypeHost ||
-        hipHostGetDevicePointer(&dmap, (void*)depth, 0) != hipSuccess || !dmap) {
-        (void)hipGetLastError();
-        return fail(ODO_ERR_ARG, "sparse depth: depth must be page-locked host memory (odo_host_alloc)");
+    if (sparse) {
+        // only HIP page-locked host memory may be read by a kernel (pageable
+        // memory would fault): check the allocation type before taking its
+        // device pointer
+        hipPointerAttribute_t attr{};
+        if (hipPointerGetAttributes(&attr, depth) != hipSuccess || attr.type != hipMemoryTypeHost ||
+            hipHostGetDevicePointer(&dmap, (void*)depth, 0) != hipSuccess || !dmap) {
+            (void)hipGetLastError();
+            return fail(ODO_ERR_ARG, "sparse depth: depth must be page-locked host memory (odo_host_alloc)");
+        }
     }
     const int k = c->in_next;
     c->in_next ^= 1;
     if (c->in_used[k]) HIPCHK(hipStreamWaitEvent(c->cstream, c->ev_in_free[k], 0));
     const size_t px = (size_t)n * c->W * c->H;
     HIPCHK(hipMemcpyAsync(c->bgr_in[k], bgr, px * 3, hipMemcpyHostToDevice, c->cstream));
+    if (!sparse) HIPCHK(hipMemcpyAsync(c->depth_in[k], depth, px * 2, hipMemcpyHostToDevice, c->cstream));
     HIPCHK(hipEventRecord(c->ev_in_copied[k], c->cstream));
-    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_in_copied[k], 0));
-    int e;
-    if ((e = odo_track_batch(c, c->bgr_in[k], (const uint16_t*)dmap, n, nullptr))) return e;
-    HIPCHK(hipEventRecord(c->ev_in_free[k], c->stream));
-    c->in_used[k] = true;
-    HIPCHK(hipEventSynchronize(c->ev_in_copied[k]));  // the BGR frames may be refilled
+    int e = ODO_OK;
+    if (hipStreamWaitEvent(c->stream, c->ev_in_copied[k], 0) != hipSuccess) e = fail(ODO_ERR_DEVICE, "hipStreamWaitEvent");
+    const uint16_t* dd = sparse ? (const uint16_t*)dmap : c->depth_in[k];
+    if (!e) e = async_res ? odo_track_batch_async(c, c->bgr_in[k], dd, n, async_res)
+                          : odo_track_batch(c, c->bgr_in[k], dd, n, nullptr);
+    if (!e) {
+        // everything that reads staging buffer k (and a sparse batch's depth
+        // frames) is queued on the extraction stream
+        if (hipEventRecord(c->ev_in_free[k], c->stream) != hipSuccess) e = fail(ODO_ERR_DEVICE, "hipEventRecord");
+        c->in_used[k] = true;
+        if (!e && sparse) {
+            if (hipEventRecord(c->ev_depth_done, c->stream) != hipSuccess) e = fail(ODO_ERR_DEVICE, "hipEventRecord");
+            c->depth_busy = true;
+        }
+    }
+    // the host buffers are free once their copy has landed, whatever happened
+    // after the copy was queued
+    const hipError_t se = hipEventSynchronize(c->ev_in_copied[k]);
+    if (e) return e;
+    if (se != hipSuccess) return fail(ODO_ERR_DEVICE, std::string("hipEventSynchronize: ") + hipGetErrorString(se));
     return finish_batch(c, c->view_set, n, h_results);
+}
+
+int odo_track_batch_host(odo_ctx* c, const uint8_t* bgr, const uint16_t* depth, int n, odo_pair_result* h_results) {
+    return track_host(c, bgr, depth, n, false, h_results, nullptr);
+}
+
+int odo_track_batch_host_async(odo_ctx* c, const uint8_t* bgr, const uint16_t* depth, int n,
+                               odo_pair_result* h_results) {
+    if (!h_results) return fail(ODO_ERR_ARG, "null results");
+    return track_host(c, bgr, depth, n, false, nullptr, h_results);
+}
+
+int odo_track_batch_host_sparse_depth(odo_ctx* c, const uint8_t* bgr, const uint16_t* depth, int n,
+                                      odo_pair_result* h_results) {
+    return track_host(c, bgr, depth, n, true, h_results, nullptr);
+}
+
+int odo_host_depth_query(odo_ctx* c) {
+    if (!c) return fail(ODO_ERR_ARG, "null ctx");
+    if (!c->depth_busy) return 0;
+    const hipError_t q = hipEventQuery(c->ev_depth_done);
+    if (q == hipSuccess) {
+        c->depth_busy = false;
+        return 0;
+    }
+    if (q == hipErrorNotReady) return 1;
+    return fail(ODO_ERR_DEVICE, std::string("hipEventQuery: ") + hipGetErrorString(q));
+}
+
+int odo_host_depth_wait(odo_ctx* c) {
+    if (!c) return fail(ODO_ERR_ARG, "null ctx");
+    if (!c->depth_busy) return ODO_OK;
+    HIPCHK(hipEventSynchronize(c->ev_depth_done));
+    c->depth_busy = false;
+    return ODO_OK;
 }
 
 void* odo_host_alloc(size_t bytes) {

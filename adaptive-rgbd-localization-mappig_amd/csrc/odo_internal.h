@@ -5,10 +5,25 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/odo_types.h"
 
 namespace odo {
+
+// Measurement / A-B knobs (stream schedules, stage skipping, retired kernel
+// forms, grid sizes). Only the tuning build (make tuning: -DODO_TUNING,
+// build_tuning/libodo_hip.so, selected with ODO_LIB) reads them from the
+// environment; the production library ignores the environment entirely, so a
+// stray variable cannot change (or invalidate) a production context.
+static inline const char* odo_knob(const char* name) {
+#ifdef ODO_TUNING
+    return getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
 
 #define FAST_ROI_MAX 72  // largest FAST cell ROI side (a level narrower than 2 cells: up to 65)
 
@@ -153,6 +168,7 @@ struct RansacCfg {
     int check_depth;
     double raster_cov_x, raster_cov_y;
     int rows0;  // hypothesis rows (of EV_WAVES) of the first eval launch; set by launch_ransac
+    int lanes_min_open;  // odo_kernel_forms.ransac_lanes_min_open (0 = default)
 };
 
 // ---- launch wrappers (defined next to their kernels)

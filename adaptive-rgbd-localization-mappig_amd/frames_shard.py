@@ -114,6 +114,17 @@ class FramesShard:
             self.odo.track_batch(bgr_ptr, dep_ptr, n, want_results=False)
         return first, n, halo
 
+    def track_step_host(self, step: int, hf, results, row: int):
+        """track_step from pinned host memory (SURVEY §8(d)'s unit): hf is a
+        HostFrames holding the halo frame followed by the chunk's frames (as
+        track_step's pointers); this rank uploads them over its own PCIe link
+        (odo_track_batch_host_async) and the records stream to results.all[row].
+        Returns (first, n, halo)."""
+        first, n, halo = batch_of(step, self.T, self.rank, self.world)
+        self.odo.seek(first, keep_prev=False)
+        self.odo.track_batch_host_async(hf, results, row, n=n, first=0 if halo else 1)
+        return first, n, halo
+
     def stitch(self, step_results: list, steps: list, G_start=None) -> list:
         """Absolute Tcw of this rank's frames for each of `steps` (their result
         records in step_results): local chains, one all_gather of the chunk

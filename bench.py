@@ -6,9 +6,17 @@ Metric (BASELINE.json): frames/sec (extract + match + RANSAC-PnP) at 640x480,
 intrinsics + distortion, 2000 kp, RANSAC 500 hypotheses) on a synthetic
 closed-loop RGB-D sequence (no datasets offline). One step = one batch of
 `--batch` frames through Tracking::Track's hot path (extract every frame,
-kNN-2 + ratio match against its predecessor, Ransac::Iterate, PnPSolver),
-inputs resident in HBM. Multi-GPU: one process per GPU, each tracking its
-own sequence (frames mode, weak scaling, no data-path collective).
+kNN-2 + ratio match against its predecessor, Ransac::Iterate, PnPSolver).
+
+`value` is timed with the inputs already resident in HBM (the measurement
+contract); `from_host` is the same path timed from BGR8 + depth16 in pinned
+host memory (SURVEY §8(d)'s unit, PCIe-inclusive), with its own kernel
+timing. Multi-GPU (N > 1): SURVEY §8(e) frames mode by default — ONE
+sequence, each step's frames split into per-rank chunks with a one-frame
+halo, the DepthCovariance latch broadcast once, the poses stitched with one
+all_gather per run (frames_shard.py); each rank uploads its own chunk over
+its own PCIe link in the from-host leg. `--shard independent` gives every
+rank its own sequence instead (no exchange).
 
 Prints ONE JSON line on rank 0.
 """
@@ -28,19 +36,17 @@ PKG_DIR = os.path.join(ROOT, "adaptive-rgbd-localization-mappig_amd")
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP64_PEAK_TFLOPS = 78.6      # MI355X_MICROARCH.md: FP64 vector spec
-I8_MFMA_PEAK_TOPS = 5033.2   # dense I8 MFMA: 2x the BF16 rate per clock (MI355X_MICROARCH.md), 256 CU x 2.4 GHz
+VALU_PEAK_TOPS = 78.6        # MI355X_MICROARCH.md: 256 CU x 4 SIMD-32 x 32 lanes x 2.4 GHz int32 lane-ops
 F4_MFMA_PEAK_TOPS = 10066.3  # dense FP4 (block-scaled f8f6f4, e2m1): 4x the BF16 rate per clock
 # the algorithmic Hamming work is 16 int32 lane-ops per (query,
 # train) comparison (8 v_xor_b32 + 8 v_bcnt_u32_b32 over the 256-bit
-# descriptors; the top-2 update is excluded). k_knn2 issues 19 (+ key, min, med3).
+# descriptors; the top-2 update is excluded)
 KNN_OPS_PER_CMP = 16
-KNN_ISSUED_OPS_PER_CMP = 19
 # SURVEY §8(d) RANSAC work: ~120 FP64 flops per non-shortcut ErrorFunction2
 # evaluation (E = sweeps x good matches) and ~40 FP32 flops per point added to
 # a TransformationFromCorrespondences fit (F)
 RANSAC_FLOPS_PER_EVAL = 120
 RANSAC_FLOPS_PER_FIT_POINT = 40
-KNN_TRAFFIC = os.path.join(ROOT, "profiles", "r01_knn2_traffic.json")
 KNN_F4_TRAFFIC = os.path.join(ROOT, "profiles", "r02_knn2_f4_traffic.json")
 # on-box peak microbenchmarks (tools/ubench_peak.hip); the fallbacks are the
 # r02 measurements
@@ -88,13 +94,15 @@ def load_synth():
 
 
 def shard_seed(rank: int) -> int:
-    """Each rank tracks its own sequence (independent scene seed)."""
+    """Scene seed of a rank's sequence: rank 0's is the cfg2 sequence (frames
+    mode: every rank tracks chunks of that one sequence; --shard independent:
+    rank r tracks its own sequence with this seed)."""
     return 0x5EED0002 + 7919 * rank
 
 
 def rank_seeds(rank: int):
-    """(scene seed, RANSAC/pair seed base) of one rank: ranks shard the frames
-    (each tracks its own sequence), no data-path collective."""
+    """(scene seed, RANSAC/pair seed base) of one rank's sequence (rank 0 in
+    frames mode, where the pair seeds come from global pair indices)."""
     return shard_seed(rank), 0x5EED0000 + 1000003 * rank
 
 
@@ -113,6 +121,25 @@ def job_throughput(frames_per_step: int, steps: int, world: int, elapsed_max: fl
     return frames_per_step * steps * world / elapsed_max
 
 
+def usable_cores() -> int:
+    """CPUs this process may run on: the affinity mask, capped by a cgroup CPU
+    quota when one is set (the GPU box shows the whole machine's CPUs to
+    nproc, but grants each GPU a share)."""
+    n = len(os.sched_getaffinity(0))
+    for path, parse in (("/sys/fs/cgroup/cpu.max", lambda t: t.split()),
+                        ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", lambda t: [t.strip(), open(
+                            "/sys/fs/cgroup/cpu/cpu.cfs_period_us").read().strip()])):
+        try:
+            with open(path) as f:
+                q, per = parse(f.read())
+            if q not in ("max", "-1"):
+                n = min(n, max(1, -(-int(q) // int(per))))
+            break
+        except (OSError, ValueError):
+            continue
+    return n
+
+
 def host_info():
     """nproc, usable cores and CPU model of this host (the GPU box's when run there)."""
     model = None
@@ -124,10 +151,11 @@ def host_info():
                     break
     except OSError:
         pass
-    return {"nproc": os.cpu_count(), "usable_cores": len(os.sched_getaffinity(0)), "model": model}
+    return {"nproc": os.cpu_count(), "affinity_cores": len(os.sched_getaffinity(0)),
+            "usable_cores": usable_cores(), "model": model}
 
 
-def cpu_baseline(bgr, dep, nfeat, iters, n_frames, reps, adaptive=False, threads=16, inner="fast"):
+def cpu_baseline(bgr, dep, nfeat, iters, n_frames, reps, adaptive=False, threads=None, inner="fast"):
     """The C++ oracle on the first n_frames frames of the same sequence.
 
     Single thread: this thread pinned to one core (taskset -c equivalent),
@@ -178,8 +206,9 @@ def cpu_baseline(bgr, dep, nfeat, iters, n_frames, reps, adaptive=False, threads
     ext_ms = sorted(te for te, _ in passes)[len(passes) // 2] / n_frames * 1e3
     trk_ms = sorted(tt for _, tt in passes)[len(passes) // 2] / max(1, n_frames - 1) * 1e3
 
-    nthr = max(1, min(threads, len(aff)))
-    nf_all = n_frames * 4
+    # all usable cores (affinity mask capped by the cgroup CPU quota)
+    nthr = max(1, min(threads or usable_cores(), len(aff)))
+    nf_all = max(n_frames * 4, 2 * nthr)
 
     def all_cores_pass():
         t0 = time.perf_counter()
@@ -201,42 +230,44 @@ def cpu_baseline(bgr, dep, nfeat, iters, n_frames, reps, adaptive=False, threads
             "all_cores": {"fps": nf_all / ta, "threads": nthr, "frames": nf_all}}
 
 
-def host_leg(pkg, odo, bgr_b, dep_b, B, W, H, steps, warmup, world, dist, coll_dev="cuda"):
-    """Frames/s from BGR8 + depth16 in (pinned) host memory (SURVEY §8(d) unit):
-    odo_track_batch_host uploads each batch on the copy stream into a staging
-    buffer while the compute of the previous batches runs."""
+def timed_leg(odo, submit, steps, warmup, world, dist, coll_dev, kernel_timing=True, inside=None):
+    """The bench contract for one leg: `warmup` untimed steps, then exactly
+    `steps` timed steps bracketed by a barrier + device synchronize on both
+    sides, the wall time taken as the max over ranks. submit(i) queues step i;
+    inside() runs inside the timed region after the last step (frames mode:
+    the pose stitch). With kernel_timing, an event pair brackets every kNN-2
+    launch of the timed steps (on the stream that runs it, odo timing mode 2).
+    Returns (elapsed s, host submit s, (kNN-2 mean ms, launches))."""
     import torch
-    hf = pkg.HostFrames(B, W, H)
-    hf.bgr[:] = bgr_b
-    hf.depth[:] = dep_b
-    for _ in range(warmup):
-        odo.track_batch_host(hf, want_results=False)
+    for i in range(warmup):
+        submit(i)
     odo.synchronize()
+    torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    if kernel_timing:
+        odo.set_timing(None, mode=2)
     t0 = time.perf_counter()
-    for _ in range(steps):
-        odo.track_batch_host(hf, want_results=False)
+    for i in range(steps):
+        submit(warmup + i)
+    sub = time.perf_counter() - t0
     odo.synchronize()
+    if inside is not None:
+        inside()
+    torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    dt = max_over_ranks(time.perf_counter() - t0, dist, world, device=coll_dev)
-    # the same with the depth frames read in place (only keypoint pixels cross PCIe)
-    for _ in range(warmup):
-        odo.track_batch_host_sparse_depth(hf, want_results=False)
-    odo.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        odo.track_batch_host_sparse_depth(hf, want_results=False)
-    odo.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt_sd = max_over_ranks(time.perf_counter() - t0, dist, world, device=coll_dev)
-    nbytes = hf.bgr.nbytes + hf.depth.nbytes
-    hf.close()
-    # raw pinned host -> HBM rate of the same bytes, no compute (the PCIe bound)
+    el = max_over_ranks(time.perf_counter() - t0, dist, world, device=coll_dev)
+    kt = (None, 0)
+    if kernel_timing:
+        kt = odo.kernel_timing()
+        odo.set_timing(False)
+    return el, sub, kt
+
+
+def raw_h2d_gbs(nbytes: int) -> float:
+    """Pinned host -> HBM copy rate of nbytes with no compute (the PCIe bound)."""
+    import torch
     hsrc = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
     ddst = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
     ddst.copy_(hsrc, non_blocking=True)
@@ -247,16 +278,7 @@ def host_leg(pkg, odo, bgr_b, dep_b, B, W, H, steps, warmup, world, dist, coll_d
     torch.cuda.synchronize()
     raw = 3 * nbytes / (time.perf_counter() - t1) / 1e9
     del hsrc, ddst
-    fps = job_throughput(B, steps, world, dt)
-    return {"value": round(fps, 2), "unit": "frames/s", "ms_per_step": round(dt / steps * 1e3, 3), "steps": steps,
-            "bytes_per_frame": nbytes // B, "h2d_gbs": round(fps / world * nbytes / B / 1e9, 2),
-            "raw_pinned_h2d_gbs": round(raw, 2),
-            "pcie_bound_fps_per_gpu": round(raw * 1e9 / (nbytes / B), 1),
-            "inputs": "pinned host buffers (odo_host_alloc), one upload per batch on the copy stream",
-            "sparse_depth": {"value": round(job_throughput(B, steps, world, dt_sd), 2), "unit": "frames/s",
-                             "ms_per_step": round(dt_sd / steps * 1e3, 3),
-                             "api": "odo_track_batch_host_sparse_depth: BGR uploaded, depth read in place "
-                                    "(keypoint pixels only) from the pinned host frames"}}
+    return raw
 
 
 class LocalExchange:
@@ -517,27 +539,10 @@ def gicp_mode(args):
 
 
 def latency_mode(args):
-    """Per-frame latency of the drop-in path: tools/build/frontend_latency runs
-    one Tracking::Track frame at a time through include/odo_frontend.hpp
-    (Extract -> KnnMatch -> Ransac::Iterate -> PnPSolver::Compute, each a
-    synchronous C-ABI call) on the cfg2 sequence; p50 / p99 ms per frame."""
-    import subprocess
-    import tempfile
-    synth = load_synth()
+    """Per-frame latency of the drop-in path alone (also the `latency` field of
+    the track line): p50 / p99 ms per frame and per-stage medians."""
     W, H = args.width, args.height
-    nf = max(args.steps, 16) + 8
-    bgr, dep, _ = synth.make_sequence(64, W, H, seed=0x5EED0002, closed_loop=True)
-    idx = np.arange(nf) % 64
-    exe = os.path.join(ROOT, "tools", "build", "frontend_latency")
-    if not os.path.exists(exe):
-        raise SystemExit("tools/build/frontend_latency missing: run make -C tools (done by __graft_entry__.build)")
-    with tempfile.NamedTemporaryFile(suffix=".bin", dir=os.environ.get("TMPDIR", "/tmp")) as f:
-        f.write(np.ascontiguousarray(bgr[idx]).tobytes())
-        f.write(np.ascontiguousarray(dep[idx]).tobytes())
-        f.flush()
-        out = subprocess.run([exe, f.name, str(W), str(H), str(nf), str(args.iters), "8"], check=True,
-                             capture_output=True, text=True).stdout
-    r = json.loads(out.strip().splitlines()[-1])
+    r = run_latency(args, W, H, max(args.steps, 16) + 8)
     print(json.dumps({"metric": "per-frame latency of the drop-in path (Tracking::Track order, one frame at a time)",
                       "value": r["p50_ms"], "unit": "ms/frame (p50)", "n_gpus": 1, "steps": r["frames"],
                       "warmup": r["warmup"], "higher_is_better": False, "p99_ms": r["p99_ms"], "p90_ms": r["p90_ms"],
@@ -563,7 +568,9 @@ def main():
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--cpu-frames", type=int, default=24, help="oracle sample (frames per timed pass)")
     ap.add_argument("--cpu-reps", type=int, default=5, help="timed oracle passes (median reported)")
-    ap.add_argument("--host-steps", type=int, default=20, help="steps of the from-host leg (0: skip it)")
+    ap.add_argument("--host-steps", type=int, default=1, help="0: skip the from-host legs (they run --steps steps)")
+    ap.add_argument("--latency-frames", type=int, default=120,
+                    help="frames of the per-frame latency leg (odo_frontend.hpp path; 0: skip it)")
     ap.add_argument("--hard-steps", type=int, default=20, help="steps of the hard-workload leg (0: skip it)")
     ap.add_argument("--workload", choices=["default", "hard"], default="default",
                     help="main leg's sequence: the cfg2 proxy or the hard variant (synth hard=True)")
@@ -611,8 +618,76 @@ def main():
             dist.destroy_process_group()
         return
 
+    track_mode(args, rank, world, local_rank, dist)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def knn_roofline(cmp: int, hbm_alg: float, knn_ms, launches, peaks, traffic, alone_ms=None, host_leg=None):
+    """SURVEY §8(d) roofline of the Hamming-match kernel (k_knn2_f4): the
+    algorithmic work is 16 int32 lane-ops per (query, train) comparison (8
+    v_xor_b32 + 8 v_bcnt_u32_b32 over 256 bits); peak = the VALU spec of
+    MI355X_MICROARCH.md (256 CU x 4 SIMD-32 x 32 lanes x 2.4 GHz = 78.6 T).
+    The kernel does the comparisons exactly as sign-vector products on the
+    matrix cores (FP4 operands, 512 MFMA ops each), reported beside it against
+    the dense FP4 spec. kernel_ms = the live mean over the timed region."""
+    if not knn_ms:
+        return None
+    ops = float(KNN_OPS_PER_CMP) * cmp
+    ach = ops / (knn_ms * 1e-3) / 1e12
+    mops = 512.0 * cmp
+
+    def fr(ms):
+        a = ops / (ms * 1e-3) / 1e12
+        return {"kernel_ms": round(ms, 4), "achieved": round(a, 2), "frac": round(a / VALU_PEAK_TOPS, 4)}
+
+    r = {"bound": "valu", "achieved": round(ach, 2), "peak": VALU_PEAK_TOPS, "unit": "Top/s",
+         "frac": round(ach / VALU_PEAK_TOPS, 4), "traffic": traffic, "kernel": "k_knn2_f4",
+         "kernel_ms": round(knn_ms, 4), "launches": launches,
+         "work": f"{cmp} descriptor comparisons x {KNN_OPS_PER_CMP} int32 lane-ops (SURVEY 8(d))",
+         "peak_source": "MI355X_MICROARCH.md VALU spec: 256 CU x 4 SIMD-32 x 32 lanes x 2.4 GHz",
+         "measured_xor_bcnt_peak": round(peaks["valu_xor_bcnt"], 2),
+         "mfma_fp4": {"achieved": round(mops / (knn_ms * 1e-3) / 1e12, 1), "peak": F4_MFMA_PEAK_TOPS,
+                      "frac": round(mops / (knn_ms * 1e-3) / 1e12 / F4_MFMA_PEAK_TOPS, 4),
+                      "work": "512 ops per comparison: v_mfma_scale_f32_16x16x128_f8f6f4, e2m1 signs, K = 256"},
+         "hbm_gbs": round(hbm_alg / (knn_ms * 1e-3) / 1e9, 1)}
+    if alone_ms:
+        r["alone"] = fr(alone_ms)
+        if "knn_f4_mix" in peaks:
+            # the kernel's per-tile instruction mix issued from registers
+            r["alone"]["frac_of_issue_ceiling"] = round(mops / (alone_ms * 1e-3) / 1e12 / peaks["knn_f4_mix"], 4)
+    if host_leg:
+        r["from_host_leg"] = fr(host_leg)
+    return r
+
+
+def run_latency(args, W, H, nframes):
+    """tools/build/frontend_latency: one Tracking::Track frame at a time through
+    include/odo_frontend.hpp (Extract -> KnnMatch -> Ransac::Iterate ->
+    PnPSolver::Compute, each a synchronous C-ABI call) on the cfg2 sequence."""
+    import subprocess
+    import tempfile
+    synth = load_synth()
+    bgr, dep, _ = synth.make_sequence(64, W, H, seed=0x5EED0002, closed_loop=True)
+    idx = np.arange(nframes) % 64
+    exe = os.path.join(ROOT, "tools", "build", "frontend_latency")
+    if not os.path.exists(exe):
+        raise SystemExit("tools/build/frontend_latency missing: run make -C tools (done by __graft_entry__.build)")
+    with tempfile.NamedTemporaryFile(suffix=".bin", dir=os.environ.get("TMPDIR", "/tmp")) as f:
+        f.write(np.ascontiguousarray(bgr[idx]).tobytes())
+        f.write(np.ascontiguousarray(dep[idx]).tobytes())
+        f.flush()
+        out = subprocess.run([exe, f.name, str(W), str(H), str(nframes), str(args.iters), "8"], check=True,
+                             capture_output=True, text=True, timeout=300).stdout
+    return json.loads(out.strip().splitlines()[-1])
+
+
+def track_mode(args, rank, world, local_rank, dist):
+    import torch
+    from importlib import import_module
     pkg = load_pkg()
     synth = load_synth()
+    tj = import_module("arlm_amd.trajectory")
     B, W, H = args.batch, args.width, args.height
     # N > 1: SURVEY §8(e) frames mode by default: ONE sequence, each step's
     # B x N frames split into per-rank chunks with a one-frame halo, the latch
@@ -636,195 +711,154 @@ def main():
         if seq_mode:
             raise SystemExit("ADAPTIVE thresholds carry from frame to frame: not frame-shardable (--shard independent)")
     fb = (W * H * 3, W * H * 2)
-    if seq_mode:
-        # every chunk starts at a multiple of L: its halo is loop frame L - 1
-        hb = np.concatenate([bgr_loop[L - 1:], bgr])
-        hd = np.concatenate([dep_loop[L - 1:], dep])
-        d_bgr = torch.from_numpy(hb).to("cuda")
-        d_dep = torch.from_numpy(hd.view(np.int16)).to("cuda")
-    else:
-        d_bgr = torch.from_numpy(bgr).to("cuda")
-        d_dep = torch.from_numpy(dep.view(np.int16)).to("cuda")
-    cfg = pkg.default_config(W, H, B + 1 if seq_mode else B, nfeatures=args.nfeatures, iterations=args.iters,
-                             seed=pair_seed,
+    # the rank's input frames; frames mode: every chunk starts at a multiple of
+    # L, so its halo is loop frame L - 1, followed by the chunk's B frames
+    hb = np.concatenate([bgr_loop[L - 1:], bgr]) if seq_mode else bgr
+    hd = np.concatenate([dep_loop[L - 1:], dep]) if seq_mode else dep
+    nb = hb.shape[0]
+    d_bgr = torch.from_numpy(hb).to("cuda")                # HBM-resident leg
+    d_dep = torch.from_numpy(hd.view(np.int16)).to("cuda")
+    hf = pkg.HostFrames(nb, W, H)                           # from-host legs (pinned)
+    hf.bgr[:] = hb
+    hf.depth[:] = hd
+    cfg = pkg.default_config(W, H, nb, nfeatures=args.nfeatures, iterations=args.iters, seed=pair_seed,
                              detector=(pkg.DETECTOR_ORB_SLAM2 if not adaptive else
                                        pkg.DETECTOR_ADAPTIVE_ORB if inner == "orb" else pkg.DETECTOR_ADAPTIVE_FAST))
     odo = pkg.Odometry(cfg, device=local_rank % max(1, torch.cuda.device_count()))
     torch.cuda.synchronize()
     coll_dev = "cuda" if args.backend == "nccl" else "cpu"  # where the exchanges' tensors live
-    from importlib import import_module
-    tj = import_module("arlm_amd.trajectory")
+    ktime = not args.no_kernel_timing
+    K, Wm = args.steps, args.warmup
 
     if seq_mode:
         fsm = import_module("arlm_amd.frames_shard")
-        shard = fsm.FramesShard(odo, dist, rank, world, B * world, device=coll_dev)
+        T = B * world
+        shard = fsm.FramesShard(odo, dist, rank, world, T, device=coll_dev)
         # the DepthCovariance latch of global pair 1 (loop frames 0, 1), broadcast
         shard.prime_latch(d_bgr.data_ptr() + fb[0], d_dep.data_ptr() + fb[1])
-        nun = args.warmup + 2
-        ring = pkg.PinnedResults(max(args.steps, nun), B + 1)
+        rows = max(K, Wm, 2) + 1
+        ring = pkg.PinnedResults(rows, B + 1)
+        kstep = [0]  # global step counter across legs (frames repeat every step)
+        timed_steps = []
 
-        def run_step(k, row=None):
-            return shard.track_step(k, d_bgr.data_ptr(), d_dep.data_ptr(), fb,
-                                    results=ring if row is not None else None, row=row or 0)
+        def step(host, keep=None):
+            k = kstep[0]
+            kstep[0] += 1
+            row = k % rows
+            if host:
+                shard.track_step_host(k, hf, ring, row)
+            else:
+                shard.track_step(k, d_bgr.data_ptr(), d_dep.data_ptr(), fb, results=ring, row=row)
+            if keep is not None:
+                keep.append(k)
 
-        for k in range(nun):  # untimed: step 0, warm-up, one more for the statistics
-            run_step(k, k)
+        def stitch_timed():
+            ks = timed_steps[-K:]
+            shard.stitch([ring.all[k % rows][:fsm.batch_of(k, T, rank, world)[1]] for k in ks], ks)
+
+        # untimed: steps 0 and 1 with results for the statistics and the ATE
+        step(False)
+        step(False)
         odo.synchronize()
-        recs = [ring.all[k][:fsm.batch_of(k, B * world, rank, world)[1]].copy() for k in range(nun)]
-        G = shard.stitch(recs, list(range(nun)), G_start=np.linalg.inv(gt_poses[0]))
+        recs = [ring.all[k][:fsm.batch_of(k, T, rank, world)[1]].copy() for k in range(2)]
+        G = shard.stitch(recs, [0, 1], G_start=np.linalg.inv(gt_poses[0]))
         # ATE over rank 0's first loop (global frames 0 .. L-1 of step 0)
         ate_mm = 1000.0 * tj.ate_rmse(tj.camera_centres(G[0][:L]), gt_poses[:L, :3, 3]) if rank == 0 else None
         res_q = recs[-1][1:]  # a halo step: B genuine pairs, record p+1 = pair (frame p, frame p+1)
         pair_frame0 = 1       # batch frame of record 0 of res_q
-        torch.cuda.synchronize()
-        dist.barrier()
-        if not args.no_kernel_timing:
-            odo.set_timing(None, mode=2)
-        t0 = time.perf_counter()
-        for s_ in range(args.steps):
-            run_step(nun + s_, s_)
-        submit = time.perf_counter() - t0
-        odo.synchronize()
-        # the cross-rank pose chain of the timed steps (one all_gather)
-        shard.stitch([ring.all[s_][:fsm.batch_of(nun + s_, B * world, rank, world)[1]] for s_ in range(args.steps)],
-                     [nun + s_ for s_ in range(args.steps)])
-        torch.cuda.synchronize()
-        dist.barrier()
-        elapsed = max_over_ranks(time.perf_counter() - t0, dist, world, device=coll_dev)
-        knn_ms, knn_launches = odo.kernel_timing() if not args.no_kernel_timing else (None, 0)
+
+        def leg(host):
+            return timed_leg(odo, lambda i: step(host, timed_steps if i >= Wm else None), K, Wm, world, dist,
+                             coll_dev, ktime, inside=stitch_timed)
+
+        # the headline: inputs resident in HBM
+        elapsed, submit, (knn_ms, knn_launches) = leg(False)
+        # from host memory: every rank uploads its chunk + halo over its own link
+        h_el, h_sub, (h_knn_ms, _) = leg(True) if args.host_steps > 0 else (None, None, (None, 0))
+        sd = None
         odo.set_timing(True)
-        run_step(nun + args.steps)
+        step(False)
         odo.synchronize()
         timings = odo.timings()
         odo.set_timing(False)
         ring.close()
+        frames_per_rank = B  # pairs (= new frames) per rank per step
     else:
         # untimed: one batch with results for the sanity summary
         res = odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=True)
-        for _ in range(args.warmup):
-            odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=False)
         # untimed: a batch whose pair 0 links to the previous batch, as in the timed
         # steps, for the kNN-2 query counts (F1 keypoints holding a VO landmark)
         res_q = odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=True)
         pair_frame0 = 0
         odo.synchronize()
-        torch.cuda.synchronize()
         # quality sanity: the untimed first batch's chained poses against the
         # sequence's ground truth (absolute trajectory error, TUM definition)
         Tcw = tj.chain_poses(res[:L], np.linalg.inv(gt_poses[0]).astype(np.float32))
         ate_mm = 1000.0 * tj.ate_rmse(tj.camera_centres(Tcw), gt_poses[:L, :3, 3])
-
-        if world > 1:
-            dist.barrier()
-        # Hamming-match (kNN-2) launches are bracketed by HIP events on the stream
-        # that runs them (a pair stream by default) inside the timed region (odo
-        # timing mode 2)
-        if not args.no_kernel_timing:
-            odo.set_timing(None, mode=2)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=False)
-        submit = time.perf_counter() - t0  # host time to queue the K steps (asynchronous)
-        odo.synchronize()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        elapsed = max_over_ranks(time.perf_counter() - t0, dist, world, device=coll_dev)
-        knn_ms, knn_launches = odo.kernel_timing() if not args.no_kernel_timing else (None, 0)
-
+        # the headline: inputs resident in HBM
+        elapsed, submit, (knn_ms, knn_launches) = timed_leg(
+            odo, lambda i: odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=False),
+            K, Wm, world, dist, coll_dev, ktime)
+        h_el = sd = None
+        h_knn_ms = None
+        if args.host_steps > 0:
+            # from pinned host memory: one upload per batch on the copy stream
+            h_el, h_sub, (h_knn_ms, _) = timed_leg(odo, lambda i: odo.track_batch_host(hf, want_results=False),
+                                                   K, Wm, world, dist, coll_dev, ktime)
+            # the same with the depth frames read in place (keypoint pixels only)
+            sd_el, _, _ = timed_leg(odo, lambda i: odo.track_batch_host_sparse_depth(hf, want_results=False),
+                                    K, Wm, world, dist, coll_dev, False)
+            sd = {"value": round(job_throughput(B, K, world, sd_el), 2), "unit": "frames/s",
+                  "ms_per_step": round(sd_el / K * 1e3, 3),
+                  "api": "odo_track_batch_host_sparse_depth: BGR uploaded, depth read in place "
+                         "(keypoint pixels only) from the pinned host frames"}
         # per-stage times: one extra (untimed) step with the stage events on
         odo.set_timing(True)
         odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=False)
         odo.synchronize()
         timings = odo.timings()
         odo.set_timing(False)
-    value = job_throughput(B, args.steps, world, elapsed)
-    ms_per_step = elapsed / args.steps * 1e3
+        frames_per_rank = B
+    value = job_throughput(frames_per_rank, K, world, elapsed)
+    ms_per_step = elapsed / K * 1e3
+
+    from_host = None
+    if h_el is not None:
+        nbytes_frame = fb[0] + fb[1]
+        fps = job_throughput(frames_per_rank, K, world, h_el)
+        raw = raw_h2d_gbs(nb * nbytes_frame)
+        from_host = {"value": round(fps, 2), "unit": "frames/s", "ms_per_step": round(h_el / K * 1e3, 3),
+                     "steps": K, "warmup": Wm, "bytes_per_frame": nbytes_frame,
+                     "h2d_gbs_per_gpu": round(nb * nbytes_frame * K / h_el / 1e9, 2),
+                     "raw_pinned_h2d_gbs": round(raw, 2),
+                     "pcie_bound_fps_per_gpu": round(raw * 1e9 / nbytes_frame * frames_per_rank / nb, 1),
+                     "inputs": ("pinned host buffers (odo_host_alloc), each rank uploading its chunk + halo "
+                                "(odo_track_batch_host_async)" if seq_mode else
+                                "pinned host buffers (odo_host_alloc), one upload per batch on the copy stream "
+                                "(odo_track_batch_host)"),
+                     "sparse_depth": sd}
+    hf.close()
 
     # keypoints of the frames the statistics' pairs match against (every batch
     # holds the same cycled frames): pair record i's train frame
     nkp = [len(odo.frame(pair_frame0 + i)["kps"]) for i in range(B)]
     nkp_mean = float(np.mean(nkp))
     peaks = measured_peaks()
-    # Roofline of the Hamming-match kernel (k_knn2), the kernel the north star
-    # names. Brute-force kNN-2 re-reads each 32-byte descriptor ~2000 times from
-    # LDS, so it is bound by the integer VALU issue rate, not by HBM: achieved =
-    # SURVEY §8(d)'s algorithmic 16 lane-ops per comparison x the launch's
-    # comparisons / its live mean duration; peak = the measured on-box rate of
-    # the same v_xor_b32 + v_bcnt_u32_b32 mix (profiles/r02_ubench_peak.jsonl).
-    roofline = None
+    # result i = pair (frame i-1, frame i): kNN-2 compares the query frame's
+    # landmark keypoints (n_queries) with every keypoint of frame i
     nq = res_q["n_queries"]
-    if knn_ms:
-        # result i = pair (frame i-1, frame i); frame -1 is the previous batch's
-        # last frame (the same sequence is tracked every step). kNN-2 compares
-        # the query frame's landmark keypoints (n_queries) with every keypoint
-        # of frame i: Matcher::KnnMatch drops the other queries' matches
-        cmp = int(sum(int(nq[i]) * nkp[i] for i in range(B)))
-        ops = float(KNN_OPS_PER_CMP) * cmp
-        ach = ops / (knn_ms * 1e-3) / 1e12
-        peak = peaks["valu_xor_bcnt"]
-        traffic = None
-        if os.path.exists(KNN_TRAFFIC):
-            with open(KNN_TRAFFIC) as f:
-                tr = json.load(f)
-            # PMC-measured HBM bytes (FETCH_SIZE x2 + WRITE_SIZE) per launch;
-            # scaled per pair when this run's batch differs from the profiled one
-            traffic = tr.get("hbm_bytes_per_launch") if tr.get("batch") == B else \
-                (tr["hbm_bytes_per_pair"] * B if "hbm_bytes_per_pair" in tr else None)
-        hbm_alg = sum(32 * int(nq[i]) + 32 * nkp[i] + 16 * int(nq[i]) for i in range(B))
-        form = os.environ.get("ODO_KNN_MFMA", "2")
-        if form != "0":
-            # the exact sign-vector formulation on the matrix cores: 256 MACs =
-            # 512 ops per comparison, against the dense MFMA peak of the operand
-            # type (MI355X_MICROARCH.md: I8 2x, FP4 4x the BF16 rate per clock).
-            # kernel_ms is the live mean inside the timed region, where the
-            # launch shares the CUs with the next batch's extraction; alone_ms
-            # is the same launch in the one-stream stage-timing step.
-            f4 = form == "2"
-            mpk = F4_MFMA_PEAK_TOPS if f4 else I8_MFMA_PEAK_TOPS
-            mops = 512.0 * cmp
-            mach = mops / (knn_ms * 1e-3) / 1e12
-            # the last batch's kNN-2 launch re-run alone (HIP events, idle device)
-            alone = odo.knn_replay_ms(20) if hasattr(odo, "knn_replay_ms") else timings.get("knn2")
-            ftraffic = None
-            if f4 and os.path.exists(KNN_F4_TRAFFIC):
-                with open(KNN_F4_TRAFFIC) as fh:
-                    tr4 = json.load(fh)
-                # PMC HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, gfx950
-                # correction), scaled per pair when the batch differs
-                ftraffic = tr4["hbm_bytes_per_launch"] if tr4.get("batch") == B else tr4["hbm_bytes_per_pair"] * B
-            roofline = {"bound": "mfma", "achieved": round(mach, 2), "peak": mpk, "unit": "Top/s",
-                        "frac": round(mach / mpk, 4), "traffic": ftraffic,
-                        "kernel": "k_knn2_f4" if f4 else "k_knn2_mx", "kernel_ms": round(knn_ms, 4),
-                        "launches": knn_launches,
-                        "work": f"{cmp} descriptor comparisons x 512 ops (" +
-                                ("v_mfma_scale_f32_16x16x128_f8f6f4, e2m1 operands" if f4 else
-                                 "v_mfma_i32_16x16x64_i8") + ", K = 256)",
-                        "measured_peak": round(peaks["mfma_scale_f32_16x16x128_f4" if f4 else
-                                                     "mfma_i32_16x16x64_i8"], 1),
-                        "equiv_valu_16op": {"achieved": round(ach, 3), "peak": round(peak, 2), "unit": "Top/s",
-                                            "frac": round(ach / peak, 4),
-                                            "note": "SURVEY 8(d) 16 lane-ops per comparison vs the measured "
-                                                    "xor+bcnt VALU rate"},
-                        "hbm_gbs": round(hbm_alg / (knn_ms * 1e-3) / 1e9, 1)}
-            if alone:
-                aach = mops / (alone * 1e-3) / 1e12
-                roofline["alone"] = {"ms": round(alone, 4), "achieved": round(aach, 2), "frac": round(aach / mpk, 4)}
-                if f4 and "knn_f4_mix" in peaks:
-                    # the kernel's irreducible per-tile instruction mix (2 MFMAs +
-                    # 8 top-2 VALU ops per 256 comparisons) issued from registers
-                    roofline["alone"]["issue_ceiling"] = round(peaks["knn_f4_mix"], 1)
-                    roofline["alone"]["frac_of_issue_ceiling"] = round(aach / peaks["knn_f4_mix"], 4)
-        else:
-            roofline = {"bound": "valu", "achieved": round(ach, 3), "peak": round(peak, 2),
-                        "unit": "Top/s", "frac": round(ach / peak, 4), "traffic": traffic,
-                        "kernel": "k_knn2", "kernel_ms": round(knn_ms, 4), "launches": knn_launches,
-                        "work": f"{cmp} descriptor comparisons x {KNN_OPS_PER_CMP} int32 lane-ops (SURVEY 8(d))",
-                        "peak_source": "measured v_xor_b32 + v_bcnt_u32_b32 rate, profiles/r02_ubench_peak.jsonl",
-                        "issued_ops_per_cmp": KNN_ISSUED_OPS_PER_CMP,
-                        # algorithmic HBM bytes: every descriptor read once, 16 B of top-2 out per query
-                        "hbm_gbs": round(hbm_alg / (knn_ms * 1e-3) / 1e9, 1)}
+    cmp = int(sum(int(nq[i]) * nkp[i] for i in range(B)))
+    hbm_alg = sum(32 * int(nq[i]) + 32 * nkp[i] + 16 * int(nq[i]) for i in range(B))
+    traffic = None
+    if os.path.exists(KNN_F4_TRAFFIC):
+        with open(KNN_F4_TRAFFIC) as fh:
+            tr4 = json.load(fh)
+        # PMC HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, gfx950
+        # correction), scaled per pair when the batch differs
+        traffic = tr4["hbm_bytes_per_launch"] if tr4.get("batch") == B else tr4["hbm_bytes_per_pair"] * B
+    alone = odo.knn_replay_ms(20) if knn_ms else None
+    roofline = knn_roofline(cmp, hbm_alg, knn_ms, knn_launches, peaks, traffic, alone, h_knn_ms) \
+        if cfg.forms.knn == pkg.KNN_FORM_FP4 else None
 
     # the other SURVEY §8(d) legs, from the per-stage (one stream, events
     # between stages) times of the untimed timing step
@@ -852,14 +886,23 @@ def main():
                           "work": f"E = sum(n_sweeps x n_good) x {RANSAC_FLOPS_PER_EVAL} FP64 flops"}
     if "pnp" in timings:
         legs["pnp"] = {"bound": "latency", "ms": round(timings["pnp"], 4)}
-
-    from_host = None
-    if args.host_steps > 0 and not seq_mode:
-        from_host = host_leg(pkg, odo, bgr, dep, B, W, H, args.host_steps, 2, world, dist, coll_dev)
+    odo.close()
+    del d_bgr, d_dep
 
     hard = None
     if args.hard_steps > 0 and world == 1 and not adaptive:
         hard = hard_leg(pkg, synth, args, B, W, H, local_rank % max(1, torch.cuda.device_count()))
+
+    latency = None
+    if args.latency_frames > 0 and world == 1 and not adaptive and rank == 0:
+        r = run_latency(args, W, H, args.latency_frames + 8)
+        latency = {"p50_ms": r["p50_ms"], "p90_ms": r["p90_ms"], "p99_ms": r["p99_ms"], "mean_ms": r["mean_ms"],
+                   "max_ms": r["max_ms"], "frames": r["frames"], "warmup": r["warmup"],
+                   "stage_median_ms": r["stage_median_ms"],
+                   "workload": f"fr1/desk proxy {W}x{H}, 1000 kp (the reference's nFeatures, common.h:77), "
+                               f"RANSAC {args.iters}, one frame at a time",
+                   "path": "include/odo_frontend.hpp Extractor / Matcher / Ransac / PnPSolver over the per-stage "
+                           "C-ABI (tools/frontend_latency.cpp), Tracking::Track order"}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -874,7 +917,7 @@ def main():
                "all_cores": {"value": round(cb["all_cores"]["fps"], 2), "unit": "frames/s",
                              "cores": cb["all_cores"]["threads"],
                              "sample": f"{cb['all_cores']['frames']} frames, frames-parallel thread pool "
-                                       f"(extraction and pairs), median of 3 passes"}}
+                                       f"(extraction and pairs) over every usable core, median of 3 passes"}}
 
     if rank == 0:
         ok = res_q
@@ -885,21 +928,23 @@ def main():
             "value": round(value, 2),
             "unit": "frames/s",
             "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
+            "steps": K,
+            "warmup": Wm,
             "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8/i32 (extract, match), f32+f64 (ransac, pnp)",
             "data": "synthetic (ray-cast textured room, closed-loop trajectory; no dataset offline)",
+            "inputs": "resident in HBM when the timed region starts (from_host: the same path from pinned host memory)",
             "config": {"workload": (f"cfg2 fr1/desk proxy {W}x{H}, {args.nfeatures} kp, RANSAC {args.iters}"
                                     + (" (hard variant)" if args.workload == "hard" else "")
                                     if not adaptive else
                                     f"fr1/desk proxy {W}x{H}, ADAPTIVE 3x3 {'cv::ORB' if inner == 'orb' else 'FAST'} "
                                     f"grid + ORB (<=1000 kp), "
                                     f"RANSAC {args.iters}"),
-                       "frames_per_step": B, "global_batch": B * world, "parallelism": (f"sequence chunks x{world} (+1-frame halo, latch broadcast, pose stitch)"
+                       "frames_per_step": B, "global_batch": B * world,
+                       "parallelism": (f"sequence chunks x{world} (+1-frame halo, latch broadcast, pose stitch)"
                                        if seq_mode else f"frames x{world}"),
                        "mean_keypoints": round(nkp_mean, 1),
                        "mean_knn_queries": round(float(np.mean(res_q["n_queries"])), 1),
@@ -908,17 +953,15 @@ def main():
                        "mean_ransac_visited": round(float(np.mean(ok["visited"])), 1),
                        "ate_mm": round(ate_mm, 3)},
             "stage_ms": {k: round(v, 4) for k, v in timings.items()},
-            "host_submit_ms_per_step": round(submit / args.steps * 1e3, 3),
+            "host_submit_ms_per_step": round(submit / K * 1e3, 3),
             "from_host": from_host,
             "hard_workload": hard,
+            "latency": latency,
             "roofline": roofline,
             "roofline_legs": legs,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    odo.close()
-    if world > 1:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

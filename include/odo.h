@@ -35,6 +35,21 @@ extern "C" {
 #define ODO_DETECTOR_ADAPTIVE_ORB 2   /* ORB / ORB / ADAPTIVE: 3x3 grid-adapted cv::ORB detector (Harris,
                                          8 levels; detectoradjuster.cpp:29) + cv::ORB descriptor */
 
+/* odo_config.forms: which of several bit-identical kernel forms runs (all
+ * produce the same results; the parity tests run each). 0 everywhere = the
+ * defaults. These are explicit per-context settings: the library reads no
+ * environment variables (measurement knobs exist only in the separate
+ * tuning build, make -C ... tuning). */
+#define ODO_KNN_FORM_FP4 0   /* default: exact sign-vector products on the matrix cores (FP4 operands) */
+#define ODO_KNN_FORM_VALU 1  /* xor + popcount on the VALUs (also taken for train sets above 8192) */
+typedef struct odo_kernel_forms {
+    int32_t knn;                    /* ODO_KNN_FORM_* */
+    int32_t knn_split;              /* VALU form: train splits per query block, 1..8 (0 = 2) */
+    int32_t ransac_lanes_min_open;  /* open pairs from which the second RANSAC launch takes the
+                                       lane-per-hypothesis kernel (0 = 32) */
+    int32_t reserved;
+} odo_kernel_forms;
+
 typedef struct odo_config {
     int32_t width, height;      /* frame size (all frames of a context share it) */
     int32_t max_batch;          /* frames per odo_track_batch() call */
@@ -45,6 +60,7 @@ typedef struct odo_config {
     uint32_t seed;              /* per-pair RNG seed base (replaces srand(clock()), main.cpp:27) */
     int32_t detector;           /* ODO_DETECTOR_* */
     odo_adaptive_params adaptive; /* ADAPTIVE grid (Extractor::CreateAdaptiveDetector, extractor.cpp:55-77) */
+    odo_kernel_forms forms;     /* bit-identical kernel alternatives (tests / A-B); zero = defaults */
 } odo_config;
 
 typedef struct odo_ctx odo_ctx;
@@ -92,9 +108,21 @@ int odo_track_batch_host(odo_ctx* ctx, const uint8_t* bgr, const uint16_t* depth
  * pixel through the mapped pointer, so about 2000 small reads per frame cross
  * PCIe instead of the 614 kB depth image. The BGR buffer is consumed when the
  * call returns; the DEPTH buffer must stay valid and unchanged until the batch
- * has finished (odo_synchronize(), or the call itself when h_results is set). */
+ * has read it: odo_host_depth_query() returns 0 / odo_host_depth_wait() returns
+ * (or odo_synchronize(), or the call itself when h_results is set). */
 int odo_track_batch_host_sparse_depth(odo_ctx* ctx, const uint8_t* bgr, const uint16_t* depth, int n,
                                       odo_pair_result* h_results);
+/* Whether the last odo_track_batch_host_sparse_depth batch may still read its
+ * depth buffer: 1 = in use (do not refill it), 0 = released (< 0 on error).
+ * odo_host_depth_wait blocks until it is released (odo_synchronize too). */
+int odo_host_depth_query(odo_ctx* ctx);
+int odo_host_depth_wait(odo_ctx* ctx);
+/* odo_track_batch_host with the result records streamed to PAGE-LOCKED host
+ * memory as odo_track_batch_async does (no host sync for the results; the host
+ * input buffers are consumed when the call returns): the from-host form of the
+ * SURVEY §8(e) frames mode, one PCIe upload per rank. */
+int odo_track_batch_host_async(odo_ctx* ctx, const uint8_t* bgr, const uint16_t* depth, int n,
+                               odo_pair_result* h_results);
 /* odo_track_batch with the n result records copied into PAGE-LOCKED host memory
  * (odo_host_alloc) asynchronously after the batch's PnP: no host sync, the
  * records are valid after odo_synchronize(). Used to stream results. */

@@ -20,13 +20,12 @@ cfg2_hard_b64 runs the hard workload (synth.make_sequence(hard=True): image and
 depth noise, two moving cuboids, repeated texture, twice the motion), where
 the inlier ratio is ~64 % and RANSAC visits ~450 of its 500 hypotheses.
 
-cfg2 also runs with every kNN-2 kernel form and ODO_KNN_SPLIT = 1, 2 and 8 (match lists and query counts
+cfg2 also runs with both kNN-2 kernel forms and VALU train splits 1, 2 and 8 (match lists and query counts
 bit-exact each time): 256 pairs give more active kNN-2 items than resident
 workgroups, so runs covering several items, split flushes and query-block
 switches inside one workgroup are all exercised. cfg4 (ICL, fy < 0) runs at
 B = 256 and cfg5 (1280x960, 8000 kp, H = 8192) at B = 32.
 """
-import os
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
@@ -64,25 +63,17 @@ def _oracle_calib(cfg):
     return O.Calib(k.fx, k.fy, k.cx, k.cy, k.k1, k.k2, k.p1, k.p2, k.k3, k.depth_factor, k.mbf, k.th_depth)
 
 
-def _run_gpu(pkg, c, bgr, dep, env=None):
-    """bench.py's timed loop: device-resident batch, BATCHES back-to-back calls."""
+def _run_gpu(pkg, c, bgr, dep, forms=None):
+    """bench.py's timed loop: device-resident batch, BATCHES back-to-back calls.
+    forms: odo_kernel_forms fields (bit-identical kernel alternatives)."""
     import torch
     B, L = c["B"], c["L"]
     idx = np.arange(B) % L
     d_bgr = torch.from_numpy(np.ascontiguousarray(bgr[idx])).to("cuda")
     d_dep = torch.from_numpy(np.ascontiguousarray(dep[idx]).view(np.int16)).to("cuda")
-    saved = {k: os.environ.get(k) for k in (env or {})}
-    os.environ.update(env or {})
-    try:
-        cfg = pkg.default_config(c["w"], c["h"], B, nfeatures=c["nf"], iterations=c["iters"], seed=c["seed"],
-                                 calib=c["calib"])
-        odo = pkg.Odometry(cfg)  # knobs are read at context creation
-    finally:
-        for k, v in saved.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+    cfg = pkg.default_config(c["w"], c["h"], B, nfeatures=c["nf"], iterations=c["iters"], seed=c["seed"],
+                             calib=c["calib"], forms=forms)
+    odo = pkg.Odometry(cfg)
     torch.cuda.synchronize()
     for _ in range(BATCHES - 1):
         odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=False)
@@ -179,17 +170,18 @@ def test_bench_configuration_full_batch(name):
         odo.close()
 
 
-@pytest.mark.parametrize("form,split", [("0", "1"), ("0", "2"), ("0", "8"), ("1", "1"), ("2", "1")])
+@pytest.mark.parametrize("form,split", [(1, 1), (1, 2), (1, 8), (0, 0)])
 def test_bench_configuration_knn_forms(form, split):
-    """Every kNN-2 kernel form (ODO_KNN_MFMA): the VALU xor/popcount kernel with
-    train splits 1 / 2 / 8 and more active items than resident workgroups, the
-    int8 MFMA kernel and the FP4 MFMA kernel (the default): match lists and
-    query counts of all 256 pairs bit-exact."""
+    """Every kNN-2 kernel form (odo_kernel_forms.knn): the VALU xor/popcount
+    kernel with train splits 1 / 2 / 8 and more active items than resident
+    workgroups, and the FP4 MFMA kernel (the default; its XCD-ordered items and
+    min3 / med3 top-2): match lists and query counts of all 256 pairs
+    bit-exact."""
     name = "cfg2_bench"
     c = CONFIGS[name]
     pkg = load_pkg()
     bgr, dep, _ = sequence(c["L"], c["w"], c["h"], intrinsics=c["intr"], seed=c["scene"], closed_loop=True)
-    odo, cfg, res = _run_gpu(pkg, c, bgr, dep, env={"ODO_KNN_MFMA": form, "ODO_KNN_SPLIT": split})
+    odo, cfg, res = _run_gpu(pkg, c, bgr, dep, forms={"knn": form, "knn_split": split})
     oracle = _oracle_cached(name, pkg, c, cfg, bgr, dep)
     try:
         _compare(name + f" kNN form {form} split {split}", c, odo, res, oracle, full=False)
@@ -200,13 +192,13 @@ def test_bench_configuration_knn_forms(form, split):
 @pytest.mark.parametrize("name", ["cfg2_bench", "cfg4_icl_b256"])
 def test_bench_configuration_ransac_lanes(name):
     """The second RANSAC launch on the lane-per-hypothesis kernel
-    (k_ransac_lanes) whatever the open-pair count (ODO_LANES_MIN_OPEN=1: from
+    (k_ransac_lanes) whatever the open-pair count (ransac_lanes_min_open = 1: from
     the fifth batch on, a set whose previous batch left a pair open takes it):
     every pair of the last batch bit-exact against the oracle."""
     c = CONFIGS[name]
     pkg = load_pkg()
     bgr, dep, _ = sequence(c["L"], c["w"], c["h"], intrinsics=c["intr"], seed=c["scene"], closed_loop=True)
-    odo, cfg, res = _run_gpu(pkg, c, bgr, dep, env={"ODO_LANES_MIN_OPEN": "1"})
+    odo, cfg, res = _run_gpu(pkg, c, bgr, dep, forms={"ransac_lanes_min_open": 1})
     oracle = _oracle_cached(name, pkg, c, cfg, bgr, dep)
     try:
         _compare(name + " lanes", c, odo, res, oracle)

@@ -3,7 +3,10 @@ both on cuda:0) track one sequence as rank chunks with a one-frame halo, the
 latch taken from global pair 1 and broadcast, the poses stitched with an
 all_gather of the chunk products. Every pair record must equal the one-rank
 batched run of the same frames bit for bit (matches, RANSAC, PnP, counts); the
-stitched absolute poses match the one-rank pose chain within 1e-5.
+stitched absolute poses match the one-rank pose chain within 1e-5. The
+from-host form (each rank uploads its chunk + halo from pinned host memory,
+odo_track_batch_host_async, as bench.py's from_host leg) is held to the same
+bar.
 """
 import os
 import socket
@@ -32,7 +35,7 @@ def _device_frames(bgr, dep):
             torch.from_numpy(np.ascontiguousarray(dep).view(np.int16)).to("cuda"))
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, out, host):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -54,8 +57,15 @@ def _worker(rank, world, port, out):
         for k in range(STEPS):
             first, n, halo = fs.batch_of(k, T, rank, world)
             lo = first if halo else 0
-            b, d = _device_frames(bgr[lo:lo + n] if halo else np.concatenate([bgr[:1], bgr[:n]]),
-                                  dep[lo:lo + n] if halo else np.concatenate([dep[:1], dep[:n]]))
+            fb_ = bgr[lo:lo + n] if halo else np.concatenate([bgr[:1], bgr[:n]])
+            fd_ = dep[lo:lo + n] if halo else np.concatenate([dep[:1], dep[:n]])
+            if host:
+                hf = pkg.HostFrames(fb_.shape[0], 640, 480)
+                hf.bgr[:], hf.depth[:] = fb_, fd_
+                bufs.append(hf)
+                sh.track_step_host(k, hf, ring, k)
+                continue
+            b, d = _device_frames(fb_, fd_)
             torch.cuda.synchronize()
             bufs.append((b, d))
             sh.track_step(k, b.data_ptr(), d.data_ptr(), fb, results=ring, row=k)
@@ -71,7 +81,8 @@ def _worker(rank, world, port, out):
         dist.destroy_process_group()
 
 
-def test_two_ranks_equal_one_rank():
+@pytest.mark.parametrize("host", [False, True], ids=["device_inputs", "host_inputs"])
+def test_two_ranks_equal_one_rank(host):
     pkg = load_pkg()
     import torch
     from arlm_amd import trajectory as tj
@@ -90,7 +101,7 @@ def test_two_ranks_equal_one_rank():
     q = ctx.Queue()
     port = _free_port()
     world = 2
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, host)) for r in range(world)]
     for p in procs:
         p.start()
     got = [q.get(timeout=300) for _ in range(world)]

@@ -138,3 +138,74 @@ def test_sparse_depth_batches_equal_device_path():
         odo.close()
         for h in hfs:
             h.close()
+
+
+def test_host_frames_are_checked():
+    """an undersized or wrongly sized HostFrames never reaches the
+    C-ABI (which trusts n * W * H bytes)."""
+    pkg = load_pkg()
+    odo = pkg.Odometry(_cfg(pkg))
+    small = pkg.HostFrames(2, 640, 480)
+    other = pkg.HostFrames(B, 320, 240)
+    try:
+        with pytest.raises(ValueError):
+            odo.track_batch_host(small, n=3)
+        with pytest.raises(ValueError):
+            odo.track_batch_host_sparse_depth(small, n=3)
+        with pytest.raises(ValueError):
+            odo.track_batch_host(other)
+        with pytest.raises(ValueError):
+            odo.track_batch_host(np.zeros((2, 480, 640, 3), np.uint8), np.zeros((2, 240, 320), np.uint16))
+    finally:
+        odo.close()
+        small.close()
+        other.close()
+
+
+def test_sparse_depth_buffer_is_held_until_read():
+    """The depth frames of a sparse-depth batch are read in place: the view is
+    read-only (a refill raises) until odo_host_depth_query / _wait release it."""
+    pkg = load_pkg()
+    b, d = _batches()[0]
+    hf = pkg.HostFrames(B, 640, 480)
+    odo = pkg.Odometry(_cfg(pkg))
+    try:
+        hf.bgr[:] = b
+        hf.depth[:] = d
+        odo.track_batch_host_sparse_depth(hf, want_results=False)
+        with pytest.raises(ValueError):
+            hf.depth[0, 0, 0] = 1
+        hf.bgr[:] = 0  # the BGR frames were consumed when the call returned
+        odo.depth_wait()
+        assert not odo.depth_busy()
+        hf.depth[:] = d
+        odo.track_batch_host_sparse_depth(hf, want_results=False)
+        odo.synchronize()
+        assert hf.depth.flags.writeable
+        assert odo.lib.odo_host_depth_query(odo.h) == 0
+    finally:
+        odo.close()
+        hf.close()
+
+
+def test_host_async_batches_equal_device_path():
+    """odo_track_batch_host_async (the frames-mode from-host call): uploads of
+    consecutive batches from one pinned buffer, refilled after each call, the
+    records streamed into a pinned ring: identical to the device path."""
+    pkg = load_pkg()
+    batches = _batches()
+    ref = _device_reference(pkg, batches)
+    hf = pkg.HostFrames(B, 640, 480)
+    ring = pkg.PinnedResults(NB, B)
+    odo = pkg.Odometry(_cfg(pkg))
+    try:
+        for k, (b, d) in enumerate(batches):
+            hf.bgr[:] = b
+            hf.depth[:] = d
+            odo.track_batch_host_async(hf, ring, k)
+        odo.synchronize()
+        _check(odo, ring.all[NB - 1].copy(), ref)
+    finally:
+        odo.close()
+        ring.close()
+        hf.close()

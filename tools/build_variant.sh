@@ -1,15 +1,11 @@
 #!/bin/bash
 # Build a variant of libodo_hip.so with extra compile flags for A/B runs:
-#   tools/build_variant.sh NAME "-DODO_WAVE_PRIO=0"  ->  build/libodo_NAME.so
-# (load it with ODO_LIB=adaptive-rgbd-localization-mappig_amd/build/libodo_NAME.so)
+#   tools/build_variant.sh NAME "-DODO_WAVE_PRIO=0"
+#     ->  adaptive-rgbd-localization-mappig_amd/build_NAME/libodo_hip.so
+# (load it with ODO_LIB=adaptive-rgbd-localization-mappig_amd/build_NAME/libodo_hip.so).
+# The source list and flags come from the package Makefile (its variant
+# target), linked with --no-undefined. Add -DODO_TUNING to read the
+# measurement knobs (ODO_SKIP, ODO_SCHED, ...) from the environment.
 set -e
 NAME=$1; EXTRA=$2
-cd "$(dirname "$0")/../adaptive-rgbd-localization-mappig_amd"
-F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -w $EXTRA"
-mkdir -p build/$NAME
-for s in k_extract.hip k_finalize.hip k_adaptive.hip k_adaptive_orb.hip k_match.hip k_project.hip k_ransac.hip k_pnp.hip odo_capi.cpp; do
-  X=""; [ $s = k_match.hip ] && X="-mllvm -amdgpu-mfma-vgpr-form"  # as the Makefile
-  /opt/rocm/bin/hipcc $F $X -x hip -c csrc/$s -o build/$NAME/$s.o &
-done
-wait
-/opt/rocm/bin/hipcc $F -shared -o build/libodo_$NAME.so build/$NAME/*.o
+make -j8 -C "$(dirname "$0")/../adaptive-rgbd-localization-mappig_amd" variant NAME="$NAME" EXTRA="$EXTRA"
