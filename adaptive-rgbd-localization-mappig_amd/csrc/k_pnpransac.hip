@@ -17,8 +17,10 @@
 //   k_pr_fold     one lane replays run()'s loop over the counts in order:
 //                 goodCount > max(maxGoodCount, 4) -> best, niters =
 //                 RANSACUpdateNumIters(0.85, outlier ratio, 5, niters);
-//   k_pr_refine   one wave: solvePnP(ITERATIVE, extrinsic guess) on the
-//                 best model's inliers = CvLevMarq (20 iterations, FLT_EPSILON)
+//   k_pr_refine   one wave: solvePnP(ITERATIVE, useExtrinsicGuess = false, as
+//                 pnpransac.cpp:34 passes) on the best model's inliers =
+//                 cvFindExtrinsicCameraParams2's own start (DLT / homography,
+//                 extrinsic_init) then CvLevMarq (20 iterations, FLT_EPSILON)
 //                 over cvProjectPoints2 residuals and Jacobians; J^T J, J^T e
 //                 and |e| reduced in a fixed lane-shuffle order.
 // All hypotheses up to `iterations` are evaluated (the fold decides how many
@@ -59,30 +61,44 @@ __device__ __forceinline__ double group_sum16(double x) {
     return __shfl(x, 0, PR_EPNP_GROUP);
 }
 
+// oracle/pnpransac_ref.cpp's kRR12: 11 rounds of 6 disjoint column pairs
+constexpr int kRR12[11][6][2] = {{{0, 11}, {1, 10}, {2, 9}, {3, 8}, {4, 7}, {5, 6}}, {{0, 1}, {2, 11}, {3, 10}, {4, 9}, {5, 8}, {6, 7}}, {{0, 2}, {1, 3}, {4, 11}, {5, 10}, {6, 9}, {7, 8}}, {{0, 3}, {2, 4}, {1, 5}, {6, 11}, {7, 10}, {8, 9}}, {{0, 4}, {3, 5}, {2, 6}, {1, 7}, {8, 11}, {9, 10}}, {{0, 5}, {4, 6}, {3, 7}, {2, 8}, {1, 9}, {10, 11}}, {{0, 6}, {5, 7}, {4, 8}, {3, 9}, {2, 10}, {1, 11}}, {{0, 7}, {6, 8}, {5, 9}, {4, 10}, {3, 11}, {1, 2}}, {{0, 8}, {7, 9}, {6, 10}, {5, 11}, {1, 4}, {2, 3}}, {{0, 9}, {8, 10}, {7, 11}, {1, 6}, {2, 5}, {3, 4}}, {{0, 10}, {9, 11}, {1, 8}, {2, 7}, {3, 6}, {4, 5}}};
+
 __device__ void svdj12_rows(double* arow, double* vrow, int r, int* ord) {
 #pragma unroll
     for (int j = 0; j < 12; j++) vrow[j] = (r == j) ? 1.0 : 0.0;
     for (int sweep = 0; sweep < 60; sweep++) {
         int changed = 0;
 #pragma unroll
-        for (int p = 0; p < 11; p++)
+        for (int rd = 0; rd < 11; rd++) {
+            // the round's six pairs are disjoint: all sums from the pre-round
+            // state, six independent rotation chains, then the lane-local updates
+            double al[6], be[6], ga[6];
 #pragma unroll
-            for (int q = p + 1; q < 12; q++) {
+            for (int k = 0; k < 6; k++) {
+                const int p = kRR12[rd][k][0], q = kRR12[rd][k][1];
                 const double ap0 = arow[p], aq0 = arow[q];
-                const double alpha = group_sum16(ap0 * ap0);
-                const double beta = group_sum16(aq0 * aq0);
-                const double gamma = group_sum16(ap0 * aq0);
+                al[k] = group_sum16(ap0 * ap0);
+                be[k] = group_sum16(aq0 * aq0);
+                ga[k] = group_sum16(ap0 * aq0);
+            }
+#pragma unroll
+            for (int k = 0; k < 6; k++) {
+                const int p = kRR12[rd][k][0], q = kRR12[rd][k][1];
+                const double alpha = al[k], beta = be[k], gamma = ga[k];
                 if (gamma == 0.0 || fabs(gamma) <= DBL_EPSILON * sqrt(alpha * beta)) continue;
                 changed = 1;
                 const double zeta = (beta - alpha) / (2.0 * gamma);
                 const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
                 const double c = 1.0 / sqrt(1.0 + t * t), s = c * t;
+                const double ap0 = arow[p], aq0 = arow[q];
                 arow[p] = c * ap0 - s * aq0;
                 arow[q] = s * ap0 + c * aq0;
                 const double vp = vrow[p], vq = vrow[q];
                 vrow[p] = c * vp - s * vq;
                 vrow[q] = s * vp + c * vq;
             }
+        }
         if (!changed) break;
     }
     double ww[12];
@@ -842,6 +858,429 @@ __device__ void lm_pass(const float* __restrict__ Xw, const float* __restrict__ 
     }
 }
 
+// ------------------------- cvFindExtrinsicCameraParams2, unseeded (calibration.cpp)
+// The final solvePnP of solvePnPRansac gets the caller's useExtrinsicGuess,
+// false at pnpransac.cpp:34, so the LM starts from cvFindExtrinsicCameraParams2's
+// own initial pose (extrinsic_init in oracle/pnpransac_ref.cpp, same
+// operation order): centroid + scatter of the object points (wave sums over
+// the inliers, point i on lane i % 64), 3x3 SVD -> planar or not; non-planar:
+// the DLT's 12 x 12 L^T L (78 wave sums), its smallest singular vector by the
+// row-parallel Jacobi of the EPnP kernel (lanes 0..15), [R | t] from it;
+// planar: the homography path on lane 0 (rare: coplanar landmarks), its
+// matrices in LDS.
+
+// one-sided Jacobi SVD on LDS arrays, one lane (oracle svdj's loop order):
+// a (m x n) is destroyed; w (n), V (n x n by columns), U (m x n) if non-null
+__device__ void svdj_lds(int m, int n, double* a, double* v, double* w, double* U, double* V, double* ww, int* ord) {
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) v[i * n + j] = i == j ? 1.0 : 0.0;
+    for (int sweep = 0; sweep < 60; sweep++) {
+        int changed = 0;
+        for (int p = 0; p < n - 1; p++)
+            for (int q = p + 1; q < n; q++) {
+                double alpha = 0, beta = 0, gamma = 0;
+                for (int i = 0; i < m; i++) {
+                    const double ap = a[i * n + p], aq = a[i * n + q];
+                    alpha += ap * ap;
+                    beta += aq * aq;
+                    gamma += ap * aq;
+                }
+                if (gamma == 0.0 || fabs(gamma) <= DBL_EPSILON * sqrt(alpha * beta)) continue;
+                changed = 1;
+                const double zeta = (beta - alpha) / (2.0 * gamma);
+                const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+                const double c = 1.0 / sqrt(1.0 + t * t), sn = c * t;
+                for (int i = 0; i < m; i++) {
+                    const double ap = a[i * n + p], aq = a[i * n + q];
+                    a[i * n + p] = c * ap - sn * aq;
+                    a[i * n + q] = sn * ap + c * aq;
+                }
+                for (int i = 0; i < n; i++) {
+                    const double vp = v[i * n + p], vq = v[i * n + q];
+                    v[i * n + p] = c * vp - sn * vq;
+                    v[i * n + q] = sn * vp + c * vq;
+                }
+            }
+        if (!changed) break;
+    }
+    for (int j = 0; j < n; j++) {
+        double sq = 0;
+        for (int i = 0; i < m; i++) sq += a[i * n + j] * a[i * n + j];
+        ww[j] = sqrt(sq);
+        ord[j] = j;
+    }
+    for (int j = 0; j < n; j++) {
+        int b = j;
+        for (int k = j + 1; k < n; k++)
+            if (ww[ord[k]] > ww[ord[b]]) b = k;
+        const int t = ord[j];
+        ord[j] = ord[b];
+        ord[b] = t;
+    }
+    for (int j = 0; j < n; j++) {
+        const int c = ord[j];
+        w[j] = ww[c];
+        const double inv = ww[c] > 0 ? 1.0 / ww[c] : 0.0;
+        if (U)
+            for (int i = 0; i < m; i++) U[i * n + j] = a[i * n + c] * inv;
+        for (int i = 0; i < n; i++) V[i * n + j] = v[i * n + c];
+    }
+}
+
+struct HomLds {  // lane-0 scratch of the planar start
+    double a[81], v[81], U[81], V[81], w[9], ww[9];
+    int ord[9];
+    double A[64], Ap[64];
+};
+
+// svd_solve (cvSolve CV_SVD) of the n x n Ap against b, on LDS
+__device__ void svd_solve_lds(int n, HomLds& h, const double* b, double* x) {
+    for (int k = 0; k < n * n; k++) h.a[k] = h.Ap[k];
+    svdj_lds(n, n, h.a, h.v, h.w, h.U, h.V, h.ww, h.ord);
+    const double thr = n * DBL_EPSILON * h.w[0];
+    double y[8];
+    for (int j = 0; j < n; j++) {
+        double sacc = 0;
+        for (int i = 0; i < n; i++) sacc += h.U[i * n + j] * b[i];
+        y[j] = h.w[j] > thr ? sacc / h.w[j] : 0.0;
+    }
+    for (int i = 0; i < n; i++) {
+        double sacc = 0;
+        for (int j = 0; j < n; j++) sacc += h.V[i * n + j] * y[j];
+        x[i] = sacc;
+    }
+}
+
+__device__ __forceinline__ double det3d(const double* a) {
+    return a[0] * (a[4] * a[8] - a[5] * a[7]) - a[1] * (a[3] * a[8] - a[5] * a[6]) + a[2] * (a[3] * a[7] - a[4] * a[6]);
+}
+
+// the planar point (Rt M + T).xy as float and the normalised image point as float
+__device__ __forceinline__ void hom_pts(const float* Xw, const float* uv, int i, const double* Rt, const double* T,
+                                        const PrK& K, double ifx, double ify, float* Mf, float* mf) {
+    const double s0 = Xw[3 * i], s1 = Xw[3 * i + 1], s2 = Xw[3 * i + 2];
+    Mf[0] = (float)(Rt[0] * s0 + Rt[1] * s1 + Rt[2] * s2 + T[0]);
+    Mf[1] = (float)(Rt[3] * s0 + Rt[4] * s1 + Rt[5] * s2 + T[1]);
+    mf[0] = (float)(((double)uv[2 * i] - K.cx) * ifx);
+    mf[1] = (float)(((double)uv[2 * i + 1] - K.cy) * ify);
+}
+
+// cv::findHomography(Mxy, mn, 0) (oracle find_homography): lane 0
+__device__ bool find_homography_lane(const float* Xw, const float* uv, const uint8_t* m, int n, int ni,
+                                     const double* Rt, const double* T, const PrK& K, double ifx, double ify,
+                                     HomLds& hs, double* H) {
+    double cMx = 0, cMy = 0, cmx = 0, cmy = 0, sMx = 0, sMy = 0, smx = 0, smy = 0;
+    float Mf[2], mf[2];
+    for (int i = 0; i < n; i++) {
+        if (!m[i]) continue;
+        hom_pts(Xw, uv, i, Rt, T, K, ifx, ify, Mf, mf);
+        cmx += mf[0];
+        cmy += mf[1];
+        cMx += Mf[0];
+        cMy += Mf[1];
+    }
+    cmx /= ni;
+    cmy /= ni;
+    cMx /= ni;
+    cMy /= ni;
+    for (int i = 0; i < n; i++) {
+        if (!m[i]) continue;
+        hom_pts(Xw, uv, i, Rt, T, K, ifx, ify, Mf, mf);
+        smx += fabs(mf[0] - cmx);
+        smy += fabs(mf[1] - cmy);
+        sMx += fabs(Mf[0] - cMx);
+        sMy += fabs(Mf[1] - cMy);
+    }
+    if (fabs(smx) < DBL_EPSILON || fabs(smy) < DBL_EPSILON || fabs(sMx) < DBL_EPSILON || fabs(sMy) < DBL_EPSILON)
+        return false;
+    smx = ni / smx;
+    smy = ni / smy;
+    sMx = ni / sMx;
+    sMy = ni / sMy;
+    const double invHnorm[9] = {1. / smx, 0, cmx, 0, 1. / smy, cmy, 0, 0, 1};
+    const double Hnorm2[9] = {sMx, 0, -cMx * sMx, 0, sMy, -cMy * sMy, 0, 0, 1};
+    double* LtL = hs.a;
+    for (int k = 0; k < 81; k++) LtL[k] = 0;
+    for (int i = 0; i < n; i++) {
+        if (!m[i]) continue;
+        hom_pts(Xw, uv, i, Rt, T, K, ifx, ify, Mf, mf);
+        const double x = (mf[0] - cmx) * smx, y = (mf[1] - cmy) * smy;
+        const double X = (Mf[0] - cMx) * sMx, Y = (Mf[1] - cMy) * sMy;
+        const double Lx[9] = {X, Y, 1, 0, 0, 0, -x * X, -x * Y, -x};
+        const double Ly[9] = {0, 0, 0, X, Y, 1, -y * X, -y * Y, -y};
+        for (int j = 0; j < 9; j++)
+            for (int k = j; k < 9; k++) LtL[j * 9 + k] += Lx[j] * Lx[k] + Ly[j] * Ly[k];
+    }
+    for (int j = 0; j < 9; j++)
+        for (int k = 0; k < j; k++) LtL[j * 9 + k] = LtL[k * 9 + j];
+    svdj_lds(9, 9, hs.a, hs.v, hs.w, hs.U, hs.V, hs.ww, hs.ord);
+    double H0[9], Ht[9];
+    for (int k = 0; k < 9; k++) H0[k] = hs.V[k * 9 + 8];
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++)
+            Ht[r * 3 + c] = invHnorm[r * 3 + 0] * H0[0 * 3 + c] + invHnorm[r * 3 + 1] * H0[1 * 3 + c] +
+                            invHnorm[r * 3 + 2] * H0[2 * 3 + c];
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++)
+            H0[r * 3 + c] = Ht[r * 3 + 0] * Hnorm2[0 * 3 + c] + Ht[r * 3 + 1] * Hnorm2[1 * 3 + c] +
+                            Ht[r * 3 + 2] * Hnorm2[2 * 3 + c];
+    const double s22 = 1. / H0[8];
+    for (int k = 0; k < 9; k++) H[k] = H0[k] * s22;
+    if (ni <= 4) return true;
+    // LMSolverImpl::run over h[0..7], streaming the residuals / Jacobian rows
+    // (J^T J, J^T r, |r|^2 and max |r| in point order)
+    double x8[8], xd[8], v[8], D[8], d[8];
+    for (int k = 0; k < 8; k++) x8[k] = H[k];
+    auto pass = [&](const double* h, bool withJ, double* S, double* rinf) {
+        if (withJ) {
+            for (int k = 0; k < 64; k++) hs.A[k] = 0;
+            for (int k = 0; k < 8; k++) v[k] = 0;
+        }
+        double s2 = 0, mx = 0;
+        for (int i = 0; i < n; i++) {
+            if (!m[i]) continue;
+            hom_pts(Xw, uv, i, Rt, T, K, ifx, ify, Mf, mf);
+            const double Mx = Mf[0], My = Mf[1];
+            double ww = h[6] * Mx + h[7] * My + 1.;
+            ww = fabs(ww) > DBL_EPSILON ? 1. / ww : 0;
+            const double xi = (h[0] * Mx + h[1] * My + h[2]) * ww;
+            const double yi = (h[3] * Mx + h[4] * My + h[5]) * ww;
+            const double r0 = xi - mf[0], r1 = yi - mf[1];
+            if (withJ) {
+                const double Jx[8] = {Mx * ww, My * ww, ww, 0., 0., 0., -Mx * ww * xi, -My * ww * xi};
+                const double Jy[8] = {0., 0., 0., Mx * ww, My * ww, ww, -Mx * ww * yi, -My * ww * yi};
+                for (int a = 0; a < 8; a++) {
+                    for (int b = 0; b < 8; b++) {
+                        hs.A[a * 8 + b] += Jx[a] * Jx[b];
+                        hs.A[a * 8 + b] += Jy[a] * Jy[b];
+                    }
+                    v[a] += Jx[a] * r0;
+                    v[a] += Jy[a] * r1;
+                }
+            }
+            s2 += r0 * r0;
+            s2 += r1 * r1;
+            mx = fmax(mx, fmax(fabs(r0), fabs(r1)));
+        }
+        *S = s2;
+        if (rinf) *rinf = mx;
+    };
+    double S, rinf;
+    pass(x8, true, &S, &rinf);
+    for (int i = 0; i < 8; i++) D[i] = hs.A[i * 9];
+    const double Rlo = 0.25, Rhi = 0.75;
+    double lambda = 1, lc = 0.75;
+    int iter = 0;
+    for (;;) {
+        for (int k = 0; k < 64; k++) hs.Ap[k] = hs.A[k];
+        for (int i = 0; i < 8; i++) hs.Ap[i * 9] += lambda * D[i];
+        svd_solve_lds(8, hs, v, d);
+        for (int i = 0; i < 8; i++) xd[i] = x8[i] - d[i];
+        double Sd;
+        pass(xd, false, &Sd, nullptr);
+        double dS = 0;
+        for (int i = 0; i < 8; i++) {
+            double t = 0;
+            for (int k = 0; k < 8; k++) t += hs.A[i * 8 + k] * d[k];
+            dS += d[i] * (2 * v[i] - t);
+        }
+        const double R = (S - Sd) / (fabs(dS) > DBL_EPSILON ? dS : 1);
+        if (R > Rhi) {
+            lambda *= 0.5;
+            if (lambda < lc) lambda = 0;
+        } else if (R < Rlo) {
+            double t = 0;
+            for (int i = 0; i < 8; i++) t += d[i] * v[i];
+            double nu = (Sd - S) / (fabs(t) > DBL_EPSILON ? t : 1) + 2;
+            nu = fmin(fmax(nu, 2.), 10.);
+            if (lambda == 0) {
+                for (int k = 0; k < 64; k++) hs.a[k] = hs.A[k];
+                svdj_lds(8, 8, hs.a, hs.v, hs.w, hs.U, hs.V, hs.ww, hs.ord);
+                const double thr = 8 * DBL_EPSILON * hs.w[0];
+                double maxval = DBL_EPSILON;
+                for (int i = 0; i < 8; i++) {
+                    double dii = 0;
+                    for (int k = 0; k < 8; k++)
+                        if (hs.w[k] > thr) dii += hs.V[i * 8 + k] * hs.U[i * 8 + k] / hs.w[k];
+                    maxval = fmax(maxval, fabs(dii));
+                }
+                lambda = lc = 1. / maxval;
+                nu *= 0.5;
+            }
+            lambda *= nu;
+        }
+        if (Sd < S) {
+            S = Sd;
+            for (int k = 0; k < 8; k++) x8[k] = xd[k];
+            pass(x8, true, &S, &rinf);
+        }
+        iter++;
+        double dinf = 0;
+        for (int i = 0; i < 8; i++) dinf = fmax(dinf, fabs(d[i]));
+        if (!(iter < 10 && dinf >= FLT_EPSILON && rinf >= FLT_EPSILON)) break;
+    }
+    for (int k = 0; k < 8; k++) H[k] = x8[k];
+    H[8] = 1.;
+    return true;
+}
+
+// -> sp[0..5] = (rvec, tvec): the whole wave calls it
+__device__ void extrinsic_init(const float* __restrict__ Xw, const float* __restrict__ uv,
+                               const uint8_t* __restrict__ m, int n, int ni, const PrK& K, double* sp) {
+    __shared__ double s_red[78];
+    __shared__ double wred[1][78];
+    __shared__ double s_mc[3], s_rrt[12];
+    __shared__ int s_planar;
+    __shared__ double s_Rt[9], s_T[3];
+    __shared__ HomLds hs;
+    const int lane = threadIdx.x;
+    const double ifx = 1. / K.fx, ify = 1. / K.fy;
+    {
+        double v[3] = {0, 0, 0};
+        for (int i = lane; i < n; i += PR_REFINE_THREADS) {
+            if (!m[i]) continue;
+            for (int k = 0; k < 3; k++) v[k] += (double)Xw[3 * i + k];
+        }
+        block_sum<3>(v, (double(*)[3])wred, s_red);
+        if (lane < 3) s_mc[lane] = s_red[lane] / ni;
+        __syncthreads();
+    }
+    const double Mc[3] = {s_mc[0], s_mc[1], s_mc[2]};
+    {
+        double v[6] = {0, 0, 0, 0, 0, 0};
+        for (int i = lane; i < n; i += PR_REFINE_THREADS) {
+            if (!m[i]) continue;
+            const double d0 = (double)Xw[3 * i] - Mc[0], d1 = (double)Xw[3 * i + 1] - Mc[1],
+                         d2 = (double)Xw[3 * i + 2] - Mc[2];
+            v[0] += d0 * d0;
+            v[1] += d0 * d1;
+            v[2] += d0 * d2;
+            v[3] += d1 * d1;
+            v[4] += d1 * d2;
+            v[5] += d2 * d2;
+        }
+        block_sum<6>(v, (double(*)[6])wred, s_red);
+    }
+    if (lane == 0) {
+        const double MM[9] = {s_red[0], s_red[1], s_red[2], s_red[1], s_red[3], s_red[4], s_red[2], s_red[4], s_red[5]};
+        double W[3], Um[9], Vm[9];
+        svdj<3, 3>(MM, W, Um, Vm);
+        s_planar = W[2] / W[1] < 1e-3;
+        for (int r = 0; r < 3; r++)
+            for (int c = 0; c < 3; c++) s_Rt[r * 3 + c] = Vm[c * 3 + r];
+    }
+    __syncthreads();
+    double R[9], t[3];
+    if (!s_planar) {
+        double v[78];
+        for (int k = 0; k < 78; k++) v[k] = 0;
+        for (int i = lane; i < n; i += PR_REFINE_THREADS) {
+            if (!m[i]) continue;
+            const double x = -(((double)uv[2 * i] - K.cx) * ifx), y = -(((double)uv[2 * i + 1] - K.cy) * ify);
+            const double X = Xw[3 * i], Y = Xw[3 * i + 1], Z = Xw[3 * i + 2];
+            const double L1[12] = {X, Y, Z, 1., 0., 0., 0., 0., x * X, x * Y, x * Z, x};
+            const double L2[12] = {0., 0., 0., 0., X, Y, Z, 1., y * X, y * Y, y * Z, y};
+            int k = 0;
+#pragma unroll
+            for (int r = 0; r < 12; r++)
+#pragma unroll
+                for (int c = r; c < 12; c++, k++) {
+                    v[k] += L1[r] * L1[c];
+                    v[k] += L2[r] * L2[c];
+                }
+        }
+        block_sum<78>(v, wred, s_red);
+        if (lane < 16) {
+            const int r = lane;
+            double arow[12], vrow[12];
+            int ord[12];
+#pragma unroll
+            for (int c = 0; c < 12; c++) {
+                const int a = r < c ? r : c, b = r < c ? c : r;  // upper-triangle index of (a, b)
+                arow[c] = r < 12 ? s_red[a * 12 - a * (a - 1) / 2 + (b - a)] : 0.0;
+            }
+            svdj12_rows(arow, vrow, r, ord);
+            double e = 0;
+#pragma unroll
+            for (int c = 0; c < 12; c++)
+                if (ord[11] == c) e = vrow[c];
+            if (r < 12) s_rrt[r] = e;  // row 11 of V^T
+        }
+        __syncthreads();
+        if (lane == 0) {
+            double RRt[12];
+            for (int k = 0; k < 12; k++) RRt[k] = s_rrt[k];
+            double RR[9] = {RRt[0], RRt[1], RRt[2], RRt[4], RRt[5], RRt[6], RRt[8], RRt[9], RRt[10]};
+            if (det3d(RR) < 0) {
+                for (int k = 0; k < 12; k++) RRt[k] = -RRt[k];
+                for (int k = 0; k < 9; k++) RR[k] = -RR[k];
+            }
+            double sc = 0;
+            for (int k = 0; k < 9; k++) sc += RR[k] * RR[k];
+            sc = sqrt(sc);
+            double w3[3], U3[9], V3[9];
+            svdj<3, 3>(RR, w3, U3, V3);
+            double nr = 0;
+            for (int r = 0; r < 3; r++)
+                for (int c = 0; c < 3; c++) {
+                    R[r * 3 + c] =
+                        U3[r * 3] * V3[c * 3] + U3[r * 3 + 1] * V3[c * 3 + 1] + U3[r * 3 + 2] * V3[c * 3 + 2];
+                    nr += R[r * 3 + c] * R[r * 3 + c];
+                }
+            const double f = sqrt(nr) / sc;
+            t[0] = RRt[3] * f;
+            t[1] = RRt[7] * f;
+            t[2] = RRt[11] * f;
+        }
+    } else if (lane == 0) {
+        double Rt[9];
+        for (int k = 0; k < 9; k++) Rt[k] = s_Rt[k];
+        if (Rt[2] * Rt[2] + Rt[5] * Rt[5] < 1e-10)
+            for (int k = 0; k < 9; k++) Rt[k] = k % 4 == 0 ? 1.0 : 0.0;
+        if (det3d(Rt) < 0)
+            for (int k = 0; k < 9; k++) Rt[k] = -Rt[k];
+        double T[3];
+        for (int r = 0; r < 3; r++) T[r] = -(Rt[r * 3] * Mc[0] + Rt[r * 3 + 1] * Mc[1] + Rt[r * 3 + 2] * Mc[2]);
+        double h[9];
+        bool okh = find_homography_lane(Xw, uv, m, n, ni, Rt, T, K, ifx, ify, hs, h);
+        for (int k = 0; k < 9 && okh; k++) okh = isfinite(h[k]);
+        if (okh) {
+            const double h1n = sqrt(h[0] * h[0] + h[3] * h[3] + h[6] * h[6]);
+            const double h2n = sqrt(h[1] * h[1] + h[4] * h[4] + h[7] * h[7]);
+            const double s1 = 1. / fmax(h1n, DBL_EPSILON), s2 = 1. / fmax(h2n, DBL_EPSILON);
+            const double s3 = 2. / fmax(h1n + h2n, DBL_EPSILON);
+            double Hm[9];
+            for (int r = 0; r < 3; r++) {
+                Hm[r * 3] = h[r * 3] * s1;
+                Hm[r * 3 + 1] = h[r * 3 + 1] * s2;
+                t[r] = h[r * 3 + 2] * s3;
+            }
+            Hm[2] = Hm[3] * Hm[7] - Hm[6] * Hm[4];
+            Hm[5] = Hm[6] * Hm[1] - Hm[0] * Hm[7];
+            Hm[8] = Hm[0] * Hm[4] - Hm[3] * Hm[1];
+            double rv[3], Hr[9];
+            rod_m2v(Hm, rv);
+            rod_v2m(rv, Hr, nullptr);
+            for (int r = 0; r < 3; r++) t[r] = Hr[r * 3] * T[0] + Hr[r * 3 + 1] * T[1] + Hr[r * 3 + 2] * T[2] + t[r];
+            for (int r = 0; r < 3; r++)
+                for (int c = 0; c < 3; c++)
+                    R[r * 3 + c] = Hr[r * 3] * Rt[c] + Hr[r * 3 + 1] * Rt[3 + c] + Hr[r * 3 + 2] * Rt[6 + c];
+        } else {
+            for (int k = 0; k < 9; k++) R[k] = k % 4 == 0 ? 1.0 : 0.0;
+            t[0] = t[1] = t[2] = 0;
+        }
+    }
+    if (lane == 0) {
+        double r[3];
+        rod_m2v(R, r);
+        for (int k = 0; k < 3; k++) {
+            sp[k] = r[k];
+            sp[3 + k] = t[k];
+        }
+    }
+    __syncthreads();
+}
+
 __global__ __launch_bounds__(PR_REFINE_THREADS) void k_pr_refine(const float* __restrict__ Xw,
                                                                  const float* __restrict__ uv,
                                                                  const int* __restrict__ offs, int H, PrK K,
@@ -877,8 +1316,9 @@ __global__ __launch_bounds__(PR_REFINE_THREADS) void k_pr_refine(const float* __
     }
     const uint8_t* m = mask + (size_t)best * n;
     for (int i = threadIdx.x; i < n; i += PR_REFINE_THREADS) mask_out[i] = m[i];
-    if (threadIdx.x < 6) sp[threadIdx.x] = model[6 * best + threadIdx.x];
-    __syncthreads();
+    // solvePnP(inliers, useExtrinsicGuess = false) (pnpransac.cpp:34): the
+    // LM starts from cvFindExtrinsicCameraParams2's own pose, not the model
+    extrinsic_init(Xw, uv, m, n, state[2], K, sp);
     double lambdaLg10 = -3, prevErrNorm = DBL_MAX;
     double JtJ[36], JtErr[6];
     int iters = 0;

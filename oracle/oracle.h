@@ -188,6 +188,9 @@ void oracle_rodrigues(const double r[3], double R[9], double* dRdr);
 void oracle_rodrigues_inv(const double R[9], double r[3]);
 void oracle_epnp(const double* pw, const double* uv, int n, const double K[4], double model[6]);
 void oracle_pnp_refine(const double* M, const double* m, int n, const double K[4], double param[6]);
+/* cvFindExtrinsicCameraParams2's start without an extrinsic guess (DLT /
+ * homography; pnpransac.cpp:34 passes useExtrinsicGuess = false) */
+void oracle_pnp_extrinsic_init(const double* M, const double* m, int n, const double K[4], double param[6]);
 
 /* ---- GeneralizedICP::Compute(source, target, guess) (generalizedicp.cpp:30-39,
  * 65-89; SURVEY §8(f) rank 4, the ADAPTIVE_RICP fallback of odometry.cpp:46-78):

@@ -12,8 +12,16 @@
 //   * cvSVD / cvSolve(CV_SVD) / cvInvert(CV_SVD) are one-sided (Hestenes)
 //     Jacobi SVDs in double, singular values sorted descending;
 //   * the final refinement is solvePnP(inliers, SOLVEPNP_ITERATIVE,
-//     useExtrinsicGuess = true) seeded with the RANSAC model, whose 6x6 damped
-//     normal equations are solved with the same SVD (solve(..., DECOMP_SVD)).
+//     useExtrinsicGuess = false), as pnpransac.cpp:34 passes false: OpenCV
+//     3.4's solvePnPRansac hands the inliers to solvePnP with the caller's
+//     flag, so cvFindExtrinsicCameraParams2 builds its own start (extrinsic_init:
+//     DLT for non-planar point sets, the homography decomposition for planar
+//     ones) and CvLevMarq refines from there; its 6x6 damped normal equations
+//     are solved with the same SVD (solve(..., DECOMP_SVD));
+//   * sums over the inlier points run in the GPU's order (lane i % 64 of one
+//     wave accumulates point i, then a shuffle-down tree: wsum64), and the
+//     12 x 12 DLT eigenproblem uses svdj12 (tree16), as the EPnP one.
+#include <algorithm>
 #include <cfloat>
 #include <cmath>
 #include <cstring>
@@ -109,7 +117,12 @@ double tree16(const double* x) {
     return y[0];
 }
 
-// svdj for the 12 x 12 M^T M with tree16 column sums; V only.
+// Round-robin (parallel) Jacobi ordering of the 66 column pairs of the 12 x 12
+// eigenproblem: 11 rounds of 6 disjoint pairs, so the GPU rotates a round's
+// pairs at once (the rotations of a round commute). Pinned choice.
+const int kRR12[11][6][2] = {{{0, 11}, {1, 10}, {2, 9}, {3, 8}, {4, 7}, {5, 6}}, {{0, 1}, {2, 11}, {3, 10}, {4, 9}, {5, 8}, {6, 7}}, {{0, 2}, {1, 3}, {4, 11}, {5, 10}, {6, 9}, {7, 8}}, {{0, 3}, {2, 4}, {1, 5}, {6, 11}, {7, 10}, {8, 9}}, {{0, 4}, {3, 5}, {2, 6}, {1, 7}, {8, 11}, {9, 10}}, {{0, 5}, {4, 6}, {3, 7}, {2, 8}, {1, 9}, {10, 11}}, {{0, 6}, {5, 7}, {4, 8}, {3, 9}, {2, 10}, {1, 11}}, {{0, 7}, {6, 8}, {5, 9}, {4, 10}, {3, 11}, {1, 2}}, {{0, 8}, {7, 9}, {6, 10}, {5, 11}, {1, 4}, {2, 3}}, {{0, 9}, {8, 10}, {7, 11}, {1, 6}, {2, 5}, {3, 4}}, {{0, 10}, {9, 11}, {1, 8}, {2, 7}, {3, 6}, {4, 5}}};
+
+// svdj for the 12 x 12 M^T M with tree16 column sums, pairs in kRR12 order; V only.
 void svdj12(const double* A, double* w, double* V) {
     double a[144], v[144];
     memcpy(a, A, sizeof(a));
@@ -117,8 +130,9 @@ void svdj12(const double* A, double* w, double* V) {
         for (int j = 0; j < 12; j++) v[i * 12 + j] = i == j ? 1.0 : 0.0;
     for (int sweep = 0; sweep < 60; sweep++) {
         int changed = 0;
-        for (int p = 0; p < 11; p++)
-            for (int q = p + 1; q < 12; q++) {
+        for (int rd = 0; rd < 11; rd++)
+            for (int pr = 0; pr < 6; pr++) {
+                const int p = kRR12[rd][pr][0], q = kRR12[rd][pr][1];
                 double pp[12], qq[12], pq[12];
                 for (int i = 0; i < 12; i++) {
                     const double ap = a[i * 12 + p], aq = a[i * 12 + q];
@@ -721,6 +735,345 @@ void refine_lm(const double* M, const double* m, int n, const double K[4], doubl
     }
 }
 
+// ----------------------------------- sums in the GPU's one-wave order
+// K running sums over n items: item i is added on lane i % 64 (in item
+// order), then lanes combine with the shuffle-down tree (offsets 32 .. 1) and
+// lane 0 holds the total (k_pnpransac.hip block_sum / wave_sums).
+struct WSum64 {
+    int K;
+    std::vector<double> acc;  // [64][K]
+    explicit WSum64(int k) : K(k), acc(64 * (size_t)k, 0.0) {}
+    double* lane(int key) { return &acc[(size_t)(key & 63) * K]; }
+    void total(double* out) {
+        for (int o = 32; o > 0; o >>= 1)
+            for (int l = 0; l < o; l++)
+                for (int k = 0; k < K; k++) acc[(size_t)l * K + k] += acc[(size_t)(l + o) * K + k];
+        for (int k = 0; k < K; k++) out[k] = acc[k];
+    }
+};
+
+inline double det3(const double* a) {
+    return a[0] * (a[4] * a[8] - a[5] * a[7]) - a[1] * (a[3] * a[8] - a[5] * a[6]) + a[2] * (a[3] * a[7] - a[4] * a[6]);
+}
+
+// cv::findHomography(src, dst, 0) on float points (findHomography converts
+// its inputs to CV_32F): HomographyEstimatorCallback::runKernel (normalised
+// DLT: centroids, mean absolute deviations, 9 x 9 LtL, eigenvector of the
+// smallest eigenvalue, denormalised, scaled to h22 = 1), then LMSolver with
+// HomographyRefineCallback (8 parameters, 10 iterations, epsx = epsf =
+// FLT_EPSILON; solve / invert with DECOMP_EIG taken as the SVD solve).
+// Returns false when the kernel fails (degenerate spread).
+bool find_homography(const float* M, const float* m, int n, double H[9]) {
+    double cMx = 0, cMy = 0, cmx = 0, cmy = 0, sMx = 0, sMy = 0, smx = 0, smy = 0;
+    for (int i = 0; i < n; i++) {
+        cmx += m[2 * i];
+        cmy += m[2 * i + 1];
+        cMx += M[2 * i];
+        cMy += M[2 * i + 1];
+    }
+    cmx /= n;
+    cmy /= n;
+    cMx /= n;
+    cMy /= n;
+    for (int i = 0; i < n; i++) {
+        smx += std::fabs(m[2 * i] - cmx);
+        smy += std::fabs(m[2 * i + 1] - cmy);
+        sMx += std::fabs(M[2 * i] - cMx);
+        sMy += std::fabs(M[2 * i + 1] - cMy);
+    }
+    if (std::fabs(smx) < DBL_EPSILON || std::fabs(smy) < DBL_EPSILON || std::fabs(sMx) < DBL_EPSILON ||
+        std::fabs(sMy) < DBL_EPSILON)
+        return false;
+    smx = n / smx;
+    smy = n / smy;
+    sMx = n / sMx;
+    sMy = n / sMy;
+    const double invHnorm[9] = {1. / smx, 0, cmx, 0, 1. / smy, cmy, 0, 0, 1};
+    const double Hnorm2[9] = {sMx, 0, -cMx * sMx, 0, sMy, -cMy * sMy, 0, 0, 1};
+    double LtL[81] = {0};
+    for (int i = 0; i < n; i++) {
+        const double x = (m[2 * i] - cmx) * smx, y = (m[2 * i + 1] - cmy) * smy;
+        const double X = (M[2 * i] - cMx) * sMx, Y = (M[2 * i + 1] - cMy) * sMy;
+        const double Lx[9] = {X, Y, 1, 0, 0, 0, -x * X, -x * Y, -x};
+        const double Ly[9] = {0, 0, 0, X, Y, 1, -y * X, -y * Y, -y};
+        for (int j = 0; j < 9; j++)
+            for (int k = j; k < 9; k++) LtL[j * 9 + k] += Lx[j] * Lx[k] + Ly[j] * Ly[k];
+    }
+    for (int j = 0; j < 9; j++)
+        for (int k = 0; k < j; k++) LtL[j * 9 + k] = LtL[k * 9 + j];
+    double w[9], U[81], V[81];
+    svdj(9, 9, LtL, w, U, V);  // eigen() of the symmetric PSD LtL: eigenvalues descending
+    double H0[9], Ht[9];
+    for (int k = 0; k < 9; k++) H0[k] = V[k * 9 + 8];
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++)
+            Ht[r * 3 + c] = invHnorm[r * 3 + 0] * H0[0 * 3 + c] + invHnorm[r * 3 + 1] * H0[1 * 3 + c] +
+                            invHnorm[r * 3 + 2] * H0[2 * 3 + c];
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++)
+            H0[r * 3 + c] = Ht[r * 3 + 0] * Hnorm2[0 * 3 + c] + Ht[r * 3 + 1] * Hnorm2[1 * 3 + c] +
+                            Ht[r * 3 + 2] * Hnorm2[2 * 3 + c];
+    const double s22 = 1. / H0[8];
+    for (int k = 0; k < 9; k++) H[k] = H0[k] * s22;
+    if (n <= 4) return true;
+    // LMSolverImpl::run over h[0..7] (h22 = 1)
+    auto compute = [&](const double* h, double* r, double* J) {
+        for (int i = 0; i < n; i++) {
+            const double Mx = M[2 * i], My = M[2 * i + 1];
+            double ww = h[6] * Mx + h[7] * My + 1.;
+            ww = std::fabs(ww) > DBL_EPSILON ? 1. / ww : 0;
+            const double xi = (h[0] * Mx + h[1] * My + h[2]) * ww;
+            const double yi = (h[3] * Mx + h[4] * My + h[5]) * ww;
+            r[2 * i] = xi - m[2 * i];
+            r[2 * i + 1] = yi - m[2 * i + 1];
+            if (J) {
+                double* j0 = J + 16 * i;
+                j0[0] = Mx * ww;
+                j0[1] = My * ww;
+                j0[2] = ww;
+                j0[3] = j0[4] = j0[5] = 0.;
+                j0[6] = -Mx * ww * xi;
+                j0[7] = -My * ww * xi;
+                j0[8] = j0[9] = j0[10] = 0.;
+                j0[11] = Mx * ww;
+                j0[12] = My * ww;
+                j0[13] = ww;
+                j0[14] = -Mx * ww * yi;
+                j0[15] = -My * ww * yi;
+            }
+        }
+    };
+    std::vector<double> r(2 * n), rd(2 * n), J(16 * (size_t)n);
+    double x[8], xd[8], A[64], Ap[64], v[8], D[8], d[8];
+    memcpy(x, H, sizeof(x));
+    auto normals = [&]() {
+        for (int a = 0; a < 8; a++) {
+            for (int b = 0; b < 8; b++) {
+                double sacc = 0;
+                for (int k = 0; k < 2 * n; k++) sacc += J[(size_t)k * 8 + a] * J[(size_t)k * 8 + b];
+                A[a * 8 + b] = sacc;
+            }
+            double sv = 0;
+            for (int k = 0; k < 2 * n; k++) sv += J[(size_t)k * 8 + a] * r[k];
+            v[a] = sv;
+        }
+    };
+    auto l2sq = [&](const std::vector<double>& e) {
+        double s2 = 0;
+        for (double t : e) s2 += t * t;
+        return s2;
+    };
+    compute(x, r.data(), J.data());
+    double S = l2sq(r);
+    normals();
+    for (int i = 0; i < 8; i++) D[i] = A[i * 9];
+    const double Rlo = 0.25, Rhi = 0.75;
+    double lambda = 1, lc = 0.75;
+    int iter = 0;
+    for (;;) {
+        memcpy(Ap, A, sizeof(Ap));
+        for (int i = 0; i < 8; i++) Ap[i * 9] += lambda * D[i];
+        svd_solve(8, 8, Ap, v, d);
+        for (int i = 0; i < 8; i++) xd[i] = x[i] - d[i];
+        compute(xd, rd.data(), nullptr);
+        const double Sd = l2sq(rd);
+        double dS = 0;
+        for (int i = 0; i < 8; i++) {
+            double t = 0;
+            for (int k = 0; k < 8; k++) t += A[i * 8 + k] * d[k];
+            dS += d[i] * (2 * v[i] - t);  // temp_d = -A d + 2 v
+        }
+        const double R = (S - Sd) / (std::fabs(dS) > DBL_EPSILON ? dS : 1);
+        if (R > Rhi) {
+            lambda *= 0.5;
+            if (lambda < lc) lambda = 0;
+        } else if (R < Rlo) {
+            double t = 0;
+            for (int i = 0; i < 8; i++) t += d[i] * v[i];
+            double nu = (Sd - S) / (std::fabs(t) > DBL_EPSILON ? t : 1) + 2;
+            nu = std::min(std::max(nu, 2.), 10.);
+            if (lambda == 0) {
+                // invert(A, Ap, DECOMP_EIG): the diagonal of the (pseudo) inverse
+                double w8[8], U8[64], V8[64];
+                svdj(8, 8, A, w8, U8, V8);
+                const double thr = 8 * DBL_EPSILON * w8[0];
+                double maxval = DBL_EPSILON;
+                for (int i = 0; i < 8; i++) {
+                    double dii = 0;
+                    for (int k = 0; k < 8; k++)
+                        if (w8[k] > thr) dii += V8[i * 8 + k] * U8[i * 8 + k] / w8[k];
+                    maxval = std::max(maxval, std::fabs(dii));
+                }
+                lambda = lc = 1. / maxval;
+                nu *= 0.5;
+            }
+            lambda *= nu;
+        }
+        if (Sd < S) {
+            S = Sd;
+            std::swap(x, xd);
+            compute(x, r.data(), J.data());
+            normals();
+        }
+        iter++;
+        double dinf = 0, rinf = 0;
+        for (int i = 0; i < 8; i++) dinf = std::max(dinf, std::fabs(d[i]));
+        for (double t : r) rinf = std::max(rinf, std::fabs(t));
+        if (!(iter < 10 && dinf >= FLT_EPSILON && rinf >= FLT_EPSILON)) break;
+    }
+    memcpy(H, x, sizeof(x));
+    H[8] = 1.;
+    return true;
+}
+
+// cvFindExtrinsicCameraParams2's initial pose without an extrinsic guess
+// (calibration.cpp): normalised image points mn = ((u - cx) / fx, (v - cy) /
+// fy) (cvUndistortPoints, no distortion); centroid Mc and scatter MM of the
+// object points, cvSVD(MM) -> W, V^T. W2 / W1 < 1e-3: planar — rotate the
+// points into their plane (V^T, T = -V^T Mc), find the homography to mn, take
+// R from its first two columns (Rodrigues round trip) and t from the third;
+// otherwise DLT — the 2n x 12 system L, the eigenvector of L^T L of the
+// smallest eigenvalue as [R | t] up to scale and sign (det(R) > 0),
+// R := U V^T of its SVD, t scaled by |R| / |RR|. -> param = (rvec, tvec).
+// key[i]: the lane of point i (its index among all RANSAC points: the GPU
+// walks the inlier mask over them); null = i.
+void extrinsic_init(const double* M, const double* m, int n, const double K[4], double param[6],
+                    const int* key = nullptr) {
+    auto L = [&](int i) { return key ? key[i] : i; };
+    const double ifx = 1. / K[0], ify = 1. / K[1];
+    std::vector<double> mn(2 * (size_t)n);
+    for (int i = 0; i < n; i++) {
+        mn[2 * i] = (m[2 * i] - K[2]) * ifx;
+        mn[2 * i + 1] = (m[2 * i + 1] - K[3]) * ify;
+    }
+    double Mc[3];
+    {
+        WSum64 s(3);
+        for (int i = 0; i < n; i++)
+            for (int k = 0; k < 3; k++) s.lane(L(i))[k] += M[3 * i + k];
+        s.total(Mc);
+        for (int k = 0; k < 3; k++) Mc[k] /= n;
+    }
+    double MM[9];
+    {
+        WSum64 s(6);
+        for (int i = 0; i < n; i++) {
+            const double d0 = M[3 * i] - Mc[0], d1 = M[3 * i + 1] - Mc[1], d2 = M[3 * i + 2] - Mc[2];
+            double* a = s.lane(L(i));
+            a[0] += d0 * d0;
+            a[1] += d0 * d1;
+            a[2] += d0 * d2;
+            a[3] += d1 * d1;
+            a[4] += d1 * d2;
+            a[5] += d2 * d2;
+        }
+        double t[6];
+        s.total(t);
+        const double full[9] = {t[0], t[1], t[2], t[1], t[3], t[4], t[2], t[4], t[5]};
+        memcpy(MM, full, sizeof(MM));
+    }
+    double W[3], Um[9], Vm[9];
+    svdj(3, 3, MM, W, Um, Vm);
+    double R[9], t[3];
+    if (W[2] / W[1] < 1e-3) {
+        // planar: R_transform = V^T (rows = right singular vectors)
+        double Rt[9];
+        for (int r = 0; r < 3; r++)
+            for (int c = 0; c < 3; c++) Rt[r * 3 + c] = Vm[c * 3 + r];
+        if (Rt[2] * Rt[2] + Rt[5] * Rt[5] < 1e-10)
+            for (int k = 0; k < 9; k++) Rt[k] = k % 4 == 0 ? 1.0 : 0.0;
+        if (det3(Rt) < 0)
+            for (int k = 0; k < 9; k++) Rt[k] = -Rt[k];
+        double T[3];
+        for (int r = 0; r < 3; r++) T[r] = -(Rt[r * 3] * Mc[0] + Rt[r * 3 + 1] * Mc[1] + Rt[r * 3 + 2] * Mc[2]);
+        std::vector<float> Mxy(2 * (size_t)n), mnf(2 * (size_t)n);
+        for (int i = 0; i < n; i++) {
+            const double* src = M + 3 * i;
+            Mxy[2 * i] = (float)(Rt[0] * src[0] + Rt[1] * src[1] + Rt[2] * src[2] + T[0]);
+            Mxy[2 * i + 1] = (float)(Rt[3] * src[0] + Rt[4] * src[1] + Rt[5] * src[2] + T[1]);
+            mnf[2 * i] = (float)mn[2 * i];
+            mnf[2 * i + 1] = (float)mn[2 * i + 1];
+        }
+        double h[9];
+        bool okh = find_homography(Mxy.data(), mnf.data(), n, h);
+        for (int k = 0; k < 9 && okh; k++) okh = std::isfinite(h[k]);
+        if (okh) {
+            const double h1n = std::sqrt(h[0] * h[0] + h[3] * h[3] + h[6] * h[6]);
+            const double h2n = std::sqrt(h[1] * h[1] + h[4] * h[4] + h[7] * h[7]);
+            const double s1 = 1. / std::max(h1n, DBL_EPSILON), s2 = 1. / std::max(h2n, DBL_EPSILON);
+            const double s3 = 2. / std::max(h1n + h2n, DBL_EPSILON);
+            double Hm[9];
+            for (int r = 0; r < 3; r++) {
+                Hm[r * 3] = h[r * 3] * s1;
+                Hm[r * 3 + 1] = h[r * 3 + 1] * s2;
+                t[r] = h[r * 3 + 2] * s3;
+            }
+            // third column = h1 x h2
+            Hm[2] = Hm[3] * Hm[7] - Hm[6] * Hm[4];
+            Hm[5] = Hm[6] * Hm[1] - Hm[0] * Hm[7];
+            Hm[8] = Hm[0] * Hm[4] - Hm[3] * Hm[1];
+            double rv[3], Hr[9];
+            rodrigues_m2v(Hm, rv);
+            rodrigues_v2m(rv, Hr, nullptr);
+            for (int r = 0; r < 3; r++) t[r] = Hr[r * 3] * T[0] + Hr[r * 3 + 1] * T[1] + Hr[r * 3 + 2] * T[2] + t[r];
+            for (int r = 0; r < 3; r++)
+                for (int c = 0; c < 3; c++)
+                    R[r * 3 + c] = Hr[r * 3] * Rt[c] + Hr[r * 3 + 1] * Rt[3 + c] + Hr[r * 3 + 2] * Rt[6 + c];
+        } else {
+            for (int k = 0; k < 9; k++) R[k] = k % 4 == 0 ? 1.0 : 0.0;
+            t[0] = t[1] = t[2] = 0;
+        }
+    } else {
+        // non-planar: DLT
+        WSum64 s(78);
+        for (int i = 0; i < n; i++) {
+            const double x = -mn[2 * i], y = -mn[2 * i + 1];
+            const double X = M[3 * i], Y = M[3 * i + 1], Z = M[3 * i + 2];
+            const double L1[12] = {X, Y, Z, 1., 0., 0., 0., 0., x * X, x * Y, x * Z, x};
+            const double L2[12] = {0., 0., 0., 0., X, Y, Z, 1., y * X, y * Y, y * Z, y};
+            double* a = s.lane(L(i));
+            int k = 0;
+            for (int r = 0; r < 12; r++)
+                for (int c = r; c < 12; c++, k++) {
+                    a[k] += L1[r] * L1[c];
+                    a[k] += L2[r] * L2[c];
+                }
+        }
+        double u[78], LL[144];
+        s.total(u);
+        for (int r = 0, k = 0; r < 12; r++)
+            for (int c = r; c < 12; c++, k++) LL[r * 12 + c] = LL[c * 12 + r] = u[k];
+        double w12[12], V12[144];
+        svdj12(LL, w12, V12);
+        double RRt[12];
+        for (int k = 0; k < 12; k++) RRt[k] = V12[k * 12 + 11];  // row 11 of V^T
+        double RR[9] = {RRt[0], RRt[1], RRt[2], RRt[4], RRt[5], RRt[6], RRt[8], RRt[9], RRt[10]};
+        if (det3(RR) < 0) {
+            for (int k = 0; k < 12; k++) RRt[k] = -RRt[k];
+            for (int k = 0; k < 9; k++) RR[k] = -RR[k];
+        }
+        double sc = 0;
+        for (int k = 0; k < 9; k++) sc += RR[k] * RR[k];
+        sc = std::sqrt(sc);
+        double w3[3], U3[9], V3[9];
+        svdj(3, 3, RR, w3, U3, V3);
+        double nr = 0;
+        for (int r = 0; r < 3; r++)
+            for (int c = 0; c < 3; c++) {
+                R[r * 3 + c] = U3[r * 3] * V3[c * 3] + U3[r * 3 + 1] * V3[c * 3 + 1] + U3[r * 3 + 2] * V3[c * 3 + 2];
+                nr += R[r * 3 + c] * R[r * 3 + c];
+            }
+        const double f = std::sqrt(nr) / sc;
+        t[0] = RRt[3] * f;
+        t[1] = RRt[7] * f;
+        t[2] = RRt[11] * f;
+    }
+    rodrigues_m2v(R, param);
+    param[3] = t[0];
+    param[4] = t[1];
+    param[5] = t[2];
+}
+
 }  // namespace
 
 extern "C" {
@@ -743,6 +1096,10 @@ void oracle_epnp(const double* pw, const double* uv, int n, const double K[4], d
 
 void oracle_pnp_refine(const double* M, const double* m, int n, const double K[4], double param[6]) {
     refine_lm(M, m, n, K, param);
+}
+
+void oracle_pnp_extrinsic_init(const double* M, const double* m, int n, const double K[4], double param[6]) {
+    extrinsic_init(M, m, n, K, param);
 }
 
 int oracle_pnp_ransac(const float* Xw, const float* uv, int n, const odo_calib* c, int iterations, float reproj_err,
@@ -806,15 +1163,18 @@ int oracle_pnp_ransac(const float* Xw, const float* uv, int n, const odo_calib* 
     memcpy(model_out, bestModel, sizeof(bestModel));
     // refinement on the inliers (float -> double as convertTo(CV_64F))
     std::vector<double> Mi, mi;
+    std::vector<int> key;
     for (int i = 0; i < n; i++)
         if (best[i]) {
             for (int k = 0; k < 3; k++) Mi.push_back((double)Xw[3 * i + k]);
             mi.push_back((double)uv[2 * i]);
             mi.push_back((double)uv[2 * i + 1]);
+            key.push_back(i);
         }
     const int ni = (int)(mi.size() / 2);
+    // solvePnP(..., useExtrinsicGuess = false): cvFindExtrinsicCameraParams2's own start
     double p[6];
-    memcpy(p, bestModel, sizeof(p));
+    extrinsic_init(Mi.data(), mi.data(), ni, K, p, key.data());
     refine_lm(Mi.data(), mi.data(), ni, K, p);
     memcpy(rt_out, p, sizeof(p));
     // Converter::toHomogeneous(r, t)

@@ -136,6 +136,7 @@ def lib():
             "oracle_rodrigues_inv": (None, [P, P]),
             "oracle_epnp": (None, [P, P, C.c_int, P, P]),
             "oracle_pnp_refine": (None, [P, P, C.c_int, P, P]),
+            "oracle_pnp_extrinsic_init": (None, [P, P, C.c_int, P, P]),
             "oracle_gicp": (C.c_int, [P, C.c_int, P, C.c_int, P, C.c_int, C.c_double, P, P, P, P]),
             "oracle_gicp_covariances": (None, [P, C.c_int, P]),
         }

@@ -11,7 +11,10 @@ GPU: odo_pnp_ransac (k_pnpransac.hip) against the oracle on the same inputs:
 every visited hypothesis' inlier count, the winning hypothesis, the iterations
 run and the inlier mask exactly; the RANSAC model within 1e-9 and the refined
 pose within 1e-7 (the device libm's cos/sin/acos are the only non-IEEE steps;
-the refinement's J^T J is reduced in a different order).
+the refinement's J^T J is reduced in a different order). The refinement
+starts where solvePnP(useExtrinsicGuess = false) starts (pnpransac.cpp:34):
+cvFindExtrinsicCameraParams2's DLT, or its homography branch for coplanar
+landmarks (test_gpu_parity_planar).
 """
 import math
 
@@ -154,6 +157,26 @@ def test_oracle_recovers_pose(seed, n, outl):
     assert rms(r["rt"]) <= rms(r["model"]) + 1e-9
 
 
+@pytest.mark.parametrize("planar", [False, True], ids=["dlt", "homography"])
+@pytest.mark.parametrize("n", [6, 40, 300])
+def test_extrinsic_init_exact(planar, n):
+    """cvFindExtrinsicCameraParams2's start without a guess (the final
+    solvePnP of solvePnPRansac: pnpransac.cpp:34 passes useExtrinsicGuess =
+    false): the DLT (non-planar points) and the homography decomposition
+    (coplanar points) recover a noise-free pose on their own, and CvLevMarq
+    from that start lands on it."""
+    Xw, uv, cal, rv, t, _ = _problem(40 + n, n, 0.0, noise=0.0, planar=planar)
+    K = np.array([cal.fx, cal.fy, cal.cx, cal.cy], np.float64)
+    M, m = Xw.astype(np.float64), uv.astype(np.float64)
+    p = np.zeros(6)
+    O.lib().oracle_pnp_extrinsic_init(O.ptr(M), O.ptr(m), n, O.ptr(K), O.ptr(p))
+    np.testing.assert_allclose(p[:3], rv, atol=2e-3)
+    np.testing.assert_allclose(p[3:], t, atol=5e-3)
+    O.lib().oracle_pnp_refine(O.ptr(M), O.ptr(m), n, O.ptr(K), O.ptr(p))
+    np.testing.assert_allclose(p[:3], rv, atol=1e-4)
+    np.testing.assert_allclose(p[3:], t, atol=1e-4)
+
+
 def test_oracle_too_few_points():
     Xw, uv, cal, *_ = _problem(5, 9, 0.0)
     r = O.pnp_ransac(Xw, uv, cal)
@@ -202,6 +225,18 @@ def odo():
 def test_gpu_parity_synthetic(odo, seed, n, outl):
     Xw, uv, cal, *_ = _problem(seed, n, outl)
     _check_gpu(odo, Xw, uv, cal)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,n,outl", [(31, 300, 0.3), (32, 40, 0.0), (33, 900, 0.5)])
+def test_gpu_parity_planar(odo, seed, n, outl):
+    """Coplanar landmarks: the final solvePnP's unseeded start takes
+    cvFindExtrinsicCameraParams2's homography branch (findHomography + its
+    LMSolver polish on lane 0) instead of the DLT."""
+    Xw, uv, cal, rv, t, _ = _problem(seed, n, outl, planar=True)
+    ref, res = _check_gpu(odo, Xw, uv, cal)
+    assert res.ok == 1
+    np.testing.assert_allclose(np.r_[res.rvec[:]], rv, atol=5e-3)
 
 
 @pytest.mark.gpu
