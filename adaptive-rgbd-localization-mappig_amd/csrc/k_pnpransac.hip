@@ -808,10 +808,10 @@ __device__ void block_sum(double* v, double (*wred)[NV], double* out) {
     if ((threadIdx.x & 63) == 0)
         for (int k = 0; k < NV; k++) wred[threadIdx.x >> 6][k] = v[k];
     __syncthreads();
-    if (threadIdx.x < NV) {
-        double s = wred[0][threadIdx.x];
-        for (int w = 1; w < PR_REFINE_THREADS / 64; w++) s += wred[w][threadIdx.x];
-        out[threadIdx.x] = s;
+    for (int k = threadIdx.x; k < NV; k += PR_REFINE_THREADS) {  // NV may exceed the thread count
+        double s = wred[0][k];
+        for (int w = 1; w < PR_REFINE_THREADS / 64; w++) s += wred[w][k];
+        out[k] = s;
     }
     __syncthreads();
 }
