@@ -99,11 +99,11 @@ ODO_INLINE void normalize_rot(SE3& s) {
         s.q.z = -s.q.z;
         s.q.w = -s.q.w;
     }
-    double n = sqrt((s.q.x * s.q.x + s.q.y * s.q.y) + (s.q.z * s.q.z + s.q.w * s.q.w));
-    s.q.x /= n;
-    s.q.y /= n;
-    s.q.z /= n;
-    s.q.w /= n;
+    const double in = 1.0 / sqrt((s.q.x * s.q.x + s.q.y * s.q.y) + (s.q.z * s.q.z + s.q.w * s.q.w));
+    s.q.x *= in;
+    s.q.y *= in;
+    s.q.z *= in;
+    s.q.w *= in;
 }
 ODO_INLINE SE3 se3_mul(const SE3& a, const SE3& b) {
     SE3 r = a;
@@ -130,8 +130,13 @@ ODO_INLINE SE3 se3_exp(const double u[6]) {
                 V[i][j] = R[i][j];
             }
     } else {
-        double a = sin(theta) / theta, b = (1 - cos(theta)) / (theta * theta);
-        double c = (theta - sin(theta)) / pow(theta, 3);
+        double sn, cs;
+        sincos(theta, &sn, &cs);  // one reduction for both (g2o: sin(), cos())
+        const double th2 = theta * theta;
+        // g2o divides by pow(theta, 3): theta * theta^2 differs in the last ulp
+        // at most (PnP parity is a tolerance, 1e-4 on the pose)
+        double a = sn / theta, b = (1 - cs) / th2;
+        double c = (theta - sn) / (theta * th2);
         for (int i = 0; i < 3; i++)
             for (int j = 0; j < 3; j++) {
                 R[i][j] = ((i == j ? 1.0 : 0.0) + a * O[i][j]) + b * O2[i][j];
@@ -147,6 +152,28 @@ ODO_INLINE SE3 se3_exp(const double u[6]) {
 ODO_INLINE void se3_map(const SE3& T, const double p[3], double o[3]) {
     qrot(T.q, p, o);
     for (int i = 0; i < 3; i++) o[i] += T.t[i];
+}
+// The pose as a rotation matrix + translation for the edge passes: 9 products
+// per point instead of the quaternion's two cross products (g2o maps with the
+// quaternion; the difference is rounding, within the PnP tolerance).
+struct SE3M {
+    double R[9], t[3];
+};
+ODO_INLINE SE3M se3_mat(const SE3& T) {
+    double r[3][3];
+    quat_to_R(T.q, r);
+    SE3M M;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+#pragma unroll
+        for (int j = 0; j < 3; j++) M.R[3 * i + j] = r[i][j];
+        M.t[i] = T.t[i];
+    }
+    return M;
+}
+ODO_INLINE void se3m_map(const SE3M& T, const double p[3], double o[3]) {
+#pragma unroll
+    for (int i = 0; i < 3; i++) o[i] = (T.R[3 * i] * p[0] + T.R[3 * i + 1] * p[1]) + (T.R[3 * i + 2] * p[2] + T.t[i]);
 }
 
 // Eigen LDLT with diagonal pivoting on a 6x6, every index static after
@@ -217,9 +244,11 @@ ODO_INLINE bool ldlt_solve6(const double Ain[6][6], const double b[6], double x[
         const double akk = m[k][k];
         const bool valid = fabs(akk) > 0;
         if (k == 0 && !valid) fail = true;
-        if (valid)
+        if (valid) {
+            const double ia = 1.0 / akk;  // one division per pivot (Eigen divides each entry)
 #pragma unroll
-            for (int i = k + 1; i < 6; i++) m[i][k] /= akk;
+            for (int i = k + 1; i < 6; i++) m[i][k] *= ia;
+        }
         if (sign == 1) {
             if (akk < 0) sign = 3;
         } else if (sign == 2) {
@@ -317,7 +346,8 @@ struct PnPCam {
 // EdgeSE3ProjectXYZOnlyPose / EdgeStereoSE3ProjectXYZOnlyPose::computeError (g2o types_six_dof_expmap)
 ODO_INLINE void edge_err(const double Xc[3], const double ob[3], bool stereo, const PnPCam& c, double e[3]) {
     if (!stereo) {
-        double px = Xc[0] / Xc[2], py = Xc[1] / Xc[2];
+        const double iz = 1.0 / Xc[2];
+        double px = Xc[0] * iz, py = Xc[1] * iz;
         e[0] = ob[0] - (px * c.fx + c.cx);
         e[1] = ob[1] - (py * c.fy + c.cy);
         e[2] = 0;
@@ -357,6 +387,7 @@ ODO_INLINE void huber_rho(double delta, double chi, double rho[3]) {
 #define PNP_NW 4
 #define PNP_NT (64 * PNP_NW)
 #define PNP_K 4  // Levenberg trials evaluated per edge pass (one per 16-lane group of wave 0)
+#define PNP_EC 1024  // edges per pair staged in LDS for the passes (29 B each, 29 KB; the rest stream)
 static_assert(PNP_K <= 4, "the trial solves run on the four 16-lane groups of one wave");
 
 // Sum of NV per-lane doubles over the workgroup, the result in every lane.
@@ -414,11 +445,11 @@ ODO_INLINE void wg_sum(double (&v)[NV], double* red) {
 
 // computeActiveErrors + activeRobustChi2 + buildSystem contribution of one edge
 // at pose T into acc (H upper triangle row-major 0..20, b 21..26, robust chi 27)
-ODO_INLINE void edge_build(const SE3& T, const double Xw[3], const double ob[3], double info, uint8_t fl,
+ODO_INLINE void edge_build(const SE3M& T, const double Xw[3], const double ob[3], double info, uint8_t fl,
                            const PnPCam& cam, double dMono, double dStereo, double (&acc)[28]) {
     const bool st = fl & PE_STEREO;
     double Xc[3], e[3];
-    se3_map(T, Xw, Xc);
+    se3m_map(T, Xw, Xc);
     edge_err(Xc, ob, st, cam, e);
     const double c2 = chi2_of(e, info, st);
     double rho[3] = {c2, 1.0, 0.0};
@@ -465,11 +496,11 @@ ODO_INLINE void edge_build(const SE3& T, const double Xw[3], const double ob[3],
 }
 
 // robust (Huber) chi2 of one edge at pose T; c2 = plain chi2 of the stored error
-ODO_INLINE double edge_robust_chi(const SE3& T, const double Xw[3], const double ob[3], double info, uint8_t fl,
+ODO_INLINE double edge_robust_chi(const SE3M& T, const double Xw[3], const double ob[3], double info, uint8_t fl,
                                   const PnPCam& cam, double dMono, double dStereo, double& c2) {
     const bool st = fl & PE_STEREO;
     double Xc[3], e[3];
-    se3_map(T, Xw, Xc);
+    se3m_map(T, Xw, Xc);
     edge_err(Xc, ob, st, cam, e);
     c2 = chi2_of(e, info, st);
     if (fl & PE_ROBUST) {
@@ -509,6 +540,8 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
     __shared__ double s_T[PNP_K][8];
     __shared__ int s_ok[PNP_K];
     __shared__ int s_ne[PNP_NW];
+    __shared__ float s_eX[3][PNP_EC], s_eO[3][PNP_EC], s_eI[PNP_EC];
+    __shared__ uint8_t s_eF[PNP_EC];
     odo_pair_result* R = res + p;
     const int s1 = slot0 + p, s2 = slot0 + p + 1;
     const int n2 = nkp[s2];
@@ -562,6 +595,20 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
     }
     const PnPCam cam{(double)cal.fx, (double)cal.fy, (double)cal.cx, (double)cal.cy, (double)cal.mbf};
     const double dMono = (double)(float)sqrt(5.991), dStereo = (double)(float)sqrt(7.815);  // pnpsolver.cpp:51-52
+    // the first PNP_EC edges staged in LDS once (SoA), read by every pass
+    // (their flags are updated there); edges past PNP_EC stream from the
+    // pair's scratch
+    const int nec = min(ne, PNP_EC);
+    for (int k = lane; k < nec; k += PNP_NT) {
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            s_eX[c][k] = E.X[3 * k + c];
+            s_eO[c][k] = E.obs[3 * k + c];
+        }
+        s_eI[k] = E.info[k];
+        s_eF[k] = E.flags[k];
+    }
+    __syncthreads();
     SE3 T0s;
     {
         double R0[3][3], t0[3];
@@ -596,12 +643,22 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
             double acc[28];
 #pragma unroll
             for (int k = 0; k < 28; k++) acc[k] = 0;
-            for (int k = lane; k < ne; k += PNP_NT) {
-                const uint8_t fl = E.flags[k];
-                if (fl & PE_OUT) continue;
-                const double Xw[3] = {E.X[3 * k], E.X[3 * k + 1], E.X[3 * k + 2]};
-                const double ob[3] = {E.obs[3 * k], E.obs[3 * k + 1], E.obs[3 * k + 2]};
-                edge_build(T, Xw, ob, (double)E.info[k], fl, cam, dMono, dStereo, acc);
+            {
+                const SE3M Tm = se3_mat(T);
+                for (int k = lane; k < nec; k += PNP_NT) {
+                    const uint8_t fl = s_eF[k];
+                    if (fl & PE_OUT) continue;
+                    const double Xw[3] = {s_eX[0][k], s_eX[1][k], s_eX[2][k]};
+                    const double ob[3] = {s_eO[0][k], s_eO[1][k], s_eO[2][k]};
+                    edge_build(Tm, Xw, ob, (double)s_eI[k], fl, cam, dMono, dStereo, acc);
+                }
+                for (int k = lane + nec; k < ne; k += PNP_NT) {
+                    const uint8_t fl = E.flags[k];
+                    if (fl & PE_OUT) continue;
+                    const double Xw[3] = {E.X[3 * k], E.X[3 * k + 1], E.X[3 * k + 2]};
+                    const double ob[3] = {E.obs[3 * k], E.obs[3 * k + 1], E.obs[3 * k + 2]};
+                    edge_build(Tm, Xw, ob, (double)E.info[k], fl, cam, dMono, dStereo, acc);
+                }
             }
             wg_sum<28>(acc, red);
             PP_ACC(tb);
@@ -690,37 +747,50 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                     }
                 }
                 __syncthreads();
-                SE3 Tc[PNP_K];
                 double sc[PNP_K];
                 bool okc[PNP_K];
 #pragma unroll
                 for (int k = 0; k < PNP_K; k++) {
-                    Tc[k].q = Quat{s_T[k][0], s_T[k][1], s_T[k][2], s_T[k][3]};
-                    Tc[k].t[0] = s_T[k][4];
-                    Tc[k].t[1] = s_T[k][5];
-                    Tc[k].t[2] = s_T[k][6];
                     sc[k] = s_T[k][7];
                     okc[k] = s_ok[k] != 0;
                 }
                 PP_ACC(tsol);
                 PP_T0();
-                // computeActiveErrors + activeRobustChi2 at every candidate
+                // computeActiveErrors + activeRobustChi2 at every candidate,
+                // candidate by candidate (one pose matrix live at a time) over
+                // the register-held edges
                 double chi[PNP_K];
 #pragma unroll
                 for (int k = 0; k < PNP_K; k++) chi[k] = 0;
-                for (int e = lane; e < ne; e += PNP_NT) {
-                    const uint8_t fl = E.flags[e];
-                    if (fl & PE_OUT) continue;
-                    const double Xw[3] = {E.X[3 * e], E.X[3 * e + 1], E.X[3 * e + 2]};
-                    const double ob[3] = {E.obs[3 * e], E.obs[3 * e + 1], E.obs[3 * e + 2]};
-                    const double info = E.info[e];
-#pragma unroll
-                    for (int k = 0; k < PNP_K; k++) {
-                        if (k >= K) break;
+                for (int k = 0; k < K; k++) {
+                    SE3 Tk;
+                    Tk.q = Quat{s_T[k][0], s_T[k][1], s_T[k][2], s_T[k][3]};
+                    Tk.t[0] = s_T[k][4];
+                    Tk.t[1] = s_T[k][5];
+                    Tk.t[2] = s_T[k][6];
+                    const SE3M Tm = se3_mat(Tk);
+                    double ck = 0;
+                    for (int e = lane; e < nec; e += PNP_NT) {
+                        const uint8_t fl = s_eF[e];
+                        if (fl & PE_OUT) continue;
+                        const double Xw[3] = {s_eX[0][e], s_eX[1][e], s_eX[2][e]};
+                        const double ob[3] = {s_eO[0][e], s_eO[1][e], s_eO[2][e]};
                         double c2;
-                        chi[k] += edge_robust_chi(Tc[k], Xw, ob, info, fl, cam, dMono, dStereo, c2);
+                        ck += edge_robust_chi(Tm, Xw, ob, (double)s_eI[e], fl, cam, dMono, dStereo, c2);
                         E.chi4[4 * e + k] = c2;
                     }
+                    for (int e = lane + nec; e < ne; e += PNP_NT) {
+                        const uint8_t fl = E.flags[e];
+                        if (fl & PE_OUT) continue;
+                        const double Xw[3] = {E.X[3 * e], E.X[3 * e + 1], E.X[3 * e + 2]};
+                        const double ob[3] = {E.obs[3 * e], E.obs[3 * e + 1], E.obs[3 * e + 2]};
+                        double c2;
+                        ck += edge_robust_chi(Tm, Xw, ob, (double)E.info[e], fl, cam, dMono, dStereo, c2);
+                        E.chi4[4 * e + k] = c2;
+                    }
+#pragma unroll
+                    for (int q = 0; q < PNP_K; q++)
+                        if (q == k) chi[q] = ck;
                 }
                 wg_sum<PNP_K>(chi, red);
                 PP_ACC(tchi);
@@ -744,7 +814,10 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                         lambda = lam[k] * sf;
                         ni = 2;
                         curChi = tempChi;
-                        T = Tc[k];
+                        T.q = Quat{s_T[k][0], s_T[k][1], s_T[k][2], s_T[k][3]};
+                        T.t[0] = s_T[k][4];
+                        T.t[1] = s_T[k][5];
+                        T.t[2] = s_T[k][6];
                         trials_done = true;
                     } else {
                         lambda = lam[k] * nis[k];  // T stays at the backup
@@ -758,28 +831,41 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
         // ---- classification (pnpsolver.cpp:157-201)
         PP_T0();
         int bad = 0;
-        for (int k = lane; k < ne; k += PNP_NT) {
-            uint8_t fl = E.flags[k];
-            const bool st = fl & PE_STEREO;
-            double c2 = E.chi4[4 * k + last_slot];
-            if (fl & PE_OUT) {  // IsOutlier: e->computeError() at the current estimate
+        {
+            const SE3M Tm = se3_mat(T);
+            // reclassify edge k (flags in / out); the stored chi2 of the last
+            // computeActiveErrors, recomputed at T for the edges that were out
+            auto classify = [&](int k, uint32_t fl, const double Xw[3], const double ob[3], double info) {
+                const bool st = fl & PE_STEREO;
+                double c2 = E.chi4[4 * k + last_slot];
+                if (fl & PE_OUT) {  // IsOutlier: e->computeError() at the current estimate
+                    double Xc[3], e[3];
+                    se3m_map(Tm, Xw, Xc);
+                    edge_err(Xc, ob, st, cam, e);
+                    c2 = chi2_of(e, info, st);
+                    E.chi4[4 * k + last_slot] = c2;
+                }
+                const float chi2 = (float)c2;
+                if (chi2 > (st ? chi2Stereo : chi2Mono)) {
+                    fl |= PE_OUT;
+                    bad++;
+                } else {
+                    fl &= ~PE_OUT;
+                }
+                if (it == 2) fl &= ~PE_ROBUST;
+                E.flags[k] = (uint8_t)fl;
+                return fl;
+            };
+            for (int k = lane; k < nec; k += PNP_NT) {
+                const double Xw[3] = {s_eX[0][k], s_eX[1][k], s_eX[2][k]};
+                const double ob[3] = {s_eO[0][k], s_eO[1][k], s_eO[2][k]};
+                s_eF[k] = (uint8_t)classify(k, s_eF[k], Xw, ob, (double)s_eI[k]);
+            }
+            for (int k = lane + nec; k < ne; k += PNP_NT) {
                 const double Xw[3] = {E.X[3 * k], E.X[3 * k + 1], E.X[3 * k + 2]};
                 const double ob[3] = {E.obs[3 * k], E.obs[3 * k + 1], E.obs[3 * k + 2]};
-                double Xc[3], e[3];
-                se3_map(T, Xw, Xc);
-                edge_err(Xc, ob, st, cam, e);
-                c2 = chi2_of(e, (double)E.info[k], st);
-                E.chi4[4 * k + last_slot] = c2;
+                classify(k, E.flags[k], Xw, ob, (double)E.info[k]);
             }
-            const float chi2 = (float)c2;
-            if (chi2 > (st ? chi2Stereo : chi2Mono)) {
-                fl |= PE_OUT;
-                bad++;
-            } else {
-                fl &= ~PE_OUT;
-            }
-            if (it == 2) fl &= ~PE_ROBUST;
-            E.flags[k] = fl;
         }
         double bd[1] = {(double)bad};
         wg_sum<1>(bd, red);
@@ -1055,7 +1141,7 @@ __global__ void __launch_bounds__(64) k_pnp1(const int32_t* __restrict__ f2_src,
                     for (int k = 0; k < PNP_K; k++) {
                         if (k >= K) break;
                         double c2;
-                        chi[k] += edge_robust_chi(Tc[k], Xw, ob, info, fl, cam, dMono, dStereo, c2);
+                        chi[k] += edge_robust_chi(se3_mat(Tc[k]), Xw, ob, info, fl, cam, dMono, dStereo, c2);
                         E.chi4[4 * e + k] = c2;
                     }
                 }

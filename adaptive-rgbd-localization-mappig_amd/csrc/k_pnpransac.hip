@@ -61,44 +61,30 @@ __device__ __forceinline__ double group_sum16(double x) {
     return __shfl(x, 0, PR_EPNP_GROUP);
 }
 
-// oracle/pnpransac_ref.cpp's kRR12: 11 rounds of 6 disjoint column pairs
-constexpr int kRR12[11][6][2] = {{{0, 11}, {1, 10}, {2, 9}, {3, 8}, {4, 7}, {5, 6}}, {{0, 1}, {2, 11}, {3, 10}, {4, 9}, {5, 8}, {6, 7}}, {{0, 2}, {1, 3}, {4, 11}, {5, 10}, {6, 9}, {7, 8}}, {{0, 3}, {2, 4}, {1, 5}, {6, 11}, {7, 10}, {8, 9}}, {{0, 4}, {3, 5}, {2, 6}, {1, 7}, {8, 11}, {9, 10}}, {{0, 5}, {4, 6}, {3, 7}, {2, 8}, {1, 9}, {10, 11}}, {{0, 6}, {5, 7}, {4, 8}, {3, 9}, {2, 10}, {1, 11}}, {{0, 7}, {6, 8}, {5, 9}, {4, 10}, {3, 11}, {1, 2}}, {{0, 8}, {7, 9}, {6, 10}, {5, 11}, {1, 4}, {2, 3}}, {{0, 9}, {8, 10}, {7, 11}, {1, 6}, {2, 5}, {3, 4}}, {{0, 10}, {9, 11}, {1, 8}, {2, 7}, {3, 6}, {4, 5}}};
-
 __device__ void svdj12_rows(double* arow, double* vrow, int r, int* ord) {
 #pragma unroll
     for (int j = 0; j < 12; j++) vrow[j] = (r == j) ? 1.0 : 0.0;
     for (int sweep = 0; sweep < 60; sweep++) {
         int changed = 0;
 #pragma unroll
-        for (int rd = 0; rd < 11; rd++) {
-            // the round's six pairs are disjoint: all sums from the pre-round
-            // state, six independent rotation chains, then the lane-local updates
-            double al[6], be[6], ga[6];
+        for (int p = 0; p < 11; p++)
 #pragma unroll
-            for (int k = 0; k < 6; k++) {
-                const int p = kRR12[rd][k][0], q = kRR12[rd][k][1];
+            for (int q = p + 1; q < 12; q++) {
                 const double ap0 = arow[p], aq0 = arow[q];
-                al[k] = group_sum16(ap0 * ap0);
-                be[k] = group_sum16(aq0 * aq0);
-                ga[k] = group_sum16(ap0 * aq0);
-            }
-#pragma unroll
-            for (int k = 0; k < 6; k++) {
-                const int p = kRR12[rd][k][0], q = kRR12[rd][k][1];
-                const double alpha = al[k], beta = be[k], gamma = ga[k];
+                const double alpha = group_sum16(ap0 * ap0);
+                const double beta = group_sum16(aq0 * aq0);
+                const double gamma = group_sum16(ap0 * aq0);
                 if (gamma == 0.0 || fabs(gamma) <= DBL_EPSILON * sqrt(alpha * beta)) continue;
                 changed = 1;
                 const double zeta = (beta - alpha) / (2.0 * gamma);
                 const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
                 const double c = 1.0 / sqrt(1.0 + t * t), s = c * t;
-                const double ap0 = arow[p], aq0 = arow[q];
                 arow[p] = c * ap0 - s * aq0;
                 arow[q] = s * ap0 + c * aq0;
                 const double vp = vrow[p], vq = vrow[q];
                 vrow[p] = c * vp - s * vq;
                 vrow[q] = s * vp + c * vq;
             }
-        }
         if (!changed) break;
     }
     double ww[12];
@@ -864,8 +850,9 @@ __device__ void lm_pass(const float* __restrict__ Xw, const float* __restrict__ 
 // own initial pose (extrinsic_init in oracle/pnpransac_ref.cpp, same
 // operation order): centroid + scatter of the object points (wave sums over
 // the inliers, point i on lane i % 64), 3x3 SVD -> planar or not; non-planar:
-// the DLT's 12 x 12 L^T L (78 wave sums), its smallest singular vector by the
-// row-parallel Jacobi of the EPnP kernel (lanes 0..15), [R | t] from it;
+// the DLT's 12 x 12 L^T L (78 wave sums), its smallest singular vector (by
+// inverse iteration: the same vector as the oracle's Jacobi SVD up to
+// rounding), [R | t] from it;
 // planar: the homography path on lane 0 (rare: coplanar landmarks), its
 // matrices in LDS.
 
@@ -1129,7 +1116,7 @@ __device__ void extrinsic_init(const float* __restrict__ Xw, const float* __rest
                                const uint8_t* __restrict__ m, int n, int ni, const PrK& K, double* sp) {
     __shared__ double s_red[78];
     __shared__ double wred[1][78];
-    __shared__ double s_mc[3], s_rrt[12];
+    __shared__ double s_mc[3];
     __shared__ int s_planar;
     __shared__ double s_Rt[9], s_T[3];
     __shared__ HomLds hs;
@@ -1190,26 +1177,54 @@ __device__ void extrinsic_init(const float* __restrict__ Xw, const float* __rest
                 }
         }
         block_sum<78>(v, wred, s_red);
-        if (lane < 16) {
-            const int r = lane;
-            double arow[12], vrow[12];
-            int ord[12];
-#pragma unroll
-            for (int c = 0; c < 12; c++) {
-                const int a = r < c ? r : c, b = r < c ? c : r;  // upper-triangle index of (a, b)
-                arow[c] = r < 12 ? s_red[a * 12 - a * (a - 1) / 2 + (b - a)] : 0.0;
-            }
-            svdj12_rows(arow, vrow, r, ord);
-            double e = 0;
-#pragma unroll
-            for (int c = 0; c < 12; c++)
-                if (ord[11] == c) e = vrow[c];
-            if (r < 12) s_rrt[r] = e;  // row 11 of V^T
-        }
-        __syncthreads();
         if (lane == 0) {
+            // row 11 of cvSVD(L^T L)'s V^T = the eigenvector of the smallest
+            // eigenvalue, here by inverse iteration (the oracle runs the
+            // Jacobi SVD of OpenCV's cvSVD; a 12 x 12 Jacobi is ~0.4 ms of
+            // dependent sqrt / div chains on the GPU, this ~20 us): Cholesky
+            // of L^T L + delta I (the shift keeps it positive definite on
+            // noise-free data and leaves the eigenvectors unchanged), six
+            // solves from a fixed start vector, unit norm; the sign is fixed
+            // below by det(R) > 0 as in calibration.cpp. Agreement with the
+            // oracle's refined pose: 1e-7 (tests/test_pnpransac.py).
+            double* A = hs.a;  // 12 x 12 Cholesky factor (lower)
+            double tr = 0;
+            for (int r = 0; r < 12; r++) tr += s_red[r * 12 - r * (r - 1) / 2];
+            const double delta = 1e-13 * tr + DBL_MIN;
+            for (int r = 0; r < 12; r++)
+                for (int c = 0; c <= r; c++) A[r * 12 + c] = s_red[c * 12 - c * (c - 1) / 2 + (r - c)] + (r == c ? delta : 0.0);
+            for (int c = 0; c < 12; c++) {
+                double d = A[c * 12 + c];
+                for (int k = 0; k < c; k++) d -= A[c * 12 + k] * A[c * 12 + k];
+                d = sqrt(fmax(d, DBL_MIN));
+                A[c * 12 + c] = d;
+                const double id = 1.0 / d;
+                for (int r = c + 1; r < 12; r++) {
+                    double e = A[r * 12 + c];
+                    for (int k = 0; k < c; k++) e -= A[r * 12 + k] * A[c * 12 + k];
+                    A[r * 12 + c] = e * id;
+                }
+            }
+            double x[12];
+            for (int k = 0; k < 12; k++) x[k] = 1.0 + 0.1 * k;  // fixed start
+            for (int it = 0; it < 6; it++) {
+                for (int r = 0; r < 12; r++) {  // L y = x
+                    double e = x[r];
+                    for (int k = 0; k < r; k++) e -= A[r * 12 + k] * x[k];
+                    x[r] = e / A[r * 12 + r];
+                }
+                for (int r = 11; r >= 0; r--) {  // L^T z = y
+                    double e = x[r];
+                    for (int k = r + 1; k < 12; k++) e -= A[k * 12 + r] * x[k];
+                    x[r] = e / A[r * 12 + r];
+                }
+                double nx = 0;
+                for (int k = 0; k < 12; k++) nx += x[k] * x[k];
+                nx = 1.0 / sqrt(nx);
+                for (int k = 0; k < 12; k++) x[k] *= nx;
+            }
             double RRt[12];
-            for (int k = 0; k < 12; k++) RRt[k] = s_rrt[k];
+            for (int k = 0; k < 12; k++) RRt[k] = x[k];
             double RR[9] = {RRt[0], RRt[1], RRt[2], RRt[4], RRt[5], RRt[6], RRt[8], RRt[9], RRt[10]};
             if (det3d(RR) < 0) {
                 for (int k = 0; k < 12; k++) RRt[k] = -RRt[k];

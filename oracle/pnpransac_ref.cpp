@@ -117,12 +117,7 @@ double tree16(const double* x) {
     return y[0];
 }
 
-// Round-robin (parallel) Jacobi ordering of the 66 column pairs of the 12 x 12
-// eigenproblem: 11 rounds of 6 disjoint pairs, so the GPU rotates a round's
-// pairs at once (the rotations of a round commute). Pinned choice.
-const int kRR12[11][6][2] = {{{0, 11}, {1, 10}, {2, 9}, {3, 8}, {4, 7}, {5, 6}}, {{0, 1}, {2, 11}, {3, 10}, {4, 9}, {5, 8}, {6, 7}}, {{0, 2}, {1, 3}, {4, 11}, {5, 10}, {6, 9}, {7, 8}}, {{0, 3}, {2, 4}, {1, 5}, {6, 11}, {7, 10}, {8, 9}}, {{0, 4}, {3, 5}, {2, 6}, {1, 7}, {8, 11}, {9, 10}}, {{0, 5}, {4, 6}, {3, 7}, {2, 8}, {1, 9}, {10, 11}}, {{0, 6}, {5, 7}, {4, 8}, {3, 9}, {2, 10}, {1, 11}}, {{0, 7}, {6, 8}, {5, 9}, {4, 10}, {3, 11}, {1, 2}}, {{0, 8}, {7, 9}, {6, 10}, {5, 11}, {1, 4}, {2, 3}}, {{0, 9}, {8, 10}, {7, 11}, {1, 6}, {2, 5}, {3, 4}}, {{0, 10}, {9, 11}, {1, 8}, {2, 7}, {3, 6}, {4, 5}}};
-
-// svdj for the 12 x 12 M^T M with tree16 column sums, pairs in kRR12 order; V only.
+// svdj for the 12 x 12 M^T M with tree16 column sums; V only.
 void svdj12(const double* A, double* w, double* V) {
     double a[144], v[144];
     memcpy(a, A, sizeof(a));
@@ -130,9 +125,8 @@ void svdj12(const double* A, double* w, double* V) {
         for (int j = 0; j < 12; j++) v[i * 12 + j] = i == j ? 1.0 : 0.0;
     for (int sweep = 0; sweep < 60; sweep++) {
         int changed = 0;
-        for (int rd = 0; rd < 11; rd++)
-            for (int pr = 0; pr < 6; pr++) {
-                const int p = kRR12[rd][pr][0], q = kRR12[rd][pr][1];
+        for (int p = 0; p < 11; p++)
+            for (int q = p + 1; q < 12; q++) {
                 double pp[12], qq[12], pq[12];
                 for (int i = 0; i < 12; i++) {
                     const double ap = a[i * 12 + p], aq = a[i * 12 + q];
