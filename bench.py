@@ -572,6 +572,8 @@ def main():
     ap.add_argument("--latency-frames", type=int, default=120,
                     help="frames of the per-frame latency leg (odo_frontend.hpp path; 0: skip it)")
     ap.add_argument("--hard-steps", type=int, default=20, help="steps of the hard-workload leg (0: skip it)")
+    ap.add_argument("--tum", default=None, help="a TUM RGB-D sequence directory with associations.txt "
+                    "(utils.cpp:16-38 format): its frames replace the synthetic loop")
     ap.add_argument("--workload", choices=["default", "hard"], default="default",
                     help="main leg's sequence: the cfg2 proxy or the hard variant (synth hard=True)")
     ap.add_argument("--no-kernel-timing", action="store_true", help="no events around the kNN-2 launches")
@@ -701,8 +703,18 @@ def track_mode(args, rank, world, local_rank, dist):
     L = min(args.seq_len, B)
     if B % L:
         raise SystemExit(f"--batch {B} must be a multiple of --seq-len {L} (pair 0 links frame B-1 to frame 0)")
-    bgr_loop, dep_loop, gt_poses = synth.make_sequence(L, W, H, seed=scene_seed, closed_loop=True,
-                                                       hard=args.workload == "hard")
+    if args.tum:
+        # a real TUM sequence (associations.txt, utils.cpp:16-38): its first L
+        # frames, cycled through the batch like the synthetic loop (the wrap
+        # pair jumps back; no ground truth, so no ATE)
+        tum = load_module("arlm_amd_tum", os.path.join(PKG_DIR, "tum.py"))
+        bgr_loop, dep_loop, _ = tum.load_sequence(args.tum, L)
+        if bgr_loop.shape[0] < L or bgr_loop.shape[1:3] != (H, W):
+            raise SystemExit(f"--tum: need {L} frames of {W}x{H}, got {bgr_loop.shape}")
+        gt_poses = None
+    else:
+        bgr_loop, dep_loop, gt_poses = synth.make_sequence(L, W, H, seed=scene_seed, closed_loop=True,
+                                                           hard=args.workload == "hard")
     bgr, dep = bgr_loop[np.arange(B) % L], dep_loop[np.arange(B) % L]
     adaptive = args.detector in ("adaptive", "adaptive-orb")
     inner = "orb" if args.detector == "adaptive-orb" else "fast"
@@ -761,9 +773,10 @@ def track_mode(args, rank, world, local_rank, dist):
         step(False)
         odo.synchronize()
         recs = [ring.all[k][:fsm.batch_of(k, T, rank, world)[1]].copy() for k in range(2)]
-        G = shard.stitch(recs, [0, 1], G_start=np.linalg.inv(gt_poses[0]))
+        G = shard.stitch(recs, [0, 1], G_start=np.linalg.inv(gt_poses[0]) if gt_poses is not None else None)
         # ATE over rank 0's first loop (global frames 0 .. L-1 of step 0)
-        ate_mm = 1000.0 * tj.ate_rmse(tj.camera_centres(G[0][:L]), gt_poses[:L, :3, 3]) if rank == 0 else None
+        ate_mm = 1000.0 * tj.ate_rmse(tj.camera_centres(G[0][:L]), gt_poses[:L, :3, 3]) \
+            if rank == 0 and gt_poses is not None else None
         res_q = recs[-1][1:]  # a halo step: B genuine pairs, record p+1 = pair (frame p, frame p+1)
         pair_frame0 = 1       # batch frame of record 0 of res_q
 
@@ -793,8 +806,10 @@ def track_mode(args, rank, world, local_rank, dist):
         odo.synchronize()
         # quality sanity: the untimed first batch's chained poses against the
         # sequence's ground truth (absolute trajectory error, TUM definition)
-        Tcw = tj.chain_poses(res[:L], np.linalg.inv(gt_poses[0]).astype(np.float32))
-        ate_mm = 1000.0 * tj.ate_rmse(tj.camera_centres(Tcw), gt_poses[:L, :3, 3])
+        ate_mm = None
+        if gt_poses is not None:
+            Tcw = tj.chain_poses(res[:L], np.linalg.inv(gt_poses[0]).astype(np.float32))
+            ate_mm = 1000.0 * tj.ate_rmse(tj.camera_centres(Tcw), gt_poses[:L, :3, 3])
         # the headline: inputs resident in HBM
         elapsed, submit, (knn_ms, knn_launches) = timed_leg(
             odo, lambda i: odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=False),
@@ -935,7 +950,8 @@ def track_mode(args, rank, world, local_rank, dist):
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8/i32 (extract, match), f32+f64 (ransac, pnp)",
-            "data": "synthetic (ray-cast textured room, closed-loop trajectory; no dataset offline)",
+            "data": (f"TUM sequence {args.tum} (first {L} frames, cycled)" if args.tum else
+                     "synthetic (ray-cast textured room, closed-loop trajectory; no dataset offline)"),
             "inputs": "resident in HBM when the timed region starts (from_host: the same path from pinned host memory)",
             "config": {"workload": (f"cfg2 fr1/desk proxy {W}x{H}, {args.nfeatures} kp, RANSAC {args.iters}"
                                     + (" (hard variant)" if args.workload == "hard" else "")
@@ -951,7 +967,7 @@ def track_mode(args, rank, world, local_rank, dist):
                        "mean_matches": round(float(np.mean(ok["n_matches"])), 1),
                        "mean_ransac_inliers": round(float(np.mean(ok["n_inliers"])), 1),
                        "mean_ransac_visited": round(float(np.mean(ok["visited"])), 1),
-                       "ate_mm": round(ate_mm, 3)},
+                       "ate_mm": round(ate_mm, 3) if ate_mm is not None else None},
             "stage_ms": {k: round(v, 4) for k, v in timings.items()},
             "host_submit_ms_per_step": round(submit / K * 1e3, 3),
             "from_host": from_host,
