@@ -130,8 +130,9 @@ ODO_INLINE SE3 se3_exp(const double u[6]) {
                 V[i][j] = R[i][j];
             }
     } else {
-        double sn, cs;
-        sincos(theta, &sn, &cs);  // one reduction for both (g2o: sin(), cos())
+        // sin / cos as g2o calls them (the device sincos takes its outputs
+        // through private memory: measured 20 VGPRs of scratch spills)
+        const double sn = sin(theta), cs = cos(theta);
         const double th2 = theta * theta;
         // g2o divides by pow(theta, 3): theta * theta^2 differs in the last ulp
         // at most (PnP parity is a tolerance, 1e-4 on the pose)
@@ -387,7 +388,6 @@ ODO_INLINE void huber_rho(double delta, double chi, double rho[3]) {
 #define PNP_NW 4
 #define PNP_NT (64 * PNP_NW)
 #define PNP_K 4  // Levenberg trials evaluated per edge pass (one per 16-lane group of wave 0)
-#define PNP_EC 1024  // edges per pair staged in LDS for the passes (29 B each, 29 KB; the rest stream)
 static_assert(PNP_K <= 4, "the trial solves run on the four 16-lane groups of one wave");
 
 // Sum of NV per-lane doubles over the workgroup, the result in every lane.
@@ -495,6 +495,22 @@ ODO_INLINE void edge_build(const SE3M& T, const double Xw[3], const double ob[3]
     }
 }
 
+// robust (Huber) chi2 of one edge at the quaternion pose T (the chi pass keeps
+// four candidates live: 7 doubles each instead of a matrix's 12)
+ODO_INLINE double edge_robust_chi_q(const SE3& T, const double Xw[3], const double ob[3], double info, uint8_t fl,
+                                    const PnPCam& cam, double dMono, double dStereo, double& c2) {
+    const bool st = fl & PE_STEREO;
+    double Xc[3], e[3];
+    se3_map(T, Xw, Xc);
+    edge_err(Xc, ob, st, cam, e);
+    c2 = chi2_of(e, info, st);
+    if (fl & PE_ROBUST) {
+        double rr[3];
+        huber_rho(st ? dStereo : dMono, c2, rr);
+        return rr[0];
+    }
+    return c2;
+}
 // robust (Huber) chi2 of one edge at pose T; c2 = plain chi2 of the stored error
 ODO_INLINE double edge_robust_chi(const SE3M& T, const double Xw[3], const double ob[3], double info, uint8_t fl,
                                   const PnPCam& cam, double dMono, double dStereo, double& c2) {
@@ -540,8 +556,6 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
     __shared__ double s_T[PNP_K][8];
     __shared__ int s_ok[PNP_K];
     __shared__ int s_ne[PNP_NW];
-    __shared__ float s_eX[3][PNP_EC], s_eO[3][PNP_EC], s_eI[PNP_EC];
-    __shared__ uint8_t s_eF[PNP_EC];
     odo_pair_result* R = res + p;
     const int s1 = slot0 + p, s2 = slot0 + p + 1;
     const int n2 = nkp[s2];
@@ -595,20 +609,6 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
     }
     const PnPCam cam{(double)cal.fx, (double)cal.fy, (double)cal.cx, (double)cal.cy, (double)cal.mbf};
     const double dMono = (double)(float)sqrt(5.991), dStereo = (double)(float)sqrt(7.815);  // pnpsolver.cpp:51-52
-    // the first PNP_EC edges staged in LDS once (SoA), read by every pass
-    // (their flags are updated there); edges past PNP_EC stream from the
-    // pair's scratch
-    const int nec = min(ne, PNP_EC);
-    for (int k = lane; k < nec; k += PNP_NT) {
-#pragma unroll
-        for (int c = 0; c < 3; c++) {
-            s_eX[c][k] = E.X[3 * k + c];
-            s_eO[c][k] = E.obs[3 * k + c];
-        }
-        s_eI[k] = E.info[k];
-        s_eF[k] = E.flags[k];
-    }
-    __syncthreads();
     SE3 T0s;
     {
         double R0[3][3], t0[3];
@@ -645,14 +645,7 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
             for (int k = 0; k < 28; k++) acc[k] = 0;
             {
                 const SE3M Tm = se3_mat(T);
-                for (int k = lane; k < nec; k += PNP_NT) {
-                    const uint8_t fl = s_eF[k];
-                    if (fl & PE_OUT) continue;
-                    const double Xw[3] = {s_eX[0][k], s_eX[1][k], s_eX[2][k]};
-                    const double ob[3] = {s_eO[0][k], s_eO[1][k], s_eO[2][k]};
-                    edge_build(Tm, Xw, ob, (double)s_eI[k], fl, cam, dMono, dStereo, acc);
-                }
-                for (int k = lane + nec; k < ne; k += PNP_NT) {
+                for (int k = lane; k < ne; k += PNP_NT) {
                     const uint8_t fl = E.flags[k];
                     if (fl & PE_OUT) continue;
                     const double Xw[3] = {E.X[3 * k], E.X[3 * k + 1], E.X[3 * k + 2]};
@@ -747,50 +740,37 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                     }
                 }
                 __syncthreads();
+                SE3 Tc[PNP_K];
                 double sc[PNP_K];
                 bool okc[PNP_K];
 #pragma unroll
                 for (int k = 0; k < PNP_K; k++) {
+                    Tc[k].q = Quat{s_T[k][0], s_T[k][1], s_T[k][2], s_T[k][3]};
+                    Tc[k].t[0] = s_T[k][4];
+                    Tc[k].t[1] = s_T[k][5];
+                    Tc[k].t[2] = s_T[k][6];
                     sc[k] = s_T[k][7];
                     okc[k] = s_ok[k] != 0;
                 }
                 PP_ACC(tsol);
                 PP_T0();
-                // computeActiveErrors + activeRobustChi2 at every candidate,
-                // candidate by candidate (one pose matrix live at a time) over
-                // the register-held edges
+                // computeActiveErrors + activeRobustChi2 at every candidate
                 double chi[PNP_K];
 #pragma unroll
                 for (int k = 0; k < PNP_K; k++) chi[k] = 0;
-                for (int k = 0; k < K; k++) {
-                    SE3 Tk;
-                    Tk.q = Quat{s_T[k][0], s_T[k][1], s_T[k][2], s_T[k][3]};
-                    Tk.t[0] = s_T[k][4];
-                    Tk.t[1] = s_T[k][5];
-                    Tk.t[2] = s_T[k][6];
-                    const SE3M Tm = se3_mat(Tk);
-                    double ck = 0;
-                    for (int e = lane; e < nec; e += PNP_NT) {
-                        const uint8_t fl = s_eF[e];
-                        if (fl & PE_OUT) continue;
-                        const double Xw[3] = {s_eX[0][e], s_eX[1][e], s_eX[2][e]};
-                        const double ob[3] = {s_eO[0][e], s_eO[1][e], s_eO[2][e]};
-                        double c2;
-                        ck += edge_robust_chi(Tm, Xw, ob, (double)s_eI[e], fl, cam, dMono, dStereo, c2);
-                        E.chi4[4 * e + k] = c2;
-                    }
-                    for (int e = lane + nec; e < ne; e += PNP_NT) {
-                        const uint8_t fl = E.flags[e];
-                        if (fl & PE_OUT) continue;
-                        const double Xw[3] = {E.X[3 * e], E.X[3 * e + 1], E.X[3 * e + 2]};
-                        const double ob[3] = {E.obs[3 * e], E.obs[3 * e + 1], E.obs[3 * e + 2]};
-                        double c2;
-                        ck += edge_robust_chi(Tm, Xw, ob, (double)E.info[e], fl, cam, dMono, dStereo, c2);
-                        E.chi4[4 * e + k] = c2;
-                    }
+                for (int e = lane; e < ne; e += PNP_NT) {
+                    const uint8_t fl = E.flags[e];
+                    if (fl & PE_OUT) continue;
+                    const double Xw[3] = {E.X[3 * e], E.X[3 * e + 1], E.X[3 * e + 2]};
+                    const double ob[3] = {E.obs[3 * e], E.obs[3 * e + 1], E.obs[3 * e + 2]};
+                    const double info = E.info[e];
 #pragma unroll
-                    for (int q = 0; q < PNP_K; q++)
-                        if (q == k) chi[q] = ck;
+                    for (int k = 0; k < PNP_K; k++) {
+                        if (k >= K) break;
+                        double c2;
+                        chi[k] += edge_robust_chi_q(Tc[k], Xw, ob, info, fl, cam, dMono, dStereo, c2);
+                        E.chi4[4 * e + k] = c2;
+                    }
                 }
                 wg_sum<PNP_K>(chi, red);
                 PP_ACC(tchi);
@@ -814,10 +794,7 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                         lambda = lam[k] * sf;
                         ni = 2;
                         curChi = tempChi;
-                        T.q = Quat{s_T[k][0], s_T[k][1], s_T[k][2], s_T[k][3]};
-                        T.t[0] = s_T[k][4];
-                        T.t[1] = s_T[k][5];
-                        T.t[2] = s_T[k][6];
+                        T = Tc[k];
                         trials_done = true;
                     } else {
                         lambda = lam[k] * nis[k];  // T stays at the backup
@@ -856,12 +833,7 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                 E.flags[k] = (uint8_t)fl;
                 return fl;
             };
-            for (int k = lane; k < nec; k += PNP_NT) {
-                const double Xw[3] = {s_eX[0][k], s_eX[1][k], s_eX[2][k]};
-                const double ob[3] = {s_eO[0][k], s_eO[1][k], s_eO[2][k]};
-                s_eF[k] = (uint8_t)classify(k, s_eF[k], Xw, ob, (double)s_eI[k]);
-            }
-            for (int k = lane + nec; k < ne; k += PNP_NT) {
+            for (int k = lane; k < ne; k += PNP_NT) {
                 const double Xw[3] = {E.X[3 * k], E.X[3 * k + 1], E.X[3 * k + 2]};
                 const double ob[3] = {E.obs[3 * k], E.obs[3 * k + 1], E.obs[3 * k + 2]};
                 classify(k, E.flags[k], Xw, ob, (double)E.info[k]);
