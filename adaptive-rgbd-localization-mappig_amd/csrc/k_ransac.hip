@@ -1091,7 +1091,14 @@ __global__ void __launch_bounds__(64 * EV_WAVES, EV_MIN_BLOCKS) k_ransac_eval_li
 // of the pair from the pair's counter, so lanes never idle while the pair has
 // hypotheses left. Inlier sets live in a per-wave global slab ([2][words][64],
 // coalesced), swapped on accept.
+ODO_INLINE double readlane_d(double v, int l) {
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
 #define LN_WAVES 4
+#define LN_RS 33  // LDS row stride (doubles) of the parked terms
 __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B, RansacCfg cfg, uint32_t* lane_slab,
                                                                    int waves_total, int min_open) {
     __builtin_amdgcn_s_setprio(ODO_WAVE_PRIO);
@@ -1102,9 +1109,12 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
     // per lane, then wave-uniform broadcast reads in point order
     __shared__ GoodPt s_pts[LN_WAVES][64];
     GoodPt* lp = s_pts[wv];
-    // the sweep's parked Mahalanobis terms: [active slot][32 points], and the
-    // active lanes in slot order
-    __shared__ double s_res[LN_WAVES][64 * 32];
+    // the sweep's parked Mahalanobis terms: [active slot][32 points, row
+    // stride LN_RS], and the active lanes in slot order. Every active lane then
+    // reads its own row in point order: with a 32-double stride all 64 lanes
+    // would hit one bank pair (a 32-way conflict per ds_read_b64 half); 33
+    // puts lane r's row on banks 2r, 2r + 1
+    __shared__ double s_res[LN_WAVES][64 * LN_RS];
     __shared__ int s_la[LN_WAVES][64];
     double* lres = s_res[wv];
     int* la = s_la[wv];
@@ -1226,11 +1236,14 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
                 const float x1[3] = {g.sx, g.sy, g.sz}, x2[3] = {g.tx, g.ty, g.tz};
                 for (int i = 0; i < nact; i += 2) {
                     const int a = i + hf;  // this half's hypothesis slot
-                    const int src0 = la[i], src1 = la[min(i + 1, nact - 1)];
+                    // the two hypotheses' lanes are wave-uniform: v_readlane into
+                    // scalars instead of an LDS-routed shuffle per element
+                    const int src0 = __builtin_amdgcn_readfirstlane(la[i]);
+                    const int src1 = __builtin_amdgcn_readfirstlane(la[min(i + 1, nact - 1)]);
                     double Ta[12];
 #pragma unroll
                     for (int q = 0; q < 12; q++) {
-                        const double t0 = __shfl(Td[q], src0), t1 = __shfl(Td[q], src1);
+                        const double t0 = readlane_d(Td[q], src0), t1 = readlane_d(Td[q], src1);
                         Ta[q] = hf ? t1 : t0;
                     }
                     double d = -1.0;  // not an inlier
@@ -1238,14 +1251,14 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
                         const double e = error_function2(x1, x2, Ta, K);
                         if (!(e > th) && (e >= 0.0)) d = e;
                     }
-                    if (a < nact) lres[a * 32 + pj] = d;
+                    if (a < nact) lres[a * LN_RS + pj] = d;
                 }
                 wave_sync();
                 uint32_t word = 0;
                 if (act) {
                     const int nj = min(32, ng - c0);
                     for (int j = 0; j < nj; j++) {
-                        const double v = lres[rank * 32 + j];
+                        const double v = lres[rank * LN_RS + j];
                         if (v >= 0.0) {
                             meanError += v;
                             c++;
