@@ -285,14 +285,19 @@ ODO_INLINE double error_function2(const float x1[3], const float x2[3], const do
     const double R10 = T[4], R11 = T[5], R12 = T[6];
     const double R20 = T[8], R21 = T[9], R22 = T[10];
     const double c00 = K.raster_cov_x * a2, c11 = K.raster_cov_y * a2, c22 = K.depth_cov;
-    // RtC[i][j] = R[0][i]*C[0][j] + (R[1][i]*C[1][j] + R[2][i]*C[2][j]), C diagonal
+    // Eigen's RtC[i][j] = R[0][i]*C[0][j] + (R[1][i]*C[1][j] + R[2][i]*C[2][j])
+    // with C diagonal is R[j][i]*C[j][j] plus two exact zeros. Adding them
+    // changes at most the sign of an exact-zero RtC entry, and every A below
+    // adds +0.0 or a positive covariance after the products, so A (and the
+    // result) is bit-identical; for a non-finite R the point is rejected either
+    // way (its delta is not finite). 9 products instead of 27 + 18 adds.
     const double R[3][3] = {{R00, R01, R02}, {R10, R11, R12}, {R20, R21, R22}};
-    const double C[3][3] = {{c00, 0.0, 0.0}, {0.0, c11, 0.0}, {0.0, 0.0, c22}};
+    const double Cd[3] = {c00, c11, c22};
     double RtC[3][3];
 #pragma unroll
     for (int i = 0; i < 3; i++)
 #pragma unroll
-        for (int j = 0; j < 3; j++) RtC[i][j] = sum3d(R[0][i] * C[0][j], R[1][i] * C[1][j], R[2][i] * C[2][j]);
+        for (int j = 0; j < 3; j++) RtC[i][j] = R[j][i] * Cd[j];
     // lower triangle of C1 = RtC * R, plus cov2 (diagonal)
     const double cov2_0 = K.raster_cov_x * mu2, cov2_1 = K.raster_cov_y * mu2, cov2_2 = K.depth_cov;
     double A00 = sum3d(RtC[0][0] * R00, RtC[0][1] * R10, RtC[0][2] * R20) + cov2_0;
