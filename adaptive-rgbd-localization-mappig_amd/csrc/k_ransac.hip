@@ -1674,7 +1674,11 @@ void launch_ransac(hipStream_t st, const void* good, const int* n_good, const in
         const char* e = odo_knob("ODO_EV_ROWS0");
         return e ? std::max(1, atoi(e)) : EV_ROWS0;
     }();
-    const int r0 = std::min(rows, rows0);
+    // a lone pair (the per-stage odo_ransac, a one-frame batch) starts every
+    // hypothesis at once: the device is otherwise idle, and the visited
+    // hypotheses beyond the first row no longer wait for the first launch
+    // (the fold and the aborts make the result independent of the schedule)
+    const int r0 = npairs == 1 ? rows : std::min(rows, rows0);
     cfg.rows0 = r0;
     if (part != 2) {
         hipLaunchKernelGGL(k_ransac_prep, dim3(npairs), dim3(256), 0, st, B, cfg);

@@ -180,6 +180,11 @@ struct odo_ctx {
     // stream): the caller's depth buffer is in use until this event
     hipEvent_t ev_depth_done = nullptr;
     bool depth_busy = false;
+    // page-locked staging of the per-stage (synchronous) entry points: their
+    // inputs are packed here and uploaded with one DMA, their outputs come
+    // back here with async copies into pinned memory and one sync
+    uint8_t* stage_h = nullptr;
+    size_t stage_cap = 0;
     int in_next = 0;
     // pair buffers ([maxb])
     int2 *knn_idx[NSETS] = {}, *knn_dist[NSETS] = {};  // per frame set
@@ -322,6 +327,35 @@ static int pair_stream_priority() {
     return greatest;
 }
 
+// Packed layout in the staging buffer: 256-byte aligned sections
+struct Pack {
+    size_t off = 0;
+    size_t add(size_t bytes) {
+        const size_t o = off;
+        off = (off + bytes + 255) & ~(size_t)255;
+        return o;
+    }
+};
+// a typed view of a section of a packed device buffer
+struct DevView {
+    uint8_t* p;
+    template <typename T>
+    T* as() const {
+        return reinterpret_cast<T*>(p);
+    }
+};
+static int stage_reserve(odo_ctx* c, size_t bytes) {
+    if (bytes <= c->stage_cap) return ODO_OK;
+    size_t cap = std::max(bytes, std::max(c->stage_cap * 2, (size_t)1 << 20));
+    if (c->stage_h) (void)hipHostFree(c->stage_h);
+    c->stage_h = nullptr;
+    c->stage_cap = 0;
+    if (hipHostMalloc((void**)&c->stage_h, cap, hipHostMallocDefault) != hipSuccess)
+        return fail(ODO_ERR_DEVICE, "hipHostMalloc (staging) failed");
+    c->stage_cap = cap;
+    return ODO_OK;
+}
+
 static int sync_all(odo_ctx* c) {
     for (hipStream_t st : c->owned) HIPCHK(hipStreamSynchronize(st));
     c->depth_busy = false;
@@ -371,6 +405,7 @@ static void free_ctx(odo_ctx* c) {
     }
     if (c->ev_latch) hipEventDestroy(c->ev_latch);
     if (c->ev_depth_done) hipEventDestroy(c->ev_depth_done);
+    if (c->stage_h) (void)hipHostFree(c->stage_h);
     for (hipStream_t st : c->owned) hipStreamDestroy(st);
     if (c->h_open) (void)hipHostFree(c->h_open);
     delete c;
@@ -1591,16 +1626,32 @@ int odo_get_frame(odo_ctx* c, int i, orb_kp* kps, uint8_t* desc, float* kps_un, 
     if ((e = sync_all(c))) return e;
     // frame i of the last batch: slot i+1 of its frame set
     const size_t slot = fbase(c, c->view_set) + i + 1;
-    int cnt = 0;
-    HIPCHK(hipMemcpy(&cnt, c->nkp + slot, sizeof(int), hipMemcpyDeviceToHost));
-    *n = cnt;
-    const int m = std::min(cnt, cap);
+    // every array at its full capacity (no round trip for the count first):
+    // async copies into the pinned staging buffer, one sync, then the
+    // caller's buffers
     const size_t KC = (size_t)c->kp_cap;
-    if (kps) HIPCHK(hipMemcpy(kps, c->kps + slot * KC, m * sizeof(orb_kp), hipMemcpyDeviceToHost));
-    if (desc) HIPCHK(hipMemcpy(desc, c->desc + slot * KC * 32, (size_t)m * 32, hipMemcpyDeviceToHost));
-    if (kps_un) HIPCHK(hipMemcpy(kps_un, c->kun + slot * KC * 2, (size_t)m * 8, hipMemcpyDeviceToHost));
-    if (xyz) HIPCHK(hipMemcpy(xyz, c->xyz + slot * KC * 3, (size_t)m * 12, hipMemcpyDeviceToHost));
-    if (u_right) HIPCHK(hipMemcpy(u_right, c->ur + slot * KC, (size_t)m * 4, hipMemcpyDeviceToHost));
+    Pack pk;
+    const size_t o_n = pk.add(sizeof(int)), o_k = pk.add(KC * sizeof(orb_kp)), o_d = pk.add(KC * 32),
+                 o_u = pk.add(KC * 8), o_x = pk.add(KC * 12), o_r = pk.add(KC * 4);
+    if ((e = stage_reserve(c, pk.off))) return e;
+    uint8_t* h = c->stage_h;
+    hipStream_t st = c->stream;
+    HIPCHK(hipMemcpyAsync(h + o_n, c->nkp + slot, sizeof(int), hipMemcpyDeviceToHost, st));
+    if (kps) HIPCHK(hipMemcpyAsync(h + o_k, c->kps + slot * KC, KC * sizeof(orb_kp), hipMemcpyDeviceToHost, st));
+    if (desc) HIPCHK(hipMemcpyAsync(h + o_d, c->desc + slot * KC * 32, KC * 32, hipMemcpyDeviceToHost, st));
+    if (kps_un) HIPCHK(hipMemcpyAsync(h + o_u, c->kun + slot * KC * 2, KC * 8, hipMemcpyDeviceToHost, st));
+    if (xyz) HIPCHK(hipMemcpyAsync(h + o_x, c->xyz + slot * KC * 3, KC * 12, hipMemcpyDeviceToHost, st));
+    if (u_right) HIPCHK(hipMemcpyAsync(h + o_r, c->ur + slot * KC, KC * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    int cnt = 0;
+    memcpy(&cnt, h + o_n, sizeof(int));
+    *n = cnt;
+    const int m = std::max(0, std::min(cnt, cap));
+    if (kps) memcpy(kps, h + o_k, (size_t)m * sizeof(orb_kp));
+    if (desc) memcpy(desc, h + o_d, (size_t)m * 32);
+    if (kps_un) memcpy(kps_un, h + o_u, (size_t)m * 8);
+    if (xyz) memcpy(xyz, h + o_x, (size_t)m * 12);
+    if (u_right) memcpy(u_right, h + o_r, (size_t)m * 4);
     return cnt > cap ? fail(ODO_ERR_CAPACITY, "cap too small") : ODO_OK;
 }
 
@@ -1999,13 +2050,23 @@ int odo_knn2_hamming(odo_ctx* c, const uint8_t* q, int nq, const uint8_t* t, int
     hipStream_t st = c->stream;
     DevArena& A = c->arena;
     A.begin();
-    DevBuf dq(A, (size_t)nq * 32), dt(A, (size_t)std::max(nt, 1) * 32), dn(A, 2 * sizeof(int));
-    DevBuf di(A, (size_t)nq * sizeof(int2)), dd(A, (size_t)nq * sizeof(int2));
+    // one packed upload (descriptors + counts) and one packed download
+    Pack pk;
+    const size_t o_q = pk.add((size_t)nq * 32), o_t = pk.add((size_t)std::max(nt, 1) * 32), o_n = pk.add(2 * sizeof(int));
+    const size_t in_bytes = pk.off;
+    const size_t o_i = pk.add((size_t)nq * sizeof(int2)), o_d = pk.add((size_t)nq * sizeof(int2));
+    int e;
+    if ((e = stage_reserve(c, pk.off))) return e;
+    DevBuf dall(A, pk.off);
     ARENA_CHECK(A);
+    uint8_t* h = c->stage_h;
+    memcpy(h + o_q, q, (size_t)nq * 32);
+    if (nt) memcpy(h + o_t, t, (size_t)nt * 32);
     const int cnt[2] = {nq, nt};
-    HIPCHK(hipMemcpyAsync(dq.p, q, (size_t)nq * 32, hipMemcpyHostToDevice, st));
-    if (nt) HIPCHK(hipMemcpyAsync(dt.p, t, (size_t)nt * 32, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(dn.p, cnt, sizeof(cnt), hipMemcpyHostToDevice, st));
+    memcpy(h + o_n, cnt, sizeof(cnt));
+    HIPCHK(hipMemcpyAsync(dall.p, h, in_bytes, hipMemcpyHostToDevice, st));
+    uint8_t* db = dall.as<uint8_t>();
+    const DevView dq{db + o_q}, dt{db + o_t}, dn{db + o_n}, di{db + o_i}, dd{db + o_d};
     if (c->knn_mx && nt <= 8192)  // the packed key holds a 13-bit train index
         launch_knn2_mx(st, dq.as<uint8_t>(), dn.as<int>(), 0, dt.as<uint8_t>(), dn.as<int>() + 1, 0, di.as<int2>(),
                        dd.as<int2>(), 0, nq, 1, nullptr, nullptr, 0, c->knn_mx);
@@ -2013,9 +2074,10 @@ int odo_knn2_hamming(odo_ctx* c, const uint8_t* q, int nq, const uint8_t* t, int
         launch_knn2(st, dq.as<uint8_t>(), dn.as<int>(), 0, dt.as<uint8_t>(), dn.as<int>() + 1, 0, di.as<int2>(),
                     dd.as<int2>(), 0, nq, 1);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(idx, di.p, (size_t)nq * 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(dist, dd.p, (size_t)nq * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(h + o_i, db + o_i, pk.off - o_i, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    memcpy(idx, h + o_i, (size_t)nq * 8);
+    memcpy(dist, h + o_d, (size_t)nq * 8);
     return ODO_OK;
 }
 
@@ -2066,40 +2128,53 @@ int odo_ransac(odo_ctx* c, const odo_dmatch* m12, int n12, const float* xyz1, in
     const int words = (ng + 31) / 32;
     DevArena& A = c->arena;
     A.begin();
-    DevBuf dxyz(A, (size_t)2 * kc * 3 * sizeof(float)), dm(A, (size_t)ng * sizeof(odo_dmatch)), dg(A, (size_t)ng * 8);
-    DevBuf dint(A, 4 * sizeof(int)), dlatch(A, sizeof(double)), drng(A, sizeof(odo_rng)),
-        dres(A, sizeof(odo_pair_result));
     const double cam_angle_x = 58.0 / 180.0 * M_PI, cam_angle_y = 45.0 / 180.0 * M_PI;
     const double rsx = 3 * tan(cam_angle_x / 640.0), rsy = 3 * tan(cam_angle_y / 480.0);
     RansacCfg cfg{p->iterations, p->min_inlier_th, p->max_mahalanobis, p->sample_size, p->check_depth, rsx * rsx,
                   rsy * rsy};
-    DevBuf dT(A, 16 * sizeof(float)), dgp(A, ransac_scratch_bytes(1, ng, words, cfg)), dbm(A, (size_t)words * 4);
+    // inputs packed into the pinned staging buffer, one upload; the outputs
+    // (result record, inlier mask, rand() state) are adjacent, one download
+    Pack pk;
+    const size_t o_xyz = pk.add((size_t)2 * kc * 12), o_m = pk.add((size_t)ng * sizeof(odo_dmatch)),
+                 o_g = pk.add((size_t)ng * 8), o_int = pk.add(4 * sizeof(int)), o_latch = pk.add(sizeof(double));
+    const size_t o_rng = pk.add(sizeof(odo_rng));
+    const size_t in_bytes = pk.off;
+    const size_t o_res = pk.add(sizeof(odo_pair_result)), o_bm = pk.add((size_t)words * 4);
+    const size_t all_bytes = pk.off;
+    int e0;
+    if ((e0 = stage_reserve(c, all_bytes))) return e0;
+    DevBuf dall(A, all_bytes), dT(A, 16 * sizeof(float)), dgp(A, ransac_scratch_bytes(1, ng, words, cfg));
     ARENA_CHECK(A);
-    std::vector<uint64_t> gl(ng);
+    uint8_t* h = c->stage_h;
+    memcpy(h + o_xyz, xyz1, (size_t)n1 * 12);
+    memcpy(h + o_xyz + (size_t)kc * 12, xyz2, (size_t)n2 * 12);
+    memcpy(h + o_m, good.data(), (size_t)ng * sizeof(odo_dmatch));
+    uint64_t* gl = reinterpret_cast<uint64_t*>(h + o_g);
     for (int k = 0; k < ng; k++) {
         uint32_t bits;
         memcpy(&bits, &good[k].distance, 4);
         gl[k] = ((uint64_t)(uint32_t)k << 32) | bits;
     }
     const int ints[4] = {ng, ng, 1, 0};  // n_good, n_matches, pair_valid
-    HIPCHK(hipMemcpyAsync(dxyz.p, xyz1, (size_t)n1 * 12, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(dxyz.as<float>() + (size_t)kc * 3, xyz2, (size_t)n2 * 12, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(dm.p, good.data(), (size_t)ng * sizeof(odo_dmatch), hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(dg.p, gl.data(), (size_t)ng * 8, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(dint.p, ints, sizeof(ints), hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(dlatch.p, latch, sizeof(double), hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(drng.p, rng, sizeof(odo_rng), hipMemcpyHostToDevice, st));
+    memcpy(h + o_int, ints, sizeof(ints));
+    memcpy(h + o_latch, latch, sizeof(double));
+    memcpy(h + o_rng, rng, sizeof(odo_rng));
+    HIPCHK(hipMemcpyAsync(dall.p, h, in_bytes, hipMemcpyHostToDevice, st));
+    uint8_t* db = dall.as<uint8_t>();
+    const DevView dxyz{db + o_xyz}, dm{db + o_m}, dg{db + o_g}, dint{db + o_int}, dlatch{db + o_latch},
+        drng{db + o_rng}, dres{db + o_res}, dbm{db + o_bm};
     launch_ransac_raw(st, dgp.p, 1, ng, words, cfg, 0, 0, drng.as<odo_rng>());
     launch_ransac(st, dg.p, dint.as<int>(), dint.as<int>() + 1, dm.as<odo_dmatch>(), dxyz.as<float>(), kc, 0, ng, cfg,
                   dlatch.as<double>(), dint.as<int>() + 2, 0, drng.as<odo_rng>(), dgp.p, dbm.as<uint32_t>(),
                   words, dres.as<odo_pair_result>(), dT.as<float>(), 1);
     HIPCHK(hipGetLastError());
-    odo_pair_result r;
-    std::vector<uint32_t> bm(words);
-    HIPCHK(hipMemcpyAsync(&r, dres.p, sizeof(r), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(bm.data(), dbm.p, (size_t)words * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(rng, drng.p, sizeof(odo_rng), hipMemcpyDeviceToHost, st));
+    // rng (updated in place) .. the mask: one contiguous download
+    HIPCHK(hipMemcpyAsync(h + o_rng, db + o_rng, all_bytes - o_rng, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    odo_pair_result r;
+    memcpy(&r, h + o_res, sizeof(r));
+    memcpy(rng, h + o_rng, sizeof(odo_rng));
+    const uint32_t* bm = reinterpret_cast<const uint32_t*>(h + o_bm);
     memcpy(T12, r.T12, sizeof(r.T12));
     *rmse = r.rmse;
     int k2 = 0;
@@ -2266,12 +2341,23 @@ int odo_pnp_motion_ba(odo_ctx* c, const float* Xw, const float* obs, int n, cons
     const int kc = std::max(n, 1);
     DevArena& A = c->arena;
     A.begin();
-    DevBuf dx(A, (size_t)kc * 12), dkun(A, (size_t)2 * kc * 8), dur(A, (size_t)2 * kc * 4), dsrc(A, (size_t)kc * 4);
-    DevBuf dint(A, 4 * sizeof(int)), dT(A, 16 * 4), dres(A, sizeof(odo_pair_result)),
-        dedges(A, (size_t)kc * pnp_edge_bytes()), dmask(A, (size_t)kc);
+    // inputs packed into the pinned staging buffer, one upload; the result
+    // record and the inlier mask adjacent, one download
+    Pack pk;
+    const size_t o_x = pk.add((size_t)kc * 12), o_kun = pk.add((size_t)2 * kc * 8), o_ur = pk.add((size_t)2 * kc * 4),
+                 o_src = pk.add((size_t)kc * 4), o_int = pk.add(4 * sizeof(int)), o_T = pk.add(16 * 4);
+    const size_t in_bytes = pk.off;
+    const size_t o_res = pk.add(sizeof(odo_pair_result)), o_mask = pk.add((size_t)kc);
+    const size_t all_bytes = pk.off;
+    int e0;
+    if ((e0 = stage_reserve(c, all_bytes))) return e0;
+    DevBuf dall(A, all_bytes), dedges(A, (size_t)kc * pnp_edge_bytes());
     ARENA_CHECK(A);
-    std::vector<float> kun(2 * kc), ur(kc);
-    std::vector<int32_t> src(kc);
+    uint8_t* h = c->stage_h;
+    float* kun = reinterpret_cast<float*>(h + o_kun) + 2 * kc;  // slot 1 of the two-slot layout
+    float* ur = reinterpret_cast<float*>(h + o_ur) + kc;
+    int32_t* src = reinterpret_cast<int32_t*>(h + o_src);
+    if (n) memcpy(h + o_x, Xw, (size_t)n * 12);
     for (int i = 0; i < n; i++) {
         kun[2 * i] = obs[3 * i];
         kun[2 * i + 1] = obs[3 * i + 1];
@@ -2279,25 +2365,23 @@ int odo_pnp_motion_ba(odo_ctx* c, const float* Xw, const float* obs, int n, cons
         src[i] = i;
     }
     const int ints[4] = {0, n, 1, 1 << 30};  // nkp[slot0], nkp[slot1], pair_valid, n_matches
-    if (n) {
-        HIPCHK(hipMemcpyAsync(dx.p, Xw, (size_t)n * 12, hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemcpyAsync(dkun.as<float>() + 2 * kc, kun.data(), (size_t)n * 8, hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemcpyAsync(dur.as<float>() + kc, ur.data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemcpyAsync(dsrc.p, src.data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
-    }
-    HIPCHK(hipMemcpyAsync(dint.p, ints, sizeof(ints), hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(dT.p, Tcw_init, 64, hipMemcpyHostToDevice, st));
+    memcpy(h + o_int, ints, sizeof(ints));
+    memcpy(h + o_T, Tcw_init, 64);
+    HIPCHK(hipMemcpyAsync(dall.p, h, in_bytes, hipMemcpyHostToDevice, st));
+    uint8_t* db = dall.as<uint8_t>();
+    const DevView dx{db + o_x}, dkun{db + o_kun}, dur{db + o_ur}, dsrc{db + o_src}, dint{db + o_int}, dT{db + o_T},
+        dres{db + o_res}, dmask{db + o_mask};
     const odo_calib& k = calib ? *calib : c->cfg.calib;
     FrameCalib cal{k.fx, k.fy, k.cx, k.cy, k.k1, k.k2, k.p1, k.p2, k.k3, k.depth_factor, k.mbf, 1.0f / k.fx, 1.0f / k.fy};
     launch_pnp(st, dsrc.as<int32_t>(), dx.as<float>(), dkun.as<float>(), dur.as<float>(), dint.as<int>(), kc, 0, cal,
                dT.as<float>(), dint.as<int>() + 2, dint.as<int>() + 3, 0, dedges.p, dres.as<odo_pair_result>(),
                dmask.as<uint8_t>(), 1);
     HIPCHK(hipGetLastError());
-    odo_pair_result r;
-    std::vector<uint8_t> mask(kc);
-    HIPCHK(hipMemcpyAsync(&r, dres.p, sizeof(r), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(mask.data(), dmask.p, kc, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(h + o_res, db + o_res, all_bytes - o_res, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    odo_pair_result r;
+    memcpy(&r, h + o_res, sizeof(r));
+    const uint8_t* mask = h + o_mask;
     memcpy(Tcw_out, r.Tcw, 64);
     *n_inliers = r.pnp_inliers;
     if (outlier)
