@@ -252,18 +252,22 @@ private:
 class Frame {
 public:
     // Frame(imColor, imDepth, timestamp) (frame.cpp:18-60): BGR8 + depth16
-    // (x5000, Calibration::mDepthFactor). The images are copied.
+    // (x5000, Calibration::mDepthFactor). The reference converts the images
+    // into members here (cvtColor / convertTo) for ExtractFeatures; the GPU
+    // does both conversions, so the frame only refers to the caller's images,
+    // which must stay valid until ExtractFeatures (Tracking::Track calls it
+    // right after construction, tracking.cpp:41), and forgets them there.
     Frame(const uint8_t* bgr, const uint16_t* depth, int width, int height, double timestamp)
-        : mTimestamp(timestamp), mW(width), mH(height), mImColor(bgr, bgr + (size_t)width * height * 3),
-          mImDepth(depth ? std::vector<uint16_t>(depth, depth + (size_t)width * height) : std::vector<uint16_t>()),
-          mTcw(Identity()) {}
+        : mTimestamp(timestamp), mW(width), mH(height), mImColor(bgr), mImDepth(depth), mTcw(Identity()) {}
 
     // Frame::ExtractFeatures (frame.cpp:135-170): Extract + UndistortKeyPoints +
     // depth backprojection (mvKeys3Dc, mvuRight), landmark slots reset.
     void ExtractFeatures(Extractor* pExtractor) {
+        if (!mImColor) throw std::logic_error("odo_hip::Frame::ExtractFeatures: the frame's images were already used");
         std::vector<float> kun, xyz;
-        pExtractor->ExtractFrame(mImColor.data(), mW, mH, 3, mImDepth.empty() ? nullptr : mImDepth.data(), mvKeys,
-                                 mDescriptors, kun, xyz, mvuRight);
+        pExtractor->ExtractFrame(mImColor, mW, mH, 3, mImDepth, mvKeys, mDescriptors, kun, xyz, mvuRight);
+        mImColor = nullptr;
+        mImDepth = nullptr;
         N = mvKeys.size();
         mvKeysUn = mvKeys;
         mvKeys3Dc.resize(N);
@@ -312,8 +316,8 @@ public:
 
 private:
     int mW, mH;
-    std::vector<uint8_t> mImColor;
-    std::vector<uint16_t> mImDepth;
+    const uint8_t* mImColor;    // the caller's BGR8 image, until ExtractFeatures
+    const uint16_t* mImDepth;   // the caller's depth16 image (or null), until ExtractFeatures
 
 public:
     Pose mTcw;
