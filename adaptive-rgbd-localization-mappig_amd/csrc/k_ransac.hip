@@ -739,6 +739,12 @@ ODO_INLINE GoodPt load_pt(const GoodPt* P, int k) {
     return P[k];
 }
 
+#ifdef ODO_RANSAC_PROFILE
+#define RPROF_MAX 4096
+__device__ uint64_t g_rprof[RPROF_MAX * 8];
+__device__ uint64_t g_rprof_done;
+#endif
+
 // Ordered fold of finished hypotheses (ransac.cpp:233-249), lane 0 only.
 // Whoever completes the visited prefix folds it; a wave that finds the lock
 // taken leaves, the holder re-checks after releasing it.
@@ -792,11 +798,136 @@ ODO_INLINE void try_fold(const RansacBufs& B, const RansacCfg& cfg, int p) {
         st_relaxed(&S->best_h, best_h);
         st_relaxed(reinterpret_cast<int*>(&S->rmse), __float_as_int(rmse));
         if (fin) st_relaxed(&S->done, 1);
+#ifdef ODO_RANSAC_PROFILE
+        if (fin) g_rprof_done = wall_clock64();
+#endif
         __threadfence();
         atomicExch(&S->lock, 0);
         __threadfence();
         if (fin) return;
         if (!__hip_atomic_load(&ready[pos], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) return;
+    }
+}
+
+// The same fold run by a whole wave (uniform control flow): the ready flags
+// and results of the next 64 hypotheses are loaded at once, one vector load
+// each, and the serial fold steps over the ready run read them with
+// v_readlane — instead of four dependent coherent loads per hypothesis (a
+// visited-to-the-end pair folds 500 of them: 215 us of serial loads at ~0.43
+// us each, longer than every hypothesis' evaluation). A holder re-checks the
+// next ready flag after releasing the lock; a finisher whose flag it still
+// missed leaves the rest to k_ransac_final, which completes the fold.
+ODO_INLINE int rdl(int v, int i) { return __builtin_amdgcn_readlane(v, i); }
+ODO_INLINE void try_fold_wave(const RansacBufs& B, const RansacCfg& cfg, int p, int lane) {
+    RState* S = B.st + p;
+    int* ready = B.ready + (size_t)p * B.hcap;
+    const HypRes* hyp = B.hyp + (size_t)p * B.hcap;
+    const unsigned minInl = (unsigned)cfg.min_inlier_th;
+    while (true) {
+        int got = 0;
+        if (lane == 0) got = atomicCAS(&S->lock, 0, 1) == 0;
+        if (!__builtin_amdgcn_readfirstlane(got)) return;
+        __threadfence();
+        const int H = __builtin_amdgcn_readfirstlane(S->H), ng = __builtin_amdgcn_readfirstlane(S->ng);
+        int pos = __builtin_amdgcn_readfirstlane(ld_relaxed(&S->fold_pos));
+        int n = __builtin_amdgcn_readfirstlane(ld_relaxed(&S->n));
+        int visited = __builtin_amdgcn_readfirstlane(ld_relaxed(&S->visited));
+        int valid = __builtin_amdgcn_readfirstlane(ld_relaxed(&S->valid));
+        int best = __builtin_amdgcn_readfirstlane(ld_relaxed(&S->best_cnt));
+        int best_h = __builtin_amdgcn_readfirstlane(ld_relaxed(&S->best_h));
+        float rmse = __int_as_float(__builtin_amdgcn_readfirstlane(ld_relaxed(reinterpret_cast<const int*>(&S->rmse))));
+        int sweeps = __builtin_amdgcn_readfirstlane(ld_relaxed(&S->sweeps));
+        int fitpts = __builtin_amdgcn_readfirstlane(ld_relaxed(&S->fitpts));
+        bool fin = n >= H;
+        while (!fin && pos < H) {
+            const int q = pos + lane;
+            int rd = 0;
+            if (q < H) rd = __hip_atomic_load(&ready[q], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t stop = __ballot(rd == 0);
+            const int m = stop ? (int)__builtin_ctzll(stop) : 64;  // ready run from pos
+            if (m == 0) break;
+            int rc = 0, work = 0, elo = 0, ehi = 0;
+            if (lane < m) {
+                rc = ld_relaxed(&hyp[q].cnt);
+                const long long e = __hip_atomic_load(reinterpret_cast<const long long*>(&hyp[q].err), __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+                elo = (int)(uint32_t)e;
+                ehi = (int)(uint32_t)((unsigned long long)e >> 32);
+                work = ld_relaxed(&hyp[q].pad);
+            }
+            // Only a hypothesis that beats the state at the run's start can
+            // be accepted (rmse only falls, best only grows along the run), so
+            // the serial steps visit those candidates alone; the entries
+            // between them just count (n++), and n crossing H ends the fold
+            // at the crossing entry.
+            uint64_t cand = __ballot(lane < m && rc > 0 && __hiloint2double(ehi, elo) <= (double)rmse &&
+                                     (unsigned)rc >= (unsigned)best && (unsigned)rc >= minInl);
+            int i = 0;  // entries of this run folded so far
+            while (i < m && !fin) {
+                const int c = cand ? (int)__builtin_ctzll(cand) : m;  // next candidate (or the run's end)
+                if (c - i >= H - n) {  // n reaches H before the candidate
+                    i += H - n;
+                    n = H;
+                    fin = true;
+                    break;
+                }
+                n += c - i;
+                i = c;
+                if (c == m) break;
+                cand &= cand - 1;
+                const unsigned rci = (unsigned)rdl(rc, c);
+                const double re = __hiloint2double(rdl(ehi, c), rdl(elo, c));
+                bool brk = false;
+                if (re <= (double)rmse && rci >= (unsigned)best) {  // rci >= minInl and > 0 already
+                    rmse = (float)re;
+                    best = (int)rci;
+                    best_h = pos + c;
+                    if (rci > ng * 0.5) n += 10;
+                    if (rci > ng * 0.75) n += 10;
+                    if (rci > ng * 0.8) brk = true;
+                }
+                n++;
+                i++;
+                if (brk) n = H;
+                fin = n >= H;
+            }
+            // the folded entries' counters, summed over the wave
+            const bool in = lane < i;
+            visited += i;
+            valid += __popcll(__ballot(in && rc > 0));
+            int sw = in ? (work & 31) : 0, fp = in ? (work >> 5) : 0;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                sw += __shfl_xor(sw, o);
+                fp += __shfl_xor(fp, o);
+            }
+            sweeps += __builtin_amdgcn_readfirstlane(sw);
+            fitpts += __builtin_amdgcn_readfirstlane(fp);
+            pos += i;
+            if (m < 64) break;
+        }
+        if (lane == 0) {
+            st_relaxed(&S->fold_pos, pos);
+            st_relaxed(&S->n, n);
+            st_relaxed(&S->visited, visited);
+            st_relaxed(&S->sweeps, sweeps);
+            st_relaxed(&S->fitpts, fitpts);
+            st_relaxed(&S->valid, valid);
+            st_relaxed(&S->best_cnt, best);
+            st_relaxed(&S->best_h, best_h);
+            st_relaxed(reinterpret_cast<int*>(&S->rmse), __float_as_int(rmse));
+            if (fin) st_relaxed(&S->done, 1);
+#ifdef ODO_RANSAC_PROFILE
+            if (fin) g_rprof_done = wall_clock64();
+#endif
+            __threadfence();
+            atomicExch(&S->lock, 0);
+            __threadfence();
+        }
+        if (fin) return;
+        int rd = 0;
+        if (lane == 0) rd = __hip_atomic_load(&ready[pos], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        if (!__builtin_amdgcn_readfirstlane(rd)) return;
     }
 }
 
@@ -959,10 +1090,19 @@ ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int 
             } else break;
         }
 #ifdef ODO_RANSAC_PROFILE
-        if (lane == 0)
-            printf("HYP p %d h %d ng %d ab %d nref %d inl %u tfc %lu get %lu sweep %lu total %lu pass %d pre %lu al %lu ch %lu\n",
-                   p, h, ng, (int)aborted, nref, refinedCnt, t_tfc, t_get, t_sweep, wall_clock64() - t_start, npass,
-                   tpp[0], tpp[1], tpp[2]);
+        // per-hypothesis record in g_rprof (read by odo_ransac_prof_read; a
+        // device printf stalls co-resident waves and delays the fold)
+        if (lane == 0 && h < RPROF_MAX) {
+            uint64_t* r = g_rprof + (size_t)h * 8;
+            r[0] = t_start;
+            r[1] = wall_clock64();
+            r[2] = (uint64_t)nref | ((uint64_t)aborted << 8) | ((uint64_t)refinedCnt << 16) | ((uint64_t)ng << 40);
+            r[3] = t_tfc;
+            r[4] = t_get;
+            r[5] = t_sweep;
+            r[6] = (uint64_t)npass;
+            r[7] = 0;
+        }
 #endif
         if (aborted) continue;
         HypRes* hr = B.hyp + (size_t)p * B.hcap + h;
@@ -982,11 +1122,22 @@ ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int 
         if (refinedCnt > 0)
             for (int w = lane; w < words; w += 64) mo[w] = L.cur[w];
         __threadfence();
-        if (lane == 0) {
+        // a lone pair folds with the whole wave (its fold is on the latency
+        // path: 500 visited hypotheses cost ~100 us of serial lane-0 loads);
+        // batches keep the lane-0 fold (the wave form measured 2.3 % slower
+        // there, where folds are short and overlap the extraction)
+        if (cfg.fold_wave) {
+            if (lane == 0)
+                __hip_atomic_store(B.ready + (size_t)p * B.hcap + h, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            if (!B.no_fold) try_fold_wave(B, cfg, p, lane);
+        } else if (lane == 0) {
             __hip_atomic_store(B.ready + (size_t)p * B.hcap + h, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
             if (!B.no_fold) try_fold(B, cfg, p);
         }
         wave_sync();
+#ifdef ODO_RANSAC_PROFILE
+        if (lane == 0 && h < RPROF_MAX) g_rprof[(size_t)h * 8 + 7] = wall_clock64();  // after ready + fold
+#endif
     }
 }
 
@@ -1335,6 +1486,12 @@ __global__ void __launch_bounds__(64) k_ransac_final(RansacBufs B, RansacCfg cfg
     odo_pair_result* R = B.res + p;
     float* T12o = B.T12 + (size_t)p * 16;
     const bool active = S->active;
+    // every hypothesis has been evaluated by now (the eval launches are
+    // ordered before this one); a fold that did not finish there - the last
+    // finisher's lock attempt raced a holder's release and re-check (the
+    // ready store and the lock CAS are not ordered with each other without a
+    // full fence, which measured 4 % of the batch step) - is completed here
+    if (active && mode != 1 && !B.no_fold && !ld_relaxed(&S->done)) try_fold_wave(B, cfg, p, lane);
     const int ng = S->ng, words = S->words;
     const unsigned minInl = (unsigned)cfg.min_inlier_th;
     uint32_t* BM = B.best_mask + (size_t)p * B.mask_words;
@@ -1629,6 +1786,7 @@ void launch_ransac(hipStream_t st, const void* good, const int* n_good, const in
                    int* phase, int* open_hint) {
     ransac_eval_lds_attr();
     cfg.rows0 = EV_ROWS0;
+    cfg.fold_wave = 0;
     RansacBufs B = carve(scratch, npairs, match_cap, mask_words, cfg);
     B.good = (const SortElR*)good;
     B.n_good = n_good;
@@ -1680,6 +1838,7 @@ void launch_ransac(hipStream_t st, const void* good, const int* n_good, const in
     // (the fold and the aborts make the result independent of the schedule)
     const int r0 = npairs == 1 ? rows : std::min(rows, rows0);
     cfg.rows0 = r0;
+    cfg.fold_wave = npairs == 1;
     if (part != 2) {
         hipLaunchKernelGGL(k_ransac_prep, dim3(npairs), dim3(256), 0, st, B, cfg);
         if (r0 > 0)
@@ -1750,3 +1909,15 @@ void launch_ransac_finish(hipStream_t st, void* scratch, int match_cap, int mask
 }
 
 }  // namespace odo
+#ifdef ODO_RANSAC_PROFILE
+// profile builds only: the per-hypothesis records of the last launch
+extern "C" int odo_ransac_prof_read(uint64_t* out, int n, uint64_t* done_t) {
+    n = std::min(n, RPROF_MAX);
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(odo::g_rprof), (size_t)n * 8 * sizeof(uint64_t)) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(done_t, HIP_SYMBOL(odo::g_rprof_done), sizeof(uint64_t)) != hipSuccess) return -1;
+    std::vector<uint64_t> z((size_t)n * 8, 0);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(odo::g_rprof), z.data(), z.size() * sizeof(uint64_t));
+    return n;
+}
+#endif

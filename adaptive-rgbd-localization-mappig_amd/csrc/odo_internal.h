@@ -169,6 +169,7 @@ struct RansacCfg {
     double raster_cov_x, raster_cov_y;
     int rows0;  // hypothesis rows (of EV_WAVES) of the first eval launch; set by launch_ransac
     int lanes_min_open;  // odo_kernel_forms.ransac_lanes_min_open (0 = default)
+    int fold_wave;       // ordered fold by the whole wave (a lone pair); set by launch_ransac
 };
 
 // ---- launch wrappers (defined next to their kernels)
