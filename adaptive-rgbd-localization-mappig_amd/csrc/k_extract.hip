@@ -968,6 +968,168 @@ __global__ void __launch_bounds__(256) k_blur(const uint8_t* __restrict__ pyr, u
     }
 }
 
+// ---------------------------------------------------------------- k_blur_rows
+// The same 7x7 GaussianBlur (exact Q8 taps, (S + 32768) >> 16) with no LDS:
+// a 16-lane group owns a strip of 16 four-pixel quads and walks BR_R output
+// rows down it. Per input row a lane loads the three aligned dwords around its
+// quad, forms the 4 horizontal sums with 8 v_dot4 (packed as u16 pairs), pairs
+// each column with the previous row's value (one v_perm per column) and adds
+// the pair into the three output rows it belongs to with v_dot2_u32_u16; the
+// row's own single tap closes the output three rows up, which is stored. The
+// six accumulators rotate with the row index mod 6 (the row loop is unrolled
+// by 6), so nothing is staged or re-read: ~10 lane-ops per pixel against 31
+// for the LDS-tiled k_blur. Interior only (no reflection): quads 1 .. nq[l]
+// (x - 3 >= 0, x + 6 <= w - 1), rows 3 .. h - 4; the border ring (first quad,
+// the columns past the last interior quad, the top and bottom 3 rows) is one
+// thread per pixel at the end of the grid, the direct 7x7 sum with reflect101
+// (the sums are exact integers, so the order does not matter).
+#define BR_R 30  // output rows per group item (a multiple of 6; levels are >= 40 rows)
+struct BlurRows {
+    int base[17];   // first item of each level (prefix); base[nlevels] = items
+    int nst[16];    // strips of 16 quads across the interior
+    int nq[16];     // interior quads (q = 1 .. nq)
+    int bbase[17];  // first border pixel of each level (prefix)
+};
+
+ODO_INLINE uint32_t pair_lo(uint32_t cur, uint32_t prev) { return __builtin_amdgcn_perm(cur, prev, 0x05040100u); }
+ODO_INLINE uint32_t pair_hi(uint32_t cur, uint32_t prev) { return __builtin_amdgcn_perm(cur, prev, 0x07060302u); }
+
+__global__ void __launch_bounds__(256) k_blur_rows(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
+                                                   size_t pyr_stride, const LevelDesc* __restrict__ lv, BlurRows S,
+                                                   int nlevels, int main_blocks) {
+    const int f = blockIdx.y;
+    if ((int)blockIdx.x >= main_blocks) {
+#ifdef BLUR_NO_BORDER
+        return;  // measurement only
+#endif
+        // ---- border ring, one pixel per thread
+        const int k = ((int)blockIdx.x - main_blocks) * 256 + (int)threadIdx.x;
+        if (k >= S.bbase[nlevels]) return;
+        int l = 0;
+        while (l + 1 < nlevels && k >= S.bbase[l + 1]) l++;
+        const LevelDesc L = lv[l];
+        int i = k - S.bbase[l], x, y;
+        const int xr = 4 * (S.nq[l] + 1), wr = L.w - xr;  // right border columns [xr, w)
+        if (i < 4 * L.h) {
+            x = i & 3, y = i >> 2;
+        } else if ((i -= 4 * L.h) < wr * L.h) {
+            y = i / wr, x = xr + (i - y * wr);
+        } else {
+            i -= wr * L.h;
+            const int mid = xr - 4;  // columns [4, xr), rows 0..2 and h-3..h-1
+            const int rr = i / mid;
+            x = 4 + (i - rr * mid);
+            y = rr < 3 ? rr : L.h - 6 + rr;
+        }
+        const uint8_t* src = pyr + (size_t)f * pyr_stride + L.off;
+        constexpr int W7[7] = {18, 34, 48, 56, 48, 34, 18};
+        int cx[7];
+#pragma unroll
+        for (int t = 0; t < 7; t++) cx[t] = reflect101(x + t - 3, L.w);
+        uint32_t sum = 32768u;
+#pragma unroll
+        for (int v = 0; v < 7; v++) {
+            const uint8_t* row = src + (size_t)reflect101(y + v - 3, L.h) * L.pitch;
+            uint32_t hs = 0;
+#pragma unroll
+            for (int t = 0; t < 7; t++) hs += (uint32_t)W7[t] * row[cx[t]];
+            sum += (uint32_t)W7[v] * hs;
+        }
+        blur[(size_t)f * pyr_stride + L.off + (size_t)y * L.pitch + x] = (uint8_t)(sum >> 16);
+        return;
+    }
+    // ---- interior strips
+    const int item = (int)blockIdx.x * 16 + ((int)threadIdx.x >> 4);
+    if (item >= S.base[nlevels]) return;
+    int l = 0;
+    while (l + 1 < nlevels && item >= S.base[l + 1]) l++;
+    const LevelDesc L = lv[l];
+    const int it = item - S.base[l];
+    const int chunk = it / S.nst[l], strip = it - chunk * S.nst[l];
+    const int q = 1 + strip * 16 + ((int)threadIdx.x & 15);
+    const bool store = q <= S.nq[l];
+    const int x = 4 * (store ? q : S.nq[l]);  // idle lanes shadow the last quad (loads stay in the row)
+    // the last chunk of a level overlaps its predecessor instead of running
+    // past the interior (both write the same bytes)
+    const int y0 = 3 + min(chunk * BR_R, L.h - 6 - BR_R);
+    const uint8_t* sp = pyr + (size_t)f * pyr_stride + L.off + (size_t)(y0 - 3) * L.pitch + (x - 4);
+    uint8_t* dp = blur + (size_t)f * pyr_stride + L.off + (size_t)y0 * L.pitch + x;
+    const size_t pitch = (size_t)L.pitch;
+    constexpr uint32_t C0 = 18u | (34u << 8) | (48u << 16) | (56u << 24);
+    constexpr uint32_t C1 = 48u | (34u << 8) | (18u << 16);
+    constexpr uint32_t K01 = 18u | (34u << 16), K23 = 48u | (56u << 16), K45 = 48u | (34u << 16);
+    constexpr uint32_t KLO = 18u, KHI = 18u << 16;
+    uint32_t acc[6][4];
+#pragma unroll
+    for (int a = 0; a < 6; a++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) acc[a][c] = 32768u;
+    uint32_t hp0 = 0, hp1 = 0;  // the previous row's (h0, h1), (h2, h3)
+    // rows are loaded a block of 6 ahead (the loads of block b + 1 are in
+    // flight while block b is computed)
+    constexpr int NB = (BR_R + 6) / 6;
+    uint32_t cw[6][3], nw[6][3];
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(sp + j * pitch);
+        cw[j][0] = w[0], cw[j][1] = w[1], cw[j][2] = w[2];
+    }
+    sp += 6 * pitch;
+    for (int b = 0; b < NB; b++) {
+        if (b + 1 < NB) {
+#pragma unroll
+            for (int j = 0; j < 6; j++) {
+                const uint32_t* w = reinterpret_cast<const uint32_t*>(sp + j * pitch);
+                nw[j][0] = w[0], nw[j][1] = w[1], nw[j][2] = w[2];
+            }
+            sp += 6 * pitch;
+        }
+#pragma unroll
+        for (int j = 0; j < 6; j++) {
+            // input row r = y0 - 3 + 6b + j
+            const uint32_t w0 = cw[j][0], w1 = cw[j][1], w2 = cw[j][2];
+            const uint32_t h0 = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 1), C1,
+                                                       __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 1), C0, 0u, false), false);
+            const uint32_t h1 = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 2), C1,
+                                                       __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 2), C0, 0u, false), false);
+            const uint32_t h2 = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 3), C1,
+                                                       __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 3), C0, 0u, false), false);
+            const uint32_t h3 = __builtin_amdgcn_udot4(w2, C1, __builtin_amdgcn_udot4(w1, C0, 0u, false), false);
+            const uint32_t hc0 = h0 | (h1 << 16), hc1 = h2 | (h3 << 16);
+            // pairs (h[r-1], h[r]) per column
+            const uint32_t P0 = pair_lo(hc0, hp0), P1 = pair_hi(hc0, hp0), P2 = pair_lo(hc1, hp1), P3 = pair_hi(hc1, hp1);
+            hp0 = hc0;
+            hp1 = hc1;
+            const int sa = (j + 5) % 6, sb = (j + 3) % 6, sc = (j + 1) % 6, sd = j;
+            // output r + 2: its first pair (taps 18, 34) opens the accumulator
+            acc[sa][0] = dot2u16(P0, K01, 32768u);
+            acc[sa][1] = dot2u16(P1, K01, 32768u);
+            acc[sa][2] = dot2u16(P2, K01, 32768u);
+            acc[sa][3] = dot2u16(P3, K01, 32768u);
+            // output r: taps 48, 56; output r - 2: taps 48, 34
+            acc[sb][0] = dot2u16(P0, K23, acc[sb][0]);
+            acc[sb][1] = dot2u16(P1, K23, acc[sb][1]);
+            acc[sb][2] = dot2u16(P2, K23, acc[sb][2]);
+            acc[sb][3] = dot2u16(P3, K23, acc[sb][3]);
+            acc[sc][0] = dot2u16(P0, K45, acc[sc][0]);
+            acc[sc][1] = dot2u16(P1, K45, acc[sc][1]);
+            acc[sc][2] = dot2u16(P2, K45, acc[sc][2]);
+            acc[sc][3] = dot2u16(P3, K45, acc[sc][3]);
+            // output r - 3: the last tap (18) closes it
+            const uint32_t s0 = dot2u16(hc0, KLO, acc[sd][0]), s1 = dot2u16(hc0, KHI, acc[sd][1]);
+            const uint32_t s2 = dot2u16(hc1, KLO, acc[sd][2]), s3 = dot2u16(hc1, KHI, acc[sd][3]);
+            if (b > 0 && store) {
+                const uint32_t lo = __builtin_amdgcn_perm(s1, s0, 0x0c0c0602u);
+                const uint32_t hi = __builtin_amdgcn_perm(s3, s2, 0x06020c0cu);
+                *reinterpret_cast<uint32_t*>(dp) = lo | hi;
+                dp += pitch;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 6; j++) cw[j][0] = nw[j][0], cw[j][1] = nw[j][1], cw[j][2] = nw[j][2];
+    }
+}
+
 // ============================================================ host-side launch helpers
 void upload_extract_constants() { upload_finalize_constants(); }
 
@@ -1020,6 +1182,34 @@ void launch_octree(hipStream_t st, const uint32_t* cand, const int* cand_cnt, co
 }
 void launch_blur(hipStream_t st, const uint8_t* pyr, uint8_t* blur, size_t pyr_stride, const LevelDesc* lv,
                  const LevelDesc* lv_host, int nlevels, int nframes) {
+    // k_blur_rows needs BR_R interior rows and one interior quad per level;
+    // smaller levels take the LDS-tiled kernel (ODO_BLUR_TILES=1 forces it)
+    bool rows = nlevels <= 16;
+    for (int l = 0; l < nlevels; l++) rows = rows && lv_host[l].h >= BR_R + 6 && lv_host[l].w >= 12;
+    static const bool tiles = [] {
+        const char* e = odo_knob("ODO_BLUR_TILES");
+        return e && e[0] == '1';
+    }();
+    if (rows && !tiles) {
+        BlurRows R{};
+        int acc = 0, bacc = 0;
+        for (int l = 0; l < nlevels; l++) {
+            const LevelDesc& L = lv_host[l];
+            R.base[l] = acc;
+            R.bbase[l] = bacc;
+            R.nq[l] = (L.w - 8) / 4;  // x + 7 <= w - 1: the lane's three dwords stay inside the row
+            R.nst[l] = (R.nq[l] + 15) / 16;
+            acc += R.nst[l] * ((L.h - 6 + BR_R - 1) / BR_R);
+            const int xr = 4 * (R.nq[l] + 1);
+            bacc += 4 * L.h + (L.w - xr) * L.h + 6 * (xr - 4);
+        }
+        R.base[nlevels] = acc;
+        R.bbase[nlevels] = bacc;
+        const int main_blocks = (acc + 15) / 16;
+        hipLaunchKernelGGL(k_blur_rows, dim3(main_blocks + (bacc + 255) / 256, nframes), dim3(256), 0, st, pyr, blur,
+                           pyr_stride, lv, R, nlevels, main_blocks);
+        return;
+    }
     BlurTiles T{};
     int acc = 0;
     for (int l = 0; l < nlevels; l++) {

@@ -935,9 +935,32 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
     // only the streams the schedule uses (each extra stream shares one of the
     // process's GPU_MAX_HW_QUEUES hardware queues with another and serialises
     // against it); the others alias
+    // ODO_PAIR_CUMASK / ODO_EXTRACT_CUMASK (tuning): comma-separated 32-bit
+    // hex words of a CU mask for the pair / extraction streams (spatial
+    // partitioning of the CUs between the latency-bound pair stages and the
+    // throughput-bound extraction)
+    auto parse_mask = [](const char* e, std::vector<uint32_t>& m) {
+        m.clear();
+        while (e && *e) {
+            char* end = nullptr;
+            m.push_back((uint32_t)strtoul(e, &end, 16));
+            if (end == e) break;
+            e = *end == ',' ? end + 1 : end;
+        }
+        return !m.empty();
+    };
+    std::vector<uint32_t> pmask, xmask;
+    const bool pm = parse_mask(odo_knob("ODO_PAIR_CUMASK"), pmask);
+    const bool xm = parse_mask(odo_knob("ODO_EXTRACT_CUMASK"), xmask);
     auto mk = [&](hipStream_t* s, bool prio) {
-        const bool r = prio ? hipStreamCreateWithPriority(s, hipStreamNonBlocking, pair_stream_priority()) == hipSuccess
-                            : hipStreamCreateWithFlags(s, hipStreamNonBlocking) == hipSuccess;
+        bool r;
+        if (prio && pm)
+            r = hipExtStreamCreateWithCUMask(s, (uint32_t)pmask.size(), pmask.data()) == hipSuccess;
+        else if (!prio && xm)
+            r = hipExtStreamCreateWithCUMask(s, (uint32_t)xmask.size(), xmask.data()) == hipSuccess;
+        else
+            r = prio ? hipStreamCreateWithPriority(s, hipStreamNonBlocking, pair_stream_priority()) == hipSuccess
+                     : hipStreamCreateWithFlags(s, hipStreamNonBlocking) == hipSuccess;
         if (r) c->owned.push_back(*s);
         return r;
     };

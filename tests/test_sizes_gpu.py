@@ -69,3 +69,36 @@ def test_gpu_adaptive_frame_sizes(w, h, inner):
         assert np.array_equal(res[p]["T12"], np.array(r.T12, np.float32)), f"{w}x{h} pair {p}: T12"
         assert np.abs(res[p]["Tcw"] - np.array(r.Tcw, np.float32)).max() < 1e-4, f"{w}x{h} pair {p}: Tcw"
     odo.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,h", [(640, 480), (330, 250), (642, 482), (517, 389)])
+def test_gpu_blur_every_frame_and_level(w, h):
+    """GaussianBlur 7x7 (orbextractor.cpp:795-796) of every pyramid level of
+    every frame, byte for byte against the oracle's blur of the GPU's own
+    pyramid (itself pinned by test_pyramid_and_blur_bit_exact): the
+    row-strip kernel's interior, its overlapping last chunk and the
+    reflect101 border ring at widths that are not multiples of 4 or 16."""
+    pkg = load_pkg()
+    n = 4
+    bgr, dep, _ = sequence(n, w, h, seed=0x5EED0042)
+    cfg = pkg.default_config(w, h, n, nfeatures=1000, iterations=50)
+    odo = pkg.Odometry(cfg)
+    odo.track_batch_host(bgr, dep)
+    lw, lh = (O.C.c_int * 8)(), (O.C.c_int * 8)()
+    O.lib().oracle_level_sizes(O.C.byref(O.orb_params(1000)), w, h, lw, lh, (O.C.c_float * 8)(), (O.C.c_int * 8)())
+    total = sum(a * b for a, b in zip(lw, lh))
+    for i in range(n):
+        pyr = odo.debug_pyramid(i, total)
+        blur = odo.debug_blur(i, total)
+        assert pyr.size == blur.size == total
+        off = 0
+        for l in range(8):
+            m = lw[l] * lh[l]
+            rb = np.zeros(m, np.uint8)
+            O.lib().oracle_blur(O.ptr(np.ascontiguousarray(pyr[off:off + m])), lw[l], lh[l], O.ptr(rb))
+            bad = np.nonzero(blur[off:off + m] != rb)[0]
+            assert bad.size == 0, f"{w}x{h} frame {i} level {l}: {bad.size} px differ, first (y, x) " \
+                                  f"{divmod(int(bad[0]), lw[l])}"
+            off += m
+    odo.close()
