@@ -12,6 +12,14 @@
 #include "odo_device.h"
 #include "odo_internal.h"
 
+// wave priority of the extraction kernels (ODO_EXTRACT_PRIO, measurement
+// builds): the pair stages' waves issue at ODO_WAVE_PRIO
+#ifndef ODO_EXTRACT_PRIO
+#define ODO_EXTRACT_PRIO 0
+#endif
+#define EXTRACT_PRIO() \
+    if (ODO_EXTRACT_PRIO) __builtin_amdgcn_s_setprio(ODO_EXTRACT_PRIO)
+
 namespace odo {
 
 // ============================================================ gray
@@ -21,6 +29,7 @@ namespace odo {
 // the rest pixel by pixel).
 __global__ void __launch_bounds__(256) k_gray(const uint8_t* __restrict__ bgr, uint8_t* __restrict__ pyr,
                                               int w, int h, int pitch, size_t in_stride, size_t pyr_stride) {
+    EXTRACT_PRIO();
     const int f = blockIdx.y;
     const int q = blockIdx.x * blockDim.x + threadIdx.x;  // quad index
     const uint8_t* src = bgr + (size_t)f * in_stride;
@@ -67,6 +76,7 @@ __global__ void __launch_bounds__(256) k_gray(const uint8_t* __restrict__ bgr, u
 __global__ void __launch_bounds__(256) k_resize(uint8_t* __restrict__ pyr, size_t pyr_stride, int src_off,
                                                 int spitch, int dst_off, int dpitch, int dw, int dh, int rb,
                                                 const ResizeX* __restrict__ xt, const ResizeY* __restrict__ yt) {
+    EXTRACT_PRIO();
     extern __shared__ __attribute__((aligned(16))) uint8_t rz_lds[];
     const int f = blockIdx.y;
     const int y0 = blockIdx.x * rb;
@@ -134,6 +144,7 @@ __global__ void __launch_bounds__(64) k_fast_cells(const uint8_t* __restrict__ p
                                                    const CellDesc* __restrict__ cells, const LevelDesc* __restrict__ lv,
                                                    uint32_t* __restrict__ cand, int* __restrict__ cand_cnt,
                                                    int ncells, int cell_cap, int ini_th, int min_th) {
+    EXTRACT_PRIO();
     // ROI rows staged as whole aligned dwords: pixel (r, c) at byte r*RS + sh + c
     constexpr int RS4 = (ROI_MAX + 3 + 3) / 4 + 1;  // dwords per staged row (>= (sh+cols+3)/4)
     constexpr int RS = 4 * RS4;
@@ -159,11 +170,16 @@ __global__ void __launch_bounds__(64) k_fast_cells(const uint8_t* __restrict__ p
     {
         // rows are pitch-aligned: dword loads from the aligned column below x0
         const uint32_t* src = reinterpret_cast<const uint32_t*>(img + (size_t)C.y0 * L.pitch + (C.x0 & ~3));
-        const int p4 = L.pitch >> 2;
-        const float inv = 1.0f / (float)nwr;
-        for (int p = lane; p < rows * nwr; p += 64) {
-            const int r = (int)(((float)p + 0.5f) * inv), k = p - r * nwr;
-            roi32[r * RS4 + k] = src[r * p4 + k];
+        const uint32_t p4 = (uint32_t)L.pitch >> 2;
+        // lane = (dword k of KW, row phase): no per-item division, and the
+        // rows' loads are independent
+        constexpr int KW = RS4 <= 16 ? 16 : 32;
+        static_assert(RS4 <= KW, "staged ROI rows wider than 32 dwords");
+        const int k = lane & (KW - 1);
+        if (k < nwr) {
+#pragma unroll 4
+            for (int r = lane / KW; r < rows; r += 64 / KW)
+                roi32[r * RS4 + k] = src[__umul24((uint32_t)r, p4) + (uint32_t)k];
         }
     }
     uint32_t* out = cand + ((size_t)f * ncells + ci) * cell_cap;
@@ -172,25 +188,29 @@ __global__ void __launch_bounds__(64) k_fast_cells(const uint8_t* __restrict__ p
     const int m0 = (sh + 3) >> 2, m1 = (sh + cols - 4) >> 2;
     const int nq = cols > 6 ? m1 - m0 + 1 : 0;
     const int nitems = drows > 0 ? drows * nq : 0;
-    const float qinv = nq > 0 ? 1.0f / (float)nq : 0.f;
+    const int qdq = nq > 0 ? 64 / nq : 0, qdr = nq > 0 ? 64 - qdq * nq : 0;
     typedef short s16x2 __attribute__((ext_vector_type(2)));
     int count = 0;
     for (int attempt = 0; attempt < 2; attempt++) {
         const int th = attempt == 0 ? ini_th : min_th;
         const int thc = th < 0 ? 0 : (th > 255 ? 255 : th);
-        for (int w = lane; w < rows * RS4; w += 64) score32[w] = 0;
+        for (int w = lane; w < (rows * RS4 + 3) >> 2; w += 64) reinterpret_cast<uint4*>(score32)[w] = uint4{0, 0, 0, 0};
         __syncthreads();
         // 1. compass pre-filter, 4 pixels per lane in 16-bit pairs: dark_k iff
         //    a_k - (v - th) < 0, bright_k iff (v + th) - a_k < 0 (sign bits)
         int n1 = 0;
         const s16x2 thv = {(short)thc, (short)thc};
+        int qii = nq > 0 ? lane / nq : 0, qmm = lane - qii * nq;  // item lane + base as (row, quad)
         for (int base = 0; base < nitems; base += 64) {
             const int it = base + lane;
             uint32_t pass4 = 0;  // bit i: pixel 4m+i survives
             int rowbase = 0, m = 0;
+            const int ii = qii;
+            m = m0 + qmm;
+            qii += qdq;
+            qmm += qdr;
+            if (qmm >= nq) qmm -= nq, qii++;
             if (it < nitems) {
-                const int ii = (int)(((float)it + 0.5f) * qinv);
-                m = m0 + (it - ii * nq);
                 const int r = 3 + ii;
                 rowbase = r * RS;
                 const uint32_t* w = roi32 + r * RS4 + m;
@@ -390,6 +410,7 @@ __global__ void __launch_bounds__(OT_THREADS) k_octree(const uint32_t* __restric
                                                        uint8_t* __restrict__ kquad_g, size_t keys_stride_frame,
                                                        uint32_t* __restrict__ okp, int* __restrict__ ocnt, int okp_stride,
                                                        int node_cap) {
+    EXTRACT_PRIO();
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // ODO_OCTREE_LPT=1: grid (frames, levels), so every frame's level 0 (the
     // longest workgroups) is dispatched first (longest-first): 129 vs 190-206
@@ -831,6 +852,8 @@ ODO_INLINE int reflect101(int i, int n) {
     while (i < 0 || i >= n) i = i < 0 ? -i : 2 * n - 2 - i;
     return i;
 }
+// one reflection (|overshoot| < n): branch-free
+ODO_INLINE int reflect101_1(int i, int n) { return i < 0 ? -i : (i >= n ? 2 * n - 2 - i : i); }
 
 struct BlurTiles {
     int base[17];  // first tile of each level (prefix), base[nlevels] = total
@@ -977,84 +1000,39 @@ __global__ void __launch_bounds__(256) k_blur(const uint8_t* __restrict__ pyr, u
 // the pair into the three output rows it belongs to with v_dot2_u32_u16; the
 // row's own single tap closes the output three rows up, which is stored. The
 // six accumulators rotate with the row index mod 6 (the row loop is unrolled
-// by 6), so nothing is staged or re-read: ~10 lane-ops per pixel against 31
-// for the LDS-tiled k_blur. Interior only (no reflection): quads 1 .. nq[l]
-// (x - 3 >= 0, x + 6 <= w - 1), rows 3 .. h - 4; the border ring (first quad,
-// the columns past the last interior quad, the top and bottom 3 rows) is one
-// thread per pixel at the end of the grid, the direct 7x7 sum with reflect101
-// (the sums are exact integers, so the order does not matter).
-#define BR_R 30  // output rows per group item (a multiple of 6; levels are >= 40 rows)
+// by 6) and rows are loaded a block of 6 ahead, so nothing is staged or
+// re-read: ~10 lane-ops per pixel against 31 for the LDS-tiled k_blur.
+// Strips cover quads 1 .. nq[l] (x - 3 >= 0 and x + 7 <= w - 1: no column
+// reflection, the three dwords inside the row) and every row; the first and
+// last chunk reflect their halo rows (reflect101). The quads left of quad 1
+// and right of quad nq run the same walk one lane each (a lane per (level,
+// chunk, edge quad), packed 64 to a wave at the end of the grid): per-lane
+// row reflection, and the row's 12 bytes rebuilt with reflect101 columns by
+// two v_perm per dword from per-lane selectors. Widths that are not a
+// multiple of 4 leave garbage in the row padding past w, never read.
+#define BR_R 30  // output rows per chunk (a multiple of 6; levels are >= 40 rows)
 struct BlurRows {
-    int base[17];   // first item of each level (prefix); base[nlevels] = items
+    int base[17];   // first strip item of each level (prefix); base[nlevels] = items
     int nst[16];    // strips of 16 quads across the interior
     int nq[16];     // interior quads (q = 1 .. nq)
-    int bbase[17];  // first border pixel of each level (prefix)
+    int nch[16];    // row chunks
+    int ebase[17];  // first edge lane of each level (prefix); ebase[nlevels] = edge lanes
 };
 
 ODO_INLINE uint32_t pair_lo(uint32_t cur, uint32_t prev) { return __builtin_amdgcn_perm(cur, prev, 0x05040100u); }
 ODO_INLINE uint32_t pair_hi(uint32_t cur, uint32_t prev) { return __builtin_amdgcn_perm(cur, prev, 0x07060302u); }
 
-__global__ void __launch_bounds__(256) k_blur_rows(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
-                                                   size_t pyr_stride, const LevelDesc* __restrict__ lv, BlurRows S,
-                                                   int nlevels, int main_blocks) {
-    const int f = blockIdx.y;
-    if ((int)blockIdx.x >= main_blocks) {
-#ifdef BLUR_NO_BORDER
-        return;  // measurement only
-#endif
-        // ---- border ring, one pixel per thread
-        const int k = ((int)blockIdx.x - main_blocks) * 256 + (int)threadIdx.x;
-        if (k >= S.bbase[nlevels]) return;
-        int l = 0;
-        while (l + 1 < nlevels && k >= S.bbase[l + 1]) l++;
-        const LevelDesc L = lv[l];
-        int i = k - S.bbase[l], x, y;
-        const int xr = 4 * (S.nq[l] + 1), wr = L.w - xr;  // right border columns [xr, w)
-        if (i < 4 * L.h) {
-            x = i & 3, y = i >> 2;
-        } else if ((i -= 4 * L.h) < wr * L.h) {
-            y = i / wr, x = xr + (i - y * wr);
-        } else {
-            i -= wr * L.h;
-            const int mid = xr - 4;  // columns [4, xr), rows 0..2 and h-3..h-1
-            const int rr = i / mid;
-            x = 4 + (i - rr * mid);
-            y = rr < 3 ? rr : L.h - 6 + rr;
-        }
-        const uint8_t* src = pyr + (size_t)f * pyr_stride + L.off;
-        constexpr int W7[7] = {18, 34, 48, 56, 48, 34, 18};
-        int cx[7];
-#pragma unroll
-        for (int t = 0; t < 7; t++) cx[t] = reflect101(x + t - 3, L.w);
-        uint32_t sum = 32768u;
-#pragma unroll
-        for (int v = 0; v < 7; v++) {
-            const uint8_t* row = src + (size_t)reflect101(y + v - 3, L.h) * L.pitch;
-            uint32_t hs = 0;
-#pragma unroll
-            for (int t = 0; t < 7; t++) hs += (uint32_t)W7[t] * row[cx[t]];
-            sum += (uint32_t)W7[v] * hs;
-        }
-        blur[(size_t)f * pyr_stride + L.off + (size_t)y * L.pitch + x] = (uint8_t)(sum >> 16);
-        return;
-    }
-    // ---- interior strips
-    const int item = (int)blockIdx.x * 16 + ((int)threadIdx.x >> 4);
-    if (item >= S.base[nlevels]) return;
-    int l = 0;
-    while (l + 1 < nlevels && item >= S.base[l + 1]) l++;
-    const LevelDesc L = lv[l];
-    const int it = item - S.base[l];
-    const int chunk = it / S.nst[l], strip = it - chunk * S.nst[l];
-    const int q = 1 + strip * 16 + ((int)threadIdx.x & 15);
-    const bool store = q <= S.nq[l];
-    const int x = 4 * (store ? q : S.nq[l]);  // idle lanes shadow the last quad (loads stay in the row)
-    // the last chunk of a level overlaps its predecessor instead of running
-    // past the interior (both write the same bytes)
-    const int y0 = 3 + min(chunk * BR_R, L.h - 6 - BR_R);
-    const uint8_t* sp = pyr + (size_t)f * pyr_stride + L.off + (size_t)(y0 - 3) * L.pitch + (x - 4);
-    uint8_t* dp = blur + (size_t)f * pyr_stride + L.off + (size_t)y0 * L.pitch + x;
-    const size_t pitch = (size_t)L.pitch;
+// the last chunk of a level overlaps its predecessor instead of running past
+// the last row (both write the same bytes)
+template <int R>
+ODO_INLINE int chunk_y0(int chunk, int h) { return min(chunk * R, h - R); }
+#define BR_RE 6  // output rows per edge-lane chunk
+
+// One quad's walk down rows y0 - 3 .. y0 + R + 2. s0: the level's row 0 at
+// byte x - 4 (interior) / the level's row 0 (EDGE); dp: row y0 at byte x.
+template <bool EDGE, int R>
+ODO_INLINE void blur_walk(const uint8_t* s0, uint8_t* dp, size_t pitch, int h, int y0, bool top, bool bottom,
+                          bool store, int o0, int o1, int o2, const uint32_t (&selA)[3], const uint32_t (&selB)[3]) {
     constexpr uint32_t C0 = 18u | (34u << 8) | (48u << 16) | (56u << 24);
     constexpr uint32_t C1 = 48u | (34u << 8) | (18u << 16);
     constexpr uint32_t K01 = 18u | (34u << 16), K23 = 48u | (56u << 16), K45 = 48u | (34u << 16);
@@ -1066,28 +1044,42 @@ __global__ void __launch_bounds__(256) k_blur_rows(const uint8_t* __restrict__ p
         for (int c = 0; c < 4; c++) acc[a][c] = 32768u;
     uint32_t hp0 = 0, hp1 = 0;  // the previous row's (h0, h1), (h2, h3)
     // rows are loaded a block of 6 ahead (the loads of block b + 1 are in
-    // flight while block b is computed)
-    constexpr int NB = (BR_R + 6) / 6;
+    // flight while block b is computed); the first and the last block of an
+    // edge chunk address their rows through reflect101
+    static_assert(R % 6 == 0, "the accumulators rotate over 6 rows");
+    constexpr int NB = (R + 6) / 6;
     uint32_t cw[6][3], nw[6][3];
+    const uint8_t* sp = s0 + (size_t)(y0 - 3) * pitch;
+    auto load_block = [&](uint32_t(&d)[6][3], int b, bool refl) {
 #pragma unroll
-    for (int j = 0; j < 6; j++) {
-        const uint32_t* w = reinterpret_cast<const uint32_t*>(sp + j * pitch);
-        cw[j][0] = w[0], cw[j][1] = w[1], cw[j][2] = w[2];
-    }
-    sp += 6 * pitch;
-    for (int b = 0; b < NB; b++) {
-        if (b + 1 < NB) {
-#pragma unroll
-            for (int j = 0; j < 6; j++) {
-                const uint32_t* w = reinterpret_cast<const uint32_t*>(sp + j * pitch);
-                nw[j][0] = w[0], nw[j][1] = w[1], nw[j][2] = w[2];
+        for (int j = 0; j < 6; j++) {
+            if (EDGE) {
+                const uint8_t* rp = s0 + (size_t)reflect101_1(y0 - 3 + 6 * b + j, h) * pitch;
+                d[j][0] = *reinterpret_cast<const uint32_t*>(rp + o0);
+                d[j][1] = *reinterpret_cast<const uint32_t*>(rp + o1);
+                d[j][2] = *reinterpret_cast<const uint32_t*>(rp + o2);
+            } else {
+                const uint8_t* rp = refl ? s0 + (size_t)reflect101_1(y0 - 3 + 6 * b + j, h) * pitch : sp + j * pitch;
+                const uint32_t* w = reinterpret_cast<const uint32_t*>(rp);
+                d[j][0] = w[0], d[j][1] = w[1], d[j][2] = w[2];
             }
-            sp += 6 * pitch;
         }
+        sp += 6 * pitch;
+    };
+    load_block(cw, 0, top);
+    for (int b = 0; b < NB; b++) {
+        if (b + 1 < NB) load_block(nw, b + 1, b + 1 == NB - 1 && bottom);
 #pragma unroll
         for (int j = 0; j < 6; j++) {
             // input row r = y0 - 3 + 6b + j
-            const uint32_t w0 = cw[j][0], w1 = cw[j][1], w2 = cw[j][2];
+            uint32_t w0 = cw[j][0], w1 = cw[j][1], w2 = cw[j][2];
+            if (EDGE) {
+                // the row's bytes x-4 .. x+7 with reflected columns
+                const uint32_t e0 = __builtin_amdgcn_perm(w1, w0, selA[0]) | __builtin_amdgcn_perm(w2, w2, selB[0]);
+                const uint32_t e1 = __builtin_amdgcn_perm(w1, w0, selA[1]) | __builtin_amdgcn_perm(w2, w2, selB[1]);
+                const uint32_t e2 = __builtin_amdgcn_perm(w1, w0, selA[2]) | __builtin_amdgcn_perm(w2, w2, selB[2]);
+                w0 = e0, w1 = e1, w2 = e2;
+            }
             const uint32_t h0 = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 1), C1,
                                                        __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 1), C0, 0u, false), false);
             const uint32_t h1 = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 2), C1,
@@ -1116,11 +1108,11 @@ __global__ void __launch_bounds__(256) k_blur_rows(const uint8_t* __restrict__ p
             acc[sc][2] = dot2u16(P2, K45, acc[sc][2]);
             acc[sc][3] = dot2u16(P3, K45, acc[sc][3]);
             // output r - 3: the last tap (18) closes it
-            const uint32_t s0 = dot2u16(hc0, KLO, acc[sd][0]), s1 = dot2u16(hc0, KHI, acc[sd][1]);
-            const uint32_t s2 = dot2u16(hc1, KLO, acc[sd][2]), s3 = dot2u16(hc1, KHI, acc[sd][3]);
+            const uint32_t s0v = dot2u16(hc0, KLO, acc[sd][0]), s1v = dot2u16(hc0, KHI, acc[sd][1]);
+            const uint32_t s2v = dot2u16(hc1, KLO, acc[sd][2]), s3v = dot2u16(hc1, KHI, acc[sd][3]);
             if (b > 0 && store) {
-                const uint32_t lo = __builtin_amdgcn_perm(s1, s0, 0x0c0c0602u);
-                const uint32_t hi = __builtin_amdgcn_perm(s3, s2, 0x06020c0cu);
+                const uint32_t lo = __builtin_amdgcn_perm(s1v, s0v, 0x0c0c0602u);
+                const uint32_t hi = __builtin_amdgcn_perm(s3v, s2v, 0x06020c0cu);
                 *reinterpret_cast<uint32_t*>(dp) = lo | hi;
                 dp += pitch;
             }
@@ -1128,6 +1120,70 @@ __global__ void __launch_bounds__(256) k_blur_rows(const uint8_t* __restrict__ p
 #pragma unroll
         for (int j = 0; j < 6; j++) cw[j][0] = nw[j][0], cw[j][1] = nw[j][1], cw[j][2] = nw[j][2];
     }
+}
+
+// Strips (quads 1 .. nq, every row); the edge quads are k_blur_edges.
+__global__ void __launch_bounds__(256) k_blur_rows(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
+                                                   size_t pyr_stride, const LevelDesc* __restrict__ lv, BlurRows S,
+                                                   int nlevels) {
+    EXTRACT_PRIO();
+    const int f = blockIdx.y;
+    const uint32_t none[3] = {0, 0, 0};
+    const int item = (int)blockIdx.x * 16 + ((int)threadIdx.x >> 4);
+    if (item >= S.base[nlevels]) return;
+    int l = 0;
+    while (l + 1 < nlevels && item >= S.base[l + 1]) l++;
+    const LevelDesc L = lv[l];
+    const int it = item - S.base[l];
+    const int chunk = it / S.nst[l], strip = it - chunk * S.nst[l];
+    const int q = 1 + strip * 16 + ((int)threadIdx.x & 15);
+    const bool store = q <= S.nq[l];
+    const int x = 4 * (store ? q : S.nq[l]);  // idle lanes shadow the last quad (loads stay in the row)
+    const int y0 = chunk_y0<BR_R>(chunk, L.h);
+    const bool top = y0 < 3, bottom = y0 + BR_R + 3 > L.h;  // halo rows to reflect (uniform per group)
+    const uint8_t* s0 = pyr + (size_t)f * pyr_stride + L.off + (x - 4);
+    uint8_t* dp = blur + (size_t)f * pyr_stride + L.off + (size_t)y0 * L.pitch + x;
+    blur_walk<false, BR_R>(s0, dp, (size_t)L.pitch, L.h, y0, top, bottom, store, 0, 0, 0, none, none);
+}
+
+// Edge quads: one lane per (level, 6-row chunk, quad left of 1 / right of nq).
+__global__ void __launch_bounds__(256) k_blur_edges(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
+                                                    size_t pyr_stride, const LevelDesc* __restrict__ lv, BlurRows S,
+                                                    int nlevels) {
+    EXTRACT_PRIO();
+    const int f = blockIdx.y;
+    const int k = (int)blockIdx.x * 256 + (int)threadIdx.x;
+    if (k >= S.ebase[nlevels]) return;
+    int l = 0;
+    while (l + 1 < nlevels && k >= S.ebase[l + 1]) l++;
+    const LevelDesc L = lv[l];
+    const int nqa = (L.w + 3) >> 2, ne = 1 + nqa - (S.nq[l] + 1);  // quad 0 and quads nq+1 .. nqa-1
+    const int i = k - S.ebase[l], chunk = i / ne, e = i - chunk * ne;
+    const int q = e == 0 ? 0 : S.nq[l] + e;
+    const int x = 4 * q;
+    const int y0 = chunk_y0<BR_RE>(chunk, L.h);
+    // selectors: byte b of dword d is position P = x - 4 + 4d + b, taken from
+    // reflect101(P) - (x - 4) of the loaded window (w0, w1, w2); a window
+    // dword that would lie outside the row is loaded from x instead and never
+    // selected
+    uint32_t selA[3], selB[3];
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+        uint32_t a = 0, bsel = 0;
+#pragma unroll
+        for (int bb = 0; bb < 4; bb++) {
+            const int src = reflect101_1(x - 4 + 4 * d + bb, L.w) - (x - 4);
+            const int sd = src >> 2, sb = src & 3;
+            a |= (uint32_t)(sd == 0 ? sb : sd == 1 ? 4 + sb : 0x0c) << (8 * bb);
+            bsel |= (uint32_t)(sd == 2 ? sb : 0x0c) << (8 * bb);
+        }
+        selA[d] = a;
+        selB[d] = bsel;
+    }
+    const int o0 = x >= 4 ? x - 4 : x, o2 = x + 8 <= L.pitch ? x + 4 : x;
+    const uint8_t* s0 = pyr + (size_t)f * pyr_stride + L.off;
+    uint8_t* dp = blur + (size_t)f * pyr_stride + L.off + (size_t)y0 * L.pitch + x;
+    blur_walk<true, BR_RE>(s0, dp, (size_t)L.pitch, L.h, y0, true, true, true, o0, x, o2, selA, selB);
 }
 
 // ============================================================ host-side launch helpers
@@ -1185,29 +1241,30 @@ void launch_blur(hipStream_t st, const uint8_t* pyr, uint8_t* blur, size_t pyr_s
     // k_blur_rows needs BR_R interior rows and one interior quad per level;
     // smaller levels take the LDS-tiled kernel (ODO_BLUR_TILES=1 forces it)
     bool rows = nlevels <= 16;
-    for (int l = 0; l < nlevels; l++) rows = rows && lv_host[l].h >= BR_R + 6 && lv_host[l].w >= 12;
+    for (int l = 0; l < nlevels; l++) rows = rows && lv_host[l].h >= BR_R && lv_host[l].w >= 12;
     static const bool tiles = [] {
         const char* e = odo_knob("ODO_BLUR_TILES");
         return e && e[0] == '1';
     }();
     if (rows && !tiles) {
         BlurRows R{};
-        int acc = 0, bacc = 0;
+        int acc = 0, eacc = 0;
         for (int l = 0; l < nlevels; l++) {
             const LevelDesc& L = lv_host[l];
             R.base[l] = acc;
-            R.bbase[l] = bacc;
+            R.ebase[l] = eacc;
             R.nq[l] = (L.w - 8) / 4;  // x + 7 <= w - 1: the lane's three dwords stay inside the row
             R.nst[l] = (R.nq[l] + 15) / 16;
-            acc += R.nst[l] * ((L.h - 6 + BR_R - 1) / BR_R);
-            const int xr = 4 * (R.nq[l] + 1);
-            bacc += 4 * L.h + (L.w - xr) * L.h + 6 * (xr - 4);
+            R.nch[l] = (L.h + BR_R - 1) / BR_R;
+            acc += R.nst[l] * R.nch[l];
+            eacc += (1 + (L.w + 3) / 4 - (R.nq[l] + 1)) * ((L.h + BR_RE - 1) / BR_RE);
         }
         R.base[nlevels] = acc;
-        R.bbase[nlevels] = bacc;
-        const int main_blocks = (acc + 15) / 16;
-        hipLaunchKernelGGL(k_blur_rows, dim3(main_blocks + (bacc + 255) / 256, nframes), dim3(256), 0, st, pyr, blur,
-                           pyr_stride, lv, R, nlevels, main_blocks);
+        R.ebase[nlevels] = eacc;
+        hipLaunchKernelGGL(k_blur_edges, dim3((eacc + 255) / 256, nframes), dim3(256), 0, st, pyr, blur, pyr_stride, lv,
+                           R, nlevels);
+        hipLaunchKernelGGL(k_blur_rows, dim3((acc + 15) / 16, nframes), dim3(256), 0, st, pyr, blur, pyr_stride, lv, R,
+                           nlevels);
         return;
     }
     BlurTiles T{};

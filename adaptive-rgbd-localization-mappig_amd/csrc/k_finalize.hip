@@ -17,6 +17,9 @@
 //                   extractor's finalisation (k_adaptive.hip)
 #include "odo_device.h"
 #include "odo_internal.h"
+#ifndef ODO_EXTRACT_PRIO
+#define ODO_EXTRACT_PRIO 0
+#endif
 #include "../../include/odo_orb_pattern.h"
 
 namespace odo {
@@ -225,6 +228,7 @@ __global__ void __launch_bounds__(64 * NW) k_finalize_lds(const uint8_t* __restr
                                                       const uint32_t* __restrict__ okp, const int* __restrict__ ocnt,
                                                       int okp_stride, orb_kp* __restrict__ kps, uint8_t* __restrict__ desc,
                                                       int* __restrict__ nkp, int kp_cap) {
+    if (ODO_EXTRACT_PRIO) __builtin_amdgcn_s_setprio(ODO_EXTRACT_PRIO);
     __shared__ uint64_t s_bal[NW][16];
     __shared__ __attribute__((aligned(16))) uint32_t s_disc[16][8];
     __shared__ __attribute__((aligned(16))) uint32_t s_patch[NW * FIN_KPW][FL_KP_DW];

@@ -385,7 +385,9 @@ ODO_INLINE void huber_rho(double delta, double chi, double rho[3]) {
 // exp map, LM bookkeeping — redundantly on identical values, so no lane ever
 // waits for a broadcast; per-edge work is split over lanes and combined with a
 // fixed xor-butterfly (deterministic).
-#define PNP_NW 4
+#ifndef PNP_NW
+#define PNP_NW 4  // waves per pair
+#endif
 #define PNP_NT (64 * PNP_NW)
 #define PNP_K 4  // Levenberg trials evaluated per edge pass (one per 16-lane group of wave 0)
 static_assert(PNP_K <= 4, "the trial solves run on the four 16-lane groups of one wave");
