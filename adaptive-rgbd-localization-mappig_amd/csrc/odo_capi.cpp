@@ -137,6 +137,11 @@ struct odo_ctx {
     int npstreams = 2;
     bool knn_pair = true;  // schedule 5 (ODO_KNN_PAIR=0: on the extraction stream): kNN-2 at the head of the pair stream, 88.2k vs 86.5k frames/s (kNN roofline 0.85 vs 0.90)
     hipStream_t cur_p = nullptr;     // pair stream of the batch being queued
+    // ODO_KNN_GATE (tuning): the next batch's extraction waits for this
+    // batch's kNN-2 (no gray / kNN-2 overlap)
+    bool knn_gate = false;
+    hipEvent_t ev_knn = nullptr;
+    bool knn_rec = false;
     std::vector<hipStream_t> owned;  // streams created (the rest alias them)
     hipEvent_t ev_latch = nullptr;   // after the last queued k_latch (schedule 5)
     bool latch_rec = false;
@@ -403,6 +408,7 @@ static void free_ctx(odo_ctx* c) {
         if (c->ev_in_copied[i]) hipEventDestroy(c->ev_in_copied[i]);
         if (c->ev_in_free[i]) hipEventDestroy(c->ev_in_free[i]);
     }
+    if (c->ev_knn) hipEventDestroy(c->ev_knn);
     if (c->ev_latch) hipEventDestroy(c->ev_latch);
     if (c->ev_depth_done) hipEventDestroy(c->ev_depth_done);
     if (c->stage_h) (void)hipHostFree(c->stage_h);
@@ -970,6 +976,7 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
     } else if (ok && c->sched == 5) {
         if (const char* np = odo_knob("ODO_PSTREAMS")) c->npstreams = std::min(3, std::max(1, atoi(np)));
         if (const char* kp = odo_knob("ODO_KNN_PAIR")) c->knn_pair = atoi(kp) != 0;
+        if (const char* kg = odo_knob("ODO_KNN_GATE")) c->knn_gate = atoi(kg) != 0;
         ok = mk(&c->pstream, true) && (c->npstreams < 2 || mk(&c->pstream2, true)) &&
              (c->npstreams < 3 || mk(&c->pstream3, true));
         if (c->npstreams < 2) c->pstream2 = c->pstream;
@@ -997,6 +1004,7 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
     if (!c->bstream) c->bstream = c->stream;
     if (ok) ok = hipEventCreateWithFlags(&c->ev_latch, hipEventDisableTiming) == hipSuccess;
     if (ok) ok = hipEventCreateWithFlags(&c->ev_depth_done, hipEventDisableTiming) == hipSuccess;
+    if (ok) ok = hipEventCreateWithFlags(&c->ev_knn, hipEventDisableTiming) == hipSuccess;
     // host-input uploads run on their own stream (the DMA engines), ordered
     // against the extraction stream by events only
     if (ok) ok = mk(&c->cstream, false);
@@ -1381,6 +1389,7 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
         HIPCHK(hipStreamWaitEvent(c->stream, c->ev_pa[s], 0));
         HIPCHK(hipStreamWaitEvent(c->stream, c->ev_pb[s], 0));
     }
+    if (c->knn_gate && c->knn_rec) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_knn, 0));
     tmark(c, 0, c->stream);
     if (c->has_prev) {
         // the previous batch's last frame becomes slot 0 (Tracking::mLastFrame)
@@ -1438,6 +1447,10 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
             c->kt_pending++;
         }
         tmark(c, 10, kst);
+        if (c->knn_gate) {
+            HIPCHK(hipEventRecord(c->ev_knn, kst));
+            c->knn_rec = true;
+        }
         return ODO_OK;
     };
     // schedule 5 runs kNN-2 at the head of the batch's pair stream (the

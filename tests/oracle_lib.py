@@ -263,11 +263,15 @@ def pnp_chi2(Tcw, Xw, ob, cal):
 
 def check_pnp_flags(got_flags, ref_flags, f1, f2, f2_src, Tcw_ref, cal, tag):
     """PnP inlier flags must agree except within a 2 % chi2 margin of the
-    classification threshold (SURVEY §7 hard part 6); returns the number of
-    (marginal) flags that differ."""
+    classification threshold (SURVEY §7 hard part 6), and at most
+    max(2, 1 % of the edges) may differ at all (a systematic shift of
+    borderline edges fails); returns the number of (marginal) flags that
+    differ."""
     bad = np.nonzero(got_flags != ref_flags)[0]
     if bad.size == 0:
         return 0
+    cap = max(2, int(0.01 * int((np.asarray(f2_src) >= 0).sum())))
+    assert bad.size <= cap, f"{tag}: {bad.size} PnP inlier flags differ (cap {cap})"
     src = f2_src[bad]
     assert (src >= 0).all(), f"{tag}: PnP flag differs on a keypoint without a landmark"
     Xw = f1["xyz"][src]
