@@ -70,7 +70,7 @@ class PairResult(C.Structure):
 class KernelForms(C.Structure):
     """odo_kernel_forms (include/odo.h): bit-identical kernel alternatives."""
     _fields_ = [("knn", C.c_int32), ("knn_split", C.c_int32), ("ransac_lanes_min_open", C.c_int32),
-                ("reserved", C.c_int32)]
+                ("pyramid", C.c_int32)]
 
 
 class Config(C.Structure):
@@ -82,6 +82,8 @@ class Config(C.Structure):
 
 KNN_FORM_FP4 = 0   # include/odo.h ODO_KNN_FORM_FP4
 KNN_FORM_VALU = 1  # include/odo.h ODO_KNN_FORM_VALU
+PYRAMID_FORM_FUSED = 0  # include/odo.h ODO_PYRAMID_FORM_FUSED
+PYRAMID_FORM_CHAIN = 1  # include/odo.h ODO_PYRAMID_FORM_CHAIN
 
 
 DETECTOR_ORB_SLAM2 = 0       # include/odo.h ODO_DETECTOR_ORB_SLAM2

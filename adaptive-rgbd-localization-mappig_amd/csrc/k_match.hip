@@ -1377,6 +1377,9 @@ void launch_knn2_mx(hipStream_t st, const uint8_t* q, const int* qn, size_t q_st
         const void* kf = (const void*)k_knn2_f4;
 #endif
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kf, 256, 0);
+        // ODO_KNN_WG_PER_CU (tuning) < occupancy leaves register room to the
+        // co-running extraction kernels
+        if (const char* e = odo_knob("ODO_KNN_WG_PER_CU")) per_cu = std::min(std::max(1, atoi(e)), std::max(1, per_cu));
         resident[f4] = std::max(1, per_cu) * cus;
     }
     if (npairs <= 0 || max_q <= 0) return;

@@ -150,6 +150,7 @@ struct odo_ctx {
     std::vector<LevelDesc> lv_h;
     std::vector<CellDesc> cells_h;
     std::vector<int> rx_off, ry_off, rz_rows;
+    bool pyr_fused = false;  // k_pyramid builds gray + levels (odo_kernel_forms.pyramid, pyramid_fusable)
     LevelDesc* lv = nullptr;
     CellDesc* cells = nullptr;
     ResizeX* rx = nullptr;
@@ -766,6 +767,8 @@ static int build_geometry(odo_ctx* c) {
         c->rz_rows[l] = mr;
         if (resize_lds_bytes(S.pitch, D.w, mr) > 64 * 1024) return fail(ODO_ERR_ARG, "image too wide for the resize band");
     }
+    c->pyr_fused = c->cfg.forms.pyramid != ODO_PYRAMID_FORM_CHAIN &&
+                   pyramid_fusable(c->lv_h.data(), rx.data(), c->rx_off.data(), p.nlevels);
     int e;
     if ((e = dalloc(&c->lv, c->lv_h.size()))) return e;
     if ((e = dalloc(&c->cells, c->cells_h.size()))) return e;
@@ -921,6 +924,11 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
     c->slots = cfg->max_batch + 1;
     if (cfg->forms.knn != ODO_KNN_FORM_FP4 && cfg->forms.knn != ODO_KNN_FORM_VALU) {
         fail(ODO_ERR_ARG, "unknown kNN-2 kernel form");
+        delete c;
+        return nullptr;
+    }
+    if (cfg->forms.pyramid != ODO_PYRAMID_FORM_FUSED && cfg->forms.pyramid != ODO_PYRAMID_FORM_CHAIN) {
+        fail(ODO_ERR_ARG, "unknown pyramid kernel form");
         delete c;
         return nullptr;
     }
@@ -1116,6 +1124,23 @@ int odo_synchronize(odo_ctx* c) {
     return sync_all(c);
 }
 
+// gray (when d_bgr is given) and the pyramid levels of n frames
+static void build_pyramid(odo_ctx* c, hipStream_t st, const uint8_t* d_bgr, uint8_t* pyr, int n) {
+    const size_t P = c->pyr_size;
+    if (c->pyr_fused) {
+        launch_pyramid(st, d_bgr, pyr, (size_t)c->W * c->H * 3, P, c->lv, c->rx, c->ry, c->rx_off.data(),
+                       c->ry_off.data(), c->nlevels, n);
+        return;
+    }
+    if (d_bgr) launch_gray(st, d_bgr, pyr, c->W, c->H, c->lv_h[0].pitch, (size_t)c->W * c->H * 3, P, n);
+    for (int l = 1; l < c->nlevels; l++) {
+        const LevelDesc& S = c->lv_h[l - 1];
+        const LevelDesc& D = c->lv_h[l];
+        launch_resize(st, pyr, P, S.off, S.pitch, D.off, D.pitch, D.w, D.h, RZ_RB, c->rz_rows[l],
+                      c->rx + c->rx_off[l], c->ry + c->ry_off[l], n);
+    }
+}
+
 // Extractor(FAST, ORB, ADAPTIVE) for frames slot0.. of `set` (k_adaptive.hip):
 // threshold-free S map -> band survivors + S histograms -> the per-cell
 // threshold chain over the batch in frame order -> keepStrongest ->
@@ -1175,13 +1200,7 @@ static int run_extract_adaptive_orb(odo_ctx* c, int set, const uint8_t* d_bgr, c
     const size_t slot = fbase(c, set) + slot0;
     uint8_t* pyr = c->pyr + slot * P;
     const int nc = c->ad_ncells, ni = (int)c->oai_h.size(), nb = (int)c->oab_h.size();
-    if (d_bgr) launch_gray(st, d_bgr, pyr, c->W, c->H, c->lv_h[0].pitch, (size_t)c->W * c->H * 3, P, n);
-    for (int l = 1; l < c->nlevels; l++) {
-        const LevelDesc& S = c->lv_h[l - 1];
-        const LevelDesc& D = c->lv_h[l];
-        launch_resize(st, pyr, P, S.off, S.pitch, D.off, D.pitch, D.w, D.h, RZ_RB, c->rz_rows[l],
-                      c->rx + c->rx_off[l], c->ry + c->ry_off[l], n);
-    }
+    build_pyramid(c, st, d_bgr, pyr, n);
     tmark(c, 1, st);
     launch_oa_pyr(st, pyr, P, c->lv_h[0].pitch, c->oac, nc, c->oai, c->oa_buf0, c->oa_buf1, c->cpyr, c->cp_stride, n);
     HIPCHK(hipMemsetAsync(c->ohist, 0, (size_t)n * ni * 256 * sizeof(int), st));
@@ -1214,13 +1233,7 @@ static int run_extract(odo_ctx* c, int set, const uint8_t* d_bgr, const uint16_t
     const size_t P = c->pyr_size;
     const size_t slot = fbase(c, set) + slot0;
     uint8_t* pyr = c->pyr + (size_t)slot * P;
-    if (d_bgr) launch_gray(st, d_bgr, pyr, c->W, c->H, c->lv_h[0].pitch, (size_t)c->W * c->H * 3, P, n);
-    for (int l = 1; l < c->nlevels; l++) {
-        const LevelDesc& S = c->lv_h[l - 1];
-        const LevelDesc& D = c->lv_h[l];
-        launch_resize(st, pyr, P, S.off, S.pitch, D.off, D.pitch, D.w, D.h, RZ_RB, c->rz_rows[l],
-                      c->rx + c->rx_off[l], c->ry + c->ry_off[l], n);
-    }
+    build_pyramid(c, st, d_bgr, pyr, n);
     tmark(c, 1, st);
     const bool split = c->bstream != st;  // blur beside FAST + octree
     if (split) {

@@ -180,6 +180,13 @@ void launch_kp_geometry(hipStream_t st, const orb_kp* kps, const int* nkp, const
 void launch_gray(hipStream_t st, const uint8_t* bgr, uint8_t* pyr, int w, int h, int pitch, size_t in_stride,
                  size_t pyr_stride, int nframes);
 size_t resize_lds_bytes(int spitch, int dw, int max_src_rows);
+// gray + every pyramid level in one launch (one workgroup per frame); bgr may be
+// null (level 0 already in place). pyramid_fusable: the host check of its
+// assumptions (<= 16 levels, <= 4096 px wide, each quad's taps inside 8 bytes)
+void launch_pyramid(hipStream_t st, const uint8_t* bgr, uint8_t* pyr, size_t in_stride, size_t pyr_stride,
+                    const LevelDesc* lv, const ResizeX* rx, const ResizeY* ry, const int* rx_off, const int* ry_off,
+                    int nlevels, int nframes);
+bool pyramid_fusable(const LevelDesc* lv_host, const ResizeX* rx, const int* rx_off, int nlevels);
 void launch_resize(hipStream_t st, uint8_t* pyr, size_t pyr_stride, int src_off, int spitch, int dst_off, int dpitch,
                    int dw, int dh, int rb, int max_src_rows, const ResizeX* xt, const ResizeY* yt, int nframes);
 void launch_fast(hipStream_t st, const uint8_t* pyr, size_t pyr_stride, const CellDesc* cells, const LevelDesc* lv,

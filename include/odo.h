@@ -42,12 +42,15 @@ extern "C" {
  * tuning build, make -C ... tuning). */
 #define ODO_KNN_FORM_FP4 0   /* default: exact sign-vector products on the matrix cores (FP4 operands) */
 #define ODO_KNN_FORM_VALU 1  /* xor + popcount on the VALUs (also taken for train sets above 8192) */
+#define ODO_PYRAMID_FORM_FUSED 0  /* default: one launch, a workgroup per frame builds every level
+                                     (falls back to the chain where its host checks fail) */
+#define ODO_PYRAMID_FORM_CHAIN 1  /* k_gray + one k_resize launch per level */
 typedef struct odo_kernel_forms {
     int32_t knn;                    /* ODO_KNN_FORM_* */
     int32_t knn_split;              /* VALU form: train splits per query block, 1..8 (0 = 2) */
     int32_t ransac_lanes_min_open;  /* open pairs from which the second RANSAC launch takes the
                                        lane-per-hypothesis kernel (0 = 32) */
-    int32_t reserved;
+    int32_t pyramid;                /* ODO_PYRAMID_FORM_*: gray + pyramid levels */
 } odo_kernel_forms;
 
 typedef struct odo_config {
