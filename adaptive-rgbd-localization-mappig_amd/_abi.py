@@ -84,6 +84,7 @@ KNN_FORM_FP4 = 0   # include/odo.h ODO_KNN_FORM_FP4
 KNN_FORM_VALU = 1  # include/odo.h ODO_KNN_FORM_VALU
 PYRAMID_FORM_FUSED = 0  # include/odo.h ODO_PYRAMID_FORM_FUSED
 PYRAMID_FORM_CHAIN = 1  # include/odo.h ODO_PYRAMID_FORM_CHAIN
+PYRAMID_FORM_FUSED_NOBLUR = 2  # include/odo.h ODO_PYRAMID_FORM_FUSED_NOBLUR
 
 
 DETECTOR_ORB_SLAM2 = 0       # include/odo.h ODO_DETECTOR_ORB_SLAM2

@@ -125,140 +125,6 @@ __global__ void __launch_bounds__(256) k_resize(uint8_t* __restrict__ pyr, size_
     }
 }
 
-// ============================================================ fused pyramid
-// k_pyramid: one 1024-thread workgroup per frame builds the whole pyramid,
-// gray (level 0) and then each level from the one before it, with a
-// workgroup barrier between levels instead of eight dependent launches (the
-// chain's per-level drain and launch latency were most of its 0.28 ms alone
-// and 0.35-0.6 ms pipelined per 256 frames, profiles/r03_b). The levels are
-// read back through the CU's own L1 / L2 (every wave of the workgroup is on
-// one CU, so workgroup-scope ordering is all the barrier needs).
-// Resize: thread t owns quad q = t mod nq of the level (4 output pixels) and
-// walks the rows ph, ph + P, ... (ph = t / nq, P = 1024 / nq), so its x taps
-// are loaded once per level into registers: the quad's source bytes lie in
-// the 8-byte window starting at sx0(4q) (host-checked), one v_alignbyte pair
-// per source row brings the window into two registers, and per pixel one
-// v_perm picks (s[sx0], s[sx1]) as a u16 pair for v_dot2 with (a0, a1).
-// Same integer arithmetic as k_resize: h = a0 s0 + a1 s1, out = (b0 h0 +
-// b1 h1 + 2^21) >> 22.
-#define PYR_TH 1024
-struct PyrLevels {
-    int rx_off[16], ry_off[16];
-};
-__global__ void __launch_bounds__(PYR_TH) k_pyramid(const uint8_t* __restrict__ bgr, uint8_t* __restrict__ pyr,
-                                                    size_t in_stride, size_t pyr_stride,
-                                                    const LevelDesc* __restrict__ lv, const ResizeX* __restrict__ xt,
-                                                    const ResizeY* __restrict__ yt, PyrLevels PL, int nlevels) {
-    EXTRACT_PRIO();
-    const int f = blockIdx.x;
-    const int t = threadIdx.x;
-    uint8_t* base = pyr + (size_t)f * pyr_stride;
-    if (bgr) {
-        // level 0: gray, 4 pixels per thread (k_gray's arithmetic)
-        const LevelDesc L0 = lv[0];
-        const int w = L0.w, h = L0.h, pitch = L0.pitch;
-        const uint8_t* src = bgr + (size_t)f * in_stride;
-        const int npix = w * h;
-        if ((w & 3) == 0) {
-            const int nq4 = npix >> 2;
-            for (int q0 = t; q0 < nq4; q0 += 4 * PYR_TH) {
-                uint32_t wv[4][3];
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const int q = q0 + u * PYR_TH;
-                    if (q < nq4) {
-                        const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src + (size_t)q * 12);
-                        wv[u][0] = s32[0], wv[u][1] = s32[1], wv[u][2] = s32[2];
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const int q = q0 + u * PYR_TH;
-                    if (q < nq4) {
-                        const int p0 = q * 4, y = p0 / w, x = p0 - y * w;
-                        uint32_t out = 0;
-#pragma unroll
-                        for (int i = 0; i < 4; i++) {
-                            const int b = 3 * i;
-                            const uint32_t B = (wv[u][b >> 2] >> (8 * (b & 3))) & 0xffu;
-                            const uint32_t G = (wv[u][(b + 1) >> 2] >> (8 * ((b + 1) & 3))) & 0xffu;
-                            const uint32_t R = (wv[u][(b + 2) >> 2] >> (8 * ((b + 2) & 3))) & 0xffu;
-                            out |= ((B * 1868u + G * 9617u + R * 4899u + 8192u) >> 14) << (8 * i);
-                        }
-                        *reinterpret_cast<uint32_t*>(base + (size_t)y * pitch + x) = out;
-                    }
-                }
-            }
-        } else {
-            for (int p = t; p < npix; p += PYR_TH) {
-                const uint8_t* s = src + (size_t)p * 3;
-                const int yy = p / w, xx = p - yy * w;
-                base[(size_t)yy * pitch + xx] =
-                    (uint8_t)(((uint32_t)s[0] * 1868u + (uint32_t)s[1] * 9617u + (uint32_t)s[2] * 4899u + 8192u) >> 14);
-            }
-        }
-    }
-    for (int l = 1; l < nlevels; l++) {
-        __syncthreads();  // level l - 1 is complete
-        const LevelDesc S = lv[l - 1], D = lv[l];
-        const int nq = (D.w + 3) >> 2;
-        const int P = PYR_TH / nq;  // row phases (the host checks nq <= PYR_TH)
-        if (t >= P * nq) continue;
-        const int ph = t / nq, q = t - ph * nq;
-        const ResizeX* X = xt + PL.rx_off[l];
-        const ResizeY* Y = yt + PL.ry_off[l];
-        // the quad's taps: window origin sx0(4q), per-pixel selectors and weights
-        const int x00 = X[4 * q].sx0;
-        const int wb = x00 & ~3, sh = x00 & 3;
-        uint32_t sel[4], wt[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int dx = 4 * q + j;
-            if (dx < D.w) {
-                const ResizeX xj = X[dx];
-                const uint32_t r0 = (uint32_t)(xj.sx0 - x00), r1 = (uint32_t)(xj.sx1 - x00);  // 0..7
-                sel[j] = r0 | (0x0cu << 8) | (r1 << 16) | (0x0cu << 24);
-                wt[j] = (uint32_t)xj.a0 | ((uint32_t)xj.a1 << 16);
-            } else {
-                sel[j] = 0x0c0c0c0cu;  // past the level width: 0 (the row padding)
-                wt[j] = 0;
-            }
-        }
-        const uint8_t* sbase = base + S.off + wb;
-        uint8_t* dbase = base + D.off + 4 * q;
-        auto hsum = [&](const uint8_t* row, uint32_t (&h)[4]) {
-            const uint32_t* w32 = reinterpret_cast<const uint32_t*>(row);
-            const uint32_t w0 = w32[0], w1 = w32[1], w2 = w32[2];
-            const uint32_t A = __builtin_amdgcn_alignbyte(w1, w0, sh), B = __builtin_amdgcn_alignbyte(w2, w1, sh);
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-                h[j] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_perm(B, A, sel[j])),
-                                              __builtin_bit_cast(u16x2, wt[j]), 0u, false);
-            }
-        };
-        for (int y = ph; y < D.h; y += 2 * P) {
-            const int y2 = y + P;
-            const ResizeY Ya = Y[y];
-            ResizeY Yb = Ya;
-            if (y2 < D.h) Yb = Y[y2];
-            uint32_t ha0[4], ha1[4], hb0[4], hb1[4];
-            hsum(sbase + (size_t)Ya.sy0 * S.pitch, ha0);
-            hsum(sbase + (size_t)Ya.sy1 * S.pitch, ha1);
-            hsum(sbase + (size_t)Yb.sy0 * S.pitch, hb0);
-            hsum(sbase + (size_t)Yb.sy1 * S.pitch, hb1);
-            uint32_t pa = 0, pb = 0;
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                pa |= min((__umul24(ha0[j], (uint32_t)Ya.b0) + __umul24(ha1[j], (uint32_t)Ya.b1) + (1u << 21)) >> 22, 255u) << (8 * j);
-                pb |= min((__umul24(hb0[j], (uint32_t)Yb.b0) + __umul24(hb1[j], (uint32_t)Yb.b1) + (1u << 21)) >> 22, 255u) << (8 * j);
-            }
-            *reinterpret_cast<uint32_t*>(dbase + (size_t)y * D.pitch) = pa;
-            if (y2 < D.h) *reinterpret_cast<uint32_t*>(dbase + (size_t)y2 * D.pitch) = pb;
-        }
-    }
-}
-
 // ============================================================ FAST per cell
 __constant__ int c_circle_dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
 __constant__ int c_circle_dy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
@@ -1324,6 +1190,173 @@ __global__ void __launch_bounds__(256) k_blur_rows(const uint8_t* __restrict__ p
     blur_walk<false, BR_R>(s0, dp, (size_t)L.pitch, L.h, y0, top, bottom, store, 0, 0, 0, none, none);
 }
 
+// ============================================================ fused pyramid
+// k_pyramid: one 1024-thread workgroup per frame builds the whole pyramid,
+// gray (level 0) and then each level from the one before it, with a
+// workgroup barrier between levels instead of eight dependent launches (the
+// chain's per-level drain and launch latency were most of its 0.28 ms alone
+// and 0.35-0.6 ms pipelined per 256 frames, profiles/r03_b). The levels are
+// read back through the CU's own L1 / L2 (every wave of the workgroup is on
+// one CU, so workgroup-scope ordering is all the barrier needs).
+// Resize: thread t owns quad q = t mod nq of the level (4 output pixels) and
+// walks the rows ph, ph + P, ... (ph = t / nq, P = 1024 / nq), so its x taps
+// are loaded once per level into registers: the quad's source bytes lie in
+// the 8-byte window starting at sx0(4q) (host-checked), one v_alignbyte pair
+// per source row brings the window into two registers, and per pixel one
+// v_perm picks (s[sx0], s[sx1]) as a u16 pair for v_dot2 with (a0, a1).
+// Same integer arithmetic as k_resize: h = a0 s0 + a1 s1, out = (b0 h0 +
+// b1 h1 + 2^21) >> 22.
+// BLUR: the workgroup also blurs each level (k_blur_rows' strip walks and
+// edge lanes) once the level is complete, beside the resize that reads it,
+// so no separate blur launch follows (uint8 blur pyramid written to `blur`).
+#define PYR_TH 1024
+struct PyrLevels {
+    int rx_off[16], ry_off[16];
+};
+// the 7x7 blur of level l of frame f by the whole workgroup (PYR_TH threads:
+// 64 strip groups of 16 lanes, then the edge lanes)
+ODO_INLINE void pyr_blur_level(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur, size_t pyr_stride,
+                               const LevelDesc* __restrict__ lv, const BlurRows& S, int nlevels, int f, int l,
+                               const LevelDesc& L, int t) {
+    const uint32_t none[3] = {0, 0, 0};
+    const int items = S.base[l + 1] - S.base[l];
+    const int g = t >> 4;
+    for (int it = g; it < items; it += PYR_TH / 16) {
+        const int chunk = it / S.nst[l], strip = it - chunk * S.nst[l];
+        const int q = 1 + strip * 16 + (t & 15);
+        const bool store = q <= S.nq[l];
+        const int x = 4 * (store ? q : S.nq[l]);
+        const int y0 = chunk_y0<BR_R>(chunk, L.h);
+        const bool top = y0 < 3, bottom = y0 + BR_R + 3 > L.h;
+        const uint8_t* s0 = pyr + (size_t)f * pyr_stride + L.off + (x - 4);
+        uint8_t* dp = blur + (size_t)f * pyr_stride + L.off + (size_t)y0 * L.pitch + x;
+        blur_walk<false, BR_R>(s0, dp, (size_t)L.pitch, L.h, y0, top, bottom, store, 0, 0, 0, none, none);
+    }
+    for (int k = S.ebase[l] + t; k < S.ebase[l + 1]; k += PYR_TH)
+        blur_edge_lane(pyr, blur, pyr_stride, lv, S, nlevels, f, k);
+}
+template <bool BLUR>
+__global__ void __launch_bounds__(PYR_TH) k_pyramid(const uint8_t* __restrict__ bgr, uint8_t* __restrict__ pyr,
+                                                    size_t in_stride, size_t pyr_stride,
+                                                    const LevelDesc* __restrict__ lv, const ResizeX* __restrict__ xt,
+                                                    const ResizeY* __restrict__ yt, PyrLevels PL, int nlevels,
+                                                    uint8_t* __restrict__ blur, BlurRows BR) {
+    EXTRACT_PRIO();
+    const int f = blockIdx.x;
+    const int t = threadIdx.x;
+    uint8_t* base = pyr + (size_t)f * pyr_stride;
+    if (bgr) {
+        // level 0: gray, 4 pixels per thread (k_gray's arithmetic)
+        const LevelDesc L0 = lv[0];
+        const int w = L0.w, h = L0.h, pitch = L0.pitch;
+        const uint8_t* src = bgr + (size_t)f * in_stride;
+        const int npix = w * h;
+        if ((w & 3) == 0) {
+            const int nq4 = npix >> 2;
+            for (int q0 = t; q0 < nq4; q0 += 4 * PYR_TH) {
+                uint32_t wv[4][3];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int q = q0 + u * PYR_TH;
+                    if (q < nq4) {
+                        const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src + (size_t)q * 12);
+                        wv[u][0] = s32[0], wv[u][1] = s32[1], wv[u][2] = s32[2];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int q = q0 + u * PYR_TH;
+                    if (q < nq4) {
+                        const int p0 = q * 4, y = p0 / w, x = p0 - y * w;
+                        uint32_t out = 0;
+#pragma unroll
+                        for (int i = 0; i < 4; i++) {
+                            const int b = 3 * i;
+                            const uint32_t B = (wv[u][b >> 2] >> (8 * (b & 3))) & 0xffu;
+                            const uint32_t G = (wv[u][(b + 1) >> 2] >> (8 * ((b + 1) & 3))) & 0xffu;
+                            const uint32_t R = (wv[u][(b + 2) >> 2] >> (8 * ((b + 2) & 3))) & 0xffu;
+                            out |= ((B * 1868u + G * 9617u + R * 4899u + 8192u) >> 14) << (8 * i);
+                        }
+                        *reinterpret_cast<uint32_t*>(base + (size_t)y * pitch + x) = out;
+                    }
+                }
+            }
+        } else {
+            for (int p = t; p < npix; p += PYR_TH) {
+                const uint8_t* s = src + (size_t)p * 3;
+                const int yy = p / w, xx = p - yy * w;
+                base[(size_t)yy * pitch + xx] =
+                    (uint8_t)(((uint32_t)s[0] * 1868u + (uint32_t)s[1] * 9617u + (uint32_t)s[2] * 4899u + 8192u) >> 14);
+            }
+        }
+    }
+    for (int l = 1; l < nlevels; l++) {
+        __syncthreads();  // level l - 1 is complete
+        const LevelDesc S = lv[l - 1], D = lv[l];
+        if (BLUR) pyr_blur_level(pyr, blur, pyr_stride, lv, BR, nlevels, f, l - 1, S, t);
+        const int nq = (D.w + 3) >> 2;
+        const int P = PYR_TH / nq;  // row phases (the host checks nq <= PYR_TH)
+        if (t >= P * nq) continue;
+        const int ph = t / nq, q = t - ph * nq;
+        const ResizeX* X = xt + PL.rx_off[l];
+        const ResizeY* Y = yt + PL.ry_off[l];
+        // the quad's taps: window origin sx0(4q), per-pixel selectors and weights
+        const int x00 = X[4 * q].sx0;
+        const int wb = x00 & ~3, sh = x00 & 3;
+        uint32_t sel[4], wt[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int dx = 4 * q + j;
+            if (dx < D.w) {
+                const ResizeX xj = X[dx];
+                const uint32_t r0 = (uint32_t)(xj.sx0 - x00), r1 = (uint32_t)(xj.sx1 - x00);  // 0..7
+                sel[j] = r0 | (0x0cu << 8) | (r1 << 16) | (0x0cu << 24);
+                wt[j] = (uint32_t)xj.a0 | ((uint32_t)xj.a1 << 16);
+            } else {
+                sel[j] = 0x0c0c0c0cu;  // past the level width: 0 (the row padding)
+                wt[j] = 0;
+            }
+        }
+        const uint8_t* sbase = base + S.off + wb;
+        uint8_t* dbase = base + D.off + 4 * q;
+        auto hsum = [&](const uint8_t* row, uint32_t (&h)[4]) {
+            const uint32_t* w32 = reinterpret_cast<const uint32_t*>(row);
+            const uint32_t w0 = w32[0], w1 = w32[1], w2 = w32[2];
+            const uint32_t A = __builtin_amdgcn_alignbyte(w1, w0, sh), B = __builtin_amdgcn_alignbyte(w2, w1, sh);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+                h[j] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_perm(B, A, sel[j])),
+                                              __builtin_bit_cast(u16x2, wt[j]), 0u, false);
+            }
+        };
+        for (int y = ph; y < D.h; y += 2 * P) {
+            const int y2 = y + P;
+            const ResizeY Ya = Y[y];
+            ResizeY Yb = Ya;
+            if (y2 < D.h) Yb = Y[y2];
+            uint32_t ha0[4], ha1[4], hb0[4], hb1[4];
+            hsum(sbase + (size_t)Ya.sy0 * S.pitch, ha0);
+            hsum(sbase + (size_t)Ya.sy1 * S.pitch, ha1);
+            hsum(sbase + (size_t)Yb.sy0 * S.pitch, hb0);
+            hsum(sbase + (size_t)Yb.sy1 * S.pitch, hb1);
+            uint32_t pa = 0, pb = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                pa |= min((__umul24(ha0[j], (uint32_t)Ya.b0) + __umul24(ha1[j], (uint32_t)Ya.b1) + (1u << 21)) >> 22, 255u) << (8 * j);
+                pb |= min((__umul24(hb0[j], (uint32_t)Yb.b0) + __umul24(hb1[j], (uint32_t)Yb.b1) + (1u << 21)) >> 22, 255u) << (8 * j);
+            }
+            *reinterpret_cast<uint32_t*>(dbase + (size_t)y * D.pitch) = pa;
+            if (y2 < D.h) *reinterpret_cast<uint32_t*>(dbase + (size_t)y2 * D.pitch) = pb;
+        }
+    }
+    if (BLUR) {
+        __syncthreads();  // the last level is complete
+        const LevelDesc L = lv[nlevels - 1];
+        pyr_blur_level(pyr, blur, pyr_stride, lv, BR, nlevels, f, nlevels - 1, L, t);
+    }
+}
+
 // ============================================================ host-side launch helpers
 void upload_extract_constants() { upload_finalize_constants(); }
 
@@ -1336,13 +1369,45 @@ void launch_gray(hipStream_t st, const uint8_t* bgr, uint8_t* pyr, int w, int h,
     dim3 g((w * h / 4 + 255) / 256 + 1, nframes);
     hipLaunchKernelGGL(k_gray, g, dim3(256), 0, st, bgr, pyr, w, h, pitch, in_stride, pyr_stride);
 }
+// k_blur_rows' work plan (strip items and edge lanes per level); false when a
+// level is too small for its strips (the LDS-tiled k_blur then)
+static bool blur_rows_plan(const LevelDesc* lv_host, int nlevels, BlurRows& R) {
+    bool rows = nlevels <= 16;
+    for (int l = 0; l < nlevels; l++) rows = rows && lv_host[l].h >= BR_R && lv_host[l].w >= 12;
+    if (!rows) return false;
+    R = BlurRows{};
+    int acc = 0, eacc = 0;
+    for (int l = 0; l < nlevels; l++) {
+        const LevelDesc& L = lv_host[l];
+        R.base[l] = acc;
+        R.ebase[l] = eacc;
+        R.nq[l] = (L.w - 8) / 4;  // x + 7 <= w - 1: the lane's three dwords stay inside the row
+        R.nst[l] = (R.nq[l] + 15) / 16;
+        R.nch[l] = (L.h + BR_R - 1) / BR_R;
+        acc += R.nst[l] * R.nch[l];
+        eacc += (1 + (L.w + 3) / 4 - (R.nq[l] + 1)) * ((L.h + BR_RE - 1) / BR_RE);
+    }
+    R.base[nlevels] = acc;
+    R.ebase[nlevels] = eacc;
+    return true;
+}
+bool pyramid_blur_fusable(const LevelDesc* lv_host, int nlevels) {
+    BlurRows R;
+    return blur_rows_plan(lv_host, nlevels, R);
+}
 void launch_pyramid(hipStream_t st, const uint8_t* bgr, uint8_t* pyr, size_t in_stride, size_t pyr_stride,
                     const LevelDesc* lv, const ResizeX* rx, const ResizeY* ry, const int* rx_off, const int* ry_off,
-                    int nlevels, int nframes) {
+                    int nlevels, int nframes, uint8_t* blur, const LevelDesc* lv_host) {
     PyrLevels PL{};
     for (int l = 0; l < nlevels && l < 16; l++) PL.rx_off[l] = rx_off[l], PL.ry_off[l] = ry_off[l];
-    hipLaunchKernelGGL(k_pyramid, dim3(nframes), dim3(PYR_TH), 0, st, bgr, pyr, in_stride, pyr_stride, lv, rx, ry, PL,
-                       nlevels);
+    BlurRows BR{};
+    if (blur && blur_rows_plan(lv_host, nlevels, BR)) {
+        hipLaunchKernelGGL(k_pyramid<true>, dim3(nframes), dim3(PYR_TH), 0, st, bgr, pyr, in_stride, pyr_stride, lv,
+                           rx, ry, PL, nlevels, blur, BR);
+        return;
+    }
+    hipLaunchKernelGGL(k_pyramid<false>, dim3(nframes), dim3(PYR_TH), 0, st, bgr, pyr, in_stride, pyr_stride, lv, rx,
+                       ry, PL, nlevels, (uint8_t*)nullptr, BR);
 }
 bool pyramid_fusable(const LevelDesc* lv_host, const ResizeX* rx, const int* rx_off, int nlevels) {
     if (nlevels > 16) return false;
@@ -1404,27 +1469,13 @@ void launch_blur(hipStream_t st, const uint8_t* pyr, uint8_t* blur, size_t pyr_s
                  const LevelDesc* lv_host, int nlevels, int nframes) {
     // k_blur_rows needs BR_R interior rows and one interior quad per level;
     // smaller levels take the LDS-tiled kernel (ODO_BLUR_TILES=1 forces it)
-    bool rows = nlevels <= 16;
-    for (int l = 0; l < nlevels; l++) rows = rows && lv_host[l].h >= BR_R && lv_host[l].w >= 12;
     static const bool tiles = [] {
         const char* e = odo_knob("ODO_BLUR_TILES");
         return e && e[0] == '1';
     }();
-    if (rows && !tiles) {
-        BlurRows R{};
-        int acc = 0, eacc = 0;
-        for (int l = 0; l < nlevels; l++) {
-            const LevelDesc& L = lv_host[l];
-            R.base[l] = acc;
-            R.ebase[l] = eacc;
-            R.nq[l] = (L.w - 8) / 4;  // x + 7 <= w - 1: the lane's three dwords stay inside the row
-            R.nst[l] = (R.nq[l] + 15) / 16;
-            R.nch[l] = (L.h + BR_R - 1) / BR_R;
-            acc += R.nst[l] * R.nch[l];
-            eacc += (1 + (L.w + 3) / 4 - (R.nq[l] + 1)) * ((L.h + BR_RE - 1) / BR_RE);
-        }
-        R.base[nlevels] = acc;
-        R.ebase[nlevels] = eacc;
+    BlurRows R{};
+    if (!tiles && blur_rows_plan(lv_host, nlevels, R)) {
+        const int acc = R.base[nlevels], eacc = R.ebase[nlevels];
         const int eblocks = (eacc + 255) / 256;
         hipLaunchKernelGGL(k_blur_rows, dim3(eblocks + (acc + 15) / 16, nframes), dim3(256), 0, st, pyr, blur,
                            pyr_stride, lv, R, nlevels, eblocks);

@@ -150,7 +150,8 @@ struct odo_ctx {
     std::vector<LevelDesc> lv_h;
     std::vector<CellDesc> cells_h;
     std::vector<int> rx_off, ry_off, rz_rows;
-    bool pyr_fused = false;  // k_pyramid builds gray + levels (odo_kernel_forms.pyramid, pyramid_fusable)
+    bool pyr_fused = false;   // k_pyramid builds gray + levels (odo_kernel_forms.pyramid, pyramid_fusable)
+    bool blur_fused = false;  // ... and the blurred levels (ODO_PYRAMID_FORM_FUSED, pyramid_blur_fusable)
     LevelDesc* lv = nullptr;
     CellDesc* cells = nullptr;
     ResizeX* rx = nullptr;
@@ -767,8 +768,10 @@ static int build_geometry(odo_ctx* c) {
         c->rz_rows[l] = mr;
         if (resize_lds_bytes(S.pitch, D.w, mr) > 64 * 1024) return fail(ODO_ERR_ARG, "image too wide for the resize band");
     }
-    c->pyr_fused = c->cfg.forms.pyramid != ODO_PYRAMID_FORM_CHAIN &&
-                   pyramid_fusable(c->lv_h.data(), rx.data(), c->rx_off.data(), p.nlevels);
+    int pform = c->cfg.forms.pyramid;
+    if (const char* e = odo_knob("ODO_PYRAMID_FORM")) pform = atoi(e);  // tuning build: A/B without a config change
+    c->pyr_fused = pform != ODO_PYRAMID_FORM_CHAIN && pyramid_fusable(c->lv_h.data(), rx.data(), c->rx_off.data(), p.nlevels);
+    c->blur_fused = c->pyr_fused && pform == ODO_PYRAMID_FORM_FUSED && pyramid_blur_fusable(c->lv_h.data(), p.nlevels);
     int e;
     if ((e = dalloc(&c->lv, c->lv_h.size()))) return e;
     if ((e = dalloc(&c->cells, c->cells_h.size()))) return e;
@@ -927,7 +930,8 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
         delete c;
         return nullptr;
     }
-    if (cfg->forms.pyramid != ODO_PYRAMID_FORM_FUSED && cfg->forms.pyramid != ODO_PYRAMID_FORM_CHAIN) {
+    if (cfg->forms.pyramid != ODO_PYRAMID_FORM_FUSED && cfg->forms.pyramid != ODO_PYRAMID_FORM_CHAIN &&
+        cfg->forms.pyramid != ODO_PYRAMID_FORM_FUSED_NOBLUR) {
         fail(ODO_ERR_ARG, "unknown pyramid kernel form");
         delete c;
         return nullptr;
@@ -1125,11 +1129,12 @@ int odo_synchronize(odo_ctx* c) {
 }
 
 // gray (when d_bgr is given) and the pyramid levels of n frames
-static void build_pyramid(odo_ctx* c, hipStream_t st, const uint8_t* d_bgr, uint8_t* pyr, int n) {
+// (and, with blur given and c->blur_fused, the blurred levels in the same launch)
+static void build_pyramid(odo_ctx* c, hipStream_t st, const uint8_t* d_bgr, uint8_t* pyr, int n, uint8_t* blur) {
     const size_t P = c->pyr_size;
     if (c->pyr_fused) {
         launch_pyramid(st, d_bgr, pyr, (size_t)c->W * c->H * 3, P, c->lv, c->rx, c->ry, c->rx_off.data(),
-                       c->ry_off.data(), c->nlevels, n);
+                       c->ry_off.data(), c->nlevels, n, c->blur_fused ? blur : nullptr, c->lv_h.data());
         return;
     }
     if (d_bgr) launch_gray(st, d_bgr, pyr, c->W, c->H, c->lv_h[0].pitch, (size_t)c->W * c->H * 3, P, n);
@@ -1200,7 +1205,7 @@ static int run_extract_adaptive_orb(odo_ctx* c, int set, const uint8_t* d_bgr, c
     const size_t slot = fbase(c, set) + slot0;
     uint8_t* pyr = c->pyr + slot * P;
     const int nc = c->ad_ncells, ni = (int)c->oai_h.size(), nb = (int)c->oab_h.size();
-    build_pyramid(c, st, d_bgr, pyr, n);
+    build_pyramid(c, st, d_bgr, pyr, n, nullptr);
     tmark(c, 1, st);
     launch_oa_pyr(st, pyr, P, c->lv_h[0].pitch, c->oac, nc, c->oai, c->oa_buf0, c->oa_buf1, c->cpyr, c->cp_stride, n);
     HIPCHK(hipMemsetAsync(c->ohist, 0, (size_t)n * ni * 256 * sizeof(int), st));
@@ -1233,9 +1238,9 @@ static int run_extract(odo_ctx* c, int set, const uint8_t* d_bgr, const uint16_t
     const size_t P = c->pyr_size;
     const size_t slot = fbase(c, set) + slot0;
     uint8_t* pyr = c->pyr + (size_t)slot * P;
-    build_pyramid(c, st, d_bgr, pyr, n);
+    build_pyramid(c, st, d_bgr, pyr, n, c->blur + (size_t)slot * P);
     tmark(c, 1, st);
-    const bool split = c->bstream != st;  // blur beside FAST + octree
+    const bool split = c->bstream != st && !c->blur_fused;  // blur beside FAST + octree
     if (split) {
         HIPCHK(hipEventRecord(c->ev_pyr[set], st));
         HIPCHK(hipStreamWaitEvent(c->bstream, c->ev_pyr[set], 0));
@@ -1254,7 +1259,7 @@ static int run_extract(odo_ctx* c, int set, const uint8_t* d_bgr, const uint16_t
     tmark(c, 3, st);
     if (split)
         HIPCHK(hipStreamWaitEvent(st, c->ev_blur[set], 0));
-    else
+    else if (!c->blur_fused)
         launch_blur(st, pyr, c->blur + (size_t)slot * P, P, c->lv, c->lv_h.data(), c->nlevels, n);
     tmark(c, 4, st);
     launch_finalize(st, pyr, c->blur + (size_t)slot * P, P, c->lv, c->nlevels,

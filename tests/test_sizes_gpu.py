@@ -107,25 +107,36 @@ def test_gpu_blur_every_frame_and_level(w, h):
 @pytest.mark.gpu
 @pytest.mark.parametrize("w,h", [(640, 480), (330, 250), (642, 482), (517, 389), (1280, 960), (320, 240)])
 def test_gpu_pyramid_forms_every_frame(w, h):
-    """ComputePyramid (orbextractor.cpp:833-857) through both kernel forms,
-    the one-launch k_pyramid (a workgroup per frame, every level) and the
-    k_gray + per-level k_resize chain, for every frame of a batch, byte for
-    byte against the oracle's pyramid of the frame (cv::resize INTER_LINEAR
-    restated): widths that are not multiples of 4 (k_gray's per-pixel path),
-    quads whose taps reach the row's last byte, 1280x960 (levels up to 320
-    quads wide)."""
+    """ComputePyramid (orbextractor.cpp:833-857) and the 7x7 GaussianBlur of
+    every level (:795-796) through the three kernel forms, the one-launch
+    k_pyramid with its blur (a workgroup per frame: every level, then each
+    level's blur once it is complete), the same without the blur (k_blur_rows
+    launch after it) and the k_gray + per-level k_resize chain, for every
+    frame of a batch, byte for byte against the oracle's pyramid of the frame
+    (cv::resize INTER_LINEAR restated) and the oracle's blur of it: widths
+    that are not multiples of 4 (k_gray's per-pixel path), quads whose taps
+    reach the row's last byte, 1280x960 (levels up to 320 quads wide), and
+    320x240 (levels under 30 rows: the LDS-tiled blur)."""
     pkg = load_pkg()
     n = 5
     bgr, dep, _ = sequence(n, w, h, seed=0x5EED0043)
     lw, lh = (O.C.c_int * 8)(), (O.C.c_int * 8)()
     O.lib().oracle_level_sizes(O.C.byref(O.orb_params(1000)), w, h, lw, lh, (O.C.c_float * 8)(), (O.C.c_int * 8)())
     total = sum(a * b for a, b in zip(lw, lh))
-    refs = []
+    refs, blurs = [], []
     for i in range(n):
         ref = np.zeros(total, np.uint8)
         O.lib().oracle_pyramid(O.ptr(O.gray(bgr[i])), w, h, O.C.byref(O.orb_params(1000)), O.ptr(ref))
         refs.append(ref)
-    for form in (pkg.PYRAMID_FORM_FUSED, pkg.PYRAMID_FORM_CHAIN):
+        rb, off = np.zeros(total, np.uint8), 0
+        for l in range(8):
+            m = lw[l] * lh[l]
+            part = np.zeros(m, np.uint8)
+            O.lib().oracle_blur(O.ptr(np.ascontiguousarray(ref[off:off + m])), lw[l], lh[l], O.ptr(part))
+            rb[off:off + m] = part
+            off += m
+        blurs.append(rb)
+    for form in (pkg.PYRAMID_FORM_FUSED, pkg.PYRAMID_FORM_FUSED_NOBLUR, pkg.PYRAMID_FORM_CHAIN):
         cfg = pkg.default_config(w, h, n, nfeatures=1000, iterations=50, forms={"pyramid": form})
         odo = pkg.Odometry(cfg)
         odo.track_batch_host(bgr, dep)
@@ -133,4 +144,7 @@ def test_gpu_pyramid_forms_every_frame(w, h):
             got = odo.debug_pyramid(i, total)
             bad = np.nonzero(got != refs[i])[0]
             assert bad.size == 0, f"{w}x{h} form {form} frame {i}: {bad.size} px differ, first at {bad[:4]}"
+            got = odo.debug_blur(i, total)
+            bad = np.nonzero(got != blurs[i])[0]
+            assert bad.size == 0, f"{w}x{h} form {form} frame {i}: {bad.size} blurred px differ, first at {bad[:4]}"
         odo.close()
