@@ -1210,6 +1210,12 @@ __global__ void __launch_bounds__(256) k_blur_rows(const uint8_t* __restrict__ p
 // edge lanes) once the level is complete, beside the resize that reads it,
 // so no separate blur launch follows (uint8 blur pyramid written to `blur`).
 #define PYR_TH 1024
+#ifndef PYR_RU
+#define PYR_RU 2  // output rows in flight per thread (resize)
+#endif
+#ifndef PYR_GU
+#define PYR_GU 4  // gray quads in flight per thread
+#endif
 struct PyrLevels {
     int rx_off[16], ry_off[16];
 };
@@ -1253,10 +1259,10 @@ __global__ void __launch_bounds__(PYR_TH) k_pyramid(const uint8_t* __restrict__ 
         const int npix = w * h;
         if ((w & 3) == 0) {
             const int nq4 = npix >> 2;
-            for (int q0 = t; q0 < nq4; q0 += 4 * PYR_TH) {
-                uint32_t wv[4][3];
+            for (int q0 = t; q0 < nq4; q0 += PYR_GU * PYR_TH) {
+                uint32_t wv[PYR_GU][3];
 #pragma unroll
-                for (int u = 0; u < 4; u++) {
+                for (int u = 0; u < PYR_GU; u++) {
                     const int q = q0 + u * PYR_TH;
                     if (q < nq4) {
                         const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src + (size_t)q * 12);
@@ -1264,7 +1270,7 @@ __global__ void __launch_bounds__(PYR_TH) k_pyramid(const uint8_t* __restrict__ 
                     }
                 }
 #pragma unroll
-                for (int u = 0; u < 4; u++) {
+                for (int u = 0; u < PYR_GU; u++) {
                     const int q = q0 + u * PYR_TH;
                     if (q < nq4) {
                         const int p0 = q * 4, y = p0 / w, x = p0 - y * w;
@@ -1330,24 +1336,25 @@ __global__ void __launch_bounds__(PYR_TH) k_pyramid(const uint8_t* __restrict__ 
                                               __builtin_bit_cast(u16x2, wt[j]), 0u, false);
             }
         };
-        for (int y = ph; y < D.h; y += 2 * P) {
-            const int y2 = y + P;
-            const ResizeY Ya = Y[y];
-            ResizeY Yb = Ya;
-            if (y2 < D.h) Yb = Y[y2];
-            uint32_t ha0[4], ha1[4], hb0[4], hb1[4];
-            hsum(sbase + (size_t)Ya.sy0 * S.pitch, ha0);
-            hsum(sbase + (size_t)Ya.sy1 * S.pitch, ha1);
-            hsum(sbase + (size_t)Yb.sy0 * S.pitch, hb0);
-            hsum(sbase + (size_t)Yb.sy1 * S.pitch, hb1);
-            uint32_t pa = 0, pb = 0;
+        for (int y = ph; y < D.h; y += PYR_RU * P) {
+            ResizeY Yr[PYR_RU];
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                pa |= min((__umul24(ha0[j], (uint32_t)Ya.b0) + __umul24(ha1[j], (uint32_t)Ya.b1) + (1u << 21)) >> 22, 255u) << (8 * j);
-                pb |= min((__umul24(hb0[j], (uint32_t)Yb.b0) + __umul24(hb1[j], (uint32_t)Yb.b1) + (1u << 21)) >> 22, 255u) << (8 * j);
+            for (int u = 0; u < PYR_RU; u++) Yr[u] = Y[min(y + u * P, D.h - 1)];
+            uint32_t h0[PYR_RU][4], h1[PYR_RU][4];
+#pragma unroll
+            for (int u = 0; u < PYR_RU; u++) {
+                hsum(sbase + (size_t)Yr[u].sy0 * S.pitch, h0[u]);
+                hsum(sbase + (size_t)Yr[u].sy1 * S.pitch, h1[u]);
             }
-            *reinterpret_cast<uint32_t*>(dbase + (size_t)y * D.pitch) = pa;
-            if (y2 < D.h) *reinterpret_cast<uint32_t*>(dbase + (size_t)y2 * D.pitch) = pb;
+#pragma unroll
+            for (int u = 0; u < PYR_RU; u++) {
+                uint32_t pk = 0;
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    pk |= min((__umul24(h0[u][j], (uint32_t)Yr[u].b0) + __umul24(h1[u][j], (uint32_t)Yr[u].b1) + (1u << 21)) >> 22,
+                              255u) << (8 * j);
+                if (y + u * P < D.h) *reinterpret_cast<uint32_t*>(dbase + (size_t)(y + u * P) * D.pitch) = pk;
+            }
         }
     }
     if (BLUR) {

@@ -1133,6 +1133,14 @@ int odo_synchronize(odo_ctx* c) {
 static void build_pyramid(odo_ctx* c, hipStream_t st, const uint8_t* d_bgr, uint8_t* pyr, int n, uint8_t* blur) {
     const size_t P = c->pyr_size;
     if (c->pyr_fused) {
+        static const bool gray_apart = [] {  // tuning: gray as its own launch before the fused levels
+            const char* e = odo_knob("ODO_PYR_GRAY");
+            return e && e[0] == '1';
+        }();
+        if (gray_apart && d_bgr) {
+            launch_gray(st, d_bgr, pyr, c->W, c->H, c->lv_h[0].pitch, (size_t)c->W * c->H * 3, P, n);
+            d_bgr = nullptr;
+        }
         launch_pyramid(st, d_bgr, pyr, (size_t)c->W * c->H * 3, P, c->lv, c->rx, c->ry, c->rx_off.data(),
                        c->ry_off.data(), c->nlevels, n, c->blur_fused ? blur : nullptr, c->lv_h.data());
         return;
