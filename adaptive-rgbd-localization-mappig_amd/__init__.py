@@ -13,14 +13,15 @@ import numpy as np
 
 from . import _abi
 from ._abi import (DETECTOR_ADAPTIVE_FAST, DETECTOR_ADAPTIVE_ORB, DETECTOR_ORB_SLAM2, KNN_FORM_FP4, KNN_FORM_VALU,
-                   PYRAMID_FORM_CHAIN, PYRAMID_FORM_FUSED, PYRAMID_FORM_FUSED_NOBLUR,
+                   PYRAMID_FORM_AUTO, PYRAMID_FORM_CHAIN, PYRAMID_FORM_FUSED, PYRAMID_FORM_FUSED_NOBLUR,
                    AdaptiveParams, Calib, Config, DMatch, PnPRansacResult,
                    DMATCH_DTYPE, KP_DTYPE, OrbParams, PAIR_DTYPE, PairResult, RansacParams, Rng, check, load, ptr)
 
 __all__ = ["Odometry", "HostFrames", "PinnedResults", "default_config", "load", "KP_DTYPE", "DMATCH_DTYPE", "PAIR_DTYPE", "rng_stream",
            "kabsch", "Calib", "OrbParams", "RansacParams", "Config", "AdaptiveParams", "DETECTOR_ORB_SLAM2",
            "DETECTOR_ADAPTIVE_FAST", "DETECTOR_ADAPTIVE_ORB", "KNN_FORM_FP4", "KNN_FORM_VALU",
-           "PYRAMID_FORM_FUSED", "PYRAMID_FORM_CHAIN", "PYRAMID_FORM_FUSED_NOBLUR"]
+           "PYRAMID_FORM_AUTO", "PYRAMID_FORM_FUSED", "PYRAMID_FORM_CHAIN",
+           "PYRAMID_FORM_FUSED_NOBLUR"]
 
 
 def default_config(width=640, height=480, max_batch=1, nfeatures=1000, iterations=200, seed=0x5EED0000,
@@ -31,7 +32,8 @@ def default_config(width=640, height=480, max_batch=1, nfeatures=1000, iteration
     DETECTOR_ADAPTIVE_ORB (Extractor(ORB, ORB, ADAPTIVE): the cv::ORB cell
     detector of detectoradjuster.cpp:29). forms: odo_kernel_forms fields
     (knn = KNN_FORM_FP4 / KNN_FORM_VALU, knn_split, ransac_lanes_min_open,
-    pyramid = PYRAMID_FORM_FUSED / PYRAMID_FORM_CHAIN / PYRAMID_FORM_FUSED_NOBLUR)."""
+    pyramid = PYRAMID_FORM_AUTO / PYRAMID_FORM_FUSED / PYRAMID_FORM_CHAIN /
+    PYRAMID_FORM_FUSED_NOBLUR)."""
     cfg = Config()
     load().odo_default_config(ptr(cfg), width, height, max_batch)
     cfg.detector = detector

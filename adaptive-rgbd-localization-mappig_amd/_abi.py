@@ -82,9 +82,10 @@ class Config(C.Structure):
 
 KNN_FORM_FP4 = 0   # include/odo.h ODO_KNN_FORM_FP4
 KNN_FORM_VALU = 1  # include/odo.h ODO_KNN_FORM_VALU
-PYRAMID_FORM_FUSED = 0  # include/odo.h ODO_PYRAMID_FORM_FUSED
+PYRAMID_FORM_AUTO = 0  # include/odo.h ODO_PYRAMID_FORM_AUTO
 PYRAMID_FORM_CHAIN = 1  # include/odo.h ODO_PYRAMID_FORM_CHAIN
 PYRAMID_FORM_FUSED_NOBLUR = 2  # include/odo.h ODO_PYRAMID_FORM_FUSED_NOBLUR
+PYRAMID_FORM_FUSED = 3  # include/odo.h ODO_PYRAMID_FORM_FUSED
 
 
 DETECTOR_ORB_SLAM2 = 0       # include/odo.h ODO_DETECTOR_ORB_SLAM2

@@ -139,8 +139,22 @@ __constant__ int c_circle_dy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0
 //      the threshold-free S exceeds th), corners listed in order with their
 //      scores in an LDS map (0 elsewhere),
 //   3. NMS (strictly greater than the 8 neighbours) over the corner list.
+// FAST_CPW cells per workgroup, one wave each (the waves are independent:
+// wave-scope syncs only), so the launch is ncells / FAST_CPW workgroups.
+#ifndef FAST_CPW
+#define FAST_CPW 1
+#endif
+ODO_INLINE void fast_wave_sync() {
+    if (FAST_CPW == 1) {
+        __syncthreads();
+    } else {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
 template <int ROI_MAX>
-__global__ void __launch_bounds__(64) k_fast_cells(const uint8_t* __restrict__ pyr, size_t pyr_stride,
+__global__ void __launch_bounds__(64 * FAST_CPW) k_fast_cells(const uint8_t* __restrict__ pyr, size_t pyr_stride,
                                                    const CellDesc* __restrict__ cells, const LevelDesc* __restrict__ lv,
                                                    uint32_t* __restrict__ cand, int* __restrict__ cand_cnt,
                                                    int ncells, int cell_cap, int ini_th, int min_th) {
@@ -148,19 +162,24 @@ __global__ void __launch_bounds__(64) k_fast_cells(const uint8_t* __restrict__ p
     // ROI rows staged as whole aligned dwords: pixel (r, c) at byte r*RS + sh + c
     constexpr int RS4 = (ROI_MAX + 3 + 3) / 4 + 1;  // dwords per staged row (>= (sh+cols+3)/4)
     constexpr int RS = 4 * RS4;
-    __shared__ __attribute__((aligned(16))) uint32_t roi32[ROI_MAX * RS4];
-    __shared__ __attribute__((aligned(16))) uint32_t score32[ROI_MAX * RS4];
+    __shared__ __attribute__((aligned(16))) uint32_t roi32_w[FAST_CPW][ROI_MAX * RS4];
+    __shared__ __attribute__((aligned(16))) uint32_t score32_w[FAST_CPW][ROI_MAX * RS4];
     // survivor queue; the corner list is compacted into it in place (a wave
     // writes entry n2 + rank <= base + lane only after reading entries
     // base..base+63, so unread entries are never overwritten): 8.9 KB of LDS
     // per single-wave workgroup, 4 waves per SIMD
-    __shared__ uint16_t q1[(ROI_MAX - 6) * (ROI_MAX - 6)];
+    __shared__ uint16_t q1_w[FAST_CPW][(ROI_MAX - 6) * (ROI_MAX - 6)];
+    const int wv = FAST_CPW == 1 ? 0 : (int)(threadIdx.x >> 6);
+    uint32_t* const roi32 = roi32_w[wv];
+    uint32_t* const score32 = score32_w[wv];
+    uint16_t* const q1 = q1_w[wv];
     uint16_t* const q2 = q1;
     const uint8_t* roi = reinterpret_cast<const uint8_t*>(roi32);
     uint8_t* score = reinterpret_cast<uint8_t*>(score32);
     const int f = blockIdx.y;
-    const int ci = blockIdx.x;
-    const int lane = threadIdx.x;
+    const int ci = blockIdx.x * FAST_CPW + wv;
+    if (ci >= ncells) return;  // wave-uniform (no workgroup barriers below)
+    const int lane = threadIdx.x & 63;
     const CellDesc C = cells[ci];
     const LevelDesc L = lv[C.level];
     const uint8_t* img = pyr + (size_t)f * pyr_stride + L.off;
@@ -195,7 +214,7 @@ __global__ void __launch_bounds__(64) k_fast_cells(const uint8_t* __restrict__ p
         const int th = attempt == 0 ? ini_th : min_th;
         const int thc = th < 0 ? 0 : (th > 255 ? 255 : th);
         for (int w = lane; w < (rows * RS4 + 3) >> 2; w += 64) reinterpret_cast<uint4*>(score32)[w] = uint4{0, 0, 0, 0};
-        __syncthreads();
+        fast_wave_sync();
         // 1. compass pre-filter, 4 pixels per lane in 16-bit pairs: dark_k iff
         //    a_k - (v - th) < 0, bright_k iff (v + th) - a_k < 0 (sign bits)
         int n1 = 0;
@@ -271,7 +290,7 @@ __global__ void __launch_bounds__(64) k_fast_cells(const uint8_t* __restrict__ p
 #pragma unroll
             for (int i = 0; i < 4; i++) n1 += __popcll(bi[i]);
         }
-        __syncthreads();
+        fast_wave_sync();
         // 2. segment test + cornerScore<16> of the survivors, two per lane in
         //    packed 16-bit lanes: d = v - p, S = max(best 9-arc min of d,
         //    -(best 9-arc max)). p is a corner at th iff S > th (a 9-arc whose
@@ -332,7 +351,7 @@ __global__ void __launch_bounds__(64) k_fast_cells(const uint8_t* __restrict__ p
             if (c1) q2[n2 + pre + (c0 ? 1 : 0)] = (uint16_t)o1;
             n2 += __popcll(b0) + __popcll(b1);
         }
-        __syncthreads();
+        fast_wave_sync();
         // 3. NMS over the corner list (row-major), ordered compaction
         for (int base = 0; base < n2; base += 64) {
             const int idx = base + lane;
@@ -354,7 +373,7 @@ __global__ void __launch_bounds__(64) k_fast_cells(const uint8_t* __restrict__ p
             count += __popcll(m);
         }
         if (count > 0) break;
-        __syncthreads();
+        fast_wave_sync();
     }
     if (lane == 0) cand_cnt[(size_t)f * ncells + ci] = count < cell_cap ? count : cell_cap;
 }
@@ -1450,18 +1469,19 @@ void launch_fast(hipStream_t st, const uint8_t* pyr, size_t pyr_stride, const Ce
     // LDS sized for the largest cell ROI of the context: the kernel is
     // occupancy-bound (one wave per workgroup), 7.5 KB at 44 px vs 8.9 KB at 48
     // (20 KB at 72, only for small images)
-    dim3 g(ncells, nframes);
+    dim3 g((ncells + FAST_CPW - 1) / FAST_CPW, nframes);
+    const dim3 blk(64 * FAST_CPW);
     if (roi_max <= 40)
-        hipLaunchKernelGGL(k_fast_cells<40>, g, dim3(64), 0, st, pyr, pyr_stride, cells, lv, cand, cand_cnt, ncells,
+        hipLaunchKernelGGL(k_fast_cells<40>, g, blk, 0, st, pyr, pyr_stride, cells, lv, cand, cand_cnt, ncells,
                            cell_cap, ini_th, min_th);
     else if (roi_max <= 44)
-        hipLaunchKernelGGL(k_fast_cells<44>, g, dim3(64), 0, st, pyr, pyr_stride, cells, lv, cand, cand_cnt, ncells,
+        hipLaunchKernelGGL(k_fast_cells<44>, g, blk, 0, st, pyr, pyr_stride, cells, lv, cand, cand_cnt, ncells,
                            cell_cap, ini_th, min_th);
     else if (roi_max <= 48)
-        hipLaunchKernelGGL(k_fast_cells<48>, g, dim3(64), 0, st, pyr, pyr_stride, cells, lv, cand, cand_cnt, ncells,
+        hipLaunchKernelGGL(k_fast_cells<48>, g, blk, 0, st, pyr, pyr_stride, cells, lv, cand, cand_cnt, ncells,
                            cell_cap, ini_th, min_th);
     else  // small images: levels narrower than two 30-px cells
-        hipLaunchKernelGGL(k_fast_cells<FAST_ROI_MAX>, g, dim3(64), 0, st, pyr, pyr_stride, cells, lv, cand, cand_cnt,
+        hipLaunchKernelGGL(k_fast_cells<FAST_ROI_MAX>, g, blk, 0, st, pyr, pyr_stride, cells, lv, cand, cand_cnt,
                            ncells, cell_cap, ini_th, min_th);
 }
 size_t octree_lds_bytes(int node_cap) { return (size_t)76 * node_cap + 1032; }

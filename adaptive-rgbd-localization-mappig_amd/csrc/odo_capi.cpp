@@ -150,8 +150,13 @@ struct odo_ctx {
     std::vector<LevelDesc> lv_h;
     std::vector<CellDesc> cells_h;
     std::vector<int> rx_off, ry_off, rz_rows;
-    bool pyr_fused = false;   // k_pyramid builds gray + levels (odo_kernel_forms.pyramid, pyramid_fusable)
-    bool blur_fused = false;  // ... and the blurred levels (ODO_PYRAMID_FORM_FUSED, pyramid_blur_fusable)
+    // k_pyramid (gray + levels, and the blurred levels) where its host checks
+    // pass (pyramid_fusable, pyramid_blur_fusable) and odo_kernel_forms.pyramid
+    // asks for it: ODO_PYRAMID_FORM_AUTO takes it for batches of at least
+    // PYR_FUSED_MIN_FRAMES frames (a workgroup per frame: a small batch would
+    // leave most CUs idle, one frame takes 0.45 vs 0.28 ms)
+    int pform = ODO_PYRAMID_FORM_AUTO;
+    bool pyr_fusable = false, blur_fusable = false;
     LevelDesc* lv = nullptr;
     CellDesc* cells = nullptr;
     ResizeX* rx = nullptr;
@@ -768,10 +773,10 @@ static int build_geometry(odo_ctx* c) {
         c->rz_rows[l] = mr;
         if (resize_lds_bytes(S.pitch, D.w, mr) > 64 * 1024) return fail(ODO_ERR_ARG, "image too wide for the resize band");
     }
-    int pform = c->cfg.forms.pyramid;
-    if (const char* e = odo_knob("ODO_PYRAMID_FORM")) pform = atoi(e);  // tuning build: A/B without a config change
-    c->pyr_fused = pform != ODO_PYRAMID_FORM_CHAIN && pyramid_fusable(c->lv_h.data(), rx.data(), c->rx_off.data(), p.nlevels);
-    c->blur_fused = c->pyr_fused && pform == ODO_PYRAMID_FORM_FUSED && pyramid_blur_fusable(c->lv_h.data(), p.nlevels);
+    c->pform = c->cfg.forms.pyramid;
+    if (const char* e = odo_knob("ODO_PYRAMID_FORM")) c->pform = atoi(e);  // tuning build: A/B without a config change
+    c->pyr_fusable = pyramid_fusable(c->lv_h.data(), rx.data(), c->rx_off.data(), p.nlevels);
+    c->blur_fusable = c->pyr_fusable && pyramid_blur_fusable(c->lv_h.data(), p.nlevels);
     int e;
     if ((e = dalloc(&c->lv, c->lv_h.size()))) return e;
     if ((e = dalloc(&c->cells, c->cells_h.size()))) return e;
@@ -930,8 +935,7 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
         delete c;
         return nullptr;
     }
-    if (cfg->forms.pyramid != ODO_PYRAMID_FORM_FUSED && cfg->forms.pyramid != ODO_PYRAMID_FORM_CHAIN &&
-        cfg->forms.pyramid != ODO_PYRAMID_FORM_FUSED_NOBLUR) {
+    if (cfg->forms.pyramid < ODO_PYRAMID_FORM_AUTO || cfg->forms.pyramid > ODO_PYRAMID_FORM_FUSED) {
         fail(ODO_ERR_ARG, "unknown pyramid kernel form");
         delete c;
         return nullptr;
@@ -1130,9 +1134,14 @@ int odo_synchronize(odo_ctx* c) {
 
 // gray (when d_bgr is given) and the pyramid levels of n frames
 // (and, with blur given and c->blur_fused, the blurred levels in the same launch)
-static void build_pyramid(odo_ctx* c, hipStream_t st, const uint8_t* d_bgr, uint8_t* pyr, int n, uint8_t* blur) {
+// Returns true when the blurred levels were written too.
+constexpr int PYR_FUSED_MIN_FRAMES = 128;
+static bool build_pyramid(odo_ctx* c, hipStream_t st, const uint8_t* d_bgr, uint8_t* pyr, int n, uint8_t* blur) {
     const size_t P = c->pyr_size;
-    if (c->pyr_fused) {
+    const bool fused = c->pyr_fusable && (c->pform == ODO_PYRAMID_FORM_FUSED || c->pform == ODO_PYRAMID_FORM_FUSED_NOBLUR ||
+                                          (c->pform == ODO_PYRAMID_FORM_AUTO && n >= PYR_FUSED_MIN_FRAMES));
+    if (fused) {
+        if (c->pform == ODO_PYRAMID_FORM_FUSED_NOBLUR || !c->blur_fusable) blur = nullptr;
         static const bool gray_apart = [] {  // tuning: gray as its own launch before the fused levels
             const char* e = odo_knob("ODO_PYR_GRAY");
             return e && e[0] == '1';
@@ -1142,8 +1151,8 @@ static void build_pyramid(odo_ctx* c, hipStream_t st, const uint8_t* d_bgr, uint
             d_bgr = nullptr;
         }
         launch_pyramid(st, d_bgr, pyr, (size_t)c->W * c->H * 3, P, c->lv, c->rx, c->ry, c->rx_off.data(),
-                       c->ry_off.data(), c->nlevels, n, c->blur_fused ? blur : nullptr, c->lv_h.data());
-        return;
+                       c->ry_off.data(), c->nlevels, n, blur, c->lv_h.data());
+        return blur != nullptr;
     }
     if (d_bgr) launch_gray(st, d_bgr, pyr, c->W, c->H, c->lv_h[0].pitch, (size_t)c->W * c->H * 3, P, n);
     for (int l = 1; l < c->nlevels; l++) {
@@ -1152,6 +1161,7 @@ static void build_pyramid(odo_ctx* c, hipStream_t st, const uint8_t* d_bgr, uint
         launch_resize(st, pyr, P, S.off, S.pitch, D.off, D.pitch, D.w, D.h, RZ_RB, c->rz_rows[l],
                       c->rx + c->rx_off[l], c->ry + c->ry_off[l], n);
     }
+    return false;
 }
 
 // Extractor(FAST, ORB, ADAPTIVE) for frames slot0.. of `set` (k_adaptive.hip):
@@ -1246,9 +1256,9 @@ static int run_extract(odo_ctx* c, int set, const uint8_t* d_bgr, const uint16_t
     const size_t P = c->pyr_size;
     const size_t slot = fbase(c, set) + slot0;
     uint8_t* pyr = c->pyr + (size_t)slot * P;
-    build_pyramid(c, st, d_bgr, pyr, n, c->blur + (size_t)slot * P);
+    const bool blur_done = build_pyramid(c, st, d_bgr, pyr, n, c->blur + (size_t)slot * P);
     tmark(c, 1, st);
-    const bool split = c->bstream != st && !c->blur_fused;  // blur beside FAST + octree
+    const bool split = c->bstream != st && !blur_done;  // blur beside FAST + octree
     if (split) {
         HIPCHK(hipEventRecord(c->ev_pyr[set], st));
         HIPCHK(hipStreamWaitEvent(c->bstream, c->ev_pyr[set], 0));
@@ -1267,7 +1277,7 @@ static int run_extract(odo_ctx* c, int set, const uint8_t* d_bgr, const uint16_t
     tmark(c, 3, st);
     if (split)
         HIPCHK(hipStreamWaitEvent(st, c->ev_blur[set], 0));
-    else if (!c->blur_fused)
+    else if (!blur_done)
         launch_blur(st, pyr, c->blur + (size_t)slot * P, P, c->lv, c->lv_h.data(), c->nlevels, n);
     tmark(c, 4, st);
     launch_finalize(st, pyr, c->blur + (size_t)slot * P, P, c->lv, c->nlevels,

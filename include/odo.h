@@ -42,11 +42,12 @@ extern "C" {
  * tuning build, make -C ... tuning). */
 #define ODO_KNN_FORM_FP4 0   /* default: exact sign-vector products on the matrix cores (FP4 operands) */
 #define ODO_KNN_FORM_VALU 1  /* xor + popcount on the VALUs (also taken for train sets above 8192) */
-#define ODO_PYRAMID_FORM_FUSED 0  /* default: one launch, a workgroup per frame builds every level
-                                     and its 7x7 blur (falls back to the chain / a separate blur
-                                     launch where its host checks fail) */
+#define ODO_PYRAMID_FORM_AUTO 0   /* default: FUSED for batches of >= 128 frames, CHAIN below */
 #define ODO_PYRAMID_FORM_CHAIN 1  /* k_gray + one k_resize launch per level, then the blur launch */
-#define ODO_PYRAMID_FORM_FUSED_NOBLUR 2  /* the one-launch pyramid, the blur as its own launch */
+#define ODO_PYRAMID_FORM_FUSED_NOBLUR 2  /* one launch, a workgroup per frame builds every level;
+                                            the blur as its own launch */
+#define ODO_PYRAMID_FORM_FUSED 3  /* one launch: every level and its 7x7 blur (falls back to the
+                                     chain / a separate blur launch where its host checks fail) */
 typedef struct odo_kernel_forms {
     int32_t knn;                    /* ODO_KNN_FORM_* */
     int32_t knn_split;              /* VALU form: train splits per query block, 1..8 (0 = 2) */

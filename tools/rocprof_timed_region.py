@@ -2,7 +2,8 @@
 its rocprofv3 kernel trace (the roofline must recompute
 from a rocprof summary of the timed region).
 
-bench.py (track mode, one GPU) launches one k_gray per batch: 2 untimed
+bench.py (track mode, one GPU) launches one k_gray (or, with the one-launch
+pyramid, one k_pyramid) per batch: 2 untimed
 statistics batches, W warm-up steps, then the K timed steps of the
 HBM-resident leg; then W + K steps of each from-host leg. The timed region of
 a leg is every kernel that starts between the leg's first timed k_gray and the
@@ -24,7 +25,7 @@ rows = list(csv.DictReader(open(trace)))
 for r in rows:
     r["s"], r["e"] = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
 rows.sort(key=lambda r: r["s"])
-gray = [r["s"] for r in rows if r["Kernel_Name"].split("(")[0].endswith("k_gray")]
+gray = [r["s"] for r in rows if r["Kernel_Name"].split("(")[0].endswith("k_gray") or "k_pyramid" in r["Kernel_Name"]]
 
 
 def short(name):
