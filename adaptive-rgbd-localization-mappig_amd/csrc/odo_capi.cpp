@@ -339,6 +339,16 @@ static int pair_stream_priority() {
     return greatest;
 }
 
+// ODO_EXTRACT_STREAM_PRIO=1 (tuning): the extraction stream (the step's
+// critical path) at the highest stream priority
+static int extract_stream_priority() {
+    const char* e = odo_knob("ODO_EXTRACT_STREAM_PRIO");
+    if (!(e && e[0] == '1')) return 0;
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return 0;
+    return greatest;
+}
+
 // Packed layout in the staging buffer: 256-byte aligned sections
 struct Pack {
     size_t off = 0;
@@ -980,6 +990,8 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
             r = hipExtStreamCreateWithCUMask(s, (uint32_t)pmask.size(), pmask.data()) == hipSuccess;
         else if (!prio && xm)
             r = hipExtStreamCreateWithCUMask(s, (uint32_t)xmask.size(), xmask.data()) == hipSuccess;
+        else if (!prio && s == &c->stream && extract_stream_priority() != 0)
+            r = hipStreamCreateWithPriority(s, hipStreamNonBlocking, extract_stream_priority()) == hipSuccess;
         else
             r = prio ? hipStreamCreateWithPriority(s, hipStreamNonBlocking, pair_stream_priority()) == hipSuccess
                      : hipStreamCreateWithFlags(s, hipStreamNonBlocking) == hipSuccess;
