@@ -155,6 +155,28 @@ def host_info():
             "usable_cores": usable_cores(), "model": model}
 
 
+ORACLE_V3 = os.path.join(ROOT, "oracle", "liboracle_v3.so")
+
+
+def oracle_for_baseline():
+    """The oracle build the CPU baselines time: liboracle_v3.so (the same
+    sources for x86-64-v3: AVX2 / FMA / BMI2 / POPCNT, FP contraction off, so
+    the results are identical) when the host CPU has those features, else the
+    x86-64 build. Returns (oracle_lib module, build description)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    try:
+        flags = set(open("/proc/cpuinfo").read().split("flags")[1].split("\n")[0].split())
+    except (OSError, IndexError):
+        flags = set()
+    need = {"avx2", "fma", "bmi2", "popcnt", "movbe", "f16c"}
+    if os.path.exists(ORACLE_V3) and need <= flags:
+        if O.LIB_PATH != ORACLE_V3:
+            O.LIB_PATH, O._lib = ORACLE_V3, None
+        return O, "g++ -O3 -march=x86-64-v3 -ffp-contract=off (oracle/liboracle_v3.so)"
+    return O, "g++ -O3 -ffp-contract=off, baseline x86-64 (oracle/liboracle.so)"
+
+
 def cpu_baseline(bgr, dep, nfeat, iters, n_frames, reps, adaptive=False, threads=None, inner="fast"):
     """The C++ oracle on the first n_frames frames of the same sequence.
 
@@ -166,8 +188,7 @@ def cpu_baseline(bgr, dep, nfeat, iters, n_frames, reps, adaptive=False, threads
     batched contract (ADAPTIVE extraction stays sequential: its thresholds
     carry from frame to frame)."""
     from concurrent.futures import ThreadPoolExecutor
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_lib as O
+    O, build = oracle_for_baseline()
     cal = O.fr1_calib()
     p = O.orb_params(nfeat)
     rp = O.ransac_params(iters)
@@ -225,7 +246,7 @@ def cpu_baseline(bgr, dep, nfeat, iters, n_frames, reps, adaptive=False, threads
 
     all_cores_pass()
     ta = sorted(all_cores_pass() for _ in range(3))[1]
-    return {"fps": n_frames / med, "seconds": med, "reps": reps, "core": core,
+    return {"fps": n_frames / med, "seconds": med, "reps": reps, "core": core, "build": build,
             "stage_ms": {"extract_per_frame": round(ext_ms, 3), "match_ransac_pnp_per_pair": round(trk_ms, 3)},
             "all_cores": {"fps": nf_all / ta, "threads": nthr, "frames": nf_all}}
 
@@ -457,8 +478,7 @@ def pnpransac_mode(args):
            "config": {"workload": f"cfg2 pair {args.width}x{args.height}, {args.nfeatures} kp, "
                                   f"iterations {args.iters}, 3 px, confidence 0.85"}}
     if not args.no_cpu_baseline:
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import oracle_lib as O
+        O, build = oracle_for_baseline()
         c = cfg.calib
         cal = O.Calib(c.fx, c.fy, c.cx, c.cy, c.k1, c.k2, c.p1, c.p2, c.k3, c.depth_factor, c.mbf, c.th_depth)
         cts = []
@@ -467,7 +487,7 @@ def pnpransac_mode(args):
             O.pnp_ransac(Xw, uv, cal, args.iters)
             cts.append((time.perf_counter() - t0) * 1e3)
         out["cpu_baseline"] = {"value": round(float(np.median(cts)), 3), "unit": "ms/call (median of 5)", "cores": 1,
-                               "kind": "port", "sample": "the same call on oracle/pnpransac_ref.cpp"}
+                               "kind": "port", "sample": "the same call on oracle/pnpransac_ref.cpp", "build": build}
     print(json.dumps(out), flush=True)
 
 
@@ -526,15 +546,14 @@ def gicp_mode(args):
            "config": {"workload": f"cfg2 pair {args.width}x{args.height}, {args.nfeatures} kp: RANSAC's matched "
                                   "clouds, guess = RANSAC T12, GeneralizedICP(10, 0.07)"}}
     if not args.no_cpu_baseline:
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import oracle_lib as O
+        O, build = oracle_for_baseline()
         cts = []
         for _ in range(3):
             t0 = time.perf_counter()
             O.gicp(src, tgt, guess, 10, 0.07)
             cts.append((time.perf_counter() - t0) * 1e3)
         out["cpu_baseline"] = {"value": round(float(np.median(cts)), 3), "unit": "ms/call (median of 3)", "cores": 1,
-                               "kind": "port", "sample": "the same call on oracle/gicp_ref.cpp"}
+                               "kind": "port", "sample": "the same call on oracle/gicp_ref.cpp", "build": build}
     print(json.dumps(out), flush=True)
 
 
@@ -928,7 +947,7 @@ def track_mode(args, rank, world, local_rank, dist):
                "sample": f"{nf} frames of the rank-0 {L}-frame closed loop through the C++ oracle's extract + "
                          f"match + RANSAC + PnP, one thread pinned to core {cb['core']}, median of {cb['reps']} "
                          f"passes after a warm-up ({cb['seconds']:.2f} s per pass)",
-               "stage_ms": cb["stage_ms"], "host": hi,
+               "stage_ms": cb["stage_ms"], "host": hi, "build": cb["build"],
                "all_cores": {"value": round(cb["all_cores"]["fps"], 2), "unit": "frames/s",
                              "cores": cb["all_cores"]["threads"],
                              "sample": f"{cb['all_cores']['frames']} frames, frames-parallel thread pool "
