@@ -1250,6 +1250,17 @@ ODO_INLINE double readlane_d(double v, int l) {
 }
 #define LN_WAVES 4
 #define LN_RS 33  // LDS row stride (doubles) of the parked terms
+#ifdef ODO_LANES_PROFILE
+// -DODO_LANES_PROFILE: per wave of the last k_ransac_lanes launch: start, end,
+// loop rounds, sum of active lanes over the rounds, TFC / sweep ticks and the
+// sweep's evaluation / ordered-sum parts (10 ns wall-clock ticks; read by
+// odo_lanes_prof_read, tools/lanes_probe.py)
+#define LPROF_MAX 4096
+__device__ uint64_t g_lprof[LPROF_MAX * 8];
+#define LP(...) __VA_ARGS__
+#else
+#define LP(...)
+#endif
 __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B, RansacCfg cfg, uint32_t* lane_slab,
                                                                    int waves_total, int min_open) {
     __builtin_amdgcn_s_setprio(ODO_WAVE_PRIO);
@@ -1286,6 +1297,8 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
     // waves_total >= open pairs: several waves per pair share its counter;
     // fewer: each wave walks its pairs in turn
     const int iters = cnt > waves_total ? (cnt + waves_total - 1) / waves_total : 1;
+    LP(uint64_t lp_t0 = wall_clock64(); uint64_t lp_rounds = 0, lp_nact = 0, lp_tfc = 0, lp_sweep = 0, lp_fold = 0;
+       uint64_t lp_q = 0; int lp_pair = -1; uint64_t lp_inner = 0, lp_sum = 0;)
     for (int it = 0; it < iters; it++) {
         const int slot = gw + it * waves_total;
         if (cnt > waves_total && slot >= cnt) break;
@@ -1318,6 +1331,7 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
             if (__ballot(h >= 0) == 0) break;
             if (ld_relaxed(&S->done)) break;  // the fold has stopped: nothing will read these
             const bool act = h >= 0;
+            LP(lp_rounds++; lp_nact += __popcll(__ballot(act)); lp_pair = p; lp_q = wall_clock64();)
             // ---- GetTransformFromMatches (ransac.cpp:295-313) in set order
             TFC tf;
             tf.reset();
@@ -1356,6 +1370,7 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
             }
             float T[12];
             tf.get(T);
+            LP(lp_tfc += wall_clock64() - lp_q; lp_q = wall_clock64();)
             double Td[12];
 #pragma unroll
             for (int i = 0; i < 12; i++) Td[i] = (double)T[i];
@@ -1377,6 +1392,7 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
             unsigned c = 0;
             const int pj = lane & 31, hf = lane >> 5;
             for (int c0 = 0; c0 < ng; c0 += 32) {
+                LP(const uint64_t lp_ca = wall_clock64();)
                 const int k = c0 + pj;
                 GoodPt g;
                 bool skip = true;
@@ -1404,6 +1420,7 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
                     }
                     if (a < nact) lres[a * LN_RS + pj] = d;
                 }
+                LP(const uint64_t lp_cb = wall_clock64(); lp_inner += lp_cb - lp_ca;)
                 wave_sync();
                 uint32_t word = 0;
                 if (act) {
@@ -1419,7 +1436,9 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
                     nw[(size_t)(c0 >> 5) * 64 + lane] = word;
                 }
                 wave_sync();
+                LP(lp_sum += wall_clock64() - lp_cb;)
             }
+            LP(lp_sweep += wall_clock64() - lp_q; lp_q = wall_clock64();)
             if (!act) continue;
             nsweep++;
             nref++;
@@ -1460,8 +1479,16 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
                 try_fold(B, cfg, p);
                 h = -1;
             }
+            LP(lp_fold += wall_clock64() - lp_q;)
         }
     }
+#ifdef ODO_LANES_PROFILE
+    if (lane == 0 && gw < LPROF_MAX) {
+        uint64_t* r = g_lprof + (size_t)gw * 8;
+        r[0] = lp_t0, r[1] = wall_clock64(), r[2] = lp_rounds, r[3] = lp_nact, r[4] = lp_tfc, r[5] = lp_sweep,
+        r[6] = lp_inner, r[7] = lp_sum;  // (fold time and pair: lp_fold, lp_pair)
+    }
+#endif
 }
 
 // ---------------------------------------------------------------- final
@@ -1909,6 +1936,15 @@ void launch_ransac_finish(hipStream_t st, void* scratch, int match_cap, int mask
 }
 
 }  // namespace odo
+#ifdef ODO_LANES_PROFILE
+// profile builds only: the per-wave records of the last k_ransac_lanes launch
+extern "C" int odo_lanes_prof_read(uint64_t* out, int n) {
+    n = std::min(n, LPROF_MAX);
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(odo::g_lprof), (size_t)n * 8 * sizeof(uint64_t)) != hipSuccess) return -1;
+    return n;
+}
+#endif
 #ifdef ODO_RANSAC_PROFILE
 // profile builds only: the per-hypothesis records of the last launch
 extern "C" int odo_ransac_prof_read(uint64_t* out, int n, uint64_t* done_t) {
