@@ -307,11 +307,17 @@ __global__ void __launch_bounds__(64 * FAST_CPW) k_fast_cells(const uint8_t* __r
                 o0 = q1[i0];
                 o1 = i1 < n1 ? q1[i1] : o0;
                 const int v0 = roi[o0], v1 = roi[o1];
+                const s16x2 vv = {(short)v0, (short)v1};
                 s16x2 d[16];
 #pragma unroll
                 for (int k = 0; k < 16; k++) {
+                    // the two circle bytes straight into the halves of one
+                    // register (ds_read_u8_d16 / _d16_hi), one packed subtract
                     const int off = c_circle_dy[k] * RS + c_circle_dx[k];
-                    d[k] = s16x2{(short)(v0 - (int)roi[o0 + off]), (short)(v1 - (int)roi[o1 + off])};
+                    s16x2 c;
+                    c.x = (short)roi[o0 + off];
+                    c.y = (short)roi[o1 + off];
+                    d[k] = vv - c;
                 }
                 // best 9-arc min / max: arcs k, k+1 (k even) share the run
                 // d[k+1 .. k+8] (odd 2-, 4-, 8-runs; the smap4 lattice form)

@@ -1250,6 +1250,9 @@ ODO_INLINE double readlane_d(double v, int l) {
 }
 #define LN_WAVES 4
 #define LN_RS 33  // LDS row stride (doubles) of the parked terms
+#ifndef LN_BPERM
+#define LN_BPERM 1  // sweep: hypothesis transforms by ds_bpermute (0: v_readlane pairs)
+#endif
 #ifdef ODO_LANES_PROFILE
 // -DODO_LANES_PROFILE: per wave of the last k_ransac_lanes launch: start, end,
 // loop rounds, sum of active lanes over the rounds, TFC / sweep ticks and the
@@ -1403,6 +1406,16 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
                 const float x1[3] = {g.sx, g.sy, g.sz}, x2[3] = {g.tx, g.ty, g.tz};
                 for (int i = 0; i < nact; i += 2) {
                     const int a = i + hf;  // this half's hypothesis slot
+#if LN_BPERM
+                    // each half fetches its hypothesis' 12 floats from the
+                    // owning lane (ds_bpermute) and widens them (exact: Td is
+                    // (double)T): 12 permutes + 12 conversions instead of 48
+                    // v_readlane, 24 selects and the SGPR hazard nops
+                    const int src = la[min(a, nact - 1)];
+                    double Ta[12];
+#pragma unroll
+                    for (int q = 0; q < 12; q++) Ta[q] = (double)__shfl(T[q], src);
+#else
                     // the two hypotheses' lanes are wave-uniform: v_readlane into
                     // scalars instead of an LDS-routed shuffle per element
                     const int src0 = __builtin_amdgcn_readfirstlane(la[i]);
@@ -1413,6 +1426,7 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
                         const double t0 = readlane_d(Td[q], src0), t1 = readlane_d(Td[q], src1);
                         Ta[q] = hf ? t1 : t0;
                     }
+#endif
                     double d = -1.0;  // not an inlier
                     if (a < nact && !skip) {
                         const double e = error_function2(x1, x2, Ta, K);
