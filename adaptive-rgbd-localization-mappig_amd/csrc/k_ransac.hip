@@ -1250,6 +1250,9 @@ ODO_INLINE double readlane_d(double v, int l) {
 }
 #define LN_WAVES 4
 #define LN_RS 33  // LDS row stride (doubles) of the parked terms
+#ifndef LN_MARKSTEIN
+#define LN_MARKSTEIN 1  // sweep: ErrorFunction2 with Markstein-corrected quotients (0: IEEE divisions)
+#endif
 #ifndef LN_BPERM
 #define LN_BPERM 1  // sweep: hypothesis transforms by ds_bpermute (0: v_readlane pairs)
 #endif
@@ -1429,7 +1432,11 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
 #endif
                     double d = -1.0;  // not an inlier
                     if (a < nact && !skip) {
+#if LN_MARKSTEIN
+                        const double e = error_function2_mk(x1, x2, Ta, K);
+#else
                         const double e = error_function2(x1, x2, Ta, K);
+#endif
                         if (!(e > th) && (e >= 0.0)) d = e;
                     }
                     if (a < nact) lres[a * LN_RS + pj] = d;

@@ -336,6 +336,93 @@ ODO_INLINE double error_function2(const float x1[3], const float x2[3], const do
     return r;
 }
 
+// a / b from y = RN(1 / b) (an IEEE division) by one Markstein correction:
+// q = RN(a y), r = a - b q (exact with the fused multiply-add), RN(q + r y)
+// is the correctly rounded quotient whenever it is a normal number
+// (Markstein's theorem) — bit-identical to a / b there, in three operations
+// instead of the ten of the IEEE division sequence. Zero / non-finite
+// denominators give NaN where the division gives +-inf: the callers below
+// reject the point either way.
+ODO_INLINE double div_mk(double a, double b, double y) {
+    const double q = a * y;
+    const double r = __builtin_fma(-b, q, a);
+    return __builtin_fma(r, y, q);
+}
+// ErrorFunction2 with the nine divisions of the LLT solve done as three
+// reciprocals (L00, L11, L22) and Markstein-corrected quotients. Same value
+// as error_function2 for every point it accepts as an inlier candidate (a
+// finite non-negative result from normal quotients); points with a zero or
+// non-finite pivot end rejected in both (DBL_MAX or a non-finite r).
+ODO_INLINE double error_function2_mk(const float x1[3], const float x2[3], const double T[12], const MahalConst& K) {
+    if (__builtin_isnan(x1[2]) || __builtin_isnan(x2[2])) return ODO_DBL_MAX;
+    const double a0 = x1[0], a1 = x1[1], a2 = x1[2];
+    const double mu0 = x2[0], mu1 = x2[1], mu2 = x2[2];
+    double m0 = ((T[0] * a0 + T[1] * a1) + T[2] * a2) + T[3] * 1.0;
+    double m1 = ((T[4] * a0 + T[5] * a1) + T[6] * a2) + T[7] * 1.0;
+    double m2 = ((T[8] * a0 + T[9] * a1) + T[10] * a2) + T[11] * 1.0;
+    double d0 = m0 - mu0, d1 = m1 - mu1, d2 = m2 - mu2;
+    {
+        double dsq = sum3d(d0 * d0, d1 * d1, d2 * d2);
+        double s1 = fmax(K.raster_cov_x, K.depth_cov);
+        double s2 = fmax(K.raster_cov_x, K.depth_cov);
+        if (dsq > 2.0 * (s1 + s2)) return ODO_DBL_MAX;
+    }
+    const double R00 = T[0], R01 = T[1], R02 = T[2];
+    const double R10 = T[4], R11 = T[5], R12 = T[6];
+    const double R20 = T[8], R21 = T[9], R22 = T[10];
+    const double c00 = K.raster_cov_x * a2, c11 = K.raster_cov_y * a2, c22 = K.depth_cov;
+    const double R[3][3] = {{R00, R01, R02}, {R10, R11, R12}, {R20, R21, R22}};
+    const double Cd[3] = {c00, c11, c22};
+    double RtC[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) RtC[i][j] = R[j][i] * Cd[j];
+    const double cov2_0 = K.raster_cov_x * mu2, cov2_1 = K.raster_cov_y * mu2, cov2_2 = K.depth_cov;
+    double A00 = sum3d(RtC[0][0] * R00, RtC[0][1] * R10, RtC[0][2] * R20) + cov2_0;
+    double A10 = sum3d(RtC[1][0] * R00, RtC[1][1] * R10, RtC[1][2] * R20) + 0.0;
+    double A11 = sum3d(RtC[1][0] * R01, RtC[1][1] * R11, RtC[1][2] * R21) + cov2_1;
+    double A20 = sum3d(RtC[2][0] * R00, RtC[2][1] * R10, RtC[2][2] * R20) + 0.0;
+    double A21 = sum3d(RtC[2][0] * R01, RtC[2][1] * R11, RtC[2][2] * R21) + 0.0;
+    double A22 = sum3d(RtC[2][0] * R02, RtC[2][1] * R12, RtC[2][2] * R22) + cov2_2;
+    if (__builtin_isnan(d2)) return ODO_DBL_MAX;
+    double L00 = A00, L10 = A10, L20 = A20, L11 = A11, L21 = A21, L22 = A22;
+    double i00, i11, i22;
+    {
+        double x = L00;
+        if (x > 0) {
+            L00 = x = sqrt(x);
+            i00 = 1.0 / x;
+            L10 = div_mk(L10, x, i00);
+            L20 = div_mk(L20, x, i00);
+            x = L11 - L10 * L10;
+            if (x > 0) {
+                L11 = x = sqrt(x);
+                i11 = 1.0 / x;
+                L21 -= L20 * L10;
+                L21 = div_mk(L21, x, i11);
+                x = L22 - (L20 * L20 + L21 * L21);
+                if (x > 0) L22 = sqrt(x);
+            } else {
+                i11 = 1.0 / L11;
+            }
+        } else {
+            i00 = 1.0 / L00;
+            i11 = 1.0 / L11;
+        }
+    }
+    i22 = 1.0 / L22;
+    double y0 = div_mk(d0, L00, i00);
+    double y1 = div_mk(d1 - L10 * y0, L11, i11);
+    double y2 = div_mk(d2 - (L20 * y0 + L21 * y1), L22, i22);
+    double z2 = div_mk(y2, L22, i22);
+    double z1 = div_mk(y1 - L21 * z2, L11, i11);
+    double z0 = div_mk(y0 - (L10 * z1 + L20 * z2), L00, i00);
+    double r = sum3d(d0 * z0, d1 * z1, d2 * z2);
+    if (!(r >= 0.0)) return ODO_DBL_MAX;
+    return r;
+}
+
 // ---------------------------------------- glibc TYPE_3 random_r (A.12)
 struct Rng {
     int32_t s[31];

@@ -1,4 +1,4 @@
-# k_ransac_lanes sweep: hypothesis transforms by ds_bpermute vs v_readlane
+# k_ransac_lanes sweep A/B (build_bp0: the variant without the change under test)
 set -e
 R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/${1:-ab6}; mkdir -p $O; cd $R
 P=adaptive-rgbd-localization-mappig_amd
