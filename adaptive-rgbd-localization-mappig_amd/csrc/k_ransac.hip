@@ -40,6 +40,9 @@ struct GoodPt {
 };
 
 #define EV_WAVES_C 4   // waves per k_ransac_eval workgroup (EV_WAVES below)
+#ifndef EV_MARKSTEIN
+#define EV_MARKSTEIN 1  // eval kernels' sweep: Markstein-corrected quotients (error_function2_mk)
+#endif
 #ifndef EV_ROWS0
 #define EV_ROWS0 1  // 4 hypotheses per pair in the first launch (most pairs break at the first); 75.7k vs 74.8k at 2
 #endif
@@ -1044,7 +1047,11 @@ ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int 
                     const GoodPt g = load_pt<CACHED>(P, k);
                     if (!(g.sz == 0.0f || g.tx == 0.0f)) {
                         const float x1[3] = {g.sx, g.sy, g.sz}, x2[3] = {g.tx, g.ty, g.tz};
+#if EV_MARKSTEIN
+                        d = error_function2_mk(x1, x2, Td, K);
+#else
                         d = error_function2(x1, x2, Td, K);
+#endif
                         in = !(d > th) && (d >= 0.0);
                     }
                 }
@@ -1286,11 +1293,6 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
     __shared__ int s_la[LN_WAVES][64];
     double* lres = s_res[wv];
     int* la = s_la[wv];
-    auto stage = [&](const GoodPt* P, int c0, int ng) {
-        wave_sync();  // the previous chunk has been read
-        if (c0 + lane < ng) lp[lane] = P[c0 + lane];
-        wave_sync();
-    };
     const int cnt = B.open_cnt[0];
     if (cnt < min_open || cnt <= 0) return;  // few open pairs: latency matters, k_ransac_eval_list takes them
     uint32_t* slab = lane_slab + (size_t)gw * 2 * B.mask_words * 64;
@@ -1358,11 +1360,21 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
             const bool inset = act && !sample;
             if (__ballot(inset) != 0) {
                 const uint32_t* cw = slab + (size_t)cur * B.mask_words * 64;
+                // the next 64-point chunk (its points and this lane's two set
+                // words) is loaded into registers while this one is folded
+                GoodPt gq = lane < ng ? P[lane] : GoodPt{};
+                uint32_t q0 = inset ? cw[lane] : 0u, q1 = inset && 32 < ng ? cw[64 + lane] : 0u;
                 for (int c0 = 0; c0 < ng; c0 += 64) {
-                    stage(P, c0, ng);
-                    const int w0 = c0 >> 5;
-                    const uint32_t b0 = inset ? cw[(size_t)w0 * 64 + lane] : 0u;
-                    const uint32_t b1 = inset && c0 + 32 < ng ? cw[(size_t)(w0 + 1) * 64 + lane] : 0u;
+                    wave_sync();  // the previous chunk has been read
+                    lp[lane] = gq;
+                    wave_sync();
+                    const uint32_t b0 = q0, b1 = q1;
+                    if (c0 + 64 < ng) {
+                        const int c1 = c0 + 64, w1 = c1 >> 5;
+                        if (c1 + lane < ng) gq = P[c1 + lane];
+                        q0 = inset ? cw[(size_t)w1 * 64 + lane] : 0u;
+                        q1 = inset && c1 + 32 < ng ? cw[(size_t)(w1 + 1) * 64 + lane] : 0u;
+                    }
                     const int n = min(64, ng - c0);
                     for (int j = 0; j < n; j++) {
                         const GoodPt g = lp[j];
@@ -1397,15 +1409,13 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
             double meanError = 0.0;
             unsigned c = 0;
             const int pj = lane & 31, hf = lane >> 5;
+            GoodPt gn = pj < ng ? P[pj] : GoodPt{};  // the next chunk's point, loaded a chunk ahead
             for (int c0 = 0; c0 < ng; c0 += 32) {
                 LP(const uint64_t lp_ca = wall_clock64();)
                 const int k = c0 + pj;
-                GoodPt g;
-                bool skip = true;
-                if (k < ng) {
-                    g = P[k];
-                    skip = g.sz == 0.0f || g.tx == 0.0f;  // sic: target.x (ransac.cpp:326)
-                }
+                const GoodPt g = gn;
+                if (k + 32 < ng) gn = P[k + 32];
+                const bool skip = k >= ng || g.sz == 0.0f || g.tx == 0.0f;  // sic: target.x (ransac.cpp:326)
                 const float x1[3] = {g.sx, g.sy, g.sz}, x2[3] = {g.tx, g.ty, g.tz};
                 for (int i = 0; i < nact; i += 2) {
                     const int a = i + hf;  // this half's hypothesis slot
