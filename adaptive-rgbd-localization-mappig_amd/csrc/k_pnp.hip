@@ -305,6 +305,71 @@ ODO_INLINE bool ldlt_solve6(const double Ain[6][6], const double b[6], double x[
     return true;
 }
 
+// The same solve without Eigen's diagonal pivoting (round 3): the damped
+// normal matrix H + lambda I of the Levenberg trial is symmetric positive
+// definite, for which the pivoted and the unpivoted LDL^T are the same
+// factorization up to rounding; dropping the pivot search and the
+// select-based row / column swaps (most of the pivoted solve's ~900
+// instructions) and dividing by the stored pivot reciprocals halves the
+// trial solve, the longest serial step of a PnP iteration. A pivot <= 0 (not
+// positive definite) fails the solve as in the pivoted form (Eigen's
+// isPositive() check; g2o then rejects the trial).
+ODO_INLINE bool ldlt_solve6_spd(const double Ain[6][6], const double b[6], double x[6]) {
+    double m[6][6];
+#pragma unroll
+    for (int i = 0; i < 6; i++)
+#pragma unroll
+        for (int j = 0; j < 6; j++) m[i][j] = Ain[i][j];
+    double inv[6];
+    bool fail = false;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        double temp[6];
+        if (k > 0) {
+#pragma unroll
+            for (int j = 0; j < k; j++) temp[j] = m[j][j] * m[k][j];
+            double s = 0;
+#pragma unroll
+            for (int j = 0; j < k; j++) s += m[k][j] * temp[j];
+            m[k][k] -= s;
+#pragma unroll
+            for (int i = k + 1; i < 6; i++) {
+                double tt = 0;
+#pragma unroll
+                for (int j = 0; j < k; j++) tt += m[i][j] * temp[j];
+                m[i][k] -= tt;
+            }
+        }
+        const double akk = m[k][k];
+        fail = fail || !(akk > 0);
+        const double ia = 1.0 / akk;
+        inv[k] = ia;
+#pragma unroll
+        for (int i = k + 1; i < 6; i++) m[i][k] *= ia;
+    }
+    if (fail) return false;
+    double y[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        double s = 0;
+#pragma unroll
+        for (int j = 0; j < i; j++) s += m[i][j] * y[j];
+        y[i] = b[i] - s;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; i++) y[i] *= inv[i];
+#pragma unroll
+    for (int i = 5; i >= 0; i--) {
+        double s = 0;
+#pragma unroll
+        for (int j = i + 1; j < 6; j++) s += m[j][i] * y[j];
+        y[i] -= s;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; i++) x[i] = y[i];
+    return true;
+}
+
 // Edge storage: SoA in HBM scratch, [pair][field][cap]. The reference keeps
 // Xw, observations and the information weight as float (cv::Mat / KeyPoint,
 // pnpsolver.cpp:74-125) and widens to double inside g2o; we store the floats.
@@ -390,6 +455,9 @@ ODO_INLINE void huber_rho(double delta, double chi, double rho[3]) {
 #endif
 #define PNP_NT (64 * PNP_NW)
 #define PNP_K 4  // Levenberg trials evaluated per edge pass (one per 16-lane group of wave 0)
+#ifndef PNP_SPD_SOLVE
+#define PNP_SPD_SOLVE 1  // trial solves without Eigen's pivoting (ldlt_solve6_spd; 0: pivoted)
+#endif
 static_assert(PNP_K <= 4, "the trial solves run on the four 16-lane groups of one wave");
 
 // Sum of NV per-lane doubles over the workgroup, the result in every lane.
@@ -627,7 +695,7 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
     SE3 T = T0s;
 #ifdef ODO_PNP_PROFILE
     // -DODO_PNP_PROFILE: phase times (10 ns ticks) of one pair via printf
-    uint64_t tb = 0, tsol = 0, tchi = 0, tcls = 0, t0 = 0, tall = wall_clock64();
+    uint64_t tb = 0, tsol = 0, tchi = 0, tcls = 0, t0 = 0, tall = wall_clock64(), tldlt = 0, texp = 0;
     int nit = 0, ntr = 0;
 #define PP_T0() t0 = wall_clock64()
 #define PP_ACC(x) x += wall_clock64() - t0
@@ -724,8 +792,24 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                     }
                     for (int j = 0; j < 6; j++) Hl[j][j] += lw;
                     double x[6] = {0, 0, 0, 0, 0, 0};
+#ifdef ODO_PNP_PROFILE
+                    const uint64_t ts0 = wall_clock64();
+#endif
+#if PNP_SPD_SOLVE
+                    const bool ok2 = ldlt_solve6_spd(Hl, b, x);
+#else
                     const bool ok2 = ldlt_solve6(Hl, b, x);
+#endif
+#ifdef ODO_PNP_PROFILE
+                    const uint64_t ts1 = wall_clock64();
+#endif
                     const SE3 Tk = se3_mul(se3_exp(x), T);
+#ifdef ODO_PNP_PROFILE
+                    if (wlane == 0) {
+                        tldlt += ts1 - ts0;
+                        texp += wall_clock64() - ts1 + (Tk.t[0] == 12345.678 ? 1 : 0);
+                    }
+#endif
                     double scale = 0;
                     for (int j = 0; j < 6; j++) scale += x[j] * (lw * x[j] + b[j]);
                     scale += 1e-3;
@@ -849,8 +933,8 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
     }
 #ifdef ODO_PNP_PROFILE
     if (lane == 0 && p < 3)
-        printf("PNP p %d ne %d iters %d trials %d: build %lu solve %lu chi %lu classify %lu total %lu (x10ns)\\n", p, ne,
-               nit, ntr, tb, tsol, tchi, tcls, wall_clock64() - tall);
+        printf("PNP p %d ne %d iters %d trials %d: build %lu solve %lu (ldlt %lu exp+mul %lu) chi %lu classify %lu total %lu (x10ns)\n",
+               p, ne, nit, ntr, tb, tsol, tldlt, texp, tchi, tcls, wall_clock64() - tall);
 #endif
     if (lane == 0) {
         double Rm[3][3];
