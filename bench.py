@@ -399,10 +399,26 @@ def hard_leg(pkg, synth, args, B, W, H, device):
         odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=False)
     odo.synchronize()
     dt = time.perf_counter() - t0
+    # SURVEY 8(d) RANSAC roofline on this workload: the stage time of one
+    # untimed step with stage events (one stream) and the step's exact count
+    # of Mahalanobis evaluations
+    odo.set_timing(True)
+    res_t = odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=True)
+    odo.synchronize()
+    tm = odo.timings()
+    odo.set_timing(False)
     Tcw = tj.chain_poses(res[:L], np.linalg.inv(gt[0]).astype(np.float32))
     ate = 1000.0 * tj.ate_rmse(tj.camera_centres(Tcw), gt[:L, :3, 3])
     odo.close()
     ratio = res_q["n_inliers"] / np.maximum(res_q["n_good"], 1)
+    rl = None
+    if tm.get("ransac", 0) > 0:
+        E = float(sum(int(r["n_sweeps"]) * int(r["n_good"]) for r in res_t))
+        tr = tm["ransac"] * 1e-3
+        rl = {"bound": "fp64", "achieved": round(E * RANSAC_FLOPS_PER_EVAL / tr / 1e12, 4), "peak": FP64_PEAK_TFLOPS,
+              "unit": "TFLOP/s", "frac": round(E * RANSAC_FLOPS_PER_EVAL / tr / 1e12 / FP64_PEAK_TFLOPS, 5),
+              "ms": round(tm["ransac"], 4), "evaluations": int(E),
+              "work": f"E = sum(n_sweeps x n_good) x {RANSAC_FLOPS_PER_EVAL} FP64 flops (one stream, stage events)"}
     return {"value": round(B * args.hard_steps / dt, 2), "unit": "frames/s",
             "ms_per_step": round(dt / args.hard_steps * 1e3, 3), "steps": args.hard_steps,
             "workload": f"cfg2 {W}x{H}, {args.nfeatures} kp, RANSAC {args.iters}; image noise sigma 3, depth noise "
@@ -412,7 +428,7 @@ def hard_leg(pkg, synth, args, B, W, H, device):
             "mean_ransac_visited": round(float(np.mean(res_q["visited"])), 1),
             "mean_ransac_sweeps": round(float(np.mean(res_q["n_sweeps"])), 1),
             "mean_pnp_inliers": round(float(np.mean(res_q["pnp_inliers"])), 1),
-            "ate_mm": round(ate, 3)}
+            "ate_mm": round(ate, 3), "ransac_roofline": rl}
 
 
 def pnpransac_mode(args):
