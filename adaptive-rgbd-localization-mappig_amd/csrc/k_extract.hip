@@ -436,6 +436,9 @@ __global__ void __launch_bounds__(OT_THREADS) k_octree(const uint32_t* __restric
                                                        uint32_t* __restrict__ okp, int* __restrict__ ocnt, int okp_stride,
                                                        int node_cap) {
     EXTRACT_PRIO();
+#ifdef ODO_OCTREE_PRIO
+    __builtin_amdgcn_s_setprio(ODO_OCTREE_PRIO);  // tuning: the barrier-bound octree's waves ahead of co-runners
+#endif
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // ODO_OCTREE_LPT=1: grid (frames, levels), so every frame's level 0 (the
     // longest workgroups) is dispatched first (longest-first): 129 vs 190-206

@@ -229,6 +229,9 @@ __global__ void __launch_bounds__(64 * NW) k_finalize_lds(const uint8_t* __restr
                                                       int okp_stride, orb_kp* __restrict__ kps, uint8_t* __restrict__ desc,
                                                       int* __restrict__ nkp, int kp_cap) {
     if (ODO_EXTRACT_PRIO) __builtin_amdgcn_s_setprio(ODO_EXTRACT_PRIO);
+#ifdef ODO_FINALIZE_PRIO
+    __builtin_amdgcn_s_setprio(ODO_FINALIZE_PRIO);  // tuning: finalize's load chains ahead of co-runners
+#endif
     __shared__ uint64_t s_bal[NW][16];
     __shared__ __attribute__((aligned(16))) uint32_t s_disc[16][8];
     __shared__ __attribute__((aligned(16))) uint32_t s_patch[NW * FIN_KPW][FL_KP_DW];
