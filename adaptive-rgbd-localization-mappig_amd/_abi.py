@@ -74,7 +74,7 @@ class KernelForms(C.Structure):
 
 
 class Config(C.Structure):
-    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("max_batch", C.c_int32),
+    _fields_ = [("struct_size", C.c_uint32), ("width", C.c_int32), ("height", C.c_int32), ("max_batch", C.c_int32),
                 ("orb", OrbParams), ("calib", Calib), ("nn_ratio", C.c_float),
                 ("ransac", RansacParams), ("seed", C.c_uint32), ("detector", C.c_int32),
                 ("adaptive", AdaptiveParams), ("forms", KernelForms)]
@@ -110,6 +110,7 @@ PAIR_DTYPE = np.dtype([("T12", "<f4", 16), ("Tcw", "<f4", 16), ("rmse", "<f4"), 
 
 # Every symbol include/odo.h declares, with its ctypes signature.
 SIGNATURES = {
+    "odo_abi_version": (C.c_int, []),
     "odo_default_config": (None, [P, C.c_int, C.c_int, C.c_int]),
     "odo_create": (P, [P, C.c_int]),
     "odo_destroy": (None, [P]),

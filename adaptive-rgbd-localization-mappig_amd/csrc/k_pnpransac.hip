@@ -1111,8 +1111,11 @@ __device__ bool find_homography_lane(const float* Xw, const float* uv, const uin
     return true;
 }
 
-// -> sp[0..5] = (rvec, tvec): the whole wave calls it
-__device__ void extrinsic_init(const float* __restrict__ Xw, const float* __restrict__ uv,
+// -> sp[0..5] = (rvec, tvec): the whole wave calls it. Returns false where
+// cvFindExtrinsicCameraParams2's DLT branch asserts count >= 6 (non-planar
+// points, ni = 5: solvePnPRansac accepts a model with goodCount > 4), i.e.
+// where OpenCV throws cv::Exception out of solvePnPRansac.
+__device__ bool extrinsic_init(const float* __restrict__ Xw, const float* __restrict__ uv,
                                const uint8_t* __restrict__ m, int n, int ni, const PrK& K, double* sp) {
     __shared__ double s_red[78];
     __shared__ double wred[1][78];
@@ -1157,6 +1160,7 @@ __device__ void extrinsic_init(const float* __restrict__ Xw, const float* __rest
             for (int c = 0; c < 3; c++) s_Rt[r * 3 + c] = Vm[c * 3 + r];
     }
     __syncthreads();
+    if (!s_planar && ni < 6) return false;  // CV_Assert(count >= 6) (calibration.cpp, DLT branch)
     double R[9], t[3];
     if (!s_planar) {
         double v[78];
@@ -1294,6 +1298,7 @@ __device__ void extrinsic_init(const float* __restrict__ Xw, const float* __rest
         }
     }
     __syncthreads();
+    return true;
 }
 
 __global__ __launch_bounds__(PR_REFINE_THREADS) void k_pr_refine(const float* __restrict__ Xw,
@@ -1333,7 +1338,23 @@ __global__ __launch_bounds__(PR_REFINE_THREADS) void k_pr_refine(const float* __
     for (int i = threadIdx.x; i < n; i += PR_REFINE_THREADS) mask_out[i] = m[i];
     // solvePnP(inliers, useExtrinsicGuess = false) (pnpransac.cpp:34): the
     // LM starts from cvFindExtrinsicCameraParams2's own pose, not the model
-    extrinsic_init(Xw, uv, m, n, state[2], K, sp);
+    if (!extrinsic_init(Xw, uv, m, n, state[2], K, sp)) {
+        // the refinement would throw (non-planar inliers, fewer than 6): no
+        // pose; the model, mask and counts are reported, ok = -1
+        if (threadIdx.x == 0) {
+            for (int k = 0; k < 3; k++) {
+                res->rvec[k] = res->tvec[k] = 0.0;
+                res->model_rvec[k] = model[6 * best + k];
+                res->model_tvec[k] = model[6 * best + 3 + k];
+            }
+            for (int k = 0; k < 16; k++) res->Tcw[k] = 0.f;
+            res->ok = -1;
+            res->n_inliers = state[2];
+            res->best_iter = best;
+            res->iterations_visited = state[1];
+        }
+        return;
+    }
     double lambdaLg10 = -3, prevErrNorm = DBL_MAX;
     double JtJ[36], JtErr[6];
     int iters = 0;

@@ -897,8 +897,11 @@ extern "C" {
 
 const char* odo_last_error(void) { return g_err.c_str(); }
 
+int odo_abi_version(void) { return ODO_ABI_VERSION; }
+
 void odo_default_config(odo_config* cfg, int width, int height, int max_batch) {
     memset(cfg, 0, sizeof(*cfg));
+    cfg->struct_size = (uint32_t)sizeof(odo_config);
     cfg->width = width;
     cfg->height = height;
     cfg->max_batch = max_batch;
@@ -917,6 +920,14 @@ void odo_default_config(odo_config* cfg, int width, int height, int max_batch) {
 }
 
 odo_ctx* odo_create(const odo_config* cfg, int device) {
+    if (cfg && cfg->struct_size != (uint32_t)sizeof(odo_config)) {
+        char msg[160];
+        snprintf(msg, sizeof(msg), "odo_config.struct_size %u != %zu: the caller was built against another odo.h "
+                 "(ODO_ABI_VERSION %d); fill it with odo_default_config", cfg->struct_size, sizeof(odo_config),
+                 ODO_ABI_VERSION);
+        fail(ODO_ERR_ARG, msg);
+        return nullptr;
+    }
     if (!cfg || cfg->width <= 0 || cfg->height <= 0 || cfg->max_batch <= 0 || cfg->orb.nlevels <= 0 ||
         cfg->orb.nlevels > 16) {
         fail(ODO_ERR_ARG, "invalid config");

@@ -589,6 +589,79 @@ def latency_mode(args):
                                  "path": "include/odo_frontend.hpp classes over the per-stage C-ABI"}}), flush=True)
 
 
+def device_record(rank: int, dev: int):
+    """This rank's GPU: index, name, arch and PCI address (domain:bus:device)."""
+    import torch
+    p = torch.cuda.get_device_properties(dev)
+    return {"rank": rank, "device": dev, "name": p.name, "arch": p.gcnArchName.split(":")[0],
+            "pci": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}",
+            "uuid": str(getattr(p, "uuid", ""))}
+
+
+def gather_devices(rank: int, world: int, dev: int, dist=None):
+    """Every rank's device_record on every rank (all_gather_object over the
+    process group; the list alone for one rank)."""
+    mine = device_record(rank, dev)
+    if world <= 1:
+        return [mine]
+    out = [None] * world
+    dist.all_gather_object(out, mine)
+    return out
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_envs(n: int, port: int, base=None):
+    """Environment of each of n local ranks (one process per GPU): RANK =
+    LOCAL_RANK = r, WORLD_SIZE = n, rendezvous on 127.0.0.1:port."""
+    base = dict(os.environ if base is None else base)
+    base.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL on this host driver
+    out = []
+    for r in range(n):
+        e = dict(base)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        out.append(e)
+    return out
+
+
+def launch_ranks(n: int, argv, script=None) -> int:
+    """`bench.py --gpus N` without a launcher: start N child processes of this
+    script, one per GPU (rank r on device r), and wait for them. Runs before
+    this process imports torch or touches a GPU, and starts children (never
+    execs). Rank 0 prints the JSON line; the exit code is the first failing
+    rank's (the others are terminated)."""
+    import subprocess
+    envs = rank_envs(n, free_port())
+    script = script or os.path.abspath(__file__)
+    procs = [subprocess.Popen([sys.executable, script] + list(argv), env=e) for e in envs]
+    rc = 0
+    try:
+        pending = set(range(n))
+        while pending:
+            for r in sorted(pending):
+                c = procs[r].poll()
+                if c is None:
+                    continue
+                pending.discard(r)
+                if c != 0 and rc == 0:
+                    rc = c
+                    for q in pending:
+                        procs[q].terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -628,6 +701,12 @@ def main():
                          "adaptive-orb: Extractor(ORB, ORB, ADAPTIVE) (cv::ORB cell detector)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU, launched here (torch.distributed.run sets
+        # WORLD_SIZE itself and lands in the branch below)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}")
     if args.mode == "latency":
         latency_mode(args)
         return
@@ -722,6 +801,7 @@ def run_latency(args, W, H, nframes):
 def track_mode(args, rank, world, local_rank, dist):
     import torch
     from importlib import import_module
+    ranks = gather_devices(rank, world, local_rank % max(1, torch.cuda.device_count()), dist)
     pkg = load_pkg()
     synth = load_synth()
     tj = import_module("arlm_amd.trajectory")
@@ -845,10 +925,21 @@ def track_mode(args, rank, world, local_rank, dist):
         if gt_poses is not None:
             Tcw = tj.chain_poses(res[:L], np.linalg.inv(gt_poses[0]).astype(np.float32))
             ate_mm = 1000.0 * tj.ate_rmse(tj.camera_centres(Tcw), gt_poses[:L, :3, 3])
-        # the headline: inputs resident in HBM
+        # the headline: inputs resident in HBM; every batch's pair records
+        # (poses, counts) stream back into a pinned ring inside the timed
+        # region, as Track hands each frame's pose to its caller
+        rows = K + Wm
+        ring = pkg.PinnedResults(rows, B)
         elapsed, submit, (knn_ms, knn_launches) = timed_leg(
-            odo, lambda i: odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=False),
+            odo, lambda i: odo.track_batch_async(d_bgr.data_ptr(), d_dep.data_ptr(), B, ring, i % rows),
             K, Wm, world, dist, coll_dev, ktime)
+        # the records of the last timed batch are those of any batch after the
+        # first (the batch cycles the same loop): check they arrived
+        last = ring.all[(K + Wm - 1) % rows][:B]
+        for f in ("n_matches", "n_inliers", "visited", "n_queries"):
+            if not np.array_equal(last[f], res_q[f]):
+                raise SystemExit(f"timed leg: streamed pair records differ from the untimed batch ({f})")
+        ring.close()
         h_el = sd = None
         h_knn_ms = None
         if args.host_steps > 0:
@@ -997,6 +1088,10 @@ def track_mode(args, rank, world, local_rank, dist):
                        "frames_per_step": B, "global_batch": B * world,
                        "parallelism": (f"sequence chunks x{world} (+1-frame halo, latch broadcast, pose stitch)"
                                        if seq_mode else f"frames x{world}"),
+                       "world_size": world,
+                       "backend": dist.get_backend() if world > 1 else None,
+                       "distinct_devices": len({r["pci"] for r in ranks}),
+                       "ranks": ranks,
                        "mean_keypoints": round(nkp_mean, 1),
                        "mean_knn_queries": round(float(np.mean(res_q["n_queries"])), 1),
                        "mean_matches": round(float(np.mean(ok["n_matches"])), 1),

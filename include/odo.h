@@ -56,7 +56,15 @@ typedef struct odo_kernel_forms {
     int32_t pyramid;                /* ODO_PYRAMID_FORM_*: gray + pyramid levels */
 } odo_kernel_forms;
 
+/* Layout version of the structs below. odo_config starts with its own size,
+ * which odo_default_config fills and odo_create checks, so a caller built
+ * against a header with a different odo_config fails with ODO_ERR_ARG instead
+ * of reading past its struct. */
+#define ODO_ABI_VERSION 4
+int odo_abi_version(void);  /* ODO_ABI_VERSION of the library */
+
 typedef struct odo_config {
+    uint32_t struct_size;       /* sizeof(odo_config): set by odo_default_config */
     int32_t width, height;      /* frame size (all frames of a context share it) */
     int32_t max_batch;          /* frames per odo_track_batch() call */
     odo_orb_params orb;         /* ORBextractor(nFeatures,1.2,8,20,7) extractor.cpp:86 */
@@ -71,7 +79,8 @@ typedef struct odo_config {
 
 typedef struct odo_ctx odo_ctx;
 
-/* Fill cfg with the reference's defaults (FR1 calibration, nfeatures=1000). */
+/* Fill cfg with the reference's defaults (FR1 calibration, nfeatures=1000)
+ * and its struct_size. */
 void odo_default_config(odo_config* cfg, int width, int height, int max_batch);
 
 /* Context: owns the HIP stream, HBM scratch and the cross-frame state the
@@ -213,7 +222,11 @@ int odo_pnp_motion_ba(odo_ctx* ctx, const float* Xw, const float* obs, int n, co
  * iterations = 500, reproj_err = 3.0f, confidence = 0.85, inliers) over the
  * frame's landmark observations. Xw: n x 3 world points (Landmark::GetWorldPos),
  * uv: n x 2 undistorted keypoints (mvKeysUn), in index order. n < 10 returns
- * res->ok = 0 without running (pnpransac.cpp:30). inlier_mask (n, optional):
+ * res->ok = 0 without running (pnpransac.cpp:30); no model with more than 4
+ * inliers gives ok = 0; a best model with exactly 5 non-planar inliers gives
+ * ok = -1 (OpenCV's final solvePnP asserts count >= 6 in its DLT start and
+ * throws; Tcw and rvec/tvec are then zero, the model, mask and n_inliers are
+ * set). inlier_mask (n, optional):
  * the RANSAC inliers (Frame::SetInlier); good_counts (iterations, optional):
  * inliers of every hypothesis, of which the first res->iterations_visited are
  * the ones RANSAC visited. Hypotheses, EPnP, counts, the ordered fold and the

@@ -248,26 +248,49 @@ private:
     int mW = 0, mH = 0, mCap = 0;
 };
 
+// Tag of Frame's zero-copy constructor.
+struct BorrowImages {};
+constexpr BorrowImages kBorrowImages{};
+
 // Core/frame.h: the members the hot path reads and writes.
 class Frame {
 public:
     // Frame(imColor, imDepth, timestamp) (frame.cpp:18-60): BGR8 + depth16
-    // (x5000, Calibration::mDepthFactor). The reference converts the images
-    // into members here (cvtColor / convertTo) for ExtractFeatures; the GPU
-    // does both conversions, so the frame only refers to the caller's images,
-    // which must stay valid until ExtractFeatures (Tracking::Track calls it
-    // right after construction, tracking.cpp:41), and forgets them there.
+    // (x5000, Calibration::mDepthFactor; depth may be null). As the
+    // reference's cv::Mat members (mImColor, mImGray and mImDepth stay with the
+    // frame, keyframe.cpp:27, matcher.cpp:318), the frame keeps its own copies:
+    // the caller may reuse its buffers at once, copies of the frame share
+    // them, and ExtractFeatures may run again. The gray / float conversions
+    // are the GPU's (odo_extract).
     Frame(const uint8_t* bgr, const uint16_t* depth, int width, int height, double timestamp)
-        : mTimestamp(timestamp), mW(width), mH(height), mImColor(bgr), mImDepth(depth), mTcw(Identity()) {}
+        : mTimestamp(timestamp), mW(width), mH(height), mTcw(Identity()) {
+        if (!bgr || width <= 0 || height <= 0) throw std::invalid_argument("odo_hip::Frame: empty image");
+        const size_t npx = (size_t)width * height;
+        auto c = std::make_shared<std::vector<uint8_t>>(bgr, bgr + 3 * npx);
+        mImColor = c->data();
+        mColorOwned = std::move(c);
+        if (depth) {
+            auto d = std::make_shared<std::vector<uint16_t>>(depth, depth + npx);
+            mImDepth = d->data();
+            mDepthOwned = std::move(d);
+        }
+    }
+
+    // Zero-copy opt-in (not a reference constructor): the frame refers to the
+    // caller's images, which must stay valid and unchanged for as long as any
+    // copy of the frame may call ExtractFeatures. For a per-frame loop that
+    // extracts right after construction (Tracking::Track, tracking.cpp:41) it
+    // saves the 1.5 MB host copy.
+    Frame(BorrowImages, const uint8_t* bgr, const uint16_t* depth, int width, int height, double timestamp)
+        : mTimestamp(timestamp), mW(width), mH(height), mImColor(bgr), mImDepth(depth), mTcw(Identity()) {
+        if (!bgr || width <= 0 || height <= 0) throw std::invalid_argument("odo_hip::Frame: empty image");
+    }
 
     // Frame::ExtractFeatures (frame.cpp:135-170): Extract + UndistortKeyPoints +
     // depth backprojection (mvKeys3Dc, mvuRight), landmark slots reset.
     void ExtractFeatures(Extractor* pExtractor) {
-        if (!mImColor) throw std::logic_error("odo_hip::Frame::ExtractFeatures: the frame's images were already used");
         std::vector<float> kun, xyz;
         pExtractor->ExtractFrame(mImColor, mW, mH, 3, mImDepth, mvKeys, mDescriptors, kun, xyz, mvuRight);
-        mImColor = nullptr;
-        mImDepth = nullptr;
         N = mvKeys.size();
         mvKeysUn = mvKeys;
         mvKeys3Dc.resize(N);
@@ -314,10 +337,15 @@ public:
     std::vector<LandmarkPtr> mvpLandmarks;
     std::vector<bool> mvbOutlier;
 
+    const uint8_t* ImColor() const { return mImColor; }
+    const uint16_t* ImDepth() const { return mImDepth; }
+
 private:
     int mW, mH;
-    const uint8_t* mImColor;    // the caller's BGR8 image, until ExtractFeatures
-    const uint16_t* mImDepth;   // the caller's depth16 image (or null), until ExtractFeatures
+    const uint8_t* mImColor = nullptr;   // BGR8: the frame's copy, or the caller's (BorrowImages)
+    const uint16_t* mImDepth = nullptr;  // depth16 (or null), likewise
+    std::shared_ptr<const std::vector<uint8_t>> mColorOwned;  // shared by copies of the frame
+    std::shared_ptr<const std::vector<uint16_t>> mDepthOwned;
 
 public:
     Pose mTcw;
@@ -584,6 +612,9 @@ public:
         Check(odo_pnp_ransac(detail::shared_ctx(), v3D.data(), v2D.data(), n, &cal, 500, 3.0f, 0.85, &r, inl.data(),
                              nullptr),
               "PnPRansac::Compute");
+        // ok = -1: cv::solvePnP's DLT start throws (CV_Assert(count >= 6)),
+        // uncaught in PnPRansac::Compute; ok = 0: "PnPRansac fail" + terminate()
+        if (r.ok < 0) throw std::runtime_error("cv::solvePnP: CV_Assert(count >= 6) in cvFindExtrinsicCameraParams2");
         if (!r.ok) throw std::runtime_error("PnPRansac fail");
         Pose T;
         std::copy(r.Tcw, r.Tcw + 16, T.begin());

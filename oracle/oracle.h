@@ -150,8 +150,8 @@ int32_t oracle_rng_next(odo_rng* r);
 void oracle_libc_rand_stream(uint32_t seed, int n, int32_t* out);
 
 /* Ransac::Iterate(Frame*,Frame*,m12) (ransac.cpp:155-267). xyz1/xyz2:
- * mvKeys3Dc of both frames. inlier_idx receives mvInliers as indices into
- * m12 order? No: as DMatch copies. latch: in/out DepthCovariance static
+ * mvKeys3Dc of both frames. inliers receives mvInliers (ransac.cpp:240, 258)
+ * as DMatch copies in list order. latch: in/out DepthCovariance static
  * (NaN = not yet latched). */
 void oracle_last_ransac_work(int* sweeps, int* fit_points);
 int oracle_ransac(const odo_dmatch* m12, int n12, const float* xyz1, const float* xyz2,
@@ -175,7 +175,10 @@ int oracle_pnp(const float* Xw, const float* obs, int n, const odo_calib* c,
  * uv n x 2 (mvKeysUn). model_out: best RANSAC model (rvec, tvec); rt_out: the
  * refined (rvec, tvec); Tcw: Converter::toHomogeneous(r, t); mask: RANSAC
  * inlier mask (n); good_counts (optional, >= iterations): inliers of every
- * visited hypothesis. Returns 1 (bOK), 0 when n < 10 or no model. */
+ * visited hypothesis. Returns 1 (bOK), 0 when n < 10 or no model, -1 when
+ * the refinement's cvFindExtrinsicCameraParams2 would throw (non-planar
+ * inliers, only 5 of them: its DLT branch asserts count >= 6; model, mask and
+ * n_inliers are set, rt_out and Tcw are zero). */
 int oracle_pnp_ransac(const float* Xw, const float* uv, int n, const odo_calib* c, int iterations, float reproj_err,
                       double confidence, double model_out[6], double rt_out[6], float* Tcw, uint8_t* mask,
                       int* n_inliers, int* best_iter, int* niters_out, int* good_counts);
@@ -190,7 +193,7 @@ void oracle_epnp(const double* pw, const double* uv, int n, const double K[4], d
 void oracle_pnp_refine(const double* M, const double* m, int n, const double K[4], double param[6]);
 /* cvFindExtrinsicCameraParams2's start without an extrinsic guess (DLT /
  * homography; pnpransac.cpp:34 passes useExtrinsicGuess = false) */
-void oracle_pnp_extrinsic_init(const double* M, const double* m, int n, const double K[4], double param[6]);
+int oracle_pnp_extrinsic_init(const double* M, const double* m, int n, const double K[4], double param[6]);
 
 /* ---- GeneralizedICP::Compute(source, target, guess) (generalizedicp.cpp:30-39,
  * 65-89; SURVEY §8(f) rank 4, the ADAPTIVE_RICP fallback of odometry.cpp:46-78):
@@ -207,13 +210,16 @@ void oracle_gicp_covariances(const float* P, int n, double* C);
 void oracle_kabsch(const float* A, const float* B, int n, float* T);
 
 /* One frame pair through the whole path (batched contract):
- * F1 pose = identity, F1 VO landmarks per UpdateLastFrame. */
+ * F1 pose = identity, F1 VO landmarks per UpdateLastFrame. matches and
+ * ransac_inliers (Ransac::mvInliers, in list order; optional) hold up to cap
+ * entries; n_ransac_inliers receives the list length. */
 int oracle_track_pair(const orb_kp* k1, const uint8_t* d1, const float* xyz1, int n1,
                       const orb_kp* k2, const uint8_t* d2, const float* kun2,
                       const float* xyz2, const float* ur2, int n2,
                       const odo_calib* c, float ratio, const odo_ransac_params* rp,
                       uint32_t seed, double* latch, odo_pair_result* res,
-                      uint8_t* inlier_mask /* n2 */, odo_dmatch* matches, int cap);
+                      uint8_t* inlier_mask /* n2 */, odo_dmatch* matches, int cap,
+                      odo_dmatch* ransac_inliers, int* n_ransac_inliers);
 
 #ifdef __cplusplus
 }

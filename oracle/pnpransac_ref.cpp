@@ -930,8 +930,10 @@ bool find_homography(const float* M, const float* m, int n, double H[9]) {
 // smallest eigenvalue as [R | t] up to scale and sign (det(R) > 0),
 // R := U V^T of its SVD, t scaled by |R| / |RR|. -> param = (rvec, tvec).
 // key[i]: the lane of point i (its index among all RANSAC points: the GPU
-// walks the inlier mask over them); null = i.
-void extrinsic_init(const double* M, const double* m, int n, const double K[4], double param[6],
+// walks the inlier mask over them); null = i. Returns false (param untouched)
+// where the DLT branch's CV_Assert(count >= 6) fails: non-planar points and
+// n < 6, which OpenCV reports by throwing cv::Exception.
+bool extrinsic_init(const double* M, const double* m, int n, const double K[4], double param[6],
                     const int* key = nullptr) {
     auto L = [&](int i) { return key ? key[i] : i; };
     const double ifx = 1. / K[0], ify = 1. / K[1];
@@ -1018,7 +1020,8 @@ void extrinsic_init(const double* M, const double* m, int n, const double K[4], 
             t[0] = t[1] = t[2] = 0;
         }
     } else {
-        // non-planar: DLT
+        // non-planar: DLT (calibration.cpp: CV_Assert(count >= 6))
+        if (n < 6) return false;
         WSum64 s(78);
         for (int i = 0; i < n; i++) {
             const double x = -mn[2 * i], y = -mn[2 * i + 1];
@@ -1066,6 +1069,7 @@ void extrinsic_init(const double* M, const double* m, int n, const double K[4], 
     param[3] = t[0];
     param[4] = t[1];
     param[5] = t[2];
+    return true;
 }
 
 }  // namespace
@@ -1092,8 +1096,8 @@ void oracle_pnp_refine(const double* M, const double* m, int n, const double K[4
     refine_lm(M, m, n, K, param);
 }
 
-void oracle_pnp_extrinsic_init(const double* M, const double* m, int n, const double K[4], double param[6]) {
-    extrinsic_init(M, m, n, K, param);
+int oracle_pnp_extrinsic_init(const double* M, const double* m, int n, const double K[4], double param[6]) {
+    return extrinsic_init(M, m, n, K, param) ? 1 : 0;
 }
 
 int oracle_pnp_ransac(const float* Xw, const float* uv, int n, const odo_calib* c, int iterations, float reproj_err,
@@ -1168,7 +1172,16 @@ int oracle_pnp_ransac(const float* Xw, const float* uv, int n, const odo_calib* 
     const int ni = (int)(mi.size() / 2);
     // solvePnP(..., useExtrinsicGuess = false): cvFindExtrinsicCameraParams2's own start
     double p[6];
-    extrinsic_init(Mi.data(), mi.data(), ni, K, p, key.data());
+    if (mask) memcpy(mask, best.data(), n);
+    *n_inliers = maxGoodCount;
+    if (!extrinsic_init(Mi.data(), mi.data(), ni, K, p, key.data())) {
+        // solvePnP's cvFindExtrinsicCameraParams2 throws (non-planar, 5
+        // inliers): the exception leaves solvePnPRansac, and PnPRansac::Compute
+        // does not catch it. Reported as -1: no pose.
+        memset(rt_out, 0, 6 * sizeof(double));
+        memset(Tcw, 0, 16 * sizeof(float));
+        return -1;
+    }
     refine_lm(Mi.data(), mi.data(), ni, K, p);
     memcpy(rt_out, p, sizeof(p));
     // Converter::toHomogeneous(r, t)
@@ -1180,8 +1193,6 @@ int oracle_pnp_ransac(const float* Xw, const float* uv, int n, const odo_calib* 
     }
     Tcw[12] = Tcw[13] = Tcw[14] = 0.f;
     Tcw[15] = 1.f;
-    if (mask) memcpy(mask, best.data(), n);
-    *n_inliers = maxGoodCount;
     return 1;
 }
 

@@ -1347,7 +1347,8 @@ int oracle_track_pair(const orb_kp* k1, const uint8_t* d1, const float* xyz1, in
                       const orb_kp* k2, const uint8_t* d2, const float* kun2, const float* xyz2,
                       const float* ur2, int n2, const odo_calib* c, float ratio,
                       const odo_ransac_params* rp, uint32_t seed, double* latch, odo_pair_result* res,
-                      uint8_t* inlier_mask, odo_dmatch* matches, int cap) {
+                      uint8_t* inlier_mask, odo_dmatch* matches, int cap,
+                      odo_dmatch* ransac_inliers, int* n_ransac_inliers) {
     (void)k1;
     (void)k2;
     memset(res, 0, sizeof(*res));
@@ -1369,6 +1370,7 @@ int oracle_track_pair(const orb_kp* k1, const uint8_t* d1, const float* xyz1, in
     memcpy(res->Tcw, I, sizeof(I));
     res->rmse = 1e6f;
     for (int i = 0; i < n2; i++) inlier_mask[i] = 0;
+    if (n_ransac_inliers) *n_ransac_inliers = 0;
     if (nm < 20) return nm;  // TrackFrame: nmatches < 20 -> return (tracking.cpp:201)
     odo_rng rng;
     oracle_rng_seed(&rng, seed);
@@ -1377,6 +1379,14 @@ int oracle_track_pair(const orb_kp* k1, const uint8_t* d1, const float* xyz1, in
     res->ransac_ok = oracle_ransac(m.data(), nm, xyz1, xyz2, rp, &rng, latch, res->T12, &res->rmse,
                                    inl.data(), &ninl, &visited, &ngood);
     res->n_inliers = ninl;
+    // Ransac::mvInliers (ransac.cpp:240 / 258): read by DrawMatches
+    // (tracking.cpp:205) and copied into F2's flags in RANSAC mode
+    // (odometry.cpp:75-76)
+    if (ransac_inliers && n_ransac_inliers) {
+        const int nc = std::min(ninl, cap);
+        for (int i = 0; i < nc; i++) ransac_inliers[i] = inl[i];
+        *n_ransac_inliers = nc;
+    }
     res->visited = visited;
     res->n_good = ngood;
     res->n_sweeps = g_last_sweeps;

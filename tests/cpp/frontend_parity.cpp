@@ -170,8 +170,22 @@ static int run(int argc, char** argv) {
     int proj_checked = -1, gicp_checked = 0, pnpransac_checked = 0;
     double max_dT = 0;
     for (int t = 0; t < F; t++) {
-        auto cur = std::make_unique<odo_hip::Frame>(&bgr[npx * 3 * t], &dep[npx * t], W, H, 0.033 * t);
+        // the frame keeps its own images: built from scratch
+        // buffers that are overwritten before ExtractFeatures
+        vector<uint8_t> sb(&bgr[npx * 3 * t], &bgr[npx * 3 * (t + 1)]);
+        vector<uint16_t> sd(&dep[npx * t], &dep[npx * (t + 1)]);
+        auto cur = std::make_unique<odo_hip::Frame>(sb.data(), sd.data(), W, H, 0.033 * t);
+        std::fill(sb.begin(), sb.end(), (uint8_t)0x5A);
+        std::fill(sd.begin(), sd.end(), (uint16_t)0);
         cur->ExtractFeatures(&extractor);
+        if (t == 0 && !adaptive && !adaptive_orb) {
+            // a copy of the frame shares the images and extracts again
+            odo_hip::Frame cp = *cur;
+            cp.ExtractFeatures(&extractor);
+            EXPECT(cp.mvKeys.size() == cur->N && cp.mDescriptors == cur->mDescriptors &&
+                       cp.mvKeys3Dc.size() == cur->N,
+                   "frame 0: re-extraction from a copy of the frame differs");
+        }
 
         OracleFrame o;
         o.kps.resize(cap);
@@ -228,11 +242,12 @@ static int run(int argc, char** argv) {
 
             odo_pair_result r;
             vector<uint8_t> mask(std::max(n, 1));
-            vector<odo_dmatch> om(std::max((int)olast.kps.size(), 1));
+            vector<odo_dmatch> om(std::max((int)olast.kps.size(), 1)), oinl(om.size());
+            int noinl = 0;
             const int onm = oracle_track_pair(olast.kps.data(), olast.desc.data(), olast.xyz.data(),
                                               (int)olast.kps.size(), o.kps.data(), o.desc.data(), o.kun.data(),
                                               o.xyz.data(), o.ur.data(), n, &cal, 0.9f, &rp, pseed, &latch, &r,
-                                              mask.data(), om.data(), (int)om.size());
+                                              mask.data(), om.data(), (int)om.size(), oinl.data(), &noinl);
             EXPECT((int)nmatches == onm, "pair %d: %zu matches vs oracle %d", t, nmatches, onm);
             if ((int)nmatches == onm)
                 EXPECT(memcmp(vMatches12.data(), om.data(), onm * sizeof(odo_dmatch)) == 0, "pair %d: match list", t);
@@ -242,6 +257,10 @@ static int run(int argc, char** argv) {
                 EXPECT(memcmp(T12.data(), r.T12, 64) == 0, "pair %d: mT12", t);
                 EXPECT((int)ransac.mvInliers.size() == r.n_inliers, "pair %d: inliers %zu vs %d", t,
                        ransac.mvInliers.size(), r.n_inliers);
+                // Ransac::mvInliers entry for entry (ransac.cpp:240, 258)
+                if ((int)ransac.mvInliers.size() == noinl)
+                    EXPECT(memcmp(ransac.mvInliers.data(), oinl.data(), noinl * sizeof(odo_dmatch)) == 0,
+                           "pair %d: mvInliers list", t);
                 EXPECT(ransac.rmse == r.rmse, "pair %d: rmse %.9g vs %.9g", t, ransac.rmse, r.rmse);
                 EXPECT(pnp == r.pnp_inliers, "pair %d: PnP inliers %d vs %d", t, pnp, r.pnp_inliers);
                 double d = 0;

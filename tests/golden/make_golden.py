@@ -51,7 +51,7 @@ def main():
     np.savez_compressed(os.path.join(HERE, "pair_ransac_pnp.npz"), seed=np.array([seed], np.uint32),
                         iters=np.array([ITERS], np.int32), matches=matches, pnp_inlier_mask=mask,
                         T12=np.array(r.T12, np.float32), Tcw=np.array(r.Tcw, np.float32),
-                        rmse=np.array([r.rmse], np.float32),
+                        rmse=np.array([r.rmse], np.float32), ransac_inliers=r.inliers,
                         counts=np.array([r.n_matches, r.n_good, r.n_inliers, r.ransac_ok, r.pnp_inliers, r.visited],
                                         np.int32),
                         latch=np.array([latch], np.float64))

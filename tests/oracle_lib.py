@@ -109,7 +109,7 @@ def lib():
             "oracle_pnp": (C.c_int, [P, P, C.c_int, P, P, P, P]),
             "oracle_kabsch": (None, [P, P, C.c_int, P]),
             "oracle_track_pair": (C.c_int, [P, P, P, C.c_int, P, P, P, P, P, C.c_int, P, C.c_float, P,
-                                            C.c_uint32, P, P, P, P, C.c_int]),
+                                            C.c_uint32, P, P, P, P, C.c_int, P, P]),
             "oracle_adaptive_default": (None, [P]),
             "oracle_image_bounds": (None, [P, C.c_int, C.c_int, P]),
             "oracle_projection_match": (C.c_int, [P, P, C.c_int, P, P, P, C.c_int, P, P, P, C.c_float, C.c_float,
@@ -136,7 +136,7 @@ def lib():
             "oracle_rodrigues_inv": (None, [P, P]),
             "oracle_epnp": (None, [P, P, C.c_int, P, P]),
             "oracle_pnp_refine": (None, [P, P, C.c_int, P, P]),
-            "oracle_pnp_extrinsic_init": (None, [P, P, C.c_int, P, P]),
+            "oracle_pnp_extrinsic_init": (C.c_int, [P, P, C.c_int, P, P]),
             "oracle_gicp": (C.c_int, [P, C.c_int, P, C.c_int, P, C.c_int, C.c_double, P, P, P, P]),
             "oracle_gicp_covariances": (None, [P, C.c_int, P]),
         }
@@ -188,17 +188,36 @@ def knn2(q: np.ndarray, t: np.ndarray):
 
 
 def track_pair(f1, f2, calib: Calib, rp: RansacParams, seed: int, latch=float("nan"), ratio=0.9):
+    """One pair through the oracle's Track path. Returns (PairResult, PnP
+    inlier mask over F2, KnnMatch list, latch); the PairResult also carries
+    `inliers`, Ransac::mvInliers as a DMATCH_DTYPE array in list order
+    (ransac.cpp:240, 258)."""
     n1, n2 = len(f1["kps"]), len(f2["kps"])
     res = PairResult()
     mask = np.zeros(max(n2, 1), np.uint8)
     matches = np.zeros(max(n1, 1), DMATCH_DTYPE)
+    rinl = np.zeros(max(n1, 1), DMATCH_DTYPE)
+    nr = C.c_int(0)
     lat = C.c_double(latch)
     L = lib()
     nm = L.oracle_track_pair(ptr(f1["kps"]), ptr(f1["desc"]), ptr(f1["xyz"]), n1,
                              ptr(f2["kps"]), ptr(f2["desc"]), ptr(f2["kun"]), ptr(f2["xyz"]), ptr(f2["ur"]), n2,
                              C.byref(calib), ratio, C.byref(rp), seed, C.byref(lat), C.byref(res),
-                             ptr(mask), ptr(matches), max(n1, 1))
+                             ptr(mask), ptr(matches), max(n1, 1), ptr(rinl), C.byref(nr))
+    assert nr.value == res.n_inliers
+    res.inliers = rinl[:nr.value]
     return res, mask[:n2], matches[:nm], lat.value
+
+
+def check_ransac_inliers(gpu_pair, ref, tag):
+    """The batched path's RANSAC inlier list (the good-match list masked by
+    the kernel's inlier bits) equals Ransac::mvInliers entry for entry:
+    queryIdx, trainIdx, imgIdx and distance, in order."""
+    got = gpu_pair["good"][gpu_pair["ransac_inliers"].astype(bool)]
+    exp = ref.inliers
+    assert len(got) == len(exp), f"{tag}: RANSAC inlier list length {len(got)} vs {len(exp)}"
+    assert np.array_equal(got, exp), (f"{tag}: RANSAC inlier list differs at "
+                                      f"{np.nonzero(got != exp)[0][:8]}")
 
 
 def adaptive_params() -> AdaptiveParams:

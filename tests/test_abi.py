@@ -52,6 +52,21 @@ def test_pair_seed_is_splitmix64():
     assert pkg.pair_seed(0, 0) == 0xE220A8397B1DCDAF & 0xFFFFFFFF
 
 
+def test_config_struct_size_checked():
+    """odo_config carries its own size; a caller built against a
+    different odo.h (a smaller or larger struct) fails in odo_create with a
+    clear message instead of reading past its struct (checked before any
+    device call, so this runs on CPU)."""
+    pkg = load_pkg()
+    lib = pkg.load()
+    assert lib.odo_abi_version() == 4
+    cfg = pkg.default_config(640, 480, 1)
+    assert cfg.struct_size == C.sizeof(pkg._abi.Config)
+    cfg.struct_size -= 8  # an older, shorter odo_config
+    assert not lib.odo_create(C.byref(cfg), 0)
+    assert b"struct_size" in lib.odo_last_error()
+
+
 @pytest.mark.skipif(gpu_available(), reason="checks the no-GPU failure path")
 def test_no_cpu_fallback():
     pkg = load_pkg()

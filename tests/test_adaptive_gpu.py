@@ -83,11 +83,13 @@ def test_adaptive_batches_match_oracle():
         frames.append(ex.extract_frame(bgr[i], dep[i], cal))
         t_ref.append(t)
     res_a = odo.track_batch_host(bgr[:6], dep[:6])
+    lists = [odo.pair(i) for i in range(6)]
     for i in range(6):
         t_used, _ = odo.adaptive_state(i)
         assert np.array_equal(t_used, t_ref[i]), f"frame {i}: cell thresholds {t_used} vs {t_ref[i]}"
         assert_frame(odo.frame(i), frames[i], f"frame {i}")
     res_b = odo.track_batch_host(bgr[6:], dep[6:])
+    lists += [odo.pair(i) for i in range(3)]
     for i in range(3):
         t_used, th = odo.adaptive_state(i)
         assert np.array_equal(t_used, t_ref[6 + i]), f"frame {6 + i}: cell thresholds"
@@ -101,6 +103,7 @@ def test_adaptive_batches_match_oracle():
         g = res[p]
         assert (g["n_matches"], g["n_good"], g["visited"], g["n_inliers"]) == \
             (r.n_matches, r.n_good, r.visited, r.n_inliers), f"pair {p}: counts"
+        O.check_ransac_inliers(lists[p], r, f"pair {p}")
         assert np.array_equal(g["T12"], np.array(r.T12, np.float32)), f"pair {p}: T12"
         assert np.abs(g["Tcw"] - np.array(r.Tcw, np.float32)).max() < 1e-4, f"pair {p}: PnP pose"
     odo.close()

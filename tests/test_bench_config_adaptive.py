@@ -85,6 +85,7 @@ def test_bench_configuration_adaptive(inner):
             assert (res[p]["n_matches"], res[p]["n_good"], res[p]["visited"], res[p]["n_inliers"],
                     res[p]["ransac_ok"]) == (r.n_matches, r.n_good, r.visited, r.n_inliers, r.ransac_ok), \
                 f"{tag}: RANSAC counts"
+            O.check_ransac_inliers(g, r, tag)
             assert np.array_equal(res[p]["T12"], np.array(r.T12, np.float32)), f"{tag}: T12"
             assert res[p]["rmse"] == np.float32(r.rmse), f"{tag}: rmse"
             Tref = np.array(r.Tcw, np.float32).reshape(4, 4)

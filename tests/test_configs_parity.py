@@ -62,6 +62,7 @@ def test_config_path_parity(name):
         assert np.array_equal(g["matches"], matches), f"{name} pair {p}: match list"
         assert (res[p]["n_good"], res[p]["visited"], res[p]["n_inliers"], res[p]["ransac_ok"]) == \
             (r.n_good, r.visited, r.n_inliers, r.ransac_ok), f"{name} pair {p}: RANSAC counts"
+        O.check_ransac_inliers(g, r, f"{name} pair {p}")
         assert np.array_equal(res[p]["T12"], np.array(r.T12, np.float32)), f"{name} pair {p}: T12"
         assert res[p]["rmse"] == np.float32(r.rmse)
         assert (res[p]["n_sweeps"], res[p]["n_fit_points"]) == (r.n_sweeps, r.n_fit_points), f"{name} pair {p}: work"

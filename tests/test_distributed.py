@@ -1,10 +1,13 @@
-"""The N>1 path of bench.py on CPU: two ranks over gloo (127.0.0.1).
+"""The N>1 host logic of bench.py on CPU: two ranks over gloo (127.0.0.1).
 
-bench.py shards whole sequences across ranks (frames mode, weak scaling): each
-rank tracks its own scene with its own RANSAC seed stream, there is no
-data-path collective, and the only cross-rank step is the MAX of the timed
-region. These tests run that host logic in two processes with the gloo
-backend (the GPU box uses RCCL through the same calls).
+bench.py's default N > 1 mode is SURVEY §8(e) frames mode (frames_shard.py,
+tested in test_frames_shard*.py): one sequence split into per-rank chunks,
+with a latch broadcast before the first step and one pose all_gather per run.
+`--shard independent` gives every rank its own scene and RANSAC seed stream
+with no data-path exchange. In both, the job clock is the MAX over ranks of
+the timed region. These tests run that host logic in two processes with the
+gloo backend (the GPU box uses RCCL through the same calls), and check the
+launcher that `bench.py --gpus N` uses when no WORLD_SIZE is set.
 """
 import importlib.util
 import os
@@ -90,3 +93,38 @@ def test_single_rank_needs_no_collective():
     bench = _load_bench()
     assert bench.max_over_ranks(2.5, None, 1) == 2.5
     assert bench.job_throughput(64, 40, 1, 2.0) == pytest.approx(1280.0)
+
+
+def test_rank_envs_distinct_local_ranks():
+    """--gpus N without a launcher: N workers, each with its own RANK /
+    LOCAL_RANK (= its device) and the same WORLD_SIZE and rendezvous."""
+    bench = _load_bench()
+    envs = bench.rank_envs(4, 29555, base={"PATH": "/usr/bin"})
+    assert [e["LOCAL_RANK"] for e in envs] == ["0", "1", "2", "3"]
+    assert [e["RANK"] for e in envs] == ["0", "1", "2", "3"]
+    assert {e["WORLD_SIZE"] for e in envs} == {"4"}
+    assert {(e["MASTER_ADDR"], e["MASTER_PORT"]) for e in envs} == {("127.0.0.1", "29555")}
+    assert all(e["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" and e["PATH"] == "/usr/bin" for e in envs)
+
+
+def test_launch_ranks_runs_n_workers(tmp_path):
+    """launch_ranks starts N child processes (no exec) that rendezvous over
+    gloo and see distinct ranks; a failing rank's exit code is returned."""
+    bench = _load_bench()
+    out = tmp_path / "ranks"
+    out.mkdir()
+    script = tmp_path / "worker.py"
+    script.write_text(
+        "import os, sys\n"
+        "import torch.distributed as dist\n"
+        "dist.init_process_group('gloo')\n"
+        "r = dist.get_rank()\n"
+        "open(os.path.join(sys.argv[1], str(r)), 'w').write(os.environ['LOCAL_RANK'] + ' ' + str(dist.get_world_size()))\n"
+        "dist.barrier()\n"
+        "dist.destroy_process_group()\n")
+    assert bench.launch_ranks(3, [str(out)], script=str(script)) == 0
+    got = sorted(p.read_text() for p in out.iterdir())
+    assert got == ["0 3", "1 3", "2 3"]
+    bad = tmp_path / "bad.py"
+    bad.write_text("import os, sys\nsys.exit(3 if os.environ['RANK'] == '1' else 0)\n")
+    assert bench.launch_ranks(2, [], script=str(bad)) == 3

@@ -61,6 +61,7 @@ def test_gpu_empty_and_ragged_frames():
         assert np.array_equal(odo.pair(p)["matches"], matches), f"pair {p}: matches"
         assert (res[p]["n_matches"], res[p]["n_good"], res[p]["ransac_ok"], res[p]["n_inliers"], res[p]["visited"]) \
             == (r.n_matches, r.n_good, r.ransac_ok, r.n_inliers, r.visited), f"pair {p}: counts"
+        O.check_ransac_inliers(odo.pair(p), r, f"pair {p}")
         assert np.array_equal(res[p]["T12"], np.array(r.T12, np.float32)), f"pair {p}: T12"
         assert np.abs(res[p]["Tcw"] - np.array(r.Tcw, np.float32)).max() < 1e-4, f"pair {p}: Tcw"
     # the next batch starts from the half-blank frame

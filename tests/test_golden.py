@@ -76,6 +76,7 @@ def test_oracle_reproduces_pair_fixture(inputs):
     r, mask, matches, latch = O.track_pair(frames[0], frames[1], O.fr1_calib(), O.ransac_params(int(g["iters"][0])),
                                            int(g["seed"][0]))
     assert np.array_equal(matches, g["matches"])
+    assert np.array_equal(r.inliers, g["ransac_inliers"]), "Ransac::mvInliers list"
     assert np.array_equal(mask, g["pnp_inlier_mask"])
     assert np.float32(r.rmse) == g["rmse"][0]
     assert np.array_equal(np.array(r.T12, np.float32), g["T12"])
@@ -98,6 +99,8 @@ def test_hip_reproduces_frame_and_pair_fixtures(inputs):
         _frame_equal(odo.frame(i), gold, i)
     p = odo.pair(1)  # pair 1 = (frame 0, frame 1), seed pair_seed(base, 1)
     assert np.array_equal(p["matches"], g["matches"]), "match list"
+    got = p["good"][p["ransac_inliers"].astype(bool)]
+    assert np.array_equal(got, g["ransac_inliers"]), "RANSAC inlier list (Ransac::mvInliers)"
     assert np.array_equal(res[1]["T12"], g["T12"]), "T12 not bit-exact"
     assert res[1]["rmse"] == g["rmse"][0]
     assert np.abs(res[1]["Tcw"] - g["Tcw"]).max() < 1e-4, "PnP pose"

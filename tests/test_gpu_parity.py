@@ -135,6 +135,7 @@ def test_pairs_match_ransac_pnp(cfg2_run):
         assert res[p]["n_good"] == r.n_good
         assert res[p]["visited"] == r.visited, f"pair {p}: visited {res[p]['visited']} vs {r.visited}"
         assert res[p]["n_inliers"] == r.n_inliers
+        O.check_ransac_inliers(g, r, f"pair {p}")
         assert res[p]["ransac_ok"] == r.ransac_ok
         assert (res[p]["n_sweeps"], res[p]["n_fit_points"]) == (r.n_sweeps, r.n_fit_points), f"pair {p}: work"
         assert np.array_equal(res[p]["T12"], np.array(r.T12, np.float32)), f"pair {p}: T12 not bit-exact"
@@ -177,6 +178,7 @@ def test_pipelined_batches_roll_and_seeds():
         g = odo.pair(p)
         assert np.array_equal(g["matches"], matches), f"frame {f}: match list differs"
         assert res[p]["visited"] == r.visited and res[p]["n_inliers"] == r.n_inliers
+        O.check_ransac_inliers(g, r, f"frame {f}")
         assert np.array_equal(res[p]["T12"], np.array(r.T12, np.float32)), f"frame {f}: T12 not bit-exact"
         T_gpu = res[p]["Tcw"].reshape(4, 4)
         assert np.abs(T_gpu - np.array(r.Tcw, np.float32).reshape(4, 4)).max() < 1e-4

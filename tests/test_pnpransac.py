@@ -177,6 +177,37 @@ def test_extrinsic_init_exact(planar, n):
     np.testing.assert_allclose(p[3:], t, atol=1e-4)
 
 
+def _five_inliers(seed):
+    """12 observations, 5 exact and 7 moved 40-120 px: the best RANSAC model
+    has exactly 5 inliers (goodCount > modelPoints - 1 accepts it)."""
+    Xw, uv, cal, *_ = _problem(seed, 12, 0.0, noise=0.0)
+    rng = np.random.default_rng(seed + 1000)
+    ang = rng.uniform(0, 2 * np.pi, 7)
+    uv[5:] += (np.c_[np.cos(ang), np.sin(ang)] * rng.uniform(40, 120, (7, 1))).astype(np.float32)
+    return Xw, uv, cal
+
+
+def test_oracle_five_inliers_dlt_asserts():
+    """with exactly 5 non-planar inliers the final solvePnP's
+    cvFindExtrinsicCameraParams2 takes its DLT branch, which asserts count >= 6
+    (OpenCV throws, PnPRansac::Compute does not catch): the oracle reports -1
+    with the RANSAC model, mask and count and no pose. A 5-point set that is
+    planar (seed 61) takes the homography branch and refines normally."""
+    Xw, uv, cal = _five_inliers(62)
+    r = O.pnp_ransac(Xw, uv, cal, 4096)
+    assert r["ok"] == -1 and r["n_inliers"] == 5 and r["mask"].sum() == 5
+    assert np.all(r["T"] == 0) and np.all(r["rt"] == 0) and np.any(r["model"] != 0)
+    Xw, uv, cal = _five_inliers(61)
+    r = O.pnp_ransac(Xw, uv, cal, 4096)
+    assert r["ok"] == 1 and r["n_inliers"] == 5
+    # the DLT start alone: 5 non-planar points fail, 6 succeed
+    Xw, uv, cal, *_ = _problem(45, 6, 0.0, noise=0.0)
+    K = np.array([cal.fx, cal.fy, cal.cx, cal.cy], np.float64)
+    M, m, p = Xw.astype(np.float64), uv.astype(np.float64), np.zeros(6)
+    assert O.lib().oracle_pnp_extrinsic_init(O.ptr(M[:5].copy()), O.ptr(m[:5].copy()), 5, O.ptr(K), O.ptr(p)) == 0
+    assert O.lib().oracle_pnp_extrinsic_init(O.ptr(M), O.ptr(m), 6, O.ptr(K), O.ptr(p)) == 1
+
+
 def test_oracle_too_few_points():
     Xw, uv, cal, *_ = _problem(5, 9, 0.0)
     r = O.pnp_ransac(Xw, uv, cal)
@@ -244,6 +275,17 @@ def test_gpu_parity_frames_problem(odo):
     Xw, uv, cal = _frames_problem()
     ref, res = _check_gpu(odo, Xw, uv, cal)
     assert res.ok == 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [60, 61, 62])
+def test_gpu_parity_five_inliers(odo, seed):
+    """Best model with exactly 5 inliers: non-planar -> ok = -1 on
+    both sides (the DLT's count >= 6 assertion), same model, mask, visited
+    hypotheses; seed 61's inliers are planar -> refined pose as usual."""
+    Xw, uv, cal = _five_inliers(seed)
+    ref, res = _check_gpu(odo, Xw, uv, cal, 4096)
+    assert res.ok == (1 if seed == 61 else -1) and res.n_inliers == 5
 
 
 @pytest.mark.gpu

@@ -35,6 +35,7 @@ def test_gpu_frame_sizes(w, h):
         assert np.array_equal(odo.pair(p)["matches"], matches), f"{w}x{h} pair {p}: matches"
         assert (res[p]["n_matches"], res[p]["n_inliers"], res[p]["visited"], res[p]["n_queries"]) == \
             (r.n_matches, r.n_inliers, r.visited, r.n_queries), f"{w}x{h} pair {p}: counts"
+        O.check_ransac_inliers(odo.pair(p), r, f"{w}x{h} pair {p}")
         assert np.array_equal(res[p]["T12"], np.array(r.T12, np.float32)), f"{w}x{h} pair {p}: T12"
         assert np.abs(res[p]["Tcw"] - np.array(r.Tcw, np.float32)).max() < 1e-4, f"{w}x{h} pair {p}: Tcw"
     odo.close()

@@ -56,7 +56,8 @@ int main(int argc, char** argv) {
         long matches = 0, inliers = 0, pairs = 0;
         for (int k = 0; k < F; k++) {
             const auto t0 = Clock::now();
-            auto cur = std::make_unique<odo_hip::Frame>(&bgr[npx * 3 * k], &dep[npx * k], W, H, 0.033 * k);
+            auto cur = std::make_unique<odo_hip::Frame>(odo_hip::kBorrowImages, &bgr[npx * 3 * k], &dep[npx * k], W, H,
+                                                        0.033 * k);  // the buffers outlive the loop
             cur->ExtractFeatures(&extractor);
             const auto t1 = Clock::now();
             auto t2 = t1, t3 = t1, t4 = t1, t5 = t1;

@@ -1,0 +1,112 @@
+#!/bin/bash
+# The one launcher for GPU sessions (run it under gpurun):
+#
+#   tools/gpu.sh OUTDIR STEP [STEP ...]
+#
+# Steps run in order; each has its own time limit and the first failure ends
+# the call (set -e), so nothing runs on the GPU after a fault or a timeout.
+#
+#   tests               pytest -m gpu, the whole suite
+#   tests=F1,F2         pytest -m gpu over the named test files (tests/F1 ...)
+#   smoke               __graft_entry__.smoke()
+#   bench               python bench.py (the driver's default line)      -> bench.json
+#   bench=NAME:ARGS     python bench.py ARGS (ARGS with '+' for spaces)  -> NAME.json
+#   multi               bench.py --gpus 2 --backend gloo: two ranks sharing the GPU
+#   kt                  rocprofv3 kernel trace of the headline command (+ timed-region split)
+#   serial              per-kernel times alone (tuning build, ODO_SERIAL_STREAMS=1),
+#                       default and hard workloads
+#   pmc=REGEX           PMC passes over the kernels matching REGEX (tuning build,
+#                       serial streams), one counter group per rocprofv3 run
+#   pmch=REGEX          the same on the hard workload
+#   ab=N:V1,V2,...      A/B of library builds on the bench (N alternations); Vi is
+#                       "default" (libodo_hip.so) or a variant name (build_Vi/);
+#                       bench arguments from $AB_ARGS
+set -e
+R=${GRAFT_REPO_ROOT:-/root/repo}
+O=$R/gpurun_out/${1:?outdir}; shift
+mkdir -p "$O"
+P=$R/adaptive-rgbd-localization-mappig_amd
+TUNING=$P/build_tuning/libodo_hip.so
+QUICK="--no-cpu-baseline --host-steps 0 --hard-steps 0 --latency-frames 0"
+export TMPDIR=/tmp
+
+lib_of() { if [ "$1" = default ]; then echo "$P/libodo_hip.so"; else echo "$P/build_$1/libodo_hip.so"; fi; }
+
+pmc_passes() {  # REGEX OUTDIR BENCH_ARGS...
+  local K=$1 D=$2; shift 2
+  mkdir -p "$D"
+  cd /tmp
+  for spec in \
+    "sq1:SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_INSTS_SALU" \
+    "sq2:SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_WAIT_ANY SQ_BUSY_CU_CYCLES" \
+    "tcc:FETCH_SIZE" "tccw:WRITE_SIZE"; do
+    local name=${spec%%:*} ctr=${spec#*:}
+    ODO_SERIAL_STREAMS=1 ODO_LIB=$TUNING timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-include-regex "$K" \
+      -d "$D/$name" -o run --output-format csv -- python3 $R/bench.py "$@" > "$D/$name.log" 2>&1
+    echo "pmc $K $name ok"
+  done
+  ODO_SERIAL_STREAMS=1 ODO_LIB=$TUNING timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d "$D/kt" -o run \
+    --output-format csv -- python3 $R/bench.py "$@" > "$D/kt.log" 2>&1
+  echo "pmc $K kernel trace ok"
+  cd $R
+}
+
+for step in "$@"; do
+  cd $R
+  case $step in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
+      tail -1 $O/pytest.log ;;
+    tests=*)
+      files=$(echo ${step#tests=} | tr ',' '\n' | sed 's|^|tests/|' | tr '\n' ' ')
+      timeout -k 10 900 python -u -m pytest $files -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_part.log 2>&1
+      tail -1 $O/pytest_part.log ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+      tail -1 $O/smoke.log ;;
+    bench)
+      timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err
+      echo "bench ok" ;;
+    bench=*)
+      spec=${step#bench=}; name=${spec%%:*}; args=$(echo ${spec#*:} | tr '+' ' ')
+      timeout -k 10 600 python bench.py $args > $O/$name.json 2> $O/$name.err
+      echo "bench $name ok" ;;
+    multi)
+      timeout -k 10 600 python bench.py --gpus 2 --backend gloo $QUICK > $O/multi_gloo.json 2> $O/multi_gloo.err
+      echo "multi ok" ;;
+    kt)
+      cd /tmp
+      timeout -s KILL 600 rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- \
+        python3 $R/bench.py --no-cpu-baseline --hard-steps 0 --latency-frames 0 > $O/kt_bench.json 2> $O/kt.err
+      cd $R
+      T=$(find $O/kt -name '*kernel_trace.csv' -print -quit)
+      python tools/rocprof_timed_region.py "$T" $O/kt_bench.json $O/rocprof_timed_region.json > $O/rtr.log 2>&1 || true
+      echo "kt ok" ;;
+    serial)
+      cd /tmp
+      ODO_SERIAL_STREAMS=1 ODO_LIB=$TUNING timeout -s KILL 300 rocprofv3 --kernel-trace --stats -d $O/serial_default \
+        -o run --output-format csv -- python3 $R/bench.py $QUICK --steps 10 > $O/serial_default.log 2>&1
+      echo "serial default ok"
+      ODO_SERIAL_STREAMS=1 ODO_LIB=$TUNING timeout -s KILL 300 rocprofv3 --kernel-trace --stats -d $O/serial_hard \
+        -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --host-steps 0 --latency-frames 0 \
+        --steps 2 --hard-steps 0 --workload hard > $O/serial_hard.log 2>&1
+      echo "serial hard ok" ;;
+    pmc=*)
+      K=${step#pmc=}
+      pmc_passes "$K" "$O/pmc_$(echo $K | tr -c 'A-Za-z0-9_\n' '_')" --steps 3 --warmup 1 $QUICK ;;
+    pmch=*)
+      K=${step#pmch=}
+      pmc_passes "$K" "$O/pmch_$(echo $K | tr -c 'A-Za-z0-9_\n' '_')" --steps 2 --warmup 1 $QUICK --workload hard ;;
+    ab=*)
+      spec=${step#ab=}; n=${spec%%:*}; vs=$(echo ${spec#*:} | tr ',' ' ')
+      for i in $(seq 1 $n); do
+        for v in $vs; do
+          ODO_LIB=$(lib_of $v) timeout -k 10 300 python bench.py --no-cpu-baseline --latency-frames 0 --host-steps 0 \
+            $AB_ARGS > $O/ab_${v}_$i.json 2> $O/ab_${v}_$i.err
+          echo "ab $v $i: $(python tools/bsum.py $O/ab_${v}_$i.json 2>/dev/null || true)"
+        done
+      done ;;
+    *)
+      echo "unknown step $step" >&2; exit 2 ;;
+  esac
+done
