@@ -163,6 +163,11 @@ SIGNATURES = {
     "odo_ransac_hyps": (C.c_int, [P, P, C.c_int, P, C.c_int, P, C.c_int, P, P, P, C.c_int, C.c_int, P, P]),
     "odo_ransac_fold": (C.c_int, [P, C.c_int, C.c_int, P, P]),
     "odo_ransac_hyps_finish": (C.c_int, [P, P, P, P, P, P, P, P, P]),
+    "odo_ransac_hyps_dev": (C.c_int, [P, P, C.c_int, P, C.c_int, P, C.c_int, P, P, P, C.c_int, C.c_int, P, P]),
+    "odo_ransac_fold_dev": (C.c_int, [P, P, C.c_int, P]),
+    "odo_ransac_hyps_payload_words": (C.c_int, [P]),
+    "odo_ransac_hyps_finish_dev": (C.c_int, [P, P, C.c_int, P, C.c_int]),
+    "odo_ransac_hyps_result": (C.c_int, [P, P, P, P, P, P, P, P, P]),
 }
 
 _lib = None

@@ -1655,6 +1655,149 @@ __global__ void k_ransac_install(RansacBufs B, int best_h, int visited, int vali
     S->done = 1;
 }
 
+// ---------------------------------------------------------------- hypotheses mode on the device
+// The exchange of SURVEY §8(e)'s hypotheses mode without host staging: every
+// rank's per-hypothesis summaries stay in HBM (a device copy of its HypRes
+// range), the ranks all_gather them over RCCL, every rank folds the gathered
+// array here, and the owner of the winner packs (T12, rmse, ok, inliers) into
+// a payload the ranks sum-reduce (the other ranks contribute zeros).
+
+// The ordered running-best fold of ransac.cpp:233-249 over the gathered
+// summaries (hypothesis order), by one wave, as try_fold_wave: only entries
+// that beat the state at the start of a 64-entry run can be accepted (rmse
+// only falls and best only grows along the run), so the serial steps visit
+// those candidates alone and the entries between them just count n++. The
+// same record as the host odo_ransac_fold.
+__global__ void __launch_bounds__(64) k_hyp_fold(const HypRes* __restrict__ all, int H, int iterations, int ng,
+                                                 int min_inl, int sample_size,
+                                                 odo_ransac_fold_result* __restrict__ out) {
+    const int lane = threadIdx.x;
+    int best_h = -1, visited = 0, valid = 0, best = 0;
+    float rmse = 1e6f;
+    if (ng >= min_inl && ng >= sample_size) {
+        const unsigned minInl = (unsigned)min_inl;
+        int n = 0, pos = 0;
+        bool fin = n >= iterations;
+        while (!fin && pos < H) {
+            const int m = min(64, H - pos);
+            const int q = pos + lane;
+            int rc = 0, elo = 0, ehi = 0;
+            if (lane < m) {
+                rc = all[q].cnt;
+                const long long e = __double_as_longlong(all[q].err);
+                elo = (int)(uint32_t)e;
+                ehi = (int)(uint32_t)((unsigned long long)e >> 32);
+            }
+            uint64_t cand = __ballot(lane < m && rc > 0 && __hiloint2double(ehi, elo) <= (double)rmse &&
+                                     (unsigned)rc >= (unsigned)best && (unsigned)rc >= minInl);
+            int i = 0;  // entries of this run visited so far
+            while (i < m && !fin) {
+                const int c = cand ? (int)__builtin_ctzll(cand) : m;
+                if (c - i >= iterations - n) {  // n reaches the limit before the candidate
+                    i += iterations - n;
+                    n = iterations;
+                    fin = true;
+                    break;
+                }
+                n += c - i;
+                i = c;
+                if (c == m) break;
+                cand &= cand - 1;
+                const unsigned rci = (unsigned)rdl(rc, c);
+                const double re = __hiloint2double(rdl(ehi, c), rdl(elo, c));
+                bool brk = false;
+                if (re <= (double)rmse && rci >= (unsigned)best) {
+                    rmse = (float)re;
+                    best = (int)rci;
+                    best_h = pos + c;
+                    if (rci > ng * 0.5) n += 10;
+                    if (rci > ng * 0.75) n += 10;
+                    if (rci > ng * 0.8) brk = true;
+                }
+                n++;
+                i++;
+                if (brk) n = iterations;
+                fin = n >= iterations;
+            }
+            visited += i;
+            valid += __popcll(__ballot(lane < i && rc > 0));
+            pos += i;
+            if (i < m) break;
+        }
+    }
+    if (lane == 0) *out = odo_ransac_fold_result{best_h, visited, valid, best, rmse, ng, {0, 0}};
+}
+
+// the fold's outcome into the pair state, read from device memory
+__global__ void k_hyp_install_dev(RansacBufs B, const odo_ransac_fold_result* __restrict__ fr) {
+    RState* S = B.st;
+    S->visited = fr->visited;
+    S->valid = fr->valid;
+    S->best_cnt = fr->n_inliers;
+    S->best_h = fr->best_h;
+    S->rmse = fr->rmse;
+    S->done = 1;
+}
+
+// The winner's owner packs the payload (HYP_PAYLOAD_HDR header words: T12 bits,
+// rmse bits, ok, n_inliers, visited; then the inlier list as DMatch records in
+// good-list order, the RANSAC mask compacted); every other rank writes zeros,
+// so a sum over the ranks delivers the owner's words exactly. Owner: the rank
+// whose range [h0, h1) holds best_h; rank 0 for the identity fallback and for
+// a pair that never sampled. One 256-thread workgroup.
+#define HYP_PAYLOAD_HDR 32
+__global__ void __launch_bounds__(256) k_hyp_payload(RansacBufs B, const odo_ransac_fold_result* __restrict__ fr,
+                                                     int h0, int h1, int rank0, const odo_dmatch* __restrict__ good,
+                                                     int ng, int* __restrict__ payload, int words) {
+    __shared__ int s_wc[4];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int active = B.st->active;
+    const int bh = fr->best_h;
+    const bool owner = (active && bh >= 0) ? (bh >= h0 && bh < h1) : rank0 != 0;
+    if (!owner) {
+        for (int w = t; w < words; w += 256) payload[w] = 0;
+        return;
+    }
+    const odo_pair_result* R = B.res;
+    if (t < HYP_PAYLOAD_HDR) {
+        int v = 0;
+        if (t < 16) v = active ? __float_as_int(R->T12[t]) : __float_as_int((t % 5 == 0) ? 1.f : 0.f);
+        else if (t == 16) v = __float_as_int(active ? R->rmse : 1e6f);
+        else if (t == 17) v = active ? R->ransac_ok : 0;
+        else if (t == 18) v = active ? R->n_inliers : 0;
+        else if (t == 19) v = active ? fr->visited : 0;
+        payload[t] = v;
+    }
+    const uint32_t* BM = B.best_mask;
+    int base = 0;
+    if (active) {
+        for (int c0 = 0; c0 < ng; c0 += 256) {
+            const int k = c0 + t;
+            const bool in = k < ng && ((BM[k >> 5] >> (k & 31)) & 1u);
+            const uint64_t bal = __ballot(in);
+            if (lane == 0) s_wc[wave] = __popcll(bal);
+            __syncthreads();
+            int before = base, tot = 0;
+            for (int w = 0; w < 4; w++) {
+                before += w < wave ? s_wc[w] : 0;
+                tot += s_wc[w];
+            }
+            if (in) {
+                const int r = before + (int)lane_rank(bal);
+                const odo_dmatch m = good[k];
+                int* o = payload + HYP_PAYLOAD_HDR + 4 * r;
+                o[0] = m.queryIdx;
+                o[1] = m.trainIdx;
+                o[2] = m.imgIdx;
+                o[3] = __float_as_int(m.distance);
+            }
+            base += tot;
+            __syncthreads();
+        }
+    }
+    for (int w = HYP_PAYLOAD_HDR + 4 * base + t; w < words; w += 256) payload[w] = 0;
+}
+
 // ---------------------------------------------------------------- host side
 size_t ransac_gpt_bytes() { return sizeof(GoodPt); }
 
@@ -1965,6 +2108,36 @@ void launch_ransac_finish(hipStream_t st, void* scratch, int match_cap, int mask
     hipLaunchKernelGGL(k_ransac_install, dim3(1), dim3(1), 0, st, B, best_h, visited, valid, best_cnt, rmse);
     hipLaunchKernelGGL(k_ransac_final, dim3(1), dim3(64), 0, st, B, cfg, 0, (int*)nullptr);
 }
+
+// hypotheses mode on the device: this rank's summaries [h0, h1) into d_block
+// (HypRes = odo_hyp_summary layout, 64 B each)
+void ransac_export_hyps(hipStream_t st, void* scratch, int match_cap, int mask_words, RansacCfg cfg, int h0, int h1,
+                        void* d_block) {
+    RansacBufs B = carve(scratch, 1, match_cap, mask_words, cfg);
+    if (h1 > h0)
+        (void)hipMemcpyAsync(d_block, B.hyp + h0, (size_t)(h1 - h0) * sizeof(HypRes), hipMemcpyDeviceToDevice, st);
+}
+void launch_hyp_fold(hipStream_t st, const void* d_all, int H, int iterations, int ng, int min_inl, int sample_size,
+                     odo_ransac_fold_result* d_out) {
+    static_assert(sizeof(HypRes) == sizeof(odo_hyp_summary), "summary layout");
+    hipLaunchKernelGGL(k_hyp_fold, dim3(1), dim3(64), 0, st, (const HypRes*)d_all, H, iterations, ng, min_inl,
+                       sample_size, d_out);
+}
+void launch_hyp_finish(hipStream_t st, void* scratch, int match_cap, int mask_words, RansacCfg cfg,
+                       const double* latch, odo_rng* rng_io, uint32_t* best_mask, odo_pair_result* res, float* T12,
+                       const odo_ransac_fold_result* d_fold, int h0, int h1, int rank0, const odo_dmatch* good, int ng,
+                       int* payload, int words) {
+    RansacBufs B = carve(scratch, 1, match_cap, mask_words, cfg);
+    B.latch = latch;
+    B.rng_io = rng_io;
+    B.best_mask = best_mask;
+    B.res = res;
+    B.T12 = T12;
+    hipLaunchKernelGGL(k_hyp_install_dev, dim3(1), dim3(1), 0, st, B, d_fold);
+    hipLaunchKernelGGL(k_ransac_final, dim3(1), dim3(64), 0, st, B, cfg, 0, (int*)nullptr);
+    hipLaunchKernelGGL(k_hyp_payload, dim3(1), dim3(256), 0, st, B, d_fold, h0, h1, rank0, good, ng, payload, words);
+}
+int hyp_payload_words(int ng) { return HYP_PAYLOAD_HDR + 4 * std::max(ng, 0); }
 
 }  // namespace odo
 #ifdef ODO_LANES_PROFILE

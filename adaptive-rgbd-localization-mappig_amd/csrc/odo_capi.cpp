@@ -2283,23 +2283,25 @@ int odo_ransac(odo_ctx* c, const odo_dmatch* m12, int n12, const float* xyz1, in
     return ODO_OK;
 }
 
-int odo_ransac_hyps(odo_ctx* c, const odo_dmatch* m12, int n12, const float* xyz1, int n1, const float* xyz2, int n2,
-                    const odo_ransac_params* p, const odo_rng* rng, double* latch, int h0, int h1,
-                    odo_hyp_summary* out, int* n_good) {
-    if (!c || !p || !rng || !latch || !n_good || n12 < 0 || (n12 && !m12) || h0 < 0 || h1 < h0 ||
-        h1 > std::max(p->iterations, 0) || (h1 > h0 && !out))
-        return fail(ODO_ERR_ARG, "bad ransac_hyps args");
+// Hypotheses mode, shared by the host and the device exchange: a new session
+// over the pair, its samples for all H hypotheses and the evaluation of
+// [h0, h1) queued on the context's stream (no fold). *active = 0 when
+// Iterate returns before sampling (too few matches).
+static int hyps_launch(odo_ctx* c, const odo_dmatch* m12, int n12, const float* xyz1, int n1, const float* xyz2,
+                       int n2, const odo_ransac_params* p, const odo_rng* rng, double* latch, int h0, int h1,
+                       int* n_good, int* active) {
     free_hyp_session(c->hs);
     c->hs = new HypSession();
     HypSession& S = *c->hs;
     S.h0 = h0;
     S.h1 = h1;
     *n_good = 0;
-    for (int h = 0; h < h1 - h0; h++) out[h] = odo_hyp_summary{1e6, 0, 0, {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0}};
+    *active = 0;
     const int r = prepare_pair_ransac(m12, n12, xyz1, n1, xyz2, n2, p, latch, S.in, c->match_cap);
     if (r < 0) return r;
     if (r == 0) return ODO_OK;  // Iterate returns before the loop (too few matches)
     S.active = 1;
+    *active = 1;
     PairRansacInput& in = S.in;
     const int ng = in.ng, kc = in.kc;
     *n_good = ng;
@@ -2340,11 +2342,27 @@ int odo_ransac_hyps(odo_ctx* c, const odo_dmatch* m12, int n12, const float* xyz
                   kc, 0, ng, in.cfg, S.latch->as<double>(), S.ints->as<int>() + 2, 0, S.rng->as<odo_rng>(), S.scr->p,
                   S.bm->as<uint32_t>(), in.words, S.res->as<odo_pair_result>(), S.T->as<float>(), 1, 3, hrange);
     HIPCHK(hipGetLastError());
+    return ODO_OK;
+}
+
+int odo_ransac_hyps(odo_ctx* c, const odo_dmatch* m12, int n12, const float* xyz1, int n1, const float* xyz2, int n2,
+                    const odo_ransac_params* p, const odo_rng* rng, double* latch, int h0, int h1,
+                    odo_hyp_summary* out, int* n_good) {
+    if (!c || !p || !rng || !latch || !n_good || n12 < 0 || (n12 && !m12) || h0 < 0 || h1 < h0 ||
+        h1 > std::max(p->iterations, 0) || (h1 > h0 && !out))
+        return fail(ODO_ERR_ARG, "bad ransac_hyps args");
+    for (int h = 0; h < h1 - h0; h++) out[h] = odo_hyp_summary{1e6, 0, 0, {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0}};
+    int active = 0;
+    const int e = hyps_launch(c, m12, n12, xyz1, n1, xyz2, n2, p, rng, latch, h0, h1, n_good, &active);
+    if (e || !active) return e;
+    HypSession& S = *c->hs;
+    PairRansacInput& in = S.in;
+    hipStream_t st = c->stream;
     if (h1 > h0) {
         std::vector<double> err(h1 - h0);
         std::vector<int> cnt(h1 - h0);
         std::vector<float> T((size_t)(h1 - h0) * 12);
-        ransac_read_hyps(st, S.scr->p, ng, in.words, in.cfg, h0, h1, err.data(), cnt.data(), T.data());
+        ransac_read_hyps(st, S.scr->p, in.ng, in.words, in.cfg, h0, h1, err.data(), cnt.data(), T.data());
         HIPCHK(hipGetLastError());
         for (int h = 0; h < h1 - h0; h++) {
             out[h].err = err[h];
@@ -2353,6 +2371,30 @@ int odo_ransac_hyps(odo_ctx* c, const odo_dmatch* m12, int n12, const float* xyz
         }
     }
     HIPCHK(hipStreamSynchronize(st));
+    return ODO_OK;
+}
+
+int odo_ransac_hyps_dev(odo_ctx* c, const odo_dmatch* m12, int n12, const float* xyz1, int n1, const float* xyz2,
+                        int n2, const odo_ransac_params* p, const odo_rng* rng, double* latch, int h0, int h1,
+                        void* d_block, int* n_good) {
+    if (!c || !p || !rng || !latch || !n_good || n12 < 0 || (n12 && !m12) || h0 < 0 || h1 < h0 ||
+        h1 > std::max(p->iterations, 0) || (h1 > h0 && !d_block))
+        return fail(ODO_ERR_ARG, "bad ransac_hyps_dev args");
+    int active = 0;
+    const int e = hyps_launch(c, m12, n12, xyz1, n1, xyz2, n2, p, rng, latch, h0, h1, n_good, &active);
+    if (e) return e;
+    hipStream_t st = c->stream;
+    if (!active) {
+        // no sampling: the default summaries (the fold returns before them)
+        if (h1 > h0) {
+            std::vector<odo_hyp_summary> d(h1 - h0, odo_hyp_summary{1e6, 0, 0, {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0}});
+            HIPCHK(hipMemcpy(d_block, d.data(), d.size() * sizeof(odo_hyp_summary), hipMemcpyHostToDevice));
+        }
+        return ODO_OK;
+    }
+    HypSession& S = *c->hs;
+    ransac_export_hyps(st, S.scr->p, S.in.ng, S.in.words, S.in.cfg, h0, h1, d_block);
+    HIPCHK(hipGetLastError());
     return ODO_OK;
 }
 
@@ -2426,6 +2468,76 @@ int odo_ransac_hyps_finish(odo_ctx* c, const odo_ransac_fold_result* r, odo_rng*
         }
     *n_inliers = k2;
     *ok = pr.ransac_ok;
+    return ODO_OK;
+}
+
+int odo_ransac_fold_dev(odo_ctx* c, const void* d_all, int H, void* d_fold) {
+    if (!c || !d_fold || H < 0 || (H && !d_all)) return fail(ODO_ERR_ARG, "bad fold_dev args");
+    if (!c->hs) return fail(ODO_ERR_STATE, "no odo_ransac_hyps_dev call to fold");
+    const HypSession& S = *c->hs;
+    const int ng = S.active ? S.in.ng : 0;
+    const RansacCfg& k = S.in.cfg;
+    launch_hyp_fold(c->stream, d_all, H, S.active ? k.iterations : 0, ng, S.active ? k.min_inlier_th : 1,
+                    S.active ? k.sample_size : 1, (odo_ransac_fold_result*)d_fold);
+    HIPCHK(hipGetLastError());
+    return ODO_OK;
+}
+
+int odo_ransac_hyps_payload_words(odo_ctx* c) {
+    if (!c || !c->hs) return fail(ODO_ERR_STATE, "no odo_ransac_hyps_dev session");
+    return hyp_payload_words(c->hs->active ? c->hs->in.ng : 0);
+}
+
+int odo_ransac_hyps_finish_dev(odo_ctx* c, const void* d_fold, int rank0, void* d_payload, int payload_words) {
+    if (!c || !d_fold || !d_payload) return fail(ODO_ERR_ARG, "bad finish_dev args");
+    if (!c->hs) return fail(ODO_ERR_STATE, "no odo_ransac_hyps_dev call to finish");
+    HypSession& S = *c->hs;
+    const int ng = S.active ? S.in.ng : 0;
+    if (payload_words < hyp_payload_words(ng)) return fail(ODO_ERR_CAPACITY, "hyps payload too small");
+    hipStream_t st = c->stream;
+    if (!S.active) {
+        // Iterate returned before sampling: rank 0 reports the reset outputs
+        // (T = I, rmse 1e6, not ok), the rand() state is untouched
+        std::vector<int> w(payload_words, 0);
+        if (rank0) {
+            for (int i = 0; i < 16; i++) {
+                const float v = (i % 5 == 0) ? 1.f : 0.f;
+                memcpy(&w[i], &v, 4);
+            }
+            const float r = 1e6f;
+            memcpy(&w[16], &r, 4);
+        }
+        HIPCHK(hipMemcpy(d_payload, w.data(), w.size() * 4, hipMemcpyHostToDevice));
+        return ODO_OK;
+    }
+    launch_hyp_finish(st, S.scr->p, S.in.ng, S.in.words, S.in.cfg, S.latch->as<double>(), S.rng->as<odo_rng>(),
+                      S.bm->as<uint32_t>(), S.res->as<odo_pair_result>(), S.T->as<float>(),
+                      (const odo_ransac_fold_result*)d_fold, S.h0, S.h1, rank0, S.m->as<odo_dmatch>(), ng,
+                      (int*)d_payload, payload_words);
+    HIPCHK(hipGetLastError());
+    return ODO_OK;
+}
+
+int odo_ransac_hyps_result(odo_ctx* c, const void* d_payload, odo_rng* rng, float T12[16], float* rmse,
+                           odo_dmatch* inliers, int* n_inliers, int* ok, int* visited) {
+    if (!c || !d_payload || !rng || !T12 || !rmse || !n_inliers || !ok || !visited)
+        return fail(ODO_ERR_ARG, "bad hyps_result args");
+    if (!c->hs) return fail(ODO_ERR_STATE, "no odo_ransac_hyps_dev session");
+    HypSession& S = *c->hs;
+    const int ng = S.active ? S.in.ng : 0;
+    const int words = hyp_payload_words(ng);
+    std::vector<int> w(words);
+    hipStream_t st = c->stream;
+    HIPCHK(hipMemcpyAsync(w.data(), d_payload, (size_t)words * 4, hipMemcpyDeviceToHost, st));
+    if (S.active) HIPCHK(hipMemcpyAsync(rng, S.rng->p, sizeof(odo_rng), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    memcpy(T12, w.data(), 64);
+    memcpy(rmse, &w[16], 4);
+    *ok = w[17];
+    *n_inliers = w[18];
+    *visited = w[19];
+    if (*n_inliers < 0 || *n_inliers > ng) return fail(ODO_ERR_STATE, "hyps payload: bad inlier count");
+    if (inliers && *n_inliers) memcpy(inliers, &w[32], (size_t)*n_inliers * sizeof(odo_dmatch));
     return ODO_OK;
 }
 

@@ -248,6 +248,16 @@ void ransac_read_hyps(hipStream_t st, void* scratch, int match_cap, int mask_wor
 void launch_ransac_finish(hipStream_t st, void* scratch, int match_cap, int mask_words, RansacCfg cfg,
                           const double* latch, odo_rng* rng_io, uint32_t* best_mask, odo_pair_result* res, float* T12,
                           int best_h, int visited, int valid, int best_cnt, float rmse);
+// hypotheses mode with the exchange on the device (odo_ransac_hyps_dev ...)
+void ransac_export_hyps(hipStream_t st, void* scratch, int match_cap, int mask_words, RansacCfg cfg, int h0, int h1,
+                        void* d_block);
+void launch_hyp_fold(hipStream_t st, const void* d_all, int H, int iterations, int ng, int min_inl, int sample_size,
+                     odo_ransac_fold_result* d_out);
+void launch_hyp_finish(hipStream_t st, void* scratch, int match_cap, int mask_words, RansacCfg cfg,
+                       const double* latch, odo_rng* rng_io, uint32_t* best_mask, odo_pair_result* res, float* T12,
+                       const odo_ransac_fold_result* d_fold, int h0, int h1, int rank0, const odo_dmatch* good, int ng,
+                       int* payload, int words);
+int hyp_payload_words(int ng);
 size_t pnp_edge_bytes();
 void launch_pnp(hipStream_t st, const int32_t* f2_src, const float* xyz, const float* kun, const float* ur,
                 const int* nkp, int kp_cap, int slot0, FrameCalib cal, const float* T12, const int* pair_valid,

@@ -15,6 +15,15 @@ group (RCCL over xGMI on the GPU box, gloo in the CPU tests):
    rand() state by exactly the visited draws (odo_ransac_hyps_finish).
 
 The result on every rank equals odo_ransac / Ransac::Iterate bit for bit.
+
+`sharded_ransac_device` is the same protocol with the exchange in HBM: the
+summaries are exported into a device tensor (odo_ransac_hyps_dev), gathered
+with all_gather_into_tensor (RCCL when the ranks hold distinct GPUs), folded
+on the GPU (odo_ransac_fold_dev), and the winner's owner writes its payload
+while every other rank writes zeros, so one int32 SUM all_reduce replaces the
+broadcast and no rank needs to know the owner on the host. All of it is
+queued on the context's stream; the host reads the outputs once at the end.
+With gloo (CPU tensors only) DeviceExchange stages through host memory.
 """
 from __future__ import annotations
 
@@ -119,3 +128,105 @@ def sharded_ransac(odo, ex: Exchange, m12: np.ndarray, xyz1: np.ndarray, xyz2: n
     inliers = got[19 * 4:].view(DMATCH_DTYPE)[:n_inl].copy()
     return (hdr[:16].reshape(4, 4).copy(), float(hdr[16]), inliers, int(hdr[17:19].view(np.int32)[0]),
             fr.visited, lat.value)
+
+
+def device_range(H: int, rank: int, world: int):
+    """[h0, h1) of one rank in the device protocol: contiguous blocks of
+    ceil(H / world), so the gathered blocks are already in hypothesis order."""
+    per = -(-H // world) if H else 0
+    return min(H, rank * per), min(H, (rank + 1) * per), per
+
+
+class DeviceExchange:
+    """Collectives on device tensors: RCCL (nccl backend) directly; gloo, which
+    takes CPU tensors only, through host copies (tests with ranks sharing one
+    GPU). Issued on `stream` (the odometry context's stream), so they are
+    ordered after the kernels that produce their inputs and before the ones
+    that consume them."""
+
+    def __init__(self, dist, world: int, rank: int, stream_ptr: int):
+        import torch
+        self.dist, self.world, self.rank = dist, world, rank
+        self.nccl = world > 1 and dist.get_backend() == "nccl"
+        self.stream = torch.cuda.ExternalStream(stream_ptr)
+
+    def all_gather(self, block):
+        import torch
+        with torch.cuda.stream(self.stream):
+            if self.world == 1:
+                return block
+            if self.nccl:
+                out = torch.empty(self.world * block.numel(), dtype=block.dtype, device=block.device)
+                self.dist.all_gather_into_tensor(out, block)
+                return out
+            host = block.cpu()
+            parts = [torch.empty_like(host) for _ in range(self.world)]
+            self.dist.all_gather(parts, host)
+            return torch.cat(parts).to(block.device)
+
+    def all_reduce_sum(self, t):
+        import torch
+        with torch.cuda.stream(self.stream):
+            if self.world == 1:
+                return t
+            if self.nccl:
+                self.dist.all_reduce(t)
+                return t
+            host = t.cpu()
+            self.dist.all_reduce(host)
+            t.copy_(host)
+            return t
+
+
+def sharded_ransac_device(odo, ex: DeviceExchange, m12: np.ndarray, xyz1: np.ndarray, xyz2: np.ndarray,
+                          params: RansacParams, rng: Rng, latch: float, timing: dict = None):
+    """sharded_ransac with the exchange in device memory (see the module
+    docstring). Same return value; rng is advanced in place. timing (optional
+    dict): the host-clock split of one call (evaluation, exchange, fold +
+    finish), each phase synchronised — measurement only."""
+    import time
+
+    import torch
+    lib = load()
+    m12 = np.ascontiguousarray(m12, DMATCH_DTYPE)
+    xyz1 = np.ascontiguousarray(xyz1, np.float32)
+    xyz2 = np.ascontiguousarray(xyz2, np.float32)
+    H = max(params.iterations, 0)
+    h0, h1, per = device_range(H, ex.rank, ex.world)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    block = torch.zeros(max(per, 1) * HYP_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    lat = C.c_double(latch)
+    ng = C.c_int(0)
+    sync = (lambda: torch.cuda.synchronize()) if timing is not None else (lambda: None)
+    t0 = time.perf_counter()
+    check(lib.odo_ransac_hyps_dev(odo.h, ptr(m12), m12.size, ptr(xyz1), xyz1.shape[0], ptr(xyz2), xyz2.shape[0],
+                                  ptr(params), ptr(rng), C.byref(lat), h0, h1, C.c_void_p(block.data_ptr()),
+                                  C.byref(ng)))
+    sync()
+    t1 = time.perf_counter()
+    allh = ex.all_gather(block)
+    sync()
+    t2 = time.perf_counter()
+    fold_rec = torch.zeros(32, dtype=torch.uint8, device=dev)
+    check(lib.odo_ransac_fold_dev(odo.h, C.c_void_p(allh.data_ptr()), H, C.c_void_p(fold_rec.data_ptr())))
+    words = lib.odo_ransac_hyps_payload_words(odo.h)
+    if words < 0:
+        check(words)
+    payload = torch.empty(words, dtype=torch.int32, device=dev)
+    check(lib.odo_ransac_hyps_finish_dev(odo.h, C.c_void_p(fold_rec.data_ptr()), 1 if ex.rank == 0 else 0,
+                                         C.c_void_p(payload.data_ptr()), words))
+    sync()
+    t3 = time.perf_counter()
+    ex.all_reduce_sum(payload)
+    sync()
+    t4 = time.perf_counter()
+    T = np.zeros(16, np.float32)
+    rmse, nin, ok, vis = C.c_float(0), C.c_int(0), C.c_int(0), C.c_int(0)
+    inl = np.zeros(max(ng.value, 1), DMATCH_DTYPE)
+    check(lib.odo_ransac_hyps_result(odo.h, C.c_void_p(payload.data_ptr()), ptr(rng), ptr(T), C.byref(rmse),
+                                     ptr(inl), C.byref(nin), C.byref(ok), C.byref(vis)))
+    t5 = time.perf_counter()
+    if timing is not None:
+        timing.update(evaluate=t1 - t0, all_gather=t2 - t1, fold_finish=t3 - t2, all_reduce=t4 - t3,
+                      readback=t5 - t4, total=t5 - t0)
+    return T.reshape(4, 4), float(rmse.value), inl[:nin.value].copy(), int(ok.value), int(vis.value), lat.value

@@ -212,6 +212,36 @@ int odo_ransac_fold(const odo_hyp_summary* all, int H, int n_good, const odo_ran
 int odo_ransac_hyps_finish(odo_ctx* ctx, const odo_ransac_fold_result* r, odo_rng* rng, float T12[16],
                            float* rmse, odo_dmatch* inliers, int* n_inliers, int* ok, int* owner);
 
+/* ---- The same hypotheses mode with the exchange in device memory (RCCL
+ * collectives on device buffers, no host staging; ransac.cpp:233-249 is the
+ * ordered fold it feeds). All work is queued on odo_stream(ctx); a caller
+ * orders its collectives after it on that stream.
+ * 1) odo_ransac_hyps_dev: as odo_ransac_hyps, the summaries of [h0, h1) into
+ *    the DEVICE buffer d_block ((h1-h0) x 64 B, odo_hyp_summary layout); no
+ *    host synchronisation. The gathered array must hold all H summaries in
+ *    hypothesis order (contiguous rank ranges). */
+int odo_ransac_hyps_dev(odo_ctx* ctx, const odo_dmatch* m12, int n12, const float* xyz1, int n1,
+                        const float* xyz2, int n2, const odo_ransac_params* p, const odo_rng* rng,
+                        double* latch, int h0, int h1, void* d_block, int* n_good);
+/* 2) the ordered fold over the gathered device array d_all (H summaries) on
+ *    the GPU; the odo_ransac_fold_result record is written to device memory
+ *    d_fold (same values as odo_ransac_fold). */
+int odo_ransac_fold_dev(odo_ctx* ctx, const void* d_all, int H, void* d_fold);
+/* 3) size in int32 words of the payload buffer of step 4 (32 header words +
+ *    4 per good match). */
+int odo_ransac_hyps_payload_words(odo_ctx* ctx);
+/* 4) the folded run's outputs: this rank's rand() state advanced on the
+ *    device by exactly the visited draws; the owner of the winner (its range
+ *    holds best_h; rank 0 when rank0 != 0 for the identity fallback or a pair
+ *    that never sampled) writes the payload [T12 bits x16, rmse bits, ok,
+ *    n_inliers, visited, 12 x 0, inliers as odo_dmatch...] to d_payload and
+ *    every other rank writes zeros, so an int32 SUM all-reduce over the ranks
+ *    leaves the owner's payload everywhere. */
+int odo_ransac_hyps_finish_dev(odo_ctx* ctx, const void* d_fold, int rank0, void* d_payload, int payload_words);
+/* 5) synchronise and unpack a (reduced) payload and this rank's rand() state. */
+int odo_ransac_hyps_result(odo_ctx* ctx, const void* d_payload, odo_rng* rng, float T12[16], float* rmse,
+                           odo_dmatch* inliers, int* n_inliers, int* ok, int* visited);
+
 /* PnPSolver::Compute (pnpsolver.cpp:17): Xw n x 3 (world), obs n x 3 (u,v,uR;
  * uR<0 = mono edge). outlier: out, per edge. Returns inliers in *n_inliers. */
 int odo_pnp_motion_ba(odo_ctx* ctx, const float* Xw, const float* obs, int n, const odo_calib* calib,
