@@ -337,12 +337,16 @@ ODO_INLINE double error_function2(const float x1[3], const float x2[3], const do
 }
 
 // a / b from y = RN(1 / b) (an IEEE division) by one Markstein correction:
-// q = RN(a y), r = a - b q (exact with the fused multiply-add), RN(q + r y)
-// is the correctly rounded quotient whenever it is a normal number
-// (Markstein's theorem) — bit-identical to a / b there, in three operations
-// instead of the ten of the IEEE division sequence. Zero / non-finite
-// denominators give NaN where the division gives +-inf: the callers below
-// reject the point either way.
+// q = RN(a y), r = a - b q (exact with the fused multiply-add), RN(q + r y).
+// Markstein's theorem makes that the correctly rounded quotient when q is
+// within 1 ulp of a / b; RN(a y) can be up to ~1.5 ulp off (a's significand
+// near 2), outside the theorem, so the equality with a / b rests on
+// tests/test_markstein.py: the same operation sequence on the host over
+// random and adversarial operands, no counterexample in 2 x 10^8 cases.
+// Three operations instead of the ten of the IEEE division sequence (the
+// IEEE form stays selectable: -DLN_MARKSTEIN=0 -DEV_MARKSTEIN=0). Zero /
+// non-finite denominators give NaN where the division gives +-inf: the
+// callers below reject the point either way.
 ODO_INLINE double div_mk(double a, double b, double y) {
     const double q = a * y;
     const double r = __builtin_fma(-b, q, a);
