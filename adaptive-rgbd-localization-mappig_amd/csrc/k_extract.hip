@@ -208,6 +208,15 @@ __global__ void __launch_bounds__(64 * FAST_CPW) k_fast_cells(const uint8_t* __r
     const int nq = cols > 6 ? m1 - m0 + 1 : 0;
     const int nitems = drows > 0 ? drows * nq : 0;
     const int qdq = nq > 0 ? 64 / nq : 0, qdr = nq > 0 ? 64 - qdq * nq : 0;
+    // detection bytes of quad m0 + j (bits i with sh+3 <= 4(m0+j)+i < sh+cols-3),
+    // 4 bits per quad: nq <= 16 for ROI_MAX <= 60 (the table is exact there;
+    // wider ROIs take the same test per quad)
+    uint64_t qmask = 0;
+    for (int j = 0; ROI_MAX <= 60 && j < nq && j < 16; j++) {
+        const int lo = sh + 3 - 4 * (m0 + j), hi = sh + cols - 3 - 4 * (m0 + j);  // valid i in [lo, hi)
+        const uint32_t vm = (lo <= 0 ? 0xFu : (0xFu << lo) & 0xFu) & (hi >= 4 ? 0xFu : ((1u << hi) - 1u));
+        qmask |= (uint64_t)vm << (4 * j);
+    }
     typedef short s16x2 __attribute__((ext_vector_type(2)));
     int count = 0;
     for (int attempt = 0; attempt < 2; attempt++) {
@@ -223,16 +232,15 @@ __global__ void __launch_bounds__(64 * FAST_CPW) k_fast_cells(const uint8_t* __r
         for (int base = 0; base < nitems; base += 64) {
             const int it = base + lane;
             uint32_t pass4 = 0;  // bit i: pixel 4m+i survives
-            int rowbase = 0, m = 0;
-            const int ii = qii;
-            m = m0 + qmm;
+            const int ii = qii, mq = qmm;
             qii += qdq;
             qmm += qdr;
             if (qmm >= nq) qmm -= nq, qii++;
+            const int m = m0 + mq;
+            // ROI byte offset of the quad (24-bit multiply: v_mul_u32_u24, not v_mul_lo_u32)
+            const int qoff = (int)__umul24((uint32_t)(3 + ii), (uint32_t)RS) + 4 * m;
             if (it < nitems) {
-                const int r = 3 + ii;
-                rowbase = r * RS;
-                const uint32_t* w = roi32 + r * RS4 + m;
+                const uint32_t* w = roi32 + (qoff >> 2);
                 const uint32_t Cw = w[0], Uw = w[-3 * RS4], Dw = w[3 * RS4];
                 const uint32_t Lw = __builtin_amdgcn_alignbyte(Cw, w[-1], 1);
                 const uint32_t Rw = __builtin_amdgcn_alignbyte(w[1], Cw, 3);
@@ -245,50 +253,44 @@ __global__ void __launch_bounds__(64 * FAST_CPW) k_fast_cells(const uint8_t* __r
                     *reinterpret_cast<uint32_t*>(&a4) = __builtin_amdgcn_perm(0u, Rw, sel);   // circle 4: +3 cols
                     *reinterpret_cast<uint32_t*>(&a8) = __builtin_amdgcn_perm(0u, Uw, sel);   // circle 8: -3 rows
                     *reinterpret_cast<uint32_t*>(&a12) = __builtin_amdgcn_perm(0u, Lw, sel);  // circle 12: -3 cols
-                    const s16x2 vm = v - thv, vp = v + thv;
-                    s16x2 t;
-                    t = a0 - vm;
-                    const uint32_t d0 = *reinterpret_cast<uint32_t*>(&t);
-                    t = a4 - vm;
-                    const uint32_t d4 = *reinterpret_cast<uint32_t*>(&t);
-                    t = a8 - vm;
-                    const uint32_t d8 = *reinterpret_cast<uint32_t*>(&t);
-                    t = a12 - vm;
-                    const uint32_t d12 = *reinterpret_cast<uint32_t*>(&t);
-                    t = vp - a0;
-                    const uint32_t b0 = *reinterpret_cast<uint32_t*>(&t);
-                    t = vp - a4;
-                    const uint32_t b4 = *reinterpret_cast<uint32_t*>(&t);
-                    t = vp - a8;
-                    const uint32_t b8 = *reinterpret_cast<uint32_t*>(&t);
-                    t = vp - a12;
-                    const uint32_t b12 = *reinterpret_cast<uint32_t*>(&t);
-                    // two adjacent compass points of one sign: (d0&d4)|(d4&d8)|(d8&d12)|(d12&d0)
-                    // = (d0|d8)&(d4|d12), on the sign bits
-                    const uint32_t pm = (((d0 | d8) & (d4 | d12)) | ((b0 | b8) & (b4 | b12))) & 0x80008000u;
+                    // two adjacent compass points below v - th: (a0|a8 dark) and
+                    // (a4|a12 dark) = max(min(a0, a8), min(a4, a12)) < v - th;
+                    // bright: min(max(a0, a8), max(a4, a12)) > v + th (sign bits of
+                    // the i16 differences; every value fits in [-255, 510])
+                    const s16x2 dk = __builtin_elementwise_max(__builtin_elementwise_min(a0, a8),
+                                                               __builtin_elementwise_min(a4, a12));
+                    const s16x2 bk = __builtin_elementwise_min(__builtin_elementwise_max(a0, a8),
+                                                               __builtin_elementwise_max(a4, a12));
+                    const s16x2 t1 = dk - (v - thv), t2 = (v + thv) - bk;
+                    const uint32_t pm =
+                        (*reinterpret_cast<const uint32_t*>(&t1) | *reinterpret_cast<const uint32_t*>(&t2)) & 0x80008000u;
                     pass4 |= ((pm >> 15) & 1u) << (2 * h);
                     pass4 |= (pm >> 31) << (2 * h + 1);
                 }
-                // keep detection bytes only: sh+3 <= 4m+i < sh+cols-3
-                const int lo = sh + 3 - 4 * m, hi = sh + cols - 3 - 4 * m;  // valid i in [lo, hi)
-                const uint32_t vm = (lo <= 0 ? 0xFu : (0xFu << lo) & 0xFu) & (hi >= 4 ? 0xFu : ((1u << hi) - 1u));
-                pass4 &= vm;
+                // keep detection bytes only: the quad's mask from the per-cell table
+                if (ROI_MAX <= 60) {
+                    pass4 &= (uint32_t)(qmask >> (4 * mq)) & 0xFu;
+                } else {
+                    const int lo = sh + 3 - 4 * m, hi = sh + cols - 3 - 4 * m;  // valid i in [lo, hi)
+                    pass4 &= (lo <= 0 ? 0xFu : (0xFu << lo) & 0xFu) & (hi >= 4 ? 0xFu : ((1u << hi) - 1u));
+                }
             }
-            // ordered compaction: lane order, then pixel order within the lane
-            int before = 0;
-            uint64_t bi[4];
+            // ordered compaction (lane order, then pixel order within the lane):
+            // this lane's survivors start after the counts of the lanes below,
+            // summed from three ballots of the count's bits
+            const uint32_t c = (uint32_t)__builtin_popcount(pass4);
+            const uint64_t B0 = __ballot(c & 1u), B1 = __ballot(c & 2u), B2 = __ballot(c & 4u);
+            int pos = n1 + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(B0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)B0, 0)) +
+                      2 * (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(B1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)B1, 0)) +
+                      4 * (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(B2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)B2, 0));
+            uint32_t pm4 = pass4;
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
-                bi[i] = __ballot((pass4 >> i) & 1u);
-                before += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bi[i] >> 32),
-                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)bi[i], 0));
-            }
-            int k = 0;
-#pragma unroll
-            for (int i = 0; i < 4; i++)
-                if ((pass4 >> i) & 1u) q1[n1 + before + k++] = (uint16_t)(rowbase + 4 * m + i);
-#pragma unroll
-            for (int i = 0; i < 4; i++) n1 += __popcll(bi[i]);
+            for (int k = 0; k < 4; k++)
+                if (pm4) {
+                    q1[pos++] = (uint16_t)(qoff + __builtin_ctz(pm4));
+                    pm4 &= pm4 - 1u;
+                }
+            n1 += __popcll(B0) + 2 * __popcll(B1) + 4 * __popcll(B2);
         }
         fast_wave_sync();
         // 2. segment test + cornerScore<16> of the survivors, two per lane in
@@ -1269,6 +1271,17 @@ ODO_INLINE void pyr_blur_level(const uint8_t* __restrict__ pyr, uint8_t* __restr
     for (int k = S.ebase[l] + t; k < S.ebase[l + 1]; k += PYR_TH)
         blur_edge_lane(pyr, blur, pyr_stride, lv, S, nlevels, f, k);
 }
+#ifdef ODO_PYR_PROFILE
+// -DODO_PYR_PROFILE: per frame of the last k_pyramid launch, wall-clock ticks
+// (10 ns) at the start, after gray, after each level's barrier and at the end
+// (read by odo_pyr_prof_read, tools/pyr_probe.py)
+#define PYR_PROF_MAX 1024
+__device__ uint64_t g_pyrprof[PYR_PROF_MAX * 20];
+#define PYR_PROF(k)                                                                   \
+    if (threadIdx.x == 0 && blockIdx.x < PYR_PROF_MAX) g_pyrprof[blockIdx.x * 20 + (k)] = wall_clock64()
+#else
+#define PYR_PROF(k)
+#endif
 template <bool BLUR>
 __global__ void __launch_bounds__(PYR_TH) k_pyramid(const uint8_t* __restrict__ bgr, uint8_t* __restrict__ pyr,
                                                     size_t in_stride, size_t pyr_stride,
@@ -1279,6 +1292,7 @@ __global__ void __launch_bounds__(PYR_TH) k_pyramid(const uint8_t* __restrict__ 
     const int f = blockIdx.x;
     const int t = threadIdx.x;
     uint8_t* base = pyr + (size_t)f * pyr_stride;
+    PYR_PROF(0);
     if (bgr) {
         // level 0: gray, 4 pixels per thread (k_gray's arithmetic)
         const LevelDesc L0 = lv[0];
@@ -1326,6 +1340,7 @@ __global__ void __launch_bounds__(PYR_TH) k_pyramid(const uint8_t* __restrict__ 
     }
     for (int l = 1; l < nlevels; l++) {
         __syncthreads();  // level l - 1 is complete
+        PYR_PROF(l);
         const LevelDesc S = lv[l - 1], D = lv[l];
         if (BLUR) pyr_blur_level(pyr, blur, pyr_stride, lv, BR, nlevels, f, l - 1, S, t);
         const int nq = (D.w + 3) >> 2;
@@ -1387,9 +1402,12 @@ __global__ void __launch_bounds__(PYR_TH) k_pyramid(const uint8_t* __restrict__ 
     }
     if (BLUR) {
         __syncthreads();  // the last level is complete
+        PYR_PROF(nlevels);
         const LevelDesc L = lv[nlevels - 1];
         pyr_blur_level(pyr, blur, pyr_stride, lv, BR, nlevels, f, nlevels - 1, L, t);
     }
+    __syncthreads();
+    PYR_PROF(nlevels + 1);
 }
 
 // ============================================================ host-side launch helpers
@@ -1573,3 +1591,12 @@ void launch_pair_valid(hipStream_t st, int* pv, int n, int first_valid) {
     hipLaunchKernelGGL(k_pair_valid, dim3((n + 255) / 256), dim3(256), 0, st, pv, n, first_valid);
 }
 }  // namespace odo
+#ifdef ODO_PYR_PROFILE
+extern "C" int odo_pyr_prof_read(uint64_t* out, int n) {
+    n = n < PYR_PROF_MAX ? n : PYR_PROF_MAX;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(odo::g_pyrprof), (size_t)n * 20 * sizeof(uint64_t)) != hipSuccess)
+        return -1;
+    return n;
+}
+#endif

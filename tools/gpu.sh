@@ -18,6 +18,8 @@
 #   pmc=REGEX           PMC passes over the kernels matching REGEX (tuning build,
 #                       serial streams), one counter group per rocprofv3 run
 #   pmch=REGEX          the same on the hard workload
+#   vtests=V:F1,F2      pytest -m gpu over the named files against variant build_V
+#   probe=V:SCRIPT      python tools/SCRIPT.py with ODO_LIB = variant build_V (probe builds)
 #   ab=N:V1,V2,...      A/B of library builds on the bench (N alternations); Vi is
 #                       "default" (libodo_hip.so) or a variant name (build_Vi/);
 #                       bench arguments from $AB_ARGS
@@ -61,6 +63,16 @@ for step in "$@"; do
       files=$(echo ${step#tests=} | tr ',' '\n' | sed 's|^|tests/|' | tr '\n' ' ')
       timeout -k 10 900 python -u -m pytest $files -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_part.log 2>&1
       tail -1 $O/pytest_part.log ;;
+    vtests=*)
+      spec=${step#vtests=}; v=${spec%%:*}
+      files=$(echo ${spec#*:} | tr ',' '\n' | sed 's|^|tests/|' | tr '\n' ' ')
+      ODO_LIB=$(lib_of $v) timeout -k 10 900 python -u -m pytest $files -m gpu -x -q --timeout 300 \
+        --timeout-method thread > $O/pytest_$v.log 2>&1
+      tail -1 $O/pytest_$v.log ;;
+    probe=*)
+      spec=${step#probe=}; v=${spec%%:*}; sc=${spec#*:}
+      ODO_LIB=$(lib_of $v) timeout -k 10 300 python tools/$sc.py > $O/probe_$sc.json 2> $O/probe_$sc.err
+      echo "probe $sc ok" ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
       tail -1 $O/smoke.log ;;
