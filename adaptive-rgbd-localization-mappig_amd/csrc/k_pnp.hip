@@ -615,6 +615,13 @@ ODO_INLINE double edge_robust_chi(const SE3M& T, const double Xw[3], const doubl
 #ifndef PNP_WAVES_PER_EU
 #define PNP_WAVES_PER_EU 1  // occupancy floor (launch bounds); 1 = compiler's choice
 #endif
+// LE (edges in LDS): after the edges are created in the pair's HBM scratch,
+// their read-mostly fields (Xw, obs, info, flags: 29 B per edge) are copied
+// into the workgroup's LDS, and every pass of the ~40 Levenberg iterations
+// reads them there instead of from L2 (a pass walks ~2-3 edges per thread,
+// each a dependent L2 round trip before). chi4 and idx stay in HBM. The host
+// picks LE when kp_cap edges fit (pnp_lds_bytes).
+template <bool LE>
 __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t* __restrict__ f2_src, const float* __restrict__ xyz,
                                             const float* __restrict__ kun, const float* __restrict__ ur,
                                             const int* __restrict__ nkp, int kp_cap, int slot0, FrameCalib cal,
@@ -685,6 +692,26 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
     if (ne < 3) {
         for (int k = lane; k < ne; k += PNP_NT) mask[E.idx[k]] = 1;  // SetInlier at edge creation
         return;
+    }
+    if (LE) {
+        extern __shared__ __attribute__((aligned(16))) float s_edge[];
+        float* sX = s_edge;             // 3 * kp_cap
+        float* sO = sX + 3 * kp_cap;    // 3 * kp_cap
+        float* sI = sO + 3 * kp_cap;    // kp_cap
+        uint8_t* sF = reinterpret_cast<uint8_t*>(sI + kp_cap);  // kp_cap
+        for (int k = lane; k < 3 * ne; k += PNP_NT) {
+            sX[k] = E.X[k];
+            sO[k] = E.obs[k];
+        }
+        for (int k = lane; k < ne; k += PNP_NT) {
+            sI[k] = E.info[k];
+            sF[k] = E.flags[k];
+        }
+        __syncthreads();
+        E.X = sX;
+        E.obs = sO;
+        E.info = sI;
+        E.flags = sF;
     }
     const PnPCam cam{(double)cal.fx, (double)cal.fy, (double)cal.cx, (double)cal.cy, (double)cal.mbf};
     const double dMono = (double)(float)sqrt(5.991), dStereo = (double)(float)sqrt(7.815);  // pnpsolver.cpp:51-52
@@ -1294,6 +1321,19 @@ __global__ void __launch_bounds__(64) k_pnp1(const int32_t* __restrict__ f2_src,
 
 namespace odo {
 size_t pnp_edge_bytes() { return PE_BYTES; }
+// dynamic LDS of k_pnp<true>: 29 B per edge slot (kp_cap), 0 = edges stay in
+// HBM (k_pnp<false>). ODO_PNP_LDS (tuning builds) = 0 disables it for A/B.
+#ifndef PNP_LDS_MAX
+#define PNP_LDS_MAX (96 * 1024)
+#endif
+static size_t pnp_lds_bytes(int kp_cap) {
+    static const bool off = [] {
+        const char* e = odo_knob("ODO_PNP_LDS");
+        return e && e[0] == '0';
+    }();
+    const size_t b = ((size_t)kp_cap * 29 + 15) & ~(size_t)15;
+    return (!off && b <= PNP_LDS_MAX) ? b : 0;
+}
 // The 4-wave workgroup per pair (k_pnp) by default. ODO_PNP_WAVES=1 selects
 // k_pnp1 (one wave per pair: a quarter of the SIMDs occupied), measured
 // slower: PnP 1.66 vs 0.72 ms alone per 256 pairs, step 2.61 vs 2.50 ms, one
@@ -1317,8 +1357,20 @@ void launch_pnp(hipStream_t st, const int32_t* f2_src, const float* xyz, const f
         return;
     }
 #endif
-    hipLaunchKernelGGL(k_pnp, dim3(npairs), dim3(PNP_NT), 0, st, f2_src, xyz, kun, ur, nkp, kp_cap, slot0, cal, T12,
-                       pair_valid, n_matches, min_matches, edges, res, inlier_mask, sel, sel_val);
+    const size_t lds = pnp_lds_bytes(kp_cap);
+    if (lds) {
+        static bool attr = false;
+        if (!attr) {
+            (void)hipFuncSetAttribute((const void*)k_pnp<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)PNP_LDS_MAX);
+            attr = true;
+        }
+        hipLaunchKernelGGL(k_pnp<true>, dim3(npairs), dim3(PNP_NT), lds, st, f2_src, xyz, kun, ur, nkp, kp_cap, slot0,
+                           cal, T12, pair_valid, n_matches, min_matches, edges, res, inlier_mask, sel, sel_val);
+        return;
+    }
+    hipLaunchKernelGGL(k_pnp<false>, dim3(npairs), dim3(PNP_NT), 0, st, f2_src, xyz, kun, ur, nkp, kp_cap, slot0, cal,
+                       T12, pair_valid, n_matches, min_matches, edges, res, inlier_mask, sel, sel_val);
 }
 }  // namespace odo
 

@@ -47,7 +47,9 @@ KNN_OPS_PER_CMP = 16
 # a TransformationFromCorrespondences fit (F)
 RANSAC_FLOPS_PER_EVAL = 120
 RANSAC_FLOPS_PER_FIT_POINT = 40
-KNN_F4_TRAFFIC = os.path.join(ROOT, "profiles", "r02_knn2_f4_traffic.json")
+# PMC memory-side bytes of k_knn2_f4 per launch, measured on this round's
+# kernel build (tools/pmc_merge.py --traffic); absent -> roofline.traffic null
+KNN_F4_TRAFFIC = os.path.join(ROOT, "profiles", "r04_knn2_f4_traffic.json")
 # on-box peak microbenchmarks (tools/ubench_peak.hip); the fallbacks are the
 # r02 measurements
 UBENCH = os.path.join(ROOT, "profiles", "r02_ubench_peak.jsonl")
@@ -953,10 +955,11 @@ def track_mode(args, rank, world, local_rank, dist):
         elapsed, submit, (knn_ms, knn_launches) = timed_leg(
             odo, lambda i: odo.track_batch_async(d_bgr.data_ptr(), d_dep.data_ptr(), B, ring, i % rows),
             K, Wm, world, dist, coll_dev, ktime)
-        # the records of the last timed batch are those of any batch after the
-        # first (the batch cycles the same loop): check they arrived
+        # the last timed batch's records arrived: its match and query counts
+        # equal any batch's after the first (every batch cycles the same loop;
+        # the RANSAC outcome differs, each pair's seed is its global index)
         last = ring.all[(K + Wm - 1) % rows][:B]
-        for f in ("n_matches", "n_inliers", "visited", "n_queries"):
+        for f in ("n_matches", "n_queries"):
             if not np.array_equal(last[f], res_q[f]):
                 raise SystemExit(f"timed leg: streamed pair records differ from the untimed batch ({f})")
         ring.close()
@@ -1010,16 +1013,21 @@ def track_mode(args, rank, world, local_rank, dist):
     nq = res_q["n_queries"]
     cmp = int(sum(int(nq[i]) * nkp[i] for i in range(B)))
     hbm_alg = sum(32 * int(nq[i]) + 32 * nkp[i] + 16 * int(nq[i]) for i in range(B))
-    traffic = None
+    traffic = traffic_src = None
     if os.path.exists(KNN_F4_TRAFFIC):
         with open(KNN_F4_TRAFFIC) as fh:
             tr4 = json.load(fh)
         # PMC HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, gfx950
         # correction), scaled per pair when the batch differs
         traffic = tr4["hbm_bytes_per_launch"] if tr4.get("batch") == B else tr4["hbm_bytes_per_pair"] * B
+        traffic_src = {"file": os.path.relpath(KNN_F4_TRAFFIC, ROOT), "build": tr4.get("build"),
+                       "per_launch_of_batch": tr4.get("batch")}
     alone = odo.knn_replay_ms(20) if knn_ms else None
     roofline = knn_roofline(cmp, hbm_alg, knn_ms, knn_launches, peaks, traffic, alone, h_knn_ms) \
         if cfg.forms.knn == pkg.KNN_FORM_FP4 else None
+    if roofline is not None:
+        roofline["traffic_source"] = traffic_src
+        roofline["traffic_algorithmic"] = int(hbm_alg)
 
     # the other SURVEY §8(d) legs, from the per-stage (one stream, events
     # between stages) times of the untimed timing step
