@@ -1257,6 +1257,9 @@ ODO_INLINE double readlane_d(double v, int l) {
 }
 #define LN_WAVES 4
 #define LN_RS 33  // LDS row stride (doubles) of the parked terms
+#ifndef LN_HELP
+#define LN_HELP 0  // 1: a wave whose pair has no hypothesis left joins another open pair that has
+#endif
 #ifndef LN_MARKSTEIN
 #define LN_MARKSTEIN 1  // sweep: ErrorFunction2 with Markstein-corrected quotients (0: IEEE divisions)
 #endif
@@ -1304,13 +1307,17 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
     const unsigned minInl = (unsigned)cfg.min_inlier_th;
     // waves_total >= open pairs: several waves per pair share its counter;
     // fewer: each wave walks its pairs in turn
-    const int iters = cnt > waves_total ? (cnt + waves_total - 1) / waves_total : 1;
     LP(uint64_t lp_t0 = wall_clock64(); uint64_t lp_rounds = 0, lp_nact = 0, lp_tfc = 0, lp_sweep = 0, lp_fold = 0;
        uint64_t lp_q = 0; int lp_pair = -1; uint64_t lp_inner = 0, lp_sum = 0;)
-    for (int it = 0; it < iters; it++) {
-        const int slot = gw + it * waves_total;
-        if (cnt > waves_total && slot >= cnt) break;
-        const int p = __builtin_amdgcn_readfirstlane(B.open_list[slot % cnt]);
+    // open-list slots: gw, gw + waves_total, ... (the pairs this wave owns),
+    // then with LN_HELP any open pair whose hypothesis counter has not run
+    // out, taken from a shared cursor (a wave leaves a pair once every lane
+    // is idle: the pair's counter is exhausted or its fold has stopped)
+    int slot = cnt > waves_total ? gw : gw % cnt;
+    int helps = 0;
+    for (;;) {
+        if (slot < 0) break;
+        const int p = __builtin_amdgcn_readfirstlane(B.open_list[slot]);
         RState* S = B.st + p;
         const int H = S->H, ng = S->ng, words = S->words;
         const GoodPt* P = B.gpts + (size_t)p * B.match_cap;
@@ -1511,6 +1518,27 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
                 h = -1;
             }
             LP(lp_fold += wall_clock64() - lp_q;)
+        }
+        // the next pair
+        if (cnt > waves_total && slot + waves_total < cnt) {
+            slot += waves_total;
+            continue;
+        }
+        slot = -1;
+        if (LN_HELP) {
+            // at most one scan of the open list per wave
+            while (helps < cnt) {
+                int c = 0;
+                if (lane == 0) c = atomicAdd(&B.open_cnt[1], 1);
+                c = __builtin_amdgcn_readfirstlane(c) % cnt;
+                helps++;
+                const int q = __builtin_amdgcn_readfirstlane(B.open_list[c]);
+                const RState* Q = B.st + q;
+                if (!ld_relaxed(&Q->done) && ld_relaxed(&Q->nexth) < Q->H) {
+                    slot = c;
+                    break;
+                }
+            }
         }
     }
 #ifdef ODO_LANES_PROFILE
@@ -1816,10 +1844,13 @@ struct Layout {
 
 // k_ransac_lanes grid: workgroups of LN_WAVES waves (ODO_RANSAC_LANES, 0 = the
 // wave-per-hypothesis work list k_ransac_eval_list instead)
+#ifndef LN_GROUPS
+#define LN_GROUPS 512
+#endif
 static int ln_groups() {
     static int r = [] {
         const char* e = odo_knob("ODO_RANSAC_LANES");
-        return e ? std::max(0, atoi(e)) : 512;
+        return e ? std::max(0, atoi(e)) : LN_GROUPS;
     }();
     return r;
 }
