@@ -144,6 +144,15 @@ __constant__ int c_circle_dy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0
 #ifndef FAST_CPW
 #define FAST_CPW 1
 #endif
+// FAST_PARTS > 1: the detection rows are tested in that many row parts, each
+// followed by its segment test and NMS, so the survivor queue holds one part
+// (+ one row: a part also scores the first row of the next, which the NMS of
+// its own last row reads; that row is scored again and output with the next
+// part). Less LDS per wave, more waves per CU; the same candidates in the
+// same order.
+#ifndef FAST_PARTS
+#define FAST_PARTS 1
+#endif
 ODO_INLINE void fast_wave_sync() {
     if (FAST_CPW == 1) {
         __syncthreads();
@@ -168,7 +177,8 @@ __global__ void __launch_bounds__(64 * FAST_CPW) k_fast_cells(const uint8_t* __r
     // writes entry n2 + rank <= base + lane only after reading entries
     // base..base+63, so unread entries are never overwritten): 8.9 KB of LDS
     // per single-wave workgroup, 4 waves per SIMD
-    __shared__ uint16_t q1_w[FAST_CPW][(ROI_MAX - 6) * (ROI_MAX - 6)];
+    constexpr int QROWS = FAST_PARTS == 1 ? ROI_MAX - 6 : (ROI_MAX - 6 + FAST_PARTS - 1) / FAST_PARTS + 1;
+    __shared__ uint16_t q1_w[FAST_CPW][QROWS * (ROI_MAX - 6)];
     const int wv = FAST_CPW == 1 ? 0 : (int)(threadIdx.x >> 6);
     uint32_t* const roi32 = roi32_w[wv];
     uint32_t* const score32 = score32_w[wv];
@@ -224,12 +234,19 @@ __global__ void __launch_bounds__(64 * FAST_CPW) k_fast_cells(const uint8_t* __r
         const int thc = th < 0 ? 0 : (th > 255 ? 255 : th);
         for (int w = lane; w < (rows * RS4 + 3) >> 2; w += 64) reinterpret_cast<uint4*>(score32)[w] = uint4{0, 0, 0, 0};
         fast_wave_sync();
+        for (int part = 0; part < FAST_PARTS; part++) {
+        // detection rows [ra, rb) are output by this part; the compass also
+        // covers row rb (scored for the NMS of row rb - 1) except in the last
+        const int ra = FAST_PARTS == 1 ? 0 : part * drows / FAST_PARTS;
+        const int rb = FAST_PARTS == 1 ? drows : (part + 1) * drows / FAST_PARTS;
+        const int rc = FAST_PARTS == 1 ? drows : min(rb + 1, drows);
+        const int ia = drows > 0 ? ra * nq : 0, ib = drows > 0 ? rc * nq : 0;
         // 1. compass pre-filter, 4 pixels per lane in 16-bit pairs: dark_k iff
         //    a_k - (v - th) < 0, bright_k iff (v + th) - a_k < 0 (sign bits)
         int n1 = 0;
         const s16x2 thv = {(short)thc, (short)thc};
-        int qii = nq > 0 ? lane / nq : 0, qmm = lane - qii * nq;  // item lane + base as (row, quad)
-        for (int base = 0; base < nitems; base += 64) {
+        int qii = nq > 0 ? (ia + lane) / nq : 0, qmm = nq > 0 ? ia + lane - qii * nq : 0;  // item as (row, quad)
+        for (int base = ia; base < ib; base += 64) {
             const int it = base + lane;
             uint32_t pass4 = 0;  // bit i: pixel 4m+i survives
             const int ii = qii, mq = qmm;
@@ -239,7 +256,7 @@ __global__ void __launch_bounds__(64 * FAST_CPW) k_fast_cells(const uint8_t* __r
             const int m = m0 + mq;
             // ROI byte offset of the quad (24-bit multiply: v_mul_u32_u24, not v_mul_lo_u32)
             const int qoff = (int)__umul24((uint32_t)(3 + ii), (uint32_t)RS) + 4 * m;
-            if (it < nitems) {
+            if (it < ib) {
                 const uint32_t* w = roi32 + (qoff >> 2);
                 const uint32_t Cw = w[0], Uw = w[-3 * RS4], Dw = w[3 * RS4];
                 const uint32_t Lw = __builtin_amdgcn_alignbyte(Cw, w[-1], 1);
@@ -360,7 +377,9 @@ __global__ void __launch_bounds__(64 * FAST_CPW) k_fast_cells(const uint8_t* __r
             n2 += __popcll(b0) + __popcll(b1);
         }
         fast_wave_sync();
-        // 3. NMS over the corner list (row-major), ordered compaction
+        // 3. NMS over the corner list (row-major), ordered compaction; the
+        //    corners of row rb (scored for this part's last row) wait for the
+        //    next part
         for (int base = 0; base < n2; base += 64) {
             const int idx = base + lane;
             bool keep = false;
@@ -368,9 +387,10 @@ __global__ void __launch_bounds__(64 * FAST_CPW) k_fast_cells(const uint8_t* __r
             if (idx < n2) {
                 const int o = q2[idx];
                 const int sc = score[o];
-                keep = sc > score[o - RS - 1] && sc > score[o - RS] && sc > score[o - RS + 1] && sc > score[o - 1] &&
-                       sc > score[o + 1] && sc > score[o + RS - 1] && sc > score[o + RS] && sc > score[o + RS + 1];
                 const int i = o / RS, j = o - i * RS - sh;
+                keep = (FAST_PARTS == 1 || i < 3 + rb) && sc > score[o - RS - 1] && sc > score[o - RS] &&
+                       sc > score[o - RS + 1] && sc > score[o - 1] && sc > score[o + 1] && sc > score[o + RS - 1] &&
+                       sc > score[o + RS] && sc > score[o + RS + 1];
                 packed = ((uint32_t)sc << 24) | ((uint32_t)(i + C.offy) << 12) | (uint32_t)(j + C.offx);
             }
             const uint64_t m = __ballot(keep);
@@ -380,6 +400,8 @@ __global__ void __launch_bounds__(64 * FAST_CPW) k_fast_cells(const uint8_t* __r
             }
             count += __popcll(m);
         }
+        if (FAST_PARTS > 1) fast_wave_sync();  // the queue is refilled by the next part
+        }  // part
         if (count > 0) break;
         fast_wave_sync();
     }
@@ -686,31 +708,20 @@ __global__ void __launch_bounds__(OT_THREADS) k_octree(const uint32_t* __restric
         } else {
             // ---------------- phase 2: divide the largest nodes first
             vcount = s_vcnt;
-            // bitonic sort of sortk[0..vcount) ascending by (cnt, seq)
-            int pw = 1;
-            while (pw < vcount) pw <<= 1;
-            for (int i = vcount + t; i < pw; i += OT_THREADS) sortk[i] = ~0ull;
-            __syncthreads();
-            for (int kk = 2; kk <= pw; kk <<= 1) {
-                for (int jj = kk >> 1; jj > 0; jj >>= 1) {
-                    for (int i = t; i < pw; i += OT_THREADS) {
-                        const int ixj = i ^ jj;
-                        if (ixj > i) {
-                            const uint64_t a = sortk[i], b = sortk[ixj];
-                            const bool up = (i & kk) == 0;
-                            if ((a > b) == up) {
-                                sortk[i] = b;
-                                sortk[ixj] = a;
-                            }
-                        }
-                    }
-                    __syncthreads();
-                }
-            }
-            // processing rank per node: node of sortk[vcount-1-j] is processed j-th
+            // processing rank per node, largest (cnt, seq) first: the node of
+            // the key with r smaller keys is processed (vcount - 1 - r)-th. The
+            // keys are distinct (seq is unique), so r is the key's position in
+            // ascending order; every thread counts it for its keys against all
+            // vcount keys (broadcast LDS reads, one barrier) instead of a
+            // bitonic sort's log^2 barrier steps.
             for (int i = t; i < S; i += OT_THREADS) iscr[i] = -1;
             __syncthreads();
-            for (int j = t; j < vcount; j += OT_THREADS) iscr[(int)(sortk[vcount - 1 - j] & 0xFFFF)] = j;
+            for (int i = t; i < vcount; i += OT_THREADS) {
+                const uint64_t ki = sortk[i];
+                int r = 0;
+                for (int j = 0; j < vcount; j++) r += sortk[j] < ki ? 1 : 0;
+                iscr[(int)(ki & 0xFFFF)] = vcount - 1 - r;
+            }
             __syncthreads();
             for (int i = t; i < 4 * S; i += OT_THREADS) cc[i] = 0;
             __syncthreads();

@@ -40,6 +40,9 @@ struct GoodPt {
 };
 
 #define EV_WAVES_C 4   // waves per k_ransac_eval workgroup (EV_WAVES below)
+#ifndef EV_ILP2
+#define EV_ILP2 0  // eval kernels' sweep: two 64-point chunks per pass, interleaved straight-line evaluations
+#endif
 #ifndef EV_MARKSTEIN
 #define EV_MARKSTEIN 1  // eval kernels' sweep: Markstein-corrected quotients (error_function2_mk)
 #endif
@@ -1039,6 +1042,46 @@ ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int 
             // ---- ComputeInliersAndError (ransac.cpp:315-348)
             double meanError = 0.0;
             unsigned cnt = 0;
+#if EV_ILP2
+            // two 64-point chunks per pass: their evaluations (straight-line,
+            // interleaved) first, then each chunk's ballot and ordered fold
+            double Tq[2][12];
+#pragma unroll
+            for (int i = 0; i < 12; i++) Tq[0][i] = Tq[1][i] = Td[i];
+            for (int c0 = 0; c0 < ng; c0 += 128) {
+                float xa[2][3], xb[2][3];
+                bool ok[2];
+#pragma unroll
+                for (int hh = 0; hh < 2; hh++) {
+                    const int k = c0 + 64 * hh + lane;
+                    GoodPt g{};
+                    if (k < ng) g = load_pt<CACHED>(P, k);
+                    ok[hh] = k < ng && !(g.sz == 0.0f || g.tx == 0.0f);
+                    xa[hh][0] = g.sx, xa[hh][1] = g.sy, xa[hh][2] = g.sz;
+                    xb[hh][0] = g.tx, xb[hh][1] = g.ty, xb[hh][2] = g.tz;
+                }
+                double e[2];
+                error_function2_bf2(xa, xb, Tq, K, e);
+#pragma unroll
+                for (int hh = 0; hh < 2; hh++) {
+                    const int cc = c0 + 64 * hh;
+                    if (cc >= ng) break;
+                    const double d = e[hh];
+                    const bool in = ok[hh] && !(d > th) && (d >= 0.0);
+                    const uint64_t bal = __ballot(in);
+                    if (in) L.dv[lane_rank(bal)] = d;
+                    if (lane == 0) {
+                        L.nw[cc >> 5] = (uint32_t)bal;
+                        if (cc + 32 < ng) L.nw[(cc >> 5) + 1] = (uint32_t)(bal >> 32);
+                    }
+                    wave_sync();
+                    const int nin = __popcll(bal);
+                    if (lane == 0) meanError = fold_dv(L, nin, meanError);
+                    cnt += (unsigned)nin;
+                    wave_sync();
+                }
+            }
+#else
             for (int c0 = 0; c0 < ng; c0 += 64) {
                 const int k = c0 + lane;
                 bool in = false;
@@ -1067,6 +1110,7 @@ ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int 
                 cnt += (unsigned)nin;
                 wave_sync();
             }
+#endif
             meanError = __shfl(meanError, 0);
             RP_ACC(t_sweep);
             // the fold already stopped before this hypothesis: nothing will read it
@@ -1266,6 +1310,12 @@ ODO_INLINE double readlane_d(double v, int l) {
 #ifndef LN_BPERM
 #define LN_BPERM 1  // sweep: hypothesis transforms by ds_bpermute (0: v_readlane pairs)
 #endif
+#ifndef LN_ILP2
+#define LN_ILP2 0  // sweep: two straight-line evaluations per lane and pass (error_function2_bf)
+#endif
+#ifndef LN_SUMB
+#define LN_SUMB 0  // sweep: a full chunk's parked terms read 8 at a time before the ordered sum
+#endif
 #ifdef ODO_LANES_PROFILE
 // -DODO_LANES_PROFILE: per wave of the last k_ransac_lanes launch: start, end,
 // loop rounds, sum of active lanes over the rounds, TFC / sweep ticks and the
@@ -1424,6 +1474,31 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
                 if (k + 32 < ng) gn = P[k + 32];
                 const bool skip = k >= ng || g.sz == 0.0f || g.tx == 0.0f;  // sic: target.x (ransac.cpp:326)
                 const float x1[3] = {g.sx, g.sy, g.sz}, x2[3] = {g.tx, g.ty, g.tz};
+#if LN_ILP2
+                // two hypotheses per lane and pass (slots i + hf, i + 2 + hf),
+                // straight-line evaluations the scheduler interleaves
+                for (int i = 0; i < nact; i += 4) {
+                    const int a0 = i + hf, a1 = i + 2 + hf;
+                    const int s0 = la[min(a0, nact - 1)], s1 = la[min(a1, nact - 1)];
+                    double Tq[2][12], e[2];
+#pragma unroll
+                    for (int q = 0; q < 12; q++) {
+                        Tq[0][q] = (double)__shfl(T[q], s0);
+                        Tq[1][q] = (double)__shfl(T[q], s1);
+                    }
+                    const float xp1[2][3] = {{x1[0], x1[1], x1[2]}, {x1[0], x1[1], x1[2]}};
+                    const float xp2[2][3] = {{x2[0], x2[1], x2[2]}, {x2[0], x2[1], x2[2]}};
+                    error_function2_bf2(xp1, xp2, Tq, K, e);
+                    const double e0 = e[0], e1 = e[1];
+                    const double v0 = (!skip & !(e0 > th) & (e0 >= 0.0)) ? e0 : -1.0;
+                    const double v1 = (!skip & !(e1 > th) & (e1 >= 0.0)) ? e1 : -1.0;
+                    // unconditional: a0, a1 <= 63, and rows >= nact are read by
+                    // no lane (a conditional store would pull each evaluation
+                    // into its own branch)
+                    lres[a0 * LN_RS + pj] = v0;
+                    lres[a1 * LN_RS + pj] = v1;
+                }
+#else
                 for (int i = 0; i < nact; i += 2) {
                     const int a = i + hf;  // this half's hypothesis slot
 #if LN_BPERM
@@ -1458,11 +1533,32 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
                     }
                     if (a < nact) lres[a * LN_RS + pj] = d;
                 }
+#endif
                 LP(const uint64_t lp_cb = wall_clock64(); lp_inner += lp_cb - lp_ca;)
                 wave_sync();
                 uint32_t word = 0;
                 if (act) {
                     const int nj = min(32, ng - c0);
+#if LN_SUMB
+                    // a full chunk: the 32 terms read 8 at a time ahead of
+                    // the (sequential, in point order) sum
+                    if (nj == 32) {
+#pragma unroll
+                        for (int j0 = 0; j0 < 32; j0 += 8) {
+                            double v[8];
+#pragma unroll
+                            for (int t = 0; t < 8; t++) v[t] = lres[rank * LN_RS + j0 + t];
+#pragma unroll
+                            for (int t = 0; t < 8; t++) {
+                                if (v[t] >= 0.0) {
+                                    meanError += v[t];
+                                    c++;
+                                    word |= 1u << (j0 + t);
+                                }
+                            }
+                        }
+                    } else
+#endif
                     for (int j = 0; j < nj; j++) {
                         const double v = lres[rank * LN_RS + j];
                         if (v >= 0.0) {

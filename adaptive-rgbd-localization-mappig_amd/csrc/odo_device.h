@@ -427,6 +427,129 @@ ODO_INLINE double error_function2_mk(const float x1[3], const float x2[3], const
     return r;
 }
 
+// error_function2_mk as straight-line code: every branch becomes a select
+// between the values both sides compute, so the scheduler can interleave two
+// evaluations (the pivots' square roots, reciprocals and quotients are one
+// long dependency chain; a wave running one evaluation at a time waits on
+// it). Same value as error_function2_mk for every point: each select takes
+// what the branch error_function2_mk follows computes, from the same
+// operations on the same operands; the values it drops are never read.
+ODO_INLINE double error_function2_bf(const float x1[3], const float x2[3], const double T[12], const MahalConst& K) {
+    const double a0 = x1[0], a1 = x1[1], a2 = x1[2];
+    const double mu0 = x2[0], mu1 = x2[1], mu2 = x2[2];
+    const double m0 = ((T[0] * a0 + T[1] * a1) + T[2] * a2) + T[3] * 1.0;
+    const double m1 = ((T[4] * a0 + T[5] * a1) + T[6] * a2) + T[7] * 1.0;
+    const double m2 = ((T[8] * a0 + T[9] * a1) + T[10] * a2) + T[11] * 1.0;
+    const double d0 = m0 - mu0, d1 = m1 - mu1, d2 = m2 - mu2;
+    const double dsq = sum3d(d0 * d0, d1 * d1, d2 * d2);
+    const double s1 = fmax(K.raster_cov_x, K.depth_cov), s2 = fmax(K.raster_cov_x, K.depth_cov);
+    // (non-short-circuit ors: no branch for the compiler to sink work into)
+    bool rej = __builtin_isnan(x1[2]) | __builtin_isnan(x2[2]) | (dsq > 2.0 * (s1 + s2)) | __builtin_isnan(d2);
+    const double R00 = T[0], R01 = T[1], R02 = T[2];
+    const double R10 = T[4], R11 = T[5], R12 = T[6];
+    const double R20 = T[8], R21 = T[9], R22 = T[10];
+    const double c00 = K.raster_cov_x * a2, c11 = K.raster_cov_y * a2, c22 = K.depth_cov;
+    const double R[3][3] = {{R00, R01, R02}, {R10, R11, R12}, {R20, R21, R22}};
+    const double Cd[3] = {c00, c11, c22};
+    double RtC[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) RtC[i][j] = R[j][i] * Cd[j];
+    const double cov2_0 = K.raster_cov_x * mu2, cov2_1 = K.raster_cov_y * mu2, cov2_2 = K.depth_cov;
+    const double A00 = sum3d(RtC[0][0] * R00, RtC[0][1] * R10, RtC[0][2] * R20) + cov2_0;
+    const double A10 = sum3d(RtC[1][0] * R00, RtC[1][1] * R10, RtC[1][2] * R20) + 0.0;
+    const double A11 = sum3d(RtC[1][0] * R01, RtC[1][1] * R11, RtC[1][2] * R21) + cov2_1;
+    const double A20 = sum3d(RtC[2][0] * R00, RtC[2][1] * R10, RtC[2][2] * R20) + 0.0;
+    const double A21 = sum3d(RtC[2][0] * R01, RtC[2][1] * R11, RtC[2][2] * R21) + 0.0;
+    const double A22 = sum3d(RtC[2][0] * R02, RtC[2][1] * R12, RtC[2][2] * R22) + cov2_2;
+    // the LLT's three nested pivot tests (p0, p1, p2): a failed test leaves
+    // the rest of the factor as A, and the reciprocals are of whatever pivot stands
+    const bool p0 = A00 > 0;
+    const double L00 = p0 ? sqrt(A00) : A00;
+    const double i00 = 1.0 / L00;
+    const double L10 = p0 ? div_mk(A10, L00, i00) : A10;
+    const double L20 = p0 ? div_mk(A20, L00, i00) : A20;
+    const double x11 = A11 - L10 * L10;
+    const bool p1 = p0 & (x11 > 0);
+    const double L11 = p1 ? sqrt(x11) : A11;
+    const double i11 = 1.0 / L11;
+    const double L21 = p1 ? div_mk(A21 - L20 * L10, L11, i11) : A21;
+    const double x22 = A22 - (L20 * L20 + L21 * L21);
+    const bool p2 = p1 & (x22 > 0);
+    const double L22 = p2 ? sqrt(x22) : A22;
+    const double i22 = 1.0 / L22;
+    const double y0 = div_mk(d0, L00, i00);
+    const double y1 = div_mk(d1 - L10 * y0, L11, i11);
+    const double y2 = div_mk(d2 - (L20 * y0 + L21 * y1), L22, i22);
+    const double z2 = div_mk(y2, L22, i22);
+    const double z1 = div_mk(y1 - L21 * z2, L11, i11);
+    const double z0 = div_mk(y0 - (L10 * z1 + L20 * z2), L00, i00);
+    const double r = sum3d(d0 * z0, d1 * z1, d2 * z2);
+    rej = rej | !(r >= 0.0);
+    return rej ? ODO_DBL_MAX : r;
+}
+
+// error_function2_bf twice, written in lockstep (each statement for both)
+// so the two dependency chains issue interleaved: e[k] ==
+// error_function2_bf(x1[k], x2[k], T[k], K). The callers pass one point under
+// two transforms (k_ransac_lanes) or two points under one transform
+// (k_ransac_eval); the shared terms fold together.
+#define EF2(stmt) _Pragma("unroll") for (int k = 0; k < 2; k++) { stmt; }
+ODO_INLINE void error_function2_bf2(const float x1[2][3], const float x2[2][3], const double T[2][12],
+                                    const MahalConst& K, double e[2]) {
+    const double s1 = fmax(K.raster_cov_x, K.depth_cov), s2 = fmax(K.raster_cov_x, K.depth_cov);
+    double a0[2], a1[2], a2[2], mu2[2], c00[2], c11[2], cov2_0[2], cov2_1[2];
+    const double c22 = K.depth_cov, cov2_2 = K.depth_cov;
+    EF2(a0[k] = x1[k][0]; a1[k] = x1[k][1]; a2[k] = x1[k][2]; mu2[k] = x2[k][2])
+    EF2(c00[k] = K.raster_cov_x * a2[k]; c11[k] = K.raster_cov_y * a2[k])
+    EF2(cov2_0[k] = K.raster_cov_x * mu2[k]; cov2_1[k] = K.raster_cov_y * mu2[k])
+    double d0[2], d1[2], d2[2];
+    bool rej[2];
+    EF2(d0[k] = (((T[k][0] * a0[k] + T[k][1] * a1[k]) + T[k][2] * a2[k]) + T[k][3] * 1.0) - (double)x2[k][0])
+    EF2(d1[k] = (((T[k][4] * a0[k] + T[k][5] * a1[k]) + T[k][6] * a2[k]) + T[k][7] * 1.0) - (double)x2[k][1])
+    EF2(d2[k] = (((T[k][8] * a0[k] + T[k][9] * a1[k]) + T[k][10] * a2[k]) + T[k][11] * 1.0) - mu2[k])
+    EF2(rej[k] = __builtin_isnan(x1[k][2]) | __builtin_isnan(x2[k][2]) |
+                 (sum3d(d0[k] * d0[k], d1[k] * d1[k], d2[k] * d2[k]) > 2.0 * (s1 + s2)) | __builtin_isnan(d2[k]))
+    // RtC[i][j] = R[j][i] * Cd[j]; A's lower triangle (error_function2_bf)
+    double A00[2], A10[2], A11[2], A20[2], A21[2], A22[2];
+    EF2(A00[k] = sum3d((T[k][0] * c00[k]) * T[k][0], (T[k][4] * c11[k]) * T[k][4], (T[k][8] * c22) * T[k][8]) +
+                 cov2_0[k])
+    EF2(A10[k] = sum3d((T[k][1] * c00[k]) * T[k][0], (T[k][5] * c11[k]) * T[k][4], (T[k][9] * c22) * T[k][8]) + 0.0)
+    EF2(A11[k] = sum3d((T[k][1] * c00[k]) * T[k][1], (T[k][5] * c11[k]) * T[k][5], (T[k][9] * c22) * T[k][9]) +
+                 cov2_1[k])
+    EF2(A20[k] = sum3d((T[k][2] * c00[k]) * T[k][0], (T[k][6] * c11[k]) * T[k][4], (T[k][10] * c22) * T[k][8]) + 0.0)
+    EF2(A21[k] = sum3d((T[k][2] * c00[k]) * T[k][1], (T[k][6] * c11[k]) * T[k][5], (T[k][10] * c22) * T[k][9]) + 0.0)
+    EF2(A22[k] = sum3d((T[k][2] * c00[k]) * T[k][2], (T[k][6] * c11[k]) * T[k][6], (T[k][10] * c22) * T[k][10]) +
+                 cov2_2)
+    bool p0[2], p1[2], p2[2];
+    double L00[2], i00[2], L10[2], L20[2], x11[2], L11[2], i11[2], L21[2], x22[2], L22[2], i22[2];
+    EF2(p0[k] = A00[k] > 0)
+    EF2(L00[k] = p0[k] ? sqrt(A00[k]) : A00[k])
+    EF2(i00[k] = 1.0 / L00[k])
+    EF2(L10[k] = p0[k] ? div_mk(A10[k], L00[k], i00[k]) : A10[k])
+    EF2(L20[k] = p0[k] ? div_mk(A20[k], L00[k], i00[k]) : A20[k])
+    EF2(x11[k] = A11[k] - L10[k] * L10[k])
+    EF2(p1[k] = p0[k] & (x11[k] > 0))
+    EF2(L11[k] = p1[k] ? sqrt(x11[k]) : A11[k])
+    EF2(i11[k] = 1.0 / L11[k])
+    EF2(L21[k] = p1[k] ? div_mk(A21[k] - L20[k] * L10[k], L11[k], i11[k]) : A21[k])
+    EF2(x22[k] = A22[k] - (L20[k] * L20[k] + L21[k] * L21[k]))
+    EF2(p2[k] = p1[k] & (x22[k] > 0))
+    EF2(L22[k] = p2[k] ? sqrt(x22[k]) : A22[k])
+    EF2(i22[k] = 1.0 / L22[k])
+    double y0[2], y1[2], y2[2], z0[2], z1[2], z2[2];
+    EF2(y0[k] = div_mk(d0[k], L00[k], i00[k]))
+    EF2(y1[k] = div_mk(d1[k] - L10[k] * y0[k], L11[k], i11[k]))
+    EF2(y2[k] = div_mk(d2[k] - (L20[k] * y0[k] + L21[k] * y1[k]), L22[k], i22[k]))
+    EF2(z2[k] = div_mk(y2[k], L22[k], i22[k]))
+    EF2(z1[k] = div_mk(y1[k] - L21[k] * z2[k], L11[k], i11[k]))
+    EF2(z0[k] = div_mk(y0[k] - (L10[k] * z1[k] + L20[k] * z2[k]), L00[k], i00[k]))
+    EF2(const double r = sum3d(d0[k] * z0[k], d1[k] * z1[k], d2[k] * z2[k]);
+        e[k] = (rej[k] | !(r >= 0.0)) ? ODO_DBL_MAX : r)
+}
+#undef EF2
+
 // ---------------------------------------- glibc TYPE_3 random_r (A.12)
 struct Rng {
     int32_t s[31];

@@ -71,8 +71,8 @@ for step in "$@"; do
       tail -1 $O/pytest_$v.log ;;
     probe=*)
       spec=${step#probe=}; v=${spec%%:*}; sc=${spec#*:}
-      ODO_LIB=$(lib_of $v) timeout -k 10 300 python tools/$sc.py > $O/probe_$sc.json 2> $O/probe_$sc.err
-      echo "probe $sc ok" ;;
+      ODO_LIB=$(lib_of $v) timeout -k 10 300 python tools/$sc.py > $O/probe_${v}_$sc.json 2> $O/probe_${v}_$sc.err
+      echo "probe $v $sc ok" ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
       tail -1 $O/smoke.log ;;
