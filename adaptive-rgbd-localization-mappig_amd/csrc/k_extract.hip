@@ -708,20 +708,31 @@ __global__ void __launch_bounds__(OT_THREADS) k_octree(const uint32_t* __restric
         } else {
             // ---------------- phase 2: divide the largest nodes first
             vcount = s_vcnt;
-            // processing rank per node, largest (cnt, seq) first: the node of
-            // the key with r smaller keys is processed (vcount - 1 - r)-th. The
-            // keys are distinct (seq is unique), so r is the key's position in
-            // ascending order; every thread counts it for its keys against all
-            // vcount keys (broadcast LDS reads, one barrier) instead of a
-            // bitonic sort's log^2 barrier steps.
+            // bitonic sort of sortk[0..vcount) ascending by (cnt, seq)
+            int pw = 1;
+            while (pw < vcount) pw <<= 1;
+            for (int i = vcount + t; i < pw; i += OT_THREADS) sortk[i] = ~0ull;
+            __syncthreads();
+            for (int kk = 2; kk <= pw; kk <<= 1) {
+                for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+                    for (int i = t; i < pw; i += OT_THREADS) {
+                        const int ixj = i ^ jj;
+                        if (ixj > i) {
+                            const uint64_t a = sortk[i], b = sortk[ixj];
+                            const bool up = (i & kk) == 0;
+                            if ((a > b) == up) {
+                                sortk[i] = b;
+                                sortk[ixj] = a;
+                            }
+                        }
+                    }
+                    __syncthreads();
+                }
+            }
+            // processing rank per node: node of sortk[vcount-1-j] is processed j-th
             for (int i = t; i < S; i += OT_THREADS) iscr[i] = -1;
             __syncthreads();
-            for (int i = t; i < vcount; i += OT_THREADS) {
-                const uint64_t ki = sortk[i];
-                int r = 0;
-                for (int j = 0; j < vcount; j++) r += sortk[j] < ki ? 1 : 0;
-                iscr[(int)(ki & 0xFFFF)] = vcount - 1 - r;
-            }
+            for (int j = t; j < vcount; j += OT_THREADS) iscr[(int)(sortk[vcount - 1 - j] & 0xFFFF)] = j;
             __syncthreads();
             for (int i = t; i < 4 * S; i += OT_THREADS) cc[i] = 0;
             __syncthreads();
@@ -1260,23 +1271,15 @@ __global__ void __launch_bounds__(256) k_blur_rows(const uint8_t* __restrict__ p
 struct PyrLevels {
     int rx_off[16], ry_off[16];
 };
-// Banded schedule (PyrBands, odo_internal.h): the frame is built in nb
-// horizontal bands; band k advances every level by the rows its sources allow
-// (level l rows whose resize source rows of level l - 1 are complete, blur
-// chunks whose 7-row window is complete), so the rows a level's blur and the
-// next level's resize read were written moments before by the same workgroup
-// and are still in the CU's L2 share, instead of a whole 307 KB level 0 that
-// 32 frames per XCD push out of the 4 MB L2 before it is read back. Every
-// pixel is computed by the same code as before: only the order changes.
 // the 7x7 blur of level l of frame f by the whole workgroup (PYR_TH threads:
 // 64 strip groups of 16 lanes, then the edge lanes)
 ODO_INLINE void pyr_blur_level(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur, size_t pyr_stride,
                                const LevelDesc* __restrict__ lv, const BlurRows& S, int nlevels, int f, int l,
-                               const LevelDesc& L, int t, int c0, int c1, int e0, int e1) {
+                               const LevelDesc& L, int t) {
     const uint32_t none[3] = {0, 0, 0};
-    const int items = c1 * S.nst[l];
+    const int items = S.base[l + 1] - S.base[l];
     const int g = t >> 4;
-    for (int it = c0 * S.nst[l] + g; it < items; it += PYR_TH / 16) {
+    for (int it = g; it < items; it += PYR_TH / 16) {
         const int chunk = it / S.nst[l], strip = it - chunk * S.nst[l];
         const int q = 1 + strip * 16 + (t & 15);
         const bool store = q <= S.nq[l];
@@ -1287,8 +1290,7 @@ ODO_INLINE void pyr_blur_level(const uint8_t* __restrict__ pyr, uint8_t* __restr
         uint8_t* dp = blur + (size_t)f * pyr_stride + L.off + (size_t)y0 * L.pitch + x;
         blur_walk<false, BR_R>(s0, dp, (size_t)L.pitch, L.h, y0, top, bottom, store, 0, 0, 0, none, none);
     }
-    const int ne = 1 + (L.w + 3) / 4 - (S.nq[l] + 1);  // edge quads per chunk (blur_edge_lane)
-    for (int k = S.ebase[l] + e0 * ne + t; k < S.ebase[l] + e1 * ne; k += PYR_TH)
+    for (int k = S.ebase[l] + t; k < S.ebase[l + 1]; k += PYR_TH)
         blur_edge_lane(pyr, blur, pyr_stride, lv, S, nlevels, f, k);
 }
 #ifdef ODO_PYR_PROFILE
@@ -1307,131 +1309,124 @@ __global__ void __launch_bounds__(PYR_TH) k_pyramid(const uint8_t* __restrict__ 
                                                     size_t in_stride, size_t pyr_stride,
                                                     const LevelDesc* __restrict__ lv, const ResizeX* __restrict__ xt,
                                                     const ResizeY* __restrict__ yt, PyrLevels PL, int nlevels,
-                                                    uint8_t* __restrict__ blur, BlurRows BR, PyrBands BP) {
+                                                    uint8_t* __restrict__ blur, BlurRows BR) {
     EXTRACT_PRIO();
     const int f = blockIdx.x;
     const int t = threadIdx.x;
     uint8_t* base = pyr + (size_t)f * pyr_stride;
     PYR_PROF(0);
-    for (int band = 0; band < BP.nb; band++) {
-        if (bgr) {
-            // level 0 rows [ga, gb): gray, 4 pixels per thread (k_gray's arithmetic)
-            const LevelDesc L0 = lv[0];
-            const int w = L0.w, pitch = L0.pitch;
-            const int ga = BP.rows[0][band], gb = BP.rows[0][band + 1];
-            const uint8_t* src = bgr + (size_t)f * in_stride;
-            if ((w & 3) == 0) {
-                const int qa = ga * (w >> 2), qb = gb * (w >> 2);
-                for (int q0 = qa + t; q0 < qb; q0 += PYR_GU * PYR_TH) {
-                    uint32_t wv[PYR_GU][3];
+    if (bgr) {
+        // level 0: gray, 4 pixels per thread (k_gray's arithmetic)
+        const LevelDesc L0 = lv[0];
+        const int w = L0.w, h = L0.h, pitch = L0.pitch;
+        const uint8_t* src = bgr + (size_t)f * in_stride;
+        const int npix = w * h;
+        if ((w & 3) == 0) {
+            const int nq4 = npix >> 2;
+            for (int q0 = t; q0 < nq4; q0 += PYR_GU * PYR_TH) {
+                uint32_t wv[PYR_GU][3];
 #pragma unroll
-                    for (int u = 0; u < PYR_GU; u++) {
-                        const int q = q0 + u * PYR_TH;
-                        if (q < qb) {
-                            const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src + (size_t)q * 12);
-                            wv[u][0] = s32[0], wv[u][1] = s32[1], wv[u][2] = s32[2];
-                        }
-                    }
-#pragma unroll
-                    for (int u = 0; u < PYR_GU; u++) {
-                        const int q = q0 + u * PYR_TH;
-                        if (q < qb) {
-                            const int p0 = q * 4, y = p0 / w, x = p0 - y * w;
-                            uint32_t out = 0;
-#pragma unroll
-                            for (int i = 0; i < 4; i++) {
-                                const int b = 3 * i;
-                                const uint32_t B = (wv[u][b >> 2] >> (8 * (b & 3))) & 0xffu;
-                                const uint32_t G = (wv[u][(b + 1) >> 2] >> (8 * ((b + 1) & 3))) & 0xffu;
-                                const uint32_t R = (wv[u][(b + 2) >> 2] >> (8 * ((b + 2) & 3))) & 0xffu;
-                                out |= ((B * 1868u + G * 9617u + R * 4899u + 8192u) >> 14) << (8 * i);
-                            }
-                            *reinterpret_cast<uint32_t*>(base + (size_t)y * pitch + x) = out;
-                        }
+                for (int u = 0; u < PYR_GU; u++) {
+                    const int q = q0 + u * PYR_TH;
+                    if (q < nq4) {
+                        const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src + (size_t)q * 12);
+                        wv[u][0] = s32[0], wv[u][1] = s32[1], wv[u][2] = s32[2];
                     }
                 }
-            } else {
-                for (int pp = ga * w + t; pp < gb * w; pp += PYR_TH) {
-                    const uint8_t* s = src + (size_t)pp * 3;
-                    const int yy = pp / w, xx = pp - yy * w;
-                    base[(size_t)yy * pitch + xx] =
-                        (uint8_t)(((uint32_t)s[0] * 1868u + (uint32_t)s[1] * 9617u + (uint32_t)s[2] * 4899u + 8192u) >> 14);
+#pragma unroll
+                for (int u = 0; u < PYR_GU; u++) {
+                    const int q = q0 + u * PYR_TH;
+                    if (q < nq4) {
+                        const int p0 = q * 4, y = p0 / w, x = p0 - y * w;
+                        uint32_t out = 0;
+#pragma unroll
+                        for (int i = 0; i < 4; i++) {
+                            const int b = 3 * i;
+                            const uint32_t B = (wv[u][b >> 2] >> (8 * (b & 3))) & 0xffu;
+                            const uint32_t G = (wv[u][(b + 1) >> 2] >> (8 * ((b + 1) & 3))) & 0xffu;
+                            const uint32_t R = (wv[u][(b + 2) >> 2] >> (8 * ((b + 2) & 3))) & 0xffu;
+                            out |= ((B * 1868u + G * 9617u + R * 4899u + 8192u) >> 14) << (8 * i);
+                        }
+                        *reinterpret_cast<uint32_t*>(base + (size_t)y * pitch + x) = out;
+                    }
                 }
             }
+        } else {
+            for (int p = t; p < npix; p += PYR_TH) {
+                const uint8_t* s = src + (size_t)p * 3;
+                const int yy = p / w, xx = p - yy * w;
+                base[(size_t)yy * pitch + xx] =
+                    (uint8_t)(((uint32_t)s[0] * 1868u + (uint32_t)s[1] * 9617u + (uint32_t)s[2] * 4899u + 8192u) >> 14);
+            }
         }
-        for (int l = 1; l < nlevels; l++) {
-            __syncthreads();  // this band's rows of level l - 1 are complete
-            if (band == 0) PYR_PROF(l);
-            const LevelDesc S = lv[l - 1], D = lv[l];
-            if (BLUR)
-                pyr_blur_level(pyr, blur, pyr_stride, lv, BR, nlevels, f, l - 1, S, t, BP.bch[l - 1][band],
-                               BP.bch[l - 1][band + 1], BP.ech[l - 1][band], BP.ech[l - 1][band + 1]);
-            const int ra = BP.rows[l][band], rb = BP.rows[l][band + 1];
-            if (ra >= rb) continue;
-            const int nq = (D.w + 3) >> 2;
-            const int P = PYR_TH / nq;  // row phases (the host checks nq <= PYR_TH)
-            if (t >= P * nq) continue;
-            const int ph = t / nq, q = t - ph * nq;
-            const ResizeX* X = xt + PL.rx_off[l];
-            const ResizeY* Y = yt + PL.ry_off[l];
-            // the quad's taps: window origin sx0(4q), per-pixel selectors and weights
-            const int x00 = X[4 * q].sx0;
-            const int wb = x00 & ~3, sh = x00 & 3;
-            uint32_t sel[4], wt[4];
+    }
+    for (int l = 1; l < nlevels; l++) {
+        __syncthreads();  // level l - 1 is complete
+        PYR_PROF(l);
+        const LevelDesc S = lv[l - 1], D = lv[l];
+        if (BLUR) pyr_blur_level(pyr, blur, pyr_stride, lv, BR, nlevels, f, l - 1, S, t);
+        const int nq = (D.w + 3) >> 2;
+        const int P = PYR_TH / nq;  // row phases (the host checks nq <= PYR_TH)
+        if (t >= P * nq) continue;
+        const int ph = t / nq, q = t - ph * nq;
+        const ResizeX* X = xt + PL.rx_off[l];
+        const ResizeY* Y = yt + PL.ry_off[l];
+        // the quad's taps: window origin sx0(4q), per-pixel selectors and weights
+        const int x00 = X[4 * q].sx0;
+        const int wb = x00 & ~3, sh = x00 & 3;
+        uint32_t sel[4], wt[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int dx = 4 * q + j;
+            if (dx < D.w) {
+                const ResizeX xj = X[dx];
+                const uint32_t r0 = (uint32_t)(xj.sx0 - x00), r1 = (uint32_t)(xj.sx1 - x00);  // 0..7
+                sel[j] = r0 | (0x0cu << 8) | (r1 << 16) | (0x0cu << 24);
+                wt[j] = (uint32_t)xj.a0 | ((uint32_t)xj.a1 << 16);
+            } else {
+                sel[j] = 0x0c0c0c0cu;  // past the level width: 0 (the row padding)
+                wt[j] = 0;
+            }
+        }
+        const uint8_t* sbase = base + S.off + wb;
+        uint8_t* dbase = base + D.off + 4 * q;
+        auto hsum = [&](const uint8_t* row, uint32_t (&h)[4]) {
+            const uint32_t* w32 = reinterpret_cast<const uint32_t*>(row);
+            const uint32_t w0 = w32[0], w1 = w32[1], w2 = w32[2];
+            const uint32_t A = __builtin_amdgcn_alignbyte(w1, w0, sh), B = __builtin_amdgcn_alignbyte(w2, w1, sh);
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                const int dx = 4 * q + j;
-                if (dx < D.w) {
-                    const ResizeX xj = X[dx];
-                    const uint32_t r0 = (uint32_t)(xj.sx0 - x00), r1 = (uint32_t)(xj.sx1 - x00);  // 0..7
-                    sel[j] = r0 | (0x0cu << 8) | (r1 << 16) | (0x0cu << 24);
-                    wt[j] = (uint32_t)xj.a0 | ((uint32_t)xj.a1 << 16);
-                } else {
-                    sel[j] = 0x0c0c0c0cu;  // past the level width: 0 (the row padding)
-                    wt[j] = 0;
-                }
+                typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+                h[j] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_perm(B, A, sel[j])),
+                                              __builtin_bit_cast(u16x2, wt[j]), 0u, false);
             }
-            const uint8_t* sbase = base + S.off + wb;
-            uint8_t* dbase = base + D.off + 4 * q;
-            auto hsum = [&](const uint8_t* row, uint32_t (&h)[4]) {
-                const uint32_t* w32 = reinterpret_cast<const uint32_t*>(row);
-                const uint32_t w0 = w32[0], w1 = w32[1], w2 = w32[2];
-                const uint32_t A = __builtin_amdgcn_alignbyte(w1, w0, sh), B = __builtin_amdgcn_alignbyte(w2, w1, sh);
+        };
+        for (int y = ph; y < D.h; y += PYR_RU * P) {
+            ResizeY Yr[PYR_RU];
 #pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-                    h[j] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_perm(B, A, sel[j])),
-                                                  __builtin_bit_cast(u16x2, wt[j]), 0u, false);
-                }
-            };
-            for (int y = ra + ph; y < rb; y += PYR_RU * P) {
-                ResizeY Yr[PYR_RU];
+            for (int u = 0; u < PYR_RU; u++) Yr[u] = Y[min(y + u * P, D.h - 1)];
+            uint32_t h0[PYR_RU][4], h1[PYR_RU][4];
 #pragma unroll
-                for (int u = 0; u < PYR_RU; u++) Yr[u] = Y[min(y + u * P, rb - 1)];
-                uint32_t h0[PYR_RU][4], h1[PYR_RU][4];
+            for (int u = 0; u < PYR_RU; u++) {
+                hsum(sbase + (size_t)Yr[u].sy0 * S.pitch, h0[u]);
+                hsum(sbase + (size_t)Yr[u].sy1 * S.pitch, h1[u]);
+            }
 #pragma unroll
-                for (int u = 0; u < PYR_RU; u++) {
-                    hsum(sbase + (size_t)Yr[u].sy0 * S.pitch, h0[u]);
-                    hsum(sbase + (size_t)Yr[u].sy1 * S.pitch, h1[u]);
-                }
+            for (int u = 0; u < PYR_RU; u++) {
+                uint32_t pk = 0;
 #pragma unroll
-                for (int u = 0; u < PYR_RU; u++) {
-                    uint32_t pk = 0;
-#pragma unroll
-                    for (int j = 0; j < 4; j++)
-                        pk |= min((__umul24(h0[u][j], (uint32_t)Yr[u].b0) + __umul24(h1[u][j], (uint32_t)Yr[u].b1) + (1u << 21)) >> 22,
-                                  255u) << (8 * j);
-                    if (y + u * P < rb) *reinterpret_cast<uint32_t*>(dbase + (size_t)(y + u * P) * D.pitch) = pk;
-                }
+                for (int j = 0; j < 4; j++)
+                    pk |= min((__umul24(h0[u][j], (uint32_t)Yr[u].b0) + __umul24(h1[u][j], (uint32_t)Yr[u].b1) + (1u << 21)) >> 22,
+                              255u) << (8 * j);
+                if (y + u * P < D.h) *reinterpret_cast<uint32_t*>(dbase + (size_t)(y + u * P) * D.pitch) = pk;
             }
         }
-        if (BLUR) {
-            __syncthreads();  // this band's rows of the last level are complete
-            if (band == BP.nb - 1) PYR_PROF(nlevels);
-            const LevelDesc L = lv[nlevels - 1];
-            pyr_blur_level(pyr, blur, pyr_stride, lv, BR, nlevels, f, nlevels - 1, L, t, BP.bch[nlevels - 1][band],
-                           BP.bch[nlevels - 1][band + 1], BP.ech[nlevels - 1][band], BP.ech[nlevels - 1][band + 1]);
-        }
+    }
+    if (BLUR) {
+        __syncthreads();  // the last level is complete
+        PYR_PROF(nlevels);
+        const LevelDesc L = lv[nlevels - 1];
+        pyr_blur_level(pyr, blur, pyr_stride, lv, BR, nlevels, f, nlevels - 1, L, t);
     }
     __syncthreads();
     PYR_PROF(nlevels + 1);
@@ -1475,51 +1470,19 @@ bool pyramid_blur_fusable(const LevelDesc* lv_host, int nlevels) {
     BlurRows R;
     return blur_rows_plan(lv_host, nlevels, R);
 }
-void pyramid_band_plan(const LevelDesc* lv_host, const ResizeY* ry_host, const int* ry_off, int nlevels, int nb,
-                       PyrBands& B) {
-    B = PyrBands{};
-    nb = std::max(1, std::min(nb, PYR_MAXB));
-    B.nb = nb;
-    nlevels = std::min(nlevels, 16);
-    for (int k = 0; k <= nb; k++) {
-        // level 0: the gray rows of bands 0..k-1
-        const int h0 = lv_host[0].h;
-        B.rows[0][k] = (int)(((long)h0 * k + nb - 1) / nb);
-        for (int l = 1; l < nlevels; l++) {
-            // level l rows whose two source rows of level l - 1 are complete
-            const int hs = lv_host[l - 1].h, hd = lv_host[l].h, done = B.rows[l - 1][k];
-            int r = 0;
-            if (done >= hs) r = hd;
-            else
-                while (r < hd && ry_host[ry_off[l] + r].sy1 < done) r++;
-            B.rows[l][k] = r;
-        }
-        for (int l = 0; l < nlevels; l++) {
-            // blur chunks whose input rows (7-row windows, reflected at the level's edges) are complete
-            const int h = lv_host[l].h, done = B.rows[l][k];
-            const int nch = (h + BR_R - 1) / BR_R, nche = (h + BR_RE - 1) / BR_RE;
-            int c = 0;
-            while (c < nch && std::min(std::min(c * BR_R, h - BR_R) + BR_R + 3, h) <= done) c++;
-            int e = 0;
-            while (e < nche && std::min(std::min(e * BR_RE, h - BR_RE) + BR_RE + 3, h) <= done) e++;
-            B.bch[l][k] = c;
-            B.ech[l][k] = e;
-        }
-    }
-}
 void launch_pyramid(hipStream_t st, const uint8_t* bgr, uint8_t* pyr, size_t in_stride, size_t pyr_stride,
                     const LevelDesc* lv, const ResizeX* rx, const ResizeY* ry, const int* rx_off, const int* ry_off,
-                    int nlevels, int nframes, uint8_t* blur, const LevelDesc* lv_host, const PyrBands& bands) {
+                    int nlevels, int nframes, uint8_t* blur, const LevelDesc* lv_host) {
     PyrLevels PL{};
     for (int l = 0; l < nlevels && l < 16; l++) PL.rx_off[l] = rx_off[l], PL.ry_off[l] = ry_off[l];
     BlurRows BR{};
     if (blur && blur_rows_plan(lv_host, nlevels, BR)) {
         hipLaunchKernelGGL(k_pyramid<true>, dim3(nframes), dim3(PYR_TH), 0, st, bgr, pyr, in_stride, pyr_stride, lv,
-                           rx, ry, PL, nlevels, blur, BR, bands);
+                           rx, ry, PL, nlevels, blur, BR);
         return;
     }
     hipLaunchKernelGGL(k_pyramid<false>, dim3(nframes), dim3(PYR_TH), 0, st, bgr, pyr, in_stride, pyr_stride, lv, rx,
-                       ry, PL, nlevels, (uint8_t*)nullptr, BR, bands);
+                       ry, PL, nlevels, (uint8_t*)nullptr, BR);
 }
 bool pyramid_fusable(const LevelDesc* lv_host, const ResizeX* rx, const int* rx_off, int nlevels) {
     if (nlevels > 16) return false;

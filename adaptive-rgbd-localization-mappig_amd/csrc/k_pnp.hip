@@ -454,6 +454,9 @@ ODO_INLINE void huber_rho(double delta, double chi, double rho[3]) {
 #define PNP_NW 4  // waves per pair
 #endif
 #define PNP_NT (64 * PNP_NW)
+#ifndef PNP_CHI_LDS
+#define PNP_CHI_LDS 0  // LE: the chi passes' per-edge chi2 as floats in LDS (16 B per edge more)
+#endif
 #define PNP_K 4  // Levenberg trials evaluated per edge pass (one per 16-lane group of wave 0)
 #ifndef PNP_SPD_SOLVE
 #define PNP_SPD_SOLVE 1  // trial solves without Eigen's pivoting (ldlt_solve6_spd; 0: pivoted)
@@ -693,12 +696,18 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
         for (int k = lane; k < ne; k += PNP_NT) mask[E.idx[k]] = 1;  // SetInlier at edge creation
         return;
     }
+    // the chi2 each chi pass stores per edge and trial slot, read back by the
+    // classification only as (float)chi2: with LE and PNP_CHI_LDS the float
+    // itself, in LDS (no global stores in the passes: every barrier would
+    // wait for them)
+    float* sC = nullptr;
     if (LE) {
         extern __shared__ __attribute__((aligned(16))) float s_edge[];
         float* sX = s_edge;             // 3 * kp_cap
         float* sO = sX + 3 * kp_cap;    // 3 * kp_cap
         float* sI = sO + 3 * kp_cap;    // kp_cap
         uint8_t* sF = reinterpret_cast<uint8_t*>(sI + kp_cap);  // kp_cap
+        if (PNP_CHI_LDS) sC = reinterpret_cast<float*>(sF + kp_cap);  // 4 * kp_cap (kp_cap % 64 == 0)
         for (int k = lane; k < 3 * ne; k += PNP_NT) {
             sX[k] = E.X[k];
             sO[k] = E.obs[k];
@@ -891,7 +900,8 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                         if (k >= K) break;
                         double c2;
                         chi[k] += edge_robust_chi_q(Tc[k], Xw, ob, info, fl, cam, dMono, dStereo, c2);
-                        E.chi4[4 * e + k] = c2;
+                        if (LE && PNP_CHI_LDS) sC[4 * e + k] = (float)c2;
+                        else E.chi4[4 * e + k] = c2;
                     }
                 }
                 wg_sum<PNP_K>(chi, red);
@@ -936,15 +946,19 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
             // computeActiveErrors, recomputed at T for the edges that were out
             auto classify = [&](int k, uint32_t fl, const double Xw[3], const double ob[3], double info) {
                 const bool st = fl & PE_STEREO;
-                double c2 = E.chi4[4 * k + last_slot];
+                float chi2;
                 if (fl & PE_OUT) {  // IsOutlier: e->computeError() at the current estimate
                     double Xc[3], e[3];
                     se3m_map(Tm, Xw, Xc);
                     edge_err(Xc, ob, st, cam, e);
-                    c2 = chi2_of(e, info, st);
-                    E.chi4[4 * k + last_slot] = c2;
+                    const double c2 = chi2_of(e, info, st);
+                    // (never read back: an edge out during the next round is
+                    // recomputed here, one in is rewritten by its chi passes)
+                    if (!(LE && PNP_CHI_LDS)) E.chi4[4 * k + last_slot] = c2;
+                    chi2 = (float)c2;
+                } else {
+                    chi2 = (LE && PNP_CHI_LDS) ? sC[4 * k + last_slot] : (float)E.chi4[4 * k + last_slot];
                 }
-                const float chi2 = (float)c2;
                 if (chi2 > (st ? chi2Stereo : chi2Mono)) {
                     fl |= PE_OUT;
                     bad++;
@@ -1331,7 +1345,7 @@ static size_t pnp_lds_bytes(int kp_cap) {
         const char* e = odo_knob("ODO_PNP_LDS");
         return e && e[0] == '0';
     }();
-    const size_t b = ((size_t)kp_cap * 29 + 15) & ~(size_t)15;
+    const size_t b = ((size_t)kp_cap * (PNP_CHI_LDS ? 45 : 29) + 15) & ~(size_t)15;
     return (!off && b <= PNP_LDS_MAX) ? b : 0;
 }
 // The 4-wave workgroup per pair (k_pnp) by default. ODO_PNP_WAVES=1 selects

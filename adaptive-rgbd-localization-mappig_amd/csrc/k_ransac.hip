@@ -1313,6 +1313,12 @@ ODO_INLINE double readlane_d(double v, int l) {
 #ifndef LN_ILP2
 #define LN_ILP2 0  // sweep: two straight-line evaluations per lane and pass (error_function2_bf)
 #endif
+#ifndef LN_TFCU
+#define LN_TFCU 0  // refinement TFC: four points per step, branch-free adds (TFC::add_sel)
+#endif
+#ifndef LN_COMPACT
+#define LN_COMPACT 0  // sweep: shortcut test for every pair first, full evaluations only for the survivors
+#endif
 #ifndef LN_SUMB
 #define LN_SUMB 0  // sweep: a full chunk's parked terms read 8 at a time before the ordered sum
 #endif
@@ -1322,7 +1328,7 @@ ODO_INLINE double readlane_d(double v, int l) {
 // sweep's evaluation / ordered-sum parts (10 ns wall-clock ticks; read by
 // odo_lanes_prof_read, tools/lanes_probe.py)
 #define LPROF_MAX 4096
-__device__ uint64_t g_lprof[LPROF_MAX * 8];
+__device__ uint64_t g_lprof[LPROF_MAX * 10];
 #define LP(...) __VA_ARGS__
 #else
 #define LP(...)
@@ -1346,6 +1352,10 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
     __shared__ int s_la[LN_WAVES][64];
     double* lres = s_res[wv];
     int* la = s_la[wv];
+#if LN_COMPACT
+    __shared__ int s_lq[LN_WAVES][128];  // phase-1 queue: (slot << 5) | point
+    int* lq = s_lq[wv];
+#endif
     const int cnt = B.open_cnt[0];
     if (cnt < min_open || cnt <= 0) return;  // few open pairs: latency matters, k_ransac_eval_list takes them
     uint32_t* slab = lane_slab + (size_t)gw * 2 * B.mask_words * 64;
@@ -1358,7 +1368,7 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
     // waves_total >= open pairs: several waves per pair share its counter;
     // fewer: each wave walks its pairs in turn
     LP(uint64_t lp_t0 = wall_clock64(); uint64_t lp_rounds = 0, lp_nact = 0, lp_tfc = 0, lp_sweep = 0, lp_fold = 0;
-       uint64_t lp_q = 0; int lp_pair = -1; uint64_t lp_inner = 0, lp_sum = 0;)
+       uint64_t lp_q = 0; int lp_pair = -1; uint64_t lp_inner = 0, lp_sum = 0, lp_p1 = 0, lp_p2 = 0;)
     // open-list slots: gw, gw + waves_total, ... (the pairs this wave owns),
     // then with LN_HELP any open pair whose hypothesis counter has not run
     // out, taken from a shared cursor (a wave leaves a pair once every lane
@@ -1433,6 +1443,22 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
                         q1 = inset && c1 + 32 < ng ? cw[(size_t)(w1 + 1) * 64 + lane] : 0u;
                     }
                     const int n = min(64, ng - c0);
+#if LN_TFCU
+                    // four points per step, their LDS reads first, the adds
+                    // branch-free (the next point's division overlaps)
+                    for (int j0 = 0; j0 < n; j0 += 4) {
+                        GoodPt g4[4];
+#pragma unroll
+                        for (int t = 0; t < 4; t++) g4[t] = lp[min(j0 + t, n - 1)];
+#pragma unroll
+                        for (int t = 0; t < 4; t++) {
+                            const int j = j0 + t;
+                            const bool in = j < n && tfc_point_ok(g4[t]) && ((((j < 32) ? b0 : b1) >> (j & 31)) & 1u);
+                            tf.add_sel(g4[t].sx, g4[t].sy, g4[t].sz, g4[t].tx, g4[t].ty, g4[t].tz, g4[t].w, in);
+                            nfit += in;
+                        }
+                    }
+#else
                     for (int j = 0; j < n; j++) {
                         const GoodPt g = lp[j];
                         if (!tfc_point_ok(g)) continue;  // uniform
@@ -1441,6 +1467,7 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
                             nfit++;
                         }
                     }
+#endif
                 }
             }
             float T[12];
@@ -1474,7 +1501,50 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
                 if (k + 32 < ng) gn = P[k + 32];
                 const bool skip = k >= ng || g.sz == 0.0f || g.tx == 0.0f;  // sic: target.x (ransac.cpp:326)
                 const float x1[3] = {g.sx, g.sy, g.sz}, x2[3] = {g.tx, g.ty, g.tz};
-#if LN_ILP2
+#if LN_COMPACT
+                // Two phases. 1: lanes (point pj, half hf) run only the
+                // shortcut test for hypothesis slot i + hf; rejected pairs park
+                // -1 at once, the others queue (slot, point) in LDS. 2: every
+                // 64 queued pairs, one full evaluation per lane. Bad
+                // hypotheses reject most points at the shortcut, so most of the
+                // covariance solves (~200 of the ~225 FP64 instructions of an
+                // evaluation) are never issued.
+                if (hf == 0) lp[pj] = g;  // the chunk's points, for phase 2
+                int qn = 0;
+                auto phase2 = [&](int base, int cnt) {
+                    wave_sync();
+                    const int e = lq[base + min(lane, cnt - 1)];
+                    const int a = e >> 5, pq = e & 31;
+                    const int src = la[a];
+                    double Ta[12];
+#pragma unroll
+                    for (int q = 0; q < 12; q++) Ta[q] = (double)__shfl(T[q], src);
+                    const GoodPt g2 = lp[pq];
+                    const float y1[3] = {g2.sx, g2.sy, g2.sz}, y2[3] = {g2.tx, g2.ty, g2.tz};
+                    const double ev = error_function2_bf(y1, y2, Ta, K);
+                    if (lane < cnt) lres[a * LN_RS + pq] = (!(ev > th) && (ev >= 0.0)) ? ev : -1.0;
+                    LP(lp_p2 += cnt;)
+                };
+                for (int i = 0; i < nact; i += 2) {
+                    const int a = i + hf;
+                    const int src = la[min(a, nact - 1)];
+                    double Ta[12];
+#pragma unroll
+                    for (int q = 0; q < 12; q++) Ta[q] = (double)__shfl(T[q], src);
+                    const bool pass = a < nact && !skip && !error_function2_shortcut(x1, x2, Ta, K);
+                    const uint64_t bal = __ballot(pass);
+                    if (pass) lq[qn + (int)lane_rank(bal)] = (a << 5) | pj;
+                    else if (a < nact) lres[a * LN_RS + pj] = -1.0;
+                    qn += __popcll(bal);
+                    LP(lp_p1 += __popcll(__ballot(a < nact));)
+                    if (qn >= 64) {
+                        phase2(qn - 64, 64);
+                        qn -= 64;
+                        wave_sync();  // the entries were read before the queue refills
+                    }
+                }
+                if (qn > 0) phase2(0, qn);
+#elif LN_ILP2
                 // two hypotheses per lane and pass (slots i + hf, i + 2 + hf),
                 // straight-line evaluations the scheduler interleaves
                 for (int i = 0; i < nact; i += 4) {
@@ -1639,9 +1709,9 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
     }
 #ifdef ODO_LANES_PROFILE
     if (lane == 0 && gw < LPROF_MAX) {
-        uint64_t* r = g_lprof + (size_t)gw * 8;
+        uint64_t* r = g_lprof + (size_t)gw * 10;
         r[0] = lp_t0, r[1] = wall_clock64(), r[2] = lp_rounds, r[3] = lp_nact, r[4] = lp_tfc, r[5] = lp_sweep,
-        r[6] = lp_inner, r[7] = lp_sum;  // (fold time and pair: lp_fold, lp_pair)
+        r[6] = lp_inner, r[7] = lp_sum, r[8] = lp_p1, r[9] = lp_p2;  // (fold time and pair: lp_fold, lp_pair)
     }
 #endif
 }
@@ -2272,7 +2342,7 @@ int hyp_payload_words(int ng) { return HYP_PAYLOAD_HDR + 4 * std::max(ng, 0); }
 extern "C" int odo_lanes_prof_read(uint64_t* out, int n) {
     n = std::min(n, LPROF_MAX);
     if (hipDeviceSynchronize() != hipSuccess) return -1;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(odo::g_lprof), (size_t)n * 8 * sizeof(uint64_t)) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(odo::g_lprof), (size_t)n * 10 * sizeof(uint64_t)) != hipSuccess) return -1;
     return n;
 }
 #endif

@@ -157,7 +157,6 @@ struct odo_ctx {
     // leave most CUs idle, one frame takes 0.45 vs 0.28 ms)
     int pform = ODO_PYRAMID_FORM_AUTO;
     bool pyr_fusable = false, blur_fusable = false;
-    PyrBands pyr_bands{};  // k_pyramid's banded schedule (computed with the resize tables)
     LevelDesc* lv = nullptr;
     CellDesc* cells = nullptr;
     ResizeX* rx = nullptr;
@@ -788,16 +787,6 @@ static int build_geometry(odo_ctx* c) {
     if (const char* e = odo_knob("ODO_PYRAMID_FORM")) c->pform = atoi(e);  // tuning build: A/B without a config change
     c->pyr_fusable = pyramid_fusable(c->lv_h.data(), rx.data(), c->rx_off.data(), p.nlevels);
     c->blur_fusable = c->pyr_fusable && pyramid_blur_fusable(c->lv_h.data(), p.nlevels);
-    {
-        // bands of k_pyramid: level-0 bands of <= ~80 KB (a CU's share of the
-        // XCD's 4 MB L2 is 128 KB); ODO_PYR_BANDS (tuning) overrides
-        int nb = std::min(PYR_MAXB, std::max(1, (int)(((long)c->lv_h[0].pitch * c->lv_h[0].h + 81919) / 81920)));
-#ifdef PYR_BANDS
-        nb = PYR_BANDS;
-#endif
-        if (const char* e = odo_knob("ODO_PYR_BANDS")) nb = std::max(1, std::min(PYR_MAXB, atoi(e)));
-        if (p.nlevels <= 16) pyramid_band_plan(c->lv_h.data(), ry.data(), c->ry_off.data(), p.nlevels, nb, c->pyr_bands);
-    }
     int e;
     if ((e = dalloc(&c->lv, c->lv_h.size()))) return e;
     if ((e = dalloc(&c->cells, c->cells_h.size()))) return e;
@@ -1185,7 +1174,7 @@ static bool build_pyramid(odo_ctx* c, hipStream_t st, const uint8_t* d_bgr, uint
             d_bgr = nullptr;
         }
         launch_pyramid(st, d_bgr, pyr, (size_t)c->W * c->H * 3, P, c->lv, c->rx, c->ry, c->rx_off.data(),
-                       c->ry_off.data(), c->nlevels, n, blur, c->lv_h.data(), c->pyr_bands);
+                       c->ry_off.data(), c->nlevels, n, blur, c->lv_h.data());
         return blur != nullptr;
     }
     if (d_bgr) launch_gray(st, d_bgr, pyr, c->W, c->H, c->lv_h[0].pitch, (size_t)c->W * c->H * 3, P, n);

@@ -229,6 +229,34 @@ struct TFC {
             m2[i] += alpha * d2[i];
         }
     }
+    // add() when `in`, else nothing, as straight-line code (selects): the
+    // same operations on the same values for an added point, so a caller can
+    // unroll over points and let the next points' divisions overlap this one's
+    // updates
+    ODO_INLINE void add_sel(float px, float py, float pz, float qx, float qy, float qz, float w, bool in) {
+        const bool u = in & (w != 0.0f);
+        const float aw = accW + w;
+        const float alpha = w / aw;
+        const float d1[3] = {px - m1[0], py - m1[1], pz - m1[2]};
+        const float d2[3] = {qx - m2[0], qy - m2[1], qz - m2[2]};
+        const float oma = 1.0f - alpha;
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            const float ad2 = alpha * d2[i];
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                const float nc = oma * (cov[i][j] + ad2 * d1[j]);
+                cov[i][j] = u ? nc : cov[i][j];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            const float n1 = m1[i] + alpha * d1[i], n2 = m2[i] + alpha * d2[i];
+            m1[i] = u ? n1 : m1[i];
+            m2[i] = u ? n2 : m2[i];
+        }
+        accW = u ? aw : accW;
+    }
     // getTransformation(): row-major 3x4 [R|t]
     ODO_INLINE void get(float T[12]) const {
         float U[3][3], S[3], V[3][3];
@@ -425,6 +453,24 @@ ODO_INLINE double error_function2_mk(const float x1[3], const float x2[3], const
     double r = sum3d(d0 * z0, d1 * z1, d2 * z2);
     if (!(r >= 0.0)) return ODO_DBL_MAX;
     return r;
+}
+
+// The shortcut of error_function2 (ransac.cpp:350-365): true when the point
+// is rejected before the covariance solve (NaN depth, the squared residual
+// beyond 2 (s1 + s2), NaN residual). The same expressions as the start of
+// error_function2_bf, which tests them again: a pre-filter, never a second
+// opinion.
+ODO_INLINE bool error_function2_shortcut(const float x1[3], const float x2[3], const double T[12],
+                                         const MahalConst& K) {
+    const double a0 = x1[0], a1 = x1[1], a2 = x1[2];
+    const double mu0 = x2[0], mu1 = x2[1], mu2 = x2[2];
+    const double m0 = ((T[0] * a0 + T[1] * a1) + T[2] * a2) + T[3] * 1.0;
+    const double m1 = ((T[4] * a0 + T[5] * a1) + T[6] * a2) + T[7] * 1.0;
+    const double m2 = ((T[8] * a0 + T[9] * a1) + T[10] * a2) + T[11] * 1.0;
+    const double d0 = m0 - mu0, d1 = m1 - mu1, d2 = m2 - mu2;
+    const double dsq = sum3d(d0 * d0, d1 * d1, d2 * d2);
+    const double s1 = fmax(K.raster_cov_x, K.depth_cov), s2 = fmax(K.raster_cov_x, K.depth_cov);
+    return __builtin_isnan(x1[2]) | __builtin_isnan(x2[2]) | (dsq > 2.0 * (s1 + s2)) | __builtin_isnan(d2);
 }
 
 // error_function2_mk as straight-line code: every branch becomes a select

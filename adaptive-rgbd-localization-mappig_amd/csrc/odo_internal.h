@@ -58,17 +58,6 @@ struct ResizeY {
     int b0, b1;
 };
 
-// k_pyramid's banded schedule (k_extract.hip): after band k, level l holds
-// rows [0, rows[l][k + 1]) and its blur strip chunks [0, bch[l][k + 1]) and
-// edge chunks [0, ech[l][k + 1]) are written; nb = 1 is the whole frame at once.
-#define PYR_MAXB 8
-struct PyrBands {
-    int nb;
-    int rows[16][PYR_MAXB + 1];
-    int bch[16][PYR_MAXB + 1];
-    int ech[16][PYR_MAXB + 1];
-};
-
 struct FrameCalib {
     float fx, fy, cx, cy;
     float k1, k2, p1, p2, k3;
@@ -196,10 +185,7 @@ size_t resize_lds_bytes(int spitch, int dw, int max_src_rows);
 // assumptions (<= 16 levels, <= 4096 px wide, each quad's taps inside 8 bytes)
 void launch_pyramid(hipStream_t st, const uint8_t* bgr, uint8_t* pyr, size_t in_stride, size_t pyr_stride,
                     const LevelDesc* lv, const ResizeX* rx, const ResizeY* ry, const int* rx_off, const int* ry_off,
-                    int nlevels, int nframes, uint8_t* blur, const LevelDesc* lv_host, const PyrBands& bands);
-// the banded schedule of nb bands (1..PYR_MAXB) from the host resize tables
-void pyramid_band_plan(const LevelDesc* lv_host, const ResizeY* ry_host, const int* ry_off, int nlevels, int nb,
-                       PyrBands& out);
+                    int nlevels, int nframes, uint8_t* blur, const LevelDesc* lv_host);
 // blur: the blurred pyramid is written by the same launch (null: not);
 // pyramid_blur_fusable: every level is large enough for the strip walks
 bool pyramid_blur_fusable(const LevelDesc* lv_host, int nlevels);

@@ -27,7 +27,7 @@ def main():
         res = odo.track_batch_host(bgr, dep)
     lib = pkg.load()
     import ctypes as C
-    rec = np.zeros((4096, 8), np.uint64)
+    rec = np.zeros((4096, 10), np.uint64)
     f = lib.odo_lanes_prof_read
     f.restype = C.c_int
     f.argtypes = [C.c_void_p, C.c_int]
@@ -44,6 +44,8 @@ def main():
            "tfc_us_mean": float((r[:, 4] / 100.0).mean()), "sweep_us_mean": float((r[:, 5] / 100.0).mean()),
            "sweep_inner_us_mean": float((r[:, 6] / 100.0).mean()),
            "sweep_sum_us_mean": float((r[:, 7] / 100.0).mean()),
+           # LN_COMPACT builds: pairs tested by the shortcut, pairs fully evaluated
+           "shortcut_pairs": float(r[:, 8].sum()), "full_evals": float(r[:, 9].sum()),
            "visited_mean": float(np.mean(res["visited"][1:])), "sweeps_mean": float(np.mean(res["n_sweeps"][1:]))}
     # the slowest waves
     idx = np.argsort(-dur)[:8]
