@@ -455,7 +455,7 @@ ODO_INLINE void huber_rho(double delta, double chi, double rho[3]) {
 #endif
 #define PNP_NT (64 * PNP_NW)
 #ifndef PNP_CHI_LDS
-#define PNP_CHI_LDS 0  // LE: the chi passes' per-edge chi2 as floats in LDS (16 B per edge more)
+#define PNP_CHI_LDS 1  // LE: the chi passes' per-edge chi2 as floats in LDS (16 B per edge more)
 #endif
 #define PNP_K 4  // Levenberg trials evaluated per edge pass (one per 16-lane group of wave 0)
 #ifndef PNP_SPD_SOLVE

@@ -1316,6 +1316,9 @@ ODO_INLINE double readlane_d(double v, int l) {
 #ifndef LN_TFCU
 #define LN_TFCU 0  // refinement TFC: four points per step, branch-free adds (TFC::add_sel)
 #endif
+#ifndef LN_BAL
+#define LN_BAL 0  // waves per open pair in proportion to its good matches (lane limit per wave)
+#endif
 #ifndef LN_COMPACT
 #define LN_COMPACT 0  // sweep: shortcut test for every pair first, full evaluations only for the survivors
 #endif
@@ -1374,6 +1377,50 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
     // out, taken from a shared cursor (a wave leaves a pair once every lane
     // is idle: the pair's counter is exhausted or its fold has stopped)
     int slot = cnt > waves_total ? gw : gw % cnt;
+    int lane_lim = 64;  // lanes that take up hypotheses
+#if LN_BAL
+    // Waves in proportion to the pairs' work: pair i of the open list gets
+    // 1 + spare * w_i / sum(w) waves (w = good matches + 1: a sweep and a
+    // refinement fit walk them all), and each of its waves takes up to
+    // ceil(remaining hypotheses / its waves) at a time. With an even split
+    // the pairs with the most matches set the launch's length (their waves
+    // carry 64 hypotheses each, the small pairs' finish early).
+    if (cnt <= waves_total) {
+        const int spare = waves_total - cnt;
+        int tot = 0;
+        for (int i0 = 0; i0 < cnt; i0 += 64) {
+            const int i = i0 + lane;
+            tot += i < cnt ? B.st[B.open_list[i]].ng + 1 : 0;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
+        int carry = 0, mine = -1, wn = 1;
+        for (int i0 = 0; i0 < cnt && mine < 0; i0 += 64) {
+            const int i = i0 + lane;
+            const int w = i < cnt ? B.st[B.open_list[i]].ng + 1 : 0;
+            int incl = w;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int t = __shfl_up(incl, o);
+                if (lane >= o) incl += t;
+            }
+            const int c0 = carry + incl - w, c1 = carry + incl;
+            const int st = i + (int)((long long)spare * c0 / tot), en = i + 1 + (int)((long long)spare * c1 / tot);
+            const uint64_t hit = __ballot(i < cnt && st <= gw && gw < en);
+            if (hit) {
+                const int src = (int)__builtin_ctzll(hit);
+                mine = i0 + src;
+                wn = __shfl(en - st, src);
+            }
+            carry += __shfl(incl, 63);
+        }
+        if (mine >= 0) {
+            slot = mine;
+            const int rem = max(1, cfg.iterations - cfg.rows0 * EV_WAVES);
+            lane_lim = min(64, (rem + wn - 1) / wn);
+        }
+    }
+#endif
     int helps = 0;
     for (;;) {
         if (slot < 0) break;
@@ -1384,7 +1431,7 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
         const int* smp0 = B.samples + (size_t)p * B.hcap * SREC;
         // lane state: hypothesis h (-1 idle), inlier set buffer, refinement bookkeeping
         int h = -1, cur = 0, nref = 0, nsweep = 0, nfit = 0;
-        bool sample = false, exhausted = false;
+        bool sample = false, exhausted = lane >= lane_lim;
         unsigned refinedCnt = 0;
         double refinedError = 1e6;
         float refinedT[12];
@@ -1686,6 +1733,7 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
             LP(lp_fold += wall_clock64() - lp_q;)
         }
         // the next pair
+        if (LN_BAL && cnt <= waves_total) break;  // one pair per wave
         if (cnt > waves_total && slot + waves_total < cnt) {
             slot += waves_total;
             continue;
@@ -2254,11 +2302,18 @@ void launch_ransac(hipStream_t st, const void* good, const int* n_good, const in
                 // host from the previous batch's open count on this frame set
                 // (open_hint, page-locked, copied back asynchronously), so
                 // only one of them is launched; both give the same results
+                // (no hint yet, -1: the first batch of a set: both are
+                // launched and the open count on the device picks one)
                 const int lanes = ln_groups();
-                const bool use_lanes =
-                    lanes && open_hint &&
-                    *reinterpret_cast<volatile int*>(open_hint) >= (cfg.lanes_min_open > 0 ? cfg.lanes_min_open : ln_min_open());
-                if (use_lanes)
+                const int tmin = cfg.lanes_min_open > 0 ? cfg.lanes_min_open : ln_min_open();
+                const int hint = open_hint ? *reinterpret_cast<volatile int*>(open_hint) : 0;
+                const bool use_lanes = lanes && open_hint && hint >= tmin;
+                if (lanes && hint < 0) {
+                    hipLaunchKernelGGL(k_ransac_eval_list, dim3(ev2_list()), dim3(64 * EV_WAVES), EV_LDS, st, B, cfg,
+                                       r0, rows - r0, tmin - 1);
+                    hipLaunchKernelGGL(k_ransac_lanes, dim3(lanes), dim3(64 * LN_WAVES), 0, st, B, cfg, B.lslab,
+                                       lanes * LN_WAVES, tmin);
+                } else if (use_lanes)
                     hipLaunchKernelGGL(k_ransac_lanes, dim3(lanes), dim3(64 * LN_WAVES), 0, st, B, cfg, B.lslab,
                                        lanes * LN_WAVES, 1);
                 else

@@ -886,7 +886,7 @@ static int alloc_buffers(odo_ctx* c) {
         if ((e = reset_adaptive(c))) return e;
     }
     HIPCHK(hipHostMalloc((void**)&c->h_open, NSETS * sizeof(int), hipHostMallocDefault));
-    for (int i = 0; i < NSETS; i++) c->h_open[i] = 0;
+    for (int i = 0; i < NSETS; i++) c->h_open[i] = -1;  // unknown: the first RANSAC launch runs both forms
     HIPCHK(hipMemset(c->nkp, 0, S * sizeof(int)));
     const double nan = std::nan("");
     HIPCHK(hipMemcpy(c->latch, &nan, sizeof(double), hipMemcpyHostToDevice));
