@@ -1079,6 +1079,9 @@ ODO_INLINE uint32_t pair_hi(uint32_t cur, uint32_t prev) { return __builtin_amdg
 template <int R>
 ODO_INLINE int chunk_y0(int chunk, int h) { return min(chunk * R, h - R); }
 #define BR_RE 6  // output rows per edge-lane chunk
+#ifndef BW_AHEAD
+#define BW_AHEAD 1  // row blocks (of 6) a blur walk loads ahead of the one it computes: 1 or 2
+#endif
 
 // One quad's walk down rows y0 - 3 .. y0 + R + 2. s0: the level's row 0 at
 // byte x - 4 (interior) / the level's row 0 (EDGE); dp: row y0 at byte x.
@@ -1101,6 +1104,9 @@ ODO_INLINE void blur_walk(const uint8_t* s0, uint8_t* dp, size_t pitch, int h, i
     static_assert(R % 6 == 0, "the accumulators rotate over 6 rows");
     constexpr int NB = (R + 6) / 6;
     uint32_t cw[6][3], nw[6][3];
+#if BW_AHEAD > 1
+    uint32_t nw2[6][3];  // two blocks ahead
+#endif
     const uint8_t* sp = s0 + (size_t)(y0 - 3) * pitch;
     auto load_block = [&](uint32_t(&d)[6][3], int b, bool refl) {
 #pragma unroll
@@ -1119,8 +1125,15 @@ ODO_INLINE void blur_walk(const uint8_t* s0, uint8_t* dp, size_t pitch, int h, i
         sp += 6 * pitch;
     };
     load_block(cw, 0, top);
+#if BW_AHEAD > 1
+    if (1 < NB) load_block(nw, 1, 1 == NB - 1 && bottom);
+#endif
     for (int b = 0; b < NB; b++) {
+#if BW_AHEAD > 1
+        if (b + 2 < NB) load_block(nw2, b + 2, b + 2 == NB - 1 && bottom);
+#else
         if (b + 1 < NB) load_block(nw, b + 1, b + 1 == NB - 1 && bottom);
+#endif
 #pragma unroll
         for (int j = 0; j < 6; j++) {
             // input row r = y0 - 3 + 6b + j
@@ -1171,6 +1184,10 @@ ODO_INLINE void blur_walk(const uint8_t* s0, uint8_t* dp, size_t pitch, int h, i
         }
 #pragma unroll
         for (int j = 0; j < 6; j++) cw[j][0] = nw[j][0], cw[j][1] = nw[j][1], cw[j][2] = nw[j][2];
+#if BW_AHEAD > 1
+#pragma unroll
+        for (int j = 0; j < 6; j++) nw[j][0] = nw2[j][0], nw[j][1] = nw2[j][1], nw[j][2] = nw2[j][2];
+#endif
     }
 }
 

@@ -1314,16 +1314,26 @@ ODO_INLINE double readlane_d(double v, int l) {
 #define LN_ILP2 0  // sweep: two straight-line evaluations per lane and pass (error_function2_bf)
 #endif
 #ifndef LN_TFCU
-#define LN_TFCU 0  // refinement TFC: four points per step, branch-free adds (TFC::add_sel)
+#define LN_TFCU 1  // refinement TFC: four points per step, branch-free adds (TFC::add_sel)
 #endif
 #ifndef LN_BAL
-#define LN_BAL 0  // waves per open pair in proportion to its good matches (lane limit per wave)
+#define LN_BAL 1  // waves per open pair in proportion to its good matches (lane limit per wave)
+#endif
+#ifndef LN_BAL_EXP
+#define LN_BAL_EXP 1  // LN_BAL weight: (good matches + 1) ^ LN_BAL_EXP (1 or 2)
+#endif
+ODO_INLINE int ln_weight(int ng) { return LN_BAL_EXP == 2 ? ((ng + 1) * (ng + 1) + 63) >> 6 : ng + 1; }
+#ifndef LN_TFCG
+#define LN_TFCG 0  // refinement TFC of few refining lanes by 9-lane groups (<= LN_TFCG_MAX lanes)
+#endif
+#ifndef LN_TFCG_MAX
+#define LN_TFCG_MAX 14
 #endif
 #ifndef LN_COMPACT
 #define LN_COMPACT 0  // sweep: shortcut test for every pair first, full evaluations only for the survivors
 #endif
 #ifndef LN_SUMB
-#define LN_SUMB 0  // sweep: a full chunk's parked terms read 8 at a time before the ordered sum
+#define LN_SUMB 1  // sweep: a full chunk's parked terms read 8 at a time before the ordered sum
 #endif
 #ifdef ODO_LANES_PROFILE
 // -DODO_LANES_PROFILE: per wave of the last k_ransac_lanes launch: start, end,
@@ -1390,14 +1400,14 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
         int tot = 0;
         for (int i0 = 0; i0 < cnt; i0 += 64) {
             const int i = i0 + lane;
-            tot += i < cnt ? B.st[B.open_list[i]].ng + 1 : 0;
+            tot += i < cnt ? ln_weight(B.st[B.open_list[i]].ng) : 0;
         }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
         int carry = 0, mine = -1, wn = 1;
         for (int i0 = 0; i0 < cnt && mine < 0; i0 += 64) {
             const int i = i0 + lane;
-            const int w = i < cnt ? B.st[B.open_list[i]].ng + 1 : 0;
+            const int w = i < cnt ? ln_weight(B.st[B.open_list[i]].ng) : 0;
             int incl = w;
 #pragma unroll
             for (int o = 1; o < 64; o <<= 1) {
@@ -1472,6 +1482,143 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
                 }
             }
             const bool inset = act && !sample;
+#if LN_TFCG
+            const uint64_t im = __ballot(inset);
+            if (im != 0 && __popcll(im) <= LN_TFCG_MAX) {
+                // Few refining lanes: each one's TFC by a group of 9 lanes,
+                // lane (i, j) of group g running m1[j], m2[i] and cov[i][j]
+                // over the set in order, after the group's serial prefix of
+                // the accumulated weight and its alphas (the operations of
+                // TFC::add, split over lanes as in tfc_fold). 7 groups per pass.
+                const uint32_t* cw = slab + (size_t)cur * B.mask_words * 64;
+                const int ni = __popcll(im), myr = (int)lane_rank(im);
+                if (inset) la[myr] = lane;
+                wave_sync();
+                float* gA = reinterpret_cast<float*>(lres);  // [7][128]: alpha, 1 - alpha per chunk point
+                const int g = lane / 9, r = lane - 9 * (lane / 9), ii = r / 3, jj = r - 3 * (r / 3);
+                for (int pass = 0; pass < ni; pass += 7) {
+                    const int sg = pass + g;
+                    const bool gl = g < 7 && sg < ni;
+                    const int ow = la[min(sg, ni - 1)];
+                    float acw = 0.f, m1v = 0.f, m2v = 0.f, cv = 0.f;
+                    int nf = 0;
+                    GoodPt gq = lane < ng ? P[lane] : GoodPt{};
+                    uint32_t q0 = inset ? cw[lane] : 0u, q1 = inset && 32 < ng ? cw[64 + lane] : 0u;
+                    for (int c0 = 0; c0 < ng; c0 += 64) {
+                        wave_sync();  // the previous chunk has been read
+                        lp[lane] = gq;
+                        const uint64_t okm = __ballot(c0 + lane < ng && tfc_point_ok(gq));
+                        wave_sync();
+                        const uint32_t b0 = q0, b1 = q1;
+                        if (c0 + 64 < ng) {
+                            const int c1 = c0 + 64, w1 = c1 >> 5;
+                            if (c1 + lane < ng) gq = P[c1 + lane];
+                            q0 = inset ? cw[(size_t)w1 * 64 + lane] : 0u;
+                            q1 = inset && c1 + 32 < ng ? cw[(size_t)(w1 + 1) * 64 + lane] : 0u;
+                        }
+                        const uint32_t w0 = (uint32_t)__shfl((int)b0, ow), w1 = (uint32_t)__shfl((int)b1, ow);
+                        const uint64_t set = gl ? ((((uint64_t)w1 << 32) | w0) & okm) : 0ull;
+                        nf += __popcll(set);
+                        float* gAl = gA + (g < 7 ? g : 0) * 128;
+                        // 1. accW after each set point: the group's serial sum,
+                        //    eight weights loaded ahead of their adds
+                        if (gl && r == 0) {
+                            uint64_t m = set;
+                            while (m) {
+                                int ks[8];
+                                bool vk[8];
+                                float ws[8];
+#pragma unroll
+                                for (int t = 0; t < 8; t++) {
+                                    vk[t] = m != 0;
+                                    ks[t] = vk[t] ? (int)__builtin_ctzll(m) : 0;
+                                    m &= m - 1;
+                                }
+#pragma unroll
+                                for (int t = 0; t < 8; t++) ws[t] = lp[ks[t]].w;
+#pragma unroll
+                                for (int t = 0; t < 8; t++)
+                                    if (vk[t]) {
+                                        acw += ws[t];
+                                        gAl[ks[t]] = acw;
+                                    }
+                            }
+                        }
+                        wave_sync();
+                        // 2. alpha = w / accW and 1 - alpha, spread over the group
+                        if (gl)
+                            for (int k = r; k < 64; k += 9)
+                                if ((set >> k) & 1ull) {
+                                    const float al = lp[k].w / gAl[k];
+                                    gAl[k] = al;
+                                    gAl[64 + k] = 1.0f - al;
+                                }
+                        wave_sync();
+                        // 3. the chains, four points per step (loads first)
+                        if (gl) {
+                            uint64_t m = set;
+                            while (m) {
+                                int ks[4];
+                                bool vk[4];
+#pragma unroll
+                                for (int t = 0; t < 4; t++) {
+                                    vk[t] = m != 0;
+                                    ks[t] = vk[t] ? (int)__builtin_ctzll(m) : 0;
+                                    m &= m - 1;
+                                }
+                                float pv[4], qv[4], al[4], om[4];
+#pragma unroll
+                                for (int t = 0; t < 4; t++) {
+                                    const GoodPt pt = lp[ks[t]];
+                                    pv[t] = jj == 0 ? pt.sx : (jj == 1 ? pt.sy : pt.sz);
+                                    qv[t] = ii == 0 ? pt.tx : (ii == 1 ? pt.ty : pt.tz);
+                                    al[t] = gAl[ks[t]];
+                                    om[t] = gAl[64 + ks[t]];
+                                }
+#pragma unroll
+                                for (int t = 0; t < 4; t++) {
+                                    const float d1 = pv[t] - m1v, d2 = qv[t] - m2v;
+                                    const float ad2 = al[t] * d2;
+                                    const float ncv = om[t] * (cv + ad2 * d1);
+                                    const float n1 = m1v + al[t] * d1, n2 = m2v + al[t] * d2;
+                                    cv = vk[t] ? ncv : cv;
+                                    m1v = vk[t] ? n1 : m1v;
+                                    m2v = vk[t] ? n2 : m2v;
+                                }
+                            }
+                        }
+                    }
+                    // 4. every refining lane of this pass takes its group's state
+                    for (int t = 0; t < 7 && pass + t < ni; t++) {
+                        const int base = 9 * t;
+                        const float A_ = __shfl(acw, base);
+                        const int nfg = __shfl(nf, base);
+                        float M1[3], M2[3], C[3][3];
+#pragma unroll
+                        for (int x = 0; x < 3; x++) {
+                            M1[x] = __shfl(m1v, base + x);
+                            M2[x] = __shfl(m2v, base + 3 * x);
+                        }
+#pragma unroll
+                        for (int x = 0; x < 3; x++)
+#pragma unroll
+                            for (int y = 0; y < 3; y++) C[x][y] = __shfl(cv, base + 3 * x + y);
+                        if (inset && myr == pass + t) {
+                            tf.accW = A_;
+#pragma unroll
+                            for (int x = 0; x < 3; x++) {
+                                tf.m1[x] = M1[x];
+                                tf.m2[x] = M2[x];
+#pragma unroll
+                                for (int y = 0; y < 3; y++) tf.cov[x][y] = C[x][y];
+                            }
+                            nfit += nfg;
+                        }
+                    }
+                }
+                wave_sync();
+            } else
+#endif
             if (__ballot(inset) != 0) {
                 const uint32_t* cw = slab + (size_t)cur * B.mask_words * 64;
                 // the next 64-point chunk (its points and this lane's two set
@@ -1491,16 +1638,36 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
                     }
                     const int n = min(64, ng - c0);
 #if LN_TFCU
-                    // four points per step, their LDS reads first, the adds
+                    // only the points some lane's set holds (the union of the
+                    // chunk's set words over the wave, valid points only: a
+                    // point no lane adds changes no lane's state), in order,
+                    // four per step: their LDS reads first, the adds
                     // branch-free (the next point's division overlaps)
-                    for (int j0 = 0; j0 < n; j0 += 4) {
-                        GoodPt g4[4];
+                    const uint64_t mine = ((uint64_t)b1 << 32) | b0;
+                    uint32_t u0 = b0, u1 = b1;
 #pragma unroll
-                        for (int t = 0; t < 4; t++) g4[t] = lp[min(j0 + t, n - 1)];
+                    for (int o = 32; o > 0; o >>= 1) {
+                        u0 |= (uint32_t)__shfl_xor((int)u0, o);
+                        u1 |= (uint32_t)__shfl_xor((int)u1, o);
+                    }
+                    uint64_t U = (((uint64_t)u1 << 32) | u0) & __ballot(lane < n && tfc_point_ok(lp[min(lane, n - 1)]));
+                    U = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(U >> 32)) << 32) |
+                        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)U);
+                    while (U) {
+                        int js[4];
+                        bool vj[4];
 #pragma unroll
                         for (int t = 0; t < 4; t++) {
-                            const int j = j0 + t;
-                            const bool in = j < n && tfc_point_ok(g4[t]) && ((((j < 32) ? b0 : b1) >> (j & 31)) & 1u);
+                            vj[t] = U != 0;
+                            js[t] = vj[t] ? (int)__builtin_ctzll(U) : 0;
+                            U &= U - 1;
+                        }
+                        GoodPt g4[4];
+#pragma unroll
+                        for (int t = 0; t < 4; t++) g4[t] = lp[js[t]];
+#pragma unroll
+                        for (int t = 0; t < 4; t++) {
+                            const bool in = vj[t] && ((mine >> js[t]) & 1u);
                             tf.add_sel(g4[t].sx, g4[t].sy, g4[t].sz, g4[t].tx, g4[t].ty, g4[t].tz, g4[t].w, in);
                             nfit += in;
                         }
