@@ -659,9 +659,22 @@ def launch_ranks(n: int, argv, script=None) -> int:
     execs). Rank 0 prints the JSON line; the exit code is the first failing
     rank's (the others are terminated)."""
     import subprocess
+    import threading
     envs = rank_envs(n, free_port())
     script = script or os.path.abspath(__file__)
-    procs = [subprocess.Popen([sys.executable, script] + list(argv), env=e) for e in envs]
+    # stdout carries rank 0's JSON line only: whatever else a rank prints there
+    # (the process-group library's connection notices, ...) goes to stderr
+    procs = [subprocess.Popen([sys.executable, script] + list(argv), env=e,
+                              stdout=subprocess.PIPE if r == 0 else 2, text=True)
+             for r, e in enumerate(envs)]
+
+    def relay(stream):
+        for line in stream:
+            (sys.stdout if line.lstrip().startswith("{") else sys.stderr).write(line)
+            sys.stdout.flush()
+
+    relay_t = threading.Thread(target=relay, args=(procs[0].stdout,), daemon=True)
+    relay_t.start()
     rc = 0
     try:
         pending = set(range(n))
@@ -681,6 +694,7 @@ def launch_ranks(n: int, argv, script=None) -> int:
             if p.poll() is None:
                 p.kill()
                 p.wait()
+        relay_t.join(timeout=5)
     return rc
 
 

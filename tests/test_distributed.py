@@ -128,3 +128,20 @@ def test_launch_ranks_runs_n_workers(tmp_path):
     bad = tmp_path / "bad.py"
     bad.write_text("import os, sys\nsys.exit(3 if os.environ['RANK'] == '1' else 0)\n")
     assert bench.launch_ranks(2, [], script=str(bad)) == 3
+
+
+def test_launch_ranks_stdout_is_the_json_line(tmp_path, capfd):
+    """Only rank 0's JSON line reaches stdout; other output of any rank (a
+    process group's connection notices, ...) goes to stderr."""
+    bench = _load_bench()
+    script = tmp_path / "noisy.py"
+    script.write_text(
+        "import os\n"
+        "r = os.environ['RANK']\n"
+        "print('[notice] rank', r, 'connected', flush=True)\n"
+        "if r == '0':\n"
+        "    print('{\"metric\": \"m\", \"value\": 1}', flush=True)\n")
+    assert bench.launch_ranks(2, [], script=str(script)) == 0
+    out, err = capfd.readouterr()
+    assert out.strip().splitlines() == ['{"metric": "m", "value": 1}']
+    assert err.count("[notice] rank") == 2
