@@ -48,8 +48,10 @@ KNN_OPS_PER_CMP = 16
 RANSAC_FLOPS_PER_EVAL = 120
 RANSAC_FLOPS_PER_FIT_POINT = 40
 # PMC memory-side bytes of k_knn2_f4 per launch, measured on this round's
-# kernel build (tools/pmc_merge.py --traffic); absent -> roofline.traffic null
-KNN_F4_TRAFFIC = os.path.join(ROOT, "profiles", "r04_knn2_f4_traffic.json")
+# kernel build (tools/pmc_merge.py --traffic); absent -> roofline.traffic null.
+# Kept outside profiles/ (which gpurun does not ship) so it is there when the
+# bench runs on a GPU box
+KNN_F4_TRAFFIC = os.path.join(ROOT, "measurements", "r04_knn2_f4_traffic.json")
 # on-box peak microbenchmarks (tools/ubench_peak.hip); the fallbacks are the
 # r02 measurements
 UBENCH = os.path.join(ROOT, "profiles", "r02_ubench_peak.jsonl")
