@@ -1319,6 +1319,9 @@ ODO_INLINE double readlane_d(double v, int l) {
 #ifndef LN_BAL
 #define LN_BAL 1  // waves per open pair in proportion to its good matches (lane limit per wave)
 #endif
+#ifndef LN_PRE
+#define LN_PRE 0  // sweep: transforms permuted as doubles with their point-independent covariance terms
+#endif
 #ifndef LN_BAL_EXP
 #define LN_BAL_EXP 1  // LN_BAL weight: (good matches + 1) ^ LN_BAL_EXP (1 or 2)
 #endif
@@ -1690,6 +1693,10 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
             double Td[12];
 #pragma unroll
             for (int i = 0; i < 12; i++) Td[i] = (double)T[i];
+#if LN_PRE
+            double Zd[6];
+            hyp_cov_terms(Td, K, Zd);
+#endif
             // ---- ComputeInliersAndError (ransac.cpp:315-348): the new set into the other buffer
             // Evaluations are spread over the lanes, not over the hypotheses:
             // per 32-point chunk, lanes (point j, half hf) evaluate point j for
@@ -1785,7 +1792,18 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
 #else
                 for (int i = 0; i < nact; i += 2) {
                     const int a = i + hf;  // this half's hypothesis slot
-#if LN_BPERM
+#if LN_PRE
+                    // the hypothesis' transform as doubles and its six
+                    // point-independent covariance terms, permuted from the
+                    // owning lane (LDS work instead of 12 conversions and 9
+                    // products per evaluation)
+                    const int src = la[min(a, nact - 1)];
+                    double Ta[12], Za[6];
+#pragma unroll
+                    for (int q = 0; q < 12; q++) Ta[q] = __shfl(Td[q], src);
+#pragma unroll
+                    for (int q = 0; q < 6; q++) Za[q] = __shfl(Zd[q], src);
+#elif LN_BPERM
                     // each half fetches its hypothesis' 12 floats from the
                     // owning lane (ds_bpermute) and widens them (exact: Td is
                     // (double)T): 12 permutes + 12 conversions instead of 48
@@ -1808,7 +1826,9 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
 #endif
                     double d = -1.0;  // not an inlier
                     if (a < nact && !skip) {
-#if LN_MARKSTEIN
+#if LN_PRE
+                        const double e = error_function2_mk(x1, x2, Ta, K, Za);
+#elif LN_MARKSTEIN
                         const double e = error_function2_mk(x1, x2, Ta, K);
 #else
                         const double e = error_function2(x1, x2, Ta, K);

@@ -385,7 +385,21 @@ ODO_INLINE double div_mk(double a, double b, double y) {
 // as error_function2 for every point it accepts as an inlier candidate (a
 // finite non-negative result from normal quotients); points with a zero or
 // non-finite pivot end rejected in both (DBL_MAX or a non-finite r).
-ODO_INLINE double error_function2_mk(const float x1[3], const float x2[3], const double T[12], const MahalConst& K) {
+// The point-independent terms of ErrorFunction2's A (the depth column of
+// RtC = R^T C times R, C[2][2] = depth_cov): Z = {A00, A10, A11, A20, A21,
+// A22}'s third products, (R[2][i] * c22) * R[2][j], the same operations as
+// the per-point form, done once per hypothesis.
+ODO_INLINE void hyp_cov_terms(const double T[12], const MahalConst& K, double Z[6]) {
+    const double c22 = K.depth_cov;
+    Z[0] = (T[8] * c22) * T[8];
+    Z[1] = (T[9] * c22) * T[8];
+    Z[2] = (T[9] * c22) * T[9];
+    Z[3] = (T[10] * c22) * T[8];
+    Z[4] = (T[10] * c22) * T[9];
+    Z[5] = (T[10] * c22) * T[10];
+}
+ODO_INLINE double error_function2_mk(const float x1[3], const float x2[3], const double T[12], const MahalConst& K,
+                                     const double* Z = nullptr) {
     if (__builtin_isnan(x1[2]) || __builtin_isnan(x2[2])) return ODO_DBL_MAX;
     const double a0 = x1[0], a1 = x1[1], a2 = x1[2];
     const double mu0 = x2[0], mu1 = x2[1], mu2 = x2[2];
@@ -411,12 +425,15 @@ ODO_INLINE double error_function2_mk(const float x1[3], const float x2[3], const
 #pragma unroll
         for (int j = 0; j < 3; j++) RtC[i][j] = R[j][i] * Cd[j];
     const double cov2_0 = K.raster_cov_x * mu2, cov2_1 = K.raster_cov_y * mu2, cov2_2 = K.depth_cov;
-    double A00 = sum3d(RtC[0][0] * R00, RtC[0][1] * R10, RtC[0][2] * R20) + cov2_0;
-    double A10 = sum3d(RtC[1][0] * R00, RtC[1][1] * R10, RtC[1][2] * R20) + 0.0;
-    double A11 = sum3d(RtC[1][0] * R01, RtC[1][1] * R11, RtC[1][2] * R21) + cov2_1;
-    double A20 = sum3d(RtC[2][0] * R00, RtC[2][1] * R10, RtC[2][2] * R20) + 0.0;
-    double A21 = sum3d(RtC[2][0] * R01, RtC[2][1] * R11, RtC[2][2] * R21) + 0.0;
-    double A22 = sum3d(RtC[2][0] * R02, RtC[2][1] * R12, RtC[2][2] * R22) + cov2_2;
+    // the third products from Z when the caller has them (hyp_cov_terms)
+    const double z00 = Z ? Z[0] : RtC[0][2] * R20, z10 = Z ? Z[1] : RtC[1][2] * R20, z11 = Z ? Z[2] : RtC[1][2] * R21;
+    const double z20 = Z ? Z[3] : RtC[2][2] * R20, z21 = Z ? Z[4] : RtC[2][2] * R21, z22 = Z ? Z[5] : RtC[2][2] * R22;
+    double A00 = sum3d(RtC[0][0] * R00, RtC[0][1] * R10, z00) + cov2_0;
+    double A10 = sum3d(RtC[1][0] * R00, RtC[1][1] * R10, z10) + 0.0;
+    double A11 = sum3d(RtC[1][0] * R01, RtC[1][1] * R11, z11) + cov2_1;
+    double A20 = sum3d(RtC[2][0] * R00, RtC[2][1] * R10, z20) + 0.0;
+    double A21 = sum3d(RtC[2][0] * R01, RtC[2][1] * R11, z21) + 0.0;
+    double A22 = sum3d(RtC[2][0] * R02, RtC[2][1] * R12, z22) + cov2_2;
     if (__builtin_isnan(d2)) return ODO_DBL_MAX;
     double L00 = A00, L10 = A10, L20 = A20, L11 = A11, L21 = A21, L22 = A22;
     double i00, i11, i22;
