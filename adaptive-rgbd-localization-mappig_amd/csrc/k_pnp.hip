@@ -457,7 +457,9 @@ ODO_INLINE void huber_rho(double delta, double chi, double rho[3]) {
 #ifndef PNP_CHI_LDS
 #define PNP_CHI_LDS 1  // LE: the chi passes' per-edge chi2 as floats in LDS (16 B per edge more)
 #endif
+#ifndef PNP_K
 #define PNP_K 4  // Levenberg trials evaluated per edge pass (one per 16-lane group of wave 0)
+#endif
 #ifndef PNP_SPD_SOLVE
 #define PNP_SPD_SOLVE 1  // trial solves without Eigen's pivoting (ldlt_solve6_spd; 0: pivoted)
 #endif

@@ -1301,6 +1301,9 @@ ODO_INLINE double readlane_d(double v, int l) {
 }
 #define LN_WAVES 4
 #define LN_RS 33  // LDS row stride (doubles) of the parked terms
+#ifndef LN_SLOTS
+#define LN_SLOTS 64  // lanes per wave that take up hypotheses (rows of parked terms per wave)
+#endif
 #ifndef LN_HELP
 #define LN_HELP 0  // 1: a wave whose pair has no hypothesis left joins another open pair that has
 #endif
@@ -1349,6 +1352,7 @@ __device__ uint64_t g_lprof[LPROF_MAX * 10];
 #else
 #define LP(...)
 #endif
+static_assert(LN_SLOTS <= 64 && !(LN_ILP2 && LN_SLOTS < 64), "LN_ILP2 writes rows up to 63");
 __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B, RansacCfg cfg, uint32_t* lane_slab,
                                                                    int waves_total, int min_open) {
     __builtin_amdgcn_s_setprio(ODO_WAVE_PRIO);
@@ -1364,7 +1368,7 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
     // reads its own row in point order: with a 32-double stride all 64 lanes
     // would hit one bank pair (a 32-way conflict per ds_read_b64 half); 33
     // puts lane r's row on banks 2r, 2r + 1
-    __shared__ double s_res[LN_WAVES][64 * LN_RS];
+    __shared__ double s_res[LN_WAVES][LN_SLOTS * LN_RS];
     __shared__ int s_la[LN_WAVES][64];
     double* lres = s_res[wv];
     int* la = s_la[wv];
@@ -1390,7 +1394,7 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
     // out, taken from a shared cursor (a wave leaves a pair once every lane
     // is idle: the pair's counter is exhausted or its fold has stopped)
     int slot = cnt > waves_total ? gw : gw % cnt;
-    int lane_lim = 64;  // lanes that take up hypotheses
+    int lane_lim = LN_SLOTS;  // lanes that take up hypotheses
 #if LN_BAL
     // Waves in proportion to the pairs' work: pair i of the open list gets
     // 1 + spare * w_i / sum(w) waves (w = good matches + 1: a sweep and a
@@ -1430,7 +1434,7 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
         if (mine >= 0) {
             slot = mine;
             const int rem = max(1, cfg.iterations - cfg.rows0 * EV_WAVES);
-            lane_lim = min(64, (rem + wn - 1) / wn);
+            lane_lim = min(LN_SLOTS, (rem + wn - 1) / wn);
         }
     }
 #endif
