@@ -13,6 +13,7 @@
 #   bench=NAME:ARGS     python bench.py ARGS (ARGS with '+' for spaces)  -> NAME.json
 #   multi               bench.py --gpus 2 --backend gloo: two ranks sharing the GPU
 #   kt                  rocprofv3 kernel trace of the headline command (+ timed-region split)
+#   kth                 rocprofv3 kernel trace of the hard workload's pipelined main leg
 #   serial              per-kernel times alone (tuning build, ODO_SERIAL_STREAMS=1),
 #                       default and hard workloads
 #   pmc=REGEX           PMC passes over the kernels matching REGEX (tuning build,
@@ -94,6 +95,14 @@ for step in "$@"; do
       T=$(find $O/kt -name '*kernel_trace.csv' -print -quit)
       python tools/rocprof_timed_region.py "$T" $O/kt_bench.json $O/rocprof_timed_region.json > $O/rtr.log 2>&1 || true
       echo "kt ok" ;;
+    kth)
+      # kernel trace of the hard workload in the main (pipelined) leg
+      cd /tmp
+      timeout -s KILL 600 rocprofv3 --kernel-trace --stats -d $O/kth -o run --output-format csv -- \
+        python3 $R/bench.py --no-cpu-baseline --host-steps 0 --hard-steps 0 --latency-frames 0 --workload hard \
+        --steps 10 > $O/kth_bench.json 2> $O/kth.err
+      cd $R
+      echo "kth ok" ;;
     serial)
       cd /tmp
       ODO_SERIAL_STREAMS=1 ODO_LIB=$TUNING timeout -s KILL 300 rocprofv3 --kernel-trace --stats -d $O/serial_default \
