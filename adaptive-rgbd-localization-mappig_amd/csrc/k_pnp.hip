@@ -454,6 +454,9 @@ ODO_INLINE void huber_rho(double delta, double chi, double rho[3]) {
 #define PNP_NW 4  // waves per pair
 #endif
 #define PNP_NT (64 * PNP_NW)
+#ifndef PNP_BUILD2
+#define PNP_BUILD2 0  // build pass: two edges per lane in lockstep (edge_build2)
+#endif
 #ifndef PNP_CHI_LDS
 #define PNP_CHI_LDS 1  // LE: the chi passes' per-edge chi2 as floats in LDS (16 B per edge more)
 #endif
@@ -578,6 +581,67 @@ ODO_INLINE void edge_build(const SE3M& T, const double Xw[3], const double ob[3]
         }
     }
 }
+
+// edge_build for two edges in lockstep (PNP_BUILD2): every statement for both
+// edges, branch-free (selects over values both sides compute), so the two
+// dependency chains issue interleaved on a wave that is alone on its SIMD.
+// has[k] false: edge k adds nothing. Each accumulator receives edge 0's term,
+// then edge 1's — the order of two consecutive edge_build calls — and every
+// term is formed by the same operations, so acc is bit-identical.
+#define EB2(...) _Pragma("unroll") for (int k = 0; k < 2; k++) { __VA_ARGS__; }
+ODO_INLINE void edge_build2(const SE3M& T, const double (&Xw)[2][3], const double (&ob)[2][3], const double (&info)[2],
+                            const uint8_t (&fl)[2], const bool (&has)[2], const PnPCam& cam, double dMono,
+                            double dStereo, double (&acc)[28]) {
+    bool st[2], rb[2];
+    double Xc[2][3], iz[2], izs[2], e[2][3], c2[2], rho0[2], r1[2];
+    EB2(st[k] = fl[k] & PE_STEREO; rb[k] = fl[k] & PE_ROBUST)
+    EB2(se3m_map(T, Xw[k], Xc[k]))
+    // edge_err: mono 1/z, stereo (float)(1/z) widened; the same products after
+    EB2(iz[k] = 1.0 / Xc[k][2])
+    EB2(izs[k] = st[k] ? (double)(float)iz[k] : iz[k])
+    EB2(const double q0 = Xc[k][0] * izs[k] * cam.fx + cam.cx; const double q1 = Xc[k][1] * izs[k] * cam.fy + cam.cy;
+        e[k][0] = ob[k][0] - q0; e[k][1] = ob[k][1] - q1; e[k][2] = st[k] ? ob[k][2] - (q0 - cam.bf * izs[k]) : 0.0)
+    EB2(const double a = e[k][0] * (info[k] * e[k][0]), b = e[k][1] * (info[k] * e[k][1]);
+        c2[k] = st[k] ? sum3d(a, b, e[k][2] * (info[k] * e[k][2])) : a + b)
+    // huber_rho (rho[0], rho[1]); not robust: (c2, 1)
+    EB2(const double dl = st[k] ? dStereo : dMono; const double dsqr = dl * dl; const double sq = sqrt(c2[k]);
+        const bool big = rb[k] & !(c2[k] <= dsqr);  // huber_rho's else branch, NaN included
+        rho0[k] = big ? 2 * sq * dl - dsqr : c2[k]; r1[k] = big ? dl / sq : 1.0)
+    double J[2][3][6], wo[2];
+    EB2(const double x = Xc[k][0], y = Xc[k][1], invz = iz[k], invz_2 = invz * invz;
+        J[k][0][0] = x * y * invz_2 * cam.fx; J[k][0][1] = -(1 + (x * x * invz_2)) * cam.fx;
+        J[k][0][2] = y * invz * cam.fx; J[k][0][3] = -invz * cam.fx; J[k][0][4] = 0; J[k][0][5] = x * invz_2 * cam.fx;
+        J[k][1][0] = (1 + y * y * invz_2) * cam.fy; J[k][1][1] = -x * y * invz_2 * cam.fy;
+        J[k][1][2] = -x * invz * cam.fy; J[k][1][3] = 0; J[k][1][4] = -invz * cam.fy; J[k][1][5] = y * invz_2 * cam.fy;
+        J[k][2][0] = st[k] ? J[k][0][0] - cam.bf * y * invz_2 : 0.0;
+        J[k][2][1] = st[k] ? J[k][0][1] + cam.bf * x * invz_2 : 0.0;
+        J[k][2][2] = st[k] ? J[k][0][2] : 0.0; J[k][2][3] = st[k] ? J[k][0][3] : 0.0; J[k][2][4] = 0;
+        J[k][2][5] = st[k] ? J[k][0][5] - cam.bf * invz_2 : 0.0;
+        wo[k] = r1[k] * info[k])
+    EB2(acc[27] = has[k] ? acc[27] + rho0[k] : acc[27])
+    constexpr bool Z[3][6] = {{false, false, false, false, true, false},
+                              {false, false, false, true, false, false},
+                              {false, false, false, false, true, false}};
+    int h = 0;
+#pragma unroll
+    for (int a = 0; a < 6; a++) {
+        double sb[2] = {0, 0};
+#pragma unroll
+        for (int kk = 0; kk < 3; kk++)
+            if (!Z[kk][a]) { EB2(sb[k] += J[k][kk][a] * (info[k] * e[k][kk])) }
+        EB2(acc[21 + a] = has[k] ? acc[21 + a] - r1[k] * sb[k] : acc[21 + a])
+#pragma unroll
+        for (int cc = a; cc < 6; cc++) {
+            double hh[2] = {0, 0};
+#pragma unroll
+            for (int kk = 0; kk < 3; kk++)
+                if (!Z[kk][a] && !Z[kk][cc]) { EB2(hh[k] += J[k][kk][a] * wo[k] * J[k][kk][cc]) }
+            EB2(acc[h] = has[k] ? acc[h] + hh[k] : acc[h])
+            h++;
+        }
+    }
+}
+#undef EB2
 
 // robust (Huber) chi2 of one edge at the quaternion pose T (the chi pass keeps
 // four candidates live: 7 doubles each instead of a matrix's 12)
@@ -762,6 +826,20 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
             for (int k = 0; k < 28; k++) acc[k] = 0;
             {
                 const SE3M Tm = se3_mat(T);
+#if PNP_BUILD2
+                // edges k and k + PNP_NT together (the lane's order: k, k + NT, k + 2 NT, ...)
+                for (int k = lane; k < ne; k += 2 * PNP_NT) {
+                    const int k2 = k + PNP_NT < ne ? k + PNP_NT : k;
+                    const uint8_t f2[2] = {E.flags[k], E.flags[k2]};
+                    const bool has[2] = {!(f2[0] & PE_OUT), k + PNP_NT < ne && !(f2[1] & PE_OUT)};
+                    const double Xw2[2][3] = {{E.X[3 * k], E.X[3 * k + 1], E.X[3 * k + 2]},
+                                              {E.X[3 * k2], E.X[3 * k2 + 1], E.X[3 * k2 + 2]}};
+                    const double ob2[2][3] = {{E.obs[3 * k], E.obs[3 * k + 1], E.obs[3 * k + 2]},
+                                              {E.obs[3 * k2], E.obs[3 * k2 + 1], E.obs[3 * k2 + 2]}};
+                    const double in2[2] = {(double)E.info[k], (double)E.info[k2]};
+                    edge_build2(Tm, Xw2, ob2, in2, f2, has, cam, dMono, dStereo, acc);
+                }
+#else
                 for (int k = lane; k < ne; k += PNP_NT) {
                     const uint8_t fl = E.flags[k];
                     if (fl & PE_OUT) continue;
@@ -769,6 +847,7 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                     const double ob[3] = {E.obs[3 * k], E.obs[3 * k + 1], E.obs[3 * k + 2]};
                     edge_build(Tm, Xw, ob, (double)E.info[k], fl, cam, dMono, dStereo, acc);
                 }
+#endif
             }
             wg_sum<28>(acc, red);
             PP_ACC(tb);
