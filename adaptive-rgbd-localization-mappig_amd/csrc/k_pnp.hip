@@ -457,6 +457,12 @@ ODO_INLINE void huber_rho(double delta, double chi, double rho[3]) {
 #ifndef PNP_BUILD2
 #define PNP_BUILD2 0  // build pass: two edges per lane in lockstep (edge_build2)
 #endif
+#ifndef PNP_RED1
+#define PNP_RED1 0  // workgroup sums with one barrier (two partial-sum buffers in turn)
+#endif
+#ifndef PNP_DPP
+#define PNP_DPP 0  // workgroup sums: cross-lane moves by permlane swaps / DPP instead of ds_bpermute
+#endif
 #ifndef PNP_CHI_LDS
 #define PNP_CHI_LDS 1  // LE: the chi passes' per-edge chi2 as floats in LDS (16 B per edge more)
 #endif
@@ -480,6 +486,57 @@ struct Pow2Pad {
     static constexpr int v = NV <= 1 ? 1 : NV <= 2 ? 2 : NV <= 4 ? 4 : NV <= 8 ? 8 : NV <= 16 ? 16 : 32;
     static constexpr int lg = NV <= 1 ? 0 : NV <= 2 ? 1 : NV <= 4 ? 2 : NV <= 8 ? 3 : NV <= 16 ? 4 : 5;
 };
+// The partner lane's v at butterfly offset O (PNP_DPP): 32 / 16 by the gfx950
+// permlane swaps (lane l <-> l ^ 32, l ^ 16), 8 / 4 by the DPP row mirror /
+// half mirror (l <-> 15 - l, 7 - l within a row: partners that differ in bit
+// log2(O) and agree on every higher bit, so at that level they hold the same
+// value indices over disjoint lane sets), 2 / 1 by quad permutes (l ^ 2,
+// l ^ 1): VALU cross-lane moves instead of LDS round trips (ds_bpermute), a
+// fixed tree.
+template <int O>
+ODO_INLINE double lane_partner(double v) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    uint32_t lo = (uint32_t)u, hi = (uint32_t)(u >> 32);
+    if constexpr (O == 32 || O == 16) {
+        const bool up = (lane & O) != 0;
+        if constexpr (O == 32) {
+            const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+            const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+            lo = up ? a[0] : a[1];
+            hi = up ? b[0] : b[1];
+        } else {
+            const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+            const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+            lo = up ? a[0] : a[1];
+            hi = up ? b[0] : b[1];
+        }
+    } else {
+        constexpr int ctrl = O == 8 ? 0x140 : O == 4 ? 0x141 : O == 2 ? 0x4E : 0xB1;
+        lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)lo, ctrl, 0xf, 0xf, false);
+        hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)hi, ctrl, 0xf, 0xf, false);
+    }
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+template <int O>
+ODO_INLINE double xor_partner(double v) {
+#if PNP_DPP
+    return lane_partner<O>(v);
+#else
+    return __shfl_xor(v, O);
+#endif
+}
+template <int NP, int O>
+ODO_INLINE void halving_level(double (&w)[NP], int lane) {
+    constexpr int n = NP * O / 32, h = n >> 1;  // values held before this level
+    const bool hi = (lane & O) != 0;
+#pragma unroll
+    for (int i = 0; i < h; i++) {
+        const double send = hi ? w[i] : w[h + i];
+        const double keep = hi ? w[h + i] : w[i];
+        w[i] = keep + xor_partner<O>(send);
+    }
+}
 template <int NV>
 ODO_INLINE double wave_sum_transposed(const double (&v)[NV]) {
     constexpr int NP = Pow2Pad<NV>::v, LG = Pow2Pad<NV>::lg;
@@ -488,37 +545,51 @@ ODO_INLINE double wave_sum_transposed(const double (&v)[NV]) {
     double w[NP];
 #pragma unroll
     for (int k = 0; k < NP; k++) w[k] = k < NV ? v[k] : 0.0;
-#pragma unroll
-    for (int s = 0; s < LG; s++) {
-        const int o = 32 >> s, n = NP >> s, h = n >> 1;
-        const bool hi = (lane & o) != 0;
-#pragma unroll
-        for (int i = 0; i < h; i++) {
-            const double send = hi ? w[i] : w[h + i];
-            const double keep = hi ? w[h + i] : w[i];
-            w[i] = keep + __shfl_xor(send, o);
-        }
-    }
+    // halving levels: at offset O the lane pair splits the vector (the lane
+    // with bit O clear keeps the low half)
+    if constexpr (LG > 0) halving_level<NP, 32>(w, lane);
+    if constexpr (LG > 1) halving_level<NP, 16>(w, lane);
+    if constexpr (LG > 2) halving_level<NP, 8>(w, lane);
+    if constexpr (LG > 3) halving_level<NP, 4>(w, lane);
+    if constexpr (LG > 4) halving_level<NP, 2>(w, lane);
     double x = w[0];
-#pragma unroll
-    for (int o = 32 >> LG; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    // the remaining offsets: every lane adds its partner's total
+    if constexpr (LG < 1) x += xor_partner<32>(x);
+    if constexpr (LG < 2) x += xor_partner<16>(x);
+    if constexpr (LG < 3) x += xor_partner<8>(x);
+    if constexpr (LG < 4) x += xor_partner<4>(x);
+    if constexpr (LG < 5) x += xor_partner<2>(x);
+    x += xor_partner<1>(x);
     return x;  // total of value (lane >> (6 - LG)) over the wave
 }
+// PNP_RED1: two partial-sum buffers used in turn, so one barrier per sum: a
+// buffer is rewritten two sums later, after every wave has passed the other
+// sum's barrier (and with it, its own reads of this buffer)
+#define PNP_RED_WORDS (PNP_NW * 28)
 template <int NV>
-ODO_INLINE void wg_sum(double (&v)[NV], double* red) {
+ODO_INLINE void wg_sum(double (&v)[NV], double* red, int& par) {
     constexpr int LG = Pow2Pad<NV>::lg;
     const double x = wave_sum_transposed(v);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int j = lane >> (6 - LG);
-    if ((lane & ((1 << (6 - LG)) - 1)) == 0 && j < NV) red[wave * NV + j] = x;
+    double* r = red;
+#if PNP_RED1
+    r += par * PNP_RED_WORDS;
+    par ^= 1;
+#else
+    (void)par;
+#endif
+    if ((lane & ((1 << (6 - LG)) - 1)) == 0 && j < NV) r[wave * NV + j] = x;
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < NV; k++) {
-        double a = red[k];
-        for (int w = 1; w < PNP_NW; w++) a += red[w * NV + k];
+        double a = r[k];
+        for (int w = 1; w < PNP_NW; w++) a += r[w * NV + k];
         v[k] = a;
     }
+#if !PNP_RED1
     __syncthreads();
+#endif
 }
 
 // computeActiveErrors + activeRobustChi2 + buildSystem contribution of one edge
@@ -706,7 +777,8 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
     if (sel && sel[p] != sel_val) return;  // pair handled by the other PnP launch
     const int lane = threadIdx.x;  // thread index within the workgroup
     const int wlane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    __shared__ double red[PNP_NW * 28];
+    __shared__ double red[(PNP_RED1 ? 2 : 1) * PNP_RED_WORDS];
+    int rpar = 0;  // which red buffer the next workgroup sum takes (PNP_RED1)
     __shared__ double s_acc[28];  // reduced H (upper, row-major), b, chi of the iteration
     __shared__ double s_T[PNP_K][8];
     __shared__ int s_ok[PNP_K];
@@ -849,7 +921,7 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                 }
 #endif
             }
-            wg_sum<28>(acc, red);
+            wg_sum<28>(acc, red, rpar);
             PP_ACC(tb);
 #ifdef ODO_PNP_PROFILE
             nit++;
@@ -985,7 +1057,7 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                         else E.chi4[4 * e + k] = c2;
                     }
                 }
-                wg_sum<PNP_K>(chi, red);
+                wg_sum<PNP_K>(chi, red, rpar);
                 PP_ACC(tchi);
                 // replay the trials in order
 #pragma unroll
@@ -1057,7 +1129,7 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
             }
         }
         double bd[1] = {(double)bad};
-        wg_sum<1>(bd, red);
+        wg_sum<1>(bd, red, rpar);
         nBad = (int)bd[0];
         PP_ACC(tcls);
         if (ne < 10) break;
