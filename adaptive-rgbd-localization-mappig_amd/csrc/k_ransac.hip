@@ -1322,6 +1322,9 @@ ODO_INLINE double readlane_d(double v, int l) {
 #ifndef LN_BAL
 #define LN_BAL 1  // waves per open pair in proportion to its good matches (lane limit per wave)
 #endif
+#ifndef LN_TLDS
+#define LN_TLDS 0  // sweep: transforms from an LDS slot table (pair with LN_SLOTS <= 48 to fit two workgroups per CU)
+#endif
 #ifndef LN_PRE
 #define LN_PRE 0  // sweep: transforms permuted as doubles with their point-independent covariance terms
 #endif
@@ -1372,6 +1375,10 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
     __shared__ int s_la[LN_WAVES][64];
     double* lres = s_res[wv];
     int* la = s_la[wv];
+#if LN_TLDS
+    __shared__ __attribute__((aligned(16))) float s_T[LN_WAVES][LN_SLOTS * 12];  // active slots' transforms
+    float* lT = s_T[wv];
+#endif
 #if LN_COMPACT
     __shared__ int s_lq[LN_WAVES][128];  // phase-1 queue: (slot << 5) | point
     int* lq = s_lq[wv];
@@ -1714,6 +1721,16 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
             const int nact = __popcll(actm);
             const int rank = (int)lane_rank(actm);  // this lane's slot among the active ones
             if (act) la[rank] = lane;
+#if LN_TLDS
+            // the active hypotheses' transforms in slot order, read back by the
+            // sweep as three broadcast 16-byte loads per slot instead of 12 permutes
+            if (act) {
+                float4* tw = reinterpret_cast<float4*>(lT + rank * 12);
+                tw[0] = make_float4(T[0], T[1], T[2], T[3]);
+                tw[1] = make_float4(T[4], T[5], T[6], T[7]);
+                tw[2] = make_float4(T[8], T[9], T[10], T[11]);
+            }
+#endif
             wave_sync();
             double meanError = 0.0;
             unsigned c = 0;
@@ -1796,7 +1813,11 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
 #else
                 for (int i = 0; i < nact; i += 2) {
                     const int a = i + hf;  // this half's hypothesis slot
-#if LN_PRE
+#if LN_TLDS
+                    const float4* tr = reinterpret_cast<const float4*>(lT + min(a, nact - 1) * 12);
+                    const float4 t0 = tr[0], t1 = tr[1], t2 = tr[2];
+                    const double Ta[12] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w, t2.x, t2.y, t2.z, t2.w};
+#elif LN_PRE
                     // the hypothesis' transform as doubles and its six
                     // point-independent covariance terms, permuted from the
                     // owning lane (LDS work instead of 12 conversions and 9
