@@ -457,6 +457,9 @@ ODO_INLINE void huber_rho(double delta, double chi, double rho[3]) {
 #ifndef PNP_BUILD2
 #define PNP_BUILD2 0  // build pass: two edges per lane in lockstep (edge_build2)
 #endif
+#ifndef PNP_CHIM
+#define PNP_CHIM 0  // chi passes map points with the candidates' matrices (LDS, built once per candidate by its solver)
+#endif
 #ifndef PNP_RED1
 #define PNP_RED1 0  // workgroup sums with one barrier (two partial-sum buffers in turn)
 #endif
@@ -781,6 +784,9 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
     int rpar = 0;  // which red buffer the next workgroup sum takes (PNP_RED1)
     __shared__ double s_acc[28];  // reduced H (upper, row-major), b, chi of the iteration
     __shared__ double s_T[PNP_K][8];
+#if PNP_CHIM
+    __shared__ double s_M[PNP_K][12];  // the candidates as rotation matrix + translation (se3_mat)
+#endif
     __shared__ int s_ok[PNP_K];
     __shared__ int s_ne[PNP_NW];
     odo_pair_result* R = res + p;
@@ -1021,6 +1027,13 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                         s_T[tg][6] = Tk.t[2];
                         s_T[tg][7] = scale;
                         s_ok[tg] = ok2 ? 1 : 0;
+#if PNP_CHIM
+                        const SE3M Mk = se3_mat(Tk);
+#pragma unroll
+                        for (int q = 0; q < 9; q++) s_M[tg][q] = Mk.R[q];
+#pragma unroll
+                        for (int q = 0; q < 3; q++) s_M[tg][9 + q] = Mk.t[q];
+#endif
                     }
                 }
                 __syncthreads();
@@ -1052,7 +1065,16 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                     for (int k = 0; k < PNP_K; k++) {
                         if (k >= K) break;
                         double c2;
+#if PNP_CHIM
+                        SE3M Mk;
+#pragma unroll
+                        for (int q = 0; q < 9; q++) Mk.R[q] = s_M[k][q];
+#pragma unroll
+                        for (int q = 0; q < 3; q++) Mk.t[q] = s_M[k][9 + q];
+                        chi[k] += edge_robust_chi(Mk, Xw, ob, info, fl, cam, dMono, dStereo, c2);
+#else
                         chi[k] += edge_robust_chi_q(Tc[k], Xw, ob, info, fl, cam, dMono, dStereo, c2);
+#endif
                         if (LE && PNP_CHI_LDS) sC[4 * e + k] = (float)c2;
                         else E.chi4[4 * e + k] = c2;
                     }
