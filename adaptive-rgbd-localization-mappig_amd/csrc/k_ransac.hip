@@ -1322,6 +1322,9 @@ ODO_INLINE double readlane_d(double v, int l) {
 #ifndef LN_BAL
 #define LN_BAL 1  // waves per open pair in proportion to its good matches (lane limit per wave)
 #endif
+#ifndef LN_PRIO
+#define LN_PRIO ODO_WAVE_PRIO  // k_ransac_lanes' wave priority
+#endif
 #ifndef LN_TLDS
 #define LN_TLDS 1  // sweep: transforms from an LDS slot table (pair with LN_SLOTS <= 48 to fit two workgroups per CU)
 #endif
@@ -1358,7 +1361,9 @@ __device__ uint64_t g_lprof[LPROF_MAX * 10];
 static_assert(LN_SLOTS <= 64 && !(LN_ILP2 && LN_SLOTS < 64), "LN_ILP2 writes rows up to 63");
 __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B, RansacCfg cfg, uint32_t* lane_slab,
                                                                    int waves_total, int min_open) {
-    __builtin_amdgcn_s_setprio(ODO_WAVE_PRIO);
+    // a throughput kernel (ms of FP64 issue): at LN_PRIO its waves do not
+    // starve the co-resident extraction waves of the next batch
+    __builtin_amdgcn_s_setprio(LN_PRIO);
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int gw = (int)blockIdx.x * LN_WAVES + wv;
