@@ -458,7 +458,7 @@ ODO_INLINE void huber_rho(double delta, double chi, double rho[3]) {
 #define PNP_BUILD2 0  // build pass: two edges per lane in lockstep (edge_build2)
 #endif
 #ifndef PNP_CHIM
-#define PNP_CHIM 0  // chi passes map points with the candidates' matrices (LDS, built once per candidate by its solver)
+#define PNP_CHIM 1  // chi passes map points with the candidates' matrices (LDS, built once per candidate by its solver)
 #endif
 #ifndef PNP_RED1
 #define PNP_RED1 0  // workgroup sums with one barrier (two partial-sum buffers in turn)
