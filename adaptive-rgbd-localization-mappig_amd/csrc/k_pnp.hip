@@ -457,6 +457,9 @@ ODO_INLINE void huber_rho(double delta, double chi, double rho[3]) {
 #ifndef PNP_BUILD2
 #define PNP_BUILD2 0  // build pass: two edges per lane in lockstep (edge_build2)
 #endif
+#ifndef PNP_ALLSOLVE
+#define PNP_ALLSOLVE 0  // every wave solves the trials (no workgroup barrier around the solves)
+#endif
 #ifndef PNP_CHIM
 #define PNP_CHIM 1  // chi passes map points with the candidates' matrices (LDS, built once per candidate by its solver)
 #endif
@@ -783,11 +786,11 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
     __shared__ double red[(PNP_RED1 ? 2 : 1) * PNP_RED_WORDS];
     int rpar = 0;  // which red buffer the next workgroup sum takes (PNP_RED1)
     __shared__ double s_acc[28];  // reduced H (upper, row-major), b, chi of the iteration
-    __shared__ double s_T[PNP_K][8];
+    __shared__ double s_T[(PNP_ALLSOLVE ? PNP_NW : 1) * PNP_K][8];
 #if PNP_CHIM
-    __shared__ double s_M[PNP_K][12];  // the candidates as rotation matrix + translation (se3_mat)
+    __shared__ double s_M[(PNP_ALLSOLVE ? PNP_NW : 1) * PNP_K][12];  // the candidates as rotation matrix + translation (se3_mat)
 #endif
-    __shared__ int s_ok[PNP_K];
+    __shared__ int s_ok[(PNP_ALLSOLVE ? PNP_NW : 1) * PNP_K];
     __shared__ int s_ne[PNP_NW];
     odo_pair_result* R = res + p;
     const int s1 = slot0 + p, s2 = slot0 + p + 1;
@@ -932,7 +935,7 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
 #ifdef ODO_PNP_PROFILE
             nit++;
 #endif
-            if (lane == 0)
+            if (!PNP_ALLSOLVE && lane == 0)
 #pragma unroll
                 for (int k = 0; k < 28; k++) s_acc[k] = acc[k];
             double curChi = acc[27];
@@ -948,7 +951,7 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                 lambda = 1e-5 * mx;
                 ni = 2;
             }
-            __syncthreads();
+            if (!PNP_ALLSOLVE) __syncthreads();
             // ---- OptimizationAlgorithmLevenberg::solve trial loop, PNP_K trials per pass
             double rho = 0;
             int qmax = 0;
@@ -975,7 +978,11 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
 #define ODO_PNP_GROUP_TRIALS 1  // 0: one wave per trial (A/B)
 #endif
                 const int tg = ODO_PNP_GROUP_TRIALS ? wlane >> 4 : wave;
-                if ((ODO_PNP_GROUP_TRIALS ? wave == 0 : true) && tg < K) {
+                // PNP_ALLSOLVE: every wave solves the K trials itself (the same
+                // operations on the same values as wave 0 would), into its own
+                // LDS slots: no workgroup barrier around the solves
+                const int tb = PNP_ALLSOLVE ? wave * PNP_K : 0;
+                if ((PNP_ALLSOLVE || (ODO_PNP_GROUP_TRIALS ? wave == 0 : true)) && tg < K) {
                     double lw = lam[0];
 #pragma unroll
                     for (int k = 1; k < PNP_K; k++)
@@ -987,12 +994,12 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                         for (int a = 0; a < 6; a++)
 #pragma unroll
                             for (int cc = a; cc < 6; cc++) {
-                                Hl[a][cc] = s_acc[h];
-                                Hl[cc][a] = s_acc[h];
+                                Hl[a][cc] = PNP_ALLSOLVE ? acc[h] : s_acc[h];
+                                Hl[cc][a] = PNP_ALLSOLVE ? acc[h] : s_acc[h];
                                 h++;
                             }
 #pragma unroll
-                        for (int a = 0; a < 6; a++) b[a] = s_acc[21 + a];
+                        for (int a = 0; a < 6; a++) b[a] = PNP_ALLSOLVE ? acc[21 + a] : s_acc[21 + a];
                     }
                     for (int j = 0; j < 6; j++) Hl[j][j] += lw;
                     double x[6] = {0, 0, 0, 0, 0, 0};
@@ -1018,36 +1025,43 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                     for (int j = 0; j < 6; j++) scale += x[j] * (lw * x[j] + b[j]);
                     scale += 1e-3;
                     if ((wlane & (ODO_PNP_GROUP_TRIALS ? 15 : 63)) == 0) {
-                        s_T[tg][0] = Tk.q.x;
-                        s_T[tg][1] = Tk.q.y;
-                        s_T[tg][2] = Tk.q.z;
-                        s_T[tg][3] = Tk.q.w;
-                        s_T[tg][4] = Tk.t[0];
-                        s_T[tg][5] = Tk.t[1];
-                        s_T[tg][6] = Tk.t[2];
-                        s_T[tg][7] = scale;
-                        s_ok[tg] = ok2 ? 1 : 0;
+                        s_T[tb + tg][0] = Tk.q.x;
+                        s_T[tb + tg][1] = Tk.q.y;
+                        s_T[tb + tg][2] = Tk.q.z;
+                        s_T[tb + tg][3] = Tk.q.w;
+                        s_T[tb + tg][4] = Tk.t[0];
+                        s_T[tb + tg][5] = Tk.t[1];
+                        s_T[tb + tg][6] = Tk.t[2];
+                        s_T[tb + tg][7] = scale;
+                        s_ok[tb + tg] = ok2 ? 1 : 0;
 #if PNP_CHIM
                         const SE3M Mk = se3_mat(Tk);
 #pragma unroll
-                        for (int q = 0; q < 9; q++) s_M[tg][q] = Mk.R[q];
+                        for (int q = 0; q < 9; q++) s_M[tb + tg][q] = Mk.R[q];
 #pragma unroll
-                        for (int q = 0; q < 3; q++) s_M[tg][9 + q] = Mk.t[q];
+                        for (int q = 0; q < 3; q++) s_M[tb + tg][9 + q] = Mk.t[q];
 #endif
                     }
                 }
-                __syncthreads();
+                if (PNP_ALLSOLVE) {
+                    // the wave's own slots: wave-scope ordering
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                } else {
+                    __syncthreads();
+                }
                 SE3 Tc[PNP_K];
                 double sc[PNP_K];
                 bool okc[PNP_K];
 #pragma unroll
                 for (int k = 0; k < PNP_K; k++) {
-                    Tc[k].q = Quat{s_T[k][0], s_T[k][1], s_T[k][2], s_T[k][3]};
-                    Tc[k].t[0] = s_T[k][4];
-                    Tc[k].t[1] = s_T[k][5];
-                    Tc[k].t[2] = s_T[k][6];
-                    sc[k] = s_T[k][7];
-                    okc[k] = s_ok[k] != 0;
+                    Tc[k].q = Quat{s_T[tb + k][0], s_T[tb + k][1], s_T[tb + k][2], s_T[tb + k][3]};
+                    Tc[k].t[0] = s_T[tb + k][4];
+                    Tc[k].t[1] = s_T[tb + k][5];
+                    Tc[k].t[2] = s_T[tb + k][6];
+                    sc[k] = s_T[tb + k][7];
+                    okc[k] = s_ok[tb + k] != 0;
                 }
                 PP_ACC(tsol);
                 PP_T0();
@@ -1068,9 +1082,9 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
 #if PNP_CHIM
                         SE3M Mk;
 #pragma unroll
-                        for (int q = 0; q < 9; q++) Mk.R[q] = s_M[k][q];
+                        for (int q = 0; q < 9; q++) Mk.R[q] = s_M[tb + k][q];
 #pragma unroll
-                        for (int q = 0; q < 3; q++) Mk.t[q] = s_M[k][9 + q];
+                        for (int q = 0; q < 3; q++) Mk.t[q] = s_M[tb + k][9 + q];
                         chi[k] += edge_robust_chi(Mk, Xw, ob, info, fl, cam, dMono, dStereo, c2);
 #else
                         chi[k] += edge_robust_chi_q(Tc[k], Xw, ob, info, fl, cam, dMono, dStereo, c2);
