@@ -1292,11 +1292,12 @@ struct PyrLevels {
 // 64 strip groups of 16 lanes, then the edge lanes)
 ODO_INLINE void pyr_blur_level(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur, size_t pyr_stride,
                                const LevelDesc* __restrict__ lv, const BlurRows& S, int nlevels, int f, int l,
-                               const LevelDesc& L, int t) {
+                               const LevelDesc& L, int t, int ca, int cb, int ea, int eb) {
+    // strip chunks [ca, cb) and edge chunks [ea, eb) of the level (its part's share)
     const uint32_t none[3] = {0, 0, 0};
-    const int items = S.base[l + 1] - S.base[l];
+    const int items = cb * S.nst[l];
     const int g = t >> 4;
-    for (int it = g; it < items; it += PYR_TH / 16) {
+    for (int it = ca * S.nst[l] + g; it < items; it += PYR_TH / 16) {
         const int chunk = it / S.nst[l], strip = it - chunk * S.nst[l];
         const int q = 1 + strip * 16 + (t & 15);
         const bool store = q <= S.nq[l];
@@ -1307,7 +1308,8 @@ ODO_INLINE void pyr_blur_level(const uint8_t* __restrict__ pyr, uint8_t* __restr
         uint8_t* dp = blur + (size_t)f * pyr_stride + L.off + (size_t)y0 * L.pitch + x;
         blur_walk<false, BR_R>(s0, dp, (size_t)L.pitch, L.h, y0, top, bottom, store, 0, 0, 0, none, none);
     }
-    for (int k = S.ebase[l] + t; k < S.ebase[l + 1]; k += PYR_TH)
+    const int ne = (S.ebase[l + 1] - S.ebase[l]) / ((L.h + BR_RE - 1) / BR_RE);  // edge quads per chunk
+    for (int k = S.ebase[l] + ea * ne + t; k < S.ebase[l] + eb * ne; k += PYR_TH)
         blur_edge_lane(pyr, blur, pyr_stride, lv, S, nlevels, f, k);
 }
 #ifdef ODO_PYR_PROFILE
@@ -1326,9 +1328,11 @@ __global__ void __launch_bounds__(PYR_TH) k_pyramid(const uint8_t* __restrict__ 
                                                     size_t in_stride, size_t pyr_stride,
                                                     const LevelDesc* __restrict__ lv, const ResizeX* __restrict__ xt,
                                                     const ResizeY* __restrict__ yt, PyrLevels PL, int nlevels,
-                                                    uint8_t* __restrict__ blur, BlurRows BR) {
+                                                    uint8_t* __restrict__ blur, BlurRows BR, PyrSplit SP) {
     EXTRACT_PRIO();
-    const int f = blockIdx.x;
+    // SP.parts == 2: two workgroups per frame, the top and the bottom part
+    const int part = SP.parts == 2 ? (int)(blockIdx.x & 1) : 0;
+    const int f = SP.parts == 2 ? (int)(blockIdx.x >> 1) : (int)blockIdx.x;
     const int t = threadIdx.x;
     uint8_t* base = pyr + (size_t)f * pyr_stride;
     PYR_PROF(0);
@@ -1338,9 +1342,10 @@ __global__ void __launch_bounds__(PYR_TH) k_pyramid(const uint8_t* __restrict__ 
         const int w = L0.w, h = L0.h, pitch = L0.pitch;
         const uint8_t* src = bgr + (size_t)f * in_stride;
         const int npix = w * h;
+        const int r0 = SP.lo[part][0], r1 = SP.hi[part][0];  // this part's rows of level 0
         if ((w & 3) == 0) {
-            const int nq4 = npix >> 2;
-            for (int q0 = t; q0 < nq4; q0 += PYR_GU * PYR_TH) {
+            const int nq4 = (r1 * w) >> 2;
+            for (int q0 = ((r0 * w) >> 2) + t; q0 < nq4; q0 += PYR_GU * PYR_TH) {
                 uint32_t wv[PYR_GU][3];
 #pragma unroll
                 for (int u = 0; u < PYR_GU; u++) {
@@ -1369,7 +1374,7 @@ __global__ void __launch_bounds__(PYR_TH) k_pyramid(const uint8_t* __restrict__ 
                 }
             }
         } else {
-            for (int p = t; p < npix; p += PYR_TH) {
+            for (int p = r0 * w + t; p < r1 * w; p += PYR_TH) {
                 const uint8_t* s = src + (size_t)p * 3;
                 const int yy = p / w, xx = p - yy * w;
                 base[(size_t)yy * pitch + xx] =
@@ -1381,7 +1386,9 @@ __global__ void __launch_bounds__(PYR_TH) k_pyramid(const uint8_t* __restrict__ 
         __syncthreads();  // level l - 1 is complete
         PYR_PROF(l);
         const LevelDesc S = lv[l - 1], D = lv[l];
-        if (BLUR) pyr_blur_level(pyr, blur, pyr_stride, lv, BR, nlevels, f, l - 1, S, t);
+        if (BLUR)
+            pyr_blur_level(pyr, blur, pyr_stride, lv, BR, nlevels, f, l - 1, S, t, SP.ca[part][l - 1], SP.cb[part][l - 1],
+                           SP.ea[part][l - 1], SP.eb[part][l - 1]);
         const int nq = (D.w + 3) >> 2;
         const int P = PYR_TH / nq;  // row phases (the host checks nq <= PYR_TH)
         if (t >= P * nq) continue;
@@ -1418,10 +1425,11 @@ __global__ void __launch_bounds__(PYR_TH) k_pyramid(const uint8_t* __restrict__ 
                                               __builtin_bit_cast(u16x2, wt[j]), 0u, false);
             }
         };
-        for (int y = ph; y < D.h; y += PYR_RU * P) {
+        const int ylo = SP.lo[part][l], yhi = SP.hi[part][l];  // this part's rows of level l
+        for (int y = ylo + ph; y < yhi; y += PYR_RU * P) {
             ResizeY Yr[PYR_RU];
 #pragma unroll
-            for (int u = 0; u < PYR_RU; u++) Yr[u] = Y[min(y + u * P, D.h - 1)];
+            for (int u = 0; u < PYR_RU; u++) Yr[u] = Y[min(y + u * P, yhi - 1)];
             uint32_t h0[PYR_RU][4], h1[PYR_RU][4];
 #pragma unroll
             for (int u = 0; u < PYR_RU; u++) {
@@ -1435,7 +1443,7 @@ __global__ void __launch_bounds__(PYR_TH) k_pyramid(const uint8_t* __restrict__ 
                 for (int j = 0; j < 4; j++)
                     pk |= min((__umul24(h0[u][j], (uint32_t)Yr[u].b0) + __umul24(h1[u][j], (uint32_t)Yr[u].b1) + (1u << 21)) >> 22,
                               255u) << (8 * j);
-                if (y + u * P < D.h) *reinterpret_cast<uint32_t*>(dbase + (size_t)(y + u * P) * D.pitch) = pk;
+                if (y + u * P < yhi) *reinterpret_cast<uint32_t*>(dbase + (size_t)(y + u * P) * D.pitch) = pk;
             }
         }
     }
@@ -1443,7 +1451,9 @@ __global__ void __launch_bounds__(PYR_TH) k_pyramid(const uint8_t* __restrict__ 
         __syncthreads();  // the last level is complete
         PYR_PROF(nlevels);
         const LevelDesc L = lv[nlevels - 1];
-        pyr_blur_level(pyr, blur, pyr_stride, lv, BR, nlevels, f, nlevels - 1, L, t);
+        const int ll = nlevels - 1;
+        pyr_blur_level(pyr, blur, pyr_stride, lv, BR, nlevels, f, ll, L, t, SP.ca[part][ll], SP.cb[part][ll],
+                       SP.ea[part][ll], SP.eb[part][ll]);
     }
     __syncthreads();
     PYR_PROF(nlevels + 1);
@@ -1489,17 +1499,68 @@ bool pyramid_blur_fusable(const LevelDesc* lv_host, int nlevels) {
 }
 void launch_pyramid(hipStream_t st, const uint8_t* bgr, uint8_t* pyr, size_t in_stride, size_t pyr_stride,
                     const LevelDesc* lv, const ResizeX* rx, const ResizeY* ry, const int* rx_off, const int* ry_off,
-                    int nlevels, int nframes, uint8_t* blur, const LevelDesc* lv_host) {
+                    int nlevels, int nframes, uint8_t* blur, const LevelDesc* lv_host, const PyrSplit& split) {
     PyrLevels PL{};
     for (int l = 0; l < nlevels && l < 16; l++) PL.rx_off[l] = rx_off[l], PL.ry_off[l] = ry_off[l];
     BlurRows BR{};
+    const dim3 g(nframes * split.parts);
     if (blur && blur_rows_plan(lv_host, nlevels, BR)) {
-        hipLaunchKernelGGL(k_pyramid<true>, dim3(nframes), dim3(PYR_TH), 0, st, bgr, pyr, in_stride, pyr_stride, lv,
-                           rx, ry, PL, nlevels, blur, BR);
+        hipLaunchKernelGGL(k_pyramid<true>, g, dim3(PYR_TH), 0, st, bgr, pyr, in_stride, pyr_stride, lv, rx, ry, PL,
+                           nlevels, blur, BR, split);
         return;
     }
-    hipLaunchKernelGGL(k_pyramid<false>, dim3(nframes), dim3(PYR_TH), 0, st, bgr, pyr, in_stride, pyr_stride, lv, rx,
-                       ry, PL, nlevels, (uint8_t*)nullptr, BR);
+    hipLaunchKernelGGL(k_pyramid<false>, g, dim3(PYR_TH), 0, st, bgr, pyr, in_stride, pyr_stride, lv, rx, ry, PL,
+                       nlevels, (uint8_t*)nullptr, BR, split);
+}
+// The part ranges of k_pyramid (PyrSplit). parts == 1: everything. parts == 2:
+// level l's blur rows split at s_l (a multiple of BR_R = 30, so the 30-row
+// strip chunks and 6-row edge chunks split with it; a level under 60 rows is
+// blurred by the top part alone); each part builds the rows its blur reads
+// (3-row halo) and the source rows of the next level's rows it builds,
+// from the top level down. Every row keeps its one arithmetic, so rows both
+// parts build are the same bytes.
+void pyramid_split_plan(const LevelDesc* lv_host, const ResizeY* ry, const int* ry_off, int nlevels, int parts,
+                        PyrSplit& S) {
+    S = PyrSplit{};
+    S.parts = parts;
+    for (int l = 0; l < nlevels && l < 16; l++) {
+        const int h = lv_host[l].h, nch = (h + BR_R - 1) / BR_R, nch6 = (h + BR_RE - 1) / BR_RE;
+        for (int p = 0; p < 2; p++) {
+            S.lo[p][l] = 0, S.hi[p][l] = h;
+            S.ca[p][l] = 0, S.cb[p][l] = nch, S.ea[p][l] = 0, S.eb[p][l] = nch6;
+        }
+    }
+    if (parts != 2 || nlevels > 16) {
+        S.parts = 1;
+        return;
+    }
+    int sp[16];
+    for (int l = 0; l < nlevels; l++) {
+        const int h = lv_host[l].h;
+        int s = ((h / 2 + BR_R / 2) / BR_R) * BR_R;  // the multiple of 30 nearest h / 2
+        if (h < 2 * BR_R) s = h;                       // too small to split: the top part blurs it all
+        s = std::min(s, h < 2 * BR_R ? h : h - BR_R);
+        sp[l] = s;
+        const int nch = (h + BR_R - 1) / BR_R, nch6 = (h + BR_RE - 1) / BR_RE;
+        S.ca[0][l] = 0, S.cb[0][l] = s == h ? nch : s / BR_R;
+        S.ca[1][l] = S.cb[0][l], S.cb[1][l] = nch;
+        S.ea[0][l] = 0, S.eb[0][l] = s == h ? nch6 : s / BR_RE;
+        S.ea[1][l] = S.eb[0][l], S.eb[1][l] = nch6;
+    }
+    // rows built per part, from the top level down
+    for (int l = nlevels - 1; l >= 0; l--) {
+        const int h = lv_host[l].h;
+        int thi = std::min(h, sp[l] + 3), blo = std::max(0, sp[l] - 3);
+        if (sp[l] == h) blo = h;  // the bottom part blurs none of this level
+        if (l + 1 < nlevels) {
+            const ResizeY* Y = ry + ry_off[l + 1];
+            if (S.hi[0][l + 1] > 0) thi = std::max(thi, Y[S.hi[0][l + 1] - 1].sy1 + 1);
+            if (S.lo[1][l + 1] < lv_host[l + 1].h) blo = std::min(blo, Y[S.lo[1][l + 1]].sy0);
+        }
+        S.lo[0][l] = 0, S.hi[0][l] = std::min(h, thi);
+        S.lo[1][l] = std::max(0, blo), S.hi[1][l] = h;
+        if (S.lo[1][l] >= h) S.lo[1][l] = h;  // nothing to build
+    }
 }
 bool pyramid_fusable(const LevelDesc* lv_host, const ResizeX* rx, const int* rx_off, int nlevels) {
     if (nlevels > 16) return false;

@@ -183,9 +183,20 @@ size_t resize_lds_bytes(int spitch, int dw, int max_src_rows);
 // gray + every pyramid level in one launch (one workgroup per frame); bgr may be
 // null (level 0 already in place). pyramid_fusable: the host check of its
 // assumptions (<= 16 levels, <= 4096 px wide, each quad's taps inside 8 bytes)
+// k_pyramid with two workgroups per frame (top / bottom part): per part and
+// level, the rows it builds [lo, hi) (its blur's halo and the next level's
+// source rows included: the parts compute the overlap twice, to the same
+// bytes), and its blur's 30-row strip chunks [ca, cb) and 6-row edge chunks
+// [ea, eb) (disjoint: each blur row is written by one part)
+struct PyrSplit {
+    int parts;  // 1: one workgroup per frame (the ranges cover everything)
+    int lo[2][16], hi[2][16], ca[2][16], cb[2][16], ea[2][16], eb[2][16];
+};
+void pyramid_split_plan(const LevelDesc* lv_host, const ResizeY* ry, const int* ry_off, int nlevels, int parts,
+                        PyrSplit& S);
 void launch_pyramid(hipStream_t st, const uint8_t* bgr, uint8_t* pyr, size_t in_stride, size_t pyr_stride,
                     const LevelDesc* lv, const ResizeX* rx, const ResizeY* ry, const int* rx_off, const int* ry_off,
-                    int nlevels, int nframes, uint8_t* blur, const LevelDesc* lv_host);
+                    int nlevels, int nframes, uint8_t* blur, const LevelDesc* lv_host, const PyrSplit& split);
 // blur: the blurred pyramid is written by the same launch (null: not);
 // pyramid_blur_fusable: every level is large enough for the strip walks
 bool pyramid_blur_fusable(const LevelDesc* lv_host, int nlevels);
