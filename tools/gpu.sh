@@ -21,6 +21,8 @@
 #   pmch=REGEX          the same on the hard workload
 #   vtests=V:F1,F2      pytest -m gpu over the named files against variant build_V
 #   probe=V:SCRIPT      python tools/SCRIPT.py with ODO_LIB = variant build_V (probe builds)
+#   envbench=NAME:ENV:ARGS  bench.py on the tuning build with knobs in the environment
+#                       (ENV: VAR=VAL joined by '/'; ARGS with '+' for spaces)
 #   ab=N:V1,V2,...      A/B of library builds on the bench (N alternations); Vi is
 #                       "default" (libodo_hip.so) or a variant name (build_Vi/);
 #                       bench arguments from $AB_ARGS
@@ -118,6 +120,14 @@ for step in "$@"; do
     pmch=*)
       K=${step#pmch=}
       pmc_passes "$K" "$O/pmch_$(echo $K | tr -c 'A-Za-z0-9_\n' '_')" --steps 2 --warmup 1 $QUICK --workload hard ;;
+    envbench=*)
+      # envbench=NAME:VAR=VAL/VAR2=VAL2:ARGS — the tuning build with knobs from the environment
+      spec=${step#envbench=}; name=${spec%%:*}; rest=${spec#*:}
+      envs=$(echo ${rest%%:*} | tr '/' ' '); args=$(echo ${rest#*:} | tr '+' ' ')
+      [ "$args" = "$rest" ] && args=""
+      env $envs ODO_LIB=$TUNING timeout -k 10 300 python bench.py --no-cpu-baseline --latency-frames 0 --host-steps 0 \
+        $args > $O/$name.json 2> $O/$name.err
+      echo "envbench $name: $(python tools/bsum.py $O/$name.json 2>/dev/null || true)" ;;
     ab=*)
       spec=${step#ab=}; n=${spec%%:*}; vs=$(echo ${spec#*:} | tr ',' ' ')
       for i in $(seq 1 $n); do
