@@ -419,7 +419,9 @@ struct ONode {
     int32_t seq;
 };
 
-#define OT_THREADS 256
+#ifndef OT_THREADS
+#define OT_THREADS 256  // threads per (frame, level) workgroup
+#endif
 
 // vSizeAndPointerToNode entry: sorts by (size, creation seq); low 16 bits carry
 // the node's list position (never compared: seq is unique).

@@ -217,6 +217,9 @@ __global__ void __launch_bounds__(256, FIN_WAVES_PER_EU) k_finalize(const uint8_
 // FIN_OVERLAY=1: the rBRIEF window overwrites the IC disc once the angle is
 // known (its loads are in flight since the start), so a keypoint holds 370
 // dwords of LDS instead of 649 and more workgroups fit a CU
+#ifndef FIN_SADDR
+#define FIN_SADDR 1  // staging loads as scalar frame base + 32-bit offsets stepped without divisions
+#endif
 #ifndef FIN_OVERLAY
 #define FIN_OVERLAY 1
 #endif
@@ -282,9 +285,45 @@ __global__ void __launch_bounds__(64 * NW) k_finalize_lds(const uint8_t* __restr
     uint32_t* P = s_patch[kslot];
     const int sh = (kx - 15) & 3, sh2 = (kx - 18) & 3;
     {
+        uint32_t v[18 + 24];
+#if FIN_SADDR
+        // 32-bit byte offsets from the frame's base (uniform over the
+        // workgroup: scalar base + vector offset loads), advanced per step
+        // of 16 staged dwords without divisions: 16 = 9 + 7 (IC rows of 9
+        // dwords) and 16 = 10 + 6 (rBRIEF rows of 10); a lane past the end
+        // reloads the last dword, as the clamped index did
+        const uint8_t* fpyr = pyr + (size_t)f * pyr_stride;
+        const uint8_t* fblur = blur + (size_t)f * pyr_stride;
+        const uint32_t pitch = (uint32_t)L.pitch;
+        {
+            const uint32_t o0 = (uint32_t)L.off + (uint32_t)(ky - 15) * pitch + (uint32_t)(kx - 15 - sh);
+            const uint32_t olast = o0 + 30u * pitch + 4u * 8u;
+            int c = sub % FL_IC_W;
+            uint32_t o = o0 + (uint32_t)(sub / FL_IC_W) * pitch + 4u * (uint32_t)c;
+#pragma unroll
+            for (int j = 0; j < 18; j++) {
+                v[j] = *reinterpret_cast<const uint32_t*>(fpyr + (sub + 16 * j < FL_IC_N ? o : olast));
+                const bool one = c < 2;
+                o += one ? pitch + 28u : 2u * pitch - 8u;
+                c = one ? c + 7 : c - 2;
+            }
+        }
+        {
+            const uint32_t o0 = (uint32_t)L.off + (uint32_t)(ky - 18) * pitch + (uint32_t)(kx - 18 - sh2);
+            const uint32_t olast = o0 + 36u * pitch + 4u * 9u;
+            int c = sub % FL_BR_W;
+            uint32_t o = o0 + (uint32_t)(sub / FL_BR_W) * pitch + 4u * (uint32_t)c;
+#pragma unroll
+            for (int j = 0; j < 24; j++) {
+                v[18 + j] = *reinterpret_cast<const uint32_t*>(fblur + (sub + 16 * j < FL_BR_N ? o : olast));
+                const bool one = c < 4;
+                o += one ? pitch + 24u : 2u * pitch - 16u;
+                c = one ? c + 6 : c - 4;
+            }
+        }
+#else
         const uint8_t* img = pyr + (size_t)f * pyr_stride + L.off + (size_t)(ky - 15) * L.pitch + (kx - 15 - sh);
         const uint8_t* bim = blur + (size_t)f * pyr_stride + L.off + (size_t)(ky - 18) * L.pitch + (kx - 18 - sh2);
-        uint32_t v[18 + 24];
 #pragma unroll
         for (int j = 0; j < 18; j++) {
             const int i = min(sub + 16 * j, FL_IC_N - 1);
@@ -297,6 +336,7 @@ __global__ void __launch_bounds__(64 * NW) k_finalize_lds(const uint8_t* __restr
             const int r = i / FL_BR_W, c = i - r * FL_BR_W;
             v[18 + j] = *reinterpret_cast<const uint32_t*>(bim + (size_t)r * L.pitch + 4 * c);
         }
+#endif
 #pragma unroll
         for (int j = 0; j < 18; j++)
             if (sub + 16 * j < FL_IC_N) P[sub + 16 * j] = v[j];
