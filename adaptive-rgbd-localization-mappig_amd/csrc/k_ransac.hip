@@ -1302,7 +1302,7 @@ ODO_INLINE double readlane_d(double v, int l) {
 #define LN_WAVES 4
 #define LN_RS 33  // LDS row stride (doubles) of the parked terms
 #ifndef LN_SLOTS
-#define LN_SLOTS 48  // lanes per wave that take up hypotheses (rows of parked terms per wave)
+#define LN_SLOTS 32  // lanes per wave that take up hypotheses (rows of parked terms per wave)
 #endif
 #ifndef LN_HELP
 #define LN_HELP 0  // 1: a wave whose pair has no hypothesis left joins another open pair that has
@@ -1326,7 +1326,7 @@ ODO_INLINE double readlane_d(double v, int l) {
 #define LN_PRIO ODO_WAVE_PRIO  // k_ransac_lanes' wave priority
 #endif
 #ifndef LN_TLDS
-#define LN_TLDS 1  // sweep: transforms from an LDS slot table (pair with LN_SLOTS <= 48 to fit two workgroups per CU)
+#define LN_TLDS 1  // sweep: transforms from an LDS slot table (LN_SLOTS <= 48 fits two workgroups per CU)
 #endif
 #ifndef LN_PRE
 #define LN_PRE 0  // sweep: transforms permuted as doubles with their point-independent covariance terms
