@@ -2274,9 +2274,12 @@ struct Layout {
 };
 
 // k_ransac_lanes grid: workgroups of LN_WAVES waves (ODO_RANSAC_LANES, 0 = the
-// wave-per-hypothesis work list k_ransac_eval_list instead)
+// wave-per-hypothesis work list k_ransac_eval_list instead). 384 = 1.5 per CU
+// of the 256: alone the launch is faster at 2 per CU (512), but in the
+// pipelined step the half-empty CUs run the other pair stream's PnP and the
+// next batch's extraction beside it (hard workload +5 %)
 #ifndef LN_GROUPS
-#define LN_GROUPS 512
+#define LN_GROUPS 384
 #endif
 static int ln_groups() {
     static int r = [] {
