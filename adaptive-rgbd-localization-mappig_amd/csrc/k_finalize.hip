@@ -484,13 +484,16 @@ void launch_finalize(hipStream_t st, const uint8_t* pyr, const uint8_t* blur, si
     dim3 g((kp_cap + FIN_KPB - 1) / FIN_KPB, nframes);
     // ODO_FIN_LDS: 0 the per-lane-gather k_finalize; 1 the staged kernel at 4
     // waves (16 keypoints, 42.5 KB LDS) per workgroup; 2 (default) at 2 waves
-    // (8 keypoints, 21 KB: more workgroups resident per CU)
+    // (8 keypoints, 21 KB: more workgroups resident per CU); 3 at 1 wave
     static const int staged = [] {
         const char* e = odo_knob("ODO_FIN_LDS");
         return e ? atoi(e) : 2;
     }();
 #ifdef ODO_TUNING
-    if (staged == 1)
+    if (staged == 3)  // one wave (4 keypoints, 6.3 KB) per workgroup
+        hipLaunchKernelGGL(k_finalize_lds<1>, dim3((kp_cap + 3) / 4, nframes), dim3(64), 0, st, pyr, blur, pyr_stride,
+                           lv, nlevels, okp, ocnt, okp_stride, kps, desc, nkp, kp_cap);
+    else if (staged == 1)
         hipLaunchKernelGGL(k_finalize_lds<4>, g, dim3(256), 0, st, pyr, blur, pyr_stride, lv, nlevels, okp, ocnt,
                            okp_stride, kps, desc, nkp, kp_cap);
     else if (staged == 0)
