@@ -2321,8 +2321,9 @@ static Layout layout(int npairs, int match_cap, int mask_words, const RansacCfg&
     o = al(o + (size_t)npairs * ransac_rawcap(cfg) * 4);
     L.open = o;
     o = al(o + (size_t)(npairs + 2) * 4);
-    L.lslab = o;  // per-wave inlier-set buffers of k_ransac_lanes
-    o = al(o + (size_t)ln_groups() * LN_WAVES * 2 * mask_words * 64 * 4);
+    L.lslab = o;  // per-wave inlier-set buffers of k_ransac_lanes (never launched for one pair:
+                  // a lone pair starts every hypothesis row in the first launch)
+    if (npairs > 1) o = al(o + (size_t)ln_groups() * LN_WAVES * 2 * mask_words * 64 * 4);
     L.total = o;
     return L;
 }

@@ -198,6 +198,15 @@ struct odo_ctx {
     // back here with async copies into pinned memory and one sync
     uint8_t* stage_h = nullptr;
     size_t stage_cap = 0;
+    // hypotheses mode (odo_ransac_hyps*): device scratch kept across sessions
+    // (grow-only: a session per pair used to hipMalloc / hipFree its own,
+    // 0.5 ms of the 1.2 ms per pair of round 4) and the session's packed
+    // inputs in page-locked memory (one DMA), reused once hyp_up has passed
+    DevArena hyp_arena;
+    uint8_t* hyp_stage_h = nullptr;
+    size_t hyp_stage_cap = 0;
+    hipEvent_t hyp_up = nullptr;
+    bool hyp_up_rec = false;
     int in_next = 0;
     // pair buffers ([maxb])
     int2 *knn_idx[NSETS] = {}, *knn_dist[NSETS] = {};  // per frame set
@@ -430,6 +439,8 @@ static void free_ctx(odo_ctx* c) {
     if (c->ev_latch) hipEventDestroy(c->ev_latch);
     if (c->ev_depth_done) hipEventDestroy(c->ev_depth_done);
     if (c->stage_h) (void)hipHostFree(c->stage_h);
+    if (c->hyp_stage_h) (void)hipHostFree(c->hyp_stage_h);
+    if (c->hyp_up) hipEventDestroy(c->hyp_up);
     for (hipStream_t st : c->owned) hipStreamDestroy(st);
     if (c->h_open) (void)hipHostFree(c->h_open);
     delete c;
@@ -2118,7 +2129,8 @@ int prepare_pair_ransac(const odo_dmatch* m12, int n12, const float* xyz1, int n
 struct HypSession {
     PairRansacInput in;
     int h0 = 0, h1 = 0, active = 0;
-    DevArena arena;  // lives from odo_ransac_hyps to odo_ransac_hyps_finish
+    DevArena& arena;  // the context's hyp_arena: this session's buffers until the next session
+    explicit HypSession(DevArena& a) : arena(a) {}
     DevBuf *xyz = nullptr, *m = nullptr, *g = nullptr, *ints = nullptr, *latch = nullptr, *rng = nullptr,
            *res = nullptr, *T = nullptr, *scr = nullptr, *bm = nullptr, *phase = nullptr;
     ~HypSession() {
@@ -2312,7 +2324,7 @@ static int hyps_launch(odo_ctx* c, const odo_dmatch* m12, int n12, const float* 
                        int n2, const odo_ransac_params* p, const odo_rng* rng, double* latch, int h0, int h1,
                        int* n_good, int* active) {
     free_hyp_session(c->hs);
-    c->hs = new HypSession();
+    c->hs = new HypSession(c->hyp_arena);
     HypSession& S = *c->hs;
     S.h0 = h0;
     S.h1 = h1;
@@ -2349,13 +2361,39 @@ static int hyps_launch(odo_ctx* c, const odo_dmatch* m12, int n12, const float* 
     }
     const int ints[4] = {ng, ng, 1, 0};
     const int range[2] = {h0, h1};
-    HIPCHK(hipMemcpyAsync(S.xyz->p, xyz1, (size_t)n1 * 12, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(S.xyz->as<float>() + (size_t)kc * 3, xyz2, (size_t)n2 * 12, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(S.m->p, in.good.data(), (size_t)ng * sizeof(odo_dmatch), hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(S.g->p, gl.data(), (size_t)ng * 8, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(S.ints->p, ints, sizeof(ints), hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(S.latch->p, latch, sizeof(double), hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(S.rng->p, rng, sizeof(odo_rng), hipMemcpyHostToDevice, st));
+    // the inputs packed in page-locked memory in their device order (the
+    // arena hands out consecutive 256-B aligned sections, as Pack does): one
+    // DMA instead of seven pageable copies. The previous session's upload
+    // must have left the buffer before it is refilled.
+    Pack pk;
+    const size_t o_xyz = pk.add((size_t)2 * kc * 3 * sizeof(float)), o_m = pk.add((size_t)ng * sizeof(odo_dmatch)),
+                 o_g = pk.add((size_t)ng * 8), o_int = pk.add(4 * sizeof(int)), o_lat = pk.add(sizeof(double)),
+                 o_rng = pk.add(sizeof(odo_rng));
+    const size_t up = o_rng + sizeof(odo_rng);
+    if ((uint8_t*)S.rng->p - (uint8_t*)S.xyz->p != (ptrdiff_t)o_rng)
+        return fail(ODO_ERR_STATE, "hyps: arena sections not contiguous");
+    if (c->hyp_up_rec) HIPCHK(hipEventSynchronize(c->hyp_up));
+    if (up > c->hyp_stage_cap) {
+        if (c->hyp_stage_h) (void)hipHostFree(c->hyp_stage_h);
+        c->hyp_stage_h = nullptr;
+        c->hyp_stage_cap = 0;
+        const size_t cap = std::max(up, (size_t)1 << 20);
+        if (hipHostMalloc((void**)&c->hyp_stage_h, cap, hipHostMallocDefault) != hipSuccess)
+            return fail(ODO_ERR_DEVICE, "hipHostMalloc (hypotheses staging) failed");
+        c->hyp_stage_cap = cap;
+    }
+    if (!c->hyp_up) HIPCHK(hipEventCreateWithFlags(&c->hyp_up, hipEventDisableTiming));
+    uint8_t* hb = c->hyp_stage_h;
+    memcpy(hb + o_xyz, xyz1, (size_t)n1 * 12);
+    memcpy(hb + o_xyz + (size_t)kc * 12, xyz2, (size_t)n2 * 12);
+    memcpy(hb + o_m, in.good.data(), (size_t)ng * sizeof(odo_dmatch));
+    memcpy(hb + o_g, gl.data(), (size_t)ng * 8);
+    memcpy(hb + o_int, ints, sizeof(ints));
+    memcpy(hb + o_lat, latch, sizeof(double));
+    memcpy(hb + o_rng, rng, sizeof(odo_rng));
+    HIPCHK(hipMemcpyAsync(S.xyz->p, hb, up, hipMemcpyHostToDevice, st));
+    HIPCHK(hipEventRecord(c->hyp_up, st));
+    c->hyp_up_rec = true;
     // the part-3 launch reads its range from host memory before returning
     int* hrange = const_cast<int*>(range);
     launch_ransac_raw(st, S.scr->p, 1, ng, in.words, in.cfg, 0, 0, S.rng->as<odo_rng>());
@@ -2408,8 +2446,11 @@ int odo_ransac_hyps_dev(odo_ctx* c, const odo_dmatch* m12, int n12, const float*
     if (!active) {
         // no sampling: the default summaries (the fold returns before them)
         if (h1 > h0) {
+            // queued on the context's stream behind its earlier work; the
+            // host vector dies at return, so this path synchronises (odo.h)
             std::vector<odo_hyp_summary> d(h1 - h0, odo_hyp_summary{1e6, 0, 0, {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0}});
-            HIPCHK(hipMemcpy(d_block, d.data(), d.size() * sizeof(odo_hyp_summary), hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpyAsync(d_block, d.data(), d.size() * sizeof(odo_hyp_summary), hipMemcpyHostToDevice, st));
+            HIPCHK(hipStreamSynchronize(st));
         }
         return ODO_OK;
     }
@@ -2528,7 +2569,8 @@ int odo_ransac_hyps_finish_dev(odo_ctx* c, const void* d_fold, int rank0, void* 
             const float r = 1e6f;
             memcpy(&w[16], &r, 4);
         }
-        HIPCHK(hipMemcpy(d_payload, w.data(), w.size() * 4, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpyAsync(d_payload, w.data(), w.size() * 4, hipMemcpyHostToDevice, st));
+        HIPCHK(hipStreamSynchronize(st));  // w dies at return (odo.h: this path synchronises)
         return ODO_OK;
     }
     launch_hyp_finish(st, S.scr->p, S.in.ng, S.in.words, S.in.cfg, S.latch->as<double>(), S.rng->as<odo_rng>(),

@@ -194,7 +194,13 @@ def sharded_ransac_device(odo, ex: DeviceExchange, m12: np.ndarray, xyz1: np.nda
     H = max(params.iterations, 0)
     h0, h1, per = device_range(H, ex.rank, ex.world)
     dev = torch.device("cuda", torch.cuda.current_device())
-    block = torch.zeros(max(per, 1) * HYP_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    # every tensor the library writes is allocated on the context's stream (its
+    # non-blocking odometry stream), so the caching allocator orders its reuse
+    # there; torch.empty: the padding and the fold record are written before
+    # they are read, so there is no fill to race with the library's writes
+    with torch.cuda.stream(ex.stream):
+        block = torch.empty(max(per, 1) * HYP_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+        fold_rec = torch.empty(32, dtype=torch.uint8, device=dev)
     lat = C.c_double(latch)
     ng = C.c_int(0)
     sync = (lambda: torch.cuda.synchronize()) if timing is not None else (lambda: None)
@@ -207,12 +213,12 @@ def sharded_ransac_device(odo, ex: DeviceExchange, m12: np.ndarray, xyz1: np.nda
     allh = ex.all_gather(block)
     sync()
     t2 = time.perf_counter()
-    fold_rec = torch.zeros(32, dtype=torch.uint8, device=dev)
     check(lib.odo_ransac_fold_dev(odo.h, C.c_void_p(allh.data_ptr()), H, C.c_void_p(fold_rec.data_ptr())))
     words = lib.odo_ransac_hyps_payload_words(odo.h)
     if words < 0:
         check(words)
-    payload = torch.empty(words, dtype=torch.int32, device=dev)
+    with torch.cuda.stream(ex.stream):
+        payload = torch.empty(words, dtype=torch.int32, device=dev)
     check(lib.odo_ransac_hyps_finish_dev(odo.h, C.c_void_p(fold_rec.data_ptr()), 1 if ex.rank == 0 else 0,
                                          C.c_void_p(payload.data_ptr()), words))
     sync()

@@ -219,7 +219,10 @@ int odo_ransac_hyps_finish(odo_ctx* ctx, const odo_ransac_fold_result* r, odo_rn
  * 1) odo_ransac_hyps_dev: as odo_ransac_hyps, the summaries of [h0, h1) into
  *    the DEVICE buffer d_block ((h1-h0) x 64 B, odo_hyp_summary layout); no
  *    host synchronisation. The gathered array must hold all H summaries in
- *    hypothesis order (contiguous rank ranges). */
+ *    hypothesis order (contiguous rank ranges). When the pair never samples
+ *    (Iterate returns before its loop: too few matches) the default summaries
+ *    are copied on odo_stream(ctx) and this call synchronises that stream
+ *    before it returns (step 4 does the same for its payload). */
 int odo_ransac_hyps_dev(odo_ctx* ctx, const odo_dmatch* m12, int n12, const float* xyz1, int n1,
                         const float* xyz2, int n2, const odo_ransac_params* p, const odo_rng* rng,
                         double* latch, int h0, int h1, void* d_block, int* n_good);
@@ -254,13 +257,14 @@ int odo_pnp_motion_ba(odo_ctx* ctx, const float* Xw, const float* obs, int n, co
  * uv: n x 2 undistorted keypoints (mvKeysUn), in index order. n < 10 returns
  * res->ok = 0 without running (pnpransac.cpp:30); no model with more than 4
  * inliers gives ok = 0; a best model with exactly 5 non-planar inliers gives
- * ok = -1 (OpenCV's final solvePnP asserts count >= 6 in its DLT start and
- * throws; Tcw and rvec/tvec are then zero, the model, mask and n_inliers are
- * set). inlier_mask (n, optional):
+ * ok = ODO_PNP_RANSAC_THROW (-1: OpenCV's final solvePnP asserts count >= 6
+ * in its DLT start and throws; Tcw and rvec/tvec are then zero, the model,
+ * mask and n_inliers are set). Test ok == 1 for success, never truthiness. inlier_mask (n, optional):
  * the RANSAC inliers (Frame::SetInlier); good_counts (iterations, optional):
  * inliers of every hypothesis, of which the first res->iterations_visited are
  * the ones RANSAC visited. Hypotheses, EPnP, counts, the ordered fold and the
  * Levenberg-Marquardt refinement all run on the GPU (k_pnpransac.hip). */
+#define ODO_PNP_RANSAC_THROW (-1)
 int odo_pnp_ransac(odo_ctx* ctx, const float* Xw, const float* uv, int n, const odo_calib* calib, int iterations,
                    float reproj_err, double confidence, odo_pnp_ransac_result* res, uint8_t* inlier_mask,
                    int32_t* good_counts);

@@ -150,6 +150,7 @@ def _device_run(pkg, ctxs, m, x1, x2, iters, seed):
         lat = O.C.c_double(float("nan"))
         ng = O.C.c_int(0)
         blk = torch.full((max(per, 1) * 64,), 0x5A, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()  # the fill runs on torch's stream, the library on its own
         pkg.check(lib.odo_ransac_hyps_dev(odo.h, pkg.ptr(m), m.size, pkg.ptr(x1), x1.shape[0], pkg.ptr(x2),
                                           x2.shape[0], pkg.ptr(params), pkg.ptr(rng), O.C.byref(lat), h0, h1,
                                           O.C.c_void_p(blk.data_ptr()), O.C.byref(ng)))
@@ -163,6 +164,7 @@ def _device_run(pkg, ctxs, m, x1, x2, iters, seed):
         pkg.check(lib.odo_ransac_fold_dev(odo.h, O.C.c_void_p(allh.data_ptr()), iters, O.C.c_void_p(rec.data_ptr())))
         words = lib.odo_ransac_hyps_payload_words(odo.h)
         pl = torch.full((words,), 7, dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
         pkg.check(lib.odo_ransac_hyps_finish_dev(odo.h, O.C.c_void_p(rec.data_ptr()), 1 if r == 0 else 0,
                                                  O.C.c_void_p(pl.data_ptr()), words))
         torch.cuda.synchronize()

@@ -21,6 +21,6 @@ out = {
     "warmup_launches": W,
     "timed_region_launches": len(timed),
     "timed_region_mean_us": round(sum(timed) / max(1, len(timed)), 1),
-    "bench_line": {"kernel_ms": b["roofline"]["kernel_ms"], "alone_ms": b["roofline"]["alone"]["ms"]},
+    "bench_line": {"kernel_ms": b["roofline"]["kernel_ms"], "alone_ms": b["roofline"]["alone"]["kernel_ms"]},
 }
 print(json.dumps(out, indent=1))

@@ -28,8 +28,24 @@ def load(dirpath):
     return acc
 
 
+N_SIMD = 1024   # 256 CUs x 4 SIMDs
+CLK_GHZ = 2.4
+
+
+def durations(dirpath):
+    """Mean dispatch duration (ns) per kernel from the kernel-trace pass."""
+    acc = defaultdict(list)
+    for path in glob.glob(os.path.join(dirpath, "**", "*kernel_trace.csv"), recursive=True):
+        with open(path) as f:
+            for r in csv.DictReader(f):
+                k = r["Kernel_Name"].split("(")[0].replace("odo::", "").replace("void ", "").strip()
+                acc[k].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
 def main():
     pdir, out = sys.argv[1], sys.argv[2]
+    durs = durations(os.path.join(pdir, "kt"))
     acc = defaultdict(dict)
     for sub in ("sq1", "sq2", "tcc", "tccw"):
         for k, cs in load(os.path.join(pdir, sub)).items():
@@ -48,8 +64,18 @@ def main():
             for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU"):
                 if c in m:
                     row[c + "_frac_of_wave_cycles"] = round(m[c] / m["SQ_WAVE_CYCLES"], 3)
-        if m.get("SQ_BUSY_CYCLES") and "SQ_VALU_MFMA_BUSY_CYCLES" in m:
-            row["mfma_busy_frac"] = round(m["SQ_VALU_MFMA_BUSY_CYCLES"] / m["SQ_BUSY_CYCLES"], 4)
+        # SQ_VALU_MFMA_BUSY_CYCLES counts shader cycles summed over the SIMDs
+        # (16 per 16x16x128 FP4 MFMA: SQ_INSTS_MFMA x 16 reproduces it), so the
+        # fraction is over the chip's SIMD-cycles during the dispatch: 1024
+        # SIMDs x the kernel's mean duration (the kt pass of the same
+        # directory) x 2.4 GHz. SQ_BUSY_CYCLES is a per-SE count and is not a
+        # denominator for it (round 4 divided by it: 13.1, not a fraction).
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in m and k in durs:
+            row["mean_duration_us"] = round(durs[k] / 1e3, 2)
+            row["mfma_busy_frac"] = round(m["SQ_VALU_MFMA_BUSY_CYCLES"] / (N_SIMD * durs[k] * CLK_GHZ), 4)
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in m and m.get("SQ_BUSY_CU_CYCLES"):
+            # SQ_BUSY_CU_CYCLES: cycles each CU had work, summed over the CUs
+            row["mfma_busy_frac_of_busy_cu"] = round(m["SQ_VALU_MFMA_BUSY_CYCLES"] / (4 * m["SQ_BUSY_CU_CYCLES"]), 4)
         fb = 2 * m["FETCH_SIZE"] * 1024 if "FETCH_SIZE" in m else None
         wb = m["WRITE_SIZE"] * 1024 if "WRITE_SIZE" in m else None
         if fb is not None and wb is not None:

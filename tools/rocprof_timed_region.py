@@ -62,9 +62,12 @@ for leg, key in (("hbm_resident", "kernel_ms"), ("from_host", None)):
     cmp = int(line["work"].split()[0]) if line.get("work") else None
     kn["bench_event_ms"] = ev
     if cmp:
-        a = 16.0 * cmp / (kn["mean_us"] * 1e-6) / 1e12
-        kn["valu16_achieved_tops"] = round(a, 2)
-        kn["valu16_frac_of_78.6T"] = round(a / 78.6, 4)
+        # the line's primary roofline: 512 FP4 MFMA ops per comparison against
+        # the dense FP4 spec; the SURVEY 8(d) 16-op VALU equivalent beside it
+        a = 512.0 * cmp / (kn["mean_us"] * 1e-6) / 1e12
+        kn["mfma_fp4_achieved_tops"] = round(a, 1)
+        kn["mfma_fp4_frac_of_10066T"] = round(a / 10066.3, 4)
+        kn["valu16_equivalent_tops"] = round(16.0 * cmp / (kn["mean_us"] * 1e-6) / 1e12, 2)
 with open(out_path, "w") as f:
     json.dump(res, f, indent=1)
 print(json.dumps(res, indent=1))
