@@ -4,7 +4,7 @@
 //
 //   k_gray        cvtColor(BGR2GRAY)                 frame.cpp:23
 //   k_resize      ComputePyramid (INTER_LINEAR 8U)    orbextractor.cpp:833-857
-//   k_fast_cells  FAST-9/16 + NMS per 30px cell       orbextractor.cpp:669-723
+//   k_fast_seg    FAST-9/16 + NMS per 30px cell       orbextractor.cpp:669-723
 //   k_octree      DistributeOctTree                   orbextractor.cpp:466-663
 //   k_blur        GaussianBlur 7x7 s=2 REFLECT_101    orbextractor.cpp:795-796
 //   k_finalize    (k_finalize.hip) IC_Angle + rBRIEF + scale; k_kp_geometry undistort + depth
@@ -125,287 +125,371 @@ __global__ void __launch_bounds__(256) k_resize(uint8_t* __restrict__ pyr, size_
     }
 }
 
-// ============================================================ FAST per cell
+// ============================================================ FAST per cell-row segment
+// ComputeKeyPointsOctTree's FAST part (orbextractor.cpp:669-723): every cell
+// ROI runs cv::FAST(th = iniThFAST, nonmax), and again at minThFAST when it
+// kept nothing (FAST_t<16> + cornerScore<16>, NMS strictly greater than the 8
+// neighbours inside the ROI's detection area).
+//
+// One 256-thread workgroup per segment: up to FS_NCM consecutive cells of one
+// cell row of one level (FastSeg, host table). The cells' ROIs overlap only
+// in their 3-pixel margins and their detection areas tile the row, so the
+// segment stages the union of its ROIs in LDS once (16-byte loads) and runs
+// each phase over the whole segment:
+//   1. compass pre-filter on 4 pixels per item (pixels 0/4/8/12 of the circle:
+//      any 9-arc holds two adjacent compass points of its sign), survivors
+//      appended to a per-wave ring in LDS; every 128 survivors the wave runs
+//   2. the segment test + cornerScore, two per lane in packed 16-bit lanes
+//      (corner iff the threshold-free S > th; score = S - 1), scores into an
+//      LDS map, corners appended to the segment's corner list;
+//   3. NMS per corner against the 8 neighbours that lie in the corner's own
+//      cell (a neighbour across a cell boundary is outside that cell's ROI
+//      detection area, i.e. 0 in its FAST score buffer); kept corners set a
+//      bit in a per-row bitmap and count per (row, cell);
+//   4. per cell an exclusive scan of the row counts; a kept corner's slot in
+//      its cell's list = the kept corners of its cell in earlier rows + the
+//      bits left of it in its row inside the cell: the cell's row-major order,
+//      with no ordered compaction anywhere.
+// Cells that kept nothing run the four phases again at minThFAST over their
+// own quads only. Scores do not depend on the threshold (S - 1 for any corner),
+// so the map is not cleared for the second pass.
+// (Until round 4: one wave per cell ROI, staged per cell with its halo, with
+// per-cell setup and ordered compactions: 988 VALU + 510 SALU per cell.)
 __constant__ int c_circle_dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
 __constant__ int c_circle_dy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
+#define FS_TH 256
+#define FS_RING 512  // survivors per wave ring (u16 offsets): <= 127 pending + 256 per compass step
+#define FS_CL 2048   // corner list; beyond it the NMS and placement scan the score map
 
-// One wave (64 lanes) per cell ROI. Candidates packed as (resp<<24)|(y<<12)|x
-// with x,y relative to the 16px border (vToDistributeKeys coordinates),
-// emitted in row-major order within the cell. Per threshold attempt:
-//   1. compass pre-filter over the detection region (pixels 0/4/8/12 of the
-//      circle: any 9-arc holds two adjacent compass points of its sign, so this
-//      is a necessary condition), survivors queued in row-major order,
-//   2. the 16-pixel test and cornerScore in one pass on the queue (corner iff
-//      the threshold-free S exceeds th), corners listed in order with their
-//      scores in an LDS map (0 elsewhere),
-//   3. NMS (strictly greater than the 8 neighbours) over the corner list.
-// FAST_CPW cells per workgroup, one wave each (the waves are independent:
-// wave-scope syncs only), so the launch is ncells / FAST_CPW workgroups.
-#ifndef FAST_CPW
-#define FAST_CPW 1
-#endif
-// FAST_PARTS > 1: the detection rows are tested in that many row parts, each
-// followed by its segment test and NMS, so the survivor queue holds one part
-// (+ one row: a part also scores the first row of the next, which the NMS of
-// its own last row reads; that row is scored again and output with the next
-// part). Less LDS per wave, more waves per CU; the same candidates in the
-// same order.
-#ifndef FAST_PARTS
-#define FAST_PARTS 1
-#endif
-ODO_INLINE void fast_wave_sync() {
-    if (FAST_CPW == 1) {
-        __syncthreads();
-    } else {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
+ODO_INLINE void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
-template <int ROI_MAX>
-__global__ void __launch_bounds__(64 * FAST_CPW) k_fast_cells(const uint8_t* __restrict__ pyr, size_t pyr_stride,
-                                                   const CellDesc* __restrict__ cells, const LevelDesc* __restrict__ lv,
-                                                   uint32_t* __restrict__ cand, int* __restrict__ cand_cnt,
-                                                   int ncells, int cell_cap, int ini_th, int min_th) {
+
+struct FastMisc {
+    int ncl, ovf, nl;
+    int tot[FS_NCM], retry[FS_NCM];
+};
+
+__global__ void __launch_bounds__(FS_TH) k_fast_seg(const uint8_t* __restrict__ pyr, size_t pyr_stride,
+                                                   const FastSeg* __restrict__ segs, const LevelDesc* __restrict__ lv,
+                                                   uint32_t* __restrict__ cand, int* __restrict__ cand_cnt, int ncells,
+                                                   int cell_cap, int ini_th, int min_th, FastLds LO) {
     EXTRACT_PRIO();
-    // ROI rows staged as whole aligned dwords: pixel (r, c) at byte r*RS + sh + c
-    constexpr int RS4 = (ROI_MAX + 3 + 3) / 4 + 1;  // dwords per staged row (>= (sh+cols+3)/4)
-    constexpr int RS = 4 * RS4;
-    __shared__ __attribute__((aligned(16))) uint32_t roi32_w[FAST_CPW][ROI_MAX * RS4];
-    __shared__ __attribute__((aligned(16))) uint32_t score32_w[FAST_CPW][ROI_MAX * RS4];
-    // survivor queue; the corner list is compacted into it in place (a wave
-    // writes entry n2 + rank <= base + lane only after reading entries
-    // base..base+63, so unread entries are never overwritten): 8.9 KB of LDS
-    // per single-wave workgroup, 4 waves per SIMD
-    constexpr int QROWS = FAST_PARTS == 1 ? ROI_MAX - 6 : (ROI_MAX - 6 + FAST_PARTS - 1) / FAST_PARTS + 1;
-    __shared__ uint16_t q1_w[FAST_CPW][QROWS * (ROI_MAX - 6)];
-    const int wv = FAST_CPW == 1 ? 0 : (int)(threadIdx.x >> 6);
-    uint32_t* const roi32 = roi32_w[wv];
-    uint32_t* const score32 = score32_w[wv];
-    uint16_t* const q1 = q1_w[wv];
-    uint16_t* const q2 = q1;
-    const uint8_t* roi = reinterpret_cast<const uint8_t*>(roi32);
-    uint8_t* score = reinterpret_cast<uint8_t*>(score32);
+    extern __shared__ __attribute__((aligned(16))) uint8_t fs_lds[];
+    const FastSeg G = segs[blockIdx.x];
     const int f = blockIdx.y;
-    const int ci = blockIdx.x * FAST_CPW + wv;
-    if (ci >= ncells) return;  // wave-uniform (no workgroup barriers below)
-    const int lane = threadIdx.x & 63;
-    const CellDesc C = cells[ci];
-    const LevelDesc L = lv[C.level];
-    const uint8_t* img = pyr + (size_t)f * pyr_stride + L.off;
-    const int rows = C.rows, cols = C.cols;
-    const int sh = C.x0 & 3;
-    const int nwr = (sh + cols + 3) >> 2;  // dwords per ROI row
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    uint8_t* const roi = fs_lds;
+    const uint32_t* const roi32 = reinterpret_cast<const uint32_t*>(fs_lds);
+    uint8_t* const score = fs_lds + LO.img;
+    uint16_t* const ring = reinterpret_cast<uint16_t*>(fs_lds + LO.ring) + wave * FS_RING;
+    uint16_t* const clist = reinterpret_cast<uint16_t*>(fs_lds + LO.clist);
+    uint32_t* const bits = reinterpret_cast<uint32_t*>(fs_lds + LO.bits);
+    int* const cnt = reinterpret_cast<int*>(fs_lds + LO.cnt);
+    uint32_t* const qlist = reinterpret_cast<uint32_t*>(fs_lds + LO.qlist);
+    FastMisc& M = *reinterpret_cast<FastMisc*>(fs_lds + LO.misc);
+    const LevelDesc L = lv[G.level];
+    const int R = G.rows, cols = G.cols, RS = G.rs, RS4 = RS >> 2, BW = G.bw, wcell = G.wcell, nc = G.ncell;
+    const int sh = G.x0 & 15;  // staged from the 16-byte column below x0: pixel (r, x) at byte r*RS + sh + x
     {
-        // rows are pitch-aligned: dword loads from the aligned column below x0
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(img + (size_t)C.y0 * L.pitch + (C.x0 & ~3));
-        const uint32_t p4 = (uint32_t)L.pitch >> 2;
-        // lane = (dword k of KW, row phase): no per-item division, and the
-        // rows' loads are independent
-        constexpr int KW = RS4 <= 16 ? 16 : 32;
-        static_assert(RS4 <= KW, "staged ROI rows wider than 32 dwords");
-        const int k = lane & (KW - 1);
-        if (k < nwr) {
-#pragma unroll 4
-            for (int r = lane / KW; r < rows; r += 64 / KW)
-                roi32[r * RS4 + k] = src[__umul24((uint32_t)r, p4) + (uint32_t)k];
-        }
+        const uint4* src = reinterpret_cast<const uint4*>(pyr + (size_t)f * pyr_stride + L.off +
+                                                          (size_t)G.y0 * L.pitch + (G.x0 & ~15));
+        const int nw = (sh + cols + 15) >> 4, p16 = L.pitch >> 4;
+        const int rstep = FS_TH / nw, k = t % nw, r0 = t / nw;
+        if (r0 < rstep)
+            for (int r = r0; r < R; r += rstep)
+                reinterpret_cast<uint4*>(roi + r * RS)[k] = src[__umul24((uint32_t)r, (uint32_t)p16) + (uint32_t)k];
+        for (int i = t; i < (R * RS) >> 4; i += FS_TH) reinterpret_cast<uint4*>(score)[i] = uint4{0, 0, 0, 0};
+        for (int i = t; i < R * BW; i += FS_TH) bits[i] = 0;
+        for (int i = t; i < R * FS_NCM; i += FS_TH) cnt[i] = 0;
+        if (t == 0) M.ncl = 0, M.ovf = 0;
     }
-    uint32_t* out = cand + ((size_t)f * ncells + ci) * cell_cap;
-    const int drows = rows - 6;
-    // detection bytes [sh+3, sh+cols-3) of rows 3..rows-4, walked as aligned dwords
+    __syncthreads();
+    const int drows = R - 6;
     const int m0 = (sh + 3) >> 2, m1 = (sh + cols - 4) >> 2;
-    const int nq = cols > 6 ? m1 - m0 + 1 : 0;
-    const int nitems = drows > 0 ? drows * nq : 0;
-    const int qdq = nq > 0 ? 64 / nq : 0, qdr = nq > 0 ? 64 - qdq * nq : 0;
-    // detection bytes of quad m0 + j (bits i with sh+3 <= 4(m0+j)+i < sh+cols-3),
-    // 4 bits per quad: nq <= 16 for ROI_MAX <= 60 (the table is exact there;
-    // wider ROIs take the same test per quad)
-    uint64_t qmask = 0;
-    for (int j = 0; ROI_MAX <= 60 && j < nq && j < 16; j++) {
-        const int lo = sh + 3 - 4 * (m0 + j), hi = sh + cols - 3 - 4 * (m0 + j);  // valid i in [lo, hi)
-        const uint32_t vm = (lo <= 0 ? 0xFu : (0xFu << lo) & 0xFu) & (hi >= 4 ? 0xFu : ((1u << hi) - 1u));
-        qmask |= (uint64_t)vm << (4 * j);
-    }
+    const uint32_t mlo = (0xFu << (sh + 3 - 4 * m0)) & 0xFu, mhi = (1u << (sh + cols - 3 - 4 * m1)) - 1u;
+    const float inv_rs = 1.0f / (float)RS, inv_w = 1.0f / (float)wcell;
+    uint32_t* const out = cand + ((size_t)f * ncells + G.ci0) * cell_cap;
     typedef short s16x2 __attribute__((ext_vector_type(2)));
-    int count = 0;
-    for (int attempt = 0; attempt < 2; attempt++) {
-        const int th = attempt == 0 ? ini_th : min_th;
+    for (int pass = 0; pass < 2; pass++) {
+        const int th = pass == 0 ? ini_th : min_th;
         const int thc = th < 0 ? 0 : (th > 255 ? 255 : th);
-        for (int w = lane; w < (rows * RS4 + 3) >> 2; w += 64) reinterpret_cast<uint4*>(score32)[w] = uint4{0, 0, 0, 0};
-        fast_wave_sync();
-        for (int part = 0; part < FAST_PARTS; part++) {
-        // detection rows [ra, rb) are output by this part; the compass also
-        // covers row rb (scored for the NMS of row rb - 1) except in the last
-        const int ra = FAST_PARTS == 1 ? 0 : part * drows / FAST_PARTS;
-        const int rb = FAST_PARTS == 1 ? drows : (part + 1) * drows / FAST_PARTS;
-        const int rc = FAST_PARTS == 1 ? drows : min(rb + 1, drows);
-        const int ia = drows > 0 ? ra * nq : 0, ib = drows > 0 ? rc * nq : 0;
-        // 1. compass pre-filter, 4 pixels per lane in 16-bit pairs: dark_k iff
-        //    a_k - (v - th) < 0, bright_k iff (v + th) - a_k < 0 (sign bits)
-        int n1 = 0;
-        const s16x2 thv = {(short)thc, (short)thc};
-        int qii = nq > 0 ? (ia + lane) / nq : 0, qmm = nq > 0 ? ia + lane - qii * nq : 0;  // item as (row, quad)
-        for (int base = ia; base < ib; base += 64) {
-            const int it = base + lane;
-            uint32_t pass4 = 0;  // bit i: pixel 4m+i survives
-            const int ii = qii, mq = qmm;
-            qii += qdq;
-            qmm += qdr;
-            if (qmm >= nq) qmm -= nq, qii++;
-            const int m = m0 + mq;
-            // ROI byte offset of the quad (24-bit multiply: v_mul_u32_u24, not v_mul_lo_u32)
-            const int qoff = (int)__umul24((uint32_t)(3 + ii), (uint32_t)RS) + 4 * m;
-            if (it < ib) {
-                const uint32_t* w = roi32 + (qoff >> 2);
-                const uint32_t Cw = w[0], Uw = w[-3 * RS4], Dw = w[3 * RS4];
-                const uint32_t Lw = __builtin_amdgcn_alignbyte(Cw, w[-1], 1);
-                const uint32_t Rw = __builtin_amdgcn_alignbyte(w[1], Cw, 3);
+        const int NL = pass == 0 ? m1 - m0 + 1 : M.nl;  // quads per detection row
+        const int items = drows > 0 && cols > 6 && NL > 0 ? drows * NL : 0;
+        // ---- 1 + 2: compass, ring, segment test
+        {
+            const s16x2 thv = {(short)thc, (short)thc};
+            // item = (detection row ii, quad kk): stepped by FS_TH without divisions
+            const int it0 = wave * 64 + lane;
+            int ii = NL > 0 ? it0 / NL : 0, kk = NL > 0 ? it0 - ii * NL : 0;
+            const int dq = NL > 0 ? FS_TH / NL : 0, dr = NL > 0 ? FS_TH - dq * NL : 0;
+            int head = 0, tail = 0;
+            // segment test + cornerScore of ring entries [h, h + n), two per lane
+            auto seg_test = [&](int h, int n) {
+                const int i0 = 2 * lane, i1 = i0 + 1;
+                bool c0 = false, c1 = false;
+                int o0 = 0, o1 = 0;
+                if (i0 < n) {
+                    o0 = ring[(h + i0) & (FS_RING - 1)];
+                    o1 = i1 < n ? ring[(h + i1) & (FS_RING - 1)] : o0;
+                    const s16x2 vv = {(short)roi[o0], (short)roi[o1]};
+                    s16x2 d[16];
 #pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    const uint32_t sel = h ? 0x0c030c02u : 0x0c010c00u;
-                    s16x2 v, a0, a4, a8, a12;
-                    *reinterpret_cast<uint32_t*>(&v) = __builtin_amdgcn_perm(0u, Cw, sel);
-                    *reinterpret_cast<uint32_t*>(&a0) = __builtin_amdgcn_perm(0u, Dw, sel);   // circle 0: +3 rows
-                    *reinterpret_cast<uint32_t*>(&a4) = __builtin_amdgcn_perm(0u, Rw, sel);   // circle 4: +3 cols
-                    *reinterpret_cast<uint32_t*>(&a8) = __builtin_amdgcn_perm(0u, Uw, sel);   // circle 8: -3 rows
-                    *reinterpret_cast<uint32_t*>(&a12) = __builtin_amdgcn_perm(0u, Lw, sel);  // circle 12: -3 cols
-                    // two adjacent compass points below v - th: (a0|a8 dark) and
-                    // (a4|a12 dark) = max(min(a0, a8), min(a4, a12)) < v - th;
-                    // bright: min(max(a0, a8), max(a4, a12)) > v + th (sign bits of
-                    // the i16 differences; every value fits in [-255, 510])
-                    const s16x2 dk = __builtin_elementwise_max(__builtin_elementwise_min(a0, a8),
-                                                               __builtin_elementwise_min(a4, a12));
-                    const s16x2 bk = __builtin_elementwise_min(__builtin_elementwise_max(a0, a8),
-                                                               __builtin_elementwise_max(a4, a12));
-                    const s16x2 t1 = dk - (v - thv), t2 = (v + thv) - bk;
-                    const uint32_t pm =
-                        (*reinterpret_cast<const uint32_t*>(&t1) | *reinterpret_cast<const uint32_t*>(&t2)) & 0x80008000u;
-                    pass4 |= ((pm >> 15) & 1u) << (2 * h);
-                    pass4 |= (pm >> 31) << (2 * h + 1);
+                    for (int k = 0; k < 16; k++) {
+                        const int off = c_circle_dy[k] * RS + c_circle_dx[k];
+                        s16x2 c;
+                        c.x = (short)roi[o0 + off];
+                        c.y = (short)roi[o1 + off];
+                        d[k] = vv - c;
+                    }
+                    // best 9-arc min / max: arcs k, k+1 (k even) share the run
+                    // d[k+1 .. k+8] (odd 2-, 4-, 8-runs)
+                    s16x2 mn2[8], mx2[8], mn4[8], mx4[8];
+#pragma unroll
+                    for (int q = 0; q < 8; q++) {
+                        const int j = 2 * q + 1;
+                        mn2[q] = __builtin_elementwise_min(d[j], d[(j + 1) & 15]);
+                        mx2[q] = __builtin_elementwise_max(d[j], d[(j + 1) & 15]);
+                    }
+#pragma unroll
+                    for (int q = 0; q < 8; q++) {
+                        mn4[q] = __builtin_elementwise_min(mn2[q], mn2[(q + 1) & 7]);
+                        mx4[q] = __builtin_elementwise_max(mx2[q], mx2[(q + 1) & 7]);
+                    }
+                    s16x2 dk = s16x2{-32768, -32768}, br = s16x2{32767, 32767};
+#pragma unroll
+                    for (int q = 0; q < 8; q++) {
+                        const int k = 2 * q;
+                        const s16x2 m8 = __builtin_elementwise_min(mn4[q], mn4[(q + 2) & 7]);
+                        const s16x2 x8 = __builtin_elementwise_max(mx4[q], mx4[(q + 2) & 7]);
+                        dk = __builtin_elementwise_max(
+                            dk, __builtin_elementwise_min(m8, __builtin_elementwise_max(d[k], d[(k + 9) & 15])));
+                        br = __builtin_elementwise_min(
+                            br, __builtin_elementwise_max(x8, __builtin_elementwise_min(d[k], d[(k + 9) & 15])));
+                    }
+                    const s16x2 sc = __builtin_elementwise_max(dk, -br);
+                    c0 = sc.x > thc;
+                    c1 = i1 < n && sc.y > thc;
+                    if (c0) score[o0] = (uint8_t)(sc.x - 1);
+                    if (c1) score[o1] = (uint8_t)(sc.y - 1);
                 }
-                // keep detection bytes only: the quad's mask from the per-cell table
-                if (ROI_MAX <= 60) {
-                    pass4 &= (uint32_t)(qmask >> (4 * mq)) & 0xFu;
-                } else {
-                    const int lo = sh + 3 - 4 * m, hi = sh + cols - 3 - 4 * m;  // valid i in [lo, hi)
-                    pass4 &= (lo <= 0 ? 0xFu : (0xFu << lo) & 0xFu) & (hi >= 4 ? 0xFu : ((1u << hi) - 1u));
+                const uint64_t b0 = __ballot(c0), b1 = __ballot(c1);
+                const int nco = __popcll(b0) + __popcll(b1);
+                if (nco) {
+                    int cb = 0;
+                    if (lane == 0) cb = atomicAdd(&M.ncl, nco);
+                    cb = __shfl(cb, 0);
+                    const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b0, 0)) +
+                                    (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b1, 0));
+                    const int p0 = cb + pre, p1 = p0 + (c0 ? 1 : 0);
+                    if (c0) { if (p0 < FS_CL) clist[p0] = (uint16_t)o0; else M.ovf = 1; }
+                    if (c1) { if (p1 < FS_CL) clist[p1] = (uint16_t)o1; else M.ovf = 1; }
+                }
+            };
+            for (int base = wave * 64; base < items; base += FS_TH) {
+                uint32_t pass4 = 0;  // bit i: pixel 4m+i survives
+                int qoff = 0;
+                if (base + lane < items) {
+                    int m;
+                    uint32_t msk;
+                    if (pass == 0) {
+                        m = m0 + kk;
+                        msk = (kk == 0 ? mlo : 0xFu) & (m == m1 ? mhi : 0xFu);
+                    } else {
+                        const uint32_t e = qlist[kk];
+                        m = (int)(e & 0xFFFFu);
+                        msk = e >> 16;
+                    }
+                    qoff = (int)__umul24((uint32_t)(3 + ii), (uint32_t)RS) + 4 * m;
+                    const uint32_t* w = roi32 + (qoff >> 2);
+                    const uint32_t Cw = w[0], Uw = w[-3 * RS4], Dw = w[3 * RS4];
+                    const uint32_t Lw = __builtin_amdgcn_alignbyte(Cw, w[-1], 1);
+                    const uint32_t Rw = __builtin_amdgcn_alignbyte(w[1], Cw, 3);
+#pragma unroll
+                    for (int hh = 0; hh < 2; hh++) {
+                        const uint32_t sel = hh ? 0x0c030c02u : 0x0c010c00u;
+                        s16x2 v, a0, a4, a8, a12;
+                        *reinterpret_cast<uint32_t*>(&v) = __builtin_amdgcn_perm(0u, Cw, sel);
+                        *reinterpret_cast<uint32_t*>(&a0) = __builtin_amdgcn_perm(0u, Dw, sel);   // circle 0: +3 rows
+                        *reinterpret_cast<uint32_t*>(&a4) = __builtin_amdgcn_perm(0u, Rw, sel);   // circle 4: +3 cols
+                        *reinterpret_cast<uint32_t*>(&a8) = __builtin_amdgcn_perm(0u, Uw, sel);   // circle 8: -3 rows
+                        *reinterpret_cast<uint32_t*>(&a12) = __builtin_amdgcn_perm(0u, Lw, sel);  // circle 12: -3 cols
+                        // two adjacent compass points darker than v - th:
+                        // max(min(a0, a8), min(a4, a12)) < v - th; brighter:
+                        // min(max(a0, a8), max(a4, a12)) > v + th (sign bits)
+                        const s16x2 dk = __builtin_elementwise_max(__builtin_elementwise_min(a0, a8),
+                                                                   __builtin_elementwise_min(a4, a12));
+                        const s16x2 bk = __builtin_elementwise_min(__builtin_elementwise_max(a0, a8),
+                                                                   __builtin_elementwise_max(a4, a12));
+                        const s16x2 t1 = dk - (v - thv), t2 = (v + thv) - bk;
+                        const uint32_t pm =
+                            (*reinterpret_cast<const uint32_t*>(&t1) | *reinterpret_cast<const uint32_t*>(&t2)) & 0x80008000u;
+                        pass4 |= ((pm >> 15) & 1u) << (2 * hh);
+                        pass4 |= (pm >> 31) << (2 * hh + 1);
+                    }
+                    pass4 &= msk;
+                }
+                ii += dq;
+                kk += dr;
+                if (kk >= NL) kk -= NL, ii++;
+                // append to the ring (any order): this lane's survivors after
+                // the counts of the lanes below (three ballots of the count's bits)
+                const uint32_t c = (uint32_t)__builtin_popcount(pass4);
+                const uint64_t B0 = __ballot(c & 1u), B1 = __ballot(c & 2u), B2 = __ballot(c & 4u);
+                int pos = tail + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(B0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)B0, 0)) +
+                          2 * (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(B1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)B1, 0)) +
+                          4 * (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(B2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)B2, 0));
+                uint32_t pm4 = pass4;
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    if (pm4) {
+                        ring[pos & (FS_RING - 1)] = (uint16_t)(qoff + __builtin_ctz(pm4));
+                        pos++;
+                        pm4 &= pm4 - 1u;
+                    }
+                tail += __popcll(B0) + 2 * __popcll(B1) + 4 * __popcll(B2);
+                if (tail - head >= 128) {
+                    wave_lds_sync();
+                    do {
+                        seg_test(head, 128);
+                        head += 128;
+                    } while (tail - head >= 128);
+                    wave_lds_sync();
                 }
             }
-            // ordered compaction (lane order, then pixel order within the lane):
-            // this lane's survivors start after the counts of the lanes below,
-            // summed from three ballots of the count's bits
-            const uint32_t c = (uint32_t)__builtin_popcount(pass4);
-            const uint64_t B0 = __ballot(c & 1u), B1 = __ballot(c & 2u), B2 = __ballot(c & 4u);
-            int pos = n1 + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(B0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)B0, 0)) +
-                      2 * (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(B1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)B1, 0)) +
-                      4 * (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(B2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)B2, 0));
-            uint32_t pm4 = pass4;
-#pragma unroll
-            for (int k = 0; k < 4; k++)
-                if (pm4) {
-                    q1[pos++] = (uint16_t)(qoff + __builtin_ctz(pm4));
-                    pm4 &= pm4 - 1u;
-                }
-            n1 += __popcll(B0) + 2 * __popcll(B1) + 4 * __popcll(B2);
+            if (tail > head) {
+                wave_lds_sync();
+                seg_test(head, tail - head);
+            }
         }
-        fast_wave_sync();
-        // 2. segment test + cornerScore<16> of the survivors, two per lane in
-        //    packed 16-bit lanes: d = v - p, S = max(best 9-arc min of d,
-        //    -(best 9-arc max)). p is a corner at th iff S > th (a 9-arc whose
-        //    every d lies beyond th), and its cornerScore is max(th, S) - 1 =
-        //    S - 1 (the segment test and the score were two passes until round 2).
-        //    Corners listed in order, in place over the survivor queue (every
-        //    lane reads its two entries before any lane writes).
-        int n2 = 0;
-        for (int base = 0; base < n1; base += 128) {
-            const int i0 = base + 2 * lane, i1 = i0 + 1;
-            bool c0 = false, c1 = false;
-            int o0 = 0, o1 = 0;
-            if (i0 < n1) {
-                o0 = q1[i0];
-                o1 = i1 < n1 ? q1[i1] : o0;
-                const int v0 = roi[o0], v1 = roi[o1];
-                const s16x2 vv = {(short)v0, (short)v1};
-                s16x2 d[16];
-#pragma unroll
-                for (int k = 0; k < 16; k++) {
-                    // the two circle bytes straight into the halves of one
-                    // register (ds_read_u8_d16 / _d16_hi), one packed subtract
-                    const int off = c_circle_dy[k] * RS + c_circle_dx[k];
-                    s16x2 c;
-                    c.x = (short)roi[o0 + off];
-                    c.y = (short)roi[o1 + off];
-                    d[k] = vv - c;
-                }
-                // best 9-arc min / max: arcs k, k+1 (k even) share the run
-                // d[k+1 .. k+8] (odd 2-, 4-, 8-runs; the smap4 lattice form)
-                s16x2 mn2[8], mx2[8], mn4[8], mx4[8];
-#pragma unroll
-                for (int i = 0; i < 8; i++) {
-                    const int j = 2 * i + 1;
-                    mn2[i] = __builtin_elementwise_min(d[j], d[(j + 1) & 15]);
-                    mx2[i] = __builtin_elementwise_max(d[j], d[(j + 1) & 15]);
-                }
-#pragma unroll
-                for (int i = 0; i < 8; i++) {
-                    mn4[i] = __builtin_elementwise_min(mn2[i], mn2[(i + 1) & 7]);
-                    mx4[i] = __builtin_elementwise_max(mx2[i], mx2[(i + 1) & 7]);
-                }
-                s16x2 dk = s16x2{-32768, -32768}, br = s16x2{32767, 32767};
-#pragma unroll
-                for (int i = 0; i < 8; i++) {
-                    const int k = 2 * i;
-                    const s16x2 m8 = __builtin_elementwise_min(mn4[i], mn4[(i + 2) & 7]);
-                    const s16x2 x8 = __builtin_elementwise_max(mx4[i], mx4[(i + 2) & 7]);
-                    dk = __builtin_elementwise_max(
-                        dk, __builtin_elementwise_min(m8, __builtin_elementwise_max(d[k], d[(k + 9) & 15])));
-                    br = __builtin_elementwise_min(
-                        br, __builtin_elementwise_max(x8, __builtin_elementwise_min(d[k], d[(k + 9) & 15])));
-                }
-                const s16x2 sc = __builtin_elementwise_max(dk, -br);
-                c0 = sc.x > thc;
-                c1 = i1 < n1 && sc.y > thc;
-                if (c0) score[o0] = (uint8_t)(sc.x - 1);
-                if (c1) score[o1] = (uint8_t)(sc.y - 1);
-            }
-            const uint64_t b0 = __ballot(c0), b1 = __ballot(c1);
-            const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b0, 0)) +
-                            (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b1, 0));
-            if (c0) q2[n2 + pre] = (uint16_t)o0;
-            if (c1) q2[n2 + pre + (c0 ? 1 : 0)] = (uint16_t)o1;
-            n2 += __popcll(b0) + __popcll(b1);
-        }
-        fast_wave_sync();
-        // 3. NMS over the corner list (row-major), ordered compaction; the
-        //    corners of row rb (scored for this part's last row) wait for the
-        //    next part
-        for (int base = 0; base < n2; base += 64) {
-            const int idx = base + lane;
-            bool keep = false;
-            uint32_t packed = 0;
-            if (idx < n2) {
-                const int o = q2[idx];
-                const int sc = score[o];
-                const int i = o / RS, j = o - i * RS - sh;
-                keep = (FAST_PARTS == 1 || i < 3 + rb) && sc > score[o - RS - 1] && sc > score[o - RS] &&
-                       sc > score[o - RS + 1] && sc > score[o - 1] && sc > score[o + 1] && sc > score[o + RS - 1] &&
-                       sc > score[o + RS] && sc > score[o + RS + 1];
-                packed = ((uint32_t)sc << 24) | ((uint32_t)(i + C.offy) << 12) | (uint32_t)(j + C.offx);
-            }
-            const uint64_t m = __ballot(keep);
+        __syncthreads();
+        // ---- 3: NMS of this pass's corners (the list, or the score map over
+        //         the pass's quads when the list overflowed)
+        const bool ovf = M.ovf != 0;
+        const int ncl = min(M.ncl, FS_CL);
+        // corner at ROI byte offset o -> (row, segment x, cell) and its cell's
+        // detection columns [xl, xh) in segment x
+        auto locate = [&](int o, int& r, int& xs, int& jl, int& xl, int& xh) {
+            r = (int)(((float)o + 0.5f) * inv_rs);
+            xs = o - r * RS - sh;
+            jl = (int)(((float)(xs - 3) + 0.5f) * inv_w);
+            xl = 3 + jl * wcell;
+            xh = min(xl + wcell, cols - 3);
+        };
+        auto nms = [&](int o) {
+            const int sc = score[o];
+            int r, xs, jl, xl, xh;
+            locate(o, r, xs, jl, xl, xh);
+            bool keep = sc > score[o - RS] && sc > score[o + RS];
+            if (xs - 1 >= xl) keep = keep && sc > score[o - RS - 1] && sc > score[o - 1] && sc > score[o + RS - 1];
+            if (xs + 1 < xh) keep = keep && sc > score[o - RS + 1] && sc > score[o + 1] && sc > score[o + RS + 1];
             if (keep) {
-                const int pos = count + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-                if (pos < cell_cap) out[pos] = packed;
+                atomicOr(&bits[r * BW + (xs >> 5)], 1u << (xs & 31));
+                atomicAdd(&cnt[r * FS_NCM + jl], 1);
             }
-            count += __popcll(m);
+        };
+        // the pass's quads as (row, quad) items, for the overflow scans
+        auto scan = [&](auto&& fn) {
+            for (int it = t; it < items; it += FS_TH) {
+                const int ii2 = it / NL, kk2 = it - ii2 * NL;
+                int m;
+                uint32_t msk;
+                if (pass == 0) {
+                    m = m0 + kk2;
+                    msk = (kk2 == 0 ? mlo : 0xFu) & (m == m1 ? mhi : 0xFu);
+                } else {
+                    const uint32_t e = qlist[kk2];
+                    m = (int)(e & 0xFFFFu);
+                    msk = e >> 16;
+                }
+                const int qo = (3 + ii2) * RS + 4 * m;
+                for (int b = 0; b < 4; b++)
+                    if (((msk >> b) & 1u) && score[qo + b]) fn(qo + b);
+            }
+        };
+        if (!ovf)
+            for (int i = t; i < ncl; i += FS_TH) nms(clist[i]);
+        else
+            scan(nms);
+        __syncthreads();
+        // ---- 4: per cell, exclusive scan of the kept counts over the rows:
+        //         wave w takes cells w, w + 4, ..., a lane per detection row
+        //         (drows <= 64: the host checks rows <= 70)
+        for (int j = wave; j < nc; j += FS_TH / 64) {
+            if (pass == 1 && !M.retry[j]) continue;  // uniform per wave
+            const int r = 3 + lane;
+            const int v = lane < drows ? cnt[r * FS_NCM + j] : 0;
+            int incl = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int y = __shfl_up(incl, o);
+                if (lane >= o) incl += y;
+            }
+            if (lane < drows) cnt[r * FS_NCM + j] = incl - v;
+            if (lane == 63) M.tot[j] = incl;
         }
-        if (FAST_PARTS > 1) fast_wave_sync();  // the queue is refilled by the next part
-        }  // part
-        if (count > 0) break;
-        fast_wave_sync();
+        __syncthreads();
+        auto place = [&](int o) {
+            int r, xs, jl, xl, xh;
+            locate(o, r, xs, jl, xl, xh);
+            const uint32_t* row = bits + r * BW;
+            if (!((row[xs >> 5] >> (xs & 31)) & 1u)) return;
+            int rank = cnt[r * FS_NCM + jl];
+            const int wl = xl >> 5, wx = xs >> 5;
+            for (int w = wl; w <= wx; w++) {
+                uint32_t v = row[w];
+                if (w == wl) v &= ~0u << (xl & 31);
+                if (w == wx) v &= (1u << (xs & 31)) - 1u;
+                rank += __builtin_popcount(v);
+            }
+            if (rank < cell_cap)
+                out[(size_t)jl * cell_cap + rank] = ((uint32_t)score[o] << 24) |
+                                                    ((uint32_t)(r + G.y0 - 16) << 12) | (uint32_t)(xs + G.x0 - 16);
+        };
+        if (!ovf)
+            for (int i = t; i < ncl; i += FS_TH) place(clist[i]);
+        else
+            scan(place);
+        // ---- cells that kept nothing: their quads, for the minThFAST pass
+        if (pass == 0) {
+            if (t < nc) M.retry[t] = M.tot[t] == 0;
+            __syncthreads();
+            if (t < nc) {
+                const int xa = sh + 3 + t * wcell, xe = sh + min(3 + (t + 1) * wcell, cols - 3);
+                if (M.retry[t]) {
+                    int at = 0;  // entries of the retry cells before this one
+                    for (int j = 0; j < t; j++)
+                        if (M.retry[j]) {
+                            const int ja = sh + 3 + j * wcell, je = sh + min(3 + (j + 1) * wcell, cols - 3);
+                            at += ((je - 1) >> 2) - (ja >> 2) + 1;
+                        }
+                    for (int m = xa >> 2; m <= (xe - 1) >> 2; m++) {
+                        const int lo = max(xa - 4 * m, 0), hi = min(xe - 4 * m, 4);
+                        qlist[at++] = (uint32_t)m | (((0xFu << lo) & ((1u << hi) - 1u)) << 16);
+                    }
+                } else {
+                    cand_cnt[(size_t)f * ncells + G.ci0 + t] = min(M.tot[t], cell_cap);
+                }
+            }
+            if (t == 0) {
+                int n = 0;
+                for (int j = 0; j < nc; j++)
+                    if (M.retry[j]) {
+                        const int ja = sh + 3 + j * wcell, je = sh + min(3 + (j + 1) * wcell, cols - 3);
+                        n += ((je - 1) >> 2) - (ja >> 2) + 1;
+                    }
+                M.nl = n;
+                M.ncl = 0;
+                M.ovf = 0;
+            }
+            __syncthreads();
+            if (M.nl == 0) return;  // uniform: no cell to retry
+        } else if (t < nc && M.retry[t]) {
+            cand_cnt[(size_t)f * ncells + G.ci0 + t] = min(M.tot[t], cell_cap);
+        }
     }
-    if (lane == 0) cand_cnt[(size_t)f * ncells + ci] = count < cell_cap ? count : cell_cap;
 }
 
 // ============================================================ octree
@@ -1592,26 +1676,36 @@ void launch_resize(hipStream_t st, uint8_t* pyr, size_t pyr_stride, int src_off,
     hipLaunchKernelGGL(k_resize, g, dim3(256), lds, st, pyr, pyr_stride, src_off, spitch, dst_off, dpitch, dw, dh, rb,
                        xt, yt);
 }
-void launch_fast(hipStream_t st, const uint8_t* pyr, size_t pyr_stride, const CellDesc* cells, const LevelDesc* lv,
-                 uint32_t* cand, int* cand_cnt, int ncells, int cell_cap, int ini_th, int min_th, int roi_max,
-                 int nframes) {
-    // LDS sized for the largest cell ROI of the context: the kernel is
-    // occupancy-bound (one wave per workgroup), 7.5 KB at 44 px vs 8.9 KB at 48
-    // (20 KB at 72, only for small images)
-    dim3 g((ncells + FAST_CPW - 1) / FAST_CPW, nframes);
-    const dim3 blk(64 * FAST_CPW);
-    if (roi_max <= 40)
-        hipLaunchKernelGGL(k_fast_cells<40>, g, blk, 0, st, pyr, pyr_stride, cells, lv, cand, cand_cnt, ncells,
-                           cell_cap, ini_th, min_th);
-    else if (roi_max <= 44)
-        hipLaunchKernelGGL(k_fast_cells<44>, g, blk, 0, st, pyr, pyr_stride, cells, lv, cand, cand_cnt, ncells,
-                           cell_cap, ini_th, min_th);
-    else if (roi_max <= 48)
-        hipLaunchKernelGGL(k_fast_cells<48>, g, blk, 0, st, pyr, pyr_stride, cells, lv, cand, cand_cnt, ncells,
-                           cell_cap, ini_th, min_th);
-    else  // small images: levels narrower than two 30-px cells
-        hipLaunchKernelGGL(k_fast_cells<FAST_ROI_MAX>, g, blk, 0, st, pyr, pyr_stride, cells, lv, cand, cand_cnt,
-                           ncells, cell_cap, ini_th, min_th);
+bool fast_lds_plan(const FastSeg* segs, int nsegs, FastLds& L) {
+    int img = 16, bw = 1, rows = 1, nl = 1;
+    for (int k = 0; k < nsegs; k++) {
+        img = std::max(img, (int)segs[k].rows * (int)segs[k].rs);
+        bw = std::max(bw, (int)segs[k].rows * (int)segs[k].bw);
+        rows = std::max(rows, (int)segs[k].rows);
+        nl = std::max(nl, (int)segs[k].rs / 4 + FS_NCM);
+        if ((int)segs[k].ncell > FS_NCM || (int)segs[k].rows * (int)segs[k].rs > 65536) return false;
+    }
+    auto al = [](int x) { return (x + 15) & ~15; };
+    L.img = al(img);
+    L.ring = 2 * L.img;
+    L.clist = L.ring + 4 * FS_RING * 2;
+    L.bits = al(L.clist + FS_CL * 2);
+    L.cnt = al(L.bits + bw * 4);
+    L.qlist = al(L.cnt + rows * FS_NCM * 4);
+    L.misc = al(L.qlist + nl * 4);
+    L.total = al(L.misc + (int)sizeof(FastMisc));
+    return L.total <= 160 * 1024;
+}
+void launch_fast(hipStream_t st, const uint8_t* pyr, size_t pyr_stride, const FastSeg* segs, int nsegs,
+                 const LevelDesc* lv, uint32_t* cand, int* cand_cnt, int ncells, int cell_cap, int ini_th, int min_th,
+                 const FastLds& lds, int nframes) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_fast_seg, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_fast_seg, dim3(nsegs, nframes), dim3(FS_TH), lds.total, st, pyr, pyr_stride, segs, lv, cand,
+                       cand_cnt, ncells, cell_cap, ini_th, min_th, lds);
 }
 size_t octree_lds_bytes(int node_cap) { return (size_t)76 * node_cap + 1032; }
 void launch_octree(hipStream_t st, const uint32_t* cand, const int* cand_cnt, const LevelDesc* lv, int ncells,

@@ -223,7 +223,14 @@ __global__ void __launch_bounds__(256, FIN_WAVES_PER_EU) k_finalize(const uint8_
 #ifndef FIN_OVERLAY
 #define FIN_OVERLAY 1
 #endif
-#define FL_KP_DW (FIN_OVERLAY ? FL_BR_N : FL_IC_N + FL_BR_N)  // dwords of LDS per keypoint
+// dwords of LDS per keypoint, padded to 16 mod 32 (round 5): a wave's lanes
+// 0-31 are two keypoints whose IC rows sit 9 dwords apart ({9s mod 32} for
+// the 16 lanes: half the banks); the second keypoint 16 banks further takes
+// exactly the other half ({16 + 9s}), where the unpadded 370 (18 mod 32)
+// shared 14 of 16 banks with the first (PMC: 35.7 M conflict cycles, 1.4x
+// the kernel's LDS cycles, round 4)
+#define FL_KP_RAW (FIN_OVERLAY ? FL_BR_N : FL_IC_N + FL_BR_N)
+#define FL_KP_DW (((FL_KP_RAW + 15) / 32) * 32 + 16)
 #define FL_BR_AT (FIN_OVERLAY ? 0 : FL_IC_N)                  // first dword of the rBRIEF window
 template <int NW>  // waves (of 4 keypoints) per workgroup
 __global__ void __launch_bounds__(64 * NW) k_finalize_lds(const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
@@ -236,7 +243,9 @@ __global__ void __launch_bounds__(64 * NW) k_finalize_lds(const uint8_t* __restr
     __builtin_amdgcn_s_setprio(ODO_FINALIZE_PRIO);  // tuning: finalize's load chains ahead of co-runners
 #endif
     __shared__ uint64_t s_bal[NW][16];
-    __shared__ __attribute__((aligned(16))) uint32_t s_disc[16][8];
+    // disc masks, rows padded to 12 dwords: the 16 lanes of a ds_read_b128
+    // group read 16 different rows, which at 8 dwords met on 2 banks each
+    __shared__ __attribute__((aligned(16))) uint32_t s_disc[16][12];
     __shared__ __attribute__((aligned(16))) uint32_t s_patch[NW * FIN_KPW][FL_KP_DW];
     for (int d = threadIdx.x; d < 128; d += 64 * NW) {
         const int av = d >> 3, i = d & 7;

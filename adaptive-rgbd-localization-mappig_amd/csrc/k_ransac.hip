@@ -46,8 +46,16 @@ struct GoodPt {
 #ifndef EV_MARKSTEIN
 #define EV_MARKSTEIN 1  // eval kernels' sweep: Markstein-corrected quotients (error_function2_mk)
 #endif
-#ifndef EV_ROWS0
-#define EV_ROWS0 1  // 4 hypotheses per pair in the first launch (most pairs break at the first); 75.7k vs 74.8k at 2
+#ifndef EV2_FOLD_WAVE
+#define EV2_FOLD_WAVE 1  // the second launch's ordered fold by the whole wave (0: lane 0)
+#endif
+#ifndef EV_H0
+// hypotheses per pair in the first eval launch of a batch (round 5: 2; a row
+// of 4 until round 4). In the bench's sequence 52 of 64 pairs break at
+// hypothesis 0 and 10 at hypothesis 1 (oracle, the 80 % break of
+// ransac.cpp:247), so the 2 further waves of a row of 4 ran for nothing
+// beside the extraction kernels
+#define EV_H0 2
 #endif
 #define MAX_SAMPLE 8
 #define SREC (MAX_SAMPLE + 2)  // sample record: count, ids[MAX_SAMPLE], end (draw pairs consumed after it)
@@ -560,7 +568,7 @@ __global__ void __launch_bounds__(256) k_ransac_prep(RansacBufs B, RansacCfg cfg
         S->rmse = 1e6f;
         S->sweeps = 0;
         S->fitpts = 0;
-        S->nexth = cfg.rows0 * EV_WAVES_C;  // the first eval launch covers [0, rows0 * EV_WAVES)
+        S->nexth = cfg.h0;  // the first eval launch covers [0, h0)
     }
     if (done) return;
     __shared__ SampWin s_win;
@@ -939,7 +947,8 @@ ODO_INLINE void try_fold_wave(const RansacBufs& B, const RansacCfg& cfg, int p, 
 
 template <bool CACHED>
 ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int wave, int lane, EvalLds& L,
-                          const GoodPt* P, int ng, int words, int H, int y0, int hlim, int yrow, int ystride) {
+                          const GoodPt* P, int ng, int words, int H, int hofs, int y0, int hlim, int yrow,
+                          int ystride) {
     RState* S = B.st + p;
     const int* smp0 = B.samples + (size_t)p * B.hcap * SREC;
     const TfcSlab TS{reinterpret_cast<float*>(ev_dyn + PCACHE * sizeof(GoodPt)) + (size_t)wave * 8 * TFC_CAP};
@@ -949,10 +958,9 @@ ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int 
     K.depth_cov = *B.latch;
     const float th = cfg.max_mahal * cfg.max_mahal;
     const unsigned minInl = (unsigned)cfg.min_inlier_th;
-    // this launch covers hypothesis rows [y0, y0 + gridDim.y)
-    // this launch's waves stride over hypotheses [y0*EV_WAVES, hlim)
+    // this launch's waves stride over hypotheses [hofs + y0*EV_WAVES, hlim)
     const int hend = min(H, hlim);
-    for (int h = (y0 + yrow) * EV_WAVES + wave; h < hend; h += ystride * EV_WAVES) {
+    for (int h = hofs + (y0 + yrow) * EV_WAVES + wave; h < hend; h += ystride * EV_WAVES) {
         if (h < B.h_lo || h >= B.h_hi) continue;  // hypotheses mode: another rank's range
         const int* smp = smp0 + (size_t)h * SREC;
         double refinedError = 1e6;
@@ -1195,14 +1203,15 @@ ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int 
 #ifndef EV_MIN_BLOCKS
 #define EV_MIN_BLOCKS 2
 #endif
-__global__ void __launch_bounds__(64 * EV_WAVES, EV_MIN_BLOCKS) k_ransac_eval(RansacBufs B, RansacCfg cfg, int y0, int hlim) {
+__global__ void __launch_bounds__(64 * EV_WAVES, EV_MIN_BLOCKS) k_ransac_eval(RansacBufs B, RansacCfg cfg, int hofs, int y0,
+                                                                                  int hlim) {
     __builtin_amdgcn_s_setprio(ODO_WAVE_PRIO);  // latency-bound: issue ahead of co-resident extraction waves
     const int p = blockIdx.x;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     __shared__ EvalLds s_w[EV_WAVES];
     RState* S = B.st + p;
     const int H = S->H;
-    if ((y0 + (int)blockIdx.y) * EV_WAVES >= H) return;
+    if (hofs + (y0 + (int)blockIdx.y) * EV_WAVES >= min(H, hlim)) return;
     __shared__ int s_done;
     if (threadIdx.x == 0) s_done = ld_relaxed(&S->done);
     __syncthreads();
@@ -1211,11 +1220,11 @@ __global__ void __launch_bounds__(64 * EV_WAVES, EV_MIN_BLOCKS) k_ransac_eval(Ra
     const GoodPt* P = B.gpts + (size_t)p * B.match_cap;
     if (PCACHE > 0 && ng <= PCACHE) {
         GoodPt* pc = reinterpret_cast<GoodPt*>(ev_dyn);
-        for (int k = threadIdx.x; k < ng; k += 64 * EV_WAVES) pc[k] = P[k];
+        for (int k = threadIdx.x; k < ng; k += blockDim.x) pc[k] = P[k];
         __syncthreads();
-        eval_hyps<true>(B, cfg, p, wave, lane, s_w[wave], P, ng, words, H, y0, hlim, blockIdx.y, gridDim.y);
+        eval_hyps<true>(B, cfg, p, wave, lane, s_w[wave], P, ng, words, H, hofs, y0, hlim, blockIdx.y, gridDim.y);
     } else {
-        eval_hyps<false>(B, cfg, p, wave, lane, s_w[wave], P, ng, words, H, y0, hlim, blockIdx.y, gridDim.y);
+        eval_hyps<false>(B, cfg, p, wave, lane, s_w[wave], P, ng, words, H, hofs, y0, hlim, blockIdx.y, gridDim.y);
     }
 }
 
@@ -1252,7 +1261,7 @@ __global__ void __launch_bounds__(256) k_ransac_open(RansacBufs B, int npairs) {
 // pair) items in row-major order (lower hypotheses first) from an atomic
 // counter, 4 hypotheses per item - no launch-sized crowd of early-exit
 // workgroups for the pairs that already broke.
-__global__ void __launch_bounds__(64 * EV_WAVES, EV_MIN_BLOCKS) k_ransac_eval_list(RansacBufs B, RansacCfg cfg, int y0,
+__global__ void __launch_bounds__(64 * EV_WAVES, EV_MIN_BLOCKS) k_ransac_eval_list(RansacBufs B, RansacCfg cfg, int hofs,
                                                                                    int rows, int max_open) {
     __builtin_amdgcn_s_setprio(ODO_WAVE_PRIO);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1270,10 +1279,10 @@ __global__ void __launch_bounds__(64 * EV_WAVES, EV_MIN_BLOCKS) k_ransac_eval_li
         const int row = item / cnt, p = B.open_list[item - row * cnt];
         RState* S = B.st + p;
         const int H = S->H;
-        if ((y0 + row) * EV_WAVES >= H || ld_relaxed(&S->done)) continue;  // uniform per item
+        if (hofs + row * EV_WAVES >= H || ld_relaxed(&S->done)) continue;  // uniform per item
         const GoodPt* P = B.gpts + (size_t)p * B.match_cap;
-        eval_hyps<false>(B, cfg, p, wave, lane, s_w[wave], P, S->ng, S->words, H, y0 + row,
-                         (y0 + row + 1) * EV_WAVES, 0, 1);
+        eval_hyps<false>(B, cfg, p, wave, lane, s_w[wave], P, S->ng, S->words, H, hofs, row,
+                         hofs + (row + 1) * EV_WAVES, 0, 1);
     }
 }
 
@@ -1445,7 +1454,7 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
         }
         if (mine >= 0) {
             slot = mine;
-            const int rem = max(1, cfg.iterations - cfg.rows0 * EV_WAVES);
+            const int rem = max(1, cfg.iterations - cfg.h0);
             lane_lim = min(LN_SLOTS, (rem + wn - 1) / wn);
         }
     }
@@ -2452,7 +2461,7 @@ void launch_ransac(hipStream_t st, const void* good, const int* n_good, const in
                    uint32_t* best_mask, int mask_words, odo_pair_result* res, float* T12, int npairs, int part,
                    int* phase, int* open_hint) {
     ransac_eval_lds_attr();
-    cfg.rows0 = EV_ROWS0;
+    cfg.h0 = EV_H0;
     cfg.fold_wave = 0;
     RansacBufs B = carve(scratch, npairs, match_cap, mask_words, cfg);
     B.good = (const SortElR*)good;
@@ -2483,40 +2492,42 @@ void launch_ransac(hipStream_t st, const void* good, const int* n_good, const in
         if (B.h_hi > B.h_lo) {
             const int ya = B.h_lo / EV_WAVES, yb = (B.h_hi + EV_WAVES - 1) / EV_WAVES;
             hipLaunchKernelGGL(k_ransac_eval, dim3(npairs, yb - ya), dim3(64 * EV_WAVES), EV_LDS, st,
-                               B, cfg, ya, yb * EV_WAVES);
+                               B, cfg, 0, ya, yb * EV_WAVES);
         }
         return;
     }
-    // Two eval launches: the first EV_ROWS0 rows of hypotheses for every pair
-    // (the >80% break usually ends a pair within them), then the rest, which
-    // only pairs still folding take up — so the speculative hypotheses of
-    // finished pairs do not compete with the long ones. part 1 = prep, first
-    // launch and the finished pairs' outputs (phase[] marks them); part 2 = the
-    // rest; part 0 = both.
-    const int rows = (H + EV_WAVES - 1) / EV_WAVES;
-    // ODO_EV_ROWS0: rows of the first launch (default EV_ROWS0)
-    static const int rows0 = [] {
-        const char* e = odo_knob("ODO_EV_ROWS0");
-        return e ? std::max(1, atoi(e)) : EV_ROWS0;
+    // Two eval launches: the first h0 hypotheses of every pair (the >80% break
+    // usually ends a pair within them), then the rest, which only pairs still
+    // folding take up — so the speculative hypotheses of finished pairs do
+    // not compete with the long ones. part 1 = prep, first launch and the
+    // finished pairs' outputs (phase[] marks them); part 2 = the rest; part 0
+    // = both.
+    // ODO_EV_H0 (tuning): hypotheses of the first launch (default EV_H0)
+    static const int h0k = [] {
+        const char* e = odo_knob("ODO_EV_H0");
+        return e ? std::max(1, atoi(e)) : EV_H0;
     }();
     // a lone pair (the per-stage odo_ransac, a one-frame batch) starts every
     // hypothesis at once: the device is otherwise idle, and the visited
     // hypotheses beyond the first row no longer wait for the first launch
     // (the fold and the aborts make the result independent of the schedule)
-    const int r0 = npairs == 1 ? rows : std::min(rows, rows0);
-    cfg.rows0 = r0;
+    const int h0 = npairs == 1 ? H : std::min(H, h0k);
+    cfg.h0 = h0;
     cfg.fold_wave = npairs == 1;
     if (part != 2) {
         hipLaunchKernelGGL(k_ransac_prep, dim3(npairs), dim3(256), 0, st, B, cfg);
-        if (r0 > 0)
-            hipLaunchKernelGGL(k_ransac_eval, dim3(npairs, r0), dim3(64 * EV_WAVES), EV_LDS, st, B,
-                               cfg, 0, r0 * EV_WAVES);
+        if (h0 > 0) {
+            // rows of EV_WAVES hypotheses; a first launch of fewer runs that many waves
+            const int r0 = (h0 + EV_WAVES - 1) / EV_WAVES, nw = std::min(h0, EV_WAVES);
+            hipLaunchKernelGGL(k_ransac_eval, dim3(npairs, r0), dim3(64 * nw), EV_LDS, st, B, cfg, 0, 0, h0);
+        }
         if (part == 1) hipLaunchKernelGGL(k_ransac_final, dim3(npairs), dim3(64), 0, st, B, cfg, 1, phase);
     }
     if (part != 1) {
-        // the second launch's waves stride over the remaining hypotheses:
-        // ev2_rows() rows of EV_WAVES per pair in flight (ODO_EV2_ROWS)
-        if (rows > r0) {
+        // the second launch's waves stride over the remaining hypotheses
+        // [h0, H): ev2_rows() rows of EV_WAVES per pair in flight (ODO_EV2_ROWS)
+        const int rows = (H - h0 + EV_WAVES - 1) / EV_WAVES;
+        if (rows > 0) {
             if (ev2_list()) {
                 hipLaunchKernelGGL(k_ransac_open, dim3(1), dim3(256), 0, st, B, npairs);
                 // which of the two kernels takes the open pairs: decided on the
@@ -2529,21 +2540,28 @@ void launch_ransac(hipStream_t st, const void* good, const int* n_good, const in
                 const int tmin = cfg.lanes_min_open > 0 ? cfg.lanes_min_open : ln_min_open();
                 const int hint = open_hint ? *reinterpret_cast<volatile int*>(open_hint) : 0;
                 const bool use_lanes = lanes && open_hint && hint >= tmin;
+                // the pairs still open after the first launch are the long
+                // ones (the bench's sequence: 2 of 64, visiting 36 and 380
+                // hypotheses): the work list folds them with the whole wave
+                // (64 ready flags per load, try_fold_wave) instead of lane
+                // 0's serial coherent loads, ~0.4 us per visited hypothesis
+                RansacCfg cfg2 = cfg;
+                cfg2.fold_wave = EV2_FOLD_WAVE;
                 if (lanes && hint < 0) {
-                    hipLaunchKernelGGL(k_ransac_eval_list, dim3(ev2_list()), dim3(64 * EV_WAVES), EV_LDS, st, B, cfg,
-                                       r0, rows - r0, tmin - 1);
+                    hipLaunchKernelGGL(k_ransac_eval_list, dim3(ev2_list()), dim3(64 * EV_WAVES), EV_LDS, st, B, cfg2,
+                                       h0, rows, tmin - 1);
                     hipLaunchKernelGGL(k_ransac_lanes, dim3(lanes), dim3(64 * LN_WAVES), 0, st, B, cfg, B.lslab,
                                        lanes * LN_WAVES, tmin);
                 } else if (use_lanes)
                     hipLaunchKernelGGL(k_ransac_lanes, dim3(lanes), dim3(64 * LN_WAVES), 0, st, B, cfg, B.lslab,
                                        lanes * LN_WAVES, 1);
                 else
-                    hipLaunchKernelGGL(k_ransac_eval_list, dim3(ev2_list()), dim3(64 * EV_WAVES), EV_LDS, st, B, cfg,
-                                       r0, rows - r0, 1 << 30);
+                    hipLaunchKernelGGL(k_ransac_eval_list, dim3(ev2_list()), dim3(64 * EV_WAVES), EV_LDS, st, B, cfg2,
+                                       h0, rows, 1 << 30);
                 if (open_hint) (void)hipMemcpyAsync(open_hint, B.open_cnt, sizeof(int), hipMemcpyDeviceToHost, st);
             } else {
-                hipLaunchKernelGGL(k_ransac_eval, dim3(npairs, std::min(rows - r0, ev2_rows())), dim3(64 * EV_WAVES),
-                                   EV_LDS, st, B, cfg, r0, H);
+                hipLaunchKernelGGL(k_ransac_eval, dim3(npairs, std::min(rows, ev2_rows())), dim3(64 * EV_WAVES),
+                                   EV_LDS, st, B, cfg, h0, 0, H);
             }
         }
         hipLaunchKernelGGL(k_ransac_final, dim3(npairs), dim3(64), 0, st, B, cfg, part == 2 ? 2 : 0, phase);

@@ -164,7 +164,10 @@ struct odo_ctx {
     ResizeY* ry = nullptr;
     int ncells = 0, cell_cap = 0, kp_cap = 0, okp_stride = 0, node_cap = 0, match_cap = 0, mask_words = 0;
     int max_blur_tiles = 0;
-    int fast_roi = 0;  // largest FAST cell ROI side (sizes the kernel's LDS)
+    int fast_roi = 0;  // largest FAST cell ROI side
+    std::vector<FastSeg> fsegs_h;  // k_fast_seg's segments (cell-row runs)
+    FastSeg* fsegs = nullptr;
+    FastLds fs_lds{};
     size_t pyr_size = 0, keys_per_frame = 0;
     FrameCalib cal{};
     RansacCfg rcfg{};
@@ -397,7 +400,7 @@ static int sync_all(odo_ctx* c) {
 static void free_ctx(odo_ctx* c) {
     if (!c) return;
     free_hyp_session(c->hs);
-    void* ptrs[] = {c->lv, c->cells, c->rx, c->ry, c->pyr, c->blur, c->cand, c->cand_cnt, c->keys, c->knode, c->kquad,
+    void* ptrs[] = {c->lv, c->cells, c->fsegs, c->rx, c->ry, c->pyr, c->blur, c->cand, c->cand_cnt, c->keys, c->knode, c->kquad,
                     c->okp, c->ocnt, c->kps, c->desc, c->kun, c->xyz, c->ur, c->nkp, c->bgr_in[0], c->depth_in[0],
                     c->bgr_in[1], c->depth_in[1],
                     c->sort_scratch, c->latch, c->masks, c->adc, c->adb, c->smap, c->acand, c->abig, c->acell,
@@ -643,6 +646,7 @@ static int build_geometry(odo_ctx* c) {
     int off = 0, maxq = 0, max_nini = 1;
     size_t key_off = 0;
     c->cells_h.clear();
+    c->fsegs_h.clear();
     int max_tiles = 0;
     for (int l = 0; l < p.nlevels; l++) {
         LevelDesc& L = c->lv_h[l];
@@ -689,6 +693,41 @@ static int build_geometry(odo_ctx* c) {
             }
         }
         L.cell_end = (int)c->cells_h.size();
+        // FAST segments (k_fast_seg): each cell row's cells in runs of at most
+        // FS_SEGC, split evenly; the segment's ROI union is cells_h[ci0 ..
+        // ci0 + ncell) (pushed above in row-major order)
+        {
+            const int nct = L.cell_end - L.cell_begin;
+            int ncj = 0;  // cells per row (the skipped columns are the last ones)
+            for (int j = 0; j < nCols; j++)
+                if ((float)(minBorderX + j * wCell) < (float)(maxBorderX - 6)) ncj++;
+            if (ncj > 0 && nct % ncj == 0) {
+                const int nrow = nct / ncj, nseg = (ncj + FS_SEGC - 1) / FS_SEGC;
+                for (int ir = 0; ir < nrow; ir++)
+                    for (int sg = 0; sg < nseg; sg++) {
+                        const int ja = ncj * sg / nseg, jb = ncj * (sg + 1) / nseg;
+                        const CellDesc& A = c->cells_h[L.cell_begin + ir * ncj + ja];
+                        const CellDesc& B = c->cells_h[L.cell_begin + ir * ncj + jb - 1];
+                        FastSeg G{};
+                        G.level = l;
+                        G.ci0 = L.cell_begin + ir * ncj + ja;
+                        G.y0 = A.y0;
+                        G.rows = A.rows;
+                        G.x0 = A.x0;
+                        G.cols = (int16_t)(B.x0 + B.cols - A.x0);
+                        G.ncell = (int16_t)(jb - ja);
+                        G.wcell = (int16_t)wCell;
+                        const int nw = ((A.x0 & 15) + G.cols + 15) >> 4;
+                        G.rs = (int16_t)(16 * nw);
+                        G.bw = (int16_t)((G.cols + 31) >> 5);
+                        if (nw > 256 || G.ncell > FS_NCM || G.rows > 70 || (int)G.rows * G.rs > 65536)
+                            return fail(ODO_ERR_ARG, "FAST segment too large");
+                        c->fsegs_h.push_back(G);
+                    }
+            } else if (nct > 0) {
+                return fail(ODO_ERR_STATE, "FAST cells not a full grid");
+            }
+        }
         L.key_off = (int)key_off;
         const int nIni = (int)roundf((float)(maxBorderX - minBorderX) / (float)(maxBorderY - minBorderY));
         max_nini = std::max(max_nini, nIni);
@@ -810,6 +849,11 @@ static int build_geometry(odo_ctx* c) {
     if ((e = dalloc(&c->ry, ry.size()))) return e;
     HIPCHK(hipMemcpy(c->lv, c->lv_h.data(), c->lv_h.size() * sizeof(LevelDesc), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c->cells, c->cells_h.data(), c->cells_h.size() * sizeof(CellDesc), hipMemcpyHostToDevice));
+    if (!fast_lds_plan(c->fsegs_h.data(), (int)c->fsegs_h.size(), c->fs_lds))
+        return fail(ODO_ERR_ARG, "FAST segments exceed LDS");
+    if ((e = dalloc(&c->fsegs, std::max<size_t>(c->fsegs_h.size(), 1)))) return e;
+    if (!c->fsegs_h.empty())
+        HIPCHK(hipMemcpy(c->fsegs, c->fsegs_h.data(), c->fsegs_h.size() * sizeof(FastSeg), hipMemcpyHostToDevice));
     if (!rx.empty()) HIPCHK(hipMemcpy(c->rx, rx.data(), rx.size() * sizeof(ResizeX), hipMemcpyHostToDevice));
     if (!ry.empty()) HIPCHK(hipMemcpy(c->ry, ry.data(), ry.size() * sizeof(ResizeY), hipMemcpyHostToDevice));
     return ODO_OK;
@@ -1320,9 +1364,9 @@ static int run_extract(odo_ctx* c, int set, const uint8_t* d_bgr, const uint16_t
         launch_blur(c->bstream, pyr, c->blur + (size_t)slot * P, P, c->lv, c->lv_h.data(), c->nlevels, n);
         HIPCHK(hipEventRecord(c->ev_blur[set], c->bstream));
     }
-    launch_fast(st, pyr, P, c->cells, c->lv, c->cand + (size_t)slot * c->ncells * c->cell_cap,
+    launch_fast(st, pyr, P, c->fsegs, (int)c->fsegs_h.size(), c->lv, c->cand + (size_t)slot * c->ncells * c->cell_cap,
                 c->cand_cnt + (size_t)slot * c->ncells, c->ncells, c->cell_cap, c->cfg.orb.ini_th_fast,
-                c->cfg.orb.min_th_fast, c->fast_roi, n);
+                c->cfg.orb.min_th_fast, c->fs_lds, n);
     tmark(c, 2, st);
     launch_octree(st, c->cand + (size_t)slot * c->ncells * c->cell_cap, c->cand_cnt + (size_t)slot * c->ncells, c->lv,
                   c->ncells, c->cell_cap, c->nlevels, c->keys + (size_t)slot * c->keys_per_frame,

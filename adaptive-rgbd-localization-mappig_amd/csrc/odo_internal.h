@@ -48,6 +48,25 @@ struct CellDesc {
     int16_t pad;
 };
 
+// A FAST segment (k_fast_seg): cells [ja, ja + ncell) of one cell row of one
+// level, whose ROIs (orbextractor.cpp:688-703) are staged in LDS as one union:
+// rows [y0, y0 + rows), cols [x0, x0 + cols) of the level; cell jl of the
+// segment is cells_h[ci0 + jl] (ROI x0 + jl*wcell).
+#define FS_NCM 16  // cells per segment (max)
+#ifndef FS_SEGC
+#define FS_SEGC 8  // cells per segment the host table aims for
+#endif
+struct FastSeg {
+    int level, ci0;
+    int16_t y0, x0, rows, cols, ncell, wcell;
+    int16_t rs, bw;  // LDS row stride (bytes, a multiple of 16), kept-bitmap words per row
+};
+// k_fast_seg's dynamic LDS: byte offsets of its regions
+struct FastLds {
+    int img;  // bytes of the staged ROI union (the score map follows at img)
+    int ring, clist, bits, cnt, qlist, misc, total;
+};
+
 // cv::resize INTER_LINEAR tables (per output column / row).
 struct ResizeX {
     int sx0, sx1;
@@ -167,7 +186,7 @@ struct RansacCfg {
     int sample_size;
     int check_depth;
     double raster_cov_x, raster_cov_y;
-    int rows0;  // hypothesis rows (of EV_WAVES) of the first eval launch; set by launch_ransac
+    int h0;     // hypotheses of the first eval launch ([0, h0)); set by launch_ransac
     int lanes_min_open;  // odo_kernel_forms.ransac_lanes_min_open (0 = default)
     int fold_wave;       // ordered fold by the whole wave (a lone pair); set by launch_ransac
 };
@@ -203,9 +222,11 @@ bool pyramid_blur_fusable(const LevelDesc* lv_host, int nlevels);
 bool pyramid_fusable(const LevelDesc* lv_host, const ResizeX* rx, const int* rx_off, int nlevels);
 void launch_resize(hipStream_t st, uint8_t* pyr, size_t pyr_stride, int src_off, int spitch, int dst_off, int dpitch,
                    int dw, int dh, int rb, int max_src_rows, const ResizeX* xt, const ResizeY* yt, int nframes);
-void launch_fast(hipStream_t st, const uint8_t* pyr, size_t pyr_stride, const CellDesc* cells, const LevelDesc* lv,
-                 uint32_t* cand, int* cand_cnt, int ncells, int cell_cap, int ini_th, int min_th, int roi_max,
-                 int nframes);
+void launch_fast(hipStream_t st, const uint8_t* pyr, size_t pyr_stride, const FastSeg* segs, int nsegs,
+                 const LevelDesc* lv, uint32_t* cand, int* cand_cnt, int ncells, int cell_cap, int ini_th, int min_th,
+                 const FastLds& lds, int nframes);
+// LDS layout of k_fast_seg for the context's largest segment (false: too large)
+bool fast_lds_plan(const FastSeg* segs, int nsegs, FastLds& L);
 size_t octree_lds_bytes(int node_cap);
 void launch_octree(hipStream_t st, const uint32_t* cand, const int* cand_cnt, const LevelDesc* lv, int ncells,
                    int cell_cap, int nlevels, uint32_t* keys, int32_t* knode, uint8_t* kquad, size_t keys_stride,

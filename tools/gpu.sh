@@ -19,6 +19,7 @@
 #   pmc=REGEX           PMC passes over the kernels matching REGEX (tuning build,
 #                       serial streams), one counter group per rocprofv3 run
 #   pmch=REGEX          the same on the hard workload
+#   vserial=V           per-kernel times alone of variant build_V (built with -DODO_TUNING)
 #   vtests=V:F1,F2      pytest -m gpu over the named files against variant build_V
 #   probe=V:SCRIPT      python tools/SCRIPT.py with ODO_LIB = variant build_V (probe builds)
 #   envbench=NAME:ENV:ARGS  bench.py on the tuning build with knobs in the environment
@@ -114,6 +115,13 @@ for step in "$@"; do
         -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --host-steps 0 --latency-frames 0 \
         --steps 2 --hard-steps 0 --workload hard > $O/serial_hard.log 2>&1
       echo "serial hard ok" ;;
+    vserial=*)
+      # per-kernel times alone (serial streams) of a tuning-flagged variant build_V
+      v=${step#vserial=}
+      cd /tmp
+      ODO_SERIAL_STREAMS=1 ODO_LIB=$(lib_of $v) timeout -s KILL 300 rocprofv3 --kernel-trace --stats \
+        -d $O/serial_$v -o run --output-format csv -- python3 $R/bench.py $QUICK --steps 10 > $O/serial_$v.log 2>&1
+      echo "vserial $v ok" ;;
     pmc=*)
       K=${step#pmc=}
       pmc_passes "$K" "$O/pmc_$(echo $K | tr -c 'A-Za-z0-9_\n' '_')" --steps 3 --warmup 1 $QUICK ;;
