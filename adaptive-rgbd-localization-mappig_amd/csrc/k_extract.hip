@@ -550,16 +550,13 @@ __global__ void __launch_bounds__(OT_THREADS) k_octree(const uint32_t* __restric
     __builtin_amdgcn_s_setprio(ODO_OCTREE_PRIO);  // tuning: the barrier-bound octree's waves ahead of co-runners
 #endif
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    // ODO_OCTREE_LPT=1: grid (frames, levels), so every frame's level 0 (the
-    // longest workgroups) is dispatched first (longest-first): 129 vs 190-206
-    // us alone, but the step is slower (110.8 k vs 113.5 k frames/s, two A/B
-    // runs each, profiles/r02_octree_ab/): the 256 level-0 workgroups at once
-    // crowd out the co-running pair stages. Default: grid (levels, frames).
-#ifndef ODO_OCTREE_LPT
-#define ODO_OCTREE_LPT 0
-#endif
-    const int f = ODO_OCTREE_LPT ? blockIdx.x : blockIdx.y;
-    const int l = ODO_OCTREE_LPT ? blockIdx.y : blockIdx.x;
+    // grid (levels, frames). Measured and retired: (frames, levels), every
+    // frame's level 0 (the longest workgroups) dispatched first: 129 vs
+    // 190-206 us alone, but the step slower (110.8 k vs 113.5 k frames/s,
+    // profiles/r02_octree_ab/): 256 level-0 workgroups at once crowd out the
+    // co-running pair stages.
+    const int f = blockIdx.y;
+    const int l = blockIdx.x;
     const int t = threadIdx.x;
     const LevelDesc L = lv[l];
     // carve LDS
@@ -1165,9 +1162,6 @@ ODO_INLINE uint32_t pair_hi(uint32_t cur, uint32_t prev) { return __builtin_amdg
 template <int R>
 ODO_INLINE int chunk_y0(int chunk, int h) { return min(chunk * R, h - R); }
 #define BR_RE 6  // output rows per edge-lane chunk
-#ifndef BW_AHEAD
-#define BW_AHEAD 1  // row blocks (of 6) a blur walk loads ahead of the one it computes: 1 or 2
-#endif
 
 // One quad's walk down rows y0 - 3 .. y0 + R + 2. s0: the level's row 0 at
 // byte x - 4 (interior) / the level's row 0 (EDGE); dp: row y0 at byte x.
@@ -1190,9 +1184,6 @@ ODO_INLINE void blur_walk(const uint8_t* s0, uint8_t* dp, size_t pitch, int h, i
     static_assert(R % 6 == 0, "the accumulators rotate over 6 rows");
     constexpr int NB = (R + 6) / 6;
     uint32_t cw[6][3], nw[6][3];
-#if BW_AHEAD > 1
-    uint32_t nw2[6][3];  // two blocks ahead
-#endif
     const uint8_t* sp = s0 + (size_t)(y0 - 3) * pitch;
     auto load_block = [&](uint32_t(&d)[6][3], int b, bool refl) {
 #pragma unroll
@@ -1211,15 +1202,8 @@ ODO_INLINE void blur_walk(const uint8_t* s0, uint8_t* dp, size_t pitch, int h, i
         sp += 6 * pitch;
     };
     load_block(cw, 0, top);
-#if BW_AHEAD > 1
-    if (1 < NB) load_block(nw, 1, 1 == NB - 1 && bottom);
-#endif
     for (int b = 0; b < NB; b++) {
-#if BW_AHEAD > 1
-        if (b + 2 < NB) load_block(nw2, b + 2, b + 2 == NB - 1 && bottom);
-#else
         if (b + 1 < NB) load_block(nw, b + 1, b + 1 == NB - 1 && bottom);
-#endif
 #pragma unroll
         for (int j = 0; j < 6; j++) {
             // input row r = y0 - 3 + 6b + j
@@ -1270,15 +1254,13 @@ ODO_INLINE void blur_walk(const uint8_t* s0, uint8_t* dp, size_t pitch, int h, i
         }
 #pragma unroll
         for (int j = 0; j < 6; j++) cw[j][0] = nw[j][0], cw[j][1] = nw[j][1], cw[j][2] = nw[j][2];
-#if BW_AHEAD > 1
-#pragma unroll
-        for (int j = 0; j < 6; j++) nw[j][0] = nw2[j][0], nw[j][1] = nw2[j][1], nw[j][2] = nw2[j][2];
-#endif
     }
 }
 
 // Edge quads: one lane per (level, 6-row chunk, quad left of 1 / right of nq).
-ODO_INLINE void blur_edge_lane(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur, size_t pyr_stride,
+// srcL: the level's row 0 (rows outside the ones the walk reads need not exist:
+// k_pyramid's level-0 bands pass an LDS band as "row 0" minus its first row)
+ODO_INLINE void blur_edge_lane(const uint8_t* srcL, uint8_t* __restrict__ blur, size_t pyr_stride,
                                 const LevelDesc* __restrict__ lv, const BlurRows& S, int nlevels, int f, int k) {
     if (k >= S.ebase[nlevels]) return;
     int l = 0;
@@ -1308,7 +1290,7 @@ ODO_INLINE void blur_edge_lane(const uint8_t* __restrict__ pyr, uint8_t* __restr
         selB[d] = bsel;
     }
     const int o0 = x >= 4 ? x - 4 : x, o2 = x + 8 <= L.pitch ? x + 4 : x;
-    const uint8_t* s0 = pyr + (size_t)f * pyr_stride + L.off;
+    const uint8_t* s0 = srcL;
     uint8_t* dp = blur + (size_t)f * pyr_stride + L.off + (size_t)y0 * L.pitch + x;
     blur_walk<true, BR_RE>(s0, dp, (size_t)L.pitch, L.h, y0, true, true, true, o0, x, o2, selA, selB);
 }
@@ -1324,7 +1306,11 @@ __global__ void __launch_bounds__(256) k_blur_rows(const uint8_t* __restrict__ p
     EXTRACT_PRIO();
     const int f = blockIdx.y;
     if ((int)blockIdx.x < eblocks) {
-        blur_edge_lane(pyr, blur, pyr_stride, lv, S, nlevels, f, (int)blockIdx.x * 256 + (int)threadIdx.x);
+        const int k = (int)blockIdx.x * 256 + (int)threadIdx.x;
+        if (k >= S.ebase[nlevels]) return;
+        int l = 0;
+        while (l + 1 < nlevels && k >= S.ebase[l + 1]) l++;
+        blur_edge_lane(pyr + (size_t)f * pyr_stride + lv[l].off, blur, pyr_stride, lv, S, nlevels, f, k);
         return;
     }
     const uint32_t none[3] = {0, 0, 0};
@@ -1350,9 +1336,15 @@ __global__ void __launch_bounds__(256) k_blur_rows(const uint8_t* __restrict__ p
 // gray (level 0) and then each level from the one before it, with a
 // workgroup barrier between levels instead of eight dependent launches (the
 // chain's per-level drain and launch latency were most of its 0.28 ms alone
-// and 0.35-0.6 ms pipelined per 256 frames, profiles/r03_b). The levels are
+// and 0.35-0.6 ms pipelined per 256 frames, profiles/r03_b). Levels >= 1 are
 // read back through the CU's own L1 / L2 (every wave of the workgroup is on
 // one CU, so workgroup-scope ordering is all the barrier needs).
+// Level 0 (round 5, PyrBands): built band by band in LDS — the band's gray
+// rows plus 3-row halos (the halos' gray recomputed) — then the band's blur
+// rows and the level-1 rows whose sources lie in it are made from LDS, so
+// level 0 is written once (FAST and finalize read it) and never read back
+// (round 4: 1.37 GB memory-side per launch against 0.72 GB compulsory, most
+// of it level 0 read again by its blur and by level 1).
 // Resize: thread t owns quad q = t mod nq of the level (4 output pixels) and
 // walks the rows ph, ph + P, ... (ph = t / nq, P = 1024 / nq), so its x taps
 // are loaded once per level into registers: the quad's source bytes lie in
@@ -1375,11 +1367,11 @@ struct PyrLevels {
     int rx_off[16], ry_off[16];
 };
 // the 7x7 blur of level l of frame f by the whole workgroup (PYR_TH threads:
-// 64 strip groups of 16 lanes, then the edge lanes)
-ODO_INLINE void pyr_blur_level(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur, size_t pyr_stride,
+// 64 strip groups of 16 lanes, then the edge lanes): strip chunks [ca, cb)
+// and edge chunks [ea, eb) of the level, read from srcL (the level's row 0)
+ODO_INLINE void pyr_blur_level(const uint8_t* srcL, uint8_t* __restrict__ blur, size_t pyr_stride,
                                const LevelDesc* __restrict__ lv, const BlurRows& S, int nlevels, int f, int l,
                                const LevelDesc& L, int t, int ca, int cb, int ea, int eb) {
-    // strip chunks [ca, cb) and edge chunks [ea, eb) of the level (its part's share)
     const uint32_t none[3] = {0, 0, 0};
     const int items = cb * S.nst[l];
     const int g = t >> 4;
@@ -1390,159 +1382,177 @@ ODO_INLINE void pyr_blur_level(const uint8_t* __restrict__ pyr, uint8_t* __restr
         const int x = 4 * (store ? q : S.nq[l]);
         const int y0 = chunk_y0<BR_R>(chunk, L.h);
         const bool top = y0 < 3, bottom = y0 + BR_R + 3 > L.h;
-        const uint8_t* s0 = pyr + (size_t)f * pyr_stride + L.off + (x - 4);
+        const uint8_t* s0 = srcL + (x - 4);
         uint8_t* dp = blur + (size_t)f * pyr_stride + L.off + (size_t)y0 * L.pitch + x;
         blur_walk<false, BR_R>(s0, dp, (size_t)L.pitch, L.h, y0, top, bottom, store, 0, 0, 0, none, none);
     }
     const int ne = (S.ebase[l + 1] - S.ebase[l]) / ((L.h + BR_RE - 1) / BR_RE);  // edge quads per chunk
     for (int k = S.ebase[l] + ea * ne + t; k < S.ebase[l] + eb * ne; k += PYR_TH)
-        blur_edge_lane(pyr, blur, pyr_stride, lv, S, nlevels, f, k);
+        blur_edge_lane(srcL, blur, pyr_stride, lv, S, nlevels, f, k);
 }
-#ifdef ODO_PYR_PROFILE
-// -DODO_PYR_PROFILE: per frame of the last k_pyramid launch, wall-clock ticks
-// (10 ns) at the start, after gray, after each level's barrier and at the end
-// (read by odo_pyr_prof_read, tools/pyr_probe.py)
-#define PYR_PROF_MAX 1024
-__device__ uint64_t g_pyrprof[PYR_PROF_MAX * 20];
-#define PYR_PROF(k)                                                                   \
-    if (threadIdx.x == 0 && blockIdx.x < PYR_PROF_MAX) g_pyrprof[blockIdx.x * 20 + (k)] = wall_clock64()
-#else
-#define PYR_PROF(k)
-#endif
+// level D's rows [ylo, yhi) from level S (whose row 0 is srcS), thread t's quad
+ODO_INLINE void pyr_resize_rows(const uint8_t* srcS, uint8_t* dstD, const LevelDesc& S, const LevelDesc& D,
+                                const ResizeX* __restrict__ X, const ResizeY* __restrict__ Y, int t, int ylo, int yhi) {
+    const int nq = (D.w + 3) >> 2;
+    const int P = PYR_TH / nq;  // row phases (the host checks nq <= PYR_TH)
+    if (t >= P * nq) return;
+    const int ph = t / nq, q = t - ph * nq;
+    // the quad's taps: window origin sx0(4q), per-pixel selectors and weights
+    const int x00 = X[4 * q].sx0;
+    const int wb = x00 & ~3, sh = x00 & 3;
+    uint32_t sel[4], wt[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int dx = 4 * q + j;
+        if (dx < D.w) {
+            const ResizeX xj = X[dx];
+            const uint32_t r0 = (uint32_t)(xj.sx0 - x00), r1 = (uint32_t)(xj.sx1 - x00);  // 0..7
+            sel[j] = r0 | (0x0cu << 8) | (r1 << 16) | (0x0cu << 24);
+            wt[j] = (uint32_t)xj.a0 | ((uint32_t)xj.a1 << 16);
+        } else {
+            sel[j] = 0x0c0c0c0cu;  // past the level width: 0 (the row padding)
+            wt[j] = 0;
+        }
+    }
+    const uint8_t* sbase = srcS + wb;
+    uint8_t* dbase = dstD + 4 * q;
+    auto hsum = [&](const uint8_t* row, uint32_t (&h)[4]) {
+        const uint32_t* w32 = reinterpret_cast<const uint32_t*>(row);
+        const uint32_t w0 = w32[0], w1 = w32[1], w2 = w32[2];
+        const uint32_t A = __builtin_amdgcn_alignbyte(w1, w0, sh), B = __builtin_amdgcn_alignbyte(w2, w1, sh);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+            h[j] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_perm(B, A, sel[j])),
+                                          __builtin_bit_cast(u16x2, wt[j]), 0u, false);
+        }
+    };
+    for (int y = ylo + ph; y < yhi; y += PYR_RU * P) {
+        ResizeY Yr[PYR_RU];
+#pragma unroll
+        for (int u = 0; u < PYR_RU; u++) Yr[u] = Y[min(y + u * P, yhi - 1)];
+        uint32_t h0[PYR_RU][4], h1[PYR_RU][4];
+#pragma unroll
+        for (int u = 0; u < PYR_RU; u++) {
+            hsum(sbase + Yr[u].sy0 * S.pitch, h0[u]);
+            hsum(sbase + Yr[u].sy1 * S.pitch, h1[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < PYR_RU; u++) {
+            uint32_t pk = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                pk |= min((__umul24(h0[u][j], (uint32_t)Yr[u].b0) + __umul24(h1[u][j], (uint32_t)Yr[u].b1) + (1u << 21)) >> 22,
+                          255u) << (8 * j);
+            if (y + u * P < yhi) *reinterpret_cast<uint32_t*>(dbase + (size_t)(y + u * P) * D.pitch) = pk;
+        }
+    }
+}
+// gray of level-0 rows [r0, r1) (k_gray's arithmetic, PYR_GU quads of 4
+// pixels in flight per thread): row y to gdst + y * pitch, and when lds is
+// given also to lds + (y - g0) * pitch (the band buffer) with the global
+// store only for rows [b0, b1)
+ODO_INLINE void pyr_gray_rows(const uint8_t* __restrict__ src, uint8_t* gdst, uint8_t* lds, int w, int pitch,
+                              int r0, int r1, int g0, int b0, int b1, int t) {
+    if ((w & 3) == 0) {
+        const int nq4 = (r1 * w) >> 2;
+        for (int q0 = ((r0 * w) >> 2) + t; q0 < nq4; q0 += PYR_GU * PYR_TH) {
+            uint32_t wv[PYR_GU][3];
+#pragma unroll
+            for (int u = 0; u < PYR_GU; u++) {
+                const int q = q0 + u * PYR_TH;
+                if (q < nq4) {
+                    const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src + (size_t)q * 12);
+                    wv[u][0] = s32[0], wv[u][1] = s32[1], wv[u][2] = s32[2];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < PYR_GU; u++) {
+                const int q = q0 + u * PYR_TH;
+                if (q < nq4) {
+                    const int p0 = q * 4, y = p0 / w, x = p0 - y * w;
+                    uint32_t out = 0;
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const int b = 3 * i;
+                        const uint32_t B = (wv[u][b >> 2] >> (8 * (b & 3))) & 0xffu;
+                        const uint32_t G = (wv[u][(b + 1) >> 2] >> (8 * ((b + 1) & 3))) & 0xffu;
+                        const uint32_t R = (wv[u][(b + 2) >> 2] >> (8 * ((b + 2) & 3))) & 0xffu;
+                        out |= ((B * 1868u + G * 9617u + R * 4899u + 8192u) >> 14) << (8 * i);
+                    }
+                    if (lds) {
+                        *reinterpret_cast<uint32_t*>(lds + (y - g0) * pitch + x) = out;
+                        if (y >= b0 && y < b1) *reinterpret_cast<uint32_t*>(gdst + (size_t)y * pitch + x) = out;
+                    } else {
+                        *reinterpret_cast<uint32_t*>(gdst + (size_t)y * pitch + x) = out;
+                    }
+                }
+            }
+        }
+    } else {
+        for (int p = r0 * w + t; p < r1 * w; p += PYR_TH) {
+            const uint8_t* s = src + (size_t)p * 3;
+            const int yy = p / w, xx = p - yy * w;
+            gdst[(size_t)yy * pitch + xx] =
+                (uint8_t)(((uint32_t)s[0] * 1868u + (uint32_t)s[1] * 9617u + (uint32_t)s[2] * 4899u + 8192u) >> 14);
+        }
+    }
+}
 template <bool BLUR>
 __global__ void __launch_bounds__(PYR_TH) k_pyramid(const uint8_t* __restrict__ bgr, uint8_t* __restrict__ pyr,
                                                     size_t in_stride, size_t pyr_stride,
                                                     const LevelDesc* __restrict__ lv, const ResizeX* __restrict__ xt,
                                                     const ResizeY* __restrict__ yt, PyrLevels PL, int nlevels,
-                                                    uint8_t* __restrict__ blur, BlurRows BR, PyrSplit SP) {
+                                                    uint8_t* __restrict__ blur, BlurRows BR, PyrBands PB) {
     EXTRACT_PRIO();
-    // SP.parts == 2: two workgroups per frame, the top and the bottom part
-    const int part = SP.parts == 2 ? (int)(blockIdx.x & 1) : 0;
-    const int f = SP.parts == 2 ? (int)(blockIdx.x >> 1) : (int)blockIdx.x;
+    extern __shared__ __attribute__((aligned(16))) uint8_t pyr_lds[];
+    const int f = blockIdx.x;
     const int t = threadIdx.x;
     uint8_t* base = pyr + (size_t)f * pyr_stride;
-    PYR_PROF(0);
+    int lfirst = 1;  // first level the level loop builds
     if (bgr) {
-        // level 0: gray, 4 pixels per thread (k_gray's arithmetic)
         const LevelDesc L0 = lv[0];
-        const int w = L0.w, h = L0.h, pitch = L0.pitch;
         const uint8_t* src = bgr + (size_t)f * in_stride;
-        const int npix = w * h;
-        const int r0 = SP.lo[part][0], r1 = SP.hi[part][0];  // this part's rows of level 0
-        if ((w & 3) == 0) {
-            const int nq4 = (r1 * w) >> 2;
-            for (int q0 = ((r0 * w) >> 2) + t; q0 < nq4; q0 += PYR_GU * PYR_TH) {
-                uint32_t wv[PYR_GU][3];
-#pragma unroll
-                for (int u = 0; u < PYR_GU; u++) {
-                    const int q = q0 + u * PYR_TH;
-                    if (q < nq4) {
-                        const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src + (size_t)q * 12);
-                        wv[u][0] = s32[0], wv[u][1] = s32[1], wv[u][2] = s32[2];
-                    }
+        if (PB.nb > 0) {
+            // level 0 band by band in LDS: gray, then its blur and level 1
+            const LevelDesc L1 = lv[1];
+            for (int k = 0; k < PB.nb; k++) {
+                const int b0 = PB.b0[k], b1 = PB.b0[k + 1];
+                const int g0 = max(b0 - 3, 0), g1 = min(b1 + 3, L0.h);
+                pyr_gray_rows(src, base + L0.off, pyr_lds, L0.w, L0.pitch, g0, g1, g0, b0, b1, t);
+                __syncthreads();  // the band is in LDS
+                // the band as the level's "row 0": row y at pyr_lds + (y - g0) * pitch
+                const uint8_t* srcB = pyr_lds - g0 * L0.pitch;
+                if (BLUR) {
+                    const int ca = b0 / BR_R, cb = b1 == L0.h ? (L0.h + BR_R - 1) / BR_R : b1 / BR_R;
+                    const int ea = b0 / BR_RE, eb = b1 == L0.h ? (L0.h + BR_RE - 1) / BR_RE : b1 / BR_RE;
+                    pyr_blur_level(srcB, blur, pyr_stride, lv, BR, nlevels, f, 0, L0, t, ca, cb, ea, eb);
                 }
-#pragma unroll
-                for (int u = 0; u < PYR_GU; u++) {
-                    const int q = q0 + u * PYR_TH;
-                    if (q < nq4) {
-                        const int p0 = q * 4, y = p0 / w, x = p0 - y * w;
-                        uint32_t out = 0;
-#pragma unroll
-                        for (int i = 0; i < 4; i++) {
-                            const int b = 3 * i;
-                            const uint32_t B = (wv[u][b >> 2] >> (8 * (b & 3))) & 0xffu;
-                            const uint32_t G = (wv[u][(b + 1) >> 2] >> (8 * ((b + 1) & 3))) & 0xffu;
-                            const uint32_t R = (wv[u][(b + 2) >> 2] >> (8 * ((b + 2) & 3))) & 0xffu;
-                            out |= ((B * 1868u + G * 9617u + R * 4899u + 8192u) >> 14) << (8 * i);
-                        }
-                        *reinterpret_cast<uint32_t*>(base + (size_t)y * pitch + x) = out;
-                    }
-                }
+                pyr_resize_rows(srcB, base + L1.off, L0, L1, xt + PL.rx_off[1], yt + PL.ry_off[1], t, PB.y1[k],
+                                PB.y1[k + 1]);
+                __syncthreads();  // the band buffer is free
             }
+            lfirst = 2;
         } else {
-            for (int p = r0 * w + t; p < r1 * w; p += PYR_TH) {
-                const uint8_t* s = src + (size_t)p * 3;
-                const int yy = p / w, xx = p - yy * w;
-                base[(size_t)yy * pitch + xx] =
-                    (uint8_t)(((uint32_t)s[0] * 1868u + (uint32_t)s[1] * 9617u + (uint32_t)s[2] * 4899u + 8192u) >> 14);
-            }
+            pyr_gray_rows(src, base + L0.off, nullptr, L0.w, L0.pitch, 0, L0.h, 0, 0, 0, t);
         }
     }
-    for (int l = 1; l < nlevels; l++) {
+    for (int l = lfirst; l < nlevels; l++) {
         __syncthreads();  // level l - 1 is complete
-        PYR_PROF(l);
         const LevelDesc S = lv[l - 1], D = lv[l];
         if (BLUR)
-            pyr_blur_level(pyr, blur, pyr_stride, lv, BR, nlevels, f, l - 1, S, t, SP.ca[part][l - 1], SP.cb[part][l - 1],
-                           SP.ea[part][l - 1], SP.eb[part][l - 1]);
-        const int nq = (D.w + 3) >> 2;
-        const int P = PYR_TH / nq;  // row phases (the host checks nq <= PYR_TH)
-        if (t >= P * nq) continue;
-        const int ph = t / nq, q = t - ph * nq;
-        const ResizeX* X = xt + PL.rx_off[l];
-        const ResizeY* Y = yt + PL.ry_off[l];
-        // the quad's taps: window origin sx0(4q), per-pixel selectors and weights
-        const int x00 = X[4 * q].sx0;
-        const int wb = x00 & ~3, sh = x00 & 3;
-        uint32_t sel[4], wt[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int dx = 4 * q + j;
-            if (dx < D.w) {
-                const ResizeX xj = X[dx];
-                const uint32_t r0 = (uint32_t)(xj.sx0 - x00), r1 = (uint32_t)(xj.sx1 - x00);  // 0..7
-                sel[j] = r0 | (0x0cu << 8) | (r1 << 16) | (0x0cu << 24);
-                wt[j] = (uint32_t)xj.a0 | ((uint32_t)xj.a1 << 16);
-            } else {
-                sel[j] = 0x0c0c0c0cu;  // past the level width: 0 (the row padding)
-                wt[j] = 0;
-            }
-        }
-        const uint8_t* sbase = base + S.off + wb;
-        uint8_t* dbase = base + D.off + 4 * q;
-        auto hsum = [&](const uint8_t* row, uint32_t (&h)[4]) {
-            const uint32_t* w32 = reinterpret_cast<const uint32_t*>(row);
-            const uint32_t w0 = w32[0], w1 = w32[1], w2 = w32[2];
-            const uint32_t A = __builtin_amdgcn_alignbyte(w1, w0, sh), B = __builtin_amdgcn_alignbyte(w2, w1, sh);
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-                h[j] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_perm(B, A, sel[j])),
-                                              __builtin_bit_cast(u16x2, wt[j]), 0u, false);
-            }
-        };
-        const int ylo = SP.lo[part][l], yhi = SP.hi[part][l];  // this part's rows of level l
-        for (int y = ylo + ph; y < yhi; y += PYR_RU * P) {
-            ResizeY Yr[PYR_RU];
-#pragma unroll
-            for (int u = 0; u < PYR_RU; u++) Yr[u] = Y[min(y + u * P, yhi - 1)];
-            uint32_t h0[PYR_RU][4], h1[PYR_RU][4];
-#pragma unroll
-            for (int u = 0; u < PYR_RU; u++) {
-                hsum(sbase + (size_t)Yr[u].sy0 * S.pitch, h0[u]);
-                hsum(sbase + (size_t)Yr[u].sy1 * S.pitch, h1[u]);
-            }
-#pragma unroll
-            for (int u = 0; u < PYR_RU; u++) {
-                uint32_t pk = 0;
-#pragma unroll
-                for (int j = 0; j < 4; j++)
-                    pk |= min((__umul24(h0[u][j], (uint32_t)Yr[u].b0) + __umul24(h1[u][j], (uint32_t)Yr[u].b1) + (1u << 21)) >> 22,
-                              255u) << (8 * j);
-                if (y + u * P < yhi) *reinterpret_cast<uint32_t*>(dbase + (size_t)(y + u * P) * D.pitch) = pk;
-            }
-        }
+            pyr_blur_level(base + S.off, blur, pyr_stride, lv, BR, nlevels, f, l - 1, S, t, 0, BR.nch[l - 1], 0,
+                           (S.h + BR_RE - 1) / BR_RE);
+        pyr_resize_rows(base + S.off, base + D.off, S, D, xt + PL.rx_off[l], yt + PL.ry_off[l], t, 0, D.h);
     }
     if (BLUR) {
         __syncthreads();  // the last level is complete
-        PYR_PROF(nlevels);
-        const LevelDesc L = lv[nlevels - 1];
         const int ll = nlevels - 1;
-        pyr_blur_level(pyr, blur, pyr_stride, lv, BR, nlevels, f, ll, L, t, SP.ca[part][ll], SP.cb[part][ll],
-                       SP.ea[part][ll], SP.eb[part][ll]);
+        const LevelDesc L = lv[ll];
+        pyr_blur_level(base + L.off, blur, pyr_stride, lv, BR, nlevels, f, ll, L, t, 0, BR.nch[ll], 0,
+                       (L.h + BR_RE - 1) / BR_RE);
     }
     __syncthreads();
-    PYR_PROF(nlevels + 1);
 }
 
 // ============================================================ host-side launch helpers
@@ -1585,68 +1595,59 @@ bool pyramid_blur_fusable(const LevelDesc* lv_host, int nlevels) {
 }
 void launch_pyramid(hipStream_t st, const uint8_t* bgr, uint8_t* pyr, size_t in_stride, size_t pyr_stride,
                     const LevelDesc* lv, const ResizeX* rx, const ResizeY* ry, const int* rx_off, const int* ry_off,
-                    int nlevels, int nframes, uint8_t* blur, const LevelDesc* lv_host, const PyrSplit& split) {
+                    int nlevels, int nframes, uint8_t* blur, const LevelDesc* lv_host, const PyrBands& bands) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_pyramid<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_pyramid<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
+    }
     PyrLevels PL{};
     for (int l = 0; l < nlevels && l < 16; l++) PL.rx_off[l] = rx_off[l], PL.ry_off[l] = ry_off[l];
     BlurRows BR{};
-    const dim3 g(nframes * split.parts);
+    PyrBands PB = bands;
+    if (!bgr) PB.nb = 0;  // level 0 already in place: nothing to band
+    const size_t lds = PB.nb > 0 ? (size_t)PB.rows * lv_host[0].pitch : 0;
     if (blur && blur_rows_plan(lv_host, nlevels, BR)) {
-        hipLaunchKernelGGL(k_pyramid<true>, g, dim3(PYR_TH), 0, st, bgr, pyr, in_stride, pyr_stride, lv, rx, ry, PL,
-                           nlevels, blur, BR, split);
+        hipLaunchKernelGGL(k_pyramid<true>, dim3(nframes), dim3(PYR_TH), lds, st, bgr, pyr, in_stride, pyr_stride, lv,
+                           rx, ry, PL, nlevels, blur, BR, PB);
         return;
     }
-    hipLaunchKernelGGL(k_pyramid<false>, g, dim3(PYR_TH), 0, st, bgr, pyr, in_stride, pyr_stride, lv, rx, ry, PL,
-                       nlevels, (uint8_t*)nullptr, BR, split);
+    hipLaunchKernelGGL(k_pyramid<false>, dim3(nframes), dim3(PYR_TH), lds, st, bgr, pyr, in_stride, pyr_stride, lv, rx,
+                       ry, PL, nlevels, (uint8_t*)nullptr, BR, PB);
 }
-// The part ranges of k_pyramid (PyrSplit). parts == 1: everything. parts == 2:
-// level l's blur rows split at s_l (a multiple of BR_R = 30, so the 30-row
-// strip chunks and 6-row edge chunks split with it; a level under 60 rows is
-// blurred by the top part alone); each part builds the rows its blur reads
-// (3-row halo) and the source rows of the next level's rows it builds,
-// from the top level down. Every row keeps its one arithmetic, so rows both
-// parts build are the same bytes.
-void pyramid_split_plan(const LevelDesc* lv_host, const ResizeY* ry, const int* ry_off, int nlevels, int parts,
-                        PyrSplit& S) {
-    S = PyrSplit{};
-    S.parts = parts;
-    for (int l = 0; l < nlevels && l < 16; l++) {
-        const int h = lv_host[l].h, nch = (h + BR_R - 1) / BR_R, nch6 = (h + BR_RE - 1) / BR_RE;
-        for (int p = 0; p < 2; p++) {
-            S.lo[p][l] = 0, S.hi[p][l] = h;
-            S.ca[p][l] = 0, S.cb[p][l] = nch, S.ea[p][l] = 0, S.eb[p][l] = nch6;
-        }
+// Level-0 bands of k_pyramid: PYR_BAND rows each (multiples of the blur's
+// 30- and 6-row chunks, so a band's blur chunks never reach outside the band
+// and its 3-row halos), a remainder under 30 rows joined to the last band;
+// band k makes the level-1 rows whose first source row sy0 lies in it (the
+// second, sy0 + 1, is at most its first halo row).
+void pyramid_band_plan(const LevelDesc* lv_host, const ResizeY* ry, const int* ry_off, int nlevels, PyrBands& B) {
+    B = PyrBands{};
+    if (nlevels < 2 || (lv_host[0].w & 3) != 0) return;
+    for (int l = 0; l < nlevels; l++)
+        if (lv_host[l].h < BR_R) return;
+    const int h = lv_host[0].h;
+    int nb = h / PYR_BAND;
+    if (nb == 0 || h - nb * PYR_BAND >= BR_R) nb++;
+    if (nb > PYR_MAXB) return;
+    int mx = 0;
+    for (int k = 0; k < nb; k++) B.b0[k] = k * PYR_BAND;
+    B.b0[nb] = h;
+    for (int k = 0; k < nb; k++) mx = std::max(mx, B.b0[k + 1] - B.b0[k]);
+    const ResizeY* Y = ry + ry_off[1];
+    const int h1 = lv_host[1].h;
+    int y = 0;
+    for (int k = 0; k < nb; k++) {
+        B.y1[k] = y;
+        while (y < h1 && Y[y].sy0 < B.b0[k + 1]) y++;
     }
-    if (parts != 2 || nlevels > 16) {
-        S.parts = 1;
-        return;
-    }
-    int sp[16];
-    for (int l = 0; l < nlevels; l++) {
-        const int h = lv_host[l].h;
-        int s = ((h / 2 + BR_R / 2) / BR_R) * BR_R;  // the multiple of 30 nearest h / 2
-        if (h < 2 * BR_R) s = h;                       // too small to split: the top part blurs it all
-        s = std::min(s, h < 2 * BR_R ? h : h - BR_R);
-        sp[l] = s;
-        const int nch = (h + BR_R - 1) / BR_R, nch6 = (h + BR_RE - 1) / BR_RE;
-        S.ca[0][l] = 0, S.cb[0][l] = s == h ? nch : s / BR_R;
-        S.ca[1][l] = S.cb[0][l], S.cb[1][l] = nch;
-        S.ea[0][l] = 0, S.eb[0][l] = s == h ? nch6 : s / BR_RE;
-        S.ea[1][l] = S.eb[0][l], S.eb[1][l] = nch6;
-    }
-    // rows built per part, from the top level down
-    for (int l = nlevels - 1; l >= 0; l--) {
-        const int h = lv_host[l].h;
-        int thi = std::min(h, sp[l] + 3), blo = std::max(0, sp[l] - 3);
-        if (sp[l] == h) blo = h;  // the bottom part blurs none of this level
-        if (l + 1 < nlevels) {
-            const ResizeY* Y = ry + ry_off[l + 1];
-            if (S.hi[0][l + 1] > 0) thi = std::max(thi, Y[S.hi[0][l + 1] - 1].sy1 + 1);
-            if (S.lo[1][l + 1] < lv_host[l + 1].h) blo = std::min(blo, Y[S.lo[1][l + 1]].sy0);
-        }
-        S.lo[0][l] = 0, S.hi[0][l] = std::min(h, thi);
-        S.lo[1][l] = std::max(0, blo), S.hi[1][l] = h;
-        if (S.lo[1][l] >= h) S.lo[1][l] = h;  // nothing to build
-    }
+    B.y1[nb] = h1;
+    for (int k = 0; k < nb; k++)
+        for (int r = B.y1[k]; r < B.y1[k + 1]; r++)
+            if (Y[r].sy0 < std::max(B.b0[k] - 3, 0) || Y[r].sy1 >= std::min(B.b0[k + 1] + 3, h)) return;  // not in the band
+    if ((size_t)(mx + 6) * lv_host[0].pitch > 160 * 1024) return;
+    B.rows = mx + 6;
+    B.nb = nb;
 }
 bool pyramid_fusable(const LevelDesc* lv_host, const ResizeX* rx, const int* rx_off, int nlevels) {
     if (nlevels > 16) return false;
@@ -1711,7 +1712,7 @@ size_t octree_lds_bytes(int node_cap) { return (size_t)76 * node_cap + 1032; }
 void launch_octree(hipStream_t st, const uint32_t* cand, const int* cand_cnt, const LevelDesc* lv, int ncells,
                    int cell_cap, int nlevels, uint32_t* keys, int32_t* knode, uint8_t* kquad, size_t keys_stride,
                    uint32_t* okp, int* ocnt, int okp_stride, int node_cap, int nframes) {
-    const dim3 g = ODO_OCTREE_LPT ? dim3(nframes, nlevels) : dim3(nlevels, nframes);
+    const dim3 g(nlevels, nframes);
     hipLaunchKernelGGL(k_octree, g, dim3(OT_THREADS), octree_lds_bytes(node_cap), st, cand, cand_cnt, lv, ncells,
                        cell_cap, nlevels, keys, knode, kquad, keys_stride, okp, ocnt, okp_stride, node_cap);
 }
@@ -1787,12 +1788,3 @@ void launch_pair_valid(hipStream_t st, int* pv, int n, int first_valid) {
     hipLaunchKernelGGL(k_pair_valid, dim3((n + 255) / 256), dim3(256), 0, st, pv, n, first_valid);
 }
 }  // namespace odo
-#ifdef ODO_PYR_PROFILE
-extern "C" int odo_pyr_prof_read(uint64_t* out, int n) {
-    n = n < PYR_PROF_MAX ? n : PYR_PROF_MAX;
-    if (hipDeviceSynchronize() != hipSuccess) return -1;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(odo::g_pyrprof), (size_t)n * 20 * sizeof(uint64_t)) != hipSuccess)
-        return -1;
-    return n;
-}
-#endif

@@ -214,24 +214,17 @@ __global__ void __launch_bounds__(256, FIN_WAVES_PER_EU) k_finalize(const uint8_
 #define FL_IC_N (31 * FL_IC_W)       // 279
 #define FL_BR_W 10                   // dwords per staged rBRIEF row
 #define FL_BR_N (37 * FL_BR_W)       // 370
-// FIN_OVERLAY=1: the rBRIEF window overwrites the IC disc once the angle is
-// known (its loads are in flight since the start), so a keypoint holds 370
-// dwords of LDS instead of 649 and more workgroups fit a CU
-#ifndef FIN_SADDR
-#define FIN_SADDR 1  // staging loads as scalar frame base + 32-bit offsets stepped without divisions
-#endif
-#ifndef FIN_OVERLAY
-#define FIN_OVERLAY 1
-#endif
+// The rBRIEF window overwrites the IC disc once the angle is known (its loads
+// are in flight since the start), so a keypoint holds 370 dwords of LDS
+// instead of 649 and more workgroups fit a CU (round 2).
 // dwords of LDS per keypoint, padded to 16 mod 32 (round 5): a wave's lanes
 // 0-31 are two keypoints whose IC rows sit 9 dwords apart ({9s mod 32} for
 // the 16 lanes: half the banks); the second keypoint 16 banks further takes
 // exactly the other half ({16 + 9s}), where the unpadded 370 (18 mod 32)
 // shared 14 of 16 banks with the first (PMC: 35.7 M conflict cycles, 1.4x
 // the kernel's LDS cycles, round 4)
-#define FL_KP_RAW (FIN_OVERLAY ? FL_BR_N : FL_IC_N + FL_BR_N)
+#define FL_KP_RAW FL_BR_N
 #define FL_KP_DW (((FL_KP_RAW + 15) / 32) * 32 + 16)
-#define FL_BR_AT (FIN_OVERLAY ? 0 : FL_IC_N)                  // first dword of the rBRIEF window
 template <int NW>  // waves (of 4 keypoints) per workgroup
 __global__ void __launch_bounds__(64 * NW) k_finalize_lds(const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
                                                       size_t pyr_stride, const LevelDesc* __restrict__ lv, int nlevels,
@@ -295,7 +288,6 @@ __global__ void __launch_bounds__(64 * NW) k_finalize_lds(const uint8_t* __restr
     const int sh = (kx - 15) & 3, sh2 = (kx - 18) & 3;
     {
         uint32_t v[18 + 24];
-#if FIN_SADDR
         // 32-bit byte offsets from the frame's base (uniform over the
         // workgroup: scalar base + vector offset loads), advanced per step
         // of 16 staged dwords without divisions: 16 = 9 + 7 (IC rows of 9
@@ -330,30 +322,9 @@ __global__ void __launch_bounds__(64 * NW) k_finalize_lds(const uint8_t* __restr
                 c = one ? c + 6 : c - 4;
             }
         }
-#else
-        const uint8_t* img = pyr + (size_t)f * pyr_stride + L.off + (size_t)(ky - 15) * L.pitch + (kx - 15 - sh);
-        const uint8_t* bim = blur + (size_t)f * pyr_stride + L.off + (size_t)(ky - 18) * L.pitch + (kx - 18 - sh2);
-#pragma unroll
-        for (int j = 0; j < 18; j++) {
-            const int i = min(sub + 16 * j, FL_IC_N - 1);
-            const int r = i / FL_IC_W, c = i - r * FL_IC_W;
-            v[j] = *reinterpret_cast<const uint32_t*>(img + (size_t)r * L.pitch + 4 * c);
-        }
-#pragma unroll
-        for (int j = 0; j < 24; j++) {
-            const int i = min(sub + 16 * j, FL_BR_N - 1);
-            const int r = i / FL_BR_W, c = i - r * FL_BR_W;
-            v[18 + j] = *reinterpret_cast<const uint32_t*>(bim + (size_t)r * L.pitch + 4 * c);
-        }
-#endif
 #pragma unroll
         for (int j = 0; j < 18; j++)
             if (sub + 16 * j < FL_IC_N) P[sub + 16 * j] = v[j];
-        if (!FIN_OVERLAY) {
-#pragma unroll
-            for (int j = 0; j < 24; j++)
-                if (sub + 16 * j < FL_BR_N) P[FL_BR_AT + sub + 16 * j] = v[18 + j];
-        }
 #pragma unroll
         for (int j = 0; j < 24; j++) vbr[j] = v[18 + j];
     }
@@ -405,14 +376,12 @@ __global__ void __launch_bounds__(64 * NW) k_finalize_lds(const uint8_t* __restr
     const f32x2 BA = {b, a}, AB = {a, b}, MAG = {RND_MAGIC, RND_MAGIC};
     // staged byte of rotated offset (iy, ix): (iy + 18) * 40 + ix + 18 + sh2; the
     // magic-rounded floats carry RND_BITS + offset in their bits
-    if (FIN_OVERLAY) {
-        __syncthreads();  // every IC disc read
+    __syncthreads();  // every IC disc read
 #pragma unroll
-        for (int j = 0; j < 24; j++)
-            if (sub + 16 * j < FL_BR_N) P[sub + 16 * j] = vbr[j];
-        __syncthreads();
-    }
-    const uint8_t* PB = reinterpret_cast<const uint8_t*>(P + FL_BR_AT);
+    for (int j = 0; j < 24; j++)
+        if (sub + 16 * j < FL_BR_N) P[sub + 16 * j] = vbr[j];
+    __syncthreads();
+    const uint8_t* PB = reinterpret_cast<const uint8_t*>(P);
     const uint32_t cofs = (uint32_t)(18 * 4 * FL_BR_W + 18 + sh2) - RND_BITS * (uint32_t)(4 * FL_BR_W + 1);  // mod 2^32
     int tv0[16], tv1[16];
 #pragma unroll

@@ -454,29 +454,8 @@ ODO_INLINE void huber_rho(double delta, double chi, double rho[3]) {
 #define PNP_NW 4  // waves per pair
 #endif
 #define PNP_NT (64 * PNP_NW)
-#ifndef PNP_BUILD2
-#define PNP_BUILD2 0  // build pass: two edges per lane in lockstep (edge_build2)
-#endif
-#ifndef PNP_ALLSOLVE
-#define PNP_ALLSOLVE 0  // every wave solves the trials (no workgroup barrier around the solves)
-#endif
-#ifndef PNP_CHIM
-#define PNP_CHIM 1  // chi passes map points with the candidates' matrices (LDS, built once per candidate by its solver)
-#endif
-#ifndef PNP_RED1
-#define PNP_RED1 0  // workgroup sums with one barrier (two partial-sum buffers in turn)
-#endif
-#ifndef PNP_DPP
-#define PNP_DPP 0  // workgroup sums: cross-lane moves by permlane swaps / DPP instead of ds_bpermute
-#endif
-#ifndef PNP_CHI_LDS
-#define PNP_CHI_LDS 1  // LE: the chi passes' per-edge chi2 as floats in LDS (16 B per edge more)
-#endif
 #ifndef PNP_K
 #define PNP_K 4  // Levenberg trials evaluated per edge pass (one per 16-lane group of wave 0)
-#endif
-#ifndef PNP_SPD_SOLVE
-#define PNP_SPD_SOLVE 1  // trial solves without Eigen's pivoting (ldlt_solve6_spd; 0: pivoted)
 #endif
 static_assert(PNP_K <= 4, "the trial solves run on the four 16-lane groups of one wave");
 
@@ -492,45 +471,9 @@ struct Pow2Pad {
     static constexpr int v = NV <= 1 ? 1 : NV <= 2 ? 2 : NV <= 4 ? 4 : NV <= 8 ? 8 : NV <= 16 ? 16 : 32;
     static constexpr int lg = NV <= 1 ? 0 : NV <= 2 ? 1 : NV <= 4 ? 2 : NV <= 8 ? 3 : NV <= 16 ? 4 : 5;
 };
-// The partner lane's v at butterfly offset O (PNP_DPP): 32 / 16 by the gfx950
-// permlane swaps (lane l <-> l ^ 32, l ^ 16), 8 / 4 by the DPP row mirror /
-// half mirror (l <-> 15 - l, 7 - l within a row: partners that differ in bit
-// log2(O) and agree on every higher bit, so at that level they hold the same
-// value indices over disjoint lane sets), 2 / 1 by quad permutes (l ^ 2,
-// l ^ 1): VALU cross-lane moves instead of LDS round trips (ds_bpermute), a
-// fixed tree.
-template <int O>
-ODO_INLINE double lane_partner(double v) {
-    const int lane = threadIdx.x & 63;
-    const uint64_t u = (uint64_t)__double_as_longlong(v);
-    uint32_t lo = (uint32_t)u, hi = (uint32_t)(u >> 32);
-    if constexpr (O == 32 || O == 16) {
-        const bool up = (lane & O) != 0;
-        if constexpr (O == 32) {
-            const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
-            const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
-            lo = up ? a[0] : a[1];
-            hi = up ? b[0] : b[1];
-        } else {
-            const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
-            const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-            lo = up ? a[0] : a[1];
-            hi = up ? b[0] : b[1];
-        }
-    } else {
-        constexpr int ctrl = O == 8 ? 0x140 : O == 4 ? 0x141 : O == 2 ? 0x4E : 0xB1;
-        lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)lo, ctrl, 0xf, 0xf, false);
-        hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)hi, ctrl, 0xf, 0xf, false);
-    }
-    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-}
 template <int O>
 ODO_INLINE double xor_partner(double v) {
-#if PNP_DPP
-    return lane_partner<O>(v);
-#else
     return __shfl_xor(v, O);
-#endif
 }
 template <int NP, int O>
 ODO_INLINE void halving_level(double (&w)[NP], int lane) {
@@ -568,23 +511,14 @@ ODO_INLINE double wave_sum_transposed(const double (&v)[NV]) {
     x += xor_partner<1>(x);
     return x;  // total of value (lane >> (6 - LG)) over the wave
 }
-// PNP_RED1: two partial-sum buffers used in turn, so one barrier per sum: a
-// buffer is rewritten two sums later, after every wave has passed the other
-// sum's barrier (and with it, its own reads of this buffer)
 #define PNP_RED_WORDS (PNP_NW * 28)
 template <int NV>
-ODO_INLINE void wg_sum(double (&v)[NV], double* red, int& par) {
+ODO_INLINE void wg_sum(double (&v)[NV], double* red) {
     constexpr int LG = Pow2Pad<NV>::lg;
     const double x = wave_sum_transposed(v);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int j = lane >> (6 - LG);
     double* r = red;
-#if PNP_RED1
-    r += par * PNP_RED_WORDS;
-    par ^= 1;
-#else
-    (void)par;
-#endif
     if ((lane & ((1 << (6 - LG)) - 1)) == 0 && j < NV) r[wave * NV + j] = x;
     __syncthreads();
 #pragma unroll
@@ -593,9 +527,7 @@ ODO_INLINE void wg_sum(double (&v)[NV], double* red, int& par) {
         for (int w = 1; w < PNP_NW; w++) a += r[w * NV + k];
         v[k] = a;
     }
-#if !PNP_RED1
     __syncthreads();
-#endif
 }
 
 // computeActiveErrors + activeRobustChi2 + buildSystem contribution of one edge
@@ -658,67 +590,6 @@ ODO_INLINE void edge_build(const SE3M& T, const double Xw[3], const double ob[3]
         }
     }
 }
-
-// edge_build for two edges in lockstep (PNP_BUILD2): every statement for both
-// edges, branch-free (selects over values both sides compute), so the two
-// dependency chains issue interleaved on a wave that is alone on its SIMD.
-// has[k] false: edge k adds nothing. Each accumulator receives edge 0's term,
-// then edge 1's — the order of two consecutive edge_build calls — and every
-// term is formed by the same operations, so acc is bit-identical.
-#define EB2(...) _Pragma("unroll") for (int k = 0; k < 2; k++) { __VA_ARGS__; }
-ODO_INLINE void edge_build2(const SE3M& T, const double (&Xw)[2][3], const double (&ob)[2][3], const double (&info)[2],
-                            const uint8_t (&fl)[2], const bool (&has)[2], const PnPCam& cam, double dMono,
-                            double dStereo, double (&acc)[28]) {
-    bool st[2], rb[2];
-    double Xc[2][3], iz[2], izs[2], e[2][3], c2[2], rho0[2], r1[2];
-    EB2(st[k] = fl[k] & PE_STEREO; rb[k] = fl[k] & PE_ROBUST)
-    EB2(se3m_map(T, Xw[k], Xc[k]))
-    // edge_err: mono 1/z, stereo (float)(1/z) widened; the same products after
-    EB2(iz[k] = 1.0 / Xc[k][2])
-    EB2(izs[k] = st[k] ? (double)(float)iz[k] : iz[k])
-    EB2(const double q0 = Xc[k][0] * izs[k] * cam.fx + cam.cx; const double q1 = Xc[k][1] * izs[k] * cam.fy + cam.cy;
-        e[k][0] = ob[k][0] - q0; e[k][1] = ob[k][1] - q1; e[k][2] = st[k] ? ob[k][2] - (q0 - cam.bf * izs[k]) : 0.0)
-    EB2(const double a = e[k][0] * (info[k] * e[k][0]), b = e[k][1] * (info[k] * e[k][1]);
-        c2[k] = st[k] ? sum3d(a, b, e[k][2] * (info[k] * e[k][2])) : a + b)
-    // huber_rho (rho[0], rho[1]); not robust: (c2, 1)
-    EB2(const double dl = st[k] ? dStereo : dMono; const double dsqr = dl * dl; const double sq = sqrt(c2[k]);
-        const bool big = rb[k] & !(c2[k] <= dsqr);  // huber_rho's else branch, NaN included
-        rho0[k] = big ? 2 * sq * dl - dsqr : c2[k]; r1[k] = big ? dl / sq : 1.0)
-    double J[2][3][6], wo[2];
-    EB2(const double x = Xc[k][0], y = Xc[k][1], invz = iz[k], invz_2 = invz * invz;
-        J[k][0][0] = x * y * invz_2 * cam.fx; J[k][0][1] = -(1 + (x * x * invz_2)) * cam.fx;
-        J[k][0][2] = y * invz * cam.fx; J[k][0][3] = -invz * cam.fx; J[k][0][4] = 0; J[k][0][5] = x * invz_2 * cam.fx;
-        J[k][1][0] = (1 + y * y * invz_2) * cam.fy; J[k][1][1] = -x * y * invz_2 * cam.fy;
-        J[k][1][2] = -x * invz * cam.fy; J[k][1][3] = 0; J[k][1][4] = -invz * cam.fy; J[k][1][5] = y * invz_2 * cam.fy;
-        J[k][2][0] = st[k] ? J[k][0][0] - cam.bf * y * invz_2 : 0.0;
-        J[k][2][1] = st[k] ? J[k][0][1] + cam.bf * x * invz_2 : 0.0;
-        J[k][2][2] = st[k] ? J[k][0][2] : 0.0; J[k][2][3] = st[k] ? J[k][0][3] : 0.0; J[k][2][4] = 0;
-        J[k][2][5] = st[k] ? J[k][0][5] - cam.bf * invz_2 : 0.0;
-        wo[k] = r1[k] * info[k])
-    EB2(acc[27] = has[k] ? acc[27] + rho0[k] : acc[27])
-    constexpr bool Z[3][6] = {{false, false, false, false, true, false},
-                              {false, false, false, true, false, false},
-                              {false, false, false, false, true, false}};
-    int h = 0;
-#pragma unroll
-    for (int a = 0; a < 6; a++) {
-        double sb[2] = {0, 0};
-#pragma unroll
-        for (int kk = 0; kk < 3; kk++)
-            if (!Z[kk][a]) { EB2(sb[k] += J[k][kk][a] * (info[k] * e[k][kk])) }
-        EB2(acc[21 + a] = has[k] ? acc[21 + a] - r1[k] * sb[k] : acc[21 + a])
-#pragma unroll
-        for (int cc = a; cc < 6; cc++) {
-            double hh[2] = {0, 0};
-#pragma unroll
-            for (int kk = 0; kk < 3; kk++)
-                if (!Z[kk][a] && !Z[kk][cc]) { EB2(hh[k] += J[k][kk][a] * wo[k] * J[k][kk][cc]) }
-            EB2(acc[h] = has[k] ? acc[h] + hh[k] : acc[h])
-            h++;
-        }
-    }
-}
-#undef EB2
 
 // robust (Huber) chi2 of one edge at the quaternion pose T (the chi pass keeps
 // four candidates live: 7 doubles each instead of a matrix's 12)
@@ -783,14 +654,11 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
     if (sel && sel[p] != sel_val) return;  // pair handled by the other PnP launch
     const int lane = threadIdx.x;  // thread index within the workgroup
     const int wlane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    __shared__ double red[(PNP_RED1 ? 2 : 1) * PNP_RED_WORDS];
-    int rpar = 0;  // which red buffer the next workgroup sum takes (PNP_RED1)
+    __shared__ double red[PNP_RED_WORDS];
     __shared__ double s_acc[28];  // reduced H (upper, row-major), b, chi of the iteration
-    __shared__ double s_T[(PNP_ALLSOLVE ? PNP_NW : 1) * PNP_K][8];
-#if PNP_CHIM
-    __shared__ double s_M[(PNP_ALLSOLVE ? PNP_NW : 1) * PNP_K][12];  // the candidates as rotation matrix + translation (se3_mat)
-#endif
-    __shared__ int s_ok[(PNP_ALLSOLVE ? PNP_NW : 1) * PNP_K];
+    __shared__ double s_T[PNP_K][8];
+    __shared__ double s_M[PNP_K][12];  // the candidates as rotation matrix + translation (se3_mat)
+    __shared__ int s_ok[PNP_K];
     __shared__ int s_ne[PNP_NW];
     odo_pair_result* R = res + p;
     const int s1 = slot0 + p, s2 = slot0 + p + 1;
@@ -844,7 +712,7 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
         return;
     }
     // the chi2 each chi pass stores per edge and trial slot, read back by the
-    // classification only as (float)chi2: with LE and PNP_CHI_LDS the float
+    // classification only as (float)chi2: with LE the float
     // itself, in LDS (no global stores in the passes: every barrier would
     // wait for them)
     float* sC = nullptr;
@@ -854,7 +722,7 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
         float* sO = sX + 3 * kp_cap;    // 3 * kp_cap
         float* sI = sO + 3 * kp_cap;    // kp_cap
         uint8_t* sF = reinterpret_cast<uint8_t*>(sI + kp_cap);  // kp_cap
-        if (PNP_CHI_LDS) sC = reinterpret_cast<float*>(sF + kp_cap);  // 4 * kp_cap (kp_cap % 64 == 0)
+        sC = reinterpret_cast<float*>(sF + kp_cap);  // 4 * kp_cap (kp_cap % 64 == 0)
         for (int k = lane; k < 3 * ne; k += PNP_NT) {
             sX[k] = E.X[k];
             sO[k] = E.obs[k];
@@ -907,20 +775,6 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
             for (int k = 0; k < 28; k++) acc[k] = 0;
             {
                 const SE3M Tm = se3_mat(T);
-#if PNP_BUILD2
-                // edges k and k + PNP_NT together (the lane's order: k, k + NT, k + 2 NT, ...)
-                for (int k = lane; k < ne; k += 2 * PNP_NT) {
-                    const int k2 = k + PNP_NT < ne ? k + PNP_NT : k;
-                    const uint8_t f2[2] = {E.flags[k], E.flags[k2]};
-                    const bool has[2] = {!(f2[0] & PE_OUT), k + PNP_NT < ne && !(f2[1] & PE_OUT)};
-                    const double Xw2[2][3] = {{E.X[3 * k], E.X[3 * k + 1], E.X[3 * k + 2]},
-                                              {E.X[3 * k2], E.X[3 * k2 + 1], E.X[3 * k2 + 2]}};
-                    const double ob2[2][3] = {{E.obs[3 * k], E.obs[3 * k + 1], E.obs[3 * k + 2]},
-                                              {E.obs[3 * k2], E.obs[3 * k2 + 1], E.obs[3 * k2 + 2]}};
-                    const double in2[2] = {(double)E.info[k], (double)E.info[k2]};
-                    edge_build2(Tm, Xw2, ob2, in2, f2, has, cam, dMono, dStereo, acc);
-                }
-#else
                 for (int k = lane; k < ne; k += PNP_NT) {
                     const uint8_t fl = E.flags[k];
                     if (fl & PE_OUT) continue;
@@ -928,14 +782,13 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                     const double ob[3] = {E.obs[3 * k], E.obs[3 * k + 1], E.obs[3 * k + 2]};
                     edge_build(Tm, Xw, ob, (double)E.info[k], fl, cam, dMono, dStereo, acc);
                 }
-#endif
             }
-            wg_sum<28>(acc, red, rpar);
+            wg_sum<28>(acc, red);
             PP_ACC(tb);
 #ifdef ODO_PNP_PROFILE
             nit++;
 #endif
-            if (!PNP_ALLSOLVE && lane == 0)
+            if (lane == 0)
 #pragma unroll
                 for (int k = 0; k < 28; k++) s_acc[k] = acc[k];
             double curChi = acc[27];
@@ -951,7 +804,7 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                 lambda = 1e-5 * mx;
                 ni = 2;
             }
-            if (!PNP_ALLSOLVE) __syncthreads();
+            __syncthreads();
             // ---- OptimizationAlgorithmLevenberg::solve trial loop, PNP_K trials per pass
             double rho = 0;
             int qmax = 0;
@@ -974,15 +827,8 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                 // the K trial solves on wave 0's four 16-lane groups (group g =
                 // trial g): the same per-lane arithmetic as one wave per trial,
                 // a quarter of the issued FP64 instructions
-#ifndef ODO_PNP_GROUP_TRIALS
-#define ODO_PNP_GROUP_TRIALS 1  // 0: one wave per trial (A/B)
-#endif
-                const int tg = ODO_PNP_GROUP_TRIALS ? wlane >> 4 : wave;
-                // PNP_ALLSOLVE: every wave solves the K trials itself (the same
-                // operations on the same values as wave 0 would), into its own
-                // LDS slots: no workgroup barrier around the solves
-                const int tb = PNP_ALLSOLVE ? wave * PNP_K : 0;
-                if ((PNP_ALLSOLVE || (ODO_PNP_GROUP_TRIALS ? wave == 0 : true)) && tg < K) {
+                const int tg = wlane >> 4;
+                if (wave == 0 && tg < K) {
                     double lw = lam[0];
 #pragma unroll
                     for (int k = 1; k < PNP_K; k++)
@@ -994,23 +840,19 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                         for (int a = 0; a < 6; a++)
 #pragma unroll
                             for (int cc = a; cc < 6; cc++) {
-                                Hl[a][cc] = PNP_ALLSOLVE ? acc[h] : s_acc[h];
-                                Hl[cc][a] = PNP_ALLSOLVE ? acc[h] : s_acc[h];
+                                Hl[a][cc] = s_acc[h];
+                                Hl[cc][a] = s_acc[h];
                                 h++;
                             }
 #pragma unroll
-                        for (int a = 0; a < 6; a++) b[a] = PNP_ALLSOLVE ? acc[21 + a] : s_acc[21 + a];
+                        for (int a = 0; a < 6; a++) b[a] = s_acc[21 + a];
                     }
                     for (int j = 0; j < 6; j++) Hl[j][j] += lw;
                     double x[6] = {0, 0, 0, 0, 0, 0};
 #ifdef ODO_PNP_PROFILE
                     const uint64_t ts0 = wall_clock64();
 #endif
-#if PNP_SPD_SOLVE
                     const bool ok2 = ldlt_solve6_spd(Hl, b, x);
-#else
-                    const bool ok2 = ldlt_solve6(Hl, b, x);
-#endif
 #ifdef ODO_PNP_PROFILE
                     const uint64_t ts1 = wall_clock64();
 #endif
@@ -1024,44 +866,35 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                     double scale = 0;
                     for (int j = 0; j < 6; j++) scale += x[j] * (lw * x[j] + b[j]);
                     scale += 1e-3;
-                    if ((wlane & (ODO_PNP_GROUP_TRIALS ? 15 : 63)) == 0) {
-                        s_T[tb + tg][0] = Tk.q.x;
-                        s_T[tb + tg][1] = Tk.q.y;
-                        s_T[tb + tg][2] = Tk.q.z;
-                        s_T[tb + tg][3] = Tk.q.w;
-                        s_T[tb + tg][4] = Tk.t[0];
-                        s_T[tb + tg][5] = Tk.t[1];
-                        s_T[tb + tg][6] = Tk.t[2];
-                        s_T[tb + tg][7] = scale;
-                        s_ok[tb + tg] = ok2 ? 1 : 0;
-#if PNP_CHIM
+                    if ((wlane & 15) == 0) {
+                        s_T[tg][0] = Tk.q.x;
+                        s_T[tg][1] = Tk.q.y;
+                        s_T[tg][2] = Tk.q.z;
+                        s_T[tg][3] = Tk.q.w;
+                        s_T[tg][4] = Tk.t[0];
+                        s_T[tg][5] = Tk.t[1];
+                        s_T[tg][6] = Tk.t[2];
+                        s_T[tg][7] = scale;
+                        s_ok[tg] = ok2 ? 1 : 0;
                         const SE3M Mk = se3_mat(Tk);
 #pragma unroll
-                        for (int q = 0; q < 9; q++) s_M[tb + tg][q] = Mk.R[q];
+                        for (int q = 0; q < 9; q++) s_M[tg][q] = Mk.R[q];
 #pragma unroll
-                        for (int q = 0; q < 3; q++) s_M[tb + tg][9 + q] = Mk.t[q];
-#endif
+                        for (int q = 0; q < 3; q++) s_M[tg][9 + q] = Mk.t[q];
                     }
                 }
-                if (PNP_ALLSOLVE) {
-                    // the wave's own slots: wave-scope ordering
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                } else {
-                    __syncthreads();
-                }
+                __syncthreads();
                 SE3 Tc[PNP_K];
                 double sc[PNP_K];
                 bool okc[PNP_K];
 #pragma unroll
                 for (int k = 0; k < PNP_K; k++) {
-                    Tc[k].q = Quat{s_T[tb + k][0], s_T[tb + k][1], s_T[tb + k][2], s_T[tb + k][3]};
-                    Tc[k].t[0] = s_T[tb + k][4];
-                    Tc[k].t[1] = s_T[tb + k][5];
-                    Tc[k].t[2] = s_T[tb + k][6];
-                    sc[k] = s_T[tb + k][7];
-                    okc[k] = s_ok[tb + k] != 0;
+                    Tc[k].q = Quat{s_T[k][0], s_T[k][1], s_T[k][2], s_T[k][3]};
+                    Tc[k].t[0] = s_T[k][4];
+                    Tc[k].t[1] = s_T[k][5];
+                    Tc[k].t[2] = s_T[k][6];
+                    sc[k] = s_T[k][7];
+                    okc[k] = s_ok[k] != 0;
                 }
                 PP_ACC(tsol);
                 PP_T0();
@@ -1079,21 +912,17 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                     for (int k = 0; k < PNP_K; k++) {
                         if (k >= K) break;
                         double c2;
-#if PNP_CHIM
                         SE3M Mk;
 #pragma unroll
-                        for (int q = 0; q < 9; q++) Mk.R[q] = s_M[tb + k][q];
+                        for (int q = 0; q < 9; q++) Mk.R[q] = s_M[k][q];
 #pragma unroll
-                        for (int q = 0; q < 3; q++) Mk.t[q] = s_M[tb + k][9 + q];
+                        for (int q = 0; q < 3; q++) Mk.t[q] = s_M[k][9 + q];
                         chi[k] += edge_robust_chi(Mk, Xw, ob, info, fl, cam, dMono, dStereo, c2);
-#else
-                        chi[k] += edge_robust_chi_q(Tc[k], Xw, ob, info, fl, cam, dMono, dStereo, c2);
-#endif
-                        if (LE && PNP_CHI_LDS) sC[4 * e + k] = (float)c2;
+                        if (LE) sC[4 * e + k] = (float)c2;
                         else E.chi4[4 * e + k] = c2;
                     }
                 }
-                wg_sum<PNP_K>(chi, red, rpar);
+                wg_sum<PNP_K>(chi, red);
                 PP_ACC(tchi);
                 // replay the trials in order
 #pragma unroll
@@ -1143,10 +972,10 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                     const double c2 = chi2_of(e, info, st);
                     // (never read back: an edge out during the next round is
                     // recomputed here, one in is rewritten by its chi passes)
-                    if (!(LE && PNP_CHI_LDS)) E.chi4[4 * k + last_slot] = c2;
+                    if (!LE) E.chi4[4 * k + last_slot] = c2;
                     chi2 = (float)c2;
                 } else {
-                    chi2 = (LE && PNP_CHI_LDS) ? sC[4 * k + last_slot] : (float)E.chi4[4 * k + last_slot];
+                    chi2 = LE ? sC[4 * k + last_slot] : (float)E.chi4[4 * k + last_slot];
                 }
                 if (chi2 > (st ? chi2Stereo : chi2Mono)) {
                     fl |= PE_OUT;
@@ -1165,7 +994,7 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
             }
         }
         double bd[1] = {(double)bad};
-        wg_sum<1>(bd, red, rpar);
+        wg_sum<1>(bd, red);
         nBad = (int)bd[0];
         PP_ACC(tcls);
         if (ne < 10) break;
@@ -1190,335 +1019,6 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
 }
 
 
-// ---------------------------------------------------------------- one wave per pair
-// The same PnPSolver::Compute with ONE wave per pair: the batched path runs
-// 256 pairs at once beside the next batch's extraction, so what matters is
-// the PnP's footprint on the CUs, not one pair's latency. A wave needs no
-// barriers: edge sums are xor-butterflies, the normal equations are read
-// into scalar registers, and the PNP_K speculative Levenberg trials are
-// solved by the wave's four 16-lane groups at once (each group runs the LDLT,
-// exp map and composition of its lambda; the candidates are broadcast from
-// lanes 0/16/32/48). Edges are an AoS record per edge (two float4 + index)
-// in the pair's scratch, streamed each pass.
-struct PEdge1 {
-    float4* a;     // X.x X.y X.z info
-    float4* b;     // obs u v uR(0 mono) | flags (int bits)
-    int* idx;      // F2 keypoint index
-    double* chi4;  // chi2 of the stored _error per trial slot
-};
-ODO_INLINE PEdge1 pedge1_view(void* base, int cap, int p) {
-    char* bp = (char*)base + (size_t)p * (size_t)cap * PE_BYTES;
-    PEdge1 E;
-    E.chi4 = (double*)bp;
-    E.a = (float4*)(bp + (size_t)cap * 32);
-    E.b = E.a + cap;
-    E.idx = (int*)(E.b + cap);
-    return E;
-}
-
-// sum of v over the wave, the result in every lane (fixed butterfly)
-template <int NV>
-ODO_INLINE void wave_allsum(double (&v)[NV]) {
-    constexpr int LG = Pow2Pad<NV>::lg;
-    const double x = wave_sum_transposed(v);  // lane l: total of value l >> (6 - LG)
-#pragma unroll
-    for (int k = 0; k < NV; k++) v[k] = __shfl(x, k << (6 - LG));
-}
-
-#ifdef ODO_TUNING  // retired one-wave-per-pair form (A/B only: the tuning build)
-__global__ void __launch_bounds__(64) k_pnp1(const int32_t* __restrict__ f2_src, const float* __restrict__ xyz,
-                                             const float* __restrict__ kun, const float* __restrict__ ur,
-                                             const int* __restrict__ nkp, int kp_cap, int slot0, FrameCalib cal,
-                                             const float* __restrict__ T12, const int* __restrict__ pair_valid,
-                                             const int* __restrict__ n_matches, int min_matches, void* edges_g,
-                                             odo_pair_result* __restrict__ res, uint8_t* __restrict__ inlier_mask,
-                                             const int* __restrict__ sel, int sel_val) {
-    __builtin_amdgcn_s_setprio(ODO_PNP_PRIO);
-    const int p = blockIdx.x;
-    if (sel && sel[p] != sel_val) return;
-    const int lane = threadIdx.x;
-    odo_pair_result* R = res + p;
-    const int s1 = slot0 + p, s2 = slot0 + p + 1;
-    const int n2 = nkp[s2];
-    uint8_t* mask = inlier_mask + (size_t)p * kp_cap;
-    for (int i = lane; i < n2; i += 64) mask[i] = 0;
-    const float* T0 = T12 + (size_t)p * 16;
-    if (lane < 16) R->Tcw[lane] = T0[lane];
-    if (lane == 0) R->pnp_inliers = 0;
-    if (!pair_valid[p] || n_matches[p] < min_matches) return;
-    // ---- edges: F2 keypoints holding a landmark, index order (pnpsolver.cpp:57-135)
-    const int32_t* src = f2_src + (size_t)p * kp_cap;
-    const float* X1 = xyz + (size_t)s1 * kp_cap * 3;
-    const float* K2 = kun + (size_t)s2 * kp_cap * 2;
-    const float* U2 = ur + (size_t)s2 * kp_cap;
-    PEdge1 E = pedge1_view(edges_g, kp_cap, p);
-    int ne = 0;
-    for (int c0 = 0; c0 < n2; c0 += 64) {
-        const int i = c0 + lane;
-        const bool has = i < n2 && src[i] >= 0;
-        const uint64_t bal = __ballot(has);
-        if (has) {
-            const int k = ne + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
-            const int s = src[i];
-            const float zw = X1[3 * s + 2];
-            const float urv = U2[i];
-            const bool st = !(urv < 0);
-            E.a[k] = make_float4(X1[3 * s], X1[3 * s + 1], zw, 1.0f / (zw * zw));
-            E.b[k] = make_float4(K2[2 * i], K2[2 * i + 1], st ? urv : 0.f,
-                                 __int_as_float((st ? PE_STEREO : 0) | PE_ROBUST));
-            E.idx[k] = i;
-        }
-        ne += __popcll(bal);
-    }
-    if (ne < 3) {
-        for (int k = lane; k < ne; k += 64) mask[E.idx[k]] = 1;  // SetInlier at edge creation
-        return;
-    }
-    const PnPCam cam{(double)cal.fx, (double)cal.fy, (double)cal.cx, (double)cal.cy, (double)cal.mbf};
-    const double dMono = (double)(float)sqrt(5.991), dStereo = (double)(float)sqrt(7.815);  // pnpsolver.cpp:51-52
-    SE3 T0s;
-    {
-        double R0[3][3], t0[3];
-        for (int i = 0; i < 3; i++) {
-            for (int j = 0; j < 3; j++) R0[i][j] = (double)T0[i * 4 + j];
-            t0[i] = (double)T0[i * 4 + 3];
-        }
-        T0s.q = quat_from_R(R0);
-        for (int i = 0; i < 3; i++) T0s.t[i] = t0[i];
-        normalize_rot(T0s);
-    }
-    const float chi2Mono = 5.991f, chi2Stereo = 7.815f;
-    int nBad = 0;
-    SE3 T = T0s;
-    int last_slot = 0;
-    const int grp = lane >> 4;  // Levenberg trial of this lane group
-    for (int it = 0; it < 4; it++) {
-        T = T0s;  // vSE3->setEstimate(pFrame->GetPose()) (pnpsolver.cpp:150)
-        double lambda = 0, ni = 2;
-        for (int iter = 0; iter < 10; iter++) {
-            // computeActiveErrors + activeRobustChi2 + buildSystem at T
-            double acc[28];
-#pragma unroll
-            for (int k = 0; k < 28; k++) acc[k] = 0;
-            for (int k = lane; k < ne; k += 64) {
-                const float4 ea = E.a[k], eb = E.b[k];
-                const uint8_t fl = (uint8_t)__float_as_int(eb.w);
-                if (fl & PE_OUT) continue;
-                const bool st = fl & PE_STEREO;
-                const double Xw[3] = {ea.x, ea.y, ea.z};
-                const double ob[3] = {eb.x, eb.y, eb.z};
-                const double info = ea.w;
-                double Xc[3], e[3];
-                se3_map(T, Xw, Xc);
-                edge_err(Xc, ob, st, cam, e);
-                const double c2 = chi2_of(e, info, st);
-                double rho[3] = {c2, 1.0, 0.0};
-                if (fl & PE_ROBUST) huber_rho(st ? dStereo : dMono, c2, rho);
-                acc[27] += rho[0];
-                const double x = Xc[0], y = Xc[1], invz = 1.0 / Xc[2], invz_2 = invz * invz;
-                double J[3][6];
-                J[0][0] = x * y * invz_2 * cam.fx;
-                J[0][1] = -(1 + (x * x * invz_2)) * cam.fx;
-                J[0][2] = y * invz * cam.fx;
-                J[0][3] = -invz * cam.fx;
-                J[0][4] = 0;
-                J[0][5] = x * invz_2 * cam.fx;
-                J[1][0] = (1 + y * y * invz_2) * cam.fy;
-                J[1][1] = -x * y * invz_2 * cam.fy;
-                J[1][2] = -x * invz * cam.fy;
-                J[1][3] = 0;
-                J[1][4] = -invz * cam.fy;
-                J[1][5] = y * invz_2 * cam.fy;
-                J[2][0] = st ? J[0][0] - cam.bf * y * invz_2 : 0.0;
-                J[2][1] = st ? J[0][1] + cam.bf * x * invz_2 : 0.0;
-                J[2][2] = st ? J[0][2] : 0.0;
-                J[2][3] = st ? J[0][3] : 0.0;
-                J[2][4] = 0;
-                J[2][5] = st ? J[0][5] - cam.bf * invz_2 : 0.0;
-                const double r1 = rho[1];
-                const double wo = r1 * info;
-                int h = 0;
-#pragma unroll
-                for (int a = 0; a < 6; a++) {
-                    double sb = 0;
-#pragma unroll
-                    for (int kk = 0; kk < 3; kk++) sb += J[kk][a] * (info * e[kk]);
-                    acc[21 + a] -= r1 * sb;
-#pragma unroll
-                    for (int cc = a; cc < 6; cc++) {
-                        double hh = 0;
-#pragma unroll
-                        for (int kk = 0; kk < 3; kk++) hh += J[kk][a] * wo * J[kk][cc];
-                        acc[h++] += hh;
-                    }
-                }
-            }
-            wave_allsum<28>(acc);
-            double curChi = acc[27];
-            if (iter == 0) {
-                double mx = 0;  // diagonal of the packed upper triangle: 0, 6, 11, 15, 18, 20
-                mx = fmax(fabs(acc[0]), mx);
-                mx = fmax(fabs(acc[6]), mx);
-                mx = fmax(fabs(acc[11]), mx);
-                mx = fmax(fabs(acc[15]), mx);
-                mx = fmax(fabs(acc[18]), mx);
-                mx = fmax(fabs(acc[20]), mx);
-                lambda = 1e-5 * mx;
-                ni = 2;
-            }
-            // ---- OptimizationAlgorithmLevenberg::solve trial loop, PNP_K trials per pass
-            double rho = 0;
-            int qmax = 0;
-            bool trials_done = false;
-            while (!trials_done) {
-                const int K = min(PNP_K, 10 - qmax);
-                double lam[PNP_K], nis[PNP_K];
-                {
-                    double l = lambda, n_ = ni;
-#pragma unroll
-                    for (int k = 0; k < PNP_K; k++) {
-                        lam[k] = l;
-                        nis[k] = n_;
-                        l *= n_;
-                        n_ *= 2;
-                    }
-                }
-                // lane group grp solves trial grp
-                double lw = lam[0];
-#pragma unroll
-                for (int k = 1; k < PNP_K; k++)
-                    if (grp == k) lw = lam[k];
-                double Hl[6][6], b[6];
-                {
-                    int h = 0;
-#pragma unroll
-                    for (int a = 0; a < 6; a++)
-#pragma unroll
-                        for (int cc = a; cc < 6; cc++) {
-                            Hl[a][cc] = acc[h];
-                            Hl[cc][a] = acc[h];
-                            h++;
-                        }
-#pragma unroll
-                    for (int a = 0; a < 6; a++) b[a] = acc[21 + a];
-                }
-#pragma unroll
-                for (int j = 0; j < 6; j++) Hl[j][j] += lw;
-                double x[6] = {0, 0, 0, 0, 0, 0};
-                const bool ok2 = ldlt_solve6(Hl, b, x);
-                const SE3 Tk = se3_mul(se3_exp(x), T);
-                double scale = 0;
-                for (int j = 0; j < 6; j++) scale += x[j] * (lw * x[j] + b[j]);
-                scale += 1e-3;
-                SE3 Tc[PNP_K];
-                double sc[PNP_K];
-                bool okc[PNP_K];
-#pragma unroll
-                for (int k = 0; k < PNP_K; k++) {
-                    const int sl = 16 * k;
-                    Tc[k].q = Quat{__shfl(Tk.q.x, sl), __shfl(Tk.q.y, sl), __shfl(Tk.q.z, sl), __shfl(Tk.q.w, sl)};
-                    Tc[k].t[0] = __shfl(Tk.t[0], sl);
-                    Tc[k].t[1] = __shfl(Tk.t[1], sl);
-                    Tc[k].t[2] = __shfl(Tk.t[2], sl);
-                    sc[k] = __shfl(scale, sl);
-                    okc[k] = __shfl(ok2 ? 1 : 0, sl) != 0;
-                }
-                // computeActiveErrors + activeRobustChi2 at every candidate
-                double chi[PNP_K];
-#pragma unroll
-                for (int k = 0; k < PNP_K; k++) chi[k] = 0;
-                for (int e = lane; e < ne; e += 64) {
-                    const float4 ea = E.a[e], eb = E.b[e];
-                    const uint8_t fl = (uint8_t)__float_as_int(eb.w);
-                    if (fl & PE_OUT) continue;
-                    const double Xw[3] = {ea.x, ea.y, ea.z};
-                    const double ob[3] = {eb.x, eb.y, eb.z};
-                    const double info = ea.w;
-#pragma unroll
-                    for (int k = 0; k < PNP_K; k++) {
-                        if (k >= K) break;
-                        double c2;
-                        chi[k] += edge_robust_chi(se3_mat(Tc[k]), Xw, ob, info, fl, cam, dMono, dStereo, c2);
-                        E.chi4[4 * e + k] = c2;
-                    }
-                }
-                wave_allsum<PNP_K>(chi);
-                // replay the trials in order
-#pragma unroll
-                for (int k = 0; k < PNP_K; k++) {
-                    if (k >= K || trials_done) break;
-                    double tempChi = chi[k];
-                    if (!okc[k]) tempChi = 1.7976931348623157e308;
-                    rho = curChi - tempChi;
-                    rho /= sc[k];
-                    last_slot = k;
-                    qmax++;
-                    if (rho > 0 && isfinite(tempChi)) {
-                        double alpha = 1. - pow((2 * rho - 1), 3);
-                        alpha = fmin(alpha, 2. / 3.);
-                        const double sf = fmax(1. / 3., alpha);
-                        lambda = lam[k] * sf;
-                        ni = 2;
-                        curChi = tempChi;
-                        T = Tc[k];
-                        trials_done = true;
-                    } else {
-                        lambda = lam[k] * nis[k];  // T stays at the backup
-                        ni = nis[k] * 2;
-                        if (!(rho < 0 && qmax < 10)) trials_done = true;
-                    }
-                }
-            }
-            if (qmax == 10 || rho == 0) break;
-        }
-        // ---- classification (pnpsolver.cpp:157-201)
-        int bad = 0;
-        for (int k = lane; k < ne; k += 64) {
-            float4 eb = E.b[k];
-            uint8_t fl = (uint8_t)__float_as_int(eb.w);
-            const bool st = fl & PE_STEREO;
-            double c2 = E.chi4[4 * k + last_slot];
-            if (fl & PE_OUT) {  // IsOutlier: e->computeError() at the current estimate
-                const float4 ea = E.a[k];
-                const double Xw[3] = {ea.x, ea.y, ea.z};
-                const double ob[3] = {eb.x, eb.y, eb.z};
-                double Xc[3], e[3];
-                se3_map(T, Xw, Xc);
-                edge_err(Xc, ob, st, cam, e);
-                c2 = chi2_of(e, (double)ea.w, st);
-                E.chi4[4 * k + last_slot] = c2;
-            }
-            const float chi2 = (float)c2;
-            if (chi2 > (st ? chi2Stereo : chi2Mono)) {
-                fl |= PE_OUT;
-                bad++;
-            } else {
-                fl &= ~PE_OUT;
-            }
-            if (it == 2) fl &= ~PE_ROBUST;
-            eb.w = __int_as_float((int)fl);
-            E.b[k] = eb;
-        }
-        double bd[1] = {(double)bad};
-        wave_allsum<1>(bd);
-        nBad = (int)bd[0];
-        if (ne < 10) break;
-    }
-    if (lane == 0) {
-        double Rm[3][3];
-        quat_to_R(T.q, Rm);
-        for (int i = 0; i < 3; i++) {
-            for (int j = 0; j < 3; j++) R->Tcw[i * 4 + j] = (float)Rm[i][j];
-            R->Tcw[i * 4 + 3] = (float)T.t[i];
-        }
-        R->Tcw[12] = R->Tcw[13] = R->Tcw[14] = 0.f;
-        R->Tcw[15] = 1.f;
-        R->pnp_inliers = ne - nBad;
-    }
-    for (int k = lane; k < ne; k += 64)
-        mask[E.idx[k]] = ((uint8_t)__float_as_int(E.b[k].w) & PE_OUT) ? 0 : 1;
-}
-#endif  // ODO_TUNING
 
 }  // namespace odo
 
@@ -1534,32 +1034,17 @@ static size_t pnp_lds_bytes(int kp_cap) {
         const char* e = odo_knob("ODO_PNP_LDS");
         return e && e[0] == '0';
     }();
-    const size_t b = ((size_t)kp_cap * (PNP_CHI_LDS ? 45 : 29) + 15) & ~(size_t)15;
+    const size_t b = ((size_t)kp_cap * 45 + 15) & ~(size_t)15;
     return (!off && b <= PNP_LDS_MAX) ? b : 0;
 }
-// The 4-wave workgroup per pair (k_pnp) by default. ODO_PNP_WAVES=1 selects
-// k_pnp1 (one wave per pair: a quarter of the SIMDs occupied), measured
-// slower: PnP 1.66 vs 0.72 ms alone per 256 pairs, step 2.61 vs 2.50 ms, one
-// frame 0.65 vs 0.49 ms — the solver is latency-bound per pair, and the freed
-// SIMDs do not buy back the 4x longer edge passes.
-static int pnp_waves() {
-    static int r = [] {
-        const char* e = odo_knob("ODO_PNP_WAVES");
-        return e && atoi(e) == 1 ? 1 : 4;
-    }();
-    return r;
-}
+// The 4-wave workgroup per pair (k_pnp). Measured and retired: one wave per
+// pair (round 2: PnP 1.66 vs 0.72 ms alone per 256 pairs, step 2.61 vs
+// 2.50 ms, one frame 0.65 vs 0.49 ms — the solver is latency-bound per pair,
+// and the freed SIMDs do not buy back the 4x longer edge passes).
 void launch_pnp(hipStream_t st, const int32_t* f2_src, const float* xyz, const float* kun, const float* ur,
                 const int* nkp, int kp_cap, int slot0, FrameCalib cal, const float* T12, const int* pair_valid,
                 const int* n_matches, int min_matches, void* edges, odo_pair_result* res, uint8_t* inlier_mask,
                 int npairs, const int* sel, int sel_val) {
-#ifdef ODO_TUNING
-    if (pnp_waves() == 1) {
-        hipLaunchKernelGGL(k_pnp1, dim3(npairs), dim3(64), 0, st, f2_src, xyz, kun, ur, nkp, kp_cap, slot0, cal, T12,
-                           pair_valid, n_matches, min_matches, edges, res, inlier_mask, sel, sel_val);
-        return;
-    }
-#endif
     const size_t lds = pnp_lds_bytes(kp_cap);
     if (lds) {
         static bool attr = false;

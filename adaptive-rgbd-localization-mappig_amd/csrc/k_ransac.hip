@@ -40,12 +40,6 @@ struct GoodPt {
 };
 
 #define EV_WAVES_C 4   // waves per k_ransac_eval workgroup (EV_WAVES below)
-#ifndef EV_ILP2
-#define EV_ILP2 0  // eval kernels' sweep: two 64-point chunks per pass, interleaved straight-line evaluations
-#endif
-#ifndef EV_MARKSTEIN
-#define EV_MARKSTEIN 1  // eval kernels' sweep: Markstein-corrected quotients (error_function2_mk)
-#endif
 #ifndef EV2_FOLD_WAVE
 #define EV2_FOLD_WAVE 1  // the second launch's ordered fold by the whole wave (0: lane 0)
 #endif
@@ -1050,46 +1044,6 @@ ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int 
             // ---- ComputeInliersAndError (ransac.cpp:315-348)
             double meanError = 0.0;
             unsigned cnt = 0;
-#if EV_ILP2
-            // two 64-point chunks per pass: their evaluations (straight-line,
-            // interleaved) first, then each chunk's ballot and ordered fold
-            double Tq[2][12];
-#pragma unroll
-            for (int i = 0; i < 12; i++) Tq[0][i] = Tq[1][i] = Td[i];
-            for (int c0 = 0; c0 < ng; c0 += 128) {
-                float xa[2][3], xb[2][3];
-                bool ok[2];
-#pragma unroll
-                for (int hh = 0; hh < 2; hh++) {
-                    const int k = c0 + 64 * hh + lane;
-                    GoodPt g{};
-                    if (k < ng) g = load_pt<CACHED>(P, k);
-                    ok[hh] = k < ng && !(g.sz == 0.0f || g.tx == 0.0f);
-                    xa[hh][0] = g.sx, xa[hh][1] = g.sy, xa[hh][2] = g.sz;
-                    xb[hh][0] = g.tx, xb[hh][1] = g.ty, xb[hh][2] = g.tz;
-                }
-                double e[2];
-                error_function2_bf2(xa, xb, Tq, K, e);
-#pragma unroll
-                for (int hh = 0; hh < 2; hh++) {
-                    const int cc = c0 + 64 * hh;
-                    if (cc >= ng) break;
-                    const double d = e[hh];
-                    const bool in = ok[hh] && !(d > th) && (d >= 0.0);
-                    const uint64_t bal = __ballot(in);
-                    if (in) L.dv[lane_rank(bal)] = d;
-                    if (lane == 0) {
-                        L.nw[cc >> 5] = (uint32_t)bal;
-                        if (cc + 32 < ng) L.nw[(cc >> 5) + 1] = (uint32_t)(bal >> 32);
-                    }
-                    wave_sync();
-                    const int nin = __popcll(bal);
-                    if (lane == 0) meanError = fold_dv(L, nin, meanError);
-                    cnt += (unsigned)nin;
-                    wave_sync();
-                }
-            }
-#else
             for (int c0 = 0; c0 < ng; c0 += 64) {
                 const int k = c0 + lane;
                 bool in = false;
@@ -1098,11 +1052,7 @@ ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int 
                     const GoodPt g = load_pt<CACHED>(P, k);
                     if (!(g.sz == 0.0f || g.tx == 0.0f)) {
                         const float x1[3] = {g.sx, g.sy, g.sz}, x2[3] = {g.tx, g.ty, g.tz};
-#if EV_MARKSTEIN
                         d = error_function2_mk(x1, x2, Td, K);
-#else
-                        d = error_function2(x1, x2, Td, K);
-#endif
                         in = !(d > th) && (d >= 0.0);
                     }
                 }
@@ -1118,7 +1068,6 @@ ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int 
                 cnt += (unsigned)nin;
                 wave_sync();
             }
-#endif
             meanError = __shfl(meanError, 0);
             RP_ACC(t_sweep);
             // the fold already stopped before this hypothesis: nothing will read it
@@ -1313,49 +1262,13 @@ ODO_INLINE double readlane_d(double v, int l) {
 #ifndef LN_SLOTS
 #define LN_SLOTS 32  // lanes per wave that take up hypotheses (rows of parked terms per wave)
 #endif
-#ifndef LN_HELP
-#define LN_HELP 0  // 1: a wave whose pair has no hypothesis left joins another open pair that has
-#endif
-#ifndef LN_MARKSTEIN
-#define LN_MARKSTEIN 1  // sweep: ErrorFunction2 with Markstein-corrected quotients (0: IEEE divisions)
-#endif
-#ifndef LN_BPERM
-#define LN_BPERM 1  // sweep: hypothesis transforms by ds_bpermute (0: v_readlane pairs)
-#endif
-#ifndef LN_ILP2
-#define LN_ILP2 0  // sweep: two straight-line evaluations per lane and pass (error_function2_bf)
-#endif
-#ifndef LN_TFCU
-#define LN_TFCU 1  // refinement TFC: four points per step, branch-free adds (TFC::add_sel)
-#endif
-#ifndef LN_BAL
-#define LN_BAL 1  // waves per open pair in proportion to its good matches (lane limit per wave)
-#endif
 #ifndef LN_PRIO
 #define LN_PRIO ODO_WAVE_PRIO  // k_ransac_lanes' wave priority
-#endif
-#ifndef LN_TLDS
-#define LN_TLDS 1  // sweep: transforms from an LDS slot table (LN_SLOTS <= 48 fits two workgroups per CU)
-#endif
-#ifndef LN_PRE
-#define LN_PRE 0  // sweep: transforms permuted as doubles with their point-independent covariance terms
 #endif
 #ifndef LN_BAL_EXP
 #define LN_BAL_EXP 1  // LN_BAL weight: (good matches + 1) ^ LN_BAL_EXP (1 or 2)
 #endif
 ODO_INLINE int ln_weight(int ng) { return LN_BAL_EXP == 2 ? ((ng + 1) * (ng + 1) + 63) >> 6 : ng + 1; }
-#ifndef LN_TFCG
-#define LN_TFCG 0  // refinement TFC of few refining lanes by 9-lane groups (<= LN_TFCG_MAX lanes)
-#endif
-#ifndef LN_TFCG_MAX
-#define LN_TFCG_MAX 14
-#endif
-#ifndef LN_COMPACT
-#define LN_COMPACT 0  // sweep: shortcut test for every pair first, full evaluations only for the survivors
-#endif
-#ifndef LN_SUMB
-#define LN_SUMB 1  // sweep: a full chunk's parked terms read 8 at a time before the ordered sum
-#endif
 #ifdef ODO_LANES_PROFILE
 // -DODO_LANES_PROFILE: per wave of the last k_ransac_lanes launch: start, end,
 // loop rounds, sum of active lanes over the rounds, TFC / sweep ticks and the
@@ -1367,7 +1280,7 @@ __device__ uint64_t g_lprof[LPROF_MAX * 10];
 #else
 #define LP(...)
 #endif
-static_assert(LN_SLOTS <= 64 && !(LN_ILP2 && LN_SLOTS < 64), "LN_ILP2 writes rows up to 63");
+static_assert(LN_SLOTS <= 64, "a wave's hypothesis slots are its lanes");
 __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B, RansacCfg cfg, uint32_t* lane_slab,
                                                                    int waves_total, int min_open) {
     // a throughput kernel (ms of FP64 issue): at LN_PRIO its waves do not
@@ -1389,14 +1302,8 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
     __shared__ int s_la[LN_WAVES][64];
     double* lres = s_res[wv];
     int* la = s_la[wv];
-#if LN_TLDS
     __shared__ __attribute__((aligned(16))) float s_T[LN_WAVES][LN_SLOTS * 12];  // active slots' transforms
     float* lT = s_T[wv];
-#endif
-#if LN_COMPACT
-    __shared__ int s_lq[LN_WAVES][128];  // phase-1 queue: (slot << 5) | point
-    int* lq = s_lq[wv];
-#endif
     const int cnt = B.open_cnt[0];
     if (cnt < min_open || cnt <= 0) return;  // few open pairs: latency matters, k_ransac_eval_list takes them
     uint32_t* slab = lane_slab + (size_t)gw * 2 * B.mask_words * 64;
@@ -1410,13 +1317,11 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
     // fewer: each wave walks its pairs in turn
     LP(uint64_t lp_t0 = wall_clock64(); uint64_t lp_rounds = 0, lp_nact = 0, lp_tfc = 0, lp_sweep = 0, lp_fold = 0;
        uint64_t lp_q = 0; int lp_pair = -1; uint64_t lp_inner = 0, lp_sum = 0, lp_p1 = 0, lp_p2 = 0;)
-    // open-list slots: gw, gw + waves_total, ... (the pairs this wave owns),
-    // then with LN_HELP any open pair whose hypothesis counter has not run
-    // out, taken from a shared cursor (a wave leaves a pair once every lane
-    // is idle: the pair's counter is exhausted or its fold has stopped)
+    // open-list slots: gw, gw + waves_total, ... (the pairs this wave owns; a
+    // wave leaves a pair once every lane is idle: the pair's counter is
+    // exhausted or its fold has stopped)
     int slot = cnt > waves_total ? gw : gw % cnt;
     int lane_lim = LN_SLOTS;  // lanes that take up hypotheses
-#if LN_BAL
     // Waves in proportion to the pairs' work: pair i of the open list gets
     // 1 + spare * w_i / sum(w) waves (w = good matches + 1: a sweep and a
     // refinement fit walk them all), and each of its waves takes up to
@@ -1458,8 +1363,6 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
             lane_lim = min(LN_SLOTS, (rem + wn - 1) / wn);
         }
     }
-#endif
-    int helps = 0;
     for (;;) {
         if (slot < 0) break;
         const int p = __builtin_amdgcn_readfirstlane(B.open_list[slot]);
@@ -1510,143 +1413,6 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
                 }
             }
             const bool inset = act && !sample;
-#if LN_TFCG
-            const uint64_t im = __ballot(inset);
-            if (im != 0 && __popcll(im) <= LN_TFCG_MAX) {
-                // Few refining lanes: each one's TFC by a group of 9 lanes,
-                // lane (i, j) of group g running m1[j], m2[i] and cov[i][j]
-                // over the set in order, after the group's serial prefix of
-                // the accumulated weight and its alphas (the operations of
-                // TFC::add, split over lanes as in tfc_fold). 7 groups per pass.
-                const uint32_t* cw = slab + (size_t)cur * B.mask_words * 64;
-                const int ni = __popcll(im), myr = (int)lane_rank(im);
-                if (inset) la[myr] = lane;
-                wave_sync();
-                float* gA = reinterpret_cast<float*>(lres);  // [7][128]: alpha, 1 - alpha per chunk point
-                const int g = lane / 9, r = lane - 9 * (lane / 9), ii = r / 3, jj = r - 3 * (r / 3);
-                for (int pass = 0; pass < ni; pass += 7) {
-                    const int sg = pass + g;
-                    const bool gl = g < 7 && sg < ni;
-                    const int ow = la[min(sg, ni - 1)];
-                    float acw = 0.f, m1v = 0.f, m2v = 0.f, cv = 0.f;
-                    int nf = 0;
-                    GoodPt gq = lane < ng ? P[lane] : GoodPt{};
-                    uint32_t q0 = inset ? cw[lane] : 0u, q1 = inset && 32 < ng ? cw[64 + lane] : 0u;
-                    for (int c0 = 0; c0 < ng; c0 += 64) {
-                        wave_sync();  // the previous chunk has been read
-                        lp[lane] = gq;
-                        const uint64_t okm = __ballot(c0 + lane < ng && tfc_point_ok(gq));
-                        wave_sync();
-                        const uint32_t b0 = q0, b1 = q1;
-                        if (c0 + 64 < ng) {
-                            const int c1 = c0 + 64, w1 = c1 >> 5;
-                            if (c1 + lane < ng) gq = P[c1 + lane];
-                            q0 = inset ? cw[(size_t)w1 * 64 + lane] : 0u;
-                            q1 = inset && c1 + 32 < ng ? cw[(size_t)(w1 + 1) * 64 + lane] : 0u;
-                        }
-                        const uint32_t w0 = (uint32_t)__shfl((int)b0, ow), w1 = (uint32_t)__shfl((int)b1, ow);
-                        const uint64_t set = gl ? ((((uint64_t)w1 << 32) | w0) & okm) : 0ull;
-                        nf += __popcll(set);
-                        float* gAl = gA + (g < 7 ? g : 0) * 128;
-                        // 1. accW after each set point: the group's serial sum,
-                        //    eight weights loaded ahead of their adds
-                        if (gl && r == 0) {
-                            uint64_t m = set;
-                            while (m) {
-                                int ks[8];
-                                bool vk[8];
-                                float ws[8];
-#pragma unroll
-                                for (int t = 0; t < 8; t++) {
-                                    vk[t] = m != 0;
-                                    ks[t] = vk[t] ? (int)__builtin_ctzll(m) : 0;
-                                    m &= m - 1;
-                                }
-#pragma unroll
-                                for (int t = 0; t < 8; t++) ws[t] = lp[ks[t]].w;
-#pragma unroll
-                                for (int t = 0; t < 8; t++)
-                                    if (vk[t]) {
-                                        acw += ws[t];
-                                        gAl[ks[t]] = acw;
-                                    }
-                            }
-                        }
-                        wave_sync();
-                        // 2. alpha = w / accW and 1 - alpha, spread over the group
-                        if (gl)
-                            for (int k = r; k < 64; k += 9)
-                                if ((set >> k) & 1ull) {
-                                    const float al = lp[k].w / gAl[k];
-                                    gAl[k] = al;
-                                    gAl[64 + k] = 1.0f - al;
-                                }
-                        wave_sync();
-                        // 3. the chains, four points per step (loads first)
-                        if (gl) {
-                            uint64_t m = set;
-                            while (m) {
-                                int ks[4];
-                                bool vk[4];
-#pragma unroll
-                                for (int t = 0; t < 4; t++) {
-                                    vk[t] = m != 0;
-                                    ks[t] = vk[t] ? (int)__builtin_ctzll(m) : 0;
-                                    m &= m - 1;
-                                }
-                                float pv[4], qv[4], al[4], om[4];
-#pragma unroll
-                                for (int t = 0; t < 4; t++) {
-                                    const GoodPt pt = lp[ks[t]];
-                                    pv[t] = jj == 0 ? pt.sx : (jj == 1 ? pt.sy : pt.sz);
-                                    qv[t] = ii == 0 ? pt.tx : (ii == 1 ? pt.ty : pt.tz);
-                                    al[t] = gAl[ks[t]];
-                                    om[t] = gAl[64 + ks[t]];
-                                }
-#pragma unroll
-                                for (int t = 0; t < 4; t++) {
-                                    const float d1 = pv[t] - m1v, d2 = qv[t] - m2v;
-                                    const float ad2 = al[t] * d2;
-                                    const float ncv = om[t] * (cv + ad2 * d1);
-                                    const float n1 = m1v + al[t] * d1, n2 = m2v + al[t] * d2;
-                                    cv = vk[t] ? ncv : cv;
-                                    m1v = vk[t] ? n1 : m1v;
-                                    m2v = vk[t] ? n2 : m2v;
-                                }
-                            }
-                        }
-                    }
-                    // 4. every refining lane of this pass takes its group's state
-                    for (int t = 0; t < 7 && pass + t < ni; t++) {
-                        const int base = 9 * t;
-                        const float A_ = __shfl(acw, base);
-                        const int nfg = __shfl(nf, base);
-                        float M1[3], M2[3], C[3][3];
-#pragma unroll
-                        for (int x = 0; x < 3; x++) {
-                            M1[x] = __shfl(m1v, base + x);
-                            M2[x] = __shfl(m2v, base + 3 * x);
-                        }
-#pragma unroll
-                        for (int x = 0; x < 3; x++)
-#pragma unroll
-                            for (int y = 0; y < 3; y++) C[x][y] = __shfl(cv, base + 3 * x + y);
-                        if (inset && myr == pass + t) {
-                            tf.accW = A_;
-#pragma unroll
-                            for (int x = 0; x < 3; x++) {
-                                tf.m1[x] = M1[x];
-                                tf.m2[x] = M2[x];
-#pragma unroll
-                                for (int y = 0; y < 3; y++) tf.cov[x][y] = C[x][y];
-                            }
-                            nfit += nfg;
-                        }
-                    }
-                }
-                wave_sync();
-            } else
-#endif
             if (__ballot(inset) != 0) {
                 const uint32_t* cw = slab + (size_t)cur * B.mask_words * 64;
                 // the next 64-point chunk (its points and this lane's two set
@@ -1665,7 +1431,6 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
                         q1 = inset && c1 + 32 < ng ? cw[(size_t)(w1 + 1) * 64 + lane] : 0u;
                     }
                     const int n = min(64, ng - c0);
-#if LN_TFCU
                     // only the points some lane's set holds (the union of the
                     // chunk's set words over the wave, valid points only: a
                     // point no lane adds changes no lane's state), in order,
@@ -1700,16 +1465,6 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
                             nfit += in;
                         }
                     }
-#else
-                    for (int j = 0; j < n; j++) {
-                        const GoodPt g = lp[j];
-                        if (!tfc_point_ok(g)) continue;  // uniform
-                        if ((((j < 32) ? b0 : b1) >> (j & 31)) & 1u) {
-                            tf.add(g.sx, g.sy, g.sz, g.tx, g.ty, g.tz, g.w);
-                            nfit++;
-                        }
-                    }
-#endif
                 }
             }
             float T[12];
@@ -1718,10 +1473,6 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
             double Td[12];
 #pragma unroll
             for (int i = 0; i < 12; i++) Td[i] = (double)T[i];
-#if LN_PRE
-            double Zd[6];
-            hyp_cov_terms(Td, K, Zd);
-#endif
             // ---- ComputeInliersAndError (ransac.cpp:315-348): the new set into the other buffer
             // Evaluations are spread over the lanes, not over the hypotheses:
             // per 32-point chunk, lanes (point j, half hf) evaluate point j for
@@ -1735,7 +1486,6 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
             const int nact = __popcll(actm);
             const int rank = (int)lane_rank(actm);  // this lane's slot among the active ones
             if (act) la[rank] = lane;
-#if LN_TLDS
             // the active hypotheses' transforms in slot order, read back by the
             // sweep as three broadcast 16-byte loads per slot instead of 12 permutes
             if (act) {
@@ -1744,7 +1494,6 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
                 tw[1] = make_float4(T[4], T[5], T[6], T[7]);
                 tw[2] = make_float4(T[8], T[9], T[10], T[11]);
             }
-#endif
             wave_sync();
             double meanError = 0.0;
             unsigned c = 0;
@@ -1757,132 +1506,23 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
                 if (k + 32 < ng) gn = P[k + 32];
                 const bool skip = k >= ng || g.sz == 0.0f || g.tx == 0.0f;  // sic: target.x (ransac.cpp:326)
                 const float x1[3] = {g.sx, g.sy, g.sz}, x2[3] = {g.tx, g.ty, g.tz};
-#if LN_COMPACT
-                // Two phases. 1: lanes (point pj, half hf) run only the
-                // shortcut test for hypothesis slot i + hf; rejected pairs park
-                // -1 at once, the others queue (slot, point) in LDS. 2: every
-                // 64 queued pairs, one full evaluation per lane. Bad
-                // hypotheses reject most points at the shortcut, so most of the
-                // covariance solves (~200 of the ~225 FP64 instructions of an
-                // evaluation) are never issued.
-                if (hf == 0) lp[pj] = g;  // the chunk's points, for phase 2
-                int qn = 0;
-                auto phase2 = [&](int base, int cnt) {
-                    wave_sync();
-                    const int e = lq[base + min(lane, cnt - 1)];
-                    const int a = e >> 5, pq = e & 31;
-                    const int src = la[a];
-                    double Ta[12];
-#pragma unroll
-                    for (int q = 0; q < 12; q++) Ta[q] = (double)__shfl(T[q], src);
-                    const GoodPt g2 = lp[pq];
-                    const float y1[3] = {g2.sx, g2.sy, g2.sz}, y2[3] = {g2.tx, g2.ty, g2.tz};
-                    const double ev = error_function2_bf(y1, y2, Ta, K);
-                    if (lane < cnt) lres[a * LN_RS + pq] = (!(ev > th) && (ev >= 0.0)) ? ev : -1.0;
-                    LP(lp_p2 += cnt;)
-                };
-                for (int i = 0; i < nact; i += 2) {
-                    const int a = i + hf;
-                    const int src = la[min(a, nact - 1)];
-                    double Ta[12];
-#pragma unroll
-                    for (int q = 0; q < 12; q++) Ta[q] = (double)__shfl(T[q], src);
-                    const bool pass = a < nact && !skip && !error_function2_shortcut(x1, x2, Ta, K);
-                    const uint64_t bal = __ballot(pass);
-                    if (pass) lq[qn + (int)lane_rank(bal)] = (a << 5) | pj;
-                    else if (a < nact) lres[a * LN_RS + pj] = -1.0;
-                    qn += __popcll(bal);
-                    LP(lp_p1 += __popcll(__ballot(a < nact));)
-                    if (qn >= 64) {
-                        phase2(qn - 64, 64);
-                        qn -= 64;
-                        wave_sync();  // the entries were read before the queue refills
-                    }
-                }
-                if (qn > 0) phase2(0, qn);
-#elif LN_ILP2
-                // two hypotheses per lane and pass (slots i + hf, i + 2 + hf),
-                // straight-line evaluations the scheduler interleaves
-                for (int i = 0; i < nact; i += 4) {
-                    const int a0 = i + hf, a1 = i + 2 + hf;
-                    const int s0 = la[min(a0, nact - 1)], s1 = la[min(a1, nact - 1)];
-                    double Tq[2][12], e[2];
-#pragma unroll
-                    for (int q = 0; q < 12; q++) {
-                        Tq[0][q] = (double)__shfl(T[q], s0);
-                        Tq[1][q] = (double)__shfl(T[q], s1);
-                    }
-                    const float xp1[2][3] = {{x1[0], x1[1], x1[2]}, {x1[0], x1[1], x1[2]}};
-                    const float xp2[2][3] = {{x2[0], x2[1], x2[2]}, {x2[0], x2[1], x2[2]}};
-                    error_function2_bf2(xp1, xp2, Tq, K, e);
-                    const double e0 = e[0], e1 = e[1];
-                    const double v0 = (!skip & !(e0 > th) & (e0 >= 0.0)) ? e0 : -1.0;
-                    const double v1 = (!skip & !(e1 > th) & (e1 >= 0.0)) ? e1 : -1.0;
-                    // unconditional: a0, a1 <= 63, and rows >= nact are read by
-                    // no lane (a conditional store would pull each evaluation
-                    // into its own branch)
-                    lres[a0 * LN_RS + pj] = v0;
-                    lres[a1 * LN_RS + pj] = v1;
-                }
-#else
                 for (int i = 0; i < nact; i += 2) {
                     const int a = i + hf;  // this half's hypothesis slot
-#if LN_TLDS
                     const float4* tr = reinterpret_cast<const float4*>(lT + min(a, nact - 1) * 12);
                     const float4 t0 = tr[0], t1 = tr[1], t2 = tr[2];
                     const double Ta[12] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w, t2.x, t2.y, t2.z, t2.w};
-#elif LN_PRE
-                    // the hypothesis' transform as doubles and its six
-                    // point-independent covariance terms, permuted from the
-                    // owning lane (LDS work instead of 12 conversions and 9
-                    // products per evaluation)
-                    const int src = la[min(a, nact - 1)];
-                    double Ta[12], Za[6];
-#pragma unroll
-                    for (int q = 0; q < 12; q++) Ta[q] = __shfl(Td[q], src);
-#pragma unroll
-                    for (int q = 0; q < 6; q++) Za[q] = __shfl(Zd[q], src);
-#elif LN_BPERM
-                    // each half fetches its hypothesis' 12 floats from the
-                    // owning lane (ds_bpermute) and widens them (exact: Td is
-                    // (double)T): 12 permutes + 12 conversions instead of 48
-                    // v_readlane, 24 selects and the SGPR hazard nops
-                    const int src = la[min(a, nact - 1)];
-                    double Ta[12];
-#pragma unroll
-                    for (int q = 0; q < 12; q++) Ta[q] = (double)__shfl(T[q], src);
-#else
-                    // the two hypotheses' lanes are wave-uniform: v_readlane into
-                    // scalars instead of an LDS-routed shuffle per element
-                    const int src0 = __builtin_amdgcn_readfirstlane(la[i]);
-                    const int src1 = __builtin_amdgcn_readfirstlane(la[min(i + 1, nact - 1)]);
-                    double Ta[12];
-#pragma unroll
-                    for (int q = 0; q < 12; q++) {
-                        const double t0 = readlane_d(Td[q], src0), t1 = readlane_d(Td[q], src1);
-                        Ta[q] = hf ? t1 : t0;
-                    }
-#endif
                     double d = -1.0;  // not an inlier
                     if (a < nact && !skip) {
-#if LN_PRE
-                        const double e = error_function2_mk(x1, x2, Ta, K, Za);
-#elif LN_MARKSTEIN
                         const double e = error_function2_mk(x1, x2, Ta, K);
-#else
-                        const double e = error_function2(x1, x2, Ta, K);
-#endif
                         if (!(e > th) && (e >= 0.0)) d = e;
                     }
                     if (a < nact) lres[a * LN_RS + pj] = d;
                 }
-#endif
                 LP(const uint64_t lp_cb = wall_clock64(); lp_inner += lp_cb - lp_ca;)
                 wave_sync();
                 uint32_t word = 0;
                 if (act) {
                     const int nj = min(32, ng - c0);
-#if LN_SUMB
                     // a full chunk: the 32 terms read 8 at a time ahead of
                     // the (sequential, in point order) sum
                     if (nj == 32) {
@@ -1901,7 +1541,6 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
                             }
                         }
                     } else
-#endif
                     for (int j = 0; j < nj; j++) {
                         const double v = lres[rank * LN_RS + j];
                         if (v >= 0.0) {
@@ -1959,27 +1598,12 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
             LP(lp_fold += wall_clock64() - lp_q;)
         }
         // the next pair
-        if (LN_BAL && cnt <= waves_total) break;  // one pair per wave
+        if (cnt <= waves_total) break;  // one pair per wave
         if (cnt > waves_total && slot + waves_total < cnt) {
             slot += waves_total;
             continue;
         }
         slot = -1;
-        if (LN_HELP) {
-            // at most one scan of the open list per wave
-            while (helps < cnt) {
-                int c = 0;
-                if (lane == 0) c = atomicAdd(&B.open_cnt[1], 1);
-                c = __builtin_amdgcn_readfirstlane(c) % cnt;
-                helps++;
-                const int q = __builtin_amdgcn_readfirstlane(B.open_list[c]);
-                const RState* Q = B.st + q;
-                if (!ld_relaxed(&Q->done) && ld_relaxed(&Q->nexth) < Q->H) {
-                    slot = c;
-                    break;
-                }
-            }
-        }
     }
 #ifdef ODO_LANES_PROFILE
     if (lane == 0 && gw < LPROF_MAX) {

@@ -157,7 +157,7 @@ struct odo_ctx {
     // leave most CUs idle, one frame takes 0.45 vs 0.28 ms)
     int pform = ODO_PYRAMID_FORM_AUTO;
     bool pyr_fusable = false, blur_fusable = false;
-    PyrSplit pyr_split1{}, pyr_split2{};  // k_pyramid's part plans: one / two workgroups per frame
+    PyrBands pyr_bands{};  // k_pyramid's level-0 band plan
     LevelDesc* lv = nullptr;
     CellDesc* cells = nullptr;
     ResizeX* rx = nullptr;
@@ -839,8 +839,7 @@ static int build_geometry(odo_ctx* c) {
     c->pyr_fusable = pyramid_fusable(c->lv_h.data(), rx.data(), c->rx_off.data(), p.nlevels);
     c->blur_fusable = c->pyr_fusable && pyramid_blur_fusable(c->lv_h.data(), p.nlevels);
     if (p.nlevels <= 16) {
-        pyramid_split_plan(c->lv_h.data(), ry.data(), c->ry_off.data(), p.nlevels, 1, c->pyr_split1);
-        pyramid_split_plan(c->lv_h.data(), ry.data(), c->ry_off.data(), p.nlevels, 2, c->pyr_split2);
+        pyramid_band_plan(c->lv_h.data(), ry.data(), c->ry_off.data(), p.nlevels, c->pyr_bands);
     }
     int e;
     if ((e = dalloc(&c->lv, c->lv_h.size()))) return e;
@@ -859,9 +858,6 @@ static int build_geometry(odo_ctx* c) {
     return ODO_OK;
 }
 
-#ifndef PYR_PARTS
-#define PYR_PARTS 1  // k_pyramid workgroups per frame (2: top and bottom parts)
-#endif
 static int alloc_buffers(odo_ctx* c) {
     const size_t S = NSETS * (size_t)c->slots, B = (size_t)c->maxb;
     int e;
@@ -1236,21 +1232,8 @@ static bool build_pyramid(odo_ctx* c, hipStream_t st, const uint8_t* d_bgr, uint
             launch_gray(st, d_bgr, pyr, c->W, c->H, c->lv_h[0].pitch, (size_t)c->W * c->H * 3, P, n);
             d_bgr = nullptr;
         }
-        // PYR_PARTS 2: two workgroups per frame while a batch leaves CUs for
-        // them (ODO_PYR_PARTS, tuning, overrides)
-        static const int parts = [] {
-            const char* e = odo_knob("ODO_PYR_PARTS");
-            return e ? atoi(e) : PYR_PARTS;
-        }();
-        static int cus = 0;
-        if (!cus) {
-            int dev = 0;
-            (void)hipGetDevice(&dev);
-            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-        }
-        const bool two = parts == 2 && n <= cus;
         launch_pyramid(st, d_bgr, pyr, (size_t)c->W * c->H * 3, P, c->lv, c->rx, c->ry, c->rx_off.data(),
-                       c->ry_off.data(), c->nlevels, n, blur, c->lv_h.data(), two ? c->pyr_split2 : c->pyr_split1);
+                       c->ry_off.data(), c->nlevels, n, blur, c->lv_h.data(), c->pyr_bands);
         return blur != nullptr;
     }
     if (d_bgr) launch_gray(st, d_bgr, pyr, c->W, c->H, c->lv_h[0].pitch, (size_t)c->W * c->H * 3, P, n);

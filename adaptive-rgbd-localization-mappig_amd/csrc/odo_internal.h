@@ -202,20 +202,24 @@ size_t resize_lds_bytes(int spitch, int dw, int max_src_rows);
 // gray + every pyramid level in one launch (one workgroup per frame); bgr may be
 // null (level 0 already in place). pyramid_fusable: the host check of its
 // assumptions (<= 16 levels, <= 4096 px wide, each quad's taps inside 8 bytes)
-// k_pyramid with two workgroups per frame (top / bottom part): per part and
-// level, the rows it builds [lo, hi) (its blur's halo and the next level's
-// source rows included: the parts compute the overlap twice, to the same
-// bytes), and its blur's 30-row strip chunks [ca, cb) and 6-row edge chunks
-// [ea, eb) (disjoint: each blur row is written by one part)
-struct PyrSplit {
-    int parts;  // 1: one workgroup per frame (the ranges cover everything)
-    int lo[2][16], hi[2][16], ca[2][16], cb[2][16], ea[2][16], eb[2][16];
+// k_pyramid's level-0 bands (round 5): level 0 is built band by band in LDS
+// (gray of the band + its 3-row halos), and its blur and level 1 are made
+// from the band in LDS, so level 0 is written once and never read back.
+// Bands of PYR_BAND rows (a multiple of the blur's 30- and 6-row chunks),
+// the last one 30..PYR_BAND+29 rows; nb = 0: level 0 is not banded (no BGR
+// input, a width that is not a multiple of 4, or a level under 30 rows).
+#define PYR_BAND 60
+#define PYR_MAXB 64
+struct PyrBands {
+    int nb;
+    int rows;               // LDS rows of the band buffer (largest band + 6)
+    int b0[PYR_MAXB + 1];   // band k: level-0 rows [b0[k], b0[k+1])
+    int y1[PYR_MAXB + 1];   // the level-1 rows it makes: [y1[k], y1[k+1]) (their sy0 in the band)
 };
-void pyramid_split_plan(const LevelDesc* lv_host, const ResizeY* ry, const int* ry_off, int nlevels, int parts,
-                        PyrSplit& S);
+void pyramid_band_plan(const LevelDesc* lv_host, const ResizeY* ry, const int* ry_off, int nlevels, PyrBands& B);
 void launch_pyramid(hipStream_t st, const uint8_t* bgr, uint8_t* pyr, size_t in_stride, size_t pyr_stride,
                     const LevelDesc* lv, const ResizeX* rx, const ResizeY* ry, const int* rx_off, const int* ry_off,
-                    int nlevels, int nframes, uint8_t* blur, const LevelDesc* lv_host, const PyrSplit& split);
+                    int nlevels, int nframes, uint8_t* blur, const LevelDesc* lv_host, const PyrBands& bands);
 // blur: the blurred pyramid is written by the same launch (null: not);
 // pyramid_blur_fusable: every level is large enough for the strip walks
 bool pyramid_blur_fusable(const LevelDesc* lv_host, int nlevels);
