@@ -159,7 +159,7 @@ __constant__ int c_circle_dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -
 __constant__ int c_circle_dy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
 #define FS_TH 256
 #define FS_RING 512  // survivors per wave ring (u16 offsets): <= 127 pending + 256 per compass step
-#define FS_CL 2048   // corner list; beyond it the NMS and placement scan the score map
+#define FS_CL 1024   // corner list (a level-0 segment of 7 cells: ~270); beyond it NMS and placement scan the score map
 
 ODO_INLINE void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

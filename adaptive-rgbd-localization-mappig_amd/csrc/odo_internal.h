@@ -52,10 +52,10 @@ struct CellDesc {
 // level, whose ROIs (orbextractor.cpp:688-703) are staged in LDS as one union:
 // rows [y0, y0 + rows), cols [x0, x0 + cols) of the level; cell jl of the
 // segment is cells_h[ci0 + jl] (ROI x0 + jl*wcell).
-#define FS_NCM 16  // cells per segment (max)
 #ifndef FS_SEGC
-#define FS_SEGC 8  // cells per segment the host table aims for
+#define FS_SEGC 8  // cells per segment (at most; the host splits a cell row evenly)
 #endif
+#define FS_NCM FS_SEGC
 struct FastSeg {
     int level, ci0;
     int16_t y0, x0, rows, cols, ncell, wcell;
