@@ -11,6 +11,9 @@
 //                 orbextractor.cpp:14-85,805-811; frame.cpp:139-164,286-313
 #include "odo_device.h"
 #include "odo_internal.h"
+#ifdef FS_STATS
+#include <cstdio>
+#endif
 
 // wave priority of the extraction kernels (ODO_EXTRACT_PRIO, measurement
 // builds): the pair stages' waves issue at ODO_WAVE_PRIO
@@ -155,10 +158,12 @@ __global__ void __launch_bounds__(256) k_resize(uint8_t* __restrict__ pyr, size_
 // so the map is not cleared for the second pass.
 // (Until round 4: one wave per cell ROI, staged per cell with its halo, with
 // per-cell setup and ordered compactions: 988 VALU + 510 SALU per cell.)
-__constant__ int c_circle_dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
-__constant__ int c_circle_dy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
+// the Bresenham circle of radius 3 (FAST_t<16>'s pixel order)
+constexpr int kCircleDx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+constexpr int kCircleDy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
 #define FS_TH 256
 #define FS_RING 512  // survivors per wave ring (u16 offsets): <= 127 pending + 256 per compass step
+#define FS_RSTRIDE (FS_RING + 8)  // a wave's ring + its trash slot (entry FS_RING), 16-byte multiple
 #define FS_CL 1024   // corner list (a level-0 segment of 7 cells: ~270); beyond it NMS and placement scan the score map
 
 ODO_INLINE void wave_lds_sync() {
@@ -167,6 +172,28 @@ ODO_INLINE void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+#ifdef FS_STATS
+// measurement build only: work counters of k_fast_seg, printed per launch
+__device__ unsigned long long fs_stats[8];
+#define FS_STAT(i, v) atomicAdd(&fs_stats[i], (unsigned long long)(v))
+#else
+#define FS_STAT(i, v) ((void)0)
+#endif
+// a quad's 4-bit pixel mask in the compass's layout: pixel i at bit 8i + 7
+ODO_INLINE uint32_t fs_msb_mask(uint32_t b4) {
+    return ((b4 & 1u) << 7) | ((b4 & 2u) << 14) | ((b4 & 4u) << 21) | ((b4 & 8u) << 28);
+}
+// inclusive prefix sum over the wave's lanes (DPP: row shifts, then the row
+// totals broadcast into the rows above)
+ODO_INLINE int wave_incl_scan(int x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);   // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);   // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);   // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);   // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+    return x;
+}
 struct FastMisc {
     int ncl, ovf, nl;
     int tot[FS_NCM], retry[FS_NCM];
@@ -184,14 +211,15 @@ __global__ void __launch_bounds__(FS_TH) k_fast_seg(const uint8_t* __restrict__ 
     uint8_t* const roi = fs_lds;
     const uint32_t* const roi32 = reinterpret_cast<const uint32_t*>(fs_lds);
     uint8_t* const score = fs_lds + LO.img;
-    uint16_t* const ring = reinterpret_cast<uint16_t*>(fs_lds + LO.ring) + wave * FS_RING;
+    uint16_t* const ring = reinterpret_cast<uint16_t*>(fs_lds + LO.ring) + wave * FS_RSTRIDE;
     uint16_t* const clist = reinterpret_cast<uint16_t*>(fs_lds + LO.clist);
     uint32_t* const bits = reinterpret_cast<uint32_t*>(fs_lds + LO.bits);
     int* const cnt = reinterpret_cast<int*>(fs_lds + LO.cnt);
-    uint32_t* const qlist = reinterpret_cast<uint32_t*>(fs_lds + LO.qlist);
+    uint2* const qlist = reinterpret_cast<uint2*>(fs_lds + LO.qlist);  // (pixel mask, 4 m)
     FastMisc& M = *reinterpret_cast<FastMisc*>(fs_lds + LO.misc);
     const LevelDesc L = lv[G.level];
-    const int R = G.rows, cols = G.cols, RS = G.rs, RS4 = RS >> 2, BW = G.bw, wcell = G.wcell, nc = G.ncell;
+    const int R = G.rows, cols = G.cols, BW = G.bw, wcell = G.wcell, nc = G.ncell;
+    constexpr int RS = FS_RS, RS4 = RS >> 2;
     const int sh = G.x0 & 15;  // staged from the 16-byte column below x0: pixel (r, x) at byte r*RS + sh + x
     {
         const uint4* src = reinterpret_cast<const uint4*>(pyr + (size_t)f * pyr_stride + L.off +
@@ -206,25 +234,33 @@ __global__ void __launch_bounds__(FS_TH) k_fast_seg(const uint8_t* __restrict__ 
         for (int i = t; i < R * FS_NCM; i += FS_TH) cnt[i] = 0;
         if (t == 0) M.ncl = 0, M.ovf = 0;
     }
-    __syncthreads();
     const int drows = R - 6;
     const int m0 = (sh + 3) >> 2, m1 = (sh + cols - 4) >> 2;
-    const uint32_t mlo = (0xFu << (sh + 3 - 4 * m0)) & 0xFu, mhi = (1u << (sh + cols - 3 - 4 * m1)) - 1u;
-    const float inv_rs = 1.0f / (float)RS, inv_w = 1.0f / (float)wcell;
+    {
+        // the first pass's quads per detection row: (its detection pixels
+        // (fs_msb_mask), byte column 4 m)
+        const uint32_t mlo = (0xFu << (sh + 3 - 4 * m0)) & 0xFu, mhi = (1u << (sh + cols - 3 - 4 * m1)) - 1u;
+        if (t <= m1 - m0) {
+            const int m = m0 + t;
+            qlist[t] = uint2{fs_msb_mask((t == 0 ? mlo : 0xFu) & (m == m1 ? mhi : 0xFu)), 4u * (uint32_t)m};
+        }
+    }
+    __syncthreads();
+    const float inv_w = 1.0f / (float)wcell;
     uint32_t* const out = cand + ((size_t)f * ncells + G.ci0) * cell_cap;
     typedef short s16x2 __attribute__((ext_vector_type(2)));
     for (int pass = 0; pass < 2; pass++) {
         const int th = pass == 0 ? ini_th : min_th;
         const int thc = th < 0 ? 0 : (th > 255 ? 255 : th);
-        const int NL = pass == 0 ? m1 - m0 + 1 : M.nl;  // quads per detection row
+        const int NL = pass == 0 ? m1 - m0 + 1 : M.nl;  // quads per detection row (qlist)
         const int items = drows > 0 && cols > 6 && NL > 0 ? drows * NL : 0;
+        if (t == 0) FS_STAT(pass, items);
         // ---- 1 + 2: compass, ring, segment test
         {
             const s16x2 thv = {(short)thc, (short)thc};
-            // item = (detection row ii, quad kk): stepped by FS_TH without divisions
-            const int it0 = wave * 64 + lane;
-            int ii = NL > 0 ? it0 / NL : 0, kk = NL > 0 ? it0 - ii * NL : 0;
-            const int dq = NL > 0 ? FS_TH / NL : 0, dr = NL > 0 ? FS_TH - dq * NL : 0;
+            // item it = (detection row ii, quad kk): ii = (it + 0.5) / NL in
+            // float (it < 2^13, so the error stays far below the 0.5 / NL margin)
+            const float inl = NL > 0 ? 1.0f / (float)NL : 0.0f, inl_h = 0.5f * inl;
             int head = 0, tail = 0;
             // segment test + cornerScore of ring entries [h, h + n), two per lane
             auto seg_test = [&](int h, int n) {
@@ -235,13 +271,20 @@ __global__ void __launch_bounds__(FS_TH) k_fast_seg(const uint8_t* __restrict__ 
                     o0 = ring[(h + i0) & (FS_RING - 1)];
                     o1 = i1 < n ? ring[(h + i1) & (FS_RING - 1)] : o0;
                     const s16x2 vv = {(short)roi[o0], (short)roi[o1]};
+                    // from the circle's top-left corner: every offset a
+                    // non-negative immediate of the LDS reads (the empty asm
+                    // keeps the compiler from folding the corner back into them)
+                    int a0 = o0 - 3 * RS - 3, a1 = o1 - 3 * RS - 3;
+                    asm("" : "+v"(a0), "+v"(a1));
+                    const uint8_t* const q0 = roi + a0;
+                    const uint8_t* const q1 = roi + a1;
                     s16x2 d[16];
 #pragma unroll
                     for (int k = 0; k < 16; k++) {
-                        const int off = c_circle_dy[k] * RS + c_circle_dx[k];
+                        const int off = (kCircleDy[k] + 3) * RS + kCircleDx[k] + 3;
                         s16x2 c;
-                        c.x = (short)roi[o0 + off];
-                        c.y = (short)roi[o1 + off];
+                        c.x = (short)q0[off];
+                        c.y = (short)q1[off];
                         d[k] = vv - c;
                     }
                     // best 9-arc min / max: arcs k, k+1 (k even) share the run
@@ -277,6 +320,7 @@ __global__ void __launch_bounds__(FS_TH) k_fast_seg(const uint8_t* __restrict__ 
                 }
                 const uint64_t b0 = __ballot(c0), b1 = __ballot(c1);
                 const int nco = __popcll(b0) + __popcll(b1);
+                if (lane == 0) FS_STAT(3, 1);
                 if (nco) {
                     int cb = 0;
                     if (lane == 0) cb = atomicAdd(&M.ncl, nco);
@@ -289,24 +333,21 @@ __global__ void __launch_bounds__(FS_TH) k_fast_seg(const uint8_t* __restrict__ 
                 }
             };
             for (int base = wave * 64; base < items; base += FS_TH) {
-                uint32_t pass4 = 0;  // bit i: pixel 4m+i survives
+                uint32_t pass4 = 0;  // bit 8i + 7: pixel 4m+i survives
                 int qoff = 0;
-                if (base + lane < items) {
-                    int m;
-                    uint32_t msk;
-                    if (pass == 0) {
-                        m = m0 + kk;
-                        msk = (kk == 0 ? mlo : 0xFu) & (m == m1 ? mhi : 0xFu);
-                    } else {
-                        const uint32_t e = qlist[kk];
-                        m = (int)(e & 0xFFFFu);
-                        msk = e >> 16;
-                    }
-                    qoff = (int)__umul24((uint32_t)(3 + ii), (uint32_t)RS) + 4 * m;
-                    const uint32_t* w = roi32 + (qoff >> 2);
-                    const uint32_t Cw = w[0], Uw = w[-3 * RS4], Dw = w[3 * RS4];
-                    const uint32_t Lw = __builtin_amdgcn_alignbyte(Cw, w[-1], 1);
-                    const uint32_t Rw = __builtin_amdgcn_alignbyte(w[1], Cw, 3);
+                const int it = base + lane;
+                if (it < items) {
+                    const int ii = (int)__builtin_fmaf((float)it, inl, inl_h);
+                    const int kk = it - __mul24(ii, NL);
+                    const uint2 e = qlist[kk];
+                    int wb = (ii << 8) + (int)e.y;  // 3 rows above the quad: offsets >= 0
+                    asm("" : "+v"(wb));
+                    qoff = wb + 3 * RS;
+                    const uint32_t* w = reinterpret_cast<const uint32_t*>(roi + wb);
+                    const uint32_t Cw = w[3 * RS4], Uw = w[0], Dw = w[6 * RS4];
+                    const uint32_t Lw = __builtin_amdgcn_alignbyte(Cw, w[3 * RS4 - 1], 1);
+                    const uint32_t Rw = __builtin_amdgcn_alignbyte(w[3 * RS4 + 1], Cw, 3);
+                    uint32_t hm[2];
 #pragma unroll
                     for (int hh = 0; hh < 2; hh++) {
                         const uint32_t sel = hh ? 0x0c030c02u : 0x0c010c00u;
@@ -324,32 +365,25 @@ __global__ void __launch_bounds__(FS_TH) k_fast_seg(const uint8_t* __restrict__ 
                         const s16x2 bk = __builtin_elementwise_min(__builtin_elementwise_max(a0, a8),
                                                                    __builtin_elementwise_max(a4, a12));
                         const s16x2 t1 = dk - (v - thv), t2 = (v + thv) - bk;
-                        const uint32_t pm =
-                            (*reinterpret_cast<const uint32_t*>(&t1) | *reinterpret_cast<const uint32_t*>(&t2)) & 0x80008000u;
-                        pass4 |= ((pm >> 15) & 1u) << (2 * hh);
-                        pass4 |= (pm >> 31) << (2 * hh + 1);
+                        hm[hh] = *reinterpret_cast<const uint32_t*>(&t1) | *reinterpret_cast<const uint32_t*>(&t2);
                     }
-                    pass4 &= msk;
+                    // pixel i's sign bit (bit 15 / 31 of half i / 2) to bit 8i + 7
+                    pass4 = __builtin_amdgcn_perm(hm[1], hm[0], 0x07050301u) & e.x;
                 }
-                ii += dq;
-                kk += dr;
-                if (kk >= NL) kk -= NL, ii++;
                 // append to the ring (any order): this lane's survivors after
-                // the counts of the lanes below (three ballots of the count's bits)
-                const uint32_t c = (uint32_t)__builtin_popcount(pass4);
-                const uint64_t B0 = __ballot(c & 1u), B1 = __ballot(c & 2u), B2 = __ballot(c & 4u);
-                int pos = tail + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(B0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)B0, 0)) +
-                          2 * (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(B1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)B1, 0)) +
-                          4 * (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(B2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)B2, 0));
-                uint32_t pm4 = pass4;
+                // those of the lanes below (a DPP prefix sum of the counts)
+                const int c = __builtin_popcount(pass4);
+                const int incl = wave_incl_scan(c);
+                const int pos = tail + incl - c;
+                // every lane writes four entries: pixel k of the quad to its
+                // ring slot if it survived, else to the wave's trash slot (no
+                // divergent branches)
 #pragma unroll
-                for (int k = 0; k < 4; k++)
-                    if (pm4) {
-                        ring[pos & (FS_RING - 1)] = (uint16_t)(qoff + __builtin_ctz(pm4));
-                        pos++;
-                        pm4 &= pm4 - 1u;
-                    }
-                tail += __popcll(B0) + 2 * __popcll(B1) + 4 * __popcll(B2);
+                for (int k = 0; k < 4; k++) {
+                    const int slot = (pos + __builtin_popcount(pass4 & ((1u << (8 * k)) - 1u))) & (FS_RING - 1);
+                    ring[(pass4 >> (8 * k + 7)) & 1u ? slot : FS_RING] = (uint16_t)(qoff + k);
+                }
+                tail += __builtin_amdgcn_readlane(incl, 63);
                 if (tail - head >= 128) {
                     wave_lds_sync();
                     do {
@@ -359,6 +393,7 @@ __global__ void __launch_bounds__(FS_TH) k_fast_seg(const uint8_t* __restrict__ 
                     wave_lds_sync();
                 }
             }
+            if (lane == 0) FS_STAT(2, tail);
             if (tail > head) {
                 wave_lds_sync();
                 seg_test(head, tail - head);
@@ -369,23 +404,29 @@ __global__ void __launch_bounds__(FS_TH) k_fast_seg(const uint8_t* __restrict__ 
         //         the pass's quads when the list overflowed)
         const bool ovf = M.ovf != 0;
         const int ncl = min(M.ncl, FS_CL);
+        if (t == 0) FS_STAT(4, M.ncl), FS_STAT(5, ovf ? 1 : 0);
         // corner at ROI byte offset o -> (row, segment x, cell) and its cell's
         // detection columns [xl, xh) in segment x
         auto locate = [&](int o, int& r, int& xs, int& jl, int& xl, int& xh) {
-            r = (int)(((float)o + 0.5f) * inv_rs);
-            xs = o - r * RS - sh;
+            r = o / RS;
+            xs = (o & (RS - 1)) - sh;
             jl = (int)(((float)(xs - 3) + 0.5f) * inv_w);
             xl = 3 + jl * wcell;
             xh = min(xl + wcell, cols - 3);
         };
         auto nms = [&](int o) {
-            const int sc = score[o];
+            int so = o - RS - 1;  // the 3x3 block's top-left
+            asm("" : "+v"(so));
+            const uint8_t* const sb = score + so;
+            const int sc = sb[RS + 1];
             int r, xs, jl, xl, xh;
             locate(o, r, xs, jl, xl, xh);
-            bool keep = sc > score[o - RS] && sc > score[o + RS];
-            if (xs - 1 >= xl) keep = keep && sc > score[o - RS - 1] && sc > score[o - 1] && sc > score[o + RS - 1];
-            if (xs + 1 < xh) keep = keep && sc > score[o - RS + 1] && sc > score[o + 1] && sc > score[o + RS + 1];
-            if (keep) {
+            // all eight neighbours read; a side column counts only inside the cell
+            const int nmid = max((int)sb[1], (int)sb[2 * RS + 1]);
+            const int nl = max(max((int)sb[0], (int)sb[RS]), (int)sb[2 * RS]);
+            const int nr = max(max((int)sb[2], (int)sb[RS + 2]), (int)sb[2 * RS + 2]);
+            const int nb = max(nmid, max(xs - 1 >= xl ? nl : 0, xs + 1 < xh ? nr : 0));
+            if (sc > nb) {
                 atomicOr(&bits[r * BW + (xs >> 5)], 1u << (xs & 31));
                 atomicAdd(&cnt[r * FS_NCM + jl], 1);
             }
@@ -394,19 +435,11 @@ __global__ void __launch_bounds__(FS_TH) k_fast_seg(const uint8_t* __restrict__ 
         auto scan = [&](auto&& fn) {
             for (int it = t; it < items; it += FS_TH) {
                 const int ii2 = it / NL, kk2 = it - ii2 * NL;
-                int m;
-                uint32_t msk;
-                if (pass == 0) {
-                    m = m0 + kk2;
-                    msk = (kk2 == 0 ? mlo : 0xFu) & (m == m1 ? mhi : 0xFu);
-                } else {
-                    const uint32_t e = qlist[kk2];
-                    m = (int)(e & 0xFFFFu);
-                    msk = e >> 16;
-                }
-                const int qo = (3 + ii2) * RS + 4 * m;
+                const uint2 e = qlist[kk2];
+                const uint32_t msk = e.x;
+                const int qo = (3 + ii2) * RS + (int)e.y;
                 for (int b = 0; b < 4; b++)
-                    if (((msk >> b) & 1u) && score[qo + b]) fn(qo + b);
+                    if (((msk >> (8 * b + 7)) & 1u) && score[qo + b]) fn(qo + b);
             }
         };
         if (!ovf)
@@ -437,11 +470,15 @@ __global__ void __launch_bounds__(FS_TH) k_fast_seg(const uint8_t* __restrict__ 
             const uint32_t* row = bits + r * BW;
             if (!((row[xs >> 5] >> (xs & 31)) & 1u)) return;
             int rank = cnt[r * FS_NCM + jl];
-            const int wl = xl >> 5, wx = xs >> 5;
-            for (int w = wl; w <= wx; w++) {
-                uint32_t v = row[w];
-                if (w == wl) v &= ~0u << (xl & 31);
-                if (w == wx) v &= (1u << (xs & 31)) - 1u;
+            // kept corners of the cell left of xs in this row: words wl .. wl + nwd
+            // (a cell spans at most four words; the words past it are masked off)
+            const int wl = xl >> 5, nwd = (xs >> 5) - wl;
+            const uint32_t hm = (1u << (xs & 31)) - 1u;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                uint32_t v = row[wl + i];
+                if (i == 0) v &= ~0u << (xl & 31);
+                v &= i < nwd ? ~0u : (i == nwd ? hm : 0u);
                 rank += __builtin_popcount(v);
             }
             if (rank < cell_cap)
@@ -456,6 +493,8 @@ __global__ void __launch_bounds__(FS_TH) k_fast_seg(const uint8_t* __restrict__ 
         if (pass == 0) {
             if (t < nc) M.retry[t] = M.tot[t] == 0;
             __syncthreads();
+            if (t < nc && M.retry[t]) FS_STAT(6, 1);
+            if (t == 0) FS_STAT(7, nc);
             if (t < nc) {
                 const int xa = sh + 3 + t * wcell, xe = sh + min(3 + (t + 1) * wcell, cols - 3);
                 if (M.retry[t]) {
@@ -467,7 +506,7 @@ __global__ void __launch_bounds__(FS_TH) k_fast_seg(const uint8_t* __restrict__ 
                         }
                     for (int m = xa >> 2; m <= (xe - 1) >> 2; m++) {
                         const int lo = max(xa - 4 * m, 0), hi = min(xe - 4 * m, 4);
-                        qlist[at++] = (uint32_t)m | (((0xFu << lo) & ((1u << hi) - 1u)) << 16);
+                        qlist[at++] = uint2{fs_msb_mask((0xFu << lo) & ((1u << hi) - 1u)), 4u * (uint32_t)m};
                     }
                 } else {
                     cand_cnt[(size_t)f * ncells + G.ci0 + t] = min(M.tot[t], cell_cap);
@@ -1339,12 +1378,9 @@ __global__ void __launch_bounds__(256) k_blur_rows(const uint8_t* __restrict__ p
 // and 0.35-0.6 ms pipelined per 256 frames, profiles/r03_b). Levels >= 1 are
 // read back through the CU's own L1 / L2 (every wave of the workgroup is on
 // one CU, so workgroup-scope ordering is all the barrier needs).
-// Level 0 (round 5, PyrBands): built band by band in LDS — the band's gray
-// rows plus 3-row halos (the halos' gray recomputed) — then the band's blur
-// rows and the level-1 rows whose sources lie in it are made from LDS, so
-// level 0 is written once (FAST and finalize read it) and never read back
-// (round 4: 1.37 GB memory-side per launch against 0.72 GB compulsory, most
-// of it level 0 read again by its blur and by level 1).
+// (Round 5 tried level 0 band by band in LDS, gray + 3-row halos, its blur
+// and level 1 made from the band so that level 0 is never read back: 356 vs
+// 329 us alone per 256 frames, step unchanged, profiles/r05_e; not kept.)
 // Resize: thread t owns quad q = t mod nq of the level (4 output pixels) and
 // walks the rows ph, ph + P, ... (ph = t / nq, P = 1024 / nq), so its x taps
 // are loaded once per level into registers: the quad's source bytes lie in
@@ -1367,15 +1403,15 @@ struct PyrLevels {
     int rx_off[16], ry_off[16];
 };
 // the 7x7 blur of level l of frame f by the whole workgroup (PYR_TH threads:
-// 64 strip groups of 16 lanes, then the edge lanes): strip chunks [ca, cb)
-// and edge chunks [ea, eb) of the level, read from srcL (the level's row 0)
+// 64 strip groups of 16 lanes, then the edge lanes), read from srcL (the
+// level's row 0)
 ODO_INLINE void pyr_blur_level(const uint8_t* srcL, uint8_t* __restrict__ blur, size_t pyr_stride,
                                const LevelDesc* __restrict__ lv, const BlurRows& S, int nlevels, int f, int l,
-                               const LevelDesc& L, int t, int ca, int cb, int ea, int eb) {
+                               const LevelDesc& L, int t) {
     const uint32_t none[3] = {0, 0, 0};
-    const int items = cb * S.nst[l];
+    const int items = S.nch[l] * S.nst[l];
     const int g = t >> 4;
-    for (int it = ca * S.nst[l] + g; it < items; it += PYR_TH / 16) {
+    for (int it = g; it < items; it += PYR_TH / 16) {
         const int chunk = it / S.nst[l], strip = it - chunk * S.nst[l];
         const int q = 1 + strip * 16 + (t & 15);
         const bool store = q <= S.nq[l];
@@ -1387,7 +1423,7 @@ ODO_INLINE void pyr_blur_level(const uint8_t* srcL, uint8_t* __restrict__ blur, 
         blur_walk<false, BR_R>(s0, dp, (size_t)L.pitch, L.h, y0, top, bottom, store, 0, 0, 0, none, none);
     }
     const int ne = (S.ebase[l + 1] - S.ebase[l]) / ((L.h + BR_RE - 1) / BR_RE);  // edge quads per chunk
-    for (int k = S.ebase[l] + ea * ne + t; k < S.ebase[l] + eb * ne; k += PYR_TH)
+    for (int k = S.ebase[l] + t; k < S.ebase[l + 1]; k += PYR_TH)
         blur_edge_lane(srcL, blur, pyr_stride, lv, S, nlevels, f, k);
 }
 // level D's rows [ylo, yhi) from level S (whose row 0 is srcS), thread t's quad
@@ -1449,14 +1485,17 @@ ODO_INLINE void pyr_resize_rows(const uint8_t* srcS, uint8_t* dstD, const LevelD
     }
 }
 // gray of level-0 rows [r0, r1) (k_gray's arithmetic, PYR_GU quads of 4
-// pixels in flight per thread): row y to gdst + y * pitch, and when lds is
-// given also to lds + (y - g0) * pitch (the band buffer) with the global
-// store only for rows [b0, b1)
-ODO_INLINE void pyr_gray_rows(const uint8_t* __restrict__ src, uint8_t* gdst, uint8_t* lds, int w, int pitch,
-                              int r0, int r1, int g0, int b0, int b1, int t) {
+// pixels in flight per thread): row y to gdst + y * pitch
+ODO_INLINE void pyr_gray_rows(const uint8_t* __restrict__ src, uint8_t* gdst, int w, int pitch, int r0, int r1,
+                              int t) {
     if ((w & 3) == 0) {
         const int nq4 = (r1 * w) >> 2;
-        for (int q0 = ((r0 * w) >> 2) + t; q0 < nq4; q0 += PYR_GU * PYR_TH) {
+        // (row, column) of the thread's next quad, stepped by PYR_TH quads
+        // (4 PYR_TH pixels) without a division per quad
+        const int q00 = ((r0 * w) >> 2) + t;
+        int cy = (4 * q00) / w, cx = 4 * q00 - cy * w;
+        const int dy = (4 * PYR_TH) / w, dx = 4 * PYR_TH - dy * w;
+        for (int q0 = q00; q0 < nq4; q0 += PYR_GU * PYR_TH) {
             uint32_t wv[PYR_GU][3];
 #pragma unroll
             for (int u = 0; u < PYR_GU; u++) {
@@ -1469,8 +1508,11 @@ ODO_INLINE void pyr_gray_rows(const uint8_t* __restrict__ src, uint8_t* gdst, ui
 #pragma unroll
             for (int u = 0; u < PYR_GU; u++) {
                 const int q = q0 + u * PYR_TH;
+                const int y = cy, x = cx;
+                cx += dx;
+                cy += dy;
+                if (cx >= w) cx -= w, cy++;
                 if (q < nq4) {
-                    const int p0 = q * 4, y = p0 / w, x = p0 - y * w;
                     uint32_t out = 0;
 #pragma unroll
                     for (int i = 0; i < 4; i++) {
@@ -1480,12 +1522,7 @@ ODO_INLINE void pyr_gray_rows(const uint8_t* __restrict__ src, uint8_t* gdst, ui
                         const uint32_t R = (wv[u][(b + 2) >> 2] >> (8 * ((b + 2) & 3))) & 0xffu;
                         out |= ((B * 1868u + G * 9617u + R * 4899u + 8192u) >> 14) << (8 * i);
                     }
-                    if (lds) {
-                        *reinterpret_cast<uint32_t*>(lds + (y - g0) * pitch + x) = out;
-                        if (y >= b0 && y < b1) *reinterpret_cast<uint32_t*>(gdst + (size_t)y * pitch + x) = out;
-                    } else {
-                        *reinterpret_cast<uint32_t*>(gdst + (size_t)y * pitch + x) = out;
-                    }
+                    *reinterpret_cast<uint32_t*>(gdst + (size_t)y * pitch + x) = out;
                 }
             }
         }
@@ -1503,54 +1540,27 @@ __global__ void __launch_bounds__(PYR_TH) k_pyramid(const uint8_t* __restrict__ 
                                                     size_t in_stride, size_t pyr_stride,
                                                     const LevelDesc* __restrict__ lv, const ResizeX* __restrict__ xt,
                                                     const ResizeY* __restrict__ yt, PyrLevels PL, int nlevels,
-                                                    uint8_t* __restrict__ blur, BlurRows BR, PyrBands PB) {
+                                                    uint8_t* __restrict__ blur, BlurRows BR) {
     EXTRACT_PRIO();
-    extern __shared__ __attribute__((aligned(16))) uint8_t pyr_lds[];
     const int f = blockIdx.x;
     const int t = threadIdx.x;
     uint8_t* base = pyr + (size_t)f * pyr_stride;
-    int lfirst = 1;  // first level the level loop builds
     if (bgr) {
         const LevelDesc L0 = lv[0];
-        const uint8_t* src = bgr + (size_t)f * in_stride;
-        if (PB.nb > 0) {
-            // level 0 band by band in LDS: gray, then its blur and level 1
-            const LevelDesc L1 = lv[1];
-            for (int k = 0; k < PB.nb; k++) {
-                const int b0 = PB.b0[k], b1 = PB.b0[k + 1];
-                const int g0 = max(b0 - 3, 0), g1 = min(b1 + 3, L0.h);
-                pyr_gray_rows(src, base + L0.off, pyr_lds, L0.w, L0.pitch, g0, g1, g0, b0, b1, t);
-                __syncthreads();  // the band is in LDS
-                // the band as the level's "row 0": row y at pyr_lds + (y - g0) * pitch
-                const uint8_t* srcB = pyr_lds - g0 * L0.pitch;
-                if (BLUR) {
-                    const int ca = b0 / BR_R, cb = b1 == L0.h ? (L0.h + BR_R - 1) / BR_R : b1 / BR_R;
-                    const int ea = b0 / BR_RE, eb = b1 == L0.h ? (L0.h + BR_RE - 1) / BR_RE : b1 / BR_RE;
-                    pyr_blur_level(srcB, blur, pyr_stride, lv, BR, nlevels, f, 0, L0, t, ca, cb, ea, eb);
-                }
-                pyr_resize_rows(srcB, base + L1.off, L0, L1, xt + PL.rx_off[1], yt + PL.ry_off[1], t, PB.y1[k],
-                                PB.y1[k + 1]);
-                __syncthreads();  // the band buffer is free
-            }
-            lfirst = 2;
-        } else {
-            pyr_gray_rows(src, base + L0.off, nullptr, L0.w, L0.pitch, 0, L0.h, 0, 0, 0, t);
-        }
+        pyr_gray_rows(bgr + (size_t)f * in_stride, base + L0.off, L0.w, L0.pitch, 0, L0.h, t);
     }
-    for (int l = lfirst; l < nlevels; l++) {
+    for (int l = 1; l < nlevels; l++) {
         __syncthreads();  // level l - 1 is complete
         const LevelDesc S = lv[l - 1], D = lv[l];
         if (BLUR)
-            pyr_blur_level(base + S.off, blur, pyr_stride, lv, BR, nlevels, f, l - 1, S, t, 0, BR.nch[l - 1], 0,
-                           (S.h + BR_RE - 1) / BR_RE);
+            pyr_blur_level(base + S.off, blur, pyr_stride, lv, BR, nlevels, f, l - 1, S, t);
         pyr_resize_rows(base + S.off, base + D.off, S, D, xt + PL.rx_off[l], yt + PL.ry_off[l], t, 0, D.h);
     }
     if (BLUR) {
         __syncthreads();  // the last level is complete
         const int ll = nlevels - 1;
         const LevelDesc L = lv[ll];
-        pyr_blur_level(base + L.off, blur, pyr_stride, lv, BR, nlevels, f, ll, L, t, 0, BR.nch[ll], 0,
-                       (L.h + BR_RE - 1) / BR_RE);
+        pyr_blur_level(base + L.off, blur, pyr_stride, lv, BR, nlevels, f, ll, L, t);
     }
     __syncthreads();
 }
@@ -1595,59 +1605,17 @@ bool pyramid_blur_fusable(const LevelDesc* lv_host, int nlevels) {
 }
 void launch_pyramid(hipStream_t st, const uint8_t* bgr, uint8_t* pyr, size_t in_stride, size_t pyr_stride,
                     const LevelDesc* lv, const ResizeX* rx, const ResizeY* ry, const int* rx_off, const int* ry_off,
-                    int nlevels, int nframes, uint8_t* blur, const LevelDesc* lv_host, const PyrBands& bands) {
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_pyramid<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute((const void*)k_pyramid<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr = true;
-    }
+                    int nlevels, int nframes, uint8_t* blur, const LevelDesc* lv_host) {
     PyrLevels PL{};
     for (int l = 0; l < nlevels && l < 16; l++) PL.rx_off[l] = rx_off[l], PL.ry_off[l] = ry_off[l];
     BlurRows BR{};
-    PyrBands PB = bands;
-    if (!bgr) PB.nb = 0;  // level 0 already in place: nothing to band
-    const size_t lds = PB.nb > 0 ? (size_t)PB.rows * lv_host[0].pitch : 0;
     if (blur && blur_rows_plan(lv_host, nlevels, BR)) {
-        hipLaunchKernelGGL(k_pyramid<true>, dim3(nframes), dim3(PYR_TH), lds, st, bgr, pyr, in_stride, pyr_stride, lv,
-                           rx, ry, PL, nlevels, blur, BR, PB);
+        hipLaunchKernelGGL(k_pyramid<true>, dim3(nframes), dim3(PYR_TH), 0, st, bgr, pyr, in_stride, pyr_stride, lv,
+                           rx, ry, PL, nlevels, blur, BR);
         return;
     }
-    hipLaunchKernelGGL(k_pyramid<false>, dim3(nframes), dim3(PYR_TH), lds, st, bgr, pyr, in_stride, pyr_stride, lv, rx,
-                       ry, PL, nlevels, (uint8_t*)nullptr, BR, PB);
-}
-// Level-0 bands of k_pyramid: PYR_BAND rows each (multiples of the blur's
-// 30- and 6-row chunks, so a band's blur chunks never reach outside the band
-// and its 3-row halos), a remainder under 30 rows joined to the last band;
-// band k makes the level-1 rows whose first source row sy0 lies in it (the
-// second, sy0 + 1, is at most its first halo row).
-void pyramid_band_plan(const LevelDesc* lv_host, const ResizeY* ry, const int* ry_off, int nlevels, PyrBands& B) {
-    B = PyrBands{};
-    if (nlevels < 2 || (lv_host[0].w & 3) != 0) return;
-    for (int l = 0; l < nlevels; l++)
-        if (lv_host[l].h < BR_R) return;
-    const int h = lv_host[0].h;
-    int nb = h / PYR_BAND;
-    if (nb == 0 || h - nb * PYR_BAND >= BR_R) nb++;
-    if (nb > PYR_MAXB) return;
-    int mx = 0;
-    for (int k = 0; k < nb; k++) B.b0[k] = k * PYR_BAND;
-    B.b0[nb] = h;
-    for (int k = 0; k < nb; k++) mx = std::max(mx, B.b0[k + 1] - B.b0[k]);
-    const ResizeY* Y = ry + ry_off[1];
-    const int h1 = lv_host[1].h;
-    int y = 0;
-    for (int k = 0; k < nb; k++) {
-        B.y1[k] = y;
-        while (y < h1 && Y[y].sy0 < B.b0[k + 1]) y++;
-    }
-    B.y1[nb] = h1;
-    for (int k = 0; k < nb; k++)
-        for (int r = B.y1[k]; r < B.y1[k + 1]; r++)
-            if (Y[r].sy0 < std::max(B.b0[k] - 3, 0) || Y[r].sy1 >= std::min(B.b0[k + 1] + 3, h)) return;  // not in the band
-    if ((size_t)(mx + 6) * lv_host[0].pitch > 160 * 1024) return;
-    B.rows = mx + 6;
-    B.nb = nb;
+    hipLaunchKernelGGL(k_pyramid<false>, dim3(nframes), dim3(PYR_TH), 0, st, bgr, pyr, in_stride, pyr_stride, lv, rx,
+                       ry, PL, nlevels, (uint8_t*)nullptr, BR);
 }
 bool pyramid_fusable(const LevelDesc* lv_host, const ResizeX* rx, const int* rx_off, int nlevels) {
     if (nlevels > 16) return false;
@@ -1680,20 +1648,21 @@ void launch_resize(hipStream_t st, uint8_t* pyr, size_t pyr_stride, int src_off,
 bool fast_lds_plan(const FastSeg* segs, int nsegs, FastLds& L) {
     int img = 16, bw = 1, rows = 1, nl = 1;
     for (int k = 0; k < nsegs; k++) {
-        img = std::max(img, (int)segs[k].rows * (int)segs[k].rs);
+        img = std::max(img, (int)segs[k].rows * FS_RS);
         bw = std::max(bw, (int)segs[k].rows * (int)segs[k].bw);
         rows = std::max(rows, (int)segs[k].rows);
-        nl = std::max(nl, (int)segs[k].rs / 4 + FS_NCM);
-        if ((int)segs[k].ncell > FS_NCM || (int)segs[k].rows * (int)segs[k].rs > 65536) return false;
+        nl = std::max(nl, FS_RS / 4 + FS_NCM);
+        if ((int)segs[k].ncell > FS_NCM || (int)segs[k].rows * FS_RS > 65536 || ((segs[k].x0 & 15) + segs[k].cols) > FS_RS)
+            return false;
     }
     auto al = [](int x) { return (x + 15) & ~15; };
     L.img = al(img);
     L.ring = 2 * L.img;
-    L.clist = L.ring + 4 * FS_RING * 2;
+    L.clist = L.ring + (FS_TH / 64) * FS_RSTRIDE * 2;
     L.bits = al(L.clist + FS_CL * 2);
     L.cnt = al(L.bits + bw * 4);
     L.qlist = al(L.cnt + rows * FS_NCM * 4);
-    L.misc = al(L.qlist + nl * 4);
+    L.misc = al(L.qlist + nl * 8);
     L.total = al(L.misc + (int)sizeof(FastMisc));
     return L.total <= 160 * 1024;
 }
@@ -1707,6 +1676,15 @@ void launch_fast(hipStream_t st, const uint8_t* pyr, size_t pyr_stride, const Fa
     }
     hipLaunchKernelGGL(k_fast_seg, dim3(nsegs, nframes), dim3(FS_TH), lds.total, st, pyr, pyr_stride, segs, lv, cand,
                        cand_cnt, ncells, cell_cap, ini_th, min_th, lds);
+#ifdef FS_STATS
+    unsigned long long h[8];
+    (void)hipStreamSynchronize(st);
+    (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(fs_stats), sizeof(h));
+    fprintf(stderr, "fs_stats frames %d segs %d items0 %llu items1 %llu survivors %llu segtest_calls %llu corners %llu ovf %llu retry_cells %llu cells %llu\n",
+            nframes, nsegs, h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]);
+    static const unsigned long long z[8] = {};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(fs_stats), z, sizeof(z));
+#endif
 }
 size_t octree_lds_bytes(int node_cap) { return (size_t)76 * node_cap + 1032; }
 void launch_octree(hipStream_t st, const uint32_t* cand, const int* cand_cnt, const LevelDesc* lv, int ncells,

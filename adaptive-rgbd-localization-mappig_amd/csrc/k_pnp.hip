@@ -884,32 +884,40 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                     }
                 }
                 __syncthreads();
-                // the candidates stay in LDS (s_T / s_M / s_ok) until the
-                // replay below reads the one it accepts: no 4 x 7 doubles held
-                // in registers across the chi pass
+                SE3 Tc[PNP_K];
+                double sc[PNP_K];
+                bool okc[PNP_K];
+#pragma unroll
+                for (int k = 0; k < PNP_K; k++) {
+                    Tc[k].q = Quat{s_T[k][0], s_T[k][1], s_T[k][2], s_T[k][3]};
+                    Tc[k].t[0] = s_T[k][4];
+                    Tc[k].t[1] = s_T[k][5];
+                    Tc[k].t[2] = s_T[k][6];
+                    sc[k] = s_T[k][7];
+                    okc[k] = s_ok[k] != 0;
+                }
                 PP_ACC(tsol);
                 PP_T0();
                 // computeActiveErrors + activeRobustChi2 at every candidate
                 double chi[PNP_K];
 #pragma unroll
                 for (int k = 0; k < PNP_K; k++) chi[k] = 0;
-                // candidate-major: one candidate's matrix live at a time (each
-                // chi[k] still sums the lane's edges in index order)
+                for (int e = lane; e < ne; e += PNP_NT) {
+                    const uint8_t fl = E.flags[e];
+                    if (fl & PE_OUT) continue;
+                    const double Xw[3] = {E.X[3 * e], E.X[3 * e + 1], E.X[3 * e + 2]};
+                    const double ob[3] = {E.obs[3 * e], E.obs[3 * e + 1], E.obs[3 * e + 2]};
+                    const double info = E.info[e];
 #pragma unroll
-                for (int k = 0; k < PNP_K; k++) {
-                    if (k >= K) break;
-                    SE3M Mk;
-#pragma unroll
-                    for (int q = 0; q < 9; q++) Mk.R[q] = s_M[k][q];
-#pragma unroll
-                    for (int q = 0; q < 3; q++) Mk.t[q] = s_M[k][9 + q];
-                    for (int e = lane; e < ne; e += PNP_NT) {
-                        const uint8_t fl = E.flags[e];
-                        if (fl & PE_OUT) continue;
-                        const double Xw[3] = {E.X[3 * e], E.X[3 * e + 1], E.X[3 * e + 2]};
-                        const double ob[3] = {E.obs[3 * e], E.obs[3 * e + 1], E.obs[3 * e + 2]};
+                    for (int k = 0; k < PNP_K; k++) {
+                        if (k >= K) break;
                         double c2;
-                        chi[k] += edge_robust_chi(Mk, Xw, ob, (double)E.info[e], fl, cam, dMono, dStereo, c2);
+                        SE3M Mk;
+#pragma unroll
+                        for (int q = 0; q < 9; q++) Mk.R[q] = s_M[k][q];
+#pragma unroll
+                        for (int q = 0; q < 3; q++) Mk.t[q] = s_M[k][9 + q];
+                        chi[k] += edge_robust_chi(Mk, Xw, ob, info, fl, cam, dMono, dStereo, c2);
                         if (LE) sC[4 * e + k] = (float)c2;
                         else E.chi4[4 * e + k] = c2;
                     }
@@ -924,9 +932,9 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                     ntr++;
 #endif
                     double tempChi = chi[k];
-                    if (s_ok[k] == 0) tempChi = 1.7976931348623157e308;
+                    if (!okc[k]) tempChi = 1.7976931348623157e308;
                     rho = curChi - tempChi;
-                    rho /= s_T[k][7];
+                    rho /= sc[k];
                     last_slot = k;
                     qmax++;
                     if (rho > 0 && isfinite(tempChi)) {
@@ -936,10 +944,7 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                         lambda = lam[k] * sf;
                         ni = 2;
                         curChi = tempChi;
-                        T.q = Quat{s_T[k][0], s_T[k][1], s_T[k][2], s_T[k][3]};
-                        T.t[0] = s_T[k][4];
-                        T.t[1] = s_T[k][5];
-                        T.t[2] = s_T[k][6];
+                        T = Tc[k];
                         trials_done = true;
                     } else {
                         lambda = lam[k] * nis[k];  // T stays at the backup

@@ -116,6 +116,9 @@ struct DevArena {
 // Frame sets in flight (4): batch k extracts into set k%NSETS while the pair and
 // PnP stages of batches k-1 and k-2 still read theirs, so the extraction
 // stream never waits on the PnP latency of the batch just before it.
+#ifndef PYR_WAIT
+#define PYR_WAIT 0
+#endif
 #ifndef ODO_NSETS
 #define ODO_NSETS 4  // measured: 4 sets 60.1k vs 3 sets 57.7k frames/s (256-frame batches)
 #endif
@@ -140,6 +143,11 @@ struct odo_ctx {
     // ODO_KNN_GATE (tuning): the next batch's extraction waits for this
     // batch's kNN-2 (no gray / kNN-2 overlap)
     bool knn_gate = false;
+    // the extraction of batch b waits for the PnP of batch b - pyr_wait (0:
+    // not), so the pyramid does not share the CUs with a PnP / RANSAC
+    // evaluation still running from an earlier batch (PYR_WAIT; ODO_PYR_WAIT)
+    int pyr_wait = PYR_WAIT;
+    int batch_set[8] = {};  // set of batch b at [b & 7]
     hipEvent_t ev_knn = nullptr;
     bool knn_rec = false;
     std::vector<hipStream_t> owned;  // streams created (the rest alias them)
@@ -157,7 +165,6 @@ struct odo_ctx {
     // leave most CUs idle, one frame takes 0.45 vs 0.28 ms)
     int pform = ODO_PYRAMID_FORM_AUTO;
     bool pyr_fusable = false, blur_fusable = false;
-    PyrBands pyr_bands{};  // k_pyramid's level-0 band plan
     LevelDesc* lv = nullptr;
     CellDesc* cells = nullptr;
     ResizeX* rx = nullptr;
@@ -694,15 +701,18 @@ static int build_geometry(odo_ctx* c) {
         }
         L.cell_end = (int)c->cells_h.size();
         // FAST segments (k_fast_seg): each cell row's cells in runs of at most
-        // FS_SEGC, split evenly; the segment's ROI union is cells_h[ci0 ..
-        // ci0 + ncell) (pushed above in row-major order)
+        // FS_SEGC whose ROI union (plus up to 15 bytes of alignment) fits the
+        // FS_RS-byte LDS row, split evenly; the segment's ROI union is
+        // cells_h[ci0 .. ci0 + ncell) (pushed above in row-major order)
         {
             const int nct = L.cell_end - L.cell_begin;
             int ncj = 0;  // cells per row (the skipped columns are the last ones)
             for (int j = 0; j < nCols; j++)
                 if ((float)(minBorderX + j * wCell) < (float)(maxBorderX - 6)) ncj++;
             if (ncj > 0 && nct % ncj == 0) {
-                const int nrow = nct / ncj, nseg = (ncj + FS_SEGC - 1) / FS_SEGC;
+                const int kmax = std::min(FS_SEGC, (FS_RS - 15 - 6) / wCell);
+                if (kmax < 1) return fail(ODO_ERR_ARG, "FAST cell wider than a segment row");
+                const int nrow = nct / ncj, nseg = (ncj + kmax - 1) / kmax;
                 for (int ir = 0; ir < nrow; ir++)
                     for (int sg = 0; sg < nseg; sg++) {
                         const int ja = ncj * sg / nseg, jb = ncj * (sg + 1) / nseg;
@@ -717,10 +727,8 @@ static int build_geometry(odo_ctx* c) {
                         G.cols = (int16_t)(B.x0 + B.cols - A.x0);
                         G.ncell = (int16_t)(jb - ja);
                         G.wcell = (int16_t)wCell;
-                        const int nw = ((A.x0 & 15) + G.cols + 15) >> 4;
-                        G.rs = (int16_t)(16 * nw);
                         G.bw = (int16_t)((G.cols + 31) >> 5);
-                        if (nw > 256 || G.ncell > FS_NCM || G.rows > 70 || (int)G.rows * G.rs > 65536)
+                        if ((A.x0 & 15) + G.cols > FS_RS || G.ncell > FS_NCM || G.rows > 70 || (int)G.rows * FS_RS > 65536)
                             return fail(ODO_ERR_ARG, "FAST segment too large");
                         c->fsegs_h.push_back(G);
                     }
@@ -839,7 +847,6 @@ static int build_geometry(odo_ctx* c) {
     c->pyr_fusable = pyramid_fusable(c->lv_h.data(), rx.data(), c->rx_off.data(), p.nlevels);
     c->blur_fusable = c->pyr_fusable && pyramid_blur_fusable(c->lv_h.data(), p.nlevels);
     if (p.nlevels <= 16) {
-        pyramid_band_plan(c->lv_h.data(), ry.data(), c->ry_off.data(), p.nlevels, c->pyr_bands);
     }
     int e;
     if ((e = dalloc(&c->lv, c->lv_h.size()))) return e;
@@ -1075,6 +1082,7 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
         if (const char* np = odo_knob("ODO_PSTREAMS")) c->npstreams = std::min(3, std::max(1, atoi(np)));
         if (const char* kp = odo_knob("ODO_KNN_PAIR")) c->knn_pair = atoi(kp) != 0;
         if (const char* kg = odo_knob("ODO_KNN_GATE")) c->knn_gate = atoi(kg) != 0;
+        if (const char* pw = odo_knob("ODO_PYR_WAIT")) c->pyr_wait = std::min(NSETS - 1, std::max(0, atoi(pw)));
         ok = mk(&c->pstream, true) && (c->npstreams < 2 || mk(&c->pstream2, true)) &&
              (c->npstreams < 3 || mk(&c->pstream3, true));
         if (c->npstreams < 2) c->pstream2 = c->pstream;
@@ -1233,7 +1241,7 @@ static bool build_pyramid(odo_ctx* c, hipStream_t st, const uint8_t* d_bgr, uint
             d_bgr = nullptr;
         }
         launch_pyramid(st, d_bgr, pyr, (size_t)c->W * c->H * 3, P, c->lv, c->rx, c->ry, c->rx_off.data(),
-                       c->ry_off.data(), c->nlevels, n, blur, c->lv_h.data(), c->pyr_bands);
+                       c->ry_off.data(), c->nlevels, n, blur, c->lv_h.data());
         return blur != nullptr;
     }
     if (d_bgr) launch_gray(st, d_bgr, pyr, c->W, c->H, c->lv_h[0].pitch, (size_t)c->W * c->H * 3, P, n);
@@ -1508,6 +1516,11 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
         HIPCHK(hipStreamWaitEvent(c->stream, c->ev_pb[s], 0));
     }
     if (c->knn_gate && c->knn_rec) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_knn, 0));
+    if (c->sched == 5 && c->pyr_wait > 0 && c->batch_counter >= (uint64_t)c->pyr_wait) {
+        const int sb = c->batch_set[(c->batch_counter - (uint64_t)c->pyr_wait) & 7];
+        HIPCHK(hipStreamWaitEvent(c->stream, c->ev_pa[sb], 0));
+        HIPCHK(hipStreamWaitEvent(c->stream, c->ev_pb[sb], 0));
+    }
     tmark(c, 0, c->stream);
     if (c->has_prev) {
         // the previous batch's last frame becomes slot 0 (Tracking::mLastFrame)
@@ -1626,6 +1639,7 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
     c->last_n = n;
     c->has_prev = true;
     c->pair_counter += (uint64_t)n;
+    c->batch_set[c->batch_counter & 7] = s;
     c->batch_counter++;
     if ((e = finish_batch(c, s, n, h_results))) return e;
     return ODO_OK;

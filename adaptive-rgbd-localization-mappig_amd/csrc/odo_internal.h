@@ -56,10 +56,15 @@ struct CellDesc {
 #define FS_SEGC 8  // cells per segment (at most; the host splits a cell row evenly)
 #endif
 #define FS_NCM FS_SEGC
+// LDS row stride of a staged segment (bytes): a compile-time constant, so the
+// kernel's neighbour offsets (the 16 circle pixels, the compass points, the
+// NMS neighbours) are instruction immediates and a byte offset splits into
+// (row, column) with a shift; the host sizes segments to fit it
+#define FS_RS 256
 struct FastSeg {
     int level, ci0;
     int16_t y0, x0, rows, cols, ncell, wcell;
-    int16_t rs, bw;  // LDS row stride (bytes, a multiple of 16), kept-bitmap words per row
+    int16_t bw, pad;  // kept-bitmap words per row
 };
 // k_fast_seg's dynamic LDS: byte offsets of its regions
 struct FastLds {
@@ -202,24 +207,9 @@ size_t resize_lds_bytes(int spitch, int dw, int max_src_rows);
 // gray + every pyramid level in one launch (one workgroup per frame); bgr may be
 // null (level 0 already in place). pyramid_fusable: the host check of its
 // assumptions (<= 16 levels, <= 4096 px wide, each quad's taps inside 8 bytes)
-// k_pyramid's level-0 bands (round 5): level 0 is built band by band in LDS
-// (gray of the band + its 3-row halos), and its blur and level 1 are made
-// from the band in LDS, so level 0 is written once and never read back.
-// Bands of PYR_BAND rows (a multiple of the blur's 30- and 6-row chunks),
-// the last one 30..PYR_BAND+29 rows; nb = 0: level 0 is not banded (no BGR
-// input, a width that is not a multiple of 4, or a level under 30 rows).
-#define PYR_BAND 60
-#define PYR_MAXB 64
-struct PyrBands {
-    int nb;
-    int rows;               // LDS rows of the band buffer (largest band + 6)
-    int b0[PYR_MAXB + 1];   // band k: level-0 rows [b0[k], b0[k+1])
-    int y1[PYR_MAXB + 1];   // the level-1 rows it makes: [y1[k], y1[k+1]) (their sy0 in the band)
-};
-void pyramid_band_plan(const LevelDesc* lv_host, const ResizeY* ry, const int* ry_off, int nlevels, PyrBands& B);
 void launch_pyramid(hipStream_t st, const uint8_t* bgr, uint8_t* pyr, size_t in_stride, size_t pyr_stride,
                     const LevelDesc* lv, const ResizeX* rx, const ResizeY* ry, const int* rx_off, const int* ry_off,
-                    int nlevels, int nframes, uint8_t* blur, const LevelDesc* lv_host, const PyrBands& bands);
+                    int nlevels, int nframes, uint8_t* blur, const LevelDesc* lv_host);
 // blur: the blurred pyramid is written by the same launch (null: not);
 // pyramid_blur_fusable: every level is large enough for the strip walks
 bool pyramid_blur_fusable(const LevelDesc* lv_host, int nlevels);
