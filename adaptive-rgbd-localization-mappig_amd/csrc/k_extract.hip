@@ -546,35 +546,72 @@ struct ONode {
 #define OT_THREADS 256  // threads per (frame, level) workgroup
 #endif
 
+// The workgroup's keys k = t, t + OT_THREADS, ... in batches of OT_KB per
+// thread: ld(k, u) issues a batch's global loads (keys / knode / kquad live in
+// HBM scratch) before pr(k, u) consumes them, so a pass over the keys waits
+// one memory latency per batch instead of one per key (round 5)
+#ifndef OT_KB
+#define OT_KB 8
+#endif
+#ifndef OT_RANK_MAX
+#define OT_RANK_MAX 512  // phase 2's node ranks counted (not sorted) up to this many entries
+#endif
+template <typename Ld, typename Pr>
+ODO_INLINE void ot_keys(int n, int t, Ld&& ld, Pr&& pr) {
+    for (int k0 = t; k0 < n; k0 += OT_THREADS * OT_KB) {
+#pragma unroll
+        for (int u = 0; u < OT_KB; u++)
+            if (k0 + u * OT_THREADS < n) ld(k0 + u * OT_THREADS, u);
+#pragma unroll
+        for (int u = 0; u < OT_KB; u++)
+            if (k0 + u * OT_THREADS < n) pr(k0 + u * OT_THREADS, u);
+    }
+}
+
 // vSizeAndPointerToNode entry: sorts by (size, creation seq); low 16 bits carry
 // the node's list position (never compared: seq is unique).
 ODO_INLINE uint64_t ot_key(int cnt, int seq, int pos) {
     return ((uint64_t)(uint32_t)cnt << 40) | ((uint64_t)(uint32_t)(seq & 0xFFFFFF) << 16) | (uint64_t)(pos & 0xFFFF);
 }
 
-// Block-wide exclusive scan in threadIdx order: inclusive wave scans with
-// shuffles, then the wave totals (tmp: OT_THREADS/64 entries) in one LDS step.
-template <typename T>
-ODO_INLINE T block_exclusive_scan(T v, T* tmp, T* total) {
+// Block-wide exclusive scans in threadIdx order: DPP wave scans
+// (wave_incl_scan), then the wave totals (tmp: OT_THREADS/64 ints per value)
+// in one LDS step. (Until round 5 the wave scans were __shfl_up chains: six
+// dependent ds_bpermute round trips per scan.)
+ODO_INLINE int block_exclusive_scan(int v, int* tmp, int* total) {
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    T x = v;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const T y = __shfl_up(x, off);
-        if (lane >= off) x += y;
-    }
+    const int x = wave_incl_scan(v);
     if (lane == 63) tmp[wave] = x;
     __syncthreads();
-    T base = 0, tot = 0;
+    int base = 0, tot = 0;
 #pragma unroll
     for (int w = 0; w < OT_THREADS / 64; w++) {
-        const T sw = tmp[w];
+        const int sw = tmp[w];
         if (w < wave) base += sw;
         tot += sw;
     }
     *total = tot;
     __syncthreads();
     return base + x - v;
+}
+// two values at once (tmp: 2 * OT_THREADS/64 ints)
+ODO_INLINE int2 block_exclusive_scan2(int a, int b, int* tmp, int2* total) {
+    constexpr int NWV = OT_THREADS / 64;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int xa = wave_incl_scan(a), xb = wave_incl_scan(b);
+    if (lane == 63) tmp[wave] = xa, tmp[NWV + wave] = xb;
+    __syncthreads();
+    int ba = 0, bb = 0, ta = 0, tb = 0;
+#pragma unroll
+    for (int w = 0; w < NWV; w++) {
+        const int sa = tmp[w], sb = tmp[NWV + w];
+        if (w < wave) ba += sa, bb += sb;
+        ta += sa;
+        tb += sb;
+    }
+    *total = int2{ta, tb};
+    __syncthreads();
+    return int2{ba + xa - a, bb + xb - b};
 }
 
 __global__ void __launch_bounds__(OT_THREADS) k_octree(const uint32_t* __restrict__ cand,
@@ -607,7 +644,6 @@ __global__ void __launch_bounds__(OT_THREADS) k_octree(const uint32_t* __restric
     int* scan = iscr + node_cap;                                   // OT_THREADS
     uint64_t* sortk = reinterpret_cast<uint64_t*>(scan + OT_THREADS + 2);  // node_cap (pow2) sort keys
     __shared__ __attribute__((aligned(16))) int s_vars[16];
-    __shared__ uint64_t s_scan64[OT_THREADS / 64];
     int& s_J = s_vars[6];
     int& s_size = s_vars[0];
     int& s_prev = s_vars[1];
@@ -629,7 +665,7 @@ __global__ void __launch_bounds__(OT_THREADS) k_octree(const uint32_t* __restric
         const int c = cb + t;
         const int cnt = c < nc ? cand_cnt[(size_t)f * ncells + c0 + c] : 0;
         int tot;
-        const int ex = block_exclusive_scan<int>(cnt, scan, &tot);
+        const int ex = block_exclusive_scan(cnt, scan, &tot);
         if (c < nc) {
             // 32 candidates in flight per batch (cell rows are 16-byte aligned):
             // a load-then-store loop would wait out one memory latency per 4 keys
@@ -674,13 +710,17 @@ __global__ void __launch_bounds__(OT_THREADS) k_octree(const uint32_t* __restric
         nodesA[i] = nd;
     }
     __syncthreads();
-    for (int k = t; k < n; k += OT_THREADS) {
-        const uint32_t key = keys[k];
-        const float x = (float)(key & 0xfff);
-        const int ni = (int)(x / hX);
-        knode[k] = ni;
-        atomicAdd(&nodesA[ni].cnt, 1);
-    }
+    uint32_t ky[OT_KB];
+    int nd[OT_KB];
+    uint8_t kq[OT_KB];
+    ot_keys(
+        n, t, [&](int k, int u) { ky[u] = keys[k]; },
+        [&](int k, int u) {
+            const float x = (float)(ky[u] & 0xfff);
+            const int ni = (int)(x / hX);
+            knode[k] = ni;
+            atomicAdd(&nodesA[ni].cnt, 1);
+        });
     __syncthreads();
     // erase empty initial nodes (keep order)
     if (t == 0) {
@@ -698,7 +738,8 @@ __global__ void __launch_bounds__(OT_THREADS) k_octree(const uint32_t* __restric
         s_phase = 1;
     }
     __syncthreads();
-    for (int k = t; k < n; k += OT_THREADS) knode[k] = iscr[knode[k]];
+    ot_keys(
+        n, t, [&](int k, int u) { nd[u] = knode[k]; }, [&](int k, int u) { knode[k] = iscr[nd[u]]; });
     for (int i = t; i < s_size; i += OT_THREADS) nodesA[i] = nodesB[i];
     __syncthreads();
 
@@ -713,19 +754,23 @@ __global__ void __launch_bounds__(OT_THREADS) k_octree(const uint32_t* __restric
             // ---------------- phase 1: divide every node with >1 keys
             for (int i = t; i < 4 * S; i += OT_THREADS) cc[i] = 0;
             __syncthreads();
-            for (int k = t; k < n; k += OT_THREADS) {
-                const int nd = knode[k];
-                const ONode N0 = cur[nd];
-                if (N0.cnt > 1) {
-                    const uint32_t key = keys[k];
-                    const int x = key & 0xfff, y = (key >> 12) & 0xfff;
-                    const int hx = (N0.x1 - N0.x0 + 1) >> 1;  // ceil((x1-x0)/2), x1>=x0
-                    const int hy = (N0.y1 - N0.y0 + 1) >> 1;
-                    const int q = (x < N0.x0 + hx) ? (y < N0.y0 + hy ? 0 : 2) : (y < N0.y0 + hy ? 1 : 3);
-                    kquad[k] = (uint8_t)q;
-                    atomicAdd(&cc[nd * 4 + q], 1);
-                }
-            }
+            ot_keys(
+                n, t,
+                [&](int k, int u) {
+                    nd[u] = knode[k];
+                    ky[u] = keys[k];
+                },
+                [&](int k, int u) {
+                    const ONode N0 = cur[nd[u]];
+                    if (N0.cnt > 1) {
+                        const int x = ky[u] & 0xfff, y = (ky[u] >> 12) & 0xfff;
+                        const int hx = (N0.x1 - N0.x0 + 1) >> 1;  // ceil((x1-x0)/2), x1>=x0
+                        const int hy = (N0.y1 - N0.y0 + 1) >> 1;
+                        const int q = (x < N0.x0 + hx) ? (y < N0.y0 + hy ? 0 : 2) : (y < N0.y0 + hy ? 1 : 3);
+                        kquad[k] = (uint8_t)q;
+                        atomicAdd(&cc[nd[u] * 4 + q], 1);
+                    }
+                });
             __syncthreads();
             // per-node children stats, scans over list order (chunks of OT_THREADS)
             int childBase = 0, survBase = 0, expBase = 0;
@@ -744,12 +789,12 @@ __global__ void __launch_bounds__(OT_THREADS) k_octree(const uint32_t* __restric
                         }
                     } else s = 1;
                 }
-                // one scan of the three counts packed in 21-bit fields
-                uint64_t tp;
-                const uint64_t ex = block_exclusive_scan<uint64_t>(
-                    (uint64_t)e | ((uint64_t)ne << 21) | ((uint64_t)s << 42), s_scan64, &tp);
-                const int ex_e = (int)(ex & 0x1FFFFF), ex_ne = (int)((ex >> 21) & 0x1FFFFF), ex_s = (int)(ex >> 42);
-                const int te = (int)(tp & 0x1FFFFF), tne = (int)((tp >> 21) & 0x1FFFFF), ts = (int)(tp >> 42);
+                // one scan of the three counts: (e, ne) packed in 16-bit
+                // fields (each <= 4 * node_cap <= 8192), s beside them
+                int2 tp;
+                const int2 ex = block_exclusive_scan2(e | (ne << 16), s, scan, &tp);
+                const int ex_e = ex.x & 0xFFFF, ex_ne = ex.x >> 16, ex_s = ex.y;
+                const int te = tp.x & 0xFFFF, tne = tp.x >> 16, ts = tp.y;
                 if (i < S) {
                     iscr[i] = childBase + ex_e;          // forward children prefix
                     npos[i * 4 + 0] = e;                 // stash e
@@ -808,11 +853,13 @@ __global__ void __launch_bounds__(OT_THREADS) k_octree(const uint32_t* __restric
                 }
             }
             __syncthreads();
-            for (int k = t; k < n; k += OT_THREADS) {
-                const int nd = knode[k];
-                if (cur[nd].cnt > 1) knode[k] = cc[nd * 4 + kquad[k]];
-                else knode[k] = cc[nd * 4 + 0];
-            }
+            ot_keys(
+                n, t,
+                [&](int k, int u) {
+                    nd[u] = knode[k];
+                    kq[u] = kquad[k];
+                },
+                [&](int k, int u) { knode[k] = cc[nd[u] * 4 + (cur[nd[u]].cnt > 1 ? kq[u] : 0)]; });
             __syncthreads();
             if (t == 0) {
                 s_prev = S;
@@ -830,47 +877,72 @@ __global__ void __launch_bounds__(OT_THREADS) k_octree(const uint32_t* __restric
         } else {
             // ---------------- phase 2: divide the largest nodes first
             vcount = s_vcnt;
-            // bitonic sort of sortk[0..vcount) ascending by (cnt, seq)
-            int pw = 1;
-            while (pw < vcount) pw <<= 1;
-            for (int i = vcount + t; i < pw; i += OT_THREADS) sortk[i] = ~0ull;
-            __syncthreads();
-            for (int kk = 2; kk <= pw; kk <<= 1) {
-                for (int jj = kk >> 1; jj > 0; jj >>= 1) {
-                    for (int i = t; i < pw; i += OT_THREADS) {
-                        const int ixj = i ^ jj;
-                        if (ixj > i) {
-                            const uint64_t a = sortk[i], b = sortk[ixj];
-                            const bool up = (i & kk) == 0;
-                            if ((a > b) == up) {
-                                sortk[i] = b;
-                                sortk[ixj] = a;
+            // processing rank per node: the entries of sortk[0..vcount)
+            // descending by (cnt, seq), the node of the j-th one processed
+            // j-th. The keys are unique (seq is), so an entry's place is the
+            // number of larger entries: counted directly while vcount is
+            // small (one barrier; round 5), a bitonic sort beyond
+            for (int i = t; i < S; i += OT_THREADS) iscr[i] = -1;
+            if (vcount <= OT_RANK_MAX) {
+                __syncthreads();  // every iscr reset
+                for (int i = t; i < vcount; i += OT_THREADS) {
+                    const uint64_t ki = sortk[i];
+                    int above = 0, j = 0;
+                    // eight broadcast reads in flight per step
+                    for (; j + 8 <= vcount; j += 8) {
+                        uint64_t kj[8];
+#pragma unroll
+                        for (int u = 0; u < 8; u++) kj[u] = sortk[j + u];
+#pragma unroll
+                        for (int u = 0; u < 8; u++) above += kj[u] > ki;
+                    }
+                    for (; j < vcount; j++) above += sortk[j] > ki;
+                    iscr[(int)(ki & 0xFFFF)] = above;
+                }
+                __syncthreads();
+            } else {
+                int pw = 1;
+                while (pw < vcount) pw <<= 1;
+                for (int i = vcount + t; i < pw; i += OT_THREADS) sortk[i] = ~0ull;
+                __syncthreads();
+                for (int kk = 2; kk <= pw; kk <<= 1) {
+                    for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+                        for (int i = t; i < pw; i += OT_THREADS) {
+                            const int ixj = i ^ jj;
+                            if (ixj > i) {
+                                const uint64_t a = sortk[i], b = sortk[ixj];
+                                const bool up = (i & kk) == 0;
+                                if ((a > b) == up) {
+                                    sortk[i] = b;
+                                    sortk[ixj] = a;
+                                }
                             }
                         }
+                        __syncthreads();
                     }
-                    __syncthreads();
                 }
+                for (int j = t; j < vcount; j += OT_THREADS) iscr[(int)(sortk[vcount - 1 - j] & 0xFFFF)] = j;
+                __syncthreads();
             }
-            // processing rank per node: node of sortk[vcount-1-j] is processed j-th
-            for (int i = t; i < S; i += OT_THREADS) iscr[i] = -1;
-            __syncthreads();
-            for (int j = t; j < vcount; j += OT_THREADS) iscr[(int)(sortk[vcount - 1 - j] & 0xFFFF)] = j;
-            __syncthreads();
             for (int i = t; i < 4 * S; i += OT_THREADS) cc[i] = 0;
             __syncthreads();
-            for (int k = t; k < n; k += OT_THREADS) {
-                const int nd = knode[k];
-                if (iscr[nd] >= 0) {
-                    const ONode N0 = cur[nd];
-                    const uint32_t key = keys[k];
-                    const int x = key & 0xfff, y = (key >> 12) & 0xfff;
-                    const int hx = (N0.x1 - N0.x0 + 1) >> 1;
-                    const int hy = (N0.y1 - N0.y0 + 1) >> 1;
-                    const int q = (x < N0.x0 + hx) ? (y < N0.y0 + hy ? 0 : 2) : (y < N0.y0 + hy ? 1 : 3);
-                    kquad[k] = (uint8_t)q;
-                    atomicAdd(&cc[nd * 4 + q], 1);
-                }
-            }
+            ot_keys(
+                n, t,
+                [&](int k, int u) {
+                    nd[u] = knode[k];
+                    ky[u] = keys[k];
+                },
+                [&](int k, int u) {
+                    if (iscr[nd[u]] >= 0) {
+                        const ONode N0 = cur[nd[u]];
+                        const int x = ky[u] & 0xfff, y = (ky[u] >> 12) & 0xfff;
+                        const int hx = (N0.x1 - N0.x0 + 1) >> 1;
+                        const int hy = (N0.y1 - N0.y0 + 1) >> 1;
+                        const int q = (x < N0.x0 + hx) ? (y < N0.y0 + hy ? 0 : 2) : (y < N0.y0 + hy ? 1 : 3);
+                        kquad[k] = (uint8_t)q;
+                        atomicAdd(&cc[nd[u] * 4 + q], 1);
+                    }
+                });
             __syncthreads();
             // Node divisions in processing order j (largest first) until the
             // list reaches N: with e_j the non-empty children of node proc[j],
@@ -899,7 +971,7 @@ __global__ void __launch_bounds__(OT_THREADS) k_octree(const uint32_t* __restric
                         }
                     }
                     int tot;
-                    const int ex = block_exclusive_scan<int>(e | (v << 16), scan, &tot);
+                    const int ex = block_exclusive_scan(e | (v << 16), scan, &tot);
                     if (j < vcount) {
                         const int ei = eb + (ex & 0xFFFF) + e;
                         eincl[j] = ei;
@@ -958,7 +1030,7 @@ __global__ void __launch_bounds__(OT_THREADS) k_octree(const uint32_t* __restric
                     sv = !(j >= 0 && j < J);
                 }
                 int tot;
-                const int ex = block_exclusive_scan<int>(sv, scan, &tot);
+                const int ex = block_exclusive_scan(sv, scan, &tot);
                 if (sv) {
                     const int pp = EJ + sb + ex;
                     nxt[pp] = cur[i];
@@ -976,11 +1048,16 @@ __global__ void __launch_bounds__(OT_THREADS) k_octree(const uint32_t* __restric
                 if (size >= N || size == S) s_finish = 1;
             }
             __syncthreads();
-            for (int k = t; k < n; k += OT_THREADS) {
-                const int nd = knode[k];
-                if (iscr[nd] == -2 || iscr[nd] == -1) knode[k] = cc[nd * 4 + 0];
-                else knode[k] = cc[nd * 4 + kquad[k]];
-            }
+            ot_keys(
+                n, t,
+                [&](int k, int u) {
+                    nd[u] = knode[k];
+                    kq[u] = kquad[k];
+                },
+                [&](int k, int u) {
+                    const int is = iscr[nd[u]];
+                    knode[k] = cc[nd[u] * 4 + (is == -2 || is == -1 ? 0 : kq[u])];
+                });
             __syncthreads();
             ONode* tmpp = cur;
             cur = nxt;
@@ -993,11 +1070,13 @@ __global__ void __launch_bounds__(OT_THREADS) k_octree(const uint32_t* __restric
     unsigned* best = reinterpret_cast<unsigned*>(cc);
     for (int i = t; i < S; i += OT_THREADS) best[i] = 0;
     __syncthreads();
-    for (int k = t; k < n; k += OT_THREADS) {
-        const uint32_t key = keys[k];
-        const unsigned v = ((key >> 24) << 23) | (0x7FFFFFu - (unsigned)k);
-        atomicMax(&best[knode[k]], v);
-    }
+    ot_keys(
+        n, t,
+        [&](int k, int u) {
+            ky[u] = keys[k];
+            nd[u] = knode[k];
+        },
+        [&](int k, int u) { atomicMax(&best[nd[u]], ((ky[u] >> 24) << 23) | (0x7FFFFFu - (unsigned)k)); });
     __syncthreads();
     const int cap = okp_stride;
     for (int i = t; i < S && i < cap; i += OT_THREADS) {
