@@ -27,6 +27,12 @@ namespace odo {
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 __constant__ float4 c_patf[256];  // ORB_SLAM2 pattern test t: (x0, y0, x1, y1)
+// the same tests as signed bytes, lane-major: c_pat8[s * 16 + w] = test w * 16 + s
+// (k_finalize_lds lane s's sixteen tests in 64 contiguous bytes)
+__constant__ uint32_t c_pat8[256];
+#ifndef FIN_PAT
+#define FIN_PAT 2  // k_finalize_lds's pattern source: 0 c_patf, 1 an LDS copy of it, 2 c_pat8
+#endif
 __constant__ int c_umax16[16];    // IC_Angle disc half-widths per |v|
 
 // 1.5 * 2^23: for |x| < 2^22, the float sum x + RND_MAGIC is x rounded half to
@@ -240,6 +246,10 @@ __global__ void __launch_bounds__(64 * NW) k_finalize_lds(const uint8_t* __restr
     // group read 16 different rows, which at 8 dwords met on 2 banks each
     __shared__ __attribute__((aligned(16))) uint32_t s_disc[16][12];
     __shared__ __attribute__((aligned(16))) uint32_t s_patch[NW * FIN_KPW][FL_KP_DW];
+#if FIN_PAT == 1
+    __shared__ float4 s_pat[256];
+    for (int d = threadIdx.x; d < 256; d += 64 * NW) s_pat[d] = c_patf[d];
+#endif
     for (int d = threadIdx.x; d < 128; d += 64 * NW) {
         const int av = d >> 3, i = d & 7;
         const int um = c_umax16[av];
@@ -283,50 +293,67 @@ __global__ void __launch_bounds__(64 * NW) k_finalize_lds(const uint8_t* __restr
     const uint32_t key = valid ? okp[((size_t)f * nlevels + lvl) * okp_stride + k] : (16u | (16u << 12));
     const int kx = (int)(key & 0xfff) + 16, ky = (int)((key >> 12) & 0xfff) + 16;
     const float resp = (float)(key >> 24);
-    uint32_t vbr[24];  // the rBRIEF window's dwords (in flight during the IC angle)
+    uint2 vbr[12];  // the rBRIEF window's dwords (in flight during the IC angle)
     uint32_t* P = s_patch[kslot];
     const int sh = (kx - 15) & 3, sh2 = (kx - 18) & 3;
     {
-        uint32_t v[18 + 24];
+        // Round 5: the windows as row chunks — the IC disc's 31 rows of 9
+        // dwords as 93 chunks of 3 (global_load_dwordx3), the rBRIEF
+        // window's 37 rows of 10 as 185 chunks of 2 (dwordx2) — chunk
+        // sub + 16 j of the keypoint's 16 lanes. Until round 4 every lane
+        // loaded single dwords: 42 load instructions per wave, and the
+        // texture address / data units ran 93 % / 94 % busy for the whole
+        // kernel (PMC, profiles/r05_l/pmcx_tex): 18 instructions now.
         // 32-bit byte offsets from the frame's base (uniform over the
-        // workgroup: scalar base + vector offset loads), advanced per step
-        // of 16 staged dwords without divisions: 16 = 9 + 7 (IC rows of 9
-        // dwords) and 16 = 10 + 6 (rBRIEF rows of 10); a lane past the end
-        // reloads the last dword, as the clamped index did
+        // workgroup: scalar base + vector offset loads); chunk rows and
+        // columns stepped by 16 chunks without divisions (16 = 5 rows of 3
+        // + 1, = 3 rows of 5 + 1); a lane past the end reloads the last chunk
         const uint8_t* fpyr = pyr + (size_t)f * pyr_stride;
         const uint8_t* fblur = blur + (size_t)f * pyr_stride;
         const uint32_t pitch = (uint32_t)L.pitch;
+        uint3 v[6];
         {
             const uint32_t o0 = (uint32_t)L.off + (uint32_t)(ky - 15) * pitch + (uint32_t)(kx - 15 - sh);
-            const uint32_t olast = o0 + 30u * pitch + 4u * 8u;
-            int c = sub % FL_IC_W;
-            uint32_t o = o0 + (uint32_t)(sub / FL_IC_W) * pitch + 4u * (uint32_t)c;
+            const uint32_t olast = o0 + 30u * pitch + 24u;
+            int p = sub % 3;
+            uint32_t o = o0 + (uint32_t)(sub / 3) * pitch + 12u * (uint32_t)p;
 #pragma unroll
-            for (int j = 0; j < 18; j++) {
-                v[j] = *reinterpret_cast<const uint32_t*>(fpyr + (sub + 16 * j < FL_IC_N ? o : olast));
-                const bool one = c < 2;
-                o += one ? pitch + 28u : 2u * pitch - 8u;
-                c = one ? c + 7 : c - 2;
+            for (int j = 0; j < 6; j++) {
+                v[j] = *reinterpret_cast<const uint3*>(fpyr + (sub + 16 * j < 93 ? o : olast));
+                const bool wrap = p == 2;
+                o += wrap ? 6u * pitch - 24u : 5u * pitch + 12u;
+                p = wrap ? 0 : p + 1;
             }
         }
         {
             const uint32_t o0 = (uint32_t)L.off + (uint32_t)(ky - 18) * pitch + (uint32_t)(kx - 18 - sh2);
-            const uint32_t olast = o0 + 36u * pitch + 4u * 9u;
-            int c = sub % FL_BR_W;
-            uint32_t o = o0 + (uint32_t)(sub / FL_BR_W) * pitch + 4u * (uint32_t)c;
+            const uint32_t olast = o0 + 36u * pitch + 32u;
+            int p = sub % 5;
+            uint32_t o = o0 + (uint32_t)(sub / 5) * pitch + 8u * (uint32_t)p;
 #pragma unroll
-            for (int j = 0; j < 24; j++) {
-                v[18 + j] = *reinterpret_cast<const uint32_t*>(fblur + (sub + 16 * j < FL_BR_N ? o : olast));
-                const bool one = c < 4;
-                o += one ? pitch + 24u : 2u * pitch - 16u;
-                c = one ? c + 6 : c - 4;
+            for (int j = 0; j < 12; j++) {
+                vbr[j] = *reinterpret_cast<const uint2*>(fblur + (sub + 16 * j < 185 ? o : olast));
+                const bool wrap = p == 4;
+                o += wrap ? 4u * pitch - 32u : 3u * pitch + 8u;
+                p = wrap ? 0 : p + 1;
             }
         }
+        // IC chunk c = sub + 16 j: row c / 3, dwords 3 (c % 3) .. + 2 of it
+        {
+            int r = sub / 3, p = sub % 3;
 #pragma unroll
-        for (int j = 0; j < 18; j++)
-            if (sub + 16 * j < FL_IC_N) P[sub + 16 * j] = v[j];
-#pragma unroll
-        for (int j = 0; j < 24; j++) vbr[j] = v[18 + j];
+            for (int j = 0; j < 6; j++) {
+                if (sub + 16 * j < 93) {
+                    uint32_t* d = P + r * FL_IC_W + 3 * p;
+                    d[0] = v[j].x;
+                    d[1] = v[j].y;
+                    d[2] = v[j].z;
+                }
+                const bool wrap = p == 2;
+                r += wrap ? 6 : 5;
+                p = wrap ? 0 : p + 1;
+            }
+        }
     }
     __syncthreads();  // s_disc, the patches
     int m10, m01;
@@ -377,22 +404,48 @@ __global__ void __launch_bounds__(64 * NW) k_finalize_lds(const uint8_t* __restr
     // staged byte of rotated offset (iy, ix): (iy + 18) * 40 + ix + 18 + sh2; the
     // magic-rounded floats carry RND_BITS + offset in their bits
     __syncthreads();  // every IC disc read
+    {
+        // rBRIEF chunk c = sub + 16 j: row c / 5, dwords 2 (c % 5), + 1
+        int r = sub / 5, p = sub % 5;
 #pragma unroll
-    for (int j = 0; j < 24; j++)
-        if (sub + 16 * j < FL_BR_N) P[sub + 16 * j] = vbr[j];
+        for (int j = 0; j < 12; j++) {
+            if (sub + 16 * j < 185) *reinterpret_cast<uint2*>(P + r * FL_BR_W + 2 * p) = vbr[j];
+            const bool wrap = p == 4;
+            r += wrap ? 4 : 3;
+            p = wrap ? 0 : p + 1;
+        }
+    }
     __syncthreads();
     const uint8_t* PB = reinterpret_cast<const uint8_t*>(P);
-    const uint32_t cofs = (uint32_t)(18 * 4 * FL_BR_W + 18 + sh2) - RND_BITS * (uint32_t)(4 * FL_BR_W + 1);  // mod 2^32
+    // iy's low 24 bits are 0x400000 + dy (a 24-bit multiply: v_mad_u32_u24,
+    // full rate, where the 32-bit product took v_mad_u64_u32 until round 5)
+    const uint32_t cofs = (uint32_t)(18 * 4 * FL_BR_W + 18 + sh2) - 0x400000u * (uint32_t)(4 * FL_BR_W) - RND_BITS;  // mod 2^32
     int tv0[16], tv1[16];
+#if FIN_PAT == 2
+    uint32_t pat8[16];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const uint4 q = reinterpret_cast<const uint4*>(c_pat8)[sub * 4 + u];
+        pat8[4 * u] = q.x, pat8[4 * u + 1] = q.y, pat8[4 * u + 2] = q.z, pat8[4 * u + 3] = q.w;
+    }
+#endif
 #pragma unroll
     for (int w = 0; w < 16; w++) {
+#if FIN_PAT == 2
+        const uint32_t pw = pat8[w];
+        const float4 Pt = {(float)(int8_t)(pw & 0xff), (float)(int8_t)((pw >> 8) & 0xff),
+                           (float)(int8_t)((pw >> 16) & 0xff), (float)(int8_t)(pw >> 24)};
+#elif FIN_PAT == 1
+        const float4 Pt = s_pat[w * 16 + sub];
+#else
         const float4 Pt = c_patf[w * 16 + sub];
+#endif
         f32x2 q0 = (f32x2){Pt.x, Pt.x} * BA + (f32x2){Pt.y, -Pt.y} * AB;
         f32x2 q1 = (f32x2){Pt.z, Pt.z} * BA + (f32x2){Pt.w, -Pt.w} * AB;
         q0 = q0 + MAG;
         q1 = q1 + MAG;
-        const uint32_t o0 = __float_as_uint(q0.x) * (uint32_t)(4 * FL_BR_W) + __float_as_uint(q0.y) + cofs;
-        const uint32_t o1 = __float_as_uint(q1.x) * (uint32_t)(4 * FL_BR_W) + __float_as_uint(q1.y) + cofs;
+        const uint32_t o0 = __umul24(__float_as_uint(q0.x), (uint32_t)(4 * FL_BR_W)) + __float_as_uint(q0.y) + cofs;
+        const uint32_t o1 = __umul24(__float_as_uint(q1.x), (uint32_t)(4 * FL_BR_W)) + __float_as_uint(q1.y) + cofs;
         tv0[w] = PB[o0];
         tv1[w] = PB[o1];
     }
@@ -444,6 +497,15 @@ void upload_finalize_constants() {
         pat[t] = make_float4((float)ODO_ORB_PATTERN[4 * t], (float)ODO_ORB_PATTERN[4 * t + 1],
                              (float)ODO_ORB_PATTERN[4 * t + 2], (float)ODO_ORB_PATTERN[4 * t + 3]);
     hipMemcpyToSymbol(HIP_SYMBOL(c_patf), pat, sizeof(pat));
+    uint32_t pat8[256];
+    for (int sl = 0; sl < 16; sl++)
+        for (int w = 0; w < 16; w++) {
+            const int t = w * 16 + sl;
+            uint32_t v = 0;
+            for (int i = 0; i < 4; i++) v |= (uint32_t)(uint8_t)(int8_t)ODO_ORB_PATTERN[4 * t + i] << (8 * i);
+            pat8[sl * 16 + w] = v;
+        }
+    hipMemcpyToSymbol(HIP_SYMBOL(c_pat8), pat8, sizeof(pat8));
     const int umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
     hipMemcpyToSymbol(HIP_SYMBOL(c_umax16), umax, sizeof(umax));
 }

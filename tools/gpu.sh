@@ -22,6 +22,8 @@
 #   vserial=V           per-kernel times alone of variant build_V (built with -DODO_TUNING)
 #   vtests=V:F1,F2      pytest -m gpu over the named files against variant build_V
 #   probe=V:SCRIPT      python tools/SCRIPT.py with ODO_LIB = variant build_V (probe builds)
+#   pmcx=NAME:REGEX:C1,C2   one PMC pass with the named counters (pmcx_NAME/)
+#   listctr             rocprofv3 -L (the box's counter names) -> counters.txt
 #   envbench=NAME:ENV:ARGS  bench.py on the tuning build with knobs in the environment
 #                       (ENV: VAR=VAL joined by '/'; ARGS with '+' for spaces)
 #   ab=N:V1,V2,...      A/B of library builds on the bench (N alternations); Vi is
@@ -125,6 +127,20 @@ for step in "$@"; do
     pmc=*)
       K=${step#pmc=}
       pmc_passes "$K" "$O/pmc_$(echo $K | tr -c 'A-Za-z0-9_\n' '_')" --steps 3 --warmup 1 $QUICK ;;
+    pmcx=*)
+      # pmcx=NAME:REGEX:CTR1,CTR2,... — one extra counter pass (tuning build,
+      # serial streams) over the kernels matching REGEX, into pmcx_NAME/
+      spec=${step#pmcx=}; name=${spec%%:*}; rest=${spec#*:}; K=${rest%%:*}; ctr=$(echo ${rest#*:} | tr ',' ' ')
+      mkdir -p $O/pmcx_$name
+      cd /tmp
+      ODO_SERIAL_STREAMS=1 ODO_LIB=$TUNING timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-include-regex "$K" \
+        -d $O/pmcx_$name/p -o run --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 $QUICK \
+        > $O/pmcx_$name/p.log 2>&1
+      cd $R
+      echo "pmcx $name ok" ;;
+    listctr)
+      timeout -k 10 60 rocprofv3 -L > $O/counters.txt 2>&1 || true
+      echo "listctr ok" ;;
     pmch=*)
       K=${step#pmch=}
       pmc_passes "$K" "$O/pmch_$(echo $K | tr -c 'A-Za-z0-9_\n' '_')" --steps 2 --warmup 1 $QUICK --workload hard ;;
