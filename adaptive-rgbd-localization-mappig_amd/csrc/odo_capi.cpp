@@ -117,7 +117,7 @@ struct DevArena {
 // PnP stages of batches k-1 and k-2 still read theirs, so the extraction
 // stream never waits on the PnP latency of the batch just before it.
 #ifndef PYR_WAIT
-#define PYR_WAIT 0
+#define PYR_WAIT 3  // measured: 1.921-1.938 vs 1.933-1.989 ms per step, hard workload unchanged (profiles/r05_q)
 #endif
 #ifndef ODO_NSETS
 #define ODO_NSETS 4  // measured: 4 sets 60.1k vs 3 sets 57.7k frames/s (256-frame batches)

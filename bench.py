@@ -986,9 +986,19 @@ def track_mode(args, rank, world, local_rank, dist):
         # region, as Track hands each frame's pose to its caller
         rows = K + Wm
         ring = pkg.PinnedResults(rows, B)
-        elapsed, submit, (knn_ms, knn_launches) = timed_leg(
-            odo, lambda i: odo.track_batch_async(d_bgr.data_ptr(), d_dep.data_ptr(), B, ring, i % rows),
-            K, Wm, world, dist, coll_dev, ktime)
+        # ODO_BENCH_PACE_MS (measurement only): the host waits this long after
+        # queueing each batch (does the pipeline state depend on how far the
+        # host runs ahead?)
+        pace = float(os.environ.get("ODO_BENCH_PACE_MS", "0")) * 1e-3
+
+        def head_step(i):
+            odo.track_batch_async(d_bgr.data_ptr(), d_dep.data_ptr(), B, ring, i % rows)
+            if pace > 0:
+                t_end = time.perf_counter() + pace
+                while time.perf_counter() < t_end:
+                    pass
+
+        elapsed, submit, (knn_ms, knn_launches) = timed_leg(odo, head_step, K, Wm, world, dist, coll_dev, ktime)
         # the last timed batch's records arrived: its match and query counts
         # equal any batch's after the first (every batch cycles the same loop;
         # the RANSAC outcome differs, each pair's seed is its global index)

@@ -13,6 +13,7 @@
 #   bench=NAME:ARGS     python bench.py ARGS (ARGS with '+' for spaces)  -> NAME.json
 #   multi               bench.py --gpus 2 --backend gloo: two ranks sharing the GPU
 #   kt                  rocprofv3 kernel trace of the headline command (+ timed-region split)
+#   ktn=NAME            the A/B bench command under a kernel trace (NAME.json, NAME/)
 #   kth                 rocprofv3 kernel trace of the hard workload's pipelined main leg
 #   serial              per-kernel times alone (tuning build, ODO_SERIAL_STREAMS=1),
 #                       default and hard workloads
@@ -100,6 +101,15 @@ for step in "$@"; do
       T=$(find $O/kt -name '*kernel_trace.csv' -print -quit)
       python tools/rocprof_timed_region.py "$T" $O/kt_bench.json $O/rocprof_timed_region.json > $O/rtr.log 2>&1 || true
       echo "kt ok" ;;
+    ktn=*)
+      # ktn=NAME: the A/B bench command under rocprofv3 --kernel-trace (does
+      # the traced run land in a different pipeline state?) -> NAME.json
+      name=${step#ktn=}
+      cd /tmp
+      timeout -s KILL 600 rocprofv3 --kernel-trace -d $O/$name -o run --output-format csv -- \
+        python3 $R/bench.py --no-cpu-baseline --latency-frames 0 --host-steps 0 $AB_ARGS > $O/$name.json 2> $O/$name.err
+      cd $R
+      echo "ktn $name: $(python tools/bsum.py $O/$name.json 2>/dev/null || true)" ;;
     kth)
       # kernel trace of the hard workload in the main (pipelined) leg
       cd /tmp
