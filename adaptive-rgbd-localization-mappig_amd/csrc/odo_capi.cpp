@@ -116,6 +116,11 @@ struct DevArena {
 // Frame sets in flight (4): batch k extracts into set k%NSETS while the pair and
 // PnP stages of batches k-1 and k-2 still read theirs, so the extraction
 // stream never waits on the PnP latency of the batch just before it.
+#ifndef ODO_EVFENCE
+#define ODO_EVFENCE 1  // stream-ordering events: 0 default (system-scope fence), 1 no system fence, 2 device-scope release
+#endif
+#define ODO_SYNC_EVENT_FLAGS \
+    (hipEventDisableTiming | (ODO_EVFENCE == 1 ? hipEventDisableSystemFence : ODO_EVFENCE == 2 ? hipEventReleaseToDevice : 0u))
 #ifndef PYR_WAIT
 #define PYR_WAIT 3  // measured: 1.921-1.938 vs 1.933-1.989 ms per step, hard workload unchanged (profiles/r05_q)
 #endif
@@ -1097,26 +1102,32 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
         if (c->sched != 1) c->pnpb = c->pnpa;
         c->pstream2 = c->pstream;
     }
+    // The context's events only order its streams against each other (and
+    // tell the host that inputs were consumed): none needs the system-scope
+    // cache writeback + invalidate a default event record performs, which on
+    // this part also disturbs every kernel then running (round 5: ~10 records
+    // per batch; DESIGN §4 Pipelining)
+    const unsigned evf = ODO_SYNC_EVENT_FLAGS;
     for (int i = 0; i < NSETS && ok; i++)
-        ok = hipEventCreateWithFlags(&c->ev_ra[i], hipEventDisableTiming) == hipSuccess &&
-             hipEventCreateWithFlags(&c->ev_rb[i], hipEventDisableTiming) == hipSuccess &&
-             hipEventCreateWithFlags(&c->ev_pa[i], hipEventDisableTiming) == hipSuccess &&
-             hipEventCreateWithFlags(&c->ev_pb[i], hipEventDisableTiming) == hipSuccess;
+        ok = hipEventCreateWithFlags(&c->ev_ra[i], evf) == hipSuccess &&
+             hipEventCreateWithFlags(&c->ev_rb[i], evf) == hipSuccess &&
+             hipEventCreateWithFlags(&c->ev_pa[i], evf) == hipSuccess &&
+             hipEventCreateWithFlags(&c->ev_pb[i], evf) == hipSuccess;
     for (int i = 0; i < NSETS && ok; i++)
-        ok = hipEventCreateWithFlags(&c->ev_xdone[i], hipEventDisableTiming) == hipSuccess &&
-             hipEventCreateWithFlags(&c->ev_raw[i], hipEventDisableTiming) == hipSuccess &&
-             hipEventCreateWithFlags(&c->ev_pyr[i], hipEventDisableTiming) == hipSuccess &&
-             hipEventCreateWithFlags(&c->ev_blur[i], hipEventDisableTiming) == hipSuccess;
+        ok = hipEventCreateWithFlags(&c->ev_xdone[i], evf) == hipSuccess &&
+             hipEventCreateWithFlags(&c->ev_raw[i], evf) == hipSuccess &&
+             hipEventCreateWithFlags(&c->ev_pyr[i], evf) == hipSuccess &&
+             hipEventCreateWithFlags(&c->ev_blur[i], evf) == hipSuccess;
     if (!c->bstream) c->bstream = c->stream;
-    if (ok) ok = hipEventCreateWithFlags(&c->ev_latch, hipEventDisableTiming) == hipSuccess;
-    if (ok) ok = hipEventCreateWithFlags(&c->ev_depth_done, hipEventDisableTiming) == hipSuccess;
-    if (ok) ok = hipEventCreateWithFlags(&c->ev_knn, hipEventDisableTiming) == hipSuccess;
+    if (ok) ok = hipEventCreateWithFlags(&c->ev_latch, evf) == hipSuccess;
+    if (ok) ok = hipEventCreateWithFlags(&c->ev_depth_done, evf) == hipSuccess;
+    if (ok) ok = hipEventCreateWithFlags(&c->ev_knn, evf) == hipSuccess;
     // host-input uploads run on their own stream (the DMA engines), ordered
     // against the extraction stream by events only
     if (ok) ok = mk(&c->cstream, false);
     for (int i = 0; i < 2 && ok; i++)
-        ok = hipEventCreateWithFlags(&c->ev_in_copied[i], hipEventDisableTiming) == hipSuccess &&
-             hipEventCreateWithFlags(&c->ev_in_free[i], hipEventDisableTiming) == hipSuccess;
+        ok = hipEventCreateWithFlags(&c->ev_in_copied[i], evf) == hipSuccess &&
+             hipEventCreateWithFlags(&c->ev_in_free[i], evf) == hipSuccess;
     if (!ok) {
         fail(ODO_ERR_DEVICE, "hipStreamCreate failed");
         free_ctx(c);
@@ -1180,9 +1191,11 @@ int odo_set_timing(odo_ctx* c, int mode) {
     c->timing = mode == 1;
     c->ktiming = mode == 2;
     if (c->ktiming) {
+        // timing only: no system-scope fence at the records (see ODO_EVFENCE)
+        const unsigned tf = ODO_EVFENCE == 1 ? hipEventDisableSystemFence : 0u;
         if (!c->kt0[0])
             for (int i = 0; i < odo_ctx::KT_RING; i++)
-                if (hipEventCreate(&c->kt0[i]) != hipSuccess || hipEventCreate(&c->kt1[i]) != hipSuccess)
+                if (hipEventCreateWithFlags(&c->kt0[i], tf) != hipSuccess || hipEventCreateWithFlags(&c->kt1[i], tf) != hipSuccess)
                     return fail(ODO_ERR_DEVICE, "hipEventCreate failed");
         c->kt_next = c->kt_pending = 0;
         c->kt_sum_ms = 0;
@@ -2423,7 +2436,7 @@ static int hyps_launch(odo_ctx* c, const odo_dmatch* m12, int n12, const float* 
             return fail(ODO_ERR_DEVICE, "hipHostMalloc (hypotheses staging) failed");
         c->hyp_stage_cap = cap;
     }
-    if (!c->hyp_up) HIPCHK(hipEventCreateWithFlags(&c->hyp_up, hipEventDisableTiming));
+    if (!c->hyp_up) HIPCHK(hipEventCreateWithFlags(&c->hyp_up, ODO_SYNC_EVENT_FLAGS));
     uint8_t* hb = c->hyp_stage_h;
     memcpy(hb + o_xyz, xyz1, (size_t)n1 * 12);
     memcpy(hb + o_xyz + (size_t)kc * 12, xyz2, (size_t)n2 * 12);

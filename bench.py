@@ -31,6 +31,15 @@ import time
 
 import numpy as np
 
+# HIP runtime dispatch mode for this process: commands go to the runtime's
+# worker thread instead of being written to the hardware queues by the
+# calling thread (direct dispatch, HIP's default). The batched pipeline's
+# steady state is 1.81-1.88 vs 1.92-2.03 ms per step with it on the same
+# boxes (profiles/r05_w, r05_x, r05_z; DESIGN §4 Pipelining). An
+# AMD_DIRECT_DISPATCH already in the environment is kept. It has to be set
+# before the HIP runtime initialises (torch is imported later).
+os.environ.setdefault("AMD_DIRECT_DISPATCH", "0")
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG_DIR = os.path.join(ROOT, "adaptive-rgbd-localization-mappig_amd")
 
@@ -1172,6 +1181,7 @@ def track_mode(args, rank, world, local_rank, dist):
                        "ate_mm": round(ate_mm, 3) if ate_mm is not None else None},
             "stage_ms": {k: round(v, 4) for k, v in timings.items()},
             "host_submit_ms_per_step": round(submit / K * 1e3, 3),
+            "hip_runtime": {"AMD_DIRECT_DISPATCH": os.environ.get("AMD_DIRECT_DISPATCH")},
             "from_host": from_host,
             "hard_workload": hard,
             "latency": latency,

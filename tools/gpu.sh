@@ -11,6 +11,7 @@
 #   smoke               __graft_entry__.smoke()
 #   bench               python bench.py (the driver's default line)      -> bench.json
 #   bench=NAME:ARGS     python bench.py ARGS (ARGS with '+' for spaces)  -> NAME.json
+#   benchenv=NAME:ENV:ARGS  the full bench line with VAR=VAL (joined by '/') in the environment
 #   multi               bench.py --gpus 2 --backend gloo: two ranks sharing the GPU
 #   kt                  rocprofv3 kernel trace of the headline command (+ timed-region split)
 #   ktn=NAME            the A/B bench command under a kernel trace (NAME.json, NAME/)
@@ -90,6 +91,14 @@ for step in "$@"; do
       spec=${step#bench=}; name=${spec%%:*}; args=$(echo ${spec#*:} | tr '+' ' ')
       timeout -k 10 600 python bench.py $args > $O/$name.json 2> $O/$name.err
       echo "bench $name ok" ;;
+    benchenv=*)
+      # benchenv=NAME:VAR=VAL/VAR2=VAL2:ARGS — the full default bench line
+      # (production library, every leg) with variables in the environment
+      spec=${step#benchenv=}; name=${spec%%:*}; rest=${spec#*:}
+      envs=$(echo ${rest%%:*} | tr '/' ' '); args=$(echo ${rest#*:} | tr '+' ' ')
+      [ "$args" = "$rest" ] && args=""
+      env $envs timeout -k 10 600 python bench.py $args > $O/$name.json 2> $O/$name.err
+      echo "benchenv $name: $(python tools/bsum.py $O/$name.json 2>/dev/null || true)" ;;
     multi)
       timeout -k 10 600 python bench.py --gpus 2 --backend gloo $QUICK > $O/multi_gloo.json 2> $O/multi_gloo.err
       echo "multi ok" ;;
