@@ -37,7 +37,10 @@ import numpy as np
 # steady state is 1.81-1.88 vs 1.92-2.03 ms per step with it on the same
 # boxes (profiles/r05_w, r05_x, r05_z; DESIGN §4 Pipelining). An
 # AMD_DIRECT_DISPATCH already in the environment is kept. It has to be set
-# before the HIP runtime initialises (torch is imported later).
+# before the HIP runtime initialises (torch is imported later). The
+# one-frame latency leg runs in its own process with direct dispatch (its
+# synchronous per-stage calls: p50 0.87 vs 0.91-0.95 ms, profiles/r05_zb).
+DIRECT_DISPATCH_FROM_ENV = "AMD_DIRECT_DISPATCH" in os.environ
 os.environ.setdefault("AMD_DIRECT_DISPATCH", "0")
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -858,9 +861,14 @@ def run_latency(args, W, H, nframes):
         f.write(np.ascontiguousarray(bgr[idx]).tobytes())
         f.write(np.ascontiguousarray(dep[idx]).tobytes())
         f.flush()
+        env = dict(os.environ)
+        if not DIRECT_DISPATCH_FROM_ENV:
+            env["AMD_DIRECT_DISPATCH"] = "1"
         out = subprocess.run([exe, f.name, str(W), str(H), str(nframes), str(args.iters), "8"], check=True,
-                             capture_output=True, text=True, timeout=300).stdout
-    return json.loads(out.strip().splitlines()[-1])
+                             capture_output=True, text=True, timeout=300, env=env).stdout
+    rec = json.loads(out.strip().splitlines()[-1])
+    rec["amd_direct_dispatch"] = env["AMD_DIRECT_DISPATCH"]
+    return rec
 
 
 def track_mode(args, rank, world, local_rank, dist):
