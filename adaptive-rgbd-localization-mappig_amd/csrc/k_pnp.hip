@@ -8,6 +8,12 @@
 #include "odo_device.h"
 #include "odo_internal.h"
 
+// a * b + c as one fused multiply-add in this file's FP64 arithmetic (the
+// library builds with -ffp-contract=off for its bit-exact stages; PnP's and
+// Kabsch's parity is a tolerance, 1e-4 on the pose): 11 % fewer FP64
+// instructions in k_pnp, and shorter dependent chains
+#pragma clang fp contract(fast)
+
 namespace odo {
 
 #define PNP_THREADS 256
@@ -399,6 +405,23 @@ ODO_INLINE PEdgeSoA pedge_view(void* base, int cap, int p) {
     return E;
 }
 
+// one edge's read-mostly fields (the edge passes' loads, issued together)
+struct EdgeIn {
+    float X[3], ob[3], info;
+    uint8_t fl;
+};
+ODO_INLINE EdgeIn load_edge(const PEdgeSoA& E, int k) {
+    EdgeIn r;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        r.X[i] = E.X[3 * k + i];
+        r.ob[i] = E.obs[3 * k + i];
+    }
+    r.info = E.info[k];
+    r.fl = E.flags[k];
+    return r;
+}
+
 ODO_INLINE double wave_sum(double x) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
@@ -591,38 +614,6 @@ ODO_INLINE void edge_build(const SE3M& T, const double Xw[3], const double ob[3]
     }
 }
 
-// robust (Huber) chi2 of one edge at the quaternion pose T (the chi pass keeps
-// four candidates live: 7 doubles each instead of a matrix's 12)
-ODO_INLINE double edge_robust_chi_q(const SE3& T, const double Xw[3], const double ob[3], double info, uint8_t fl,
-                                    const PnPCam& cam, double dMono, double dStereo, double& c2) {
-    const bool st = fl & PE_STEREO;
-    double Xc[3], e[3];
-    se3_map(T, Xw, Xc);
-    edge_err(Xc, ob, st, cam, e);
-    c2 = chi2_of(e, info, st);
-    if (fl & PE_ROBUST) {
-        double rr[3];
-        huber_rho(st ? dStereo : dMono, c2, rr);
-        return rr[0];
-    }
-    return c2;
-}
-// robust (Huber) chi2 of one edge at pose T; c2 = plain chi2 of the stored error
-ODO_INLINE double edge_robust_chi(const SE3M& T, const double Xw[3], const double ob[3], double info, uint8_t fl,
-                                  const PnPCam& cam, double dMono, double dStereo, double& c2) {
-    const bool st = fl & PE_STEREO;
-    double Xc[3], e[3];
-    se3m_map(T, Xw, Xc);
-    edge_err(Xc, ob, st, cam, e);
-    c2 = chi2_of(e, info, st);
-    if (fl & PE_ROBUST) {
-        double rr[3];
-        huber_rho(st ? dStereo : dMono, c2, rr);
-        return rr[0];
-    }
-    return c2;
-}
-
 // One workgroup (4 waves) per pair. OptimizationAlgorithmLevenberg's trial
 // loop (reject -> lambda *= ni, ni *= 2) is run speculatively: the next
 // PNP_K lambdas of a rejection run are known in advance, so waves 0..K-1 each
@@ -775,12 +766,18 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
             for (int k = 0; k < 28; k++) acc[k] = 0;
             {
                 const SE3M Tm = se3_mat(T);
-                for (int k = lane; k < ne; k += PNP_NT) {
-                    const uint8_t fl = E.flags[k];
-                    if (fl & PE_OUT) continue;
-                    const double Xw[3] = {E.X[3 * k], E.X[3 * k + 1], E.X[3 * k + 2]};
-                    const double ob[3] = {E.obs[3 * k], E.obs[3 * k + 1], E.obs[3 * k + 2]};
-                    edge_build(Tm, Xw, ob, (double)E.info[k], fl, cam, dMono, dStereo, acc);
+                // the next edge's fields are loaded before this one is built
+                if (lane < ne) {
+                    EdgeIn cur = load_edge(E, lane);
+                    for (int k = lane; k < ne; k += PNP_NT) {
+                        const EdgeIn nx = load_edge(E, min(k + PNP_NT, ne - 1));
+                        if (!(cur.fl & PE_OUT)) {
+                            const double Xw[3] = {cur.X[0], cur.X[1], cur.X[2]};
+                            const double ob[3] = {cur.ob[0], cur.ob[1], cur.ob[2]};
+                            edge_build(Tm, Xw, ob, (double)cur.info, cur.fl, cam, dMono, dStereo, acc);
+                        }
+                        cur = nx;
+                    }
                 }
             }
             wg_sum<28>(acc, red);
@@ -804,7 +801,13 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                 lambda = 1e-5 * mx;
                 ni = 2;
             }
-            __syncthreads();
+            // s_acc is written by lane 0 and read by wave 0 only (the trial
+            // solves): a wave-level fence instead of a workgroup barrier
+            if (wave == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
             // ---- OptimizationAlgorithmLevenberg::solve trial loop, PNP_K trials per pass
             double rho = 0;
             int qmax = 0;
@@ -902,24 +905,58 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                 double chi[PNP_K];
 #pragma unroll
                 for (int k = 0; k < PNP_K; k++) chi[k] = 0;
+                // all PNP_K candidates of an edge as independent chains, phase
+                // by phase (maps, divisions, errors, chi2, Huber) with no
+                // branch between them, so their latencies overlap; the same
+                // expressions as edge_err + chi2_of + huber_rho (computeError,
+                // chi2, RobustKernelHuber::robustify; candidates >= K are computed
+                // from stale slots and dropped: their chi2 slots are never read)
+                EdgeIn cur = load_edge(E, min(lane, ne - 1));
                 for (int e = lane; e < ne; e += PNP_NT) {
-                    const uint8_t fl = E.flags[e];
+                    const EdgeIn ed = cur;
+                    cur = load_edge(E, min(e + PNP_NT, ne - 1));
+                    const uint8_t fl = ed.fl;
                     if (fl & PE_OUT) continue;
-                    const double Xw[3] = {E.X[3 * e], E.X[3 * e + 1], E.X[3 * e + 2]};
-                    const double ob[3] = {E.obs[3 * e], E.obs[3 * e + 1], E.obs[3 * e + 2]};
-                    const double info = E.info[e];
+                    const double Xw[3] = {ed.X[0], ed.X[1], ed.X[2]};
+                    const double ob[3] = {ed.ob[0], ed.ob[1], ed.ob[2]};
+                    const double info = ed.info;
+                    const bool st = fl & PE_STEREO;
+                    double c2[PNP_K];
 #pragma unroll
                     for (int k = 0; k < PNP_K; k++) {
-                        if (k >= K) break;
-                        double c2;
                         SE3M Mk;
 #pragma unroll
                         for (int q = 0; q < 9; q++) Mk.R[q] = s_M[k][q];
 #pragma unroll
                         for (int q = 0; q < 3; q++) Mk.t[q] = s_M[k][9 + q];
-                        chi[k] += edge_robust_chi(Mk, Xw, ob, info, fl, cam, dMono, dStereo, c2);
-                        if (LE) sC[4 * e + k] = (float)c2;
-                        else E.chi4[4 * e + k] = c2;
+                        double Xc[3];
+                        se3m_map(Mk, Xw, Xc);
+                        const double d = 1.0 / Xc[2];
+                        const double iz = st ? (double)(float)d : d;
+                        const double r0 = Xc[0] * iz * cam.fx + cam.cx;
+                        const double r1 = Xc[1] * iz * cam.fy + cam.cy;
+                        const double e0 = ob[0] - r0, e1 = ob[1] - r1;
+                        const double e2 = st ? ob[2] - (r0 - cam.bf * iz) : 0.0;
+                        c2[k] = sum3d(e0 * (info * e0), e1 * (info * e1), e2 * (info * e2));
+                    }
+                    const double delta = st ? dStereo : dMono, dsqr = delta * delta;
+                    bool huber = false;
+#pragma unroll
+                    for (int k = 0; k < PNP_K; k++) huber |= c2[k] > dsqr;
+                    huber = huber && (fl & PE_ROBUST);
+                    double sq[PNP_K];
+#pragma unroll
+                    for (int k = 0; k < PNP_K; k++) sq[k] = 0.0;
+                    if (huber) {
+#pragma unroll
+                        for (int k = 0; k < PNP_K; k++) sq[k] = sqrt(c2[k]);
+                    }
+#pragma unroll
+                    for (int k = 0; k < PNP_K; k++) {
+                        const double r = (huber && c2[k] > dsqr) ? 2 * sq[k] * delta - dsqr : c2[k];
+                        chi[k] += r;
+                        if (LE) sC[4 * e + k] = (float)c2[k];
+                        else if (k < K) E.chi4[4 * e + k] = c2[k];
                     }
                 }
                 wg_sum<PNP_K>(chi, red);
@@ -938,7 +975,8 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                     last_slot = k;
                     qmax++;
                     if (rho > 0 && isfinite(tempChi)) {
-                        double alpha = 1. - pow((2 * rho - 1), 3);
+                        const double tr = 2 * rho - 1;
+                        double alpha = 1. - tr * tr * tr;
                         alpha = fmin(alpha, 2. / 3.);
                         const double sf = fmax(1. / 3., alpha);
                         lambda = lam[k] * sf;
@@ -1000,7 +1038,10 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
         if (ne < 10) break;
     }
 #ifdef ODO_PNP_PROFILE
-    if (lane == 0 && p < 3)
+#ifndef PNP_PROF_PAIRS
+#define PNP_PROF_PAIRS 3
+#endif
+    if (lane == 0 && p < PNP_PROF_PAIRS)
         printf("PNP p %d ne %d iters %d trials %d: build %lu solve %lu (ldlt %lu exp+mul %lu) chi %lu classify %lu total %lu (x10ns)\n",
                p, ne, nit, ntr, tb, tsol, tldlt, texp, tchi, tcls, wall_clock64() - tall);
 #endif

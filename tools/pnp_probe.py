@@ -13,9 +13,10 @@ from conftest import load_pkg, load_synth  # noqa: E402
 def main():
     pkg = load_pkg()
     synth = load_synth()
-    bgr, dep, _ = synth.make_sequence(4, 640, 480, seed=0x5EED0002, closed_loop=True)
+    nfr = int(os.environ.get("PNP_PROBE_FRAMES", "4"))
+    bgr, dep, _ = synth.make_sequence(nfr, 640, 480, seed=0x5EED0002, closed_loop=True)
     for nf in (1000, 2000):
-        cfg = pkg.default_config(640, 480, 4, nfeatures=nf, iterations=500)
+        cfg = pkg.default_config(640, 480, nfr, nfeatures=nf, iterations=500)
         odo = pkg.Odometry(cfg)
         print(f"nfeatures {nf}", flush=True)
         res = odo.track_batch_host(bgr, dep)
