@@ -26,23 +26,6 @@ struct SE3 {
     double t[3];
 };
 
-ODO_INLINE void cross3(const double a[3], const double b[3], double o[3]) {
-    o[0] = a[1] * b[2] - a[2] * b[1];
-    o[1] = a[2] * b[0] - a[0] * b[2];
-    o[2] = a[0] * b[1] - a[1] * b[0];
-}
-ODO_INLINE void qrot(const Quat& q, const double v[3], double o[3]) {
-    const double qv[3] = {q.x, q.y, q.z};
-    double uv[3], uv2[3];
-    cross3(qv, v, uv);
-    for (int i = 0; i < 3; i++) uv[i] += uv[i];
-    cross3(qv, uv, uv2);
-    for (int i = 0; i < 3; i++) o[i] = v[i] + q.w * uv[i] + uv2[i];
-}
-ODO_INLINE Quat qmul(const Quat& a, const Quat& b) {
-    return Quat{a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y, a.w * b.y + a.y * b.w + a.z * b.x - a.x * b.z,
-                a.w * b.z + a.z * b.w + a.x * b.y - a.y * b.x, a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z};
-}
 ODO_INLINE Quat quat_from_R(const double m[3][3]) {
     // Eigen quaternionbase_assign_impl<Matrix3>, branches written with static indices
     Quat q;
@@ -111,24 +94,14 @@ ODO_INLINE void normalize_rot(SE3& s) {
     s.q.z *= in;
     s.q.w *= in;
 }
-ODO_INLINE SE3 se3_mul(const SE3& a, const SE3& b) {
-    SE3 r = a;
-    double rt[3];
-    qrot(a.q, b.t, rt);
-    for (int i = 0; i < 3; i++) r.t[i] += rt[i];
-    r.q = qmul(a.q, b.q);
-    normalize_rot(r);
-    return r;
-}
-ODO_INLINE SE3 se3_exp(const double u[6]) {
+// Rodrigues' R and V of SE3Quat::exp (g2o se3quat.h)
+ODO_INLINE void se3_exp_rv(const double u[6], double R[3][3], double V[3][3]) {
     const double w[3] = {u[0], u[1], u[2]};
-    const double up[3] = {u[3], u[4], u[5]};
     double theta = sqrt(sum3d(w[0] * w[0], w[1] * w[1], w[2] * w[2]));
     double O[3][3] = {{0, -w[2], w[1]}, {w[2], 0, -w[0]}, {-w[1], w[0], 0}};
     double O2[3][3];
     for (int i = 0; i < 3; i++)
         for (int j = 0; j < 3; j++) O2[i][j] = sum3d(O[i][0] * O[0][j], O[i][1] * O[1][j], O[i][2] * O[2][j]);
-    double R[3][3], V[3][3];
     if (theta < 0.00001) {
         for (int i = 0; i < 3; i++)
             for (int j = 0; j < 3; j++) {
@@ -150,15 +123,6 @@ ODO_INLINE SE3 se3_exp(const double u[6]) {
                 V[i][j] = ((i == j ? 1.0 : 0.0) + b * O[i][j]) + c * O2[i][j];
             }
     }
-    SE3 s;
-    for (int i = 0; i < 3; i++) s.t[i] = sum3d(V[i][0] * up[0], V[i][1] * up[1], V[i][2] * up[2]);
-    s.q = quat_from_R(R);
-    normalize_rot(s);
-    return s;
-}
-ODO_INLINE void se3_map(const SE3& T, const double p[3], double o[3]) {
-    qrot(T.q, p, o);
-    for (int i = 0; i < 3; i++) o[i] += T.t[i];
 }
 // The pose as a rotation matrix + translation for the edge passes: 9 products
 // per point instead of the quaternion's two cross products (g2o maps with the
@@ -181,6 +145,22 @@ ODO_INLINE SE3M se3_mat(const SE3& T) {
 ODO_INLINE void se3m_map(const SE3M& T, const double p[3], double o[3]) {
 #pragma unroll
     for (int i = 0; i < 3; i++) o[i] = (T.R[3 * i] * p[0] + T.R[3 * i + 1] * p[1]) + (T.R[3 * i + 2] * p[2] + T.t[i]);
+}
+// exp(u) * T (VertexSE3Expmap::oplusImpl) with the pose kept as a matrix:
+// R = R_exp R_T, t = R_exp t_T + V u_t. g2o composes unit quaternions and
+// renormalizes; the matrices agree with that to rounding (the PnP tolerance)
+ODO_INLINE SE3M se3m_exp_mul(const double u[6], const SE3M& T) {
+    double R[3][3], V[3][3];
+    se3_exp_rv(u, R, V);
+    SE3M M;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+#pragma unroll
+        for (int j = 0; j < 3; j++) M.R[3 * i + j] = sum3d(R[i][0] * T.R[j], R[i][1] * T.R[3 + j], R[i][2] * T.R[6 + j]);
+        M.t[i] = sum3d(R[i][0] * T.t[0], R[i][1] * T.t[1], R[i][2] * T.t[2]) +
+                 sum3d(V[i][0] * u[3], V[i][1] * u[4], V[i][2] * u[5]);
+    }
+    return M;
 }
 
 // Eigen LDLT with diagonal pivoting on a 6x6, every index static after
@@ -743,7 +723,8 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
     }
     const float chi2Mono = 5.991f, chi2Stereo = 7.815f;
     int nBad = 0;
-    SE3 T = T0s;
+    const SE3M T0m = se3_mat(T0s);
+    SE3M T = T0m;
 #ifdef ODO_PNP_PROFILE
     // -DODO_PNP_PROFILE: phase times (10 ns ticks) of one pair via printf
     uint64_t tb = 0, tsol = 0, tchi = 0, tcls = 0, t0 = 0, tall = wall_clock64(), tldlt = 0, texp = 0;
@@ -756,7 +737,7 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
 #endif
     int last_slot = 0;  // trial slot whose errors the edges store (last computeActiveErrors)
     for (int it = 0; it < 4; it++) {
-        T = T0s;  // vSE3->setEstimate(pFrame->GetPose()) (pnpsolver.cpp:150)
+        T = T0m;  // vSE3->setEstimate(pFrame->GetPose()) (pnpsolver.cpp:150)
         double lambda = 0, ni = 2;
         for (int iter = 0; iter < 10; iter++) {
             // computeActiveErrors + activeRobustChi2 + buildSystem at T
@@ -765,7 +746,7 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
 #pragma unroll
             for (int k = 0; k < 28; k++) acc[k] = 0;
             {
-                const SE3M Tm = se3_mat(T);
+                const SE3M& Tm = T;
                 // the next edge's fields are loaded before this one is built
                 if (lane < ne) {
                     EdgeIn cur = load_edge(E, lane);
@@ -859,7 +840,7 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
 #ifdef ODO_PNP_PROFILE
                     const uint64_t ts1 = wall_clock64();
 #endif
-                    const SE3 Tk = se3_mul(se3_exp(x), T);
+                    const SE3M Tk = se3m_exp_mul(x, T);
 #ifdef ODO_PNP_PROFILE
                     if (wlane == 0) {
                         tldlt += ts1 - ts0;
@@ -870,32 +851,19 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                     for (int j = 0; j < 6; j++) scale += x[j] * (lw * x[j] + b[j]);
                     scale += 1e-3;
                     if ((wlane & 15) == 0) {
-                        s_T[tg][0] = Tk.q.x;
-                        s_T[tg][1] = Tk.q.y;
-                        s_T[tg][2] = Tk.q.z;
-                        s_T[tg][3] = Tk.q.w;
-                        s_T[tg][4] = Tk.t[0];
-                        s_T[tg][5] = Tk.t[1];
-                        s_T[tg][6] = Tk.t[2];
                         s_T[tg][7] = scale;
                         s_ok[tg] = ok2 ? 1 : 0;
-                        const SE3M Mk = se3_mat(Tk);
 #pragma unroll
-                        for (int q = 0; q < 9; q++) s_M[tg][q] = Mk.R[q];
+                        for (int q = 0; q < 9; q++) s_M[tg][q] = Tk.R[q];
 #pragma unroll
-                        for (int q = 0; q < 3; q++) s_M[tg][9 + q] = Mk.t[q];
+                        for (int q = 0; q < 3; q++) s_M[tg][9 + q] = Tk.t[q];
                     }
                 }
                 __syncthreads();
-                SE3 Tc[PNP_K];
                 double sc[PNP_K];
                 bool okc[PNP_K];
 #pragma unroll
                 for (int k = 0; k < PNP_K; k++) {
-                    Tc[k].q = Quat{s_T[k][0], s_T[k][1], s_T[k][2], s_T[k][3]};
-                    Tc[k].t[0] = s_T[k][4];
-                    Tc[k].t[1] = s_T[k][5];
-                    Tc[k].t[2] = s_T[k][6];
                     sc[k] = s_T[k][7];
                     okc[k] = s_ok[k] != 0;
                 }
@@ -982,7 +950,12 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                         lambda = lam[k] * sf;
                         ni = 2;
                         curChi = tempChi;
-                        T = Tc[k];
+                        // the accepted candidate's matrix (s_M is not written
+                        // again before the next trial solves)
+#pragma unroll
+                        for (int q = 0; q < 9; q++) T.R[q] = s_M[k][q];
+#pragma unroll
+                        for (int q = 0; q < 3; q++) T.t[q] = s_M[k][9 + q];
                         trials_done = true;
                     } else {
                         lambda = lam[k] * nis[k];  // T stays at the backup
@@ -997,7 +970,7 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
         PP_T0();
         int bad = 0;
         {
-            const SE3M Tm = se3_mat(T);
+            const SE3M& Tm = T;
             // reclassify edge k (flags in / out); the stored chi2 of the last
             // computeActiveErrors, recomputed at T for the edges that were out
             auto classify = [&](int k, uint32_t fl, const double Xw[3], const double ob[3], double info) {
@@ -1047,7 +1020,8 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
 #endif
     if (lane == 0) {
         double Rm[3][3];
-        quat_to_R(T.q, Rm);
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) Rm[i][j] = T.R[3 * i + j];
         for (int i = 0; i < 3; i++) {
             for (int j = 0; j < 3; j++) R->Tcw[i * 4 + j] = (float)Rm[i][j];
             R->Tcw[i * 4 + 3] = (float)T.t[i];
