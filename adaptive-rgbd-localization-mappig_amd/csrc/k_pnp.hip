@@ -412,16 +412,39 @@ struct PnPCam {
     double fx, fy, cx, cy, bf;
 };
 
+// 1 / z for the edge passes: v_rcp_f64 refined by two Newton steps (within an
+// ulp of the IEEE quotient g2o divides by, about half the instructions of the
+// correctly rounded division; z = +-0 keeps rcp's +-inf)
+ODO_INLINE double pnp_inv(double z) {
+    const double r0 = __builtin_amdgcn_rcp(z);
+    double e = __builtin_fma(-z, r0, 1.0);
+    double r = __builtin_fma(r0, e, r0);
+    e = __builtin_fma(-z, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    return __builtin_isinf(r0) ? r0 : r;
+}
+// sqrt(x) for the Huber kernel (x > delta^2 > 0 where it is used; inf kept)
+ODO_INLINE double pnp_sqrt(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = 0.5 * y;
+    const double r = __builtin_fma(-g, h, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    const double d = __builtin_fma(-g, g, x);
+    g = __builtin_fma(d, h, g);
+    return __builtin_isinf(x) ? x : g;
+}
+
 // EdgeSE3ProjectXYZOnlyPose / EdgeStereoSE3ProjectXYZOnlyPose::computeError (g2o types_six_dof_expmap)
 ODO_INLINE void edge_err(const double Xc[3], const double ob[3], bool stereo, const PnPCam& c, double e[3]) {
     if (!stereo) {
-        const double iz = 1.0 / Xc[2];
+        const double iz = pnp_inv(Xc[2]);
         double px = Xc[0] * iz, py = Xc[1] * iz;
         e[0] = ob[0] - (px * c.fx + c.cx);
         e[1] = ob[1] - (py * c.fy + c.cy);
         e[2] = 0;
     } else {
-        const float invz = (float)(1.0 / Xc[2]);
+        const float invz = (float)pnp_inv(Xc[2]);
         const double iz = (double)invz;
         double r0 = Xc[0] * iz * c.fx + c.cx;
         double r1 = Xc[1] * iz * c.fy + c.cy;
@@ -442,9 +465,9 @@ ODO_INLINE void huber_rho(double delta, double chi, double rho[3]) {
         rho[1] = 1.;
         rho[2] = 0.;
     } else {
-        double sq = sqrt(chi);
+        double sq = pnp_sqrt(chi);
         rho[0] = 2 * sq * delta - dsqr;
-        rho[1] = delta / sq;
+        rho[1] = delta * pnp_inv(sq);
         rho[2] = -0.5 * rho[1] / chi;
     }
 }
@@ -545,7 +568,7 @@ ODO_INLINE void edge_build(const SE3M& T, const double Xw[3], const double ob[3]
     double rho[3] = {c2, 1.0, 0.0};
     if (fl & PE_ROBUST) huber_rho(st ? dStereo : dMono, c2, rho);
     acc[27] += rho[0];
-    const double x = Xc[0], y = Xc[1], invz = 1.0 / Xc[2], invz_2 = invz * invz;
+    const double x = Xc[0], y = Xc[1], invz = pnp_inv(Xc[2]), invz_2 = invz * invz;
     double J[3][6];
     J[0][0] = x * y * invz_2 * cam.fx;
     J[0][1] = -(1 + (x * x * invz_2)) * cam.fx;
@@ -585,11 +608,10 @@ ODO_INLINE void edge_build(const SE3M& T, const double Xw[3], const double ob[3]
         acc[21 + a] -= r1 * sb;
 #pragma unroll
         for (int cc = a; cc < 6; cc++) {
-            double hh = 0;
 #pragma unroll
             for (int kk = 0; kk < 3; kk++)
-                if (!Z[kk][a] && !Z[kk][cc]) hh += J[kk][a] * wo * J[kk][cc];
-            acc[h++] += hh;
+                if (!Z[kk][a] && !Z[kk][cc]) acc[h] += J[kk][a] * wo * J[kk][cc];
+            h++;
         }
     }
 }
@@ -727,7 +749,7 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
     SE3M T = T0m;
 #ifdef ODO_PNP_PROFILE
     // -DODO_PNP_PROFILE: phase times (10 ns ticks) of one pair via printf
-    uint64_t tb = 0, tsol = 0, tchi = 0, tcls = 0, t0 = 0, tall = wall_clock64(), tldlt = 0, texp = 0;
+    uint64_t tb = 0, tsol = 0, tchi = 0, tcls = 0, t0 = 0, tall = wall_clock64(), tldlt = 0, texp = 0, tbl = 0, tcl = 0;
     int nit = 0, ntr = 0;
 #define PP_T0() t0 = wall_clock64()
 #define PP_ACC(x) x += wall_clock64() - t0
@@ -761,6 +783,9 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                     }
                 }
             }
+#ifdef ODO_PNP_PROFILE
+            tbl += wall_clock64() - t0;  // the edge trips, without the sum
+#endif
             wg_sum<28>(acc, red);
             PP_ACC(tb);
 #ifdef ODO_PNP_PROFILE
@@ -899,7 +924,7 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                         for (int q = 0; q < 3; q++) Mk.t[q] = s_M[k][9 + q];
                         double Xc[3];
                         se3m_map(Mk, Xw, Xc);
-                        const double d = 1.0 / Xc[2];
+                        const double d = pnp_inv(Xc[2]);
                         const double iz = st ? (double)(float)d : d;
                         const double r0 = Xc[0] * iz * cam.fx + cam.cx;
                         const double r1 = Xc[1] * iz * cam.fy + cam.cy;
@@ -917,7 +942,7 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                     for (int k = 0; k < PNP_K; k++) sq[k] = 0.0;
                     if (huber) {
 #pragma unroll
-                        for (int k = 0; k < PNP_K; k++) sq[k] = sqrt(c2[k]);
+                        for (int k = 0; k < PNP_K; k++) sq[k] = pnp_sqrt(c2[k]);
                     }
 #pragma unroll
                     for (int k = 0; k < PNP_K; k++) {
@@ -927,6 +952,9 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                         else if (k < K) E.chi4[4 * e + k] = c2[k];
                     }
                 }
+#ifdef ODO_PNP_PROFILE
+                tcl += wall_clock64() - t0;
+#endif
                 wg_sum<PNP_K>(chi, red);
                 PP_ACC(tchi);
                 // replay the trials in order
@@ -1015,8 +1043,8 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
 #define PNP_PROF_PAIRS 3
 #endif
     if (lane == 0 && p < PNP_PROF_PAIRS)
-        printf("PNP p %d ne %d iters %d trials %d: build %lu solve %lu (ldlt %lu exp+mul %lu) chi %lu classify %lu total %lu (x10ns)\n",
-               p, ne, nit, ntr, tb, tsol, tldlt, texp, tchi, tcls, wall_clock64() - tall);
+        printf("PNP p %d ne %d iters %d trials %d: build %lu (trips %lu) solve %lu (ldlt %lu exp+mul %lu) chi %lu (trips %lu) classify %lu total %lu (x10ns)\n",
+               p, ne, nit, ntr, tb, tbl, tsol, tldlt, texp, tchi, tcl, tcls, wall_clock64() - tall);
 #endif
     if (lane == 0) {
         double Rm[3][3];
