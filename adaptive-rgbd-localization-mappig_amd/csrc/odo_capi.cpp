@@ -121,6 +121,9 @@ struct DevArena {
 #endif
 #define ODO_SYNC_EVENT_FLAGS \
     (hipEventDisableTiming | (ODO_EVFENCE == 1 ? hipEventDisableSystemFence : ODO_EVFENCE == 2 ? hipEventReleaseToDevice : 0u))
+#ifndef KNN_GATE
+#define KNN_GATE 0
+#endif
 #ifndef PYR_WAIT
 #define PYR_WAIT 3  // measured: 1.921-1.938 vs 1.933-1.989 ms per step, hard workload unchanged (profiles/r05_q)
 #endif
@@ -145,9 +148,9 @@ struct odo_ctx {
     int npstreams = 2;
     bool knn_pair = true;  // schedule 5 (ODO_KNN_PAIR=0: on the extraction stream): kNN-2 at the head of the pair stream, 88.2k vs 86.5k frames/s (kNN roofline 0.85 vs 0.90)
     hipStream_t cur_p = nullptr;     // pair stream of the batch being queued
-    // ODO_KNN_GATE (tuning): the next batch's extraction waits for this
-    // batch's kNN-2 (no gray / kNN-2 overlap)
-    bool knn_gate = false;
+    // KNN_GATE / ODO_KNN_GATE (tuning): the next batch's extraction waits
+    // for this batch's kNN-2 (no pyramid / kNN-2 overlap)
+    bool knn_gate = KNN_GATE != 0;
     // the extraction of batch b waits for the PnP of batch b - pyr_wait (0:
     // not), so the pyramid does not share the CUs with a PnP / RANSAC
     // evaluation still running from an earlier batch (PYR_WAIT; ODO_PYR_WAIT)
