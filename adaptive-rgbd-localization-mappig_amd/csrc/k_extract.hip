@@ -1471,7 +1471,9 @@ __global__ void __launch_bounds__(256) k_blur_rows(const uint8_t* __restrict__ p
 // BLUR: the workgroup also blurs each level (k_blur_rows' strip walks and
 // edge lanes) once the level is complete, beside the resize that reads it,
 // so no separate blur launch follows (uint8 blur pyramid written to `blur`).
-#define PYR_TH 1024
+#ifndef PYR_TH
+#define PYR_TH 1024  // threads per frame workgroup
+#endif
 #ifndef PYR_RU
 #define PYR_RU 2  // output rows in flight per thread (resize)
 #endif
