@@ -340,7 +340,7 @@ __global__ void __launch_bounds__(FS_TH) k_fast_seg(const uint8_t* __restrict__ 
                     const int ii = (int)__builtin_fmaf((float)it, inl, inl_h);
                     const int kk = it - __mul24(ii, NL);
                     const uint2 e = qlist[kk];
-                    int wb = (ii << 8) + (int)e.y;  // 3 rows above the quad: offsets >= 0
+                    int wb = ii * RS + (int)e.y;  // 3 rows above the quad: offsets >= 0
                     asm("" : "+v"(wb));
                     qoff = wb + 3 * RS;
                     const uint32_t* w = reinterpret_cast<const uint32_t*>(roi + wb);
@@ -409,7 +409,7 @@ __global__ void __launch_bounds__(FS_TH) k_fast_seg(const uint8_t* __restrict__ 
         // detection columns [xl, xh) in segment x
         auto locate = [&](int o, int& r, int& xs, int& jl, int& xl, int& xh) {
             r = o / RS;
-            xs = (o & (RS - 1)) - sh;
+            xs = (o - r * RS) - sh;
             jl = (int)(((float)(xs - 3) + 0.5f) * inv_w);
             xl = 3 + jl * wcell;
             xh = min(xl + wcell, cols - 3);

@@ -58,9 +58,14 @@ struct CellDesc {
 #define FS_NCM FS_SEGC
 // LDS row stride of a staged segment (bytes): a compile-time constant, so the
 // kernel's neighbour offsets (the 16 circle pixels, the compass points, the
-// NMS neighbours) are instruction immediates and a byte offset splits into
-// (row, column) with a shift; the host sizes segments to fit it
-#define FS_RS 256
+// NMS neighbours) are instruction immediates; the host sizes segments to fit
+// it. 272 = 68 dwords, a 16-byte multiple (the staging stores) that moves each
+// row 4 banks over: with 256 every row of a column fell in the same bank, and
+// the segment test's scattered circle reads of candidates from different rows
+// conflicted (profiles/r05_rs)
+#ifndef FS_RS
+#define FS_RS 272
+#endif
 struct FastSeg {
     int level, ci0;
     int16_t y0, x0, rows, cols, ncell, wcell;
