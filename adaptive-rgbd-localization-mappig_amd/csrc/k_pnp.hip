@@ -649,8 +649,8 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
     const int wlane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     __shared__ double red[PNP_RED_WORDS];
     __shared__ double s_acc[28];  // reduced H (upper, row-major), b, chi of the iteration
-    __shared__ double s_T[PNP_K][8];
-    __shared__ double s_M[PNP_K][12];  // the candidates as rotation matrix + translation (se3_mat)
+    __shared__ double s_sc[PNP_K];  // the trials' gain denominators (scale)
+    __shared__ double s_M[PNP_K][12];  // the candidates as rotation matrix + translation
     __shared__ int s_ok[PNP_K];
     __shared__ int s_ne[PNP_NW];
     odo_pair_result* R = res + p;
@@ -876,7 +876,7 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                     for (int j = 0; j < 6; j++) scale += x[j] * (lw * x[j] + b[j]);
                     scale += 1e-3;
                     if ((wlane & 15) == 0) {
-                        s_T[tg][7] = scale;
+                        s_sc[tg] = scale;
                         s_ok[tg] = ok2 ? 1 : 0;
 #pragma unroll
                         for (int q = 0; q < 9; q++) s_M[tg][q] = Tk.R[q];
@@ -889,7 +889,7 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                 bool okc[PNP_K];
 #pragma unroll
                 for (int k = 0; k < PNP_K; k++) {
-                    sc[k] = s_T[k][7];
+                    sc[k] = s_sc[k];
                     okc[k] = s_ok[k] != 0;
                 }
                 PP_ACC(tsol);
