@@ -713,14 +713,27 @@ __global__ void __launch_bounds__(OT_THREADS) k_octree(const uint32_t* __restric
     uint32_t ky[OT_KB];
     int nd[OT_KB];
     uint8_t kq[OT_KB];
+    // the initial nodes' key counts: nIni is 1-2 for 4:3 frames, so every
+    // key's atomic hit the same one or two LDS words (a 64-way serialised
+    // atomic per key batch); the first four nodes are counted in registers
+    // and added once per thread (the same integer counts)
+    int ic0 = 0, ic1 = 0, ic2 = 0, ic3 = 0;
     ot_keys(
         n, t, [&](int k, int u) { ky[u] = keys[k]; },
         [&](int k, int u) {
             const float x = (float)(ky[u] & 0xfff);
             const int ni = (int)(x / hX);
             knode[k] = ni;
-            atomicAdd(&nodesA[ni].cnt, 1);
+            ic0 += ni == 0;
+            ic1 += ni == 1;
+            ic2 += ni == 2;
+            ic3 += ni == 3;
+            if (ni > 3) atomicAdd(&nodesA[ni].cnt, 1);
         });
+    if (ic0) atomicAdd(&nodesA[0].cnt, ic0);
+    if (ic1) atomicAdd(&nodesA[1].cnt, ic1);
+    if (ic2) atomicAdd(&nodesA[2].cnt, ic2);
+    if (ic3) atomicAdd(&nodesA[3].cnt, ic3);
     __syncthreads();
     // erase empty initial nodes (keep order)
     if (t == 0) {
