@@ -467,7 +467,7 @@ ODO_INLINE void huber_rho(double delta, double chi, double rho[3]) {
     } else {
         double sq = pnp_sqrt(chi);
         rho[0] = 2 * sq * delta - dsqr;
-        rho[1] = delta * pnp_inv(sq);
+        rho[1] = __builtin_isinf(sq) ? 0.0 : delta * pnp_inv(sq);  // delta / inf = 0, as the IEEE quotient
         rho[2] = -0.5 * rho[1] / chi;
     }
 }
