@@ -266,6 +266,18 @@ class Odometry:
         check(self.lib.odo_kernel_timing(self.h, C.byref(avg), C.byref(n)))
         return avg.value, n.value
 
+    def step_marks(self):
+        """odo_step_marks: the start (ms after set_timing mode 2) of every batch's
+        kNN-2 launch since then; np.diff gives the per-step times."""
+        n = self.lib.odo_step_marks(self.h, None, 0)
+        if n < 0:
+            check(n)
+        buf = (C.c_double * max(1, n))()
+        k = self.lib.odo_step_marks(self.h, buf, n)
+        if k < 0:
+            check(k)
+        return [float(buf[i]) for i in range(min(k, n))]
+
     def synchronize(self):
         check(self.lib.odo_synchronize(self.h))
         self._release_depth()

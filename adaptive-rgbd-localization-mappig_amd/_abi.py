@@ -151,6 +151,7 @@ SIGNATURES = {
     "odo_knn_replay_time": (C.c_int, [P, C.c_int, C.POINTER(C.c_float)]),
     "odo_set_timing": (C.c_int, [P, C.c_int]),
     "odo_kernel_timing": (C.c_int, [P, P, P]),
+    "odo_step_marks": (C.c_int, [P, C.POINTER(C.c_double), C.c_int]),
     "odo_debug_blur": (C.c_int, [P, C.c_int, P, C.c_size_t]),
     "odo_last_timings": (C.c_int, [P, P, C.c_int, P]),
     "odo_debug_adaptive": (C.c_int, [P, C.c_int, P, P]),

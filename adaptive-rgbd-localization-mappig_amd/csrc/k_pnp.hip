@@ -1122,6 +1122,10 @@ ODO_INLINE void block_reduce(double (&v)[NV], double* red /* 4*NV */) {
 }
 }  // namespace odo
 
+// Kabsch is not part of the PnP measurements that paid for contraction: back to
+// the library's -ffp-contract=off from here on
+#pragma clang fp contract(off)
+
 // ============================================================ Kabsch::Compute
 // Odometry/kabsch.cpp:14-57 (dead code in the reference, exported for
 // completeness): centroids, A = (A-cA)^T (B-cB), JacobiSVD (same 3x3 Jacobi as

@@ -71,8 +71,10 @@ uint32_t splitmix_host(uint64_t base, uint64_t pair) { return pair_seed(base, pa
 // per call. A call that outgrows the block takes an extra block; the next call
 // replaces the blocks by one of their total size. Every allocation is checked
 // (a failed one sets `failed`, which the entry point turns into
-// ODO_ERR_DEVICE). The entry points are synchronous, so no kernel of an
-// earlier call still uses the blocks when begin() replaces them.
+// ODO_ERR_DEVICE). begin() may hipFree the blocks: its callers first make sure
+// that no kernel of an earlier call still uses them (the per-stage entry
+// points are synchronous; hypotheses mode, whose _dev / _finish calls queue
+// kernels asynchronously, synchronises its stream before begin()).
 struct DevArena {
     std::vector<std::pair<uint8_t*, size_t>> blocks;
     size_t used = 0;
@@ -131,6 +133,9 @@ struct DevArena {
 #define ODO_NSETS 4  // measured: 4 sets 60.1k vs 3 sets 57.7k frames/s (256-frame batches)
 #endif
 constexpr int NSETS = ODO_NSETS;
+// batch b - PYR_WAIT must not share batch b's frame set: its PnP events are
+// re-recorded by batch b - PYR_WAIT + NSETS
+static_assert(PYR_WAIT >= 0 && PYR_WAIT < ODO_NSETS, "PYR_WAIT must be below ODO_NSETS");
 // output rows per resize workgroup
 constexpr int RZ_RB = 16;
 
@@ -342,6 +347,10 @@ struct odo_ctx {
     int kt_next = 0, kt_pending = 0;
     double kt_sum_ms = 0;
     long kt_count = 0;
+    // per-step marks (odo_step_marks): every collected kNN-2 start as ms after
+    // kt_ref, an event recorded when mode 2 was set
+    hipEvent_t kt_ref = nullptr;
+    std::vector<double> kt_marks;
 };
 
 static inline size_t fbase(const odo_ctx* c, int set) { return (size_t)set * c->slots; }
@@ -440,6 +449,7 @@ static void free_ctx(odo_ctx* c) {
         if (c->kt0[i]) hipEventDestroy(c->kt0[i]);
         if (c->kt1[i]) hipEventDestroy(c->kt1[i]);
     }
+    if (c->kt_ref) hipEventDestroy(c->kt_ref);
     for (int i = 0; i < NSETS; i++) {
         hipEvent_t* evs[] = {&c->ev_ra[i], &c->ev_rb[i], &c->ev_pa[i], &c->ev_pb[i]};
         for (hipEvent_t* e : evs)
@@ -1203,6 +1213,10 @@ int odo_set_timing(odo_ctx* c, int mode) {
         c->kt_next = c->kt_pending = 0;
         c->kt_sum_ms = 0;
         c->kt_count = 0;
+        if (!c->kt_ref && hipEventCreateWithFlags(&c->kt_ref, tf) != hipSuccess)
+            return fail(ODO_ERR_DEVICE, "hipEventCreate failed");
+        HIPCHK(hipEventRecord(c->kt_ref, c->stream));  // every stream is idle (sync_all above)
+        c->kt_marks.clear();
     }
     return ODO_OK;
 }
@@ -1214,6 +1228,9 @@ static int kt_collect(odo_ctx* c, int i) {
     HIPCHK(hipEventElapsedTime(&t, c->kt0[i], c->kt1[i]));
     c->kt_sum_ms += t;
     c->kt_count++;
+    float m = 0;
+    HIPCHK(hipEventElapsedTime(&m, c->kt_ref, c->kt0[i]));
+    c->kt_marks.push_back(m);
     return ODO_OK;
 }
 
@@ -1231,6 +1248,20 @@ int odo_kernel_timing(odo_ctx* c, double* avg_ms, long* launches) {
     *launches = c->kt_count;
     *avg_ms = c->kt_count ? c->kt_sum_ms / (double)c->kt_count : 0.0;
     return ODO_OK;
+}
+
+// The kNN-2 launch of batch b starts once b's extraction has finished (and
+// its pair stream is free): the marks' differences are the pipeline's
+// per-step times, read without adding any event to the extraction stream.
+int odo_step_marks(odo_ctx* c, double* ms, int cap) {
+    if (!c || cap < 0 || (cap > 0 && !ms)) return fail(ODO_ERR_ARG, "step_marks: bad arguments");
+    double avg = 0;
+    long n = 0;
+    int e;
+    if ((e = odo_kernel_timing(c, &avg, &n))) return e;  // collects the pending marks
+    const int k = (int)c->kt_marks.size();
+    for (int i = 0; i < k && i < cap; i++) ms[i] = c->kt_marks[i];
+    return k;
 }
 
 int odo_synchronize(odo_ctx* c) {
@@ -1959,6 +1990,12 @@ int odo_knn_replay_time(odo_ctx* c, int reps, float* avg_ms) {
     if (c->last_knn_set < 0) return fail(ODO_ERR_ARG, "knn_replay_time: no batch tracked yet");
     int e;
     if ((e = sync_all(c))) return e;
+    // hipGetLastError is sticky per thread: an error left by an earlier call
+    // is reported as that, not as a failure of the replay
+    const hipError_t pending = hipGetLastError();
+    if (pending != hipSuccess)
+        return fail(ODO_ERR_DEVICE, std::string("knn_replay_time: HIP error pending from an earlier call: ") +
+                                        hipGetErrorString(pending));
     const int s = c->last_knn_set, n = c->last_knn_n;
     const size_t b = fbase(c, s), KC = (size_t)c->kp_cap;
     uint8_t* desc = c->desc + b * KC * 32;
@@ -2397,6 +2434,9 @@ static int hyps_launch(odo_ctx* c, const odo_dmatch* m12, int n12, const float* 
     *n_good = ng;
     hipStream_t st = c->stream;
     DevArena& A = S.arena;
+    // the previous session's kernels (queued asynchronously by _dev / _finish)
+    // may still read the arena that begin() may free and replace
+    HIPCHK(hipStreamSynchronize(st));
     A.begin();
     S.xyz = new DevBuf(A, (size_t)2 * kc * 3 * sizeof(float));
     S.m = new DevBuf(A, (size_t)ng * sizeof(odo_dmatch));

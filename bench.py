@@ -267,13 +267,15 @@ def cpu_baseline(bgr, dep, nfeat, iters, n_frames, reps, adaptive=False, threads
             "all_cores": {"fps": nf_all / ta, "threads": nthr, "frames": nf_all}}
 
 
-def timed_leg(odo, submit, steps, warmup, world, dist, coll_dev, kernel_timing=True, inside=None):
+def timed_leg(odo, submit, steps, warmup, world, dist, coll_dev, kernel_timing=True, inside=None, marks_out=None):
     """The bench contract for one leg: `warmup` untimed steps, then exactly
     `steps` timed steps bracketed by a barrier + device synchronize on both
     sides, the wall time taken as the max over ranks. submit(i) queues step i;
     inside() runs inside the timed region after the last step (frames mode:
     the pose stitch). With kernel_timing, an event pair brackets every kNN-2
-    launch of the timed steps (on the stream that runs it, odo timing mode 2).
+    launch of the timed steps (on the stream that runs it, odo timing mode 2),
+    and marks_out (a list) receives each timed batch's kNN-2 start (ms,
+    odo_step_marks), whose differences are the per-step times.
     Returns (elapsed s, host submit s, (kNN-2 mean ms, launches))."""
     import torch
     for i in range(warmup):
@@ -298,8 +300,24 @@ def timed_leg(odo, submit, steps, warmup, world, dist, coll_dev, kernel_timing=T
     kt = (None, 0)
     if kernel_timing:
         kt = odo.kernel_timing()
+        if marks_out is not None:
+            marks_out.extend(odo.step_marks())
         odo.set_timing(False)
     return el, sub, kt
+
+
+def step_stats(marks):
+    """Per-step time distribution of a timed leg from its step marks (ms): one
+    step = the interval between consecutive batches' kNN-2 starts, which
+    follow each batch's extraction (the pipeline's critical stream)."""
+    d = np.diff(np.asarray(marks, dtype=np.float64))
+    if d.size == 0:
+        return None
+    med = float(np.median(d))
+    return {"min": round(float(d.min()), 4), "median": round(med, 4), "p90": round(float(np.percentile(d, 90)), 4),
+            "max": round(float(d.max()), 4), "mean": round(float(d.mean()), 4), "n": int(d.size),
+            "max_over_median": round(float(d.max()) / med, 4) if med > 0 else None,
+            "source": "differences of consecutive batches' kNN-2 start events (odo_step_marks, rank 0)"}
 
 
 def raw_h2d_gbs(nbytes: int) -> float:
@@ -929,6 +947,7 @@ def track_mode(args, rank, world, local_rank, dist):
     coll_dev = "cuda" if args.backend == "nccl" else "cpu"  # where the exchanges' tensors live
     ktime = not args.no_kernel_timing
     K, Wm = args.steps, args.warmup
+    head_marks = []  # the headline leg's per-batch step marks (kernel timing on)
 
     if seq_mode:
         fsm = import_module("arlm_amd.frames_shard")
@@ -968,12 +987,12 @@ def track_mode(args, rank, world, local_rank, dist):
         res_q = recs[-1][1:]  # a halo step: B genuine pairs, record p+1 = pair (frame p, frame p+1)
         pair_frame0 = 1       # batch frame of record 0 of res_q
 
-        def leg(host):
+        def leg(host, marks_out=None):
             return timed_leg(odo, lambda i: step(host, timed_steps if i >= Wm else None), K, Wm, world, dist,
-                             coll_dev, ktime, inside=stitch_timed)
+                             coll_dev, ktime, inside=stitch_timed, marks_out=marks_out)
 
         # the headline: inputs resident in HBM
-        elapsed, submit, (knn_ms, knn_launches) = leg(False)
+        elapsed, submit, (knn_ms, knn_launches) = leg(False, head_marks)
         # from host memory: every rank uploads its chunk + halo over its own link
         h_el, h_sub, (h_knn_ms, _) = leg(True) if args.host_steps > 0 else (None, None, (None, 0))
         sd = None
@@ -1015,7 +1034,8 @@ def track_mode(args, rank, world, local_rank, dist):
                 while time.perf_counter() < t_end:
                     pass
 
-        elapsed, submit, (knn_ms, knn_launches) = timed_leg(odo, head_step, K, Wm, world, dist, coll_dev, ktime)
+        elapsed, submit, (knn_ms, knn_launches) = timed_leg(odo, head_step, K, Wm, world, dist, coll_dev, ktime,
+                                                            marks_out=head_marks)
         # the last timed batch's records arrived: its match and query counts
         # equal any batch's after the first (every batch cycles the same loop;
         # the RANSAC outcome differs, each pair's seed is its global index)
@@ -1161,6 +1181,7 @@ def track_mode(args, rank, world, local_rank, dist):
             "steps": K,
             "warmup": Wm,
             "ms_per_step": round(ms_per_step, 3),
+            "step_ms": step_stats(head_marks),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

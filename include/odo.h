@@ -379,6 +379,11 @@ int odo_debug_select(odo_ctx* ctx, const uint32_t* in, int n, int nth, int mode,
  * odo_kernel_timing reports the mean launch duration since the mode was set. */
 int odo_set_timing(odo_ctx* ctx, int mode);
 int odo_kernel_timing(odo_ctx* ctx, double* avg_ms, long* launches);
+/* Measurement only (mode 2): the start of every batch's kNN-2 launch since the
+ * mode was set, in ms after odo_set_timing, batch order. A batch's kNN-2 starts
+ * when its extraction has finished, so consecutive differences are the
+ * pipeline's per-step times. Copies up to cap marks; returns how many exist. */
+int odo_step_marks(odo_ctx* ctx, double* ms, int cap);
 /* Per-stage device time of the last odo_track_batch (ms), via HIP events. */
 int odo_last_timings(odo_ctx* ctx, float* ms, int cap, const char** names);
 
