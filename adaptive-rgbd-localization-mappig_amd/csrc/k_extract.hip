@@ -1277,6 +1277,9 @@ __global__ void __launch_bounds__(256) k_blur(const uint8_t* __restrict__ pyr, u
 // two v_perm per dword from per-lane selectors. Widths that are not a
 // multiple of 4 leave garbage in the row padding past w, never read.
 #define BR_R 30  // output rows per chunk (a multiple of 6; levels are >= 40 rows)
+#ifndef BW_ROLL
+#define BW_ROLL 0  // blur walk rows loaded as a rolling 6-row queue (see blur_walk)
+#endif
 struct BlurRows {
     int base[17];   // first strip item of each level (prefix); base[nlevels] = items
     int nst[16];    // strips of 16 quads across the interior
@@ -1314,31 +1317,46 @@ ODO_INLINE void blur_walk(const uint8_t* s0, uint8_t* dp, size_t pitch, int h, i
     // edge chunk address their rows through reflect101
     static_assert(R % 6 == 0, "the accumulators rotate over 6 rows");
     constexpr int NB = (R + 6) / 6;
-    uint32_t cw[6][3], nw[6][3];
+    uint32_t cw[6][3];
+#if !BW_ROLL
+    uint32_t nw[6][3];
+#endif
     const uint8_t* sp = s0 + (size_t)(y0 - 3) * pitch;
+    // input row 6b + j of the walk (rows y0 - 3 ...) into d
+    auto load_row = [&](uint32_t(&d)[3], int b, int j, bool refl) {
+        if (EDGE) {
+            const uint8_t* rp = s0 + (size_t)reflect101_1(y0 - 3 + 6 * b + j, h) * pitch;
+            d[0] = *reinterpret_cast<const uint32_t*>(rp + o0);
+            d[1] = *reinterpret_cast<const uint32_t*>(rp + o1);
+            d[2] = *reinterpret_cast<const uint32_t*>(rp + o2);
+        } else {
+            const uint8_t* rp = refl ? s0 + (size_t)reflect101_1(y0 - 3 + 6 * b + j, h) * pitch : sp + j * pitch;
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(rp);
+            d[0] = w[0], d[1] = w[1], d[2] = w[2];
+        }
+    };
     auto load_block = [&](uint32_t(&d)[6][3], int b, bool refl) {
 #pragma unroll
-        for (int j = 0; j < 6; j++) {
-            if (EDGE) {
-                const uint8_t* rp = s0 + (size_t)reflect101_1(y0 - 3 + 6 * b + j, h) * pitch;
-                d[j][0] = *reinterpret_cast<const uint32_t*>(rp + o0);
-                d[j][1] = *reinterpret_cast<const uint32_t*>(rp + o1);
-                d[j][2] = *reinterpret_cast<const uint32_t*>(rp + o2);
-            } else {
-                const uint8_t* rp = refl ? s0 + (size_t)reflect101_1(y0 - 3 + 6 * b + j, h) * pitch : sp + j * pitch;
-                const uint32_t* w = reinterpret_cast<const uint32_t*>(rp);
-                d[j][0] = w[0], d[j][1] = w[1], d[j][2] = w[2];
-            }
-        }
+        for (int j = 0; j < 6; j++) load_row(d[j], b, j, refl);
         sp += 6 * pitch;
     };
     load_block(cw, 0, top);
     for (int b = 0; b < NB; b++) {
+#if !BW_ROLL
         if (b + 1 < NB) load_block(nw, b + 1, b + 1 == NB - 1 && bottom);
+#else
+        // BW_ROLL: a 6-row queue instead of two 6-row blocks: row j of block b
+        // + 1 is loaded into row j's registers as soon as row j of block b has
+        // been consumed (6 rows in flight, 18 registers fewer)
+        const bool nref = b + 1 == NB - 1 && bottom;
+#endif
 #pragma unroll
         for (int j = 0; j < 6; j++) {
             // input row r = y0 - 3 + 6b + j
             uint32_t w0 = cw[j][0], w1 = cw[j][1], w2 = cw[j][2];
+#if BW_ROLL
+            if (b + 1 < NB) load_row(cw[j], b + 1, j, nref);
+#endif
             if (EDGE) {
                 // the row's bytes x-4 .. x+7 with reflected columns
                 const uint32_t e0 = __builtin_amdgcn_perm(w1, w0, selA[0]) | __builtin_amdgcn_perm(w2, w2, selB[0]);
@@ -1383,8 +1401,12 @@ ODO_INLINE void blur_walk(const uint8_t* s0, uint8_t* dp, size_t pitch, int h, i
                 dp += pitch;
             }
         }
+#if BW_ROLL
+        sp += 6 * pitch;
+#else
 #pragma unroll
         for (int j = 0; j < 6; j++) cw[j][0] = nw[j][0], cw[j][1] = nw[j][1], cw[j][2] = nw[j][2];
+#endif
     }
 }
 
@@ -1486,6 +1508,13 @@ __global__ void __launch_bounds__(256) k_blur_rows(const uint8_t* __restrict__ p
 // so no separate blur launch follows (uint8 blur pyramid written to `blur`).
 #ifndef PYR_TH
 #define PYR_TH 1024  // threads per frame workgroup
+#endif
+#ifndef PYR_VGPR
+#define PYR_ATTR
+#else
+// a VGPR cap (PYR_VGPR registers) on the fused pyramid, so that its
+// workgroups fit beside the pair kernels' register footprints
+#define PYR_ATTR __attribute__((amdgpu_waves_per_eu(PYR_VGPR)))
 #endif
 #ifndef PYR_RU
 #define PYR_RU 2  // output rows in flight per thread (resize)
@@ -1630,7 +1659,7 @@ ODO_INLINE void pyr_gray_rows(const uint8_t* __restrict__ src, uint8_t* gdst, in
     }
 }
 template <bool BLUR>
-__global__ void __launch_bounds__(PYR_TH) k_pyramid(const uint8_t* __restrict__ bgr, uint8_t* __restrict__ pyr,
+__global__ void __launch_bounds__(PYR_TH) PYR_ATTR k_pyramid(const uint8_t* __restrict__ bgr, uint8_t* __restrict__ pyr,
                                                     size_t in_stride, size_t pyr_stride,
                                                     const LevelDesc* __restrict__ lv, const ResizeX* __restrict__ xt,
                                                     const ResizeY* __restrict__ yt, PyrLevels PL, int nlevels,

@@ -1305,9 +1305,15 @@ __global__ void __launch_bounds__(PM_THREADS) k_pair_match(
 __global__ void k_latch(double* __restrict__ latch, const SortEl* __restrict__ good, const int* __restrict__ n_good,
                         const int* __restrict__ n_matches, const odo_dmatch* __restrict__ matches,
                         const float* __restrict__ xyz, int kp_cap, int slot0, int npairs, int match_cap,
-                        int min_inl, int sample_size, int iterations, const int* __restrict__ pair_valid) {
+                        int min_inl, int sample_size, int iterations, const int* __restrict__ pair_valid,
+                        int* __restrict__ set_flag) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    if (!__builtin_isnan(*latch)) return;
+    // set_flag (page-locked host memory, may be null): 1 once the latch holds
+    // a value, so the host can stop ordering later batches' latch kernels
+    if (!__builtin_isnan(*latch)) {
+        if (set_flag) *set_flag = 1;
+        return;
+    }
     for (int p = 0; p < npairs; p++) {
         if (!pair_valid[p]) continue;
         if (n_matches[p] < 20 || n_matches[p] < min_inl) continue;
@@ -1325,6 +1331,7 @@ __global__ void k_latch(double* __restrict__ latch, const SortEl* __restrict__ g
             const double z = (double)X1[3 * m.queryIdx + 2];
             const double sd = 0.01 * z * z;
             *latch = sd * sd;
+            if (set_flag) *set_flag = 1;
             return;
         }
     }
@@ -1452,8 +1459,8 @@ int launch_sort_dbg(hipStream_t st, void* a, int n) {
 
 void launch_latch(hipStream_t st, double* latch, const void* good, const int* n_good, const int* n_matches,
                   const odo_dmatch* matches, const float* xyz, int kp_cap, int slot0, int npairs, int match_cap,
-                  int min_inl, int sample_size, int iterations, const int* pair_valid) {
+                  int min_inl, int sample_size, int iterations, const int* pair_valid, int* set_flag) {
     hipLaunchKernelGGL(k_latch, dim3(1), dim3(64), 0, st, latch, (const SortEl*)good, n_good, n_matches, matches, xyz,
-                       kp_cap, slot0, npairs, match_cap, min_inl, sample_size, iterations, pair_valid);
+                       kp_cap, slot0, npairs, match_cap, min_inl, sample_size, iterations, pair_valid, set_flag);
 }
 }  // namespace odo

@@ -166,6 +166,7 @@ struct odo_ctx {
     std::vector<hipStream_t> owned;  // streams created (the rest alias them)
     hipEvent_t ev_latch = nullptr;   // after the last queued k_latch (schedule 5)
     bool latch_rec = false;
+    bool latched = false;  // this batch leaves the latch kernel out (see run_pairs)
     uint64_t batch_counter = 0;
     int W = 0, H = 0, maxb = 0, slots = 0, nlevels = 0;
     std::vector<LevelDesc> lv_h;
@@ -285,6 +286,7 @@ struct odo_ctx {
     // per set: RANSAC part 1 / part 2 done, PnP A / PnP B done
     hipEvent_t ev_ra[NSETS] = {}, ev_rb[NSETS] = {}, ev_pa[NSETS] = {}, ev_pb[NSETS] = {};
     bool pdone_rec[NSETS] = {};
+    hipStream_t pdone_st[NSETS] = {};  // the stream that last recorded ev_pa / ev_pb of a set
     bool serial = false;
     bool timing = false;
     // stream layout (ODO_SCHED). Only the streams a schedule uses are created:
@@ -339,6 +341,10 @@ struct odo_ctx {
     uint64_t *ocell = nullptr, *oakp = nullptr;
     DevArena arena;  // per-stage entry points' device scratch
     int* h_open = nullptr;  // page-locked [NSETS]: RANSAC open pairs of the last batch per set (launch hint)
+    // page-locked, host-coherent: k_latch writes 1 once the latch holds a
+    // value; with ev_latch complete the host then stops ordering (and
+    // launching) the no-op latch kernels of later batches
+    int* latch_set_h = nullptr;
     // Hamming-match kernel timing (odo_set_timing mode 2): an event pair
     // around the kNN-2 launch of every batch, read back and summed lazily
     static constexpr int KT_RING = 256;
@@ -356,6 +362,24 @@ struct odo_ctx {
 static inline size_t fbase(const odo_ctx* c, int set) { return (size_t)set * c->slots; }
 // the set the next batch extracts into
 static inline int next_set(const odo_ctx* c) { return (c->seq_set + 1) % NSETS; }
+
+#ifndef ODO_WAIT_DEDUP
+#define ODO_WAIT_DEDUP 1
+#endif
+// `st` waits until the PnP launches (and, async, the result copy) of the batch
+// that last used frame set `set` are done. Every wait is a barrier packet the
+// queue processes in order: schedule 5 records ev_pa and ev_pb at the same
+// point of one stream, so one of them is enough, and none is needed on that
+// stream itself (ODO_WAIT_DEDUP; 0 = the round-5 waits on both events).
+static int wait_pnp_done(odo_ctx* c, hipStream_t st, int set) {
+    if (ODO_WAIT_DEDUP && c->sched == 5) {
+        if (st != c->pdone_st[set]) HIPCHK(hipStreamWaitEvent(st, c->ev_pb[set], 0));
+        return ODO_OK;
+    }
+    HIPCHK(hipStreamWaitEvent(st, c->ev_pa[set], 0));
+    HIPCHK(hipStreamWaitEvent(st, c->ev_pb[set], 0));
+    return ODO_OK;
+}
 
 // Stage-timing marks (odo_last_timings) are recorded only when enabled with
 // odo_set_timing: timing events serialise the queue they sit on, which costs
@@ -471,6 +495,7 @@ static void free_ctx(odo_ctx* c) {
     if (c->hyp_up) hipEventDestroy(c->hyp_up);
     for (hipStream_t st : c->owned) hipStreamDestroy(st);
     if (c->h_open) (void)hipHostFree(c->h_open);
+    if (c->latch_set_h) (void)hipHostFree(c->latch_set_h);
     delete c;
 }
 
@@ -971,6 +996,8 @@ static int alloc_buffers(odo_ctx* c) {
     }
     HIPCHK(hipHostMalloc((void**)&c->h_open, NSETS * sizeof(int), hipHostMallocDefault));
     for (int i = 0; i < NSETS; i++) c->h_open[i] = -1;  // unknown: the first RANSAC launch runs both forms
+    HIPCHK(hipHostMalloc((void**)&c->latch_set_h, sizeof(int), hipHostMallocCoherent));
+    *c->latch_set_h = 0;
     HIPCHK(hipMemset(c->nkp, 0, S * sizeof(int)));
     const double nan = std::nan("");
     HIPCHK(hipMemcpy(c->latch, &nan, sizeof(double), hipMemcpyHostToDevice));
@@ -1179,6 +1206,7 @@ int odo_reset(odo_ctx* c) {
     c->pair_counter = 0;
     const double nan = std::nan("");
     HIPCHK(hipMemcpy(c->latch, &nan, sizeof(double), hipMemcpyHostToDevice));
+    if (c->latch_set_h) *c->latch_set_h = 0;
     return reset_adaptive(c);
 }
 
@@ -1187,6 +1215,7 @@ int odo_set_latch(odo_ctx* c, double cov) {
     int e;
     if ((e = sync_all(c))) return e;
     HIPCHK(hipMemcpy(c->latch, &cov, sizeof(double), hipMemcpyHostToDevice));
+    if (c->latch_set_h) *c->latch_set_h = std::isnan(cov) ? 0 : 1;
     return ODO_OK;
 }
 
@@ -1464,12 +1493,18 @@ static int run_pairs(odo_ctx* c, int set, int n) {
                       c->sort_scratch, c->match_cap, n);
     // the DepthCovariance latch is taken from the first valid pair ever: with
     // two pair streams, a batch's latch kernel runs after the previous one's
-    if (c->sched == 5 && c->latch_rec) HIPCHK(hipStreamWaitEvent(st, c->ev_latch, 0));
-    launch_latch(st, c->latch, P.good, P.n_good, P.n_matches, P.matches, xyz, c->kp_cap, 0, n, c->match_cap,
-                 c->cfg.ransac.min_inlier_th, c->cfg.ransac.sample_size, c->cfg.ransac.iterations, P.pair_valid);
-    if (c->sched == 5) {
-        HIPCHK(hipEventRecord(c->ev_latch, st));
-        c->latch_rec = true;
+    // Once the latch holds a value (k_latch's host flag) and the kernel that
+    // set it has completed (ev_latch), the latch kernel is a no-op: it and its
+    // two ordering packets are left out (ODO_WAIT_DEDUP)
+    if (!c->latched) {
+        if (c->sched == 5 && c->latch_rec) HIPCHK(hipStreamWaitEvent(st, c->ev_latch, 0));
+        launch_latch(st, c->latch, P.good, P.n_good, P.n_matches, P.matches, xyz, c->kp_cap, 0, n, c->match_cap,
+                     c->cfg.ransac.min_inlier_th, c->cfg.ransac.sample_size, c->cfg.ransac.iterations, P.pair_valid,
+                     c->latch_set_h);
+        if (c->sched == 5) {
+            HIPCHK(hipEventRecord(c->ev_latch, st));
+            c->latch_rec = true;
+        }
     }
     tmark(c, 7, st);
     if (c->sched != 1) {
@@ -1481,8 +1516,10 @@ static int run_pairs(odo_ctx* c, int set, int n) {
                       c->latch, P.pair_valid, 20, nullptr, c->rscr[set], P.best_mask, c->mask_words, P.res, P.T12, n,
                       0, P.pair_phase, c->h_open + set);
         tmark(c, 8, st);
-        HIPCHK(hipEventRecord(c->ev_rb[set], st));
-        // schedule 5: PnP follows RANSAC on the batch's own pair stream
+        // schedule 5: PnP follows RANSAC on the batch's own pair stream, and
+        // nothing waits on ev_rb (the side stream of schedules 0-3 does): no
+        // marker packet between the RANSAC and PnP launches (ODO_WAIT_DEDUP)
+        if (!(ODO_WAIT_DEDUP && c->sched == 5)) HIPCHK(hipEventRecord(c->ev_rb[set], st));
         hipStream_t ps = c->sched == 5 ? st : c->pnpa;
         if (ps != st) HIPCHK(hipStreamWaitEvent(ps, c->ev_rb[set], 0));
         if (!(c->skip & 1))
@@ -1491,6 +1528,7 @@ static int run_pairs(odo_ctx* c, int set, int n) {
         tmark(c, 9, ps);
         HIPCHK(hipEventRecord(c->ev_pa[set], ps));
         HIPCHK(hipEventRecord(c->ev_pb[set], ps));
+        c->pdone_st[set] = ps;
         HIPCHK(hipGetLastError());
         return ODO_OK;
     }
@@ -1518,6 +1556,7 @@ static int run_pairs(odo_ctx* c, int set, int n) {
                P.pair_valid, P.n_matches, 20, P.edges, P.res, P.pnp_mask, n, P.pair_phase, 0);
     tmark(c, 9, c->pnpb);
     HIPCHK(hipEventRecord(c->ev_pb[set], c->pnpb));
+    c->pdone_st[set] = nullptr;  // two streams: wait on both events
     HIPCHK(hipGetLastError());
     return ODO_OK;
 }
@@ -1554,19 +1593,24 @@ static int finish_batch(odo_ctx* c, int set, int n, odo_pair_result* h_results) 
 int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, int n, odo_pair_result* h_results) {
     if (!c || !d_bgr || !d_depth || n <= 0 || n > c->maxb) return fail(ODO_ERR_ARG, "bad track args");
     int e;
+    // decided before this call queues anything: a not-ready query leaves
+    // hipErrorNotReady as the thread's last error, cleared here
+    c->latched = false;
+    if (ODO_WAIT_DEDUP && c->sched == 5 && c->latch_rec && __atomic_load_n(c->latch_set_h, __ATOMIC_ACQUIRE) != 0) {
+        const hipError_t q = hipEventQuery(c->ev_latch);
+        if (q == hipSuccess) c->latched = true;
+        else if (q == hipErrorNotReady) (void)hipGetLastError();
+        else return fail(ODO_ERR_DEVICE, std::string("hipEventQuery: ") + hipGetErrorString(q));
+    }
     const int s = next_set(c);
     const size_t KC = (size_t)c->kp_cap;
     // ---- extraction stream: set s is free once the pair stages of the batch
     // before the previous one (which read it) are done
-    if (c->pdone_rec[s]) {
-        HIPCHK(hipStreamWaitEvent(c->stream, c->ev_pa[s], 0));
-        HIPCHK(hipStreamWaitEvent(c->stream, c->ev_pb[s], 0));
-    }
+    if (c->pdone_rec[s] && (e = wait_pnp_done(c, c->stream, s))) return e;
     if (c->knn_gate && c->knn_rec) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_knn, 0));
     if (c->sched == 5 && c->pyr_wait > 0 && c->batch_counter >= (uint64_t)c->pyr_wait) {
         const int sb = c->batch_set[(c->batch_counter - (uint64_t)c->pyr_wait) & 7];
-        HIPCHK(hipStreamWaitEvent(c->stream, c->ev_pa[sb], 0));
-        HIPCHK(hipStreamWaitEvent(c->stream, c->ev_pb[sb], 0));
+        if (!(ODO_WAIT_DEDUP && sb == s && c->pdone_rec[s]) && (e = wait_pnp_done(c, c->stream, sb))) return e;
     }
     tmark(c, 0, c->stream);
     if (c->has_prev) {
@@ -1655,10 +1699,7 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
         } else {
             c->cur_p = c->pstream;
         }
-        if (c->pdone_rec[s]) {
-            HIPCHK(hipStreamWaitEvent(c->cur_p, c->ev_pa[s], 0));
-            HIPCHK(hipStreamWaitEvent(c->cur_p, c->ev_pb[s], 0));
-        }
+        if (c->pdone_rec[s] && (e = wait_pnp_done(c, c->cur_p, s))) return e;
         HIPCHK(hipEventRecord(c->ev_xdone[s], c->stream));
         launch_ransac_raw(c->cur_p, c->rscr[s], n, c->match_cap, c->mask_words, c->rcfg, (uint64_t)c->cfg.seed,
                           c->pair_counter, nullptr);
@@ -1703,8 +1744,7 @@ int odo_track_batch_async(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_de
     const int s = c->view_set;
     auto& P = c->pb[s];
     hipStream_t st = c->cur_p ? c->cur_p : c->pstream;  // the batch's pair stream (its PnP ran there last)
-    HIPCHK(hipStreamWaitEvent(st, c->ev_pa[s], 0));
-    HIPCHK(hipStreamWaitEvent(st, c->ev_pb[s], 0));
+    if ((e = wait_pnp_done(c, st, s))) return e;
     hipLaunchKernelGGL(k_res_patch, dim3((n + 255) / 256), dim3(256), 0, st, P.res, P.n_matches, c->qcnt[s], n,
                        first_valid);
     HIPCHK(hipGetLastError());
@@ -1712,6 +1752,7 @@ int odo_track_batch_async(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_de
     // the batch that next reuses set s waits for these events: include the copy
     HIPCHK(hipEventRecord(c->ev_pa[s], st));
     HIPCHK(hipEventRecord(c->ev_pb[s], st));
+    c->pdone_st[s] = st;
     return ODO_OK;
 }
 

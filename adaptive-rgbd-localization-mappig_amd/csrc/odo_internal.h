@@ -262,7 +262,7 @@ void launch_pair_match(hipStream_t st, const int2* knn_idx, const int2* knn_dist
 int launch_sort_dbg(hipStream_t st, void* a, int n);
 void launch_latch(hipStream_t st, double* latch, const void* good, const int* n_good, const int* n_matches,
                   const odo_dmatch* matches, const float* xyz, int kp_cap, int slot0, int npairs, int match_cap,
-                  int min_inl, int sample_size, int iterations, const int* pair_valid);
+                  int min_inl, int sample_size, int iterations, const int* pair_valid, int* set_flag = nullptr);
 size_t ransac_gpt_bytes();
 // rand() words for every pair (data independent): launched at batch start on
 // a side stream; launch_ransac's stream must wait for it.

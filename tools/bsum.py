@@ -9,4 +9,5 @@ for p in sys.argv[1:]:
     print(p, "value", d["value"], "ms", d["ms_per_step"], "host", (d.get("from_host") or {}).get("value"),
           "hard", (d.get("hard_workload") or {}).get("value"), "lat p50", lat.get("p50_ms"), "p99", lat.get("p99_ms"),
           " ".join(f"{k}={v}" for k, v in st.items()), "knn frac", (d.get("roofline") or {}).get("frac"),
+          "steps", {k: (d.get("step_ms") or {}).get(k) for k in ("min", "median", "p90", "max")},
           "stages", d.get("stage_ms"))
