@@ -1278,7 +1278,14 @@ __global__ void __launch_bounds__(256) k_blur(const uint8_t* __restrict__ pyr, u
 // multiple of 4 leave garbage in the row padding past w, never read.
 #define BR_R 30  // output rows per chunk (a multiple of 6; levels are >= 40 rows)
 #ifndef BW_ROLL
-#define BW_ROLL 0  // blur walk rows loaded as a rolling 6-row queue (see blur_walk)
+#define BW_ROLL 1  // blur walk rows loaded as a rolling 6-row queue (see blur_walk)
+#endif
+#ifndef PYR_NT
+// nontemporal (streaming) accesses for the pyramid's data that is not read
+// again soon: bit 0 the BGR loads, bit 1 the blurred-level stores (finalize
+// reads them a millisecond later), so they do not evict from L2 the levels the
+// next resize and blur walks read back
+#define PYR_NT 0
 #endif
 struct BlurRows {
     int base[17];   // first strip item of each level (prefix); base[nlevels] = items
@@ -1397,7 +1404,10 @@ ODO_INLINE void blur_walk(const uint8_t* s0, uint8_t* dp, size_t pitch, int h, i
             if (b > 0 && store) {
                 const uint32_t lo = __builtin_amdgcn_perm(s1v, s0v, 0x0c0c0602u);
                 const uint32_t hi = __builtin_amdgcn_perm(s3v, s2v, 0x06020c0cu);
-                *reinterpret_cast<uint32_t*>(dp) = lo | hi;
+                if (PYR_NT & 2)
+                    __builtin_nontemporal_store(lo | hi, reinterpret_cast<uint32_t*>(dp));
+                else
+                    *reinterpret_cast<uint32_t*>(dp) = lo | hi;
                 dp += pitch;
             }
         }
@@ -1507,7 +1517,11 @@ __global__ void __launch_bounds__(256) k_blur_rows(const uint8_t* __restrict__ p
 // edge lanes) once the level is complete, beside the resize that reads it,
 // so no separate blur launch follows (uint8 blur pyramid written to `blur`).
 #ifndef PYR_TH
-#define PYR_TH 1024  // threads per frame workgroup
+// threads per frame workgroup. 512 (round 6): 2 waves per SIMD at <= 80
+// VGPRs (BW_ROLL) = 160 registers, so a frame's workgroup fits on a CU that
+// holds a k_pnp workgroup (328 per SIMD); at 1024 (352) it waited for PnP
+// to drain off the CU on every other step (DESIGN §4 Pipelining)
+#define PYR_TH 512
 #endif
 #ifndef PYR_VGPR
 #define PYR_ATTR
@@ -1625,7 +1639,13 @@ ODO_INLINE void pyr_gray_rows(const uint8_t* __restrict__ src, uint8_t* gdst, in
                 const int q = q0 + u * PYR_TH;
                 if (q < nq4) {
                     const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src + (size_t)q * 12);
-                    wv[u][0] = s32[0], wv[u][1] = s32[1], wv[u][2] = s32[2];
+                    if (PYR_NT & 1) {
+                        wv[u][0] = __builtin_nontemporal_load(s32);
+                        wv[u][1] = __builtin_nontemporal_load(s32 + 1);
+                        wv[u][2] = __builtin_nontemporal_load(s32 + 2);
+                    } else {
+                        wv[u][0] = s32[0], wv[u][1] = s32[1], wv[u][2] = s32[2];
+                    }
                 }
             }
 #pragma unroll

@@ -15,6 +15,7 @@
 #   multi               bench.py --gpus 2 --backend gloo: two ranks sharing the GPU
 #   kt                  rocprofv3 kernel trace of the headline command (+ timed-region split)
 #   ktn=NAME            the A/B bench command under a kernel trace (NAME.json, NAME/)
+#   ktv=V               the A/B bench command under a kernel trace, variant build_V
 #   kth                 rocprofv3 kernel trace of the hard workload's pipelined main leg
 #   serial              per-kernel times alone (tuning build, ODO_SERIAL_STREAMS=1),
 #                       default and hard workloads
@@ -25,6 +26,7 @@
 #   vtests=V:F1,F2      pytest -m gpu over the named files against variant build_V
 #   probe=V:SCRIPT      python tools/SCRIPT.py with ODO_LIB = variant build_V (probe builds)
 #   pmcx=NAME:REGEX:C1,C2   one PMC pass with the named counters (pmcx_NAME/)
+#   vpmcx=V:NAME:REGEX:C1,C2  pmcx with variant build_V
 #   listctr             rocprofv3 -L (the box's counter names) -> counters.txt
 #   envbench=NAME:ENV:ARGS  bench.py on the tuning build with knobs in the environment
 #                       (ENV: VAR=VAL joined by '/'; ARGS with '+' for spaces)
@@ -119,6 +121,15 @@ for step in "$@"; do
         python3 $R/bench.py --no-cpu-baseline --latency-frames 0 --host-steps 0 $AB_ARGS > $O/$name.json 2> $O/$name.err
       cd $R
       echo "ktn $name: $(python tools/bsum.py $O/$name.json 2>/dev/null || true)" ;;
+    ktv=*)
+      # ktv=V: the A/B bench command under a kernel trace with variant build_V
+      v=${step#ktv=}
+      cd /tmp
+      ODO_LIB=$(lib_of $v) timeout -s KILL 600 rocprofv3 --kernel-trace -d $O/ktv_$v -o run --output-format csv -- \
+        python3 $R/bench.py --no-cpu-baseline --latency-frames 0 --host-steps 0 --hard-steps 0 $AB_ARGS \
+        > $O/ktv_$v.json 2> $O/ktv_$v.err
+      cd $R
+      echo "ktv $v: $(python tools/bsum.py $O/ktv_$v.json 2>/dev/null || true)" ;;
     kth)
       # kernel trace of the hard workload in the main (pipelined) leg
       cd /tmp
@@ -157,6 +168,18 @@ for step in "$@"; do
         > $O/pmcx_$name/p.log 2>&1
       cd $R
       echo "pmcx $name ok" ;;
+    vpmcx=*)
+      # vpmcx=V:NAME:REGEX:C1,C2 — pmcx with variant build_V (built with -DODO_TUNING
+      # for ODO_SERIAL_STREAMS; else the pipelined bench) -> pmcx_NAME/
+      spec=${step#vpmcx=}; v=${spec%%:*}; rest=${spec#*:}; name=${rest%%:*}; rest=${rest#*:}
+      K=${rest%%:*}; ctr=$(echo ${rest#*:} | tr ',' ' ')
+      mkdir -p $O/pmcx_$name
+      cd /tmp
+      ODO_SERIAL_STREAMS=1 ODO_LIB=$(lib_of $v) timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-include-regex "$K" \
+        -d $O/pmcx_$name/p -o run --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 $QUICK \
+        > $O/pmcx_$name/p.log 2>&1
+      cd $R
+      echo "vpmcx $v $name ok" ;;
     listctr)
       timeout -k 10 60 rocprofv3 -L > $O/counters.txt 2>&1 || true
       echo "listctr ok" ;;
