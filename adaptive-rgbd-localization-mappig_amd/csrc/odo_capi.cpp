@@ -13,6 +13,7 @@
 // pair stages; per-set events order the reuse (set s is rewritten only after
 // the pair stages of batch k-1 that read it have finished).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <cmath>
 #include <cstdlib>
@@ -167,6 +168,11 @@ struct odo_ctx {
     hipEvent_t ev_latch = nullptr;   // after the last queued k_latch (schedule 5)
     bool latch_rec = false;
     bool latched = false;  // this batch leaves the latch kernel out (see run_pairs)
+    // the batch's extraction-done event, when run_extract may complete it with
+    // its last kernel (hipExtLaunchKernel's stop event) instead of a marker
+    // packet after it (ODO_XDONE_EXT); xdone_set: it did
+    hipEvent_t xdone_ev = nullptr;
+    bool xdone_set = false;
     uint64_t batch_counter = 0;
     int W = 0, H = 0, maxb = 0, slots = 0, nlevels = 0;
     std::vector<LevelDesc> lv_h;
@@ -365,6 +371,9 @@ static inline int next_set(const odo_ctx* c) { return (c->seq_set + 1) % NSETS; 
 
 #ifndef ODO_WAIT_DEDUP
 #define ODO_WAIT_DEDUP 1
+#endif
+#ifndef ODO_XDONE_EXT
+#define ODO_XDONE_EXT 1
 #endif
 // `st` waits until the PnP launches (and, async, the result copy) of the batch
 // that last used frame set `set` are done. Every wait is a barrier packet the
@@ -1451,7 +1460,8 @@ static int run_extract(odo_ctx* c, int set, const uint8_t* d_bgr, const uint16_t
                     c->okp_stride, d_depth, (size_t)c->W * c->H, c->W, c->cal, c->kps + (size_t)slot * c->kp_cap,
                     c->desc + (size_t)slot * c->kp_cap * 32, c->kun + (size_t)slot * c->kp_cap * 2,
                     c->xyz + (size_t)slot * c->kp_cap * 3, c->ur + (size_t)slot * c->kp_cap, c->nkp + slot, c->kp_cap,
-                    n);
+                    n, c->xdone_ev);
+    if (c->xdone_ev) c->xdone_set = true;
     tmark(c, 5, st);
     HIPCHK(hipGetLastError());
     return ODO_OK;
@@ -1621,7 +1631,12 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
                           c->desc + dst * KC * 32, c->kun + dst * KC * 2, c->xyz + dst * KC * 3, c->ur + dst * KC,
                           c->nkp + dst, c->kp_cap);
     }
-    if ((e = run_extract(c, s, d_bgr, d_depth, n, 1))) return e;
+    // schedule 5: ev_xdone completes with the extraction's last kernel
+    c->xdone_ev = ODO_XDONE_EXT && c->sched == 5 && !c->timing ? c->ev_xdone[s] : nullptr;
+    c->xdone_set = false;
+    e = run_extract(c, s, d_bgr, d_depth, n, 1);
+    c->xdone_ev = nullptr;
+    if (e) return e;
     // the kNN-2 stream: the extraction stream, or the side stream (sched 3)
     hipStream_t ks = c->stream;
     if (c->sched == 3) {
@@ -1700,7 +1715,7 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
             c->cur_p = c->pstream;
         }
         if (c->pdone_rec[s] && (e = wait_pnp_done(c, c->cur_p, s))) return e;
-        HIPCHK(hipEventRecord(c->ev_xdone[s], c->stream));
+        if (!c->xdone_set) HIPCHK(hipEventRecord(c->ev_xdone[s], c->stream));
         launch_ransac_raw(c->cur_p, c->rscr[s], n, c->match_cap, c->mask_words, c->rcfg, (uint64_t)c->cfg.seed,
                           c->pair_counter, nullptr);
         HIPCHK(hipEventRecord(c->ev_raw[s], c->cur_p));
