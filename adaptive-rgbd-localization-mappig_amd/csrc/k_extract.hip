@@ -1531,10 +1531,10 @@ __global__ void __launch_bounds__(256) k_blur_rows(const uint8_t* __restrict__ p
 #define PYR_ATTR __attribute__((amdgpu_waves_per_eu(PYR_VGPR)))
 #endif
 #ifndef PYR_RU
-#define PYR_RU 2  // output rows in flight per thread (resize)
+#define PYR_RU 4  // output rows in flight per thread (resize; 2 until round 5, at 1024 threads)
 #endif
 #ifndef PYR_GU
-#define PYR_GU 4  // gray quads in flight per thread
+#define PYR_GU 8  // gray quads in flight per thread (4 until round 5, at 1024 threads)
 #endif
 struct PyrLevels {
     int rx_off[16], ry_off[16];

@@ -15,8 +15,6 @@
 //   k_kp_geometry   one keypoint per lane: undistortion (5 double iterations)
 //                   and the depth back-projection, shared with the ADAPTIVE
 //                   extractor's finalisation (k_adaptive.hip)
-#include <hip/hip_ext.h>
-
 #include "odo_device.h"
 #include "odo_internal.h"
 #ifndef ODO_EXTRACT_PRIO
@@ -513,21 +511,16 @@ void upload_finalize_constants() {
 }
 
 void launch_kp_geometry(hipStream_t st, const orb_kp* kps, const int* nkp, const uint16_t* depth, size_t depth_stride,
-                        int img_w, FrameCalib cal, float* kun, float* xyz, float* ur, int kp_cap, int nframes,
-                        hipEvent_t done) {
+                        int img_w, FrameCalib cal, float* kun, float* xyz, float* ur, int kp_cap, int nframes) {
     dim3 g((kp_cap + 255) / 256, nframes);
-    if (done)  // the event completes with this kernel: no marker packet of its own
-        hipExtLaunchKernelGGL(k_kp_geometry, g, dim3(256), 0, st, nullptr, done, 0, kps, nkp, depth, depth_stride,
-                              img_w, cal, kun, xyz, ur, kp_cap);
-    else
-        hipLaunchKernelGGL(k_kp_geometry, g, dim3(256), 0, st, kps, nkp, depth, depth_stride, img_w, cal, kun, xyz, ur,
-                           kp_cap);
+    hipLaunchKernelGGL(k_kp_geometry, g, dim3(256), 0, st, kps, nkp, depth, depth_stride, img_w, cal, kun, xyz, ur,
+                       kp_cap);
 }
 
 void launch_finalize(hipStream_t st, const uint8_t* pyr, const uint8_t* blur, size_t pyr_stride, const LevelDesc* lv,
                      int nlevels, const uint32_t* okp, const int* ocnt, int okp_stride, const uint16_t* depth,
                      size_t depth_stride, int img_w, FrameCalib cal, orb_kp* kps, uint8_t* desc, float* kun, float* xyz,
-                     float* ur, int* nkp, int kp_cap, int nframes, hipEvent_t done) {
+                     float* ur, int* nkp, int kp_cap, int nframes, bool geometry) {
     dim3 g((kp_cap + FIN_KPB - 1) / FIN_KPB, nframes);
     // ODO_FIN_LDS: 0 the per-lane-gather k_finalize; 1 the staged kernel at 4
     // waves (16 keypoints, 42.5 KB LDS) per workgroup; 2 (default) at 2 waves
@@ -550,7 +543,7 @@ void launch_finalize(hipStream_t st, const uint8_t* pyr, const uint8_t* blur, si
 #endif
         hipLaunchKernelGGL(k_finalize_lds<2>, dim3((kp_cap + 7) / 8, nframes), dim3(128), 0, st, pyr, blur, pyr_stride,
                            lv, nlevels, okp, ocnt, okp_stride, kps, desc, nkp, kp_cap);
-    launch_kp_geometry(st, kps, nkp, depth, depth_stride, img_w, cal, kun, xyz, ur, kp_cap, nframes, done);
+    if (geometry) launch_kp_geometry(st, kps, nkp, depth, depth_stride, img_w, cal, kun, xyz, ur, kp_cap, nframes);
 }
 
 }  // namespace odo

@@ -13,7 +13,6 @@
 // pair stages; per-set events order the reuse (set s is rewritten only after
 // the pair stages of batch k-1 that read it have finished).
 #include <hip/hip_runtime.h>
-#include <hip/hip_ext.h>
 
 #include <cmath>
 #include <cstdlib>
@@ -168,11 +167,13 @@ struct odo_ctx {
     hipEvent_t ev_latch = nullptr;   // after the last queued k_latch (schedule 5)
     bool latch_rec = false;
     bool latched = false;  // this batch leaves the latch kernel out (see run_pairs)
-    // the batch's extraction-done event, when run_extract may complete it with
-    // its last kernel (hipExtLaunchKernel's stop event) instead of a marker
-    // packet after it (ODO_XDONE_EXT); xdone_set: it did
-    hipEvent_t xdone_ev = nullptr;
-    bool xdone_set = false;
+    // ODO_GEO_PAIR: this batch's geometry and roll are on its pair stream;
+    // ev_geo[set] follows the set's geometry kernel (the next batch's roll
+    // reads the last frame's kun / xyz / uR); host_call: a track_host
+    // batch (its depth reads must stay on the extraction stream)
+    bool geo_pair = false, host_call = false;
+    hipEvent_t ev_geo[NSETS] = {};
+    bool geo_rec[NSETS] = {};
     uint64_t batch_counter = 0;
     int W = 0, H = 0, maxb = 0, slots = 0, nlevels = 0;
     std::vector<LevelDesc> lv_h;
@@ -372,8 +373,11 @@ static inline int next_set(const odo_ctx* c) { return (c->seq_set + 1) % NSETS; 
 #ifndef ODO_WAIT_DEDUP
 #define ODO_WAIT_DEDUP 1
 #endif
-#ifndef ODO_XDONE_EXT
-#define ODO_XDONE_EXT 1
+#ifndef ODO_GEO_PAIR
+// schedule 5, device inputs: the keypoint geometry (undistort, depth) and the
+// slot-0 roll run at the head of the batch's pair stream instead of at the
+// end of the extraction stream, the step's critical path
+#define ODO_GEO_PAIR 0
 #endif
 // `st` waits until the PnP launches (and, async, the result copy) of the batch
 // that last used frame set `set` are done. Every wait is a barrier packet the
@@ -491,6 +495,7 @@ static void free_ctx(odo_ctx* c) {
         if (c->ev_raw[i]) hipEventDestroy(c->ev_raw[i]);
         if (c->ev_pyr[i]) hipEventDestroy(c->ev_pyr[i]);
         if (c->ev_blur[i]) hipEventDestroy(c->ev_blur[i]);
+        if (c->ev_geo[i]) hipEventDestroy(c->ev_geo[i]);
     }
     for (int i = 0; i < 2; i++) {
         if (c->ev_in_copied[i]) hipEventDestroy(c->ev_in_copied[i]);
@@ -1166,7 +1171,8 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
         ok = hipEventCreateWithFlags(&c->ev_xdone[i], evf) == hipSuccess &&
              hipEventCreateWithFlags(&c->ev_raw[i], evf) == hipSuccess &&
              hipEventCreateWithFlags(&c->ev_pyr[i], evf) == hipSuccess &&
-             hipEventCreateWithFlags(&c->ev_blur[i], evf) == hipSuccess;
+             hipEventCreateWithFlags(&c->ev_blur[i], evf) == hipSuccess &&
+             hipEventCreateWithFlags(&c->ev_geo[i], evf) == hipSuccess;
     if (!c->bstream) c->bstream = c->stream;
     if (ok) ok = hipEventCreateWithFlags(&c->ev_latch, evf) == hipSuccess;
     if (ok) ok = hipEventCreateWithFlags(&c->ev_depth_done, evf) == hipSuccess;
@@ -1460,8 +1466,7 @@ static int run_extract(odo_ctx* c, int set, const uint8_t* d_bgr, const uint16_t
                     c->okp_stride, d_depth, (size_t)c->W * c->H, c->W, c->cal, c->kps + (size_t)slot * c->kp_cap,
                     c->desc + (size_t)slot * c->kp_cap * 32, c->kun + (size_t)slot * c->kp_cap * 2,
                     c->xyz + (size_t)slot * c->kp_cap * 3, c->ur + (size_t)slot * c->kp_cap, c->nkp + slot, c->kp_cap,
-                    n, c->xdone_ev);
-    if (c->xdone_ev) c->xdone_set = true;
+                    n, !c->geo_pair);
     tmark(c, 5, st);
     HIPCHK(hipGetLastError());
     return ODO_OK;
@@ -1623,7 +1628,9 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
         if (!(ODO_WAIT_DEDUP && sb == s && c->pdone_rec[s]) && (e = wait_pnp_done(c, c->stream, sb))) return e;
     }
     tmark(c, 0, c->stream);
-    if (c->has_prev) {
+    c->geo_pair = ODO_GEO_PAIR && c->sched == 5 && c->knn_pair && !c->adaptive && !c->adaptive_orb && !c->timing &&
+                  !c->host_call && c->ev_geo[0];
+    if (c->has_prev && !c->geo_pair) {
         // the previous batch's last frame becomes slot 0 (Tracking::mLastFrame)
         const size_t src = fbase(c, c->seq_set) + c->seq_n, dst = fbase(c, s);
         launch_copy_frame(c->stream, c->kps + src * KC, c->desc + src * KC * 32, c->kun + src * KC * 2,
@@ -1631,12 +1638,12 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
                           c->desc + dst * KC * 32, c->kun + dst * KC * 2, c->xyz + dst * KC * 3, c->ur + dst * KC,
                           c->nkp + dst, c->kp_cap);
     }
-    // schedule 5: ev_xdone completes with the extraction's last kernel
-    c->xdone_ev = ODO_XDONE_EXT && c->sched == 5 && !c->timing ? c->ev_xdone[s] : nullptr;
-    c->xdone_set = false;
-    e = run_extract(c, s, d_bgr, d_depth, n, 1);
-    c->xdone_ev = nullptr;
-    if (e) return e;
+    // (Round 6 measured ev_xdone completed by the last extraction kernel,
+    // hipExtLaunchKernel's stop event, instead of a marker packet: with the
+    // runtime's worker-thread dispatch the pair stream's wait on it did not
+    // always hold (a batch's kNN-2 started before the previous batch's, seen
+    // in the step marks), and the step was no faster. Not kept.)
+    if ((e = run_extract(c, s, d_bgr, d_depth, n, 1))) return e;
     // the kNN-2 stream: the extraction stream, or the side stream (sched 3)
     hipStream_t ks = c->stream;
     if (c->sched == 3) {
@@ -1715,7 +1722,7 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
             c->cur_p = c->pstream;
         }
         if (c->pdone_rec[s] && (e = wait_pnp_done(c, c->cur_p, s))) return e;
-        if (!c->xdone_set) HIPCHK(hipEventRecord(c->ev_xdone[s], c->stream));
+        HIPCHK(hipEventRecord(c->ev_xdone[s], c->stream));
         launch_ransac_raw(c->cur_p, c->rscr[s], n, c->match_cap, c->mask_words, c->rcfg, (uint64_t)c->cfg.seed,
                           c->pair_counter, nullptr);
         HIPCHK(hipEventRecord(c->ev_raw[s], c->cur_p));
@@ -1731,6 +1738,25 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
     if (c->sched != 4 && c->sched != 5) c->cur_p = c->pstream;
     HIPCHK(hipStreamWaitEvent(c->cur_p, c->ev_xdone[s], 0));
     HIPCHK(hipStreamWaitEvent(c->cur_p, c->ev_raw[s], 0));
+    if (c->geo_pair) {
+        // the roll (the previous batch's last frame into slot 0, once that
+        // batch's geometry is done) and this batch's geometry, ahead of kNN-2
+        const size_t b = fbase(c, s);
+        if (c->has_prev) {
+            const size_t src = fbase(c, c->seq_set) + c->seq_n, dst = b;
+            if (c->geo_rec[c->seq_set]) HIPCHK(hipStreamWaitEvent(c->cur_p, c->ev_geo[c->seq_set], 0));
+            launch_copy_frame(c->cur_p, c->kps + src * KC, c->desc + src * KC * 32, c->kun + src * KC * 2,
+                              c->xyz + src * KC * 3, c->ur + src * KC, c->nkp + src, c->kps + dst * KC,
+                              c->desc + dst * KC * 32, c->kun + dst * KC * 2, c->xyz + dst * KC * 3, c->ur + dst * KC,
+                              c->nkp + dst, c->kp_cap);
+        }
+        launch_kp_geometry(c->cur_p, c->kps + (b + 1) * KC, c->nkp + b + 1, d_depth, (size_t)c->W * c->H, c->W, c->cal,
+                           c->kun + (b + 1) * KC * 2, c->xyz + (b + 1) * KC * 3, c->ur + (b + 1) * KC, c->kp_cap, n);
+        HIPCHK(hipEventRecord(c->ev_geo[s], c->cur_p));
+        c->geo_rec[s] = true;
+    } else {
+        c->geo_rec[s] = false;
+    }
     if (knn_pair && (e = knn_on(c->cur_p))) return e;
     c->valid_h.assign(n, 1);
     c->valid_h[0] = c->has_prev ? 1 : 0;
@@ -1821,8 +1847,10 @@ static int track_host(odo_ctx* c, const uint8_t* bgr, const uint16_t* depth, int
     int e = ODO_OK;
     if (hipStreamWaitEvent(c->stream, c->ev_in_copied[k], 0) != hipSuccess) e = fail(ODO_ERR_DEVICE, "hipStreamWaitEvent");
     const uint16_t* dd = sparse ? (const uint16_t*)dmap : c->depth_in[k];
+    c->host_call = true;  // the batch's depth reads stay on the extraction stream (ev_in_free, ev_depth_done)
     if (!e) e = async_res ? odo_track_batch_async(c, c->bgr_in[k], dd, n, async_res)
                           : odo_track_batch(c, c->bgr_in[k], dd, n, nullptr);
+    c->host_call = false;
     if (!e) {
         // everything that reads staging buffer k (and a sparse batch's depth
         // frames) is queued on the extraction stream

@@ -398,8 +398,50 @@ ODO_INLINE void hyp_cov_terms(const double T[12], const MahalConst& K, double Z[
     Z[4] = (T[10] * c22) * T[9];
     Z[5] = (T[10] * c22) * T[10];
 }
-ODO_INLINE double error_function2_mk(const float x1[3], const float x2[3], const double T[12], const MahalConst& K,
-                                     const double* Z = nullptr) {
+#ifndef EF_FAST
+// ErrorFunction2's three square roots and three reciprocals (error_function2_mk)
+// as the cores of LLVM's correctly rounded AMDGPU f64 sequences without their
+// range fix-ups, which are inactive on the ranges below (ef_sqrt / ef_rcp);
+// an evaluation with an operand outside them is redone with the IEEE
+// sequences, so the results are bit-identical
+#define EF_FAST 0
+#endif
+// sqrt: v_rsq_f64, then the Goldschmidt iteration and two corrections of
+// LLVM's lowering (its ldexp scaling only acts below 2^-767, its class test
+// only at 0 and +inf)
+template <bool FAST>
+ODO_INLINE double ef_sqrt(double x, bool& ok) {
+    if (!FAST) return sqrt(x);
+    ok = ok & (x >= 0x1p-767) & (x <= ODO_DBL_MAX);
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = y * 0.5;
+    const double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    double d = __builtin_fma(-g, g, x);
+    g = __builtin_fma(d, h, g);
+    d = __builtin_fma(-g, g, x);
+    return __builtin_fma(d, h, g);
+}
+// 1 / b: v_rcp_f64 and the Newton steps of LLVM's f64 division with the
+// numerator 1.0 (v_div_scale leaves 1.0 and b unscaled, v_div_fmas is a plain
+// fma and v_div_fixup returns its input for 2^-500 <= |b| <= 2^500)
+template <bool FAST>
+ODO_INLINE double ef_rcp(double b, bool& ok) {
+    if (!FAST) return 1.0 / b;
+    const double ab = __builtin_fabs(b);
+    ok = ok & (ab >= 0x1p-500) & (ab <= 0x1p500);
+    double y = __builtin_amdgcn_rcp(b);
+    double e = __builtin_fma(-b, y, 1.0);
+    y = __builtin_fma(y, e, y);
+    e = __builtin_fma(-b, y, 1.0);
+    y = __builtin_fma(y, e, y);
+    e = __builtin_fma(-b, y, 1.0);
+    return __builtin_fma(e, y, y);
+}
+template <bool FAST>
+ODO_INLINE double error_function2_mk_t(const float x1[3], const float x2[3], const double T[12], const MahalConst& K,
+                                       const double* Z, bool& ok) {
     if (__builtin_isnan(x1[2]) || __builtin_isnan(x2[2])) return ODO_DBL_MAX;
     const double a0 = x1[0], a1 = x1[1], a2 = x1[2];
     const double mu0 = x2[0], mu1 = x2[1], mu2 = x2[2];
@@ -440,27 +482,27 @@ ODO_INLINE double error_function2_mk(const float x1[3], const float x2[3], const
     {
         double x = L00;
         if (x > 0) {
-            L00 = x = sqrt(x);
-            i00 = 1.0 / x;
+            L00 = x = ef_sqrt<FAST>(x, ok);
+            i00 = ef_rcp<FAST>(x, ok);
             L10 = div_mk(L10, x, i00);
             L20 = div_mk(L20, x, i00);
             x = L11 - L10 * L10;
             if (x > 0) {
-                L11 = x = sqrt(x);
-                i11 = 1.0 / x;
+                L11 = x = ef_sqrt<FAST>(x, ok);
+                i11 = ef_rcp<FAST>(x, ok);
                 L21 -= L20 * L10;
                 L21 = div_mk(L21, x, i11);
                 x = L22 - (L20 * L20 + L21 * L21);
-                if (x > 0) L22 = sqrt(x);
+                if (x > 0) L22 = ef_sqrt<FAST>(x, ok);
             } else {
-                i11 = 1.0 / L11;
+                i11 = ef_rcp<FAST>(L11, ok);
             }
         } else {
-            i00 = 1.0 / L00;
-            i11 = 1.0 / L11;
+            i00 = ef_rcp<FAST>(L00, ok);
+            i11 = ef_rcp<FAST>(L11, ok);
         }
     }
-    i22 = 1.0 / L22;
+    i22 = ef_rcp<FAST>(L22, ok);
     double y0 = div_mk(d0, L00, i00);
     double y1 = div_mk(d1 - L10 * y0, L11, i11);
     double y2 = div_mk(d2 - (L20 * y0 + L21 * y1), L22, i22);
@@ -469,6 +511,14 @@ ODO_INLINE double error_function2_mk(const float x1[3], const float x2[3], const
     double z0 = div_mk(y0 - (L10 * z1 + L20 * z2), L00, i00);
     double r = sum3d(d0 * z0, d1 * z1, d2 * z2);
     if (!(r >= 0.0)) return ODO_DBL_MAX;
+    return r;
+}
+
+ODO_INLINE double error_function2_mk(const float x1[3], const float x2[3], const double T[12], const MahalConst& K,
+                                     const double* Z = nullptr) {
+    bool ok = true;
+    double r = error_function2_mk_t<EF_FAST != 0>(x1, x2, T, K, Z, ok);
+    if (EF_FAST && __builtin_expect(!ok, 0)) r = error_function2_mk_t<false>(x1, x2, T, K, Z, ok);
     return r;
 }
 

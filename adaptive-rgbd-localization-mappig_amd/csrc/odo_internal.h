@@ -205,8 +205,7 @@ struct RansacCfg {
 void upload_extract_constants();
 void upload_finalize_constants();
 void launch_kp_geometry(hipStream_t st, const orb_kp* kps, const int* nkp, const uint16_t* depth, size_t depth_stride,
-                        int img_w, FrameCalib cal, float* kun, float* xyz, float* ur, int kp_cap, int nframes,
-                        hipEvent_t done = nullptr);
+                        int img_w, FrameCalib cal, float* kun, float* xyz, float* ur, int kp_cap, int nframes);
 void launch_gray(hipStream_t st, const uint8_t* bgr, uint8_t* pyr, int w, int h, int pitch, size_t in_stride,
                  size_t pyr_stride, int nframes);
 size_t resize_lds_bytes(int spitch, int dw, int max_src_rows);
@@ -236,7 +235,7 @@ void launch_blur(hipStream_t st, const uint8_t* pyr, uint8_t* blur, size_t pyr_s
 void launch_finalize(hipStream_t st, const uint8_t* pyr, const uint8_t* blur, size_t pyr_stride, const LevelDesc* lv,
                      int nlevels, const uint32_t* okp, const int* ocnt, int okp_stride, const uint16_t* depth,
                      size_t depth_stride, int img_w, FrameCalib cal, orb_kp* kps, uint8_t* desc, float* kun, float* xyz,
-                     float* ur, int* nkp, int kp_cap, int nframes, hipEvent_t done = nullptr);
+                     float* ur, int* nkp, int kp_cap, int nframes, bool geometry = true);
 void launch_pair_valid(hipStream_t st, int* pv, int n, int first_valid);
 void launch_copy_frame(hipStream_t st, const orb_kp* kps_s, const uint8_t* desc_s, const float* kun_s,
                        const float* xyz_s, const float* ur_s, const int* n_s, orb_kp* kps_d, uint8_t* desc_d,

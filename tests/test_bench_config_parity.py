@@ -63,23 +63,44 @@ def _oracle_calib(cfg):
     return O.Calib(k.fx, k.fy, k.cx, k.cy, k.k1, k.k2, k.p1, k.p2, k.k3, k.depth_factor, k.mbf, k.th_depth)
 
 
+def _pos(c, b, i):
+    """Loop position of frame i of batch b: batch b starts b (B + 1) frames
+    into the cycled loop, so no two of the BATCHES batches hold the same frames
+    (a batch reading a frame set's data from before its own extraction -- a
+    broken cross-stream dependency -- would read other frames), and pair 0 of
+    batch b pairs positions b (B + 1) - 2 and b (B + 1)."""
+    return (b * (c["B"] + 1) + i) % c["L"]
+
+
 def _run_gpu(pkg, c, bgr, dep, forms=None):
-    """bench.py's timed loop: device-resident batch, BATCHES back-to-back calls.
+    """bench.py's timed loop: device-resident batches, BATCHES back-to-back
+    calls without a host sync (batch b's frames at _pos(c, b, .)).
     forms: odo_kernel_forms fields (bit-identical kernel alternatives)."""
     import torch
     B, L = c["B"], c["L"]
-    idx = np.arange(B) % L
-    d_bgr = torch.from_numpy(np.ascontiguousarray(bgr[idx])).to("cuda")
-    d_dep = torch.from_numpy(np.ascontiguousarray(dep[idx]).view(np.int16)).to("cuda")
+    idx = torch.from_numpy(np.arange(BATCHES * (B + 1)) % L).to("cuda")
+    d_bgr = torch.from_numpy(np.ascontiguousarray(bgr)).to("cuda")[idx].contiguous()
+    d_dep = torch.from_numpy(np.ascontiguousarray(dep).view(np.int16)).to("cuda")[idx].contiguous()
+    fb, fd = d_bgr[0].numel(), 2 * d_dep[0].numel()  # bytes per frame
     cfg = pkg.default_config(c["w"], c["h"], B, nfeatures=c["nf"], iterations=c["iters"], seed=c["seed"],
                              calib=c["calib"], forms=forms)
     odo = pkg.Odometry(cfg)
     torch.cuda.synchronize()
-    for _ in range(BATCHES - 1):
-        odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=False)
-    res = odo.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, want_results=True)
+    for b in range(BATCHES):
+        o = b * (B + 1)
+        last = b == BATCHES - 1
+        res = odo.track_batch(d_bgr.data_ptr() + o * fb, d_dep.data_ptr() + o * fd, B, want_results=last)
     odo.synchronize()
+    del d_bgr, d_dep
     return odo, cfg, res
+
+
+def _pair_frames(c, frames, p):
+    """(F1, F2) of pair p of the last batch."""
+    b = BATCHES - 1
+    f2 = frames[_pos(c, b, p)]
+    f1 = frames[_pos(c, b, p - 1)] if p > 0 else frames[(b * (c["B"] + 1) - 2) % c["L"]]
+    return f1, f2
 
 
 def _oracle_run(pkg, c, cfg, bgr, dep):
@@ -98,8 +119,8 @@ def _oracle_run(pkg, c, cfg, bgr, dep):
     g0 = (BATCHES - 1) * B
 
     def pair(p):
-        g = g0 + p
-        return O.track_pair(frames[(g - 1) % L], frames[g % L], cal, rp, pkg.pair_seed(cfg.seed, g), latch)
+        f1, f2 = _pair_frames(c, frames, p)
+        return O.track_pair(f1, f2, cal, rp, pkg.pair_seed(cfg.seed, g0 + p), latch)
 
     with ThreadPoolExecutor(THREADS) as ex:
         pairs = list(ex.map(pair, range(B)))
@@ -121,7 +142,7 @@ def _compare(name, c, odo, res, oracle, full=True):
     g0 = (BATCHES - 1) * B
     if full:
         for i in range(B):
-            got, ref = odo.frame(i), frames[(g0 + i) % L]
+            got, ref = odo.frame(i), frames[_pos(c, BATCHES - 1, i)]
             assert len(got["kps"]) == len(ref["kps"]), f"{name} frame {i}: N"
             assert np.array_equal(got["kps"], ref["kps"]), f"{name} frame {i}: keypoints"
             assert np.array_equal(got["desc"], ref["desc"]), f"{name} frame {i}: descriptors"
@@ -146,7 +167,7 @@ def _compare(name, c, odo, res, oracle, full=True):
         Tref = np.array(r.Tcw, np.float32).reshape(4, 4)
         dT = np.abs(res[p]["Tcw"].reshape(4, 4) - Tref).max()
         assert dT < 1e-4, f"{tag}: PnP pose differs by {dT}"
-        f1, f2 = frames[(g0 + p - 1) % L], frames[(g0 + p) % L]
+        f1, f2 = _pair_frames(c, frames, p)
         n2 = len(f2["kps"])
         O.check_pnp_flags(g["pnp_inliers"][:n2], mask, f1, f2, g["f2_src"][:n2], Tref, cal, tag)
     assert odo.latch == latch, f"{name}: latch {odo.latch} vs {latch}"
