@@ -1539,16 +1539,28 @@ __global__ void __launch_bounds__(256) k_blur_rows(const uint8_t* __restrict__ p
 struct PyrLevels {
     int rx_off[16], ry_off[16];
 };
+#ifndef PYR_PARTS
+#define PYR_PARTS 1  // workgroups per frame (PyrSplit; the host falls back to 1 where a split does not fit)
+#endif
+// k_pyramid's split of a frame over `parts` workgroups (pyramid_split_plan):
+// part p builds rows [lo, hi) of level l and blurs its strip chunks [ca, cb)
+// and 6-row edge chunks [ea, eb)
+struct PyrSplit {
+    int parts;
+    int lo[2][16], hi[2][16], ca[2][16], cb[2][16], ea[2][16], eb[2][16];
+};
 // the 7x7 blur of level l of frame f by the whole workgroup (PYR_TH threads:
 // 64 strip groups of 16 lanes, then the edge lanes), read from srcL (the
 // level's row 0)
 ODO_INLINE void pyr_blur_level(const uint8_t* srcL, uint8_t* __restrict__ blur, size_t pyr_stride,
                                const LevelDesc* __restrict__ lv, const BlurRows& S, int nlevels, int f, int l,
-                               const LevelDesc& L, int t) {
+                               const LevelDesc& L, int t, int ca, int cb, int ea, int eb) {
+    // strip chunks [ca, cb) and edge chunks [ea, eb) of the level: this
+    // workgroup's part of the frame (PyrSplit)
     const uint32_t none[3] = {0, 0, 0};
-    const int items = S.nch[l] * S.nst[l];
+    const int items = cb * S.nst[l];
     const int g = t >> 4;
-    for (int it = g; it < items; it += PYR_TH / 16) {
+    for (int it = ca * S.nst[l] + g; it < items; it += PYR_TH / 16) {
         const int chunk = it / S.nst[l], strip = it - chunk * S.nst[l];
         const int q = 1 + strip * 16 + (t & 15);
         const bool store = q <= S.nq[l];
@@ -1560,7 +1572,7 @@ ODO_INLINE void pyr_blur_level(const uint8_t* srcL, uint8_t* __restrict__ blur, 
         blur_walk<false, BR_R>(s0, dp, (size_t)L.pitch, L.h, y0, top, bottom, store, 0, 0, 0, none, none);
     }
     const int ne = (S.ebase[l + 1] - S.ebase[l]) / ((L.h + BR_RE - 1) / BR_RE);  // edge quads per chunk
-    for (int k = S.ebase[l] + t; k < S.ebase[l + 1]; k += PYR_TH)
+    for (int k = S.ebase[l] + ea * ne + t; k < S.ebase[l] + eb * ne; k += PYR_TH)
         blur_edge_lane(srcL, blur, pyr_stride, lv, S, nlevels, f, k);
 }
 // level D's rows [ylo, yhi) from level S (whose row 0 is srcS), thread t's quad
@@ -1683,27 +1695,34 @@ __global__ void __launch_bounds__(PYR_TH) PYR_ATTR k_pyramid(const uint8_t* __re
                                                     size_t in_stride, size_t pyr_stride,
                                                     const LevelDesc* __restrict__ lv, const ResizeX* __restrict__ xt,
                                                     const ResizeY* __restrict__ yt, PyrLevels PL, int nlevels,
-                                                    uint8_t* __restrict__ blur, BlurRows BR) {
+                                                    uint8_t* __restrict__ blur, BlurRows BR, PyrSplit SP) {
     EXTRACT_PRIO();
-    const int f = blockIdx.x;
+    // SP.parts == 2: two workgroups per frame, the top and the bottom part;
+    // each builds every row it reads itself (rows both build are the same
+    // bytes), so the parts never wait for each other
+    const int part = SP.parts == 2 ? (int)(blockIdx.x & 1) : 0;
+    const int f = SP.parts == 2 ? (int)(blockIdx.x >> 1) : (int)blockIdx.x;
     const int t = threadIdx.x;
     uint8_t* base = pyr + (size_t)f * pyr_stride;
     if (bgr) {
         const LevelDesc L0 = lv[0];
-        pyr_gray_rows(bgr + (size_t)f * in_stride, base + L0.off, L0.w, L0.pitch, 0, L0.h, t);
+        pyr_gray_rows(bgr + (size_t)f * in_stride, base + L0.off, L0.w, L0.pitch, SP.lo[part][0], SP.hi[part][0], t);
     }
     for (int l = 1; l < nlevels; l++) {
-        __syncthreads();  // level l - 1 is complete
+        __syncthreads();  // level l - 1 is complete (this part's rows)
         const LevelDesc S = lv[l - 1], D = lv[l];
         if (BLUR)
-            pyr_blur_level(base + S.off, blur, pyr_stride, lv, BR, nlevels, f, l - 1, S, t);
-        pyr_resize_rows(base + S.off, base + D.off, S, D, xt + PL.rx_off[l], yt + PL.ry_off[l], t, 0, D.h);
+            pyr_blur_level(base + S.off, blur, pyr_stride, lv, BR, nlevels, f, l - 1, S, t, SP.ca[part][l - 1],
+                           SP.cb[part][l - 1], SP.ea[part][l - 1], SP.eb[part][l - 1]);
+        pyr_resize_rows(base + S.off, base + D.off, S, D, xt + PL.rx_off[l], yt + PL.ry_off[l], t, SP.lo[part][l],
+                        SP.hi[part][l]);
     }
     if (BLUR) {
         __syncthreads();  // the last level is complete
         const int ll = nlevels - 1;
         const LevelDesc L = lv[ll];
-        pyr_blur_level(base + L.off, blur, pyr_stride, lv, BR, nlevels, f, ll, L, t);
+        pyr_blur_level(base + L.off, blur, pyr_stride, lv, BR, nlevels, f, ll, L, t, SP.ca[part][ll], SP.cb[part][ll],
+                       SP.ea[part][ll], SP.eb[part][ll]);
     }
     __syncthreads();
 }
@@ -1746,19 +1765,72 @@ bool pyramid_blur_fusable(const LevelDesc* lv_host, int nlevels) {
     BlurRows R;
     return blur_rows_plan(lv_host, nlevels, R);
 }
-void launch_pyramid(hipStream_t st, const uint8_t* bgr, uint8_t* pyr, size_t in_stride, size_t pyr_stride,
-                    const LevelDesc* lv, const ResizeX* rx, const ResizeY* ry, const int* rx_off, const int* ry_off,
-                    int nlevels, int nframes, uint8_t* blur, const LevelDesc* lv_host) {
-    PyrLevels PL{};
-    for (int l = 0; l < nlevels && l < 16; l++) PL.rx_off[l] = rx_off[l], PL.ry_off[l] = ry_off[l];
-    BlurRows BR{};
-    if (blur && blur_rows_plan(lv_host, nlevels, BR)) {
-        hipLaunchKernelGGL(k_pyramid<true>, dim3(nframes), dim3(PYR_TH), 0, st, bgr, pyr, in_stride, pyr_stride, lv,
-                           rx, ry, PL, nlevels, blur, BR);
+// The part ranges of k_pyramid (PyrSplit). parts == 1: everything. parts == 2:
+// level l's blur rows split at s_l (a multiple of BR_R = 30, so the 30-row
+// strip chunks and 6-row edge chunks split with it; a level under 60 rows is
+// blurred by the top part alone); each part builds the rows its blur reads
+// (3-row halo) and the source rows of the next level's rows it builds, from
+// the top level down. Every row keeps its one arithmetic, so rows both parts
+// build are the same bytes. ry_h: the host copy of the vertical resize table.
+static void pyramid_split_plan(const LevelDesc* lv_host, const ResizeY* ry_h, const int* ry_off, int nlevels,
+                               int parts, PyrSplit& S) {
+    S = PyrSplit{};
+    S.parts = parts;
+    for (int l = 0; l < nlevels && l < 16; l++) {
+        const int h = lv_host[l].h, nch = (h + BR_R - 1) / BR_R, nch6 = (h + BR_RE - 1) / BR_RE;
+        for (int p = 0; p < 2; p++) {
+            S.lo[p][l] = 0, S.hi[p][l] = h;
+            S.ca[p][l] = 0, S.cb[p][l] = nch, S.ea[p][l] = 0, S.eb[p][l] = nch6;
+        }
+    }
+    if (parts != 2 || nlevels > 16 || !ry_h) {
+        S.parts = 1;
         return;
     }
-    hipLaunchKernelGGL(k_pyramid<false>, dim3(nframes), dim3(PYR_TH), 0, st, bgr, pyr, in_stride, pyr_stride, lv, rx,
-                       ry, PL, nlevels, (uint8_t*)nullptr, BR);
+    int sp[16];
+    for (int l = 0; l < nlevels; l++) {
+        const int h = lv_host[l].h;
+        int s = ((h / 2 + BR_R / 2) / BR_R) * BR_R;  // the multiple of 30 nearest h / 2
+        if (h < 2 * BR_R) s = h;                       // too small to split: the top part blurs it all
+        s = std::min(s, h < 2 * BR_R ? h : h - BR_R);
+        sp[l] = s;
+        const int nch = (h + BR_R - 1) / BR_R, nch6 = (h + BR_RE - 1) / BR_RE;
+        S.ca[0][l] = 0, S.cb[0][l] = s == h ? nch : s / BR_R;
+        S.ca[1][l] = S.cb[0][l], S.cb[1][l] = nch;
+        S.ea[0][l] = 0, S.eb[0][l] = s == h ? nch6 : s / BR_RE;
+        S.ea[1][l] = S.eb[0][l], S.eb[1][l] = nch6;
+    }
+    // rows built per part, from the top level down
+    for (int l = nlevels - 1; l >= 0; l--) {
+        const int h = lv_host[l].h;
+        int thi = std::min(h, sp[l] + 3), blo = std::max(0, sp[l] - 3);
+        if (sp[l] == h) blo = h;  // the bottom part blurs none of this level
+        if (l + 1 < nlevels) {
+            const ResizeY* Y = ry_h + ry_off[l + 1];
+            if (S.hi[0][l + 1] > 0) thi = std::max(thi, Y[S.hi[0][l + 1] - 1].sy1 + 1);
+            if (S.lo[1][l + 1] < lv_host[l + 1].h) blo = std::min(blo, Y[S.lo[1][l + 1]].sy0);
+        }
+        S.lo[0][l] = 0, S.hi[0][l] = std::min(h, thi);
+        S.lo[1][l] = std::max(0, blo), S.hi[1][l] = h;
+        if (S.lo[1][l] >= h) S.lo[1][l] = h;  // nothing to build
+    }
+}
+void launch_pyramid(hipStream_t st, const uint8_t* bgr, uint8_t* pyr, size_t in_stride, size_t pyr_stride,
+                    const LevelDesc* lv, const ResizeX* rx, const ResizeY* ry, const int* rx_off, const int* ry_off,
+                    int nlevels, int nframes, uint8_t* blur, const LevelDesc* lv_host, const ResizeY* ry_h) {
+    PyrLevels PL{};
+    for (int l = 0; l < nlevels && l < 16; l++) PL.rx_off[l] = rx_off[l], PL.ry_off[l] = ry_off[l];
+    PyrSplit SP;
+    pyramid_split_plan(lv_host, ry_h, ry_off, nlevels, PYR_PARTS, SP);
+    const dim3 g(nframes * SP.parts);
+    BlurRows BR{};
+    if (blur && blur_rows_plan(lv_host, nlevels, BR)) {
+        hipLaunchKernelGGL(k_pyramid<true>, g, dim3(PYR_TH), 0, st, bgr, pyr, in_stride, pyr_stride, lv, rx, ry, PL,
+                           nlevels, blur, BR, SP);
+        return;
+    }
+    hipLaunchKernelGGL(k_pyramid<false>, g, dim3(PYR_TH), 0, st, bgr, pyr, in_stride, pyr_stride, lv, rx, ry, PL,
+                       nlevels, (uint8_t*)nullptr, BR, SP);
 }
 bool pyramid_fusable(const LevelDesc* lv_host, const ResizeX* rx, const int* rx_off, int nlevels) {
     if (nlevels > 16) return false;

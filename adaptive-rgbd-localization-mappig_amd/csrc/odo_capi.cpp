@@ -190,6 +190,7 @@ struct odo_ctx {
     CellDesc* cells = nullptr;
     ResizeX* rx = nullptr;
     ResizeY* ry = nullptr;
+    std::vector<ResizeY> ry_h;  // host copy (k_pyramid's split plan)
     int ncells = 0, cell_cap = 0, kp_cap = 0, okp_stride = 0, node_cap = 0, match_cap = 0, mask_words = 0;
     int max_blur_tiles = 0;
     int fast_roi = 0;  // largest FAST cell ROI side
@@ -919,6 +920,7 @@ static int build_geometry(odo_ctx* c) {
         HIPCHK(hipMemcpy(c->fsegs, c->fsegs_h.data(), c->fsegs_h.size() * sizeof(FastSeg), hipMemcpyHostToDevice));
     if (!rx.empty()) HIPCHK(hipMemcpy(c->rx, rx.data(), rx.size() * sizeof(ResizeX), hipMemcpyHostToDevice));
     if (!ry.empty()) HIPCHK(hipMemcpy(c->ry, ry.data(), ry.size() * sizeof(ResizeY), hipMemcpyHostToDevice));
+    c->ry_h = ry;
     return ODO_OK;
 }
 
@@ -1332,7 +1334,8 @@ static bool build_pyramid(odo_ctx* c, hipStream_t st, const uint8_t* d_bgr, uint
             d_bgr = nullptr;
         }
         launch_pyramid(st, d_bgr, pyr, (size_t)c->W * c->H * 3, P, c->lv, c->rx, c->ry, c->rx_off.data(),
-                       c->ry_off.data(), c->nlevels, n, blur, c->lv_h.data());
+                       c->ry_off.data(), c->nlevels, n, blur, c->lv_h.data(),
+                       c->ry_h.data());
         return blur != nullptr;
     }
     if (d_bgr) launch_gray(st, d_bgr, pyr, c->W, c->H, c->lv_h[0].pitch, (size_t)c->W * c->H * 3, P, n);

@@ -214,7 +214,8 @@ size_t resize_lds_bytes(int spitch, int dw, int max_src_rows);
 // assumptions (<= 16 levels, <= 4096 px wide, each quad's taps inside 8 bytes)
 void launch_pyramid(hipStream_t st, const uint8_t* bgr, uint8_t* pyr, size_t in_stride, size_t pyr_stride,
                     const LevelDesc* lv, const ResizeX* rx, const ResizeY* ry, const int* rx_off, const int* ry_off,
-                    int nlevels, int nframes, uint8_t* blur, const LevelDesc* lv_host);
+                    int nlevels, int nframes, uint8_t* blur, const LevelDesc* lv_host,
+                    const ResizeY* ry_h);
 // blur: the blurred pyramid is written by the same launch (null: not);
 // pyramid_blur_fusable: every level is large enough for the strip walks
 bool pyramid_blur_fusable(const LevelDesc* lv_host, int nlevels);
