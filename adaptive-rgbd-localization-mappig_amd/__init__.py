@@ -33,7 +33,7 @@ def default_config(width=640, height=480, max_batch=1, nfeatures=1000, iteration
     detector of detectoradjuster.cpp:29). forms: odo_kernel_forms fields
     (knn = KNN_FORM_FP4 / KNN_FORM_VALU, knn_split, ransac_lanes_min_open,
     pyramid = PYRAMID_FORM_AUTO / PYRAMID_FORM_FUSED / PYRAMID_FORM_CHAIN /
-    PYRAMID_FORM_FUSED_NOBLUR)."""
+    PYRAMID_FORM_FUSED_NOBLUR, ransac_first_hyps)."""
     cfg = Config()
     load().odo_default_config(ptr(cfg), width, height, max_batch)
     cfg.detector = detector

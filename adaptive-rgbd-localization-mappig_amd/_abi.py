@@ -70,7 +70,7 @@ class PairResult(C.Structure):
 class KernelForms(C.Structure):
     """odo_kernel_forms (include/odo.h): bit-identical kernel alternatives."""
     _fields_ = [("knn", C.c_int32), ("knn_split", C.c_int32), ("ransac_lanes_min_open", C.c_int32),
-                ("pyramid", C.c_int32)]
+                ("pyramid", C.c_int32), ("ransac_first_hyps", C.c_int32)]
 
 
 class Config(C.Structure):

@@ -2126,11 +2126,13 @@ void launch_ransac(hipStream_t st, const void* good, const int* n_good, const in
     // not compete with the long ones. part 1 = prep, first launch and the
     // finished pairs' outputs (phase[] marks them); part 2 = the rest; part 0
     // = both.
-    // ODO_EV_H0 (tuning): hypotheses of the first launch (default EV_H0)
-    static const int h0k = [] {
+    // hypotheses of the first launch: odo_kernel_forms.ransac_first_hyps, else
+    // ODO_EV_H0 (tuning), else EV_H0
+    static const int h0env = [] {
         const char* e = odo_knob("ODO_EV_H0");
         return e ? std::max(1, atoi(e)) : EV_H0;
     }();
+    const int h0k = cfg.first_hyps > 0 ? cfg.first_hyps : h0env;
     // a lone pair (the per-stage odo_ransac, a one-frame batch) starts every
     // hypothesis at once: the device is otherwise idle, and the visited
     // hypotheses beyond the first row no longer wait for the first launch

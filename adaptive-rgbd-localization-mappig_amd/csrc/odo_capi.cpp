@@ -377,8 +377,9 @@ static inline int next_set(const odo_ctx* c) { return (c->seq_set + 1) % NSETS; 
 #ifndef ODO_GEO_PAIR
 // schedule 5, device inputs: the keypoint geometry (undistort, depth) and the
 // slot-0 roll run at the head of the batch's pair stream instead of at the
-// end of the extraction stream, the step's critical path
-#define ODO_GEO_PAIR 0
+// end of the extraction stream, the step's critical path (round 6: 152.0-152.6
+// vs 150.9-151.3 k frames/s, three alternations on one box, profiles/r06_d)
+#define ODO_GEO_PAIR 1
 #endif
 // `st` waits until the PnP launches (and, async, the result copy) of the batch
 // that last used frame set `set` are done. Every wait is a barrier packet the
@@ -1088,6 +1089,11 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
         delete c;
         return nullptr;
     }
+    if (cfg->forms.ransac_first_hyps < 0 || cfg->forms.ransac_first_hyps > 64) {
+        fail(ODO_ERR_ARG, "ransac_first_hyps: 0 (default) or 1..64");
+        delete c;
+        return nullptr;
+    }
     if (cfg->detector != ODO_DETECTOR_ORB_SLAM2 && cfg->detector != ODO_DETECTOR_ADAPTIVE_FAST &&
         cfg->detector != ODO_DETECTOR_ADAPTIVE_ORB) {
         fail(ODO_ERR_ARG, "unsupported detector");  // extractor.cpp:26-27 terminates here
@@ -1195,7 +1201,7 @@ odo_ctx* odo_create(const odo_config* cfg, int device) {
     const double rsx = 3 * tan(cam_angle_x / 640.0), rsy = 3 * tan(cam_angle_y / 480.0);
     c->rcfg = RansacCfg{cfg->ransac.iterations, cfg->ransac.min_inlier_th, cfg->ransac.max_mahalanobis,
                         cfg->ransac.sample_size, cfg->ransac.check_depth, rsx * rsx, rsy * rsy, 0,
-                        cfg->forms.ransac_lanes_min_open};
+                        cfg->forms.ransac_lanes_min_open, 0, cfg->forms.ransac_first_hyps};
     if (build_geometry(c) != ODO_OK || alloc_buffers(c) != ODO_OK) {
         free_ctx(c);
         return nullptr;
@@ -1631,10 +1637,16 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
         if (!(ODO_WAIT_DEDUP && sb == s && c->pdone_rec[s]) && (e = wait_pnp_done(c, c->stream, sb))) return e;
     }
     tmark(c, 0, c->stream);
-    c->geo_pair = ODO_GEO_PAIR && c->sched == 5 && c->knn_pair && !c->adaptive && !c->adaptive_orb && !c->timing &&
-                  !c->host_call && c->ev_geo[0];
-    if (c->has_prev && !c->geo_pair) {
-        // the previous batch's last frame becomes slot 0 (Tracking::mLastFrame)
+    // (the next batch's roll reads this set's last frame on its pair stream,
+    // before its PnP: the batch that reuses this set waits for that PnP
+    // through PYR_WAIT, which therefore has to lie in [1, NSETS - 1])
+    const bool geo_pair = ODO_GEO_PAIR && c->sched == 5 && c->knn_pair && !c->adaptive && !c->adaptive_orb &&
+                          !c->timing && !c->host_call && c->ev_geo[0] && c->pyr_wait >= 1 &&
+                          c->pyr_wait <= NSETS - 1;
+    if (c->has_prev && !geo_pair) {
+        // the previous batch's last frame becomes slot 0 (Tracking::mLastFrame);
+        // its geometry ran on that batch's pair stream when it took that path
+        if (c->geo_rec[c->seq_set]) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_geo[c->seq_set], 0));
         const size_t src = fbase(c, c->seq_set) + c->seq_n, dst = fbase(c, s);
         launch_copy_frame(c->stream, c->kps + src * KC, c->desc + src * KC * 32, c->kun + src * KC * 2,
                           c->xyz + src * KC * 3, c->ur + src * KC, c->nkp + src, c->kps + dst * KC,
@@ -1646,7 +1658,10 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
     // runtime's worker-thread dispatch the pair stream's wait on it did not
     // always hold (a batch's kNN-2 started before the previous batch's, seen
     // in the step marks), and the step was no faster. Not kept.)
-    if ((e = run_extract(c, s, d_bgr, d_depth, n, 1))) return e;
+    c->geo_pair = geo_pair;  // run_extract leaves the geometry out (only for this call)
+    e = run_extract(c, s, d_bgr, d_depth, n, 1);
+    c->geo_pair = false;
+    if (e) return e;
     // the kNN-2 stream: the extraction stream, or the side stream (sched 3)
     hipStream_t ks = c->stream;
     if (c->sched == 3) {
@@ -1741,7 +1756,7 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
     if (c->sched != 4 && c->sched != 5) c->cur_p = c->pstream;
     HIPCHK(hipStreamWaitEvent(c->cur_p, c->ev_xdone[s], 0));
     HIPCHK(hipStreamWaitEvent(c->cur_p, c->ev_raw[s], 0));
-    if (c->geo_pair) {
+    if (geo_pair) {
         // the roll (the previous batch's last frame into slot 0, once that
         // batch's geometry is done) and this batch's geometry, ahead of kNN-2
         const size_t b = fbase(c, s);

@@ -518,7 +518,7 @@ ODO_INLINE double error_function2_mk(const float x1[3], const float x2[3], const
                                      const double* Z = nullptr) {
     bool ok = true;
     double r = error_function2_mk_t<EF_FAST != 0>(x1, x2, T, K, Z, ok);
-    if (EF_FAST && __builtin_expect(!ok, 0)) r = error_function2_mk_t<false>(x1, x2, T, K, Z, ok);
+    if (EF_FAST == 1 && __builtin_expect(!ok, 0)) r = error_function2_mk_t<false>(x1, x2, T, K, Z, ok);
     return r;
 }
 

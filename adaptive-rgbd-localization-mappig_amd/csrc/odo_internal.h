@@ -199,6 +199,7 @@ struct RansacCfg {
     int h0;     // hypotheses of the first eval launch ([0, h0)); set by launch_ransac
     int lanes_min_open;  // odo_kernel_forms.ransac_lanes_min_open (0 = default)
     int fold_wave;       // ordered fold by the whole wave (a lone pair); set by launch_ransac
+    int first_hyps;      // odo_kernel_forms.ransac_first_hyps (0 = EV_H0)
 };
 
 // ---- launch wrappers (defined next to their kernels)

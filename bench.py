@@ -753,6 +753,8 @@ def main():
     ap.add_argument("--workload", choices=["default", "hard"], default="default",
                     help="main leg's sequence: the cfg2 proxy or the hard variant (synth hard=True)")
     ap.add_argument("--no-kernel-timing", action="store_true", help="no events around the kNN-2 launches")
+    ap.add_argument("--no-direct-dispatch-leg", action="store_true",
+                    help="skip the headline leg re-run with AMD_DIRECT_DISPATCH=1 (child process)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", choices=["track", "hyp", "latency", "pnpransac", "gicp"], default="track",
                     help="track: the frames/s metric; hyp: SURVEY 8(e) hypotheses mode latency (cfg3, H=4096); "
@@ -887,6 +889,24 @@ def run_latency(args, W, H, nframes):
     rec = json.loads(out.strip().splitlines()[-1])
     rec["amd_direct_dispatch"] = env["AMD_DIRECT_DISPATCH"]
     return rec
+
+
+def run_direct_dispatch(args):
+    """The headline leg again in a child process with the HIP runtime's
+    default direct dispatch (AMD_DIRECT_DISPATCH=1: the calling thread writes
+    the packets), which is what a caller gets without setting anything; the
+    headline runs with the worker-thread dispatch (DESIGN §4 Pipelining)."""
+    import subprocess
+    env = dict(os.environ)
+    env["AMD_DIRECT_DISPATCH"] = "1"
+    cmd = [sys.executable, os.path.abspath(__file__), "--steps", str(args.steps), "--warmup", str(args.warmup),
+           "--batch", str(args.batch), "--no-cpu-baseline", "--host-steps", "0", "--hard-steps", "0",
+           "--latency-frames", "0", "--no-direct-dispatch-leg"]
+    out = subprocess.run(cmd, check=True, capture_output=True, text=True, timeout=300, env=env).stdout
+    d = json.loads(out.strip().splitlines()[-1])
+    return {"value": d["value"], "unit": d["unit"], "ms_per_step": d["ms_per_step"], "step_ms": d.get("step_ms"),
+            "amd_direct_dispatch": "1",
+            "what": "the headline leg in a child process with HIP's default direct dispatch"}
 
 
 def track_mode(args, rank, world, local_rank, dist):
@@ -1154,6 +1174,11 @@ def track_mode(args, rank, world, local_rank, dist):
                    "path": "include/odo_frontend.hpp Extractor / Matcher / Ransac / PnPSolver over the per-stage "
                            "C-ABI (tools/frontend_latency.cpp), Tracking::Track order"}
 
+    direct = None
+    if rank == 0 and world == 1 and not args.no_direct_dispatch_leg and not adaptive and args.workload == "default" \
+            and not args.tum:
+        direct = run_direct_dispatch(args)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         nf = args.cpu_frames
@@ -1210,7 +1235,9 @@ def track_mode(args, rank, world, local_rank, dist):
                        "ate_mm": round(ate_mm, 3) if ate_mm is not None else None},
             "stage_ms": {k: round(v, 4) for k, v in timings.items()},
             "host_submit_ms_per_step": round(submit / K * 1e3, 3),
-            "hip_runtime": {"AMD_DIRECT_DISPATCH": os.environ.get("AMD_DIRECT_DISPATCH")},
+            "hip_runtime": {"AMD_DIRECT_DISPATCH": os.environ.get("AMD_DIRECT_DISPATCH"),
+                            "dispatch": "worker thread" if os.environ.get("AMD_DIRECT_DISPATCH") == "0" else "direct",
+                            "direct_dispatch_leg": direct},
             "from_host": from_host,
             "hard_workload": hard,
             "latency": latency,

@@ -54,13 +54,15 @@ typedef struct odo_kernel_forms {
     int32_t ransac_lanes_min_open;  /* open pairs from which the second RANSAC launch takes the
                                        lane-per-hypothesis kernel (0 = 32) */
     int32_t pyramid;                /* ODO_PYRAMID_FORM_*: gray + pyramid levels */
+    int32_t ransac_first_hyps;      /* batched path: hypotheses per pair in the first RANSAC
+                                       evaluation launch, 1..64 (0 = 2) */
 } odo_kernel_forms;
 
 /* Layout version of the structs below. odo_config starts with its own size,
  * which odo_default_config fills and odo_create checks, so a caller built
  * against a header with a different odo_config fails with ODO_ERR_ARG instead
  * of reading past its struct. */
-#define ODO_ABI_VERSION 4
+#define ODO_ABI_VERSION 5
 int odo_abi_version(void);  /* ODO_ABI_VERSION of the library */
 
 typedef struct odo_config {
@@ -104,8 +106,9 @@ double odo_get_latch(odo_ctx* ctx);
  * results[n] (host): results[i] is the pair (frame i-1 -> frame i); frame -1
  * is the last frame of the previous call. When h_results is NULL the call is
  * asynchronous: the work runs on the library's streams (extraction =
- * odo_stream(), plus pair / PnP / side streams), d_bgr and d_depth are read by
- * the extraction stream, and odo_synchronize() waits for all of them. */
+ * odo_stream(), plus pair / PnP / side streams), d_bgr is read by the
+ * extraction stream and d_depth by the batch's pair stream (the keypoint
+ * geometry), and odo_synchronize() waits for all of them. */
 int odo_track_batch(odo_ctx* ctx, const uint8_t* d_bgr, const uint16_t* d_depth, int n,
                     odo_pair_result* h_results);
 /* Same with host inputs, as Tracking::Track receives them (main.cpp:93-102).

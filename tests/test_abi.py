@@ -59,7 +59,7 @@ def test_config_struct_size_checked():
     device call, so this runs on CPU)."""
     pkg = load_pkg()
     lib = pkg.load()
-    assert lib.odo_abi_version() == 4
+    assert lib.odo_abi_version() == 5
     cfg = pkg.default_config(640, 480, 1)
     assert cfg.struct_size == C.sizeof(pkg._abi.Config)
     cfg.struct_size -= 8  # an older, shorter odo_config

@@ -224,3 +224,22 @@ def test_bench_configuration_ransac_lanes(name):
         _compare(name + " lanes", c, odo, res, oracle)
     finally:
         odo.close()
+
+
+@pytest.mark.parametrize("h0", [1, 3, 5, 8])
+def test_bench_configuration_first_ransac_launch(h0):
+    """The first RANSAC evaluation launch at other widths
+    (odo_kernel_forms.ransac_first_hyps): h0 hypotheses per pair,
+    fewer waves per workgroup than rows of four when h0 < 4 and a partly
+    filled second row at 5: every pair of the last batch bit-exact (visited
+    counts, T12, inlier lists, work counts)."""
+    name = "cfg2_bench"
+    c = CONFIGS[name]
+    pkg = load_pkg()
+    bgr, dep, _ = sequence(c["L"], c["w"], c["h"], intrinsics=c["intr"], seed=c["scene"], closed_loop=True)
+    odo, cfg, res = _run_gpu(pkg, c, bgr, dep, forms={"ransac_first_hyps": h0})
+    oracle = _oracle_cached(name, pkg, c, cfg, bgr, dep)
+    try:
+        _compare(name + f" first launch h0 {h0}", c, odo, res, oracle)
+    finally:
+        odo.close()

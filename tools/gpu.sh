@@ -39,7 +39,7 @@ O=$R/gpurun_out/${1:?outdir}; shift
 mkdir -p "$O"
 P=$R/adaptive-rgbd-localization-mappig_amd
 TUNING=$P/build_tuning/libodo_hip.so
-QUICK="--no-cpu-baseline --host-steps 0 --hard-steps 0 --latency-frames 0"
+QUICK="--no-cpu-baseline --no-direct-dispatch-leg --host-steps 0 --hard-steps 0 --latency-frames 0"
 export TMPDIR=/tmp
 
 lib_of() { if [ "$1" = default ]; then echo "$P/libodo_hip.so"; else echo "$P/build_$1/libodo_hip.so"; fi; }
@@ -107,7 +107,7 @@ for step in "$@"; do
     kt)
       cd /tmp
       timeout -s KILL 600 rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- \
-        python3 $R/bench.py --no-cpu-baseline --hard-steps 0 --latency-frames 0 > $O/kt_bench.json 2> $O/kt.err
+        python3 $R/bench.py --no-cpu-baseline --no-direct-dispatch-leg --hard-steps 0 --latency-frames 0 > $O/kt_bench.json 2> $O/kt.err
       cd $R
       T=$(find $O/kt -name '*kernel_trace.csv' -print -quit)
       python tools/rocprof_timed_region.py "$T" $O/kt_bench.json $O/rocprof_timed_region.json > $O/rtr.log 2>&1 || true
@@ -118,7 +118,7 @@ for step in "$@"; do
       name=${step#ktn=}
       cd /tmp
       timeout -s KILL 600 rocprofv3 --kernel-trace -d $O/$name -o run --output-format csv -- \
-        python3 $R/bench.py --no-cpu-baseline --latency-frames 0 --host-steps 0 $AB_ARGS > $O/$name.json 2> $O/$name.err
+        python3 $R/bench.py --no-cpu-baseline --no-direct-dispatch-leg --latency-frames 0 --host-steps 0 $AB_ARGS > $O/$name.json 2> $O/$name.err
       cd $R
       echo "ktn $name: $(python tools/bsum.py $O/$name.json 2>/dev/null || true)" ;;
     ktv=*)
@@ -126,7 +126,7 @@ for step in "$@"; do
       v=${step#ktv=}
       cd /tmp
       ODO_LIB=$(lib_of $v) timeout -s KILL 600 rocprofv3 --kernel-trace -d $O/ktv_$v -o run --output-format csv -- \
-        python3 $R/bench.py --no-cpu-baseline --latency-frames 0 --host-steps 0 --hard-steps 0 $AB_ARGS \
+        python3 $R/bench.py --no-cpu-baseline --no-direct-dispatch-leg --latency-frames 0 --host-steps 0 --hard-steps 0 $AB_ARGS \
         > $O/ktv_$v.json 2> $O/ktv_$v.err
       cd $R
       echo "ktv $v: $(python tools/bsum.py $O/ktv_$v.json 2>/dev/null || true)" ;;
@@ -134,7 +134,7 @@ for step in "$@"; do
       # kernel trace of the hard workload in the main (pipelined) leg
       cd /tmp
       timeout -s KILL 600 rocprofv3 --kernel-trace --stats -d $O/kth -o run --output-format csv -- \
-        python3 $R/bench.py --no-cpu-baseline --host-steps 0 --hard-steps 0 --latency-frames 0 --workload hard \
+        python3 $R/bench.py --no-cpu-baseline --no-direct-dispatch-leg --host-steps 0 --hard-steps 0 --latency-frames 0 --workload hard \
         --steps 10 > $O/kth_bench.json 2> $O/kth.err
       cd $R
       echo "kth ok" ;;
@@ -144,7 +144,7 @@ for step in "$@"; do
         -o run --output-format csv -- python3 $R/bench.py $QUICK --steps 10 > $O/serial_default.log 2>&1
       echo "serial default ok"
       ODO_SERIAL_STREAMS=1 ODO_LIB=$TUNING timeout -s KILL 300 rocprofv3 --kernel-trace --stats -d $O/serial_hard \
-        -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --host-steps 0 --latency-frames 0 \
+        -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --no-direct-dispatch-leg --host-steps 0 --latency-frames 0 \
         --steps 2 --hard-steps 0 --workload hard > $O/serial_hard.log 2>&1
       echo "serial hard ok" ;;
     vserial=*)
@@ -191,14 +191,14 @@ for step in "$@"; do
       spec=${step#envbench=}; name=${spec%%:*}; rest=${spec#*:}
       envs=$(echo ${rest%%:*} | tr '/' ' '); args=$(echo ${rest#*:} | tr '+' ' ')
       [ "$args" = "$rest" ] && args=""
-      env $envs ODO_LIB=$TUNING timeout -k 10 300 python bench.py --no-cpu-baseline --latency-frames 0 --host-steps 0 \
+      env $envs ODO_LIB=$TUNING timeout -k 10 300 python bench.py --no-cpu-baseline --no-direct-dispatch-leg --latency-frames 0 --host-steps 0 \
         $args > $O/$name.json 2> $O/$name.err
       echo "envbench $name: $(python tools/bsum.py $O/$name.json 2>/dev/null || true)" ;;
     ab=*)
       spec=${step#ab=}; n=${spec%%:*}; vs=$(echo ${spec#*:} | tr ',' ' ')
       for i in $(seq 1 $n); do
         for v in $vs; do
-          ODO_LIB=$(lib_of $v) timeout -k 10 300 python bench.py --no-cpu-baseline --latency-frames 0 --host-steps 0 \
+          ODO_LIB=$(lib_of $v) timeout -k 10 300 python bench.py --no-cpu-baseline --no-direct-dispatch-leg --latency-frames 0 --host-steps 0 \
             $AB_ARGS > $O/ab_${v}_$i.json 2> $O/ab_${v}_$i.err
           echo "ab $v $i: $(python tools/bsum.py $O/ab_${v}_$i.json 2>/dev/null || true)"
         done
