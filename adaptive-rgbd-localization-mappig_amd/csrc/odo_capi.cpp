@@ -172,6 +172,11 @@ struct odo_ctx {
     // reads the last frame's kun / xyz / uR); host_call: a track_host
     // batch (its depth reads must stay on the extraction stream)
     bool geo_pair = false, host_call = false;
+    // ODO_EARLY_WAIT (run_extract): the next batch's extraction-stream waits
+    // were queued during this one (pre_waited = that batch's counter)
+    bool early_waits = false;
+    bool defer_pdone = false;  // odo_track_batch_async: PnP-done events after the result copy
+    uint64_t pre_waited = ~(uint64_t)0;
     hipEvent_t ev_geo[NSETS] = {};
     bool geo_rec[NSETS] = {};
     uint64_t batch_counter = 0;
@@ -374,6 +379,9 @@ static inline int next_set(const odo_ctx* c) { return (c->seq_set + 1) % NSETS; 
 #ifndef ODO_WAIT_DEDUP
 #define ODO_WAIT_DEDUP 1
 #endif
+#ifndef ODO_EARLY_WAIT
+#define ODO_EARLY_WAIT 0
+#endif
 #ifndef ODO_GEO_PAIR
 // schedule 5, device inputs: the keypoint geometry (undistort, depth) and the
 // slot-0 roll run at the head of the batch's pair stream instead of at the
@@ -393,6 +401,20 @@ static int wait_pnp_done(odo_ctx* c, hipStream_t st, int set) {
     }
     HIPCHK(hipStreamWaitEvent(st, c->ev_pa[set], 0));
     HIPCHK(hipStreamWaitEvent(st, c->ev_pb[set], 0));
+    return ODO_OK;
+}
+
+// The extraction stream's waits before batch number `bc` (the batch_counter it
+// will have): its frame set is free once the PnP of the batch that last used
+// it is done, and (schedule 5) the PnP of batch bc - pyr_wait is done.
+static int queue_batch_waits(odo_ctx* c, uint64_t bc) {
+    int e;
+    const int s = (int)((c->seq_set + (int)(bc - c->batch_counter) + 1) % NSETS);  // the set batch bc extracts into
+    if (c->pdone_rec[s] && (e = wait_pnp_done(c, c->stream, s))) return e;
+    if (c->sched == 5 && c->pyr_wait > 0 && bc >= (uint64_t)c->pyr_wait) {
+        const int sb = c->batch_set[(bc - (uint64_t)c->pyr_wait) & 7];
+        if (!(ODO_WAIT_DEDUP && sb == s && c->pdone_rec[s]) && (e = wait_pnp_done(c, c->stream, sb))) return e;
+    }
     return ODO_OK;
 }
 
@@ -1465,6 +1487,14 @@ static int run_extract(odo_ctx* c, int set, const uint8_t* d_bgr, const uint16_t
                   c->keys_per_frame, c->okp + (size_t)slot * c->nlevels * c->okp_stride,
                   c->ocnt + (size_t)slot * c->nlevels, c->okp_stride, c->node_cap, n);
     tmark(c, 3, st);
+    if (c->early_waits) {
+        // ODO_EARLY_WAIT: the next batch's frame-set and PYR_WAIT waits, queued
+        // here, ahead of this batch's finalize, instead of between its end and
+        // the next pyramid (their events were recorded by earlier batches)
+        int e;
+        if ((e = queue_batch_waits(c, c->batch_counter + 1))) return e;
+        c->pre_waited = c->batch_counter + 1;
+    }
     if (split)
         HIPCHK(hipStreamWaitEvent(st, c->ev_blur[set], 0));
     else if (!blur_done)
@@ -1550,8 +1580,10 @@ static int run_pairs(odo_ctx* c, int set, int n) {
             launch_pnp(ps, P.f2_src, xyz, c->kun + b * KC * 2, c->ur + b * KC, nkp, c->kp_cap, 0, c->cal, P.T12,
                        P.pair_valid, P.n_matches, 20, P.edges, P.res, P.pnp_mask, n);
         tmark(c, 9, ps);
-        HIPCHK(hipEventRecord(c->ev_pa[set], ps));
-        HIPCHK(hipEventRecord(c->ev_pb[set], ps));
+        // schedule 5 waits on ev_pb alone (wait_pnp_done), and an async batch
+        // records it again after its result copy, before anything waits on it
+        if (!(ODO_WAIT_DEDUP && c->sched == 5)) HIPCHK(hipEventRecord(c->ev_pa[set], ps));
+        if (!(ODO_WAIT_DEDUP && c->sched == 5 && c->defer_pdone)) HIPCHK(hipEventRecord(c->ev_pb[set], ps));
         c->pdone_st[set] = ps;
         HIPCHK(hipGetLastError());
         return ODO_OK;
@@ -1630,12 +1662,8 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
     const size_t KC = (size_t)c->kp_cap;
     // ---- extraction stream: set s is free once the pair stages of the batch
     // before the previous one (which read it) are done
-    if (c->pdone_rec[s] && (e = wait_pnp_done(c, c->stream, s))) return e;
+    if (c->pre_waited != c->batch_counter && (e = queue_batch_waits(c, c->batch_counter))) return e;
     if (c->knn_gate && c->knn_rec) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_knn, 0));
-    if (c->sched == 5 && c->pyr_wait > 0 && c->batch_counter >= (uint64_t)c->pyr_wait) {
-        const int sb = c->batch_set[(c->batch_counter - (uint64_t)c->pyr_wait) & 7];
-        if (!(ODO_WAIT_DEDUP && sb == s && c->pdone_rec[s]) && (e = wait_pnp_done(c, c->stream, sb))) return e;
-    }
     tmark(c, 0, c->stream);
     // (the next batch's roll reads this set's last frame on its pair stream,
     // before its PnP: the batch that reuses this set waits for that PnP
@@ -1659,8 +1687,10 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
     // always hold (a batch's kNN-2 started before the previous batch's, seen
     // in the step marks), and the step was no faster. Not kept.)
     c->geo_pair = geo_pair;  // run_extract leaves the geometry out (only for this call)
+    c->early_waits = ODO_EARLY_WAIT && c->sched == 5 && !c->adaptive && !c->adaptive_orb;
     e = run_extract(c, s, d_bgr, d_depth, n, 1);
     c->geo_pair = false;
+    c->early_waits = false;
     if (e) return e;
     // the kNN-2 stream: the extraction stream, or the side stream (sched 3)
     hipStream_t ks = c->stream;
@@ -1743,7 +1773,8 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
         HIPCHK(hipEventRecord(c->ev_xdone[s], c->stream));
         launch_ransac_raw(c->cur_p, c->rscr[s], n, c->match_cap, c->mask_words, c->rcfg, (uint64_t)c->cfg.seed,
                           c->pair_counter, nullptr);
-        HIPCHK(hipEventRecord(c->ev_raw[s], c->cur_p));
+        // the words and their reader share the stream: no marker (ODO_WAIT_DEDUP)
+        if (!ODO_WAIT_DEDUP) HIPCHK(hipEventRecord(c->ev_raw[s], c->cur_p));
     } else {
         HIPCHK(hipEventRecord(c->ev_xdone[s], c->stream));
         // ---- side stream: RANSAC's rand() words depend on the pair seeds only
@@ -1755,7 +1786,7 @@ int odo_track_batch(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, i
     // ---- pair stream
     if (c->sched != 4 && c->sched != 5) c->cur_p = c->pstream;
     HIPCHK(hipStreamWaitEvent(c->cur_p, c->ev_xdone[s], 0));
-    HIPCHK(hipStreamWaitEvent(c->cur_p, c->ev_raw[s], 0));
+    if (!(ODO_WAIT_DEDUP && (c->sched == 4 || c->sched == 5))) HIPCHK(hipStreamWaitEvent(c->cur_p, c->ev_raw[s], 0));
     if (geo_pair) {
         // the roll (the previous batch's last frame into slot 0, once that
         // batch's geometry is done) and this batch's geometry, ahead of kNN-2
@@ -1799,7 +1830,10 @@ int odo_track_batch_async(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_de
     if (!h_results) return fail(ODO_ERR_ARG, "null results");
     const int first_valid = c && c->has_prev ? 1 : 0;
     int e;
-    if ((e = odo_track_batch(c, d_bgr, d_depth, n, nullptr))) return e;
+    c->defer_pdone = true;  // the PnP-done events are recorded after the copy below
+    e = odo_track_batch(c, d_bgr, d_depth, n, nullptr);
+    c->defer_pdone = false;
+    if (e) return e;
     const int s = c->view_set;
     auto& P = c->pb[s];
     hipStream_t st = c->cur_p ? c->cur_p : c->pstream;  // the batch's pair stream (its PnP ran there last)
@@ -1809,7 +1843,7 @@ int odo_track_batch_async(odo_ctx* c, const uint8_t* d_bgr, const uint16_t* d_de
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(h_results, P.res, (size_t)n * sizeof(odo_pair_result), hipMemcpyDeviceToHost, st));
     // the batch that next reuses set s waits for these events: include the copy
-    HIPCHK(hipEventRecord(c->ev_pa[s], st));
+    if (!(ODO_WAIT_DEDUP && c->sched == 5)) HIPCHK(hipEventRecord(c->ev_pa[s], st));
     HIPCHK(hipEventRecord(c->ev_pb[s], st));
     c->pdone_st[s] = st;
     return ODO_OK;
