@@ -59,7 +59,8 @@ struct RState {
     int32_t rng0_f, rng0_r;
     int active, done, ng, S, words, H;
     // ordered fold (ransac.cpp:233-249), updated under `lock`
-    int lock, fold_pos, n, visited, valid, best_cnt, best_h, pad;
+    int lock, fold_pos, n, visited, valid, best_cnt, best_h;
+    int efast;  // every evaluated point's depths in ef_fast_range (k_ransac_prep): ErrorFunction2's fast form is exact
     float rmse;
     int sweeps, fitpts;  // work of the visited prefix (odo_pair_result.n_sweeps / n_fit_points)
     int nexth;           // k_ransac_lanes: the next hypothesis a lane takes up
@@ -499,6 +500,7 @@ __global__ void __launch_bounds__(256) k_ransac_prep(RansacBufs B, RansacCfg cfg
     const int Ssz = min(max(cfg.sample_size, 1), MAX_SAMPLE);
     const int H = cfg.iterations;
     bool active = B.pair_valid[p] && nm >= B.min_matches && nm >= cfg.min_inlier_th;
+    __shared__ int s_efast_ok;
     if (t == 0) {
         R->rmse = 1e6f;
         R->n_good = active ? ng : 0;
@@ -518,6 +520,7 @@ __global__ void __launch_bounds__(256) k_ransac_prep(RansacBufs B, RansacCfg cfg
         const float* X1 = B.xyz + (size_t)(B.slot0 + p) * B.kp_cap * 3;
         const float* X2 = B.xyz + (size_t)(B.slot0 + p + 1) * B.kp_cap * 3;
         GoodPt* P = B.gpts + (size_t)p * B.match_cap;
+        bool zok = true;  // ErrorFunction2's fast form (ef_fast_pt)
         for (int k = t; k < ng; k += 256) {
             // defensive: an index outside the match list (never produced by a
             // correct sort) yields an excluded NaN point instead of a stray read
@@ -537,7 +540,11 @@ __global__ void __launch_bounds__(256) k_ransac_prep(RansacBufs B, RansacCfg cfg
             g.w = 1.0f / (g.sz * g.tz);  // ransac.cpp:305
             g.pad = 0.f;
             P[k] = g;
+            zok = zok && ef_fast_pt(g.sz, g.tx, g.sz, g.tz);
         }
+        s_efast_ok = 1;
+        __syncthreads();
+        if (!zok) s_efast_ok = 0;  // benign race: every writer stores 0
         uint32_t* BM = B.best_mask + (size_t)p * B.mask_words;
         for (int w = t; w < words; w += 256) BM[w] = 0;
         if (!done) {
@@ -545,7 +552,9 @@ __global__ void __launch_bounds__(256) k_ransac_prep(RansacBufs B, RansacCfg cfg
             for (int h = t; h < H; h += 256) rd[h] = 0;
         }
     }
+    __syncthreads();
     if (t == 0) {
+        S->efast = active && EF_FAST == 2 && s_efast_ok;
         S->active = active ? 1 : 0;
         S->ng = ng;
         S->S = Ssz;
@@ -950,6 +959,7 @@ ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int 
     K.raster_cov_x = cfg.raster_cov_x;
     K.raster_cov_y = cfg.raster_cov_y;
     K.depth_cov = *B.latch;
+    const bool efast = __builtin_amdgcn_readfirstlane(S->efast) && ef_fast_cov(K);  // wave-uniform
     const float th = cfg.max_mahal * cfg.max_mahal;
     const unsigned minInl = (unsigned)cfg.min_inlier_th;
     // this launch's waves stride over hypotheses [hofs + y0*EV_WAVES, hlim)
@@ -1052,7 +1062,7 @@ ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int 
                     const GoodPt g = load_pt<CACHED>(P, k);
                     if (!(g.sz == 0.0f || g.tx == 0.0f)) {
                         const float x1[3] = {g.sx, g.sy, g.sz}, x2[3] = {g.tx, g.ty, g.tz};
-                        d = error_function2_mk(x1, x2, Td, K);
+                        d = error_function2_mk(x1, x2, Td, K, nullptr, efast);
                         in = !(d > th) && (d >= 0.0);
                     }
                 }
@@ -1367,6 +1377,7 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
         if (slot < 0) break;
         const int p = __builtin_amdgcn_readfirstlane(B.open_list[slot]);
         RState* S = B.st + p;
+        const bool efast = __builtin_amdgcn_readfirstlane(S->efast) && ef_fast_cov(K);  // wave-uniform
         const int H = S->H, ng = S->ng, words = S->words;
         const GoodPt* P = B.gpts + (size_t)p * B.match_cap;
         const int* smp0 = B.samples + (size_t)p * B.hcap * SREC;
@@ -1513,7 +1524,7 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
                     const double Ta[12] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w, t2.x, t2.y, t2.z, t2.w};
                     double d = -1.0;  // not an inlier
                     if (a < nact && !skip) {
-                        const double e = error_function2_mk(x1, x2, Ta, K);
+                        const double e = error_function2_mk(x1, x2, Ta, K, nullptr, efast);
                         if (!(e > th) && (e >= 0.0)) d = e;
                     }
                     if (a < nact) lres[a * LN_RS + pj] = d;

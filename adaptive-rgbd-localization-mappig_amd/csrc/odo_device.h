@@ -514,9 +514,30 @@ ODO_INLINE double error_function2_mk_t(const float x1[3], const float x2[3], con
     return r;
 }
 
+// EF_FAST == 2 (k_ransac_eval / _lanes): the fast form without the per-call
+// check, for pairs whose evaluated points all have depths in [2^-20, 2^20]
+// (ef_fast_pt, checked once per pair by k_ransac_prep: RState.efast) under a
+// DepthCovariance latch in [2^-200, 2^200] (ef_fast_cov). There every operand
+// lies in the ranges above whenever the result can be accepted: with C2 =
+// diag(rcx mu2, rcy mu2, dcov) positive, A00 >= rcx mu2 > 2^-40, a positive
+// Schur complement of entries >= 2^-200 is at least one of their ulps (above
+// 2^-260), T comes from the float fit (|T| < 2^128, so A < 2^300), and a
+// NaN / infinite delta rejects the point before its value is read.
+ODO_INLINE bool ef_fast_pt(float sz, float tx, float sz2, float tz) {
+    // points ComputeInliersAndError skips (origin.z == 0 || target.x == 0,
+    // ransac.cpp:326) or rejects first (NaN depth) do not count
+    if (sz == 0.0f || tx == 0.0f || __builtin_isnan(sz2) || __builtin_isnan(tz)) return true;
+    return sz2 >= 0x1p-20f && sz2 <= 0x1p20f && tz >= 0x1p-20f && tz <= 0x1p20f;
+}
+ODO_INLINE bool ef_fast_cov(const MahalConst& K) {
+    return K.depth_cov >= 0x1p-200 && K.depth_cov <= 0x1p200 && K.raster_cov_x > 0x1p-40 &&
+           K.raster_cov_y > 0x1p-40 && K.raster_cov_x < 1.0 && K.raster_cov_y < 1.0;
+}
 ODO_INLINE double error_function2_mk(const float x1[3], const float x2[3], const double T[12], const MahalConst& K,
-                                     const double* Z = nullptr) {
+                                     const double* Z = nullptr, bool fast = false) {
     bool ok = true;
+    if (EF_FAST == 2) return fast ? error_function2_mk_t<true>(x1, x2, T, K, Z, ok)
+                                  : error_function2_mk_t<false>(x1, x2, T, K, Z, ok);
     double r = error_function2_mk_t<EF_FAST != 0>(x1, x2, T, K, Z, ok);
     if (EF_FAST == 1 && __builtin_expect(!ok, 0)) r = error_function2_mk_t<false>(x1, x2, T, K, Z, ok);
     return r;
