@@ -72,13 +72,18 @@ def _pos(c, b, i):
     return (b * (c["B"] + 1) + i) % c["L"]
 
 
+def _nb(c):
+    return c.get("batches", BATCHES)
+
+
 def _run_gpu(pkg, c, bgr, dep, forms=None):
-    """bench.py's timed loop: device-resident batches, BATCHES back-to-back
-    calls without a host sync (batch b's frames at _pos(c, b, .)).
+    """bench.py's timed loop: device-resident batches, _nb(c) back-to-back
+    calls without a host sync (batch b's frames at _pos(c, b, .)), except
+    one after batch c["sync_after"] when the config names it.
     forms: odo_kernel_forms fields (bit-identical kernel alternatives)."""
     import torch
-    B, L = c["B"], c["L"]
-    idx = torch.from_numpy(np.arange(BATCHES * (B + 1)) % L).to("cuda")
+    B, L, NB = c["B"], c["L"], _nb(c)
+    idx = torch.from_numpy(np.arange(NB * (B + 1)) % L).to("cuda")
     d_bgr = torch.from_numpy(np.ascontiguousarray(bgr)).to("cuda")[idx].contiguous()
     d_dep = torch.from_numpy(np.ascontiguousarray(dep).view(np.int16)).to("cuda")[idx].contiguous()
     fb, fd = d_bgr[0].numel(), 2 * d_dep[0].numel()  # bytes per frame
@@ -86,10 +91,12 @@ def _run_gpu(pkg, c, bgr, dep, forms=None):
                              calib=c["calib"], forms=forms)
     odo = pkg.Odometry(cfg)
     torch.cuda.synchronize()
-    for b in range(BATCHES):
+    for b in range(NB):
         o = b * (B + 1)
-        last = b == BATCHES - 1
+        last = b == NB - 1
         res = odo.track_batch(d_bgr.data_ptr() + o * fb, d_dep.data_ptr() + o * fd, B, want_results=last)
+        if b == c.get("sync_after", -1):
+            odo.synchronize()
     odo.synchronize()
     del d_bgr, d_dep
     return odo, cfg, res
@@ -97,7 +104,7 @@ def _run_gpu(pkg, c, bgr, dep, forms=None):
 
 def _pair_frames(c, frames, p):
     """(F1, F2) of pair p of the last batch."""
-    b = BATCHES - 1
+    b = _nb(c) - 1
     f2 = frames[_pos(c, b, p)]
     f1 = frames[_pos(c, b, p - 1)] if p > 0 else frames[(b * (c["B"] + 1) - 2) % c["L"]]
     return f1, f2
@@ -116,7 +123,7 @@ def _oracle_run(pkg, c, cfg, bgr, dep):
     while np.isnan(latch):
         _, _, _, latch = O.track_pair(frames[(g - 1) % L], frames[g % L], cal, rp, pkg.pair_seed(cfg.seed, g), latch)
         g += 1
-    g0 = (BATCHES - 1) * B
+    g0 = (_nb(c) - 1) * B
 
     def pair(p):
         f1, f2 = _pair_frames(c, frames, p)
@@ -139,10 +146,10 @@ def _oracle_cached(name, pkg, c, cfg, bgr, dep):
 def _compare(name, c, odo, res, oracle, full=True):
     cal, frames, pairs, latch = oracle
     B, L = c["B"], c["L"]
-    g0 = (BATCHES - 1) * B
+    g0 = (_nb(c) - 1) * B
     if full:
         for i in range(B):
-            got, ref = odo.frame(i), frames[_pos(c, BATCHES - 1, i)]
+            got, ref = odo.frame(i), frames[_pos(c, _nb(c) - 1, i)]
             assert len(got["kps"]) == len(ref["kps"]), f"{name} frame {i}: N"
             assert np.array_equal(got["kps"], ref["kps"]), f"{name} frame {i}: keypoints"
             assert np.array_equal(got["desc"], ref["desc"]), f"{name} frame {i}: descriptors"
@@ -241,5 +248,23 @@ def test_bench_configuration_first_ransac_launch(h0):
     oracle = _oracle_cached(name, pkg, c, cfg, bgr, dep)
     try:
         _compare(name + f" first launch h0 {h0}", c, odo, res, oracle)
+    finally:
+        odo.close()
+
+
+def test_bench_configuration_latched():
+    """Two batches, a host sync, then six more without one: from the third
+    batch on the DepthCovariance latch is known to be set (k_latch's host flag
+    after its event completed) and the batches leave the latch kernel and its
+    ordering packets out (odo_capi.cpp run_pairs). Every pair of the last
+    batch bit-exact, the latch included."""
+    name = "cfg2_latched"
+    c = dict(CONFIGS["cfg2_bench"], batches=8, sync_after=1)
+    pkg = load_pkg()
+    bgr, dep, _ = sequence(c["L"], c["w"], c["h"], intrinsics=c["intr"], seed=c["scene"], closed_loop=True)
+    odo, cfg, res = _run_gpu(pkg, c, bgr, dep)
+    oracle = _oracle_cached(name, pkg, c, cfg, bgr, dep)
+    try:
+        _compare(name, c, odo, res, oracle)
     finally:
         odo.close()
