@@ -25,6 +25,7 @@
 #   vserial=V           per-kernel times alone of variant build_V (built with -DODO_TUNING)
 #   vtests=V:F1,F2      pytest -m gpu over the named files against variant build_V
 #   probe=V:SCRIPT      python tools/SCRIPT.py with ODO_LIB = variant build_V (probe builds)
+#   vpmc=V:REGEX        pmc= with variant build_V (a tuning-flagged build)
 #   pmcx=NAME:REGEX:C1,C2   one PMC pass with the named counters (pmcx_NAME/)
 #   vpmcx=V:NAME:REGEX:C1,C2  pmcx with variant build_V
 #   listctr             rocprofv3 -L (the box's counter names) -> counters.txt
@@ -44,8 +45,9 @@ export TMPDIR=/tmp
 
 lib_of() { if [ "$1" = default ]; then echo "$P/libodo_hip.so"; else echo "$P/build_$1/libodo_hip.so"; fi; }
 
-pmc_passes() {  # REGEX OUTDIR BENCH_ARGS...
+pmc_passes() {  # REGEX OUTDIR BENCH_ARGS...  (library: $PMC_LIB, default the tuning build)
   local K=$1 D=$2; shift 2
+  local LIB=${PMC_LIB:-$TUNING}
   mkdir -p "$D"
   cd /tmp
   for spec in \
@@ -53,11 +55,11 @@ pmc_passes() {  # REGEX OUTDIR BENCH_ARGS...
     "sq2:SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_WAIT_ANY SQ_BUSY_CU_CYCLES" \
     "tcc:FETCH_SIZE" "tccw:WRITE_SIZE"; do
     local name=${spec%%:*} ctr=${spec#*:}
-    ODO_SERIAL_STREAMS=1 ODO_LIB=$TUNING timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-include-regex "$K" \
+    ODO_SERIAL_STREAMS=1 ODO_LIB=$LIB timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-include-regex "$K" \
       -d "$D/$name" -o run --output-format csv -- python3 $R/bench.py "$@" > "$D/$name.log" 2>&1
     echo "pmc $K $name ok"
   done
-  ODO_SERIAL_STREAMS=1 ODO_LIB=$TUNING timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d "$D/kt" -o run \
+  ODO_SERIAL_STREAMS=1 ODO_LIB=$LIB timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d "$D/kt" -o run \
     --output-format csv -- python3 $R/bench.py "$@" > "$D/kt.log" 2>&1
   echo "pmc $K kernel trace ok"
   cd $R
@@ -157,6 +159,10 @@ for step in "$@"; do
     pmc=*)
       K=${step#pmc=}
       pmc_passes "$K" "$O/pmc_$(echo $K | tr -c 'A-Za-z0-9_\n' '_')" --steps 3 --warmup 1 $QUICK ;;
+    vpmc=*)
+      # vpmc=V:REGEX — the four PMC passes of pmc= with variant build_V (-DODO_TUNING)
+      spec=${step#vpmc=}; v=${spec%%:*}; K=${spec#*:}
+      PMC_LIB=$(lib_of $v) pmc_passes "$K" "$O/pmc_${v}_$(echo $K | tr -c 'A-Za-z0-9_\n' '_')" --steps 3 --warmup 1 $QUICK ;;
     pmcx=*)
       # pmcx=NAME:REGEX:CTR1,CTR2,... — one extra counter pass (tuning build,
       # serial streams) over the kernels matching REGEX, into pmcx_NAME/
