@@ -640,7 +640,10 @@ __global__ void __launch_bounds__(PNP_NT, PNP_WAVES_PER_EU) k_pnp(const int32_t*
                                             odo_pair_result* __restrict__ res, uint8_t* __restrict__ inlier_mask,
                                             const int* __restrict__ sel, int sel_val) {
 #ifndef ODO_PNP_PRIO
-#define ODO_PNP_PRIO 3  // round 5 (the shorter kernel): 1.702-1.715 vs 1.726-1.730 ms per step at 0, 1.718-1.725 at 2 (profiles/r05_pr)
+// round 6: 0 — PnP ends ~80 us before the extraction step does and runs beside
+// finalize, which gets the issue slots (with ODO_WAVE_PRIO 1: profiles/r06_h;
+// round 5, PnP on the step's critical path: 3, profiles/r05_pr)
+#define ODO_PNP_PRIO 0
 #endif
     __builtin_amdgcn_s_setprio(ODO_PNP_PRIO);
     const int p = blockIdx.x;

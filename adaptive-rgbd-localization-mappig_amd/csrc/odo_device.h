@@ -11,10 +11,14 @@
 
 #define ODO_INLINE __device__ __forceinline__
 
-// s_setprio level of the latency-bound kernels (pair match, RANSAC, PnP) so
-// their waves issue ahead of co-resident extraction waves
+// s_setprio level of the latency-bound pair kernels (pair match, RANSAC) so
+// their waves issue ahead of co-resident extraction waves. Round 6: 1 (3
+// until round 5, when the pair chain was longer than the extraction step;
+// with the 512-thread pyramid it fits inside the step with slack, and at 1
+// the extraction kernels issue more: +0.3-0.9 % on the default workload and
+// +1.1 % on the hard one, profiles/r06_f, r06_g, r06_h)
 #ifndef ODO_WAVE_PRIO
-#define ODO_WAVE_PRIO 3
+#define ODO_WAVE_PRIO 1
 #endif
 
 namespace odo {
