@@ -99,7 +99,7 @@ struct RansacBufs {
     // hypotheses mode: evaluate only [h_lo, h_hi), no fold
     int h_lo, h_hi, no_fold;
     int* open_list;  // [pair] pairs still folding after the first launch
-    int* open_cnt;   // [0] their count, [1] the second launch's work counter
+    int* open_cnt;   // [0] their count, [1] the second launch's work counter, [2] all passed the EF guard
     uint32_t* lslab;  // k_ransac_lanes: [wave][2][mask_words][64] inlier sets
 };
 
@@ -959,7 +959,6 @@ ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int 
     K.raster_cov_x = cfg.raster_cov_x;
     K.raster_cov_y = cfg.raster_cov_y;
     K.depth_cov = *B.latch;
-    const bool efast = __builtin_amdgcn_readfirstlane(S->efast) && ef_fast_cov(K);  // wave-uniform
     const float th = cfg.max_mahal * cfg.max_mahal;
     const unsigned minInl = (unsigned)cfg.min_inlier_th;
     // this launch's waves stride over hypotheses [hofs + y0*EV_WAVES, hlim)
@@ -1062,7 +1061,7 @@ ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int 
                     const GoodPt g = load_pt<CACHED>(P, k);
                     if (!(g.sz == 0.0f || g.tx == 0.0f)) {
                         const float x1[3] = {g.sx, g.sy, g.sz}, x2[3] = {g.tx, g.ty, g.tz};
-                        d = error_function2_mk(x1, x2, Td, K, nullptr, efast);
+                        d = error_function2_mk(x1, x2, Td, K);
                         in = !(d > th) && (d >= 0.0);
                     }
                 }
@@ -1190,12 +1189,13 @@ __global__ void __launch_bounds__(64 * EV_WAVES, EV_MIN_BLOCKS) k_ransac_eval(Ra
 // The pairs still folding after the first launch, in pair order, and a work
 // counter for the second launch (one workgroup).
 __global__ void __launch_bounds__(256) k_ransac_open(RansacBufs B, int npairs) {
-    __shared__ int s_base;
-    if (threadIdx.x == 0) s_base = 0;
+    __shared__ int s_base, s_fast;
+    if (threadIdx.x == 0) s_base = 0, s_fast = 1;
     __syncthreads();
     for (int p0 = 0; p0 < npairs; p0 += 256) {
         const int p = p0 + (int)threadIdx.x;
         const bool open = p < npairs && !ld_relaxed(&B.st[p].done);
+        if (open && !B.st[p].efast) s_fast = 0;  // benign race: every writer stores 0
         const uint64_t bal = __ballot(open);
         __shared__ int s_cnt[4];
         if ((threadIdx.x & 63) == 0) s_cnt[threadIdx.x >> 6] = __popcll(bal);
@@ -1213,6 +1213,7 @@ __global__ void __launch_bounds__(256) k_ransac_open(RansacBufs B, int npairs) {
     if (threadIdx.x == 0) {
         B.open_cnt[0] = s_base;
         B.open_cnt[1] = 0;  // work counter
+        B.open_cnt[2] = s_fast;  // every open pair passed the fast-form guard (k_ransac_lanes)
     }
 }
 
@@ -1291,29 +1292,13 @@ __device__ uint64_t g_lprof[LPROF_MAX * 10];
 #define LP(...)
 #endif
 static_assert(LN_SLOTS <= 64, "a wave's hypothesis slots are its lanes");
-__global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B, RansacCfg cfg, uint32_t* lane_slab,
-                                                                   int waves_total, int min_open) {
-    // a throughput kernel (ms of FP64 issue): at LN_PRIO its waves do not
-    // starve the co-resident extraction waves of the next batch
-    __builtin_amdgcn_s_setprio(LN_PRIO);
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int gw = (int)blockIdx.x * LN_WAVES + wv;
-    // the good points stream through a per-wave LDS chunk: one coalesced load
-    // per lane, then wave-uniform broadcast reads in point order
-    __shared__ GoodPt s_pts[LN_WAVES][64];
-    GoodPt* lp = s_pts[wv];
-    // the sweep's parked Mahalanobis terms: [active slot][32 points, row
-    // stride LN_RS], and the active lanes in slot order. Every active lane then
-    // reads its own row in point order: with a 32-double stride all 64 lanes
-    // would hit one bank pair (a 32-way conflict per ds_read_b64 half); 33
-    // puts lane r's row on banks 2r, 2r + 1
-    __shared__ double s_res[LN_WAVES][LN_SLOTS * LN_RS];
-    __shared__ int s_la[LN_WAVES][64];
-    double* lres = s_res[wv];
-    int* la = s_la[wv];
-    __shared__ __attribute__((aligned(16))) float s_T[LN_WAVES][LN_SLOTS * 12];  // active slots' transforms
-    float* lT = s_T[wv];
+// EFAST: every open pair's points passed k_ransac_prep's guard (RState.efast)
+// under a latch in ef_fast_cov's range: ErrorFunction2 in its fast form, which
+// gives the same bits there (odo_device.h). Two instantiations, chosen once per
+// launch, so neither carries the other's registers.
+template <bool EFAST>
+ODO_INLINE void lanes_body(const RansacBufs& B, const RansacCfg& cfg, uint32_t* lane_slab, int waves_total,
+                           int min_open, int lane, int wv, int gw, GoodPt* lp, double* lres, int* la, float* lT) {
     const int cnt = B.open_cnt[0];
     if (cnt < min_open || cnt <= 0) return;  // few open pairs: latency matters, k_ransac_eval_list takes them
     uint32_t* slab = lane_slab + (size_t)gw * 2 * B.mask_words * 64;
@@ -1377,7 +1362,6 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
         if (slot < 0) break;
         const int p = __builtin_amdgcn_readfirstlane(B.open_list[slot]);
         RState* S = B.st + p;
-        const bool efast = __builtin_amdgcn_readfirstlane(S->efast) && ef_fast_cov(K);  // wave-uniform
         const int H = S->H, ng = S->ng, words = S->words;
         const GoodPt* P = B.gpts + (size_t)p * B.match_cap;
         const int* smp0 = B.samples + (size_t)p * B.hcap * SREC;
@@ -1524,7 +1508,7 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
                     const double Ta[12] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w, t2.x, t2.y, t2.z, t2.w};
                     double d = -1.0;  // not an inlier
                     if (a < nact && !skip) {
-                        const double e = error_function2_mk(x1, x2, Ta, K, nullptr, efast);
+                        const double e = error_function2_mk(x1, x2, Ta, K, nullptr, EFAST);
                         if (!(e > th) && (e >= 0.0)) d = e;
                     }
                     if (a < nact) lres[a * LN_RS + pj] = d;
@@ -1623,6 +1607,37 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
         r[6] = lp_inner, r[7] = lp_sum, r[8] = lp_p1, r[9] = lp_p2;  // (fold time and pair: lp_fold, lp_pair)
     }
 #endif
+}
+
+__global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B, RansacCfg cfg, uint32_t* lane_slab,
+                                                                   int waves_total, int min_open) {
+    // a throughput kernel (ms of FP64 issue): at LN_PRIO its waves do not
+    // starve the co-resident extraction waves of the next batch
+    __builtin_amdgcn_s_setprio(LN_PRIO);
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int gw = (int)blockIdx.x * LN_WAVES + wv;
+    // the good points stream through a per-wave LDS chunk: one coalesced load
+    // per lane, then wave-uniform broadcast reads in point order
+    __shared__ GoodPt s_pts[LN_WAVES][64];
+    // the sweep's parked Mahalanobis terms: [active slot][32 points, row
+    // stride LN_RS], and the active lanes in slot order. Every active lane then
+    // reads its own row in point order: with a 32-double stride all 64 lanes
+    // would hit one bank pair (a 32-way conflict per ds_read_b64 half); 33
+    // puts lane r's row on banks 2r, 2r + 1
+    __shared__ double s_res[LN_WAVES][LN_SLOTS * LN_RS];
+    __shared__ int s_la[LN_WAVES][64];
+    __shared__ __attribute__((aligned(16))) float s_T[LN_WAVES][LN_SLOTS * 12];  // active slots' transforms
+    MahalConst K;
+    K.raster_cov_x = cfg.raster_cov_x;
+    K.raster_cov_y = cfg.raster_cov_y;
+    K.depth_cov = *B.latch;
+    if (EF_FAST == 2 && __builtin_amdgcn_readfirstlane(B.open_cnt[2]) && ef_fast_cov(K))
+        lanes_body<true>(B, cfg, lane_slab, waves_total, min_open, lane, wv, gw, s_pts[wv], s_res[wv], s_la[wv],
+                         s_T[wv]);
+    else
+        lanes_body<false>(B, cfg, lane_slab, waves_total, min_open, lane, wv, gw, s_pts[wv], s_res[wv], s_la[wv],
+                          s_T[wv]);
 }
 
 // ---------------------------------------------------------------- final
@@ -1964,7 +1979,7 @@ static Layout layout(int npairs, int match_cap, int mask_words, const RansacCfg&
     L.raw = o;
     o = al(o + (size_t)npairs * ransac_rawcap(cfg) * 4);
     L.open = o;
-    o = al(o + (size_t)(npairs + 2) * 4);
+    o = al(o + (size_t)(npairs + 4) * 4);
     L.lslab = o;  // per-wave inlier-set buffers of k_ransac_lanes (never launched for one pair:
                   // a lone pair starts every hypothesis row in the first launch)
     if (npairs > 1) o = al(o + (size_t)ln_groups() * LN_WAVES * 2 * mask_words * 64 * 4);

@@ -405,10 +405,15 @@ ODO_INLINE void hyp_cov_terms(const double T[12], const MahalConst& K, double Z[
 #ifndef EF_FAST
 // ErrorFunction2's three square roots and three reciprocals (error_function2_mk)
 // as the cores of LLVM's correctly rounded AMDGPU f64 sequences without their
-// range fix-ups, which are inactive on the ranges below (ef_sqrt / ef_rcp);
-// an evaluation with an operand outside them is redone with the IEEE
-// sequences, so the results are bit-identical
-#define EF_FAST 0
+// range fix-ups, which are inactive on the ranges below (ef_sqrt / ef_rcp).
+// 1: every evaluation in the fast form, redone with the IEEE sequences when an
+// operand falls outside them (bit-identical; costs k_ransac_lanes registers:
+// 187 VGPRs, which break its co-residency with k_pnp). 2 (default):
+// k_ransac_lanes picks the fast form once per launch when every open pair
+// passed k_ransac_prep's range guard (below), else the IEEE form; the other
+// kernels keep the IEEE form. Round 6, hard workload, 3 alternations each:
+// 53.1k vs 51.4k frames/s (profiles/r06_ef2); 46 parity tests green on it.
+#define EF_FAST 2
 #endif
 // sqrt: v_rsq_f64, then the Goldschmidt iteration and two corrections of
 // LLVM's lowering (its ldexp scaling only acts below 2^-767, its class test
@@ -518,7 +523,7 @@ ODO_INLINE double error_function2_mk_t(const float x1[3], const float x2[3], con
     return r;
 }
 
-// EF_FAST == 2 (k_ransac_eval / _lanes): the fast form without the per-call
+// EF_FAST == 2 (k_ransac_lanes): the fast form without the per-call
 // check, for pairs whose evaluated points all have depths in [2^-20, 2^20]
 // (ef_fast_pt, checked once per pair by k_ransac_prep: RState.efast) under a
 // DepthCovariance latch in [2^-200, 2^200] (ef_fast_cov). There every operand
