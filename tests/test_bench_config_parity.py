@@ -143,7 +143,7 @@ def _oracle_cached(name, pkg, c, cfg, bgr, dep):
     return _ORACLE[name]
 
 
-def _compare(name, c, odo, res, oracle, full=True):
+def _compare(name, c, odo, res, oracle, full=True, pnp=True):
     cal, frames, pairs, latch = oracle
     B, L = c["B"], c["L"]
     g0 = (_nb(c) - 1) * B
@@ -171,6 +171,8 @@ def _compare(name, c, odo, res, oracle, full=True):
         assert np.array_equal(res[p]["T12"], np.array(r.T12, np.float32)), f"{tag}: T12"
         assert res[p]["rmse"] == np.float32(r.rmse), f"{tag}: rmse"
         O.check_ransac_inliers(g, r, tag)
+        if not pnp:
+            continue
         Tref = np.array(r.Tcw, np.float32).reshape(4, 4)
         dT = np.abs(res[p]["Tcw"].reshape(4, 4) - Tref).max()
         assert dT < 1e-4, f"{tag}: PnP pose differs by {dT}"
@@ -266,5 +268,33 @@ def test_bench_configuration_latched():
     oracle = _oracle_cached(name, pkg, c, cfg, bgr, dep)
     try:
         _compare(name, c, odo, res, oracle)
+    finally:
+        odo.close()
+
+
+def test_bench_configuration_ransac_lanes_ieee_form():
+    """k_ransac_lanes in its IEEE ErrorFunction2 form. The fast square-root /
+    reciprocal form (EF_FAST=2, the default) is chosen per launch only when
+    every open pair's points have depths in [2^-20, 2^20] (k_ransac_prep's
+    guard); with depth_factor 1e-10 (z = raw * depth_factor; TUM's is
+    1 / 5000) the bench scene's depths (raw 4614-17886) become
+    4.6e-7-1.8e-6 m, partly below it, so the launch takes the IEEE form.
+    Forced onto the lanes kernel as in test_bench_configuration_ransac_lanes:
+    every pair's RANSAC result bit-exact (counts, work counts, T12, rmse,
+    inlier lists) and the latch exact. PnP is not compared: at these depths
+    its stereo terms (u - mbf / z ~ -4e7) leave float resolution, which the
+    pose tolerance does not cover, and this test is about RANSAC."""
+    name = "cfg2_tiny_depth"
+    c = dict(CONFIGS["cfg2_bench"], calib=dict(depth_factor=1e-10))
+    pkg = load_pkg()
+    bgr, dep, _ = sequence(c["L"], c["w"], c["h"], intrinsics=c["intr"], seed=c["scene"], closed_loop=True)
+    odo, cfg, res = _run_gpu(pkg, c, bgr, dep, forms={"ransac_lanes_min_open": 1})
+    oracle = _oracle_cached(name, pkg, c, cfg, bgr, dep)
+    try:
+        for i in range(c["B"]):
+            z = odo.frame(i)["xyz"].reshape(-1, 3)[:, 2]
+            z = z[np.isfinite(z) & (z > 0)]
+            assert z.size and (z < 2.0 ** -20).mean() > 0.05, f"frame {i}: depths not below the fast-form guard"
+        _compare(name + " lanes IEEE form", c, odo, res, oracle, pnp=False)
     finally:
         odo.close()
