@@ -1270,6 +1270,17 @@ ODO_INLINE double readlane_d(double v, int l) {
 }
 #define LN_WAVES 4
 #define LN_RS 33  // LDS row stride (doubles) of the parked terms
+#ifndef LN_TD
+// 1: the active slots' transforms parked in LDS as doubles, with their
+// point-independent covariance terms (hyp_cov_terms), so the sweep's
+// evaluations read them instead of converting twelve floats and forming six
+// products each time (the same values: the conversions are exact and Z's
+// products are the ones error_function2_mk forms without it)
+#define LN_TD 1
+#endif
+// LDS words per slot: 12 + 6 doubles (1), 12 doubles without the covariance
+// terms (2), or 12 floats (0)
+#define LN_TW (LN_TD == 1 ? 18 : 12)
 #ifndef LN_SLOTS
 #define LN_SLOTS 32  // lanes per wave that take up hypotheses (rows of parked terms per wave)
 #endif
@@ -1298,7 +1309,8 @@ static_assert(LN_SLOTS <= 64, "a wave's hypothesis slots are its lanes");
 // launch, so neither carries the other's registers.
 template <bool EFAST>
 ODO_INLINE void lanes_body(const RansacBufs& B, const RansacCfg& cfg, uint32_t* lane_slab, int waves_total,
-                           int min_open, int lane, int wv, int gw, GoodPt* lp, double* lres, int* la, float* lT) {
+                           int min_open, int lane, int wv, int gw, GoodPt* lp, double* lres, int* la, double* lTd) {
+    float* const lT = reinterpret_cast<float*>(lTd);
     const int cnt = B.open_cnt[0];
     if (cnt < min_open || cnt <= 0) return;  // few open pairs: latency matters, k_ransac_eval_list takes them
     uint32_t* slab = lane_slab + (size_t)gw * 2 * B.mask_words * 64;
@@ -1484,10 +1496,22 @@ ODO_INLINE void lanes_body(const RansacBufs& B, const RansacCfg& cfg, uint32_t* 
             // the active hypotheses' transforms in slot order, read back by the
             // sweep as three broadcast 16-byte loads per slot instead of 12 permutes
             if (act) {
-                float4* tw = reinterpret_cast<float4*>(lT + rank * 12);
-                tw[0] = make_float4(T[0], T[1], T[2], T[3]);
-                tw[1] = make_float4(T[4], T[5], T[6], T[7]);
-                tw[2] = make_float4(T[8], T[9], T[10], T[11]);
+                if (LN_TD) {
+                    double* tw = lTd + rank * LN_TW;
+                    double Z[6];
+#pragma unroll
+                    for (int i = 0; i < 12; i += 2) *reinterpret_cast<double2*>(tw + i) = double2{Td[i], Td[i + 1]};
+                    if (LN_TD == 1) {
+                        hyp_cov_terms(Td, K, Z);
+#pragma unroll
+                        for (int i = 0; i < 6; i += 2) *reinterpret_cast<double2*>(tw + 12 + i) = double2{Z[i], Z[i + 1]};
+                    }
+                } else {
+                    float4* tw = reinterpret_cast<float4*>(lT + rank * 12);
+                    tw[0] = make_float4(T[0], T[1], T[2], T[3]);
+                    tw[1] = make_float4(T[4], T[5], T[6], T[7]);
+                    tw[2] = make_float4(T[8], T[9], T[10], T[11]);
+                }
             }
             wave_sync();
             double meanError = 0.0;
@@ -1503,12 +1527,26 @@ ODO_INLINE void lanes_body(const RansacBufs& B, const RansacCfg& cfg, uint32_t* 
                 const float x1[3] = {g.sx, g.sy, g.sz}, x2[3] = {g.tx, g.ty, g.tz};
                 for (int i = 0; i < nact; i += 2) {
                     const int a = i + hf;  // this half's hypothesis slot
-                    const float4* tr = reinterpret_cast<const float4*>(lT + min(a, nact - 1) * 12);
-                    const float4 t0 = tr[0], t1 = tr[1], t2 = tr[2];
-                    const double Ta[12] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w, t2.x, t2.y, t2.z, t2.w};
+                    double Ta[12];
+                    const double* Za = nullptr;
+                    if (LN_TD) {
+                        const double* tr = lTd + min(a, nact - 1) * LN_TW;
+#pragma unroll
+                        for (int q = 0; q < 12; q += 2) {
+                            const double2 v = *reinterpret_cast<const double2*>(tr + q);
+                            Ta[q] = v.x, Ta[q + 1] = v.y;
+                        }
+                        if (LN_TD == 1) Za = tr + 12;
+                    } else {
+                        const float4* tr = reinterpret_cast<const float4*>(lT + min(a, nact - 1) * 12);
+                        const float4 t0 = tr[0], t1 = tr[1], t2 = tr[2];
+                        const float tf[12] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w, t2.x, t2.y, t2.z, t2.w};
+#pragma unroll
+                        for (int q = 0; q < 12; q++) Ta[q] = tf[q];
+                    }
                     double d = -1.0;  // not an inlier
                     if (a < nact && !skip) {
-                        const double e = error_function2_mk(x1, x2, Ta, K, nullptr, EFAST);
+                        const double e = error_function2_mk(x1, x2, Ta, K, Za, EFAST);
                         if (!(e > th) && (e >= 0.0)) d = e;
                     }
                     if (a < nact) lres[a * LN_RS + pj] = d;
@@ -1627,7 +1665,7 @@ __global__ void __launch_bounds__(64 * LN_WAVES, 2) k_ransac_lanes(RansacBufs B,
     // puts lane r's row on banks 2r, 2r + 1
     __shared__ double s_res[LN_WAVES][LN_SLOTS * LN_RS];
     __shared__ int s_la[LN_WAVES][64];
-    __shared__ __attribute__((aligned(16))) float s_T[LN_WAVES][LN_SLOTS * 12];  // active slots' transforms
+    __shared__ __attribute__((aligned(16))) double s_T[LN_WAVES][LN_SLOTS * LN_TW / (LN_TD ? 1 : 2)];  // active slots' transforms
     MahalConst K;
     K.raster_cov_x = cfg.raster_cov_x;
     K.raster_cov_y = cfg.raster_cov_y;
