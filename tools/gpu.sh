@@ -22,6 +22,7 @@
 #   pmc=REGEX           PMC passes over the kernels matching REGEX (tuning build,
 #                       serial streams), one counter group per rocprofv3 run
 #   pmch=REGEX          the same on the hard workload
+#   vpmch=V:REGEX       pmch= with variant build_V (a tuning-flagged build)
 #   vserial=V           per-kernel times alone of variant build_V (built with -DODO_TUNING)
 #   vtests=V:F1,F2      pytest -m gpu over the named files against variant build_V
 #   probe=V:SCRIPT      python tools/SCRIPT.py with ODO_LIB = variant build_V (probe builds)
@@ -192,6 +193,10 @@ for step in "$@"; do
     pmch=*)
       K=${step#pmch=}
       pmc_passes "$K" "$O/pmch_$(echo $K | tr -c 'A-Za-z0-9_\n' '_')" --steps 2 --warmup 1 $QUICK --workload hard ;;
+    vpmch=*)
+      # vpmch=V:REGEX — pmch= with variant build_V (a tuning-flagged build)
+      spec=${step#vpmch=}; v=${spec%%:*}; K=${spec#*:}
+      PMC_LIB=$(lib_of $v) pmc_passes "$K" "$O/pmch_${v}_$(echo $K | tr -c 'A-Za-z0-9_\n' '_')" --steps 2 --warmup 1 $QUICK --workload hard ;;
     envbench=*)
       # envbench=NAME:VAR=VAL/VAR2=VAL2:ARGS — the tuning build with knobs from the environment
       spec=${step#envbench=}; name=${spec%%:*}; rest=${spec#*:}
