@@ -948,6 +948,12 @@ ODO_INLINE void try_fold_wave(const RansacBufs& B, const RansacCfg& cfg, int p, 
     }
 }
 
+#ifndef EV_EFAST
+#define EV_EFAST 1  // the evaluation kernels take the fast ErrorFunction2 form for guarded pairs
+#endif
+#ifndef EV_Z
+#define EV_Z 1  // ... and the per-hypothesis covariance products (hyp_cov_terms)
+#endif
 template <bool CACHED>
 ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int wave, int lane, EvalLds& L,
                           const GoodPt* P, int ng, int words, int H, int hofs, int y0, int hlim, int yrow,
@@ -961,6 +967,9 @@ ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int 
     K.depth_cov = *B.latch;
     const float th = cfg.max_mahal * cfg.max_mahal;
     const unsigned minInl = (unsigned)cfg.min_inlier_th;
+    // the pair's points passed k_ransac_prep's range guard (RState.efast):
+    // ErrorFunction2's fast form, the same bits (odo_device.h); wave-uniform
+    const bool efast = EV_EFAST && EF_FAST == 2 && __builtin_amdgcn_readfirstlane(S->efast) && ef_fast_cov(K);
     // this launch's waves stride over hypotheses [hofs + y0*EV_WAVES, hlim)
     const int hend = min(H, hlim);
     for (int h = hofs + (y0 + yrow) * EV_WAVES + wave; h < hend; h += ystride * EV_WAVES) {
@@ -1044,6 +1053,8 @@ ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int 
             double Td[12];
 #pragma unroll
             for (int i = 0; i < 12; i++) Td[i] = (double)T[i];
+            double Zd[6];  // the covariance's point-independent products, once per sweep
+            if (EV_Z) hyp_cov_terms(Td, K, Zd);
             RP_ACC(t_get);
             RP_T0();
             // poll the fold's stop flag once per refinement: issued here, read
@@ -1061,7 +1072,7 @@ ODO_INLINE void eval_hyps(const RansacBufs& B, const RansacCfg& cfg, int p, int 
                     const GoodPt g = load_pt<CACHED>(P, k);
                     if (!(g.sz == 0.0f || g.tx == 0.0f)) {
                         const float x1[3] = {g.sx, g.sy, g.sz}, x2[3] = {g.tx, g.ty, g.tz};
-                        d = error_function2_mk(x1, x2, Td, K);
+                        d = error_function2_mk(x1, x2, Td, K, EV_Z ? Zd : nullptr, efast);
                         in = !(d > th) && (d >= 0.0);
                     }
                 }

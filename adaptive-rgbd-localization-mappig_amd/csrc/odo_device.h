@@ -410,8 +410,9 @@ ODO_INLINE void hyp_cov_terms(const double T[12], const MahalConst& K, double Z[
 // operand falls outside them (bit-identical; costs k_ransac_lanes registers:
 // 187 VGPRs, which break its co-residency with k_pnp). 2 (default):
 // k_ransac_lanes picks the fast form once per launch when every open pair
-// passed k_ransac_prep's range guard (below), else the IEEE form; the other
-// kernels keep the IEEE form. Round 6, hard workload, 3 alternations each:
+// passed k_ransac_prep's range guard (below), else the IEEE form;
+// k_ransac_eval / _eval_list pick it per pair (EV_EFAST; a wave holds one
+// pair, so the branch is uniform). Round 6, hard workload, 3 alternations each:
 // 53.1k vs 51.4k frames/s (profiles/r06_ef2); 46 parity tests green on it.
 #define EF_FAST 2
 #endif
@@ -523,7 +524,7 @@ ODO_INLINE double error_function2_mk_t(const float x1[3], const float x2[3], con
     return r;
 }
 
-// EF_FAST == 2 (k_ransac_lanes): the fast form without the per-call
+// EF_FAST == 2 (k_ransac_lanes, k_ransac_eval*): the fast form without the per-call
 // check, for pairs whose evaluated points all have depths in [2^-20, 2^20]
 // (ef_fast_pt, checked once per pair by k_ransac_prep: RState.efast) under a
 // DepthCovariance latch in [2^-200, 2^200] (ef_fast_cov). There every operand
