@@ -164,6 +164,9 @@ constexpr int kCircleDy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 
 #define FS_TH 256
 #define FS_RING 512  // survivors per wave ring (u16 offsets): <= 127 pending + 256 per compass step
 #define FS_RSTRIDE (FS_RING + 8)  // a wave's ring + its trash slot (entry FS_RING), 16-byte multiple
+#ifndef FS_APPEND
+#define FS_APPEND 1  // the ring append by per-pixel ballots (1) or a DPP prefix sum (0)
+#endif
 #define FS_CL 1024   // corner list (a level-0 segment of 7 cells: ~270); beyond it NMS and placement scan the score map
 
 ODO_INLINE void wave_lds_sync() {
@@ -340,7 +343,7 @@ __global__ void __launch_bounds__(FS_TH) k_fast_seg(const uint8_t* __restrict__ 
                     const int ii = (int)__builtin_fmaf((float)it, inl, inl_h);
                     const int kk = it - __mul24(ii, NL);
                     const uint2 e = qlist[kk];
-                    int wb = ii * RS + (int)e.y;  // 3 rows above the quad: offsets >= 0
+                    int wb = (int)__umul24((uint32_t)ii, (uint32_t)RS) + (int)e.y;  // 3 rows above the quad: offsets >= 0
                     asm("" : "+v"(wb));
                     qoff = wb + 3 * RS;
                     const uint32_t* w = reinterpret_cast<const uint32_t*>(roi + wb);
@@ -370,6 +373,31 @@ __global__ void __launch_bounds__(FS_TH) k_fast_seg(const uint8_t* __restrict__ 
                     // pixel i's sign bit (bit 15 / 31 of half i / 2) to bit 8i + 7
                     pass4 = __builtin_amdgcn_perm(hm[1], hm[0], 0x07050301u) & e.x;
                 }
+#if FS_APPEND
+                // append to the ring (any order): pixel 0 of every lane's quad
+                // in lane order, then pixel 1, ...: a pixel's slot is the tail
+                // plus the survivors before it in that order (one ballot per
+                // pixel, mbcnt with the running tail as its addend). Every lane
+                // writes four entries, a pixel that did not survive to the
+                // wave's trash slot (no divergent branches). Until round 6:
+                // a DPP prefix sum of the lanes' counts and per-lane popcounts
+                // (the select takes the ballot itself as its lane mask: bit l
+                // of the ballot is lane l's condition)
+                uint32_t pos = (uint32_t)tail;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const bool sv = (pass4 >> (8 * k + 7)) & 1u;
+                    const uint64_t bk = __ballot(sv);
+                    const uint32_t slot =
+                        __builtin_amdgcn_mbcnt_hi((uint32_t)(bk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bk, pos)) &
+                        (FS_RING - 1);
+                    uint32_t at;
+                    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(at) : "v"((uint32_t)FS_RING), "v"(slot), "s"(bk));
+                    ring[at] = (uint16_t)(qoff + k);
+                    pos += (uint32_t)__popcll(bk);
+                }
+                tail = (int)pos;
+#else
                 // append to the ring (any order): this lane's survivors after
                 // those of the lanes below (a DPP prefix sum of the counts)
                 const int c = __builtin_popcount(pass4);
@@ -384,6 +412,7 @@ __global__ void __launch_bounds__(FS_TH) k_fast_seg(const uint8_t* __restrict__ 
                     ring[(pass4 >> (8 * k + 7)) & 1u ? slot : FS_RING] = (uint16_t)(qoff + k);
                 }
                 tail += __builtin_amdgcn_readlane(incl, 63);
+#endif
                 if (tail - head >= 128) {
                     wave_lds_sync();
                     do {
