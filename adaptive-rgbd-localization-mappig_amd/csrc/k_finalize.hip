@@ -30,6 +30,9 @@ __constant__ float4 c_patf[256];  // ORB_SLAM2 pattern test t: (x0, y0, x1, y1)
 // the same tests as signed bytes, lane-major: c_pat8[s * 16 + w] = test w * 16 + s
 // (k_finalize_lds lane s's sixteen tests in 64 contiguous bytes)
 __constant__ uint32_t c_pat8[256];
+#ifndef FIN_STAGE
+#define FIN_STAGE 1  // k_finalize_lds's window staging: uniform-stride lane grid (1) or the chunk walk (0)
+#endif
 #ifndef FIN_PAT
 #define FIN_PAT 2  // k_finalize_lds's pattern source: 0 c_patf, 1 an LDS copy of it, 2 c_pat8
 #endif
@@ -293,6 +296,64 @@ __global__ void __launch_bounds__(64 * NW) k_finalize_lds(const uint8_t* __restr
     const uint32_t key = valid ? okp[((size_t)f * nlevels + lvl) * okp_stride + k] : (16u | (16u << 12));
     const int kx = (int)(key & 0xfff) + 16, ky = (int)((key >> 12) & 0xfff) + 16;
     const float resp = (float)(key >> 24);
+#if FIN_STAGE
+    // Round 6: lanes sub < 15 as a fixed grid over each window's chunks —
+    // the IC disc's 31 rows of 3 chunks (12 bytes) as 5 rows x 3 chunks per
+    // step, the rBRIEF window's 37 rows of 5 chunks (8 bytes) as 3 rows x 5
+    // chunks per step — so every step is one uniform address increment (5 or
+    // 3 rows) instead of the wrap selects of the chunk walk below (7 + 13
+    // loads instead of 6 + 12, ≈130 fewer VALU per wave); lane 15 and the
+    // rows past a window's end load an in-window dummy and store nothing
+    constexpr int IC_STEPS = 7, BR_STEPS = 13;
+    uint2 vbr[BR_STEPS];  // the rBRIEF window's dwords (in flight during the IC angle)
+    uint32_t* P = s_patch[kslot];
+    const int sh = (kx - 15) & 3, sh2 = (kx - 18) & 3;
+    const bool glane = sub < 15;
+    const int ir = sub / 3, ic = sub - 3 * ir;  // IC: row in the step, chunk
+    const int br = sub / 5, bc = sub - 5 * br;  // rBRIEF
+    {
+        const uint8_t* fpyr = pyr + (size_t)f * pyr_stride;
+        const uint8_t* fblur = blur + (size_t)f * pyr_stride;
+        const uint32_t pitch = (uint32_t)L.pitch;
+        uint3 v[IC_STEPS];
+        {
+            const uint32_t o0 = (uint32_t)L.off + (uint32_t)(ky - 15) * pitch + (uint32_t)(kx - 15 - sh);
+            uint32_t o = o0 + (uint32_t)ir * pitch + 12u * (uint32_t)ic;
+#pragma unroll
+            for (int j = 0; j < IC_STEPS; j++) {
+                // rows ir + 5 j <= 30 for every lane (ir <= 5) until the last
+                // step, which holds row 30 only (ir == 0)
+                const bool ok = j + 1 < IC_STEPS || ir == 0;
+                v[j] = *reinterpret_cast<const uint3*>(fpyr + (ok ? o : o0));
+                o += 5u * pitch;
+            }
+        }
+        {
+            const uint32_t o0 = (uint32_t)L.off + (uint32_t)(ky - 18) * pitch + (uint32_t)(kx - 18 - sh2);
+            uint32_t o = o0 + (uint32_t)br * pitch + 8u * (uint32_t)bc;
+#pragma unroll
+            for (int j = 0; j < BR_STEPS; j++) {
+                // rows br + 3 j <= 36 for every lane (br <= 3) until the last
+                // step, which holds row 36 only (br == 0)
+                const bool ok = j + 1 < BR_STEPS || br == 0;
+                vbr[j] = *reinterpret_cast<const uint2*>(fblur + (ok ? o : o0));
+                o += 3u * pitch;
+            }
+        }
+        {
+            uint32_t* d = P + ir * FL_IC_W + 3 * ic;
+#pragma unroll
+            for (int j = 0; j < IC_STEPS; j++) {
+                if (glane && (j + 1 < IC_STEPS || ir == 0)) {
+                    d[0] = v[j].x;
+                    d[1] = v[j].y;
+                    d[2] = v[j].z;
+                }
+                d += 5 * FL_IC_W;
+            }
+        }
+    }
+#else
     uint2 vbr[12];  // the rBRIEF window's dwords (in flight during the IC angle)
     uint32_t* P = s_patch[kslot];
     const int sh = (kx - 15) & 3, sh2 = (kx - 18) & 3;
@@ -355,6 +416,7 @@ __global__ void __launch_bounds__(64 * NW) k_finalize_lds(const uint8_t* __restr
             }
         }
     }
+#endif
     __syncthreads();  // s_disc, the patches
     int m10, m01;
     {
@@ -404,6 +466,16 @@ __global__ void __launch_bounds__(64 * NW) k_finalize_lds(const uint8_t* __restr
     // staged byte of rotated offset (iy, ix): (iy + 18) * 40 + ix + 18 + sh2; the
     // magic-rounded floats carry RND_BITS + offset in their bits
     __syncthreads();  // every IC disc read
+#if FIN_STAGE
+    {
+        uint32_t* d = P + br * FL_BR_W + 2 * bc;
+#pragma unroll
+        for (int j = 0; j < BR_STEPS; j++) {
+            if (glane && (j + 1 < BR_STEPS || br == 0)) *reinterpret_cast<uint2*>(d) = vbr[j];
+            d += 3 * FL_BR_W;
+        }
+    }
+#else
     {
         // rBRIEF chunk c = sub + 16 j: row c / 5, dwords 2 (c % 5), + 1
         int r = sub / 5, p = sub % 5;
@@ -415,6 +487,7 @@ __global__ void __launch_bounds__(64 * NW) k_finalize_lds(const uint8_t* __restr
             p = wrap ? 0 : p + 1;
         }
     }
+#endif
     __syncthreads();
     const uint8_t* PB = reinterpret_cast<const uint8_t*>(P);
     // iy's low 24 bits are 0x400000 + dy (a 24-bit multiply: v_mad_u32_u24,
