@@ -481,7 +481,13 @@ ODO_INLINE void huber_rho(double delta, double chi, double rho[3]) {
 #endif
 #define PNP_NT (64 * PNP_NW)
 #ifndef PNP_K
-#define PNP_K 4  // Levenberg trials evaluated per edge pass (one per 16-lane group of wave 0)
+// Levenberg trials evaluated per edge pass (one per 16-lane group of wave 0).
+// Round 6: 2 — with the pair chain off the step's critical path, the
+// speculative trials' chi2 passes are issue slots the extraction kernels
+// beside PnP lose: 154.7-155.0 vs 153.7-154.3 k frames/s (4) and
+// 152.3-153.9 k (1); PnP alone 0.386-0.397 vs 0.380-0.385 ms (4), 0.44 (1);
+// hard workload unchanged (profiles/r06_w, r06_wh)
+#define PNP_K 2
 #endif
 static_assert(PNP_K <= 4, "the trial solves run on the four 16-lane groups of one wave");
 
