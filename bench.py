@@ -317,6 +317,7 @@ def step_stats(marks):
     return {"min": round(float(d.min()), 4), "median": round(med, 4), "p90": round(float(np.percentile(d, 90)), 4),
             "max": round(float(d.max()), 4), "mean": round(float(d.mean()), 4), "n": int(d.size),
             "max_over_median": round(float(d.max()) / med, 4) if med > 0 else None,
+            "argmax": int(np.argmax(d)), "intervals": [round(float(x), 3) for x in d],
             "source": "differences of consecutive batches' kNN-2 start events (odo_step_marks, rank 0)"}
 
 
