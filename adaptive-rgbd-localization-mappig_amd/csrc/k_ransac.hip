@@ -541,6 +541,9 @@ __global__ void __launch_bounds__(256) k_ransac_prep(RansacBufs B, RansacCfg cfg
             g.pad = 0.f;
             P[k] = g;
             zok = zok && ef_fast_pt(g.sz, g.tx, g.sz, g.tz);
+            // the TFC weights (tfc_div's range): every point the TFC adds
+            if (!__builtin_isnan(g.sz) && !__builtin_isnan(g.tz) && g.w != 0.0f)  // tfc_point_ok
+                zok = zok && g.w >= 0x1p-20f && g.w <= 0x1p20f;
         }
         s_efast_ok = 1;
         __syncthreads();
@@ -1281,6 +1284,9 @@ ODO_INLINE double readlane_d(double v, int l) {
 }
 #define LN_WAVES 4
 #define LN_RS 33  // LDS row stride (doubles) of the parked terms
+#ifndef LN_TFAST
+#define LN_TFAST 1  // the fast-form launch also takes the TFC division's fast form (tfc_div)
+#endif
 #ifndef LN_TD
 // 1: the active slots' transforms parked in LDS as doubles, with their
 // point-independent covariance terms (hyp_cov_terms), so the sweep's
@@ -1424,7 +1430,7 @@ ODO_INLINE void lanes_body(const RansacBufs& B, const RansacCfg& cfg, uint32_t* 
                     if (j < ns) {
                         const GoodPt g = P[smp[1 + j]];
                         if (tfc_point_ok(g)) {
-                            tf.add(g.sx, g.sy, g.sz, g.tx, g.ty, g.tz, g.w);
+                            tf.add<EFAST && LN_TFAST>(g.sx, g.sy, g.sz, g.tx, g.ty, g.tz, g.w);
                             nfit++;
                         }
                     }
@@ -1479,7 +1485,8 @@ ODO_INLINE void lanes_body(const RansacBufs& B, const RansacCfg& cfg, uint32_t* 
 #pragma unroll
                         for (int t = 0; t < 4; t++) {
                             const bool in = vj[t] && ((mine >> js[t]) & 1u);
-                            tf.add_sel(g4[t].sx, g4[t].sy, g4[t].sz, g4[t].tx, g4[t].ty, g4[t].tz, g4[t].w, in);
+                            tf.add_sel<EFAST && LN_TFAST>(g4[t].sx, g4[t].sy, g4[t].sz, g4[t].tx, g4[t].ty, g4[t].tz,
+                                                          g4[t].w, in);
                             nfit += in;
                         }
                     }

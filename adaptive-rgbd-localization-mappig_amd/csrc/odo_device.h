@@ -201,6 +201,26 @@ ODO_INLINE float det3(const float M[3][3]) {
 }
 
 // ------------------------------------------------ PCL TFC (A.7) accumulator
+// w / aw of the TFC recurrence: LLVM's f32 division sequence without its
+// v_div_scale / v_div_fixup (rcp, one Newton step, two Markstein corrections,
+// the last as a plain fma where v_div_fmas adds no scale). They are inactive,
+// so the quotient is the same bits, when the numerator lies in [2^-20, 2^20]
+// and the denominator in [2^-20, 2^40] (no operand scaling below an exponent
+// difference of 96, a normal quotient in (0, 1]): every weight a pair's TFC
+// adds in that range (k_ransac_prep's guard, RState.efast), a sum of at most
+// 2^20 of them (k_ransac_lanes' fast-form launch, LN_TFAST)
+template <bool FAST>
+ODO_INLINE float tfc_div(float a, float b) {
+    if (!FAST) return a / b;
+    float y = __builtin_amdgcn_rcpf(b);
+    const float e = __builtin_fmaf(-b, y, 1.0f);
+    y = __builtin_fmaf(e, y, y);
+    float q = a * y;
+    float r = __builtin_fmaf(-b, q, a);
+    q = __builtin_fmaf(r, y, q);
+    r = __builtin_fmaf(-b, q, a);
+    return __builtin_fmaf(r, y, q);
+}
 struct TFC {
     float accW;
     float m1[3], m2[3];
@@ -214,10 +234,11 @@ struct TFC {
             for (int j = 0; j < 3; j++) cov[i][j] = 0.f;
         }
     }
+    template <bool FD = false>
     ODO_INLINE void add(float px, float py, float pz, float qx, float qy, float qz, float w) {
         if (w == 0.0f) return;
         accW += w;
-        float alpha = w / accW;
+        float alpha = tfc_div<FD>(w, accW);
         float d1[3] = {px - m1[0], py - m1[1], pz - m1[2]};
         float d2[3] = {qx - m2[0], qy - m2[1], qz - m2[2]};
         const float oma = 1.0f - alpha;
@@ -237,10 +258,11 @@ struct TFC {
     // same operations on the same values for an added point, so a caller can
     // unroll over points and let the next points' divisions overlap this one's
     // updates
+    template <bool FD = false>
     ODO_INLINE void add_sel(float px, float py, float pz, float qx, float qy, float qz, float w, bool in) {
         const bool u = in & (w != 0.0f);
         const float aw = accW + w;
-        const float alpha = w / aw;
+        const float alpha = tfc_div<FD>(w, aw);
         const float d1[3] = {px - m1[0], py - m1[1], pz - m1[2]};
         const float d2[3] = {qx - m2[0], qy - m2[1], qz - m2[2]};
         const float oma = 1.0f - alpha;
