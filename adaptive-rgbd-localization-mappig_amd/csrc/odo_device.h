@@ -266,6 +266,27 @@ struct TFC {
         const float d1[3] = {px - m1[0], py - m1[1], pz - m1[2]};
         const float d2[3] = {qx - m2[0], qy - m2[1], qz - m2[2]};
         const float oma = 1.0f - alpha;
+        if (FD) {
+            // guarded launch (finite coordinates): a point the lane does not
+            // add updates with alpha = 0, 1 - alpha = 1, which leaves every
+            // accumulator's bits as they are — x + (+-0) = x, as none of them
+            // is ever -0 (they start at +0, and a sum is -0 only when both
+            // terms are) — so 2 selects replace the 15 below
+            const float al = u ? alpha : 0.0f, om = u ? oma : 1.0f;
+#pragma unroll
+            for (int i = 0; i < 3; i++) {
+                const float ad2 = al * d2[i];
+#pragma unroll
+                for (int j = 0; j < 3; j++) cov[i][j] = om * (cov[i][j] + ad2 * d1[j]);
+            }
+#pragma unroll
+            for (int i = 0; i < 3; i++) {
+                m1[i] = m1[i] + al * d1[i];
+                m2[i] = m2[i] + al * d2[i];
+            }
+            accW = u ? aw : accW;
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < 3; i++) {
             const float ad2 = alpha * d2[i];
