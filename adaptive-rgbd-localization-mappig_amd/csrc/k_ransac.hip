@@ -1476,7 +1476,10 @@ ODO_INLINE void lanes_body(const RansacBufs& B, const RansacCfg& cfg, uint32_t* 
 #pragma unroll
                         for (int t = 0; t < 4; t++) {
                             vj[t] = U != 0;
-                            js[t] = vj[t] ? (int)__builtin_ctzll(U) : 0;
+                            // a step past the union's end re-reads its first
+                            // point (in U: finite, so the guarded alpha = 0
+                            // no-op of add_sel stays exact)
+                            js[t] = vj[t] ? (int)__builtin_ctzll(U) : js[0];
                             U &= U - 1;
                         }
                         GoodPt g4[4];
