@@ -40,8 +40,13 @@ import numpy as np
 # before the HIP runtime initialises (torch is imported later). The
 # one-frame latency leg runs in its own process with direct dispatch (its
 # synchronous per-stage calls: p50 0.87 vs 0.91-0.95 ms, profiles/r05_zb).
+# The single-call latency modes (--mode pnpransac / gicp / hyp: one
+# synchronous call at a time, nothing to pipeline) keep HIP's direct
+# dispatch: the worker thread's hand-off is pure latency there.
 DIRECT_DISPATCH_FROM_ENV = "AMD_DIRECT_DISPATCH" in os.environ
-os.environ.setdefault("AMD_DIRECT_DISPATCH", "0")
+_MODE = next((sys.argv[i + 1] for i, a in enumerate(sys.argv[:-1]) if a == "--mode"),
+             next((a.split("=", 1)[1] for a in sys.argv if a.startswith("--mode=")), "track"))
+os.environ.setdefault("AMD_DIRECT_DISPATCH", "1" if _MODE in ("pnpransac", "gicp", "hyp") else "0")
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG_DIR = os.path.join(ROOT, "adaptive-rgbd-localization-mappig_amd")
